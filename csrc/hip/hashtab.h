@@ -1,0 +1,91 @@
+// hashtab.h — HBM-resident open-addressing hash table for (128-bit key -> int64
+// value, rep) aggregation.  This is the MI355X replacement for the reference's
+// map-side `result[key][N+1] = value` grouping (/root/reference/mapreduce/job.lua:83-97)
+// combined with the combiner (job.lua:92-96,198-202): values are folded with
+// an associative op at insert time instead of being appended to Lua tables.
+//
+// Layout is structure-of-arrays so every array is a plain torch tensor on the
+// Python side: tag[cap], hi[cap], lo[cap], val[cap], rep[cap] (u64 each) and a
+// 2-word control block {nclaimed, overflow}.
+//
+// Concurrency protocol (agent scope, placement independent — guide §6 G16):
+//   claim:   CAS tag 0 -> key_tag(hi,lo)            (relaxed, agent)
+//   publish: store hi, rep (relaxed) ; fold value ; store lo (RELEASE, agent)
+//   lookup:  tag match -> load lo (relaxed); lo==0 => not yet published, retry;
+//            lo match -> load hi; on mismatch re-check after an acquire fence.
+//   lo is never 0 for a valid key (mr_common.h), so lo doubles as "published".
+#pragma once
+#include <hip/hip_runtime.h>
+#include "mr_common.h"
+
+namespace mr {
+
+struct GTab {
+  u64* tag;
+  u64* hi;
+  u64* lo;
+  long long* val;
+  u64* rep;
+  u32* ctrl;      // [0] = claimed slots, [1] = overflow flag
+  u64 mask;       // capacity - 1 (capacity is a power of two)
+};
+
+constexpr u32 GTAB_MAX_PROBES = 1u << 14;
+
+__device__ __forceinline__ u64 ld_agent(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(u64* p, u64 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void fold_value(long long* p, long long v, int op) {
+  if (op == OP_MIN) atomicMin(p, v);
+  else if (op == OP_MAX) atomicMax(p, v);
+  else atomicAdd((unsigned long long*)p, (unsigned long long)v);
+}
+
+// Insert (hi,lo) with value v; returns false only when the probe budget is
+// exhausted (overflow flag set; the host re-runs with a larger table).
+__device__ __forceinline__ bool gtab_insert(const GTab& t, u64 hi, u64 lo, long long v, u64 rep, int op) {
+  const u64 tag = key_tag(hi, lo);
+  u64 slot = (tag >> 7) & t.mask;
+  u32 probes = 0;
+  while (probes < GTAB_MAX_PROBES) {
+    u64 cur = ld_agent(&t.tag[slot]);
+    if (cur == 0) {
+      u64 expected = 0;
+      if (__hip_atomic_compare_exchange_strong(&t.tag[slot], &expected, tag, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        st_agent(&t.hi[slot], hi);
+        st_agent(&t.rep[slot], rep);
+        fold_value(&t.val[slot], v, op);
+        __hip_atomic_store(&t.lo[slot], lo, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&t.ctrl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return true;
+      }
+      cur = expected;
+    }
+    if (cur == tag) {
+      const u64 l = ld_agent(&t.lo[slot]);
+      if (l == 0) continue;  // claimed but not yet published: re-read this slot
+      if (l == lo) {
+        u64 h = ld_agent(&t.hi[slot]);
+        if (h != hi) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          h = ld_agent(&t.hi[slot]);
+        }
+        if (h == hi) {
+          fold_value(&t.val[slot], v, op);
+          return true;
+        }
+      }
+    }
+    slot = (slot + 1) & t.mask;
+    ++probes;
+  }
+  __hip_atomic_fetch_or(&t.ctrl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return false;
+}
+
+}  // namespace mr

@@ -1,0 +1,86 @@
+// mr_common.h — shared device/host definitions for the MI355X MapReduce kernels.
+//
+// Key model (replaces the reference's interned Lua string/tuple keys,
+// /root/reference/mapreduce/tuple.lua:121-140 and the string keys emitted by
+// examples/WordCount/mapfn.lua:4-7):
+//
+//   Every key is a 128-bit value (hi, lo):
+//     * len <= 15  ("packed", exact):  hi = bytes[0..7] big-endian,
+//                                     lo = bytes[8..14] big-endian << 8 | len
+//       -> (hi, lo) compared as unsigned 128-bit == byte-lexicographic order
+//          (the order Lua's string `<` gives, utils.lua:126).
+//     * len >= 16  ("long", hashed):   hi = bytes[0..7] big-endian (exact prefix),
+//                                     lo = hash56(bytes) << 8 | 0xFF
+//       -> identity is (prefix, 56-bit hash); order is exact on the prefix.
+//   lo is never 0, so lo == 0 marks an unwritten table slot.
+//
+//   A "rep" word locates the key bytes of a long key inside a byte source:
+//       rep = (offset << 24) | min(len, 2^24-1)
+#pragma once
+#include <stdint.h>
+
+#ifndef MR_HD
+#if defined(__HIPCC__)
+#define MR_HD __host__ __device__ __forceinline__
+#else
+#define MR_HD inline
+#endif
+#endif
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+typedef uint8_t u8;
+
+namespace mr {
+
+constexpr u64 LONG_MARK = 0xFFull;
+constexpr int PACK_MAX = 15;          // longest exactly-packed key
+constexpr u64 REP_LEN_BITS = 24;
+constexpr u64 REP_LEN_MASK = (1ull << REP_LEN_BITS) - 1;
+
+// Lua 5.2 "%s" in the C locale: \t \n \v \f \r and space
+// (examples/WordCount/mapfn.lua:5 uses "[^%s]+").
+MR_HD bool is_ws(u32 c) { return c == 32u || (c - 9u) < 5u; }
+
+MR_HD u64 fmix64(u64 x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+// Slot tag of a key: never 0 (0 marks an empty slot).
+MR_HD u64 key_tag(u64 hi, u64 lo) { return fmix64(hi ^ fmix64(lo + 0x9E3779B97F4A7C15ull)) | 1ull; }
+
+// Hash of a long key, word-at-a-time over little-endian 8-byte words (the last
+// one zero padded).  Identical on host and device.
+MR_HD u64 long_hash_step(u64 h, u64 w) { return fmix64(h ^ w) * 0x9E3779B97F4A7C15ull; }
+MR_HD u64 long_hash_init(u64 len) { return 0x243F6A8885A308D3ull ^ (len * 0x13198A2E03707344ull); }
+MR_HD u64 long_lo(u64 h) { return (fmix64(h) << 8) | LONG_MARK; }
+
+MR_HD bool key_is_long(u64 lo) { return (lo & 0xFFull) == LONG_MARK; }
+MR_HD u32 packed_len(u64 lo) { return (u32)(lo & 0xFFull); }
+
+// Byte i (0-based) of a packed key.
+MR_HD u32 packed_byte(u64 hi, u64 lo, u32 i) {
+  return i < 8 ? (u32)((hi >> (56 - 8 * i)) & 0xFF) : (u32)((lo >> (56 - 8 * (i - 8))) & 0xFF);
+}
+
+// Exact uint32 FNV-1 (multiply, then xor), the hash of the reference
+// partitionfn (examples/WordCount/partitionfn.lua:8-16).  The reference computes
+// it in Lua doubles, which drops low bits once h*prime exceeds 2^53; this is the
+// exact 32-bit form (documented difference).
+constexpr u32 FNV_PRIME = 16777619u;
+constexpr u32 FNV_OFFSET = 2166136261u;
+MR_HD u32 fnv1_step(u32 h, u32 b) { return (h * FNV_PRIME) ^ b; }
+
+MR_HD u64 make_rep(u64 off, u64 len) { return (off << REP_LEN_BITS) | (len < REP_LEN_MASK ? len : REP_LEN_MASK); }
+MR_HD u64 rep_off(u64 rep) { return rep >> REP_LEN_BITS; }
+MR_HD u64 rep_len(u64 rep) { return rep & REP_LEN_MASK; }
+
+// Reduction operators for hash aggregation / reduce-by-key.
+enum ReduceOp : int { OP_SUM = 0, OP_MIN = 1, OP_MAX = 2, OP_COUNT = 3 };
+
+}  // namespace mr

@@ -1,0 +1,329 @@
+// sort.hip — LDS-tiled LSD radix sort, device-wide scans and segmented
+// primitives for gfx950 (wave64).
+//
+// Replaces the reference's ordering/merging hot loops:
+//   K6 map-side key sort   utils.lua:123-128 keys_sorted + job.lua:194
+//   K9 k-way merge         utils.lua:206-271 merge_iterator + heap.lua:29-70
+//   K8 reducer fold        job.lua:264-284 (per merged key)
+// Instead of a heap merge of 197 sorted runs per partition, the receiver
+// re-sorts the whole received buffer (radix sort is O(n) and bandwidth bound)
+// and folds equal keys with a segmented reduce.
+//
+// Radix pass = 3 launches: per-tile 256-bin histogram (LDS atomics), one
+// device-wide exclusive scan over the digit-major [256][tiles] histogram, and a
+// stable scatter in which each wave64 ranks its keys with 8 ballots (one per
+// digit bit): peers = AND_b (bit_b ? ballot_b : ~ballot_b), rank = popc(peers &
+// lanes_below).  Tiles are ITEMS = 16 x 256 keys; keys are visited round by
+// round (item = round*256 + thread) so a tile keeps input order (stability).
+#include <hip/hip_runtime.h>
+#include "mr_common.h"
+
+namespace mr {
+
+constexpr int RS_THREADS = 256;
+constexpr int RS_ROUNDS = 16;
+constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;  // 4096 keys per tile
+constexpr int RS_BINS = 256;
+constexpr int RS_WAVES = RS_THREADS / 64;
+
+__global__ void __launch_bounds__(RS_THREADS) rs_hist_kernel(const u64* keys, u64 n, int shift, u32* hist,
+                                                             u32 ntiles) {
+  __shared__ u32 h[RS_BINS];
+  const int t = threadIdx.x;
+  h[t] = 0;
+  __syncthreads();
+  const u64 base = (u64)blockIdx.x * RS_TILE;
+#pragma unroll 4
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const u64 i = base + (u64)r * RS_THREADS + t;
+    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1u);
+  }
+  __syncthreads();
+  hist[(u64)t * ntiles + blockIdx.x] = h[t];
+}
+
+template <typename V>
+__global__ void __launch_bounds__(RS_THREADS) rs_scatter_kernel(const u64* keys_in, const V* vals_in, u64* keys_out,
+                                                                V* vals_out, u64 n, int shift, const u32* offs,
+                                                                u32 ntiles) {
+  __shared__ u32 base_run[RS_BINS];
+  __shared__ u32 wcnt[RS_WAVES][RS_BINS];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  base_run[t] = offs[(u64)t * ntiles + blockIdx.x];
+  const u64 tile = (u64)blockIdx.x * RS_TILE;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const u64 i = tile + (u64)r * RS_THREADS + t;
+    const bool valid = i < n;
+    u64 k = 0;
+    V v{};
+    if (valid) {
+      k = keys_in[i];
+      if (vals_in) v = vals_in[i];
+    }
+    const u32 d = (u32)((k >> shift) & 0xFF);
+#pragma unroll
+    for (int w = 0; w < RS_WAVES; ++w) wcnt[w][t] = 0;
+    __syncthreads();
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const unsigned long long m = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? m : ~m;
+    }
+    const u32 rank = (u32)__popcll(peers & below);
+    if (valid && rank == 0) wcnt[wave][d] = (u32)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      u32 pos = base_run[d] + rank;
+      for (int w = 0; w < wave; ++w) pos += wcnt[w][d];
+      keys_out[pos] = k;
+      if (vals_in) vals_out[pos] = v;
+    }
+    __syncthreads();
+    u32 tot = 0;
+#pragma unroll
+    for (int w = 0; w < RS_WAVES; ++w) tot += wcnt[w][t];
+    base_run[t] += tot;
+    // next round clears wcnt after this barrier-free update: base_run[t] is
+    // only read after the next round's first barrier.
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Device-wide exclusive scan (reduce-then-scan, 3 launches).
+constexpr int SC_THREADS = 256;
+constexpr int SC_ITEMS = 16;
+constexpr int SC_TILE = SC_THREADS * SC_ITEMS;
+
+template <typename T>
+__device__ __forceinline__ T block_exclusive_scan(T x, T* sh, T* total) {
+  // Hillis-Steele over 256 threads in LDS (small; used once per tile).
+  const int t = threadIdx.x;
+  sh[t] = x;
+  __syncthreads();
+  for (int o = 1; o < SC_THREADS; o <<= 1) {
+    T y = t >= o ? sh[t - o] : (T)0;
+    __syncthreads();
+    sh[t] += y;
+    __syncthreads();
+  }
+  const T incl = sh[t];
+  if (total) *total = sh[SC_THREADS - 1];
+  __syncthreads();
+  return incl - x;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SC_THREADS) scan_reduce_kernel(const T* in, u64 n, T* partials) {
+  __shared__ T sh[SC_THREADS];
+  const u64 base = (u64)blockIdx.x * SC_TILE;
+  T s = 0;
+  for (int r = 0; r < SC_ITEMS; ++r) {
+    const u64 i = base + (u64)r * SC_THREADS + threadIdx.x;
+    if (i < n) s += in[i];
+  }
+  T tot;
+  block_exclusive_scan<T>(s, sh, &tot);
+  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SC_THREADS) scan_partials_kernel(T* partials, u64 np, T* total_out) {
+  // single block: each thread scans a contiguous strip, then block scan of strips
+  __shared__ T sh[SC_THREADS];
+  const u64 per = (np + SC_THREADS - 1) / SC_THREADS;
+  const u64 b = (u64)threadIdx.x * per;
+  T s = 0;
+  for (u64 i = b; i < b + per && i < np; ++i) s += partials[i];
+  T tot;
+  T off = block_exclusive_scan<T>(s, sh, &tot);
+  for (u64 i = b; i < b + per && i < np; ++i) {
+    T x = partials[i];
+    partials[i] = off;
+    off += x;
+  }
+  if (threadIdx.x == 0 && total_out) *total_out = tot;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SC_THREADS) scan_apply_kernel(const T* in, u64 n, T* out, const T* partials) {
+  __shared__ T sh[SC_THREADS];
+  const u64 base = (u64)blockIdx.x * SC_TILE;
+  // each thread owns SC_ITEMS contiguous items -> local sums, block scan, rescan
+  const u64 my = base + (u64)threadIdx.x * SC_ITEMS;
+  T vals[SC_ITEMS];
+  T s = 0;
+#pragma unroll
+  for (int r = 0; r < SC_ITEMS; ++r) {
+    const u64 i = my + r;
+    vals[r] = i < n ? in[i] : (T)0;
+    s += vals[r];
+  }
+  T off = block_exclusive_scan<T>(s, sh, nullptr) + partials[blockIdx.x];
+#pragma unroll
+  for (int r = 0; r < SC_ITEMS; ++r) {
+    const u64 i = my + r;
+    if (i < n) out[i] = off;
+    off += vals[r];
+  }
+}
+
+// ---------------------------------------------------------------------------
+__global__ void gather_u64_kernel(const u64* src, const u32* idx, u64* dst, u64 n) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[idx[i]];
+}
+
+__global__ void iota_u32_kernel(u32* dst, u64 n) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = (u32)i;
+}
+
+// heads[i] = 1 if (hi,lo)[i] starts a new run (keys sorted)
+__global__ void segment_heads_kernel(const u64* hi, const u64* lo, u64 n, u32* heads) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    heads[i] = (i == 0 || hi[i] != hi[i - 1] || (lo && lo[i] != lo[i - 1])) ? 1u : 0u;
+  }
+}
+
+// segment id (inclusive scan of heads - 1) is computed by the caller as
+// exclusive_scan(heads) + heads - 1; here fold values per segment with atomics
+// (segments are contiguous, so contention is bounded by a segment's length).
+__global__ void segment_fold_kernel(const u32* seg_excl, const u32* heads, const long long* vals, u64 n, int op,
+                                    long long* out) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u32 s = seg_excl[i] + heads[i] - 1u;
+    const long long v = vals ? vals[i] : 1ll;
+    if (op == OP_MIN) atomicMin(&out[s], v);
+    else if (op == OP_MAX) atomicMax(&out[s], v);
+    else atomicAdd((unsigned long long*)&out[s], (unsigned long long)v);
+  }
+}
+
+// unique keys: out[s] = key[i] for every head i
+__global__ void segment_keys_kernel(const u32* seg_excl, const u32* heads, const u64* hi, const u64* lo,
+                                    const u64* rep, u64 n, u64* out_hi, u64* out_lo, u64* out_rep, u64* out_start) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (heads[i]) {
+      const u32 s = seg_excl[i];
+      out_hi[s] = hi[i];
+      if (lo) out_lo[s] = lo[i];
+      if (rep) out_rep[s] = rep[i];
+      if (out_start) out_start[s] = i;
+    }
+  }
+}
+
+// histogram of small-integer ids (partition / destination counts)
+__global__ void bincount_kernel(const u32* ids, u64 n, u32 nbins, long long* counts) {
+  extern __shared__ u32 sh[];
+  for (u32 b = threadIdx.x; b < nbins; b += blockDim.x) sh[b] = 0;
+  __syncthreads();
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) atomicAdd(&sh[ids[i]], 1u);
+  __syncthreads();
+  for (u32 b = threadIdx.x; b < nbins; b += blockDim.x)
+    if (sh[b]) atomicAdd((unsigned long long*)&counts[b], (unsigned long long)sh[b]);
+}
+
+}  // namespace mr
+
+using namespace mr;
+
+static inline int grid_n(u64 n, int block, int maxg = 8192) {
+  u64 g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > (u64)maxg) g = maxg;
+  return (int)g;
+}
+
+template <typename T>
+static int scan_impl(const T* in, T* out, u64 n, T* partials, T* total, hipStream_t s) {
+  if (n == 0) return 0;
+  const u64 nt = (n + SC_TILE - 1) / SC_TILE;
+  hipLaunchKernelGGL(scan_reduce_kernel<T>, dim3((unsigned)nt), dim3(SC_THREADS), 0, s, in, n, partials);
+  hipLaunchKernelGGL(scan_partials_kernel<T>, dim3(1), dim3(SC_THREADS), 0, s, partials, nt, total);
+  hipLaunchKernelGGL(scan_apply_kernel<T>, dim3((unsigned)nt), dim3(SC_THREADS), 0, s, in, n, out, partials);
+  return (int)hipGetLastError();
+}
+
+extern "C" {
+
+u64 mr_scan_partials_len(u64 n) { return (n + SC_TILE - 1) / SC_TILE + 1; }
+u64 mr_rs_tiles(u64 n) { return (n + RS_TILE - 1) / RS_TILE; }
+
+// exclusive scans; `total` (device, 1 element, may be null) receives the sum
+int mr_exclusive_scan_u32(const void* in, void* out, u64 n, void* partials, void* total, hipStream_t s) {
+  return scan_impl<u32>((const u32*)in, (u32*)out, n, (u32*)partials, (u32*)total, s);
+}
+int mr_exclusive_scan_i64(const void* in, void* out, u64 n, void* partials, void* total, hipStream_t s) {
+  return scan_impl<long long>((const long long*)in, (long long*)out, n, (long long*)partials, (long long*)total, s);
+}
+
+// One LSD radix pass on 8 bits at `shift` of u64 keys with optional u32
+// payload.  hist_ws must hold 256 * tiles u32; scan_ws mr_scan_partials_len(256*tiles).
+int mr_radix_pass_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
+                       void* hist_ws, void* scan_ws, hipStream_t s) {
+  if (n == 0) return 0;
+  const u32 nt = (u32)((n + RS_TILE - 1) / RS_TILE);
+  hipLaunchKernelGGL(rs_hist_kernel, dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in, n, shift, (u32*)hist_ws,
+                     nt);
+  int e = scan_impl<u32>((const u32*)hist_ws, (u32*)hist_ws, (u64)RS_BINS * nt, (u32*)scan_ws, nullptr, s);
+  if (e) return e;
+  hipLaunchKernelGGL(rs_scatter_kernel<u32>, dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
+                     (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)hist_ws, nt);
+  return (int)hipGetLastError();
+}
+
+int mr_gather_u64(const void* src, const void* idx, void* dst, u64 n, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(gather_u64_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)src, (const u32*)idx,
+                     (u64*)dst, n);
+  return (int)hipGetLastError();
+}
+
+int mr_iota_u32(void* dst, u64 n, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(iota_u32_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (u32*)dst, n);
+  return (int)hipGetLastError();
+}
+
+int mr_segment_heads(const void* hi, const void* lo, u64 n, void* heads, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(segment_heads_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)hi, (const u64*)lo, n,
+                     (u32*)heads);
+  return (int)hipGetLastError();
+}
+
+int mr_segment_fold(const void* seg_excl, const void* heads, const void* vals, u64 n, int op, void* out,
+                    hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(segment_fold_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u32*)seg_excl,
+                     (const u32*)heads, (const long long*)vals, n, op, (long long*)out);
+  return (int)hipGetLastError();
+}
+
+int mr_segment_keys(const void* seg_excl, const void* heads, const void* hi, const void* lo, const void* rep, u64 n,
+                    void* out_hi, void* out_lo, void* out_rep, void* out_start, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(segment_keys_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u32*)seg_excl,
+                     (const u32*)heads, (const u64*)hi, (const u64*)lo, (const u64*)rep, n, (u64*)out_hi,
+                     (u64*)out_lo, (u64*)out_rep, (u64*)out_start);
+  return (int)hipGetLastError();
+}
+
+int mr_bincount(const void* ids, u64 n, u32 nbins, void* counts, hipStream_t s) {
+  if (n == 0) return 0;
+  if (nbins > 16384) return -1;
+  hipLaunchKernelGGL(bincount_kernel, dim3(grid_n(n, 256, 1024)), dim3(256), nbins * sizeof(u32), s,
+                     (const u32*)ids, n, nbins, (long long*)counts);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

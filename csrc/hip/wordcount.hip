@@ -1,0 +1,461 @@
+// wordcount.hip — fused map-side kernels of the MapReduce hot path on gfx950.
+//
+// What this replaces in the reference (/root/reference):
+//   K1 line reading      examples/WordCount/mapfn.lua:4, utils.lua:133-200
+//   K2 tokenizer         examples/WordCount/mapfn.lua:5-7  (line:gmatch("[^%s]+"))
+//   K3 key hashing       tuple.lua:121-140
+//   K4 map-side group-by job.lua:83-97 (result[key][N+1] = value)
+//   K5 combiner          job.lua:92-96, 198-202
+// One launch tokenizes a byte stream, builds exact 128-bit keys, combines them
+// in an LDS hash table per workgroup (the combiner, with no 5000-value
+// threshold) and folds the per-workgroup partials into an HBM hash table.
+//
+// Geometry: 256 threads (4 wave64) per workgroup; each thread owns 16 bytes of
+// a 4 KiB tile (one global_load_dwordx4 per lane, fully coalesced); a
+// workgroup walks `chunk_bytes` of contiguous input tile by tile, so the LDS
+// table amortises the global atomics over ~10^4 tokens.
+#include <hip/hip_runtime.h>
+#include "mr_common.h"
+#include "hashtab.h"
+
+namespace mr {
+
+constexpr int WC_THREADS = 256;
+constexpr int WC_SEG = 16;                      // bytes per thread per tile
+constexpr int WC_TILE = WC_THREADS * WC_SEG;    // 4096 bytes
+constexpr int WC_PAD = 16;                      // front pad; txt[PAD-1] = byte before tile
+constexpr int WC_HALO = 64;                     // bytes of the next tile staged in LDS
+constexpr int WC_LDS_SLOTS = 2048;
+constexpr int WC_LDS_CLAIM_LIMIT = (WC_LDS_SLOTS * 3) / 4;
+constexpr int WC_LDS_PROBES = 24;
+
+struct TxtView {
+  const u8* text;
+  u64 nbytes;
+};
+
+__device__ __forceinline__ u32 load_byte(const TxtView& v, u64 p) {
+  return p < v.nbytes ? (u32)v.text[p] : 32u;
+}
+
+// 56-bit hash part of a long key, read straight from global memory (rare path).
+__device__ u64 long_key_lo_global(const TxtView& v, u64 p0, u64 len) {
+  u64 h = long_hash_init(len);
+  for (u64 w = 0; w < len; w += 8) {
+    u64 word = 0;
+    const u64 n = (len - w) < 8 ? (len - w) : 8;
+    for (u64 j = 0; j < n; ++j) word |= (u64)v.text[p0 + w + j] << (8 * j);
+    h = long_hash_step(h, word);
+  }
+  return long_lo(h);
+}
+
+// Stage tile [tile_base, tile_base + TILE + HALO) into LDS (bytes past nbytes
+// read as whitespace).  txt[PAD-1] must already hold the byte before the tile.
+__device__ __forceinline__ void stage_tile(const TxtView& v, u64 tile_base, u8* txt, bool aligned) {
+  const int t = threadIdx.x;
+  const u64 g = tile_base + (u64)t * WC_SEG;
+  uint4 q;
+  if (aligned && g + WC_SEG <= v.nbytes) {
+    q = *reinterpret_cast<const uint4*>(v.text + g);
+  } else {
+    u32 w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      w[k] = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[k] |= load_byte(v, g + 4 * k + j) << (8 * j);
+    }
+    q = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  *reinterpret_cast<uint4*>(txt + WC_PAD + t * WC_SEG) = q;
+  if (t < WC_HALO / WC_SEG) {
+    const u64 gh = tile_base + WC_TILE + (u64)t * WC_SEG;
+    u32 w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      w[k] = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[k] |= load_byte(v, gh + 4 * k + j) << (8 * j);
+    }
+    *reinterpret_cast<uint4*>(txt + WC_PAD + WC_TILE + t * WC_SEG) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// Walk the tokens that START in this thread's 16-byte segment of the staged
+// tile and that start before `own_end` (global offset).  For each one,
+// fn(hi, lo, gpos, len) is called with the exact 128-bit key.
+template <typename Fn>
+__device__ __forceinline__ void for_each_token(const TxtView& v, u64 tile_base, const u8* txt, u64 own_end, Fn&& fn) {
+  const int t = threadIdx.x;
+  const int li0 = WC_PAD + t * WC_SEG;
+  const uint4 q = *reinterpret_cast<const uint4*>(txt + li0);
+  const u32 words[4] = {q.x, q.y, q.z, q.w};
+  u32 wsmask = 0;  // bit i => byte i is whitespace
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const u32 c = (words[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+    wsmask |= (is_ws(c) ? 1u : 0u) << i;
+  }
+  const u32 prev_ws = is_ws(txt[li0 - 1]) ? 1u : 0u;
+  u32 starts = (~wsmask) & ((wsmask << 1) | prev_ws) & 0xFFFFu;
+  const u64 seg_base = tile_base + (u64)t * WC_SEG;
+  if (seg_base >= own_end) return;
+  const u64 lim_own = own_end - seg_base;  // starts at index >= this are not ours
+  if (lim_own < 16) starts &= (1u << lim_own) - 1u;
+  constexpr int LIM = WC_PAD + WC_TILE + WC_HALO;
+  while (starts) {
+    const int i = __builtin_ctz(starts);
+    starts &= starts - 1;
+    int li = li0 + i;
+    u64 hi = 0, lo = 0;
+    u32 k = 0;
+    u32 c = txt[li];
+    while (true) {
+      if (k < 8) hi |= (u64)c << (56 - 8 * k);
+      else if (k < 15) lo |= (u64)c << (56 - 8 * (k - 8));
+      ++k;
+      ++li;
+      if (li >= LIM) break;
+      c = txt[li];
+      if (is_ws(c)) break;
+    }
+    const u64 gpos = seg_base + i;
+    u64 len = k;
+    if (li >= LIM) {  // token runs past the staged halo: finish it from global memory
+      u64 p = gpos + len;
+      while (p < v.nbytes && !is_ws(v.text[p])) ++p;
+      len = p - gpos;
+    }
+    if (len <= (u64)PACK_MAX) {
+      lo |= len;
+    } else {
+      lo = long_key_lo_global(v, gpos, len);
+    }
+    fn(hi, lo, gpos, len);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LDS combine table (per workgroup).
+struct LdsTab {
+  u32 tag[WC_LDS_SLOTS];
+  u64 hi[WC_LDS_SLOTS];
+  u64 lo[WC_LDS_SLOTS];
+  u64 rep[WC_LDS_SLOTS];
+  u32 cnt[WC_LDS_SLOTS];
+  u32 nclaimed;
+};
+
+__device__ __forceinline__ bool lds_insert(LdsTab& L, u64 hi, u64 lo, u64 rep) {
+  const u64 tag64 = key_tag(hi, lo);
+  const u32 tag = (u32)(tag64 >> 32) | 1u;
+  u32 slot = (u32)tag64 & (WC_LDS_SLOTS - 1);
+  int probes = 0;
+  while (probes < WC_LDS_PROBES) {
+    u32 cur = __hip_atomic_load(&L.tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == 0) {
+      if (__hip_atomic_load(&L.nclaimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (u32)WC_LDS_CLAIM_LIMIT)
+        return false;
+      u32 expected = 0;
+      if (__hip_atomic_compare_exchange_strong(&L.tag[slot], &expected, tag, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        L.hi[slot] = hi;
+        L.rep[slot] = rep;
+        __hip_atomic_fetch_add(&L.cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&L.nclaimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&L.lo[slot], lo, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return true;
+      }
+      cur = expected;
+    }
+    if (cur == tag) {
+      const u64 l = __hip_atomic_load(&L.lo[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (l == 0) continue;  // claimer has not published yet
+      if (l == lo && L.hi[slot] == hi) {
+        __hip_atomic_fetch_add(&L.cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return true;
+      }
+    }
+    slot = (slot + 1) & (WC_LDS_SLOTS - 1);
+    ++probes;
+  }
+  return false;
+}
+
+// Word-count map + combine.  rep_base is added to the in-buffer offset of
+// each key's first occurrence (so several H2D chunks can share one table).
+__global__ void __launch_bounds__(WC_THREADS) wc_map_kernel(TxtView v, u64 chunk_bytes, u64 rep_base, GTab g,
+                                                            int aligned) {
+  __shared__ __attribute__((aligned(16))) u8 txt[WC_PAD + WC_TILE + WC_HALO];
+  __shared__ LdsTab L;
+  const int t = threadIdx.x;
+  const u64 chunk_begin = (u64)blockIdx.x * chunk_bytes;
+  if (chunk_begin >= v.nbytes) return;
+  const u64 chunk_end = min(chunk_begin + chunk_bytes, v.nbytes);
+  for (int s = t; s < WC_LDS_SLOTS; s += WC_THREADS) {
+    L.tag[s] = 0;
+    L.lo[s] = 0;
+    L.cnt[s] = 0;
+  }
+  if (t == 0) {
+    L.nclaimed = 0;
+    txt[WC_PAD - 1] = chunk_begin > 0 ? v.text[chunk_begin - 1] : (u8)' ';
+  }
+  __syncthreads();
+  for (u64 tile_base = chunk_begin; tile_base < chunk_end; tile_base += WC_TILE) {
+    stage_tile(v, tile_base, txt, aligned != 0);
+    __syncthreads();
+    for_each_token(v, tile_base, txt, chunk_end, [&](u64 hi, u64 lo, u64 gpos, u64 len) {
+      const u64 rep = make_rep(rep_base + gpos, len);
+      if (!lds_insert(L, hi, lo, rep)) gtab_insert(g, hi, lo, 1, rep, OP_SUM);
+    });
+    __syncthreads();
+    if (t == 0) txt[WC_PAD - 1] = txt[WC_PAD + WC_TILE - 1];
+    __syncthreads();
+  }
+  // flush the workgroup's partial counts (the combiner output) to HBM
+  for (int s = t; s < WC_LDS_SLOTS; s += WC_THREADS) {
+    if (L.tag[s] != 0) gtab_insert(g, L.hi[s], L.lo[s], (long long)L.cnt[s], L.rep[s], OP_SUM);
+  }
+}
+
+// Per-token emit (no combining): writes one (hi, lo, rep) triple per token,
+// appended with one atomic per wave.  Used by map functions that need every
+// occurrence (inverted index: key + document of each token).
+__global__ void __launch_bounds__(WC_THREADS) tokenize_kernel(TxtView v, u64 chunk_bytes, u64 rep_base, u64* out_hi,
+                                                              u64* out_lo, u64* out_rep, u64 cap,
+                                                              unsigned long long* counter, int aligned) {
+  __shared__ __attribute__((aligned(16))) u8 txt[WC_PAD + WC_TILE + WC_HALO];
+  const int t = threadIdx.x;
+  const u64 chunk_begin = (u64)blockIdx.x * chunk_bytes;
+  if (chunk_begin >= v.nbytes) return;
+  const u64 chunk_end = min(chunk_begin + chunk_bytes, v.nbytes);
+  if (t == 0) txt[WC_PAD - 1] = chunk_begin > 0 ? v.text[chunk_begin - 1] : (u8)' ';
+  __syncthreads();
+  for (u64 tile_base = chunk_begin; tile_base < chunk_end; tile_base += WC_TILE) {
+    stage_tile(v, tile_base, txt, aligned != 0);
+    __syncthreads();
+    for_each_token(v, tile_base, txt, chunk_end, [&](u64 hi, u64 lo, u64 gpos, u64 len) {
+      const unsigned long long idx = atomicAdd(counter, 1ull);
+      if (idx < cap) {
+        out_hi[idx] = hi;
+        out_lo[idx] = lo;
+        out_rep[idx] = make_rep(rep_base + gpos, len);
+      }
+    });
+    __syncthreads();
+    if (t == 0) txt[WC_PAD - 1] = txt[WC_PAD + WC_TILE - 1];
+    __syncthreads();
+  }
+}
+
+// Count tokens only (for sizing tokenize outputs exactly).
+__global__ void __launch_bounds__(WC_THREADS) count_tokens_kernel(TxtView v, u64 chunk_bytes,
+                                                                  unsigned long long* counter, int aligned) {
+  __shared__ __attribute__((aligned(16))) u8 txt[WC_PAD + WC_TILE + WC_HALO];
+  __shared__ u32 block_count;
+  const int t = threadIdx.x;
+  const u64 chunk_begin = (u64)blockIdx.x * chunk_bytes;
+  if (chunk_begin >= v.nbytes) return;
+  const u64 chunk_end = min(chunk_begin + chunk_bytes, v.nbytes);
+  if (t == 0) {
+    block_count = 0;
+    txt[WC_PAD - 1] = chunk_begin > 0 ? v.text[chunk_begin - 1] : (u8)' ';
+  }
+  __syncthreads();
+  u32 mine = 0;
+  for (u64 tile_base = chunk_begin; tile_base < chunk_end; tile_base += WC_TILE) {
+    stage_tile(v, tile_base, txt, aligned != 0);
+    __syncthreads();
+    const int li0 = WC_PAD + t * WC_SEG;
+    const u64 seg_base = tile_base + (u64)t * WC_SEG;
+    if (seg_base < chunk_end) {
+      u32 wsmask = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) wsmask |= (is_ws(txt[li0 + i]) ? 1u : 0u) << i;
+      u32 starts = (~wsmask) & ((wsmask << 1) | (is_ws(txt[li0 - 1]) ? 1u : 0u)) & 0xFFFFu;
+      const u64 lim_own = chunk_end - seg_base;
+      if (lim_own < 16) starts &= (1u << lim_own) - 1u;
+      mine += __builtin_popcount(starts);
+    }
+    __syncthreads();
+    if (t == 0) txt[WC_PAD - 1] = txt[WC_PAD + WC_TILE - 1];
+    __syncthreads();
+  }
+  atomicAdd(&block_count, mine);
+  __syncthreads();
+  if (t == 0) atomicAdd(counter, (unsigned long long)block_count);
+}
+
+// ---------------------------------------------------------------------------
+// Generic (key, value) insert, e.g. received shuffle records or batch emits.
+__global__ void hash_agg_kernel(const u64* hi, const u64* lo, const long long* val, const u64* rep, u64 n, GTab g,
+                               int op, u64 rep_add) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 r = rep ? rep[i] + (rep_add << REP_LEN_BITS) : 0;
+    gtab_insert(g, hi[i], lo[i], val ? val[i] : 1ll, r, op);
+  }
+}
+
+// Compact occupied slots into dense arrays (order is not deterministic; the
+// caller sorts afterwards).  One atomic per wave (ballot + mbcnt).
+__global__ void table_compact_kernel(GTab g, u64 cap, u64* out_hi, u64* out_lo, long long* out_val, u64* out_rep,
+                                     unsigned long long* counter) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  const int lane = threadIdx.x & 63;
+  for (u64 base = (u64)blockIdx.x * blockDim.x; base < cap; base += stride) {
+    const u64 i = base + threadIdx.x;
+    const bool occ = i < cap && g.tag[i] != 0;
+    const unsigned long long m = __ballot(occ);
+    unsigned long long wbase = 0;
+    if (lane == 0 && m) wbase = atomicAdd(counter, (unsigned long long)__popcll(m));
+    wbase = __shfl(wbase, 0);
+    if (occ) {
+      const u64 o = wbase + __popcll(m & ((1ull << lane) - 1ull));
+      out_hi[o] = g.hi[i];
+      out_lo[o] = g.lo[i];
+      out_val[o] = g.val[i];
+      out_rep[o] = g.rep[i];
+    }
+  }
+}
+
+// Key length and (optional) FNV-1 partition of each key.  Long-key bytes are
+// read from `src` at rep offsets.
+__global__ void key_meta_kernel(const u64* hi, const u64* lo, const u64* rep, u64 n, const u8* src, u32 nparts,
+                                u32* out_part, long long* out_len) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 h = hi[i], l = lo[i];
+    u32 f = FNV_OFFSET;
+    u64 len;
+    if (!key_is_long(l)) {
+      len = packed_len(l);
+      for (u32 k = 0; k < len; ++k) f = fnv1_step(f, packed_byte(h, l, k));
+    } else {
+      len = rep_len(rep[i]);
+      const u8* p = src + rep_off(rep[i]);
+      for (u64 k = 0; k < len; ++k) f = fnv1_step(f, p[k]);
+    }
+    if (out_part) out_part[i] = nparts ? f % nparts : f;
+    if (out_len) out_len[i] = (long long)len;
+  }
+}
+
+// Materialise key bytes: dst[off[i] .. off[i]+len) = bytes of key i.
+__global__ void gather_key_bytes_kernel(const u64* hi, const u64* lo, const u64* rep, const long long* off, u64 n,
+                                        const u8* src, u8* dst) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 h = hi[i], l = lo[i];
+    u8* d = dst + off[i];
+    if (!key_is_long(l)) {
+      const u32 len = packed_len(l);
+      for (u32 k = 0; k < len; ++k) d[k] = (u8)packed_byte(h, l, k);
+    } else {
+      const u64 len = rep_len(rep[i]);
+      const u8* p = src + rep_off(rep[i]);
+      for (u64 k = 0; k < len; ++k) d[k] = p[k];
+    }
+  }
+}
+
+}  // namespace mr
+
+// ---------------------------------------------------------------------------
+// C ABI (called from Python through ctypes with torch-owned buffers; no
+// allocation or synchronisation inside, so every launch is graph-capturable).
+using namespace mr;
+
+static inline GTab make_gtab(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap) {
+  GTab g;
+  g.tag = (u64*)tag;
+  g.hi = (u64*)hi;
+  g.lo = (u64*)lo;
+  g.val = (long long*)val;
+  g.rep = (u64*)rep;
+  g.ctrl = (u32*)ctrl;
+  g.mask = cap - 1;
+  return g;
+}
+
+static inline int grid_for(u64 n, int block, int maxg = 8192) {
+  u64 g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > (u64)maxg) g = maxg;
+  return (int)g;
+}
+
+extern "C" {
+
+int mr_wc_map(const void* text, u64 nbytes, u64 chunk_bytes, u64 rep_base, void* tag, void* hi, void* lo, void* val,
+              void* rep, void* ctrl, u64 cap, hipStream_t stream) {
+  if (nbytes == 0) return 0;
+  if (chunk_bytes % WC_TILE) return -1;
+  TxtView v{(const u8*)text, nbytes};
+  const u64 nblocks = (nbytes + chunk_bytes - 1) / chunk_bytes;
+  const int aligned = ((uintptr_t)text & 15) == 0;
+  hipLaunchKernelGGL(wc_map_kernel, dim3((unsigned)nblocks), dim3(WC_THREADS), 0, stream, v, chunk_bytes, rep_base,
+                     make_gtab(tag, hi, lo, val, rep, ctrl, cap), aligned);
+  return (int)hipGetLastError();
+}
+
+int mr_count_tokens(const void* text, u64 nbytes, u64 chunk_bytes, void* counter, hipStream_t stream) {
+  if (nbytes == 0) return 0;
+  if (chunk_bytes % WC_TILE) return -1;
+  TxtView v{(const u8*)text, nbytes};
+  const u64 nblocks = (nbytes + chunk_bytes - 1) / chunk_bytes;
+  const int aligned = ((uintptr_t)text & 15) == 0;
+  hipLaunchKernelGGL(count_tokens_kernel, dim3((unsigned)nblocks), dim3(WC_THREADS), 0, stream, v, chunk_bytes,
+                     (unsigned long long*)counter, aligned);
+  return (int)hipGetLastError();
+}
+
+int mr_tokenize(const void* text, u64 nbytes, u64 chunk_bytes, u64 rep_base, void* out_hi, void* out_lo, void* out_rep,
+                u64 cap, void* counter, hipStream_t stream) {
+  if (nbytes == 0) return 0;
+  if (chunk_bytes % WC_TILE) return -1;
+  TxtView v{(const u8*)text, nbytes};
+  const u64 nblocks = (nbytes + chunk_bytes - 1) / chunk_bytes;
+  const int aligned = ((uintptr_t)text & 15) == 0;
+  hipLaunchKernelGGL(tokenize_kernel, dim3((unsigned)nblocks), dim3(WC_THREADS), 0, stream, v, chunk_bytes, rep_base,
+                     (u64*)out_hi, (u64*)out_lo, (u64*)out_rep, cap, (unsigned long long*)counter, aligned);
+  return (int)hipGetLastError();
+}
+
+int mr_hash_agg(const void* hi, const void* lo, const void* val, const void* rep, u64 n, u64 rep_add, int op, void* tag,
+                void* thi, void* tlo, void* tval, void* trep, void* ctrl, u64 cap, hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(hash_agg_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)hi, (const u64*)lo,
+                     (const long long*)val, (const u64*)rep, n, make_gtab(tag, thi, tlo, tval, trep, ctrl, cap), op,
+                     rep_add);
+  return (int)hipGetLastError();
+}
+
+int mr_table_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, void* out_hi,
+                     void* out_lo, void* out_val, void* out_rep, void* counter, hipStream_t stream) {
+  hipLaunchKernelGGL(table_compact_kernel, dim3(grid_for(cap, 256, 4096)), dim3(256), 0, stream,
+                     make_gtab(tag, hi, lo, val, rep, ctrl, cap), cap, (u64*)out_hi, (u64*)out_lo,
+                     (long long*)out_val, (u64*)out_rep, (unsigned long long*)counter);
+  return (int)hipGetLastError();
+}
+
+int mr_key_meta(const void* hi, const void* lo, const void* rep, u64 n, const void* src, u32 nparts, void* out_part,
+                void* out_len, hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(key_meta_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)hi, (const u64*)lo,
+                     (const u64*)rep, n, (const u8*)src, nparts, (u32*)out_part, (long long*)out_len);
+  return (int)hipGetLastError();
+}
+
+int mr_gather_key_bytes(const void* hi, const void* lo, const void* rep, const void* off, u64 n, const void* src,
+                        void* dst, hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(gather_key_bytes_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)hi,
+                     (const u64*)lo, (const u64*)rep, (const long long*)off, n, (const u8*)src, (u8*)dst);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

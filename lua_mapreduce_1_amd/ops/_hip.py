@@ -1,0 +1,88 @@
+"""ctypes binding of ``_lib/libmrhip.so`` (the gfx950 HIP kernels).
+
+Every entry point takes raw device pointers of torch-owned tensors and the
+current HIP stream; nothing inside allocates or synchronises, so the calls are
+hipGraph-capturable.  On a machine with a GPU the library is mandatory: if it
+cannot be loaded, :func:`lib` raises instead of silently falling back.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be imported first: provides libamdhip64.so.7)
+
+from .. import _build
+
+_LOCK = threading.Lock()
+_LIB = None
+
+_u64 = ctypes.c_uint64
+_i32 = ctypes.c_int
+_u32 = ctypes.c_uint32
+_p = ctypes.c_void_p
+
+_SIGS = {
+    "mr_wc_map": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p],
+    "mr_count_tokens": [_p, _u64, _u64, _p, _p],
+    "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
+    "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p],
+    "mr_table_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
+    "mr_key_meta": [_p, _p, _p, _u64, _p, _u32, _p, _p, _p],
+    "mr_gather_key_bytes": [_p, _p, _p, _p, _u64, _p, _p, _p],
+    "mr_exclusive_scan_u32": [_p, _p, _u64, _p, _p, _p],
+    "mr_exclusive_scan_i64": [_p, _p, _u64, _p, _p, _p],
+    "mr_radix_pass_u32v": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p],
+    "mr_gather_u64": [_p, _p, _p, _u64, _p],
+    "mr_iota_u32": [_p, _u64, _p],
+    "mr_segment_heads": [_p, _p, _u64, _p, _p],
+    "mr_segment_fold": [_p, _p, _p, _u64, _i32, _p, _p],
+    "mr_segment_keys": [_p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p],
+    "mr_bincount": [_p, _u64, _u32, _p, _p],
+    "mr_scan_partials_len": [_u64],
+    "mr_rs_tiles": [_u64],
+}
+_RESTYPE_U64 = {"mr_scan_partials_len", "mr_rs_tiles"}
+
+
+def lib():
+    """Load (building first if needed) the HIP kernel library."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = _build.HIP_LIB
+        if not os.path.exists(path):
+            _build.build_hip()
+        L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = _u64 if name in _RESTYPE_U64 else _i32
+        _LIB = L
+    return _LIB
+
+
+def available() -> bool:
+    return torch.cuda.is_available()
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"HIP kernel launch failed in {what}: error {rc}")
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    check(rc, name)

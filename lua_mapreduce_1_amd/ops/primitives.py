@@ -1,0 +1,352 @@
+"""Device primitives of the MapReduce data plane.
+
+Each function runs the gfx950 HIP kernel for CUDA(HIP) tensors and an
+equivalent NumPy implementation for CPU tensors (tests / non-GPU workers).
+u64 quantities are carried in ``torch.int64`` tensors (bit patterns), u32 in
+``torch.int32``.
+
+Kernel inventory -> function here:
+  K1+K2+K3+K4+K5  wordcount_map (fused tokenize, exact key, LDS combine)
+  K2+K3           tokenize
+  K4 (generic)    HashTable.insert
+  K6/K9           sort_keys (LSD radix sort, 8-bit digits, wave64 ballots)
+  K7              bincount + sort by partition (pack)
+  K8              reduce_by_key (segmented fold)
+  K3 (partition)  key_meta (exact FNV-1 partition, key lengths)
+  K10/K11         gather_key_bytes (materialise key bytes for output)
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import keys as K
+from . import _hip
+
+OPS = {"sum": 0, "min": 1, "max": 2}
+_I64_MAX = (1 << 63) - 1
+_I64_MIN = -(1 << 63)
+
+
+def _op_init(op: str) -> int:
+    return {"sum": 0, "min": _I64_MAX, "max": _I64_MIN}[op]
+
+
+def next_pow2(n: int) -> int:
+    return 1 << max(0, (int(n) - 1).bit_length())
+
+
+def _np(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().numpy()
+
+
+def _u64(t: torch.Tensor) -> np.ndarray:
+    return _np(t).view(np.uint64)
+
+
+def _t64(a: np.ndarray, device="cpu") -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(device)
+
+
+# ---------------------------------------------------------------------------
+class HashTable:
+    """Open-addressing (128-bit key -> int64 value, rep) table.
+
+    GPU: five HBM arrays + control words, filled by ``csrc/hip/hashtab.h``.
+    CPU: pending arrays, reduced with ``np.unique`` at compaction.
+    """
+
+    def __init__(self, capacity: int, device="cpu", op: str = "sum"):
+        self.device = torch.device(device)
+        self.op = op
+        self.cap = next_pow2(max(1024, int(capacity)))
+        if self.device.type == "cuda":
+            d = self.device
+            self.tag = torch.zeros(self.cap, dtype=torch.int64, device=d)
+            self.hi = torch.empty(self.cap, dtype=torch.int64, device=d)
+            self.lo = torch.zeros(self.cap, dtype=torch.int64, device=d)
+            self.val = torch.full((self.cap,), _op_init(op), dtype=torch.int64, device=d)
+            self.rep = torch.zeros(self.cap, dtype=torch.int64, device=d)
+            self.ctrl = torch.zeros(2, dtype=torch.int32, device=d)
+        else:
+            self._pending: list[tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]] = []
+
+    @property
+    def is_cuda(self) -> bool:
+        return self.device.type == "cuda"
+
+    def reset(self) -> None:
+        if self.is_cuda:
+            self.tag.zero_()
+            self.lo.zero_()
+            self.val.fill_(_op_init(self.op))
+            self.ctrl.zero_()
+        else:
+            self._pending = []
+
+    def _gtab(self):
+        return (_hip.ptr(self.tag), _hip.ptr(self.hi), _hip.ptr(self.lo), _hip.ptr(self.val),
+                _hip.ptr(self.rep), _hip.ptr(self.ctrl))
+
+    # -- inserts -------------------------------------------------------------
+    def insert(self, hi: torch.Tensor, lo: torch.Tensor, val: torch.Tensor | None = None,
+               rep: torch.Tensor | None = None, rep_add: int = 0) -> None:
+        n = hi.numel()
+        if n == 0:
+            return
+        if self.is_cuda:
+            _hip.call("mr_hash_agg", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), n, rep_add,
+                      OPS[self.op], *self._gtab(), self.cap, _hip.stream(self.device))
+        else:
+            v = _np(val).astype(np.int64) if val is not None else np.ones(n, np.int64)
+            r = _u64(rep).copy() if rep is not None else np.zeros(n, np.uint64)
+            if rep is not None and rep_add:
+                r = r + np.uint64(rep_add << K.REP_LEN_BITS)
+            self._pending.append((_u64(hi).copy(), _u64(lo).copy(), v, r))
+
+    def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, chunk_bytes: int = 64 * 1024) -> None:
+        """Fused tokenize + exact key + combine of every whitespace token (value 1)."""
+        nbytes = text.numel()
+        if nbytes == 0:
+            return
+        if self.is_cuda:
+            assert text.dtype == torch.uint8 and text.is_contiguous()
+            _hip.call("mr_wc_map", _hip.ptr(text), nbytes, chunk_bytes, rep_base, *self._gtab(), self.cap,
+                      _hip.stream(self.device))
+        else:
+            buf = _np(text)
+            starts, lens = K.token_spans(buf)
+            hi, lo = K.span_keys(buf, starts, lens)
+            rep = ((starts.astype(np.uint64) + np.uint64(rep_base)) << np.uint64(K.REP_LEN_BITS)) | \
+                np.minimum(lens, K.REP_LEN_MASK).astype(np.uint64)
+            self._pending.append((hi, lo, np.ones(hi.size, np.int64), rep))
+
+    # -- state ---------------------------------------------------------------
+    def stats(self) -> tuple[int, bool]:
+        """(occupied slots, overflowed).  Synchronises on GPU."""
+        if self.is_cuda:
+            c = self.ctrl.cpu().tolist()
+            return int(c[0]), bool(c[1])
+        return sum(p[0].size for p in self._pending), False
+
+    def compact(self):
+        """Dense (hi, lo, val, rep) of all occupied slots (unsorted on GPU)."""
+        if self.is_cuda:
+            n, ovf = self.stats()
+            if ovf:
+                raise OverflowError("hash table overflow")
+            d = self.device
+            out = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(4)]
+            counter = torch.zeros(1, dtype=torch.int64, device=d)
+            _hip.call("mr_table_compact", *self._gtab(), self.cap, *[_hip.ptr(o) for o in out],
+                      _hip.ptr(counter), _hip.stream(d))
+            return tuple(out)
+        if not self._pending:
+            z = torch.zeros(0, dtype=torch.int64)
+            return z, z.clone(), z.clone(), z.clone()
+        hi = np.concatenate([p[0] for p in self._pending])
+        lo = np.concatenate([p[1] for p in self._pending])
+        v = np.concatenate([p[2] for p in self._pending])
+        r = np.concatenate([p[3] for p in self._pending])
+        keys = np.empty(hi.size, dtype=[("hi", np.uint64), ("lo", np.uint64)])
+        keys["hi"], keys["lo"] = hi, lo
+        uk, first, inv = np.unique(keys, return_index=True, return_inverse=True)
+        if self.op == "sum":
+            agg = np.zeros(uk.size, np.int64)
+            np.add.at(agg, inv, v)
+        elif self.op == "min":
+            agg = np.full(uk.size, _I64_MAX, np.int64)
+            np.minimum.at(agg, inv, v)
+        else:
+            agg = np.full(uk.size, _I64_MIN, np.int64)
+            np.maximum.at(agg, inv, v)
+        return (_t64(uk["hi"].copy()), _t64(uk["lo"].copy()), torch.from_numpy(agg), _t64(r[first]))
+
+
+# ---------------------------------------------------------------------------
+def tokenize(text: torch.Tensor, rep_base: int = 0, chunk_bytes: int = 64 * 1024):
+    """Per-token (hi, lo, rep) in text order on CPU, arbitrary order on GPU."""
+    nbytes = text.numel()
+    if text.is_cuda:
+        d = text.device
+        counter = torch.zeros(1, dtype=torch.int64, device=d)
+        _hip.call("mr_count_tokens", _hip.ptr(text), nbytes, chunk_bytes, _hip.ptr(counter), _hip.stream(d))
+        n = int(counter.item())
+        out = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(3)]
+        counter.zero_()
+        _hip.call("mr_tokenize", _hip.ptr(text), nbytes, chunk_bytes, rep_base, *[_hip.ptr(o) for o in out], n,
+                  _hip.ptr(counter), _hip.stream(d))
+        return tuple(out)
+    buf = _np(text)
+    starts, lens = K.token_spans(buf)
+    hi, lo = K.span_keys(buf, starts, lens)
+    rep = ((starts.astype(np.uint64) + np.uint64(rep_base)) << np.uint64(K.REP_LEN_BITS)) | \
+        np.minimum(lens, K.REP_LEN_MASK).astype(np.uint64)
+    return _t64(hi), _t64(lo), _t64(rep)
+
+
+def key_meta(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.Tensor | None,
+             nparts: int = 0, want_part: bool = True, want_len: bool = True):
+    """(partition id int32 | None, key length int64 | None).
+
+    Partition = exact uint32 FNV-1 of the key bytes mod ``nparts`` (raw hash
+    when nparts == 0).  Long-key bytes are read from ``src`` at rep offsets.
+    """
+    n = hi.numel()
+    if hi.is_cuda:
+        d = hi.device
+        part = torch.empty(n, dtype=torch.int32, device=d) if want_part else None
+        ln = torch.empty(n, dtype=torch.int64, device=d) if want_len else None
+        srcp = _hip.ptr(src) if src is not None else None
+        _hip.call("mr_key_meta", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), n, srcp, nparts, _hip.ptr(part),
+                  _hip.ptr(ln), _hip.stream(d))
+        return part, ln
+    b = key_bytes_list(hi, lo, rep, src)
+    part = None
+    if want_part:
+        h = np.array([K.fnv1(x) for x in b], dtype=np.uint64)
+        part = torch.from_numpy((h % np.uint64(nparts) if nparts else h).astype(np.uint32).view(np.int32))
+    ln = torch.tensor([len(x) for x in b], dtype=torch.int64) if want_len else None
+    return part, ln
+
+
+def key_bytes_list(hi, lo, rep, src) -> list[bytes]:
+    """Host list of key byte strings (CPU helper; also used after D2H)."""
+    h = _u64(hi)
+    lw = _u64(lo)
+    r = _u64(rep) if rep is not None else None
+    s = _np(src) if src is not None else None
+    out = []
+    for i in range(h.size):
+        l_ = int(lw[i])
+        if (l_ & 0xFF) != K.LONG_MARK:
+            out.append(K.unpack_key(int(h[i]), l_))
+        else:
+            rr = int(r[i])
+            off, ln = rr >> K.REP_LEN_BITS, rr & K.REP_LEN_MASK
+            out.append(bytes(s[off:off + ln]))
+    return out
+
+
+def exclusive_scan(x: torch.Tensor):
+    """Exclusive prefix sum of an int32/int64 tensor -> (out, total)."""
+    n = x.numel()
+    if x.is_cuda:
+        d = x.device
+        out = torch.empty_like(x)
+        lib = _hip.lib()
+        parts = torch.empty(int(lib.mr_scan_partials_len(max(n, 1))), dtype=x.dtype, device=d)
+        total = torch.zeros(1, dtype=x.dtype, device=d)
+        name = "mr_exclusive_scan_u32" if x.dtype == torch.int32 else "mr_exclusive_scan_i64"
+        _hip.call(name, _hip.ptr(x), _hip.ptr(out), n, _hip.ptr(parts), _hip.ptr(total), _hip.stream(d))
+        return out, total
+    c = torch.cumsum(x, 0)
+    tot = c[-1:].clone() if n else torch.zeros(1, dtype=x.dtype)
+    return (c - x).to(x.dtype), tot
+
+
+def gather_key_bytes(hi, lo, rep, src, lengths: torch.Tensor | None = None):
+    """Materialise key bytes: (offsets int64[n+1], blob uint8)."""
+    n = hi.numel()
+    if lengths is None:
+        _, lengths = key_meta(hi, lo, rep, src, want_part=False)
+    off, total = exclusive_scan(lengths)
+    if hi.is_cuda:
+        d = hi.device
+        nb = int(total.item())
+        blob = torch.empty(nb, dtype=torch.uint8, device=d)
+        srcp = _hip.ptr(src) if src is not None else None
+        _hip.call("mr_gather_key_bytes", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), _hip.ptr(off), n, srcp,
+                  _hip.ptr(blob), _hip.stream(d))
+        return torch.cat([off, total]), blob
+    b = key_bytes_list(hi, lo, rep, src)
+    blob = torch.frombuffer(bytearray(b"".join(b)), dtype=torch.uint8) if b else torch.zeros(0, dtype=torch.uint8)
+    return torch.cat([off, total]), blob
+
+
+# ---------------------------------------------------------------------------
+def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None) -> torch.Tensor:
+    """Stable permutation sorting rows by unsigned multi-word keys.
+
+    ``words[0]`` is the most significant u64 word.  ``bits[j]`` limits the
+    number of low bits of word j that participate (e.g. partition ids).
+    Returns int32 (GPU) / int64 (CPU) permutation.
+    """
+    n = words[0].numel()
+    bits = bits or [64] * len(words)
+    if words[0].is_cuda:
+        d = words[0].device
+        if n == 0:
+            return torch.zeros(0, dtype=torch.int32, device=d)
+        lib = _hip.lib()
+        s = _hip.stream(d)
+        tiles = int(lib.mr_rs_tiles(n))
+        hist = torch.empty(256 * tiles, dtype=torch.int32, device=d)
+        scan_ws = torch.empty(int(lib.mr_scan_partials_len(256 * tiles)), dtype=torch.int32, device=d)
+        perm = torch.empty(n, dtype=torch.int32, device=d)
+        _hip.call("mr_iota_u32", _hip.ptr(perm), n, s)
+        perm2 = torch.empty_like(perm)
+        k1 = torch.empty(n, dtype=torch.int64, device=d)
+        k2 = torch.empty_like(k1)
+        first = True
+        for w, nb in zip(reversed(words), reversed(bits)):
+            if first:
+                k1.copy_(w)
+                first = False
+            else:
+                _hip.call("mr_gather_u64", _hip.ptr(w), _hip.ptr(perm), _hip.ptr(k1), n, s)
+            for shift in range(0, nb, 8):
+                _hip.call("mr_radix_pass_u32v", _hip.ptr(k1), _hip.ptr(perm), _hip.ptr(k2), _hip.ptr(perm2), n,
+                          shift, _hip.ptr(hist), _hip.ptr(scan_ws), s)
+                k1, k2 = k2, k1
+                perm, perm2 = perm2, perm
+        return perm
+    cols = [_u64(w) for w in words]
+    for j, nb in enumerate(bits):
+        if nb < 64:
+            cols[j] = cols[j] & np.uint64((1 << nb) - 1)
+    return torch.from_numpy(np.lexsort(tuple(reversed(cols))).astype(np.int64))
+
+
+def bincount(ids: torch.Tensor, nbins: int) -> torch.Tensor:
+    if ids.is_cuda:
+        d = ids.device
+        out = torch.zeros(nbins, dtype=torch.int64, device=d)
+        _hip.call("mr_bincount", _hip.ptr(ids), ids.numel(), nbins, _hip.ptr(out), _hip.stream(d))
+        return out
+    return torch.bincount(ids.long(), minlength=nbins)[:nbins]
+
+
+def reduce_by_key(hi: torch.Tensor, lo: torch.Tensor | None, vals: torch.Tensor | None, op: str = "sum",
+                  rep: torch.Tensor | None = None):
+    """Fold runs of equal (hi, lo) in SORTED input -> (uhi, ulo, uval, urep, start)."""
+    n = hi.numel()
+    if hi.is_cuda:
+        d = hi.device
+        s = _hip.stream(d)
+        heads = torch.empty(n, dtype=torch.int32, device=d)
+        _hip.call("mr_segment_heads", _hip.ptr(hi), _hip.ptr(lo), n, _hip.ptr(heads), s)
+        seg, total = exclusive_scan(heads)
+        m = int(total.item()) if n else 0
+        uhi = torch.empty(m, dtype=torch.int64, device=d)
+        ulo = torch.empty(m, dtype=torch.int64, device=d) if lo is not None else None
+        urep = torch.empty(m, dtype=torch.int64, device=d) if rep is not None else None
+        start = torch.empty(m, dtype=torch.int64, device=d)
+        uval = torch.full((m,), _op_init(op), dtype=torch.int64, device=d)
+        _hip.call("mr_segment_keys", _hip.ptr(seg), _hip.ptr(heads), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), n,
+                  _hip.ptr(uhi), _hip.ptr(ulo), _hip.ptr(urep), _hip.ptr(start), s)
+        _hip.call("mr_segment_fold", _hip.ptr(seg), _hip.ptr(heads), _hip.ptr(vals), n, OPS[op], _hip.ptr(uval), s)
+        return uhi, ulo, uval, urep, start
+    h = _u64(hi)
+    lw = _u64(lo) if lo is not None else np.zeros_like(h)
+    if n == 0:
+        z = torch.zeros(0, dtype=torch.int64)
+        return z, (z.clone() if lo is not None else None), z.clone(), (z.clone() if rep is not None else None), z
+    heads = np.ones(n, bool)
+    heads[1:] = (h[1:] != h[:-1]) | (lw[1:] != lw[:-1])
+    start = np.flatnonzero(heads)
+    v = _np(vals).astype(np.int64) if vals is not None else np.ones(n, np.int64)
+    ufunc = {"sum": np.add, "min": np.minimum, "max": np.maximum}[op]
+    uval = ufunc.reduceat(v, start)
+    return (_t64(h[start]), _t64(lw[start]) if lo is not None else None, torch.from_numpy(uval),
+            _t64(_u64(rep)[start]) if rep is not None else None, torch.from_numpy(start.astype(np.int64)))
