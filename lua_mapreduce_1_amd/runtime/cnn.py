@@ -1,0 +1,210 @@
+"""Connection layer to the coordinator (reference: mapreduce/cnn.lua).
+
+``cnn(connection_string, dbname, auth_table)`` exposes the same surface as the
+reference: ``connect``, ``gridfs`` (blob store), ``grid_file_builder``,
+``get_dbname``, the error channel (``insert_error``/``get_errors``/
+``remove_errors``) and batched inserts (``annotate_insert`` /
+``flush_pending_inserts`` with per-document callbacks, flushed at
+``MAX_PENDING_INSERTS``).
+"""
+from __future__ import annotations
+
+import json
+import re
+from typing import Callable, Iterator
+
+from .. import utils
+from .coordinator import Client, decode_jobs
+
+
+class GridFS:
+    """Blob store in the coordinator (the GridFS replacement)."""
+
+    def __init__(self, client: Client, dbname: str):
+        self.c = client
+        self.db = dbname
+
+    def store_data(self, data: bytes, filename: str) -> bool:
+        self.c.request("BLOB_PUT", self.db, filename, bytes(data))
+        return True
+
+    def get(self, filename: str) -> bytes | None:
+        st, f = self.c.request("BLOB_GET", self.db, filename)
+        return f[0] if st == 0 else None
+
+    find_file = get
+
+    def list(self, match: dict | str | None = None) -> list[dict]:
+        """Files whose name matches a regex (``{"filename": {"$regex": r}}``
+        or a plain regex string); all files when ``match`` is None."""
+        _, f = self.c.request("BLOB_LIST", self.db, "")
+        names = [(f[i].decode("utf-8", "surrogateescape"), int(f[i + 1])) for i in range(0, len(f), 2)]
+        rx = _regex_of(match)
+        return [{"filename": n, "length": sz} for n, sz in names if rx is None or rx.search(n)]
+
+    def remove_file(self, filename: str) -> bool:
+        _, f = self.c.request("BLOB_DEL", self.db, filename)
+        return int(f[0]) > 0
+
+    def lines(self, filename: str) -> Iterator[bytes]:
+        data = self.get(filename) or b""
+        for line in data.split(b"\n"):
+            if line:
+                yield line
+
+
+def _regex_of(match):
+    if match is None:
+        return None
+    if isinstance(match, dict):
+        match = match["filename"]["$regex"]
+    return re.compile(match)
+
+
+class GridFileBuilder:
+    def __init__(self, gridfs: GridFS):
+        self.fs = gridfs
+        self.parts: list[bytes] = []
+
+    def append(self, data) -> bool:
+        self.parts.append(data if isinstance(data, bytes) else str(data).encode("utf-8", "surrogateescape"))
+        return True
+
+    write = append
+
+    def build(self, filename: str) -> bool:
+        self.fs.store_data(b"".join(self.parts), filename)
+        self.parts = []
+        return True
+
+
+class cnn:  # noqa: N801
+    _VERSION = "0.2"
+    _NAME = "cnn"
+
+    def __init__(self, connection_string: str | None = None, dbname: str = "tmp", auth_table=None):
+        self.connection_string = connection_string
+        self.dbname = dbname
+        self.gridfs_dbname = dbname
+        self.auth_table = auth_table
+        self.db: Client | None = None
+        self.pending_inserts: dict[str, list] = {}
+        self.pending_callbacks: dict[str, list] = {}
+
+    def connect(self) -> Client:
+        if self.db is None:
+            self.db = Client(self.connection_string)
+        return self.db
+
+    def gridfs(self) -> GridFS:
+        return GridFS(self.connect(), self.gridfs_dbname)
+
+    def grid_file_builder(self) -> GridFileBuilder:
+        return GridFileBuilder(self.gridfs())
+
+    def get_dbname(self) -> str:
+        return self.dbname
+
+    # -- error channel -------------------------------------------------------
+    def insert_error(self, who: str, msg: str) -> None:
+        self.connect().request("ERR_INSERT", self.dbname, who, msg)
+
+    def get_errors(self) -> list[dict]:
+        """Take (and remove) all pending error documents."""
+        _, f = self.connect().request("ERR_TAKE", self.dbname)
+        return [{"_id": i // 2, "worker": f[i].decode(), "msg": f[i + 1].decode("utf-8", "replace")}
+                for i in range(0, len(f), 2)]
+
+    def remove_errors(self, ids) -> None:
+        # errors are removed atomically by get_errors (ERR_TAKE)
+        return None
+
+    # -- batched inserts -------------------------------------------------------
+    def annotate_insert(self, ns: str, tbl: dict, callback: Callable | None = None) -> None:
+        self.pending_inserts.setdefault(ns, []).append(tbl)
+        cbs = self.pending_callbacks.setdefault(ns, [])
+        if callback:
+            cbs.append(callback)
+        if len(self.pending_inserts[ns]) >= utils.MAX_PENDING_INSERTS:
+            self._insert_batch(ns, self.pending_inserts[ns])
+            for i, f in enumerate(self.pending_callbacks[ns]):
+                f(self.pending_inserts[ns][i])
+            self.pending_inserts[ns] = []
+            self.pending_callbacks[ns] = []
+
+    def flush_pending_inserts(self, max_pending: int = 0) -> None:
+        for ns, tbl in list(self.pending_inserts.items()):
+            if len(tbl) > max_pending:
+                self._insert_batch(ns, tbl)
+                for i, f in enumerate(self.pending_callbacks.get(ns, [])):
+                    f(tbl[i])
+        self.pending_inserts = {}
+        self.pending_callbacks = {}
+
+    def _insert_batch(self, ns: str, docs: list[dict]) -> None:
+        c = self.connect()
+        for d in docs:
+            c.request("JOB_INSERT", self.dbname, ns, d["_id"], json.dumps(d.get("value")),
+                      d.get("creation_time", utils.time()))
+
+    # -- job collections (the <db>.map_jobs / <db>.red_jobs namespaces) -------
+    def jobs(self, ns: str) -> "JobCollection":
+        return JobCollection(self.connect(), self.dbname, ns)
+
+
+def status_mask(*statuses: int) -> int:
+    m = 0
+    for s in statuses:
+        m |= 1 << s
+    return m
+
+
+class JobCollection:
+    def __init__(self, client: Client, dbname: str, ns: str):
+        self.c, self.db, self.ns = client, dbname, ns
+
+    def insert(self, job: dict) -> bool:
+        st, _ = self.c.request("JOB_INSERT", self.db, self.ns, job["_id"], json.dumps(job["value"]),
+                               job.get("creation_time", utils.time()))
+        return st == 0
+
+    def remove_status(self, *statuses: int) -> int:
+        return int(self.c.request("JOB_REMOVE_STATUS", self.db, self.ns, status_mask(*statuses))[1][0])
+
+    def fail_broken(self, max_reps: int) -> int:
+        return int(self.c.request("JOB_FAIL_BROKEN", self.db, self.ns, max_reps)[1][0])
+
+    def count(self, *statuses: int) -> int:
+        return int(self.c.request("JOB_COUNT", self.db, self.ns, status_mask(*statuses))[1][0])
+
+    def claim(self, worker: str, tmpname: str, t: float, statuses=(0, 2), only_ids=None) -> dict | None:
+        ids = list(only_ids) if only_ids else []
+        if only_ids is not None and not ids:
+            return None
+        st, f = self.c.request("JOB_CLAIM", self.db, self.ns, worker, tmpname, t, status_mask(*statuses), *ids)
+        return decode_jobs(f)[0] if st == 0 else None
+
+    def update(self, job_id: str, guard_tmpname: str = "", **fields) -> dict | None:
+        args = []
+        for k, v in fields.items():
+            args += [k, v]
+        st, f = self.c.request("JOB_UPDATE", self.db, self.ns, job_id, guard_tmpname, *args)
+        return decode_jobs(f)[0] if st == 0 else None
+
+    def get(self, job_id: str) -> dict | None:
+        st, f = self.c.request("JOB_GET", self.db, self.ns, job_id)
+        return decode_jobs(f)[0] if st == 0 else None
+
+    def list(self) -> list[dict]:
+        return decode_jobs(self.c.request("JOB_LIST", self.db, self.ns)[1])
+
+    def drop(self) -> None:
+        self.c.request("JOB_DROP", self.db, self.ns)
+
+    def stats(self) -> dict:
+        f = self.c.request("JOB_STATS", self.db, self.ns)[1]
+        return {"sum_cpu_time": float(f[0]), "sum_real_time": float(f[1]), "real_time": float(f[2]),
+                "counts": [int(x) for x in f[3:9]]}
+
+    def expire(self, now: float, lease: float) -> int:
+        return int(self.c.request("JOB_EXPIRE", self.db, self.ns, now, lease)[1][0])

@@ -1,0 +1,96 @@
+"""Data-only codecs for intermediate (``map_results.P<p>.M<m>``) and result
+(``result.P<NN>``) files.
+
+The reference writes executable Lua lines ``return k,{v1,...}`` and reads
+them back with ``load(line)()`` (job.lua:212-214, utils.lua:222-224,
+server.lua:380-382) — code execution on the data path.  Two data-only formats
+replace it:
+
+* ``MRK1`` — msgpack stream of ``[key, [values...]]`` records in key order
+  (host plane: arbitrary Python keys/values from user map/reduce functions).
+* ``MRC1`` — columnar device format: u64 key words (hi, lo), int64 values and
+  the key bytes (offsets + blob), straight from HBM buffers (device plane).
+"""
+from __future__ import annotations
+
+import struct
+from typing import Iterable, Iterator
+
+import msgpack
+import numpy as np
+
+MAGIC_REC = b"MRK1"
+MAGIC_COL = b"MRC1"
+
+
+def _default(o):
+    if isinstance(o, (set, frozenset)):
+        return list(o)
+    if isinstance(o, np.integer):
+        return int(o)
+    if isinstance(o, np.floating):
+        return float(o)
+    raise TypeError(f"cannot serialize {type(o).__name__}")
+
+
+def encode_records(records: Iterable[tuple]) -> bytes:
+    pk = msgpack.Packer(use_bin_type=True, default=_default)
+    out = [MAGIC_REC]
+    for k, vals in records:
+        out.append(pk.pack([k, list(vals)]))
+    return b"".join(out)
+
+
+def _fix(x):
+    # msgpack arrays decode as tuples (use_list=False): keep tuples for keys
+    # (hashable, like the reference's interned tuples) and values.
+    return x
+
+
+def decode_records(data: bytes) -> Iterator[tuple]:
+    if not data:
+        return iter(())
+    if data[:4] == MAGIC_COL:
+        return iter_columnar(decode_columnar(data))
+    if data[:4] != MAGIC_REC:
+        raise ValueError("unknown intermediate file format")
+    up = msgpack.Unpacker(use_list=False, raw=False, strict_map_key=False, unicode_errors="surrogateescape")
+    up.feed(memoryview(data)[4:])
+    return ((k, list(v)) for k, v in up)
+
+
+# ---------------------------------------------------------------------------
+def encode_columnar(hi: np.ndarray, lo: np.ndarray, val: np.ndarray, key_off: np.ndarray,
+                    key_blob: np.ndarray) -> bytes:
+    n = int(hi.size)
+    nb = int(key_blob.size)
+    head = MAGIC_COL + struct.pack("<QQ", n, nb)
+    return b"".join([head, np.ascontiguousarray(hi, np.uint64).tobytes(), np.ascontiguousarray(lo, np.uint64).tobytes(),
+                     np.ascontiguousarray(val, np.int64).tobytes(), np.ascontiguousarray(key_off, np.int64).tobytes(),
+                     np.ascontiguousarray(key_blob, np.uint8).tobytes()])
+
+
+def decode_columnar(data: bytes) -> dict:
+    if data[:4] != MAGIC_COL:
+        raise ValueError("not a columnar file")
+    n, nb = struct.unpack("<QQ", data[4:20])
+    p = 20
+    out = {}
+    for name, dt, cnt in (("hi", np.uint64, n), ("lo", np.uint64, n), ("val", np.int64, n),
+                          ("key_off", np.int64, n + 1), ("key_blob", np.uint8, nb)):
+        sz = np.dtype(dt).itemsize * cnt
+        out[name] = np.frombuffer(data, dtype=dt, count=cnt, offset=p)
+        p += sz
+    return out
+
+
+def key_str(b: bytes) -> str:
+    return b.decode("utf-8", "surrogateescape")
+
+
+def iter_columnar(cols: dict) -> Iterator[tuple]:
+    off = cols["key_off"]
+    blob = cols["key_blob"].tobytes()
+    val = cols["val"]
+    for i in range(int(cols["hi"].size)):
+        yield key_str(blob[off[i]:off[i + 1]]), [int(val[i])]

@@ -1,0 +1,305 @@
+"""Map / reduce job execution on a worker (reference: mapreduce/job.lua).
+
+Host plane (any Python mapfn/reducefn): ``emit(k, v)`` groups values per key
+(keys/values go through ``tuple()`` like job.lua:84), the combiner — taken
+from the *reducefn* module's ``combinerfn`` as in task.lua:325 — fires when a
+key exceeds ``MAX_MAP_RESULT`` values and again per key at the end; keys are
+written sorted, one ``map_results.P<p>.M<m>`` file per partition.  Reduce
+merges the partition's files (heap k-way merge), calls ``reducefn`` (skipping
+singleton lists when the module declares all three ACI flags, job.lua:264-274)
+and writes ``result.P<NN>``.
+
+Device plane (module defines ``device_mapfn`` / ``device_reduce``): see
+:mod:`.device` — the same files, in the columnar ``MRC1`` format.
+"""
+from __future__ import annotations
+
+import os
+import re
+import time as _time
+
+import numpy as np
+import torch
+
+from .. import utils
+from ..utils import STATUS, TASK_STATUS
+from ..utils.tuple import tuple as tuple_
+from . import codec, device as dev, fs as fsmod, modules
+
+_VERSION = "0.4"
+INDEX_PREFIX = "__idx__"
+INDEX_SEP = "\x1f"
+_NAME = "job"
+
+_cache: dict = {}
+
+
+def cached(func):
+    """Memoise a 1-argument function (job.lua:42-55; used for partitionfn)."""
+    local = _cache.setdefault(func, {})
+
+    def f(key):
+        try:
+            return local[key]
+        except KeyError:
+            r = func(key)
+            local[key] = r
+            return r
+        except TypeError:  # unhashable key
+            return func(key)
+    return f
+
+
+def reset_cache() -> None:
+    _cache.clear()
+    modules.reset()
+
+
+def _use_device(task_tbl: dict | None, mod_map) -> bool:
+    want = (task_tbl or {}).get("device", "auto")
+    if want in (False, "never", "host"):
+        return False
+    return modules.field(mod_map, "device_mapfn") is not None
+
+
+class job:  # noqa: N801
+    def __init__(self, cnn, job_tbl: dict, task_status, fname, init_args, jobs, results_ns,
+                 not_executable: bool = False, combiner=None, partitioner=None, storage="gridfs", path="/tmp",
+                 task_tbl: dict | None = None):
+        self.cnn = cnn
+        self.job_tbl = job_tbl
+        self.jobs = jobs
+        self.results_ns = results_ns
+        self.t = utils.time()
+        self.written = False
+        self.task_tbl = task_tbl or {}
+        self.storage, self.path = storage, path
+        self.init_args = init_args
+        if task_status == TASK_STATUS.MAP:
+            func = "mapfn"
+        elif task_status == TASK_STATUS.REDUCE:
+            func = "reducefn"
+        else:
+            raise ValueError(f"Incorrect task_status: {task_status}")
+        self.func = func
+        self.fn = None
+        if not not_executable:
+            self.module = modules.load(fname)
+            modules.init_once(self.module, init_args)
+            if func == "mapfn":
+                self.fn = self._prepare_map(combiner, partitioner)
+            else:
+                self.fn = self._prepare_reduce()
+
+    # -- accessors ---------------------------------------------------------------
+    def execute(self):
+        if self.fn is None:
+            raise RuntimeError("Forbidden execution of jobs here")
+        return self.fn()
+
+    def get_id(self):
+        return self.job_tbl["_id"]
+
+    def get_pair(self):
+        return self.job_tbl["_id"], self.job_tbl["value"]
+
+    def status_string(self):
+        return self.get_id()
+
+    def get_results_ns(self):
+        return self.results_ns
+
+    def heartbeat(self) -> None:
+        self.jobs.update(self.get_id(), self.job_tbl.get("tmpname", ""), heartbeat=utils.time())
+
+    def mark_as_finished(self) -> None:
+        self.jobs.update(self.get_id(), self.job_tbl.get("tmpname", ""), status=STATUS.FINISHED,
+                         finished_time=utils.time())
+
+    def mark_as_written(self, cpu_time: float) -> None:
+        self.written = True
+        now = utils.time()
+        self.jobs.update(self.get_id(), self.job_tbl.get("tmpname", ""), status=STATUS.WRITTEN, written_time=now,
+                         cpu_time=cpu_time, real_time=now - self.t)
+
+    def mark_as_broken(self) -> None:
+        if not self.written:
+            self.jobs.update(self.get_id(), "", status=STATUS.BROKEN, broken_time=utils.time(), inc_repetitions=1)
+
+    # -- map -----------------------------------------------------------------------
+    def _prepare_map(self, combiner_fname, partitioner_fname):
+        pmod = modules.load(partitioner_fname)
+        modules.init_once(pmod, self.init_args)
+        partitioner = cached(modules.field(pmod, "partitionfn"))
+        cmod = modules.load(combiner_fname) if combiner_fname else None
+        if cmod is not None:
+            modules.init_once(cmod, self.init_args)
+        combiner = modules.field(cmod, "combinerfn") if cmod is not None else None
+        if _use_device(self.task_tbl, self.module):
+            return lambda: self._run_device_map(pmod, cmod)
+        g = modules.field(self.module, "mapfn")
+        map_key, map_value = self.get_pair()
+
+        def run():
+            clock1 = _time.process_time()
+            result: dict = {}
+            max_res = utils.MAX_MAP_RESULT
+
+            def combine(key, values):
+                out = []
+                combiner(key, values, out.append)
+                values[:] = [tuple_(v) for v in out]
+
+            def emit(key, value):
+                key, value = tuple_(key), tuple_(value)
+                lst = result.get(key)
+                if lst is None:
+                    result[key] = lst = []
+                lst.append(value)
+                if combiner is not None and len(lst) > max_res:
+                    combine(key, lst)
+
+            g(map_key, map_value, emit)
+            self.mark_as_finished()
+            fs, make_builder, _ = fsmod.router(self.cnn, None, self.storage, self.path)
+            parts: dict[int, list] = {}
+            for key in utils.keys_sorted(result):
+                values = result[key]
+                if len(values) > 1 and combiner is not None:
+                    combine(key, values)
+                p = partitioner(key)
+                try:
+                    pi = int(p)
+                except (TypeError, ValueError):
+                    raise ValueError("Partition key must be a number")
+                if pi != p:
+                    raise ValueError("Partition key must be an integer")
+                parts.setdefault(pi, []).append((key, values))
+            for pi, recs in parts.items():
+                name = f"{self.path}/{self.results_ns}.P{pi}.M{map_key}"
+                b = make_builder()
+                b.append(codec.encode_records(recs))
+                fs.remove_file(name)
+                b.build(name)
+                self._register_output(name)
+            elapsed = _time.process_time() - clock1
+            self.mark_as_written(elapsed)
+            return elapsed
+        return run
+
+    def _register_output(self, name: str) -> None:
+        """Index the file in the coordinator so the server can find partitions
+        whatever the storage (sshfs files are only on the mapper's host)."""
+        self.cnn.gridfs().store_data(b"", INDEX_PREFIX + name + INDEX_SEP + utils.get_hostname())
+
+    def _run_device_map(self, pmod, rmod):
+        clock1 = _time.process_time()
+        map_key, map_value = self.get_pair()
+        op = modules.field(rmod, "device_reduce", "sum") if rmod is not None else "sum"
+        extra = self.task_tbl.get("extra") or {}
+        spec = modules.field(pmod, "device_partition")
+        nparts = int(extra.get("num_partitions") or (spec[1] if spec else 0) or 1)
+        ctx = dev.DeviceMapContext(op=op, capacity=int(extra.get("table_capacity") or 1 << 20))
+        modules.field(self.module, "device_mapfn")(map_key, map_value, ctx.emit)
+        ctx.flush_host_pairs()
+        self.mark_as_finished()
+        hi, lo, val, rep = ctx.table.compact()
+        cols = dev.finalize(hi, lo, val, rep, ctx.source(), nparts, pmod)
+        fs, make_builder, _ = fsmod.router(self.cnn, None, self.storage, self.path)
+        for p in range(nparts):
+            if cols["bounds"][p + 1] == cols["bounds"][p]:
+                continue
+            s = dev.partition_slice(cols, p)
+            name = f"{self.path}/{self.results_ns}.P{p}.M{map_key}"
+            b = make_builder()
+            b.append(codec.encode_columnar(s["hi"], s["lo"], s["val"], s["key_off"], s["key_blob"]))
+            fs.remove_file(name)
+            b.build(name)
+            self._register_output(name)
+        elapsed = _time.process_time() - clock1
+        self.mark_as_written(elapsed)
+        return elapsed
+
+    # -- reduce --------------------------------------------------------------------
+    def _prepare_reduce(self):
+        g = modules.field(self.module, "reducefn")
+        aci = all(bool(modules.field(self.module, f)) for f in
+                  ("associative_reducer", "commutative_reducer", "idempotent_reducer"))
+        dev_op = modules.field(self.module, "device_reduce")
+        part_key, value = self.get_pair()
+
+        def run():
+            clock1 = _time.process_time()
+            job_file, res_file, mappers = value["file"], value["result"], value.get("mappers", [])
+            fs, _, make_lines_iterator = fsmod.router(self.cnn, mappers, self.storage, self.path)
+            import re
+            filenames = [v["filename"] for v in fs.list({"filename": {"$regex": "^" + re.escape(job_file) + r"\..*"}})]
+            rstore, rbuilder = result_store(self.cnn, self.storage, self.path)
+            rstore.remove_file(res_file)
+            blobs = None
+            if dev_op is not None and filenames:
+                blobs = [fsmod.read_blob(self.cnn, self.storage, self.path, n) for n in filenames]
+                if not all(b[:4] == codec.MAGIC_COL for b in blobs):
+                    blobs = None
+            b = rbuilder()
+            if blobs is not None:
+                b.append(_device_reduce(blobs, dev_op))
+            else:
+                recs = []
+                for k, v in utils.merge_iterator(fs, filenames, make_lines_iterator):
+                    if not aci or len(v) > 1:
+                        out = []
+                        g(k, v, out.append)
+                        v = [tuple_(x) for x in out]
+                    recs.append((k, v))
+                b.append(codec.encode_records(recs))
+            b.build(res_file)
+            elapsed = _time.process_time() - clock1
+            self.mark_as_written(elapsed)
+            gfs = self.cnn.gridfs()
+            for n in filenames:
+                fs.remove_file(n)
+            for f in gfs.list({"filename": {"$regex": "^" + re.escape(INDEX_PREFIX + job_file) + r"\."}}):
+                gfs.remove_file(f["filename"])
+            return elapsed
+        return run
+
+
+def _device_reduce(blobs: list[bytes], op: str) -> bytes:
+    """Merge columnar partition files on the device: hash-aggregate all
+    (key, value) rows, sort, write one columnar result."""
+    cols = [codec.decode_columnar(b) for b in blobs]
+    d = dev.default_device()
+    n = sum(int(c["hi"].size) for c in cols)
+    hi = torch.from_numpy(np.concatenate([c["hi"] for c in cols]).view(np.int64)).to(d)
+    lo = torch.from_numpy(np.concatenate([c["lo"] for c in cols]).view(np.int64)).to(d)
+    val = torch.from_numpy(np.concatenate([c["val"] for c in cols])).to(d)
+    # key bytes: concatenate blobs, rep = global offset of each key
+    bases = np.cumsum([0] + [int(c["key_blob"].size) for c in cols])[:-1]
+    offs = np.concatenate([c["key_off"][:-1] + b for c, b in zip(cols, bases)]).astype(np.uint64)
+    lens = np.concatenate([np.diff(c["key_off"]) for c in cols]).astype(np.uint64)
+    rep = torch.from_numpy(((offs << np.uint64(24)) | lens).view(np.int64)).to(d)
+    src = torch.from_numpy(np.concatenate([c["key_blob"] for c in cols])).to(d)
+    tab = dev.ops.HashTable(max(1024, 2 * n), device=d, op=op)
+    tab.insert(hi, lo, val, rep)
+    uhi, ulo, uval, urep = tab.compact()
+    out = dev.finalize(uhi, ulo, uval, urep, src, 1, None, part=torch.zeros(uhi.numel(), dtype=torch.int32,
+                                                                              device=d))
+    return codec.encode_columnar(out["hi"], out["lo"], out["val"], out["key_off"], out["key_blob"])
+
+
+def result_store(cnn, storage: str, path: str):
+    """Where reduce results live: the coordinator blob store (results always go
+    to GridFS in the reference, job.lua:249-251), or process memory for hbm."""
+    if storage == "hbm":
+        m = fsmod.MemFS(path)
+        return m, (lambda: fsmod.MemBuilder(m))
+    g = cnn.gridfs()
+    return g, (lambda: cnn.grid_file_builder())
+
+
+def utest() -> None:
+    f = cached(lambda i: i)
+    for _ in range(2):
+        for i in range(1, 11):
+            assert f(i) == i
