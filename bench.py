@@ -1,0 +1,130 @@
+#!/usr/bin/env python
+"""Headline benchmark: Europarl-v7-shaped word-count, words/s for the whole node.
+
+Workload (BASELINE.json / BASELINE.md; reference README.md:43-75): 197 input
+splits of <=10,000 lines, 1,965,734 lines and 49,158,635 whitespace tokens
+(synthetic, Zipf-Mandelbrot vocabulary, ~291 MB — no network for the real
+corpus), one map job per split, sum reducer used as combiner, 10 reduce
+partitions (README.md:59).
+
+One timed step = one full MapReduce iteration through the SPMD engine
+(parallel/spmd.py): taskfn -> host(pinned) -> HBM staging of every split ->
+fused tokenize/key/combine kernels -> partition -> RCCL all-to-all shuffle
+(N>1) -> per-partition reduce -> (partition, key) radix sort -> key bytes +
+counts of every ``result.P<NN>`` copied back to host memory.  As in the
+reference's "Server time" (server.lua:464-536), the user finalfn that prints
+results is not part of the step; it runs once after timing to validate.
+
+The corpus is fixed, so adding GPUs divides it (strong scaling).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from lua_mapreduce_1_amd.parallel import dist as D  # noqa: E402
+from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore  # noqa: E402
+from lua_mapreduce_1_amd.utils import corpus  # noqa: E402
+
+BASELINE_WORDS_PER_S = 49_158_635 / 49.229152  # README.md:73 (4 workers, 1 machine)
+METRIC = "words/sec (whole node), Europarl-v7 word-count 197 splits, 1/2/4/8 MI355X"
+MODEL = "lua_mapreduce_1_amd.models.wordcount"
+
+
+def load_corpus(seed: int, rank: int, local_rank: int, world: int, device) -> list[bytes]:
+    """Generate once per box (cached under /tmp), shared by all local ranks."""
+    cache = f"/tmp/lmr_europarl_like_{seed}.npz"
+    if local_rank == 0 and not os.path.exists(cache):
+        t0 = time.time()
+        splits = corpus.europarl_like(seed=seed)
+        off = np.zeros(len(splits) + 1, np.int64)
+        np.cumsum([len(s) for s in splits], out=off[1:])
+        tmp = cache + f".tmp{os.getpid()}.npz"
+        np.savez(tmp, data=np.frombuffer(b"".join(splits), np.uint8), off=off)
+        os.replace(tmp, cache)
+        print(f"# corpus generated in {time.time() - t0:.1f}s -> {cache}", file=sys.stderr, flush=True)
+    D.barrier(device=device)
+    z = np.load(cache)
+    data, off = z["data"], z["off"]
+    return [data[off[i]:off[i + 1]].tobytes() for i in range(len(off) - 1)]
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--reducers", type=int, default=10)
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, device = D.init_from_env()
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus and rank == 0:
+        print(f"# warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    splits = load_corpus(args.seed, rank, local_rank, world, device)
+    total_words = corpus.EUROPARL_WORDS
+    total_bytes = sum(len(s) for s in splits)
+    store = SplitStore(splits)
+    del splits
+    params = dict(taskfn=MODEL, mapfn=MODEL, partitionfn=MODEL, reducefn=MODEL, finalfn=MODEL,
+                  init_args={"nsplits": len(store), "num_reducers": args.reducers})
+    eng = SPMDEngine(params, device=device, split_store=store, verbose=args.verbose)
+
+    for _ in range(args.warmup):
+        eng.run_iteration()
+    D.barrier(device=device)
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(args.steps):
+        last = eng.run_iteration()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    D.barrier(device=device)
+    elapsed = time.perf_counter() - t0
+    elapsed = D.all_reduce_max(elapsed, device)
+    ms = 1000.0 * elapsed / max(1, args.steps)
+
+    # validation outside the timed region: every token counted exactly once
+    counted = D.all_reduce_sum_int(last.total_value, device) if last is not None else 0
+    distinct = D.all_reduce_sum_int(last.distinct_keys, device) if last is not None else 0
+    if rank == 0:
+        print(eng.stats_block(last), file=sys.stderr, end="")
+        print(f"# tokens counted {counted} (expected {total_words}), distinct words {distinct}, "
+              f"bytes {total_bytes}, per-phase s: {last.timings}", file=sys.stderr, flush=True)
+        if counted != total_words:
+            print("# ERROR: token count mismatch", file=sys.stderr, flush=True)
+        value = total_words / (ms / 1000.0)
+        out = {
+            "metric": METRIC, "value": value, "unit": "words/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": value / BASELINE_WORDS_PER_S, "dtype": "int64",
+            "data": "synthetic Europarl-v7-shaped corpus (197 splits, 1,965,734 lines, 49,158,635 words, "
+                    f"{total_bytes} bytes), host-resident pinned splits staged to HBM every step",
+            "config": {"model": "wordcount (MapReduce: taskfn/mapfn/partitionfn/reducefn)", "global_batch": 197,
+                       "seq_len": 10000, "parallelism": f"dp{world}", "num_reducers": args.reducers,
+                       "words": total_words, "bytes": total_bytes, "valid": counted == total_words},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

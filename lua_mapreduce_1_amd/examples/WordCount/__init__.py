@@ -38,7 +38,8 @@ def mapfn(key, value, emit):
 
 
 def device_mapfn(key, value, emit):
-    emit.words(_io.load_file(value, emit.device))
+    # value: a file path (server/worker jobs) or the staged input tensor (SPMD engine)
+    emit.words(value if hasattr(value, "data_ptr") else _io.load_file(value, emit.device))
 
 
 def partitionfn(key):

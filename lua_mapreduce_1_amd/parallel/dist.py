@@ -1,0 +1,126 @@
+"""Process-group plumbing and the shuffle collectives.
+
+One process per GPU; ``torch.distributed`` with backend ``nccl`` (= RCCL on
+ROCm, over xGMI inside a node) for device tensors, ``gloo`` for CPU runs and
+tests.  The MapReduce shuffle (GridFS / scp / shared FS
+in the reference) is an all-to-all-v in two steps: the int64 per-destination
+counts first, then the payload, each a single ``all_to_all_single`` so every
+xGMI link is driven concurrently (an all-to-all is bounded by per-link
+bandwidth x 7 links, not by a ring).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_world() -> tuple[int, int, int]:
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def init_from_env(backend: str | None = None, timeout_s: float = 600.0):
+    """Initialise the default group from torchrun's env (no-op for WORLD_SIZE=1).
+
+    Returns (rank, world, device)."""
+    rank, world, local = env_world()
+    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    device = torch.device("cuda", local) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    if world > 1 and not dist.is_initialized():
+        be = backend or ("nccl" if use_gpu else "gloo")
+        kw = {}
+        if be == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s),
+                                **kw)
+    return rank, world, device
+
+
+def world_info(group=None) -> tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1
+
+
+def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None):
+    if inp.is_cuda or dist.get_backend(group) != "gloo":
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+        return
+    # gloo: all_to_all_single is supported for CPU tensors on recent torch; fall
+    # back to point-to-point if not.
+    try:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+    except RuntimeError:
+        rank, world = world_info(group)
+        ins = list(torch.split(inp, in_splits))
+        outs = list(torch.split(out, out_splits))
+        reqs = []
+        for p in range(world):
+            if p == rank:
+                outs[p].copy_(ins[p])
+                continue
+            reqs.append(dist.isend(ins[p].contiguous(), p, group=group))
+            reqs.append(dist.irecv(outs[p], p, group=group))
+        for r in reqs:
+            r.wait()
+
+
+def exchange_counts(counts: torch.Tensor, group=None) -> torch.Tensor:
+    """counts[p] = items this rank sends to p -> recv[p] = items p sends here."""
+    recv = torch.empty_like(counts)
+    _a2a(recv, counts, None, None, group)
+    return recv
+
+
+def all_to_all_v(payload: torch.Tensor, send_counts: list[int], recv_counts: list[int], group=None) -> torch.Tensor:
+    """Variable all-to-all along dim 0 (rows of any trailing shape)."""
+    shape = (sum(recv_counts),) + tuple(payload.shape[1:])
+    out = torch.empty(shape, dtype=payload.dtype, device=payload.device)
+    _a2a(out, payload.contiguous(), list(recv_counts), list(send_counts), group)
+    return out
+
+
+def barrier(group=None, device=None) -> None:
+    if dist.is_available() and dist.is_initialized():
+        if device is not None and torch.device(device).type == "cuda":
+            dist.barrier(group=group, device_ids=[torch.device(device).index])
+        else:
+            dist.barrier(group=group)
+
+
+def all_reduce_max(x: float, device, group=None) -> float:
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def all_reduce_sum_int(x: int, device, group=None) -> int:
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    t = torch.tensor([x], dtype=torch.int64, device=device)
+    dist.all_reduce(t, group=group)
+    return int(t.item())
+
+
+def broadcast_object(obj, src: int = 0, group=None, device=None):
+    if not (dist.is_available() and dist.is_initialized()):
+        return obj
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=src, group=group, device=device)
+    return lst[0]
+
+
+def gather_objects(obj, dst: int = 0, group=None):
+    if not (dist.is_available() and dist.is_initialized()):
+        return [obj]
+    rank, world = world_info(group)
+    out = [None] * world if rank == dst else None
+    dist.gather_object(obj, out, dst=dst, group=group)
+    return out

@@ -1,0 +1,408 @@
+"""SPMD MapReduce engine: one rank per GPU, HBM-resident data plane, RCCL shuffle.
+
+This is the MI355X-first execution mode of the same user contract as the
+server/worker roles (taskfn / mapfn / partitionfn / reducefn / finalfn,
+``map_results`` -> ``result.P<NN>`` layout, iterative ``"loop"``), designed for
+throughput instead of a MongoDB-mediated job queue:
+
+* rank 0 runs ``taskfn`` and broadcasts the job list; map jobs are assigned to
+  ranks in contiguous byte-balanced blocks (P1 data parallelism);
+* inputs are staged host(pinned) -> HBM on a copy stream in growing chunks
+  while the map kernels consume the previous chunk on the compute stream;
+* map + combine run in one per-rank HBM hash table across all the rank's jobs
+  (P3 map-side combining, the combiner fused into the table);
+* the shuffle is partition -> destination rank ``p % W``, a radix pack by
+  destination and two ``all_to_all_single`` calls (counts, then payload) over
+  RCCL/xGMI (P2);
+* each rank reduces the partitions it owns in a second hash table, sorts them
+  by (partition, key) and writes ``result.P<NN>`` columnar files to host memory;
+* ``finalfn`` runs on rank 0 over the gathered, filename-sorted results; a
+  ``"loop"`` reply starts the next iteration with the inputs still resident
+  (P4/P6).
+
+Per-job status (WAITING/RUNNING/WRITTEN/BROKEN/FAILED, repetitions) and the
+reference's statistics block are kept in process; a map chunk that raises is
+retried up to ``MAX_JOB_RETRIES`` times and then marked FAILED (server.lua
+semantics), with the failure flag agreed across ranks before the shuffle.
+"""
+from __future__ import annotations
+
+import sys
+import time
+import traceback
+
+import numpy as np
+import torch
+
+from .. import ops, utils
+from ..runtime import device as devmod
+from ..runtime import modules
+from ..utils import STATUS
+from . import dist as D
+
+
+class SplitStore:
+    """Host-resident input splits in ONE pinned buffer (the page-cache analogue
+    of the reference's split files).  Every split is followed by a newline so
+    tokens never straddle two splits."""
+
+    def __init__(self, splits: list[bytes] | None = None, pin: bool = True):
+        splits = splits or []
+        sizes = [len(s) + (0 if (s and s[-1:] in (b"\n", b" ")) else 1) for s in splits]
+        self.offsets = np.zeros(len(splits) + 1, dtype=np.int64)
+        np.cumsum(sizes, out=self.offsets[1:])
+        total = int(self.offsets[-1])
+        self.buffer = torch.empty(total, dtype=torch.uint8, pin_memory=pin and torch.cuda.is_available())
+        view = self.buffer.numpy()
+        for i, s in enumerate(splits):
+            a = int(self.offsets[i])
+            view[a:a + len(s)] = np.frombuffer(s, dtype=np.uint8)
+            if sizes[i] > len(s):
+                view[a + len(s)] = 10
+
+    def __len__(self) -> int:
+        return len(self.offsets) - 1
+
+    def size(self, i: int) -> int:
+        return int(self.offsets[i + 1] - self.offsets[i])
+
+    def region(self, i0: int, i1: int) -> tuple[int, int]:
+        return int(self.offsets[i0]), int(self.offsets[i1])
+
+
+class JobRecord:
+    __slots__ = ("key", "value", "status", "repetitions", "started", "written", "cpu_time", "real_time", "worker")
+
+    def __init__(self, key, value):
+        self.key, self.value = key, value
+        self.status = STATUS.WAITING
+        self.repetitions = 0
+        self.started = self.written = 0.0
+        self.cpu_time = self.real_time = 0.0
+        self.worker = -1
+
+
+class IterationResult:
+    def __init__(self):
+        self.partitions: dict[int, dict] = {}   # partition -> columnar host arrays
+        self.result_names: dict[int, str] = {}
+        self.map_jobs: list[JobRecord] = []
+        self.red_jobs: list[JobRecord] = []
+        self.timings: dict[str, float] = {}
+        self.distinct_keys = 0
+        self.total_value = 0
+
+
+class SPMDEngine:
+    def __init__(self, params: dict, group=None, device=None, split_store: SplitStore | None = None,
+                 chunk_mb: tuple = (4, 8, 16, 32), verbose: bool = False, table_capacity: int = 1 << 21):
+        self.params = dict(params)
+        self.group = group
+        self.rank, self.world = D.world_info(group)
+        if device is None:
+            device = devmod.default_device()
+        self.device = torch.device(device)
+        self.splits = split_store
+        self.chunk_bytes = [int(c * (1 << 20)) for c in chunk_mb]
+        self.verbose = verbose
+        self.result_ns = self.params.get("result_ns") or "result"
+        self.init_args = self.params.get("init_args")
+        self.taskfn = modules.load(self.params["taskfn"])
+        self.mapmod = modules.load(self.params["mapfn"])
+        self.partmod = modules.load(self.params["partitionfn"])
+        self.redmod = modules.load(self.params["reducefn"])
+        self.finalmod = modules.load(self.params.get("finalfn")) if self.params.get("finalfn") else None
+        for m in (self.taskfn, self.mapmod, self.partmod, self.redmod, self.finalmod):
+            modules.init_once(m, self.init_args)
+        self.op = modules.field(self.redmod, "device_reduce", "sum")
+        spec = modules.field(self.partmod, "device_partition")
+        self.nparts = int(self.params.get("num_partitions") or (spec[1] if spec else 0) or self.world)
+        self.device_input = modules.field(self.mapmod, "device_input")
+        self.dmap = modules.field(self.mapmod, "device_mapfn")
+        if self.dmap is None:
+            raise ValueError("SPMD engine needs a map module with device_mapfn (use server/worker for host-only "
+                             "map functions)")
+        self.table = ops.HashTable(table_capacity, device=self.device, op=self.op)
+        self.red_table: ops.HashTable | None = None
+        self.arena: torch.Tensor | None = None
+        self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self.iteration = 0
+        self.finished = False
+
+    # ------------------------------------------------------------------------
+    def _log(self, msg: str) -> None:
+        if self.verbose and self.rank == 0:
+            sys.stderr.write(msg)
+            sys.stderr.flush()
+
+    def _sync(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def _jobs(self) -> list[tuple]:
+        jobs = []
+        if self.rank == 0:
+            seen = set()
+
+            def emit(k, v):
+                if k in seen:
+                    raise ValueError(f"Duplicate key: {k}")
+                seen.add(k)
+                jobs.append((k, v))
+            modules.field(self.taskfn, "taskfn")(emit)
+        if self.world > 1:
+            jobs = D.broadcast_object(jobs, 0, self.group, self.device if self.device.type == "cuda" else None)
+        return jobs
+
+    def _job_bytes(self, value) -> int:
+        if self.device_input == "split":
+            return self.splits.size(int(value["split"] if isinstance(value, dict) else value))
+        if self.device_input == "file":
+            import os
+            return os.path.getsize(value) + 1
+        return 1
+
+    def _assign(self, jobs: list[tuple]) -> tuple[int, int]:
+        """Contiguous block of jobs for this rank, balanced by input bytes."""
+        n = len(jobs)
+        if self.world == 1:
+            return 0, n
+        w = np.array([self._job_bytes(v) for _, v in jobs], dtype=np.float64)
+        c = np.concatenate([[0.0], np.cumsum(w)])
+        tot = c[-1]
+        cuts = [int(np.searchsorted(c, tot * r / self.world, side="left")) for r in range(self.world + 1)]
+        cuts[0], cuts[-1] = 0, n
+        return cuts[self.rank], max(cuts[self.rank], cuts[self.rank + 1])
+
+    # -- map ------------------------------------------------------------------
+    def _stage_chunks(self, jobs, j0, j1):
+        """Yield (job index range, device tensor) chunks, H2D overlapped with compute."""
+        if self.device_input == "split":
+            ids = [int(v["split"] if isinstance(v, dict) else v) for _, v in jobs[j0:j1]]
+            if ids and ids != list(range(ids[0], ids[0] + len(ids))):
+                raise ValueError("split jobs of a rank must be contiguous splits")
+            if not ids:
+                return
+            a, b = self.splits.region(ids[0], ids[-1] + 1)
+            nbytes = b - a
+            if self.arena is None or self.arena.numel() < nbytes:
+                self.arena = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            # chunk boundaries at split boundaries, sizes growing 4 -> 32 MB
+            bounds = [0]
+            k = 0
+            while bounds[-1] < len(ids):
+                target = self.splits.offsets[ids[0] + bounds[-1]] + self.chunk_bytes[min(k, len(self.chunk_bytes) - 1)]
+                nxt = int(np.searchsorted(self.splits.offsets, target, side="left")) - ids[0]
+                nxt = max(bounds[-1] + 1, min(len(ids), nxt))
+                bounds.append(nxt)
+                k += 1
+            events = []
+            host = self.splits.buffer
+            cs = self.copy_stream
+            for i in range(len(bounds) - 1):
+                ca, cb = self.splits.region(ids[0] + bounds[i], ids[0] + bounds[i + 1])
+                dst = self.arena[ca - a:cb - a]
+                if cs is not None:
+                    with torch.cuda.stream(cs):
+                        dst.copy_(host[ca:cb], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(cs)
+                else:
+                    dst.copy_(host[ca:cb])
+                    ev = None
+                events.append((i, dst, ev))
+            cur = torch.cuda.current_stream(self.device) if cs is not None else None
+            for i, dst, ev in events:
+                if ev is not None:
+                    cur.wait_event(ev)
+                yield (j0 + bounds[i], j0 + bounds[i + 1]), dst
+        elif self.device_input == "file":
+            from ..ops import io as mio
+            for j in range(j0, j1):
+                yield (j, j + 1), mio.load_file(jobs[j][1], self.device)
+        else:
+            for j in range(j0, j1):
+                yield (j, j + 1), jobs[j][1]
+
+    def _run_map(self, jobs, recs, j0, j1) -> None:
+        ctx = devmod.DeviceMapContext.__new__(devmod.DeviceMapContext)
+        ctx.device, ctx.op, ctx.table = self.device, self.op, self.table
+        ctx.sources, ctx.base, ctx.host_pairs = [], 0, []
+        ctx.emit = devmod.DeviceEmitter(ctx)
+        self._ctx = ctx
+        # the rank's whole staged input is ONE byte source (rep offsets index it)
+        for (a, b), data in self._stage_chunks(jobs, j0, j1):
+            t0 = time.time()
+            c0 = time.process_time()
+            for j in range(a, b):
+                recs[j].status, recs[j].started, recs[j].worker = STATUS.RUNNING, t0, self.rank
+            keys = [jobs[j][0] for j in range(a, b)]
+            done = False
+            while not done:
+                try:
+                    if isinstance(data, torch.Tensor) and self.device_input == "split" and self.arena is not None:
+                        # rep offsets relative to the arena start
+                        base = data.data_ptr() - self.arena.data_ptr()
+                        ctx.base = base
+                        self.dmap(keys if b - a > 1 else keys[0], data, ctx.emit)
+                    else:
+                        self.dmap(keys[0] if b - a == 1 else keys, data, ctx.emit)
+                    done = True
+                except Exception:  # noqa: BLE001
+                    for j in range(a, b):
+                        recs[j].repetitions += 1
+                        recs[j].status = STATUS.BROKEN
+                    sys.stderr.write("Error executing a job: %s\n" % traceback.format_exc())
+                    if recs[a].repetitions >= utils.MAX_JOB_RETRIES:
+                        for j in range(a, b):
+                            recs[j].status = STATUS.FAILED
+                        done = True
+            t1 = time.time()
+            for j in range(a, b):
+                if recs[j].status != STATUS.FAILED:
+                    recs[j].status = STATUS.WRITTEN
+                recs[j].written = t1
+                recs[j].real_time = (t1 - t0) / (b - a)
+                recs[j].cpu_time = (time.process_time() - c0) / (b - a)
+        ctx.flush_host_pairs()
+
+    # -- shuffle + reduce -------------------------------------------------------
+    def _source(self) -> torch.Tensor | None:
+        if self.device_input == "split":
+            return self.arena
+        return self._ctx.source()
+
+    def _shuffle(self, hi, lo, val, rep, src, part):
+        """Send each key to rank part % W; returns received (hi, lo, val, rep, src)."""
+        W = self.world
+        dest = torch.remainder(part, W).to(torch.int64)
+        perm = ops.sort_keys([dest], bits=[max(1, (W - 1).bit_length())]).long()
+        hi, lo, val, rep = hi[perm], lo[perm], val[perm], rep[perm]
+        off, blob = ops.gather_key_bytes(hi, lo, rep, src)
+        lens = off[1:] - off[:-1]
+        counts = ops.bincount(dest.to(torch.int32), W)
+        bcounts = torch.zeros(W, dtype=torch.int64, device=hi.device)
+        bcounts.index_add_(0, dest[perm], lens)
+        send = torch.stack([counts, bcounts])
+        recv = D.exchange_counts(send.t().contiguous().view(-1), self.group).view(W, 2)
+        send_h = send.cpu().tolist()
+        recv_h = recv.cpu().tolist()
+        rec = torch.stack([hi, lo, val, lens], dim=1)
+        rrec = D.all_to_all_v(rec, send_h[0], [r[0] for r in recv_h], self.group)
+        rblob = D.all_to_all_v(blob, send_h[1], [r[1] for r in recv_h], self.group)
+        rl = rrec[:, 3]
+        roff, _ = ops.exclusive_scan(rl)
+        rrep = (roff << 24) | rl
+        return rrec[:, 0].contiguous(), rrec[:, 1].contiguous(), rrec[:, 2].contiguous(), rrep, rblob
+
+    def _reduce(self, hi, lo, val, rep, src):
+        n = hi.numel()
+        cap = ops.next_pow2(max(1 << 16, 2 * n))
+        if self.red_table is None or self.red_table.cap < cap:
+            self.red_table = ops.HashTable(cap, device=self.device, op=self.op)
+        else:
+            self.red_table.reset()
+        self.red_table.insert(hi, lo, val, rep)
+        return self.red_table.compact()
+
+    # ------------------------------------------------------------------------
+    def run_iteration(self) -> IterationResult:
+        self.iteration += 1
+        res = IterationResult()
+        T = res.timings
+        t_start = time.time()
+        jobs = self._jobs()
+        recs = [JobRecord(k, v) for k, v in jobs]
+        res.map_jobs = recs
+        j0, j1 = self._assign(jobs)
+        self.table.reset()
+        t0 = time.time()
+        self._run_map(jobs, recs, j0, j1)
+        n_claimed, overflow = self.table.stats()   # synchronises the map phase
+        if overflow or n_claimed > self.table.cap // 2:
+            # grow and redo this rank's map (results with an overflowed table are unusable)
+            self.table = ops.HashTable(ops.next_pow2(4 * max(n_claimed, 1)), device=self.device, op=self.op)
+            self._run_map(jobs, recs, j0, j1)
+            n_claimed, overflow = self.table.stats()
+        T["map"] = time.time() - t0
+        t1 = time.time()
+        hi, lo, val, rep = self.table.compact()
+        src = self._source()
+        part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
+        if self.world > 1:
+            hi, lo, val, rep, src = self._shuffle(hi, lo, val, rep, src, part)
+            hi, lo, val, rep = self._reduce(hi, lo, val, rep, src)
+            part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
+        T["shuffle"] = time.time() - t1
+        t2 = time.time()
+        cols = devmod.finalize(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
+        digits = len(str(max(self.nparts - 1, 0)))
+        for p in range(self.nparts):
+            if cols["bounds"][p + 1] > cols["bounds"][p]:
+                res.partitions[p] = devmod.partition_slice(cols, p)
+                res.result_names[p] = ("%s.P%0" + str(digits) + "d") % (self.result_ns, p)
+                r = JobRecord(p, {"result": res.result_names[p]})
+                r.status, r.started, r.written, r.worker = STATUS.WRITTEN, t1, time.time(), self.rank
+                r.real_time = r.written - t1
+                res.red_jobs.append(r)
+        res.distinct_keys = int(cols["hi"].size)
+        res.total_value = int(cols["val"].sum()) if cols["val"].size else 0
+        T["reduce"] = time.time() - t2
+        T["iteration"] = time.time() - t_start
+        failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
+        res.failed_maps = D.all_reduce_sum_int(failed, self.device, self.group) if self.world > 1 else failed
+        return res
+
+    # ------------------------------------------------------------------------
+    def gather_results(self, res: IterationResult) -> list[tuple[str, dict]]:
+        """All ranks' result partitions on rank 0, sorted by filename (the
+        order server_final hands them to finalfn, server.lua:358-383)."""
+        mine = [(res.result_names[p], res.partitions[p]) for p in res.partitions]
+        if self.world > 1:
+            allp = D.gather_objects(mine, 0, self.group)
+            if self.rank != 0:
+                return []
+            mine = [x for lst in allp for x in lst]
+        return sorted(mine, key=lambda t: t[0])
+
+    def pairs(self, gathered):
+        from ..runtime import codec
+        for _name, cols in gathered:
+            yield from codec.iter_columnar(cols)
+
+    def stats_block(self, res: IterationResult) -> str:
+        m = res.map_jobs
+        r = res.red_jobs
+        ms = sum(x.cpu_time for x in m)
+        rs = sum(x.cpu_time for x in r)
+        mr = sum(x.real_time for x in m)
+        rr = sum(x.real_time for x in r)
+        T = res.timings
+        lines = [
+            "#   Map sum(cpu_time)     %f" % ms, "#   Reduce sum(cpu_time)  %f" % rs,
+            "# Sum(cpu_time)           %f" % (ms + rs), "#   Map sum(real_time)    %f" % mr,
+            "#   Reduce sum(real_time) %f" % rr, "# Sum(real_time)          %f" % (mr + rr),
+            "# Sum(sys_time)           %f" % (mr + rr - ms - rs), "#   Map cluster time      %f" % T["map"],
+            "#   Reduce cluster time   %f" % (T["shuffle"] + T["reduce"]),
+            "# Cluster time            %f" % (T["map"] + T["shuffle"] + T["reduce"]),
+            "# Failed maps     %d" % getattr(res, "failed_maps", 0), "# Failed reduces  0",
+            "# Server time %f" % T["iteration"],
+        ]
+        return "\n".join(lines) + "\n"
+
+    def run(self) -> IterationResult:
+        """Iterate until finalfn returns something other than "loop"."""
+        while True:
+            self._log("# Iteration %d\n" % (self.iteration + 1))
+            res = self.run_iteration()
+            self._log(self.stats_block(res))
+            gathered = self.gather_results(res)
+            reply = None
+            if self.rank == 0 and self.finalmod is not None:
+                reply = modules.field(self.finalmod, "finalfn")(self.pairs(gathered))
+            if self.world > 1:
+                reply = D.broadcast_object(reply, 0, self.group, self.device if self.device.type == "cuda" else None)
+            if reply != "loop":
+                self.finished = True
+                return res
+            self._log("# LOOP again\n")
