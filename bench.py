@@ -127,4 +127,9 @@ def main() -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    rc = main()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    if os.environ.get("MR_FAST_EXIT"):
+        os._exit(rc)  # skip library finalizers (seen to segfault under rocprofv3 --memory-copy-trace)
+    sys.exit(rc)

@@ -30,6 +30,7 @@
 typedef uint64_t u64;
 typedef uint32_t u32;
 typedef uint8_t u8;
+typedef uint16_t u16;
 
 namespace mr {
 

@@ -104,15 +104,32 @@ class HashTable:
                 r = r + np.uint64(rep_add << K.REP_LEN_BITS)
             self._pending.append((_u64(hi).copy(), _u64(lo).copy(), v, r))
 
-    def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, chunk_bytes: int = 64 * 1024) -> None:
+    def _overflow(self, nbytes: int):
+        need = min(1 << 24, max(1 << 16, nbytes // 8))
+        if getattr(self, "_ovf", None) is None or self._ovf[0].numel() < need:
+            d = self.device
+            self._ovf = [torch.empty(need, dtype=torch.int64, device=d) for _ in range(3)]
+            self._ovf_counter = torch.zeros(1, dtype=torch.int64, device=d)
+        return self._ovf, self._ovf_counter
+
+    def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, chunk_bytes: int = 32 * 1024,
+                      version: int = 2, mode: int = 0) -> None:
         """Fused tokenize + exact key + combine of every whitespace token (value 1)."""
         nbytes = text.numel()
         if nbytes == 0:
             return
         if self.is_cuda:
             assert text.dtype == torch.uint8 and text.is_contiguous()
-            _hip.call("mr_wc_map", _hip.ptr(text), nbytes, chunk_bytes, rep_base, *self._gtab(), self.cap,
-                      _hip.stream(self.device))
+            if version == 1:
+                _hip.call("mr_wc_map", _hip.ptr(text), nbytes, chunk_bytes, rep_base, *self._gtab(), self.cap,
+                          _hip.stream(self.device))
+                return
+            ovf, counter = self._overflow(nbytes)
+            counter.zero_()
+            chunk = min(65536, max(8192, (chunk_bytes + 8191) // 8192 * 8192))
+            _hip.call("mr_wc_map2", _hip.ptr(text), nbytes, chunk, rep_base, *self._gtab(),
+                      self.cap, _hip.ptr(ovf[0]), _hip.ptr(ovf[1]), _hip.ptr(ovf[2]), ovf[0].numel(),
+                      _hip.ptr(counter), mode, _hip.stream(self.device))
         else:
             buf = _np(text)
             starts, lens = K.token_spans(buf)
