@@ -10,7 +10,7 @@
 //
 // Concurrency protocol (agent scope, placement independent — guide §6 G16):
 //   claim:   CAS tag 0 -> key_tag(hi,lo)            (relaxed, agent)
-//   publish: store hi, rep (relaxed) ; fold value ; store lo (RELEASE, agent)
+//   publish: sc1 stores of hi, rep ; fold value ; s_waitcnt vmcnt(0) ; sc1 store lo
 //   lookup:  tag match -> load lo (relaxed); lo==0 => not yet published, retry;
 //            lo match -> load hi; on mismatch re-check after an acquire fence.
 //   lo is never 0 for a valid key (mr_common.h), so lo doubles as "published".
@@ -45,9 +45,12 @@ __device__ __forceinline__ void fold_value(long long* p, long long v, int op) {
   else atomicAdd((unsigned long long*)p, (unsigned long long)v);
 }
 
-// Insert (hi,lo) with value v; returns false only when the probe budget is
-// exhausted (overflow flag set; the host re-runs with a larger table).
-__device__ __forceinline__ bool gtab_insert(const GTab& t, u64 hi, u64 lo, long long v, u64 rep, int op) {
+// Insert (hi,lo) with value v.  Returns 2 when this call claimed a new slot,
+// 1 when it folded into an existing key, 0 when the probe budget is exhausted
+// (overflow flag set; the host re-runs with a larger table).  Callers count
+// claims locally and publish them with gtab_count_claims (one atomic per wave:
+// a same-address atomic per claim serialised ~3e5 adds in the map kernel).
+__device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long long v, u64 rep, int op) {
   const u64 tag = key_tag(hi, lo);
   u64 slot = (tag >> 7) & t.mask;
   u32 probes = 0;
@@ -57,12 +60,16 @@ __device__ __forceinline__ bool gtab_insert(const GTab& t, u64 hi, u64 lo, long 
       u64 expected = 0;
       if (__hip_atomic_compare_exchange_strong(&t.tag[slot], &expected, tag, __ATOMIC_RELAXED,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        // publish (guide §6 G16 R1): write-through (sc1) stores of the payload,
+        // drain them with vmcnt(0), then the sc1 store of `lo` that readers poll —
+        // no buffer_wbl2 L2 write-back (a release fence per new key cost ~1 ms
+        // over the 3e5 claims of the benchmark corpus).
         st_agent(&t.hi[slot], hi);
         st_agent(&t.rep[slot], rep);
         fold_value(&t.val[slot], v, op);
-        __hip_atomic_store(&t.lo[slot], lo, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(&t.ctrl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return true;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_agent(&t.lo[slot], lo);
+        return 2;
       }
       cur = expected;
     }
@@ -77,7 +84,7 @@ __device__ __forceinline__ bool gtab_insert(const GTab& t, u64 hi, u64 lo, long 
         }
         if (h == hi) {
           fold_value(&t.val[slot], v, op);
-          return true;
+          return 1;
         }
       }
     }
@@ -85,7 +92,16 @@ __device__ __forceinline__ bool gtab_insert(const GTab& t, u64 hi, u64 lo, long 
     ++probes;
   }
   __hip_atomic_fetch_or(&t.ctrl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return false;
+  return 0;
+}
+
+// Wave-reduce per-lane claim counts and add them to ctrl[0] (call with the
+// whole wave active, e.g. at kernel end).
+__device__ __forceinline__ void gtab_count_claims(const GTab& t, u32 claims) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) claims += __shfl_xor(claims, o);
+  if ((threadIdx.x & 63) == 0 && claims)
+    __hip_atomic_fetch_add(&t.ctrl[0], claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace mr

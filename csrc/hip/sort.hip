@@ -54,15 +54,171 @@ __global__ void __launch_bounds__(RS_THREADS) rs_scatter_kernel(const u64* keys_
   base_run[t] = offs[(u64)t * ntiles + blockIdx.x];
   const u64 tile = (u64)blockIdx.x * RS_TILE;
   const unsigned long long below = (1ull << lane) - 1ull;
+  // preload the whole tile into registers: one memory latency instead of one
+  // per round (the rounds are separated by barriers the loads cannot cross)
+  u64 kr[RS_ROUNDS];
+  V vr[RS_ROUNDS];
+#pragma unroll
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const u64 i = tile + (u64)r * RS_THREADS + t;
+    kr[r] = i < n ? keys_in[i] : 0;
+    vr[r] = (i < n && vals_in) ? vals_in[i] : V{};
+  }
+#pragma unroll
   for (int r = 0; r < RS_ROUNDS; ++r) {
     const u64 i = tile + (u64)r * RS_THREADS + t;
     const bool valid = i < n;
-    u64 k = 0;
-    V v{};
-    if (valid) {
-      k = keys_in[i];
-      if (vals_in) v = vals_in[i];
+    const u64 k = kr[r];
+    const u32 d = (u32)((k >> shift) & 0xFF);
+#pragma unroll
+    for (int w = 0; w < RS_WAVES; ++w) wcnt[w][t] = 0;
+    __syncthreads();
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const unsigned long long m = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? m : ~m;
     }
+    const u32 rank = (u32)__popcll(peers & below);
+    if (valid && rank == 0) wcnt[wave][d] = (u32)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      u32 pos = base_run[d] + rank;
+      for (int w = 0; w < wave; ++w) pos += wcnt[w][d];
+      keys_out[pos] = k;
+      if (vals_in) vals_out[pos] = vr[r];
+    }
+    __syncthreads();
+    u32 tot = 0;
+#pragma unroll
+    for (int w = 0; w < RS_WAVES; ++w) tot += wcnt[w][t];
+    base_run[t] += tot;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Onesweep-style LSD pass: ONE launch per 8-bit digit.
+//   * rs_ghist8_kernel computes the global 256-bin histograms of all 8 digits of
+//     a u64 word at once (digit counts do not depend on the current order);
+//   * rs_onesweep_kernel: tiles are taken in dispatch order from an atomic
+//     counter (so every predecessor tile is already resident: no deadlock),
+//     each tile publishes its per-digit count as a tagged 64-bit granule
+//     {epoch:24 | flag:2 | count:38} (guide §6 G16 R2: the data is the flag),
+//     looks back over predecessors for its exclusive prefix, republishes the
+//     inclusive prefix, then scatters with the same stable wave64-ballot ranking
+//     as rs_scatter_kernel.  A digit shared by every key makes the pass a copy.
+//   * every spin is bounded (s_sleep + give-up sets err[0]).
+constexpr u64 GR_AGG = 1ull, GR_INC = 2ull;
+
+__device__ __forceinline__ u64 gr_pack(u32 epoch, u64 flag, u64 count) {
+  return ((u64)(epoch & 0xFFFFFFu) << 40) | (flag << 38) | (count & ((1ull << 38) - 1));
+}
+
+__global__ void __launch_bounds__(RS_THREADS) rs_ghist8_kernel(const u64* keys, u64 n, u32* ghist /*[8][256]*/) {
+  __shared__ u32 h[8][RS_BINS];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) h[b][t] = 0;
+  __syncthreads();
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + t; i < n; i += stride) {
+    const u64 k = keys[i];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 0xFF], 1u);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+    if (h[b][t]) atomicAdd(&ghist[b * RS_BINS + t], h[b][t]);
+}
+
+template <typename V>
+__global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys_in, const V* vals_in, u64* keys_out,
+                                                                 V* vals_out, u64 n, int shift, const u32* ghist,
+                                                                 u64* granules, u32* tile_counter, u32 epoch,
+                                                                 u32* err) {
+  __shared__ u32 base_run[RS_BINS];
+  __shared__ u32 wcnt[RS_WAVES][RS_BINS];
+  __shared__ u32 lhist[RS_BINS];
+  __shared__ u32 sh_tile;
+  __shared__ u32 sh_uniform;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  if (t == 0) {
+    sh_tile = atomicAdd(tile_counter, 1u);
+    sh_uniform = 0;
+  }
+  lhist[t] = 0;
+  // exclusive scan of the global histogram (digit base offsets)
+  const u32 gcount = ghist[t];
+  wcnt[0][t] = gcount;
+  __syncthreads();
+  if (gcount == n) sh_uniform = 1;
+  for (int o = 1; o < RS_BINS; o <<= 1) {
+    const u32 y = t >= o ? wcnt[0][t - o] : 0u;
+    __syncthreads();
+    wcnt[0][t] += y;
+    __syncthreads();
+  }
+  const u32 gbase = wcnt[0][t] - gcount;
+  const u32 tile = sh_tile;
+  const u64 t0 = (u64)tile * RS_TILE;
+  if (sh_uniform) {  // every key has this digit: order unchanged
+    for (int r = 0; r < RS_ROUNDS; ++r) {
+      const u64 i = t0 + (u64)r * RS_THREADS + t;
+      if (i < n) {
+        keys_out[i] = keys_in[i];
+        if (vals_in) vals_out[i] = vals_in[i];
+      }
+    }
+    return;
+  }
+  // local histogram of this tile (keys preloaded into registers)
+  u64 kr[RS_ROUNDS];
+  V vr[RS_ROUNDS];
+#pragma unroll
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const u64 i = t0 + (u64)r * RS_THREADS + t;
+    kr[r] = i < n ? keys_in[i] : 0;
+    vr[r] = (i < n && vals_in) ? vals_in[i] : V{};
+    if (i < n) atomicAdd(&lhist[(kr[r] >> shift) & 0xFF], 1u);
+  }
+  __syncthreads();
+  const u32 mine = lhist[t];
+  u64* G = granules + (u64)tile * RS_BINS;
+  __hip_atomic_store(&G[t], gr_pack(epoch, tile == 0 ? GR_INC : GR_AGG, mine), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  u64 excl = 0;
+  if (tile > 0) {
+    long long j = (long long)tile - 1;
+    u32 spins = 0;
+    while (j >= 0) {
+      const u64 g = __hip_atomic_load(&granules[(u64)j * RS_BINS + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const u32 ep = (u32)(g >> 40);
+      const u64 fl = (g >> 38) & 3ull;
+      if (ep != (epoch & 0xFFFFFFu) || fl == 0) {
+        if (++spins > (1u << 22)) {
+          atomicOr(err, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      excl += g & ((1ull << 38) - 1);
+      if (fl == GR_INC) break;
+      --j;
+    }
+    __hip_atomic_store(&G[t], gr_pack(epoch, GR_INC, excl + mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  base_run[t] = gbase + (u32)excl;
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const u64 i = t0 + (u64)r * RS_THREADS + t;
+    const bool valid = i < n;
+    const u64 k = kr[r];
+    const V v = vr[r];
     const u32 d = (u32)((k >> shift) & 0xFF);
 #pragma unroll
     for (int w = 0; w < RS_WAVES; ++w) wcnt[w][t] = 0;
@@ -87,8 +243,6 @@ __global__ void __launch_bounds__(RS_THREADS) rs_scatter_kernel(const u64* keys_
 #pragma unroll
     for (int w = 0; w < RS_WAVES; ++w) tot += wcnt[w][t];
     base_run[t] += tot;
-    // next round clears wcnt after this barrier-free update: base_run[t] is
-    // only read after the next round's first barrier.
   }
 }
 
@@ -232,6 +386,57 @@ __global__ void bincount_kernel(const u32* ids, u64 n, u32 nbins, long long* cou
     if (sh[b]) atomicAdd((unsigned long long*)&counts[b], (unsigned long long)sh[b]);
 }
 
+// After sorting by a composite key c = (part << 56) | (hi >> 8), finish the
+// (part, hi, lo) order: runs of equal c (same partition and same first 7 key
+// bytes) are insertion-sorted by (hi & 0xFF, lo) together with their payload
+// columns.  Runs longer than FIX_MAX set *bad (caller falls back to the full
+// 136-bit sort).
+constexpr int FIX_MAX = 64;
+__global__ void tie_fixup_kernel(const u64* c, u64* hi, u64* lo, long long* val, u64* rep, u32* part, u64 n,
+                                 u32* bad) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (i > 0 && c[i] == c[i - 1]) continue;  // not a run head
+    u64 e = i + 1;
+    while (e < n && c[e] == c[i] && e - i <= (u64)FIX_MAX) ++e;
+    if (e - i <= 1) continue;
+    if (e - i > (u64)FIX_MAX) {
+      atomicOr(bad, 1u);
+      continue;
+    }
+    for (u64 a = i + 1; a < e; ++a) {  // insertion sort on (hi, lo)
+      const u64 h = hi[a], l = lo[a], r = rep[a];
+      const long long v = val[a];
+      const u32 p = part[a];
+      u64 b = a;
+      while (b > i && (hi[b - 1] > h || (hi[b - 1] == h && lo[b - 1] > l))) {
+        hi[b] = hi[b - 1];
+        lo[b] = lo[b - 1];
+        val[b] = val[b - 1];
+        rep[b] = rep[b - 1];
+        part[b] = part[b - 1];
+        --b;
+      }
+      hi[b] = h;
+      lo[b] = l;
+      val[b] = v;
+      rep[b] = r;
+      part[b] = p;
+    }
+    // bit 2: two adjacent keys share the 8-byte prefix and one is a long
+    // (hashed) key -> their relative order needs a bytewise check on the host
+    for (u64 a = i + 1; a < e; ++a)
+      if (hi[a] == hi[a - 1] && part[a] == part[a - 1] && (key_is_long(lo[a]) || key_is_long(lo[a - 1])))
+        atomicOr(bad, 2u);
+  }
+}
+
+__global__ void composite_key_kernel(const u32* part, const u64* hi, u64 n, u64* out) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = ((u64)part[i] << 56) | (hi[i] >> 8);
+}
+
 }  // namespace mr
 
 using namespace mr;
@@ -243,9 +448,40 @@ static inline int grid_n(u64 n, int block, int maxg = 8192) {
   return (int)g;
 }
 
+// single-launch exclusive scan for small arrays (<= 1024 * 64 elements)
+constexpr int SS_THREADS = 1024;
+template <typename T>
+__global__ void __launch_bounds__(SS_THREADS) scan_small_kernel(const T* in, T* out, u64 n, T* total) {
+  __shared__ T sh[SS_THREADS];
+  const int t = threadIdx.x;
+  const u64 per = (n + SS_THREADS - 1) / SS_THREADS;
+  const u64 b = (u64)t * per;
+  T s = 0;
+  for (u64 i = b; i < b + per && i < n; ++i) s += in[i];
+  sh[t] = s;
+  __syncthreads();
+  for (int o = 1; o < SS_THREADS; o <<= 1) {
+    const T y = t >= o ? sh[t - o] : (T)0;
+    __syncthreads();
+    sh[t] += y;
+    __syncthreads();
+  }
+  T off = sh[t] - s;
+  for (u64 i = b; i < b + per && i < n; ++i) {
+    const T x = in[i];
+    out[i] = off;
+    off += x;
+  }
+  if (t == SS_THREADS - 1 && total) *total = sh[t];
+}
+
 template <typename T>
 static int scan_impl(const T* in, T* out, u64 n, T* partials, T* total, hipStream_t s) {
   if (n == 0) return 0;
+  if (n <= (u64)SS_THREADS * 64) {
+    hipLaunchKernelGGL(scan_small_kernel<T>, dim3(1), dim3(SS_THREADS), 0, s, in, out, n, total);
+    return (int)hipGetLastError();
+  }
   const u64 nt = (n + SC_TILE - 1) / SC_TILE;
   hipLaunchKernelGGL(scan_reduce_kernel<T>, dim3((unsigned)nt), dim3(SC_THREADS), 0, s, in, n, partials);
   hipLaunchKernelGGL(scan_partials_kernel<T>, dim3(1), dim3(SC_THREADS), 0, s, partials, nt, total);
@@ -278,6 +514,28 @@ int mr_radix_pass_u32v(const void* keys_in, const void* vals_in, void* keys_out,
   if (e) return e;
   hipLaunchKernelGGL(rs_scatter_kernel<u32>, dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
                      (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)hist_ws, nt);
+  return (int)hipGetLastError();
+}
+
+// Global histograms of all 8 digits of a u64 word (ghist: 2048 u32, zeroed by caller).
+int mr_radix_ghist8(const void* keys, u64 n, void* ghist, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(rs_ghist8_kernel, dim3(grid_n(n, RS_THREADS, 1024)), dim3(RS_THREADS), 0, s,
+                     (const u64*)keys, n, (u32*)ghist);
+  return (int)hipGetLastError();
+}
+
+// One onesweep pass on the 8-bit digit at `shift` (ghist: that digit's 256 bins;
+// granules: tiles*256 u64, never needs clearing — entries are epoch tagged;
+// tile_counter: one u32 zeroed before the pass; epoch unique per pass).
+int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
+                           const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err,
+                           hipStream_t s) {
+  if (n == 0) return 0;
+  const u32 nt = (u32)((n + RS_TILE - 1) / RS_TILE);
+  hipLaunchKernelGGL(rs_onesweep_kernel<u32>, dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
+                     (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
+                     (u64*)granules, (u32*)tile_counter, epoch, (u32*)err);
   return (int)hipGetLastError();
 }
 
@@ -315,6 +573,21 @@ int mr_segment_keys(const void* seg_excl, const void* heads, const void* hi, con
   hipLaunchKernelGGL(segment_keys_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u32*)seg_excl,
                      (const u32*)heads, (const u64*)hi, (const u64*)lo, (const u64*)rep, n, (u64*)out_hi,
                      (u64*)out_lo, (u64*)out_rep, (u64*)out_start);
+  return (int)hipGetLastError();
+}
+
+int mr_composite_key(const void* part, const void* hi, u64 n, void* out, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(composite_key_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u32*)part, (const u64*)hi,
+                     n, (u64*)out);
+  return (int)hipGetLastError();
+}
+
+int mr_tie_fixup(const void* c, void* hi, void* lo, void* val, void* rep, void* part, u64 n, void* bad,
+                 hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(tie_fixup_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)c, (u64*)hi, (u64*)lo,
+                     (long long*)val, (u64*)rep, (u32*)part, n, (u32*)bad);
   return (int)hipGetLastError();
 }
 

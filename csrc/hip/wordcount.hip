@@ -193,6 +193,7 @@ __global__ void __launch_bounds__(WC_THREADS) wc_map_kernel(TxtView v, u64 chunk
   const u64 chunk_begin = (u64)blockIdx.x * chunk_bytes;
   if (chunk_begin >= v.nbytes) return;
   const u64 chunk_end = min(chunk_begin + chunk_bytes, v.nbytes);
+  u32 claims = 0;
   for (int s = t; s < WC_LDS_SLOTS; s += WC_THREADS) {
     L.tag[s] = 0;
     L.lo[s] = 0;
@@ -208,7 +209,7 @@ __global__ void __launch_bounds__(WC_THREADS) wc_map_kernel(TxtView v, u64 chunk
     __syncthreads();
     for_each_token(v, tile_base, txt, chunk_end, [&](u64 hi, u64 lo, u64 gpos, u64 len) {
       const u64 rep = make_rep(rep_base + gpos, len);
-      if (!lds_insert(L, hi, lo, rep)) gtab_insert(g, hi, lo, 1, rep, OP_SUM);
+      if (!lds_insert(L, hi, lo, rep)) claims += gtab_insert(g, hi, lo, 1, rep, OP_SUM) == 2;
     });
     __syncthreads();
     if (t == 0) txt[WC_PAD - 1] = txt[WC_PAD + WC_TILE - 1];
@@ -216,8 +217,9 @@ __global__ void __launch_bounds__(WC_THREADS) wc_map_kernel(TxtView v, u64 chunk
   }
   // flush the workgroup's partial counts (the combiner output) to HBM
   for (int s = t; s < WC_LDS_SLOTS; s += WC_THREADS) {
-    if (L.tag[s] != 0) gtab_insert(g, L.hi[s], L.lo[s], (long long)L.cnt[s], L.rep[s], OP_SUM);
+    if (L.tag[s] != 0) claims += gtab_insert(g, L.hi[s], L.lo[s], (long long)L.cnt[s], L.rep[s], OP_SUM) == 2;
   }
+  gtab_count_claims(g, claims);
 }
 
 // Per-token emit (no combining): writes one (hi, lo, rep) triple per token,
@@ -293,31 +295,54 @@ __global__ void __launch_bounds__(WC_THREADS) count_tokens_kernel(TxtView v, u64
 __global__ void hash_agg_kernel(const u64* hi, const u64* lo, const long long* val, const u64* rep, u64 n, GTab g,
                                int op, u64 rep_add) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
+  u32 claims = 0;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const u64 r = rep ? rep[i] + (rep_add << REP_LEN_BITS) : 0;
-    gtab_insert(g, hi[i], lo[i], val ? val[i] : 1ll, r, op);
+    claims += gtab_insert(g, hi[i], lo[i], val ? val[i] : 1ll, r, op) == 2;
   }
+  gtab_count_claims(g, claims);
 }
 
-// Compact occupied slots into dense arrays (order is not deterministic; the
-// caller sorts afterwards).  One atomic per wave (ballot + mbcnt).
-__global__ void table_compact_kernel(GTab g, u64 cap, u64* out_hi, u64* out_lo, long long* out_val, u64* out_rep,
-                                     unsigned long long* counter) {
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  const int lane = threadIdx.x & 63;
-  for (u64 base = (u64)blockIdx.x * blockDim.x; base < cap; base += stride) {
-    const u64 i = base + threadIdx.x;
-    const bool occ = i < cap && g.tag[i] != 0;
-    const unsigned long long m = __ballot(occ);
-    unsigned long long wbase = 0;
-    if (lane == 0 && m) wbase = atomicAdd(counter, (unsigned long long)__popcll(m));
-    wbase = __shfl(wbase, 0);
-    if (occ) {
-      const u64 o = wbase + __popcll(m & ((1ull << lane) - 1ull));
+// Compact occupied slots into dense arrays.  Each 256-thread block owns a
+// contiguous range of 4096 slots: per-thread counts -> LDS scan -> ONE atomic
+// per block for the output base (a per-wave atomic on one counter serialised
+// ~3e4 same-address atomics: 0.4 ms for a 2M-slot table).
+constexpr int CP_ITEMS = 16;
+__global__ void __launch_bounds__(256) table_compact_kernel(GTab g, u64 cap, u64* out_hi, u64* out_lo,
+                                                            long long* out_val, u64* out_rep,
+                                                            unsigned long long* counter) {
+  __shared__ u32 sh[256];
+  __shared__ unsigned long long base;
+  const int t = threadIdx.x;
+  const u64 b0 = (u64)blockIdx.x * 256 * CP_ITEMS;
+  u32 occ = 0, n = 0;
+#pragma unroll
+  for (int k = 0; k < CP_ITEMS; ++k) {
+    const u64 i = b0 + (u64)k * 256 + t;
+    const bool o = i < cap && g.tag[i] != 0;
+    occ |= (o ? 1u : 0u) << k;
+    n += o ? 1u : 0u;
+  }
+  sh[t] = n;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const u32 y = t >= o ? sh[t - o] : 0u;
+    __syncthreads();
+    sh[t] += y;
+    __syncthreads();
+  }
+  if (t == 255) base = atomicAdd(counter, (unsigned long long)sh[255]);
+  __syncthreads();
+  u64 o = base + sh[t] - n;
+#pragma unroll
+  for (int k = 0; k < CP_ITEMS; ++k) {
+    if (occ & (1u << k)) {
+      const u64 i = b0 + (u64)k * 256 + t;
       out_hi[o] = g.hi[i];
       out_lo[o] = g.lo[i];
       out_val[o] = g.val[i];
       out_rep[o] = g.rep[i];
+      ++o;
     }
   }
 }
@@ -436,7 +461,8 @@ int mr_hash_agg(const void* hi, const void* lo, const void* val, const void* rep
 
 int mr_table_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, void* out_hi,
                      void* out_lo, void* out_val, void* out_rep, void* counter, hipStream_t stream) {
-  hipLaunchKernelGGL(table_compact_kernel, dim3(grid_for(cap, 256, 4096)), dim3(256), 0, stream,
+  const u64 nb = (cap + 256 * CP_ITEMS - 1) / (256 * CP_ITEMS);
+  hipLaunchKernelGGL(table_compact_kernel, dim3((unsigned)nb), dim3(256), 0, stream,
                      make_gtab(tag, hi, lo, val, rep, ctrl, cap), cap, (u64*)out_hi, (u64*)out_lo,
                      (long long*)out_val, (u64*)out_rep, (unsigned long long*)counter);
   return (int)hipGetLastError();

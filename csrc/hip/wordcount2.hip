@@ -119,15 +119,15 @@ __device__ __forceinline__ bool lds_insert(Lds& L, u64 hi, u64 lo, u32 rep) {
   return false;
 }
 
-__device__ __forceinline__ void overflow_push(const Ovf& o, const GTab& g, u64 hi, u64 lo, u64 rep) {
+__device__ __forceinline__ u32 overflow_push(const Ovf& o, const GTab& g, u64 hi, u64 lo, u64 rep) {
   const unsigned long long idx = atomicAdd(o.counter, 1ull);
   if (idx < o.cap) {
     o.hi[idx] = hi;
     o.lo[idx] = lo;
     o.rep[idx] = rep;
-  } else {
-    gtab_insert(g, hi, lo, 1, rep, OP_SUM);
+    return 0;
   }
+  return gtab_insert(g, hi, lo, 1, rep, OP_SUM) == 2;
 }
 
 template <int MODE>
@@ -152,6 +152,7 @@ __global__ void __launch_bounds__(T) wc_map2_kernel(const u8* __restrict__ text,
     L.ws[WSW - 1] = 0xFFFFFFFFu;
   }
   u64 acc = 0;
+  u32 claims = 0;
   u16* ws16 = reinterpret_cast<u16*>(L.ws);
   const u32* txt32 = reinterpret_cast<const u32*>(L.txt);
   for (u64 tile_base = chunk_begin; tile_base < chunk_end; tile_base += TILE) {
@@ -247,7 +248,7 @@ __global__ void __launch_bounds__(T) wc_map2_kernel(const u8* __restrict__ text,
         }
         const u64 grep = make_rep(rep_base + gpos, len);
         const bool ok = len < 65536 && lds_insert(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16));
-        if (!ok && MODE == FULL) overflow_push(ovf, g, hi, lo, grep);
+        if (!ok && MODE == FULL) claims += overflow_push(ovf, g, hi, lo, grep);
       }
     }
     __syncthreads();
@@ -265,18 +266,21 @@ __global__ void __launch_bounds__(T) wc_map2_kernel(const u8* __restrict__ text,
   for (int s = t; s < SLOTS; s += T) {
     if (L.tag[s] != 0) {
       const u32 r = L.rep[s];
-      gtab_insert(g, L.hi[s], L.lo[s], (long long)L.cnt[s], make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16),
-                  OP_SUM);
+      claims += gtab_insert(g, L.hi[s], L.lo[s], (long long)L.cnt[s],
+                            make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16), OP_SUM) == 2;
     }
   }
+  gtab_count_claims(g, claims);
 }
 
 __global__ void __launch_bounds__(256) ovf_agg_kernel(Ovf o, GTab g) {
   const unsigned long long n0 = *o.counter;
   const u64 n = n0 < o.cap ? n0 : o.cap;
   const u64 stride = (u64)gridDim.x * blockDim.x;
+  u32 claims = 0;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    gtab_insert(g, o.hi[i], o.lo[i], 1, o.rep[i], OP_SUM);
+    claims += gtab_insert(g, o.hi[i], o.lo[i], 1, o.rep[i], OP_SUM) == 2;
+  gtab_count_claims(g, claims);
 }
 
 }  // namespace v2

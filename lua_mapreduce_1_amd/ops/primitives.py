@@ -282,12 +282,30 @@ def gather_key_bytes(hi, lo, rep, src, lengths: torch.Tensor | None = None):
 
 
 # ---------------------------------------------------------------------------
-def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None) -> torch.Tensor:
+_EPOCH = [0]
+_SORT_WS: dict = {}
+
+
+def _sort_ws(d, n: int):
+    """Per-device workspace for the onesweep sort (grown, never shrunk)."""
+    tiles = (n + 4095) // 4096
+    ws = _SORT_WS.get(d)
+    if ws is None or ws["tiles"] < tiles:
+        ws = {"tiles": max(tiles, 64),
+              "granules": torch.zeros(max(tiles, 64) * 256, dtype=torch.int64, device=d),
+              "small": torch.zeros(2048 + 64 + 1, dtype=torch.int32, device=d)}
+        _SORT_WS[d] = ws
+    return ws
+
+
+def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: str = "onesweep") -> torch.Tensor:
     """Stable permutation sorting rows by unsigned multi-word keys.
 
     ``words[0]`` is the most significant u64 word.  ``bits[j]`` limits the
     number of low bits of word j that participate (e.g. partition ids).
-    Returns int32 (GPU) / int64 (CPU) permutation.
+    Returns int32 (GPU) / int64 (CPU) permutation.  GPU: LSD radix sort, one
+    onesweep launch per 8-bit digit (``method="onesweep"``) or the 3-phase
+    histogram/scan/scatter passes (``method="3phase"``).
     """
     n = words[0].numel()
     bits = bits or [64] * len(words)
@@ -297,14 +315,21 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None) -> torch
             return torch.zeros(0, dtype=torch.int32, device=d)
         lib = _hip.lib()
         s = _hip.stream(d)
-        tiles = int(lib.mr_rs_tiles(n))
-        hist = torch.empty(256 * tiles, dtype=torch.int32, device=d)
-        scan_ws = torch.empty(int(lib.mr_scan_partials_len(256 * tiles)), dtype=torch.int32, device=d)
         perm = torch.empty(n, dtype=torch.int32, device=d)
         _hip.call("mr_iota_u32", _hip.ptr(perm), n, s)
         perm2 = torch.empty_like(perm)
         k1 = torch.empty(n, dtype=torch.int64, device=d)
         k2 = torch.empty_like(k1)
+        if method == "onesweep":
+            ws = _sort_ws(d, n)
+            small = ws["small"]
+            small.zero_()  # [0:2048) ghist, [2048:2112) tile counters, [2112] error flag
+            ghist = small[:2048]
+            pass_id = 0
+        else:
+            tiles = int(lib.mr_rs_tiles(n))
+            hist = torch.empty(256 * tiles, dtype=torch.int32, device=d)
+            scan_ws = torch.empty(int(lib.mr_scan_partials_len(256 * tiles)), dtype=torch.int32, device=d)
         first = True
         for w, nb in zip(reversed(words), reversed(bits)):
             if first:
@@ -312,9 +337,20 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None) -> torch
                 first = False
             else:
                 _hip.call("mr_gather_u64", _hip.ptr(w), _hip.ptr(perm), _hip.ptr(k1), n, s)
+            if method == "onesweep":
+                if pass_id:
+                    ghist.zero_()
+                _hip.call("mr_radix_ghist8", _hip.ptr(k1), n, _hip.ptr(ghist), s)
             for shift in range(0, nb, 8):
-                _hip.call("mr_radix_pass_u32v", _hip.ptr(k1), _hip.ptr(perm), _hip.ptr(k2), _hip.ptr(perm2), n,
-                          shift, _hip.ptr(hist), _hip.ptr(scan_ws), s)
+                if method == "onesweep":
+                    _EPOCH[0] = (_EPOCH[0] + 1) & 0xFFFFFF or 1
+                    _hip.call("mr_radix_onesweep_u32v", _hip.ptr(k1), _hip.ptr(perm), _hip.ptr(k2), _hip.ptr(perm2),
+                              n, shift, _hip.ptr(ghist[shift // 8 * 256:]), _hip.ptr(ws["granules"]),
+                              _hip.ptr(small[2048 + pass_id:]), _EPOCH[0], _hip.ptr(small[2112:]), s)
+                    pass_id += 1
+                else:
+                    _hip.call("mr_radix_pass_u32v", _hip.ptr(k1), _hip.ptr(perm), _hip.ptr(k2), _hip.ptr(perm2), n,
+                              shift, _hip.ptr(hist), _hip.ptr(scan_ws), s)
                 k1, k2 = k2, k1
                 perm, perm2 = perm2, perm
         return perm
@@ -323,6 +359,41 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None) -> torch
         if nb < 64:
             cols[j] = cols[j] & np.uint64((1 << nb) - 1)
     return torch.from_numpy(np.lexsort(tuple(reversed(cols))).astype(np.int64))
+
+
+def sort_by_partition_key(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, val: torch.Tensor,
+                          rep: torch.Tensor, nparts: int):
+    """Rows ordered by (partition, hi, lo) -> (part, hi, lo, val, rep, bad).
+
+    GPU fast path (nparts <= 256): radix-sort ONE u64 composite word
+    ``part << 56 | hi >> 8`` (8 passes instead of 17) and insertion-sort the
+    short runs that tie on it by (hi, lo) in a fixup kernel; ``bad`` (device
+    int32) is non-zero when a run exceeded the fixup limit, in which case the
+    caller must use the full multi-word sort.  CPU: lexsort.
+    """
+    n = hi.numel()
+    if not hi.is_cuda or nparts > 256:
+        perm = sort_keys([part.to(torch.int64), hi, lo], bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
+        # bit 2: the host must check the order of long keys sharing a prefix
+        bad = torch.full((1,), 2, dtype=torch.int32, device=hi.device)
+        return part[perm], hi[perm], lo[perm], val[perm], rep[perm], bad
+    d = hi.device
+    s = _hip.stream(d)
+    part = part.to(torch.int32).contiguous()
+    c = torch.empty(n, dtype=torch.int64, device=d)
+    _hip.call("mr_composite_key", _hip.ptr(part), _hip.ptr(hi), n, _hip.ptr(c), s)
+    perm = sort_keys([c]).long()
+    c, part, hi, lo, val, rep = c[perm], part[perm], hi[perm], lo[perm], val[perm], rep[perm]
+    bad = torch.zeros(1, dtype=torch.int32, device=d)
+    _hip.call("mr_tie_fixup", _hip.ptr(c), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part),
+              n, _hip.ptr(bad), s)
+    return part, hi, lo, val, rep, bad
+
+
+def sort_error(device) -> bool:
+    """True if a onesweep look-back gave up (result of that sort is invalid)."""
+    ws = _SORT_WS.get(torch.device(device))
+    return bool(ws is not None and int(ws["small"][2112].item()) != 0)
 
 
 def bincount(ids: torch.Tensor, nbins: int) -> torch.Tensor:

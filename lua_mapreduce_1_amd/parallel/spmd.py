@@ -95,7 +95,7 @@ class IterationResult:
 
 class SPMDEngine:
     def __init__(self, params: dict, group=None, device=None, split_store: SplitStore | None = None,
-                 chunk_mb: tuple = (4, 8, 16, 32), verbose: bool = False, table_capacity: int = 1 << 21):
+                 chunk_mb: tuple = (6, 16, 32), verbose: bool = False, table_capacity: int = 1 << 20):
         self.params = dict(params)
         self.group = group
         self.rank, self.world = D.world_info(group)
@@ -345,7 +345,7 @@ class SPMDEngine:
                 r.status, r.started, r.written, r.worker = STATUS.WRITTEN, t1, time.time(), self.rank
                 r.real_time = r.written - t1
                 res.red_jobs.append(r)
-        res.distinct_keys = int(cols["hi"].size)
+        res.distinct_keys = int(cols["val"].size)
         res.total_value = int(cols["val"].sum()) if cols["val"].size else 0
         T["reduce"] = time.time() - t2
         T["iteration"] = time.time() - t_start

@@ -130,57 +130,116 @@ def fix_long_key_order(hi: np.ndarray, lo: np.ndarray, off: np.ndarray, blob: np
 
     Keys are sorted by (hi, lo); for long keys lo is a hash, so runs sharing the
     8-byte prefix ``hi`` that contain a long key are re-sorted by their bytes.
+    Returns None when the order is already exact (the common case).
     """
     n = hi.size
-    perm = np.arange(n)
-    if n == 0:
-        return perm
+    if n < 2:
+        return None
     is_long = (lo & np.uint64(0xFF)) == np.uint64(0xFF)
     if not is_long.any():
-        return perm
-    starts = np.flatnonzero(np.concatenate([[True], hi[1:] != hi[:-1]]))
+        return None
+    same = hi[1:] == hi[:-1]
+    if not ((is_long[1:] | is_long[:-1]) & same).any():
+        return None
+    perm = np.arange(n)
+    starts = np.flatnonzero(np.concatenate([[True], ~same]))
     ends = np.concatenate([starts[1:], [n]])
     has_long = np.add.reduceat(is_long.astype(np.int64), starts) > 0
     b = blob.tobytes() if isinstance(blob, np.ndarray) else bytes(blob)
+    changed = False
     for s, e in zip(starts[has_long], ends[has_long]):
         if e - s > 1:
             idx = list(range(s, e))
             idx.sort(key=lambda i: b[off[i]:off[i + 1]])
-            perm[s:e] = idx
-    return perm
+            if idx != list(range(s, e)):
+                perm[s:e] = idx
+                changed = True
+    return perm if changed else None
 
 
-def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: torch.Tensor | None = None):
+class _PinnedPool:
+    """Reusable pinned host buffers for device -> host result copies."""
+
+    def __init__(self):
+        self.bufs: dict[str, torch.Tensor] = {}
+
+    def get(self, name: str, n: int, dtype) -> torch.Tensor:
+        b = self.bufs.get(name)
+        if b is None or b.numel() < n or b.dtype != dtype:
+            b = torch.empty(max(n, 1024) * 5 // 4, dtype=dtype, pin_memory=torch.cuda.is_available())
+            self.bufs[name] = b
+        return b[:n]
+
+
+_POOL = _PinnedPool()
+
+
+def _to_host(t: torch.Tensor, name: str) -> torch.Tensor:
+    if not t.is_cuda:
+        return t
+    h = _POOL.get(name, t.numel(), t.dtype)
+    h.copy_(t, non_blocking=True)
+    return h
+
+
+def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: torch.Tensor | None = None,
+             _presorted: bool = False, need_keys: bool = False):
     """Partition, sort by (partition, key) and materialise key bytes.
 
     Returns a dict of host numpy arrays: hi, lo, val, key_off, key_blob and
-    ``bounds`` (partition p occupies rows bounds[p]:bounds[p+1]).
+    ``bounds`` (partition p occupies rows bounds[p]:bounds[p+1]).  All device
+    work is queued first; results come back through reusable pinned buffers
+    with a single synchronisation.  NOTE: the arrays alias the pinned pool and
+    stay valid until the next finalize() call (copy them to keep them longer).
     """
     n = hi.numel()
     if part is None:
         part = partition_of(hi, lo, rep, src, nparts, partition_module)
-    perm = ops.sort_keys([part.to(torch.int64), hi, lo], bits=[max(8, int(nparts - 1).bit_length()), 64, 64])
-    perm = perm.long()
-    hi, lo, val, rep, part = hi[perm], lo[perm], val[perm], rep[perm], part[perm]
+    args = (hi, lo, val, rep)
+    if _presorted:
+        bad = torch.zeros(1, dtype=torch.int32, device=hi.device)
+    else:
+        part, hi, lo, val, rep, bad = ops.sort_by_partition_key(part, hi, lo, val, rep, nparts)
     off, blob = ops.gather_key_bytes(hi, lo, rep, src)
-    counts = ops.bincount(part, nparts).cpu().numpy() if n else np.zeros(nparts, np.int64)
+    counts = ops.bincount(part, nparts) if n else torch.zeros(nparts, dtype=torch.int64, device=hi.device)
+    if hi.is_cuda:
+        hv = _to_host(val, "val")
+        ho = _to_host(off.to(torch.int32), "off32") if blob.numel() < 2**31 else _to_host(off, "off64")
+        hb = _to_host(blob, "blob")
+        hc = _to_host(counts, "counts")
+        hbad = _to_host(bad, "bad")
+        torch.cuda.current_stream(hi.device).synchronize()
+        flag = int(hbad[0])
+        if flag & 1:
+            # a tie run was too long for the fixup kernel: redo with the full sort
+            ahi, alo, aval, arep = args
+            p2 = partition_of(ahi, alo, arep, src, nparts, partition_module)
+            perm = ops.sort_keys([p2.to(torch.int64), ahi, alo],
+                                 bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
+            return finalize(ahi[perm], alo[perm], aval[perm], arep[perm], src, nparts, partition_module,
+                            part=p2[perm], _presorted=True, need_keys=need_keys)
+        h_val, h_off, h_blob, h_counts = hv.numpy(), ho.numpy().astype(np.int64), hb.numpy(), hc.numpy()
+        need_fix = bool(flag & 2) or _presorted
+        h_hi = hi.cpu().numpy().view(np.uint64) if (need_fix or need_keys) else None
+        h_lo = lo.cpu().numpy().view(np.uint64) if (need_fix or need_keys) else None
+    else:
+        h_hi, h_lo = hi.numpy().view(np.uint64), lo.numpy().view(np.uint64)
+        h_val, h_off, h_blob, h_counts = val.numpy(), off.numpy(), blob.numpy(), counts.numpy()
+        need_fix = True
     bounds = np.zeros(nparts + 1, np.int64)
-    np.cumsum(counts, out=bounds[1:])
-    out = {"hi": hi.cpu().numpy().view(np.uint64), "lo": lo.cpu().numpy().view(np.uint64),
-           "val": val.cpu().numpy(), "key_off": off.cpu().numpy(), "key_blob": blob.cpu().numpy(),
-           "bounds": bounds}
-    # exact bytewise order inside each partition (long keys)
-    perms = []
-    for p in range(nparts):
-        a, b = int(bounds[p]), int(bounds[p + 1])
-        if b - a > 1:
-            pp = fix_long_key_order(out["hi"][a:b], out["lo"][a:b], out["key_off"][a:b + 1] - 0, out["key_blob"])
-            perms.append(pp + a)
-        else:
-            perms.append(np.arange(a, b))
-    gp = np.concatenate(perms) if perms else np.zeros(0, np.int64)
-    if not np.array_equal(gp, np.arange(n)):
-        out = reorder(out, gp)
+    np.cumsum(h_counts, out=bounds[1:])
+    out = {"hi": h_hi, "lo": h_lo, "val": h_val, "key_off": h_off, "key_blob": h_blob, "bounds": bounds}
+    if need_fix:
+        # exact bytewise order inside each partition (long keys sharing a prefix)
+        perms = []
+        for p in range(nparts):
+            a, b = int(bounds[p]), int(bounds[p + 1])
+            pp = fix_long_key_order(h_hi[a:b], h_lo[a:b], h_off[a:b + 1], h_blob) if b - a > 1 else None
+            perms.append(None if pp is None else pp + a)
+        if any(pp is not None for pp in perms):
+            gp = np.concatenate([pp if pp is not None else np.arange(int(bounds[p]), int(bounds[p + 1]))
+                                 for p, pp in enumerate(perms)])
+            out = reorder(out, gp)
     return out
 
 
@@ -201,5 +260,6 @@ def reorder(cols: dict, perm: np.ndarray) -> dict:
 def partition_slice(cols: dict, p: int) -> dict:
     a, b = int(cols["bounds"][p]), int(cols["bounds"][p + 1])
     off = cols["key_off"][a:b + 1]
-    return {"hi": cols["hi"][a:b], "lo": cols["lo"][a:b], "val": cols["val"][a:b], "key_off": off - off[0],
-            "key_blob": cols["key_blob"][off[0]:off[-1]]}
+    return {"hi": None if cols["hi"] is None else cols["hi"][a:b],
+            "lo": None if cols["lo"] is None else cols["lo"][a:b], "val": cols["val"][a:b],
+            "key_off": off - off[0], "key_blob": cols["key_blob"][off[0]:off[-1]]}

@@ -204,7 +204,7 @@ class job:  # noqa: N801
         ctx.flush_host_pairs()
         self.mark_as_finished()
         hi, lo, val, rep = ctx.table.compact()
-        cols = dev.finalize(hi, lo, val, rep, ctx.source(), nparts, pmod)
+        cols = dev.finalize(hi, lo, val, rep, ctx.source(), nparts, pmod, need_keys=True)
         fs, make_builder, _ = fsmod.router(self.cnn, None, self.storage, self.path)
         for p in range(nparts):
             if cols["bounds"][p + 1] == cols["bounds"][p]:
@@ -284,7 +284,7 @@ def _device_reduce(blobs: list[bytes], op: str) -> bytes:
     tab.insert(hi, lo, val, rep)
     uhi, ulo, uval, urep = tab.compact()
     out = dev.finalize(uhi, ulo, uval, urep, src, 1, None, part=torch.zeros(uhi.numel(), dtype=torch.int32,
-                                                                              device=d))
+                                                                              device=d), need_keys=True)
     return codec.encode_columnar(out["hi"], out["lo"], out["val"], out["key_off"], out["key_blob"])
 
 

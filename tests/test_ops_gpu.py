@@ -142,3 +142,56 @@ def test_hash_agg_pairs(gpu):
         ga = {(int(x), int(y)): int(z) for x, y, z in zip(a[0].cpu()[pa], a[1].cpu()[pa], a[2].cpu()[pa])}
         gb = {(int(x), int(y)): int(z) for x, y, z in zip(b[0], b[1], b[2])}
         assert ga == gb
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4097, 100_000, 2_000_003])
+@pytest.mark.parametrize("method", ["onesweep", "3phase"])
+def test_sort_methods(gpu, n, method):
+    rng = np.random.default_rng(n)
+    w0 = torch.from_numpy(rng.integers(0, 10, n).astype(np.int64))
+    w1 = torch.from_numpy(rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64))
+    w1[1::3] = 42  # many ties + a uniform-ish digit pattern
+    pg = ops.sort_keys([w0.to(gpu), w1.to(gpu)], bits=[8, 64], method=method).cpu().long()
+    pc = ops.sort_keys([w0, w1], bits=[8, 64])
+    assert torch.equal(pg, pc)
+    from lua_mapreduce_1_amd.ops.primitives import sort_error
+    assert not sort_error(gpu)
+
+
+@pytest.mark.parametrize("runlen", [3, 200])
+def test_sort_by_partition_key(gpu, runlen):
+    rng = np.random.default_rng(runlen)
+    n = 50_000
+    hi = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64)
+    hi[: runlen * 20] = (hi[: runlen * 20] & ~0xFF) | 0  # ...
+    hi[: runlen * 20] = np.repeat(rng.integers(-2**63, 2**63 - 1, 20, dtype=np.int64), runlen)
+    hi[: runlen * 20] ^= rng.integers(0, 256, runlen * 20)  # same top 7 bytes, different low byte
+    lo = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64)
+    part = rng.integers(0, 3, n).astype(np.int32)
+    part[: runlen * 20] = 1
+    val = np.arange(n, dtype=np.int64)
+    t = [torch.from_numpy(x) for x in (part, hi, lo, val, val.copy())]
+    g = ops.sort_by_partition_key(*[x.to(gpu) for x in t], 3)
+    c = ops.sort_by_partition_key(*t, 3)
+    bad = int(g[5].item())
+    if runlen > 64:
+        assert bad == 1
+    else:
+        assert bad == 0
+        for a, b in zip(g[:5], c[:5]):
+            assert torch.equal(a.cpu().long(), b.long())
+
+
+def test_finalize_long_tie_runs(gpu):
+    from lua_mapreduce_1_amd.runtime import device as dv
+    words = [b"abcdefg" + bytes([65 + i % 26, 97 + i // 26]) for i in range(300)] + [b"x", b"y", b"abcdefgh" * 3]
+    text = b" ".join(words * 2) + b"\n"
+    t = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(gpu)
+    tab = ops.HashTable(1 << 12, device=gpu)
+    tab.wordcount_map(t)
+    hi, lo, val, rep = tab.compact()
+    cols = dv.finalize(hi, lo, val, rep, t, 1)
+    blob = cols["key_blob"].tobytes()
+    keys = [blob[cols["key_off"][i]:cols["key_off"][i + 1]] for i in range(len(cols["val"]))]
+    assert keys == sorted(set(words))
+    assert set(cols["val"].tolist()) == {2}
