@@ -437,6 +437,24 @@ __global__ void composite_key_kernel(const u32* part, const u64* hi, u64 n, u64*
     out[i] = ((u64)part[i] << 56) | (hi[i] >> 8);
 }
 
+// Device -> pinned-host copy whose length lives in device memory
+// (n_bytes = nelem[0] * elem_size, clamped to max_bytes): lets the result
+// download be queued without a host synchronisation to learn the size.
+// 16-byte stores when both ends are 16-byte aligned; system-scope fence at the
+// end so the host sees the data after the stream completes.
+__global__ void copy_to_host_kernel(const u8* src, u8* dst, const long long* nelem, u64 elem_size, u64 max_bytes) {
+  u64 nb = (u64)nelem[0] * elem_size;
+  if (nb > max_bytes) nb = max_bytes;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  const u64 tid = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
+  const u64 nv = vec ? nb / 16 : 0;
+  for (u64 i = tid; i < nv; i += stride)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  for (u64 i = nv * 16 + tid; i < nb; i += stride) dst[i] = src[i];
+  __threadfence_system();
+}
+
 }  // namespace mr
 
 using namespace mr;
@@ -573,6 +591,15 @@ int mr_segment_keys(const void* seg_excl, const void* heads, const void* hi, con
   hipLaunchKernelGGL(segment_keys_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u32*)seg_excl,
                      (const u32*)heads, (const u64*)hi, (const u64*)lo, (const u64*)rep, n, (u64*)out_hi,
                      (u64*)out_lo, (u64*)out_rep, (u64*)out_start);
+  return (int)hipGetLastError();
+}
+
+int mr_copy_to_host(const void* src, void* host_dst, const void* nelem, u64 elem_size, u64 max_bytes,
+                    hipStream_t s) {
+  void* dptr = nullptr;
+  if (hipHostGetDevicePointer(&dptr, host_dst, 0) != hipSuccess || dptr == nullptr) dptr = host_dst;
+  hipLaunchKernelGGL(copy_to_host_kernel, dim3(1024), dim3(256), 0, s, (const u8*)src, (u8*)dptr,
+                     (const long long*)nelem, elem_size, max_bytes);
   return (int)hipGetLastError();
 }
 

@@ -44,6 +44,7 @@ _SIGS = {
     "mr_segment_keys": [_p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p],
     "mr_bincount": [_p, _u64, _u32, _p, _p],
     "mr_composite_key": [_p, _p, _u64, _p, _p],
+    "mr_copy_to_host": [_p, _p, _p, _u64, _u64, _p],
     "mr_tie_fixup": [_p, _p, _p, _p, _p, _p, _u64, _p, _p],
     "mr_scan_partials_len": [_u64],
     "mr_rs_tiles": [_u64],

@@ -262,26 +262,40 @@ def exclusive_scan(x: torch.Tensor):
     return (c - x).to(x.dtype), tot
 
 
-def gather_key_bytes(hi, lo, rep, src, lengths: torch.Tensor | None = None):
-    """Materialise key bytes: (offsets int64[n+1], blob uint8)."""
+def gather_key_bytes(hi, lo, rep, src, lengths: torch.Tensor | None = None, capacity: int | None = None):
+    """Materialise key bytes: (offsets int64[n+1], blob uint8).
+
+    With ``capacity`` (GPU) the blob is allocated at that size and NOT trimmed,
+    so no host synchronisation is needed; the used size is ``offsets[-1]``
+    (a device value).  Any bound >= the total works, e.g. the byte size of the
+    text the keys came from (distinct keys occupy disjoint occurrences).
+    """
     n = hi.numel()
     if lengths is None:
         _, lengths = key_meta(hi, lo, rep, src, want_part=False)
     off, total = exclusive_scan(lengths)
     if hi.is_cuda:
         d = hi.device
-        nb = int(total.item())
-        blob = torch.empty(nb, dtype=torch.uint8, device=d)
+        nb = int(total.item()) if capacity is None else int(capacity)
+        blob = torch.empty(max(nb, 1), dtype=torch.uint8, device=d)
         srcp = _hip.ptr(src) if src is not None else None
         _hip.call("mr_gather_key_bytes", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), _hip.ptr(off), n, srcp,
                   _hip.ptr(blob), _hip.stream(d))
+        if capacity is None:
+            blob = blob[:nb]
         return torch.cat([off, total]), blob
     b = key_bytes_list(hi, lo, rep, src)
     blob = torch.frombuffer(bytearray(b"".join(b)), dtype=torch.uint8) if b else torch.zeros(0, dtype=torch.uint8)
     return torch.cat([off, total]), blob
 
 
-# ---------------------------------------------------------------------------
+def copy_to_host(t: torch.Tensor, host: torch.Tensor, nelem: torch.Tensor) -> None:
+    """Queue a device->pinned-host copy of ``nelem[0]`` elements of ``t``
+    (count read on the device; no host synchronisation)."""
+    _hip.call("mr_copy_to_host", _hip.ptr(t), _hip.ptr(host), _hip.ptr(nelem), t.element_size(),
+              host.numel() * host.element_size(), _hip.stream(t.device))
+
+
 _EPOCH = [0]
 _SORT_WS: dict = {}
 

@@ -95,7 +95,8 @@ class IterationResult:
 
 class SPMDEngine:
     def __init__(self, params: dict, group=None, device=None, split_store: SplitStore | None = None,
-                 chunk_mb: tuple = (6, 16, 32), verbose: bool = False, table_capacity: int = 1 << 20):
+                 chunk_mb: tuple = (6, 16, 32), verbose: bool = False, table_capacity: int = 1 << 20,
+                 tail_mb: tuple = (8, 3)):
         self.params = dict(params)
         self.group = group
         self.rank, self.world = D.world_info(group)
@@ -104,6 +105,9 @@ class SPMDEngine:
         self.device = torch.device(device)
         self.splits = split_store
         self.chunk_bytes = [int(c * (1 << 20)) for c in chunk_mb]
+        # the last chunks shrink again so the kernel that runs after the final
+        # H2D copy is short (the map is copy-bound on one PCIe link)
+        self.tail_bytes = [int(c * (1 << 20)) for c in tail_mb]
         self.verbose = verbose
         self.result_ns = self.params.get("result_ns") or "result"
         self.init_args = self.params.get("init_args")
@@ -187,15 +191,28 @@ class SPMDEngine:
             nbytes = b - a
             if self.arena is None or self.arena.numel() < nbytes:
                 self.arena = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-            # chunk boundaries at split boundaries, sizes growing 4 -> 32 MB
-            bounds = [0]
+            # chunk boundaries at split boundaries: sizes ramp up (first copy is
+            # exposed) and back down (last kernel is exposed)
+            offs = self.splits.offsets
+            sizes = []
+            rem = nbytes
+            tail = [t for t in self.tail_bytes]
             k = 0
-            while bounds[-1] < len(ids):
-                target = self.splits.offsets[ids[0] + bounds[-1]] + self.chunk_bytes[min(k, len(self.chunk_bytes) - 1)]
-                nxt = int(np.searchsorted(self.splits.offsets, target, side="left")) - ids[0]
-                nxt = max(bounds[-1] + 1, min(len(ids), nxt))
-                bounds.append(nxt)
+            while rem > 0:
+                if tail and rem <= sum(tail) + self.chunk_bytes[-1]:
+                    # enter the ramp-down once what is left fits the tail sizes
+                    if rem > sum(tail):
+                        sz = rem - sum(tail)
+                    else:
+                        sz = tail.pop(0)
+                else:
+                    sz = self.chunk_bytes[min(k, len(self.chunk_bytes) - 1)]
+                sizes.append(min(sz, rem))
+                rem -= sizes[-1]
                 k += 1
+            rel = offs[ids[0]:ids[-1] + 2] - offs[ids[0]]
+            bidx = np.searchsorted(rel, np.cumsum(sizes), side="left")
+            bounds = sorted({0, len(ids)} | {min(int(x), len(ids)) for x in bidx})
             events = []
             host = self.splits.buffer
             cs = self.copy_stream

@@ -92,5 +92,5 @@ def iter_columnar(cols: dict) -> Iterator[tuple]:
     off = cols["key_off"]
     blob = cols["key_blob"].tobytes()
     val = cols["val"]
-    for i in range(int(cols["hi"].size)):
+    for i in range(int(val.size)):
         yield key_str(blob[off[i]:off[i + 1]]), [int(val[i])]

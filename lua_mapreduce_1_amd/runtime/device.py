@@ -200,15 +200,27 @@ def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: to
         bad = torch.zeros(1, dtype=torch.int32, device=hi.device)
     else:
         part, hi, lo, val, rep, bad = ops.sort_by_partition_key(part, hi, lo, val, rep, nparts)
-    off, blob = ops.gather_key_bytes(hi, lo, rep, src)
+    if hi.is_cuda:
+        # blob capacity bound: distinct keys occupy disjoint bytes of their source
+        cap = src.numel() if src is not None else max(16 * n, 1)
+        off, blob = ops.gather_key_bytes(hi, lo, rep, src, capacity=cap)
+    else:
+        off, blob = ops.gather_key_bytes(hi, lo, rep, src)
     counts = ops.bincount(part, nparts) if n else torch.zeros(nparts, dtype=torch.int64, device=hi.device)
     if hi.is_cuda:
         hv = _to_host(val, "val")
-        ho = _to_host(off.to(torch.int32), "off32") if blob.numel() < 2**31 else _to_host(off, "off64")
-        hb = _to_host(blob, "blob")
+        ho = _to_host(off.to(torch.int32), "off32") if cap < 2**31 else _to_host(off, "off64")
+        est = _POOL.bufs.get("blob")
+        hb = _POOL.get("blob", max(1 << 20, est.numel() if est is not None else 16 * n), torch.uint8)
+        ops.copy_to_host(blob, hb, off[n:])  # size read on the device: no sync before the copy
         hc = _to_host(counts, "counts")
         hbad = _to_host(bad, "bad")
         torch.cuda.current_stream(hi.device).synchronize()
+        nbytes = int(ho[n]) if n else 0
+        if nbytes > hb.numel():  # estimate too small: grow and copy again (rare)
+            hb = _POOL.get("blob", nbytes, torch.uint8)
+            hb.copy_(blob[:nbytes])
+        hb = hb[:nbytes]
         flag = int(hbad[0])
         if flag & 1:
             # a tie run was too long for the fixup kernel: redo with the full sort
