@@ -60,9 +60,7 @@ def lib():
     with _LOCK:
         if _LIB is not None:
             return _LIB
-        path = _build.HIP_LIB
-        if not os.path.exists(path):
-            _build.build_hip()
+        path = _build.build_hip()  # no-op unless a source is newer than the .so
         L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         for name, args in _SIGS.items():
             f = getattr(L, name)

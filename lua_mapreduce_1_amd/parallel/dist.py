@@ -22,19 +22,23 @@ def env_world() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
-def init_from_env(backend: str | None = None, timeout_s: float = 600.0):
+def init_from_env(backend: str | None = None, timeout_s: float = 600.0, use_gpu: bool | None = None):
     """Initialise the default group from torchrun's env (no-op for WORLD_SIZE=1).
 
     Returns (rank, world, device)."""
     rank, world, local = env_world()
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available() and backend != "gloo"
+    if use_gpu:
+        ndev = torch.cuda.device_count()
+        local = local % max(ndev, 1)  # several ranks may share a GPU (gloo tests)
     device = torch.device("cuda", local) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
     if world > 1 and not dist.is_initialized():
         be = backend or ("nccl" if use_gpu else "gloo")
         kw = {}
-        if be == "nccl":
+        if be == "nccl" and use_gpu:
             kw["device_id"] = device
         dist.init_process_group(be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s),
                                 **kw)
@@ -47,18 +51,26 @@ def world_info(group=None) -> tuple[int, int]:
     return 0, 1
 
 
+def _is_gloo(group=None) -> bool:
+    return dist.get_backend(group) == "gloo"
+
+
 def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None):
-    if inp.is_cuda or dist.get_backend(group) != "gloo":
+    if not _is_gloo(group):
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
         return
-    # gloo: all_to_all_single is supported for CPU tensors on recent torch; fall
-    # back to point-to-point if not.
+    # gloo (CPU tests, or several ranks sharing one GPU): collectives run on
+    # host copies; point-to-point fallback when all_to_all is unavailable.
+    dev = inp.device
+    ci, co = inp.cpu(), torch.empty(out.shape, dtype=out.dtype)
     try:
-        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+        dist.all_to_all_single(co, ci, out_splits, in_splits, group=group)
     except RuntimeError:
         rank, world = world_info(group)
-        ins = list(torch.split(inp, in_splits))
-        outs = list(torch.split(out, out_splits))
+        n_in = in_splits or [ci.shape[0] // world] * world
+        n_out = out_splits or [co.shape[0] // world] * world
+        ins = list(torch.split(ci, n_in))
+        outs = list(torch.split(co, n_out))
         reqs = []
         for p in range(world):
             if p == rank:
@@ -68,6 +80,7 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None
             reqs.append(dist.irecv(outs[p], p, group=group))
         for r in reqs:
             r.wait()
+    out.copy_(co.to(dev) if dev.type != "cpu" else co)
 
 
 def exchange_counts(counts: torch.Tensor, group=None) -> torch.Tensor:
@@ -87,16 +100,20 @@ def all_to_all_v(payload: torch.Tensor, send_counts: list[int], recv_counts: lis
 
 def barrier(group=None, device=None) -> None:
     if dist.is_available() and dist.is_initialized():
-        if device is not None and torch.device(device).type == "cuda":
+        if device is not None and torch.device(device).type == "cuda" and not _is_gloo(group):
             dist.barrier(group=group, device_ids=[torch.device(device).index])
         else:
             dist.barrier(group=group)
 
 
+def _coll_device(device, group=None):
+    return torch.device("cpu") if _is_gloo(group) else device
+
+
 def all_reduce_max(x: float, device, group=None) -> float:
     if not (dist.is_available() and dist.is_initialized()):
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64, device=_coll_device(device, group))
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
 
@@ -104,7 +121,7 @@ def all_reduce_max(x: float, device, group=None) -> float:
 def all_reduce_sum_int(x: int, device, group=None) -> int:
     if not (dist.is_available() and dist.is_initialized()):
         return x
-    t = torch.tensor([x], dtype=torch.int64, device=device)
+    t = torch.tensor([x], dtype=torch.int64, device=_coll_device(device, group))
     dist.all_reduce(t, group=group)
     return int(t.item())
 
@@ -113,7 +130,7 @@ def broadcast_object(obj, src: int = 0, group=None, device=None):
     if not (dist.is_available() and dist.is_initialized()):
         return obj
     lst = [obj]
-    dist.broadcast_object_list(lst, src=src, group=group, device=device)
+    dist.broadcast_object_list(lst, src=src, group=group, device=None if _is_gloo(group) else device)
     return lst[0]
 
 

@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, on_gpu=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import torch.distributed as dist
@@ -27,12 +27,14 @@ def _worker(rank, world, port, q):
     from lua_mapreduce_1_amd.runtime import codec
     from lua_mapreduce_1_amd.utils.corpus import europarl_like
 
-    D.init_from_env(backend="gloo")
+    _, _, device = D.init_from_env(backend="gloo", use_gpu=on_gpu)
     splits = europarl_like(seed=9, lines=12_000, words=200_000, vocab_size=8_000, split_lines=1000)
-    store = SplitStore(splits, pin=False)
+    store = SplitStore(splits, pin=on_gpu)
     eng = SPMDEngine(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
                           init_args={"nsplits": len(splits), "num_reducers": 7}),
-                     split_store=store, device="cpu")
+                     split_store=store, device=device)
+    if on_gpu:
+        assert eng.table.is_cuda
     res = eng.run()
     owned = sorted(res.partitions)
     assert all(p % world == rank for p in owned)
@@ -63,6 +65,24 @@ def test_spmd_gloo_wordcount(world):
         p.start()
     for p in procs:
         p.join(240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    ok, sorted_names, n = q.get(timeout=5)
+    assert ok and sorted_names and n > 1000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_spmd_multirank_on_one_gpu(world):
+    """Several ranks share the GPU (gloo carries the collectives through host
+    copies): exercises the device shuffle/reduce/finalize kernels at W > 1."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     ok, sorted_names, n = q.get(timeout=5)
     assert ok and sorted_names and n > 1000
