@@ -75,7 +75,12 @@ def available() -> bool:
 
 
 def ptr(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        # kernels index raw memory: a strided view would be read as garbage
+        raise ValueError("HIP kernels need contiguous tensors")
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def stream(device=None):

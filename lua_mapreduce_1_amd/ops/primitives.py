@@ -23,7 +23,27 @@ import torch
 from . import keys as K
 from . import _hip
 
+import os as _os
+
 OPS = {"sum": 0, "min": 1, "max": 2}
+# MR_DEBUG_CHECKS=1: validate the offsets/indices a kernel will dereference
+# (with safe torch ops) before launching it, so a bad input raises in Python
+# instead of faulting the GPU.
+DEBUG_CHECKS = _os.environ.get("MR_DEBUG_CHECKS", "0") not in ("", "0")
+
+
+def _check_reps(lo: torch.Tensor, rep: torch.Tensor, src, what: str) -> None:
+    if not DEBUG_CHECKS or lo.numel() == 0:
+        return
+    is_long = (lo & 0xFF) == 0xFF
+    if not bool(is_long.any()):
+        return
+    if src is None:
+        raise RuntimeError(f"{what}: long keys but no byte source")
+    r = rep[is_long]
+    end = (r >> 24) + (r & ((1 << 24) - 1))
+    if int(end.max()) > src.numel() or int(r.min()) < 0:
+        raise RuntimeError(f"{what}: key bytes out of range (max end {int(end.max())} > {src.numel()})")
 _I64_MAX = (1 << 63) - 1
 _I64_MIN = -(1 << 63)
 
@@ -211,6 +231,7 @@ def key_meta(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.T
     """
     n = hi.numel()
     if hi.is_cuda:
+        _check_reps(lo, rep, src, "key_meta")
         d = hi.device
         part = torch.empty(n, dtype=torch.int32, device=d) if want_part else None
         ln = torch.empty(n, dtype=torch.int64, device=d) if want_len else None
@@ -275,6 +296,9 @@ def gather_key_bytes(hi, lo, rep, src, lengths: torch.Tensor | None = None, capa
         _, lengths = key_meta(hi, lo, rep, src, want_part=False)
     off, total = exclusive_scan(lengths)
     if hi.is_cuda:
+        _check_reps(lo, rep, src, "gather_key_bytes")
+        if DEBUG_CHECKS and capacity is not None and int(total.item()) > capacity:
+            raise RuntimeError(f"gather_key_bytes: {int(total.item())} bytes > capacity {capacity}")
         d = hi.device
         nb = int(total.item()) if capacity is None else int(capacity)
         blob = torch.empty(max(nb, 1), dtype=torch.uint8, device=d)
@@ -412,6 +436,8 @@ def sort_error(device) -> bool:
 
 def bincount(ids: torch.Tensor, nbins: int) -> torch.Tensor:
     if ids.is_cuda:
+        if DEBUG_CHECKS and ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= nbins):
+            raise RuntimeError(f"bincount: ids out of [0, {nbins})")
         d = ids.device
         out = torch.zeros(nbins, dtype=torch.int64, device=d)
         _hip.call("mr_bincount", _hip.ptr(ids), ids.numel(), nbins, _hip.ptr(out), _hip.stream(d))

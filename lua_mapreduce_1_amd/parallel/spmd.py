@@ -307,7 +307,7 @@ class SPMDEngine:
         rec = torch.stack([hi, lo, val, lens], dim=1)
         rrec = D.all_to_all_v(rec, send_h[0], [r[0] for r in recv_h], self.group)
         rblob = D.all_to_all_v(blob, send_h[1], [r[1] for r in recv_h], self.group)
-        rl = rrec[:, 3]
+        rl = rrec[:, 3].contiguous()
         roff, _ = ops.exclusive_scan(rl)
         rrep = (roff << 24) | rl
         return rrec[:, 0].contiguous(), rrec[:, 1].contiguous(), rrec[:, 2].contiguous(), rrep, rblob
