@@ -116,15 +116,19 @@ class job:  # noqa: N801
         self.jobs.update(self.get_id(), self.job_tbl.get("tmpname", ""), status=STATUS.FINISHED,
                          finished_time=utils.time())
 
-    def mark_as_written(self, cpu_time: float) -> None:
+    def mark_as_written(self, cpu_time: float) -> bool:
+        """False when the job is no longer ours (lease expired, or a restarted
+        server re-created it): the caller must then leave its inputs alone,
+        the job's new owner will consume them."""
         self.written = True
         now = utils.time()
-        self.jobs.update(self.get_id(), self.job_tbl.get("tmpname", ""), status=STATUS.WRITTEN, written_time=now,
-                         cpu_time=cpu_time, real_time=now - self.t)
+        return self.jobs.update(self.get_id(), self.job_tbl.get("tmpname", ""), status=STATUS.WRITTEN,
+                                written_time=now, cpu_time=cpu_time, real_time=now - self.t) is not None
 
     def mark_as_broken(self) -> None:
         if not self.written:
-            self.jobs.update(self.get_id(), "", status=STATUS.BROKEN, broken_time=utils.time(), inc_repetitions=1)
+            self.jobs.update(self.get_id(), self.job_tbl.get("tmpname", ""), status=STATUS.BROKEN,
+                             broken_time=utils.time(), inc_repetitions=1)
 
     # -- map -----------------------------------------------------------------------
     def _prepare_map(self, combiner_fname, partitioner_fname):
@@ -255,7 +259,8 @@ class job:  # noqa: N801
                 b.append(codec.encode_records(recs))
             b.build(res_file)
             elapsed = _time.process_time() - clock1
-            self.mark_as_written(elapsed)
+            if not self.mark_as_written(elapsed):
+                return elapsed
             gfs = self.cnn.gridfs()
             for n in filenames:
                 fs.remove_file(n)

@@ -68,6 +68,7 @@ class worker:  # noqa: N801
         self.poll_sleep = utils.DEFAULT_SLEEP
         self._hb_stop = threading.Event()
         self._hb_thread = None
+        self._stop = threading.Event()
 
     @classmethod
     def new(cls, connection_string=None, dbname: str = "tmp", auth_table=None) -> "worker":
@@ -116,8 +117,8 @@ class worker:  # noqa: N801
         iter_sleep = self.poll_sleep
         ntasks = 0
         job_done = False
-        while it < self.max_iter and ntasks < self.max_tasks:
-            while True:
+        while it < self.max_iter and ntasks < self.max_tasks and not self._stop.is_set():
+            while not self._stop.is_set():
                 task.update()
                 status, j = task.take_next_job(self.tmpname, self.name)
                 self.current_job = j
@@ -155,6 +156,10 @@ class worker:  # noqa: N801
                 iter_sleep = min(self.max_sleep, iter_sleep * 1.5)
             it += 1
 
+    def stop(self) -> None:
+        """Ask the worker loop to return after its current job (embedding/tests)."""
+        self._stop.set()
+
     def execute(self) -> None:
         failed: set = set()
         self._start_heartbeat()
@@ -163,6 +168,17 @@ class worker:  # noqa: N801
                 try:
                     self._worker_execute()
                     break
+                except (ConnectionError, OSError) as e:
+                    # coordinator unreachable (e.g. the server that hosted it
+                    # finished): back off like an idle poll, give up quietly
+                    lost = getattr(self, "_lost", 0) + 1
+                    self._lost = lost
+                    if self.current_job is None and lost > self.max_iter:
+                        self._print("# coordinator unreachable (%s): exiting" % e)
+                        break
+                    utils.sleep(min(self.max_sleep, self.poll_sleep * lost))
+                    self.cnn.db = None
+                    continue
                 except Exception:  # noqa: BLE001
                     msg = traceback.format_exc()
                     if self.current_job is not None:

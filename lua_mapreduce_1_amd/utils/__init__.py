@@ -9,6 +9,7 @@ text-compatible output, while intermediate data uses a data-only binary codec
 """
 from __future__ import annotations
 
+import builtins
 import json
 import math
 import os
@@ -150,7 +151,7 @@ def escape(v) -> str:
         return _lua_number(v)
     if isinstance(v, (str, bytes)):
         return lua_quote(v)
-    if isinstance(v, (list, tuple)) and not isinstance(v, str):
+    if isinstance(v, (list, builtins.tuple)) and not isinstance(v, str):
         return "tuple{ " + ", ".join(escape(x) for x in v) + " }"
     return str(v)
 
@@ -172,13 +173,13 @@ def sort_key(k):
         return (1, k.encode("utf-8", "surrogateescape"))
     if isinstance(k, bytes):
         return (1, k)
-    if isinstance(k, (tuple, list)):
+    if isinstance(k, (builtins.tuple, list)):
         return (2, len(k), builtins_tuple_map(sort_key, k))
     return (3, str(k))
 
 
 def builtins_tuple_map(f, seq):
-    return __import__("builtins").tuple(f(x) for x in seq)
+    return builtins.tuple(f(x) for x in seq)
 
 
 def keys_sorted(result: dict) -> list:
@@ -267,7 +268,7 @@ def assert_check(value) -> None:
             raise ValueError("Impossible to mix not string keys with string keys")
         for k, v in value.items():
             assert_check(v)
-    elif isinstance(value, (list, tuple)):
+    elif isinstance(value, (list, builtins.tuple)):
         for v in value:
             assert_check(v)
     elif callable(value):
@@ -277,4 +278,4 @@ def assert_check(value) -> None:
 
 
 def tojson(v) -> str:
-    return json.dumps(v, default=lambda o: list(o) if isinstance(o, (tuple, set)) else str(o))
+    return json.dumps(v, default=lambda o: list(o) if isinstance(o, (builtins.tuple, set)) else str(o))
