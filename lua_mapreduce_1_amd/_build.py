@@ -55,14 +55,17 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     objs = []
     objdir = os.path.join(ROOT, "build", "hip")
     os.makedirs(objdir, exist_ok=True)
+    headers = sorted(glob.glob(os.path.join(srcdir, "*.h")))
     for s in srcs:
         o = os.path.join(objdir, os.path.basename(s) + ".o")
+        objs.append(o)
+        if not force and not _newer(o, [s] + headers):
+            continue
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall",
                "-Wno-unused-function", "-I", srcdir, "-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd))
         _run(cmd)
-        objs.append(o)
     tmp = HIP_LIB + ".tmp"
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
     os.replace(tmp, HIP_LIB)
