@@ -47,10 +47,12 @@ __device__ __forceinline__ void fold_value(long long* p, long long v, int op) {
 
 // Insert (hi,lo) with value v.  Returns 2 when this call claimed a new slot,
 // 1 when it folded into an existing key, 0 when the probe budget is exhausted
-// (overflow flag set; the host re-runs with a larger table).  Callers count
+// (overflow flag set; the host re-runs with a larger table).  ``out_slot``
+// (optional) receives the key's slot index — a dense-ish key id.  Callers count
 // claims locally and publish them with gtab_count_claims (one atomic per wave:
 // a same-address atomic per claim serialised ~3e5 adds in the map kernel).
-__device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long long v, u64 rep, int op) {
+__device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long long v, u64 rep, int op,
+                                           u64* out_slot = nullptr) {
   const u64 tag = key_tag(hi, lo);
   u64 slot = (tag >> 7) & t.mask;
   u32 probes = 0;
@@ -69,6 +71,7 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
         fold_value(&t.val[slot], v, op);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         st_agent(&t.lo[slot], lo);
+        if (out_slot) *out_slot = slot;
         return 2;
       }
       cur = expected;
@@ -84,6 +87,7 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
         }
         if (h == hi) {
           fold_value(&t.val[slot], v, op);
+          if (out_slot) *out_slot = slot;
           return 1;
         }
       }

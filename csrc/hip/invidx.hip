@@ -1,0 +1,505 @@
+// invidx.hip — inverted-index build kernels (gfx950): word -> sorted list of
+// the documents (lines) it occurs in.  The BASELINE "inverted-index build on
+// the same corpus shape" workload: a MapReduce whose map emits a variable
+// number of (word, doc) pairs per line and whose reduce concatenates them
+// (reference hot loops K1-K4 and the segmented concat of K8, SURVEY.md §2.2;
+// the emit/group machinery is job.lua:83-97 and utils.lua:206-271).
+//
+// Device formulation: every token becomes ONE 64-bit posting key
+//     (dest << (slot_bits + doc_bits)) | (word_slot << doc_bits) | doc
+// where word_slot is the word's slot in the HBM hash table (a dense key id),
+// doc the line index and dest the owning rank (added after the map).  A radix
+// sort of those keys groups by destination, then word, then document — exactly
+// the shuffle + k-way merge of the reference — and adjacent duplicates (a word
+// repeated in one line) are dropped by a compaction.
+//
+// ii_map_kernel (one 512-thread workgroup per chunk, 8 KiB tiles):
+//   1. stage the tile + halo into LDS with a whitespace bitmap and a newline
+//      bitmap (16 bytes per thread);
+//   2. per-thread newline prefix (wave scan + cross-wave LDS) -> every token's
+//      line without any per-byte loop;
+//   3. tokens probe a 4096-slot LDS table (exact 128-bit keys) — a chunk's
+//      vocabulary costs one HBM insert per distinct word, not per token;
+//      LDS misses (table 3/4 full) insert into HBM directly;
+//   4. newly claimed LDS slots get their global slot (one gtab_insert each);
+//   5. the tile's tokens are written with ONE atomic reservation per tile.
+#include <hip/hip_runtime.h>
+#include "mr_common.h"
+#include "hashtab.h"
+
+namespace mr {
+namespace ii {
+
+constexpr int T = 512;
+constexpr int SEG = 16;
+constexpr int TILE = T * SEG;           // 8192 bytes
+constexpr int PAD = 16;
+constexpr int HALO = 64;
+constexpr int STAGED = TILE + HALO;
+constexpr int TXT = PAD + STAGED + 32;
+constexpr int WSW = STAGED / 32 + 2;
+constexpr int SLOTS = 4096;
+constexpr int CLAIM_LIMIT = SLOTS * 3 / 4;
+constexpr int PROBES = 32;
+constexpr int MAX_TOK = TILE / 2;       // tokens start at non-ws bytes after ws: <= TILE/2 (+1)
+constexpr u32 GFLAG = 0x80000000u;      // token ref is a global slot (LDS miss)
+constexpr u32 UNRESOLVED = 0xFFFFFFFFu;
+
+struct Lds {
+  u8 txt[TXT];
+  u32 ws[WSW];
+  u32 tag[SLOTS];
+  u32 rep[SLOTS];    // chunk-relative offset | len << 16 (len < 65536)
+  u32 gslot[SLOTS];
+  u64 hi[SLOTS];
+  u64 lo[SLOTS];
+  u32 tok_ref[MAX_TOK + 8];
+  u32 tok_line[MAX_TOK + 8];
+  u32 wave_nl[T / 64];
+  u32 ntok;
+  u32 nclaimed;
+  u32 tile_lines;
+  unsigned long long out_base;
+};
+static_assert(sizeof(Lds) <= 160 * 1024, "LDS budget");
+
+__device__ __forceinline__ u32 mask16(uint4 q, u32 c0, bool ws) {
+  u32 m = 0;
+  const u32 w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32 b = (w[k] >> (8 * j)) & 0xFFu;
+      m |= (ws ? (is_ws(b) ? 1u : 0u) : (b == c0 ? 1u : 0u)) << (4 * k + j);
+    }
+  return m;
+}
+
+__device__ __forceinline__ u32 funnel(u32 a, u32 b, u32 r8) { return r8 ? ((a >> r8) | (b << (32 - r8))) : a; }
+
+__device__ u64 long_lo_global(const u8* text, u64 p0, u64 len) {
+  u64 h = long_hash_init(len);
+  for (u64 w = 0; w < len; w += 8) {
+    u64 word = 0;
+    const u64 n = (len - w) < 8 ? (len - w) : 8;
+    for (u64 j = 0; j < n; ++j) word |= (u64)text[p0 + w + j] << (8 * j);
+    h = long_hash_step(h, word);
+  }
+  return long_lo(h);
+}
+
+// LDS probe/claim; returns the local slot or -1 (table full / probe budget).
+__device__ __forceinline__ int lds_find_or_claim(Lds& L, u64 hi, u64 lo, u32 rep) {
+  u64 h = hi ^ (lo * 0x9E3779B97F4A7C15ull);
+  h ^= h >> 31;
+  h *= 0xC2B2AE3D27D4EB4Full;
+  h ^= h >> 29;
+  const u32 tag = (u32)(h >> 32) | 1u;
+  u32 slot = (u32)h & (SLOTS - 1);
+  for (int probes = 0; probes < PROBES;) {
+    u32 cur = __hip_atomic_load(&L.tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == 0) {
+      if (__hip_atomic_load(&L.nclaimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (u32)CLAIM_LIMIT)
+        return -1;
+      u32 expected = 0;
+      if (__hip_atomic_compare_exchange_strong(&L.tag[slot], &expected, tag, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        L.hi[slot] = hi;
+        L.rep[slot] = rep;
+        __hip_atomic_fetch_add(&L.nclaimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&L.lo[slot], lo, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return (int)slot;
+      }
+      cur = expected;
+    }
+    if (cur == tag) {
+      const u64 l = __hip_atomic_load(&L.lo[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (l == 0) continue;  // being published by its claimer
+      if (l == lo && L.hi[slot] == hi) return (int)slot;
+    }
+    slot = (slot + 1) & (SLOTS - 1);
+    ++probes;
+  }
+  return -1;
+}
+
+// Newlines per chunk (for the chunk line bases).
+__global__ void __launch_bounds__(256) count_newlines_kernel(const u8* __restrict__ text, u64 nbytes, u64 chunk,
+                                                             u32* __restrict__ out) {
+  const u64 b0 = (u64)blockIdx.x * chunk;
+  const u64 b1 = min(b0 + chunk, nbytes);
+  u32 c = 0;
+  for (u64 p = b0 + threadIdx.x * 16; p < b1; p += 256 * 16) {
+    if (p + 16 <= b1 && ((uintptr_t)(text + p) & 15) == 0) {
+      const uint4 q = *reinterpret_cast<const uint4*>(text + p);
+      c += __builtin_popcount(mask16(q, 10u, false));
+    } else {
+      for (u64 k = p; k < min(p + 16, b1); ++k) c += text[k] == '\n';
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  __shared__ u32 part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+__global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, u64 nbytes, u64 chunk_bytes,
+                                                   u64 rep_base, const u32* __restrict__ chunk_line_base, GTab g,
+                                                   u32 doc_bits, u64* __restrict__ out,
+                                                   unsigned long long* __restrict__ out_counter, u64 out_cap,
+                                                   u32* __restrict__ err) {
+  __shared__ __attribute__((aligned(16))) Lds L;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const u64 chunk_begin = (u64)blockIdx.x * chunk_bytes;
+  if (chunk_begin >= nbytes) return;
+  const u64 chunk_end = min(chunk_begin + chunk_bytes, nbytes);
+  for (int s = t; s < SLOTS; s += T) {
+    L.tag[s] = 0;
+    L.lo[s] = 0;
+    L.gslot[s] = UNRESOLVED;
+  }
+  if (t == 0) {
+    L.nclaimed = 0;
+    L.ntok = 0;
+    L.txt[PAD - 1] = chunk_begin > 0 ? text[chunk_begin - 1] : (u8)' ';
+    L.ws[WSW - 2] = 0xFFFFFFFFu;
+    L.ws[WSW - 1] = 0xFFFFFFFFu;
+  }
+  u32 line_base = chunk_line_base[blockIdx.x];
+  u16* ws16 = reinterpret_cast<u16*>(L.ws);
+  const u32* txt32 = reinterpret_cast<const u32*>(L.txt);
+  const int aligned = ((uintptr_t)text & 15) == 0;
+  u32 claims = 0;
+  for (u64 tile_base = chunk_begin; tile_base < chunk_end; tile_base += TILE) {
+    // ---- 1. stage + bitmaps
+    u32 nlm;
+    {
+      const u64 gpos = tile_base + (u64)t * SEG;
+      uint4 q;
+      if (aligned && gpos + SEG <= nbytes) {
+        q = *reinterpret_cast<const uint4*>(text + gpos);
+      } else {
+        u32 w[4];
+        for (int k = 0; k < 4; ++k) {
+          w[k] = 0;
+          for (int j = 0; j < 4; ++j) {
+            const u64 p = gpos + 4 * k + j;
+            w[k] |= (p < nbytes ? (u32)text[p] : 32u) << (8 * j);
+          }
+        }
+        q = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      *reinterpret_cast<uint4*>(L.txt + PAD + t * SEG) = q;
+      ws16[t] = (u16)mask16(q, 0, true);
+      nlm = mask16(q, 10u, false);
+      // newlines past the chunk end belong to the next chunk
+      if (gpos >= chunk_end) nlm = 0;
+      else if (chunk_end - gpos < 16) nlm &= (1u << (chunk_end - gpos)) - 1u;
+      if (t < HALO / SEG) {
+        const u64 gh = tile_base + TILE + (u64)t * SEG;
+        u32 w[4];
+        for (int k = 0; k < 4; ++k) {
+          w[k] = 0;
+          for (int j = 0; j < 4; ++j) {
+            const u64 p = gh + 4 * k + j;
+            w[k] |= (p < nbytes ? (u32)text[p] : 32u) << (8 * j);
+          }
+        }
+        const uint4 hq = make_uint4(w[0], w[1], w[2], w[3]);
+        *reinterpret_cast<uint4*>(L.txt + PAD + TILE + t * SEG) = hq;
+        ws16[T + t] = (u16)mask16(hq, 0, true);
+      }
+    }
+    // ---- 2. newline prefix: inclusive wave scan, then cross-wave bases
+    const u32 mine = __builtin_popcount(nlm);
+    u32 incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) L.wave_nl[wave] = incl;
+    __syncthreads();
+    u32 wbase = 0, tile_nl = 0;
+#pragma unroll
+    for (int w = 0; w < T / 64; ++w) {
+      const u32 c = L.wave_nl[w];
+      wbase += w < wave ? c : 0;
+      tile_nl += c;
+    }
+    const u32 thread_line = line_base + wbase + incl - mine;
+    // ---- 3. tokens of this thread's segment
+    const u64 seg_base = tile_base + (u64)t * SEG;
+    if (seg_base < chunk_end) {
+      const u32 m = ws16[t];
+      const u32 prev_ws = t ? ((ws16[t - 1] >> 15) & 1u) : (is_ws(L.txt[PAD - 1]) ? 1u : 0u);
+      u32 starts = (~m) & ((m << 1) | prev_ws) & 0xFFFFu;
+      const u64 lim_own = chunk_end - seg_base;
+      if (lim_own < 16) starts &= (1u << lim_own) - 1u;
+      while (starts) {
+        const int i = __builtin_ctz(starts);
+        starts &= starts - 1;
+        const u32 p = (u32)t * SEG + i;
+        u32 q = p + 1;
+        u32 wd = L.ws[q >> 5] >> (q & 31);
+        u32 end;
+        if (wd) {
+          end = q + __builtin_ctz(wd);
+        } else {
+          u32 k = (q >> 5) + 1;
+          while (L.ws[k] == 0) ++k;
+          end = 32 * k + __builtin_ctz(L.ws[k]);
+        }
+        u64 len = end - p;
+        const u64 gpos = tile_base + p;
+        const u32 b = PAD + p;
+        const u32 a = b >> 2;
+        const u32 r8 = (b & 3u) * 8u;
+        const u32 x0 = txt32[a], x1 = txt32[a + 1], x2 = txt32[a + 2], x3 = txt32[a + 3], x4 = txt32[a + 4];
+        const u64 le_hi = (u64)funnel(x0, x1, r8) | ((u64)funnel(x1, x2, r8) << 32);
+        const u64 le_lo = (u64)funnel(x2, x3, r8) | ((u64)funnel(x3, x4, r8) << 32);
+        u64 hi = __builtin_bswap64(le_hi);
+        u64 lo;
+        if (end >= (u32)STAGED) {
+          u64 pe = tile_base + STAGED;
+          while (pe < nbytes && !is_ws(text[pe])) ++pe;
+          len = pe - gpos;
+        }
+        if (len <= (u64)PACK_MAX) {
+          if (len < 8) hi &= ~0ull << (8 * (8 - len));
+          lo = len > 8 ? (__builtin_bswap64(le_lo) & (~0ull << (8 * (16 - len)))) : 0ull;
+          lo |= len;
+        } else {
+          lo = long_lo_global(text, gpos, len);
+        }
+        const u32 line = thread_line + __builtin_popcount(nlm & ((1u << i) - 1u));
+        int ls = len < 65536 ? lds_find_or_claim(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16)) : -1;
+        u32 ref;
+        if (ls >= 0) {
+          ref = (u32)ls;
+        } else {
+          u64 gs = 0;
+          const int r = gtab_insert(g, hi, lo, 1, make_rep(rep_base + gpos, len), OP_SUM, &gs);
+          claims += r == 2;
+          if (r == 0) gs = 0;  // table overflow: flagged in ctrl[1], host re-runs bigger
+          ref = GFLAG | (u32)gs;
+        }
+        const u32 k = __hip_atomic_fetch_add(&L.ntok, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        L.tok_ref[k] = ref;
+        L.tok_line[k] = line;
+      }
+    }
+    __syncthreads();
+    // ---- 4. resolve the global slots of new LDS keys
+    for (int s = t; s < SLOTS; s += T) {
+      if (L.tag[s] != 0 && L.gslot[s] == UNRESOLVED) {
+        const u32 r = L.rep[s];
+        u64 gs = 0;
+        const int rc = gtab_insert(g, L.hi[s], L.lo[s], 1, make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16),
+                                   OP_SUM, &gs);
+        claims += rc == 2;
+        L.gslot[s] = rc ? (u32)gs : 0u;
+      }
+    }
+    if (t == 0) {
+      const u32 n = L.ntok;
+      const unsigned long long base = atomicAdd(out_counter, (unsigned long long)n);
+      L.out_base = base;
+      if (base + n > out_cap) atomicOr(err, 1u);
+    }
+    __syncthreads();
+    // ---- 5. write the tile's posting keys
+    {
+      const u32 n = L.ntok;
+      const unsigned long long base = L.out_base;
+      for (u32 k = t; k < n; k += T) {
+        const u32 ref = L.tok_ref[k];
+        const u32 gs = (ref & GFLAG) ? (ref & ~GFLAG) : L.gslot[ref];
+        if (base + k < out_cap) out[base + k] = ((u64)gs << doc_bits) | (u64)L.tok_line[k];
+      }
+    }
+    line_base += tile_nl;
+    __syncthreads();
+    if (t == 0) {
+      L.ntok = 0;
+      L.txt[PAD - 1] = L.txt[PAD + TILE - 1];
+    }
+    __syncthreads();
+  }
+  gtab_count_claims(g, claims);
+}
+
+// key |= dest[slot(key)] << shift, slot(key) = (key >> doc_bits) & slot_mask
+__global__ void ii_add_dest_kernel(u64* __restrict__ keys, u64 n, const u32* __restrict__ dest, u32 doc_bits,
+                                   u64 slot_mask, u32 shift) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 k = keys[i];
+    keys[i] = k | ((u64)dest[(k >> doc_bits) & slot_mask] << shift);
+  }
+}
+
+// Unique sorted keys -> keep flags (1 at i if i == 0 or key[i] != key[i-1]).
+__global__ void ii_unique_flags_kernel(const u64* __restrict__ keys, u64 n, u32* __restrict__ flags) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+
+// Scatter kept keys: out[pos[i]] = keys[i] where flags[i].
+__global__ void ii_compact_kernel(const u64* __restrict__ keys, const u32* __restrict__ flags,
+                                  const u32* __restrict__ pos, u64 n, u64* __restrict__ out) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    if (flags[i]) out[pos[i]] = keys[i];
+}
+
+// Split unique posting keys into word boundaries and doc ids:
+//   wflag[i] = 1 if the word part (key >> doc_bits) differs from key[i-1]'s;
+//   doc[i]   = (key & doc_mask) + doc_base.
+__global__ void ii_split_kernel(const u64* __restrict__ keys, u64 n, u32 doc_bits, long long doc_base,
+                                u32* __restrict__ wflag, int* __restrict__ doc) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  const u64 dm = (1ull << doc_bits) - 1;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 k = keys[i];
+    wflag[i] = (i == 0 || (k >> doc_bits) != (keys[i - 1] >> doc_bits)) ? 1u : 0u;
+    doc[i] = (int)((long long)(k & dm) + doc_base);
+  }
+}
+
+// Word heads -> per-word (slot, start): wid = wpos[i] at heads.
+__global__ void ii_word_heads_kernel(const u64* __restrict__ keys, const u32* __restrict__ wflag,
+                                     const u32* __restrict__ wpos, u64 n, u32 doc_bits, u64 slot_mask,
+                                     long long* __restrict__ word_slot, long long* __restrict__ word_start) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (wflag[i]) {
+      const u32 w = wpos[i];
+      word_slot[w] = (long long)((keys[i] >> doc_bits) & slot_mask);
+      word_start[w] = (long long)i;
+    }
+  }
+}
+
+}  // namespace ii
+}  // namespace mr
+
+using namespace mr;
+
+static inline unsigned grid_n(u64 n, unsigned block, unsigned cap = 4096) {
+  u64 g = (n + block - 1) / block;
+  if (g > cap) g = cap;
+  return (unsigned)(g ? g : 1);
+}
+
+extern "C" {
+
+int mr_ii_chunk_bytes() { return 32 * 1024; }
+
+int mr_count_newlines(const void* text, u64 nbytes, u64 chunk, void* out, hipStream_t s) {
+  if (nbytes == 0) return 0;
+  const u64 nb = (nbytes + chunk - 1) / chunk;
+  hipLaunchKernelGGL(ii::count_newlines_kernel, dim3((unsigned)nb), dim3(256), 0, s, (const u8*)text, nbytes, chunk,
+                     (u32*)out);
+  return (int)hipGetLastError();
+}
+
+int mr_ii_map(const void* text, u64 nbytes, u64 chunk, u64 rep_base, const void* chunk_line_base, void* tag, void* hi,
+              void* lo, void* val, void* rep, void* ctrl, u64 cap, u32 doc_bits, void* out, void* out_counter,
+              u64 out_cap, void* err, hipStream_t s) {
+  if (nbytes == 0) return 0;
+  if (chunk % ii::TILE) return -1;
+  GTab g;
+  g.tag = (u64*)tag;
+  g.hi = (u64*)hi;
+  g.lo = (u64*)lo;
+  g.val = (long long*)val;
+  g.rep = (u64*)rep;
+  g.ctrl = (u32*)ctrl;
+  g.mask = cap - 1;
+  const u64 nb = (nbytes + chunk - 1) / chunk;
+  hipLaunchKernelGGL(ii::ii_map_kernel, dim3((unsigned)nb), dim3(ii::T), 0, s, (const u8*)text, nbytes, chunk,
+                     rep_base, (const u32*)chunk_line_base, g, doc_bits, (u64*)out, (unsigned long long*)out_counter,
+                     out_cap, (u32*)err);
+  return (int)hipGetLastError();
+}
+
+int mr_ii_add_dest(void* keys, u64 n, const void* dest, u32 doc_bits, u64 slot_mask, u32 shift, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ii::ii_add_dest_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (u64*)keys, n, (const u32*)dest,
+                     doc_bits, slot_mask, shift);
+  return (int)hipGetLastError();
+}
+
+int mr_ii_unique_flags(const void* keys, u64 n, void* flags, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ii::ii_unique_flags_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)keys, n,
+                     (u32*)flags);
+  return (int)hipGetLastError();
+}
+
+int mr_ii_compact(const void* keys, const void* flags, const void* pos, u64 n, void* out, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ii::ii_compact_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)keys,
+                     (const u32*)flags, (const u32*)pos, n, (u64*)out);
+  return (int)hipGetLastError();
+}
+
+int mr_ii_split(const void* keys, u64 n, u32 doc_bits, long long doc_base, void* wflag, void* doc, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ii::ii_split_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)keys, n, doc_bits,
+                     doc_base, (u32*)wflag, (int*)doc);
+  return (int)hipGetLastError();
+}
+
+int mr_ii_word_heads(const void* keys, const void* wflag, const void* wpos, u64 n, u32 doc_bits, u64 slot_mask,
+                     void* word_slot, void* word_start, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ii::ii_word_heads_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)keys,
+                     (const u32*)wflag, (const u32*)wpos, n, doc_bits, slot_mask, (long long*)word_slot,
+                     (long long*)word_start);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Insert n keys, returning each key's slot (the receive-side merge of words
+// arriving from several ranks).
+namespace mr {
+namespace ii {
+__global__ void ii_insert_slots_kernel(GTab g, const u64* __restrict__ hi, const u64* __restrict__ lo,
+                                       const u64* __restrict__ rep, u64 n, long long* __restrict__ out_slot) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  u32 claims = 0;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u64 s = 0;
+    const int r = gtab_insert(g, hi[i], lo[i], 1, rep[i], OP_SUM, &s);
+    claims += r == 2;
+    out_slot[i] = r ? (long long)s : -1;
+  }
+  gtab_count_claims(g, claims);
+}
+}  // namespace ii
+}  // namespace mr
+
+extern "C" int mr_ii_insert_slots(void* tag, void* thi, void* tlo, void* val, void* trep, void* ctrl, u64 cap,
+                                  const void* hi, const void* lo, const void* rep, u64 n, void* out_slot,
+                                  hipStream_t s) {
+  if (n == 0) return 0;
+  GTab g;
+  g.tag = (u64*)tag;
+  g.hi = (u64*)thi;
+  g.lo = (u64*)tlo;
+  g.val = (long long*)val;
+  g.rep = (u64*)trep;
+  g.ctrl = (u32*)ctrl;
+  g.mask = cap - 1;
+  hipLaunchKernelGGL(ii::ii_insert_slots_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, g, (const u64*)hi,
+                     (const u64*)lo, (const u64*)rep, n, (long long*)out_slot);
+  return (int)hipGetLastError();
+}

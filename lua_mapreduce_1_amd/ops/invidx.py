@@ -1,0 +1,178 @@
+"""Inverted-index primitives (HIP kernels in ``csrc/hip/invidx.hip``; NumPy /
+torch on CPU tensors).
+
+A posting is ONE 64-bit key ``[dest | word id | doc]`` (see invidx.hip): the
+map emits one per token, a radix sort groups them by destination rank, word
+and document, and a compaction drops repeats of a word inside one line.
+Word ids are the slots of an HBM hash table on the GPU (dense ids from
+``np.unique`` on the CPU); the table also keeps each word's (hi, lo, rep) so key
+bytes are materialised only for the final words.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _hip
+from . import keys as K
+from .primitives import HashTable, _t64, _u64, exclusive_scan, sort_keys
+
+CHUNK = 32 * 1024
+
+
+def bits_for(n: int) -> int:
+    """Bits needed to hold values 0..n-1 (>= 1)."""
+    return max(1, int(max(n, 1) - 1).bit_length())
+
+
+class Vocab:
+    """Word ids of one rank: ``hi/lo/rep`` indexed by id, ``id_bits``."""
+
+    def __init__(self, device, capacity: int = 1 << 21):
+        self.device = torch.device(device)
+        if self.device.type == "cuda":
+            self.table = HashTable(capacity, self.device, "sum")
+            self.id_bits = bits_for(self.table.cap)
+        else:
+            self.table = None
+            self.id_bits = 1
+            self.hi = self.lo = self.rep = torch.zeros(0, dtype=torch.int64)
+
+    @property
+    def overflowed(self) -> bool:
+        return self.table is not None and int(self.table.ctrl[1].item()) != 0
+
+    def arrays(self):
+        if self.table is not None:
+            return self.table.hi, self.table.lo, self.table.rep
+        return self.hi, self.lo, self.rep
+
+    def reset(self) -> None:
+        if self.table is not None:
+            self.table.reset()
+
+    # -- CPU helpers --------------------------------------------------------------
+    def _assign_cpu(self, hi: np.ndarray, lo: np.ndarray, rep: np.ndarray) -> np.ndarray:
+        """Dense ids for (hi, lo) (first occurrence keeps its rep)."""
+        keys = np.empty(hi.size, dtype=[("h", "<u8"), ("l", "<u8")])
+        keys["h"], keys["l"] = hi, lo
+        uk, first, inv = np.unique(keys, return_index=True, return_inverse=True)
+        self.hi = _t64(uk["h"].copy())
+        self.lo = _t64(uk["l"].copy())
+        self.rep = _t64(rep[first])
+        self.id_bits = bits_for(uk.size)
+        return inv.astype(np.int64)
+
+
+def map_postings(text: torch.Tensor, vocab: Vocab, doc_bits: int, rep_base: int = 0):
+    """Posting keys ``id << doc_bits | line`` of every token of ``text``
+    (unsorted on the GPU) -> int64 tensor.  ``line`` = newlines before the token."""
+    nbytes = text.numel()
+    if text.is_cuda:
+        d = text.device
+        s = _hip.stream(d)
+        nchunks = max(1, (nbytes + CHUNK - 1) // CHUNK)
+        cnt = torch.zeros(nchunks, dtype=torch.int32, device=d)
+        _hip.call("mr_count_newlines", _hip.ptr(text), nbytes, CHUNK, _hip.ptr(cnt), s)
+        base, _ = exclusive_scan(cnt)
+        cap = nbytes // 2 + 2  # tokens are separated by >= 1 whitespace byte
+        out = torch.empty(cap, dtype=torch.int64, device=d)
+        counter = torch.zeros(1, dtype=torch.int64, device=d)
+        err = torch.zeros(1, dtype=torch.int32, device=d)
+        t = vocab.table
+        _hip.call("mr_ii_map", _hip.ptr(text), nbytes, CHUNK, rep_base, _hip.ptr(base), *t._gtab(), t.cap, doc_bits,
+                  _hip.ptr(out), _hip.ptr(counter), cap, _hip.ptr(err), s)
+        n, e = torch.cat([counter, err.to(torch.int64)]).tolist()
+        if e:
+            raise RuntimeError("inverted index map: posting buffer overflow")
+        if vocab.overflowed:
+            raise RuntimeError("inverted index map: vocabulary table overflow (raise capacity)")
+        return out[:n]
+    buf = text.numpy()
+    starts, lens = K.token_spans(buf)
+    hi, lo = K.span_keys(buf, starts, lens)
+    rep = ((starts.astype(np.uint64) + np.uint64(rep_base)) << np.uint64(K.REP_LEN_BITS)) | \
+        np.minimum(lens, K.REP_LEN_MASK).astype(np.uint64)
+    ids = vocab._assign_cpu(hi, lo, rep.view(np.int64))
+    nl = np.flatnonzero(buf == 10)
+    line = np.searchsorted(nl, starts, side="left").astype(np.int64)
+    return torch.from_numpy((ids << doc_bits) | line)
+
+
+def sort_unique(keys: torch.Tensor, bits: int) -> torch.Tensor:
+    """Sorted distinct posting keys (keys < 2^bits, bits <= 63)."""
+    n = keys.numel()
+    if keys.is_cuda:
+        if n == 0:
+            return keys
+        d = keys.device
+        s = _hip.stream(d)
+        _, sk = sort_keys([keys], bits=[bits], return_keys=True)
+        flags = torch.empty(n, dtype=torch.int32, device=d)
+        _hip.call("mr_ii_unique_flags", _hip.ptr(sk), n, _hip.ptr(flags), s)
+        pos, total = exclusive_scan(flags)
+        m = int(total.item())
+        out = torch.empty(m, dtype=torch.int64, device=d)
+        _hip.call("mr_ii_compact", _hip.ptr(sk), _hip.ptr(flags), _hip.ptr(pos), n, _hip.ptr(out), s)
+        return out
+    return torch.unique(keys)
+
+
+def split_words(ukeys: torch.Tensor, doc_bits: int, id_bits: int, doc_base: int = 0):
+    """Sorted unique posting keys -> (word ids int64[nw], word starts
+    int64[nw+1], docs int32[n]).  Words are runs of equal ``key >> doc_bits``
+    (destination bits included, so a word never spans two destinations)."""
+    n = ukeys.numel()
+    id_mask = (1 << id_bits) - 1
+    if ukeys.is_cuda:
+        d = ukeys.device
+        s = _hip.stream(d)
+        if n == 0:
+            z = torch.zeros(0, dtype=torch.int64, device=d)
+            return z, torch.zeros(1, dtype=torch.int64, device=d), torch.zeros(0, dtype=torch.int32, device=d)
+        wflag = torch.empty(n, dtype=torch.int32, device=d)
+        docs = torch.empty(n, dtype=torch.int32, device=d)
+        _hip.call("mr_ii_split", _hip.ptr(ukeys), n, doc_bits, int(doc_base), _hip.ptr(wflag), _hip.ptr(docs), s)
+        wpos, total = exclusive_scan(wflag)
+        nw = int(total.item())
+        wid = torch.empty(nw, dtype=torch.int64, device=d)
+        wstart = torch.empty(nw + 1, dtype=torch.int64, device=d)
+        wstart[nw:].fill_(n)
+        _hip.call("mr_ii_word_heads", _hip.ptr(ukeys), _hip.ptr(wflag), _hip.ptr(wpos), n, doc_bits, id_mask,
+                  _hip.ptr(wid), _hip.ptr(wstart), s)
+        return wid, wstart, docs
+    wk = ukeys >> doc_bits
+    flags = torch.ones(n, dtype=torch.bool)
+    if n > 1:
+        flags[1:] = wk[1:] != wk[:-1]
+    starts = torch.nonzero(flags).flatten()
+    wid = wk[starts] & id_mask
+    wstart = torch.cat([starts, torch.tensor([n])]).to(torch.int64)
+    docs = ((ukeys & ((1 << doc_bits) - 1)) + doc_base).to(torch.int32)
+    return wid, wstart, docs
+
+
+def add_dest(keys: torch.Tensor, dest_of_id: torch.Tensor, doc_bits: int, id_bits: int) -> int:
+    """keys |= dest[id(key)] << (id_bits + doc_bits) in place; returns the shift."""
+    shift = id_bits + doc_bits
+    if keys.is_cuda:
+        _hip.call("mr_ii_add_dest", _hip.ptr(keys), keys.numel(), _hip.ptr(dest_of_id.to(torch.int32).contiguous()),
+                  doc_bits, (1 << id_bits) - 1, shift, _hip.stream(keys.device))
+        return shift
+    ids = (keys >> doc_bits) & ((1 << id_bits) - 1)
+    keys |= dest_of_id.to(torch.int64)[ids] << shift
+    return shift
+
+
+def insert_ids(vocab: Vocab, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor) -> torch.Tensor:
+    """Ids of (hi, lo) in ``vocab`` (inserting new words) -> int64."""
+    n = hi.numel()
+    if hi.is_cuda:
+        t = vocab.table
+        out = torch.empty(n, dtype=torch.int64, device=hi.device)
+        _hip.call("mr_ii_insert_slots", *t._gtab(), t.cap, _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), n,
+                  _hip.ptr(out), _hip.stream(hi.device))
+        if vocab.overflowed:
+            raise RuntimeError("inverted index reduce: vocabulary table overflow")
+        return out
+    return torch.from_numpy(vocab._assign_cpu(_u64(hi), _u64(lo), rep.numpy()))

@@ -336,12 +336,14 @@ def _sort_ws(d, n: int):
     return ws
 
 
-def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: str = "onesweep") -> torch.Tensor:
+def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: str = "onesweep",
+              return_keys: bool = False):
     """Stable permutation sorting rows by unsigned multi-word keys.
 
     ``words[0]`` is the most significant u64 word.  ``bits[j]`` limits the
     number of low bits of word j that participate (e.g. partition ids).
-    Returns int32 (GPU) / int64 (CPU) permutation.  GPU: LSD radix sort, one
+    Returns int32 (GPU) / int64 (CPU) permutation (and, with ``return_keys``,
+    ``words[0]`` in sorted order as a second value).  GPU: LSD radix sort, one
     onesweep launch per 8-bit digit (``method="onesweep"``) or the 3-phase
     histogram/scan/scatter passes (``method="3phase"``).
     """
@@ -350,7 +352,8 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
     if words[0].is_cuda:
         d = words[0].device
         if n == 0:
-            return torch.zeros(0, dtype=torch.int32, device=d)
+            z = torch.zeros(0, dtype=torch.int32, device=d)
+            return (z, words[0][:0]) if return_keys else z
         lib = _hip.lib()
         s = _hip.stream(d)
         perm = torch.empty(n, dtype=torch.int32, device=d)
@@ -391,12 +394,13 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
                               shift, _hip.ptr(hist), _hip.ptr(scan_ws), s)
                 k1, k2 = k2, k1
                 perm, perm2 = perm2, perm
-        return perm
+        return (perm, k1) if return_keys else perm
     cols = [_u64(w) for w in words]
     for j, nb in enumerate(bits):
         if nb < 64:
             cols[j] = cols[j] & np.uint64((1 << nb) - 1)
-    return torch.from_numpy(np.lexsort(tuple(reversed(cols))).astype(np.int64))
+    perm = torch.from_numpy(np.lexsort(tuple(reversed(cols))).astype(np.int64))
+    return (perm, words[0][perm]) if return_keys else perm
 
 
 def sort_by_partition_key(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, val: torch.Tensor,

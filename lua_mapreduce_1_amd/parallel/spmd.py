@@ -69,6 +69,29 @@ class SplitStore:
     def region(self, i0: int, i1: int) -> tuple[int, int]:
         return int(self.offsets[i0]), int(self.offsets[i1])
 
+    def line_offsets(self) -> np.ndarray:
+        """Cumulative newline counts at split boundaries (global line ids)."""
+        lo = getattr(self, "_line_offsets", None)
+        if lo is None:
+            view = self.buffer.numpy()
+            per = [int(np.count_nonzero(view[self.offsets[i]:self.offsets[i + 1]] == 10)) for i in range(len(self))]
+            lo = np.zeros(len(self) + 1, dtype=np.int64)
+            np.cumsum(per, out=lo[1:])
+            self._line_offsets = lo
+        return lo
+
+
+def assign_contiguous(weights, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous block [j0, j1) of items for ``rank``, balanced by weight."""
+    n = len(weights)
+    if world == 1:
+        return 0, n
+    c = np.concatenate([[0.0], np.cumsum(np.asarray(weights, dtype=np.float64))])
+    tot = c[-1]
+    cuts = [int(np.searchsorted(c, tot * r / world, side="left")) for r in range(world + 1)]
+    cuts[0], cuts[-1] = 0, n
+    return cuts[rank], max(cuts[rank], cuts[rank + 1])
+
 
 class JobRecord:
     __slots__ = ("key", "value", "status", "repetitions", "started", "written", "cpu_time", "real_time", "worker")
@@ -168,15 +191,9 @@ class SPMDEngine:
 
     def _assign(self, jobs: list[tuple]) -> tuple[int, int]:
         """Contiguous block of jobs for this rank, balanced by input bytes."""
-        n = len(jobs)
         if self.world == 1:
-            return 0, n
-        w = np.array([self._job_bytes(v) for _, v in jobs], dtype=np.float64)
-        c = np.concatenate([[0.0], np.cumsum(w)])
-        tot = c[-1]
-        cuts = [int(np.searchsorted(c, tot * r / self.world, side="left")) for r in range(self.world + 1)]
-        cuts[0], cuts[-1] = 0, n
-        return cuts[self.rank], max(cuts[self.rank], cuts[self.rank + 1])
+            return 0, len(jobs)
+        return assign_contiguous([self._job_bytes(v) for _, v in jobs], self.rank, self.world)
 
     # -- map ------------------------------------------------------------------
     def _stage_chunks(self, jobs, j0, j1):
