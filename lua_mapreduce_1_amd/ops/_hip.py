@@ -58,6 +58,12 @@ _SIGS = {
     "mr_ii_split": [_p, _u64, _u32, ctypes.c_longlong, _p, _p, _p],
     "mr_ii_word_heads": [_p, _p, _p, _u64, _u32, _u64, _p, _p, _p],
     "mr_ii_insert_slots": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _p],
+    "mr_ts_gen": [_p, _u64, _u64, _u64, _p],
+    "mr_ts_keys": [_p, _u64, _p, _p, _p],
+    "mr_ts_dest": [_p, _u64, _p, _u32, _p, _p],
+    "mr_ts_gather": [_p, _p, _u64, _p, _p],
+    "mr_ts_checksum": [_p, _u64, _p, _p],
+    "mr_ts_unsorted": [_p, _p, _u64, _p, _p],
     "mr_scan_partials_len": [_u64],
     "mr_rs_tiles": [_u64],
 }

@@ -1,0 +1,116 @@
+"""TeraSort record primitives (HIP kernels in ``csrc/hip/terasort.hip``; NumPy
+on CPU tensors — the CPU path is the executable specification).
+
+Records: 100 bytes = 10-byte key + 90-byte value, row-major uint8 tensors of
+shape [n, 100].  Sort order: unsigned bytewise on the key = (hi, lo) with
+hi = key bytes 0-7 big-endian and lo = key bytes 8-9 big-endian.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _hip
+
+REC = 100
+KEY = 10
+M64 = (1 << 64) - 1
+
+
+def _splitmix(x: np.ndarray) -> np.ndarray:
+    x = (x + np.uint64(0x9E3779B97F4A7C15)) & np.uint64(M64)
+    x = ((x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & np.uint64(M64)
+    x = ((x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & np.uint64(M64)
+    return x ^ (x >> np.uint64(31))
+
+
+def generate(n: int, first: int, seed: int, device="cpu") -> torch.Tensor:
+    """TeraGen analogue: records first .. first+n-1 of ``seed``."""
+    d = torch.device(device)
+    out = torch.empty((n, REC), dtype=torch.uint8, device=d)
+    if d.type == "cuda":
+        _hip.call("mr_ts_gen", _hip.ptr(out), n, first, seed, _hip.stream(d))
+        return out
+    with np.errstate(over="ignore"):
+        r = np.arange(first, first + n, dtype=np.uint64)
+        s = np.uint64(seed)
+        k0 = _splitmix(s ^ (r * np.uint64(2)))
+        k1 = _splitmix(s ^ (r * np.uint64(2) + np.uint64(1)))
+        a = out.numpy()
+        a[:, 0:8] = k0.astype(">u8").view(np.uint8).reshape(n, 8)
+        a[:, 8:10] = k1.astype(">u8").view(np.uint8).reshape(n, 8)[:, 0:2]
+        a[:, 10:18] = r.astype("<u8").view(np.uint8).reshape(n, 8)
+        b = np.arange(18, REC, dtype=np.uint64)
+        a[:, 18:] = (((r[:, None] * np.uint64(31) + b[None, :] * np.uint64(7)) & np.uint64(0x3F))
+                     + np.uint64(0x30)).astype(np.uint8)
+    return out
+
+
+def keys(rec: torch.Tensor):
+    """(hi, lo) int64 sort words of each record."""
+    n = rec.shape[0]
+    if rec.is_cuda:
+        hi = torch.empty(n, dtype=torch.int64, device=rec.device)
+        lo = torch.empty(n, dtype=torch.int64, device=rec.device)
+        _hip.call("mr_ts_keys", _hip.ptr(rec), n, _hip.ptr(hi), _hip.ptr(lo), _hip.stream(rec.device))
+        return hi, lo
+    a = rec.numpy()
+    hi = np.ascontiguousarray(a[:, 0:8]).view(">u8").reshape(n).astype(np.uint64)
+    lo = a[:, 8].astype(np.uint64) << np.uint64(8) | a[:, 9].astype(np.uint64)
+    return torch.from_numpy(hi.view(np.int64)), torch.from_numpy(lo.view(np.int64))
+
+
+def dest_of(hi: torch.Tensor, splitters: torch.Tensor) -> torch.Tensor:
+    """Number of splitters <= hi (unsigned), int32."""
+    if hi.is_cuda:
+        out = torch.empty(hi.numel(), dtype=torch.int32, device=hi.device)
+        sp = splitters.to(hi.device).contiguous()
+        _hip.call("mr_ts_dest", _hip.ptr(hi), hi.numel(), _hip.ptr(sp), sp.numel(), _hip.ptr(out),
+                  _hip.stream(hi.device))
+        return out
+    h = hi.numpy().view(np.uint64)
+    s = splitters.numpy().view(np.uint64)
+    return torch.from_numpy(np.searchsorted(s, h, side="right").astype(np.int32))
+
+
+def gather(rec: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
+    """rec[perm] (rows)."""
+    n = perm.numel()
+    if rec.is_cuda:
+        out = torch.empty((n, REC), dtype=torch.uint8, device=rec.device)
+        p = perm if perm.dtype == torch.int32 else perm.to(torch.int32)
+        _hip.call("mr_ts_gather", _hip.ptr(rec), _hip.ptr(p.contiguous()), n, _hip.ptr(out), _hip.stream(rec.device))
+        return out
+    return rec[perm.long()]
+
+
+def checksum(rec: torch.Tensor) -> int:
+    """Order-independent 64-bit checksum of the records."""
+    n = rec.shape[0]
+    if rec.is_cuda:
+        out = torch.zeros(1, dtype=torch.int64, device=rec.device)
+        _hip.call("mr_ts_checksum", _hip.ptr(rec), n, _hip.ptr(out), _hip.stream(rec.device))
+        return int(out.item()) & M64
+    w = rec.numpy().view(np.uint32).reshape(n, REC // 4).astype(np.uint64)
+    h = np.full(n, 0x243F6A8885A308D3, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for j in range(REC // 4):
+            x = h ^ w[:, j]
+            x ^= x >> np.uint64(33)
+            x *= np.uint64(0xFF51AFD7ED558CCD)
+            x ^= x >> np.uint64(33)
+            x *= np.uint64(0xC4CEB9FE1A85EC53)
+            x ^= x >> np.uint64(33)
+            h = x + np.uint64(j)
+        return int(h.sum(dtype=np.uint64)) & M64
+
+
+def unsorted_pairs(hi: torch.Tensor, lo: torch.Tensor) -> int:
+    n = hi.numel()
+    if hi.is_cuda:
+        out = torch.zeros(1, dtype=torch.int64, device=hi.device)
+        _hip.call("mr_ts_unsorted", _hip.ptr(hi), _hip.ptr(lo), n, _hip.ptr(out), _hip.stream(hi.device))
+        return int(out.item())
+    h = hi.numpy().view(np.uint64)
+    lw = lo.numpy().view(np.uint64)
+    return int(np.count_nonzero((h[:-1] > h[1:]) | ((h[:-1] == h[1:]) & (lw[:-1] > lw[1:]))))

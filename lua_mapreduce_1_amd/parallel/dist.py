@@ -141,3 +141,18 @@ def gather_objects(obj, dst: int = 0, group=None):
     out = [None] * world if rank == dst else None
     dist.gather_object(obj, out, dst=dst, group=group)
     return out
+
+
+def all_gather_tensor(t: torch.Tensor, group=None) -> torch.Tensor:
+    """Concatenation of every rank's equally-shaped ``t`` along dim 0."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return t
+    _, world = world_info(group)
+    if _is_gloo(group):
+        h = t.cpu().contiguous()
+        out = [torch.empty_like(h) for _ in range(world)]
+        dist.all_gather(out, h, group=group)
+        return torch.cat(out).to(t.device)
+    out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    return out
