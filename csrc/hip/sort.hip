@@ -137,9 +137,18 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
                                                                  V* vals_out, u64 n, int shift, const u32* ghist,
                                                                  u64* granules, u32* tile_counter, u32 epoch,
                                                                  u32* err) {
-  __shared__ u32 base_run[RS_BINS];
-  __shared__ u32 wcnt[RS_WAVES][RS_BINS];
-  __shared__ u32 lhist[RS_BINS];
+  // Each wave ranks its own contiguous quarter of the tile (16 rounds of 64
+  // keys) against WAVE-PRIVATE digit counters in LDS — no block barrier inside
+  // the rounds (the first version paid 3 barriers per round).  The tile
+  // histogram falls out of the four wave counters; keys (and values) are then
+  // placed in an LDS image of the tile in digit order and streamed out so
+  // consecutive lanes write consecutive addresses of one digit run.
+  constexpr int SUB = RS_TILE / RS_WAVES;  // keys per wave
+  __shared__ u64 sk[RS_TILE];
+  __shared__ V sv[RS_TILE];
+  __shared__ u32 wc[RS_WAVES][RS_BINS];
+  __shared__ u32 gout[RS_BINS];
+  __shared__ u32 scan[RS_BINS];
   __shared__ u32 sh_tile;
   __shared__ u32 sh_uniform;
   const int t = threadIdx.x;
@@ -149,19 +158,20 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
     sh_tile = atomicAdd(tile_counter, 1u);
     sh_uniform = 0;
   }
-  lhist[t] = 0;
+#pragma unroll
+  for (int w = 0; w < RS_WAVES; ++w) wc[w][t] = 0;
   // exclusive scan of the global histogram (digit base offsets)
   const u32 gcount = ghist[t];
-  wcnt[0][t] = gcount;
+  scan[t] = gcount;
   __syncthreads();
   if (gcount == n) sh_uniform = 1;
   for (int o = 1; o < RS_BINS; o <<= 1) {
-    const u32 y = t >= o ? wcnt[0][t - o] : 0u;
+    const u32 y = t >= o ? scan[t - o] : 0u;
     __syncthreads();
-    wcnt[0][t] += y;
+    scan[t] += y;
     __syncthreads();
   }
-  const u32 gbase = wcnt[0][t] - gcount;
+  const u32 gbase = scan[t] - gcount;
   const u32 tile = sh_tile;
   const u64 t0 = (u64)tile * RS_TILE;
   if (sh_uniform) {  // every key has this digit: order unchanged
@@ -174,21 +184,78 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
     }
     return;
   }
-  // local histogram of this tile (keys preloaded into registers)
+  // this wave's keys: tile[wave*SUB + r*64 + lane]
+  const u64 w0 = t0 + (u64)wave * SUB;
   u64 kr[RS_ROUNDS];
   V vr[RS_ROUNDS];
 #pragma unroll
   for (int r = 0; r < RS_ROUNDS; ++r) {
-    const u64 i = t0 + (u64)r * RS_THREADS + t;
+    const u64 i = w0 + (u64)r * 64 + lane;
     kr[r] = i < n ? keys_in[i] : 0;
     vr[r] = (i < n && vals_in) ? vals_in[i] : V{};
-    if (i < n) atomicAdd(&lhist[(kr[r] >> shift) & 0xFF], 1u);
+  }
+  const unsigned long long below = (1ull << lane) - 1ull;
+  u32 myrank[RS_ROUNDS];
+  u32* mywc = wc[wave];
+#pragma unroll
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const u64 i = w0 + (u64)r * 64 + lane;
+    const bool valid = i < n;
+    const u32 d = (u32)((kr[r] >> shift) & 0xFF);
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const unsigned long long m = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? m : ~m;
+    }
+    const u32 before = valid ? mywc[d] : 0u;
+    myrank[r] = before + (u32)__popcll(peers & below);
+    // every lane has read its counter before the leader updates it (LDS ops of
+    // one wave complete in order)
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    if (valid && (peers & below) == 0) mywc[d] = before + (u32)__popcll(peers);
   }
   __syncthreads();
-  const u32 mine = lhist[t];
+  // tile histogram + per-wave offsets for digit t
+  u32 cnt_w[RS_WAVES];
+  u32 mine = 0;
+#pragma unroll
+  for (int w = 0; w < RS_WAVES; ++w) {
+    cnt_w[w] = wc[w][t];
+    mine += cnt_w[w];
+  }
   u64* G = granules + (u64)tile * RS_BINS;
   __hip_atomic_store(&G[t], gr_pack(epoch, tile == 0 ? GR_INC : GR_AGG, mine), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
+  scan[t] = mine;
+  __syncthreads();
+  for (int o = 1; o < RS_BINS; o <<= 1) {
+    const u32 y = t >= o ? scan[t - o] : 0u;
+    __syncthreads();
+    scan[t] += y;
+    __syncthreads();
+  }
+  const u32 lbase = scan[t] - mine;
+  {
+    u32 off = lbase;
+#pragma unroll
+    for (int w = 0; w < RS_WAVES; ++w) {
+      wc[w][t] = off;  // now: LDS start of wave w's keys of digit t
+      off += cnt_w[w];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const u64 i = w0 + (u64)r * 64 + lane;
+    if (i < n) {
+      const u32 d = (u32)((kr[r] >> shift) & 0xFF);
+      const u32 pos = mywc[d] + myrank[r];
+      sk[pos] = kr[r];
+      if (vals_in) sv[pos] = vr[r];
+    }
+  }
+  // decoupled look-back for this tile's global prefix of digit t
   u64 excl = 0;
   if (tile > 0) {
     long long j = (long long)tile - 1;
@@ -211,38 +278,14 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
     }
     __hip_atomic_store(&G[t], gr_pack(epoch, GR_INC, excl + mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  base_run[t] = gbase + (u32)excl;
-  const unsigned long long below = (1ull << lane) - 1ull;
-#pragma unroll
-  for (int r = 0; r < RS_ROUNDS; ++r) {
-    const u64 i = t0 + (u64)r * RS_THREADS + t;
-    const bool valid = i < n;
-    const u64 k = kr[r];
-    const V v = vr[r];
-    const u32 d = (u32)((k >> shift) & 0xFF);
-#pragma unroll
-    for (int w = 0; w < RS_WAVES; ++w) wcnt[w][t] = 0;
-    __syncthreads();
-    unsigned long long peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const unsigned long long m = __ballot((d >> b) & 1u);
-      peers &= ((d >> b) & 1u) ? m : ~m;
-    }
-    const u32 rank = (u32)__popcll(peers & below);
-    if (valid && rank == 0) wcnt[wave][d] = (u32)__popcll(peers);
-    __syncthreads();
-    if (valid) {
-      u32 pos = base_run[d] + rank;
-      for (int w = 0; w < wave; ++w) pos += wcnt[w][d];
-      keys_out[pos] = k;
-      if (vals_in) vals_out[pos] = v;
-    }
-    __syncthreads();
-    u32 tot = 0;
-#pragma unroll
-    for (int w = 0; w < RS_WAVES; ++w) tot += wcnt[w][t];
-    base_run[t] += tot;
+  gout[t] = gbase + (u32)excl - lbase;  // global pos of LDS index i with digit d = gout[d] + i
+  __syncthreads();
+  const u32 cnt = (u32)min((u64)RS_TILE, n - t0);
+  for (u32 i = t; i < cnt; i += RS_THREADS) {
+    const u64 k = sk[i];
+    const u32 pos = gout[(k >> shift) & 0xFF] + i;
+    keys_out[pos] = k;
+    if (vals_in) vals_out[pos] = sv[i];
   }
 }
 
