@@ -114,7 +114,10 @@ __device__ __forceinline__ u64 gr_pack(u32 epoch, u64 flag, u64 count) {
   return ((u64)(epoch & 0xFFFFFFu) << 40) | (flag << 38) | (count & ((1ull << 38) - 1));
 }
 
-__global__ void __launch_bounds__(RS_THREADS) rs_ghist8_kernel(const u64* keys, u64 n, u32* ghist /*[8][256]*/) {
+__global__ void __launch_bounds__(RS_THREADS) rs_ghist8_kernel(const u64* keys, u64 n, u32* ghist /*[8][256]*/,
+                                                               int ndigits) {
+  // only the digits the sort will visit: a 16-bit word used to pay 6 extra
+  // all-in-bin-0 (maximally contended) LDS atomics per key
   __shared__ u32 h[8][RS_BINS];
   const int t = threadIdx.x;
 #pragma unroll
@@ -124,19 +127,22 @@ __global__ void __launch_bounds__(RS_THREADS) rs_ghist8_kernel(const u64* keys, 
   for (u64 i = (u64)blockIdx.x * blockDim.x + t; i < n; i += stride) {
     const u64 k = keys[i];
 #pragma unroll
-    for (int b = 0; b < 8; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 0xFF], 1u);
+    for (int b = 0; b < 8; ++b)
+      if (b < ndigits) atomicAdd(&h[b][(k >> (8 * b)) & 0xFF], 1u);
   }
   __syncthreads();
 #pragma unroll
   for (int b = 0; b < 8; ++b)
-    if (h[b][t]) atomicAdd(&ghist[b * RS_BINS + t], h[b][t]);
+    if (b < ndigits && h[b][t]) atomicAdd(&ghist[b * RS_BINS + t], h[b][t]);
 }
 
 template <typename V>
 __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys_in, const V* vals_in, u64* keys_out,
                                                                  V* vals_out, u64 n, int shift, const u32* ghist,
                                                                  u64* granules, u32* tile_counter, u32 epoch,
-                                                                 u32* err) {
+                                                                 u32* err, int iota) {
+  // iota: vals_in is absent and the value of key i is i (first pass of a
+  // permutation sort; saves the separate iota launch).
   // Each wave ranks its own contiguous quarter of the tile (16 rounds of 64
   // keys) against WAVE-PRIVATE digit counters in LDS — no block barrier inside
   // the rounds (the first version paid 3 barriers per round).  The tile
@@ -180,10 +186,12 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
       if (i < n) {
         keys_out[i] = keys_in[i];
         if (vals_in) vals_out[i] = vals_in[i];
+        else if (iota) vals_out[i] = (V)i;
       }
     }
     return;
   }
+  const bool has_v = vals_in != nullptr || iota;
   // this wave's keys: tile[wave*SUB + r*64 + lane]
   const u64 w0 = t0 + (u64)wave * SUB;
   u64 kr[RS_ROUNDS];
@@ -192,7 +200,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
   for (int r = 0; r < RS_ROUNDS; ++r) {
     const u64 i = w0 + (u64)r * 64 + lane;
     kr[r] = i < n ? keys_in[i] : 0;
-    vr[r] = (i < n && vals_in) ? vals_in[i] : V{};
+    vr[r] = (i < n && vals_in) ? vals_in[i] : (iota ? (V)i : V{});
   }
   const unsigned long long below = (1ull << lane) - 1ull;
   u32 myrank[RS_ROUNDS];
@@ -252,7 +260,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
       const u32 d = (u32)((kr[r] >> shift) & 0xFF);
       const u32 pos = mywc[d] + myrank[r];
       sk[pos] = kr[r];
-      if (vals_in) sv[pos] = vr[r];
+      if (has_v) sv[pos] = vr[r];
     }
   }
   // decoupled look-back for this tile's global prefix of digit t
@@ -285,7 +293,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
     const u64 k = sk[i];
     const u32 pos = gout[(k >> shift) & 0xFF] + i;
     keys_out[pos] = k;
-    if (vals_in) vals_out[pos] = sv[i];
+    if (has_v) vals_out[pos] = sv[i];
   }
 }
 
@@ -579,10 +587,10 @@ int mr_radix_pass_u32v(const void* keys_in, const void* vals_in, void* keys_out,
 }
 
 // Global histograms of all 8 digits of a u64 word (ghist: 2048 u32, zeroed by caller).
-int mr_radix_ghist8(const void* keys, u64 n, void* ghist, hipStream_t s) {
+int mr_radix_ghist8(const void* keys, u64 n, void* ghist, int ndigits, hipStream_t s) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(rs_ghist8_kernel, dim3(grid_n(n, RS_THREADS, 1024)), dim3(RS_THREADS), 0, s,
-                     (const u64*)keys, n, (u32*)ghist);
+                     (const u64*)keys, n, (u32*)ghist, ndigits);
   return (int)hipGetLastError();
 }
 
@@ -590,13 +598,13 @@ int mr_radix_ghist8(const void* keys, u64 n, void* ghist, hipStream_t s) {
 // granules: tiles*256 u64, never needs clearing — entries are epoch tagged;
 // tile_counter: one u32 zeroed before the pass; epoch unique per pass).
 int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
-                           const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err,
+                           const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
                            hipStream_t s) {
   if (n == 0) return 0;
   const u32 nt = (u32)((n + RS_TILE - 1) / RS_TILE);
   hipLaunchKernelGGL(rs_onesweep_kernel<u32>, dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
                      (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
-                     (u64*)granules, (u32*)tile_counter, epoch, (u32*)err);
+                     (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota);
   return (int)hipGetLastError();
 }
 

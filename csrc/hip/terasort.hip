@@ -122,6 +122,35 @@ __global__ void __launch_bounds__(256) ts_unsorted_kernel(const u64* __restrict_
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd(out, (unsigned long long)bad);
 }
 
+// Rows sorted by hi only: order each run of equal hi by lo (insertion sort of
+// the permutation; stable because the LSD pass left ties in input order).
+// Random 64-bit prefixes almost never tie, so this replaces 2 radix passes +
+// a key gather.  Runs longer than 64 set *bad (caller falls back).
+__global__ void ts_tie_fixup_kernel(const u64* __restrict__ shi, u32* __restrict__ perm, const u64* __restrict__ lo,
+                                    u64 n, u32* __restrict__ bad) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += stride) {
+    const u64 h = shi[i];
+    if (shi[i + 1] != h || (i > 0 && shi[i - 1] == h)) continue;
+    u64 e = i + 2;
+    while (e < n && shi[e] == h && e - i <= 64) ++e;
+    if (e - i > 64) {
+      atomicOr(bad, 1u);
+      continue;
+    }
+    for (u64 a = i + 1; a < e; ++a) {
+      const u32 p = perm[a];
+      const u64 l = lo[p];
+      u64 b = a;
+      while (b > i && lo[perm[b - 1]] > l) {
+        perm[b] = perm[b - 1];
+        --b;
+      }
+      perm[b] = p;
+    }
+  }
+}
+
 }  // namespace ts
 }  // namespace mr
 
@@ -158,6 +187,13 @@ int mr_ts_gather(const void* in, const void* perm, u64 n, void* out, hipStream_t
   if (n == 0) return 0;
   hipLaunchKernelGGL(ts::ts_gather_kernel, dim3(ts_grid(n * ts::WORDS)), dim3(256), 0, s, (const u32*)in,
                      (const u32*)perm, n, (u32*)out);
+  return (int)hipGetLastError();
+}
+
+int mr_ts_tie_fixup(const void* shi, void* perm, const void* lo, u64 n, void* bad, hipStream_t s) {
+  if (n < 2) return 0;
+  hipLaunchKernelGGL(ts::ts_tie_fixup_kernel, dim3(ts_grid(n)), dim3(256), 0, s, (const u64*)shi, (u32*)perm,
+                     (const u64*)lo, n, (u32*)bad);
   return (int)hipGetLastError();
 }
 

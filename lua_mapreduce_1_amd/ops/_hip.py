@@ -36,8 +36,8 @@ _SIGS = {
     "mr_exclusive_scan_i64": [_p, _p, _u64, _p, _p, _p],
     "mr_radix_pass_u32v": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p],
     "mr_gather_u64": [_p, _p, _p, _u64, _p],
-    "mr_radix_ghist8": [_p, _u64, _p, _p],
-    "mr_radix_onesweep_u32v": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p, _u32, _p, _p],
+    "mr_radix_ghist8": [_p, _u64, _p, _i32, _p],
+    "mr_radix_onesweep_u32v": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p, _u32, _p, _i32, _p],
     "mr_iota_u32": [_p, _u64, _p],
     "mr_segment_heads": [_p, _p, _u64, _p, _p],
     "mr_segment_fold": [_p, _p, _p, _u64, _i32, _p, _p],
@@ -63,6 +63,7 @@ _SIGS = {
     "mr_ts_dest": [_p, _u64, _p, _u32, _p, _p],
     "mr_ts_gather": [_p, _p, _u64, _p, _p],
     "mr_ts_checksum": [_p, _u64, _p, _p],
+    "mr_ts_tie_fixup": [_p, _p, _p, _u64, _p, _p],
     "mr_ts_unsorted": [_p, _p, _u64, _p, _p],
     "mr_scan_partials_len": [_u64],
     "mr_rs_tiles": [_u64],

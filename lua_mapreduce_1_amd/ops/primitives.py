@@ -356,21 +356,52 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
             return (z, words[0][:0]) if return_keys else z
         lib = _hip.lib()
         s = _hip.stream(d)
+        if method == "onesweep":
+            # no input copy and no iota launch: the first pass reads the
+            # caller's word and generates the identity permutation itself
+            ws = _sort_ws(d, n)
+            small = ws["small"]
+            small.zero_()  # [0:2048) ghist, [2048:2112) tile counters, [2112] error flag
+            ghist = small[:2048]
+            kbuf = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(2)]
+            pbuf = [torch.empty(n, dtype=torch.int32, device=d) for _ in range(2)]
+            kin, pin = None, None
+            pass_id = 0
+            for j, (w, nb) in enumerate(zip(reversed(words), reversed(bits))):
+                if pin is None:
+                    kin = w.contiguous()
+                else:
+                    dst = kbuf[0] if kin is not kbuf[0] else kbuf[1]
+                    _hip.call("mr_gather_u64", _hip.ptr(w), _hip.ptr(pin), _hip.ptr(dst), n, s)
+                    kin = dst
+                if nb <= 0:
+                    continue
+                if pass_id:
+                    ghist.zero_()
+                _hip.call("mr_radix_ghist8", _hip.ptr(kin), n, _hip.ptr(ghist), (nb + 7) // 8, s)
+                for shift in range(0, nb, 8):
+                    _EPOCH[0] = (_EPOCH[0] + 1) & 0xFFFFFF or 1
+                    kout = kbuf[0] if kin is not kbuf[0] else kbuf[1]
+                    pout = pbuf[0] if pin is not pbuf[0] else pbuf[1]
+                    _hip.call("mr_radix_onesweep_u32v", _hip.ptr(kin), _hip.ptr(pin), _hip.ptr(kout), _hip.ptr(pout),
+                              n, shift, _hip.ptr(ghist[shift // 8 * 256:]), _hip.ptr(ws["granules"]),
+                              _hip.ptr(small[2048 + pass_id:]), _EPOCH[0], _hip.ptr(small[2112:]),
+                              1 if pin is None else 0, s)
+                    pass_id += 1
+                    kin, pin = kout, pout
+            if pin is None:
+                pin = torch.empty(n, dtype=torch.int32, device=d)
+                _hip.call("mr_iota_u32", _hip.ptr(pin), n, s)
+                kin = words[0].clone()
+            return (pin, kin) if return_keys else pin
         perm = torch.empty(n, dtype=torch.int32, device=d)
         _hip.call("mr_iota_u32", _hip.ptr(perm), n, s)
         perm2 = torch.empty_like(perm)
         k1 = torch.empty(n, dtype=torch.int64, device=d)
         k2 = torch.empty_like(k1)
-        if method == "onesweep":
-            ws = _sort_ws(d, n)
-            small = ws["small"]
-            small.zero_()  # [0:2048) ghist, [2048:2112) tile counters, [2112] error flag
-            ghist = small[:2048]
-            pass_id = 0
-        else:
-            tiles = int(lib.mr_rs_tiles(n))
-            hist = torch.empty(256 * tiles, dtype=torch.int32, device=d)
-            scan_ws = torch.empty(int(lib.mr_scan_partials_len(256 * tiles)), dtype=torch.int32, device=d)
+        tiles = int(lib.mr_rs_tiles(n))
+        hist = torch.empty(256 * tiles, dtype=torch.int32, device=d)
+        scan_ws = torch.empty(int(lib.mr_scan_partials_len(256 * tiles)), dtype=torch.int32, device=d)
         first = True
         for w, nb in zip(reversed(words), reversed(bits)):
             if first:
@@ -378,20 +409,9 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
                 first = False
             else:
                 _hip.call("mr_gather_u64", _hip.ptr(w), _hip.ptr(perm), _hip.ptr(k1), n, s)
-            if method == "onesweep":
-                if pass_id:
-                    ghist.zero_()
-                _hip.call("mr_radix_ghist8", _hip.ptr(k1), n, _hip.ptr(ghist), s)
             for shift in range(0, nb, 8):
-                if method == "onesweep":
-                    _EPOCH[0] = (_EPOCH[0] + 1) & 0xFFFFFF or 1
-                    _hip.call("mr_radix_onesweep_u32v", _hip.ptr(k1), _hip.ptr(perm), _hip.ptr(k2), _hip.ptr(perm2),
-                              n, shift, _hip.ptr(ghist[shift // 8 * 256:]), _hip.ptr(ws["granules"]),
-                              _hip.ptr(small[2048 + pass_id:]), _EPOCH[0], _hip.ptr(small[2112:]), s)
-                    pass_id += 1
-                else:
-                    _hip.call("mr_radix_pass_u32v", _hip.ptr(k1), _hip.ptr(perm), _hip.ptr(k2), _hip.ptr(perm2), n,
-                              shift, _hip.ptr(hist), _hip.ptr(scan_ws), s)
+                _hip.call("mr_radix_pass_u32v", _hip.ptr(k1), _hip.ptr(perm), _hip.ptr(k2), _hip.ptr(perm2), n,
+                          shift, _hip.ptr(hist), _hip.ptr(scan_ws), s)
                 k1, k2 = k2, k1
                 perm, perm2 = perm2, perm
         return (perm, k1) if return_keys else perm

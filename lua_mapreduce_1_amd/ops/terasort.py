@@ -114,3 +114,20 @@ def unsorted_pairs(hi: torch.Tensor, lo: torch.Tensor) -> int:
     h = hi.numpy().view(np.uint64)
     lw = lo.numpy().view(np.uint64)
     return int(np.count_nonzero((h[:-1] > h[1:]) | ((h[:-1] == h[1:]) & (lw[:-1] > lw[1:]))))
+
+
+def sort_perm(hi: torch.Tensor, lo: torch.Tensor) -> torch.Tensor:
+    """Permutation sorting rows by the 80-bit key (hi, lo).
+
+    GPU: radix-sort hi alone (8 onesweep passes) and order the rare runs of
+    equal hi by lo in a fix-up kernel; full (hi, lo) sort if a run is long."""
+    from .primitives import sort_keys
+    if not hi.is_cuda:
+        return sort_keys([hi, lo], bits=[64, 16])
+    perm, shi = sort_keys([hi], bits=[64], return_keys=True)
+    bad = torch.zeros(1, dtype=torch.int32, device=hi.device)
+    _hip.call("mr_ts_tie_fixup", _hip.ptr(shi), _hip.ptr(perm), _hip.ptr(lo), hi.numel(), _hip.ptr(bad),
+              _hip.stream(hi.device))
+    if int(bad.item()):
+        return sort_keys([hi, lo], bits=[64, 16])
+    return perm

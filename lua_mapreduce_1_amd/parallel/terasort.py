@@ -13,8 +13,9 @@ K6/K7/K9/C1).  MI355X pipeline, one rank per GPU, data resident in HBM:
      one 8-bit radix pass orders the rows by destination, a row gather packs
      them contiguously, and ONE ``all_to_all_single`` moves the 100-byte rows
      (RCCL over xGMI; all 7 links at once);
-  3. local LSD radix sort of the (hi, lo) 80-bit keys (onesweep, 10 passes over
-     (key, index) pairs — the 100-byte rows are not moved per pass) and one
+  3. local LSD radix sort of the 64-bit key prefixes (onesweep, 8 passes over
+     (key, index) pairs — the 100-byte rows are not moved per pass), a fix-up
+     kernel ordering the rare equal-prefix runs by the last 2 key bytes, and one
      final row gather.
 
 Rank r's output holds keys in [splitter r-1, splitter r); concatenated in
@@ -87,7 +88,7 @@ class TeraSort:
             del packed
         t_shuf = time.perf_counter()
         hi, lo = TS.keys(rec)
-        perm = ops.sort_keys([hi, lo], bits=[64, 16])
+        perm = TS.sort_perm(hi, lo)
         out = TS.gather(rec, perm)
         self._sync()
         t1 = time.perf_counter()

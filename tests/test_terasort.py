@@ -112,3 +112,19 @@ def test_gpu_single_rank_sort(gpu):
 @pytest.mark.gpu
 def test_gpu_multi_rank_on_one_gpu(gpu):
     _run(2, on_gpu=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mod", [200_000, 50, 0])
+def test_gpu_sort_perm_with_prefix_ties(gpu, mod):
+    """Equal 8-byte prefixes: short runs go through the tie fix-up kernel,
+    long runs (mod=50) through the full (hi, lo) fallback; both stable."""
+    g = torch.Generator().manual_seed(mod + 1)
+    n = 300_000
+    hi = torch.randint(-2**63, 2**63 - 1, (n,), generator=g, dtype=torch.int64)
+    if mod:
+        hi = hi % mod
+    lo = torch.randint(0, 1 << 16, (n,), generator=g, dtype=torch.int64)
+    ref = TS.sort_perm(hi, lo)
+    got = TS.sort_perm(hi.to(gpu), lo.to(gpu)).cpu().long()
+    assert torch.equal(got, ref.long())
