@@ -208,3 +208,39 @@ class JobCollection:
 
     def expire(self, now: float, lease: float) -> int:
         return int(self.c.request("JOB_EXPIRE", self.db, self.ns, now, lease)[1][0])
+
+
+def utest(connection_string=None) -> None:
+    """cnn.lua:119-161: connection, blob store + builder, the error channel and
+    batched inserts flushed at MAX_PENDING_INSERTS with per-document callbacks."""
+    c = cnn(connection_string, "test")
+    assert c.connect() is not None and c.get_dbname() == "test"
+    g = c.gridfs()
+    b = c.grid_file_builder()
+    b.append(b"hello ")
+    b.append(b"world")
+    g.remove_file("cnn_utest")
+    b.build("cnn_utest")
+    assert g.get("cnn_utest") == b"hello world"
+    g.remove_file("cnn_utest")
+    assert g.get("cnn_utest") is None
+    c.get_errors()
+    c.insert_error("w1", "msg1")
+    c.insert_error("w2", "msg2")
+    errs = c.get_errors()
+    assert [(e["worker"], e["msg"]) for e in errs] == [("w1", "msg1"), ("w2", "msg2")]
+    assert c.get_errors() == []
+    ns = "cnn_utest_jobs"
+    c.jobs(ns).drop()
+    seen = []
+    old = utils.MAX_PENDING_INSERTS
+    utils.MAX_PENDING_INSERTS = 50
+    try:
+        for i in range(120):
+            c.annotate_insert(ns, utils.make_job(i, {"v": i}), lambda doc: seen.append(doc["_id"]))
+        assert c.jobs(ns).count() == 100 and len(seen) == 100  # two automatic flushes
+        c.flush_pending_inserts(0)
+        assert c.jobs(ns).count() == 120 and len(seen) == 120
+    finally:
+        utils.MAX_PENDING_INSERTS = old
+    c.jobs(ns).drop()

@@ -204,3 +204,31 @@ def read_blob(cnn, storage: str, path: str, name: str) -> bytes:
         return MemFS(path).get(name) or b""
     with open(name, "rb") as f:
         return f.read()
+
+
+def utest(connection_string=None) -> None:
+    """fs.lua:213-251: wildcard conversion; for every storage write two files,
+    list them, read them back, remove them (sshfs through local paths)."""
+    from .cnn import cnn as cnn_cls
+    assert make_wildcard_from_mongo_match({"filename": {"$regex": "^/tmp/a\\.P1\\..*$"}}) == "/tmp/a.P1.*"
+    c = cnn_cls(connection_string, "test")
+    base = tempfile.mkdtemp(prefix="mr_fs_utest_")
+    try:
+        for storage in ("gridfs", "shared", "sshfs", "hbm"):
+            path = os.path.join(base, storage)
+            fs, make_builder, lines = router(c, [utils.get_hostname()], storage, path)
+            names = [f"{path}/fs_utest.P0.M1", f"{path}/fs_utest.P0.M2"]
+            for i, name in enumerate(names):
+                fs.remove_file(name)
+                bld = make_builder()
+                bld.append(codec.encode_records([("k%d" % i, [i])]))
+                bld.build(name)
+            got = sorted(f["filename"] for f in fs.list({"filename": {"$regex": "^" + re.escape(path) +
+                                                                      r"/fs_utest\.P0\..*"}}))
+            assert got == names, (storage, got)
+            for i, name in enumerate(names):
+                assert list(lines(name)) == [("k%d" % i, [i])]
+                fs.remove_file(name)
+            assert not fs.list({"filename": {"$regex": "^" + re.escape(path) + r"/fs_utest.*"}})
+    finally:
+        shutil.rmtree(base, ignore_errors=True)

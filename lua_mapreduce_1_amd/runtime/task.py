@@ -204,3 +204,8 @@ class task:  # noqa: N801
         return status, job(self.cnn, job_tbl, status, self.get_fname(), self.get_args(), jobs, self.get_results_ns(),
                            combiner=self.get_reduce_fname(), partitioner=self.get_partition_fname(),
                            storage=storage, path=path, task_tbl=self.tbl)
+
+
+def utest() -> None:
+    """task.lua:365-367."""
+    assert tmpname_summary("/tmp/lua_worker_abc") == "lua_worker_abc"

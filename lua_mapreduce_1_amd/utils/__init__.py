@@ -279,3 +279,47 @@ def assert_check(value) -> None:
 
 def tojson(v) -> str:
     return json.dumps(v, default=lambda o: list(o) if isinstance(o, (builtins.tuple, set)) else str(o))
+
+
+def utest(connection_string=None) -> None:
+    """utils.lua:340-406: hostname/time, Lua-literal serialization golden
+    strings, the GridFS line iterator, a golden k-way merge of two sorted
+    runs, storage-spec parsing, rename/remove, clear/copy table."""
+    from ..runtime import codec
+    from ..runtime.cnn import cnn as cnn_cls
+    assert isinstance(get_hostname(), str)
+    assert abs(time() - _time.time()) < 5
+    assert escape(120) == "120"
+    assert escape("30") == '"30"'
+    assert escape("30\n") == '"30\\n"'
+    assert serialize_table_ipairs([1, 2, 3, "hola"]) == '{1,2,3,"hola"}'
+    assert serialize_table_ipairs(keys_sorted({"c": 1, "a": 2, "b": 3})) == '{"a","b","c"}'
+    g = cnn_cls(connection_string, "test").gridfs()
+    lines = [b"first line", b"second", b"third longer line", b"a"]
+    g.remove_file("lines")
+    g.store_data(b"\n".join(lines), "lines")
+    assert list(g.lines("lines")) == lines
+    f1 = [(1, [1, 1]), (2, [1]), (3, [1])]
+    f2 = [(1, [1, 1, 1, 1]), (3, [1]), (4, [1])]
+    for name, recs in (("f1", f1), ("f2", f2)):
+        g.remove_file(name)
+        g.store_data(codec.encode_records(recs), name)
+    got = list(merge_iterator(g, ["f1", "f2"], lambda n: codec.decode_records(g.get(n))))
+    assert got == [(1, [1] * 6), (2, [1]), (3, [1, 1]), (4, [1])], got
+    for storage in ("gridfs", "sshfs", "shared"):
+        for path in ("", ":/tmp/dir"):
+            a, b = get_storage_from(storage + path, True)
+            assert a == storage and b and (path == "" or ":" + b == path)
+    fd1, tmp1 = tempfile.mkstemp()
+    os.close(fd1)
+    tmp2 = tmp1 + ".renamed"
+    assert rename(tmp1, tmp2)
+    assert remove(tmp2)
+    t = {1: 1, 2: 3, "a": 4, "b": 5}
+    clear_table(t)
+    assert not t
+    src = [1, 2, 3, 4]
+    dst1, dst2 = [5, 6, 7], [5, 6, 7, 8, 9, 10]
+    copy_table_ipairs(dst1, src)
+    copy_table_ipairs(dst2, src)
+    assert dst1 == src and dst2 == src

@@ -66,3 +66,24 @@ class heap:  # noqa: N801  (mirrors the reference's lowercase class name)
 
     def __len__(self) -> int:
         return len(self.data)
+
+
+def utest() -> None:
+    """heap.lua:99-118: pop order against a sort."""
+    import random
+    rng = random.Random(1234)
+    data = [rng.random() for _ in range(1000)]
+    h = heap()
+    for x in data:
+        h.push(x)
+    out = []
+    while not h.empty():
+        out.append(h.top())
+        h.pop()
+    assert out == sorted(data)
+    h2 = heap(lambda a, b: a > b)
+    for x in data:
+        h2.push(x)
+    assert h2.size() == len(data) and h2.top() == max(data)
+    h2.clear()
+    assert h2.empty()

@@ -25,8 +25,11 @@ builtins_tuple = builtins.tuple
 
 
 def _convert(v: Any):
+    """Nested lists/tuples -> interned tuples, innermost first (tuple.lua:
+    230-247 builds nested tuples through the same constructor)."""
     if isinstance(v, (list, builtins_tuple)):
-        return builtins_tuple(_convert(x) for x in v)
+        t = builtins_tuple(_convert(x) for x in v)
+        return _INTERN.setdefault(t, t)
     return v
 
 
@@ -76,12 +79,7 @@ class _TupleFactory:
                 return t  # scalars are returned unchanged (tuple.lua:254-256)
         else:
             t = args
-        t = _convert(t)
-        got = _INTERN.get(t)
-        if got is None:
-            _INTERN[t] = t
-            got = t
-        return got
+        return _convert(t)
 
     @staticmethod
     def stats():
@@ -105,3 +103,19 @@ class _TupleFactory:
 
 tuple = _TupleFactory()  # noqa: A001
 _FREE_REFS = 5  # dict key + dict value + list + loop variable + call argument
+
+
+def utest() -> None:
+    """tuple.lua:309-328: interning identity, nested tuples, many live
+    tuples released once unreferenced, scalars pass through."""
+    a = tuple(2, 4, 5, "a", (1, 4, 5))
+    b = tuple(2, 4, 5, "a", (1, 4, 5))
+    c = tuple([2, 4, 5, "a", [1, 4, 5]])
+    assert a is b and a is c
+    assert a[4] is tuple(1, 4, 5)
+    assert tuple(5) == 5 and tuple("x") == "x"
+    base = tuple.stats()[0]
+    live = [tuple(i, i + 1) for i in range(10000)]
+    assert tuple.stats()[0] >= base + 10000
+    del live
+    assert tuple.stats()[0] <= base + 1
