@@ -17,19 +17,45 @@ from .. import utils
 from .coordinator import Client, decode_jobs
 
 
-class GridFS:
-    """Blob store in the coordinator (the GridFS replacement)."""
+def split_endpoints(connection_string: str | None) -> list:
+    """``"h1:p1,h2:p2,..."`` -> endpoints; the first is the primary (job
+    tables, task, errors, persistent tables), all of them hold blobs."""
+    if not connection_string or "," not in str(connection_string):
+        return [connection_string]
+    return [e.strip() for e in str(connection_string).split(",") if e.strip()]
 
-    def __init__(self, client: Client, dbname: str):
-        self.c = client
+
+def shard_of(filename: str, nshards: int) -> int:
+    """Home shard of a blob: exact uint32 FNV-1 of the name mod nshards."""
+    h = 2166136261
+    for b in filename.encode("utf-8", "surrogateescape"):
+        h = ((h * 16777619) & 0xFFFFFFFF) ^ b
+    return h % nshards
+
+
+class GridFS:
+    """Blob store in the coordinator(s) (the GridFS replacement).
+
+    With several coordinator endpoints the blobs are hash-partitioned by file
+    name over all of them (the horizontal scale-out the reference gets from
+    sharding ``fs.chunks``, misc/make_sharded.lua:69-72); ``list`` merges the
+    shards.
+    """
+
+    def __init__(self, client, dbname: str):
+        self.shards = list(client) if isinstance(client, (list, tuple)) else [client]
+        self.c = self.shards[0]
         self.db = dbname
 
+    def _home(self, filename: str):
+        return self.shards[shard_of(filename, len(self.shards))] if len(self.shards) > 1 else self.c
+
     def store_data(self, data: bytes, filename: str) -> bool:
-        self.c.request("BLOB_PUT", self.db, filename, bytes(data))
+        self._home(filename).request("BLOB_PUT", self.db, filename, bytes(data))
         return True
 
     def get(self, filename: str) -> bytes | None:
-        st, f = self.c.request("BLOB_GET", self.db, filename)
+        st, f = self._home(filename).request("BLOB_GET", self.db, filename)
         return f[0] if st == 0 else None
 
     find_file = get
@@ -37,13 +63,16 @@ class GridFS:
     def list(self, match: dict | str | None = None) -> list[dict]:
         """Files whose name matches a regex (``{"filename": {"$regex": r}}``
         or a plain regex string); all files when ``match`` is None."""
-        _, f = self.c.request("BLOB_LIST", self.db, "")
-        names = [(f[i].decode("utf-8", "surrogateescape"), int(f[i + 1])) for i in range(0, len(f), 2)]
         rx = _regex_of(match)
-        return [{"filename": n, "length": sz} for n, sz in names if rx is None or rx.search(n)]
+        out = []
+        for c in self.shards:
+            _, f = c.request("BLOB_LIST", self.db, "")
+            names = [(f[i].decode("utf-8", "surrogateescape"), int(f[i + 1])) for i in range(0, len(f), 2)]
+            out += [{"filename": n, "length": sz} for n, sz in names if rx is None or rx.search(n)]
+        return out
 
     def remove_file(self, filename: str) -> bool:
-        _, f = self.c.request("BLOB_DEL", self.db, filename)
+        _, f = self._home(filename).request("BLOB_DEL", self.db, filename)
         return int(f[0]) > 0
 
     def lines(self, filename: str) -> Iterator[bytes]:
@@ -93,11 +122,16 @@ class cnn:  # noqa: N801
 
     def connect(self) -> Client:
         if self.db is None:
-            self.db = Client(self.connection_string)
+            self.db = Client(split_endpoints(self.connection_string)[0])
         return self.db
 
     def gridfs(self) -> GridFS:
-        return GridFS(self.connect(), self.gridfs_dbname)
+        eps = split_endpoints(self.connection_string)
+        if len(eps) == 1:
+            return GridFS(self.connect(), self.gridfs_dbname)
+        if getattr(self, "_blob_clients", None) is None:
+            self._blob_clients = [self.connect()] + [Client(e) for e in eps[1:]]
+        return GridFS(self._blob_clients, self.gridfs_dbname)
 
     def grid_file_builder(self) -> GridFileBuilder:
         return GridFileBuilder(self.gridfs())

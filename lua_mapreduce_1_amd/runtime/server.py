@@ -166,8 +166,9 @@ class server:  # noqa: N801
         return self._monitor(red_ns), len(mappers)
 
     def _drop_collections(self) -> None:
-        c = self.cnn.connect()
-        c.request("DB_DROP", self.cnn.get_dbname())
+        # every coordinator endpoint (blob shards included) — server.lua:331-343
+        for c in self.cnn.gridfs().shards:
+            c.request("DB_DROP", self.cnn.get_dbname())
 
     def _final(self) -> None:
         storage, path = self.task.get_storage()

@@ -1,0 +1,30 @@
+"""Blob-store sharding over several coordinators (reference:
+misc/make_sharded.lua): a full WordCount run with the intermediate files
+spread over 3 coordinator endpoints, and the admin tool's rebalance."""
+from lua_mapreduce_1_amd.cli import make_sharded as MS
+from lua_mapreduce_1_amd.runtime import coordinator
+from lua_mapreduce_1_amd.runtime.cnn import cnn as cnn_cls, shard_of
+from test_e2e_wordcount import SCENARIOS, naive_output, run_job
+
+
+def test_wordcount_over_sharded_blob_store():
+    eps = ",".join(coordinator.start_local() for _ in range(3))
+    got, s = run_job(eps, "wc_sharded", dict(SCENARIOS["combiner_aci"], storage="gridfs", device="host"))
+    assert got == naive_output()
+
+
+def test_rebalance_after_adding_a_shard():
+    a, b = coordinator.start_local(), coordinator.start_local()
+    g1 = cnn_cls(a, "shard_db").gridfs()
+    for i in range(40):
+        g1.store_data(b"x" * i, f"blob{i}")
+    both = f"{a},{b}"
+    before = MS.status(both, "shard_db")
+    assert before[0]["blobs"] == 40 and before[0]["misplaced"] > 0
+    moved = MS.rebalance(both, "shard_db")
+    after = MS.status(both, "shard_db")
+    assert moved == before[0]["misplaced"]
+    assert all(r["misplaced"] == 0 for r in after) and sum(r["blobs"] for r in after) == 40
+    g2 = cnn_cls(both, "shard_db").gridfs()
+    assert all(g2.get(f"blob{i}") == b"x" * i for i in range(40))
+    assert sum(1 for i in range(40) if shard_of(f"blob{i}", 2) == 1) == after[1]["blobs"]
