@@ -18,10 +18,9 @@
 // Each block owns 16 rows of the bunch (4 waves; wave w owns hidden columns
 // [32w, 32w+32)).  X rows are gathered straight from the HBM-resident dataset by
 // index (no host-side batch assembly) into LDS, H and dH stay in LDS, and the
-// per-block parameter gradients go to a workspace.  The LAST block to finish
-// (agent-scope counter, so it works across the 8 XCDs' L2s) sums the partials
-// in fixed block order — deterministic — and resets the counter, so the whole
-// step is one launch and can live in a hipGraph.
+// per-block parameter gradients go to a workspace; a second, chip-wide kernel
+// folds them in fixed block order (deterministic, no atomics).  Both launches
+// are capture-safe (no host synchronisation).
 //
 // f32-in MFMA on gfx950 is exact f32 (a k-ordered fmaf chain), so results match
 // a PyTorch fp32 reference to rounding.  The optimizer step (SGD + momentum +
@@ -64,7 +63,6 @@ __global__ __launch_bounds__(MLP_THREADS) void mlp_grad_kernel(
   __shared__ float rowloss[MLP_ROWS];
   __shared__ float rowok[MLP_ROWS];
   __shared__ int ys[MLP_ROWS];
-  __shared__ unsigned last;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -198,34 +196,20 @@ __global__ __launch_bounds__(MLP_THREADS) void mlp_grad_kernel(
     }
   }
 
-  // ---- last block folds the partials in block order (deterministic)
-  __threadfence();
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = (prev == gridDim.x - 1) ? 1u : 0u;
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  const int nb = gridDim.x;
-  if (do_grad) {
-    for (int p = tid; p < Lay::P; p += MLP_THREADS) {
-      float g = 0.f;
-      for (int b = 0; b < nb; ++b) g += __builtin_nontemporal_load(partials + (size_t)b * (Lay::P + 2) + p);
-      grads[p] = g;
-    }
-  }
-  if (tid == 0) {
-    float l = 0.f, ok = 0.f;
-    for (int b = 0; b < nb; ++b) {
-      l += __builtin_nontemporal_load(partials + (size_t)b * (Lay::P + 2) + Lay::P);
-      ok += __builtin_nontemporal_load(partials + (size_t)b * (Lay::P + 2) + Lay::P + 1);
-    }
-    loss_out[0] = l;
-    loss_out[1] = ok;
-    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+}
+
+// Fold the per-block partials in block order (deterministic): one thread per
+// parameter (+2 loss slots), so the fold is spread over the whole chip (a
+// last-block fold by ONE workgroup cost 0.3 ms at B=128 and grew with B).
+__global__ void __launch_bounds__(256) mlp_fold_kernel(const float* __restrict__ partials, int nb, int P,
+                                                       float* __restrict__ grads, float* __restrict__ loss_out,
+                                                       int do_grad) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P + 2 || (!do_grad && p < P)) return;
+  float g = 0.f;
+  for (int b = 0; b < nb; ++b) g += partials[(size_t)b * (P + 2) + p];
+  if (p < P) grads[p] = g;
+  else loss_out[p - P] = g;
 }
 
 // w <- w + v,  v <- momentum * v - lr * (scale * g + wd * decay(p) * w)
@@ -250,7 +234,7 @@ extern "C" {
 int mr_mlp_param_count(int in, int hid, int out) { return in * hid + hid + hid * out + out; }
 int mr_mlp_rows_per_block() { return MLP_ROWS; }
 
-// partials: ceil(B/16) * (P + 2) floats; counter: one zeroed u32 (left zeroed).
+// partials: ceil(B/16) * (P + 2) floats; counter: unused (kept for ABI stability).
 int mr_mlp_grad(const void* X, const void* labels, const void* idx, int B, int in, int hid, int out,
                 const void* params, void* grads, void* loss_out, void* partials, void* counter, int do_grad,
                 hipStream_t s) {
@@ -260,6 +244,9 @@ int mr_mlp_grad(const void* X, const void* labels, const void* idx, int B, int i
   hipLaunchKernelGGL((mlp_grad_kernel<256, 128, 10>), dim3(nb), dim3(MLP_THREADS), 0, s, (const float*)X,
                      (const int*)labels, (const int*)idx, B, (const float*)params, (float*)grads, (float*)loss_out,
                      (float*)partials, (unsigned*)counter, do_grad);
+  const int P = MlpLayout<256, 128, 10>::P;
+  hipLaunchKernelGGL(mlp_fold_kernel, dim3((P + 2 + 255) / 256), dim3(256), 0, s, (const float*)partials, nb, P,
+                     (float*)grads, (float*)loss_out, do_grad);
   return (int)hipGetLastError();
 }
 
