@@ -12,9 +12,9 @@ Reference semantics (examples/APRIL-ANN/init.lua, common.lua):
   step, validation loss, checkpoint, then ``"loop"`` until the stopping rule
   (``max_epochs_wo_imp_relative(2)``, min 20 / max 40 epochs, init.lua:48-54).
 
-MI355X design: the whole step is two kernel launches (fused MFMA
-forward/backward with in-kernel deterministic partial reduction, then the
-element-wise SGD), parameters are ONE flat fp32 vector, and across ranks the
+MI355X design: the gradient is one fused MFMA forward/backward kernel plus a
+deterministic fold, the update one element-wise SGD kernel, both halves of an
+epoch replayed as hipGraphs; parameters are ONE flat fp32 vector, and across ranks the
 "reduce" phase is ONE RCCL all-reduce of ``[grads | loss, correct, count]``
 (SUM) — the shuffle of 4 weight-name partitions degenerates to an all-reduce
 because every key goes everywhere.  The server/worker form of the same
@@ -124,26 +124,72 @@ class DigitsTrainer:
     def state(self) -> dict:
         return {"w": self.w.cpu().numpy(), "v": self.v.cpu().numpy()}
 
+    # -- hipGraph-captured epoch -------------------------------------------------
+    def capture(self, n_local: int, global_count: int) -> None:
+        """Capture the two launch-bound halves of an epoch as hipGraphs (via
+        torch.cuda.CUDAGraph, which is hipGraph on ROCm):
+          A: fused gradient of the bunch in ``self.static_idx`` -> ``buf``;
+          B: SGD update (global bunch count is fixed, so is the smoothing
+             scale) + validation forward -> ``self.report``.
+        The all-reduce between them stays eager (RCCL), and one 5-float D2H per
+        epoch feeds the host-side stopping rule."""
+        d = self.device
+        self.static_idx = torch.zeros(max(n_local, 1), dtype=torch.int32, device=d)
+        self.report = torch.zeros(5, dtype=torch.float32, device=d)
+        self.report_host = torch.zeros(5, dtype=torch.float32, pin_memory=True)
+        scale = 1.0 / math.sqrt(max(global_count, 1)) if self.h["smooth_gradients"] else 1.0
+        h = self.h
+        from ..ops import _hip
+        _hip.lib()  # load outside capture
+        self.graph_a = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_a):
+            if n_local:
+                loss = M.grad_step(self.tx, self.ty, self.static_idx, self.w, self.grads, self.ws)
+                self.buf[-3:-1].copy_(loss)
+                self.buf[-1].fill_(float(n_local))
+            else:
+                self.buf.zero_()
+        self.graph_b = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_b):
+            M.sgd_step(self.w, self.grads, self.v, h["learning_rate"], h["momentum"], h["weight_decay"], scale)
+            vl = M.grad_step(self.vx, self.vy, self.vidx, self.w, None, self.vws, want_grad=False)
+            self.report[0:3].copy_(self.buf[-3:])
+            self.report[3:5].copy_(vl)
+
 
 def train_spmd(device="cpu", group=None, data=None, hyper: dict | None = None, epochs: int | None = None,
-               verbose: bool = False) -> dict:
+               verbose: bool = False, graphs: bool | None = None) -> dict:
     """Iterative DP-SGD, one process per GPU: each rank computes the gradients
     of its share of the iteration's map jobs (one fused launch), one all-reduce
     SUMs ``[grads | loss, correct, count]`` over ranks (RCCL on GPUs), then every
     rank applies the identical optimizer step (replicated parameters, like the
-    reference's single finalfn).  Returns the training history."""
+    reference's single finalfn).  On a GPU the two halves of the epoch are
+    replayed hipGraphs (``graphs=False`` runs them eagerly).  Returns the
+    training history."""
     from ..parallel import dist as D
     import torch.distributed as tdist
     rank, world = D.world_info(group)
     tr = DigitsTrainer(device, data, hyper)
     J = tr.h["jobs_per_iteration"]
+    jobs = [j for j in range(1, J + 1) if (j - 1) % world == rank]
+    B = tr.h["bunch_size"]
+    use_graphs = graphs if graphs is not None else tr.device.type == "cuda"
+    if use_graphs:
+        tr.capture(len(jobs) * B, J * B)
+        max_it = epochs if epochs is not None else tr.h["max_epochs"]
+        # every epoch's bunch indices, generated once (same streams as eager)
+        table = torch.stack([tr.bunch_indices(e, jobs) for e in range(1, max_it + 1)]) if jobs else None
     hist = []
     it = 0
     t0 = time.perf_counter()
     while True:
         it += 1
-        jobs = [j for j in range(1, J + 1) if (j - 1) % world == rank]
-        tr.compute_gradients(tr.bunch_indices(it, jobs))
+        if use_graphs:
+            if table is not None:
+                tr.static_idx.copy_(table[it - 1])
+            tr.graph_a.replay()
+        else:
+            tr.compute_gradients(tr.bunch_indices(it, jobs))
         if world > 1:
             if D._is_gloo(group) and tr.buf.is_cuda:
                 h = tr.buf.cpu()
@@ -151,9 +197,17 @@ def train_spmd(device="cpu", group=None, data=None, hyper: dict | None = None, e
                 tr.buf.copy_(h)
             else:
                 tdist.all_reduce(tr.buf, group=group)
-        tot = tr.buf[-3:].tolist()
-        tr.apply(tr.grads, tot[2])
-        va_loss, va_acc = tr.validate()
+        if use_graphs:
+            tr.graph_b.replay()
+            tr.report_host.copy_(tr.report)  # the one synchronising read per epoch
+            tot0, tot1, tot2, vl, vok = tr.report_host.tolist()
+            tot = [tot0, tot1, tot2]
+            nv = tr.vx.shape[0]
+            va_loss, va_acc = vl / nv, vok / nv
+        else:
+            tot = tr.buf[-3:].tolist()
+            tr.apply(tr.grads, tot[2])
+            va_loss, va_acc = tr.validate()
         tr_loss = tot[0] / max(tot[2], 1.0)
         go = tr.stop.update(tr_loss, va_loss)
         hist.append({"epoch": it, "tr_loss": tr_loss, "va_loss": va_loss, "va_acc": va_acc,

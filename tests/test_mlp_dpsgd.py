@@ -199,3 +199,11 @@ def test_train_spmd_gpu_matches_cpu(gpu):
     rc = T.train_spmd("cpu", data=DATA, epochs=6)
     np.testing.assert_allclose([h["va_loss"] for h in rg["history"]], [h["va_loss"] for h in rc["history"]],
                                rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_graph_epochs_equal_eager(gpu):
+    rg = T.train_spmd(gpu, data=DATA, epochs=5, graphs=True)
+    re_ = T.train_spmd(gpu, data=DATA, epochs=5, graphs=False)
+    assert torch.equal(rg["params"], re_["params"])
+    assert [h["va_loss"] for h in rg["history"]] == [h["va_loss"] for h in re_["history"]]
