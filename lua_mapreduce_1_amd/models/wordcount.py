@@ -24,6 +24,10 @@ def taskfn(emit):
         emit(i + 1, {"split": i})
 
 
+# the job list is a pure function of init args: SPMD ranks evaluate it locally
+spmd_replicated_taskfn = True
+
+
 device_input = "split"
 
 

@@ -168,7 +168,10 @@ class SPMDEngine:
 
     def _jobs(self) -> list[tuple]:
         jobs = []
-        if self.rank == 0:
+        # a taskfn declared pure (``spmd_replicated_taskfn = True``: its job list
+        # depends only on init args) is evaluated by every rank: no broadcast
+        replicated = bool(modules.field(self.taskfn, "spmd_replicated_taskfn"))
+        if self.rank == 0 or replicated:
             seen = set()
 
             def emit(k, v):
@@ -177,7 +180,7 @@ class SPMDEngine:
                 seen.add(k)
                 jobs.append((k, v))
             modules.field(self.taskfn, "taskfn")(emit)
-        if self.world > 1:
+        if self.world > 1 and not replicated:
             jobs = D.broadcast_object(jobs, 0, self.group, self.device if self.device.type == "cuda" else None)
         return jobs
 
@@ -306,8 +309,10 @@ class SPMDEngine:
             return self.arena
         return self._ctx.source()
 
-    def _shuffle(self, hi, lo, val, rep, src, part):
-        """Send each key to rank part % W; returns received (hi, lo, val, rep, src)."""
+    def _shuffle(self, hi, lo, val, rep, src, part, failed: int = 0):
+        """Send each key to rank part % W; returns received (hi, lo, val, rep,
+        src) and the job-wide number of failed map jobs (this rank's count rides
+        along with the count exchange instead of a separate all-reduce)."""
         W = self.world
         dest = torch.remainder(part, W).to(torch.int64)
         perm = ops.sort_keys([dest], bits=[max(1, (W - 1).bit_length())]).long()
@@ -317,10 +322,12 @@ class SPMDEngine:
         counts = ops.bincount(dest.to(torch.int32), W)
         bcounts = torch.zeros(W, dtype=torch.int64, device=hi.device)
         bcounts.index_add_(0, dest[perm], lens)
-        send = torch.stack([counts, bcounts])
-        recv = D.exchange_counts(send.t().contiguous().view(-1), self.group).view(W, 2)
-        send_h = send.cpu().tolist()
-        recv_h = recv.cpu().tolist()
+        send = torch.stack([counts, bcounts, torch.full_like(counts, int(failed))])
+        recv = D.exchange_counts(send.t().contiguous().view(-1), self.group).view(W, 3)
+        both = torch.cat([send, recv.t()], 1).cpu().tolist()  # one host sync
+        send_h = [row[:W] for row in both]
+        recv_h = [[both[0][W + r], both[1][W + r], both[2][W + r]] for r in range(W)]
+        self._failed_total = sum(r[2] for r in recv_h)
         rec = torch.stack([hi, lo, val, lens], dim=1)
         rrec = D.all_to_all_v(rec, send_h[0], [r[0] for r in recv_h], self.group)
         rblob = D.all_to_all_v(blob, send_h[1], [r[1] for r in recv_h], self.group)
@@ -363,8 +370,10 @@ class SPMDEngine:
         hi, lo, val, rep = self.table.compact()
         src = self._source()
         part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
+        failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
+        self._failed_total = failed
         if self.world > 1:
-            hi, lo, val, rep, src = self._shuffle(hi, lo, val, rep, src, part)
+            hi, lo, val, rep, src = self._shuffle(hi, lo, val, rep, src, part, failed)
             hi, lo, val, rep = self._reduce(hi, lo, val, rep, src)
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         T["shuffle"] = time.time() - t1
@@ -383,8 +392,7 @@ class SPMDEngine:
         res.total_value = int(cols["val"].sum()) if cols["val"].size else 0
         T["reduce"] = time.time() - t2
         T["iteration"] = time.time() - t_start
-        failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
-        res.failed_maps = D.all_reduce_sum_int(failed, self.device, self.group) if self.world > 1 else failed
+        res.failed_maps = self._failed_total
         return res
 
     # ------------------------------------------------------------------------
