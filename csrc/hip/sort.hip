@@ -443,8 +443,26 @@ __global__ void bincount_kernel(const u32* ids, u64 n, u32 nbins, long long* cou
 // columns.  Runs longer than FIX_MAX set *bad (caller falls back to the full
 // 136-bit sort).
 constexpr int FIX_MAX = 64;
+
+// Byte k of a key (or -1 past its end): packed keys from (hi, lo), long keys
+// from their bytes in src at rep's offset.
+__device__ __forceinline__ int key_byte_at(u64 h, u64 l, u64 r, const u8* src, u32 k) {
+  if (!key_is_long(l)) return k < packed_len(l) ? (int)packed_byte(h, l, k) : -1;
+  return k < rep_len(r) ? (int)src[rep_off(r) + k] : -1;
+}
+
+// Exact bytewise "a < b" for keys with EQUAL hi (the first 8 bytes).
+__device__ __forceinline__ bool tail_less(u64 h, u64 la, u64 ra, u64 lb, u64 rb, const u8* src) {
+  if (!key_is_long(la) && !key_is_long(lb)) return la < lb;
+  for (u32 k = 8;; ++k) {
+    const int x = key_byte_at(h, la, ra, src, k), y = key_byte_at(h, lb, rb, src, k);
+    if (x != y) return x < y;  // -1 (end) sorts first: a prefix is smaller
+    if (x < 0) return false;
+  }
+}
+
 __global__ void tie_fixup_kernel(const u64* c, u64* hi, u64* lo, long long* val, u64* rep, u32* part, u64 n,
-                                 u32* bad) {
+                                 u32* bad, const u8* src) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     if (i > 0 && c[i] == c[i - 1]) continue;  // not a run head
@@ -455,12 +473,20 @@ __global__ void tie_fixup_kernel(const u64* c, u64* hi, u64* lo, long long* val,
       atomicOr(bad, 1u);
       continue;
     }
-    for (u64 a = i + 1; a < e; ++a) {  // insertion sort on (hi, lo)
+    // insertion sort by exact key order: (hi, lo) for packed keys; with the
+    // key bytes (src) also for long keys sharing the 8-byte prefix
+    for (u64 a = i + 1; a < e; ++a) {
       const u64 h = hi[a], l = lo[a], r = rep[a];
       const long long v = val[a];
       const u32 p = part[a];
       u64 b = a;
-      while (b > i && (hi[b - 1] > h || (hi[b - 1] == h && lo[b - 1] > l))) {
+      while (b > i) {
+        const u64 hb = hi[b - 1];
+        bool greater;
+        if (hb != h) greater = hb > h;
+        else if (src) greater = tail_less(h, l, r, lo[b - 1], rep[b - 1], src);
+        else greater = lo[b - 1] > l;
+        if (!greater) break;
         hi[b] = hi[b - 1];
         lo[b] = lo[b - 1];
         val[b] = val[b - 1];
@@ -474,11 +500,29 @@ __global__ void tie_fixup_kernel(const u64* c, u64* hi, u64* lo, long long* val,
       rep[b] = r;
       part[b] = p;
     }
-    // bit 2: two adjacent keys share the 8-byte prefix and one is a long
-    // (hashed) key -> their relative order needs a bytewise check on the host
-    for (u64 a = i + 1; a < e; ++a)
-      if (hi[a] == hi[a - 1] && part[a] == part[a - 1] && (key_is_long(lo[a]) || key_is_long(lo[a - 1])))
-        atomicOr(bad, 2u);
+    // bit 2 (no key bytes given): two adjacent keys share the 8-byte prefix and
+    // one is a long (hashed) key -> the host must check their order bytewise
+    if (!src)
+      for (u64 a = i + 1; a < e; ++a)
+        if (hi[a] == hi[a - 1] && part[a] == part[a - 1] && (key_is_long(lo[a]) || key_is_long(lo[a - 1])))
+          atomicOr(bad, 2u);
+  }
+}
+
+// Gather up to 5 u64 columns and one u32 column by an int32 permutation in
+// one launch (the sort's row reorder; replaces one framework gather per column).
+__global__ void gather_cols_kernel(const u32* __restrict__ perm, u64 n, const u64* a0, const u64* a1, const u64* a2,
+                                   const u64* a3, const u64* a4, const u32* b0, u64* o0, u64* o1, u64* o2, u64* o3,
+                                   u64* o4, u32* q0) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 j = perm[i];
+    if (a0) o0[i] = a0[j];
+    if (a1) o1[i] = a1[j];
+    if (a2) o2[i] = a2[j];
+    if (a3) o3[i] = a3[j];
+    if (a4) o4[i] = a4[j];
+    if (b0) q0[i] = b0[j];
   }
 }
 
@@ -662,10 +706,20 @@ int mr_composite_key(const void* part, const void* hi, u64 n, void* out, hipStre
 }
 
 int mr_tie_fixup(const void* c, void* hi, void* lo, void* val, void* rep, void* part, u64 n, void* bad,
-                 hipStream_t s) {
+                 const void* src, hipStream_t s) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(tie_fixup_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)c, (u64*)hi, (u64*)lo,
-                     (long long*)val, (u64*)rep, (u32*)part, n, (u32*)bad);
+                     (long long*)val, (u64*)rep, (u32*)part, n, (u32*)bad, (const u8*)src);
+  return (int)hipGetLastError();
+}
+
+int mr_gather_cols(const void* perm, u64 n, const void* a0, const void* a1, const void* a2, const void* a3,
+                   const void* a4, const void* b0, void* o0, void* o1, void* o2, void* o3, void* o4, void* q0,
+                   hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(gather_cols_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u32*)perm, n,
+                     (const u64*)a0, (const u64*)a1, (const u64*)a2, (const u64*)a3, (const u64*)a4,
+                     (const u32*)b0, (u64*)o0, (u64*)o1, (u64*)o2, (u64*)o3, (u64*)o4, (u32*)q0);
   return (int)hipGetLastError();
 }
 

@@ -132,12 +132,20 @@ class HashTable:
             self._ovf_counter = torch.zeros(1, dtype=torch.int64, device=d)
         return self._ovf, self._ovf_counter
 
-    def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, chunk_bytes: int = 32 * 1024,
+    def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, chunk_bytes: int | None = None,
                       version: int = 2, mode: int = 0) -> None:
-        """Fused tokenize + exact key + combine of every whitespace token (value 1)."""
+        """Fused tokenize + exact key + combine of every whitespace token (value 1).
+
+        ``chunk_bytes`` = bytes per workgroup; by default ~nbytes/1024 rounded to
+        the 8 KiB tile and clamped to [8, 32] KiB: a workgroup's latency (LDS
+        combine + flush of its distinct words) is ~130 us at 32 KiB and the
+        kernel runs one workgroup per CU, so small launches need small chunks
+        to spread over the 256 CUs."""
         nbytes = text.numel()
         if nbytes == 0:
             return
+        if chunk_bytes is None:
+            chunk_bytes = min(32 * 1024, max(8192, (nbytes // 1024 + 8191) // 8192 * 8192))
         if self.is_cuda:
             assert text.dtype == torch.uint8 and text.is_contiguous()
             if version == 1:
@@ -166,10 +174,12 @@ class HashTable:
             return int(c[0]), bool(c[1])
         return sum(p[0].size for p in self._pending), False
 
-    def compact(self):
-        """Dense (hi, lo, val, rep) of all occupied slots (unsorted on GPU)."""
+    def compact(self, known_stats: tuple[int, bool] | None = None):
+        """Dense (hi, lo, val, rep) of all occupied slots (unsorted on GPU).
+        ``known_stats``: the (n, overflow) of a stats() call made since the last
+        insert (saves a second host synchronisation)."""
         if self.is_cuda:
-            n, ovf = self.stats()
+            n, ovf = known_stats if known_stats is not None else self.stats()
             if ovf:
                 raise OverflowError("hash table overflow")
             d = self.device
@@ -424,19 +434,21 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
 
 
 def sort_by_partition_key(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, val: torch.Tensor,
-                          rep: torch.Tensor, nparts: int):
-    """Rows ordered by (partition, hi, lo) -> (part, hi, lo, val, rep, bad).
+                          rep: torch.Tensor, nparts: int, src: torch.Tensor | None = None):
+    """Rows ordered by (partition, key) -> (part, hi, lo, val, rep, bad).
 
     GPU fast path (nparts <= 256): radix-sort ONE u64 composite word
-    ``part << 56 | hi >> 8`` (8 passes instead of 17) and insertion-sort the
-    short runs that tie on it by (hi, lo) in a fixup kernel; ``bad`` (device
-    int32) is non-zero when a run exceeded the fixup limit, in which case the
-    caller must use the full multi-word sort.  CPU: lexsort.
+    ``part << 56 | hi >> 8`` (8 passes instead of 17), reorder the columns with
+    one gather launch, and insertion-sort the short runs that tie on it in a
+    fixup kernel — by exact key order when the key bytes ``src`` are given
+    (long keys sharing the 8-byte prefix compared bytewise on the device).
+    ``bad`` (device int32): bit 0 = a run exceeded the fixup limit (caller must
+    use the full multi-word sort); bit 1 = no ``src`` and a long-key prefix tie
+    exists (the host must check those keys bytewise).  CPU: lexsort (+bit 1).
     """
     n = hi.numel()
     if not hi.is_cuda or nparts > 256:
         perm = sort_keys([part.to(torch.int64), hi, lo], bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
-        # bit 2: the host must check the order of long keys sharing a prefix
         bad = torch.full((1,), 2, dtype=torch.int32, device=hi.device)
         return part[perm], hi[perm], lo[perm], val[perm], rep[perm], bad
     d = hi.device
@@ -444,12 +456,16 @@ def sort_by_partition_key(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor
     part = part.to(torch.int32).contiguous()
     c = torch.empty(n, dtype=torch.int64, device=d)
     _hip.call("mr_composite_key", _hip.ptr(part), _hip.ptr(hi), n, _hip.ptr(c), s)
-    perm = sort_keys([c]).long()
-    c, part, hi, lo, val, rep = c[perm], part[perm], hi[perm], lo[perm], val[perm], rep[perm]
+    perm, c = sort_keys([c], return_keys=True)
+    cols = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(4)]
+    part2 = torch.empty(n, dtype=torch.int32, device=d)
+    _hip.call("mr_gather_cols", _hip.ptr(perm), n, _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), None,
+              _hip.ptr(part), *[_hip.ptr(x) for x in cols], None, _hip.ptr(part2), s)
+    hi, lo, val, rep = cols
     bad = torch.zeros(1, dtype=torch.int32, device=d)
-    _hip.call("mr_tie_fixup", _hip.ptr(c), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part),
-              n, _hip.ptr(bad), s)
-    return part, hi, lo, val, rep, bad
+    _hip.call("mr_tie_fixup", _hip.ptr(c), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part2),
+              n, _hip.ptr(bad), _hip.ptr(src) if src is not None else None, s)
+    return part2, hi, lo, val, rep, bad
 
 
 def sort_error(device) -> bool:

@@ -118,8 +118,8 @@ class IterationResult:
 
 class SPMDEngine:
     def __init__(self, params: dict, group=None, device=None, split_store: SplitStore | None = None,
-                 chunk_mb: tuple = (6, 16, 32), verbose: bool = False, table_capacity: int = 1 << 20,
-                 tail_mb: tuple = (8, 3)):
+                 chunk_mb: tuple = (2, 8, 32), verbose: bool = False, table_capacity: int = 1 << 20,
+                 tail_mb: tuple = (8, 2)):
         self.params = dict(params)
         self.group = group
         self.rank, self.world = D.world_info(group)
@@ -211,25 +211,30 @@ class SPMDEngine:
             nbytes = b - a
             if self.arena is None or self.arena.numel() < nbytes:
                 self.arena = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-            # chunk boundaries at split boundaries: sizes ramp up (first copy is
-            # exposed) and back down (last kernel is exposed)
+            # chunk boundaries at split boundaries: sizes ramp up (the first
+            # copy is exposed), run at the big size, and ramp down at the end
+            # (the last kernel is exposed) — also for small per-rank inputs
             offs = self.splits.offsets
             sizes = []
             rem = nbytes
-            tail = [t for t in self.tail_bytes]
-            k = 0
-            while rem > 0:
-                if tail and rem <= sum(tail) + self.chunk_bytes[-1]:
-                    # enter the ramp-down once what is left fits the tail sizes
-                    if rem > sum(tail):
-                        sz = rem - sum(tail)
-                    else:
-                        sz = tail.pop(0)
-                else:
-                    sz = self.chunk_bytes[min(k, len(self.chunk_bytes) - 1)]
-                sizes.append(min(sz, rem))
+            up = list(self.chunk_bytes[:-1])
+            big = self.chunk_bytes[-1]
+            tail = list(self.tail_bytes)
+            ts = sum(tail)
+            while up and rem > up[0] + ts:
+                sizes.append(up.pop(0))
                 rem -= sizes[-1]
-                k += 1
+            while rem > big + ts:
+                sizes.append(big)
+                rem -= big
+            if rem > ts:
+                sizes.append(rem - ts)
+                rem = ts
+            for t in tail:
+                if rem <= 0:
+                    break
+                sizes.append(min(t, rem))
+                rem -= sizes[-1]
             rel = offs[ids[0]:ids[-1] + 2] - offs[ids[0]]
             bidx = np.searchsorted(rel, np.cumsum(sizes), side="left")
             bounds = sorted({0, len(ids)} | {min(int(x), len(ids)) for x in bidx})
@@ -367,7 +372,7 @@ class SPMDEngine:
             n_claimed, overflow = self.table.stats()
         T["map"] = time.time() - t0
         t1 = time.time()
-        hi, lo, val, rep = self.table.compact()
+        hi, lo, val, rep = self.table.compact((n_claimed, overflow))
         src = self._source()
         part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)

@@ -195,3 +195,30 @@ def test_finalize_long_tie_runs(gpu):
     keys = [blob[cols["key_off"][i]:cols["key_off"][i + 1]] for i in range(len(cols["val"]))]
     assert keys == sorted(set(words))
     assert set(cols["val"].tolist()) == {2}
+
+
+def test_device_long_key_order_without_host_fix(gpu):
+    """Long keys sharing 8-byte prefixes (and packed keys with the same
+    prefix) come out in exact bytewise order from the device tie fix-up; the
+    host fallback flag (bit 1) is not raised."""
+    rng = np.random.default_rng(5)
+    pre = [b"internat", b"responsi", b"abcdefgh"]
+    words = set()
+    for p in pre:
+        for _ in range(20):
+            tail = bytes(rng.integers(97, 123, int(rng.integers(0, 14))).astype(np.uint8))
+            words.add(p + tail)
+    words |= {b"a", b"zz", b"internat", b"internatio"}
+    words = sorted(words)
+    text = b" ".join(words * 3) + b"\n"
+    t = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(gpu)
+    tab = ops.HashTable(1 << 12, device=gpu)
+    tab.wordcount_map(t)
+    hi, lo, val, rep = tab.compact()
+    part = torch.zeros(hi.numel(), dtype=torch.int32, device=gpu)
+    p2, h2, l2, v2, r2, bad = ops.sort_by_partition_key(part, hi, lo, val, rep, 1, src=t)
+    assert int(bad.item()) & 2 == 0
+    off, blob = ops.gather_key_bytes(h2, l2, r2, t)
+    off, blob = off.cpu().numpy(), blob.cpu().numpy().tobytes()
+    got = [blob[off[i]:off[i + 1]] for i in range(h2.numel())]
+    assert got == words
