@@ -372,6 +372,10 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
             ws = _sort_ws(d, n)
             small = ws["small"]
             small.zero_()  # [0:2048) ghist, [2048:2112) tile counters, [2112] error flag
+            if torch.cuda.is_current_stream_capturing():
+                # a replayed graph reuses its pass epochs: clear the look-back
+                # granules so a replay never sees the previous replay's tags
+                ws["granules"][: ((n + 4095) // 4096) * 256].zero_()
             ghist = small[:2048]
             kbuf = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(2)]
             pbuf = [torch.empty(n, dtype=torch.int32, device=d) for _ in range(2)]

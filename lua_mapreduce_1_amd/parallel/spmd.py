@@ -113,7 +113,13 @@ class IterationResult:
         self.red_jobs: list[JobRecord] = []
         self.timings: dict[str, float] = {}
         self.distinct_keys = 0
-        self.total_value = 0
+        self._vals = None
+
+    @property
+    def total_value(self) -> int:
+        """Sum of all reduced values of this rank (computed on first use)."""
+        v = self._vals
+        return int(v.sum()) if v is not None and v.size else 0
 
 
 class SPMDEngine:
@@ -153,6 +159,11 @@ class SPMDEngine:
         self.red_table: ops.HashTable | None = None
         self.arena: torch.Tensor | None = None
         self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self._plans: dict = {}
+        import os as _os
+        self.use_graphs = _os.environ.get("MR_GRAPHS", "1") != "0"
+        self._tail_graphs: dict = {}
+        self._tail_seen: set = set()
         self.iteration = 0
         self.finished = False
 
@@ -199,6 +210,50 @@ class SPMDEngine:
         return assign_contiguous([self._job_bytes(v) for _, v in jobs], self.rank, self.world)
 
     # -- map ------------------------------------------------------------------
+    def _plan_chunks(self, ids: list[int]):
+        """Chunking of a contiguous split range (cached per range): boundaries
+        at split boundaries, sizes ramping up (the first copy is exposed), big
+        in the middle, ramping down at the end (the last kernel is exposed) —
+        also for small per-rank inputs.  Returns (split bounds, arena views,
+        pinned host views, reusable events)."""
+        a, b = self.splits.region(ids[0], ids[-1] + 1)
+        nbytes = b - a
+        if self.arena is None or self.arena.numel() < nbytes:
+            self.arena = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self._plans = {}
+        offs = self.splits.offsets
+        sizes = []
+        rem = nbytes
+        up = list(self.chunk_bytes[:-1])
+        big = self.chunk_bytes[-1]
+        tail = list(self.tail_bytes)
+        ts = sum(tail)
+        while up and rem > up[0] + ts:
+            sizes.append(up.pop(0))
+            rem -= sizes[-1]
+        while rem > big + ts:
+            sizes.append(big)
+            rem -= big
+        if rem > ts:
+            sizes.append(rem - ts)
+            rem = ts
+        for t in tail:
+            if rem <= 0:
+                break
+            sizes.append(min(t, rem))
+            rem -= sizes[-1]
+        rel = offs[ids[0]:ids[-1] + 2] - offs[ids[0]]
+        bidx = np.searchsorted(rel, np.cumsum(sizes), side="left")
+        bounds = sorted({0, len(ids)} | {min(int(x), len(ids)) for x in bidx})
+        host = self.splits.buffer
+        views, host_views, events = [], [], []
+        for i in range(len(bounds) - 1):
+            ca, cb = self.splits.region(ids[0] + bounds[i], ids[0] + bounds[i + 1])
+            views.append(self.arena[ca - a:cb - a])
+            host_views.append(host[ca:cb])
+            events.append(torch.cuda.Event() if self.copy_stream is not None else None)
+        return bounds, views, host_views, events
+
     def _stage_chunks(self, jobs, j0, j1):
         """Yield (job index range, device tensor) chunks, H2D overlapped with compute."""
         if self.device_input == "split":
@@ -207,57 +262,26 @@ class SPMDEngine:
                 raise ValueError("split jobs of a rank must be contiguous splits")
             if not ids:
                 return
-            a, b = self.splits.region(ids[0], ids[-1] + 1)
-            nbytes = b - a
-            if self.arena is None or self.arena.numel() < nbytes:
-                self.arena = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-            # chunk boundaries at split boundaries: sizes ramp up (the first
-            # copy is exposed), run at the big size, and ramp down at the end
-            # (the last kernel is exposed) — also for small per-rank inputs
-            offs = self.splits.offsets
-            sizes = []
-            rem = nbytes
-            up = list(self.chunk_bytes[:-1])
-            big = self.chunk_bytes[-1]
-            tail = list(self.tail_bytes)
-            ts = sum(tail)
-            while up and rem > up[0] + ts:
-                sizes.append(up.pop(0))
-                rem -= sizes[-1]
-            while rem > big + ts:
-                sizes.append(big)
-                rem -= big
-            if rem > ts:
-                sizes.append(rem - ts)
-                rem = ts
-            for t in tail:
-                if rem <= 0:
-                    break
-                sizes.append(min(t, rem))
-                rem -= sizes[-1]
-            rel = offs[ids[0]:ids[-1] + 2] - offs[ids[0]]
-            bidx = np.searchsorted(rel, np.cumsum(sizes), side="left")
-            bounds = sorted({0, len(ids)} | {min(int(x), len(ids)) for x in bidx})
-            events = []
-            host = self.splits.buffer
+            plan = self._plans.get((ids[0], len(ids)))
+            if plan is None:
+                plan = self._plan_chunks(ids)
+                self._plans[(ids[0], len(ids))] = plan
+            bounds, views, host_views, events = plan
             cs = self.copy_stream
-            for i in range(len(bounds) - 1):
-                ca, cb = self.splits.region(ids[0] + bounds[i], ids[0] + bounds[i + 1])
-                dst = self.arena[ca - a:cb - a]
-                if cs is not None:
-                    with torch.cuda.stream(cs):
-                        dst.copy_(host[ca:cb], non_blocking=True)
-                        ev = torch.cuda.Event()
+            if cs is not None:
+                cur = torch.cuda.current_stream(self.device)
+                cs.wait_stream(cur)  # the arena may still be read by earlier work
+                with torch.cuda.stream(cs):
+                    for dst, src, ev in zip(views, host_views, events):
+                        dst.copy_(src, non_blocking=True)
                         ev.record(cs)
-                else:
-                    dst.copy_(host[ca:cb])
-                    ev = None
-                events.append((i, dst, ev))
-            cur = torch.cuda.current_stream(self.device) if cs is not None else None
-            for i, dst, ev in events:
-                if ev is not None:
+                for i, (dst, ev) in enumerate(zip(views, events)):
                     cur.wait_event(ev)
-                yield (j0 + bounds[i], j0 + bounds[i + 1]), dst
+                    yield (j0 + bounds[i], j0 + bounds[i + 1]), dst
+            else:
+                for i, (dst, src) in enumerate(zip(views, host_views)):
+                    dst.copy_(src)
+                    yield (j0 + bounds[i], j0 + bounds[i + 1]), dst
         elif self.device_input == "file":
             from ..ops import io as mio
             for j in range(j0, j1):
@@ -352,6 +376,37 @@ class SPMDEngine:
         return self.red_table.compact()
 
     # ------------------------------------------------------------------------
+    def _graph_tail_ok(self) -> bool:
+        return (self.use_graphs and self.device.type == "cuda" and self.partmod is not None
+                and getattr(self.partmod, "device_partition", None) is not None)
+
+    def _graphed_tail(self, n: int, overflow: bool, src):
+        """Device tail of a W=1 iteration as a hipGraph, captured the second
+        time the same (table fill, input) shows up and replayed afterwards —
+        the tail is ~25 short launches whose Python/launch overhead would
+        otherwise dominate small per-rank inputs."""
+        key = (n, src.data_ptr(), src.numel(), self.table.tag.data_ptr())
+        hit = self._tail_graphs.get(key)
+        if hit is not None:
+            g, pend = hit
+            g.replay()
+            return pend
+        if key not in self._tail_seen:
+            self._tail_seen.add(key)
+            hi, lo, val, rep = self.table.compact((n, overflow))
+            part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
+            return devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
+        if len(self._tail_graphs) >= 4:
+            self._tail_graphs.clear()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            hi, lo, val, rep = self.table.compact((n, overflow))
+            part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
+            pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
+        self._tail_graphs[key] = (g, pend)
+        g.replay()
+        return pend
+
     def run_iteration(self) -> IterationResult:
         self.iteration += 1
         res = IterationResult()
@@ -372,18 +427,26 @@ class SPMDEngine:
             n_claimed, overflow = self.table.stats()
         T["map"] = time.time() - t0
         t1 = time.time()
-        hi, lo, val, rep = self.table.compact((n_claimed, overflow))
         src = self._source()
-        part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
         self._failed_total = failed
+        pend = None
+        if self.world == 1 and self._graph_tail_ok():
+            # the whole device tail (compact -> partition -> sort -> key bytes
+            # -> downloads) is one replayed hipGraph once a table size repeats
+            pend = self._graphed_tail(n_claimed, overflow, src)
+        else:
+            hi, lo, val, rep = self.table.compact((n_claimed, overflow))
+            part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         if self.world > 1:
             hi, lo, val, rep, src = self._shuffle(hi, lo, val, rep, src, part, failed)
             hi, lo, val, rep = self._reduce(hi, lo, val, rep, src)
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         T["shuffle"] = time.time() - t1
         t2 = time.time()
-        cols = devmod.finalize(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
+        if pend is None:
+            pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
+        cols = devmod.finalize_host(pend, self.partmod)
         digits = len(str(max(self.nparts - 1, 0)))
         for p in range(self.nparts):
             if cols["bounds"][p + 1] > cols["bounds"][p]:
@@ -394,7 +457,7 @@ class SPMDEngine:
                 r.real_time = r.written - t1
                 res.red_jobs.append(r)
         res.distinct_keys = int(cols["val"].size)
-        res.total_value = int(cols["val"].sum()) if cols["val"].size else 0
+        res._vals = cols["val"]
         T["reduce"] = time.time() - t2
         T["iteration"] = time.time() - t_start
         res.failed_maps = self._failed_total

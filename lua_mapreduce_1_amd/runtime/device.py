@@ -193,6 +193,15 @@ def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: to
     with a single synchronisation.  NOTE: the arrays alias the pinned pool and
     stay valid until the next finalize() call (copy them to keep them longer).
     """
+    pend = finalize_device(hi, lo, val, rep, src, nparts, partition_module, part, _presorted)
+    return finalize_host(pend, partition_module, need_keys)
+
+
+def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, part: torch.Tensor | None = None,
+                    _presorted: bool = False) -> dict:
+    """The device half of :func:`finalize`: every kernel and device->pinned
+    copy, no host synchronisation (so it can be captured in a hipGraph once
+    the pinned buffers exist).  Returns the pending state for finalize_host."""
     n = hi.numel()
     if part is None:
         part = partition_of(hi, lo, rep, src, nparts, partition_module)
@@ -202,29 +211,40 @@ def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: to
     else:
         part, hi, lo, val, rep, bad = ops.sort_by_partition_key(part, hi, lo, val, rep, nparts,
                                                                 src=src if hi.is_cuda else None)
-    if hi.is_cuda:
-        # blob capacity bound: distinct keys occupy disjoint bytes of their source
-        cap = src.numel() if src is not None else max(16 * n, 1)
-        off, blob = ops.gather_key_bytes(hi, lo, rep, src, capacity=cap)
-    else:
+    pend = {"n": n, "nparts": nparts, "args": args, "src": src, "presorted": _presorted, "hi": hi, "lo": lo}
+    if not hi.is_cuda:
         off, blob = ops.gather_key_bytes(hi, lo, rep, src)
+        counts = ops.bincount(part, nparts) if n else torch.zeros(nparts, dtype=torch.int64)
+        pend.update(val=val, off=off, blob=blob, counts=counts)
+        return pend
+    # blob capacity bound: distinct keys occupy disjoint bytes of their source
+    cap = src.numel() if src is not None else max(16 * n, 1)
+    off, blob = ops.gather_key_bytes(hi, lo, rep, src, capacity=cap)
     counts = ops.bincount(part, nparts) if n else torch.zeros(nparts, dtype=torch.int64, device=hi.device)
+    hv = _to_host(val, "val")
+    ho = _to_host(off.to(torch.int32), "off32") if cap < 2**31 else _to_host(off, "off64")
+    est = _BLOB_EST.get(hi.device)
+    if est is not None:
+        # steady state: DMA (SDMA engine, full PCIe rate) a little more than
+        # last time's size; the rare overflow is topped up after the sync
+        est = min(est, blob.numel())
+        hb = _POOL.get("blob", max(est, 1 << 16), torch.uint8)
+        hb[:est].copy_(blob[:est], non_blocking=True)
+    else:
+        hb = _POOL.get("blob", max(1 << 20, 16 * n), torch.uint8)
+        ops.copy_to_host(blob, hb, off[n:])  # size read on the device: no sync before the copy
+    pend.update(off=off, blob=blob, est=est, hv=hv, ho=ho, hb=hb, hc=_to_host(counts, "counts"),
+                hbad=_to_host(bad, "bad"))
+    return pend
+
+
+def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) -> dict:
+    """The host half of :func:`finalize`: one synchronisation, then numpy."""
+    n, nparts = pend["n"], pend["nparts"]
+    hi, lo = pend["hi"], pend["lo"]
     if hi.is_cuda:
-        hv = _to_host(val, "val")
-        ho = _to_host(off.to(torch.int32), "off32") if cap < 2**31 else _to_host(off, "off64")
-        est = _BLOB_EST.get(hi.device)
-        if est is not None:
-            # steady state: DMA (SDMA engine, full PCIe rate) a little more than
-            # last time's size; the rare overflow is topped up after the sync
-            est = min(est, blob.numel())
-            hb = _POOL.get("blob", max(est, 1 << 16), torch.uint8)
-            hb[:est].copy_(blob[:est], non_blocking=True)
-        else:
-            hb = _POOL.get("blob", max(1 << 20, 16 * n), torch.uint8)
-            ops.copy_to_host(blob, hb, off[n:])  # size read on the device: no sync before the copy
-        hc = _to_host(counts, "counts")
-        hbad = _to_host(bad, "bad")
         torch.cuda.current_stream(hi.device).synchronize()
+        ho, hb, est, blob = pend["ho"], pend["hb"], pend["est"], pend["blob"]
         nbytes = int(ho[n]) if n else 0
         if est is not None and nbytes > est:  # grew past the estimate: copy the rest
             hb = _POOL.get("blob", nbytes, torch.uint8)
@@ -234,22 +254,25 @@ def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: to
             hb.copy_(blob[:nbytes])
         _BLOB_EST[hi.device] = nbytes + nbytes // 16 + 4096
         hb = hb[:nbytes]
-        flag = int(hbad[0])
+        flag = int(pend["hbad"][0])
         if flag & 1:
             # a tie run was too long for the fixup kernel: redo with the full sort
-            ahi, alo, aval, arep = args
+            ahi, alo, aval, arep = pend["args"]
+            src = pend["src"]
             p2 = partition_of(ahi, alo, arep, src, nparts, partition_module)
             perm = ops.sort_keys([p2.to(torch.int64), ahi, alo],
                                  bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
             return finalize(ahi[perm], alo[perm], aval[perm], arep[perm], src, nparts, partition_module,
                             part=p2[perm], _presorted=True, need_keys=need_keys)
-        h_val, h_off, h_blob, h_counts = hv.numpy(), ho.numpy().astype(np.int64), hb.numpy(), hc.numpy()
-        need_fix = bool(flag & 2) or _presorted
+        # offsets stay int32 when the blob is < 2 GiB (no host-side widening pass)
+        h_val, h_off, h_blob, h_counts = pend["hv"].numpy(), ho.numpy(), hb.numpy(), pend["hc"].numpy()
+        need_fix = bool(flag & 2) or pend["presorted"]
         h_hi = hi.cpu().numpy().view(np.uint64) if (need_fix or need_keys) else None
         h_lo = lo.cpu().numpy().view(np.uint64) if (need_fix or need_keys) else None
     else:
         h_hi, h_lo = hi.numpy().view(np.uint64), lo.numpy().view(np.uint64)
-        h_val, h_off, h_blob, h_counts = val.numpy(), off.numpy(), blob.numpy(), counts.numpy()
+        h_val, h_off, h_blob, h_counts = (pend["val"].numpy(), pend["off"].numpy(), pend["blob"].numpy(),
+                                          pend["counts"].numpy())
         need_fix = True
     bounds = np.zeros(nparts + 1, np.int64)
     np.cumsum(h_counts, out=bounds[1:])

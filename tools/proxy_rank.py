@@ -27,6 +27,7 @@ def main() -> int:
     ap.add_argument("--of", type=int, default=8)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--freeze", action="store_true", help="gc.freeze() after warm-up")
     a = ap.parse_args()
     rank, world, device = D.init_from_env()
     splits = load_corpus(1234, 0, 0, 1, device)
@@ -38,12 +39,22 @@ def main() -> int:
     for _ in range(a.warmup):
         eng.run_iteration()
     torch.cuda.synchronize()
+    if a.freeze:
+        import gc
+        gc.collect()
+        gc.freeze()
+    per = []
     t0 = time.perf_counter()
     for _ in range(a.steps):
+        t1 = time.perf_counter()
         res = eng.run_iteration()
+        per.append(1000 * (time.perf_counter() - t1))
     torch.cuda.synchronize()
     ms = 1000 * (time.perf_counter() - t0) / a.steps
-    print(json.dumps({"of": a.of, "splits": k, "bytes": int(store.offsets[-1]), "ms_per_step": ms,
+    seq = [round(x, 2) for x in per]
+    per.sort()
+    print(json.dumps({"of": a.of, "splits": k, "bytes": int(store.offsets[-1]), "ms_per_step": ms, "seq": seq,
+                      "min": per[0], "median": per[len(per) // 2], "max": per[-1],
                       "timings": res.timings}), flush=True)
     return 0
 
