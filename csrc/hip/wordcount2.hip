@@ -34,7 +34,7 @@ constexpr int SLOTS = 4096;
 constexpr int CLAIM_LIMIT = SLOTS * 3 / 4;
 constexpr int PROBES = 32;
 
-enum Mode : int { FULL = 0, TOKENIZE_ONLY = 1, NO_GLOBAL = 2, NO_OVERFLOW = 3 };
+enum Mode : int { FULL = 0, TOKENIZE_ONLY = 1, NO_GLOBAL = 2, NO_OVERFLOW = 3, STAGED_FLUSH = 4 };
 
 struct Lds {
   u8 txt[TXT];
@@ -53,6 +53,7 @@ struct Ovf {
   u64* rep;
   u64 cap;
   unsigned long long* counter;
+  u32* cnt;  // per-entry count (STAGED mode); null: every entry counts 1
 };
 
 __device__ __forceinline__ u32 ws_mask_word(u32 w) {
@@ -125,6 +126,7 @@ __device__ __forceinline__ u32 overflow_push(const Ovf& o, const GTab& g, u64 hi
     o.hi[idx] = hi;
     o.lo[idx] = lo;
     o.rep[idx] = rep;
+    if (o.cnt) o.cnt[idx] = 1u;
     return 0;
   }
   return gtab_insert(g, hi, lo, 1, rep, OP_SUM) == 2;
@@ -248,7 +250,7 @@ __global__ void __launch_bounds__(T) wc_map2_kernel(const u8* __restrict__ text,
         }
         const u64 grep = make_rep(rep_base + gpos, len);
         const bool ok = len < 65536 && lds_insert(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16));
-        if (!ok && MODE == FULL) claims += overflow_push(ovf, g, hi, lo, grep);
+        if (!ok && (MODE == FULL || MODE == STAGED_FLUSH)) claims += overflow_push(ovf, g, hi, lo, grep);
       }
     }
     __syncthreads();
@@ -261,6 +263,54 @@ __global__ void __launch_bounds__(T) wc_map2_kernel(const u8* __restrict__ text,
   }
   if (MODE == NO_GLOBAL) {
     if (t == 0 && L.nclaimed == 0x7FFFFFFF) sink[0] = 1;
+    return;
+  }
+  if (MODE == STAGED_FLUSH) {
+    // append the block's distinct keys (with counts) to the staging buffer —
+    // coalesced stores, ONE global atomic per block — and leave the HBM-table
+    // inserts to a full-occupancy kernel (this kernel runs 1 workgroup/CU, too
+    // few waves to hide the latency of dependent global atomics)
+    constexpr int PER = SLOTS / T;
+    u32 mine = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) mine += L.tag[t * PER + k] != 0;
+    const int lane = t & 63, wave = t >> 6;
+    u32 incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    __shared__ u32 wsum[T / 64];
+    __shared__ unsigned long long base;
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    u32 before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < T / 64; ++w) {
+      before += w < wave ? wsum[w] : 0u;
+      total += wsum[w];
+    }
+    if (t == 0) base = atomicAdd(ovf.counter, (unsigned long long)total);
+    __syncthreads();
+    unsigned long long pos = base + before + incl - mine;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int s = t * PER + k;
+      if (L.tag[s] == 0) continue;
+      const u32 r = L.rep[s];
+      const u64 rp = make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16);
+      if (pos < ovf.cap) {
+        ovf.hi[pos] = L.hi[s];
+        ovf.lo[pos] = L.lo[s];
+        ovf.rep[pos] = rp;
+        ovf.cnt[pos] = L.cnt[s];
+      } else {
+        claims += gtab_insert(g, L.hi[s], L.lo[s], (long long)L.cnt[s], rp, OP_SUM) == 2;
+      }
+      ++pos;
+    }
+    gtab_count_claims(g, claims);
     return;
   }
   for (int s = t; s < SLOTS; s += T) {
@@ -279,7 +329,7 @@ __global__ void __launch_bounds__(256) ovf_agg_kernel(Ovf o, GTab g) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   u32 claims = 0;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    claims += gtab_insert(g, o.hi[i], o.lo[i], 1, o.rep[i], OP_SUM) == 2;
+    claims += gtab_insert(g, o.hi[i], o.lo[i], o.cnt ? (long long)o.cnt[i] : 1ll, o.rep[i], OP_SUM) == 2;
   gtab_count_claims(g, claims);
 }
 
@@ -294,7 +344,7 @@ extern "C" {
 // modes 1-3 exist for ablation timing only (their tables are incomplete).
 int mr_wc_map2(const void* text, u64 nbytes, u64 chunk_bytes, u64 rep_base, void* tag, void* hi, void* lo, void* val,
                void* rep, void* ctrl, u64 cap, void* ovf_hi, void* ovf_lo, void* ovf_rep, u64 ovf_cap,
-               void* ovf_counter, int mode, hipStream_t stream) {
+               void* ovf_counter, int mode, void* ovf_cnt, hipStream_t stream) {
   if (nbytes == 0) return 0;
   if (chunk_bytes % v2::TILE || chunk_bytes > 65536) return -1;
   GTab g;
@@ -305,7 +355,8 @@ int mr_wc_map2(const void* text, u64 nbytes, u64 chunk_bytes, u64 rep_base, void
   g.rep = (u64*)rep;
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
-  v2::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter};
+  v2::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter, (u32*)ovf_cnt};
+  if (mode == 4 && !ovf_cnt) return -1;
   const u64 nblocks = (nbytes + chunk_bytes - 1) / chunk_bytes;
   const int aligned = ((uintptr_t)text & 15) == 0;
   const u8* tx = (const u8*)text;
@@ -317,7 +368,13 @@ int mr_wc_map2(const void* text, u64 nbytes, u64 chunk_bytes, u64 rep_base, void
                                aligned, (u64*)ovf_counter); break;
     case 3: hipLaunchKernelGGL(v2::wc_map2_kernel<3>, grid, block, 0, stream, tx, nbytes, chunk_bytes, rep_base, g, o,
                                aligned, (u64*)ovf_counter); break;
+    case 4:
+      hipLaunchKernelGGL(v2::wc_map2_kernel<4>, grid, block, 0, stream, tx, nbytes, chunk_bytes, rep_base, g, o,
+                         aligned, (u64*)ovf_counter);
+      hipLaunchKernelGGL(v2::ovf_agg_kernel, dim3(4096), dim3(256), 0, stream, o, g);
+      break;
     default:
+      o.cnt = nullptr;
       hipLaunchKernelGGL(v2::wc_map2_kernel<0>, grid, block, 0, stream, tx, nbytes, chunk_bytes, rep_base, g, o,
                          aligned, (u64*)ovf_counter);
       hipLaunchKernelGGL(v2::ovf_agg_kernel, dim3(2048), dim3(256), 0, stream, o, g);

@@ -17,6 +17,8 @@ Kernel inventory -> function here:
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -69,6 +71,9 @@ def _t64(a: np.ndarray, device="cpu") -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------
+_WC_CHUNK_MAX = int(os.environ.get("MR_WC_CHUNK_MAX", 16 * 1024))
+
+
 class HashTable:
     """Open-addressing (128-bit key -> int64 value, rep) table.
 
@@ -125,10 +130,14 @@ class HashTable:
             self._pending.append((_u64(hi).copy(), _u64(lo).copy(), v, r))
 
     def _overflow(self, nbytes: int):
-        need = min(1 << 24, max(1 << 16, nbytes // 8))
+        """Staging / overflow entries (hi, lo, rep, count): sized for the
+        distinct-per-workgroup keys of a launch (a bit under one entry per 8
+        input bytes); entries past the end are inserted directly."""
+        need = min(1 << 24, max(1 << 16, nbytes // 6))
         if getattr(self, "_ovf", None) is None or self._ovf[0].numel() < need:
             d = self.device
             self._ovf = [torch.empty(need, dtype=torch.int64, device=d) for _ in range(3)]
+            self._ovf_cnt = torch.empty(need, dtype=torch.int32, device=d)
             self._ovf_counter = torch.zeros(1, dtype=torch.int64, device=d)
         return self._ovf, self._ovf_counter
 
@@ -145,7 +154,7 @@ class HashTable:
         if nbytes == 0:
             return
         if chunk_bytes is None:
-            chunk_bytes = min(32 * 1024, max(8192, (nbytes // 1024 + 8191) // 8192 * 8192))
+            chunk_bytes = min(_WC_CHUNK_MAX, max(8192, (nbytes // 1024 + 8191) // 8192 * 8192))
         if self.is_cuda:
             assert text.dtype == torch.uint8 and text.is_contiguous()
             if version == 1:
@@ -157,7 +166,7 @@ class HashTable:
             chunk = min(65536, max(8192, (chunk_bytes + 8191) // 8192 * 8192))
             _hip.call("mr_wc_map2", _hip.ptr(text), nbytes, chunk, rep_base, *self._gtab(),
                       self.cap, _hip.ptr(ovf[0]), _hip.ptr(ovf[1]), _hip.ptr(ovf[2]), ovf[0].numel(),
-                      _hip.ptr(counter), mode, _hip.stream(self.device))
+                      _hip.ptr(counter), mode, _hip.ptr(self._ovf_cnt), _hip.stream(self.device))
         else:
             buf = _np(text)
             starts, lens = K.token_spans(buf)

@@ -161,7 +161,10 @@ class SPMDEngine:
         self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self._plans: dict = {}
         import os as _os
-        self.use_graphs = _os.environ.get("MR_GRAPHS", "1") != "0"
+        # hipGraph replay of the device tail: measured (tools/proxy_rank.py) to
+        # save ~0.05 ms on small per-rank inputs but to cost ~0.25 ms (and show
+        # rare multi-ms stalls) on the full single-GPU corpus, so it is opt-in
+        self.use_graphs = _os.environ.get("MR_GRAPHS", "0") == "1"
         self._tail_graphs: dict = {}
         self._tail_seen: set = set()
         self.iteration = 0

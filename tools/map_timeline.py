@@ -21,6 +21,9 @@ eng = SPMDEngine(dict(taskfn=MODEL, mapfn=MODEL, partitionfn=MODEL, reducefn=MOD
 for _ in range(3):
     eng.run_iteration()
 torch.cuda.synchronize()
+key = next(iter(eng._plans))
+b_, v_, h_, e_ = eng._plans[key]
+eng._plans[key] = (b_, v_, h_, [torch.cuda.Event(enable_timing=True) for _ in e_])
 # instrument: wrap copy + map with events
 jobs = eng._jobs()
 evs = []
@@ -37,6 +40,9 @@ for (a, b), data in gen:
     e2.record()
     chunks.append((data.numel(), e1, e2))
 torch.cuda.synchronize()
+plan = next(iter(eng._plans.values()))
+for i, ev in enumerate(plan[3]):
+    print(f"copy {i} done at {t0.elapsed_time(ev)*1000:8.1f} us")
 for n, e1, e2 in chunks:
     print(f"chunk {n/1e6:7.2f} MB  kernel {t0.elapsed_time(e1)*1000:8.1f} -> {t0.elapsed_time(e2)*1000:8.1f} us"
           f"  ({(t0.elapsed_time(e2)-t0.elapsed_time(e1))*1000:7.1f} us, "

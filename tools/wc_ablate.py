@@ -22,6 +22,9 @@ for name, fn in [
     ("v2 full 64K", lambda: tab.wordcount_map(dev, chunk_bytes=65536)),
     ("v2 full 32K", lambda: tab.wordcount_map(dev, chunk_bytes=32768)),
     ("v2 full 16K", lambda: tab.wordcount_map(dev, chunk_bytes=16384)),
+    ("v2 full staged 64K", lambda: tab.wordcount_map(dev, chunk_bytes=65536, mode=4)),
+    ("v2 full staged 32K", lambda: tab.wordcount_map(dev, chunk_bytes=32768, mode=4)),
+    ("v2 full staged 16K", lambda: tab.wordcount_map(dev, chunk_bytes=16384, mode=4)),
     ("v2 tokenize-only 64K", lambda: tab.wordcount_map(dev, chunk_bytes=65536, mode=1)),
     ("v2 lds-only 64K", lambda: tab.wordcount_map(dev, chunk_bytes=65536, mode=2)),
     ("v2 lds+flush 64K", lambda: tab.wordcount_map(dev, chunk_bytes=65536, mode=3)),
