@@ -157,7 +157,12 @@ class SPMDEngine:
                              "map functions)")
         self.table = ops.HashTable(table_capacity, device=self.device, op=self.op)
         self.red_table: ops.HashTable | None = None
-        self.arena: torch.Tensor | None = None
+        # two input arenas: iteration i maps arenas[slot] while the copies of
+        # iteration i+1 (prefetch) fill the other one
+        self.arenas: list = [None, None]
+        self.slot = 0
+        self._prefetched = None
+        self.prefetch = False
         self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self._plans: dict = {}
         import os as _os
@@ -213,7 +218,11 @@ class SPMDEngine:
         return assign_contiguous([self._job_bytes(v) for _, v in jobs], self.rank, self.world)
 
     # -- map ------------------------------------------------------------------
-    def _plan_chunks(self, ids: list[int]):
+    @property
+    def arena(self):
+        return self.arenas[self.slot]
+
+    def _plan_chunks(self, ids: list[int], slot: int):
         """Chunking of a contiguous split range (cached per range): boundaries
         at split boundaries, sizes ramping up (the first copy is exposed), big
         in the middle, ramping down at the end (the last kernel is exposed) —
@@ -221,9 +230,10 @@ class SPMDEngine:
         pinned host views, reusable events)."""
         a, b = self.splits.region(ids[0], ids[-1] + 1)
         nbytes = b - a
-        if self.arena is None or self.arena.numel() < nbytes:
-            self.arena = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-            self._plans = {}
+        if self.arenas[slot] is None or self.arenas[slot].numel() < nbytes:
+            self.arenas[slot] = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self._plans = {k: v for k, v in self._plans.items() if k[2] != slot}
+        arena = self.arenas[slot]
         offs = self.splits.offsets
         sizes = []
         rem = nbytes
@@ -252,32 +262,70 @@ class SPMDEngine:
         views, host_views, events = [], [], []
         for i in range(len(bounds) - 1):
             ca, cb = self.splits.region(ids[0] + bounds[i], ids[0] + bounds[i + 1])
-            views.append(self.arena[ca - a:cb - a])
+            views.append(arena[ca - a:cb - a])
             host_views.append(host[ca:cb])
             events.append(torch.cuda.Event() if self.copy_stream is not None else None)
         return bounds, views, host_views, events
 
+    def _get_plan(self, ids: list[int], slot: int):
+        key = (ids[0], len(ids), slot)
+        plan = self._plans.get(key)
+        if plan is None:
+            plan = self._plan_chunks(ids, slot)
+            self._plans[key] = plan
+        return plan
+
+    def _issue_copies(self, plan, wait_for=None) -> None:
+        bounds, views, host_views, events = plan
+        cs = self.copy_stream
+        if wait_for is not None:
+            cs.wait_stream(wait_for)  # the arena may still be read by earlier work
+        with torch.cuda.stream(cs):
+            for dst, src, ev in zip(views, host_views, events):
+                dst.copy_(src, non_blocking=True)
+                ev.record(cs)
+
+    def _split_ids(self, jobs, j0, j1):
+        ids = [int(v["split"] if isinstance(v, dict) else v) for _, v in jobs[j0:j1]]
+        if ids and ids != list(range(ids[0], ids[0] + len(ids))):
+            raise ValueError("split jobs of a rank must be contiguous splits")
+        return ids
+
+    def _prefetch(self, jobs, j0, j1) -> None:
+        """Start the next iteration's host->HBM copies (same splits) into the
+        other arena now, so the copy engine keeps streaming while this
+        iteration reduces and finalizes.  Only for a pure taskfn (the next job
+        list is known) and split inputs; a mismatching next plan is re-copied."""
+        if (self.copy_stream is None or self.device_input != "split"
+                or not modules.field(self.taskfn, "spmd_replicated_taskfn")):
+            return
+        ids = self._split_ids(jobs, j0, j1)
+        if not ids:
+            return
+        nslot = 1 - self.slot
+        plan = self._get_plan(ids, nslot)
+        # arenas[nslot] was last read by the previous iteration, which has
+        # completed (its finalize synchronised): no stream dependency needed
+        self._issue_copies(plan)
+        self._prefetched = (ids[0], len(ids), nslot)
+
     def _stage_chunks(self, jobs, j0, j1):
         """Yield (job index range, device tensor) chunks, H2D overlapped with compute."""
         if self.device_input == "split":
-            ids = [int(v["split"] if isinstance(v, dict) else v) for _, v in jobs[j0:j1]]
-            if ids and ids != list(range(ids[0], ids[0] + len(ids))):
-                raise ValueError("split jobs of a rank must be contiguous splits")
+            ids = self._split_ids(jobs, j0, j1)
             if not ids:
                 return
-            plan = self._plans.get((ids[0], len(ids)))
-            if plan is None:
-                plan = self._plan_chunks(ids)
-                self._plans[(ids[0], len(ids))] = plan
+            key = (ids[0], len(ids), self.slot)
+            plan = self._get_plan(ids, self.slot)
             bounds, views, host_views, events = plan
             cs = self.copy_stream
             if cs is not None:
                 cur = torch.cuda.current_stream(self.device)
-                cs.wait_stream(cur)  # the arena may still be read by earlier work
-                with torch.cuda.stream(cs):
-                    for dst, src, ev in zip(views, host_views, events):
-                        dst.copy_(src, non_blocking=True)
-                        ev.record(cs)
+                if self._prefetched == key:
+                    self._prefetched = None  # copies already in flight (prefetch)
+                else:
+                    self._prefetched = None
+                    self._issue_copies(plan, wait_for=cur)
                 for i, (dst, ev) in enumerate(zip(views, events)):
                     cur.wait_event(ev)
                     yield (j0 + bounds[i], j0 + bounds[i + 1]), dst
@@ -410,8 +458,14 @@ class SPMDEngine:
         g.replay()
         return pend
 
-    def run_iteration(self) -> IterationResult:
+    def run_iteration(self, prefetch_next: bool | None = None) -> IterationResult:
+        """One MapReduce iteration.  ``prefetch_next`` (default ``self.prefetch``)
+        starts the next iteration's input copies as soon as this map is done."""
         self.iteration += 1
+        if prefetch_next is None:
+            prefetch_next = self.prefetch
+        if self._prefetched is not None:
+            self.slot = self._prefetched[2]
         res = IterationResult()
         T = res.timings
         t_start = time.time()
@@ -429,6 +483,8 @@ class SPMDEngine:
             self._run_map(jobs, recs, j0, j1)
             n_claimed, overflow = self.table.stats()
         T["map"] = time.time() - t0
+        if prefetch_next:
+            self._prefetch(jobs, j0, j1)
         t1 = time.time()
         src = self._source()
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)

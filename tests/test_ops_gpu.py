@@ -222,3 +222,22 @@ def test_device_long_key_order_without_host_fix(gpu):
     off, blob = off.cpu().numpy(), blob.cpu().numpy().tobytes()
     got = [blob[off[i]:off[i + 1]] for i in range(h2.numel())]
     assert got == words
+
+
+def test_spmd_prefetch_pipelined_iterations_match(gpu):
+    """Iterations whose input copies were prefetched into the other arena give
+    the same results as non-pipelined ones (and the counts stay exact)."""
+    from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore
+    from lua_mapreduce_1_amd.utils.corpus import europarl_like
+    M = "lua_mapreduce_1_amd.models.wordcount"
+    splits = europarl_like(seed=3, lines=20_000, words=400_000, vocab_size=20_000, split_lines=1000)
+    params = dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                  init_args={"nsplits": len(splits), "num_reducers": 10})
+    eng = SPMDEngine(params, device=gpu, split_store=SplitStore(splits))
+    ref = eng.run_iteration()
+    ref_total, ref_keys = ref.total_value, ref.distinct_keys
+    eng.prefetch = True
+    for i in range(5):
+        r = eng.run_iteration(prefetch_next=i < 4)
+        assert r.total_value == ref_total == 400_000 and r.distinct_keys == ref_keys
+    assert eng._prefetched is None

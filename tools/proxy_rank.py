@@ -28,6 +28,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--freeze", action="store_true", help="gc.freeze() after warm-up")
+    ap.add_argument("--no-prefetch", action="store_true")
     a = ap.parse_args()
     rank, world, device = D.init_from_env()
     splits = load_corpus(1234, 0, 0, 1, device)
@@ -36,6 +37,7 @@ def main() -> int:
     params = dict(taskfn=MODEL, mapfn=MODEL, partitionfn=MODEL, reducefn=MODEL, finalfn=MODEL,
                   init_args={"nsplits": k, "num_reducers": 10})
     eng = SPMDEngine(params, device=device, split_store=store)
+    eng.prefetch = not a.no_prefetch
     for _ in range(a.warmup):
         eng.run_iteration()
     torch.cuda.synchronize()
