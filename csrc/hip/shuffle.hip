@@ -1,0 +1,182 @@
+// shuffle.hip — pack a rank's combined (key, value) table by destination rank
+// for the all-to-all shuffle (reference: the per-partition map_results files
+// job.lua:203-221 and their transport), and fix up the
+// received key locations.
+//
+// One record per distinct key: [hi, lo, val, loc] where loc = (byte offset in
+// the destination's key-byte segment) << 24 | key length.  Key bytes of every
+// record are packed into per-destination contiguous segments, so the payload
+// is two all_to_all_single calls (records, bytes) after one count exchange.
+// Records and bytes are placed with per-workgroup range reservations (one
+// global atomic per (workgroup, destination)), so there is no sort by
+// destination and no separate gather: order inside a destination segment is
+// irrelevant because the receiver re-aggregates by key.
+//
+//   pk_count   : per-destination record and byte counts
+//   pk_scan    : exclusive scans -> segment starts; counts -> exchange buffer
+//   pk_scatter : records + key bytes into their segments
+//   pk_fix_loc : received loc -> absolute (offset in the received byte blob)
+#include <hip/hip_runtime.h>
+#include "mr_common.h"
+
+namespace mr {
+namespace pk {
+
+constexpr int T = 256;
+constexpr int MAXW = 256;
+
+__device__ __forceinline__ u32 key_len(u64 lo, u64 rep) { return key_is_long(lo) ? (u32)rep_len(rep) : packed_len(lo); }
+
+__global__ void __launch_bounds__(T) pk_count_kernel(const u64* __restrict__ lo, const u64* __restrict__ rep,
+                                                     const u32* __restrict__ part, u64 n, u32 W,
+                                                     unsigned long long* __restrict__ cnt /*[2W]*/) {
+  __shared__ u32 rc[MAXW];
+  __shared__ unsigned long long bc[MAXW];
+  for (u32 d = threadIdx.x; d < W; d += T) {
+    rc[d] = 0;
+    bc[d] = 0;
+  }
+  __syncthreads();
+  const u64 stride = (u64)gridDim.x * T;
+  for (u64 i = (u64)blockIdx.x * T + threadIdx.x; i < n; i += stride) {
+    const u32 d = part[i] % W;
+    atomicAdd(&rc[d], 1u);
+    atomicAdd(&bc[d], (unsigned long long)key_len(lo[i], rep[i]));
+  }
+  __syncthreads();
+  for (u32 d = threadIdx.x; d < W; d += T) {
+    if (rc[d]) atomicAdd(&cnt[d], (unsigned long long)rc[d]);
+    if (bc[d]) atomicAdd(&cnt[W + d], bc[d]);
+  }
+}
+
+// cnt [2W] -> start [2W] (exclusive scans), cursors zeroed, and the exchange
+// row per destination: xchg[3d] = records, xchg[3d+1] = bytes, xchg[3d+2] = extra.
+__global__ void pk_scan_kernel(const unsigned long long* __restrict__ cnt, u32 W, unsigned long long* __restrict__ start,
+                               unsigned long long* __restrict__ cursor, long long* __restrict__ xchg, long long extra) {
+  if (threadIdx.x != 0) return;
+  unsigned long long r = 0, b = 0;
+  for (u32 d = 0; d < W; ++d) {
+    start[d] = r;
+    start[W + d] = b;
+    cursor[d] = 0;
+    cursor[W + d] = 0;
+    xchg[3 * d] = (long long)cnt[d];
+    xchg[3 * d + 1] = (long long)cnt[W + d];
+    xchg[3 * d + 2] = extra;
+    r += cnt[d];
+    b += cnt[W + d];
+  }
+}
+
+__global__ void __launch_bounds__(T) pk_scatter_kernel(const u64* __restrict__ hi, const u64* __restrict__ lo,
+                                                       const long long* __restrict__ val, const u64* __restrict__ rep,
+                                                       const u32* __restrict__ part, u64 n, u32 W,
+                                                       const u8* __restrict__ src,
+                                                       const unsigned long long* __restrict__ start,
+                                                       unsigned long long* __restrict__ cursor,
+                                                       u64* __restrict__ rec /*[n][4]*/, u8* __restrict__ blob) {
+  __shared__ u32 rc[MAXW];
+  __shared__ u32 bc[MAXW];
+  __shared__ unsigned long long rbase[MAXW];
+  __shared__ unsigned long long bbase[MAXW];
+  const u64 i = (u64)blockIdx.x * T + threadIdx.x;
+  for (u32 d = threadIdx.x; d < W; d += T) {
+    rc[d] = 0;
+    bc[d] = 0;
+  }
+  __syncthreads();
+  u32 d = 0, len = 0, rpos = 0, bpos = 0;
+  const bool live = i < n;
+  if (live) {
+    d = part[i] % W;
+    len = key_len(lo[i], rep[i]);
+    rpos = atomicAdd(&rc[d], 1u);
+    bpos = atomicAdd(&bc[d], len);
+  }
+  __syncthreads();
+  for (u32 k = threadIdx.x; k < W; k += T) {
+    rbase[k] = rc[k] ? atomicAdd(&cursor[k], (unsigned long long)rc[k]) : 0;
+    bbase[k] = bc[k] ? atomicAdd(&cursor[W + k], (unsigned long long)bc[k]) : 0;
+  }
+  __syncthreads();
+  if (!live) return;
+  const u64 r = start[d] + rbase[d] + rpos;
+  const u64 boff = bbase[d] + bpos;  // offset inside destination d's byte segment
+  const u64 h = hi[i], l = lo[i];
+  rec[4 * r + 0] = h;
+  rec[4 * r + 1] = l;
+  rec[4 * r + 2] = (u64)val[i];
+  rec[4 * r + 3] = make_rep(boff, len);
+  u8* out = blob + start[W + d] + boff;
+  if (!key_is_long(l)) {
+    for (u32 k = 0; k < len; ++k) out[k] = (u8)packed_byte(h, l, k);
+  } else {
+    const u8* p = src + rep_off(rep[i]);
+    for (u32 k = 0; k < len; ++k) out[k] = p[k];
+  }
+}
+
+// Received records from source s carry offsets relative to s's byte segment;
+// make them absolute: loc += byte_start(s) << 24, s found from the record
+// prefix counts (rstart[W+1] / bstart[W] on the device).
+__global__ void pk_fix_loc_kernel(u64* __restrict__ rec, u64 n, const long long* __restrict__ rstart,
+                                  const long long* __restrict__ bstart, u32 W, u64* __restrict__ rep_out) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u32 a = 0, b = W;  // source s: rstart[s] <= i < rstart[s+1]
+    while (b - a > 1) {
+      const u32 m = (a + b) >> 1;
+      if ((long long)i >= rstart[m]) a = m;
+      else b = m;
+    }
+    const u64 loc = rec[4 * i + 3];
+    rep_out[i] = make_rep(rep_off(loc) + (u64)bstart[a], rep_len(loc));
+  }
+}
+
+}  // namespace pk
+}  // namespace mr
+
+using namespace mr;
+
+static inline unsigned pk_grid(u64 n, unsigned cap = 4096) {
+  u64 g = (n + pk::T - 1) / pk::T;
+  return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+extern "C" {
+
+// ws: 6*W u64 (cnt[2W], start[2W], cursor[2W]); xchg: 3*W int64 (device)
+int mr_pack_by_dest(const void* hi, const void* lo, const void* val, const void* rep, const void* part, u64 n, u32 W,
+                    const void* src, void* ws, void* xchg, long long extra, void* rec, void* blob, hipStream_t s) {
+  if (W == 0 || W > (u32)pk::MAXW) return -1;
+  unsigned long long* cnt = (unsigned long long*)ws;
+  unsigned long long* start = cnt + 2 * W;
+  unsigned long long* cursor = start + 2 * W;
+  hipMemsetAsync(cnt, 0, 2 * W * sizeof(unsigned long long), s);
+  if (n) {
+    hipLaunchKernelGGL(pk::pk_count_kernel, dim3(pk_grid(n, 1024)), dim3(pk::T), 0, s, (const u64*)lo,
+                       (const u64*)rep, (const u32*)part, n, W, cnt);
+  }
+  hipLaunchKernelGGL(pk::pk_scan_kernel, dim3(1), dim3(64), 0, s, (const unsigned long long*)cnt, W, start, cursor,
+                     (long long*)xchg, extra);
+  if (n) {
+    // one record per thread (the per-block reservation needs every key of the
+    // block in flight at once): grid = ceil(n / 256), not capped
+    const u64 g = (n + pk::T - 1) / pk::T;
+    hipLaunchKernelGGL(pk::pk_scatter_kernel, dim3((unsigned)g), dim3(pk::T), 0, s, (const u64*)hi, (const u64*)lo,
+                       (const long long*)val, (const u64*)rep, (const u32*)part, n, W, (const u8*)src,
+                       (const unsigned long long*)start, cursor, (u64*)rec, (u8*)blob);
+  }
+  return (int)hipGetLastError();
+}
+
+int mr_fix_loc(void* rec, u64 n, const void* rstart, const void* bstart, u32 W, void* rep_out, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(pk::pk_fix_loc_kernel, dim3(pk_grid(n)), dim3(256), 0, s, (u64*)rec, n, (const long long*)rstart,
+                     (const long long*)bstart, W, (u64*)rep_out);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -391,29 +391,24 @@ class SPMDEngine:
 
     def _shuffle(self, hi, lo, val, rep, src, part, failed: int = 0):
         """Send each key to rank part % W; returns received (hi, lo, val, rep,
-        src) and the job-wide number of failed map jobs (this rank's count rides
-        along with the count exchange instead of a separate all-reduce)."""
+        src) and sets the job-wide number of failed map jobs (this rank's count
+        rides along with the count exchange instead of a separate all-reduce).
+
+        Pack (3 launches, no sort: ops/shuffle.py) -> one count exchange (the
+        only host synchronisation) -> two all_to_all_single (records, key
+        bytes) -> received locations made absolute in the received blob."""
+        from ..ops import shuffle as SH
         W = self.world
-        dest = torch.remainder(part, W).to(torch.int64)
-        perm = ops.sort_keys([dest], bits=[max(1, (W - 1).bit_length())]).long()
-        hi, lo, val, rep = hi[perm], lo[perm], val[perm], rep[perm]
-        off, blob = ops.gather_key_bytes(hi, lo, rep, src)
-        lens = off[1:] - off[:-1]
-        counts = ops.bincount(dest.to(torch.int32), W)
-        bcounts = torch.zeros(W, dtype=torch.int64, device=hi.device)
-        bcounts.index_add_(0, dest[perm], lens)
-        send = torch.stack([counts, bcounts, torch.full_like(counts, int(failed))])
-        recv = D.exchange_counts(send.t().contiguous().view(-1), self.group).view(W, 3)
-        both = torch.cat([send, recv.t()], 1).cpu().tolist()  # one host sync
-        send_h = [row[:W] for row in both]
-        recv_h = [[both[0][W + r], both[1][W + r], both[2][W + r]] for r in range(W)]
+        rec, blob, xchg = SH.pack_by_dest(hi, lo, val, rep, part, W, src, extra=failed)
+        recv = D.exchange_counts(xchg, self.group)
+        both = torch.cat([xchg, recv]).view(2, W, 3).cpu().tolist()  # one host sync
+        send_h, recv_h = both
         self._failed_total = sum(r[2] for r in recv_h)
-        rec = torch.stack([hi, lo, val, lens], dim=1)
-        rrec = D.all_to_all_v(rec, send_h[0], [r[0] for r in recv_h], self.group)
-        rblob = D.all_to_all_v(blob, send_h[1], [r[1] for r in recv_h], self.group)
-        rl = rrec[:, 3].contiguous()
-        roff, _ = ops.exclusive_scan(rl)
-        rrep = (roff << 24) | rl
+        send_rows, send_bytes = [r[0] for r in send_h], [r[1] for r in send_h]
+        recv_rows, recv_bytes = [r[0] for r in recv_h], [r[1] for r in recv_h]
+        rrec = D.all_to_all_v(rec, send_rows, recv_rows, self.group)
+        rblob = D.all_to_all_v(blob[:sum(send_bytes)], send_bytes, recv_bytes, self.group)
+        rrep = SH.absolute_reps(rrec, recv_rows, recv_bytes)
         return rrec[:, 0].contiguous(), rrec[:, 1].contiguous(), rrec[:, 2].contiguous(), rrep, rblob
 
     def _reduce(self, hi, lo, val, rep, src):

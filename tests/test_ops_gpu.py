@@ -241,3 +241,39 @@ def test_spmd_prefetch_pipelined_iterations_match(gpu):
         r = eng.run_iteration(prefetch_next=i < 4)
         assert r.total_value == ref_total == 400_000 and r.distinct_keys == ref_keys
     assert eng._prefetched is None
+
+
+@pytest.mark.parametrize("W", [1, 3, 8])
+def test_pack_by_dest_matches_cpu(gpu, W):
+    """Per destination, the GPU pack holds the same (key bytes, value) set as
+    the CPU specification, and absolute reps index the right bytes."""
+    from lua_mapreduce_1_amd.ops import shuffle as SH
+    rng = np.random.default_rng(W)
+    words = [bytes(rng.integers(97, 123, int(rng.integers(1, 30))).astype(np.uint8)) for _ in range(3000)]
+    text = b" ".join(words) + b"\n"
+    t = torch.frombuffer(bytearray(text), dtype=torch.uint8)
+    tab = ops.HashTable(1 << 13, device=gpu)
+    tab.wordcount_map(t.to(gpu))
+    hi, lo, val, rep = tab.compact()
+    part, _ = ops.key_meta(hi, lo, rep, t.to(gpu), nparts=10)
+    rg, bg, xg = SH.pack_by_dest(hi, lo, val, rep, part, W, t.to(gpu), extra=7)
+    rc, bc, xc = SH.pack_by_dest(hi.cpu(), lo.cpu(), val.cpu(), rep.cpu(), part.cpu(), W, t, extra=7)
+    assert torch.equal(xg.cpu(), xc)
+    x = xc.view(W, 3).numpy()
+    rows = x[:, 0].tolist()
+    nb = x[:, 1].tolist()
+
+    def per_dest(rec, blob):
+        # rebuild (bytes, val) per destination as a receiver would (one source)
+        reps = SH.absolute_reps(rec, rows, nb).cpu().numpy()
+        b = blob.cpu().numpy().tobytes()
+        out, r0 = [], 0
+        for d in range(W):
+            s = set()
+            for i in range(r0, r0 + rows[d]):
+                off, ln = int(reps[i]) >> 24, int(reps[i]) & 0xFFFFFF
+                s.add((b[off:off + ln], int(rec[i, 2])))
+            out.append(s)
+            r0 += rows[d]
+        return out
+    assert per_dest(rg.cpu(), bg[:sum(nb)]) == per_dest(rc, bc)
