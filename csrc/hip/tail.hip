@@ -1,0 +1,192 @@
+// tail.hip — fused kernels of the reduce-side tail (compact -> partition ->
+// (partition, key) sort -> key bytes -> download), the work that turns the
+// HBM hash table into the sorted ``result.P<NN>`` columns (reference:
+// job.lua:264-294 reduce + write, server.lua:346-411 result listing, SURVEY.md
+// §2.2 K6/K8/K10/K11).
+//
+// The unfused tail was ~28 short launches; at small per-rank inputs (8-GPU
+// strong scaling) the drain/fill between dependent kernels dominated.  Here:
+//   tail_compact : table -> dense rows + FNV-1 partition + composite sort key
+//                  (part << 56 | hi >> 8) + the 8 digit histograms of that key
+//                  (so the sort skips its histogram pass) + partition counts;
+//   [onesweep passes, sort.hip]
+//   tail_gather  : rows reordered by the sort permutation + key lengths;
+//   [tie fix-up, scan, key-byte gather: existing kernels]
+//   tail_pack    : values, 32-bit offsets, partition counts and the fix-up
+//                  flag packed into one buffer -> ONE device->host DMA.
+#include <hip/hip_runtime.h>
+#include "mr_common.h"
+#include "hashtab.h"
+
+namespace mr {
+namespace tl {
+
+constexpr int T = 256;
+constexpr int ITEMS = 16;
+
+__device__ __forceinline__ u32 key_fnv(u64 h, u64 l, u64 r, const u8* src, u32* len_out) {
+  u32 f = FNV_OFFSET;
+  u32 len;
+  if (!key_is_long(l)) {
+    len = packed_len(l);
+    for (u32 k = 0; k < len; ++k) f = fnv1_step(f, packed_byte(h, l, k));
+  } else {
+    len = (u32)rep_len(r);
+    const u8* p = src + rep_off(r);
+    for (u32 k = 0; k < len; ++k) f = fnv1_step(f, p[k]);
+  }
+  *len_out = len;
+  return f;
+}
+
+__global__ void __launch_bounds__(T) tail_compact_kernel(GTab g, u64 cap, u32 nparts, const u8* __restrict__ src,
+                                                         u64* __restrict__ out_hi, u64* __restrict__ out_lo,
+                                                         long long* __restrict__ out_val, u64* __restrict__ out_rep,
+                                                         u32* __restrict__ out_part, u64* __restrict__ out_c,
+                                                         unsigned long long* __restrict__ counter,
+                                                         u32* __restrict__ ghist /*[8][256]*/,
+                                                         long long* __restrict__ pcount /*[nparts]*/) {
+  __shared__ u32 sh[T];
+  __shared__ u32 hist[8][256];
+  __shared__ u32 pc[256];
+  __shared__ unsigned long long base;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) hist[b][t] = 0;
+  pc[t] = 0;
+  const u64 b0 = (u64)blockIdx.x * T * ITEMS;
+  u32 occ = 0, n = 0;
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const u64 i = b0 + (u64)k * T + t;
+    const bool o = i < cap && g.tag[i] != 0;
+    occ |= (o ? 1u : 0u) << k;
+    n += o ? 1u : 0u;
+  }
+  sh[t] = n;
+  __syncthreads();
+  for (int o = 1; o < T; o <<= 1) {
+    const u32 y = t >= o ? sh[t - o] : 0u;
+    __syncthreads();
+    sh[t] += y;
+    __syncthreads();
+  }
+  if (t == T - 1) base = sh[T - 1] ? atomicAdd(counter, (unsigned long long)sh[T - 1]) : 0ull;
+  __syncthreads();
+  u64 o = base + sh[t] - n;
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    if (occ & (1u << k)) {
+      const u64 i = b0 + (u64)k * T + t;
+      const u64 h = g.hi[i], l = g.lo[i], r = g.rep[i];
+      u32 len;
+      const u32 f = key_fnv(h, l, r, src, &len);
+      const u32 p = nparts ? f % nparts : f;
+      const u64 c = ((u64)p << 56) | (h >> 8);
+      out_hi[o] = h;
+      out_lo[o] = l;
+      out_val[o] = g.val[i];
+      out_rep[o] = r;
+      out_part[o] = p;
+      out_c[o] = c;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) atomicAdd(&hist[b][(c >> (8 * b)) & 0xFF], 1u);
+      if (p < 256) atomicAdd(&pc[p], 1u);
+      ++o;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+    if (hist[b][t]) atomicAdd(&ghist[b * 256 + t], hist[b][t]);
+  if ((u32)t < nparts && pc[t]) atomicAdd((unsigned long long*)&pcount[t], (unsigned long long)pc[t]);
+}
+
+__global__ void tail_gather_kernel(const u32* __restrict__ perm, u64 n, const u64* __restrict__ hi,
+                                   const u64* __restrict__ lo, const long long* __restrict__ val,
+                                   const u64* __restrict__ rep, const u32* __restrict__ part, u64* __restrict__ o_hi,
+                                   u64* __restrict__ o_lo, long long* __restrict__ o_val, u64* __restrict__ o_rep,
+                                   u32* __restrict__ o_part, long long* __restrict__ o_len) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 j = perm[i];
+    const u64 l = lo[j], r = rep[j];
+    o_hi[i] = hi[j];
+    o_lo[i] = l;
+    o_val[i] = val[j];
+    o_rep[i] = r;
+    o_part[i] = part[j];
+    o_len[i] = key_is_long(l) ? (long long)rep_len(r) : (long long)packed_len(l);
+  }
+}
+
+// [val: n x i64][off: (n+1) x i32][counts: nparts x i64][bad: u32] (8-byte aligned sections)
+__global__ void tail_pack_kernel(const long long* __restrict__ val, const long long* __restrict__ off, u64 n,
+                                 const long long* __restrict__ counts, u32 nparts, const u32* __restrict__ bad,
+                                 u8* __restrict__ out) {
+  long long* ov = (long long*)out;
+  int* oo = (int*)(out + 8 * n);
+  const u64 off_bytes = ((4 * (n + 1)) + 7) & ~7ull;
+  long long* oc = (long long*)(out + 8 * n + off_bytes);
+  u32* ob = (u32*)(out + 8 * n + off_bytes + 8 * (u64)nparts);
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += stride) {
+    if (i < n) ov[i] = val[i];
+    oo[i] = (int)off[i];
+    if (i < nparts) oc[i] = counts[i];
+    if (i == 0) ob[0] = bad[0];
+  }
+  if (blockIdx.x == 0 && threadIdx.x < nparts && n + 1 <= threadIdx.x) oc[threadIdx.x] = counts[threadIdx.x];
+}
+
+}  // namespace tl
+}  // namespace mr
+
+using namespace mr;
+
+extern "C" {
+
+u64 mr_tail_pack_bytes(u64 n, u32 nparts) { return 8 * n + (((4 * (n + 1)) + 7) & ~7ull) + 8 * (u64)nparts + 8; }
+
+int mr_tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, u32 nparts,
+                    const void* src, void* out_hi, void* out_lo, void* out_val, void* out_rep, void* out_part,
+                    void* out_c, void* counter, void* ghist, void* pcount, hipStream_t s) {
+  if (nparts > 256) return -1;
+  GTab g;
+  g.tag = (u64*)tag;
+  g.hi = (u64*)hi;
+  g.lo = (u64*)lo;
+  g.val = (long long*)val;
+  g.rep = (u64*)rep;
+  g.ctrl = (u32*)ctrl;
+  g.mask = cap - 1;
+  const u64 nb = (cap + tl::T * tl::ITEMS - 1) / (tl::T * tl::ITEMS);
+  hipLaunchKernelGGL(tl::tail_compact_kernel, dim3((unsigned)nb), dim3(tl::T), 0, s, g, cap, nparts, (const u8*)src,
+                     (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
+                     (unsigned long long*)counter, (u32*)ghist, (long long*)pcount);
+  return (int)hipGetLastError();
+}
+
+int mr_tail_gather(const void* perm, u64 n, const void* hi, const void* lo, const void* val, const void* rep,
+                   const void* part, void* o_hi, void* o_lo, void* o_val, void* o_rep, void* o_part, void* o_len,
+                   hipStream_t s) {
+  if (n == 0) return 0;
+  u64 g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(tl::tail_gather_kernel, dim3((unsigned)g), dim3(256), 0, s, (const u32*)perm, n, (const u64*)hi,
+                     (const u64*)lo, (const long long*)val, (const u64*)rep, (const u32*)part, (u64*)o_hi,
+                     (u64*)o_lo, (long long*)o_val, (u64*)o_rep, (u32*)o_part, (long long*)o_len);
+  return (int)hipGetLastError();
+}
+
+int mr_tail_pack(const void* val, const void* off, u64 n, const void* counts, u32 nparts, const void* bad, void* out,
+                 hipStream_t s) {
+  if (nparts > 256) return -1;
+  u64 g = (n + 1 + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(tl::tail_pack_kernel, dim3((unsigned)g), dim3(256), 0, s, (const long long*)val,
+                     (const long long*)off, n, (const long long*)counts, nparts, (const u32*)bad, (u8*)out);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -68,10 +68,14 @@ _SIGS = {
     "mr_ts_unsorted": [_p, _p, _u64, _p, _p],
     "mr_pack_by_dest": [_p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, ctypes.c_longlong, _p, _p, _p],
     "mr_fix_loc": [_p, _u64, _p, _p, _u32, _p, _p],
+    "mr_tail_compact": [_p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
+    "mr_tail_gather": [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
+    "mr_tail_pack": [_p, _p, _u64, _p, _u32, _p, _p, _p],
+    "mr_tail_pack_bytes": [_u64, _u32],
     "mr_scan_partials_len": [_u64],
     "mr_rs_tiles": [_u64],
 }
-_RESTYPE_U64 = {"mr_scan_partials_len", "mr_rs_tiles"}
+_RESTYPE_U64 = {"mr_scan_partials_len", "mr_rs_tiles", "mr_tail_pack_bytes"}
 
 
 def lib():

@@ -356,13 +356,14 @@ def _sort_ws(d, n: int):
 
 
 def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: str = "onesweep",
-              return_keys: bool = False):
+              return_keys: bool = False, ghist: torch.Tensor | None = None):
     """Stable permutation sorting rows by unsigned multi-word keys.
 
     ``words[0]`` is the most significant u64 word.  ``bits[j]`` limits the
     number of low bits of word j that participate (e.g. partition ids).
     Returns int32 (GPU) / int64 (CPU) permutation (and, with ``return_keys``,
-    ``words[0]`` in sorted order as a second value).  GPU: LSD radix sort, one
+    ``words[0]`` in sorted order as a second value).  ``ghist``: precomputed
+    [8][256] digit histograms of a single-word key (skips that pass).  GPU: LSD radix sort, one
     onesweep launch per 8-bit digit (``method="onesweep"``) or the 3-phase
     histogram/scan/scatter passes (``method="3phase"``).
     """
@@ -385,7 +386,8 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
                 # a replayed graph reuses its pass epochs: clear the look-back
                 # granules so a replay never sees the previous replay's tags
                 ws["granules"][: ((n + 4095) // 4096) * 256].zero_()
-            ghist = small[:2048]
+            ghist_ws = small[:2048]
+            pre_hist = ghist
             kbuf = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(2)]
             pbuf = [torch.empty(n, dtype=torch.int32, device=d) for _ in range(2)]
             kin, pin = None, None
@@ -399,15 +401,19 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
                     kin = dst
                 if nb <= 0:
                     continue
-                if pass_id:
-                    ghist.zero_()
-                _hip.call("mr_radix_ghist8", _hip.ptr(kin), n, _hip.ptr(ghist), (nb + 7) // 8, s)
+                gh = ghist_ws
+                if pre_hist is not None and len(words) == 1:
+                    gh = pre_hist
+                else:
+                    if pass_id:
+                        ghist_ws.zero_()
+                    _hip.call("mr_radix_ghist8", _hip.ptr(kin), n, _hip.ptr(ghist_ws), (nb + 7) // 8, s)
                 for shift in range(0, nb, 8):
                     _EPOCH[0] = (_EPOCH[0] + 1) & 0xFFFFFF or 1
                     kout = kbuf[0] if kin is not kbuf[0] else kbuf[1]
                     pout = pbuf[0] if pin is not pbuf[0] else pbuf[1]
                     _hip.call("mr_radix_onesweep_u32v", _hip.ptr(kin), _hip.ptr(pin), _hip.ptr(kout), _hip.ptr(pout),
-                              n, shift, _hip.ptr(ghist[shift // 8 * 256:]), _hip.ptr(ws["granules"]),
+                              n, shift, _hip.ptr(gh[shift // 8 * 256:]), _hip.ptr(ws["granules"]),
                               _hip.ptr(small[2048 + pass_id:]), _EPOCH[0], _hip.ptr(small[2112:]),
                               1 if pin is None else 0, s)
                     pass_id += 1

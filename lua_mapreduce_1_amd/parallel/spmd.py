@@ -27,6 +27,7 @@ semantics), with the failure flag agreed across ranks before the shuffle.
 """
 from __future__ import annotations
 
+import os
 import sys
 import time
 import traceback
@@ -411,6 +412,27 @@ class SPMDEngine:
         rrep = SH.absolute_reps(rrec, recv_rows, recv_bytes)
         return rrec[:, 0].contiguous(), rrec[:, 1].contiguous(), rrec[:, 2].contiguous(), rrep, rblob
 
+    def _fused_tail_ok(self) -> bool:
+        """The fused tail kernels need a GPU, the built-in FNV-1 partitioner
+        and at most 256 partitions."""
+        spec = getattr(self.partmod, "device_partition", None) if self.partmod is not None else None
+        return (self.device.type == "cuda" and spec is not None and spec[0] == "fnv1"
+                and self.nparts <= 256 and os.environ.get("MR_FUSED_TAIL", "1") != "0")
+
+    def _reduce_insert(self, hi, lo, val, rep) -> int:
+        """Received rows -> this rank's reduce table; returns its key count."""
+        n = hi.numel()
+        cap = ops.next_pow2(max(1 << 16, 2 * n))
+        if self.red_table is None or self.red_table.cap < cap:
+            self.red_table = ops.HashTable(cap, device=self.device, op=self.op)
+        else:
+            self.red_table.reset()
+        self.red_table.insert(hi, lo, val, rep)
+        m, ovf = self.red_table.stats()
+        if ovf:
+            raise OverflowError("reduce table overflow")
+        return m
+
     def _reduce(self, hi, lo, val, rep, src):
         n = hi.numel()
         cap = ops.next_pow2(max(1 << 16, 2 * n))
@@ -485,17 +507,24 @@ class SPMDEngine:
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
         self._failed_total = failed
         pend = None
+        fused = self._fused_tail_ok()
         if self.world == 1 and self._graph_tail_ok():
             # the whole device tail (compact -> partition -> sort -> key bytes
             # -> downloads) is one replayed hipGraph once a table size repeats
             pend = self._graphed_tail(n_claimed, overflow, src)
+        elif self.world == 1 and fused:
+            pend = devmod.finalize_table_device(self.table, n_claimed, src, self.nparts)
         else:
             hi, lo, val, rep = self.table.compact((n_claimed, overflow))
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         if self.world > 1:
             hi, lo, val, rep, src = self._shuffle(hi, lo, val, rep, src, part, failed)
-            hi, lo, val, rep = self._reduce(hi, lo, val, rep, src)
-            part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
+            if fused:
+                n_red = self._reduce_insert(hi, lo, val, rep)
+                pend = devmod.finalize_table_device(self.red_table, n_red, src, self.nparts)
+            else:
+                hi, lo, val, rep = self._reduce(hi, lo, val, rep, src)
+                part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         T["shuffle"] = time.time() - t1
         t2 = time.time()
         if pend is None:

@@ -238,14 +238,77 @@ def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, p
     return pend
 
 
+def finalize_table_device(table, n: int, src, nparts: int) -> dict:
+    """Fused device tail straight from an HBM hash table (csrc/hip/tail.hip):
+    compact + FNV partition + composite key + digit histograms in one kernel,
+    the composite onesweep sort (no histogram pass), one gather that also
+    yields key lengths, the exact-order tie fix-up, key bytes, and ONE packed
+    download of values/offsets/partition counts (+ the key-byte DMA).
+    ``n`` = occupied slots (table.stats()).  Requires nparts <= 256."""
+    from ..ops import _hip
+    d = table.device
+    s = _hip.stream(d)
+    z = lambda dt: torch.empty(n, dtype=dt, device=d)  # noqa: E731
+    hi0, lo0, val0, rep0, c = z(torch.int64), z(torch.int64), z(torch.int64), z(torch.int64), z(torch.int64)
+    part0 = z(torch.int32)
+    small = torch.zeros(1 + 2048 // 2 + nparts, dtype=torch.int64, device=d)  # counter | ghist (u32) | pcount
+    counter, ghist, pcount = small[:1], small[1:1 + 1024].view(torch.int32), small[1 + 1024:]
+    _hip.call("mr_tail_compact", *table._gtab(), table.cap, nparts, _hip.ptr(src), _hip.ptr(hi0), _hip.ptr(lo0),
+              _hip.ptr(val0), _hip.ptr(rep0), _hip.ptr(part0), _hip.ptr(c), _hip.ptr(counter), _hip.ptr(ghist),
+              _hip.ptr(pcount), s)
+    perm, cs = ops.sort_keys([c], return_keys=True, ghist=ghist)
+    hi, lo, val, rep, ln = z(torch.int64), z(torch.int64), z(torch.int64), z(torch.int64), z(torch.int64)
+    part = z(torch.int32)
+    _hip.call("mr_tail_gather", _hip.ptr(perm), n, _hip.ptr(hi0), _hip.ptr(lo0), _hip.ptr(val0), _hip.ptr(rep0),
+              _hip.ptr(part0), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), _hip.ptr(ln), s)
+    bad = torch.zeros(1, dtype=torch.int32, device=d)
+    _hip.call("mr_tie_fixup", _hip.ptr(cs), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part),
+              n, _hip.ptr(bad), _hip.ptr(src), s)
+    cap = src.numel()
+    off, blob = ops.gather_key_bytes(hi, lo, rep, src, lengths=ln, capacity=cap)
+    nb = int(_hip.lib().mr_tail_pack_bytes(n, nparts))
+    packed = torch.empty(nb, dtype=torch.uint8, device=d)
+    _hip.call("mr_tail_pack", _hip.ptr(val), _hip.ptr(off), n, _hip.ptr(pcount), nparts, _hip.ptr(bad),
+              _hip.ptr(packed), s)
+    hp = _POOL.get("pack", nb, torch.uint8)
+    hp.copy_(packed, non_blocking=True)
+    est = _BLOB_EST.get(d)
+    if est is not None:
+        est = min(est, blob.numel())
+        hb = _POOL.get("blob", max(est, 1 << 16), torch.uint8)
+        hb[:est].copy_(blob[:est], non_blocking=True)
+    else:
+        hb = _POOL.get("blob", max(1 << 20, 16 * n), torch.uint8)
+        ops.copy_to_host(blob, hb, off[n:])
+    return {"n": n, "nparts": nparts, "args": (hi0, lo0, val0, rep0), "src": src, "presorted": False, "hi": hi,
+            "lo": lo, "fused": True, "hp": hp, "off": off, "blob": blob, "est": est, "hb": hb}
+
+
+def _unpack_fused(pend: dict):
+    """(val int64[n], off int32[n+1], counts int64[nparts], bad) views of the packed download."""
+    n, nparts = pend["n"], pend["nparts"]
+    raw = pend["hp"].numpy()
+    offb = ((4 * (n + 1)) + 7) & ~7
+    val = raw[:8 * n].view(np.int64)
+    off = raw[8 * n:8 * n + 4 * (n + 1)].view(np.int32)
+    counts = raw[8 * n + offb:8 * n + offb + 8 * nparts].view(np.int64)
+    bad = int(raw[8 * n + offb + 8 * nparts:8 * n + offb + 8 * nparts + 4].view(np.uint32)[0])
+    return val, off, counts, bad
+
+
 def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) -> dict:
     """The host half of :func:`finalize`: one synchronisation, then numpy."""
     n, nparts = pend["n"], pend["nparts"]
     hi, lo = pend["hi"], pend["lo"]
     if hi.is_cuda:
         torch.cuda.current_stream(hi.device).synchronize()
-        ho, hb, est, blob = pend["ho"], pend["hb"], pend["est"], pend["blob"]
-        nbytes = int(ho[n]) if n else 0
+        hb, est, blob = pend["hb"], pend["est"], pend["blob"]
+        if pend.get("fused"):
+            f_val, f_off, f_counts, f_bad = _unpack_fused(pend)
+            nbytes = int(f_off[n]) if n else 0
+        else:
+            ho = pend["ho"]
+            nbytes = int(ho[n]) if n else 0
         if est is not None and nbytes > est:  # grew past the estimate: copy the rest
             hb = _POOL.get("blob", nbytes, torch.uint8)
             hb.copy_(blob[:nbytes])
@@ -254,7 +317,7 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
             hb.copy_(blob[:nbytes])
         _BLOB_EST[hi.device] = nbytes + nbytes // 16 + 4096
         hb = hb[:nbytes]
-        flag = int(pend["hbad"][0])
+        flag = f_bad if pend.get("fused") else int(pend["hbad"][0])
         if flag & 1:
             # a tie run was too long for the fixup kernel: redo with the full sort
             ahi, alo, aval, arep = pend["args"]
@@ -265,7 +328,10 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
             return finalize(ahi[perm], alo[perm], aval[perm], arep[perm], src, nparts, partition_module,
                             part=p2[perm], _presorted=True, need_keys=need_keys)
         # offsets stay int32 when the blob is < 2 GiB (no host-side widening pass)
-        h_val, h_off, h_blob, h_counts = pend["hv"].numpy(), ho.numpy(), hb.numpy(), pend["hc"].numpy()
+        if pend.get("fused"):
+            h_val, h_off, h_blob, h_counts = f_val, f_off, hb.numpy(), f_counts
+        else:
+            h_val, h_off, h_blob, h_counts = pend["hv"].numpy(), ho.numpy(), hb.numpy(), pend["hc"].numpy()
         need_fix = bool(flag & 2) or pend["presorted"]
         h_hi = hi.cpu().numpy().view(np.uint64) if (need_fix or need_keys) else None
         h_lo = lo.cpu().numpy().view(np.uint64) if (need_fix or need_keys) else None

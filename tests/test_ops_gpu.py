@@ -277,3 +277,24 @@ def test_pack_by_dest_matches_cpu(gpu, W):
             r0 += rows[d]
         return out
     assert per_dest(rg.cpu(), bg[:sum(nb)]) == per_dest(rc, bc)
+
+
+@pytest.mark.parametrize("nparts", [1, 10, 256])
+def test_fused_tail_matches_unfused(gpu, nparts):
+    from lua_mapreduce_1_amd.runtime import device as dv
+    from lua_mapreduce_1_amd.utils.corpus import tricky_text
+    rng = np.random.default_rng(nparts)
+    text = tricky_text(rng, 400_000) + b" " + b" ".join(
+        bytes(rng.integers(97, 123, int(rng.integers(1, 24))).astype(np.uint8)) for _ in range(20000)) + b"\n"
+    t = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(gpu)
+    tab = ops.HashTable(1 << 16, device=gpu)
+    tab.wordcount_map(t)
+    n, _ = tab.stats()
+    a = dv.finalize_host(dv.finalize_table_device(tab, n, t, nparts))
+    a = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in a.items()}
+    hi, lo, val, rep = tab.compact()
+    b = dv.finalize(hi, lo, val, rep, t, nparts)
+    assert np.array_equal(a["bounds"], b["bounds"])
+    assert np.array_equal(a["val"], b["val"])
+    assert np.array_equal(np.asarray(a["key_off"], np.int64), np.asarray(b["key_off"], np.int64))
+    assert a["key_blob"].tobytes() == b["key_blob"].tobytes()
