@@ -387,6 +387,17 @@ __global__ void gather_key_bytes_kernel(const u64* hi, const u64* lo, const u64*
   }
 }
 
+// Reset a table in one launch: tag = lo = 0, val = init, ctrl = 0.
+__global__ void table_reset_kernel(u64* tag, u64* lo, long long* val, u32* ctrl, u64 cap, long long init) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
+    tag[i] = 0;
+    lo[i] = 0;
+    val[i] = init;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 2) ctrl[threadIdx.x] = 0;
+}
+
 }  // namespace mr
 
 // ---------------------------------------------------------------------------
@@ -465,6 +476,12 @@ int mr_table_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* 
   hipLaunchKernelGGL(table_compact_kernel, dim3((unsigned)nb), dim3(256), 0, stream,
                      make_gtab(tag, hi, lo, val, rep, ctrl, cap), cap, (u64*)out_hi, (u64*)out_lo,
                      (long long*)out_val, (u64*)out_rep, (unsigned long long*)counter);
+  return (int)hipGetLastError();
+}
+
+int mr_table_reset(void* tag, void* lo, void* val, void* ctrl, u64 cap, long long init, hipStream_t stream) {
+  hipLaunchKernelGGL(table_reset_kernel, dim3(grid_for(cap, 256)), dim3(256), 0, stream, (u64*)tag, (u64*)lo,
+                     (long long*)val, (u32*)ctrl, cap, init);
   return (int)hipGetLastError();
 }
 

@@ -72,6 +72,7 @@ _SIGS = {
     "mr_tail_gather": [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "mr_tail_pack": [_p, _p, _u64, _p, _u32, _p, _p, _p],
     "mr_tail_pack_bytes": [_u64, _u32],
+    "mr_table_reset": [_p, _p, _p, _p, _u64, ctypes.c_longlong, _p],
     "mr_scan_partials_len": [_u64],
     "mr_rs_tiles": [_u64],
 }

@@ -102,10 +102,8 @@ class HashTable:
 
     def reset(self) -> None:
         if self.is_cuda:
-            self.tag.zero_()
-            self.lo.zero_()
-            self.val.fill_(_op_init(self.op))
-            self.ctrl.zero_()
+            _hip.call("mr_table_reset", _hip.ptr(self.tag), _hip.ptr(self.lo), _hip.ptr(self.val), _hip.ptr(self.ctrl),
+                      self.cap, _op_init(self.op), _hip.stream(self.device))
         else:
             self._pending = []
 

@@ -108,13 +108,20 @@ class JobRecord:
 
 class IterationResult:
     def __init__(self):
-        self.partitions: dict[int, dict] = {}   # partition -> columnar host arrays
+        self._parts: dict[int, dict] | None = {}  # partition -> columnar host arrays (built on first use)
+        self._cols = None
         self.result_names: dict[int, str] = {}
         self.map_jobs: list[JobRecord] = []
         self.red_jobs: list[JobRecord] = []
         self.timings: dict[str, float] = {}
         self.distinct_keys = 0
         self._vals = None
+
+    @property
+    def partitions(self) -> dict[int, dict]:
+        if self._parts is None:
+            self._parts = {p: devmod.partition_slice(self._cols, p) for p in self.result_names}
+        return self._parts
 
     @property
     def total_value(self) -> int:
@@ -500,8 +507,6 @@ class SPMDEngine:
             self._run_map(jobs, recs, j0, j1)
             n_claimed, overflow = self.table.stats()
         T["map"] = time.time() - t0
-        if prefetch_next:
-            self._prefetch(jobs, j0, j1)
         t1 = time.time()
         src = self._source()
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
@@ -529,11 +534,13 @@ class SPMDEngine:
         t2 = time.time()
         if pend is None:
             pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
+        if prefetch_next:
+            # the tail kernels are queued: start the next iteration's copies
+            self._prefetch(jobs, j0, j1)
         cols = devmod.finalize_host(pend, self.partmod)
         digits = len(str(max(self.nparts - 1, 0)))
         for p in range(self.nparts):
             if cols["bounds"][p + 1] > cols["bounds"][p]:
-                res.partitions[p] = devmod.partition_slice(cols, p)
                 res.result_names[p] = ("%s.P%0" + str(digits) + "d") % (self.result_ns, p)
                 r = JobRecord(p, {"result": res.result_names[p]})
                 r.status, r.started, r.written, r.worker = STATUS.WRITTEN, t1, time.time(), self.rank
@@ -541,6 +548,7 @@ class SPMDEngine:
                 res.red_jobs.append(r)
         res.distinct_keys = int(cols["val"].size)
         res._vals = cols["val"]
+        res._cols, res._parts = cols, None
         T["reduce"] = time.time() - t2
         T["iteration"] = time.time() - t_start
         res.failed_maps = self._failed_total
