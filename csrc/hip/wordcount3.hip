@@ -1,0 +1,402 @@
+// wordcount3.hip — third-generation fused word-count map kernel (gfx950).
+//
+// Same contract as wc_map2_kernel (wordcount2.hip; reference hot loops K1-K5:
+// examples/WordCount/mapfn.lua:4-7, job.lua:83-97, job.lua:92-96): tokenize a
+// byte stream on Lua-%s whitespace, build exact 128-bit keys, combine in an LDS
+// hash table, fold each workgroup's distinct words into the HBM table.
+//
+// What v2's ablation showed (tools/wc_ablate2.py, full corpus, 16 KiB chunks):
+// tokenize 0.90 ms + LDS combine 0.90 ms + flush to HBM 1.47 ms = 3.40 ms.  The
+// kernel ran ONE 512-thread workgroup per CU (112 KiB LDS table): every phase's
+// latency was exposed — the HBM load of each tile (no other workgroup to
+// overlap it) and the flush's chain of dependent global atomics (~1,600
+// distinct words per chunk; device atomics execute at the memory side at
+// ~24 G/s chip-wide, tools/probe/atomic_probe.hip).  v3 therefore:
+//   * sizes the LDS table so several workgroups share a CU (the flush of one
+//     overlaps the tokenizing of another): T threads, SLOTS slots, TPC tiles per
+//     chunk are template parameters (ablated in tools/wc_ablate2.py);
+//   * prefetches the next tile's bytes into registers before the token loop of
+//     the current tile (the HBM latency of a tile hides behind the LDS work);
+//   * reads the halo with the same 16-byte loads as the body (no byte loops).
+#include <hip/hip_runtime.h>
+#include "mr_common.h"
+#include "hashtab.h"
+
+namespace mr {
+namespace v3 {
+
+constexpr int SEG = 16;
+constexpr int PAD = 16;   // txt[PAD-1] = byte before the tile
+constexpr int HALO = 64;  // staged bytes of the next tile
+constexpr int PROBES = 32;
+
+template <int T, int SLOTS>
+struct Lds {
+  static constexpr int TILE = T * SEG;
+  static constexpr int STAGED = TILE + HALO;
+  static constexpr int TXT = PAD + STAGED + 32;
+  static constexpr int WSW = STAGED / 32 + 2;
+  u8 txt[TXT];
+  u32 ws[WSW];
+  u32 tag[SLOTS];
+  u32 cnt[SLOTS];
+  u32 rep[SLOTS];  // local offset (16 bits) | len (16 bits) << 16
+  u64 lo[SLOTS];
+  u64 hi[SLOTS];
+  u32 nclaimed;
+};
+
+struct Ovf {
+  u64* hi;
+  u64* lo;
+  u64* rep;
+  u64 cap;
+  unsigned long long* counter;
+  u64* stamps;  // optional per-workgroup phase timestamps (tools/wc_stamps.py), 4 per workgroup
+};
+
+__device__ __forceinline__ u32 ws_mask_word(u32 w) {
+  u32 m = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m |= (is_ws((w >> (8 * j)) & 0xFFu) ? 1u : 0u) << j;
+  return m;
+}
+
+__device__ __forceinline__ u32 ws_mask16(uint4 q) {
+  return ws_mask_word(q.x) | (ws_mask_word(q.y) << 4) | (ws_mask_word(q.z) << 8) | (ws_mask_word(q.w) << 12);
+}
+
+__device__ __forceinline__ u32 funnel(u32 a, u32 b, u32 r8) { return r8 ? ((a >> r8) | (b << (32 - r8))) : a; }
+
+__device__ u64 long_lo_global(const u8* text, u64 p0, u64 len) {
+  u64 h = long_hash_init(len);
+  for (u64 w = 0; w < len; w += 8) {
+    u64 word = 0;
+    const u64 n = (len - w) < 8 ? (len - w) : 8;
+    for (u64 j = 0; j < n; ++j) word |= (u64)text[p0 + w + j] << (8 * j);
+    h = long_hash_step(h, word);
+  }
+  return long_lo(h);
+}
+
+// 16 bytes at gpos (bytes past nbytes read as spaces)
+__device__ __forceinline__ uint4 load16(const u8* __restrict__ text, u64 gpos, u64 nbytes, int aligned) {
+  if (aligned && gpos + SEG <= nbytes) {
+    typedef u32 v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(text + gpos));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  u32 w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    w[k] = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u64 p = gpos + 4 * k + j;
+      w[k] |= (p < nbytes ? (u32)text[p] : 32u) << (8 * j);
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <int T, int SLOTS>
+__device__ __forceinline__ bool lds_insert(Lds<T, SLOTS>& L, u64 hi, u64 lo, u32 rep) {
+  u64 h = hi ^ (lo * 0x9E3779B97F4A7C15ull);
+  h ^= h >> 31;
+  h *= 0xC2B2AE3D27D4EB4Full;
+  h ^= h >> 29;
+  const u32 tag = (u32)(h >> 32) | 1u;
+  u32 slot = (u32)h & (SLOTS - 1);
+  constexpr u32 LIMIT = SLOTS * 3 / 4;
+  for (int probes = 0; probes < PROBES;) {
+    u32 cur = __hip_atomic_load(&L.tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == 0) {
+      if (__hip_atomic_load(&L.nclaimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= LIMIT) return false;
+      u32 expected = 0;
+      if (__hip_atomic_compare_exchange_strong(&L.tag[slot], &expected, tag, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        L.hi[slot] = hi;
+        L.rep[slot] = rep;
+        __hip_atomic_fetch_add(&L.cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&L.nclaimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&L.lo[slot], lo, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return true;
+      }
+      cur = expected;
+    }
+    if (cur == tag) {
+      const u64 l = __hip_atomic_load(&L.lo[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (l == 0) continue;  // claimer has not published yet: re-read this slot
+      if (l == lo && L.hi[slot] == hi) {
+        __hip_atomic_fetch_add(&L.cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return true;
+      }
+    }
+    slot = (slot + 1) & (SLOTS - 1);
+    ++probes;
+  }
+  return false;
+}
+
+// T threads, SLOTS LDS slots, TPC tiles of T*16 bytes per workgroup chunk.
+template <int T, int SLOTS, int TPC>
+__global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text, u64 nbytes, u64 rep_base, GTab g,
+                                                    Ovf ovf, int aligned) {
+  using L_t = Lds<T, SLOTS>;
+  constexpr int TILE = L_t::TILE;
+  constexpr int STAGED = L_t::STAGED;
+  constexpr int WSW = L_t::WSW;
+  constexpr u64 CHUNK = (u64)TILE * TPC;
+  __shared__ __attribute__((aligned(16))) L_t L;
+  const int t = threadIdx.x;
+  const u64 chunk_begin = (u64)blockIdx.x * CHUNK;
+  if (chunk_begin >= nbytes) return;
+  const u64 chunk_end = min(chunk_begin + CHUNK, nbytes);
+  u64* stamp = ovf.stamps ? ovf.stamps + 4 * (u64)blockIdx.x : nullptr;
+  if (stamp && t == 0) stamp[0] = wall_clock64();
+  for (int s = t; s < SLOTS; s += T) {
+    L.tag[s] = 0;
+    L.cnt[s] = 0;
+    L.lo[s] = 0;
+  }
+  if (t == 0) {
+    L.nclaimed = 0;
+    L.txt[PAD - 1] = chunk_begin > 0 ? text[chunk_begin - 1] : (u8)' ';
+    L.ws[WSW - 2] = 0xFFFFFFFFu;
+    L.ws[WSW - 1] = 0xFFFFFFFFu;
+  }
+  u32 claims = 0;
+  u16* ws16 = reinterpret_cast<u16*>(L.ws);
+  const u32* txt32 = reinterpret_cast<const u32*>(L.txt);
+  constexpr int NH = HALO / SEG;
+  // registers hold the NEXT tile's bytes while the current tile is processed
+  uint4 q = load16(text, chunk_begin + (u64)t * SEG, nbytes, aligned);
+  uint4 qh = make_uint4(0, 0, 0, 0);
+  if (t < NH) qh = load16(text, chunk_begin + TILE + (u64)t * SEG, nbytes, aligned);
+  for (u64 tile_base = chunk_begin; tile_base < chunk_end; tile_base += TILE) {
+    // the byte before this tile: the last byte of the previous tile, which
+    // thread T-1 held (nobody reads txt[PAD-1] between the previous tile's
+    // final barrier and this tile's staging barrier)
+    if (t == T - 1 && tile_base != chunk_begin) L.txt[PAD - 1] = L.txt[PAD + TILE - 1];
+    __syncthreads();
+    *reinterpret_cast<uint4*>(L.txt + PAD + t * SEG) = q;
+    ws16[t] = (u16)ws_mask16(q);
+    if (t < NH) {
+      *reinterpret_cast<uint4*>(L.txt + PAD + TILE + t * SEG) = qh;
+      ws16[T + t] = (u16)ws_mask16(qh);
+    }
+    __syncthreads();
+    const u64 next = tile_base + TILE;
+    if (next < chunk_end) {  // prefetch: consumed after this tile's token loop
+      q = load16(text, next + (u64)t * SEG, nbytes, aligned);
+      if (t < NH) qh = load16(text, next + TILE + (u64)t * SEG, nbytes, aligned);
+    }
+    const u64 seg_base = tile_base + (u64)t * SEG;
+    if (seg_base < chunk_end) {
+      const u32 m = ws16[t];
+      const u32 prev_ws = t ? ((ws16[t - 1] >> 15) & 1u) : (is_ws(L.txt[PAD - 1]) ? 1u : 0u);
+      u32 starts = (~m) & ((m << 1) | prev_ws) & 0xFFFFu;
+      const u64 lim_own = chunk_end - seg_base;
+      if (lim_own < 16) starts &= (1u << lim_own) - 1u;
+      while (starts) {
+        const int i = __builtin_ctz(starts);
+        starts &= starts - 1;
+        const u32 p = (u32)t * SEG + i;
+        u32 qq = p + 1;
+        u32 wd = L.ws[qq >> 5] >> (qq & 31);
+        u32 end;
+        if (wd) {
+          end = qq + __builtin_ctz(wd);
+        } else {
+          u32 k = (qq >> 5) + 1;
+          while (L.ws[k] == 0) ++k;
+          end = 32 * k + __builtin_ctz(L.ws[k]);
+        }
+        u64 len = end - p;
+        const u64 gpos = tile_base + p;
+        const u32 b = PAD + p;
+        const u32 a = b >> 2;
+        const u32 r8 = (b & 3u) * 8u;
+        const u32 x0 = txt32[a], x1 = txt32[a + 1], x2 = txt32[a + 2], x3 = txt32[a + 3], x4 = txt32[a + 4];
+        const u64 le_hi = (u64)funnel(x0, x1, r8) | ((u64)funnel(x1, x2, r8) << 32);
+        const u64 le_lo = (u64)funnel(x2, x3, r8) | ((u64)funnel(x3, x4, r8) << 32);
+        u64 hi = __builtin_bswap64(le_hi);
+        u64 lo;
+        if (end >= (u32)STAGED) {  // runs past the staged halo: measure from global memory
+          u64 pe = tile_base + STAGED;
+          while (pe < nbytes && !is_ws(text[pe])) ++pe;
+          len = pe - gpos;
+        }
+        if (len <= (u64)PACK_MAX) {
+          if (len < 8) hi &= ~0ull << (8 * (8 - len));
+          lo = len > 8 ? (__builtin_bswap64(le_lo) & (~0ull << (8 * (16 - len)))) : 0ull;
+          lo |= len;
+        } else {
+          lo = long_lo_global(text, gpos, len);
+        }
+        const bool ok = len < 65536 && lds_insert(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16));
+        if (!ok) {
+          const u64 grep = make_rep(rep_base + gpos, len);
+          const unsigned long long idx = atomicAdd(ovf.counter, 1ull);
+          if (idx < ovf.cap) {
+            ovf.hi[idx] = hi;
+            ovf.lo[idx] = lo;
+            ovf.rep[idx] = grep;
+          } else {
+            claims += gtab_insert(g, hi, lo, 1, grep, OP_SUM) == 2;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (stamp && t == 0) stamp[1] = wall_clock64();
+  // flush: each thread folds its PER slots.  The common case is a key already
+  // in the HBM table at its home slot, so tag/lo/hi of every home slot are
+  // loaded speculatively in ONE batch (one memory round trip instead of a
+  // dependent tag -> lo -> hi chain per key); a full match needs only the
+  // atomic add, anything else takes the general gtab_insert path.
+  constexpr int PER = SLOTS / T;
+  static_assert(SLOTS % T == 0, "slots must be a multiple of the block size");
+  u64 khi[PER], klo[PER], ktag[PER], kslot[PER], gt[PER], gl[PER], gh[PER];
+  u32 kcnt[PER], krep[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int s = t + k * T;
+    kcnt[k] = L.tag[s] != 0 ? L.cnt[s] : 0u;
+    khi[k] = L.hi[s];
+    klo[k] = L.lo[s];
+    krep[k] = L.rep[s];
+    ktag[k] = key_tag(khi[k], klo[k]);
+    kslot[k] = (ktag[k] >> 7) & g.mask;
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (kcnt[k]) {
+      gt[k] = ld_agent(&g.tag[kslot[k]]);
+      gl[k] = ld_agent(&g.lo[kslot[k]]);
+      gh[k] = ld_agent(&g.hi[kslot[k]]);
+    }
+  }
+  // new keys whose home slot is empty are claimed in a batch too: all CASes,
+  // one wait, all payload stores, ONE vmcnt drain, all publishing stores
+  // (hashtab.h protocol) — a per-key claim costs two serial memory round
+  // trips, and a cold table (first map of an iteration) is claim-heavy
+  u32 state = 0;  // bit k: entry k is done
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (!kcnt[k]) {
+      state |= 1u << k;
+    } else if (gt[k] == ktag[k] && gl[k] == klo[k] && gh[k] == khi[k]) {
+      fold_value(&g.val[kslot[k]], (long long)kcnt[k], OP_SUM);
+      state |= 1u << k;
+    }
+  }
+  u32 won = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (!(state & (1u << k)) && gt[k] == 0) {
+      u64 expected = 0;
+      if (__hip_atomic_compare_exchange_strong(&g.tag[kslot[k]], &expected, ktag[k], __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        won |= 1u << k;
+    }
+  }
+  if (won) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (won & (1u << k)) {
+        const u32 r = krep[k];
+        st_agent(&g.hi[kslot[k]], khi[k]);
+        st_agent(&g.rep[kslot[k]], make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16));
+        fold_value(&g.val[kslot[k]], (long long)kcnt[k], OP_SUM);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (won & (1u << k)) st_agent(&g.lo[kslot[k]], klo[k]);
+    claims += __builtin_popcount(won);
+    state |= won;
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (state & (1u << k)) continue;
+    const u32 r = krep[k];
+    claims += gtab_insert(g, khi[k], klo[k], (long long)kcnt[k],
+                          make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16), OP_SUM) == 2;
+  }
+  gtab_count_claims(g, claims);
+  if (stamp) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      stamp[2] = wall_clock64();
+      u32 xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      u32 cu;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(cu));
+      stamp[3] = ((u64)xcc << 32) | cu;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) ovf_agg3_kernel(Ovf o, GTab g) {
+  const unsigned long long n0 = *o.counter;
+  const u64 n = n0 < o.cap ? n0 : o.cap;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  u32 claims = 0;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    claims += gtab_insert(g, o.hi[i], o.lo[i], 1ll, o.rep[i], OP_SUM) == 2;
+  gtab_count_claims(g, claims);
+}
+
+template <int T, int SLOTS, int TPC>
+int launch(const u8* tx, u64 nbytes, u64 rep_base, const GTab& g, const Ovf& o, int aligned, hipStream_t stream) {
+  constexpr u64 CHUNK = (u64)T * SEG * TPC;
+  const u64 nblocks = (nbytes + CHUNK - 1) / CHUNK;
+  hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC>), dim3((unsigned)nblocks), dim3(T), 0, stream, tx, nbytes,
+                     rep_base, g, o, aligned);
+  return 0;
+}
+
+}  // namespace v3
+}  // namespace mr
+
+using namespace mr;
+
+extern "C" {
+
+// config: 0 = 512 threads / 2048 slots / 1 tile (8 KiB chunks, 2 workgroups per CU)
+//         1 = 512 / 2048 / 2 (16 KiB)      2 = 1024 / 4096 / 1 (16 KiB, 1 per CU)
+//         3 = 256 / 1024 / 1 (4 KiB, 4 per CU)   4 = 256 / 2048 / 2 (8 KiB, 2 per CU)
+//         5 = 512 / 4096 / 2 (16 KiB, 1 per CU: v2's shape + prefetch)
+int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, void* lo, void* val, void* rep,
+               void* ctrl, u64 cap, void* ovf_hi, void* ovf_lo, void* ovf_rep, u64 ovf_cap, void* ovf_counter,
+               int config, void* stamps, hipStream_t stream) {
+  if (nbytes == 0) return 0;
+  GTab g;
+  g.tag = (u64*)tag;
+  g.hi = (u64*)hi;
+  g.lo = (u64*)lo;
+  g.val = (long long*)val;
+  g.rep = (u64*)rep;
+  g.ctrl = (u32*)ctrl;
+  g.mask = cap - 1;
+  v3::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter, (u64*)stamps};
+  const int aligned = ((uintptr_t)text & 15) == 0;
+  const u8* tx = (const u8*)text;
+  switch (config) {
+    case 0: v3::launch<512, 2048, 1>(tx, nbytes, rep_base, g, o, aligned, stream); break;
+    case 1: v3::launch<512, 2048, 2>(tx, nbytes, rep_base, g, o, aligned, stream); break;
+    case 2: v3::launch<1024, 4096, 1>(tx, nbytes, rep_base, g, o, aligned, stream); break;
+    case 3: v3::launch<256, 1024, 1>(tx, nbytes, rep_base, g, o, aligned, stream); break;
+    case 4: v3::launch<256, 2048, 2>(tx, nbytes, rep_base, g, o, aligned, stream); break;
+    case 5: v3::launch<512, 4096, 2>(tx, nbytes, rep_base, g, o, aligned, stream); break;
+    default: return -1;
+  }
+  hipLaunchKernelGGL(v3::ovf_agg3_kernel, dim3(1024), dim3(256), 0, stream, o, g);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

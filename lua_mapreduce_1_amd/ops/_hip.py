@@ -27,6 +27,7 @@ _SIGS = {
     "mr_wc_map": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p],
     "mr_count_tokens": [_p, _u64, _u64, _p, _p],
     "mr_wc_map2": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
+    "mr_wc_map3": [_p, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
     "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p],
     "mr_table_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],

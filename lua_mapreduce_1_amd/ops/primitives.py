@@ -72,6 +72,8 @@ def _t64(a: np.ndarray, device="cpu") -> torch.Tensor:
 
 # ---------------------------------------------------------------------------
 _WC_CHUNK_MAX = int(os.environ.get("MR_WC_CHUNK_MAX", 16 * 1024))
+_WC_VERSION = int(os.environ.get("MR_WC_VERSION", 3))
+_OVF_COUNTERS = 64
 
 
 class HashTable:
@@ -104,6 +106,9 @@ class HashTable:
         if self.is_cuda:
             _hip.call("mr_table_reset", _hip.ptr(self.tag), _hip.ptr(self.lo), _hip.ptr(self.val), _hip.ptr(self.ctrl),
                       self.cap, _op_init(self.op), _hip.stream(self.device))
+            if getattr(self, "_ovf_counters", None) is not None and self._ovf_next:
+                self._ovf_counters.zero_()
+                self._ovf_next = 0
         else:
             self._pending = []
 
@@ -136,11 +141,19 @@ class HashTable:
             d = self.device
             self._ovf = [torch.empty(need, dtype=torch.int64, device=d) for _ in range(3)]
             self._ovf_cnt = torch.empty(need, dtype=torch.int32, device=d)
-            self._ovf_counter = torch.zeros(1, dtype=torch.int64, device=d)
+            # one overflow counter per map launch between two resets (no fill
+            # kernel in front of every chunk's map launch)
+            self._ovf_counters = torch.zeros(_OVF_COUNTERS, dtype=torch.int64, device=d)
+            self._ovf_next = 0
+        if self._ovf_next == _OVF_COUNTERS:
+            self._ovf_counters.zero_()
+            self._ovf_next = 0
+        self._ovf_counter = self._ovf_counters[self._ovf_next:self._ovf_next + 1]
+        self._ovf_next += 1
         return self._ovf, self._ovf_counter
 
     def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, chunk_bytes: int | None = None,
-                      version: int = 2, mode: int = 0) -> None:
+                      version: int | None = None, mode: int = 0, stamps: torch.Tensor | None = None) -> None:
         """Fused tokenize + exact key + combine of every whitespace token (value 1).
 
         ``chunk_bytes`` = bytes per workgroup; by default ~nbytes/1024 rounded to
@@ -151,6 +164,10 @@ class HashTable:
         nbytes = text.numel()
         if nbytes == 0:
             return
+        if version is None:
+            # v3 (8 KiB chunks, two workgroups per CU) unless the caller pins a
+            # v2 chunk size; MR_WC_VERSION=2 restores v2 for ablations
+            version = 2 if chunk_bytes is not None else _WC_VERSION
         if chunk_bytes is None:
             chunk_bytes = min(_WC_CHUNK_MAX, max(8192, (nbytes // 1024 + 8191) // 8192 * 8192))
         if self.is_cuda:
@@ -160,6 +177,11 @@ class HashTable:
                           _hip.stream(self.device))
                 return
             ovf, counter = self._overflow(nbytes)
+            if version == 3:
+                _hip.call("mr_wc_map3", _hip.ptr(text), nbytes, rep_base, *self._gtab(), self.cap,
+                          _hip.ptr(ovf[0]), _hip.ptr(ovf[1]), _hip.ptr(ovf[2]), ovf[0].numel(), _hip.ptr(counter),
+                          mode, _hip.ptr(stamps) if stamps is not None else None, _hip.stream(self.device))
+                return
             counter.zero_()
             chunk = min(65536, max(8192, (chunk_bytes + 8191) // 8192 * 8192))
             _hip.call("mr_wc_map2", _hip.ptr(text), nbytes, chunk, rep_base, *self._gtab(),

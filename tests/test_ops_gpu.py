@@ -46,6 +46,29 @@ def test_wordcount_map_unaligned_and_chunks(gpu):
         assert _wc_dict(hi, lo, val, rep, t) == _naive(text)
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
+def test_wordcount_map3_configs_match_naive(gpu, cfg):
+    """Every v3 launch shape (threads / LDS slots / tiles per chunk) on tricky
+    bytes (long tokens crossing tiles, all whitespace kinds, NULs), aligned and
+    misaligned, in several launches into one table (per-launch overflow
+    counters), plus a tiny table that forces the overflow path."""
+    rng = np.random.default_rng(100 + cfg)
+    text = tricky_text(rng, 700_001)
+    base = torch.frombuffer(bytearray(b"x" + text), dtype=torch.uint8).to(gpu)
+    for t in (base[1:].contiguous(), base[1:]):
+        tab = ops.HashTable(1 << 16, device=gpu)
+        cut = [0, 12_345, 400_000, len(text)]
+        for a, b in zip(cut[:-1], cut[1:]):  # a token cut by a launch boundary counts as two
+            tab.wordcount_map(t[a:b], rep_base=a, version=3, mode=cfg)
+        hi, lo, val, rep = tab.compact()
+        got = _wc_dict(hi, lo, val, rep, t)
+        want = {}
+        for a, b in zip(cut[:-1], cut[1:]):
+            for w, c in _naive(text[a:b]).items():
+                want[w] = want.get(w, 0) + c
+        assert got == want
+
+
 def test_wordcount_europarl_like_shape(gpu):
     splits = europarl_like(seed=5, lines=20_000, words=500_000, vocab_size=50_000)
     text = b"".join(splits)

@@ -62,4 +62,8 @@ def main() -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    rc = main()
+    sys.stdout.flush()
+    if os.environ.get("MR_FAST_EXIT"):
+        os._exit(rc)
+    sys.exit(rc)
