@@ -9,7 +9,8 @@
 // 2-word control block {nclaimed, overflow}.
 //
 // Concurrency protocol (agent scope, placement independent — guide §6 G16):
-//   claim:   CAS tag 0 -> key_tag(hi,lo)            (relaxed, agent)
+//   claim:   CAS tag 0 -> gtab_tag(hi,lo)           (relaxed, agent); for keys of <= 7
+//            bytes the tag IS the key (mr_common.h) and a tag match is final
 //   publish: sc1 stores of hi, rep ; fold value ; s_waitcnt vmcnt(0) ; sc1 store lo
 //   lookup:  tag match -> load lo (relaxed); lo==0 => not yet published, retry;
 //            lo match -> load hi; on mismatch re-check after an acquire fence.
@@ -26,11 +27,20 @@ struct GTab {
   u64* lo;
   long long* val;
   u64* rep;
-  u32* ctrl;      // [0] = claimed slots, [1] = overflow flag
+  u32* ctrl;      // [0] = claimed slots (host-side inserts), [1] = overflow flag,
+                  // [CTRL_SHARD0 + CTRL_STRIDE * s] = claim-count shard s (s < CTRL_SHARDS)
   u64 mask;       // capacity - 1 (capacity is a power of two)
 };
 
 constexpr u32 GTAB_MAX_PROBES = 1u << 14;
+// Claim counts go to 64 shards, each on its own 128-byte line: same-address
+// device atomics serialise at the memory side (~12 ns each,
+// tools/probe/atomic_probe.hip), and one counter took an add from every wave
+// of every map launch.  The host sums the shards (HashTable.stats()).
+constexpr u32 CTRL_SHARD0 = 32;
+constexpr u32 CTRL_STRIDE = 32;
+constexpr u32 CTRL_SHARDS = 64;
+constexpr u32 CTRL_WORDS = CTRL_SHARD0 + CTRL_STRIDE * CTRL_SHARDS;
 
 __device__ __forceinline__ u64 ld_agent(const u64* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -53,8 +63,9 @@ __device__ __forceinline__ void fold_value(long long* p, long long v, int op) {
 // a same-address atomic per claim serialised ~3e5 adds in the map kernel).
 __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long long v, u64 rep, int op,
                                            u64* out_slot = nullptr) {
-  const u64 tag = key_tag(hi, lo);
-  u64 slot = (tag >> 7) & t.mask;
+  const u64 tag = gtab_tag(hi, lo);
+  const bool exact = gtab_tag_exact(tag);
+  u64 slot = gtab_home(tag, t.mask);
   u32 probes = 0;
   while (probes < GTAB_MAX_PROBES) {
     u64 cur = ld_agent(&t.tag[slot]);
@@ -75,6 +86,11 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
         return 2;
       }
       cur = expected;
+    }
+    if (cur == tag && exact) {  // the tag is the key: fold without waiting for the payload
+      fold_value(&t.val[slot], v, op);
+      if (out_slot) *out_slot = slot;
+      return 1;
     }
     if (cur == tag) {
       const u64 l = ld_agent(&t.lo[slot]);
@@ -99,13 +115,16 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
   return 0;
 }
 
-// Wave-reduce per-lane claim counts and add them to ctrl[0] (call with the
-// whole wave active, e.g. at kernel end).
+// Wave-reduce per-lane claim counts and add them to a claim-count shard (call
+// with the whole wave active, e.g. at kernel end).
 __device__ __forceinline__ void gtab_count_claims(const GTab& t, u32 claims) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) claims += __shfl_xor(claims, o);
-  if ((threadIdx.x & 63) == 0 && claims)
-    __hip_atomic_fetch_add(&t.ctrl[0], claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((threadIdx.x & 63) == 0 && claims) {
+    const u32 shard = (blockIdx.x * 4u + (threadIdx.x >> 6)) & (CTRL_SHARDS - 1);
+    __hip_atomic_fetch_add(&t.ctrl[CTRL_SHARD0 + CTRL_STRIDE * shard], claims, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 }  // namespace mr

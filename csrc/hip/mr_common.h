@@ -55,6 +55,21 @@ MR_HD u64 fmix64(u64 x) {
 // Slot tag of a key: never 0 (0 marks an empty slot).
 MR_HD u64 key_tag(u64 hi, u64 lo) { return fmix64(hi ^ fmix64(lo + 0x9E3779B97F4A7C15ull)) | 1ull; }
 
+// Claim word of a key in the HBM table (hashtab.h).  A packed key of at most
+// 7 bytes has lo == len (1..7) and zero low byte in hi, so hi | lo IS the key:
+// claiming its slot publishes the key in one atomic and a tag match is a key
+// match (no wait for the claimer's payload stores).  These are the frequent
+// words of natural text, whose slots every workgroup hits at once on a cold
+// table.  Other keys get a 56-bit hash with low byte 0x80 (never an exact tag).
+MR_HD bool gtab_tag_exact(u64 tag) { return (tag & 0xF8ull) == 0; }
+MR_HD u64 gtab_tag(u64 hi, u64 lo) {
+  // (generic callers may insert arbitrary (hi, lo): the exact form is used only
+  // where it is injective — 1 <= lo <= 7 and a zero low byte in hi)
+  return (lo - 1 < 7 && (hi & 0xFFull) == 0) ? (hi | lo)
+                                             : ((fmix64(hi ^ fmix64(lo + 0x9E3779B97F4A7C15ull)) & ~0xFFull) | 0x80ull);
+}
+MR_HD u64 gtab_home(u64 tag, u64 mask) { return fmix64(tag ^ 0x2545F4914F6CDD1Dull) & mask; }
+
 // Hash of a long key, word-at-a-time over little-endian 8-byte words (the last
 // one zero padded).  Identical on host and device.
 MR_HD u64 long_hash_step(u64 h, u64 w) { return fmix64(h ^ w) * 0x9E3779B97F4A7C15ull; }

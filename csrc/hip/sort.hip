@@ -462,7 +462,7 @@ __device__ __forceinline__ bool tail_less(u64 h, u64 la, u64 ra, u64 lb, u64 rb,
 }
 
 __global__ void tie_fixup_kernel(const u64* c, u64* hi, u64* lo, long long* val, u64* rep, u32* part, u64 n,
-                                 u32* bad, const u8* src) {
+                                 u32* bad, const u8* src, u64* ln /* optional: key lengths, permuted too */) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     if (i > 0 && c[i] == c[i - 1]) continue;  // not a run head
@@ -479,6 +479,7 @@ __global__ void tie_fixup_kernel(const u64* c, u64* hi, u64* lo, long long* val,
       const u64 h = hi[a], l = lo[a], r = rep[a];
       const long long v = val[a];
       const u32 p = part[a];
+      const u64 k = ln ? ln[a] : 0;
       u64 b = a;
       while (b > i) {
         const u64 hb = hi[b - 1];
@@ -492,6 +493,7 @@ __global__ void tie_fixup_kernel(const u64* c, u64* hi, u64* lo, long long* val,
         val[b] = val[b - 1];
         rep[b] = rep[b - 1];
         part[b] = part[b - 1];
+        if (ln) ln[b] = ln[b - 1];
         --b;
       }
       hi[b] = h;
@@ -499,6 +501,7 @@ __global__ void tie_fixup_kernel(const u64* c, u64* hi, u64* lo, long long* val,
       val[b] = v;
       rep[b] = r;
       part[b] = p;
+      if (ln) ln[b] = k;
     }
     // bit 2 (no key bytes given): two adjacent keys share the 8-byte prefix and
     // one is a long (hashed) key -> the host must check their order bytewise
@@ -706,10 +709,10 @@ int mr_composite_key(const void* part, const void* hi, u64 n, void* out, hipStre
 }
 
 int mr_tie_fixup(const void* c, void* hi, void* lo, void* val, void* rep, void* part, u64 n, void* bad,
-                 const void* src, hipStream_t s) {
+                 const void* src, void* ln, hipStream_t s) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(tie_fixup_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)c, (u64*)hi, (u64*)lo,
-                     (long long*)val, (u64*)rep, (u32*)part, n, (u32*)bad, (const u8*)src);
+                     (long long*)val, (u64*)rep, (u32*)part, n, (u32*)bad, (const u8*)src, (u64*)ln);
   return (int)hipGetLastError();
 }
 

@@ -395,7 +395,8 @@ __global__ void table_reset_kernel(u64* tag, u64* lo, long long* val, u32* ctrl,
     lo[i] = 0;
     val[i] = init;
   }
-  if (blockIdx.x == 0 && threadIdx.x < 2) ctrl[threadIdx.x] = 0;
+  if (blockIdx.x == 0)
+    for (u32 w = threadIdx.x; w < CTRL_WORDS; w += blockDim.x) ctrl[w] = 0;
 }
 
 }  // namespace mr

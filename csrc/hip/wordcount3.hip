@@ -267,15 +267,20 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
     khi[k] = L.hi[s];
     klo[k] = L.lo[s];
     krep[k] = L.rep[s];
-    ktag[k] = key_tag(khi[k], klo[k]);
-    kslot[k] = (ktag[k] >> 7) & g.mask;
+    ktag[k] = gtab_tag(khi[k], klo[k]);
+    kslot[k] = gtab_home(ktag[k], g.mask);
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (kcnt[k]) {
       gt[k] = ld_agent(&g.tag[kslot[k]]);
-      gl[k] = ld_agent(&g.lo[kslot[k]]);
-      gh[k] = ld_agent(&g.hi[kslot[k]]);
+      if (!gtab_tag_exact(ktag[k])) {
+        gl[k] = ld_agent(&g.lo[kslot[k]]);
+        gh[k] = ld_agent(&g.hi[kslot[k]]);
+      } else {
+        gl[k] = klo[k];
+        gh[k] = khi[k];
+      }
     }
   }
   // new keys whose home slot is empty are claimed in a batch too: all CASes,

@@ -46,7 +46,7 @@ _SIGS = {
     "mr_bincount": [_p, _u64, _u32, _p, _p],
     "mr_composite_key": [_p, _p, _u64, _p, _p],
     "mr_copy_to_host": [_p, _p, _p, _u64, _u64, _p],
-    "mr_tie_fixup": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p],
+    "mr_tie_fixup": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p],
     "mr_gather_cols": [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "mr_mlp_grad": [_p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _i32, _p],
     "mr_mlp_sgd": [_p, _p, _p, _i32, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _i32, _i32,

@@ -74,6 +74,8 @@ def _t64(a: np.ndarray, device="cpu") -> torch.Tensor:
 _WC_CHUNK_MAX = int(os.environ.get("MR_WC_CHUNK_MAX", 16 * 1024))
 _WC_VERSION = int(os.environ.get("MR_WC_VERSION", 3))
 _OVF_COUNTERS = 64
+_CTRL_SHARD0, _CTRL_STRIDE, _CTRL_SHARDS = 32, 32, 64  # csrc/hip/hashtab.h
+_CTRL_WORDS = _CTRL_SHARD0 + _CTRL_STRIDE * _CTRL_SHARDS
 
 
 class HashTable:
@@ -94,7 +96,9 @@ class HashTable:
             self.lo = torch.zeros(self.cap, dtype=torch.int64, device=d)
             self.val = torch.full((self.cap,), _op_init(op), dtype=torch.int64, device=d)
             self.rep = torch.zeros(self.cap, dtype=torch.int64, device=d)
-            self.ctrl = torch.zeros(2, dtype=torch.int32, device=d)
+            # [0] claims, [1] overflow flag, then 64 claim-count shards 128 B
+            # apart (csrc/hip/hashtab.h CTRL_*): stats() sums them
+            self.ctrl = torch.zeros(_CTRL_WORDS, dtype=torch.int32, device=d)
         else:
             self._pending: list[tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]] = []
 
@@ -199,8 +203,8 @@ class HashTable:
     def stats(self) -> tuple[int, bool]:
         """(occupied slots, overflowed).  Synchronises on GPU."""
         if self.is_cuda:
-            c = self.ctrl.cpu().tolist()
-            return int(c[0]), bool(c[1])
+            c = self.ctrl.cpu()
+            return int(c[0]) + int(c[_CTRL_SHARD0::_CTRL_STRIDE].sum()), bool(c[1])
         return sum(p[0].size for p in self._pending), False
 
     def compact(self, known_stats: tuple[int, bool] | None = None):
@@ -503,7 +507,7 @@ def sort_by_partition_key(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor
     hi, lo, val, rep = cols
     bad = torch.zeros(1, dtype=torch.int32, device=d)
     _hip.call("mr_tie_fixup", _hip.ptr(c), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part2),
-              n, _hip.ptr(bad), _hip.ptr(src) if src is not None else None, s)
+              n, _hip.ptr(bad), _hip.ptr(src) if src is not None else None, None, s)
     return part2, hi, lo, val, rep, bad
 
 

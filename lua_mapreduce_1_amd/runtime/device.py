@@ -263,7 +263,7 @@ def finalize_table_device(table, n: int, src, nparts: int) -> dict:
               _hip.ptr(part0), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), _hip.ptr(ln), s)
     bad = torch.zeros(1, dtype=torch.int32, device=d)
     _hip.call("mr_tie_fixup", _hip.ptr(cs), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part),
-              n, _hip.ptr(bad), _hip.ptr(src), s)
+              n, _hip.ptr(bad), _hip.ptr(src), _hip.ptr(ln), s)  # ln is permuted with the rows
     cap = src.numel()
     off, blob = ops.gather_key_bytes(hi, lo, rep, src, lengths=ln, capacity=cap)
     nb = int(_hip.lib().mr_tail_pack_bytes(n, nparts))

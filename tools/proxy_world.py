@@ -1,0 +1,69 @@
+#!/usr/bin/env python
+"""Per-rank proxy of the W>1 SPMD iteration on ONE GPU: rank 0 of a simulated
+world of N ranks maps its 1/N of the corpus and runs the whole multi-rank
+path (compact -> FNV partition -> pack by destination -> count exchange ->
+two all-to-alls -> reduce table -> fused tail -> host results) with the
+collectives replaced by a loopback (every peer is assumed to send what this
+rank sends: same volumes, no xGMI time).  Shows the device work and the host
+overheads of the W>1 path that RCCL latency then adds to.
+
+    python tools/proxy_world.py --world 8 [--steps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from bench import MODEL, load_corpus  # noqa: E402
+from lua_mapreduce_1_amd.parallel import dist as D  # noqa: E402
+from lua_mapreduce_1_amd.parallel import spmd as S  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    a = ap.parse_args()
+    _, _, device = D.init_from_env()
+    splits = load_corpus(1234, 0, 0, 1, device)
+    store = S.SplitStore(splits)
+    W = a.world
+    # loopback collectives
+    D.exchange_counts = lambda counts, group=None: counts.clone()
+    D.all_to_all_v = lambda payload, send, recv, group=None: payload[:sum(recv)].clone()
+    S.D.world_info = lambda group=None: (0, W)
+    params = dict(taskfn=MODEL, mapfn=MODEL, partitionfn=MODEL, reducefn=MODEL, finalfn=MODEL,
+                  init_args={"nsplits": len(store), "num_reducers": 10})
+    eng = S.SPMDEngine(params, device=device, split_store=store)
+    assert eng.world == W and eng.rank == 0
+    eng.prefetch = True
+    for _ in range(a.warmup):
+        eng.run_iteration()
+    torch.cuda.synchronize()
+    per = []
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        t1 = time.perf_counter()
+        res = eng.run_iteration(prefetch_next=i < a.steps - 1)
+        per.append(1000 * (time.perf_counter() - t1))
+    torch.cuda.synchronize()
+    ms = 1000 * (time.perf_counter() - t0) / a.steps
+    seq = [round(x, 2) for x in per]
+    per.sort()
+    print(json.dumps({"world": W, "ms_per_step": ms, "median": per[len(per) // 2], "min": per[0], "seq": seq,
+                      "distinct_after_reduce": res.distinct_keys, "timings": res.timings}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    rc = main()
+    sys.stdout.flush()
+    sys.exit(rc)
