@@ -23,6 +23,7 @@ The corpus is fixed, so adding GPUs divides it (strong scaling).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -83,13 +84,24 @@ def main() -> int:
                   init_args={"nsplits": len(store), "num_reducers": args.reducers})
     eng = SPMDEngine(params, device=device, split_store=store, verbose=args.verbose)
 
-    # consecutive iterations are pipelined: once an iteration's map is done,
-    # the next iteration's input copies start (double-buffered HBM arena)
-    # while this one reduces; the last timed step prefetches nothing, so the
-    # timed region holds exactly `steps` iterations of work
+    # consecutive iterations are pipelined: the next iteration's input copies
+    # start as soon as the HBM arena they fill is free (double-buffered), and
+    # its map as soon as this map is done; neither the last warm-up step nor
+    # the last timed step starts anything for the next one, so the timed
+    # region holds exactly `steps` iterations of work (and one pipeline fill)
     eng.prefetch = True
-    for _ in range(args.warmup):
-        eng.run_iteration()
+    # ... and pipelined: iteration i+1's map runs on a second stream while
+    # iteration i shuffles, reduces and downloads its results
+    eng.pipeline = os.environ.get("MR_PIPELINE", "1") != "0"
+    # the last warm-up step starts nothing for the next one: every copy and map
+    # of the K timed iterations happens inside the timed region
+    for w in range(args.warmup):
+        eng.run_iteration(prefetch_next=w < args.warmup - 1)
+    # long-lived objects (modules, corpus, engine) move to the permanent GC
+    # generation: a full collection over them stalled an iteration by ~5 ms
+    # every few dozen iterations (the per-iteration host work is ~1 ms at 8 GPUs)
+    gc.collect()
+    gc.freeze()
     D.barrier(device=device)
     if device.type == "cuda":
         torch.cuda.synchronize(device)

@@ -18,6 +18,7 @@
 //   pk_fix_loc : received loc -> absolute (offset in the received byte blob)
 #include <hip/hip_runtime.h>
 #include "mr_common.h"
+#include "hashtab.h"
 
 namespace mr {
 namespace pk {
@@ -135,6 +136,45 @@ __global__ void pk_fix_loc_kernel(u64* __restrict__ rec, u64 n, const long long*
   }
 }
 
+// Receive side in ONE launch: records [hi, lo, val, loc] from W sources (row
+// and byte counts per source in `recv` = the count-exchange row [W][3] on the
+// device) are folded into the reduce table with absolute rep words (loc made
+// relative to the received byte blob).  Replaces the column splits, the
+// host-built prefix arrays and their H2D copies, fix_loc and hash_agg.
+constexpr int MAXW_RECV = 1024;
+__global__ void __launch_bounds__(256) pk_insert_received_kernel(const u64* __restrict__ rec, u64 n,
+                                                                 const long long* __restrict__ recv, u32 W, GTab g,
+                                                                 int op) {
+  __shared__ long long rstart[MAXW_RECV + 1];
+  __shared__ long long bstart[MAXW_RECV + 1];
+  if (threadIdx.x == 0) {  // W is small (ranks of one job): a serial prefix sum
+    long long r = 0, b = 0;
+    for (u32 k = 0; k < W; ++k) {
+      rstart[k] = r;
+      bstart[k] = b;
+      r += recv[3 * k];
+      b += recv[3 * k + 1];
+    }
+    rstart[W] = r;
+    bstart[W] = b;
+  }
+  __syncthreads();
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  u32 claims = 0;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u32 a = 0, b = W;
+    while (b - a > 1) {
+      const u32 m = (a + b) >> 1;
+      if ((long long)i >= rstart[m]) a = m;
+      else b = m;
+    }
+    const u64 loc = rec[4 * i + 3];
+    const u64 rep = make_rep(rep_off(loc) + (u64)bstart[a], rep_len(loc));
+    claims += gtab_insert(g, rec[4 * i], rec[4 * i + 1], (long long)rec[4 * i + 2], rep, op) == 2;
+  }
+  gtab_count_claims(g, claims);
+}
+
 }  // namespace pk
 }  // namespace mr
 
@@ -169,6 +209,23 @@ int mr_pack_by_dest(const void* hi, const void* lo, const void* val, const void*
                        (const long long*)val, (const u64*)rep, (const u32*)part, n, W, (const u8*)src,
                        (const unsigned long long*)start, cursor, (u64*)rec, (u8*)blob);
   }
+  return (int)hipGetLastError();
+}
+
+int mr_insert_received(const void* rec, u64 n, const void* recv, u32 W, void* tag, void* hi, void* lo, void* val,
+                       void* rep, void* ctrl, u64 cap, int op, hipStream_t s) {
+  if (n == 0) return 0;
+  if (W == 0 || W > (u32)pk::MAXW_RECV) return -1;
+  GTab g;
+  g.tag = (u64*)tag;
+  g.hi = (u64*)hi;
+  g.lo = (u64*)lo;
+  g.val = (long long*)val;
+  g.rep = (u64*)rep;
+  g.ctrl = (u32*)ctrl;
+  g.mask = cap - 1;
+  hipLaunchKernelGGL(pk::pk_insert_received_kernel, dim3(pk_grid(n, 2048)), dim3(256), 0, s, (const u64*)rec, n,
+                     (const long long*)recv, W, g, op);
   return (int)hipGetLastError();
 }
 

@@ -564,37 +564,52 @@ static inline int grid_n(u64 n, int block, int maxg = 8192) {
   return (int)g;
 }
 
-// single-launch exclusive scan for small arrays (<= 1024 * 64 elements)
+// single-launch exclusive scan for small arrays (<= 1024 * SS_ITEMS elements):
+// each thread keeps its (contiguous) elements in registers — one batch of
+// independent loads instead of a serial chain of strided ones (the old form
+// read up to 64 elements per thread one after another: 114 us at n = 54k).
 constexpr int SS_THREADS = 1024;
+constexpr int SS_ITEMS = 16;
 template <typename T>
 __global__ void __launch_bounds__(SS_THREADS) scan_small_kernel(const T* in, T* out, u64 n, T* total) {
-  __shared__ T sh[SS_THREADS];
-  const int t = threadIdx.x;
-  const u64 per = (n + SS_THREADS - 1) / SS_THREADS;
+  __shared__ T sh[SS_THREADS / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const u64 per = (n + SS_THREADS - 1) / SS_THREADS;  // <= SS_ITEMS
   const u64 b = (u64)t * per;
+  T v[SS_ITEMS];
   T s = 0;
-  for (u64 i = b; i < b + per && i < n; ++i) s += in[i];
-  sh[t] = s;
+#pragma unroll
+  for (int k = 0; k < SS_ITEMS; ++k) {
+    v[k] = ((u64)k < per && b + k < n) ? in[b + k] : (T)0;
+    s += v[k];
+  }
+  T incl = s;  // wave-inclusive scan of the per-thread sums
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) sh[wave] = incl;
   __syncthreads();
-  for (int o = 1; o < SS_THREADS; o <<= 1) {
-    const T y = t >= o ? sh[t - o] : (T)0;
-    __syncthreads();
-    sh[t] += y;
-    __syncthreads();
+  T before = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < SS_THREADS / 64; ++w) {
+    before += w < wave ? sh[w] : (T)0;
+    all += sh[w];
   }
-  T off = sh[t] - s;
-  for (u64 i = b; i < b + per && i < n; ++i) {
-    const T x = in[i];
-    out[i] = off;
-    off += x;
+  T off = before + incl - s;
+#pragma unroll
+  for (int k = 0; k < SS_ITEMS; ++k) {
+    if ((u64)k < per && b + k < n) out[b + k] = off;
+    off += v[k];
   }
-  if (t == SS_THREADS - 1 && total) *total = sh[t];
+  if (t == 0 && total) *total = all;
 }
 
 template <typename T>
 static int scan_impl(const T* in, T* out, u64 n, T* partials, T* total, hipStream_t s) {
   if (n == 0) return 0;
-  if (n <= (u64)SS_THREADS * 64) {
+  if (n <= (u64)SS_THREADS * SS_ITEMS) {
     hipLaunchKernelGGL(scan_small_kernel<T>, dim3(1), dim3(SS_THREADS), 0, s, in, out, n, total);
     return (int)hipGetLastError();
   }
@@ -699,6 +714,17 @@ int mr_copy_to_host(const void* src, void* host_dst, const void* nelem, u64 elem
   hipLaunchKernelGGL(copy_to_host_kernel, dim3(1024), dim3(256), 0, s, (const u8*)src, (u8*)dptr,
                      (const long long*)nelem, elem_size, max_bytes);
   return (int)hipGetLastError();
+}
+
+// Async DMA between pinned host memory and HBM (kind: 1 = H2D, 2 = D2H).
+// Used instead of torch's copy_ for the input staging: copy_ also records an
+// event for the pinned block in torch's host allocator on every call, and the
+// first few of those stalled the host by ~6 ms (tools/first_iter.py).
+int mr_memcpy_async(void* dst, const void* src, u64 nbytes, int kind, hipStream_t s) {
+  if (nbytes == 0) return 0;
+  const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : (kind == 2 ? hipMemcpyDeviceToHost
+                                                                          : hipMemcpyDeviceToDevice);
+  return (int)hipMemcpyAsync(dst, src, nbytes, k, s);
 }
 
 int mr_composite_key(const void* part, const void* hi, u64 n, void* out, hipStream_t s) {

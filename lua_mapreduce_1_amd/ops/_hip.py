@@ -28,6 +28,8 @@ _SIGS = {
     "mr_count_tokens": [_p, _u64, _u64, _p, _p],
     "mr_wc_map2": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
     "mr_wc_map3": [_p, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
+    "mr_insert_received": [_p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p, _u64, _i32, _p],
+    "mr_memcpy_async": [_p, _p, _u64, _i32, _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
     "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p],
     "mr_table_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
@@ -113,6 +115,11 @@ def ptr(t):
 
 def stream(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def stream_ptr(s) -> ctypes.c_void_p:
+    """Raw hipStream_t of a torch stream object."""
+    return ctypes.c_void_p(s.cuda_stream)
 
 
 def check(rc: int, what: str) -> None:

@@ -74,6 +74,7 @@ def _t64(a: np.ndarray, device="cpu") -> torch.Tensor:
 _WC_CHUNK_MAX = int(os.environ.get("MR_WC_CHUNK_MAX", 16 * 1024))
 _WC_VERSION = int(os.environ.get("MR_WC_VERSION", 3))
 _OVF_COUNTERS = 64
+_OVF_ENTRIES = 1 << 18
 _CTRL_SHARD0, _CTRL_STRIDE, _CTRL_SHARDS = 32, 32, 64  # csrc/hip/hashtab.h
 _CTRL_WORDS = _CTRL_SHARD0 + _CTRL_STRIDE * _CTRL_SHARDS
 
@@ -136,11 +137,15 @@ class HashTable:
                 r = r + np.uint64(rep_add << K.REP_LEN_BITS)
             self._pending.append((_u64(hi).copy(), _u64(lo).copy(), v, r))
 
-    def _overflow(self, nbytes: int):
-        """Staging / overflow entries (hi, lo, rep, count): sized for the
-        distinct-per-workgroup keys of a launch (a bit under one entry per 8
-        input bytes); entries past the end are inserted directly."""
-        need = min(1 << 24, max(1 << 16, nbytes // 6))
+    def _overflow(self, nbytes: int, staged: bool = False):
+        """Overflow entries (hi, lo, rep, count) of the map kernels: tokens that
+        found their workgroup's LDS table full (v3: ~10 per launch on the
+        benchmark corpus; v2's staged mode: up to one per 8 input bytes).
+        Entries past the end are inserted into the HBM table directly, so the
+        capacity only matters for speed: a fixed size (no re-allocation when a
+        bigger launch comes along — a hipMalloc in the middle of an iteration
+        cost ~5 ms), larger only for v2's staged ablation mode."""
+        need = min(1 << 24, max(_OVF_ENTRIES, nbytes // 6)) if staged else _OVF_ENTRIES
         if getattr(self, "_ovf", None) is None or self._ovf[0].numel() < need:
             d = self.device
             self._ovf = [torch.empty(need, dtype=torch.int64, device=d) for _ in range(3)]
@@ -180,7 +185,7 @@ class HashTable:
                 _hip.call("mr_wc_map", _hip.ptr(text), nbytes, chunk_bytes, rep_base, *self._gtab(), self.cap,
                           _hip.stream(self.device))
                 return
-            ovf, counter = self._overflow(nbytes)
+            ovf, counter = self._overflow(nbytes, staged=(version == 2 and mode == 4))
             if version == 3:
                 _hip.call("mr_wc_map3", _hip.ptr(text), nbytes, rep_base, *self._gtab(), self.cap,
                           _hip.ptr(ovf[0]), _hip.ptr(ovf[1]), _hip.ptr(ovf[2]), ovf[0].numel(), _hip.ptr(counter),
@@ -198,6 +203,24 @@ class HashTable:
             rep = ((starts.astype(np.uint64) + np.uint64(rep_base)) << np.uint64(K.REP_LEN_BITS)) | \
                 np.minimum(lens, K.REP_LEN_MASK).astype(np.uint64)
             self._pending.append((hi, lo, np.ones(hi.size, np.int64), rep))
+
+    def insert_received(self, rec: torch.Tensor, recv_counts: torch.Tensor, W: int) -> None:
+        """Fold all-to-all-received records ``rec`` [n, 4] = (hi, lo, val, loc)
+        into the table; ``recv_counts`` = the device count-exchange row [W, 3]
+        (rows, key bytes, extra) per source; rep words become offsets into the
+        concatenated received key bytes.  One launch (csrc/hip/shuffle.hip)."""
+        n = rec.shape[0]
+        if n == 0:
+            return
+        if self.is_cuda:
+            assert rec.is_contiguous() and recv_counts.is_contiguous()
+            _hip.call("mr_insert_received", _hip.ptr(rec), n, _hip.ptr(recv_counts), W, *self._gtab(), self.cap,
+                      OPS[self.op], _hip.stream(self.device))
+            return
+        from .shuffle import absolute_reps
+        rc = recv_counts.view(W, 3).tolist()
+        rep = absolute_reps(rec, [r[0] for r in rc], [r[1] for r in rc])
+        self.insert(rec[:, 0].contiguous(), rec[:, 1].contiguous(), rec[:, 2].contiguous(), rep)
 
     # -- state ---------------------------------------------------------------
     def stats(self) -> tuple[int, bool]:

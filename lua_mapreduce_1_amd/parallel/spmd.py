@@ -42,6 +42,14 @@ from ..utils import STATUS
 from . import dist as D
 
 
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
 class SplitStore:
     """Host-resident input splits in ONE pinned buffer (the page-cache analogue
     of the reference's split files).  Every split is followed by a newline so
@@ -163,7 +171,10 @@ class SPMDEngine:
         if self.dmap is None:
             raise ValueError("SPMD engine needs a map module with device_mapfn (use server/worker for host-only "
                              "map functions)")
-        self.table = ops.HashTable(table_capacity, device=self.device, op=self.op)
+        # one map table per input slot: with pipelining, iteration i+1 maps into
+        # tables[1-s] while iteration i's shuffle/reduce still reads tables[s]
+        self._table_capacity = table_capacity
+        self.tables: list = [ops.HashTable(table_capacity, device=self.device, op=self.op), None]
         self.red_table: ops.HashTable | None = None
         # two input arenas: iteration i maps arenas[slot] while the copies of
         # iteration i+1 (prefetch) fill the other one
@@ -171,7 +182,14 @@ class SPMDEngine:
         self.slot = 0
         self._prefetched = None
         self.prefetch = False
+        # iteration pipelining (needs prefetch): the next iteration's map is
+        # queued on the other slot's stream as soon as this map has finished,
+        # and runs while this iteration shuffles, reduces and downloads
+        self.pipeline = False
+        self._pending = None
         self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self.streams = ([torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]
+                        if self.device.type == "cuda" else [None, None])
         self._plans: dict = {}
         import os as _os
         # hipGraph replay of the device tail: measured (tools/proxy_rank.py) to
@@ -182,6 +200,7 @@ class SPMDEngine:
         self._tail_seen: set = set()
         self.iteration = 0
         self.finished = False
+
 
     # ------------------------------------------------------------------------
     def _log(self, msg: str) -> None:
@@ -230,6 +249,17 @@ class SPMDEngine:
     def arena(self):
         return self.arenas[self.slot]
 
+    @property
+    def table(self) -> ops.HashTable:
+        t = self.tables[self.slot]
+        if t is None:
+            t = self.tables[self.slot] = ops.HashTable(self._table_capacity, device=self.device, op=self.op)
+        return t
+
+    @table.setter
+    def table(self, t: ops.HashTable) -> None:
+        self.tables[self.slot] = t
+
     def _plan_chunks(self, ids: list[int], slot: int):
         """Chunking of a contiguous split range (cached per range): boundaries
         at split boundaries, sizes ramping up (the first copy is exposed), big
@@ -241,6 +271,7 @@ class SPMDEngine:
         if self.arenas[slot] is None or self.arenas[slot].numel() < nbytes:
             self.arenas[slot] = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
             self._plans = {k: v for k, v in self._plans.items() if k[2] != slot}
+
         arena = self.arenas[slot]
         offs = self.splits.offsets
         sizes = []
@@ -281,17 +312,34 @@ class SPMDEngine:
         if plan is None:
             plan = self._plan_chunks(ids, slot)
             self._plans[key] = plan
+            if self.copy_stream is not None:
+                # the first two rounds of a plan's copies behind a cross-stream
+                # wait each stalled the host 5-7 ms inside hipMemcpyAsync (a
+                # one-time runtime set-up, tools/first_iter.py): take that hit
+                # here, once per plan, not in an iteration's copy issue
+                for _ in range(2):
+                    self._issue_copies(plan, wait_for=torch.cuda.current_stream(self.device))
+                    self.copy_stream.synchronize()
         return plan
 
     def _issue_copies(self, plan, wait_for=None) -> None:
         bounds, views, host_views, events = plan
         cs = self.copy_stream
         if wait_for is not None:
-            cs.wait_stream(wait_for)  # the arena may still be read by earlier work
-        with torch.cuda.stream(cs):
-            for dst, src, ev in zip(views, host_views, events):
-                dst.copy_(src, non_blocking=True)
-                ev.record(cs)
+            # the arena may still be read by earlier work (a reused event: a
+            # fresh one per iteration grows the runtime's event/signal pool)
+            ev0 = getattr(self, "_copy_gate", None)
+            if ev0 is None:
+                ev0 = self._copy_gate = torch.cuda.Event()
+            ev0.record(wait_for)
+            cs.wait_event(ev0)
+        from ..ops import _hip
+        sp = _hip.stream_ptr(cs)
+        for dst, src, ev in zip(views, host_views, events):
+            # direct hipMemcpyAsync (pinned -> HBM) instead of copy_: no
+            # host-allocator event bookkeeping per chunk (it stalled the host)
+            _hip.call("mr_memcpy_async", _hip.ptr(dst), _hip.ptr(src), dst.numel(), 1, sp)
+            ev.record(cs)
 
     def _split_ids(self, jobs, j0, j1):
         ids = [int(v["split"] if isinstance(v, dict) else v) for _, v in jobs[j0:j1]]
@@ -334,9 +382,21 @@ class SPMDEngine:
                 else:
                     self._prefetched = None
                     self._issue_copies(plan, wait_for=cur)
-                for i, (dst, ev) in enumerate(zip(views, events)):
-                    cur.wait_event(ev)
-                    yield (j0 + bounds[i], j0 + bounds[i + 1]), dst
+                # chunks whose copies have already landed (prefetched during the
+                # previous iteration's tail) are mapped by ONE launch: a launch's
+                # ramp-up and drain cost more than its chunking saves
+                done = 0
+                while done < len(events) and events[done].query():
+                    done += 1
+                i0 = 0
+                if done >= 2:
+                    a0 = views[0].data_ptr() - self.arena.data_ptr()
+                    nb = sum(v.numel() for v in views[:done])
+                    yield (j0 + bounds[0], j0 + bounds[done]), self.arena[a0:a0 + nb]
+                    i0 = done
+                for i in range(i0, len(views)):
+                    cur.wait_event(events[i])
+                    yield (j0 + bounds[i], j0 + bounds[i + 1]), views[i]
             else:
                 for i, (dst, src) in enumerate(zip(views, host_views)):
                     dst.copy_(src)
@@ -397,7 +457,7 @@ class SPMDEngine:
             return self.arena
         return self._ctx.source()
 
-    def _shuffle(self, hi, lo, val, rep, src, part, failed: int = 0):
+    def _shuffle(self, hi, lo, val, rep, src, part, failed: int = 0, raw: bool = False):
         """Send each key to rank part % W; returns received (hi, lo, val, rep,
         src) and sets the job-wide number of failed map jobs (this rank's count
         rides along with the count exchange instead of a separate all-reduce).
@@ -416,6 +476,8 @@ class SPMDEngine:
         recv_rows, recv_bytes = [r[0] for r in recv_h], [r[1] for r in recv_h]
         rrec = D.all_to_all_v(rec, send_rows, recv_rows, self.group)
         rblob = D.all_to_all_v(blob[:sum(send_bytes)], send_bytes, recv_bytes, self.group)
+        if raw:  # the receive-side insert kernel makes the locs absolute itself
+            return rrec, recv.view(W, 3), rblob
         rrep = SH.absolute_reps(rrec, recv_rows, recv_bytes)
         return rrec[:, 0].contiguous(), rrec[:, 1].contiguous(), rrec[:, 2].contiguous(), rrep, rblob
 
@@ -426,19 +488,32 @@ class SPMDEngine:
         return (self.device.type == "cuda" and spec is not None and spec[0] == "fnv1"
                 and self.nparts <= 256 and os.environ.get("MR_FUSED_TAIL", "1") != "0")
 
-    def _reduce_insert(self, hi, lo, val, rep) -> int:
-        """Received rows -> this rank's reduce table; returns its key count."""
-        n = hi.numel()
-        cap = ops.next_pow2(max(1 << 16, 2 * n))
-        if self.red_table is None or self.red_table.cap < cap:
-            self.red_table = ops.HashTable(cap, device=self.device, op=self.op)
-        else:
-            self.red_table.reset()
-        self.red_table.insert(hi, lo, val, rep)
-        m, ovf = self.red_table.stats()
-        if ovf:
-            raise OverflowError("reduce table overflow")
-        return m
+    def _reduce_insert_received(self, rrec, recv_counts) -> int:
+        """Received records -> this rank's reduce table (one insert launch);
+        returns its key count.  The table is sized from the previous
+        iteration's distinct-key count (its compaction scans every slot), not
+        from the received rows (every peer sends the popular keys); a table
+        that ends up more than half full is regrown and refilled."""
+        n = rrec.shape[0]
+        guess = getattr(self, "_red_distinct", None)
+        want = 2 * (guess + guess // 4) if guess is not None else 2 * n
+        cap = ops.next_pow2(max(1 << 16, min(2 * n, want)))
+        while True:
+            if self.red_table is None or self.red_table.cap != cap:
+                self.red_table = ops.HashTable(cap, device=self.device, op=self.op)
+            else:
+                self.red_table.reset()
+            self.red_table.insert_received(rrec, recv_counts, self.world)
+            m, ovf = self.red_table.stats()
+            if not ovf and m <= cap // 2:
+                self._red_distinct = m
+                return m
+            if cap >= ops.next_pow2(2 * n):
+                if ovf:
+                    raise OverflowError("reduce table overflow")
+                self._red_distinct = m
+                return m
+            cap = ops.next_pow2(max(2 * m, 2 * cap))
 
     def _reduce(self, hi, lo, val, rep, src):
         n = hi.numel()
@@ -482,31 +557,77 @@ class SPMDEngine:
         g.replay()
         return pend
 
+    def _can_pipeline(self) -> bool:
+        return (self.copy_stream is not None and self.device_input == "split"
+                and bool(modules.field(self.taskfn, "spmd_replicated_taskfn")))
+
+    def _issue_next_map(self, jobs, j0, j1) -> None:
+        """Queue the NEXT iteration's input copies and map (same job list: the
+        taskfn is pure) on the other slot — its arena, table and stream — and
+        return to this iteration's slot.  Both were last used by the previous
+        iteration, which has fully completed (its results were downloaded)."""
+        cur = self.slot
+        nxt = 1 - cur
+        if self._prefetched is None or self._prefetched[2] != nxt:
+            self._prefetch(jobs, j0, j1)
+        recs = [JobRecord(k, v) for k, v in jobs]
+        self.slot = nxt
+        try:
+            with torch.cuda.stream(self.streams[nxt]):
+                self.table.reset()
+                t0 = time.time()
+                self._run_map(jobs, recs, j0, j1)
+        finally:
+            self.slot = cur
+        self._pending = {"slot": nxt, "jobs": jobs, "recs": recs, "j0": j0, "j1": j1, "t0": t0}
+
     def run_iteration(self, prefetch_next: bool | None = None) -> IterationResult:
         """One MapReduce iteration.  ``prefetch_next`` (default ``self.prefetch``)
-        starts the next iteration's input copies as soon as this map is done."""
+        starts the next iteration's input copies as soon as this map is done;
+        with ``self.pipeline`` it also queues the next iteration's map then."""
         self.iteration += 1
         if prefetch_next is None:
             prefetch_next = self.prefetch
-        if self._prefetched is not None:
-            self.slot = self._prefetched[2]
         res = IterationResult()
         T = res.timings
         t_start = time.time()
-        jobs = self._jobs()
-        recs = [JobRecord(k, v) for k, v in jobs]
+        pending, self._pending = self._pending, None
+        if pending is not None:  # this iteration's map was queued by the previous one
+            self.slot = pending["slot"]
+            jobs, recs, j0, j1, t0 = pending["jobs"], pending["recs"], pending["j0"], pending["j1"], pending["t0"]
+            stream = self.streams[self.slot]
+            if prefetch_next and self.pipeline:
+                # the other arena is free (the previous iteration completed):
+                # keep the copy engine streaming — the next input's copies
+                # queue behind this one's right away
+                self._prefetch(jobs, j0, j1)
+        else:
+            if self._prefetched is not None:
+                self.slot = self._prefetched[2]
+            jobs = self._jobs()
+            recs = [JobRecord(k, v) for k, v in jobs]
+            j0, j1 = self._assign(jobs)
+            stream = None
         res.map_jobs = recs
-        j0, j1 = self._assign(jobs)
-        self.table.reset()
-        t0 = time.time()
-        self._run_map(jobs, recs, j0, j1)
+        with torch.cuda.stream(stream) if stream is not None else _nullctx():
+            if pending is None:
+                self.table.reset()
+                t0 = time.time()
+                self._run_map(jobs, recs, j0, j1)
+            return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, prefetch_next)
+
+    def _finish_iteration(self, res, T, t_start, t0, jobs, recs, j0, j1, prefetch_next) -> IterationResult:
         n_claimed, overflow = self.table.stats()   # synchronises the map phase
         if overflow or n_claimed > self.table.cap // 2:
             # grow and redo this rank's map (results with an overflowed table are unusable)
             self.table = ops.HashTable(ops.next_pow2(4 * max(n_claimed, 1)), device=self.device, op=self.op)
+            self._table_capacity = self.table.cap
             self._run_map(jobs, recs, j0, j1)
             n_claimed, overflow = self.table.stats()
         T["map"] = time.time() - t0
+        pipelined = prefetch_next and self.pipeline and self._can_pipeline()
+        if pipelined:
+            self._issue_next_map(jobs, j0, j1)
         t1 = time.time()
         src = self._source()
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
@@ -523,18 +644,19 @@ class SPMDEngine:
             hi, lo, val, rep = self.table.compact((n_claimed, overflow))
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         if self.world > 1:
-            hi, lo, val, rep, src = self._shuffle(hi, lo, val, rep, src, part, failed)
             if fused:
-                n_red = self._reduce_insert(hi, lo, val, rep)
+                rrec, rcounts, src = self._shuffle(hi, lo, val, rep, src, part, failed, raw=True)
+                n_red = self._reduce_insert_received(rrec, rcounts)
                 pend = devmod.finalize_table_device(self.red_table, n_red, src, self.nparts)
             else:
+                hi, lo, val, rep, src = self._shuffle(hi, lo, val, rep, src, part, failed)
                 hi, lo, val, rep = self._reduce(hi, lo, val, rep, src)
                 part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         T["shuffle"] = time.time() - t1
         t2 = time.time()
         if pend is None:
             pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
-        if prefetch_next:
+        if prefetch_next and not pipelined:
             # the tail kernels are queued: start the next iteration's copies
             self._prefetch(jobs, j0, j1)
         cols = devmod.finalize_host(pend, self.partmod)

@@ -175,11 +175,23 @@ _POOL = _PinnedPool()
 _BLOB_EST: dict = {}  # device -> expected key-blob bytes of the next finalize()
 
 
+def dma_to_host(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """Queue a device -> pinned-host DMA of ``src`` into ``dst`` on the current
+    stream (direct hipMemcpyAsync: torch's non_blocking copy_ also records an
+    event for the pinned block in its host allocator on every call, and that
+    event pool's growth stalled the host for ~5 ms now and then)."""
+    from ..ops import _hip
+    assert src.is_contiguous() and dst.is_contiguous() and dst.numel() * dst.element_size() >= \
+        src.numel() * src.element_size()
+    _hip.call("mr_memcpy_async", _hip.ptr(dst), _hip.ptr(src), src.numel() * src.element_size(), 2,
+              _hip.stream(src.device))
+
+
 def _to_host(t: torch.Tensor, name: str) -> torch.Tensor:
     if not t.is_cuda:
         return t
     h = _POOL.get(name, t.numel(), t.dtype)
-    h.copy_(t, non_blocking=True)
+    dma_to_host(h, t.contiguous())
     return h
 
 
@@ -229,7 +241,7 @@ def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, p
         # last time's size; the rare overflow is topped up after the sync
         est = min(est, blob.numel())
         hb = _POOL.get("blob", max(est, 1 << 16), torch.uint8)
-        hb[:est].copy_(blob[:est], non_blocking=True)
+        dma_to_host(hb[:est], blob[:est])
     else:
         hb = _POOL.get("blob", max(1 << 20, 16 * n), torch.uint8)
         ops.copy_to_host(blob, hb, off[n:])  # size read on the device: no sync before the copy
@@ -271,12 +283,12 @@ def finalize_table_device(table, n: int, src, nparts: int) -> dict:
     _hip.call("mr_tail_pack", _hip.ptr(val), _hip.ptr(off), n, _hip.ptr(pcount), nparts, _hip.ptr(bad),
               _hip.ptr(packed), s)
     hp = _POOL.get("pack", nb, torch.uint8)
-    hp.copy_(packed, non_blocking=True)
+    dma_to_host(hp, packed)
     est = _BLOB_EST.get(d)
     if est is not None:
         est = min(est, blob.numel())
         hb = _POOL.get("blob", max(est, 1 << 16), torch.uint8)
-        hb[:est].copy_(blob[:est], non_blocking=True)
+        dma_to_host(hb[:est], blob[:est])
     else:
         hb = _POOL.get("blob", max(1 << 20, 16 * n), torch.uint8)
         ops.copy_to_host(blob, hb, off[n:])

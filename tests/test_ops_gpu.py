@@ -259,11 +259,23 @@ def test_spmd_prefetch_pipelined_iterations_match(gpu):
     eng = SPMDEngine(params, device=gpu, split_store=SplitStore(splits))
     ref = eng.run_iteration()
     ref_total, ref_keys = ref.total_value, ref.distinct_keys
+    from lua_mapreduce_1_amd.runtime import codec
+    want = {k: v[0] for _n, cols in eng.gather_results(ref) for k, v in codec.iter_columnar(cols)}
+    assert sum(want.values()) == 400_000
     eng.prefetch = True
     for i in range(5):
         r = eng.run_iteration(prefetch_next=i < 4)
         assert r.total_value == ref_total == 400_000 and r.distinct_keys == ref_keys
     assert eng._prefetched is None
+    # pipelined: the next iteration's map is queued on the other stream/table
+    # while this one finalizes; every result is identical to the reference
+    eng.pipeline = True
+    for i in range(6):
+        r = eng.run_iteration(prefetch_next=i < 5)
+        assert r.total_value == ref_total and r.distinct_keys == ref_keys
+        got = {k: v[0] for _n, cols in eng.gather_results(r) for k, v in codec.iter_columnar(cols)}
+        assert got == want
+    assert eng._pending is None and eng._prefetched is None
 
 
 @pytest.mark.parametrize("W", [1, 3, 8])

@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, on_gpu=False):
+def _worker(rank, world, port, q, on_gpu=False, pipelined=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import torch.distributed as dist
@@ -35,7 +35,13 @@ def _worker(rank, world, port, q, on_gpu=False):
                      split_store=store, device=device)
     if on_gpu:
         assert eng.table.is_cuda
-    res = eng.run()
+    if pipelined:  # iteration i+1's copies and map overlap iteration i's shuffle/reduce
+        eng.prefetch = eng.pipeline = True
+        for i in range(4):
+            res = eng.run_iteration(prefetch_next=i < 3)
+        assert eng._pending is None
+    else:
+        res = eng.run()
     owned = sorted(res.partitions)
     assert all(p % world == rank for p in owned)
     gathered = eng.gather_results(res)
@@ -71,14 +77,15 @@ def test_spmd_gloo_wordcount(world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
-def test_spmd_multirank_on_one_gpu(world):
+@pytest.mark.parametrize("world,pipelined", [(2, False), (4, False), (3, True)])
+def test_spmd_multirank_on_one_gpu(world, pipelined):
     """Several ranks share the GPU (gloo carries the collectives through host
-    copies): exercises the device shuffle/reduce/finalize kernels at W > 1."""
+    copies): exercises the device shuffle/reduce/finalize kernels at W > 1,
+    also with pipelined iterations (next map on a second stream)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, True)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, True, pipelined)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

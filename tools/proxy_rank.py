@@ -38,8 +38,9 @@ def main() -> int:
                   init_args={"nsplits": k, "num_reducers": 10})
     eng = SPMDEngine(params, device=device, split_store=store)
     eng.prefetch = not a.no_prefetch
-    for _ in range(a.warmup):
-        eng.run_iteration()
+    eng.pipeline = os.environ.get("MR_PIPELINE", "1") != "0"
+    for w in range(a.warmup):
+        eng.run_iteration(prefetch_next=w < a.warmup - 1)
     torch.cuda.synchronize()
     if a.freeze:
         import gc
@@ -47,9 +48,9 @@ def main() -> int:
         gc.freeze()
     per = []
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
         t1 = time.perf_counter()
-        res = eng.run_iteration()
+        res = eng.run_iteration(prefetch_next=i < a.steps - 1)
         per.append(1000 * (time.perf_counter() - t1))
     torch.cuda.synchronize()
     ms = 1000 * (time.perf_counter() - t0) / a.steps

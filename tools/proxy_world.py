@@ -36,17 +36,29 @@ def main() -> int:
     splits = load_corpus(1234, 0, 0, 1, device)
     store = S.SplitStore(splits)
     W = a.world
-    # loopback collectives
-    D.exchange_counts = lambda counts, group=None: counts.clone()
-    D.all_to_all_v = lambda payload, send, recv, group=None: payload[:sum(recv)].clone()
+    # loopback collectives: every peer sends this rank what this rank sends to
+    # rank 0 (its own partitions) — the received volume and the distinct keys
+    # after the reduce are those of a real rank of a W-rank job
+    def exchange_counts(counts, group=None):
+        c = counts.view(W, 3)
+        return c[0:1].expand(W, 3).reshape(-1).clone()
+
+    def all_to_all_v(payload, send, recv, group=None):
+        return payload[:send[0]].repeat((W,) + (1,) * (payload.dim() - 1))
+    D.exchange_counts = exchange_counts
+    D.all_to_all_v = all_to_all_v
     S.D.world_info = lambda group=None: (0, W)
     params = dict(taskfn=MODEL, mapfn=MODEL, partitionfn=MODEL, reducefn=MODEL, finalfn=MODEL,
                   init_args={"nsplits": len(store), "num_reducers": 10})
     eng = S.SPMDEngine(params, device=device, split_store=store)
     assert eng.world == W and eng.rank == 0
     eng.prefetch = True
-    for _ in range(a.warmup):
-        eng.run_iteration()
+    eng.pipeline = os.environ.get("MR_PIPELINE", "1") != "0"
+    for w in range(a.warmup):
+        eng.run_iteration(prefetch_next=w < a.warmup - 1)
+    import gc
+    gc.collect()
+    gc.freeze()
     torch.cuda.synchronize()
     per = []
     t0 = time.perf_counter()
@@ -54,6 +66,8 @@ def main() -> int:
         t1 = time.perf_counter()
         res = eng.run_iteration(prefetch_next=i < a.steps - 1)
         per.append(1000 * (time.perf_counter() - t1))
+        if os.environ.get("MR_PHASES") and i < 3:
+            print(i, {k: round(1000 * v, 3) for k, v in res.timings.items()}, file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     ms = 1000 * (time.perf_counter() - t0) / a.steps
     seq = [round(x, 2) for x in per]
