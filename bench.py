@@ -96,7 +96,7 @@ def main() -> int:
     # the last warm-up step starts nothing for the next one: every copy and map
     # of the K timed iterations happens inside the timed region
     for w in range(args.warmup):
-        eng.run_iteration(prefetch_next=w < args.warmup - 1)
+        eng.run_iteration(prefetch_next=w < args.warmup - 1, lookahead=args.warmup - 1 - w)
     # long-lived objects (modules, corpus, engine) move to the permanent GC
     # generation: a full collection over them stalled an iteration by ~5 ms
     # every few dozen iterations (the per-iteration host work is ~1 ms at 8 GPUs)
@@ -108,7 +108,7 @@ def main() -> int:
     t0 = time.perf_counter()
     last = None
     for i in range(args.steps):
-        last = eng.run_iteration(prefetch_next=i < args.steps - 1)
+        last = eng.run_iteration(prefetch_next=i < args.steps - 1, lookahead=args.steps - 1 - i)
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     D.barrier(device=device)

@@ -42,6 +42,9 @@ from ..utils import STATUS
 from . import dist as D
 
 
+N_ARENAS = 3
+
+
 class _nullctx:
     def __enter__(self):
         return None
@@ -176,11 +179,15 @@ class SPMDEngine:
         self._table_capacity = table_capacity
         self.tables: list = [ops.HashTable(table_capacity, device=self.device, op=self.op), None]
         self.red_table: ops.HashTable | None = None
-        # two input arenas: iteration i maps arenas[slot] while the copies of
-        # iteration i+1 (prefetch) fill the other one
-        self.arenas: list = [None, None]
-        self.slot = 0
-        self._prefetched = None
+        # input arenas, used round-robin by iteration sequence number q: while
+        # iteration q maps/reduces arenas[q % 3], the copies of q+1 and q+2
+        # (prefetch, up to two ahead) fill the other two, so the copy engine
+        # streams without pause; tables and streams alternate by q % 2
+        self.arenas: list = [None] * N_ARENAS
+        self.slot = 0   # arena of the iteration being run / issued
+        self.tslot = 0  # its table and stream
+        self._seq = 0   # sequence number of the next iteration
+        self._inflight: dict = {}  # arena slot -> plan key of copies issued ahead
         self.prefetch = False
         # iteration pipelining (needs prefetch): the next iteration's map is
         # queued on the other slot's stream as soon as this map has finished,
@@ -251,14 +258,18 @@ class SPMDEngine:
 
     @property
     def table(self) -> ops.HashTable:
-        t = self.tables[self.slot]
+        t = self.tables[self.tslot]
         if t is None:
-            t = self.tables[self.slot] = ops.HashTable(self._table_capacity, device=self.device, op=self.op)
+            t = self.tables[self.tslot] = ops.HashTable(self._table_capacity, device=self.device, op=self.op)
         return t
 
     @table.setter
     def table(self, t: ops.HashTable) -> None:
-        self.tables[self.slot] = t
+        self.tables[self.tslot] = t
+
+    def _use(self, q: int) -> None:
+        """Make iteration q's arena, table and stream current."""
+        self.slot, self.tslot = q % N_ARENAS, q % 2
 
     def _plan_chunks(self, ids: list[int], slot: int):
         """Chunking of a contiguous split range (cached per range): boundaries
@@ -347,23 +358,22 @@ class SPMDEngine:
             raise ValueError("split jobs of a rank must be contiguous splits")
         return ids
 
-    def _prefetch(self, jobs, j0, j1) -> None:
-        """Start the next iteration's host->HBM copies (same splits) into the
-        other arena now, so the copy engine keeps streaming while this
-        iteration reduces and finalizes.  Only for a pure taskfn (the next job
-        list is known) and split inputs; a mismatching next plan is re-copied."""
-        if (self.copy_stream is None or self.device_input != "split"
-                or not modules.field(self.taskfn, "spmd_replicated_taskfn")):
+    def _prefetch(self, jobs, j0, j1, q: int) -> None:
+        """Start iteration q's host->HBM copies (same splits: the taskfn is
+        pure) into its arena now, so the copy engine keeps streaming while
+        earlier iterations map, reduce and finalize.  Only for a pure taskfn
+        and split inputs; a mismatching plan is re-copied when q runs."""
+        if not self._can_pipeline():
             return
+        aslot = q % N_ARENAS
         ids = self._split_ids(jobs, j0, j1)
-        if not ids:
+        if not ids or aslot in self._inflight:
             return
-        nslot = 1 - self.slot
-        plan = self._get_plan(ids, nslot)
-        # arenas[nslot] was last read by the previous iteration, which has
+        plan = self._get_plan(ids, aslot)
+        # arenas[aslot] was last read by iteration q - N_ARENAS, which has
         # completed (its finalize synchronised): no stream dependency needed
         self._issue_copies(plan)
-        self._prefetched = (ids[0], len(ids), nslot)
+        self._inflight[aslot] = (ids[0], len(ids))
 
     def _stage_chunks(self, jobs, j0, j1):
         """Yield (job index range, device tensor) chunks, H2D overlapped with compute."""
@@ -371,16 +381,12 @@ class SPMDEngine:
             ids = self._split_ids(jobs, j0, j1)
             if not ids:
                 return
-            key = (ids[0], len(ids), self.slot)
             plan = self._get_plan(ids, self.slot)
             bounds, views, host_views, events = plan
             cs = self.copy_stream
             if cs is not None:
                 cur = torch.cuda.current_stream(self.device)
-                if self._prefetched == key:
-                    self._prefetched = None  # copies already in flight (prefetch)
-                else:
-                    self._prefetched = None
+                if self._inflight.pop(self.slot, None) != (ids[0], len(ids)):  # else: prefetched, in flight
                     self._issue_copies(plan, wait_for=cur)
                 # chunks whose copies have already landed (prefetched during the
                 # previous iteration's tail) are mapped by ONE launch: a launch's
@@ -561,62 +567,63 @@ class SPMDEngine:
         return (self.copy_stream is not None and self.device_input == "split"
                 and bool(modules.field(self.taskfn, "spmd_replicated_taskfn")))
 
-    def _issue_next_map(self, jobs, j0, j1) -> None:
-        """Queue the NEXT iteration's input copies and map (same job list: the
-        taskfn is pure) on the other slot — its arena, table and stream — and
-        return to this iteration's slot.  Both were last used by the previous
-        iteration, which has fully completed (its results were downloaded)."""
-        cur = self.slot
-        nxt = 1 - cur
-        if self._prefetched is None or self._prefetched[2] != nxt:
-            self._prefetch(jobs, j0, j1)
+    def _issue_next_map(self, jobs, j0, j1, q: int) -> None:
+        """Queue iteration q+1's map (same job list: the taskfn is pure) on its
+        own arena, table and stream, then return to iteration q's.  Its table
+        and stream were last used by iteration q-1, which has fully completed
+        (its results were downloaded)."""
+        self._prefetch(jobs, j0, j1, q + 1)
         recs = [JobRecord(k, v) for k, v in jobs]
-        self.slot = nxt
+        self._use(q + 1)
         try:
-            with torch.cuda.stream(self.streams[nxt]):
+            with torch.cuda.stream(self.streams[self.tslot]):
                 self.table.reset()
                 t0 = time.time()
                 self._run_map(jobs, recs, j0, j1)
         finally:
-            self.slot = cur
-        self._pending = {"slot": nxt, "jobs": jobs, "recs": recs, "j0": j0, "j1": j1, "t0": t0}
+            self._use(q)
+        self._pending = {"q": q + 1, "jobs": jobs, "recs": recs, "j0": j0, "j1": j1, "t0": t0}
 
-    def run_iteration(self, prefetch_next: bool | None = None) -> IterationResult:
+    def run_iteration(self, prefetch_next: bool | None = None, lookahead: int | None = None) -> IterationResult:
         """One MapReduce iteration.  ``prefetch_next`` (default ``self.prefetch``)
-        starts the next iteration's input copies as soon as this map is done;
-        with ``self.pipeline`` it also queues the next iteration's map then."""
+        starts the input copies of the next ``lookahead`` (default 2, at most
+        N_ARENAS - 1) iterations as soon as their arenas are free; with
+        ``self.pipeline`` the next iteration's map is also queued as soon as
+        this map is done.  ``prefetch_next=False`` starts nothing ahead."""
         self.iteration += 1
         if prefetch_next is None:
             prefetch_next = self.prefetch
+        ahead = 0 if not prefetch_next else (N_ARENAS - 1 if lookahead is None else min(lookahead, N_ARENAS - 1))
+        q = self._seq
+        self._seq += 1
+        self._use(q)
         res = IterationResult()
         T = res.timings
         t_start = time.time()
         pending, self._pending = self._pending, None
         if pending is not None:  # this iteration's map was queued by the previous one
-            self.slot = pending["slot"]
+            assert pending["q"] == q
             jobs, recs, j0, j1, t0 = pending["jobs"], pending["recs"], pending["j0"], pending["j1"], pending["t0"]
-            stream = self.streams[self.slot]
-            if prefetch_next and self.pipeline:
-                # the other arena is free (the previous iteration completed):
-                # keep the copy engine streaming — the next input's copies
-                # queue behind this one's right away
-                self._prefetch(jobs, j0, j1)
+            stream = self.streams[self.tslot]
         else:
-            if self._prefetched is not None:
-                self.slot = self._prefetched[2]
             jobs = self._jobs()
             recs = [JobRecord(k, v) for k, v in jobs]
             j0, j1 = self._assign(jobs)
-            stream = None
+            stream = self.streams[self.tslot] if ahead and self.pipeline else None
         res.map_jobs = recs
         with torch.cuda.stream(stream) if stream is not None else _nullctx():
             if pending is None:
                 self.table.reset()
                 t0 = time.time()
                 self._run_map(jobs, recs, j0, j1)
-            return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, prefetch_next)
+            # the arenas of q+1..q+ahead are free (iterations up to q-1
+            # completed): their copies queue behind this iteration's (the
+            # copy stream is FIFO), so the copy engine never idles
+            for k in range(1, ahead + 1):
+                self._prefetch(jobs, j0, j1, q + k)
+            return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, ahead > 0, q)
 
-    def _finish_iteration(self, res, T, t_start, t0, jobs, recs, j0, j1, prefetch_next) -> IterationResult:
+    def _finish_iteration(self, res, T, t_start, t0, jobs, recs, j0, j1, prefetch_next, q) -> IterationResult:
         n_claimed, overflow = self.table.stats()   # synchronises the map phase
         if overflow or n_claimed > self.table.cap // 2:
             # grow and redo this rank's map (results with an overflowed table are unusable)
@@ -627,7 +634,7 @@ class SPMDEngine:
         T["map"] = time.time() - t0
         pipelined = prefetch_next and self.pipeline and self._can_pipeline()
         if pipelined:
-            self._issue_next_map(jobs, j0, j1)
+            self._issue_next_map(jobs, j0, j1, q)
         t1 = time.time()
         src = self._source()
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
@@ -656,9 +663,7 @@ class SPMDEngine:
         t2 = time.time()
         if pend is None:
             pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
-        if prefetch_next and not pipelined:
-            # the tail kernels are queued: start the next iteration's copies
-            self._prefetch(jobs, j0, j1)
+
         cols = devmod.finalize_host(pend, self.partmod)
         digits = len(str(max(self.nparts - 1, 0)))
         for p in range(self.nparts):

@@ -264,18 +264,18 @@ def test_spmd_prefetch_pipelined_iterations_match(gpu):
     assert sum(want.values()) == 400_000
     eng.prefetch = True
     for i in range(5):
-        r = eng.run_iteration(prefetch_next=i < 4)
+        r = eng.run_iteration(prefetch_next=i < 4, lookahead=4 - i)
         assert r.total_value == ref_total == 400_000 and r.distinct_keys == ref_keys
-    assert eng._prefetched is None
+    assert not eng._inflight
     # pipelined: the next iteration's map is queued on the other stream/table
     # while this one finalizes; every result is identical to the reference
     eng.pipeline = True
     for i in range(6):
-        r = eng.run_iteration(prefetch_next=i < 5)
+        r = eng.run_iteration(prefetch_next=i < 5, lookahead=5 - i)
         assert r.total_value == ref_total and r.distinct_keys == ref_keys
         got = {k: v[0] for _n, cols in eng.gather_results(r) for k, v in codec.iter_columnar(cols)}
         assert got == want
-    assert eng._pending is None and eng._prefetched is None
+    assert eng._pending is None and not eng._inflight
 
 
 @pytest.mark.parametrize("W", [1, 3, 8])

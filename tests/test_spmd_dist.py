@@ -38,8 +38,8 @@ def _worker(rank, world, port, q, on_gpu=False, pipelined=False):
     if pipelined:  # iteration i+1's copies and map overlap iteration i's shuffle/reduce
         eng.prefetch = eng.pipeline = True
         for i in range(4):
-            res = eng.run_iteration(prefetch_next=i < 3)
-        assert eng._pending is None
+            res = eng.run_iteration(prefetch_next=i < 3, lookahead=3 - i)
+        assert eng._pending is None and not eng._inflight
     else:
         res = eng.run()
     owned = sorted(res.partitions)

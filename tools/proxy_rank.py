@@ -40,7 +40,7 @@ def main() -> int:
     eng.prefetch = not a.no_prefetch
     eng.pipeline = os.environ.get("MR_PIPELINE", "1") != "0"
     for w in range(a.warmup):
-        eng.run_iteration(prefetch_next=w < a.warmup - 1)
+        eng.run_iteration(prefetch_next=w < a.warmup - 1, lookahead=a.warmup - 1 - w)
     torch.cuda.synchronize()
     if a.freeze:
         import gc
@@ -50,7 +50,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for i in range(a.steps):
         t1 = time.perf_counter()
-        res = eng.run_iteration(prefetch_next=i < a.steps - 1)
+        res = eng.run_iteration(prefetch_next=i < a.steps - 1, lookahead=a.steps - 1 - i)
         per.append(1000 * (time.perf_counter() - t1))
     torch.cuda.synchronize()
     ms = 1000 * (time.perf_counter() - t0) / a.steps

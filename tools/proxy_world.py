@@ -55,7 +55,7 @@ def main() -> int:
     eng.prefetch = True
     eng.pipeline = os.environ.get("MR_PIPELINE", "1") != "0"
     for w in range(a.warmup):
-        eng.run_iteration(prefetch_next=w < a.warmup - 1)
+        eng.run_iteration(prefetch_next=w < a.warmup - 1, lookahead=a.warmup - 1 - w)
     import gc
     gc.collect()
     gc.freeze()
@@ -64,7 +64,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for i in range(a.steps):
         t1 = time.perf_counter()
-        res = eng.run_iteration(prefetch_next=i < a.steps - 1)
+        res = eng.run_iteration(prefetch_next=i < a.steps - 1, lookahead=a.steps - 1 - i)
         per.append(1000 * (time.perf_counter() - t1))
         if os.environ.get("MR_PHASES") and i < 3:
             print(i, {k: round(1000 * v, 3) for k, v in res.timings.items()}, file=sys.stderr, flush=True)
