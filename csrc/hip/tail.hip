@@ -189,4 +189,107 @@ int mr_tail_pack(const void* val, const void* off, u64 n, const void* counts, u3
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// The whole fused tail in ONE host call: every launch and both downloads are
+// queued from C++ instead of ~20 Python-level calls and tensor allocations per
+// iteration (at 8-GPU strong scaling the per-iteration host time was a large
+// part of the ~1 ms step).  All buffers live in one caller-owned workspace
+// (layout below, mr_tail_ws_layout), reused across iterations; the
+// decoupled-look-back granules of its sort are its own (own epoch counter).
+
+int mr_exclusive_scan_i64(const void* in, void* out, u64 n, void* partials, void* total, hipStream_t s);
+u64 mr_scan_partials_len(u64 n);
+int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
+                           const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
+                           hipStream_t s);
+int mr_tie_fixup(const void* c, void* hi, void* lo, void* val, void* rep, void* part, u64 n, void* bad,
+                 const void* src, void* ln, hipStream_t s);
+int mr_gather_key_bytes(const void* hi, const void* lo, const void* rep, const void* off, u64 n, const void* src,
+                        void* dst, hipStream_t stream);
+int mr_copy_to_host(const void* src, void* host_dst, const void* nelem, u64 elem_size, u64 max_bytes, hipStream_t s);
+
+enum TailBuf : int {
+  TB_HI0, TB_LO0, TB_VAL0, TB_REP0, TB_C, TB_PART0, TB_ZERO /* counter|ghist|pcount|sort ctrs|err|bad */,
+  TB_K0, TB_K1, TB_P0, TB_P1, TB_GRAN, TB_HI, TB_LO, TB_VAL, TB_REP, TB_PART, TB_LN, TB_OFF, TB_PARTIALS,
+  TB_BLOB, TB_PACKED, TB_COUNT
+};
+// TB_ZERO sub-layout (bytes): counter u64 @0 | ghist u32[2048] @8 | pcount i64[256] @8200 |
+// sort tile counters u32[64] @10248 | sort err u32 @10504 | bad u32 @10508
+constexpr u64 TZ_GHIST = 8, TZ_PCOUNT = 8200, TZ_TILES = 10248, TZ_ERR = 10504, TZ_BAD = 10508, TZ_BYTES = 10512;
+
+u64 mr_tail_ws_layout(u64 n, u32 nparts, u64 blob_cap, u64* off) {
+  (void)nparts;
+  const u64 m = n ? n : 1;
+  const u64 tiles = (m + 4095) / 4096;
+  const u64 sz[TB_COUNT] = {8 * m, 8 * m, 8 * m, 8 * m, 8 * m, 4 * m, TZ_BYTES, 8 * m, 8 * m, 4 * m, 4 * m,
+                            tiles * 256 * 8, 8 * m, 8 * m, 8 * m, 8 * m, 4 * m, 8 * m, 8 * (m + 1),
+                            8 * mr_scan_partials_len(m), blob_cap ? blob_cap : 1, mr_tail_pack_bytes(m, 256)};
+  u64 o = 0;
+  for (int i = 0; i < TB_COUNT; ++i) {
+    off[i] = o;
+    o += (sz[i] + 255) & ~255ull;
+  }
+  return o;
+}
+
+static u32 g_tail_epoch = 0;
+
+// n = occupied slots of the table; src = the key-byte source (map arena or the
+// received blob); hp / hb = pinned host buffers of the packed columns and the
+// key bytes; est >= 0: DMA min(est, hb_cap) key bytes, else a device-sized copy.
+int mr_tail_run(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, u64 n, u32 nparts,
+                const void* src, void* ws, u64 blob_cap, void* hp, void* hb, long long est, u64 hb_cap,
+                hipStream_t s) {
+  if (nparts > 256) return -1;
+  u64 off[TB_COUNT];
+  mr_tail_ws_layout(n, nparts, blob_cap, off);
+  u8* w = (u8*)ws;
+  auto P = [&](int b) { return (void*)(w + off[b]); };
+  u8* z = w + off[TB_ZERO];
+  int rc = (int)hipMemsetAsync(z, 0, TZ_BYTES, s);
+  if (rc) return rc;
+  rc = mr_tail_compact(tag, hi, lo, val, rep, ctrl, cap, nparts, src, P(TB_HI0), P(TB_LO0), P(TB_VAL0), P(TB_REP0),
+                       P(TB_PART0), P(TB_C), z, z + TZ_GHIST, z + TZ_PCOUNT, s);
+  if (rc) return rc;
+  // 8 onesweep passes over the composite key (ghist from tail_compact)
+  const void* kin = P(TB_C);
+  const void* pin = nullptr;
+  for (int pass = 0; pass < 8; ++pass) {
+    g_tail_epoch = (g_tail_epoch + 1) & 0xFFFFFFu;
+    if (!g_tail_epoch) g_tail_epoch = 1;
+    void* kout = P(pass & 1 ? TB_K1 : TB_K0);
+    void* pout = P(pass & 1 ? TB_P1 : TB_P0);
+    rc = mr_radix_onesweep_u32v(kin, pin, kout, pout, n, 8 * pass, z + TZ_GHIST + 4 * 256 * pass, P(TB_GRAN),
+                                z + TZ_TILES + 4 * pass, g_tail_epoch, z + TZ_ERR, pass == 0 ? 1 : 0, s);
+    if (rc) return rc;
+    kin = kout;
+    pin = pout;
+  }
+  rc = mr_tail_gather(pin, n, P(TB_HI0), P(TB_LO0), P(TB_VAL0), P(TB_REP0), P(TB_PART0), P(TB_HI), P(TB_LO),
+                      P(TB_VAL), P(TB_REP), P(TB_PART), P(TB_LN), s);
+  if (rc) return rc;
+  rc = mr_tie_fixup(kin, P(TB_HI), P(TB_LO), P(TB_VAL), P(TB_REP), P(TB_PART), n, z + TZ_BAD, src, P(TB_LN), s);
+  if (rc) return rc;
+  long long* offs = (long long*)P(TB_OFF);
+  if (n) {
+    rc = mr_exclusive_scan_i64(P(TB_LN), offs, n, P(TB_PARTIALS), offs + n, s);
+  } else {
+    rc = (int)hipMemsetAsync(offs, 0, 8, s);
+  }
+  if (rc) return rc;
+  rc = mr_gather_key_bytes(P(TB_HI), P(TB_LO), P(TB_REP), offs, n, src, P(TB_BLOB), s);
+  if (rc) return rc;
+  rc = mr_tail_pack(P(TB_VAL), offs, n, z + TZ_PCOUNT, nparts, z + TZ_BAD, P(TB_PACKED), s);
+  if (rc) return rc;
+  rc = (int)hipMemcpyAsync(hp, P(TB_PACKED), mr_tail_pack_bytes(n, nparts), hipMemcpyDeviceToHost, s);
+  if (rc) return rc;
+  if (est >= 0) {
+    const u64 nb = (u64)est < hb_cap ? (u64)est : hb_cap;
+    if (nb) rc = (int)hipMemcpyAsync(hb, P(TB_BLOB), nb < blob_cap ? nb : blob_cap, hipMemcpyDeviceToHost, s);
+  } else {
+    rc = mr_copy_to_host(P(TB_BLOB), hb, offs + n, 1, hb_cap, s);
+  }
+  return rc;
+}
+
 }  // extern "C"

@@ -30,6 +30,7 @@ _SIGS = {
     "mr_wc_map3": [_p, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
     "mr_insert_received": [_p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p, _u64, _i32, _p],
     "mr_memcpy_async": [_p, _p, _u64, _i32, _p],
+    "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64, _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
     "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p],
     "mr_table_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
@@ -75,11 +76,12 @@ _SIGS = {
     "mr_tail_gather": [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "mr_tail_pack": [_p, _p, _u64, _p, _u32, _p, _p, _p],
     "mr_tail_pack_bytes": [_u64, _u32],
+    "mr_tail_ws_layout": [_u64, _u32, _u64, ctypes.POINTER(ctypes.c_uint64)],
     "mr_table_reset": [_p, _p, _p, _p, _u64, ctypes.c_longlong, _p],
     "mr_scan_partials_len": [_u64],
     "mr_rs_tiles": [_u64],
 }
-_RESTYPE_U64 = {"mr_scan_partials_len", "mr_rs_tiles", "mr_tail_pack_bytes"}
+_RESTYPE_U64 = {"mr_scan_partials_len", "mr_rs_tiles", "mr_tail_pack_bytes", "mr_tail_ws_layout"}
 
 
 def lib():

@@ -494,6 +494,13 @@ class SPMDEngine:
         return (self.device.type == "cuda" and spec is not None and spec[0] == "fnv1"
                 and self.nparts <= 256 and os.environ.get("MR_FUSED_TAIL", "1") != "0")
 
+    def _finalize_table(self, table, n: int, src) -> dict:
+        """The fused device tail of a table: one native call (mr_tail_run) by
+        default, the Python-sequenced launches with MR_NATIVE_TAIL=0."""
+        if os.environ.get("MR_NATIVE_TAIL", "1") != "0":
+            return devmod.finalize_table_native(table, n, src, self.nparts)
+        return devmod.finalize_table_device(table, n, src, self.nparts)
+
     def _reduce_insert_received(self, rrec, recv_counts) -> int:
         """Received records -> this rank's reduce table (one insert launch);
         returns its key count.  The table is sized from the previous
@@ -646,7 +653,7 @@ class SPMDEngine:
             # -> downloads) is one replayed hipGraph once a table size repeats
             pend = self._graphed_tail(n_claimed, overflow, src)
         elif self.world == 1 and fused:
-            pend = devmod.finalize_table_device(self.table, n_claimed, src, self.nparts)
+            pend = self._finalize_table(self.table, n_claimed, src)
         else:
             hi, lo, val, rep = self.table.compact((n_claimed, overflow))
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
@@ -654,7 +661,7 @@ class SPMDEngine:
             if fused:
                 rrec, rcounts, src = self._shuffle(hi, lo, val, rep, src, part, failed, raw=True)
                 n_red = self._reduce_insert_received(rrec, rcounts)
-                pend = devmod.finalize_table_device(self.red_table, n_red, src, self.nparts)
+                pend = self._finalize_table(self.red_table, n_red, src)
             else:
                 hi, lo, val, rep, src = self._shuffle(hi, lo, val, rep, src, part, failed)
                 hi, lo, val, rep = self._reduce(hi, lo, val, rep, src)

@@ -296,6 +296,62 @@ def finalize_table_device(table, n: int, src, nparts: int) -> dict:
             "lo": lo, "fused": True, "hp": hp, "off": off, "blob": blob, "est": est, "hb": hb}
 
 
+_TAIL_WS: dict = {}  # device -> (workspace uint8 tensor, {layout key: (offsets, views)})
+_TB = {name: i for i, name in enumerate(
+    "HI0 LO0 VAL0 REP0 C PART0 ZERO K0 K1 P0 P1 GRAN HI LO VAL REP PART LN OFF PARTIALS BLOB PACKED".split())}
+
+
+def _tail_ws(d, n: int, nparts: int, blob_cap: int):
+    """Workspace of mr_tail_run (csrc/hip/tail.hip) and int64 views of the
+    buffers the host half reads, cached per (n, nparts, blob capacity)."""
+    import ctypes
+    from ..ops import _hip
+    lib = _hip.lib()
+    offs = (ctypes.c_uint64 * len(_TB))()
+    need = int(lib.mr_tail_ws_layout(ctypes.c_uint64(n), ctypes.c_uint32(nparts), ctypes.c_uint64(blob_cap), offs))
+    ws, views = _TAIL_WS.get(d, (None, {}))
+    if ws is None or ws.numel() < need:
+        ws = torch.zeros(need + need // 4, dtype=torch.uint8, device=d)  # zeroed once: sort look-back granules
+        views = {}
+    key = (n, nparts, blob_cap)
+    v = views.get(key)
+    if v is None:
+        o = list(offs)
+        m = max(n, 1)
+        i64 = lambda b, k: ws[o[_TB[b]]:o[_TB[b]] + 8 * k].view(torch.int64)  # noqa: E731
+        v = {"args": tuple(i64(b, n) for b in ("HI0", "LO0", "VAL0", "REP0")), "hi": i64("HI", n), "lo": i64("LO", n),
+             "off": i64("OFF", m + 1), "blob": ws[o[_TB["BLOB"]]:o[_TB["BLOB"]] + max(blob_cap, 1)]}
+        if len(views) > 8:
+            views.clear()
+        views[key] = v
+    _TAIL_WS[d] = (ws, views)
+    return ws, v
+
+
+def finalize_table_native(table, n: int, src, nparts: int) -> dict:
+    """finalize_table_device with every launch and download queued by ONE
+    native call (mr_tail_run): same kernels, same packed download, same
+    pending-state contract for finalize_host."""
+    from ..ops import _hip
+    d = table.device
+    cap = src.numel()
+    ws, v = _tail_ws(d, n, nparts, cap)
+    nb = int(_hip.lib().mr_tail_pack_bytes(n, nparts))
+    hp = _POOL.get("pack", nb, torch.uint8)
+    est = _BLOB_EST.get(d)
+    if est is not None:
+        est = min(est, cap)
+        hb = _POOL.get("blob", max(est, 1 << 16), torch.uint8)
+        est_arg = est
+    else:
+        hb = _POOL.get("blob", max(1 << 20, 16 * n), torch.uint8)
+        est_arg = -1
+    _hip.call("mr_tail_run", *table._gtab(), table.cap, n, nparts, _hip.ptr(src), _hip.ptr(ws), cap, _hip.ptr(hp),
+              _hip.ptr(hb), est_arg, hb.numel(), _hip.stream(d))
+    return {"n": n, "nparts": nparts, "args": v["args"], "src": src, "presorted": False, "hi": v["hi"], "lo": v["lo"],
+            "fused": True, "hp": hp, "off": v["off"], "blob": v["blob"], "est": est, "hb": hb}
+
+
 def _unpack_fused(pend: dict):
     """(val int64[n], off int32[n+1], counts int64[nparts], bad) views of the packed download."""
     n, nparts = pend["n"], pend["nparts"]

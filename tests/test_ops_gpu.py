@@ -327,6 +327,14 @@ def test_fused_tail_matches_unfused(gpu, nparts):
     n, _ = tab.stats()
     a = dv.finalize_host(dv.finalize_table_device(tab, n, t, nparts))
     a = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in a.items()}
+    # the one-call native tail (mr_tail_run) gives the same columns, twice
+    # (the second run reuses its cached workspace and the blob-size estimate)
+    for _ in range(2):
+        c = dv.finalize_host(dv.finalize_table_native(tab, n, t, nparts))
+        for key in ("bounds", "val"):
+            assert np.array_equal(a[key], c[key])
+        assert np.array_equal(np.asarray(a["key_off"], np.int64), np.asarray(c["key_off"], np.int64))
+        assert a["key_blob"].tobytes() == c["key_blob"].tobytes()
     hi, lo, val, rep = tab.compact()
     b = dv.finalize(hi, lo, val, rep, t, nparts)
     assert np.array_equal(a["bounds"], b["bounds"])

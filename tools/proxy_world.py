@@ -61,6 +61,11 @@ def main() -> int:
     gc.freeze()
     torch.cuda.synchronize()
     per = []
+    prof = None
+    if os.environ.get("MR_CPROFILE"):
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for i in range(a.steps):
         t1 = time.perf_counter()
@@ -70,6 +75,10 @@ def main() -> int:
             print(i, {k: round(1000 * v, 3) for k, v in res.timings.items()}, file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     ms = 1000 * (time.perf_counter() - t0) / a.steps
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
     seq = [round(x, 2) for x in per]
     per.sort()
     print(json.dumps({"world": W, "ms_per_step": ms, "median": per[len(per) // 2], "min": per[0], "seq": seq,
