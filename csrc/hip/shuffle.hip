@@ -51,22 +51,37 @@ __global__ void __launch_bounds__(T) pk_count_kernel(const u64* __restrict__ lo,
   }
 }
 
-// cnt [2W] -> start [2W] (exclusive scans), cursors zeroed, and the exchange
-// row per destination: xchg[3d] = records, xchg[3d+1] = bytes, xchg[3d+2] = extra.
+// Bytes of destination/source d's segment in the combined layout: its
+// records (32 B each), then its key bytes padded to 8.
+__host__ __device__ __forceinline__ u64 seg_bytes(u64 rows, u64 bytes) { return 32 * rows + ((bytes + 7) & ~7ull); }
+
+// cnt [2W] -> start [2W] = BYTE offsets of destination d's records (start[d])
+// and key bytes (start[W+d]), cursors zeroed, and the exchange row per
+// destination: xchg[3d] = records, xchg[3d+1] = bytes, xchg[3d+2] = extra.
+// Separate layout: records in one array, key bytes in another.  Combined
+// layout: ONE buffer of per-destination segments [records | key bytes], so
+// the payload is a single all_to_all_single.
 __global__ void pk_scan_kernel(const unsigned long long* __restrict__ cnt, u32 W, unsigned long long* __restrict__ start,
-                               unsigned long long* __restrict__ cursor, long long* __restrict__ xchg, long long extra) {
+                               unsigned long long* __restrict__ cursor, long long* __restrict__ xchg, long long extra,
+                               int combined) {
   if (threadIdx.x != 0) return;
   unsigned long long r = 0, b = 0;
   for (u32 d = 0; d < W; ++d) {
-    start[d] = r;
-    start[W + d] = b;
+    if (combined) {
+      start[d] = r;
+      start[W + d] = r + 32 * cnt[d];
+      r += seg_bytes(cnt[d], cnt[W + d]);
+    } else {
+      start[d] = 32 * r;
+      start[W + d] = b;
+      r += cnt[d];
+      b += cnt[W + d];
+    }
     cursor[d] = 0;
     cursor[W + d] = 0;
     xchg[3 * d] = (long long)cnt[d];
     xchg[3 * d + 1] = (long long)cnt[W + d];
     xchg[3 * d + 2] = extra;
-    r += cnt[d];
-    b += cnt[W + d];
   }
 }
 
@@ -76,7 +91,8 @@ __global__ void __launch_bounds__(T) pk_scatter_kernel(const u64* __restrict__ h
                                                        const u8* __restrict__ src,
                                                        const unsigned long long* __restrict__ start,
                                                        unsigned long long* __restrict__ cursor,
-                                                       u64* __restrict__ rec /*[n][4]*/, u8* __restrict__ blob) {
+                                                       u8* __restrict__ rec /*records, byte-addressed*/,
+                                                       u8* __restrict__ blob) {
   __shared__ u32 rc[MAXW];
   __shared__ u32 bc[MAXW];
   __shared__ unsigned long long rbase[MAXW];
@@ -102,13 +118,13 @@ __global__ void __launch_bounds__(T) pk_scatter_kernel(const u64* __restrict__ h
   }
   __syncthreads();
   if (!live) return;
-  const u64 r = start[d] + rbase[d] + rpos;
+  u64* rr = reinterpret_cast<u64*>(rec + start[d] + 32 * (rbase[d] + rpos));
   const u64 boff = bbase[d] + bpos;  // offset inside destination d's byte segment
   const u64 h = hi[i], l = lo[i];
-  rec[4 * r + 0] = h;
-  rec[4 * r + 1] = l;
-  rec[4 * r + 2] = (u64)val[i];
-  rec[4 * r + 3] = make_rep(boff, len);
+  rr[0] = h;
+  rr[1] = l;
+  rr[2] = (u64)val[i];
+  rr[3] = make_rep(boff, len);
   u8* out = blob + start[W + d] + boff;
   if (!key_is_long(l)) {
     for (u32 k = 0; k < len; ++k) out[k] = (u8)packed_byte(h, l, k);
@@ -142,16 +158,24 @@ __global__ void pk_fix_loc_kernel(u64* __restrict__ rec, u64 n, const long long*
 // relative to the received byte blob).  Replaces the column splits, the
 // host-built prefix arrays and their H2D copies, fix_loc and hash_agg.
 constexpr int MAXW_RECV = 1024;
-__global__ void __launch_bounds__(256) pk_insert_received_kernel(const u64* __restrict__ rec, u64 n,
+__global__ void __launch_bounds__(256) pk_insert_received_kernel(const u8* __restrict__ rec, u64 n,
                                                                  const long long* __restrict__ recv, u32 W, GTab g,
-                                                                 int op) {
-  __shared__ long long rstart[MAXW_RECV + 1];
-  __shared__ long long bstart[MAXW_RECV + 1];
+                                                                 int op, int combined) {
+  __shared__ long long rstart[MAXW_RECV + 1];   // first row of source k
+  __shared__ long long rbyte[MAXW_RECV + 1];    // byte offset of source k's records
+  __shared__ long long bstart[MAXW_RECV + 1];   // byte offset of source k's key bytes
   if (threadIdx.x == 0) {  // W is small (ranks of one job): a serial prefix sum
-    long long r = 0, b = 0;
+    long long r = 0, b = 0, seg = 0;
     for (u32 k = 0; k < W; ++k) {
       rstart[k] = r;
-      bstart[k] = b;
+      if (combined) {
+        rbyte[k] = seg;
+        bstart[k] = seg + 32 * recv[3 * k];
+        seg += (long long)seg_bytes((u64)recv[3 * k], (u64)recv[3 * k + 1]);
+      } else {
+        rbyte[k] = 32 * r;
+        bstart[k] = b;
+      }
       r += recv[3 * k];
       b += recv[3 * k + 1];
     }
@@ -168,9 +192,10 @@ __global__ void __launch_bounds__(256) pk_insert_received_kernel(const u64* __re
       if ((long long)i >= rstart[m]) a = m;
       else b = m;
     }
-    const u64 loc = rec[4 * i + 3];
+    const u64* r = reinterpret_cast<const u64*>(rec + rbyte[a] + 32 * (i - (u64)rstart[a]));
+    const u64 loc = r[3];
     const u64 rep = make_rep(rep_off(loc) + (u64)bstart[a], rep_len(loc));
-    claims += gtab_insert(g, rec[4 * i], rec[4 * i + 1], (long long)rec[4 * i + 2], rep, op) == 2;
+    claims += gtab_insert(g, r[0], r[1], (long long)r[2], rep, op) == 2;
   }
   gtab_count_claims(g, claims);
 }
@@ -188,8 +213,11 @@ static inline unsigned pk_grid(u64 n, unsigned cap = 4096) {
 extern "C" {
 
 // ws: 6*W u64 (cnt[2W], start[2W], cursor[2W]); xchg: 3*W int64 (device)
+// combined != 0: rec == blob == one buffer of per-destination [records | key
+// bytes] segments (mr_pack_seg_bytes), sent with a single all-to-all.
 int mr_pack_by_dest(const void* hi, const void* lo, const void* val, const void* rep, const void* part, u64 n, u32 W,
-                    const void* src, void* ws, void* xchg, long long extra, void* rec, void* blob, hipStream_t s) {
+                    const void* src, void* ws, void* xchg, long long extra, void* rec, void* blob, int combined,
+                    hipStream_t s) {
   if (W == 0 || W > (u32)pk::MAXW) return -1;
   unsigned long long* cnt = (unsigned long long*)ws;
   unsigned long long* start = cnt + 2 * W;
@@ -200,20 +228,20 @@ int mr_pack_by_dest(const void* hi, const void* lo, const void* val, const void*
                        (const u64*)rep, (const u32*)part, n, W, cnt);
   }
   hipLaunchKernelGGL(pk::pk_scan_kernel, dim3(1), dim3(64), 0, s, (const unsigned long long*)cnt, W, start, cursor,
-                     (long long*)xchg, extra);
+                     (long long*)xchg, extra, combined);
   if (n) {
     // one record per thread (the per-block reservation needs every key of the
     // block in flight at once): grid = ceil(n / 256), not capped
     const u64 g = (n + pk::T - 1) / pk::T;
     hipLaunchKernelGGL(pk::pk_scatter_kernel, dim3((unsigned)g), dim3(pk::T), 0, s, (const u64*)hi, (const u64*)lo,
                        (const long long*)val, (const u64*)rep, (const u32*)part, n, W, (const u8*)src,
-                       (const unsigned long long*)start, cursor, (u64*)rec, (u8*)blob);
+                       (const unsigned long long*)start, cursor, (u8*)rec, (u8*)blob);
   }
   return (int)hipGetLastError();
 }
 
 int mr_insert_received(const void* rec, u64 n, const void* recv, u32 W, void* tag, void* hi, void* lo, void* val,
-                       void* rep, void* ctrl, u64 cap, int op, hipStream_t s) {
+                       void* rep, void* ctrl, u64 cap, int op, int combined, hipStream_t s) {
   if (n == 0) return 0;
   if (W == 0 || W > (u32)pk::MAXW_RECV) return -1;
   GTab g;
@@ -224,8 +252,8 @@ int mr_insert_received(const void* rec, u64 n, const void* recv, u32 W, void* ta
   g.rep = (u64*)rep;
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
-  hipLaunchKernelGGL(pk::pk_insert_received_kernel, dim3(pk_grid(n, 2048)), dim3(256), 0, s, (const u64*)rec, n,
-                     (const long long*)recv, W, g, op);
+  hipLaunchKernelGGL(pk::pk_insert_received_kernel, dim3(pk_grid(n, 2048)), dim3(256), 0, s, (const u8*)rec, n,
+                     (const long long*)recv, W, g, op, combined);
   return (int)hipGetLastError();
 }
 

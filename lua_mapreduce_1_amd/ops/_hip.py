@@ -28,7 +28,7 @@ _SIGS = {
     "mr_count_tokens": [_p, _u64, _u64, _p, _p],
     "mr_wc_map2": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
     "mr_wc_map3": [_p, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
-    "mr_insert_received": [_p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p, _u64, _i32, _p],
+    "mr_insert_received": [_p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p, _u64, _i32, _i32, _p],
     "mr_memcpy_async": [_p, _p, _u64, _i32, _p],
     "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64, _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
@@ -70,7 +70,7 @@ _SIGS = {
     "mr_ts_checksum": [_p, _u64, _p, _p],
     "mr_ts_tie_fixup": [_p, _p, _p, _u64, _p, _p],
     "mr_ts_unsorted": [_p, _p, _u64, _p, _p],
-    "mr_pack_by_dest": [_p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, ctypes.c_longlong, _p, _p, _p],
+    "mr_pack_by_dest": [_p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, ctypes.c_longlong, _p, _p, _i32, _p],
     "mr_fix_loc": [_p, _u64, _p, _p, _u32, _p, _p],
     "mr_tail_compact": [_p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "mr_tail_gather": [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],

@@ -204,19 +204,24 @@ class HashTable:
                 np.minimum(lens, K.REP_LEN_MASK).astype(np.uint64)
             self._pending.append((hi, lo, np.ones(hi.size, np.int64), rep))
 
-    def insert_received(self, rec: torch.Tensor, recv_counts: torch.Tensor, W: int) -> None:
-        """Fold all-to-all-received records ``rec`` [n, 4] = (hi, lo, val, loc)
-        into the table; ``recv_counts`` = the device count-exchange row [W, 3]
-        (rows, key bytes, extra) per source; rep words become offsets into the
-        concatenated received key bytes.  One launch (csrc/hip/shuffle.hip)."""
-        n = rec.shape[0]
+    def insert_received(self, rec: torch.Tensor, recv_counts: torch.Tensor, W: int, rows: int | None = None) -> None:
+        """Fold all-to-all-received records into the table; ``recv_counts`` =
+        the device count-exchange row [W, 3] (rows, key bytes, extra) per
+        source.  ``rec``: int64 [n, 4] records (hi, lo, val, loc) whose key
+        bytes were received separately (rep words become offsets into the
+        concatenated received bytes), or — with ``rows`` = n — the uint8
+        buffer of the combined layout (ops/shuffle.pack_by_dest_combined),
+        whose rep words then index that same buffer.  One launch."""
+        combined = rows is not None
+        n = rows if combined else rec.shape[0]
         if n == 0:
             return
         if self.is_cuda:
             assert rec.is_contiguous() and recv_counts.is_contiguous()
             _hip.call("mr_insert_received", _hip.ptr(rec), n, _hip.ptr(recv_counts), W, *self._gtab(), self.cap,
-                      OPS[self.op], _hip.stream(self.device))
+                      OPS[self.op], 1 if combined else 0, _hip.stream(self.device))
             return
+        assert not combined, "the combined layout is GPU-only"
         from .shuffle import absolute_reps
         rc = recv_counts.view(W, 3).tolist()
         rep = absolute_reps(rec, [r[0] for r in rc], [r[1] for r in rc])

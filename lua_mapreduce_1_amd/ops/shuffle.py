@@ -31,7 +31,7 @@ def pack_by_dest(hi, lo, val, rep, part, W: int, src, extra: int = 0, blob_capac
         xchg = torch.empty(3 * W, dtype=torch.int64, device=d)
         _hip.call("mr_pack_by_dest", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), n, W,
                   _hip.ptr(src) if src is not None else None, _hip.ptr(ws), _hip.ptr(xchg), int(extra),
-                  _hip.ptr(rec), _hip.ptr(blob), _hip.stream(d))
+                  _hip.ptr(rec), _hip.ptr(blob), 0, _hip.stream(d))
         return rec, blob, xchg
     dest = (part.numpy().astype(np.int64) % W)
     order = np.argsort(dest, kind="stable")
@@ -52,6 +52,44 @@ def pack_by_dest(hi, lo, val, rep, part, W: int, src, extra: int = 0, blob_capac
     counts = np.bincount(dest, minlength=W).astype(np.int64)
     xchg = np.stack([counts, seg_start[1:] - seg_start[:-1], np.full(W, extra, np.int64)], 1).reshape(-1)
     return torch.from_numpy(rec), torch.from_numpy(blob), torch.from_numpy(xchg)
+
+
+def seg_bytes(rows: int, nbytes: int) -> int:
+    """Bytes of one destination's segment in the combined layout."""
+    return 32 * rows + ((nbytes + 7) & ~7)
+
+
+def pack_by_dest_combined(hi, lo, val, rep, part, W: int, src, extra: int = 0):
+    """GPU: ONE uint8 buffer of per-destination segments [records (32 B:
+    hi, lo, val, loc) | key bytes, padded to 8] + the count-exchange row
+    [records, bytes, extra] per destination; destination d's segment is
+    seg_bytes(rows_d, bytes_d) long, so the payload is a single all-to-all.
+    -> (buf uint8, xchg int64 [3W])."""
+    assert hi.is_cuda
+    n = hi.numel()
+    d = hi.device
+    part = part.to(torch.int32).contiguous()
+    cap = 32 * n + ((src.numel() if src is not None else 0) + 16 * n) + 8 * W
+    ws, buf = _combined_bufs(d, W, cap)
+    xchg = torch.empty(3 * W, dtype=torch.int64, device=d)
+    _hip.call("mr_pack_by_dest", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), n, W,
+              _hip.ptr(src) if src is not None else None, _hip.ptr(ws), _hip.ptr(xchg), int(extra),
+              _hip.ptr(buf), _hip.ptr(buf), 1, _hip.stream(d))
+    return buf, xchg
+
+
+_COMBINED: dict = {}
+
+
+def _combined_bufs(d, W: int, cap: int):
+    """Reused pack workspace and send buffer (grown as needed)."""
+    ws, buf = _COMBINED.get(d, (None, None))
+    if ws is None or ws.numel() < 6 * W:
+        ws = torch.empty(6 * W, dtype=torch.int64, device=d)
+    if buf is None or buf.numel() < cap:
+        buf = torch.empty(cap + cap // 8, dtype=torch.uint8, device=d)
+    _COMBINED[d] = (ws, buf)
+    return ws, buf
 
 
 def absolute_reps(rrec: torch.Tensor, recv_rows: list[int], recv_bytes: list[int]) -> torch.Tensor:

@@ -473,6 +473,18 @@ class SPMDEngine:
         bytes) -> received locations made absolute in the received blob."""
         from ..ops import shuffle as SH
         W = self.world
+        if raw:
+            # GPU: records and key bytes in ONE buffer of per-destination
+            # segments -> one payload all-to-all; the receive-side insert
+            # kernel locates records and bytes from the exchanged counts
+            buf, xchg = SH.pack_by_dest_combined(hi, lo, val, rep, part, W, src, extra=failed)
+            recv = D.exchange_counts(xchg, self.group)
+            send_h, recv_h = torch.cat([xchg, recv]).view(2, W, 3).cpu().tolist()  # one host sync
+            self._failed_total = sum(r[2] for r in recv_h)
+            send_sz = [SH.seg_bytes(r[0], r[1]) for r in send_h]
+            recv_sz = [SH.seg_bytes(r[0], r[1]) for r in recv_h]
+            rbuf = D.all_to_all_v(buf[:sum(send_sz)], send_sz, recv_sz, self.group)
+            return rbuf, recv.view(W, 3), sum(r[0] for r in recv_h)
         rec, blob, xchg = SH.pack_by_dest(hi, lo, val, rep, part, W, src, extra=failed)
         recv = D.exchange_counts(xchg, self.group)
         both = torch.cat([xchg, recv]).view(2, W, 3).cpu().tolist()  # one host sync
@@ -482,8 +494,6 @@ class SPMDEngine:
         recv_rows, recv_bytes = [r[0] for r in recv_h], [r[1] for r in recv_h]
         rrec = D.all_to_all_v(rec, send_rows, recv_rows, self.group)
         rblob = D.all_to_all_v(blob[:sum(send_bytes)], send_bytes, recv_bytes, self.group)
-        if raw:  # the receive-side insert kernel makes the locs absolute itself
-            return rrec, recv.view(W, 3), rblob
         rrep = SH.absolute_reps(rrec, recv_rows, recv_bytes)
         return rrec[:, 0].contiguous(), rrec[:, 1].contiguous(), rrec[:, 2].contiguous(), rrep, rblob
 
@@ -501,13 +511,13 @@ class SPMDEngine:
             return devmod.finalize_table_native(table, n, src, self.nparts)
         return devmod.finalize_table_device(table, n, src, self.nparts)
 
-    def _reduce_insert_received(self, rrec, recv_counts) -> int:
+    def _reduce_insert_received(self, rbuf, recv_counts, rows: int) -> int:
         """Received records -> this rank's reduce table (one insert launch);
         returns its key count.  The table is sized from the previous
         iteration's distinct-key count (its compaction scans every slot), not
         from the received rows (every peer sends the popular keys); a table
         that ends up more than half full is regrown and refilled."""
-        n = rrec.shape[0]
+        n = rows
         guess = getattr(self, "_red_distinct", None)
         want = 2 * (guess + guess // 4) if guess is not None else 2 * n
         cap = ops.next_pow2(max(1 << 16, min(2 * n, want)))
@@ -516,7 +526,7 @@ class SPMDEngine:
                 self.red_table = ops.HashTable(cap, device=self.device, op=self.op)
             else:
                 self.red_table.reset()
-            self.red_table.insert_received(rrec, recv_counts, self.world)
+            self.red_table.insert_received(rbuf, recv_counts, self.world, rows=rows)
             m, ovf = self.red_table.stats()
             if not ovf and m <= cap // 2:
                 self._red_distinct = m
@@ -659,8 +669,8 @@ class SPMDEngine:
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         if self.world > 1:
             if fused:
-                rrec, rcounts, src = self._shuffle(hi, lo, val, rep, src, part, failed, raw=True)
-                n_red = self._reduce_insert_received(rrec, rcounts)
+                src, rcounts, rows = self._shuffle(hi, lo, val, rep, src, part, failed, raw=True)
+                n_red = self._reduce_insert_received(src, rcounts, rows)
                 pend = self._finalize_table(self.red_table, n_red, src)
             else:
                 hi, lo, val, rep, src = self._shuffle(hi, lo, val, rep, src, part, failed)

@@ -314,6 +314,40 @@ def test_pack_by_dest_matches_cpu(gpu, W):
     assert per_dest(rg.cpu(), bg[:sum(nb)]) == per_dest(rc, bc)
 
 
+@pytest.mark.parametrize("W", [1, 3, 8])
+def test_combined_pack_and_receive_insert(gpu, W):
+    """Combined one-buffer shuffle layout: destination d's segment, received W
+    times (as from W identical peers), folds into a table holding exactly the
+    keys of partitions p % W == d with W times their counts and rep words that
+    index the received buffer."""
+    from lua_mapreduce_1_amd.ops import shuffle as SH
+    rng = np.random.default_rng(40 + W)
+    words = [bytes(rng.integers(97, 123, int(rng.integers(1, 30))).astype(np.uint8)) for _ in range(5000)]
+    text = b" ".join(words) + b"\n"
+    t = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(gpu)
+    tab = ops.HashTable(1 << 14, device=gpu)
+    tab.wordcount_map(t)
+    hi, lo, val, rep = tab.compact()
+    part, _ = ops.key_meta(hi, lo, rep, t, nparts=10)
+    src_dict = _wc_dict(hi, lo, val, rep, t)
+    pmap = dict(zip(ops.key_bytes_list(hi.cpu(), lo.cpu(), rep.cpu(), t.cpu()), part.cpu().tolist()))
+    buf, xchg = SH.pack_by_dest_combined(hi, lo, val, rep, part, W, t, extra=5)
+    x = xchg.view(W, 3).cpu().tolist()
+    assert all(r[2] == 5 for r in x) and sum(r[0] for r in x) == hi.numel()
+    seg = [SH.seg_bytes(r[0], r[1]) for r in x]
+    starts = np.concatenate([[0], np.cumsum(seg)]).astype(np.int64)
+    for d in range(W):
+        segd = buf[int(starts[d]):int(starts[d + 1])]
+        rbuf = segd.repeat(W).contiguous()
+        recv = torch.tensor([x[d]] * W, dtype=torch.int64, device=gpu).contiguous()
+        red = ops.HashTable(1 << 14, device=gpu)
+        red.insert_received(rbuf, recv, W, rows=W * x[d][0])
+        rh, rl, rv, rr = red.compact()
+        got = _wc_dict(rh, rl, rv, rr, rbuf)
+        want = {k: W * v for k, v in src_dict.items() if pmap[k] % W == d}
+        assert got == want
+
+
 @pytest.mark.parametrize("nparts", [1, 10, 256])
 def test_fused_tail_matches_unfused(gpu, nparts):
     from lua_mapreduce_1_amd.runtime import device as dv
