@@ -22,7 +22,7 @@ namespace mr {
 namespace tl {
 
 constexpr int T = 256;
-constexpr int ITEMS = 16;
+constexpr int ITEMS = 4;  // 4096-slot blocks left most CUs idle on a reduce-side table (64 blocks)
 
 __device__ __forceinline__ u32 key_fnv(u64 h, u64 l, u64 r, const u8* src, u32* len_out) {
   u32 f = FNV_OFFSET;
@@ -89,16 +89,19 @@ __global__ void __launch_bounds__(T) tail_compact_kernel(GTab g, u64 cap, u32 np
       out_rep[o] = r;
       out_part[o] = p;
       out_c[o] = c;
+      // digit 7 of c is the partition: its histogram is pc (no second set of
+      // same-address LDS atomics on the few partition bins)
 #pragma unroll
-      for (int b = 0; b < 8; ++b) atomicAdd(&hist[b][(c >> (8 * b)) & 0xFF], 1u);
-      if (p < 256) atomicAdd(&pc[p], 1u);
+      for (int b = 0; b < 7; ++b) atomicAdd(&hist[b][(c >> (8 * b)) & 0xFF], 1u);
+      atomicAdd(&pc[p & 255], 1u);
       ++o;
     }
   }
   __syncthreads();
 #pragma unroll
-  for (int b = 0; b < 8; ++b)
+  for (int b = 0; b < 7; ++b)
     if (hist[b][t]) atomicAdd(&ghist[b * 256 + t], hist[b][t]);
+  if (pc[t]) atomicAdd(&ghist[7 * 256 + t], pc[t]);
   if ((u32)t < nparts && pc[t]) atomicAdd((unsigned long long*)&pcount[t], (unsigned long long)pc[t]);
 }
 

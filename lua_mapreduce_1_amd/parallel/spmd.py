@@ -664,6 +664,11 @@ class SPMDEngine:
             pend = self._graphed_tail(n_claimed, overflow, src)
         elif self.world == 1 and fused:
             pend = self._finalize_table(self.table, n_claimed, src)
+        elif self.world > 1 and fused:
+            # compact + FNV partition in one kernel (the send side of the shuffle)
+            if overflow:
+                raise OverflowError("hash table overflow")
+            hi, lo, val, rep, part = devmod.compact_partition(self.table, n_claimed, src, self.nparts)
         else:
             hi, lo, val, rep = self.table.compact((n_claimed, overflow))
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)

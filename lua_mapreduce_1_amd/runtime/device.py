@@ -328,6 +328,33 @@ def _tail_ws(d, n: int, nparts: int, blob_cap: int):
     return ws, v
 
 
+_CP_WS: dict = {}
+
+
+def compact_partition(table, n: int, src, nparts: int):
+    """Occupied slots of a table -> dense (hi, lo, val, rep) + exact FNV-1
+    partition (int32), in ONE kernel (tail_compact; its composite sort key and
+    digit histograms are by-products).  The send side of the shuffle; buffers
+    are reused across iterations (valid until the next call)."""
+    from ..ops import _hip
+    d = table.device
+    ws = _CP_WS.get(d)
+    m = max(n, 1)
+    if ws is None or ws["cap"] < m:
+        c = m + m // 4
+        ws = {"cap": c, "cols": torch.empty((6, c), dtype=torch.int64, device=d),
+              "part": torch.empty(c, dtype=torch.int32, device=d),
+              "small": torch.empty(1 + 1024 + 256, dtype=torch.int64, device=d)}
+        _CP_WS[d] = ws
+    cols, part, small = ws["cols"], ws["part"], ws["small"]
+    small.zero_()
+    hi, lo, val, rep, c = (cols[i, :n] for i in range(5))
+    _hip.call("mr_tail_compact", *table._gtab(), table.cap, nparts, _hip.ptr(src), _hip.ptr(hi), _hip.ptr(lo),
+              _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), _hip.ptr(c), _hip.ptr(small[:1]),
+              _hip.ptr(small[1:1025]), _hip.ptr(small[1025:]), _hip.stream(d))
+    return hi, lo, val, rep, part[:n]
+
+
 def finalize_table_native(table, n: int, src, nparts: int) -> dict:
     """finalize_table_device with every launch and download queued by ONE
     native call (mr_tail_run): same kernels, same packed download, same
