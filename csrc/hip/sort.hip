@@ -136,11 +136,17 @@ __global__ void __launch_bounds__(RS_THREADS) rs_ghist8_kernel(const u64* keys, 
     if (b < ndigits && h[b][t]) atomicAdd(&ghist[b * RS_BINS + t], h[b][t]);
 }
 
-template <typename V>
+// ROUNDS: tiles of 256 x ROUNDS keys.  16 (4096-key tiles) for large sorts;
+// 4 (1024-key tiles) below ONESWEEP_SMALL keys, where a pass is one tile's
+// latency and 4096-key tiles left most CUs idle (54k keys = 14 tiles).
+constexpr u64 ONESWEEP_SMALL = 1ull << 18;
+template <typename V, int ROUNDS>
 __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys_in, const V* vals_in, u64* keys_out,
                                                                  V* vals_out, u64 n, int shift, const u32* ghist,
                                                                  u64* granules, u32* tile_counter, u32 epoch,
                                                                  u32* err, int iota) {
+  constexpr int RS_TILE = RS_THREADS * ROUNDS;
+  constexpr int RS_ROUNDS = ROUNDS;
   // iota: vals_in is absent and the value of key i is i (first pass of a
   // permutation sort; saves the separate iota launch).
   // Each wave ranks its own contiguous quarter of the tile (16 rounds of 64
@@ -659,14 +665,25 @@ int mr_radix_ghist8(const void* keys, u64 n, void* ghist, int ndigits, hipStream
 // One onesweep pass on the 8-bit digit at `shift` (ghist: that digit's 256 bins;
 // granules: tiles*256 u64, never needs clearing — entries are epoch tagged;
 // tile_counter: one u32 zeroed before the pass; epoch unique per pass).
+// granules must hold 256 * mr_onesweep_tiles(n) u64
+u64 mr_onesweep_tiles(u64 n) {
+  return n <= ONESWEEP_SMALL ? (n + RS_THREADS * 4 - 1) / (RS_THREADS * 4) : (n + RS_TILE - 1) / RS_TILE;
+}
+
 int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
                            const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
                            hipStream_t s) {
   if (n == 0) return 0;
-  const u32 nt = (u32)((n + RS_TILE - 1) / RS_TILE);
-  hipLaunchKernelGGL(rs_onesweep_kernel<u32>, dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
-                     (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
-                     (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota);
+  const u32 nt = (u32)mr_onesweep_tiles(n);
+  if (n <= ONESWEEP_SMALL) {
+    hipLaunchKernelGGL((rs_onesweep_kernel<u32, 4>), dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
+                       (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
+                       (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota);
+  } else {
+    hipLaunchKernelGGL((rs_onesweep_kernel<u32, RS_ROUNDS>), dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
+                       (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
+                       (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota);
+  }
   return (int)hipGetLastError();
 }
 

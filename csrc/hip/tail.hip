@@ -202,6 +202,7 @@ int mr_tail_pack(const void* val, const void* off, u64 n, const void* counts, u3
 
 int mr_exclusive_scan_i64(const void* in, void* out, u64 n, void* partials, void* total, hipStream_t s);
 u64 mr_scan_partials_len(u64 n);
+u64 mr_onesweep_tiles(u64 n);
 int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
                            const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
                            hipStream_t s);
@@ -223,7 +224,7 @@ constexpr u64 TZ_GHIST = 8, TZ_PCOUNT = 8200, TZ_TILES = 10248, TZ_ERR = 10504, 
 u64 mr_tail_ws_layout(u64 n, u32 nparts, u64 blob_cap, u64* off) {
   (void)nparts;
   const u64 m = n ? n : 1;
-  const u64 tiles = (m + 4095) / 4096;
+  const u64 tiles = mr_onesweep_tiles(m);
   const u64 sz[TB_COUNT] = {8 * m, 8 * m, 8 * m, 8 * m, 8 * m, 4 * m, TZ_BYTES, 8 * m, 8 * m, 4 * m, 4 * m,
                             tiles * 256 * 8, 8 * m, 8 * m, 8 * m, 8 * m, 4 * m, 8 * m, 8 * (m + 1),
                             8 * mr_scan_partials_len(m), blob_cap ? blob_cap : 1, mr_tail_pack_bytes(m, 256)};

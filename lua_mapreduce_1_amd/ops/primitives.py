@@ -395,9 +395,15 @@ _EPOCH = [0]
 _SORT_WS: dict = {}
 
 
+def _onesweep_tiles(n: int) -> int:
+    """Tiles (= look-back granule rows) of one onesweep pass over n keys:
+    1024-key tiles up to 2^18 keys, 4096-key tiles above (csrc/hip/sort.hip)."""
+    return (n + 1023) // 1024 if n <= (1 << 18) else (n + 4095) // 4096
+
+
 def _sort_ws(d, n: int):
     """Per-device workspace for the onesweep sort (grown, never shrunk)."""
-    tiles = (n + 4095) // 4096
+    tiles = _onesweep_tiles(n)
     ws = _SORT_WS.get(d)
     if ws is None or ws["tiles"] < tiles:
         ws = {"tiles": max(tiles, 64),
@@ -437,7 +443,7 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
             if torch.cuda.is_current_stream_capturing():
                 # a replayed graph reuses its pass epochs: clear the look-back
                 # granules so a replay never sees the previous replay's tags
-                ws["granules"][: ((n + 4095) // 4096) * 256].zero_()
+                ws["granules"][: _onesweep_tiles(n) * 256].zero_()
             ghist_ws = small[:2048]
             pre_hist = ghist
             kbuf = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(2)]
