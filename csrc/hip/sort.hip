@@ -136,6 +136,25 @@ __global__ void __launch_bounds__(RS_THREADS) rs_ghist8_kernel(const u64* keys, 
     if (b < ndigits && h[b][t]) atomicAdd(&ghist[b * RS_BINS + t], h[b][t]);
 }
 
+// Inclusive scan of one value per thread over a 256-thread block: wave64
+// shuffles, then the 4 wave totals through LDS (2 barriers instead of the 16
+// of a Hillis-Steele loop over LDS).  `tmp` is 4 words of LDS.
+__device__ __forceinline__ u32 block_scan_256(u32 v, u32* tmp) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = __shfl_up(v, o);
+    if (lane >= o) v += y;
+  }
+  __syncthreads();  // tmp may still be read by a previous scan
+  if (lane == 63) tmp[wave] = v;
+  __syncthreads();
+  u32 add = 0;
+#pragma unroll
+  for (int w = 0; w < RS_WAVES; ++w) add += w < wave ? tmp[w] : 0u;
+  return v + add;
+}
+
 // ROUNDS: tiles of 256 x ROUNDS keys.  16 (4096-key tiles) for large sorts;
 // 4 (1024-key tiles) below ONESWEEP_SMALL keys, where a pass is one tile's
 // latency and 4096-key tiles left most CUs idle (54k keys = 14 tiles).
@@ -160,9 +179,9 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
   __shared__ V sv[RS_TILE];
   __shared__ u32 wc[RS_WAVES][RS_BINS];
   __shared__ u32 gout[RS_BINS];
-  __shared__ u32 scan[RS_BINS];
   __shared__ u32 sh_tile;
   __shared__ u32 sh_uniform;
+  __shared__ u32 wsum[RS_WAVES];
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = t >> 6;
@@ -174,16 +193,10 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
   for (int w = 0; w < RS_WAVES; ++w) wc[w][t] = 0;
   // exclusive scan of the global histogram (digit base offsets)
   const u32 gcount = ghist[t];
-  scan[t] = gcount;
   __syncthreads();
   if (gcount == n) sh_uniform = 1;
-  for (int o = 1; o < RS_BINS; o <<= 1) {
-    const u32 y = t >= o ? scan[t - o] : 0u;
-    __syncthreads();
-    scan[t] += y;
-    __syncthreads();
-  }
-  const u32 gbase = scan[t] - gcount;
+  const u32 gbase = block_scan_256(gcount, wsum) - gcount;
+  __syncthreads();
   const u32 tile = sh_tile;
   const u64 t0 = (u64)tile * RS_TILE;
   if (sh_uniform) {  // every key has this digit: order unchanged
@@ -241,15 +254,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
   u64* G = granules + (u64)tile * RS_BINS;
   __hip_atomic_store(&G[t], gr_pack(epoch, tile == 0 ? GR_INC : GR_AGG, mine), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
-  scan[t] = mine;
-  __syncthreads();
-  for (int o = 1; o < RS_BINS; o <<= 1) {
-    const u32 y = t >= o ? scan[t - o] : 0u;
-    __syncthreads();
-    scan[t] += y;
-    __syncthreads();
-  }
-  const u32 lbase = scan[t] - mine;
+  const u32 lbase = block_scan_256(mine, wsum) - mine;
   {
     u32 off = lbase;
 #pragma unroll
