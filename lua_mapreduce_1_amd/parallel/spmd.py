@@ -463,7 +463,7 @@ class SPMDEngine:
             return self.arena
         return self._ctx.source()
 
-    def _shuffle(self, hi, lo, val, rep, src, part, failed: int = 0, raw: bool = False):
+    def _shuffle(self, hi, lo, val, rep, src, part, failed: int = 0, raw: bool = False, before_sync=None):
         """Send each key to rank part % W; returns received (hi, lo, val, rep,
         src) and sets the job-wide number of failed map jobs (this rank's count
         rides along with the count exchange instead of a separate all-reduce).
@@ -479,6 +479,8 @@ class SPMDEngine:
             # kernel locates records and bytes from the exchanged counts
             buf, xchg = SH.pack_by_dest_combined(hi, lo, val, rep, part, W, src, extra=failed)
             recv = D.exchange_counts(xchg, self.group)
+            if before_sync is not None:
+                before_sync()  # host work that overlaps the pack and count exchange
             send_h, recv_h = torch.cat([xchg, recv]).view(2, W, 3).cpu().tolist()  # one host sync
             self._failed_total = sum(r[2] for r in recv_h)
             send_sz = [SH.seg_bytes(r[0], r[1]) for r in send_h]
@@ -650,8 +652,15 @@ class SPMDEngine:
             n_claimed, overflow = self.table.stats()
         T["map"] = time.time() - t0
         pipelined = prefetch_next and self.pipeline and self._can_pipeline()
-        if pipelined:
-            self._issue_next_map(jobs, j0, j1, q)
+        # the next iteration's map is queued right after this iteration's first
+        # tail kernels: those get the GPU first, and the host queues the map
+        # while they run instead of in front of them
+        next_map = [pipelined]
+
+        def issue_next_map():
+            if next_map[0]:
+                next_map[0] = False
+                self._issue_next_map(jobs, j0, j1, q)
         t1 = time.time()
         src = self._source()
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
@@ -664,6 +673,7 @@ class SPMDEngine:
             pend = self._graphed_tail(n_claimed, overflow, src)
         elif self.world == 1 and fused:
             pend = self._finalize_table(self.table, n_claimed, src)
+            issue_next_map()
         elif self.world > 1 and fused:
             # compact + FNV partition in one kernel (the send side of the shuffle)
             if overflow:
@@ -674,7 +684,8 @@ class SPMDEngine:
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         if self.world > 1:
             if fused:
-                src, rcounts, rows = self._shuffle(hi, lo, val, rep, src, part, failed, raw=True)
+                src, rcounts, rows = self._shuffle(hi, lo, val, rep, src, part, failed, raw=True,
+                                                  before_sync=issue_next_map)
                 n_red = self._reduce_insert_received(src, rcounts, rows)
                 pend = self._finalize_table(self.red_table, n_red, src)
             else:
@@ -685,6 +696,7 @@ class SPMDEngine:
         t2 = time.time()
         if pend is None:
             pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
+        issue_next_map()
 
         cols = devmod.finalize_host(pend, self.partmod)
         digits = len(str(max(self.nparts - 1, 0)))
