@@ -39,6 +39,7 @@ from .. import ops, utils
 from ..runtime import device as devmod
 from ..runtime import modules
 from ..utils import STATUS
+from ..utils import trace
 from . import dist as D
 
 
@@ -604,6 +605,10 @@ class SPMDEngine:
         self._pending = {"q": q + 1, "jobs": jobs, "recs": recs, "j0": j0, "j1": j1, "t0": t0}
 
     def run_iteration(self, prefetch_next: bool | None = None, lookahead: int | None = None) -> IterationResult:
+        with trace.range("mr.iteration"):
+            return self._run_iteration(prefetch_next, lookahead)
+
+    def _run_iteration(self, prefetch_next, lookahead) -> IterationResult:
         """One MapReduce iteration.  ``prefetch_next`` (default ``self.prefetch``)
         starts the input copies of the next ``lookahead`` (default 2, at most
         N_ARENAS - 1) iterations as soon as their arenas are free; with
@@ -643,7 +648,9 @@ class SPMDEngine:
             return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, ahead > 0, q)
 
     def _finish_iteration(self, res, T, t_start, t0, jobs, recs, j0, j1, prefetch_next, q) -> IterationResult:
+        trace.push("mr.map.wait")
         n_claimed, overflow = self.table.stats()   # synchronises the map phase
+        trace.pop()
         if overflow or n_claimed > self.table.cap // 2:
             # grow and redo this rank's map (results with an overflowed table are unusable)
             self.table = ops.HashTable(ops.next_pow2(4 * max(n_claimed, 1)), device=self.device, op=self.op)
@@ -660,7 +667,8 @@ class SPMDEngine:
         def issue_next_map():
             if next_map[0]:
                 next_map[0] = False
-                self._issue_next_map(jobs, j0, j1, q)
+                with trace.range("mr.map.issue_next"):
+                    self._issue_next_map(jobs, j0, j1, q)
         t1 = time.time()
         src = self._source()
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
@@ -683,6 +691,7 @@ class SPMDEngine:
             hi, lo, val, rep = self.table.compact((n_claimed, overflow))
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
         if self.world > 1:
+            trace.push("mr.shuffle_reduce")
             if fused:
                 src, rcounts, rows = self._shuffle(hi, lo, val, rep, src, part, failed, raw=True,
                                                   before_sync=issue_next_map)
@@ -692,13 +701,15 @@ class SPMDEngine:
                 hi, lo, val, rep, src = self._shuffle(hi, lo, val, rep, src, part, failed)
                 hi, lo, val, rep = self._reduce(hi, lo, val, rep, src)
                 part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
+            trace.pop()
         T["shuffle"] = time.time() - t1
         t2 = time.time()
         if pend is None:
             pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
         issue_next_map()
 
-        cols = devmod.finalize_host(pend, self.partmod)
+        with trace.range("mr.finalize_host"):
+            cols = devmod.finalize_host(pend, self.partmod)
         digits = len(str(max(self.nparts - 1, 0)))
         for p in range(self.nparts):
             if cols["bounds"][p + 1] > cols["bounds"][p]:
