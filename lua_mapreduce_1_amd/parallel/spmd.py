@@ -223,8 +223,11 @@ class SPMDEngine:
     def _jobs(self) -> list[tuple]:
         jobs = []
         # a taskfn declared pure (``spmd_replicated_taskfn = True``: its job list
-        # depends only on init args) is evaluated by every rank: no broadcast
+        # depends only on init args) is evaluated by every rank: no broadcast —
+        # and once per engine: pipelined iterations reuse the job list anyway
         replicated = bool(modules.field(self.taskfn, "spmd_replicated_taskfn"))
+        if replicated and getattr(self, "_jobs_cache", None) is not None:
+            return self._jobs_cache
         if self.rank == 0 or replicated:
             seen = set()
 
@@ -236,6 +239,8 @@ class SPMDEngine:
             modules.field(self.taskfn, "taskfn")(emit)
         if self.world > 1 and not replicated:
             jobs = D.broadcast_object(jobs, 0, self.group, self.device if self.device.type == "cuda" else None)
+        if replicated:
+            self._jobs_cache = jobs
         return jobs
 
     def _job_bytes(self, value) -> int:
@@ -247,10 +252,16 @@ class SPMDEngine:
         return 1
 
     def _assign(self, jobs: list[tuple]) -> tuple[int, int]:
-        """Contiguous block of jobs for this rank, balanced by input bytes."""
+        """Contiguous block of jobs for this rank, balanced by input bytes
+        (memoised for the cached job list of a pure taskfn)."""
         if self.world == 1:
             return 0, len(jobs)
-        return assign_contiguous([self._job_bytes(v) for _, v in jobs], self.rank, self.world)
+        memo = getattr(self, "_assign_memo", None)
+        if memo is not None and memo[0] is jobs:
+            return memo[1]
+        r = assign_contiguous([self._job_bytes(v) for _, v in jobs], self.rank, self.world)
+        self._assign_memo = (jobs, r)
+        return r
 
     # -- map ------------------------------------------------------------------
     @property
@@ -388,7 +399,8 @@ class SPMDEngine:
             if cs is not None:
                 cur = torch.cuda.current_stream(self.device)
                 if self._inflight.pop(self.slot, None) != (ids[0], len(ids)):  # else: prefetched, in flight
-                    self._issue_copies(plan, wait_for=cur)
+                    with trace.range("mr.copies"):
+                        self._issue_copies(plan, wait_for=cur)
                 # chunks whose copies have already landed (prefetched during the
                 # previous iteration's tail) are mapped by ONE launch: a launch's
                 # ramp-up and drain cost more than its chunking saves
@@ -630,21 +642,27 @@ class SPMDEngine:
             jobs, recs, j0, j1, t0 = pending["jobs"], pending["recs"], pending["j0"], pending["j1"], pending["t0"]
             stream = self.streams[self.tslot]
         else:
+            trace.push("mr.jobs")
             jobs = self._jobs()
             recs = [JobRecord(k, v) for k, v in jobs]
             j0, j1 = self._assign(jobs)
+            trace.pop()
             stream = self.streams[self.tslot] if ahead and self.pipeline else None
         res.map_jobs = recs
         with torch.cuda.stream(stream) if stream is not None else _nullctx():
             if pending is None:
-                self.table.reset()
+                with trace.range("mr.table_reset"):
+                    self.table.reset()
                 t0 = time.time()
-                self._run_map(jobs, recs, j0, j1)
+                with trace.range("mr.map.issue"):
+                    self._run_map(jobs, recs, j0, j1)
             # the arenas of q+1..q+ahead are free (iterations up to q-1
             # completed): their copies queue behind this iteration's (the
             # copy stream is FIFO), so the copy engine never idles
+            trace.push("mr.prefetch")
             for k in range(1, ahead + 1):
                 self._prefetch(jobs, j0, j1, q + k)
+            trace.pop()
             return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, ahead > 0, q)
 
     def _finish_iteration(self, res, T, t_start, t0, jobs, recs, j0, j1, prefetch_next, q) -> IterationResult:
