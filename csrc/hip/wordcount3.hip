@@ -38,7 +38,7 @@ struct Lds {
   static constexpr int WSW = STAGED / 32 + 2;
   u8 txt[TXT];
   u32 ws[WSW];
-  u32 tag[SLOTS];
+  u64 tag[SLOTS];  // gtab_tag-style: a packed key of <= 7 bytes IS its tag
   u32 cnt[SLOTS];
   u32 rep[SLOTS];  // local offset (16 bits) | len (16 bits) << 16
   u64 lo[SLOTS];
@@ -99,32 +99,42 @@ __device__ __forceinline__ uint4 load16(const u8* __restrict__ text, u64 gpos, u
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// LDS combine.  Tags are 64-bit: for a packed key of <= 7 bytes (the frequent
+// words) the tag is the key itself (hi | len, gtab_tag in mr_common.h), so a
+// hit is ONE LDS read and a claim publishes the key in its CAS; other keys use
+// a hashed tag plus the published (hi, lo) check (lo released last).
 template <int T, int SLOTS>
 __device__ __forceinline__ bool lds_insert(Lds<T, SLOTS>& L, u64 hi, u64 lo, u32 rep) {
   u64 h = hi ^ (lo * 0x9E3779B97F4A7C15ull);
   h ^= h >> 31;
   h *= 0xC2B2AE3D27D4EB4Full;
   h ^= h >> 29;
-  const u32 tag = (u32)(h >> 32) | 1u;
-  u32 slot = (u32)h & (SLOTS - 1);
+  const bool exact = (lo - 1 < 7) && (hi & 0xFFull) == 0;
+  const u64 tag = exact ? (hi | lo) : ((h & ~0xFFull) | 0x80ull);
+  u32 slot = (u32)(h >> 40) & (SLOTS - 1);
   constexpr u32 LIMIT = SLOTS * 3 / 4;
   for (int probes = 0; probes < PROBES;) {
-    u32 cur = __hip_atomic_load(&L.tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    u64 cur = __hip_atomic_load(&L.tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (cur == 0) {
       if (__hip_atomic_load(&L.nclaimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= LIMIT) return false;
-      u32 expected = 0;
+      u64 expected = 0;
       if (__hip_atomic_compare_exchange_strong(&L.tag[slot], &expected, tag, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP)) {
         L.hi[slot] = hi;
         L.rep[slot] = rep;
         __hip_atomic_fetch_add(&L.cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add(&L.nclaimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_store(&L.lo[slot], lo, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (exact) L.lo[slot] = lo;  // read only by the flush, after a barrier
+        else __hip_atomic_store(&L.lo[slot], lo, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         return true;
       }
       cur = expected;
     }
     if (cur == tag) {
+      if (exact) {  // the tag is the key
+        __hip_atomic_fetch_add(&L.cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return true;
+      }
       const u64 l = __hip_atomic_load(&L.lo[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (l == 0) continue;  // claimer has not published yet: re-read this slot
       if (l == lo && L.hi[slot] == hi) {
@@ -141,7 +151,9 @@ __device__ __forceinline__ bool lds_insert(Lds<T, SLOTS>& L, u64 hi, u64 lo, u32
 // T threads, SLOTS LDS slots, TPC tiles of T*16 bytes per workgroup chunk.
 template <int T, int SLOTS, int TPC>
 __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text, u64 nbytes, u64 rep_base, GTab g,
-                                                    Ovf ovf, int aligned) {
+                                                    Ovf ovf, int aligned, int ablate) {
+  // ablate (timing only, the table is then incomplete): 1 = no flush to HBM,
+  // 2 = tokenize + key packing only (no LDS combine, no flush)
   using L_t = Lds<T, SLOTS>;
   constexpr int TILE = L_t::TILE;
   constexpr int STAGED = L_t::STAGED;
@@ -234,6 +246,10 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
         } else {
           lo = long_lo_global(text, gpos, len);
         }
+        if (ablate == 2) {
+          if ((hi ^ lo) == 0x123456789ull) ovf.counter[1] = hi;  // keep the key live
+          continue;
+        }
         const bool ok = len < 65536 && lds_insert(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16));
         if (!ok) {
           const u64 grep = make_rep(rep_base + gpos, len);
@@ -251,6 +267,7 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
     __syncthreads();
   }
   if (stamp && t == 0) stamp[1] = wall_clock64();
+  if (ablate) return;
   // flush: each thread folds its PER slots.  The common case is a key already
   // in the HBM table at its home slot, so tag/lo/hi of every home slot are
   // loaded speculatively in ONE batch (one memory round trip instead of a
@@ -357,11 +374,12 @@ __global__ void __launch_bounds__(256) ovf_agg3_kernel(Ovf o, GTab g) {
 }
 
 template <int T, int SLOTS, int TPC>
-int launch(const u8* tx, u64 nbytes, u64 rep_base, const GTab& g, const Ovf& o, int aligned, hipStream_t stream) {
+int launch(const u8* tx, u64 nbytes, u64 rep_base, const GTab& g, const Ovf& o, int aligned, int ablate,
+           hipStream_t stream) {
   constexpr u64 CHUNK = (u64)T * SEG * TPC;
   const u64 nblocks = (nbytes + CHUNK - 1) / CHUNK;
   hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC>), dim3((unsigned)nblocks), dim3(T), 0, stream, tx, nbytes,
-                     rep_base, g, o, aligned);
+                     rep_base, g, o, aligned, ablate);
   return 0;
 }
 
@@ -391,13 +409,15 @@ int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, 
   v3::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter, (u64*)stamps};
   const int aligned = ((uintptr_t)text & 15) == 0;
   const u8* tx = (const u8*)text;
+  const int ablate = config >> 8;  // ablation modes ride in the high bits of config
+  config &= 0xFF;
   switch (config) {
-    case 0: v3::launch<512, 2048, 1>(tx, nbytes, rep_base, g, o, aligned, stream); break;
-    case 1: v3::launch<512, 2048, 2>(tx, nbytes, rep_base, g, o, aligned, stream); break;
-    case 2: v3::launch<1024, 4096, 1>(tx, nbytes, rep_base, g, o, aligned, stream); break;
-    case 3: v3::launch<256, 1024, 1>(tx, nbytes, rep_base, g, o, aligned, stream); break;
-    case 4: v3::launch<256, 2048, 2>(tx, nbytes, rep_base, g, o, aligned, stream); break;
-    case 5: v3::launch<512, 4096, 2>(tx, nbytes, rep_base, g, o, aligned, stream); break;
+    case 0: v3::launch<512, 2048, 1>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
+    case 1: v3::launch<512, 2048, 2>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
+    case 2: v3::launch<1024, 4096, 1>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
+    case 3: v3::launch<256, 1024, 1>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
+    case 4: v3::launch<256, 2048, 2>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
+    case 5: v3::launch<512, 4096, 2>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
     default: return -1;
   }
   hipLaunchKernelGGL(v3::ovf_agg3_kernel, dim3(1024), dim3(256), 0, stream, o, g);

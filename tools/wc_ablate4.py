@@ -1,0 +1,20 @@
+"""v3 map kernel phase ablation (config 0): full / no flush / tokenize only,
+full corpus and one rank's 1/8 share, plus the warm-table (no claims) case."""
+import sys
+import torch
+sys.path.insert(0, ".")
+from lua_mapreduce_1_amd import ops
+from lua_mapreduce_1_amd.utils.corpus import europarl_like
+
+text = b"".join(europarl_like())
+dev = torch.frombuffer(bytearray(text), dtype=torch.uint8).cuda()
+tab = ops.HashTable(1 << 21, device="cuda")
+for data, tag in ((dev, "full"), (dev[: len(text) // 8], "1/8 ")):
+    for mode, name in ((0, "full"), (1, "no-flush"), (2, "tokenize")):
+        ts = []
+        for _ in range(5):
+            tab.reset(); torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(); tab.wordcount_map(data, version=3, mode=(mode << 8)); e1.record(); torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        print(f"{tag} {name:9s} min {min(ts):7.3f} ms  {data.numel() / min(ts) / 1e6:7.1f} GB/s", flush=True)
