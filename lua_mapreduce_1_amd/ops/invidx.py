@@ -99,6 +99,50 @@ def map_postings(text: torch.Tensor, vocab: Vocab, doc_bits: int, rep_base: int 
     return torch.from_numpy((ids << doc_bits) | line)
 
 
+class PostingSink:
+    """Device output of map_postings_chunk: one posting buffer and counter
+    shared by several launches (chunks of one rank's text, mapped as their
+    host->HBM copies land)."""
+
+    def __init__(self, device, nbytes: int):
+        self.cap = nbytes // 2 + 2  # tokens are separated by >= 1 whitespace byte
+        self.out = torch.empty(self.cap, dtype=torch.int64, device=device)
+        self.ctrl = torch.zeros(2, dtype=torch.int64, device=device)  # [count, error]
+
+    def reset(self) -> None:
+        self.ctrl.zero_()
+
+    def finish(self, vocab: "Vocab") -> torch.Tensor:
+        n, e = self.ctrl.tolist()  # the one host synchronisation of the map phase
+        if e:
+            raise RuntimeError("inverted index map: posting buffer overflow")
+        if vocab.overflowed:
+            raise RuntimeError("inverted index map: vocabulary table overflow (raise capacity)")
+        return self.out[:n]
+
+
+def map_postings_chunk(text: torch.Tensor, a: int, b: int, line_base: int, vocab: Vocab, doc_bits: int,
+                       sink: PostingSink) -> None:
+    """GPU: postings of text[a:b] (a split-aligned piece of a rank's text) into
+    ``sink``; ``line_base`` = newlines of the rank's text before byte a.  Line
+    ids come from the piece's own newline counts (one count + one scan launch)."""
+    d = text.device
+    s = _hip.stream(d)
+    piece = text[a:b]
+    nbytes = piece.numel()
+    if nbytes == 0:
+        return
+    nchunks = max(1, (nbytes + CHUNK - 1) // CHUNK)
+    cnt = torch.empty(nchunks, dtype=torch.int32, device=d)
+    _hip.call("mr_count_newlines", _hip.ptr(piece), nbytes, CHUNK, _hip.ptr(cnt), s)
+    base, _ = exclusive_scan(cnt)
+    if line_base:
+        base.add_(line_base)
+    t = vocab.table
+    _hip.call("mr_ii_map", _hip.ptr(piece), nbytes, CHUNK, a, _hip.ptr(base), *t._gtab(), t.cap, doc_bits,
+              _hip.ptr(sink.out), _hip.ptr(sink.ctrl[:1]), sink.cap, _hip.ptr(sink.ctrl[1:]), s)
+
+
 def sort_unique(keys: torch.Tensor, bits: int) -> torch.Tensor:
     """Sorted distinct posting keys (keys < 2^bits, bits <= 63)."""
     n = keys.numel()

@@ -30,6 +30,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..ops import _hip
 from ..ops import invidx as II
 from ..ops.keys import REP_LEN_BITS
 from . import dist as D
@@ -86,6 +87,44 @@ class InvertedIndexBuilder:
         self.doc_bits = II.bits_for(self.rank_lines + 1)
         self.text = None
         self.timings: dict[str, float] = {}
+        # GPU staging: the rank's text arrives in split-aligned pieces on a copy
+        # stream and each piece is mapped as soon as it has landed; two arenas,
+        # so build(prefetch_next=True) can start the next build's copies while
+        # this one sorts
+        cuda = self.device.type == "cuda"
+        self.copy_stream = torch.cuda.Stream(self.device) if cuda else None
+        self.arenas = [None, None]
+        self.slot = 0
+        self._prefetched = None  # slot whose copies are in flight
+        self.pieces = self._plan_pieces() if cuda else []
+        self.events = [[torch.cuda.Event() for _ in self.pieces] for _ in range(2)] if cuda else None
+        self.sink = None
+
+    def _plan_pieces(self, first_mb: float = 2, big_mb: float = 24) -> list[tuple[int, int, int]]:
+        """Split-aligned pieces (byte start, byte end, line base) of the rank's
+        text: a small first piece (its copy is exposed), then ~big_mb ones."""
+        offs = self.store.offsets
+        lines = self.store.line_offsets()
+        out, i = [], self.j0
+        target = int(first_mb * (1 << 20))
+        while i < self.j1:
+            k = i + 1
+            while k < self.j1 and offs[k + 1] - offs[i] <= target:
+                k += 1
+            out.append((int(offs[i] - offs[self.j0]), int(offs[k] - offs[self.j0]), int(lines[i] - lines[self.j0])))
+            i = k
+            target = int(big_mb * (1 << 20))
+        return out
+
+    def _issue_copies(self, slot: int) -> None:
+        host = self.store.buffer[self.a:self.b]
+        if self.arenas[slot] is None:
+            self.arenas[slot] = torch.empty(host.numel(), dtype=torch.uint8, device=self.device)
+        dst = self.arenas[slot]
+        sp = _hip.stream_ptr(self.copy_stream)
+        for (a, b, _), ev in zip(self.pieces, self.events[slot]):
+            _hip.call("mr_memcpy_async", _hip.ptr(dst[a:b]), _hip.ptr(host[a:b]), b - a, 1, sp)
+            ev.record(self.copy_stream)
 
     def _sync(self):
         if self.device.type == "cuda":
@@ -102,12 +141,41 @@ class InvertedIndexBuilder:
             self.text = host
         return self.text
 
-    def build(self, stage: bool = True) -> IndexShard:
+    def _map_staged(self) -> torch.Tensor:
+        """GPU: copies of the rank's pieces (unless prefetched) and one map
+        launch per piece once its copy has landed -> posting keys."""
+        cur = torch.cuda.current_stream(self.device)
+        if self._prefetched != self.slot:
+            gate = torch.cuda.Event()
+            gate.record(cur)  # the arena may still be read by earlier work
+            self.copy_stream.wait_event(gate)
+            self._issue_copies(self.slot)
+        self._prefetched = None
+        text = self.text = self.arenas[self.slot]
+        if self.sink is None:
+            self.sink = II.PostingSink(self.device, text.numel())
+        self.sink.reset()
+        for (a, b, lb), ev in zip(self.pieces, self.events[self.slot]):
+            cur.wait_event(ev)
+            II.map_postings_chunk(text, a, b, lb, self.vocab, self.doc_bits, self.sink)
+        return self.sink.finish(self.vocab)
+
+    def build(self, stage: bool = True, prefetch_next: bool = False) -> IndexShard:
+        """One inverted-index build of the rank's splits.  ``prefetch_next``:
+        start the next build's host->HBM copies (into the other arena) as soon
+        as this build's map is done, overlapping them with its sort/shuffle."""
         t0 = time.perf_counter()
-        text = self.stage() if (stage or self.text is None) else self.text
         vocab = self.vocab
         vocab.reset()
-        keys = II.map_postings(text, vocab, self.doc_bits)
+        if self.device.type == "cuda" and self.b > self.a and (stage or self.text is None):
+            keys = self._map_staged()
+            text = self.text
+            if prefetch_next:
+                self._issue_copies(1 - self.slot)
+                self._prefetched = 1 - self.slot
+        else:
+            text = self.stage() if (stage or self.text is None) else self.text
+            keys = II.map_postings(text, vocab, self.doc_bits)
         t_map = time.perf_counter()
         bits = vocab.id_bits + self.doc_bits
         if self.world > 1:
@@ -131,6 +199,8 @@ class InvertedIndexBuilder:
         part, klen = ops.key_meta(hi, lo, rep, src, nparts=self.R)
         koff, kblob = ops.gather_key_bytes(hi, lo, rep, src, lengths=klen)
         self._sync()
+        if self._prefetched is not None:
+            self.slot = self._prefetched  # the next build maps the prefetched arena
         t1 = time.perf_counter()
         self.timings = {"map": t_map - t0, "sort": t_sort - t_map, "shuffle": t_shuf - t_sort,
                         "finalize": t1 - t_shuf, "total": t1 - t0}

@@ -99,6 +99,23 @@ def test_gpu_single_rank_matches_oracle(gpu):
 
 
 @pytest.mark.gpu
+def test_gpu_staged_pieces_and_prefetch(gpu):
+    """Split-aligned pieces mapped as their copies land (line ids continue
+    across pieces), and builds whose copies were prefetched into the other
+    arena during the previous build's sort."""
+    import torch
+    splits = _splits()
+    b = InvertedIndexBuilder(SplitStore(splits, pin=True), device=gpu, capacity=1 << 16)
+    b.pieces = b._plan_pieces(first_mb=0.01, big_mb=0.03)
+    b.events = [[torch.cuda.Event() for _ in b.pieces] for _ in range(2)]
+    assert len(b.pieces) >= 3
+    want = naive_index(splits)
+    for i in range(4):
+        assert b.build(prefetch_next=i < 3).to_host() == want
+    assert b._prefetched is None
+
+
+@pytest.mark.gpu
 def test_gpu_long_lines_and_many_lines(gpu):
     """Lines longer than a tile / chunk, and more lines than one tile's worth."""
     rng = np.random.default_rng(4)
