@@ -43,12 +43,14 @@ METRIC = "words/sec (whole node), Europarl-v7 word-count 197 splits, 1/2/4/8 MI3
 MODEL = "lua_mapreduce_1_amd.models.wordcount"
 
 
-def load_corpus(seed: int, rank: int, local_rank: int, world: int, device) -> list[bytes]:
+def load_corpus(seed: int, rank: int, local_rank: int, world: int, device, lines: int = corpus.EUROPARL_LINES,
+                words: int = corpus.EUROPARL_WORDS) -> list[bytes]:
     """Generate once per box (cached under /tmp), shared by all local ranks."""
-    cache = f"/tmp/lmr_europarl_like_{seed}.npz"
+    shape = "" if (lines, words) == (corpus.EUROPARL_LINES, corpus.EUROPARL_WORDS) else f"_{lines}_{words}"
+    cache = f"/tmp/lmr_europarl_like_{seed}{shape}.npz"
     if local_rank == 0 and not os.path.exists(cache):
         t0 = time.time()
-        splits = corpus.europarl_like(seed=seed)
+        splits = corpus.europarl_like(seed=seed, lines=lines, words=words)
         off = np.zeros(len(splits) + 1, np.int64)
         np.cumsum([len(s) for s in splits], out=off[1:])
         tmp = cache + f".tmp{os.getpid()}.npz"
@@ -69,14 +71,19 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--reducers", type=int, default=10)
     ap.add_argument("--verbose", action="store_true")
+    # smaller corpora only for smoke tests of the harness (the headline number
+    # is the full Europarl shape; a reduced one is flagged in "data"/"config")
+    ap.add_argument("--lines", type=int, default=corpus.EUROPARL_LINES)
+    ap.add_argument("--words", type=int, default=corpus.EUROPARL_WORDS)
     args = ap.parse_args()
 
     rank, world, device = D.init_from_env()
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     if world != args.gpus and rank == 0:
         print(f"# warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    splits = load_corpus(args.seed, rank, local_rank, world, device)
-    total_words = corpus.EUROPARL_WORDS
+    splits = load_corpus(args.seed, rank, local_rank, world, device, args.lines, args.words)
+    total_words = args.words
+    full = (args.lines, args.words) == (corpus.EUROPARL_LINES, corpus.EUROPARL_WORDS)
     total_bytes = sum(len(s) for s in splits)
     store = SplitStore(splits)
     del splits
@@ -130,10 +137,11 @@ def main() -> int:
             "metric": METRIC, "value": value, "unit": "words/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": value / BASELINE_WORDS_PER_S, "dtype": "int64",
-            "data": "synthetic Europarl-v7-shaped corpus (197 splits, 1,965,734 lines, 49,158,635 words, "
-                    f"{total_bytes} bytes), host-resident pinned splits staged to HBM every step "
-                    "(next step's copy overlaps this step's reduce)",
-            "config": {"model": "wordcount (MapReduce: taskfn/mapfn/partitionfn/reducefn)", "global_batch": 197,
+            "data": (f"synthetic Europarl-v7-shaped corpus ({len(store)} splits, {args.lines:,} lines, "
+                     f"{total_words:,} words, {total_bytes} bytes)" + ("" if full else " REDUCED (smoke test only)")
+                     + ", host-resident pinned splits staged to HBM every step (later steps' copies overlap "
+                     "this step's map/reduce)"),
+            "config": {"model": "wordcount (MapReduce: taskfn/mapfn/partitionfn/reducefn)", "global_batch": len(store),
                        "seq_len": 10000, "parallelism": f"dp{world}", "num_reducers": args.reducers,
                        "words": total_words, "bytes": total_bytes, "valid": counted == total_words},
         }
