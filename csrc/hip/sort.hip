@@ -551,8 +551,9 @@ __global__ void composite_key_kernel(const u32* part, const u64* hi, u64 n, u64*
 // download be queued without a host synchronisation to learn the size.
 // 16-byte stores when both ends are 16-byte aligned; system-scope fence at the
 // end so the host sees the data after the stream completes.
+// nelem == nullptr: copy exactly max_bytes (size known on the host)
 __global__ void copy_to_host_kernel(const u8* src, u8* dst, const long long* nelem, u64 elem_size, u64 max_bytes) {
-  u64 nb = (u64)nelem[0] * elem_size;
+  u64 nb = nelem ? (u64)nelem[0] * elem_size : max_bytes;
   if (nb > max_bytes) nb = max_bytes;
   const u64 stride = (u64)gridDim.x * blockDim.x;
   const u64 tid = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -735,6 +736,26 @@ int mr_copy_to_host(const void* src, void* host_dst, const void* nelem, u64 elem
   if (hipHostGetDevicePointer(&dptr, host_dst, 0) != hipSuccess || dptr == nullptr) dptr = host_dst;
   hipLaunchKernelGGL(copy_to_host_kernel, dim3(1024), dim3(256), 0, s, (const u8*)src, (u8*)dptr,
                      (const long long*)nelem, elem_size, max_bytes);
+  return (int)hipGetLastError();
+}
+
+// Device -> pinned-host download on stream s.  Default: shader stores over
+// PCIe (copy_to_host_kernel).  An SDMA download (hipMemcpyAsync) is queued
+// behind every host->device copy issued before it on ANY stream — the engine
+// is shared — so with the next iterations' input copies in flight a 1 MB
+// result download finished 2 ms late instead of after 0.1 ms
+// (tools/d2h_queue_probe.py, profiles/r1/d2h_queue_probe.log).  Mode 1 = SDMA.
+static int g_d2h_mode = 0;
+void mr_set_d2h_mode(int mode) { g_d2h_mode = mode; }
+
+int mr_d2h_async(void* host_dst, const void* src, u64 nbytes, hipStream_t s) {
+  if (nbytes == 0) return 0;
+  if (g_d2h_mode == 1) return (int)hipMemcpyAsync(host_dst, src, nbytes, hipMemcpyDeviceToHost, s);
+  void* dptr = nullptr;
+  if (hipHostGetDevicePointer(&dptr, host_dst, 0) != hipSuccess || dptr == nullptr) dptr = host_dst;
+  const u64 g = (nbytes + 16 * 256 - 1) / (16 * 256);
+  hipLaunchKernelGGL(copy_to_host_kernel, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s, (const u8*)src,
+                     (u8*)dptr, (const long long*)nullptr, (u64)1, nbytes);
   return (int)hipGetLastError();
 }
 

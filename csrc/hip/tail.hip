@@ -211,6 +211,7 @@ int mr_tie_fixup(const void* c, void* hi, void* lo, void* val, void* rep, void* 
 int mr_gather_key_bytes(const void* hi, const void* lo, const void* rep, const void* off, u64 n, const void* src,
                         void* dst, hipStream_t stream);
 int mr_copy_to_host(const void* src, void* host_dst, const void* nelem, u64 elem_size, u64 max_bytes, hipStream_t s);
+int mr_d2h_async(void* host_dst, const void* src, u64 nbytes, hipStream_t s);
 
 enum TailBuf : int {
   TB_HI0, TB_LO0, TB_VAL0, TB_REP0, TB_C, TB_PART0, TB_ZERO /* counter|ghist|pcount|sort ctrs|err|bad */,
@@ -285,11 +286,11 @@ int mr_tail_run(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl,
   if (rc) return rc;
   rc = mr_tail_pack(P(TB_VAL), offs, n, z + TZ_PCOUNT, nparts, z + TZ_BAD, P(TB_PACKED), s);
   if (rc) return rc;
-  rc = (int)hipMemcpyAsync(hp, P(TB_PACKED), mr_tail_pack_bytes(n, nparts), hipMemcpyDeviceToHost, s);
+  rc = mr_d2h_async(hp, P(TB_PACKED), mr_tail_pack_bytes(n, nparts), s);
   if (rc) return rc;
   if (est >= 0) {
     const u64 nb = (u64)est < hb_cap ? (u64)est : hb_cap;
-    if (nb) rc = (int)hipMemcpyAsync(hb, P(TB_BLOB), nb < blob_cap ? nb : blob_cap, hipMemcpyDeviceToHost, s);
+    if (nb) rc = mr_d2h_async(hb, P(TB_BLOB), nb < blob_cap ? nb : blob_cap, s);
   } else {
     rc = mr_copy_to_host(P(TB_BLOB), hb, offs + n, 1, hb_cap, s);
   }

@@ -30,6 +30,8 @@ _SIGS = {
     "mr_wc_map3": [_p, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
     "mr_insert_received": [_p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p, _u64, _i32, _i32, _p],
     "mr_memcpy_async": [_p, _p, _u64, _i32, _p],
+    "mr_d2h_async": [_p, _p, _u64, _p],
+    "mr_set_d2h_mode": [_i32],
     "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64, _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
     "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p],
@@ -98,6 +100,9 @@ def lib():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = _u64 if name in _RESTYPE_U64 else _i32
+        L.mr_set_d2h_mode.restype = None
+        # downloads: shader stores by default, SDMA with MR_D2H=sdma (see sort.hip mr_d2h_async)
+        L.mr_set_d2h_mode(1 if os.environ.get("MR_D2H", "kernel") == "sdma" else 0)
         _LIB = L
     return _LIB
 
@@ -116,7 +121,15 @@ def ptr(t):
 
 
 def stream(device=None):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """Raw hipStream_t of the current stream (torch's raw-stream accessor:
+    torch.cuda.current_stream() builds a Stream object, ~5 us per call)."""
+    if device is None:
+        idx = torch.cuda.current_device()
+    elif isinstance(device, int):
+        idx = device
+    else:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(idx))
 
 
 def stream_ptr(s) -> ctypes.c_void_p:

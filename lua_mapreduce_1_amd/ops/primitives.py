@@ -118,8 +118,13 @@ class HashTable:
             self._pending = []
 
     def _gtab(self):
-        return (_hip.ptr(self.tag), _hip.ptr(self.hi), _hip.ptr(self.lo), _hip.ptr(self.val),
-                _hip.ptr(self.rep), _hip.ptr(self.ctrl))
+        """ctypes pointers of the table columns (cached: the columns of a
+        table never move)."""
+        g = self.__dict__.get("_gtab_ptrs")
+        if g is None or g[0] is not self.tag:
+            g = self._gtab_ptrs = (self.tag, (_hip.ptr(self.tag), _hip.ptr(self.hi), _hip.ptr(self.lo),
+                                              _hip.ptr(self.val), _hip.ptr(self.rep), _hip.ptr(self.ctrl)))
+        return g[1]
 
     # -- inserts -------------------------------------------------------------
     def insert(self, hi: torch.Tensor, lo: torch.Tensor, val: torch.Tensor | None = None,
@@ -231,7 +236,7 @@ class HashTable:
     def stats(self) -> tuple[int, bool]:
         """(occupied slots, overflowed).  Synchronises on GPU."""
         if self.is_cuda:
-            c = self.ctrl.cpu()
+            c = host_read(self.ctrl)
             return int(c[0]) + int(c[_CTRL_SHARD0::_CTRL_STRIDE].sum()), bool(c[1])
         return sum(p[0].size for p in self._pending), False
 
@@ -382,6 +387,32 @@ def gather_key_bytes(hi, lo, rep, src, lengths: torch.Tensor | None = None, capa
     b = key_bytes_list(hi, lo, rep, src)
     blob = torch.frombuffer(bytearray(b"".join(b)), dtype=torch.uint8) if b else torch.zeros(0, dtype=torch.uint8)
     return torch.cat([off, total]), blob
+
+
+_HOST_READ: dict = {}
+
+
+def host_read(t: torch.Tensor) -> np.ndarray:
+    """Small device tensor -> host numpy copy: download on the current stream
+    (mr_d2h_async: shader stores into a reused pinned buffer, so it does not
+    wait behind input copies queued on the shared SDMA engine, as ``.cpu()``
+    does), then wait for the current stream only."""
+    if not t.is_cuda:
+        return t.detach().numpy().copy()
+    t = t.contiguous()
+    nb = t.numel() * t.element_size()
+    buf = _HOST_READ.get(t.device)
+    if buf is None or buf.numel() < nb:
+        buf = torch.empty(max(nb, 1 << 12), dtype=torch.uint8, pin_memory=True)
+        _HOST_READ[t.device] = buf
+    s = torch.cuda.current_stream(t.device)
+    _hip.call("mr_d2h_async", _hip.ptr(buf), _hip.ptr(t), nb, _hip.stream_ptr(s))
+    s.synchronize()
+    return buf[:nb].numpy().view(_NP_DTYPE[t.dtype]).reshape(tuple(t.shape)).copy()
+
+
+_NP_DTYPE = {torch.int64: np.int64, torch.int32: np.int32, torch.uint8: np.uint8, torch.float32: np.float32,
+             torch.float64: np.float64, torch.uint32: np.uint32, torch.int16: np.int16}
 
 
 def copy_to_host(t: torch.Tensor, host: torch.Tensor, nelem: torch.Tensor) -> None:

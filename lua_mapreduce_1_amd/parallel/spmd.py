@@ -44,6 +44,8 @@ from . import dist as D
 
 
 N_ARENAS = 3
+_PREFETCH_LATE = os.environ.get("MR_PREFETCH_LATE", "1") == "1"
+_PREFETCH_SINGLE = os.environ.get("MR_PREFETCH_SINGLE", "1") == "1"
 
 
 class _nullctx:
@@ -195,6 +197,7 @@ class SPMDEngine:
         # and runs while this iteration shuffles, reduces and downloads
         self.pipeline = False
         self._pending = None
+        self._rec_tmpl = None
         self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self.streams = ([torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]
                         if self.device.type == "cuda" else [None, None])
@@ -283,7 +286,7 @@ class SPMDEngine:
         """Make iteration q's arena, table and stream current."""
         self.slot, self.tslot = q % N_ARENAS, q % 2
 
-    def _plan_chunks(self, ids: list[int], slot: int):
+    def _plan_chunks(self, ids: list[int], slot: int, single: bool = False):
         """Chunking of a contiguous split range (cached per range): boundaries
         at split boundaries, sizes ramping up (the first copy is exposed), big
         in the middle, ramping down at the end (the last kernel is exposed) —
@@ -302,6 +305,8 @@ class SPMDEngine:
         up = list(self.chunk_bytes[:-1])
         big = self.chunk_bytes[-1]
         tail = list(self.tail_bytes)
+        if single:  # prefetched copies: landed long before the map, one DMA is enough
+            up, big, tail = [], max(nbytes, 1), []
         ts = sum(tail)
         while up and rem > up[0] + ts:
             sizes.append(up.pop(0))
@@ -329,11 +334,24 @@ class SPMDEngine:
             events.append(torch.cuda.Event() if self.copy_stream is not None else None)
         return bounds, views, host_views, events
 
-    def _get_plan(self, ids: list[int], slot: int):
-        key = (ids[0], len(ids), slot)
+    def _get_plan(self, ids: list[int], slot: int, single: bool = False):
+        key = (ids[0], len(ids), slot, single)
         plan = self._plans.get(key)
+        if plan is None and self.copy_stream is not None and self._can_pipeline() and not getattr(
+                self, "_priming", False):
+            # a pure taskfn maps the same splits every iteration: build (and
+            # prime) both copy plans of every arena now, so that no plan is
+            # first used — and primed — inside a later, timed iteration
+            self._priming = True
+            try:
+                for sl in range(N_ARENAS):
+                    for sg in (False, True):
+                        self._get_plan(ids, sl, sg)
+            finally:
+                self._priming = False
+            return self._plans[key]
         if plan is None:
-            plan = self._plan_chunks(ids, slot)
+            plan = self._plan_chunks(ids, slot, single)
             self._plans[key] = plan
             if self.copy_stream is not None:
                 # the first two rounds of a plan's copies behind a cross-stream
@@ -381,7 +399,7 @@ class SPMDEngine:
         ids = self._split_ids(jobs, j0, j1)
         if not ids or aslot in self._inflight:
             return
-        plan = self._get_plan(ids, aslot)
+        plan = self._get_plan(ids, aslot, single=_PREFETCH_SINGLE)
         # arenas[aslot] was last read by iteration q - N_ARENAS, which has
         # completed (its finalize synchronised): no stream dependency needed
         self._issue_copies(plan)
@@ -393,12 +411,13 @@ class SPMDEngine:
             ids = self._split_ids(jobs, j0, j1)
             if not ids:
                 return
-            plan = self._get_plan(ids, self.slot)
-            bounds, views, host_views, events = plan
             cs = self.copy_stream
+            prefetched = cs is not None and self._inflight.pop(self.slot, None) == (ids[0], len(ids))
+            plan = self._get_plan(ids, self.slot, single=prefetched and _PREFETCH_SINGLE)
+            bounds, views, host_views, events = plan
             if cs is not None:
                 cur = torch.cuda.current_stream(self.device)
-                if self._inflight.pop(self.slot, None) != (ids[0], len(ids)):  # else: prefetched, in flight
+                if not prefetched:
                     with trace.range("mr.copies"):
                         self._issue_copies(plan, wait_for=cur)
                 # chunks whose copies have already landed (prefetched during the
@@ -494,7 +513,7 @@ class SPMDEngine:
             recv = D.exchange_counts(xchg, self.group)
             if before_sync is not None:
                 before_sync()  # host work that overlaps the pack and count exchange
-            send_h, recv_h = torch.cat([xchg, recv]).view(2, W, 3).cpu().tolist()  # one host sync
+            send_h, recv_h = self._host_counts(xchg, recv, W)  # one host sync
             self._failed_total = sum(r[2] for r in recv_h)
             send_sz = [SH.seg_bytes(r[0], r[1]) for r in send_h]
             recv_sz = [SH.seg_bytes(r[0], r[1]) for r in recv_h]
@@ -502,7 +521,7 @@ class SPMDEngine:
             return rbuf, recv.view(W, 3), sum(r[0] for r in recv_h)
         rec, blob, xchg = SH.pack_by_dest(hi, lo, val, rep, part, W, src, extra=failed)
         recv = D.exchange_counts(xchg, self.group)
-        both = torch.cat([xchg, recv]).view(2, W, 3).cpu().tolist()  # one host sync
+        both = self._host_counts(xchg, recv, W)  # one host sync
         send_h, recv_h = both
         self._failed_total = sum(r[2] for r in recv_h)
         send_rows, send_bytes = [r[0] for r in send_h], [r[1] for r in send_h]
@@ -511,6 +530,12 @@ class SPMDEngine:
         rblob = D.all_to_all_v(blob[:sum(send_bytes)], send_bytes, recv_bytes, self.group)
         rrep = SH.absolute_reps(rrec, recv_rows, recv_bytes)
         return rrec[:, 0].contiguous(), rrec[:, 1].contiguous(), rrec[:, 2].contiguous(), rrep, rblob
+
+    @staticmethod
+    def _host_counts(xchg, recv, W: int):
+        """[send, recv] count rows on the host (one download + stream wait)."""
+        both = torch.cat([xchg, recv]).view(2, W, 3)
+        return (ops.host_read(both) if both.is_cuda else both.numpy()).tolist()
 
     def _fused_tail_ok(self) -> bool:
         """The fused tail kernels need a GPU, the built-in FNV-1 partitioner
@@ -605,7 +630,7 @@ class SPMDEngine:
         and stream were last used by iteration q-1, which has fully completed
         (its results were downloaded)."""
         self._prefetch(jobs, j0, j1, q + 1)
-        recs = [JobRecord(k, v) for k, v in jobs]
+        recs = self._new_records(jobs, j0, j1)
         self._use(q + 1)
         try:
             with torch.cuda.stream(self.streams[self.tslot]):
@@ -619,6 +644,18 @@ class SPMDEngine:
     def run_iteration(self, prefetch_next: bool | None = None, lookahead: int | None = None) -> IterationResult:
         with trace.range("mr.iteration"):
             return self._run_iteration(prefetch_next, lookahead)
+
+    def _new_records(self, jobs, j0: int, j1: int) -> list[JobRecord]:
+        """Fresh records for this rank's jobs [j0, j1); the other ranks' jobs
+        share WAITING records that nothing mutates (cached per job list: a
+        record per job per iteration cost ~40 us of host time at 8 ranks)."""
+        tmpl = self._rec_tmpl
+        if tmpl is None or tmpl[0] is not jobs:
+            tmpl = self._rec_tmpl = (jobs, [JobRecord(k, v) for k, v in jobs])
+        recs = list(tmpl[1])
+        for j in range(j0, j1):
+            recs[j] = JobRecord(*jobs[j])
+        return recs
 
     def _run_iteration(self, prefetch_next, lookahead) -> IterationResult:
         """One MapReduce iteration.  ``prefetch_next`` (default ``self.prefetch``)
@@ -644,8 +681,8 @@ class SPMDEngine:
         else:
             trace.push("mr.jobs")
             jobs = self._jobs()
-            recs = [JobRecord(k, v) for k, v in jobs]
             j0, j1 = self._assign(jobs)
+            recs = self._new_records(jobs, j0, j1)
             trace.pop()
             stream = self.streams[self.tslot] if ahead and self.pipeline else None
         res.map_jobs = recs
@@ -656,16 +693,28 @@ class SPMDEngine:
                 t0 = time.time()
                 with trace.range("mr.map.issue"):
                     self._run_map(jobs, recs, j0, j1)
-            # the arenas of q+1..q+ahead are free (iterations up to q-1
-            # completed): their copies queue behind this iteration's (the
-            # copy stream is FIFO), so the copy engine never idles
-            trace.push("mr.prefetch")
-            for k in range(1, ahead + 1):
-                self._prefetch(jobs, j0, j1, q + k)
-            trace.pop()
-            return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, ahead > 0, q)
+            if ahead and not _PREFETCH_LATE:
+                self._prefetch_ahead(jobs, j0, j1, q, ahead)
+            elif ahead and (q + 1) % N_ARENAS not in self._inflight:
+                # nothing queued behind this iteration's copies: start q+1's
+                # now, or the copy engine idles through this map
+                self._prefetch(jobs, j0, j1, q + 1)
+            return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, ahead, q)
 
-    def _finish_iteration(self, res, T, t_start, t0, jobs, recs, j0, j1, prefetch_next, q) -> IterationResult:
+    def _prefetch_ahead(self, jobs, j0, j1, q: int, ahead: int) -> None:
+        """Copies of iterations q+1..q+ahead (their arenas are free: iterations
+        up to q-1 completed).  Issued once this iteration's tail is queued —
+        the host would otherwise wait for the tail there, and the copy stream
+        still holds the rest of q+1's copies, so the engine does not idle."""
+        trace.push("mr.prefetch")
+        mapped = self._pending["q"] if self._pending is not None else q
+        for k in range(1, ahead + 1):
+            if q + k > mapped:  # an issued map already consumed its copies
+                self._prefetch(jobs, j0, j1, q + k)
+        trace.pop()
+
+    def _finish_iteration(self, res, T, t_start, t0, jobs, recs, j0, j1, ahead, q) -> IterationResult:
+        prefetch_next = ahead > 0
         trace.push("mr.map.wait")
         n_claimed, overflow = self.table.stats()   # synchronises the map phase
         trace.pop()
@@ -725,6 +774,8 @@ class SPMDEngine:
         if pend is None:
             pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
         issue_next_map()
+        if _PREFETCH_LATE:
+            self._prefetch_ahead(jobs, j0, j1, q, ahead)
 
         with trace.range("mr.finalize_host"):
             cols = devmod.finalize_host(pend, self.partmod)

@@ -176,14 +176,16 @@ _BLOB_EST: dict = {}  # device -> expected key-blob bytes of the next finalize()
 
 
 def dma_to_host(dst: torch.Tensor, src: torch.Tensor) -> None:
-    """Queue a device -> pinned-host DMA of ``src`` into ``dst`` on the current
-    stream (direct hipMemcpyAsync: torch's non_blocking copy_ also records an
-    event for the pinned block in its host allocator on every call, and that
-    event pool's growth stalled the host for ~5 ms now and then)."""
+    """Queue a device -> pinned-host download of ``src`` into ``dst`` on the
+    current stream (mr_d2h_async: shader stores, so it is not queued behind
+    the input copies of later iterations on the shared SDMA engine; and not
+    torch's non_blocking copy_, which also records an event for the pinned
+    block in its host allocator on every call — that event pool's growth
+    stalled the host for ~5 ms now and then)."""
     from ..ops import _hip
     assert src.is_contiguous() and dst.is_contiguous() and dst.numel() * dst.element_size() >= \
         src.numel() * src.element_size()
-    _hip.call("mr_memcpy_async", _hip.ptr(dst), _hip.ptr(src), src.numel() * src.element_size(), 2,
+    _hip.call("mr_d2h_async", _hip.ptr(dst), _hip.ptr(src), src.numel() * src.element_size(),
               _hip.stream(src.device))
 
 
