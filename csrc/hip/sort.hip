@@ -759,6 +759,36 @@ int mr_d2h_async(void* host_dst, const void* src, u64 nbytes, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Host -> device copy by shader loads from pinned host memory (the
+// alternative to an SDMA transfer; tools/h2d_probe.py compares them).
+__global__ void __launch_bounds__(256) h2d_pull_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                       u64 n16, const u8* __restrict__ src_b, u8* __restrict__ dst_b,
+                                                       u64 nbytes) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  const u64 tid = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  u64 i = tid;
+  for (; i + 3 * stride < n16; i += 4 * stride) {  // four independent 16-byte loads in flight per thread
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+  for (u64 j = n16 * 16 + tid; j < nbytes; j += stride) dst_b[j] = src_b[j];
+}
+
+int mr_h2d_pull(void* dst, const void* host_src, u64 nbytes, int blocks, hipStream_t s) {
+  if (nbytes == 0) return 0;
+  void* sp = nullptr;
+  if (hipHostGetDevicePointer(&sp, const_cast<void*>(host_src), 0) != hipSuccess || sp == nullptr)
+    sp = const_cast<void*>(host_src);
+  if ((((uintptr_t)sp | (uintptr_t)dst) & 15) != 0) return -1;
+  hipLaunchKernelGGL(h2d_pull_kernel, dim3(blocks > 0 ? blocks : 2048), dim3(256), 0, s, (const uint4*)sp,
+                     (uint4*)dst, nbytes / 16, (const u8*)sp, (u8*)dst, nbytes);
+  return (int)hipGetLastError();
+}
+
 // Async DMA between pinned host memory and HBM (kind: 1 = H2D, 2 = D2H).
 // Used instead of torch's copy_ for the input staging: copy_ also records an
 // event for the pinned block in torch's host allocator on every call, and the

@@ -31,6 +31,7 @@ _SIGS = {
     "mr_insert_received": [_p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p, _u64, _i32, _i32, _p],
     "mr_memcpy_async": [_p, _p, _u64, _i32, _p],
     "mr_d2h_async": [_p, _p, _u64, _p],
+    "mr_h2d_pull": [_p, _p, _u64, _i32, _p],
     "mr_set_d2h_mode": [_i32],
     "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64, _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],

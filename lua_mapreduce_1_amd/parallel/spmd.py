@@ -44,7 +44,7 @@ from . import dist as D
 
 
 N_ARENAS = 3
-_PREFETCH_LATE = os.environ.get("MR_PREFETCH_LATE", "1") == "1"
+_PREFETCH_LATE = os.environ.get("MR_PREFETCH_LATE", "0") == "1"
 _PREFETCH_SINGLE = os.environ.get("MR_PREFETCH_SINGLE", "1") == "1"
 
 
@@ -509,15 +509,19 @@ class SPMDEngine:
             # GPU: records and key bytes in ONE buffer of per-destination
             # segments -> one payload all-to-all; the receive-side insert
             # kernel locates records and bytes from the exchanged counts
-            buf, xchg = SH.pack_by_dest_combined(hi, lo, val, rep, part, W, src, extra=failed)
-            recv = D.exchange_counts(xchg, self.group)
+            with trace.range("mr.pack"):
+                buf, xchg = SH.pack_by_dest_combined(hi, lo, val, rep, part, W, src, extra=failed)
+            with trace.range("mr.count_exchange"):
+                recv = D.exchange_counts(xchg, self.group)
             if before_sync is not None:
                 before_sync()  # host work that overlaps the pack and count exchange
-            send_h, recv_h = self._host_counts(xchg, recv, W)  # one host sync
+            with trace.range("mr.count_sync"):
+                send_h, recv_h = self._host_counts(xchg, recv, W)  # one host sync
             self._failed_total = sum(r[2] for r in recv_h)
             send_sz = [SH.seg_bytes(r[0], r[1]) for r in send_h]
             recv_sz = [SH.seg_bytes(r[0], r[1]) for r in recv_h]
-            rbuf = D.all_to_all_v(buf[:sum(send_sz)], send_sz, recv_sz, self.group)
+            with trace.range("mr.all_to_all"):
+                rbuf = D.all_to_all_v(buf[:sum(send_sz)], send_sz, recv_sz, self.group)
             return rbuf, recv.view(W, 3), sum(r[0] for r in recv_h)
         rec, blob, xchg = SH.pack_by_dest(hi, lo, val, rep, part, W, src, extra=failed)
         recv = D.exchange_counts(xchg, self.group)
@@ -567,7 +571,8 @@ class SPMDEngine:
             else:
                 self.red_table.reset()
             self.red_table.insert_received(rbuf, recv_counts, self.world, rows=rows)
-            m, ovf = self.red_table.stats()
+            with trace.range("mr.reduce_sync"):
+                m, ovf = self.red_table.stats()
             if not ovf and m <= cap // 2:
                 self._red_distinct = m
                 return m
@@ -753,7 +758,8 @@ class SPMDEngine:
             # compact + FNV partition in one kernel (the send side of the shuffle)
             if overflow:
                 raise OverflowError("hash table overflow")
-            hi, lo, val, rep, part = devmod.compact_partition(self.table, n_claimed, src, self.nparts)
+            with trace.range("mr.compact"):
+                hi, lo, val, rep, part = devmod.compact_partition(self.table, n_claimed, src, self.nparts)
         else:
             hi, lo, val, rep = self.table.compact((n_claimed, overflow))
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
@@ -763,7 +769,8 @@ class SPMDEngine:
                 src, rcounts, rows = self._shuffle(hi, lo, val, rep, src, part, failed, raw=True,
                                                   before_sync=issue_next_map)
                 n_red = self._reduce_insert_received(src, rcounts, rows)
-                pend = self._finalize_table(self.red_table, n_red, src)
+                with trace.range("mr.tail_issue"):
+                    pend = self._finalize_table(self.red_table, n_red, src)
             else:
                 hi, lo, val, rep, src = self._shuffle(hi, lo, val, rep, src, part, failed)
                 hi, lo, val, rep = self._reduce(hi, lo, val, rep, src)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# host-side cost of the 8-rank loopback proxy: cProfile + roctx phase ranges
+# host-side cost of the 8-rank loopback proxy: cProfile + roctx phase ranges with the kernel trace
 set -e
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"

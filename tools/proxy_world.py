@@ -78,7 +78,7 @@ def main() -> int:
     if prof is not None:
         import pstats
         prof.disable()
-        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
+        pstats.Stats(prof, stream=sys.stderr).sort_stats(os.environ.get("MR_CPROFILE_SORT", "tottime")).print_stats(45)
     seq = [round(x, 2) for x in per]
     per.sort()
     print(json.dumps({"world": W, "ms_per_step": ms, "median": per[len(per) // 2], "min": per[0], "seq": seq,
