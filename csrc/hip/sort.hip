@@ -16,6 +16,7 @@
 // lanes_below).  Tiles are ITEMS = 16 x 256 keys; keys are visited round by
 // round (item = round*256 + thread) so a tile keeps input order (stability).
 #include <hip/hip_runtime.h>
+#include <cstring>
 #include "mr_common.h"
 
 namespace mr {
@@ -756,6 +757,31 @@ int mr_d2h_async(void* host_dst, const void* src, u64 nbytes, hipStream_t s) {
   const u64 g = (nbytes + 16 * 256 - 1) / (16 * 256);
   hipLaunchKernelGGL(copy_to_host_kernel, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s, (const u8*)src,
                      (u8*)dptr, (const long long*)nullptr, (u64)1, nbytes);
+  return (int)hipGetLastError();
+}
+
+// Host-visible completion flags.  A waiting host that sleeps in
+// hipStreamSynchronize wakes ~20 us (short waits) to ~130 us (long waits)
+// after the GPU work ended (tools/host_gpu_timeline.py); the engine's four
+// per-iteration waits instead spin on a word of coherent pinned memory that a
+// one-thread kernel queued behind the awaited work stores with release
+// semantics at system scope.
+__global__ void signal_host_kernel(unsigned int* flag, unsigned int seq) {
+  __threadfence_system();
+  __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void* mr_host_alloc_coherent(u64 nbytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, nbytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
+  memset(p, 0, nbytes);
+  return p;
+}
+
+int mr_signal_host(void* flag_host, unsigned int seq, hipStream_t s) {
+  void* dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, flag_host, 0) != hipSuccess || dp == nullptr) return -1;
+  hipLaunchKernelGGL(signal_host_kernel, dim3(1), dim3(1), 0, s, (unsigned int*)dp, seq);
   return (int)hipGetLastError();
 }
 

@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import time
 
 import torch  # noqa: F401  (must be imported first: provides libamdhip64.so.7)
 
@@ -32,6 +33,7 @@ _SIGS = {
     "mr_memcpy_async": [_p, _p, _u64, _i32, _p],
     "mr_d2h_async": [_p, _p, _u64, _p],
     "mr_h2d_pull": [_p, _p, _u64, _i32, _p],
+    "mr_signal_host": [_p, _u32, _p],
     "mr_set_d2h_mode": [_i32],
     "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64, _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
@@ -102,6 +104,8 @@ def lib():
             f.argtypes = args
             f.restype = _u64 if name in _RESTYPE_U64 else _i32
         L.mr_set_d2h_mode.restype = None
+        L.mr_host_alloc_coherent.argtypes = [_u64]
+        L.mr_host_alloc_coherent.restype = _p
         # downloads: shader stores by default, SDMA with MR_D2H=sdma (see sort.hip mr_d2h_async)
         L.mr_set_d2h_mode(1 if os.environ.get("MR_D2H", "kernel") == "sdma" else 0)
         _LIB = L
@@ -146,3 +150,55 @@ def check(rc: int, what: str) -> None:
 def call(name: str, *args) -> None:
     rc = getattr(lib(), name)(*args)
     check(rc, name)
+
+
+class _HostFlags:
+    """Completion flags in coherent pinned memory, one word per stream."""
+
+    def __init__(self):
+        import numpy as np
+        self.nslots = 1024
+        p = lib().mr_host_alloc_coherent(4 * self.nslots)
+        if not p:
+            raise RuntimeError("hipHostMalloc of the completion flags failed")
+        self.base = p
+        self.words = np.ctypeslib.as_array((ctypes.c_uint32 * self.nslots).from_address(p))
+        self.slot: dict = {}
+        self.seq = 0
+
+
+_FLAGS = None
+SPIN_S = float(os.environ.get("MR_SPIN_US", "2000")) * 1e-6
+
+
+def wait_stream(device=None) -> None:
+    """Wait for the work queued so far on the current stream: a one-thread
+    kernel behind it stores a sequence number into coherent pinned memory
+    (mr_signal_host) and the host spins on that word — no sleep/interrupt
+    wake-up.  After ``MR_SPIN_US`` (2000) of spinning, falls back to
+    hipStreamSynchronize (which also reports a failed kernel).
+    ``MR_SPIN_US=0``: always hipStreamSynchronize."""
+    global _FLAGS
+    if SPIN_S <= 0:
+        torch.cuda.current_stream(device).synchronize()
+        return
+    if _FLAGS is None:
+        _FLAGS = _HostFlags()
+    F = _FLAGS
+    sp = stream(device)
+    k = F.slot.get(sp.value)
+    if k is None:
+        k = F.slot[sp.value] = len(F.slot) % F.nslots
+    F.seq = (F.seq + 1) & 0x7FFFFFFF or 1
+    seq = F.seq
+    call("mr_signal_host", ctypes.c_void_p(F.base + 4 * k), seq, sp)
+    w = F.words
+    if w[k] == seq:
+        return
+    t_end = time.perf_counter() + SPIN_S
+    n = 0
+    while w[k] != seq:
+        n += 1
+        if (n & 255) == 0 and time.perf_counter() > t_end:
+            torch.cuda.current_stream(device).synchronize()
+            return

@@ -405,9 +405,8 @@ def host_read(t: torch.Tensor) -> np.ndarray:
     if buf is None or buf.numel() < nb:
         buf = torch.empty(max(nb, 1 << 12), dtype=torch.uint8, pin_memory=True)
         _HOST_READ[t.device] = buf
-    s = torch.cuda.current_stream(t.device)
-    _hip.call("mr_d2h_async", _hip.ptr(buf), _hip.ptr(t), nb, _hip.stream_ptr(s))
-    s.synchronize()
+    _hip.call("mr_d2h_async", _hip.ptr(buf), _hip.ptr(t), nb, _hip.stream(t.device))
+    _hip.wait_stream(t.device)
     return buf[:nb].numpy().view(_NP_DTYPE[t.dtype]).reshape(tuple(t.shape)).copy()
 
 

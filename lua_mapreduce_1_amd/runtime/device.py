@@ -398,7 +398,8 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
     n, nparts = pend["n"], pend["nparts"]
     hi, lo = pend["hi"], pend["lo"]
     if hi.is_cuda:
-        torch.cuda.current_stream(hi.device).synchronize()
+        from ..ops import _hip
+        _hip.wait_stream(hi.device)
         hb, est, blob = pend["hb"], pend["est"], pend["blob"]
         if pend.get("fused"):
             f_val, f_off, f_counts, f_bad = _unpack_fused(pend)

@@ -60,6 +60,10 @@ def main() -> int:
     gc.collect()
     gc.freeze()
     torch.cuda.synchronize()
+    if os.environ.get("MR_HOT_CPU"):  # diagnosis only: is the first timed step slow because the core idled?
+        t_hot = time.perf_counter() + float(os.environ["MR_HOT_CPU"]) * 1e-3
+        while time.perf_counter() < t_hot:
+            pass
     per = []
     prof = None
     if os.environ.get("MR_CPROFILE"):
