@@ -193,12 +193,18 @@ def wait_stream(device=None) -> None:
     seq = F.seq
     call("mr_signal_host", ctypes.c_void_p(F.base + 4 * k), seq, sp)
     w = F.words
-    if w[k] == seq:
-        return
-    t_end = time.perf_counter() + SPIN_S
-    n = 0
-    while w[k] != seq:
-        n += 1
-        if (n & 255) == 0 and time.perf_counter() > t_end:
-            torch.cuda.current_stream(device).synchronize()
-            return
+    if WAIT_LOG is not None:
+        t_a = time.perf_counter()
+    if w[k] != seq:
+        t_end = time.perf_counter() + SPIN_S
+        n = 0
+        while w[k] != seq:
+            n += 1
+            if (n & 255) == 0 and time.perf_counter() > t_end:
+                torch.cuda.current_stream(device).synchronize()
+                break
+    if WAIT_LOG is not None:
+        WAIT_LOG.append((t_a, time.perf_counter(), bool(w[k] == seq)))
+
+
+WAIT_LOG = [] if os.environ.get("MR_WAIT_LOG") else None  # (start, end, flag seen) of each wait_stream

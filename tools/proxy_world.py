@@ -70,6 +70,9 @@ def main() -> int:
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+    from lua_mapreduce_1_amd.ops import _hip
+    if _hip.WAIT_LOG is not None:
+        _hip.WAIT_LOG.clear()
     t0 = time.perf_counter()
     for i in range(a.steps):
         t1 = time.perf_counter()
@@ -83,6 +86,10 @@ def main() -> int:
         import pstats
         prof.disable()
         pstats.Stats(prof, stream=sys.stderr).sort_stats(os.environ.get("MR_CPROFILE_SORT", "tottime")).print_stats(45)
+    if _hip.WAIT_LOG is not None:
+        for ta, tb, ok in _hip.WAIT_LOG[:12]:
+            print(f"wait_stream at {1e6 * (ta - t0):9.1f} us: {1e6 * (tb - ta):7.1f} us (flag seen {ok})",
+                  file=sys.stderr)
     seq = [round(x, 2) for x in per]
     per.sort()
     print(json.dumps({"world": W, "ms_per_step": ms, "median": per[len(per) // 2], "min": per[0], "seq": seq,
