@@ -375,3 +375,38 @@ def test_fused_tail_matches_unfused(gpu, nparts):
     assert np.array_equal(a["val"], b["val"])
     assert np.array_equal(np.asarray(a["key_off"], np.int64), np.asarray(b["key_off"], np.int64))
     assert a["key_blob"].tobytes() == b["key_blob"].tobytes()
+
+
+@pytest.mark.parametrize("nbytes", [1, 37, 4096, 5 << 20])
+def test_downloads_and_host_waits(gpu, nbytes):
+    """mr_d2h_async (shader stores into pinned memory) + wait_stream (spin on
+    the completion word) deliver exactly the device bytes, also behind a
+    queued kernel and with large H2D copies in flight on another stream."""
+    from lua_mapreduce_1_amd.ops import _hip
+    from lua_mapreduce_1_amd.runtime import device as devmod
+    g = torch.Generator(device="cpu").manual_seed(nbytes)
+    src_h = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, generator=g)
+    d = src_h.to(gpu)
+    big_h = torch.empty(64 << 20, dtype=torch.uint8, pin_memory=True)
+    big_d = torch.empty_like(big_h, device=gpu)
+    cs = torch.cuda.Stream(gpu)
+    _hip.call("mr_memcpy_async", _hip.ptr(big_d), _hip.ptr(big_h), big_h.numel(), 1, _hip.stream_ptr(cs))
+    d.add_(1)  # a kernel the download must wait for
+    out = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    devmod.dma_to_host(out, d)
+    _hip.wait_stream(gpu)
+    assert torch.equal(out, src_h + 1)
+    # small reads of typed tensors
+    t = torch.arange(3 * 8, dtype=torch.int64, device=gpu).view(2, 4, 3) * 7
+    assert np.array_equal(ops.host_read(t), t.cpu().numpy())
+    torch.cuda.synchronize()
+
+
+def test_h2d_pull_matches_copy(gpu):
+    from lua_mapreduce_1_amd.ops import _hip
+    n = (3 << 20) + 45
+    h = torch.randint(0, 256, (n,), dtype=torch.uint8).pin_memory()
+    d = torch.zeros(n, dtype=torch.uint8, device=gpu)
+    _hip.call("mr_h2d_pull", _hip.ptr(d), _hip.ptr(h), n, 512, _hip.stream(gpu))
+    torch.cuda.synchronize()
+    assert torch.equal(d.cpu(), h)
