@@ -100,15 +100,19 @@ def main() -> int:
     # ... and pipelined: iteration i+1's map runs on a second stream while
     # iteration i shuffles, reduces and downloads its results
     eng.pipeline = os.environ.get("MR_PIPELINE", "1") != "0"
+    # long-lived objects (modules, corpus, engine) move to the permanent GC
+    # generation: a full collection over them stalled an iteration by ~5 ms
+    # every few dozen iterations (the per-iteration host work is ~1 ms at 8
+    # GPUs).  Collected BEFORE the warm-up: the heap walk evicts the CPU caches,
+    # and right before the timed region it made the first step's host work
+    # 2-4x slower (8-rank proxy: first step 2.2 -> 1.7 ms)
+    gc.collect()
+    gc.freeze()
     # the last warm-up step starts nothing for the next one: every copy and map
     # of the K timed iterations happens inside the timed region
     for w in range(args.warmup):
         eng.run_iteration(prefetch_next=w < args.warmup - 1, lookahead=args.warmup - 1 - w)
-    # long-lived objects (modules, corpus, engine) move to the permanent GC
-    # generation: a full collection over them stalled an iteration by ~5 ms
-    # every few dozen iterations (the per-iteration host work is ~1 ms at 8 GPUs)
-    gc.collect()
-    gc.freeze()
+    gc.freeze()  # the warm-up's survivors too (no heap walk)
     D.barrier(device=device)
     if device.type == "cuda":
         torch.cuda.synchronize(device)

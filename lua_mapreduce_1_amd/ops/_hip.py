@@ -148,8 +148,19 @@ def check(rc: int, what: str) -> None:
 
 
 def call(name: str, *args) -> None:
-    rc = getattr(lib(), name)(*args)
+    if _TLOG is not None:
+        t = time.perf_counter()
+        rc = getattr(lib(), name)(*args)
+        _TLOG.append(("hip:" + name, t, time.perf_counter()))
+    else:
+        rc = getattr(lib(), name)(*args)
     check(rc, name)
+
+
+_TLOG = None
+if os.environ.get("MR_HOST_TIMELINE_HIP"):  # every native call in the host timeline (utils/trace.LOG)
+    from ..utils import trace as _trace
+    _TLOG = _trace.LOG
 
 
 class _HostFlags:

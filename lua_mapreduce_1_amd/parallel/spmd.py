@@ -689,7 +689,9 @@ class SPMDEngine:
             j0, j1 = self._assign(jobs)
             recs = self._new_records(jobs, j0, j1)
             trace.pop()
-            stream = self.streams[self.tslot] if ahead and self.pipeline else None
+            # the pipeline streams also when nothing is started ahead (the last
+            # warm-up step): the first timed step then launches on warm streams
+            stream = self.streams[self.tslot] if self.pipeline and self._can_pipeline() else None
         res.map_jobs = recs
         with torch.cuda.stream(stream) if stream is not None else _nullctx():
             if pending is None:

@@ -18,9 +18,14 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
+import time
 
 _LIB = None
 _ENABLED = os.environ.get("MR_ROCTX", "0") == "1"
+# host-only timeline without a profiler: MR_HOST_TIMELINE=1 records
+# (name, start, end) perf_counter stamps of every range into LOG
+LOG: list | None = [] if os.environ.get("MR_HOST_TIMELINE") else None
+_STACK: list = []
 _CANDIDATES = ("librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so", "libroctx64.so.4", "libroctx64.so")
 
 
@@ -58,11 +63,16 @@ def enable(on: bool = True) -> bool:
 
 
 def push(name: str) -> None:
+    if LOG is not None:
+        _STACK.append((name, time.perf_counter()))
     if _ENABLED and _lib():
         _LIB.roctxRangePushA(name.encode())
 
 
 def pop() -> None:
+    if LOG is not None and _STACK:
+        name, t = _STACK.pop()
+        LOG.append((name, t, time.perf_counter()))
     if _ENABLED and _LIB:
         _LIB.roctxRangePop()
 
@@ -74,7 +84,7 @@ def mark(name: str) -> None:
 
 @contextlib.contextmanager
 def range(name: str):  # noqa: A001 - mirrors the roctx name
-    if not _ENABLED:
+    if not _ENABLED and LOG is None:
         yield
         return
     push(name)

@@ -54,10 +54,15 @@ def main() -> int:
     assert eng.world == W and eng.rank == 0
     eng.prefetch = True
     eng.pipeline = os.environ.get("MR_PIPELINE", "1") != "0"
+    import gc
+    gc_early = os.environ.get("MR_GC_EARLY", "1") == "1"  # as bench.py
+    if gc_early:  # collect before the warm-up: the heap walk evicts the caches the timed steps run from
+        gc.collect()
+        gc.freeze()
     for w in range(a.warmup):
         eng.run_iteration(prefetch_next=w < a.warmup - 1, lookahead=a.warmup - 1 - w)
-    import gc
-    gc.collect()
+    if not gc_early:
+        gc.collect()
     gc.freeze()
     torch.cuda.synchronize()
     if os.environ.get("MR_HOT_CPU"):  # diagnosis only: is the first timed step slow because the core idled?
@@ -74,10 +79,20 @@ def main() -> int:
     if _hip.WAIT_LOG is not None:
         _hip.WAIT_LOG.clear()
     t0 = time.perf_counter()
+    prof_at = {int(x) for x in os.environ.get("MR_CPROFILE_ITERS", "").split(",") if x}
     for i in range(a.steps):
         t1 = time.perf_counter()
+        if i in prof_at:  # cProfile of single iterations (first timed vs steady state)
+            import cProfile
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
         res = eng.run_iteration(prefetch_next=i < a.steps - 1, lookahead=a.steps - 1 - i)
         per.append(1000 * (time.perf_counter() - t1))
+        if i in prof_at:
+            pr.disable()
+            print(f"== cProfile of timed iteration {i}", file=sys.stderr)
+            pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(18)
         if os.environ.get("MR_PHASES") and i < 3:
             print(i, {k: round(1000 * v, 3) for k, v in res.timings.items()}, file=sys.stderr, flush=True)
     torch.cuda.synchronize()
@@ -90,6 +105,14 @@ def main() -> int:
         for ta, tb, ok in _hip.WAIT_LOG[:12]:
             print(f"wait_stream at {1e6 * (ta - t0):9.1f} us: {1e6 * (tb - ta):7.1f} us (flag seen {ok})",
                   file=sys.stderr)
+    from lua_mapreduce_1_amd.utils import trace
+    if trace.LOG is not None:
+        its = [e for e in trace.LOG if e[0] == "mr.iteration" and e[1] >= t0]
+        for k in (0, 1, len(its) // 2):
+            a, b = its[k][1], its[k][2]
+            print(f"-- host timeline of timed iteration {k} ({1e6 * (b - a):.1f} us)", file=sys.stderr)
+            for name, s0, s1 in sorted((e for e in trace.LOG if a <= e[1] <= b), key=lambda e: e[1]):
+                print(f"   {1e6 * (s0 - a):8.1f} +{1e6 * (s1 - s0):7.1f}  {name}", file=sys.stderr)
     seq = [round(x, 2) for x in per]
     per.sort()
     print(json.dumps({"world": W, "ms_per_step": ms, "median": per[len(per) // 2], "min": per[0], "seq": seq,
