@@ -35,6 +35,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from lua_mapreduce_1_amd.parallel import dist as D  # noqa: E402
+from lua_mapreduce_1_amd.utils.config import TUNABLES  # noqa: E402
 from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore  # noqa: E402
 from lua_mapreduce_1_amd.utils import corpus  # noqa: E402
 
@@ -99,7 +100,7 @@ def main() -> int:
     eng.prefetch = True
     # ... and pipelined: iteration i+1's map runs on a second stream while
     # iteration i shuffles, reduces and downloads its results
-    eng.pipeline = os.environ.get("MR_PIPELINE", "1") != "0"
+    eng.pipeline = TUNABLES.pipeline  # MR_PIPELINE
     # long-lived objects (modules, corpus, engine) move to the permanent GC
     # generation: a full collection over them stalled an iteration by ~5 ms
     # every few dozen iterations (the per-iteration host work is ~1 ms at 8

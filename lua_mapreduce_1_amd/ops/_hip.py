@@ -15,6 +15,7 @@ import time
 import torch  # noqa: F401  (must be imported first: provides libamdhip64.so.7)
 
 from .. import _build
+from ..utils.config import TUNABLES
 
 _LOCK = threading.Lock()
 _LIB = None
@@ -107,7 +108,7 @@ def lib():
         L.mr_host_alloc_coherent.argtypes = [_u64]
         L.mr_host_alloc_coherent.restype = _p
         # downloads: shader stores by default, SDMA with MR_D2H=sdma (see sort.hip mr_d2h_async)
-        L.mr_set_d2h_mode(1 if os.environ.get("MR_D2H", "kernel") == "sdma" else 0)
+        L.mr_set_d2h_mode(1 if TUNABLES.d2h == "sdma" else 0)
         _LIB = L
     return _LIB
 
@@ -158,7 +159,7 @@ def call(name: str, *args) -> None:
 
 
 _TLOG = None
-if os.environ.get("MR_HOST_TIMELINE_HIP"):  # every native call in the host timeline (utils/trace.LOG)
+if TUNABLES.host_timeline_hip:  # every native call in the host timeline (utils/trace.LOG)
     from ..utils import trace as _trace
     _TLOG = _trace.LOG
 
@@ -179,7 +180,7 @@ class _HostFlags:
 
 
 _FLAGS = None
-SPIN_S = float(os.environ.get("MR_SPIN_US", "2000")) * 1e-6
+SPIN_S = TUNABLES.spin_us * 1e-6
 
 
 def wait_stream(device=None) -> None:
@@ -218,4 +219,4 @@ def wait_stream(device=None) -> None:
         WAIT_LOG.append((t_a, time.perf_counter(), bool(w[k] == seq)))
 
 
-WAIT_LOG = [] if os.environ.get("MR_WAIT_LOG") else None  # (start, end, flag seen) of each wait_stream
+WAIT_LOG = [] if TUNABLES.wait_log else None  # (start, end, flag seen) of each wait_stream

@@ -24,6 +24,7 @@ import torch
 
 from . import keys as K
 from . import _hip
+from ..utils.config import TUNABLES
 
 import os as _os
 
@@ -31,7 +32,7 @@ OPS = {"sum": 0, "min": 1, "max": 2}
 # MR_DEBUG_CHECKS=1: validate the offsets/indices a kernel will dereference
 # (with safe torch ops) before launching it, so a bad input raises in Python
 # instead of faulting the GPU.
-DEBUG_CHECKS = _os.environ.get("MR_DEBUG_CHECKS", "0") not in ("", "0")
+DEBUG_CHECKS = TUNABLES.debug_checks
 
 
 def _check_reps(lo: torch.Tensor, rep: torch.Tensor, src, what: str) -> None:
@@ -71,8 +72,8 @@ def _t64(a: np.ndarray, device="cpu") -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------
-_WC_CHUNK_MAX = int(os.environ.get("MR_WC_CHUNK_MAX", 16 * 1024))
-_WC_VERSION = int(os.environ.get("MR_WC_VERSION", 3))
+_WC_CHUNK_MAX = TUNABLES.wc_chunk_max
+_WC_VERSION = TUNABLES.wc_version
 _OVF_COUNTERS = 64
 _OVF_ENTRIES = 1 << 18
 _CTRL_SHARD0, _CTRL_STRIDE, _CTRL_SHARDS = 32, 32, 64  # csrc/hip/hashtab.h

@@ -16,6 +16,8 @@ import os
 import torch
 import torch.distributed as dist
 
+from ..utils.config import TUNABLES
+
 
 def env_world() -> tuple[int, int, int]:
     return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
@@ -54,7 +56,7 @@ def gpu_numa_cpus(device) -> list[int] | None:
 def bind_to_gpu_numa(device) -> list[int] | None:
     """Pin this process to its GPU's NUMA node (before pinned buffers are
     allocated, so their pages are node-local).  ``MR_NUMA_BIND=0`` disables."""
-    if os.environ.get("MR_NUMA_BIND", "1") == "0" or not hasattr(os, "sched_setaffinity"):
+    if not TUNABLES.numa_bind or not hasattr(os, "sched_setaffinity"):
         return None
     cpus = gpu_numa_cpus(device)
     if not cpus:

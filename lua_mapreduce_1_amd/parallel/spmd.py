@@ -36,6 +36,7 @@ import numpy as np
 import torch
 
 from .. import ops, utils
+from ..utils.config import TUNABLES
 from ..runtime import device as devmod
 from ..runtime import modules
 from ..utils import STATUS
@@ -44,8 +45,8 @@ from . import dist as D
 
 
 N_ARENAS = 3
-_PREFETCH_LATE = os.environ.get("MR_PREFETCH_LATE", "0") == "1"
-_PREFETCH_SINGLE = os.environ.get("MR_PREFETCH_SINGLE", "1") == "1"
+_PREFETCH_LATE = TUNABLES.prefetch_late
+_PREFETCH_SINGLE = TUNABLES.prefetch_single
 
 
 class _nullctx:
@@ -206,7 +207,7 @@ class SPMDEngine:
         # hipGraph replay of the device tail: measured (tools/proxy_rank.py) to
         # save ~0.05 ms on small per-rank inputs but to cost ~0.25 ms (and show
         # rare multi-ms stalls) on the full single-GPU corpus, so it is opt-in
-        self.use_graphs = _os.environ.get("MR_GRAPHS", "0") == "1"
+        self.use_graphs = TUNABLES.graphs
         self._tail_graphs: dict = {}
         self._tail_seen: set = set()
         self.iteration = 0
@@ -546,12 +547,12 @@ class SPMDEngine:
         and at most 256 partitions."""
         spec = getattr(self.partmod, "device_partition", None) if self.partmod is not None else None
         return (self.device.type == "cuda" and spec is not None and spec[0] == "fnv1"
-                and self.nparts <= 256 and os.environ.get("MR_FUSED_TAIL", "1") != "0")
+                and self.nparts <= 256 and TUNABLES.fused_tail)
 
     def _finalize_table(self, table, n: int, src) -> dict:
         """The fused device tail of a table: one native call (mr_tail_run) by
         default, the Python-sequenced launches with MR_NATIVE_TAIL=0."""
-        if os.environ.get("MR_NATIVE_TAIL", "1") != "0":
+        if TUNABLES.native_tail:
             return devmod.finalize_table_native(table, n, src, self.nparts)
         return devmod.finalize_table_device(table, n, src, self.nparts)
 

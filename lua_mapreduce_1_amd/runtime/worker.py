@@ -24,6 +24,7 @@ import traceback
 
 from .. import utils
 from ..utils import TASK_STATUS
+from ..utils.config import TUNABLES
 from . import job as job_mod
 from .cnn import cnn as cnn_cls
 from .task import task as task_cls
@@ -35,7 +36,7 @@ _fault_counts: dict[str, int] = {}
 
 
 def _maybe_inject_fault(status: str, job_id: str) -> None:
-    spec = os.environ.get("MR_FAULT", "")
+    spec = os.environ.get("MR_FAULT", TUNABLES.fault)  # read per call: tests inject faults at run time
     if not spec:
         return
     phase = "map" if status == TASK_STATUS.MAP else "reduce"

@@ -19,6 +19,7 @@ import tempfile
 import time as _time
 from typing import Any, Callable, Iterable, Iterator
 
+from .config import TUNABLES
 from .heap import heap  # noqa: F401
 
 
@@ -26,7 +27,7 @@ _VERSION = "0.3"
 _NAME = "mapreduce.utils"
 
 DEFAULT_RW_TIMEOUT = 300          # seconds
-DEFAULT_SLEEP = float(os.environ.get("MR_DEFAULT_SLEEP", 1.0))  # seconds (poll period)
+DEFAULT_SLEEP = TUNABLES.default_sleep  # seconds (poll period; MR_DEFAULT_SLEEP)
 DEFAULT_MICRO_SLEEP = 0.1
 DEFAULT_HOSTNAME = "<unknown>"
 DEFAULT_TMPNAME = "<NONE>"
@@ -61,7 +62,7 @@ GRP_TMP_DIR = os.path.join(tempfile.gettempdir(), "grouped")
 # new in this framework: liveness lease for RUNNING jobs (reference has none,
 # SURVEY.md §5.3); a RUNNING job whose worker stops heart-beating for this long
 # is re-queued as BROKEN.
-JOB_LEASE_SECONDS = float(os.environ.get("MR_JOB_LEASE", 120.0))
+JOB_LEASE_SECONDS = TUNABLES.job_lease  # MR_JOB_LEASE
 
 
 def get_hostname() -> str:

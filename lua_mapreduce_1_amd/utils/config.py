@@ -1,0 +1,86 @@
+"""Every tunable of the framework in one place, with environment overrides.
+
+The reference has no flag system: its knobs are the constants of
+``mapreduce/utils.lua:24-56`` plus the positional CLI arguments
+(SURVEY.md §5.6).  Here the user-facing configuration stays the reference's
+``server:configure{...}`` table and CLI, and the framework's own knobs — the
+reference constants that make sense to change, the device data-plane switches
+and the diagnostics — are fields of one frozen dataclass, each with an
+``MR_*`` environment override, read once at import.
+
+    python -m lua_mapreduce_1_amd.utils.config      # print every knob, its value and source
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass, field
+
+
+def _flag(v: str) -> bool:
+    return v.strip().lower() not in ("", "0", "false", "no", "off")
+
+
+def _knob(env: str, default, doc: str):
+    return field(default=default, metadata={"env": env, "doc": doc})
+
+
+@dataclass(frozen=True)
+class Tunables:
+    # -- reference constants (utils.lua:24-56) that are tunable here
+    default_sleep: float = _knob("MR_DEFAULT_SLEEP", 1.0, "poll period of server and workers, s (utils.lua:28)")
+    job_lease: float = _knob("MR_JOB_LEASE", 120.0,
+                             "a RUNNING job whose worker stopped heart-beating this long is re-queued, s (new)")
+    fault: str = _knob("MR_FAULT", "",
+                       "worker fault injection 'phase:job:action[:times]', e.g. 'map:2:raise:1' (tests)")
+    # -- device data plane
+    wc_version: int = _knob("MR_WC_VERSION", 3, "word-count map kernel generation (3 = wordcount3.hip)")
+    wc_chunk_max: int = _knob("MR_WC_CHUNK_MAX", 16 * 1024, "v2 map: max bytes per workgroup")
+    fused_tail: bool = _knob("MR_FUSED_TAIL", True, "fused reduce-side tail kernels (tail.hip)")
+    native_tail: bool = _knob("MR_NATIVE_TAIL", True, "queue the whole tail from one native call (mr_tail_run)")
+    graphs: bool = _knob("MR_GRAPHS", False, "replay the W=1 tail as a hipGraph (stalls the copy stream: off)")
+    pipeline: bool = _knob("MR_PIPELINE", True, "bench/proxies: map of iteration i+1 overlaps the tail of i")
+    prefetch_single: bool = _knob("MR_PREFETCH_SINGLE", True, "prefetched inputs: one DMA per iteration")
+    prefetch_late: bool = _knob("MR_PREFETCH_LATE", False, "issue prefetches after the tail instead of first")
+    d2h: str = _knob("MR_D2H", "kernel", "downloads: 'kernel' (shader stores) or 'sdma' (queued behind H2D)")
+    spin_us: float = _knob("MR_SPIN_US", 2000.0, "host spin on completion words before hipStreamSynchronize, us")
+    numa_bind: bool = _knob("MR_NUMA_BIND", True, "pin each rank to the CPUs of its GPU's NUMA node")
+    # -- diagnostics
+    debug_checks: bool = _knob("MR_DEBUG_CHECKS", False, "extra host-side consistency checks (slow)")
+    roctx: bool = _knob("MR_ROCTX", False, "roctx ranges around every phase (rocprofv3 --marker-trace)")
+    host_timeline: bool = _knob("MR_HOST_TIMELINE", False, "record phase ranges with perf_counter (trace.LOG)")
+    host_timeline_hip: bool = _knob("MR_HOST_TIMELINE_HIP", False, "... and every native call")
+    wait_log: bool = _knob("MR_WAIT_LOG", False, "log every host wait (ops._hip.WAIT_LOG)")
+
+    @classmethod
+    def from_env(cls, env=None) -> "Tunables":
+        env = os.environ if env is None else env
+        kw = {}
+        for f in dataclasses.fields(cls):
+            v = env.get(f.metadata["env"])
+            if v is None:
+                continue
+            if f.type in ("bool", bool):
+                kw[f.name] = _flag(v)
+            elif f.type in ("int", int):
+                kw[f.name] = int(v)
+            elif f.type in ("float", float):
+                kw[f.name] = float(v)
+            else:
+                kw[f.name] = v
+        return cls(**kw)
+
+    def describe(self) -> str:
+        rows = []
+        for f in dataclasses.fields(self):
+            env = f.metadata["env"]
+            src = "env" if env in os.environ else "default"
+            rows.append(f"{f.name:18s} {env:22s} {str(getattr(self, f.name)):10s} {src:7s} {f.metadata['doc']}")
+        return "\n".join(rows)
+
+
+TUNABLES = Tunables.from_env()
+
+
+if __name__ == "__main__":
+    print(TUNABLES.describe())

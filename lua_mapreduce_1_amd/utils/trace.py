@@ -20,11 +20,13 @@ import ctypes
 import os
 import time
 
+from .config import TUNABLES
+
 _LIB = None
-_ENABLED = os.environ.get("MR_ROCTX", "0") == "1"
+_ENABLED = TUNABLES.roctx
 # host-only timeline without a profiler: MR_HOST_TIMELINE=1 records
 # (name, start, end) perf_counter stamps of every range into LOG
-LOG: list | None = [] if os.environ.get("MR_HOST_TIMELINE") else None
+LOG: list | None = [] if TUNABLES.host_timeline else None
 _STACK: list = []
 _CANDIDATES = ("librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so", "libroctx64.so.4", "libroctx64.so")
 

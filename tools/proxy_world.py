@@ -23,6 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from bench import MODEL, load_corpus  # noqa: E402
 from lua_mapreduce_1_amd.parallel import dist as D  # noqa: E402
+from lua_mapreduce_1_amd.utils.config import TUNABLES  # noqa: E402
 from lua_mapreduce_1_amd.parallel import spmd as S  # noqa: E402
 
 
@@ -53,7 +54,7 @@ def main() -> int:
     eng = S.SPMDEngine(params, device=device, split_store=store)
     assert eng.world == W and eng.rank == 0
     eng.prefetch = True
-    eng.pipeline = os.environ.get("MR_PIPELINE", "1") != "0"
+    eng.pipeline = TUNABLES.pipeline  # MR_PIPELINE
     import gc
     gc_early = os.environ.get("MR_GC_EARLY", "1") == "1"  # as bench.py
     if gc_early:  # collect before the warm-up: the heap walk evicts the caches the timed steps run from
