@@ -192,6 +192,10 @@ class SPMDEngine:
         self.tslot = 0  # its table and stream
         self._seq = 0   # sequence number of the next iteration
         self._inflight: dict = {}  # arena slot -> plan key of copies issued ahead
+        # HBM-resident input (P6 locality, SURVEY.md §2.5: "data stays in HBM"):
+        # an arena that already holds an iteration's splits is not copied again
+        self.resident = False
+        self._arena_holds: dict = {}  # arena slot -> plan key of the splits it holds
         self.prefetch = False
         # iteration pipelining (needs prefetch): the next iteration's map is
         # queued on the other slot's stream as soon as this map has finished,
@@ -297,6 +301,7 @@ class SPMDEngine:
         nbytes = b - a
         if self.arenas[slot] is None or self.arenas[slot].numel() < nbytes:
             self.arenas[slot] = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self._arena_holds.pop(slot, None)
             self._plans = {k: v for k, v in self._plans.items() if k[2] != slot}
 
         arena = self.arenas[slot]
@@ -400,11 +405,13 @@ class SPMDEngine:
         ids = self._split_ids(jobs, j0, j1)
         if not ids or aslot in self._inflight:
             return
+        if self.resident and self._arena_holds.get(aslot) == (ids[0], len(ids)):
+            return  # HBM-resident input: the arena still holds these splits
         plan = self._get_plan(ids, aslot, single=_PREFETCH_SINGLE)
         # arenas[aslot] was last read by iteration q - N_ARENAS, which has
         # completed (its finalize synchronised): no stream dependency needed
         self._issue_copies(plan)
-        self._inflight[aslot] = (ids[0], len(ids))
+        self._inflight[aslot] = self._arena_holds[aslot] = (ids[0], len(ids))
 
     def _stage_chunks(self, jobs, j0, j1):
         """Yield (job index range, device tensor) chunks, H2D overlapped with compute."""
@@ -413,7 +420,14 @@ class SPMDEngine:
             if not ids:
                 return
             cs = self.copy_stream
-            prefetched = cs is not None and self._inflight.pop(self.slot, None) == (ids[0], len(ids))
+            key = (ids[0], len(ids))
+            prefetched = cs is not None and self._inflight.pop(self.slot, None) == key
+            if self.resident and not prefetched and self._arena_holds.get(self.slot) == key:
+                # HBM-resident input: these splits were copied into this arena by
+                # an earlier, completed iteration — map them in place
+                a, b = self.splits.region(ids[0], ids[-1] + 1)
+                yield (j0, j0 + len(ids)), self.arena[:b - a]
+                return
             plan = self._get_plan(ids, self.slot, single=prefetched and _PREFETCH_SINGLE)
             bounds, views, host_views, events = plan
             if cs is not None:
@@ -421,6 +435,7 @@ class SPMDEngine:
                 if not prefetched:
                     with trace.range("mr.copies"):
                         self._issue_copies(plan, wait_for=cur)
+                    self._arena_holds[self.slot] = key
                 # chunks whose copies have already landed (prefetched during the
                 # previous iteration's tail) are mapped by ONE launch: a launch's
                 # ramp-up and drain cost more than its chunking saves

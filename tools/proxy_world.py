@@ -54,6 +54,7 @@ def main() -> int:
     eng = S.SPMDEngine(params, device=device, split_store=store)
     assert eng.world == W and eng.rank == 0
     eng.prefetch = True
+    eng.resident = os.environ.get("MR_RESIDENT") == "1"
     eng.pipeline = TUNABLES.pipeline  # MR_PIPELINE
     import gc
     gc_early = os.environ.get("MR_GC_EARLY", "1") == "1"  # as bench.py
