@@ -96,6 +96,54 @@ __global__ void ts_gather_kernel(const u32* __restrict__ in, const u32* __restri
   }
 }
 
+// v2: the same dword mapping, UNROLL independent elements per thread per
+// step — all permutation loads, then all record loads, then all stores — so a
+// wave has UNROLL loads in flight instead of a perm -> data -> store chain
+template <int UNROLL>
+__global__ void __launch_bounds__(256) ts_gather_unrolled_kernel(const u32* __restrict__ in,
+                                                                 const u32* __restrict__ perm, u64 n,
+                                                                 u32* __restrict__ out) {
+  const u64 nw = n * WORDS;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 w0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; w0 < nw; w0 += stride * UNROLL) {
+    u32 src[UNROLL];
+    u32 v[UNROLL];
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      const u64 w = w0 + (u64)k * stride;
+      const u64 r = w / WORDS;
+      src[k] = w < nw ? perm[r] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      const u64 w = w0 + (u64)k * stride;
+      const u64 r = w / WORDS;
+      const u32 j = (u32)(w - r * WORDS);
+      v[k] = w < nw ? __builtin_nontemporal_load(in + (u64)src[k] * WORDS + j) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      const u64 w = w0 + (u64)k * stride;
+      if (w < nw) __builtin_nontemporal_store(v[k], out + w);
+    }
+  }
+}
+
+// v3: one record per thread: 25 independent dword loads, 25 stores
+__global__ void __launch_bounds__(256) ts_gather_rec_kernel(const u32* __restrict__ in, const u32* __restrict__ perm,
+                                                            u64 n, u32* __restrict__ out) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
+    const u32* p = in + (u64)perm[r] * WORDS;
+    u32 v[WORDS];
+#pragma unroll
+    for (int j = 0; j < WORDS; ++j) v[j] = __builtin_nontemporal_load(p + j);
+    u32* o = out + r * WORDS;
+#pragma unroll
+    for (int j = 0; j < WORDS; ++j) o[j] = v[j];
+  }
+}
+
 __global__ void __launch_bounds__(256) ts_checksum_kernel(const u32* __restrict__ rec, u64 n,
                                                           unsigned long long* __restrict__ out) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
@@ -183,10 +231,32 @@ int mr_ts_dest(const void* hi, u64 n, const void* split, u32 nsplit, void* dest,
   return (int)hipGetLastError();
 }
 
+int mr_ts_gather_mode(const void* in, const void* perm, u64 n, void* out, int mode, int grid, hipStream_t s);
+
+// Row gather: 8 independent elements per thread per step, 16384 workgroups
+// (tools/ts_gather_probe.py at 100 M records: 8.05 -> 6.58 ms; ~5 TB/s of HBM
+// traffic counting the 1.77 128-byte lines a random 100-byte record touches).
 int mr_ts_gather(const void* in, const void* perm, u64 n, void* out, hipStream_t s) {
   if (n == 0) return 0;
-  hipLaunchKernelGGL(ts::ts_gather_kernel, dim3(ts_grid(n * ts::WORDS)), dim3(256), 0, s, (const u32*)in,
-                     (const u32*)perm, n, (u32*)out);
+  return mr_ts_gather_mode(in, perm, n, out, 2, (int)ts_grid(n * ts::WORDS, 16384), s);
+}
+
+// mode 0: dword per thread (ts_gather_kernel); 1/2/3: UNROLL 4/8/16; 4: record per thread
+int mr_ts_gather_mode(const void* in, const void* perm, u64 n, void* out, int mode, int grid, hipStream_t s) {
+  if (n == 0) return 0;
+  const u32* I = (const u32*)in;
+  const u32* P = (const u32*)perm;
+  u32* O = (u32*)out;
+  const unsigned g = grid > 0 ? (unsigned)grid : ts_grid(n * ts::WORDS);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(ts::ts_gather_kernel, dim3(g), dim3(256), 0, s, I, P, n, O); break;
+    case 1: hipLaunchKernelGGL(ts::ts_gather_unrolled_kernel<4>, dim3(g), dim3(256), 0, s, I, P, n, O); break;
+    case 2: hipLaunchKernelGGL(ts::ts_gather_unrolled_kernel<8>, dim3(g), dim3(256), 0, s, I, P, n, O); break;
+    case 3: hipLaunchKernelGGL(ts::ts_gather_unrolled_kernel<16>, dim3(g), dim3(256), 0, s, I, P, n, O); break;
+    case 4: hipLaunchKernelGGL(ts::ts_gather_rec_kernel, dim3(grid > 0 ? (unsigned)grid : ts_grid(n)), dim3(256), 0,
+                               s, I, P, n, O); break;
+    default: return -1;
+  }
   return (int)hipGetLastError();
 }
 
