@@ -174,27 +174,37 @@ __global__ void __launch_bounds__(256) ts_unsorted_kernel(const u64* __restrict_
 // the permutation; stable because the LSD pass left ties in input order).
 // Random 64-bit prefixes almost never tie, so this replaces 2 radix passes +
 // a key gather.  Runs longer than 64 set *bad (caller falls back).
-__global__ void ts_tie_fixup_kernel(const u64* __restrict__ shi, u32* __restrict__ perm, const u64* __restrict__ lo,
-                                    u64 n, u32* __restrict__ bad) {
+// Rows of equal (shi >> top_shift) — the bits the radix sort looked at — are
+// ordered by the rest of the key, (shi, lo), with an insertion sort per run
+// (one thread per run; runs longer than 64 set bad[0]: the caller then sorts
+// the full key).  top_shift = 0: runs of equal hi ordered by lo; 32: the sort
+// visited only the top 32 bits of hi (uniform TeraGen keys: ~2% of the rows
+// sit in a run, almost all of length 2).
+__global__ void ts_tie_fixup_kernel(u64* __restrict__ shi, u32* __restrict__ perm, const u64* __restrict__ lo,
+                                    u64 n, u32* __restrict__ bad, int top_shift) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += stride) {
-    const u64 h = shi[i];
-    if (shi[i + 1] != h || (i > 0 && shi[i - 1] == h)) continue;
+    const u64 h = shi[i] >> top_shift;
+    if ((shi[i + 1] >> top_shift) != h || (i > 0 && (shi[i - 1] >> top_shift) == h)) continue;
     u64 e = i + 2;
-    while (e < n && shi[e] == h && e - i <= 64) ++e;
+    while (e < n && (shi[e] >> top_shift) == h && e - i <= 64) ++e;
     if (e - i > 64) {
       atomicOr(bad, 1u);
       continue;
     }
     for (u64 a = i + 1; a < e; ++a) {
       const u32 p = perm[a];
-      const u64 l = lo[p];
+      const u64 kh = shi[a], kl = lo[p];
       u64 b = a;
-      while (b > i && lo[perm[b - 1]] > l) {
+      while (b > i) {
+        const u64 ph = shi[b - 1];
+        if (ph < kh || (ph == kh && lo[perm[b - 1]] <= kl)) break;
         perm[b] = perm[b - 1];
+        shi[b] = ph;
         --b;
       }
       perm[b] = p;
+      shi[b] = kh;
     }
   }
 }
@@ -260,11 +270,15 @@ int mr_ts_gather_mode(const void* in, const void* perm, u64 n, void* out, int mo
   return (int)hipGetLastError();
 }
 
-int mr_ts_tie_fixup(const void* shi, void* perm, const void* lo, u64 n, void* bad, hipStream_t s) {
+int mr_ts_tie_fixup2(void* shi, void* perm, const void* lo, u64 n, void* bad, int top_shift, hipStream_t s) {
   if (n < 2) return 0;
-  hipLaunchKernelGGL(ts::ts_tie_fixup_kernel, dim3(ts_grid(n)), dim3(256), 0, s, (const u64*)shi, (u32*)perm,
-                     (const u64*)lo, n, (u32*)bad);
+  hipLaunchKernelGGL(ts::ts_tie_fixup_kernel, dim3(ts_grid(n)), dim3(256), 0, s, (u64*)shi, (u32*)perm,
+                     (const u64*)lo, n, (u32*)bad, top_shift);
   return (int)hipGetLastError();
+}
+
+int mr_ts_tie_fixup(const void* shi, void* perm, const void* lo, u64 n, void* bad, hipStream_t s) {
+  return mr_ts_tie_fixup2(const_cast<void*>(shi), perm, lo, n, bad, 0, s);
 }
 
 int mr_ts_checksum(const void* rec, u64 n, void* out, hipStream_t s) {

@@ -445,14 +445,16 @@ def _sort_ws(d, n: int):
 
 
 def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: str = "onesweep",
-              return_keys: bool = False, ghist: torch.Tensor | None = None):
+              return_keys: bool = False, ghist: torch.Tensor | None = None, from_bit: int = 0):
     """Stable permutation sorting rows by unsigned multi-word keys.
 
     ``words[0]`` is the most significant u64 word.  ``bits[j]`` limits the
     number of low bits of word j that participate (e.g. partition ids).
     Returns int32 (GPU) / int64 (CPU) permutation (and, with ``return_keys``,
     ``words[0]`` in sorted order as a second value).  ``ghist``: precomputed
-    [8][256] digit histograms of a single-word key (skips that pass).  GPU: LSD radix sort, one
+    [8][256] digit histograms of a single-word key (skips that pass).  ``from_bit``
+    (single word, GPU onesweep): only bits >= from_bit are sorted — rows equal
+    in those bits keep their input order.  GPU: LSD radix sort, one
     onesweep launch per 8-bit digit (``method="onesweep"``) or the 3-phase
     histogram/scan/scatter passes (``method="3phase"``).
     """
@@ -497,7 +499,7 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
                     if pass_id:
                         ghist_ws.zero_()
                     _hip.call("mr_radix_ghist8", _hip.ptr(kin), n, _hip.ptr(ghist_ws), (nb + 7) // 8, s)
-                for shift in range(0, nb, 8):
+                for shift in range(from_bit if len(words) == 1 else 0, nb, 8):
                     _EPOCH[0] = (_EPOCH[0] + 1) & 0xFFFFFF or 1
                     kout = kbuf[0] if kin is not kbuf[0] else kbuf[1]
                     pout = pbuf[0] if pin is not pbuf[0] else pbuf[1]

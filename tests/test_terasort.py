@@ -128,3 +128,26 @@ def test_gpu_sort_perm_with_prefix_ties(gpu, mod):
     ref = TS.sort_perm(hi, lo)
     got = TS.sort_perm(hi.to(gpu), lo.to(gpu)).cpu().long()
     assert torch.equal(got, ref.long())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["uniform", "runs", "skewed"])
+def test_gpu_sort_perm_top32_fixup(gpu, case):
+    """sort_perm sorts only the top 32 bits of hi and fixes runs of equal top
+    bits by (hi, lo): uniform keys, many short runs (2..40 rows sharing the
+    top 32 bits), and a skewed key set whose runs exceed the fix-up limit
+    (full-sort fallback) all give the exact 80-bit order."""
+    g = np.random.default_rng({"uniform": 1, "runs": 2, "skewed": 3}[case])
+    n = 200_000
+    hi = g.integers(0, 2**63, n, dtype=np.int64).view(np.uint64) * np.uint64(2) + g.integers(0, 2, n).astype(np.uint64)
+    if case == "runs":
+        top = g.integers(0, n // 20, n).astype(np.uint64) << np.uint64(32)
+        hi = top | (hi & np.uint64(0xFFFFFFFF))
+    elif case == "skewed":
+        hi = (np.uint64(7) << np.uint64(32)) | (hi & np.uint64(0xFFFF))
+    lo = g.integers(0, 1 << 16, n).astype(np.uint64)
+    th = torch.from_numpy(hi.view(np.int64)).to(gpu)
+    tl = torch.from_numpy(lo.view(np.int64)).to(gpu)
+    perm = TS.sort_perm(th, tl).cpu().numpy().astype(np.int64)
+    want = np.lexsort((lo, hi))
+    assert np.array_equal(hi[perm], hi[want]) and np.array_equal(lo[perm], lo[want])
