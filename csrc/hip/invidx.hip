@@ -357,6 +357,86 @@ __global__ void ii_compact_kernel(const u64* __restrict__ keys, const u32* __res
     if (flags[i]) out[pos[i]] = keys[i];
 }
 
+// Fused "sorted keys -> distinct keys" (replaces flags + 3-launch scan +
+// compact, which wrote and re-read two n-word arrays): uq_count_kernel counts
+// the run heads of each 4096-key tile, the tile counts are scanned, and
+// uq_scatter_kernel recomputes the heads in registers and writes them at the
+// tile's offset + a block scan.  Keys are read twice, nothing else is stored.
+constexpr int UQ_T = 256, UQ_ITEMS = 16, UQ_TILE = UQ_T * UQ_ITEMS;
+
+// Coalesced: round r, lane t reads key tile0 + r*UQ_T + t; its predecessor is
+// the neighbouring lane's key (lane 0 of a wave loads it).
+__global__ void __launch_bounds__(UQ_T) uq_count_kernel(const u64* __restrict__ keys, u64 n, u32* __restrict__ tc) {
+  const int t = threadIdx.x, lane = t & 63;
+  const u64 tile0 = (u64)blockIdx.x * UQ_TILE;
+  u32 c = 0;
+#pragma unroll 4
+  for (int r = 0; r < UQ_ITEMS; ++r) {
+    const u64 i = tile0 + (u64)r * UQ_T + t;
+    const u64 k = i < n ? keys[i] : 0;
+    u64 prev = __shfl_up(k, 1);
+    if (lane == 0) prev = (i > 0 && i - 1 < n) ? keys[i - 1] : ~k;
+    c += (i < n && (i == 0 || k != prev)) ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  __shared__ u32 w[UQ_T / 64];
+  if (lane == 0) w[t >> 6] = c;
+  __syncthreads();
+  if (t == 0) tc[blockIdx.x] = w[0] + w[1] + w[2] + w[3];
+}
+
+// The tile goes through LDS: coalesced load, each thread takes 16 contiguous
+// keys (run heads + block scan = their order), the kept keys are packed in LDS
+// and streamed out with coalesced stores.
+__global__ void __launch_bounds__(UQ_T) uq_scatter_kernel(const u64* __restrict__ keys, u64 n,
+                                                          const u32* __restrict__ tile_off, u64* __restrict__ out) {
+  __shared__ u64 sk[UQ_TILE + 1];  // sk[0] = the key before the tile
+  __shared__ u32 w[UQ_T / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const u64 tile0 = (u64)blockIdx.x * UQ_TILE;
+#pragma unroll 4
+  for (int r = 0; r < UQ_ITEMS; ++r) {
+    const u64 i = tile0 + (u64)r * UQ_T + t;
+    sk[1 + r * UQ_T + t] = i < n ? keys[i] : 0;
+  }
+  if (t == 0) sk[0] = tile0 > 0 ? keys[tile0 - 1] : ~keys[0];
+  __syncthreads();
+  u64 k[UQ_ITEMS];
+  u32 m = 0;
+  {
+    u64 prev = sk[t * UQ_ITEMS];
+#pragma unroll
+    for (int j = 0; j < UQ_ITEMS; ++j) {
+      k[j] = sk[1 + t * UQ_ITEMS + j];
+      const u64 i = tile0 + (u64)t * UQ_ITEMS + j;
+      if (i < n && k[j] != prev) m |= 1u << j;
+      prev = k[j];
+    }
+  }
+  const u32 c = __builtin_popcount(m);
+  u32 incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) w[wave] = incl;
+  __syncthreads();  // also: every thread has read its keys from sk
+  u32 base = 0, total = 0;
+#pragma unroll
+  for (int x = 0; x < UQ_T / 64; ++x) {
+    base += x < wave ? w[x] : 0u;
+    total += w[x];
+  }
+  u32 o = base + incl - c;
+#pragma unroll
+  for (int j = 0; j < UQ_ITEMS; ++j)
+    if (m & (1u << j)) sk[o++] = k[j];
+  __syncthreads();
+  const u64 ob = tile_off[blockIdx.x];
+  for (u32 x = t; x < total; x += UQ_T) out[ob + x] = sk[x];
+}
+
 // Split unique posting keys into word boundaries and doc ids:
 //   wflag[i] = 1 if the word part (key >> doc_bits) differs from key[i-1]'s;
 //   doc[i]   = (key & doc_mask) + doc_base.
@@ -439,6 +519,24 @@ int mr_ii_unique_flags(const void* keys, u64 n, void* flags, hipStream_t s) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(ii::ii_unique_flags_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)keys, n,
                      (u32*)flags);
+  return (int)hipGetLastError();
+}
+
+u64 mr_ii_unique_tiles(u64 n) { return (n + ii::UQ_TILE - 1) / ii::UQ_TILE; }
+
+// pass 1: per-tile head counts into tc[mr_ii_unique_tiles(n)]
+int mr_ii_unique_count(const void* keys, u64 n, void* tc, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ii::uq_count_kernel, dim3((unsigned)mr_ii_unique_tiles(n)), dim3(ii::UQ_T), 0, s,
+                     (const u64*)keys, n, (u32*)tc);
+  return (int)hipGetLastError();
+}
+
+// pass 2 (after an exclusive scan of tc into tile_off): write the distinct keys
+int mr_ii_unique_scatter(const void* keys, u64 n, const void* tile_off, void* out, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ii::uq_scatter_kernel, dim3((unsigned)mr_ii_unique_tiles(n)), dim3(ii::UQ_T), 0, s,
+                     (const u64*)keys, n, (const u32*)tile_off, (u64*)out);
   return (int)hipGetLastError();
 }
 

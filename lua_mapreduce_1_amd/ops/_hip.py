@@ -66,6 +66,9 @@ _SIGS = {
     "mr_ii_add_dest": [_p, _u64, _p, _u32, _u64, _u32, _p],
     "mr_ii_unique_flags": [_p, _u64, _p, _p],
     "mr_ii_compact": [_p, _p, _p, _u64, _p, _p],
+    "mr_ii_unique_tiles": [_u64],
+    "mr_ii_unique_count": [_p, _u64, _p, _p],
+    "mr_ii_unique_scatter": [_p, _u64, _p, _p, _p],
     "mr_ii_split": [_p, _u64, _u32, ctypes.c_longlong, _p, _p, _p],
     "mr_ii_word_heads": [_p, _p, _p, _u64, _u32, _u64, _p, _p, _p],
     "mr_ii_insert_slots": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _p],
@@ -89,7 +92,7 @@ _SIGS = {
     "mr_scan_partials_len": [_u64],
     "mr_rs_tiles": [_u64],
 }
-_RESTYPE_U64 = {"mr_scan_partials_len", "mr_rs_tiles", "mr_tail_pack_bytes", "mr_tail_ws_layout"}
+_RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_scan_partials_len", "mr_rs_tiles", "mr_tail_pack_bytes", "mr_tail_ws_layout"}
 
 
 def lib():

@@ -151,13 +151,16 @@ def sort_unique(keys: torch.Tensor, bits: int) -> torch.Tensor:
             return keys
         d = keys.device
         s = _hip.stream(d)
-        _, sk = sort_keys([keys], bits=[bits], return_keys=True)
-        flags = torch.empty(n, dtype=torch.int32, device=d)
-        _hip.call("mr_ii_unique_flags", _hip.ptr(sk), n, _hip.ptr(flags), s)
-        pos, total = exclusive_scan(flags)
+        # keys-only radix sort (no permutation carried), then the fused
+        # two-pass unique (per-tile head counts -> scan -> scatter)
+        _, sk = sort_keys([keys], bits=[bits], return_keys=True, keys_only=True)
+        tiles = int(_hip.lib().mr_ii_unique_tiles(n))
+        tc = torch.empty(tiles, dtype=torch.int32, device=d)
+        _hip.call("mr_ii_unique_count", _hip.ptr(sk), n, _hip.ptr(tc), s)
+        off, total = exclusive_scan(tc)
         m = int(total.item())
         out = torch.empty(m, dtype=torch.int64, device=d)
-        _hip.call("mr_ii_compact", _hip.ptr(sk), _hip.ptr(flags), _hip.ptr(pos), n, _hip.ptr(out), s)
+        _hip.call("mr_ii_unique_scatter", _hip.ptr(sk), n, _hip.ptr(off), _hip.ptr(out), s)
         return out
     return torch.unique(keys)
 

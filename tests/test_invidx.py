@@ -130,3 +130,18 @@ def test_gpu_long_lines_and_many_lines(gpu):
 @pytest.mark.gpu
 def test_gpu_multi_rank_on_one_gpu(gpu):
     _run(2, on_gpu=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 4095, 4096, 4097, 300_000, 1_500_000])
+def test_gpu_sort_unique_matches_torch(gpu, n):
+    """keys-only radix sort + fused two-pass unique == torch.unique (sorted)."""
+    from lua_mapreduce_1_amd.ops import invidx as II
+    from lua_mapreduce_1_amd.ops.primitives import sort_keys
+    g = torch.Generator().manual_seed(n)
+    keys = torch.randint(0, max(2, n // 3), (n,), generator=g, dtype=torch.int64) << 7
+    keys |= torch.randint(0, 3, (n,), generator=g, dtype=torch.int64)
+    got = II.sort_unique(keys.to(gpu), 40).cpu()
+    assert torch.equal(got, torch.unique(keys))
+    _, sk = sort_keys([keys.to(gpu)], bits=[40], return_keys=True, keys_only=True)
+    assert torch.equal(sk.cpu(), torch.sort(keys).values)
