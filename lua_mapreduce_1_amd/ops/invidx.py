@@ -10,6 +10,8 @@ bytes are materialised only for the final words.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -17,7 +19,10 @@ from . import _hip
 from . import keys as K
 from .primitives import HashTable, _t64, _u64, exclusive_scan, sort_keys
 
-CHUNK = 32 * 1024
+# bytes per ii_map workgroup: ONE 8 KiB tile (1 workgroup per CU fits; 8/16/32/64 KiB
+# measured 10.5 / 11.5 / 12.4 / 15.5 ms per build: more, shorter workgroups balance the
+# CUs and their LDS tables fill less), MR_II_CHUNK for A/B runs
+CHUNK = int(os.environ.get("MR_II_CHUNK", 8 * 1024))
 
 
 def bits_for(n: int) -> int:
