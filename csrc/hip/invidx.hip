@@ -38,10 +38,14 @@ constexpr int HALO = 64;
 constexpr int STAGED = TILE + HALO;
 constexpr int TXT = PAD + STAGED + 32;
 constexpr int WSW = STAGED / 32 + 2;
-constexpr int SLOTS = 4096;
+// 2048 slots and 2048 buffered tokens keep the LDS at ~77 KiB: TWO workgroups
+// per CU (one tile per workgroup by default: ~880 distinct words per tile)
+constexpr int SLOTS = 2048;
 constexpr int CLAIM_LIMIT = SLOTS * 3 / 4;
 constexpr int PROBES = 32;
-constexpr int MAX_TOK = TILE / 2;       // tokens start at non-ws bytes after ws: <= TILE/2 (+1)
+// a tile holds up to TILE/2 (+1) tokens; tokens past MAX_TOK (tiles of one-letter
+// words) are resolved and written directly (one global atomic each)
+constexpr int MAX_TOK = 2048;
 constexpr u32 GFLAG = 0x80000000u;      // token ref is a global slot (LDS miss)
 constexpr u32 UNRESOLVED = 0xFFFFFFFFu;
 
@@ -54,7 +58,7 @@ struct Lds {
   u64 hi[SLOTS];
   u64 lo[SLOTS];
   u32 tok_ref[MAX_TOK + 8];
-  u32 tok_line[MAX_TOK + 8];
+  u16 tok_line[MAX_TOK + 8];  // line - the tile's first line (< TILE)
   u32 wave_nl[T / 64];
   u32 ntok;
   u32 nclaimed;
@@ -288,8 +292,20 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
           ref = GFLAG | (u32)gs;
         }
         const u32 k = __hip_atomic_fetch_add(&L.ntok, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        L.tok_ref[k] = ref;
-        L.tok_line[k] = line;
+        if (k < (u32)MAX_TOK) {
+          L.tok_ref[k] = ref;
+          L.tok_line[k] = (u16)(line - line_base);
+        } else {
+          u64 gs = ref & ~GFLAG;
+          if (!(ref & GFLAG)) {
+            const int r = gtab_insert(g, hi, lo, 1, make_rep(rep_base + gpos, len), OP_SUM, &gs);
+            claims += r == 2;
+            if (r == 0) gs = 0;
+          }
+          const unsigned long long o = atomicAdd(out_counter, 1ull);
+          if (o < out_cap) out[o] = (gs << doc_bits) | (u64)line;
+          else atomicOr(err, 1u);
+        }
       }
     }
     __syncthreads();
@@ -305,7 +321,7 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
       }
     }
     if (t == 0) {
-      const u32 n = L.ntok;
+      const u32 n = min(L.ntok, (u32)MAX_TOK);
       const unsigned long long base = atomicAdd(out_counter, (unsigned long long)n);
       L.out_base = base;
       if (base + n > out_cap) atomicOr(err, 1u);
@@ -313,12 +329,12 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
     __syncthreads();
     // ---- 5. write the tile's posting keys
     {
-      const u32 n = L.ntok;
+      const u32 n = min(L.ntok, (u32)MAX_TOK);
       const unsigned long long base = L.out_base;
       for (u32 k = t; k < n; k += T) {
         const u32 ref = L.tok_ref[k];
         const u32 gs = (ref & GFLAG) ? (ref & ~GFLAG) : L.gslot[ref];
-        if (base + k < out_cap) out[base + k] = ((u64)gs << doc_bits) | (u64)L.tok_line[k];
+        if (base + k < out_cap) out[base + k] = ((u64)gs << doc_bits) | (u64)(line_base + L.tok_line[k]);
       }
     }
     line_base += tile_nl;

@@ -128,6 +128,19 @@ def test_gpu_long_lines_and_many_lines(gpu):
 
 
 @pytest.mark.gpu
+def test_gpu_dense_one_letter_tokens(gpu):
+    """Tiles with more tokens than the map kernel buffers (one-letter words:
+    up to 4096 tokens per 8 KiB tile > 2048) take the direct-write path."""
+    rng = np.random.default_rng(5)
+    letters = [bytes([c]) for c in b"abcdefghijklmnopqrstuvwxyz0123456789"]
+    lines = [b" ".join(letters[i] for i in rng.integers(0, len(letters), int(n))) + b"\n"
+             for n in rng.integers(1, 3000, 120)]
+    splits = [b"".join(lines[:60]), b"".join(lines[60:])]
+    sh = InvertedIndexBuilder(SplitStore(splits, pin=True), device=gpu, capacity=1 << 12).build()
+    assert sh.to_host() == naive_index(splits)
+
+
+@pytest.mark.gpu
 def test_gpu_multi_rank_on_one_gpu(gpu):
     _run(2, on_gpu=True)
 
