@@ -49,6 +49,10 @@ enum Op : uint16_t {
   JOB_UPDATE = 25, JOB_GET = 26, JOB_LIST = 27, JOB_DROP = 28, JOB_STATS = 29, JOB_EXPIRE = 30,
   ERR_INSERT = 40, ERR_TAKE = 41,
   BLOB_PUT = 50, BLOB_GET = 51, BLOB_LIST = 52, BLOB_DEL = 53,
+  // batched forms (one round trip for all outputs of a job, all inputs of a
+  // reduce job): PUT_MANY name,data,name,data...; GET_MANY names -> (found, data)...;
+  // DEL_MANY names -> count
+  BLOB_PUT_MANY = 54, BLOB_GET_MANY = 55, BLOB_DEL_MANY = 56,
   PT_OPEN = 60, PT_UPDATE = 61, PT_LOCK = 62, PT_UNLOCK = 63, PT_DROP = 64,
   DB_DROP = 70, COLLECTIONS = 71, SHUTDOWN = 99,
 };
@@ -59,7 +63,7 @@ bool is_mutating(uint16_t op) {
   switch (op) {
     case TASK_SET: case TASK_DROP: case JOB_INSERT: case JOB_REMOVE_STATUS: case JOB_FAIL_BROKEN:
     case JOB_CLAIM: case JOB_UPDATE: case JOB_DROP: case JOB_EXPIRE: case ERR_INSERT: case ERR_TAKE:
-    case BLOB_PUT: case BLOB_DEL: case PT_OPEN: case PT_UPDATE: case PT_LOCK: case PT_UNLOCK: case PT_DROP:
+    case BLOB_PUT: case BLOB_DEL: case BLOB_PUT_MANY: case BLOB_DEL_MANY: case PT_OPEN: case PT_UPDATE: case PT_LOCK: case PT_UNLOCK: case PT_DROP:
     case DB_DROP:
       return true;
     default:
@@ -331,6 +335,34 @@ class Store {
         return 0;
       }
       case BLOB_DEL: { w.i((long long)db.blobs.erase(r.str())); return 0; }
+      case BLOB_PUT_MANY: {
+        while (r.more() && r.ok) {
+          std::string n = r.str();
+          std::string d = r.str();
+          if (!r.ok) return -1;
+          db.blobs[n] = std::move(d);
+        }
+        return r.ok ? 0 : -1;
+      }
+      case BLOB_GET_MANY: {
+        while (r.more() && r.ok) {
+          auto it = db.blobs.find(r.str());
+          if (it == db.blobs.end()) {
+            w.i(0);
+            w.str(std::string());
+          } else {
+            w.i(1);
+            w.str(it->second);
+          }
+        }
+        return r.ok ? 0 : -1;
+      }
+      case BLOB_DEL_MANY: {
+        long long c = 0;
+        while (r.more() && r.ok) c += (long long)db.blobs.erase(r.str());
+        w.i(c);
+        return 0;
+      }
       case PT_OPEN: {
         std::string d_ = r.str(); std::string key = d_ + "\x1f" + r.str();
         PTable& t = db.ptables[key];

@@ -5,6 +5,7 @@
 from __future__ import annotations
 
 import argparse
+import os
 import sys
 
 
@@ -19,12 +20,31 @@ def main(argv=None) -> int:
     ap.add_argument("--quiet", action="store_true")
     a = ap.parse_args(argv)
     from .. import worker
+    prof_dir = os.environ.get("MR_WORKER_PROFILE")
+    if prof_dir:  # diagnosis: cProfile of the whole worker, written when it is stopped
+        import cProfile
+        import pstats
+        import signal
+        prof = cProfile.Profile()
+
+        def _dump(*_):
+            prof.disable()
+            os.makedirs(prof_dir, exist_ok=True)
+            with open(os.path.join(prof_dir, f"worker_{os.getpid()}.txt"), "w") as f:
+                pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(60)
+                pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
+            os._exit(0)
+        signal.signal(signal.SIGTERM, _dump)
+        prof_dir = os.path.abspath(prof_dir)
+        prof.enable()
     w = worker.new(a.connection_string, a.dbname)
     cfg = dict(max_iter=a.max_iter, max_sleep=a.max_sleep, max_tasks=a.max_tasks, verbose=not a.quiet)
     if a.poll is not None:
         cfg["poll_sleep"] = a.poll
     w.configure(cfg)
     w.execute()
+    if prof_dir:
+        _dump()
     return 0
 
 

@@ -60,13 +60,43 @@ class GridFS:
 
     find_file = get
 
-    def list(self, match: dict | str | None = None) -> list[dict]:
+    # -- batched forms: one round trip per shard (a map job's 15 partition
+    # files + their index entries, a reduce job's 197 inputs)
+    def _by_shard(self, names):
+        groups: dict = {}
+        for i, n in enumerate(names):
+            c = self._home(n)
+            groups.setdefault(id(c), (c, []))[1].append(i)
+        return groups.values()
+
+    def store_many(self, items: list[tuple[str, bytes]]) -> None:
+        for c, idx in self._by_shard([n for n, _ in items]):
+            c.request("BLOB_PUT_MANY", self.db, *[x for i in idx for x in (items[i][0], bytes(items[i][1]))])
+
+    def get_many(self, names: list[str]) -> list[bytes | None]:
+        out: list = [None] * len(names)
+        for c, idx in self._by_shard(names):
+            _, f = c.request("BLOB_GET_MANY", self.db, *[names[i] for i in idx])
+            for j, i in enumerate(idx):
+                out[i] = f[2 * j + 1] if int(f[2 * j]) else None
+        return out
+
+    def remove_many(self, names: list[str]) -> int:
+        n = 0
+        for c, idx in self._by_shard(names):
+            _, f = c.request("BLOB_DEL_MANY", self.db, *[names[i] for i in idx])
+            n += int(f[0])
+        return n
+
+    def list(self, match: dict | str | None = None, prefix: str = "") -> list[dict]:
         """Files whose name matches a regex (``{"filename": {"$regex": r}}``
-        or a plain regex string); all files when ``match`` is None."""
+        or a plain regex string); all files when ``match`` is None.
+        ``prefix``: a literal prefix every match has (filtered by the
+        coordinator: the whole store is not sent over)."""
         rx = _regex_of(match)
         out = []
         for c in self.shards:
-            _, f = c.request("BLOB_LIST", self.db, "")
+            _, f = c.request("BLOB_LIST", self.db, prefix)
             names = [(f[i].decode("utf-8", "surrogateescape"), int(f[i + 1])) for i in range(0, len(f), 2)]
             out += [{"filename": n, "length": sz} for n, sz in names if rx is None or rx.search(n)]
         return out

@@ -210,16 +210,29 @@ class job:  # noqa: N801
         hi, lo, val, rep = ctx.table.compact()
         cols = dev.finalize(hi, lo, val, rep, ctx.source(), nparts, pmod, need_keys=True)
         fs, make_builder, _ = fsmod.router(self.cnn, None, self.storage, self.path)
+        # every storage's build replaces an existing file (BLOB_PUT overwrites,
+        # file builders rename over), so the reference's remove-before-build
+        # (job.lua:217-221) is one round trip per file with no effect; with the
+        # coordinator blob store, all partition files and their index entries
+        # of this job go in ONE request
+        host = utils.get_hostname()
+        outputs, index = [], []
         for p in range(nparts):
             if cols["bounds"][p + 1] == cols["bounds"][p]:
                 continue
             s = dev.partition_slice(cols, p)
             name = f"{self.path}/{self.results_ns}.P{p}.M{map_key}"
-            b = make_builder()
-            b.append(codec.encode_columnar(s["hi"], s["lo"], s["val"], s["key_off"], s["key_blob"]))
-            fs.remove_file(name)
-            b.build(name)
-            self._register_output(name)
+            outputs.append((name, codec.encode_columnar(s["hi"], s["lo"], s["val"], s["key_off"], s["key_blob"])))
+            index.append((INDEX_PREFIX + name + INDEX_SEP + host, b""))
+        gfs = self.cnn.gridfs()
+        if self.storage == "gridfs":
+            gfs.store_many(outputs + index)
+        else:
+            for name, blob in outputs:
+                b = make_builder()
+                b.append(blob)
+                b.build(name)
+            gfs.store_many(index)
         elapsed = _time.process_time() - clock1
         self.mark_as_written(elapsed)
         return elapsed
@@ -237,12 +250,19 @@ class job:  # noqa: N801
             job_file, res_file, mappers = value["file"], value["result"], value.get("mappers", [])
             fs, _, make_lines_iterator = fsmod.router(self.cnn, mappers, self.storage, self.path)
             import re
-            filenames = [v["filename"] for v in fs.list({"filename": {"$regex": "^" + re.escape(job_file) + r"\..*"}})]
+            match = {"filename": {"$regex": "^" + re.escape(job_file) + r"\..*"}}
+            if self.storage == "gridfs":
+                filenames = [v["filename"] for v in fs.list(match, prefix=job_file + ".")]
+            else:
+                filenames = [v["filename"] for v in fs.list(match)]
             rstore, rbuilder = result_store(self.cnn, self.storage, self.path)
             rstore.remove_file(res_file)
             blobs = None
             if dev_op is not None and filenames:
-                blobs = [fsmod.read_blob(self.cnn, self.storage, self.path, n) for n in filenames]
+                if self.storage == "gridfs":  # all inputs in one round trip per shard
+                    blobs = [b or b"" for b in self.cnn.gridfs().get_many(filenames)]
+                else:
+                    blobs = [fsmod.read_blob(self.cnn, self.storage, self.path, n) for n in filenames]
                 if not all(b[:4] == codec.MAGIC_COL for b in blobs):
                     blobs = None
             b = rbuilder()
@@ -262,10 +282,13 @@ class job:  # noqa: N801
             if not self.mark_as_written(elapsed):
                 return elapsed
             gfs = self.cnn.gridfs()
-            for n in filenames:
-                fs.remove_file(n)
-            for f in gfs.list({"filename": {"$regex": "^" + re.escape(INDEX_PREFIX + job_file) + r"\."}}):
-                gfs.remove_file(f["filename"])
+            if self.storage == "gridfs":
+                gfs.remove_many(filenames)
+            else:
+                for n in filenames:
+                    fs.remove_file(n)
+            ipre = INDEX_PREFIX + job_file + "."
+            gfs.remove_many([f["filename"] for f in gfs.list(None, prefix=ipre)])
             return elapsed
         return run
 

@@ -149,7 +149,8 @@ class server:  # noqa: N801
         match = re.compile("^" + re.escape(INDEX_PREFIX + path) + r"/.*P.*M.*$")
         parse = re.compile(r"^.*\.P([^.]+)\.M([^.]*)$")
         mappers: dict[int, set] = {}
-        for f in self.cnn.gridfs().list({"filename": {"$regex": match.pattern}}):
+        gfs = self.cnn.gridfs()
+        for f in gfs.list({"filename": {"$regex": match.pattern}}, prefix=INDEX_PREFIX + path + "/"):
             name, _, host = f["filename"].partition(INDEX_SEP)
             m = parse.match(name)
             if not m:

@@ -28,3 +28,22 @@ def test_rebalance_after_adding_a_shard():
     g2 = cnn_cls(both, "shard_db").gridfs()
     assert all(g2.get(f"blob{i}") == b"x" * i for i in range(40))
     assert sum(1 for i in range(40) if shard_of(f"blob{i}", 2) == 1) == after[1]["blobs"]
+
+
+def test_batched_blob_ops_over_shards():
+    """BLOB_PUT_MANY / GET_MANY / DEL_MANY and prefix listing, one request per
+    shard, same results as the one-blob operations."""
+    eps = ",".join(coordinator.start_local() for _ in range(3))
+    g = cnn_cls(eps, "batch_db").gridfs()
+    items = [(f"job/out.P{i}.M7", bytes([i]) * (i + 1)) for i in range(30)] + [("other/x", b"")]
+    g.store_many(items)
+    names = [n for n, _ in items] + ["missing"]
+    assert g.get_many(names) == [d for _, d in items] + [None]
+    assert all(g.get(n) == d for n, d in items)
+    listed = sorted(f["filename"] for f in g.list(None, prefix="job/out."))
+    assert listed == sorted(n for n, _ in items[:30])
+    g.store_many([("job/out.P0.M7", b"new")])  # PUT_MANY replaces
+    assert g.get("job/out.P0.M7") == b"new"
+    assert g.remove_many(names) == 31 and g.list(None, prefix="job/") == []
+    g.store_many([])
+    assert g.remove_many([]) == 0
