@@ -26,8 +26,14 @@ from .. import ops
 from ..ops import keys as K
 
 
+_HAS_GPU: bool | None = None
+
+
 def default_device():
-    if torch.cuda.is_available():
+    global _HAS_GPU
+    if _HAS_GPU is None:  # torch.cuda.is_available() costs ~2.6 ms a call
+        _HAS_GPU = torch.cuda.is_available()
+    if _HAS_GPU:
         return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
 
