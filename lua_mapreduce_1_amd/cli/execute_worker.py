@@ -18,6 +18,7 @@ def main(argv=None) -> int:
     ap.add_argument("--max-tasks", type=int, default=1)
     ap.add_argument("--poll", type=float, default=None)
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--gpu", default="auto", help="auto (one GPU per worker on a multi-GPU node), an index, or none")
     a = ap.parse_args(argv)
     from .. import worker
     prof_dir = os.environ.get("MR_WORKER_PROFILE")
@@ -38,7 +39,8 @@ def main(argv=None) -> int:
         prof_dir = os.path.abspath(prof_dir)
         prof.enable()
     w = worker.new(a.connection_string, a.dbname)
-    cfg = dict(max_iter=a.max_iter, max_sleep=a.max_sleep, max_tasks=a.max_tasks, verbose=not a.quiet)
+    cfg = dict(max_iter=a.max_iter, max_sleep=a.max_sleep, max_tasks=a.max_tasks, verbose=not a.quiet,
+               gpu=a.gpu if a.gpu in ("auto", "none") else int(a.gpu))
     if a.poll is not None:
         cfg["poll_sleep"] = a.poll
     w.configure(cfg)

@@ -10,6 +10,9 @@ traceback to the error channel, sleeps and retries, dying after
 New over the reference:
 * a heartbeat thread keeps the claimed job's lease alive, so the server can
   re-queue jobs of workers that die without raising (SIGKILL, node loss);
+* GPU placement: ``configure(gpu="auto")`` (the default) gives each worker
+  on a multi-GPU node its own device through a lock-file slot
+  (utils/gpu_slots.py); an int pins a device, ``"none"`` leaves torch's default;
 * a fault-injection hook for tests: ``MR_FAULT="map:<id>:raise[:n]"`` or
   ``"reduce:<id>:kill"`` raises (the first n times) or ``os._exit(137)``s when
   that job starts.
@@ -23,7 +26,7 @@ import threading
 import traceback
 
 from .. import utils
-from ..utils import TASK_STATUS
+from ..utils import TASK_STATUS, gpu_slots
 from ..utils.config import TUNABLES
 from . import job as job_mod
 from .cnn import cnn as cnn_cls
@@ -67,6 +70,8 @@ class worker:  # noqa: N801
         self.name = utils.get_hostname()
         self.verbose = True
         self.poll_sleep = utils.DEFAULT_SLEEP
+        self.gpu = "auto"
+        self._gpu_slot = None
         self._hb_stop = threading.Event()
         self._hb_thread = None
         self._stop = threading.Event()
@@ -77,7 +82,7 @@ class worker:  # noqa: N801
 
     def configure(self, t: dict | None = None, **kw) -> None:
         t = dict(t or {}, **kw)
-        allowed = {"max_iter", "max_sleep", "max_tasks", "verbose", "poll_sleep", "name"}
+        allowed = {"max_iter", "max_sleep", "max_tasks", "verbose", "poll_sleep", "name", "gpu"}
         for k, v in t.items():
             if k not in allowed:
                 raise ValueError(f"Unknown parameter: {k}")
@@ -163,6 +168,8 @@ class worker:  # noqa: N801
 
     def execute(self) -> None:
         failed: set = set()
+        if self._gpu_slot is None:  # before any job touches the GPU
+            self._gpu_slot = gpu_slots.place_worker(self.gpu)
         self._start_heartbeat()
         try:
             while True:
