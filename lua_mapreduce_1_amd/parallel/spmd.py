@@ -216,6 +216,12 @@ class SPMDEngine:
         self._tail_seen: set = set()
         self.iteration = 0
         self.finished = False
+        # iteration manifest: rank 0 records every iteration
+        # whose finalfn asked for another one, so a relaunched job (torchrun
+        # --max-restarts after a rank died and tore the communicator down)
+        # resumes there instead of at iteration 1
+        self.checkpoint_dir = self.params.get("checkpoint_dir") or TUNABLES.spmd_checkpoint or None
+        self.resumed_from = 0
 
 
     # ------------------------------------------------------------------------
@@ -857,9 +863,76 @@ class SPMDEngine:
         ]
         return "\n".join(lines) + "\n"
 
+    # -- checkpoint / resume and fault injection -------------------------------
+    def _manifest_path(self) -> str | None:
+        if not self.checkpoint_dir:
+            return None
+        return os.path.join(self.checkpoint_dir, "%s.spmd.json" % self.result_ns)
+
+    def _manifest_key(self) -> dict:
+        p = self.params
+        return {k: p.get(k) for k in ("taskfn", "mapfn", "partitionfn", "reducefn", "finalfn")} | {
+            "world": self.world}
+
+    def _load_manifest(self) -> int:
+        """Iterations already finished by an earlier launch of this same task
+        (server.lua:469-502 restart semantics: an unfinished task resumes, a
+        FINISHED one starts again from scratch).  Rank 0 decides, all agree."""
+        start = 0
+        path = self._manifest_path()
+        if self.rank == 0 and path and os.path.exists(path):
+            import json
+            with open(path) as f:
+                m = json.load(f)
+            if m.get("key") == self._manifest_key() and not m.get("finished"):
+                start = int(m.get("iteration", 0))
+        if self.world > 1:
+            start = D.broadcast_object(start, 0, self.group, self.device if self.device.type == "cuda" else None)
+        return start
+
+    def _save_manifest(self, finished: bool) -> None:
+        path = self._manifest_path()
+        if self.rank != 0 or not path:
+            return
+        import json
+        os.makedirs(self.checkpoint_dir, exist_ok=True)
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump({"key": self._manifest_key(), "iteration": self.iteration, "finished": finished,
+                       "time": time.time()}, f)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)  # atomic: a crash leaves the old or the new manifest
+
+    def _maybe_inject_fault(self) -> None:
+        """``MR_SPMD_FAULT=<iteration>:<rank>:raise|exit``:
+        that rank fails at the start of that iteration — ``exit`` leaves its
+        peers blocked in a collective, as a lost GPU or node would."""
+        spec = os.environ.get("MR_SPMD_FAULT", TUNABLES.spmd_fault)
+        if not spec:
+            return
+        it, rk, action = spec.split(":")[:3]
+        if int(it) != self.iteration + 1 or int(rk) != self.rank:
+            return
+        if action == "exit":
+            sys.stderr.write("# injected fault: rank %d exits at iteration %d\n" % (self.rank, self.iteration + 1))
+            sys.stderr.flush()
+            os._exit(17)
+        raise RuntimeError("injected fault: rank %d at iteration %d" % (self.rank, self.iteration + 1))
+
     def run(self) -> IterationResult:
-        """Iterate until finalfn returns something other than "loop"."""
+        """Iterate until finalfn returns something other than "loop".  With a
+        ``checkpoint_dir`` (param or MR_SPMD_CKPT) the job resumes after the
+        last iteration an earlier launch finished.  User state that must
+        survive a relaunch lives in a persistent_table, as in the reference;
+        a crash between finalfn and the manifest write re-runs that iteration
+        (finalfn is at-least-once, like the reference's restart)."""
+        start = self._load_manifest()
+        if start > self.iteration:
+            self._log("# Resuming after iteration %d\n" % start)
+            self.iteration = self.resumed_from = start
         while True:
+            self._maybe_inject_fault()
             self._log("# Iteration %d\n" % (self.iteration + 1))
             res = self.run_iteration()
             self._log(self.stats_block(res))
@@ -871,5 +944,7 @@ class SPMDEngine:
                 reply = D.broadcast_object(reply, 0, self.group, self.device if self.device.type == "cuda" else None)
             if reply != "loop":
                 self.finished = True
+                self._save_manifest(finished=True)
                 return res
+            self._save_manifest(finished=False)
             self._log("# LOOP again\n")

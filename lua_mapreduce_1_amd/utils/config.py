@@ -33,6 +33,10 @@ class Tunables:
                              "a RUNNING job whose worker stopped heart-beating this long is re-queued, s (new)")
     fault: str = _knob("MR_FAULT", "",
                        "worker fault injection 'phase:job:action[:times]', e.g. 'map:2:raise:1' (tests)")
+    spmd_checkpoint: str = _knob("MR_SPMD_CKPT", "",
+                                 "SPMD engine: directory of the iteration manifest (resume after a relaunch)")
+    spmd_fault: str = _knob("MR_SPMD_FAULT", "",
+                            "SPMD fault injection 'iteration:rank:raise|exit' at the start of that iteration")
     # -- device data plane
     wc_version: int = _knob("MR_WC_VERSION", 3, "word-count map kernel generation (3 = wordcount3.hip)")
     wc_chunk_max: int = _knob("MR_WC_CHUNK_MAX", 16 * 1024, "v2 map: max bytes per workgroup")
