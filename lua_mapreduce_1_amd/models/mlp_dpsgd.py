@@ -157,19 +157,67 @@ class DigitsTrainer:
             self.report[3:5].copy_(vl)
 
 
+def save_checkpoint(path: str, tr: DigitsTrainer, epoch: int, hist: list, finished: bool) -> None:
+    """Trainer snapshot after ``epoch`` (examples/APRIL-ANN/common.lua:191
+    serialises the whole trainer to GridFS every iteration): parameters,
+    momentum, stopping-rule state and history.  Written atomically."""
+    import json
+    import os
+    st = tr.stop
+    meta = {"epoch": epoch, "finished": finished, "hist": hist, "stop": {
+        "epoch": st.epoch, "best_epoch": st.best_epoch, "best_val": st.best_val,
+        "history": [list(h) for h in st.history]}}
+    blob = {"w": tr.w.detach().cpu(), "v": tr.v.detach().cpu(), "meta": json.dumps(meta)}
+    tmp = path + ".tmp"
+    torch.save(blob, tmp)
+    os.replace(tmp, path)
+
+
+def load_checkpoint(path: str) -> dict | None:
+    """The snapshot of an unfinished run, or None (missing file, or a finished
+    run: common.lua:59-64 resets when ``conf.finished``)."""
+    import json
+    import os
+    if not path or not os.path.exists(path):
+        return None
+    blob = torch.load(path, weights_only=True)  # tensors + a JSON string: nothing executable
+    meta = json.loads(blob["meta"])
+    if meta["finished"]:
+        return None
+    return {"w": blob["w"], "v": blob["v"], **meta}
+
+
 def train_spmd(device="cpu", group=None, data=None, hyper: dict | None = None, epochs: int | None = None,
-               verbose: bool = False, graphs: bool | None = None) -> dict:
+               verbose: bool = False, graphs: bool | None = None, checkpoint: str | None = None,
+               checkpoint_every: int = 1) -> dict:
     """Iterative DP-SGD, one process per GPU: each rank computes the gradients
     of its share of the iteration's map jobs (one fused launch), one all-reduce
     SUMs ``[grads | loss, correct, count]`` over ranks (RCCL on GPUs), then every
     rank applies the identical optimizer step (replicated parameters, like the
     reference's single finalfn).  On a GPU the two halves of the epoch are
-    replayed hipGraphs (``graphs=False`` runs them eagerly).  Returns the
-    training history."""
+    replayed hipGraphs (``graphs=False`` runs them eagerly).  With
+    ``checkpoint`` (a file path) rank 0 snapshots the trainer every
+    ``checkpoint_every`` epochs and a relaunch resumes from the snapshot of an
+    unfinished run (common.lua:57-77), bit-identical to an uninterrupted run.
+    Returns the training history."""
     from ..parallel import dist as D
     import torch.distributed as tdist
     rank, world = D.world_info(group)
     tr = DigitsTrainer(device, data, hyper)
+    snap = load_checkpoint(checkpoint) if rank == 0 and checkpoint else None
+    if world > 1 and checkpoint:
+        snap = D.broadcast_object(snap, 0, group, tr.device if tr.device.type == "cuda" else None)
+    hist = []
+    it = 0
+    if snap is not None:  # before capture: the graphs read w/v in place
+        tr.w.copy_(snap["w"])
+        tr.v.copy_(snap["v"])
+        s = snap["stop"]
+        tr.stop.epoch, tr.stop.best_epoch, tr.stop.best_val = s["epoch"], s["best_epoch"], s["best_val"]
+        tr.stop.history = [tuple(h) for h in s["history"]]
+        hist = list(snap["hist"])
+        it = int(snap["epoch"])
+    resumed_from = it
     J = tr.h["jobs_per_iteration"]
     jobs = [j for j in range(1, J + 1) if (j - 1) % world == rank]
     B = tr.h["bunch_size"]
@@ -179,8 +227,6 @@ def train_spmd(device="cpu", group=None, data=None, hyper: dict | None = None, e
         max_it = epochs if epochs is not None else tr.h["max_epochs"]
         # every epoch's bunch indices, generated once (same streams as eager)
         table = torch.stack([tr.bunch_indices(e, jobs) for e in range(1, max_it + 1)]) if jobs else None
-    hist = []
-    it = 0
     t0 = time.perf_counter()
     while True:
         it += 1
@@ -214,6 +260,10 @@ def train_spmd(device="cpu", group=None, data=None, hyper: dict | None = None, e
                      "tr_acc": tot[1] / max(tot[2], 1.0)})
         if verbose and rank == 0:
             print(tr.stop.state_string(), flush=True)
-        if (epochs is not None and it >= epochs) or (epochs is None and not go):
+        done = (epochs is not None and it >= epochs) or (epochs is None and not go)
+        if checkpoint and rank == 0 and (done or it % checkpoint_every == 0):
+            save_checkpoint(checkpoint, tr, it, hist, finished=done and epochs is None)
+        if done:
             break
-    return {"history": hist, "seconds": time.perf_counter() - t0, "params": tr.w, "best_epoch": tr.stop.best_epoch}
+    return {"history": hist, "seconds": time.perf_counter() - t0, "params": tr.w, "best_epoch": tr.stop.best_epoch,
+            "resumed_from": resumed_from}

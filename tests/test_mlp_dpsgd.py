@@ -193,6 +193,32 @@ def test_sgd_kernel_matches_cpu(gpu):
     assert torch.allclose(wd.cpu(), w, atol=1e-6) and torch.allclose(vd.cpu(), v, atol=1e-6)
 
 
+def _resume_check(device, ckpt, graphs=None):
+    full = T.train_spmd(device, data=DATA, epochs=8, graphs=graphs)
+    first = T.train_spmd(device, data=DATA, epochs=5, graphs=graphs, checkpoint=ckpt)
+    assert first["resumed_from"] == 0
+    rest = T.train_spmd(device, data=DATA, epochs=8, graphs=graphs, checkpoint=ckpt)
+    assert rest["resumed_from"] == 5
+    assert torch.equal(rest["params"], full["params"])
+    assert [h["va_loss"] for h in rest["history"]] == [h["va_loss"] for h in full["history"]]
+
+
+def test_checkpoint_resume_is_bit_identical(tmp_path):
+    """A run stopped after epoch 5 and relaunched from its snapshot ends with
+    the parameters of an uninterrupted 8-epoch run (APRIL-ANN restore,
+    common.lua:57-77); a finished run's snapshot is not resumed."""
+    ckpt = str(tmp_path / "mlp.pt")
+    _resume_check("cpu", ckpt)
+    T.train_spmd("cpu", data=DATA, hyper={"min_epochs": 2, "max_epochs": 3}, checkpoint=ckpt)
+    assert T.load_checkpoint(ckpt) is None  # finished by the stopping rule
+    assert T.train_spmd("cpu", data=DATA, epochs=2, checkpoint=ckpt)["resumed_from"] == 0
+
+
+@pytest.mark.gpu
+def test_checkpoint_resume_graphs_gpu(gpu, tmp_path):
+    _resume_check(gpu, str(tmp_path / "mlp.pt"), graphs=True)
+
+
 @pytest.mark.gpu
 def test_train_spmd_gpu_matches_cpu(gpu):
     rg = T.train_spmd(gpu, data=DATA, epochs=6)
