@@ -68,10 +68,18 @@ def bind_to_gpu_numa(device) -> list[int] | None:
     return use or None
 
 
-def init_from_env(backend: str | None = None, timeout_s: float = 600.0, use_gpu: bool | None = None):
+def init_from_env(backend: str | None = None, timeout_s: float | None = None, use_gpu: bool | None = None):
     """Initialise the default group from torchrun's env (no-op for WORLD_SIZE=1).
 
+    ``timeout_s`` (default ``MR_COLL_TIMEOUT``) bounds every collective: a
+    rank that hangs or dies makes its peers' collectives fail after it instead
+    of blocking forever (SURVEY.md §5.3 failure detection), and torchrun's
+    ``--max-restarts`` then relaunches the job.
+
     Returns (rank, world, device)."""
+    if timeout_s is None:
+        from ..utils.config import TUNABLES
+        timeout_s = TUNABLES.coll_timeout
     rank, world, local = env_world()
     if use_gpu is None:
         use_gpu = torch.cuda.is_available() and backend != "gloo"

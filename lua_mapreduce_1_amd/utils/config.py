@@ -35,6 +35,8 @@ class Tunables:
                        "worker fault injection 'phase:job:action[:times]', e.g. 'map:2:raise:1' (tests)")
     spmd_checkpoint: str = _knob("MR_SPMD_CKPT", "",
                                  "SPMD engine: directory of the iteration manifest (resume after a relaunch)")
+    coll_timeout: float = _knob("MR_COLL_TIMEOUT", 600.0,
+                                "collective timeout, s: a hung or dead rank fails its peers' collectives")
     spmd_fault: str = _knob("MR_SPMD_FAULT", "",
                             "SPMD fault injection 'iteration:rank:raise|exit' at the start of that iteration")
     # -- device data plane
