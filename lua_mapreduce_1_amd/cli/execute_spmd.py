@@ -5,7 +5,7 @@ string and database (there is no job queue to share):
 
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
         [--max-restarts 3] -m lua_mapreduce_1_amd.cli.execute_spmd \\
-        [--checkpoint-dir DIR] [--device auto|cpu] [--num-partitions R] [-v] \\
+        [--checkpoint-dir DIR] [--device auto|cpu] [--num-partitions R] [--split-glob G]... [-v] \\
         TASKFN MAPFN PARTITIONFN REDUCEFN [FINALFN|nil] [INIT_ARGS...]
 
 One process (no torchrun) runs world size 1.  ``--checkpoint-dir`` makes an
@@ -28,6 +28,9 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default="auto", choices=("auto", "cpu"))
     ap.add_argument("--num-partitions", type=int, default=None)
     ap.add_argument("--result-ns", default=None)
+    ap.add_argument("--split-glob", action="append", default=[],
+                    help="files loaded (sorted, in order of the options) into the pinned SplitStore that "
+                         "map modules with device_input='split' read; repeatable")
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("taskfn")
     ap.add_argument("mapfn")
@@ -57,7 +60,17 @@ def main(argv=None) -> int:
     params = {"taskfn": n(a.taskfn), "mapfn": n(a.mapfn), "partitionfn": n(a.partitionfn),
               "reducefn": n(a.reducefn), "finalfn": n(finalfn) if finalfn else None, "init_args": init_args,
               "checkpoint_dir": a.checkpoint_dir, "num_partitions": a.num_partitions, "result_ns": a.result_ns}
-    eng = SPMDEngine(params, device=device, verbose=a.verbose or rank == 0)
+    store = None
+    if a.split_glob:
+        import glob
+        from ..parallel.spmd import SplitStore
+        files = [f for g in a.split_glob for f in sorted(glob.glob(g))]
+        splits = []
+        for f in files:
+            with open(f, "rb") as fh:
+                splits.append(fh.read())
+        store = SplitStore(splits, pin=device.type == "cuda")
+    eng = SPMDEngine(params, device=device, split_store=store, verbose=a.verbose or rank == 0)
     eng.run()
     if world > 1:
         D.barrier(device=device if device.type == "cuda" else None)

@@ -78,7 +78,6 @@ def init_from_env(backend: str | None = None, timeout_s: float | None = None, us
 
     Returns (rank, world, device)."""
     if timeout_s is None:
-        from ..utils.config import TUNABLES
         timeout_s = TUNABLES.coll_timeout
     rank, world, local = env_world()
     if use_gpu is None:
@@ -95,8 +94,16 @@ def init_from_env(backend: str | None = None, timeout_s: float | None = None, us
         kw = {}
         if be == "nccl" and use_gpu:
             kw["device_id"] = device
-        dist.init_process_group(be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s),
-                                **kw)
+        td = datetime.timedelta(seconds=timeout_s)
+        attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+        if attempt != "0" and os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true":
+            # a torchrun relaunch (--max-restarts) talks to the same agent-hosted
+            # store as the failed attempt, whose peer addresses are still in it:
+            # key this attempt's rendezvous apart
+            store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                                  is_master=False, timeout=td)
+            kw["store"] = dist.PrefixStore("mr_attempt_%s" % attempt, store)
+        dist.init_process_group(be, rank=rank, world_size=world, timeout=td, **kw)
     return rank, world, device
 
 

@@ -905,14 +905,18 @@ class SPMDEngine:
         os.replace(tmp, path)  # atomic: a crash leaves the old or the new manifest
 
     def _maybe_inject_fault(self) -> None:
-        """``MR_SPMD_FAULT=<iteration>:<rank>:raise|exit``:
+        """``MR_SPMD_FAULT=<iteration>:<rank>:raise|exit[:<attempt>]``:
         that rank fails at the start of that iteration — ``exit`` leaves its
         peers blocked in a collective, as a lost GPU or node would."""
         spec = os.environ.get("MR_SPMD_FAULT", TUNABLES.spmd_fault)
         if not spec:
             return
-        it, rk, action = spec.split(":")[:3]
+        f = spec.split(":")
+        it, rk, action = f[:3]
         if int(it) != self.iteration + 1 or int(rk) != self.rank:
+            return
+        # optional 4th field: only in that torchrun attempt (0 = first launch)
+        if len(f) > 3 and int(f[3]) != int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")):
             return
         if action == "exit":
             sys.stderr.write("# injected fault: rank %d exits at iteration %d\n" % (self.rank, self.iteration + 1))

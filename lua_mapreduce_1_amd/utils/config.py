@@ -38,7 +38,7 @@ class Tunables:
     coll_timeout: float = _knob("MR_COLL_TIMEOUT", 600.0,
                                 "collective timeout, s: a hung or dead rank fails its peers' collectives")
     spmd_fault: str = _knob("MR_SPMD_FAULT", "",
-                            "SPMD fault injection 'iteration:rank:raise|exit' at the start of that iteration")
+                            "SPMD fault injection 'iteration:rank:raise|exit[:attempt]' at the start of that iteration")
     # -- device data plane
     wc_version: int = _knob("MR_WC_VERSION", 3, "word-count map kernel generation (3 = wordcount3.hip)")
     wc_chunk_max: int = _knob("MR_WC_CHUNK_MAX", 16 * 1024, "v2 map: max bytes per workgroup")

@@ -65,3 +65,30 @@ def test_execute_spmd_wordcount_gpu():
     assert p.returncode == 0, p.stderr.decode(errors="replace")[-3000:]
     got = sorted(line for line in p.stdout.splitlines() if line.strip())
     assert got == _naive()
+
+
+def test_execute_spmd_torchrun_restart_resumes(tmp_path):
+    """Elastic recovery end to end: under ``torchrun --max-restarts 1`` rank 1
+    dies at the start of iteration 2 of the first attempt only; torchrun tears
+    the job down and relaunches both ranks, which resume after iteration 1 from
+    the manifest and finish iterations 2 and 3 (3 finalfn calls in all)."""
+    import json
+    state = str(tmp_path / "state.json")
+    it = "lua_mapreduce_1_amd.examples.IterativeWordCount"
+    init = json.dumps({"nsplits": 4, "num_reducers": 3, "state_file": state, "iterations": 3})
+    env = dict(_env(), MR_SPMD_FAULT="2:1:exit:0")
+    import importlib
+    files = importlib.import_module(WC + "taskfn").FILES  # the oracle's files, as SplitStore splits
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--max-restarts", "1", "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "execute_spmd.py"), "--device", "cpu", "--checkpoint-dir", str(tmp_path / "ckpt"),
+           *[a for f in files for a in ("--split-glob", f)], it, it, it, it, it, init]
+    p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, timeout=300)
+    err = p.stderr.decode(errors="replace")
+    assert p.returncode == 0, err[-3000:]
+    assert "injected fault: rank 1 exits at iteration 2" in err
+    assert "# Resuming after iteration 1" in err
+    with open(state) as f:
+        totals = json.load(f)["totals"]
+    assert len(totals) == 3 and len(set(totals)) == 1
+    assert totals[0] == sum(int(line.split()[0]) for line in _naive())
