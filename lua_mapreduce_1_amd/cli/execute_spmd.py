@@ -6,13 +6,15 @@ string and database (there is no job queue to share):
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
         [--max-restarts 3] -m lua_mapreduce_1_amd.cli.execute_spmd \\
         [--checkpoint-dir DIR] [--device auto|cpu] [--num-partitions R] [--split-glob G]... [-v] \\
-        TASKFN MAPFN PARTITIONFN REDUCEFN [FINALFN|nil] [INIT_ARGS...]
+        TASKFN MAPFN PARTITIONFN REDUCEFN [FINALFN|nil] [COMBINERFN|nil] [STORAGE|nil] [INIT_ARGS...]
 
 One process (no torchrun) runs world size 1.  ``--checkpoint-dir`` makes an
 iterative task resume after its last finished iteration when torchrun
-relaunches the ranks after a failure (``--max-restarts``).  The map module
-needs a ``device_mapfn``; host-only map functions run under
-execute_server/execute_worker.  INIT_ARGS are passed to every module's
+relaunches the ranks after a failure (``--max-restarts``).  A map module
+with a ``device_mapfn`` runs on the HIP data plane (parallel/spmd.py); a
+plain ``mapfn`` runs the reference's host semantics on every rank
+(parallel/spmd_host.py).  STORAGE is accepted for parity and ignored (the
+shuffle goes over collectives).  INIT_ARGS are passed to every module's
 ``init`` (execute_server.lua:50); a single JSON object argument is decoded.
 """
 from __future__ import annotations
@@ -40,8 +42,10 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     rest = list(a.rest)
     finalfn = rest.pop(0) if rest else None
-    if finalfn == "nil":
-        finalfn = None
+    combinerfn = rest.pop(0) if rest else None
+    _storage = rest.pop(0) if rest else None  # accepted for CLI parity: SPMD ranks shuffle over collectives
+    finalfn = None if finalfn == "nil" else finalfn
+    combinerfn = None if combinerfn == "nil" else combinerfn
     init_args = rest
     if len(rest) == 1 and rest[0].startswith("{"):
         init_args = json.loads(rest[0])
@@ -58,7 +62,8 @@ def main(argv=None) -> int:
     rank, world, device = D.init_from_env(use_gpu=use_gpu)
     n = modules.normalize
     params = {"taskfn": n(a.taskfn), "mapfn": n(a.mapfn), "partitionfn": n(a.partitionfn),
-              "reducefn": n(a.reducefn), "finalfn": n(finalfn) if finalfn else None, "init_args": init_args,
+              "reducefn": n(a.reducefn), "finalfn": n(finalfn) if finalfn else None,
+              "combinerfn": n(combinerfn) if combinerfn else None, "init_args": init_args,
               "checkpoint_dir": a.checkpoint_dir, "num_partitions": a.num_partitions, "result_ns": a.result_ns}
     store = None
     if a.split_glob:
@@ -70,7 +75,11 @@ def main(argv=None) -> int:
             with open(f, "rb") as fh:
                 splits.append(fh.read())
         store = SplitStore(splits, pin=device.type == "cuda")
-    eng = SPMDEngine(params, device=device, split_store=store, verbose=a.verbose or rank == 0)
+    if modules.field(modules.load(params["mapfn"]), "device_mapfn") is not None:
+        eng = SPMDEngine(params, device=device, split_store=store, verbose=a.verbose or rank == 0)
+    else:  # a reference-style host mapfn: same launch, host map/reduce (parallel/spmd_host.py)
+        from ..parallel.spmd_host import HostSPMDEngine
+        eng = HostSPMDEngine(params, device=device, verbose=a.verbose or rank == 0)
     eng.run()
     if world > 1:
         D.barrier(device=device if device.type == "cuda" else None)

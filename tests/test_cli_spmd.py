@@ -82,7 +82,7 @@ def test_execute_spmd_torchrun_restart_resumes(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--max-restarts", "1", "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "execute_spmd.py"), "--device", "cpu", "--checkpoint-dir", str(tmp_path / "ckpt"),
-           *[a for f in files for a in ("--split-glob", f)], it, it, it, it, it, init]
+           *[a for f in files for a in ("--split-glob", f)], it, it, it, it, it, "nil", "nil", init]
     p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, timeout=300)
     err = p.stderr.decode(errors="replace")
     assert p.returncode == 0, err[-3000:]
@@ -92,3 +92,41 @@ def test_execute_spmd_torchrun_restart_resumes(tmp_path):
         totals = json.load(f)["totals"]
     assert len(totals) == 3 and len(set(totals)) == 1
     assert totals[0] == sum(int(line.split()[0]) for line in _naive())
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_execute_spmd_host_modules(world, tmp_path):
+    """A plain host mapfn (no device_mapfn) runs on every rank with the
+    reference's host semantics: combiner, integer partitions, ordered reduce."""
+    mod = tmp_path / "hostwc.py"
+    mod.write_text(
+        "import importlib\n"
+        "FILES = importlib.import_module('lua_mapreduce_1_amd.examples.WordCount.taskfn').FILES\n"
+        "def taskfn(emit):\n"
+        "    for i, f in enumerate(FILES, 1):\n"
+        "        emit(i, f)\n"
+        "def mapfn(k, v, emit):\n"
+        "    for line in open(v, 'rb'):\n"
+        "        for w in line.split():\n"
+        "            emit(w.decode('utf-8', 'surrogateescape'), 1)\n"
+        "def partitionfn(k):\n"
+        "    return sum(k.encode('utf-8', 'surrogateescape')) % 7\n"
+        "def reducefn(k, vs, emit):\n"
+        "    emit(sum(vs))\n"
+        "combinerfn = reducefn\n"
+        "def finalfn(pairs):\n"
+        "    for k, v in pairs:\n"
+        "        print(v[0], k)\n"
+        "    return True\n")
+    env = dict(_env(), PYTHONPATH=ROOT + os.pathsep + str(tmp_path))
+    args = ["hostwc"] * 5 + ["hostwc"]  # FINALFN, COMBINERFN
+    if world == 1:
+        cmd = [sys.executable, os.path.join(ROOT, "execute_spmd.py"), "--device", "cpu", *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "execute_spmd.py"),
+               "--device", "cpu", *args]
+    p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, timeout=240)
+    assert p.returncode == 0, p.stderr.decode(errors="replace")[-3000:]
+    got = sorted(line for line in p.stdout.splitlines() if line.strip() and b"[Gloo]" not in line)
+    assert got == _naive()
