@@ -23,4 +23,17 @@ def utest(connection_string=None, dbname: str = "test") -> None:
     _s.utest(connection_string, dbname)
 
 
-__all__ = ["_VERSION", "_NAME", "worker", "server", "utils", "tuple", "persistent_table", "utest"]
+def spmd(params: dict, **kw):
+    """SPMD engine for a task table (server:configure's keys plus
+    ``checkpoint_dir``): the HIP data plane when the map module has a
+    ``device_mapfn`` (parallel/spmd.py), the reference's host semantics
+    otherwise (parallel/spmd_host.py).  ``.run()`` iterates to completion."""
+    from .runtime import modules
+    if modules.field(modules.load(params["mapfn"]), "device_mapfn") is not None:
+        from .parallel.spmd import SPMDEngine
+        return SPMDEngine(params, **kw)
+    from .parallel.spmd_host import HostSPMDEngine
+    return HostSPMDEngine(params, **kw)
+
+
+__all__ = ["_VERSION", "_NAME", "worker", "server", "utils", "tuple", "persistent_table", "utest", "spmd"]

@@ -55,7 +55,6 @@ def main(argv=None) -> int:
         pass
     import torch
     from ..parallel import dist as D
-    from ..parallel.spmd import SPMDEngine
     from ..runtime import modules
 
     use_gpu = a.device == "auto" and torch.cuda.is_available()
@@ -75,11 +74,8 @@ def main(argv=None) -> int:
             with open(f, "rb") as fh:
                 splits.append(fh.read())
         store = SplitStore(splits, pin=device.type == "cuda")
-    if modules.field(modules.load(params["mapfn"]), "device_mapfn") is not None:
-        eng = SPMDEngine(params, device=device, split_store=store, verbose=a.verbose or rank == 0)
-    else:  # a reference-style host mapfn: same launch, host map/reduce (parallel/spmd_host.py)
-        from ..parallel.spmd_host import HostSPMDEngine
-        eng = HostSPMDEngine(params, device=device, verbose=a.verbose or rank == 0)
+    from .. import spmd
+    eng = spmd(params, device=device, split_store=store, verbose=a.verbose or rank == 0)
     eng.run()
     if world > 1:
         D.barrier(device=device if device.type == "cuda" else None)
