@@ -101,3 +101,52 @@ def test_spmd_resume_after_rank_failure(tmp_path):
     os.remove(state)
     codes, (resumed, iters, _got) = _launch(2, ckpt, state, "")
     assert codes == [0, 0] and resumed == 0 and iters == 4
+
+
+def test_host_spmd_resume_in_process(tmp_path, monkeypatch):
+    """The host-plane engine (reference-style mapfn) shares the manifest logic:
+    a fault raised at the start of iteration 2 leaves iteration 1 recorded and
+    a new engine resumes after it."""
+    import sys
+    mod = tmp_path / "hostiter.py"
+    mod.write_text(
+        "import json, os\n"
+        "STATE = None\n"
+        "def init(a):\n"
+        "    global STATE\n"
+        "    STATE = a['state']\n"
+        "def taskfn(emit):\n"
+        "    for i in range(1, 4):\n"
+        "        emit(i, i)\n"
+        "def mapfn(k, v, emit):\n"
+        "    emit('sum', v)\n"
+        "def partitionfn(k):\n"
+        "    return 0\n"
+        "def reducefn(k, vs, emit):\n"
+        "    emit(sum(vs))\n"
+        "def finalfn(pairs):\n"
+        "    st = json.load(open(STATE)) if os.path.exists(STATE) else []\n"
+        "    st += [v[0] for _k, v in pairs]\n"
+        "    json.dump(st, open(STATE, 'w'))\n"
+        "    return 'loop' if len(st) < 3 else True\n")
+    monkeypatch.syspath_prepend(str(tmp_path))
+    from lua_mapreduce_1_amd import spmd
+    from lua_mapreduce_1_amd.parallel.spmd_host import HostSPMDEngine
+    state = str(tmp_path / "st.json")
+    params = dict(taskfn="hostiter", mapfn="hostiter", partitionfn="hostiter", reducefn="hostiter",
+                  finalfn="hostiter", init_args={"state": state}, checkpoint_dir=str(tmp_path / "ck"))
+    monkeypatch.setenv("MR_SPMD_FAULT", "2:0:raise")
+    eng = spmd(params)
+    assert isinstance(eng, HostSPMDEngine)
+    try:
+        eng.run()
+        raise AssertionError("fault not injected")
+    except RuntimeError as e:
+        assert "injected fault" in str(e)
+    monkeypatch.delenv("MR_SPMD_FAULT")
+    eng = spmd(params)
+    eng.run()
+    assert eng.resumed_from == 1 and eng.iteration == 3
+    with open(state) as f:
+        assert json.load(f) == [6, 6, 6]
+    sys.modules.pop("hostiter", None)
