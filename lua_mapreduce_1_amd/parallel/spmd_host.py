@@ -23,7 +23,9 @@ plane (device_mapfn) keeps using the HIP kernels through SPMDEngine.
 """
 from __future__ import annotations
 
+import sys
 import time
+import traceback
 
 import torch.distributed as tdist
 
@@ -103,7 +105,10 @@ class HostSPMDEngine(SPMDEngine):
         t_start = time.time()
         jobs = self._jobs()
         j0, j1 = assign_contiguous([1] * len(jobs), self.rank, self.world)
-        combiner = modules.field(self.combmod, "combinerfn") if self.combmod is not None else None
+        # the reducefn module's combinerfn, as the workers use (task.lua:325,
+        # job.lua:160-161; runtime/job.py), else the configured combinerfn module's
+        combiner = modules.field(self.redmod, "combinerfn") or (
+            modules.field(self.combmod, "combinerfn") if self.combmod is not None else None)
         partitioner = modules.field(self.partmod, "partitionfn")
         local: dict = {}  # partition -> key -> values, in job order
         failed = 0
@@ -115,9 +120,11 @@ class HostSPMDEngine(SPMDEngine):
                 try:
                     parts = self._map_job(r.key, r.value, combiner, partitioner)
                     break
-                except Exception:
+                except Exception:  # BROKEN -> retried; FAILED after MAX_JOB_RETRIES (server.lua:194-213)
                     r.repetitions += 1
                     parts = None
+                    sys.stderr.write("# rank %d map job %r attempt %d failed:\n%s" % (
+                        self.rank, r.key, attempt + 1, traceback.format_exc()))
             if parts is None:
                 r.status = STATUS.FAILED
                 failed += 1
