@@ -150,3 +150,39 @@ def test_host_spmd_resume_in_process(tmp_path, monkeypatch):
     with open(state) as f:
         assert json.load(f) == [6, 6, 6]
     sys.modules.pop("hostiter", None)
+
+
+def test_host_spmd_failed_job_after_retries(tmp_path, monkeypatch, capsys):
+    """A map job that always raises is retried MAX_JOB_RETRIES times, then
+    counted FAILED and left out of the results (server.lua:194-213)."""
+    mod = tmp_path / "hostfail.py"
+    mod.write_text(
+        "CALLS = {}\n"
+        "def taskfn(emit):\n"
+        "    for i in range(1, 5):\n"
+        "        emit(i, i)\n"
+        "def mapfn(k, v, emit):\n"
+        "    CALLS[k] = CALLS.get(k, 0) + 1\n"
+        "    if k == 2:\n"
+        "        raise ValueError('bad split')\n"
+        "    emit('sum', v)\n"
+        "def partitionfn(k):\n"
+        "    return 0\n"
+        "def reducefn(k, vs, emit):\n"
+        "    emit(sum(vs))\n"
+        "OUT = []\n"
+        "def finalfn(pairs):\n"
+        "    OUT.extend(pairs)\n"
+        "    return True\n")
+    monkeypatch.syspath_prepend(str(tmp_path))
+    monkeypatch.delenv("MR_SPMD_FAULT", raising=False)
+    import importlib
+    from lua_mapreduce_1_amd import spmd, utils
+    eng = spmd(dict(taskfn="hostfail", mapfn="hostfail", partitionfn="hostfail", reducefn="hostfail",
+                    finalfn="hostfail"), verbose=True)
+    res = eng.run()
+    m = importlib.import_module("hostfail")
+    assert m.CALLS[2] == utils.MAX_JOB_RETRIES and m.CALLS[1] == 1
+    assert res.failed_maps == 1 and m.OUT == [("sum", [1 + 3 + 4])]
+    err = capsys.readouterr().err
+    assert "# Failed maps     1" in err and "bad split" in err
