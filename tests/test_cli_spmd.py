@@ -46,7 +46,7 @@ def test_execute_spmd_wordcount_matches_naive(world):
     if world == 1:
         cmd = [sys.executable, os.path.join(ROOT, "execute_spmd.py"), "--device", "cpu", *ARGS]
     else:
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}", "--local-ranks-filter", "0",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "execute_spmd.py"),
                "--device", "cpu", *ARGS]
     p = subprocess.run(cmd, cwd="/tmp", env=_env(), capture_output=True, timeout=240)
@@ -123,7 +123,7 @@ def test_execute_spmd_host_modules(world, tmp_path):
     if world == 1:
         cmd = [sys.executable, os.path.join(ROOT, "execute_spmd.py"), "--device", "cpu", *args]
     else:
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}", "--local-ranks-filter", "0",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "execute_spmd.py"),
                "--device", "cpu", *args]
     p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, timeout=240)
