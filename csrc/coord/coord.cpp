@@ -418,11 +418,21 @@ class Store {
     }
   }
 
+  // Journal record: u32 length | u32 FNV-1a of the body | body.  A record cut
+  // short by a crash (or one whose checksum does not match) ends the replay,
+  // and the file is truncated there before appending resumes, so the next
+  // record never lands behind a stale length prefix.
+  static uint32_t body_sum(const std::string& body) {
+    uint32_t h = 2166136261u;
+    for (unsigned char c : body) h = (h ^ c) * 16777619u;
+    return h;
+  }
+
   void log(const std::string& body) {
     if (!journal || replaying) return;
-    uint32_t n = (uint32_t)body.size();
-    fwrite(&n, 4, 1, journal);
-    fwrite(body.data(), 1, n, journal);
+    uint32_t hdr[2] = {(uint32_t)body.size(), body_sum(body)};
+    fwrite(hdr, 4, 2, journal);
+    fwrite(body.data(), 1, body.size(), journal);
     fflush(journal);
   }
 
@@ -441,18 +451,22 @@ class Store {
   bool open_journal(const char* path) {
     if (!path || !*path) return true;
     FILE* f = fopen(path, "rb");
+    long good = 0;  // end of the last complete, intact record
     if (f) {
       replaying = true;
       for (;;) {
-        uint32_t n;
-        if (fread(&n, 4, 1, f) != 1) break;
-        std::string body(n, '\0');
-        if (fread(&body[0], 1, n, f) != n) break;
+        uint32_t hdr[2];
+        if (fread(hdr, 4, 2, f) != 2) break;
+        std::string body(hdr[0], '\0');
+        if (fread(&body[0], 1, hdr[0], f) != hdr[0]) break;
+        if (body_sum(body) != hdr[1]) break;
         Writer w;
         handle(body, w);
+        good = ftell(f);
       }
       replaying = false;
       fclose(f);
+      if (truncate(path, good) != 0) return false;
     }
     journal = fopen(path, "ab");
     return journal != nullptr;

@@ -858,7 +858,8 @@ class SPMDEngine:
             "# Sum(sys_time)           %f" % (mr + rr - ms - rs), "#   Map cluster time      %f" % T["map"],
             "#   Reduce cluster time   %f" % (T["shuffle"] + T["reduce"]),
             "# Cluster time            %f" % (T["map"] + T["shuffle"] + T["reduce"]),
-            "# Failed maps     %d" % getattr(res, "failed_maps", 0), "# Failed reduces  0",
+            "# Failed maps     %d" % getattr(res, "failed_maps", 0),
+            "# Failed reduces  %d" % getattr(res, "failed_reduces", 0),
             "# Server time %f" % T["iteration"],
         ]
         return "\n".join(lines) + "\n"
@@ -870,9 +871,18 @@ class SPMDEngine:
         return os.path.join(self.checkpoint_dir, "%s.spmd.json" % self.result_ns)
 
     def _manifest_key(self) -> dict:
+        """Identity of the job a manifest belongs to: a relaunch with other
+        modules, partition count or init args starts from scratch."""
+        import hashlib
+        import json
         p = self.params
-        return {k: p.get(k) for k in ("taskfn", "mapfn", "partitionfn", "reducefn", "finalfn")} | {
-            "world": self.world}
+        try:
+            args = json.dumps(p.get("init_args"), sort_keys=True, default=repr)
+        except (TypeError, ValueError):
+            args = repr(p.get("init_args"))
+        return {k: p.get(k) for k in ("taskfn", "mapfn", "partitionfn", "reducefn", "finalfn", "combinerfn",
+                                      "num_partitions")} | {
+            "world": self.world, "init_args": hashlib.sha1(args.encode()).hexdigest()}
 
     def _load_manifest(self) -> int:
         """Iterations already finished by an earlier launch of this same task

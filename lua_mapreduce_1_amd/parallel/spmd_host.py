@@ -167,28 +167,53 @@ class HostSPMDEngine(SPMDEngine):
             pmax = D.broadcast_object(pmax, 0, self.group)
         digits = len(str(max(pmax, 0)))
         self._host_parts = {}
+        failed_red = 0
         for p in sorted(local):
             c0, t0 = time.process_time(), time.time()
-            recs = []
-            for k in utils.keys_sorted(local[p]):
-                v = local[p][k]
-                if not aci or len(v) > 1:
-                    out = []
-                    red(k, v, out.append)
-                    v = [tuple_(x) for x in out]
-                recs.append((k, v))
-            name = ("%s.P%0" + str(digits) + "d") % (self.result_ns, p)
-            res.result_names[p] = name
-            self._host_parts[p] = recs
-            r = JobRecord(p, {"result": name})
-            r.status, r.started, r.written, r.worker = STATUS.WRITTEN, t0, time.time(), self.rank
+            r = JobRecord(p, {"result": ("%s.P%0" + str(digits) + "d") % (self.result_ns, p)})
+            r.worker, r.started = self.rank, t0
+            recs = None
+            # a reduce job that raises is BROKEN and re-run; after
+            # MAX_JOB_RETRIES it is FAILED and its partition is dropped
+            # (server.lua:194-213, job.lua:322-342)
+            for attempt in range(utils.MAX_JOB_RETRIES):
+                try:
+                    recs = self._reduce_partition(local[p], red, aci)
+                    break
+                except Exception:  # noqa: BLE001
+                    r.repetitions += 1
+                    sys.stderr.write("# rank %d reduce job P%d attempt %d failed:\n%s" % (
+                        self.rank, p, attempt + 1, traceback.format_exc()))
+            r.written = time.time()
             r.cpu_time, r.real_time = time.process_time() - c0, r.written - t0
+            if recs is None:
+                r.status = STATUS.FAILED
+                failed_red += 1
+            else:
+                r.status = STATUS.WRITTEN
+                res.result_names[p] = r.value["result"]
+                self._host_parts[p] = recs
             res.red_jobs.append(r)
+        if self.world > 1:
+            failed_red = D.all_reduce_sum_int(failed_red, self.device)
+        res.failed_reduces = failed_red
         res.failed_maps = failed
         res.distinct_keys = sum(len(v) for v in self._host_parts.values())
         t_end = time.time()
         T.update(map=t_map - t_start, shuffle=t_shuf - t_map, reduce=t_end - t_shuf, iteration=t_end - t_start)
         return res
+
+    @staticmethod
+    def _reduce_partition(kv: dict, red, aci: bool) -> list:
+        recs = []
+        for k in utils.keys_sorted(kv):
+            v = kv[k]
+            if not aci or len(v) > 1:
+                out = []
+                red(k, v, out.append)
+                v = [tuple_(x) for x in out]
+            recs.append((k, v))
+        return recs
 
     def gather_results(self, res: IterationResult) -> list:
         mine = [(res.result_names[p], self._host_parts[p]) for p in res.result_names]

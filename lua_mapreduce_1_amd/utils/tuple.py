@@ -8,6 +8,12 @@ this module keeps the reference's *API* — ``tuple(...)`` converts (nested)
 lists into tuples, returns a single scalar unchanged, and interns the result;
 ``tuple.stats()`` reports live interned tuples — plus the Jenkins OAAT hash
 (used by :mod:`..utils` for stable tuple hashing across processes).
+
+Interning mimics the reference's weak-valued buckets (tuple.lua:250-302): a
+CPython tuple cannot be weakly referenced, so the intern table is pruned of
+entries nobody else references whenever it has doubled since the last prune
+(amortised O(1) per insert) — a long-running worker that emits millions of
+distinct list keys keeps only the live ones.
 """
 from __future__ import annotations
 
@@ -16,12 +22,27 @@ import sys
 from typing import Any
 
 NUM_BUCKETS = 2 ** 18
-_INTERN: dict = {}
-
-
-
+PRUNE_MIN = 1 << 16  # entries before the first prune
 
 builtins_tuple = builtins.tuple
+_INTERN: dict = {}
+_limit = PRUNE_MIN
+
+
+def _prune() -> None:
+    """Drop entries referenced only by the table (key and value are the same
+    object: 2 references, plus the loop variable and getrefcount's argument).
+    Outer tuples go first, so a pass repeats while it frees anything."""
+    global _limit
+    while True:
+        dead = [k for k in _INTERN if sys.getrefcount(k) <= 4]
+        for k in dead:
+            del _INTERN[k]
+        n = len(dead)
+        del dead
+        if not n:
+            break
+    _limit = max(PRUNE_MIN, 2 * len(_INTERN))
 
 
 def _convert(v: Any):
@@ -29,7 +50,10 @@ def _convert(v: Any):
     230-247 builds nested tuples through the same constructor)."""
     if isinstance(v, (list, builtins_tuple)):
         t = builtins_tuple(_convert(x) for x in v)
-        return _INTERN.setdefault(t, t)
+        r = _INTERN.setdefault(t, t)
+        if r is t and len(_INTERN) > _limit:
+            _prune()
+        return r
     return v
 
 
@@ -83,15 +107,9 @@ class _TupleFactory:
 
     @staticmethod
     def stats():
-        """(live tuples, used buckets, load factor) — tuple.lua:332-343.
-
-        Entries referenced only by the intern table are released first (the
-        Python analogue of the reference's weak-valued buckets).
-        """
-        for k in list(_INTERN):
-            if sys.getrefcount(k) <= _FREE_REFS:
-                del _INTERN[k]
-            del k
+        """(live tuples, used buckets, load factor) — tuple.lua:332-343
+        (unreferenced entries are released first)."""
+        _prune()
         n = len(_INTERN)
         buckets = len({compute_hash(k) % NUM_BUCKETS for k in _INTERN}) if n else 1
         return n, buckets, n / NUM_BUCKETS
@@ -102,7 +120,6 @@ class _TupleFactory:
 
 
 tuple = _TupleFactory()  # noqa: A001
-_FREE_REFS = 5  # dict key + dict value + list + loop variable + call argument
 
 
 def utest() -> None:

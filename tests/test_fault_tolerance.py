@@ -139,3 +139,33 @@ def test_iterative_loop_with_persistent_table(cs):
     conf = mr.persistent_table("iter_state", cs, "ft_iter")
     assert conf.iterations == 3
     assert conf.totals == [10, 20, 30]
+
+
+def test_journal_cut_mid_record_is_truncated_before_appending(tmp_path):
+    """A crash that leaves a partial record at the end of the journal: the
+    replay stops at the last intact record and the file is cut there, so the
+    records appended afterwards replay correctly on the next start (ADVICE r1:
+    appending behind a stale length prefix misparsed every later record)."""
+    journal = str(tmp_path / "coord.journal")
+    c1 = coordinator.Client(coordinator.start_local(journal=journal))
+    c1.request("BLOB_PUT", "jdb", "a", b"first")
+    good = os.path.getsize(journal)
+    with open(journal, "ab") as f:  # torn write: header + half of a body
+        f.write((200).to_bytes(4, "little") + (0).to_bytes(4, "little") + b"\x32\x00partial")
+    c2 = coordinator.Client(coordinator.start_local(journal=journal))
+    assert os.path.getsize(journal) == good
+    assert c2.request("BLOB_GET", "jdb", "a")[1] == [b"first"]
+    c2.request("BLOB_PUT", "jdb", "b", b"second")
+    c3 = coordinator.Client(coordinator.start_local(journal=journal))
+    assert c3.request("BLOB_GET", "jdb", "a")[1] == [b"first"]
+    assert c3.request("BLOB_GET", "jdb", "b")[1] == [b"second"]
+    # a record whose checksum does not match ends the replay too
+    with open(journal, "r+b") as f:
+        f.seek(good + 8)
+        b = f.read(1)
+        f.seek(good + 8)
+        f.write(bytes([b[0] ^ 0xFF]))
+    c4 = coordinator.Client(coordinator.start_local(journal=journal))
+    assert c4.request("BLOB_GET", "jdb", "a")[1] == [b"first"]
+    assert c4.request("BLOB_GET", "jdb", "b")[0] == 1  # not found
+    assert os.path.getsize(journal) == good
