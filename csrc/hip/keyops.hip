@@ -1,19 +1,18 @@
-// wordcount.hip — fused map-side kernels of the MapReduce hot path on gfx950.
+// keyops.hip — generic key kernels of the MapReduce data plane on gfx950.
 //
 // What this replaces in the reference (/root/reference):
-//   K1 line reading      examples/WordCount/mapfn.lua:4, utils.lua:133-200
-//   K2 tokenizer         examples/WordCount/mapfn.lua:5-7  (line:gmatch("[^%s]+"))
-//   K3 key hashing       tuple.lua:121-140
-//   K4 map-side group-by job.lua:83-97 (result[key][N+1] = value)
-//   K5 combiner          job.lua:92-96, 198-202
-// One launch tokenizes a byte stream, builds exact 128-bit keys, combines them
-// in an LDS hash table per workgroup (the combiner, with no 5000-value
-// threshold) and folds the per-workgroup partials into an HBM hash table.
+//   K2 tokenizer         examples/WordCount/mapfn.lua:5-7  (line:gmatch("[^%s]+")):
+//                        per-token (key, rep) emit for map functions that need
+//                        every occurrence (no combining), and an exact count
+//   K4 map-side group-by job.lua:83-97 (result[key][N+1] = value): the generic
+//                        (key, value) insert into the HBM hash table (hashtab.h)
+//   K8/K11               table compaction, key lengths + exact FNV-1 partition
+//                        (examples/WordCount/partitionfn.lua), key-byte gather
+// The fused word-count map (tokenize + LDS combine + flush) is wordcount3.hip.
 //
-// Geometry: 256 threads (4 wave64) per workgroup; each thread owns 16 bytes of
-// a 4 KiB tile (one global_load_dwordx4 per lane, fully coalesced); a
-// workgroup walks `chunk_bytes` of contiguous input tile by tile, so the LDS
-// table amortises the global atomics over ~10^4 tokens.
+// Geometry of the token walkers: 256 threads (4 wave64) per workgroup; each
+// thread owns 16 bytes of a 4 KiB tile (one global_load_dwordx4 per lane,
+// fully coalesced); a workgroup walks `chunk_bytes` of input tile by tile.
 #include <hip/hip_runtime.h>
 #include "mr_common.h"
 #include "hashtab.h"
@@ -25,9 +24,6 @@ constexpr int WC_SEG = 16;                      // bytes per thread per tile
 constexpr int WC_TILE = WC_THREADS * WC_SEG;    // 4096 bytes
 constexpr int WC_PAD = 16;                      // front pad; txt[PAD-1] = byte before tile
 constexpr int WC_HALO = 64;                     // bytes of the next tile staged in LDS
-constexpr int WC_LDS_SLOTS = 2048;
-constexpr int WC_LDS_CLAIM_LIMIT = (WC_LDS_SLOTS * 3) / 4;
-constexpr int WC_LDS_PROBES = 24;
 
 struct TxtView {
   const u8* text;
@@ -134,92 +130,6 @@ __device__ __forceinline__ void for_each_token(const TxtView& v, u64 tile_base, 
     }
     fn(hi, lo, gpos, len);
   }
-}
-
-// ---------------------------------------------------------------------------
-// LDS combine table (per workgroup).
-struct LdsTab {
-  u32 tag[WC_LDS_SLOTS];
-  u64 hi[WC_LDS_SLOTS];
-  u64 lo[WC_LDS_SLOTS];
-  u64 rep[WC_LDS_SLOTS];
-  u32 cnt[WC_LDS_SLOTS];
-  u32 nclaimed;
-};
-
-__device__ __forceinline__ bool lds_insert(LdsTab& L, u64 hi, u64 lo, u64 rep) {
-  const u64 tag64 = key_tag(hi, lo);
-  const u32 tag = (u32)(tag64 >> 32) | 1u;
-  u32 slot = (u32)tag64 & (WC_LDS_SLOTS - 1);
-  int probes = 0;
-  while (probes < WC_LDS_PROBES) {
-    u32 cur = __hip_atomic_load(&L.tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (cur == 0) {
-      if (__hip_atomic_load(&L.nclaimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (u32)WC_LDS_CLAIM_LIMIT)
-        return false;
-      u32 expected = 0;
-      if (__hip_atomic_compare_exchange_strong(&L.tag[slot], &expected, tag, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP)) {
-        L.hi[slot] = hi;
-        L.rep[slot] = rep;
-        __hip_atomic_fetch_add(&L.cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(&L.nclaimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_store(&L.lo[slot], lo, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return true;
-      }
-      cur = expected;
-    }
-    if (cur == tag) {
-      const u64 l = __hip_atomic_load(&L.lo[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (l == 0) continue;  // claimer has not published yet
-      if (l == lo && L.hi[slot] == hi) {
-        __hip_atomic_fetch_add(&L.cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return true;
-      }
-    }
-    slot = (slot + 1) & (WC_LDS_SLOTS - 1);
-    ++probes;
-  }
-  return false;
-}
-
-// Word-count map + combine.  rep_base is added to the in-buffer offset of
-// each key's first occurrence (so several H2D chunks can share one table).
-__global__ void __launch_bounds__(WC_THREADS) wc_map_kernel(TxtView v, u64 chunk_bytes, u64 rep_base, GTab g,
-                                                            int aligned) {
-  __shared__ __attribute__((aligned(16))) u8 txt[WC_PAD + WC_TILE + WC_HALO];
-  __shared__ LdsTab L;
-  const int t = threadIdx.x;
-  const u64 chunk_begin = (u64)blockIdx.x * chunk_bytes;
-  if (chunk_begin >= v.nbytes) return;
-  const u64 chunk_end = min(chunk_begin + chunk_bytes, v.nbytes);
-  u32 claims = 0;
-  for (int s = t; s < WC_LDS_SLOTS; s += WC_THREADS) {
-    L.tag[s] = 0;
-    L.lo[s] = 0;
-    L.cnt[s] = 0;
-  }
-  if (t == 0) {
-    L.nclaimed = 0;
-    txt[WC_PAD - 1] = chunk_begin > 0 ? v.text[chunk_begin - 1] : (u8)' ';
-  }
-  __syncthreads();
-  for (u64 tile_base = chunk_begin; tile_base < chunk_end; tile_base += WC_TILE) {
-    stage_tile(v, tile_base, txt, aligned != 0);
-    __syncthreads();
-    for_each_token(v, tile_base, txt, chunk_end, [&](u64 hi, u64 lo, u64 gpos, u64 len) {
-      const u64 rep = make_rep(rep_base + gpos, len);
-      if (!lds_insert(L, hi, lo, rep)) claims += gtab_insert(g, hi, lo, 1, rep, OP_SUM) == 2;
-    });
-    __syncthreads();
-    if (t == 0) txt[WC_PAD - 1] = txt[WC_PAD + WC_TILE - 1];
-    __syncthreads();
-  }
-  // flush the workgroup's partial counts (the combiner output) to HBM
-  for (int s = t; s < WC_LDS_SLOTS; s += WC_THREADS) {
-    if (L.tag[s] != 0) claims += gtab_insert(g, L.hi[s], L.lo[s], (long long)L.cnt[s], L.rep[s], OP_SUM) == 2;
-  }
-  gtab_count_claims(g, claims);
 }
 
 // Per-token emit (no combining): writes one (hi, lo, rep) triple per token,
@@ -426,18 +336,6 @@ static inline int grid_for(u64 n, int block, int maxg = 8192) {
 }
 
 extern "C" {
-
-int mr_wc_map(const void* text, u64 nbytes, u64 chunk_bytes, u64 rep_base, void* tag, void* hi, void* lo, void* val,
-              void* rep, void* ctrl, u64 cap, hipStream_t stream) {
-  if (nbytes == 0) return 0;
-  if (chunk_bytes % WC_TILE) return -1;
-  TxtView v{(const u8*)text, nbytes};
-  const u64 nblocks = (nbytes + chunk_bytes - 1) / chunk_bytes;
-  const int aligned = ((uintptr_t)text & 15) == 0;
-  hipLaunchKernelGGL(wc_map_kernel, dim3((unsigned)nblocks), dim3(WC_THREADS), 0, stream, v, chunk_bytes, rep_base,
-                     make_gtab(tag, hi, lo, val, rep, ctrl, cap), aligned);
-  return (int)hipGetLastError();
-}
 
 int mr_count_tokens(const void* text, u64 nbytes, u64 chunk_bytes, void* counter, hipStream_t stream) {
   if (nbytes == 0) return 0;

@@ -27,76 +27,6 @@ constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;  // 4096 keys per tile
 constexpr int RS_BINS = 256;
 constexpr int RS_WAVES = RS_THREADS / 64;
 
-__global__ void __launch_bounds__(RS_THREADS) rs_hist_kernel(const u64* keys, u64 n, int shift, u32* hist,
-                                                             u32 ntiles) {
-  __shared__ u32 h[RS_BINS];
-  const int t = threadIdx.x;
-  h[t] = 0;
-  __syncthreads();
-  const u64 base = (u64)blockIdx.x * RS_TILE;
-#pragma unroll 4
-  for (int r = 0; r < RS_ROUNDS; ++r) {
-    const u64 i = base + (u64)r * RS_THREADS + t;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1u);
-  }
-  __syncthreads();
-  hist[(u64)t * ntiles + blockIdx.x] = h[t];
-}
-
-template <typename V>
-__global__ void __launch_bounds__(RS_THREADS) rs_scatter_kernel(const u64* keys_in, const V* vals_in, u64* keys_out,
-                                                                V* vals_out, u64 n, int shift, const u32* offs,
-                                                                u32 ntiles) {
-  __shared__ u32 base_run[RS_BINS];
-  __shared__ u32 wcnt[RS_WAVES][RS_BINS];
-  const int t = threadIdx.x;
-  const int lane = t & 63;
-  const int wave = t >> 6;
-  base_run[t] = offs[(u64)t * ntiles + blockIdx.x];
-  const u64 tile = (u64)blockIdx.x * RS_TILE;
-  const unsigned long long below = (1ull << lane) - 1ull;
-  // preload the whole tile into registers: one memory latency instead of one
-  // per round (the rounds are separated by barriers the loads cannot cross)
-  u64 kr[RS_ROUNDS];
-  V vr[RS_ROUNDS];
-#pragma unroll
-  for (int r = 0; r < RS_ROUNDS; ++r) {
-    const u64 i = tile + (u64)r * RS_THREADS + t;
-    kr[r] = i < n ? keys_in[i] : 0;
-    vr[r] = (i < n && vals_in) ? vals_in[i] : V{};
-  }
-#pragma unroll
-  for (int r = 0; r < RS_ROUNDS; ++r) {
-    const u64 i = tile + (u64)r * RS_THREADS + t;
-    const bool valid = i < n;
-    const u64 k = kr[r];
-    const u32 d = (u32)((k >> shift) & 0xFF);
-#pragma unroll
-    for (int w = 0; w < RS_WAVES; ++w) wcnt[w][t] = 0;
-    __syncthreads();
-    unsigned long long peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const unsigned long long m = __ballot((d >> b) & 1u);
-      peers &= ((d >> b) & 1u) ? m : ~m;
-    }
-    const u32 rank = (u32)__popcll(peers & below);
-    if (valid && rank == 0) wcnt[wave][d] = (u32)__popcll(peers);
-    __syncthreads();
-    if (valid) {
-      u32 pos = base_run[d] + rank;
-      for (int w = 0; w < wave; ++w) pos += wcnt[w][d];
-      keys_out[pos] = k;
-      if (vals_in) vals_out[pos] = vr[r];
-    }
-    __syncthreads();
-    u32 tot = 0;
-#pragma unroll
-    for (int w = 0; w < RS_WAVES; ++w) tot += wcnt[w][t];
-    base_run[t] += tot;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Onesweep-style LSD pass: ONE launch per 8-bit digit.
 //   * rs_ghist8_kernel computes the global 256-bin histograms of all 8 digits of
@@ -107,7 +37,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_scatter_kernel(const u64* keys_
 //     {epoch:24 | flag:2 | count:38} (guide §6 G16 R2: the data is the flag),
 //     looks back over predecessors for its exclusive prefix, republishes the
 //     inclusive prefix, then scatters with the same stable wave64-ballot ranking
-//     as rs_scatter_kernel.  A digit shared by every key makes the pass a copy.
+//     as the LDS tile ranking.  A digit shared by every key makes the pass a copy.
 //   * every spin is bounded (s_sleep + give-up sets err[0]).
 constexpr u64 GR_AGG = 1ull, GR_INC = 2ull;
 
@@ -636,7 +566,6 @@ static int scan_impl(const T* in, T* out, u64 n, T* partials, T* total, hipStrea
 extern "C" {
 
 u64 mr_scan_partials_len(u64 n) { return (n + SC_TILE - 1) / SC_TILE + 1; }
-u64 mr_rs_tiles(u64 n) { return (n + RS_TILE - 1) / RS_TILE; }
 
 // exclusive scans; `total` (device, 1 element, may be null) receives the sum
 int mr_exclusive_scan_u32(const void* in, void* out, u64 n, void* partials, void* total, hipStream_t s) {
@@ -644,21 +573,6 @@ int mr_exclusive_scan_u32(const void* in, void* out, u64 n, void* partials, void
 }
 int mr_exclusive_scan_i64(const void* in, void* out, u64 n, void* partials, void* total, hipStream_t s) {
   return scan_impl<long long>((const long long*)in, (long long*)out, n, (long long*)partials, (long long*)total, s);
-}
-
-// One LSD radix pass on 8 bits at `shift` of u64 keys with optional u32
-// payload.  hist_ws must hold 256 * tiles u32; scan_ws mr_scan_partials_len(256*tiles).
-int mr_radix_pass_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
-                       void* hist_ws, void* scan_ws, hipStream_t s) {
-  if (n == 0) return 0;
-  const u32 nt = (u32)((n + RS_TILE - 1) / RS_TILE);
-  hipLaunchKernelGGL(rs_hist_kernel, dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in, n, shift, (u32*)hist_ws,
-                     nt);
-  int e = scan_impl<u32>((const u32*)hist_ws, (u32*)hist_ws, (u64)RS_BINS * nt, (u32*)scan_ws, nullptr, s);
-  if (e) return e;
-  hipLaunchKernelGGL(rs_scatter_kernel<u32>, dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
-                     (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)hist_ws, nt);
-  return (int)hipGetLastError();
 }
 
 // Global histograms of all 8 digits of a u64 word (ghist: 2048 u32, zeroed by caller).

@@ -31,8 +31,8 @@ def main(argv=None) -> int:
     ap.add_argument("--num-partitions", type=int, default=None)
     ap.add_argument("--result-ns", default=None)
     ap.add_argument("--split-glob", action="append", default=[],
-                    help="files loaded (sorted, in order of the options) into the pinned SplitStore that "
-                         "map modules with device_input='split' read; repeatable")
+                    help="split files (sorted, in order of the options) that map modules with "
+                         "device_input='split' read; each rank loads only its own share; repeatable")
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("taskfn")
     ap.add_argument("mapfn")
@@ -69,11 +69,9 @@ def main(argv=None) -> int:
         import glob
         from ..parallel.spmd import SplitStore
         files = [f for g in a.split_glob for f in sorted(glob.glob(g))]
-        splits = []
-        for f in files:
-            with open(f, "rb") as fh:
-                splits.append(fh.read())
-        store = SplitStore(splits, pin=device.type == "cuda")
+        # each rank reads (native loader, in parallel) and pins only the
+        # splits assigned to it; the engine's copies start as they land
+        store = SplitStore.from_files(files, rank, world, pin=device.type == "cuda")
     from .. import spmd
     eng = spmd(params, device=device, split_store=store, verbose=a.verbose or rank == 0)
     eng.run()

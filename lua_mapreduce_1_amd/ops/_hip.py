@@ -26,9 +26,7 @@ _u32 = ctypes.c_uint32
 _p = ctypes.c_void_p
 
 _SIGS = {
-    "mr_wc_map": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p],
     "mr_count_tokens": [_p, _u64, _u64, _p, _p],
-    "mr_wc_map2": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
     "mr_wc_map3": [_p, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
     "mr_insert_received": [_p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p, _u64, _i32, _i32, _p],
     "mr_memcpy_async": [_p, _p, _u64, _i32, _p],
@@ -44,7 +42,6 @@ _SIGS = {
     "mr_gather_key_bytes": [_p, _p, _p, _p, _u64, _p, _p, _p],
     "mr_exclusive_scan_u32": [_p, _p, _u64, _p, _p, _p],
     "mr_exclusive_scan_i64": [_p, _p, _u64, _p, _p, _p],
-    "mr_radix_pass_u32v": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p],
     "mr_gather_u64": [_p, _p, _p, _u64, _p],
     "mr_radix_ghist8": [_p, _u64, _p, _i32, _p],
     "mr_radix_onesweep_u32v": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p, _u32, _p, _i32, _p],
@@ -90,9 +87,8 @@ _SIGS = {
     "mr_tail_ws_layout": [_u64, _u32, _u64, ctypes.POINTER(ctypes.c_uint64)],
     "mr_table_reset": [_p, _p, _p, _p, _u64, ctypes.c_longlong, _p],
     "mr_scan_partials_len": [_u64],
-    "mr_rs_tiles": [_u64],
 }
-_RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_scan_partials_len", "mr_rs_tiles", "mr_tail_pack_bytes", "mr_tail_ws_layout"}
+_RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout"}
 
 
 def lib():

@@ -72,8 +72,6 @@ def _t64(a: np.ndarray, device="cpu") -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------
-_WC_CHUNK_MAX = TUNABLES.wc_chunk_max
-_WC_VERSION = TUNABLES.wc_version
 _OVF_COUNTERS = 64
 _OVF_ENTRIES = 1 << 18
 _CTRL_SHARD0, _CTRL_STRIDE, _CTRL_SHARDS = 32, 32, 64  # csrc/hip/hashtab.h
@@ -143,19 +141,17 @@ class HashTable:
                 r = r + np.uint64(rep_add << K.REP_LEN_BITS)
             self._pending.append((_u64(hi).copy(), _u64(lo).copy(), v, r))
 
-    def _overflow(self, nbytes: int, staged: bool = False):
-        """Overflow entries (hi, lo, rep, count) of the map kernels: tokens that
-        found their workgroup's LDS table full (v3: ~10 per launch on the
-        benchmark corpus; v2's staged mode: up to one per 8 input bytes).
-        Entries past the end are inserted into the HBM table directly, so the
-        capacity only matters for speed: a fixed size (no re-allocation when a
-        bigger launch comes along — a hipMalloc in the middle of an iteration
-        cost ~5 ms), larger only for v2's staged ablation mode."""
-        need = min(1 << 24, max(_OVF_ENTRIES, nbytes // 6)) if staged else _OVF_ENTRIES
+    def _overflow(self, nbytes: int):
+        """Overflow entries (hi, lo, rep) of the map kernel: tokens that found
+        their workgroup's LDS table full (~10 per launch on the benchmark
+        corpus).  Entries past the end are inserted into the HBM table
+        directly, so the capacity only matters for speed: a fixed size (no
+        re-allocation when a bigger launch comes along — a hipMalloc in the
+        middle of an iteration cost ~5 ms)."""
+        need = _OVF_ENTRIES
         if getattr(self, "_ovf", None) is None or self._ovf[0].numel() < need:
             d = self.device
             self._ovf = [torch.empty(need, dtype=torch.int64, device=d) for _ in range(3)]
-            self._ovf_cnt = torch.empty(need, dtype=torch.int32, device=d)
             # one overflow counter per map launch between two resets (no fill
             # kernel in front of every chunk's map launch)
             self._ovf_counters = torch.zeros(_OVF_COUNTERS, dtype=torch.int64, device=d)
@@ -167,41 +163,20 @@ class HashTable:
         self._ovf_next += 1
         return self._ovf, self._ovf_counter
 
-    def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, chunk_bytes: int | None = None,
-                      version: int | None = None, mode: int = 0, stamps: torch.Tensor | None = None) -> None:
-        """Fused tokenize + exact key + combine of every whitespace token (value 1).
-
-        ``chunk_bytes`` = bytes per workgroup; by default ~nbytes/1024 rounded to
-        the 8 KiB tile and clamped to [8, 32] KiB: a workgroup's latency (LDS
-        combine + flush of its distinct words) is ~130 us at 32 KiB and the
-        kernel runs one workgroup per CU, so small launches need small chunks
-        to spread over the 256 CUs."""
+    def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, mode: int = 0,
+                      stamps: torch.Tensor | None = None) -> None:
+        """Fused tokenize + exact key + combine of every whitespace token
+        (value 1): csrc/hip/wordcount3.hip.  ``mode`` = kernel config in the
+        low byte, ablation (timing only) in the high byte."""
         nbytes = text.numel()
         if nbytes == 0:
             return
-        if version is None:
-            # v3 (8 KiB chunks, two workgroups per CU) unless the caller pins a
-            # v2 chunk size; MR_WC_VERSION=2 restores v2 for ablations
-            version = 2 if chunk_bytes is not None else _WC_VERSION
-        if chunk_bytes is None:
-            chunk_bytes = min(_WC_CHUNK_MAX, max(8192, (nbytes // 1024 + 8191) // 8192 * 8192))
         if self.is_cuda:
             assert text.dtype == torch.uint8 and text.is_contiguous()
-            if version == 1:
-                _hip.call("mr_wc_map", _hip.ptr(text), nbytes, chunk_bytes, rep_base, *self._gtab(), self.cap,
-                          _hip.stream(self.device))
-                return
-            ovf, counter = self._overflow(nbytes, staged=(version == 2 and mode == 4))
-            if version == 3:
-                _hip.call("mr_wc_map3", _hip.ptr(text), nbytes, rep_base, *self._gtab(), self.cap,
-                          _hip.ptr(ovf[0]), _hip.ptr(ovf[1]), _hip.ptr(ovf[2]), ovf[0].numel(), _hip.ptr(counter),
-                          mode, _hip.ptr(stamps) if stamps is not None else None, _hip.stream(self.device))
-                return
-            counter.zero_()
-            chunk = min(65536, max(8192, (chunk_bytes + 8191) // 8192 * 8192))
-            _hip.call("mr_wc_map2", _hip.ptr(text), nbytes, chunk, rep_base, *self._gtab(),
-                      self.cap, _hip.ptr(ovf[0]), _hip.ptr(ovf[1]), _hip.ptr(ovf[2]), ovf[0].numel(),
-                      _hip.ptr(counter), mode, _hip.ptr(self._ovf_cnt), _hip.stream(self.device))
+            ovf, counter = self._overflow(nbytes)
+            _hip.call("mr_wc_map3", _hip.ptr(text), nbytes, rep_base, *self._gtab(), self.cap,
+                      _hip.ptr(ovf[0]), _hip.ptr(ovf[1]), _hip.ptr(ovf[2]), ovf[0].numel(), _hip.ptr(counter),
+                      mode, _hip.ptr(stamps) if stamps is not None else None, _hip.stream(self.device))
         else:
             buf = _np(text)
             starts, lens = K.token_spans(buf)
@@ -444,7 +419,7 @@ def _sort_ws(d, n: int):
     return ws
 
 
-def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: str = "onesweep",
+def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None,
               return_keys: bool = False, ghist: torch.Tensor | None = None, from_bit: int = 0,
               keys_only: bool = False):
     """Stable permutation sorting rows by unsigned multi-word keys.
@@ -457,9 +432,8 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
     (single word, GPU onesweep): only bits >= from_bit are sorted — rows equal
     in those bits keep their input order.  ``keys_only`` (single word, GPU
     onesweep): no permutation is carried (a third less traffic per pass);
-    returns ``(None, sorted keys)``.  GPU: LSD radix sort, one
-    onesweep launch per 8-bit digit (``method="onesweep"``) or the 3-phase
-    histogram/scan/scatter passes (``method="3phase"``).
+    returns ``(None, sorted keys)``.  GPU: LSD radix sort, one onesweep
+    launch per 8-bit digit (decoupled look-back, csrc/hip/sort.hip).
     """
     n = words[0].numel()
     bits = bits or [64] * len(words)
@@ -470,78 +444,57 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None, method: 
             return (z, words[0][:0]) if return_keys else z
         lib = _hip.lib()
         s = _hip.stream(d)
-        if method == "onesweep":
-            # no input copy and no iota launch: the first pass reads the
-            # caller's word and generates the identity permutation itself
-            ws = _sort_ws(d, n)
-            small = ws["small"]
-            small.zero_()  # [0:2048) ghist, [2048:2112) tile counters, [2112] error flag
-            if torch.cuda.is_current_stream_capturing():
-                # a replayed graph reuses its pass epochs: clear the look-back
-                # granules so a replay never sees the previous replay's tags
-                ws["granules"][: _onesweep_tiles(n) * 256].zero_()
-            ghist_ws = small[:2048]
-            pre_hist = ghist
-            kbuf = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(2)]
-            pbuf = ([None, None] if keys_only and len(words) == 1
-                    else [torch.empty(n, dtype=torch.int32, device=d) for _ in range(2)])
-            kin, pin = None, None
-            pass_id = 0
-            for j, (w, nb) in enumerate(zip(reversed(words), reversed(bits))):
-                if pin is None:
-                    kin = w.contiguous()
-                else:
-                    dst = kbuf[0] if kin is not kbuf[0] else kbuf[1]
-                    _hip.call("mr_gather_u64", _hip.ptr(w), _hip.ptr(pin), _hip.ptr(dst), n, s)
-                    kin = dst
-                if nb <= 0:
-                    continue
-                gh = ghist_ws
-                if pre_hist is not None and len(words) == 1:
-                    gh = pre_hist
-                else:
-                    if pass_id:
-                        ghist_ws.zero_()
-                    _hip.call("mr_radix_ghist8", _hip.ptr(kin), n, _hip.ptr(ghist_ws), (nb + 7) // 8, s)
-                ko = keys_only and len(words) == 1
-                for shift in range(from_bit if len(words) == 1 else 0, nb, 8):
-                    _EPOCH[0] = (_EPOCH[0] + 1) & 0xFFFFFF or 1
-                    kout = kbuf[0] if kin is not kbuf[0] else kbuf[1]
-                    pout = None if ko else (pbuf[0] if pin is not pbuf[0] else pbuf[1])
-                    _hip.call("mr_radix_onesweep_u32v", _hip.ptr(kin), _hip.ptr(pin), _hip.ptr(kout), _hip.ptr(pout),
-                              n, shift, _hip.ptr(gh[shift // 8 * 256:]), _hip.ptr(ws["granules"]),
-                              _hip.ptr(small[2048 + pass_id:]), _EPOCH[0], _hip.ptr(small[2112:]),
-                              1 if (pin is None and not ko) else 0, s)
-                    pass_id += 1
-                    kin, pin = kout, pout
-                if ko:
-                    return None, (kin if pass_id else words[0].clone())
+        # onesweep LSD passes (csrc/hip/sort.hip)
+        # no input copy and no iota launch: the first pass reads the
+        # caller's word and generates the identity permutation itself
+        ws = _sort_ws(d, n)
+        small = ws["small"]
+        small.zero_()  # [0:2048) ghist, [2048:2112) tile counters, [2112] error flag
+        if torch.cuda.is_current_stream_capturing():
+            # a replayed graph reuses its pass epochs: clear the look-back
+            # granules so a replay never sees the previous replay's tags
+            ws["granules"][: _onesweep_tiles(n) * 256].zero_()
+        ghist_ws = small[:2048]
+        pre_hist = ghist
+        kbuf = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(2)]
+        pbuf = ([None, None] if keys_only and len(words) == 1
+                else [torch.empty(n, dtype=torch.int32, device=d) for _ in range(2)])
+        kin, pin = None, None
+        pass_id = 0
+        for j, (w, nb) in enumerate(zip(reversed(words), reversed(bits))):
             if pin is None:
-                pin = torch.empty(n, dtype=torch.int32, device=d)
-                _hip.call("mr_iota_u32", _hip.ptr(pin), n, s)
-                kin = words[0].clone()
-            return (pin, kin) if return_keys else pin
-        perm = torch.empty(n, dtype=torch.int32, device=d)
-        _hip.call("mr_iota_u32", _hip.ptr(perm), n, s)
-        perm2 = torch.empty_like(perm)
-        k1 = torch.empty(n, dtype=torch.int64, device=d)
-        k2 = torch.empty_like(k1)
-        tiles = int(lib.mr_rs_tiles(n))
-        hist = torch.empty(256 * tiles, dtype=torch.int32, device=d)
-        scan_ws = torch.empty(int(lib.mr_scan_partials_len(256 * tiles)), dtype=torch.int32, device=d)
-        first = True
-        for w, nb in zip(reversed(words), reversed(bits)):
-            if first:
-                k1.copy_(w)
-                first = False
+                kin = w.contiguous()
             else:
-                _hip.call("mr_gather_u64", _hip.ptr(w), _hip.ptr(perm), _hip.ptr(k1), n, s)
-            for shift in range(0, nb, 8):
-                _hip.call("mr_radix_pass_u32v", _hip.ptr(k1), _hip.ptr(perm), _hip.ptr(k2), _hip.ptr(perm2), n,
-                          shift, _hip.ptr(hist), _hip.ptr(scan_ws), s)
-                k1, k2 = k2, k1
-                perm, perm2 = perm2, perm
-        return (perm, k1) if return_keys else perm
+                dst = kbuf[0] if kin is not kbuf[0] else kbuf[1]
+                _hip.call("mr_gather_u64", _hip.ptr(w), _hip.ptr(pin), _hip.ptr(dst), n, s)
+                kin = dst
+            if nb <= 0:
+                continue
+            gh = ghist_ws
+            if pre_hist is not None and len(words) == 1:
+                gh = pre_hist
+            else:
+                if pass_id:
+                    ghist_ws.zero_()
+                _hip.call("mr_radix_ghist8", _hip.ptr(kin), n, _hip.ptr(ghist_ws), (nb + 7) // 8, s)
+            ko = keys_only and len(words) == 1
+            for shift in range(from_bit if len(words) == 1 else 0, nb, 8):
+                _EPOCH[0] = (_EPOCH[0] + 1) & 0xFFFFFF or 1
+                kout = kbuf[0] if kin is not kbuf[0] else kbuf[1]
+                pout = None if ko else (pbuf[0] if pin is not pbuf[0] else pbuf[1])
+                _hip.call("mr_radix_onesweep_u32v", _hip.ptr(kin), _hip.ptr(pin), _hip.ptr(kout), _hip.ptr(pout),
+                          n, shift, _hip.ptr(gh[shift // 8 * 256:]), _hip.ptr(ws["granules"]),
+                          _hip.ptr(small[2048 + pass_id:]), _EPOCH[0], _hip.ptr(small[2112:]),
+                          1 if (pin is None and not ko) else 0, s)
+                pass_id += 1
+                kin, pin = kout, pout
+            if ko:
+                return None, (kin if pass_id else words[0].clone())
+        if pin is None:
+            pin = torch.empty(n, dtype=torch.int32, device=d)
+            _hip.call("mr_iota_u32", _hip.ptr(pin), n, s)
+            kin = words[0].clone()
+        return (pin, kin) if return_keys else pin
     cols = [_u64(w) for w in words]
     for j, nb in enumerate(bits):
         if nb < 64:

@@ -90,7 +90,9 @@ def init_from_env(backend: str | None = None, timeout_s: float | None = None, us
         torch.cuda.set_device(device)
         bind_to_gpu_numa(device)
     if world > 1 and not dist.is_initialized():
-        be = backend or ("nccl" if use_gpu else "gloo")
+        # more ranks than GPUs (a rehearsal on a 1-GPU box): RCCL refuses two
+        # ranks on one device, so such a job runs its collectives over gloo
+        be = backend or ("nccl" if use_gpu and world <= torch.cuda.device_count() else "gloo")
         kw = {}
         if be == "nccl" and use_gpu:
             kw["device_id"] = device
@@ -105,6 +107,10 @@ def init_from_env(backend: str | None = None, timeout_s: float | None = None, us
             kw["store"] = dist.PrefixStore("mr_attempt_%s" % attempt, store)
         dist.init_process_group(be, rank=rank, world_size=world, timeout=td, **kw)
     return rank, world, device
+
+
+def initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
 
 
 def world_info(group=None) -> tuple[int, int]:

@@ -60,21 +60,77 @@ class _nullctx:
 class SplitStore:
     """Host-resident input splits in ONE pinned buffer (the page-cache analogue
     of the reference's split files).  Every split is followed by a newline so
-    tokens never straddle two splits."""
+    tokens never straddle two splits.
+
+    ``offsets`` are global (every split's padded size is known to every rank,
+    for the byte-balanced job assignment); the buffer holds only the owned
+    splits ``own = (i0, i1)`` — a rank pins and reads just its share
+    (:meth:`from_files` / :meth:`from_blob` with ``rank, world``).  Those two
+    fill the buffer asynchronously with the native loader (ops/io.py);
+    :meth:`wait_ready` blocks until a range of splits has landed, so the
+    engine's host->HBM copies start while later splits are still being read."""
 
     def __init__(self, splits: list[bytes] | None = None, pin: bool = True):
         splits = splits or []
         sizes = [len(s) + (0 if (s and s[-1:] in (b"\n", b" ")) else 1) for s in splits]
-        self.offsets = np.zeros(len(splits) + 1, dtype=np.int64)
-        np.cumsum(sizes, out=self.offsets[1:])
-        total = int(self.offsets[-1])
-        self.buffer = torch.empty(total, dtype=torch.uint8, pin_memory=pin and torch.cuda.is_available())
+        self._layout(sizes, (0, len(splits)), pin)
         view = self.buffer.numpy()
         for i, s in enumerate(splits):
             a = int(self.offsets[i])
             view[a:a + len(s)] = np.frombuffer(s, dtype=np.uint8)
             if sizes[i] > len(s):
                 view[a + len(s)] = 10
+
+    def _layout(self, sizes, own, pin: bool) -> None:
+        self.offsets = np.zeros(len(sizes) + 1, dtype=np.int64)
+        np.cumsum(np.asarray(sizes, dtype=np.int64), out=self.offsets[1:])
+        self.own = (int(own[0]), int(own[1]))
+        self.base = int(self.offsets[self.own[0]])
+        nbytes = int(self.offsets[self.own[1]]) - self.base
+        self.buffer = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin and torch.cuda.is_available())
+        self._load = None
+        self.paths = None
+
+    @classmethod
+    def _async(cls, paths, file_off, lens, pad, own, pin: bool, threads: int) -> "SplitStore":
+        self = cls.__new__(cls)
+        sizes = np.asarray(lens, dtype=np.int64) + np.asarray(pad, dtype=np.int64)
+        self._layout(sizes, own, pin)
+        i0, i1 = self.own
+        if i1 > i0:
+            from ..ops import io as mio
+            dst_off = self.offsets[i0:i1] - self.base
+            self._load = mio.AsyncLoad([paths[i] for i in range(i0, i1)], np.asarray(file_off)[i0:i1],
+                                       np.asarray(lens)[i0:i1], dst_off, np.asarray(pad)[i0:i1], self.buffer,
+                                       threads=threads)
+        return self
+
+    @classmethod
+    def from_files(cls, paths: list[str], rank: int = 0, world: int = 1, pin: bool = True,
+                   threads: int = 8) -> "SplitStore":
+        """One split per file (the reference's split files, WordCountBig
+        taskfn.lua:6-10).  Sizes come from stat (+1 for the terminating
+        newline); only this rank's contiguous byte-balanced share is read."""
+        lens = [os.path.getsize(p) for p in paths]
+        pad = [1] * len(paths)
+        own = assign_contiguous([n + 1 for n in lens], rank, world)
+        self = cls._async(list(paths), [0] * len(paths), lens, pad, own, pin, threads)
+        self.paths = list(paths)
+        return self
+
+    @classmethod
+    def from_blob(cls, path: str, offsets, rank: int = 0, world: int = 1, pin: bool = True,
+                  threads: int = 8) -> "SplitStore":
+        """Splits stored back to back in one file, split i at bytes
+        ``[offsets[i], offsets[i+1])`` (the benchmark's corpus cache)."""
+        offsets = np.asarray(offsets, dtype=np.int64)
+        lens = offsets[1:] - offsets[:-1]
+        mm = np.memmap(path, dtype=np.uint8, mode="r") if offsets[-1] else None
+        last = [int(mm[o - 1]) if n else 0 for o, n in zip(offsets[1:], lens)] if mm is not None else []
+        del mm
+        pad = [0 if (n and b in (10, 32)) else 1 for n, b in zip(lens, last)]
+        own = assign_contiguous((lens + np.asarray(pad, dtype=np.int64)).tolist(), rank, world)
+        return cls._async([path] * len(lens), offsets[:-1], lens, pad, own, pin, threads)
 
     def __len__(self) -> int:
         return len(self.offsets) - 1
@@ -83,12 +139,32 @@ class SplitStore:
         return int(self.offsets[i + 1] - self.offsets[i])
 
     def region(self, i0: int, i1: int) -> tuple[int, int]:
-        return int(self.offsets[i0]), int(self.offsets[i1])
+        """Byte range of splits [i0, i1) in :attr:`buffer` (owned splits only)."""
+        if i0 < i1 and not (self.own[0] <= i0 and i1 <= self.own[1]):
+            raise ValueError(f"splits [{i0}, {i1}) are not held by this store (own {self.own})")
+        return int(self.offsets[i0]) - self.base, int(self.offsets[i1]) - self.base
+
+    def all_ready(self) -> bool:
+        return self._load is None or self._load.done() == self._load.n
+
+    def wait_ready(self, i0: int, i1: int) -> None:
+        """Block until splits [i0, i1) are in the buffer."""
+        if self._load is not None and i1 > i0:
+            self._load.wait_jobs(i0 - self.own[0], i1 - self.own[0])
+
+    def finish_loading(self) -> None:
+        if self._load is not None:
+            self._load.wait()
+            self._load = None
 
     def line_offsets(self) -> np.ndarray:
-        """Cumulative newline counts at split boundaries (global line ids)."""
+        """Cumulative newline counts at split boundaries (global line ids;
+        needs every split in this store)."""
         lo = getattr(self, "_line_offsets", None)
         if lo is None:
+            self.finish_loading()
+            if self.own != (0, len(self)):
+                raise ValueError("line_offsets needs a store holding every split")
             view = self.buffer.numpy()
             per = [int(np.count_nonzero(view[self.offsets[i]:self.offsets[i + 1]] == 10)) for i in range(len(self))]
             lo = np.zeros(len(self) + 1, dtype=np.int64)
@@ -197,6 +273,13 @@ class SPMDEngine:
         self.resident = False
         self._arena_holds: dict = {}  # arena slot -> plan key of the splits it holds
         self.prefetch = False
+        # build and prime the copy plans of every arena on first use (absorbs
+        # one-time runtime set-up before timed iterations); off for a cold,
+        # single-iteration run, where it would only add copies
+        self.prime_plans = True
+        self.force_shuffle = bool(self.params.get("force_shuffle", TUNABLES.force_shuffle))
+        if self.force_shuffle and self.world == 1 and not D.initialized():
+            raise RuntimeError("force_shuffle at world size 1 needs an initialised process group")
         # iteration pipelining (needs prefetch): the next iteration's map is
         # queued on the other slot's stream as soon as this map has finished,
         # and runs while this iteration shuffles, reduces and downloads
@@ -344,12 +427,12 @@ class SPMDEngine:
             views.append(arena[ca - a:cb - a])
             host_views.append(host[ca:cb])
             events.append(torch.cuda.Event() if self.copy_stream is not None else None)
-        return bounds, views, host_views, events
+        return bounds, views, host_views, events, ids[0]
 
     def _get_plan(self, ids: list[int], slot: int, single: bool = False):
         key = (ids[0], len(ids), slot, single)
         plan = self._plans.get(key)
-        if plan is None and self.copy_stream is not None and self._can_pipeline() and not getattr(
+        if plan is None and self.copy_stream is not None and self._can_pipeline() and self.prime_plans and not getattr(
                 self, "_priming", False):
             # a pure taskfn maps the same splits every iteration: build (and
             # prime) both copy plans of every arena now, so that no plan is
@@ -365,7 +448,7 @@ class SPMDEngine:
         if plan is None:
             plan = self._plan_chunks(ids, slot, single)
             self._plans[key] = plan
-            if self.copy_stream is not None:
+            if self.copy_stream is not None and self.prime_plans:
                 # the first two rounds of a plan's copies behind a cross-stream
                 # wait each stalled the host 5-7 ms inside hipMemcpyAsync (a
                 # one-time runtime set-up, tools/first_iter.py): take that hit
@@ -376,23 +459,30 @@ class SPMDEngine:
         return plan
 
     def _issue_copies(self, plan, wait_for=None) -> None:
-        bounds, views, host_views, events = plan
+        bounds, views, host_views, events, id0 = plan
+        streaming = not self.splits.all_ready()
         cs = self.copy_stream
         if wait_for is not None:
             # the arena may still be read by earlier work (a reused event: a
             # fresh one per iteration grows the runtime's event/signal pool)
-            ev0 = getattr(self, "_copy_gate", None)
-            if ev0 is None:
-                ev0 = self._copy_gate = torch.cuda.Event()
+            ev0 = self._copy_gate_event()
             ev0.record(wait_for)
             cs.wait_event(ev0)
         from ..ops import _hip
         sp = _hip.stream_ptr(cs)
-        for dst, src, ev in zip(views, host_views, events):
+        for i, (dst, src, ev) in enumerate(zip(views, host_views, events)):
+            if streaming:  # the native loader is still reading: copy each chunk once it has landed
+                self.splits.wait_ready(id0 + bounds[i], id0 + bounds[i + 1])
             # direct hipMemcpyAsync (pinned -> HBM) instead of copy_: no
             # host-allocator event bookkeeping per chunk (it stalled the host)
             _hip.call("mr_memcpy_async", _hip.ptr(dst), _hip.ptr(src), dst.numel(), 1, sp)
             ev.record(cs)
+
+    def _copy_gate_event(self):
+        ev0 = getattr(self, "_copy_gate", None)
+        if ev0 is None:
+            ev0 = self._copy_gate = torch.cuda.Event()
+        return ev0
 
     def _split_ids(self, jobs, j0, j1):
         ids = [int(v["split"] if isinstance(v, dict) else v) for _, v in jobs[j0:j1]]
@@ -435,7 +525,26 @@ class SPMDEngine:
                 yield (j0, j0 + len(ids)), self.arena[:b - a]
                 return
             plan = self._get_plan(ids, self.slot, single=prefetched and _PREFETCH_SINGLE)
-            bounds, views, host_views, events = plan
+            bounds, views, host_views, events, _ = plan
+            if cs is not None and not prefetched and not self.splits.all_ready():
+                # input still being read from files (cold start): each chunk is
+                # copied as soon as its splits have landed and mapped right
+                # behind its copy, so file reads, PCIe and the map overlap
+                cur = torch.cuda.current_stream(self.device)
+                with trace.range("mr.copies"):
+                    gate = self._copy_gate_event()
+                    gate.record(cur)
+                    cs.wait_event(gate)
+                from ..ops import _hip
+                sp = _hip.stream_ptr(cs)
+                for i in range(len(views)):
+                    self.splits.wait_ready(ids[0] + bounds[i], ids[0] + bounds[i + 1])
+                    _hip.call("mr_memcpy_async", _hip.ptr(views[i]), _hip.ptr(host_views[i]), views[i].numel(), 1, sp)
+                    events[i].record(cs)
+                    cur.wait_event(events[i])
+                    yield (j0 + bounds[i], j0 + bounds[i + 1]), views[i]
+                self._arena_holds[self.slot] = key
+                return
             if cs is not None:
                 cur = torch.cuda.current_stream(self.device)
                 if not prefetched:
@@ -459,6 +568,7 @@ class SPMDEngine:
                     yield (j0 + bounds[i], j0 + bounds[i + 1]), views[i]
             else:
                 for i, (dst, src) in enumerate(zip(views, host_views)):
+                    self.splits.wait_ready(ids[0] + bounds[i], ids[0] + bounds[i + 1])
                     dst.copy_(src)
                     yield (j0 + bounds[i], j0 + bounds[i + 1]), dst
         elif self.device_input == "file":
@@ -771,14 +881,18 @@ class SPMDEngine:
         self._failed_total = failed
         pend = None
         fused = self._fused_tail_ok()
-        if self.world == 1 and self._graph_tail_ok():
+        # the shuffle runs at W > 1, or at W = 1 with MR_FORCE_SHUFFLE (the
+        # RCCL data path exercised on a single GPU: pack -> count exchange ->
+        # all_to_all_single -> receive-side insert)
+        sh = self.world > 1 or self.force_shuffle
+        if not sh and self._graph_tail_ok():
             # the whole device tail (compact -> partition -> sort -> key bytes
             # -> downloads) is one replayed hipGraph once a table size repeats
             pend = self._graphed_tail(n_claimed, overflow, src)
-        elif self.world == 1 and fused:
+        elif not sh and fused:
             pend = self._finalize_table(self.table, n_claimed, src)
             issue_next_map()
-        elif self.world > 1 and fused:
+        elif sh and fused:
             # compact + FNV partition in one kernel (the send side of the shuffle)
             if overflow:
                 raise OverflowError("hash table overflow")
@@ -787,7 +901,7 @@ class SPMDEngine:
         else:
             hi, lo, val, rep = self.table.compact((n_claimed, overflow))
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
-        if self.world > 1:
+        if sh:
             trace.push("mr.shuffle_reduce")
             if fused:
                 src, rcounts, rows = self._shuffle(hi, lo, val, rep, src, part, failed, raw=True,

@@ -40,8 +40,6 @@ class Tunables:
     spmd_fault: str = _knob("MR_SPMD_FAULT", "",
                             "SPMD fault injection 'iteration:rank:raise|exit[:attempt]' at the start of that iteration")
     # -- device data plane
-    wc_version: int = _knob("MR_WC_VERSION", 3, "word-count map kernel generation (3 = wordcount3.hip)")
-    wc_chunk_max: int = _knob("MR_WC_CHUNK_MAX", 16 * 1024, "v2 map: max bytes per workgroup")
     fused_tail: bool = _knob("MR_FUSED_TAIL", True, "fused reduce-side tail kernels (tail.hip)")
     native_tail: bool = _knob("MR_NATIVE_TAIL", True, "queue the whole tail from one native call (mr_tail_run)")
     graphs: bool = _knob("MR_GRAPHS", False, "replay the W=1 tail as a hipGraph (stalls the copy stream: off)")
@@ -50,6 +48,9 @@ class Tunables:
     prefetch_late: bool = _knob("MR_PREFETCH_LATE", False, "issue prefetches after the tail instead of first")
     d2h: str = _knob("MR_D2H", "kernel", "downloads: 'kernel' (shader stores) or 'sdma' (queued behind H2D)")
     spin_us: float = _knob("MR_SPIN_US", 2000.0, "host spin on completion words before hipStreamSynchronize, us")
+    force_shuffle: bool = _knob("MR_FORCE_SHUFFLE", False,
+                                "SPMD: run the W>1 shuffle (pack, count exchange, all-to-all, receive insert) also "
+                                "at world size 1 (needs an initialised process group; tests RCCL on one GPU)")
     numa_bind: bool = _knob("MR_NUMA_BIND", True, "pin each rank to the CPUs of its GPU's NUMA node")
     # -- diagnostics
     debug_checks: bool = _knob("MR_DEBUG_CHECKS", False, "extra host-side consistency checks (slow)")

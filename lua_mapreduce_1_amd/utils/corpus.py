@@ -53,8 +53,10 @@ def zipf_probs(size: int, s: float = 1.05, q: float = 2.7) -> np.ndarray:
 
 
 def europarl_like(seed: int = 1234, lines: int = EUROPARL_LINES, words: int = EUROPARL_WORDS,
-                  split_lines: int = EUROPARL_SPLIT_LINES, vocab_size: int = 300_000) -> list[bytes]:
-    """List of split byte strings (each ends with a newline)."""
+                  split_lines: int = EUROPARL_SPLIT_LINES, vocab_size: int = 300_000, return_counts: bool = False):
+    """List of split byte strings (each ends with a newline); with
+    ``return_counts`` also the vocabulary and every word's exact number of
+    occurrences (the per-key ground truth of a word count)."""
     rng = np.random.default_rng(seed)
     vocab = make_vocab(vocab_size, rng)
     vlen = np.array([len(w) for w in vocab], dtype=np.int64)
@@ -76,11 +78,14 @@ def europarl_like(seed: int = 1234, lines: int = EUROPARL_LINES, words: int = EU
             np.add.at(wpl, idx[ok], -1)
         diff = int(words - wpl.sum())
     splits = []
+    counts = np.zeros(vocab_size, dtype=np.int64)
     for s0 in range(0, lines, split_lines):
         lw = wpl[s0:s0 + split_lines]
         nt = int(lw.sum())
         tok = np.searchsorted(cdf, rng.random(nt), side="right")
         tok = np.minimum(tok, vocab_size - 1)
+        if return_counts:
+            counts += np.bincount(tok, minlength=vocab_size)
         tl = vlen[tok]
         # separator after each token: space, or newline at end of line
         sep = np.full(nt, ord(" "), dtype=np.uint8)
@@ -95,6 +100,8 @@ def europarl_like(seed: int = 1234, lines: int = EUROPARL_LINES, words: int = EU
         buf[isw] = vbytes[voff[tok[ti[isw]]] + ci[isw]]
         buf[~isw] = sep
         splits.append(buf.tobytes())
+    if return_counts:
+        return splits, vocab, counts
     return splits
 
 

@@ -35,3 +35,16 @@ def test_bench_json_contract_cpu(n):
     assert out["config"]["valid"] is True and out["config"]["words"] == 60000
     assert out["value"] > 0 and out["higher_is_better"] is True
     assert "REDUCED" in out["data"]
+    assert out["world"] == n and out["backend"] in ("gloo", "single-process-cpu")
+    assert out["config"]["per_key_valid"] is True
+    assert out["cold_first_iteration_ms"] > 0
+
+
+def test_bench_spawns_its_own_ranks_cpu():
+    """``python bench.py --gpus 2`` with no torchrun environment starts the two
+    ranks itself and relays rank 0's single JSON line (the driver's N>1 form
+    must never silently measure one rank)."""
+    out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--lines", "4000",
+                "--words", "60000"])
+    assert out["n_gpus"] == 2 and out["world"] == 2 and out["backend"] == "gloo"
+    assert out["config"]["valid"] is True and out["config"]["per_key_valid"] is True

@@ -18,21 +18,32 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, on_gpu=False, pipelined=False):
+def _worker(rank, world, port, q, on_gpu=False, pipelined=False, backend="gloo", force_shuffle=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
+    import torch
     import torch.distributed as dist
     from lua_mapreduce_1_amd.parallel import dist as D
     from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore
     from lua_mapreduce_1_amd.runtime import codec
     from lua_mapreduce_1_amd.utils.corpus import europarl_like
 
-    _, _, device = D.init_from_env(backend="gloo", use_gpu=on_gpu)
+    if force_shuffle:
+        # a one-rank group: init_from_env skips it at W = 1
+        import datetime
+        dist.init_process_group(backend, rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}",
+                                timeout=datetime.timedelta(seconds=120),
+                                **({"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}))
+        device = torch.device("cuda", 0) if on_gpu else torch.device("cpu")
+    else:
+        _, _, device = D.init_from_env(backend=backend, use_gpu=on_gpu)
     splits = europarl_like(seed=9, lines=12_000, words=200_000, vocab_size=8_000, split_lines=1000)
     store = SplitStore(splits, pin=on_gpu)
     eng = SPMDEngine(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
-                          init_args={"nsplits": len(splits), "num_reducers": 7}),
+                          init_args={"nsplits": len(splits), "num_reducers": 7}, force_shuffle=force_shuffle),
                      split_store=store, device=device)
+    if force_shuffle:
+        assert dist.get_backend() == backend
     if on_gpu:
         assert eng.table.is_cuda
     if pipelined:  # iteration i+1's copies and map overlap iteration i's shuffle/reduce
@@ -93,3 +104,32 @@ def test_spmd_multirank_on_one_gpu(world, pipelined):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     ok, sorted_names, n = q.get(timeout=5)
     assert ok and sorted_names and n > 1000
+
+
+def _run(world, **kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q), kwargs=kw) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    ok, sorted_names, n = q.get(timeout=5)
+    assert ok and sorted_names and n > 1000
+
+
+def test_spmd_forced_shuffle_one_rank_gloo():
+    """MR_FORCE_SHUFFLE / force_shuffle: the W>1 data path (pack, count
+    exchange, all-to-all, receive-side reduce) at world size 1."""
+    _run(1, force_shuffle=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_spmd_forced_shuffle_rccl_one_gpu(pipelined):
+    """The RCCL branch of the shuffle (dist._a2a -> all_to_all_single on the
+    nccl backend, device buffers) on the single GPU of the box: a one-rank
+    nccl group with the W>1 path forced, checked against the naive count."""
+    _run(1, on_gpu=True, backend="nccl", force_shuffle=True, pipelined=pipelined)

@@ -21,8 +21,8 @@ def timeit(fn, reps=5):
     return min(ts), sorted(ts)[len(ts)//2]
 cfgs = [int(x) for x in sys.argv[1:]] or [0, 1, 2, 3, 4, 5]
 for data, tag in ((dev, "full"), (sub, "1/8 ")):
-    runs = [("v2 16K", lambda: tab.wordcount_map(data, chunk_bytes=16384))]
-    runs += [(f"v3 cfg{c}", (lambda c=c: tab.wordcount_map(data, version=3, mode=c))) for c in cfgs]
+    runs = []
+    runs += [(f"v3 cfg{c}", (lambda c=c: tab.wordcount_map(data, mode=c))) for c in cfgs]
     for name, fn in runs:
         mn, md = timeit(fn)
         n, ovf = tab.stats(); cnt = int(tab._ovf_counter.item())
@@ -34,8 +34,8 @@ for data, tag in ((dev, "full"), (sub, "1/8 ")):
 for c in cfgs[:3]:
     ts = []
     for _ in range(5):
-        tab.reset(); tab.wordcount_map(sub, version=3, mode=c); torch.cuda.synchronize()
+        tab.reset(); tab.wordcount_map(sub, mode=c); torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(); tab.wordcount_map(sub, version=3, mode=c); e1.record(); torch.cuda.synchronize()
+        e0.record(); tab.wordcount_map(sub, mode=c); e1.record(); torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
     print(f"1/8 warm-table v3 cfg{c} min {min(ts):7.3f} ms", flush=True)

@@ -15,6 +15,6 @@ for data, tag in ((dev, "full"), (dev[: len(text) // 8], "1/8 ")):
         for _ in range(5):
             tab.reset(); torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(); tab.wordcount_map(data, version=3, mode=(mode << 8)); e1.record(); torch.cuda.synchronize()
+            e0.record(); tab.wordcount_map(data, mode=(mode << 8)); e1.record(); torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
         print(f"{tag} {name:9s} min {min(ts):7.3f} ms  {data.numel() / min(ts) / 1e6:7.1f} GB/s", flush=True)

@@ -18,7 +18,7 @@ for frac, name in ((1, "full"), (8, "1/8")):
     st = torch.zeros(4 * nwg, dtype=torch.int64, device="cuda")
     for _ in range(3):
         tab.reset()
-        tab.wordcount_map(data, version=3, mode=cfg, stamps=st)
+        tab.wordcount_map(data, mode=cfg, stamps=st)
     torch.cuda.synchronize()
     s = st.view(-1, 4).cpu().numpy()
     t0 = s[:, 0].min()
