@@ -13,7 +13,10 @@
 //            bytes the tag IS the key (mr_common.h) and a tag match is final
 //   publish: sc1 stores of hi, rep ; fold value ; s_waitcnt vmcnt(0) ; sc1 store lo
 //   lookup:  tag match -> load lo (relaxed); lo==0 => not yet published, retry;
-//            lo match -> load hi; on mismatch re-check after an acquire fence.
+//            lo match -> load hi; on mismatch re-check after an acquire fence;
+//            a long key (lo low byte 0xFF) must also match byte for byte
+//            through the rep words (exact identity, mr_common.h) — keys that
+//            collide on (prefix, hash) take separate slots.
 //   lo is never 0 for a valid key (mr_common.h), so lo doubles as "published".
 #pragma once
 #include <hip/hip_runtime.h>
@@ -30,7 +33,14 @@ struct GTab {
   u32* ctrl;      // [0] = claimed slots (host-side inserts), [1] = overflow flag,
                   // [CTRL_SHARD0 + CTRL_STRIDE * s] = claim-count shard s (s < CTRL_SHARDS)
   u64 mask;       // capacity - 1 (capacity is a power of two)
+  const u8* src;  // byte source every rep word of this table indexes (long-key
+                  // verification); null = identity on (prefix, 56-bit hash)
 };
+
+// Exact identity of a long key already matched on (tag, hi, lo): compare its
+// bytes with the slot's (rep published before lo; re-read after an acquire
+// fence on a mismatch, as hi below).
+__device__ __forceinline__ bool gtab_long_equal(const GTab& t, u64 slot, u64 rep);
 
 constexpr u32 GTAB_MAX_PROBES = 1u << 14;
 // Claim counts go to 64 shards, each on its own 128-byte line: same-address
@@ -101,7 +111,7 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           h = ld_agent(&t.hi[slot]);
         }
-        if (h == hi) {
+        if (h == hi && (!key_is_long(lo) || t.src == nullptr || gtab_long_equal(t, slot, rep))) {
           fold_value(&t.val[slot], v, op);
           if (out_slot) *out_slot = slot;
           return 1;
@@ -113,6 +123,14 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
   }
   __hip_atomic_fetch_or(&t.ctrl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return 0;
+}
+
+__device__ __forceinline__ bool gtab_long_equal(const GTab& t, u64 slot, u64 rep) {
+  u64 r = ld_agent(&t.rep[slot]);
+  if (rep_bytes_equal(t.src, r, rep)) return true;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  r = ld_agent(&t.rep[slot]);
+  return rep_bytes_equal(t.src, r, rep);
 }
 
 // Wave-reduce per-lane claim counts and add them to a claim-count shard (call

@@ -27,6 +27,8 @@
 #include "mr_common.h"
 #include "hashtab.h"
 
+MR_LONG_MASK_SYMBOL(invidx)
+
 namespace mr {
 namespace ii {
 
@@ -90,7 +92,7 @@ __device__ u64 long_lo_global(const u8* text, u64 p0, u64 len) {
     for (u64 j = 0; j < n; ++j) word |= (u64)text[p0 + w + j] << (8 * j);
     h = long_hash_step(h, word);
   }
-  return long_lo(h);
+  return long_lo(h, mr_long_mask);
 }
 
 // LDS probe/claim; returns the local slot or -1 (table full / probe budget).
@@ -517,6 +519,7 @@ int mr_ii_map(const void* text, u64 nbytes, u64 chunk, u64 rep_base, const void*
   g.rep = (u64*)rep;
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
+  g.src = nullptr;
   const u64 nb = (nbytes + chunk - 1) / chunk;
   hipLaunchKernelGGL(ii::ii_map_kernel, dim3((unsigned)nb), dim3(ii::T), 0, s, (const u8*)text, nbytes, chunk,
                      rep_base, (const u32*)chunk_line_base, g, doc_bits, (u64*)out, (unsigned long long*)out_counter,
@@ -613,6 +616,7 @@ extern "C" int mr_ii_insert_slots(void* tag, void* thi, void* tlo, void* val, vo
   g.rep = (u64*)trep;
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
+  g.src = nullptr;
   hipLaunchKernelGGL(ii::ii_insert_slots_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, g, (const u64*)hi,
                      (const u64*)lo, (const u64*)rep, n, (long long*)out_slot);
   return (int)hipGetLastError();

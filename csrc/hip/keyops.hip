@@ -17,6 +17,8 @@
 #include "mr_common.h"
 #include "hashtab.h"
 
+MR_LONG_MASK_SYMBOL(keyops)
+
 namespace mr {
 
 constexpr int WC_THREADS = 256;
@@ -43,7 +45,7 @@ __device__ u64 long_key_lo_global(const TxtView& v, u64 p0, u64 len) {
     for (u64 j = 0; j < n; ++j) word |= (u64)v.text[p0 + w + j] << (8 * j);
     h = long_hash_step(h, word);
   }
-  return long_lo(h);
+  return long_lo(h, mr_long_mask);
 }
 
 // Stage tile [tile_base, tile_base + TILE + HALO) into LDS (bytes past nbytes
@@ -281,16 +283,21 @@ __global__ void key_meta_kernel(const u64* hi, const u64* lo, const u64* rep, u6
 
 // Materialise key bytes: dst[off[i] .. off[i]+len) = bytes of key i.
 __global__ void gather_key_bytes_kernel(const u64* hi, const u64* lo, const u64* rep, const long long* off, u64 n,
-                                        const u8* src, u8* dst) {
+                                        const u8* src, u8* dst, u64 dst_cap) {
+  // writes stop at dst_cap: offsets built from rows of a flagged (given-up)
+  // sort may overrun the capacity bound, and must never write past it
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const u64 h = hi[i], l = lo[i];
-    u8* d = dst + off[i];
+    const u64 o = (u64)off[i];
+    if (o >= dst_cap) continue;
+    u8* d = dst + o;
+    const u64 room = dst_cap - o;
     if (!key_is_long(l)) {
       const u32 len = packed_len(l);
-      for (u32 k = 0; k < len; ++k) d[k] = (u8)packed_byte(h, l, k);
+      for (u32 k = 0; k < len && k < room; ++k) d[k] = (u8)packed_byte(h, l, k);
     } else {
-      const u64 len = rep_len(rep[i]);
+      const u64 len = rep_len(rep[i]) < room ? rep_len(rep[i]) : room;
       const u8* p = src + rep_off(rep[i]);
       for (u64 k = 0; k < len; ++k) d[k] = p[k];
     }
@@ -316,7 +323,8 @@ __global__ void table_reset_kernel(u64* tag, u64* lo, long long* val, u32* ctrl,
 // allocation or synchronisation inside, so every launch is graph-capturable).
 using namespace mr;
 
-static inline GTab make_gtab(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap) {
+static inline GTab make_gtab(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap,
+                             const void* src = nullptr) {
   GTab g;
   g.tag = (u64*)tag;
   g.hi = (u64*)hi;
@@ -325,6 +333,7 @@ static inline GTab make_gtab(void* tag, void* hi, void* lo, void* val, void* rep
   g.rep = (u64*)rep;
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
+  g.src = (const u8*)src;
   return g;
 }
 
@@ -360,12 +369,15 @@ int mr_tokenize(const void* text, u64 nbytes, u64 chunk_bytes, u64 rep_base, voi
   return (int)hipGetLastError();
 }
 
+// src (may be null): the byte source the table's rep words index (after
+// rep_add), for the exact identity of long keys (hashtab.h)
 int mr_hash_agg(const void* hi, const void* lo, const void* val, const void* rep, u64 n, u64 rep_add, int op, void* tag,
-                void* thi, void* tlo, void* tval, void* trep, void* ctrl, u64 cap, hipStream_t stream) {
+                void* thi, void* tlo, void* tval, void* trep, void* ctrl, u64 cap, const void* src,
+                hipStream_t stream) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(hash_agg_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)hi, (const u64*)lo,
-                     (const long long*)val, (const u64*)rep, n, make_gtab(tag, thi, tlo, tval, trep, ctrl, cap), op,
-                     rep_add);
+                     (const long long*)val, (const u64*)rep, n, make_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src),
+                     op, rep_add);
   return (int)hipGetLastError();
 }
 
@@ -393,10 +405,10 @@ int mr_key_meta(const void* hi, const void* lo, const void* rep, u64 n, const vo
 }
 
 int mr_gather_key_bytes(const void* hi, const void* lo, const void* rep, const void* off, u64 n, const void* src,
-                        void* dst, hipStream_t stream) {
+                        void* dst, u64 dst_cap, hipStream_t stream) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(gather_key_bytes_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)hi,
-                     (const u64*)lo, (const u64*)rep, (const long long*)off, n, (const u8*)src, (u8*)dst);
+                     (const u64*)lo, (const u64*)rep, (const long long*)off, n, (const u8*)src, (u8*)dst, dst_cap);
   return (int)hipGetLastError();
 }
 

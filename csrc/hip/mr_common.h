@@ -11,7 +11,9 @@
 //          (the order Lua's string `<` gives, utils.lua:126).
 //     * len >= 16  ("long", hashed):   hi = bytes[0..7] big-endian (exact prefix),
 //                                     lo = hash56(bytes) << 8 | 0xFF
-//       -> identity is (prefix, 56-bit hash); order is exact on the prefix.
+//       -> (prefix, 56-bit hash) selects the slot; identity is EXACT: a table
+//          insert that matches a long key on (hi, lo) compares the key bytes
+//          through the rep words (hashtab.h), so colliding keys stay apart.
 //   lo is never 0, so lo == 0 marks an unwritten table slot.
 //
 //   A "rep" word locates the key bytes of a long key inside a byte source:
@@ -74,7 +76,20 @@ MR_HD u64 gtab_home(u64 tag, u64 mask) { return fmix64(tag ^ 0x2545F4914F6CDD1Du
 // one zero padded).  Identical on host and device.
 MR_HD u64 long_hash_step(u64 h, u64 w) { return fmix64(h ^ w) * 0x9E3779B97F4A7C15ull; }
 MR_HD u64 long_hash_init(u64 len) { return 0x243F6A8885A308D3ull ^ (len * 0x13198A2E03707344ull); }
-MR_HD u64 long_lo(u64 h) { return (fmix64(h) << 8) | LONG_MARK; }
+// `mask` keeps the low bits of the 56-bit hash: all of them in production; a
+// debug knob (mr_set_long_mask_*, ops.set_long_hash_bits) truncates it so that
+// distinct long keys collide and the byte verification of the tables is tested.
+MR_HD u64 long_lo(u64 h, u64 mask) { return ((fmix64(h) & mask) << 8) | LONG_MARK; }
+
+#if defined(__HIPCC__)
+// Per translation unit (no -fgpu-rdc): the long-key hash mask read by its
+// kernels and the host setter of that copy.
+#define MR_LONG_MASK_SYMBOL(tu)                                                        \
+  static __constant__ u64 mr_long_mask = ~0ull;                                         \
+  extern "C" int mr_set_long_mask_##tu(u64 m) {                                         \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(mr_long_mask), &m, sizeof(m));              \
+  }
+#endif
 
 MR_HD bool key_is_long(u64 lo) { return (lo & 0xFFull) == LONG_MARK; }
 MR_HD u32 packed_len(u64 lo) { return (u32)(lo & 0xFFull); }
@@ -91,6 +106,23 @@ MR_HD u32 packed_byte(u64 hi, u64 lo, u32 i) {
 constexpr u32 FNV_PRIME = 16777619u;
 constexpr u32 FNV_OFFSET = 2166136261u;
 MR_HD u32 fnv1_step(u32 h, u32 b) { return (h * FNV_PRIME) ^ b; }
+
+// Two keys' bytes (rep words into one byte source) are equal.
+MR_HD bool rep_bytes_equal(const u8* src, u64 a, u64 b) {
+  const u64 n = a & REP_LEN_MASK;
+  if (n != (b & REP_LEN_MASK)) return false;
+  const u64 oa = a >> REP_LEN_BITS, ob = b >> REP_LEN_BITS;
+  if (oa == ob) return true;
+  for (u64 i = 0; i < n; ++i)
+    if (src[oa + i] != src[ob + i]) return false;
+  return true;
+}
+
+// Row index read from a sort permutation, clamped into [0, n): a radix pass
+// whose look-back gave up (flagged, the result is discarded and re-sorted)
+// may leave stale permutation entries, which must never become an
+// out-of-bounds read in the gathers that follow.
+MR_HD u64 clamp_row(u64 j, u64 n) { return j < n ? j : 0; }
 
 MR_HD u64 make_rep(u64 off, u64 len) { return (off << REP_LEN_BITS) | (len < REP_LEN_MASK ? len : REP_LEN_MASK); }
 MR_HD u64 rep_off(u64 rep) { return rep >> REP_LEN_BITS; }

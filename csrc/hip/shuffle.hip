@@ -240,8 +240,10 @@ int mr_pack_by_dest(const void* hi, const void* lo, const void* val, const void*
   return (int)hipGetLastError();
 }
 
+// src: the received key bytes the rep words index (combined layout: `rec`
+// itself; may be null = no long-key byte verification)
 int mr_insert_received(const void* rec, u64 n, const void* recv, u32 W, void* tag, void* hi, void* lo, void* val,
-                       void* rep, void* ctrl, u64 cap, int op, int combined, hipStream_t s) {
+                       void* rep, void* ctrl, u64 cap, int op, int combined, const void* src, hipStream_t s) {
   if (n == 0) return 0;
   if (W == 0 || W > (u32)pk::MAXW_RECV) return -1;
   GTab g;
@@ -252,6 +254,7 @@ int mr_insert_received(const void* rec, u64 n, const void* recv, u32 W, void* ta
   g.rep = (u64*)rep;
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
+  g.src = (const u8*)(combined ? rec : src);
   hipLaunchKernelGGL(pk::pk_insert_received_kernel, dim3(pk_grid(n, 2048)), dim3(256), 0, s, (const u8*)rec, n,
                      (const long long*)recv, W, g, op, combined);
   return (int)hipGetLastError();

@@ -94,7 +94,7 @@ template <typename V, int ROUNDS>
 __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys_in, const V* vals_in, u64* keys_out,
                                                                  V* vals_out, u64 n, int shift, const u32* ghist,
                                                                  u64* granules, u32* tile_counter, u32 epoch,
-                                                                 u32* err, int iota) {
+                                                                 u32* err, int iota, int debug_fail) {
   constexpr int RS_TILE = RS_THREADS * ROUNDS;
   constexpr int RS_ROUNDS = ROUNDS;
   // iota: vals_in is absent and the value of key i is i (first pass of a
@@ -210,6 +210,10 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
   if (tile > 0) {
     long long j = (long long)tile - 1;
     u32 spins = 0;
+    if (debug_fail && tile == 1) {  // test knob (mr_sort_debug_fail): this tile gives up at once
+      atomicOr(err, 1u);
+      j = -1;
+    }
     while (j >= 0) {
       const u64 g = __hip_atomic_load(&granules[(u64)j * RS_BINS + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const u32 ep = (u32)(g >> 40);
@@ -321,7 +325,7 @@ __global__ void __launch_bounds__(SC_THREADS) scan_apply_kernel(const T* in, u64
 // ---------------------------------------------------------------------------
 __global__ void gather_u64_kernel(const u64* src, const u32* idx, u64* dst, u64 n) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[idx[i]];
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[clamp_row(idx[i], n)];
 }
 
 __global__ void iota_u32_kernel(u32* dst, u64 n) {
@@ -461,7 +465,7 @@ __global__ void gather_cols_kernel(const u32* __restrict__ perm, u64 n, const u6
                                    u64* o4, u32* q0) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const u64 j = perm[i];
+    const u64 j = clamp_row(perm[i], n);
     if (a0) o0[i] = a0[j];
     if (a1) o1[i] = a1[j];
     if (a2) o2[i] = a2[j];
@@ -587,6 +591,16 @@ int mr_radix_ghist8(const void* keys, u64 n, void* ghist, int ndigits, hipStream
 // granules: tiles*256 u64, never needs clearing — entries are epoch tagged;
 // tile_counter: one u32 zeroed before the pass; epoch unique per pass).
 // granules must hold 256 * mr_onesweep_tiles(n) u64
+static int g_onesweep_debug_fail = 0;
+
+// Test knob: the next `passes` onesweep passes (of sorts with at least two
+// tiles) give up the look-back of tile 1 — they set the error word and
+// scatter with a wrong prefix, as a real give-up would; callers must detect it.
+int mr_sort_debug_fail(int passes) {
+  g_onesweep_debug_fail = passes;
+  return 0;
+}
+
 u64 mr_onesweep_tiles(u64 n) {
   return n <= ONESWEEP_SMALL ? (n + RS_THREADS * 4 - 1) / (RS_THREADS * 4) : (n + RS_TILE - 1) / RS_TILE;
 }
@@ -594,16 +608,21 @@ u64 mr_onesweep_tiles(u64 n) {
 int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
                            const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
                            hipStream_t s) {
+  int debug_fail = 0;
+  if (g_onesweep_debug_fail > 0 && mr_onesweep_tiles(n) > 1) {
+    debug_fail = 1;
+    --g_onesweep_debug_fail;
+  }
   if (n == 0) return 0;
   const u32 nt = (u32)mr_onesweep_tiles(n);
   if (n <= ONESWEEP_SMALL) {
     hipLaunchKernelGGL((rs_onesweep_kernel<u32, 4>), dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
                        (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
-                       (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota);
+                       (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota, debug_fail);
   } else {
     hipLaunchKernelGGL((rs_onesweep_kernel<u32, RS_ROUNDS>), dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
                        (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
-                       (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota);
+                       (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota, debug_fail);
   }
   return (int)hipGetLastError();
 }

@@ -112,7 +112,7 @@ __global__ void tail_gather_kernel(const u32* __restrict__ perm, u64 n, const u6
                                    u32* __restrict__ o_part, long long* __restrict__ o_len) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const u64 j = perm[i];
+    const u64 j = clamp_row(perm[i], n);
     const u64 l = lo[j], r = rep[j];
     o_hi[i] = hi[j];
     o_lo[i] = l;
@@ -124,9 +124,12 @@ __global__ void tail_gather_kernel(const u32* __restrict__ perm, u64 n, const u6
 }
 
 // [val: n x i64][off: (n+1) x i32][counts: nparts x i64][bad: u32] (8-byte aligned sections)
+// bad: bit 0 = a tie run too long for the fixup, bit 1 = unchecked long-key
+// prefix tie, bit 2 = the sort's decoupled look-back gave up (`err`: the
+// order is wrong; the host re-sorts or raises)
 __global__ void tail_pack_kernel(const long long* __restrict__ val, const long long* __restrict__ off, u64 n,
                                  const long long* __restrict__ counts, u32 nparts, const u32* __restrict__ bad,
-                                 u8* __restrict__ out) {
+                                 const u32* __restrict__ err, u8* __restrict__ out) {
   long long* ov = (long long*)out;
   int* oo = (int*)(out + 8 * n);
   const u64 off_bytes = ((4 * (n + 1)) + 7) & ~7ull;
@@ -137,7 +140,7 @@ __global__ void tail_pack_kernel(const long long* __restrict__ val, const long l
     if (i < n) ov[i] = val[i];
     oo[i] = (int)off[i];
     if (i < nparts) oc[i] = counts[i];
-    if (i == 0) ob[0] = bad[0];
+    if (i == 0) ob[0] = bad[0] | ((err && err[0]) ? 4u : 0u);
   }
   if (blockIdx.x == 0 && threadIdx.x < nparts && n + 1 <= threadIdx.x) oc[threadIdx.x] = counts[threadIdx.x];
 }
@@ -163,6 +166,7 @@ int mr_tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* c
   g.rep = (u64*)rep;
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
+  g.src = nullptr;
   const u64 nb = (cap + tl::T * tl::ITEMS - 1) / (tl::T * tl::ITEMS);
   hipLaunchKernelGGL(tl::tail_compact_kernel, dim3((unsigned)nb), dim3(tl::T), 0, s, g, cap, nparts, (const u8*)src,
                      (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
@@ -182,13 +186,14 @@ int mr_tail_gather(const void* perm, u64 n, const void* hi, const void* lo, cons
   return (int)hipGetLastError();
 }
 
-int mr_tail_pack(const void* val, const void* off, u64 n, const void* counts, u32 nparts, const void* bad, void* out,
-                 hipStream_t s) {
+int mr_tail_pack(const void* val, const void* off, u64 n, const void* counts, u32 nparts, const void* bad,
+                 const void* err, void* out, hipStream_t s) {
   if (nparts > 256) return -1;
   u64 g = (n + 1 + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(tl::tail_pack_kernel, dim3((unsigned)g), dim3(256), 0, s, (const long long*)val,
-                     (const long long*)off, n, (const long long*)counts, nparts, (const u32*)bad, (u8*)out);
+                     (const long long*)off, n, (const long long*)counts, nparts, (const u32*)bad, (const u32*)err,
+                     (u8*)out);
   return (int)hipGetLastError();
 }
 
@@ -209,7 +214,7 @@ int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_
 int mr_tie_fixup(const void* c, void* hi, void* lo, void* val, void* rep, void* part, u64 n, void* bad,
                  const void* src, void* ln, hipStream_t s);
 int mr_gather_key_bytes(const void* hi, const void* lo, const void* rep, const void* off, u64 n, const void* src,
-                        void* dst, hipStream_t stream);
+                        void* dst, u64 dst_cap, hipStream_t stream);
 int mr_copy_to_host(const void* src, void* host_dst, const void* nelem, u64 elem_size, u64 max_bytes, hipStream_t s);
 int mr_d2h_async(void* host_dst, const void* src, u64 nbytes, hipStream_t s);
 
@@ -282,9 +287,9 @@ int mr_tail_run(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl,
     rc = (int)hipMemsetAsync(offs, 0, 8, s);
   }
   if (rc) return rc;
-  rc = mr_gather_key_bytes(P(TB_HI), P(TB_LO), P(TB_REP), offs, n, src, P(TB_BLOB), s);
+  rc = mr_gather_key_bytes(P(TB_HI), P(TB_LO), P(TB_REP), offs, n, src, P(TB_BLOB), blob_cap ? blob_cap : 1, s);
   if (rc) return rc;
-  rc = mr_tail_pack(P(TB_VAL), offs, n, z + TZ_PCOUNT, nparts, z + TZ_BAD, P(TB_PACKED), s);
+  rc = mr_tail_pack(P(TB_VAL), offs, n, z + TZ_PCOUNT, nparts, z + TZ_BAD, z + TZ_ERR, P(TB_PACKED), s);
   if (rc) return rc;
   rc = mr_d2h_async(hp, P(TB_PACKED), mr_tail_pack_bytes(n, nparts), s);
   if (rc) return rc;

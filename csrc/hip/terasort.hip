@@ -92,7 +92,7 @@ __global__ void ts_gather_kernel(const u32* __restrict__ in, const u32* __restri
   for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
     const u64 r = w / WORDS;
     const u32 j = (u32)(w - r * WORDS);
-    out[w] = __builtin_nontemporal_load(in + (u64)perm[r] * WORDS + j);
+    out[w] = __builtin_nontemporal_load(in + clamp_row(perm[r], n) * WORDS + j);
   }
 }
 
@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(256) ts_gather_unrolled_kernel(const u32* __re
     for (int k = 0; k < UNROLL; ++k) {
       const u64 w = w0 + (u64)k * stride;
       const u64 r = w / WORDS;
-      src[k] = w < nw ? perm[r] : 0u;
+      src[k] = w < nw ? (u32)clamp_row(perm[r], n) : 0u;
     }
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(256) ts_gather_rec_kernel(const u32* __restric
                                                             u64 n, u32* __restrict__ out) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
-    const u32* p = in + (u64)perm[r] * WORDS;
+    const u32* p = in + clamp_row(perm[r], n) * WORDS;
     u32 v[WORDS];
 #pragma unroll
     for (int j = 0; j < WORDS; ++j) v[j] = __builtin_nontemporal_load(p + j);
@@ -194,11 +194,11 @@ __global__ void ts_tie_fixup_kernel(u64* __restrict__ shi, u32* __restrict__ per
     }
     for (u64 a = i + 1; a < e; ++a) {
       const u32 p = perm[a];
-      const u64 kh = shi[a], kl = lo[p];
+      const u64 kh = shi[a], kl = lo[clamp_row(p, n)];
       u64 b = a;
       while (b > i) {
         const u64 ph = shi[b - 1];
-        if (ph < kh || (ph == kh && lo[perm[b - 1]] <= kl)) break;
+        if (ph < kh || (ph == kh && lo[clamp_row(perm[b - 1], n)] <= kl)) break;
         perm[b] = perm[b - 1];
         shi[b] = ph;
         --b;

@@ -22,6 +22,8 @@
 #include "mr_common.h"
 #include "hashtab.h"
 
+MR_LONG_MASK_SYMBOL(wc3)
+
 namespace mr {
 namespace v3 {
 
@@ -76,7 +78,7 @@ __device__ u64 long_lo_global(const u8* text, u64 p0, u64 len) {
     for (u64 j = 0; j < n; ++j) word |= (u64)text[p0 + w + j] << (8 * j);
     h = long_hash_step(h, word);
   }
-  return long_lo(h);
+  return long_lo(h, mr_long_mask);
 }
 
 // 16 bytes at gpos (bytes past nbytes read as spaces)
@@ -103,8 +105,11 @@ __device__ __forceinline__ uint4 load16(const u8* __restrict__ text, u64 gpos, u
 // words) the tag is the key itself (hi | len, gtab_tag in mr_common.h), so a
 // hit is ONE LDS read and a claim publishes the key in its CAS; other keys use
 // a hashed tag plus the published (hi, lo) check (lo released last).
+// A long key (>= 16 bytes) matched on (hi, lo) is compared byte for byte with
+// the slot's first occurrence (both inside this chunk, `kb` = its first byte):
+// colliding long keys take separate slots (exact identity, mr_common.h).
 template <int T, int SLOTS>
-__device__ __forceinline__ bool lds_insert(Lds<T, SLOTS>& L, u64 hi, u64 lo, u32 rep) {
+__device__ __forceinline__ bool lds_insert(Lds<T, SLOTS>& L, u64 hi, u64 lo, u32 rep, const u8* kb) {
   u64 h = hi ^ (lo * 0x9E3779B97F4A7C15ull);
   h ^= h >> 31;
   h *= 0xC2B2AE3D27D4EB4Full;
@@ -137,7 +142,9 @@ __device__ __forceinline__ bool lds_insert(Lds<T, SLOTS>& L, u64 hi, u64 lo, u32
       }
       const u64 l = __hip_atomic_load(&L.lo[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (l == 0) continue;  // claimer has not published yet: re-read this slot
-      if (l == lo && L.hi[slot] == hi) {
+      if (l == lo && L.hi[slot] == hi &&
+          (!key_is_long(lo) || rep_bytes_equal(kb, make_rep(L.rep[slot] & 0xFFFFu, L.rep[slot] >> 16),
+                                               make_rep(rep & 0xFFFFu, rep >> 16)))) {
         __hip_atomic_fetch_add(&L.cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return true;
       }
@@ -250,7 +257,8 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
           if ((hi ^ lo) == 0x123456789ull) ovf.counter[1] = hi;  // keep the key live
           continue;
         }
-        const bool ok = len < 65536 && lds_insert(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16));
+        const bool ok = len < 65536 && lds_insert(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16),
+                                                   text + chunk_begin);
         if (!ok) {
           const u64 grep = make_rep(rep_base + gpos, len);
           const unsigned long long idx = atomicAdd(ovf.counter, 1ull);
@@ -309,7 +317,8 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
   for (int k = 0; k < PER; ++k) {
     if (!kcnt[k]) {
       state |= 1u << k;
-    } else if (gt[k] == ktag[k] && gl[k] == klo[k] && gh[k] == khi[k]) {
+    } else if (gt[k] == ktag[k] && gl[k] == klo[k] && gh[k] == khi[k] && !key_is_long(klo[k])) {
+      // (a long key takes gtab_insert below: its bytes are verified there)
       fold_value(&g.val[kslot[k]], (long long)kcnt[k], OP_SUM);
       state |= 1u << k;
     }
@@ -406,6 +415,7 @@ int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, 
   g.rep = (u64*)rep;
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
+  g.src = (const u8*)text - rep_base;  // every rep word of this table indexes the caller's byte source
   v3::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter, (u64*)stamps};
   const int aligned = ((uintptr_t)text & 15) == 0;
   const u8* tx = (const u8*)text;

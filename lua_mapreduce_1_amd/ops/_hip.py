@@ -28,7 +28,7 @@ _p = ctypes.c_void_p
 _SIGS = {
     "mr_count_tokens": [_p, _u64, _u64, _p, _p],
     "mr_wc_map3": [_p, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
-    "mr_insert_received": [_p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p, _u64, _i32, _i32, _p],
+    "mr_insert_received": [_p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p, _u64, _i32, _i32, _p, _p],
     "mr_memcpy_async": [_p, _p, _u64, _i32, _p],
     "mr_d2h_async": [_p, _p, _u64, _p],
     "mr_h2d_pull": [_p, _p, _u64, _i32, _p],
@@ -36,10 +36,10 @@ _SIGS = {
     "mr_set_d2h_mode": [_i32],
     "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64, _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
-    "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p],
+    "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p, _p],
     "mr_table_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
     "mr_key_meta": [_p, _p, _p, _u64, _p, _u32, _p, _p, _p],
-    "mr_gather_key_bytes": [_p, _p, _p, _p, _u64, _p, _p, _p],
+    "mr_gather_key_bytes": [_p, _p, _p, _p, _u64, _p, _p, _u64, _p],
     "mr_exclusive_scan_u32": [_p, _p, _u64, _p, _p, _p],
     "mr_exclusive_scan_i64": [_p, _p, _u64, _p, _p, _p],
     "mr_gather_u64": [_p, _p, _p, _u64, _p],
@@ -82,7 +82,11 @@ _SIGS = {
     "mr_fix_loc": [_p, _u64, _p, _p, _u32, _p, _p],
     "mr_tail_compact": [_p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "mr_tail_gather": [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
-    "mr_tail_pack": [_p, _p, _u64, _p, _u32, _p, _p, _p],
+    "mr_tail_pack": [_p, _p, _u64, _p, _u32, _p, _p, _p, _p],
+    "mr_sort_debug_fail": [_i32],
+    "mr_set_long_mask_wc3": [_u64],
+    "mr_set_long_mask_keyops": [_u64],
+    "mr_set_long_mask_invidx": [_u64],
     "mr_tail_pack_bytes": [_u64, _u32],
     "mr_tail_ws_layout": [_u64, _u32, _u64, ctypes.POINTER(ctypes.c_uint64)],
     "mr_table_reset": [_p, _p, _p, _p, _u64, ctypes.c_longlong, _p],
@@ -112,6 +116,16 @@ def lib():
         L.mr_set_d2h_mode(1 if TUNABLES.d2h == "sdma" else 0)
         _LIB = L
     return _LIB
+
+
+_LONG_MASK_SETTERS = ("mr_set_long_mask_wc3", "mr_set_long_mask_keyops", "mr_set_long_mask_invidx")
+
+
+def set_long_mask(mask: int) -> None:
+    """Long-key hash mask of every kernel translation unit (debug knob; see
+    ops.keys.set_long_hash_bits)."""
+    for name in _LONG_MASK_SETTERS:
+        call(name, mask)
 
 
 def available() -> bool:

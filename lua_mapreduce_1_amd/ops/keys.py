@@ -49,6 +49,27 @@ def long_hash(b: bytes) -> int:
     return h
 
 
+# Debug knob: only the low bits of the 56-bit long-key hash are kept, so
+# distinct long keys collide (tests of the exact byte verification).  Host and
+# device must agree: set it with :func:`set_long_hash_bits`.
+LONG_HASH_MASK = M64
+
+
+def set_long_hash_bits(bits: int | None) -> None:
+    """Keep ``bits`` bits of the long-key hash (None: all of them) on the host
+    and in every loaded kernel translation unit."""
+    global LONG_HASH_MASK
+    LONG_HASH_MASK = M64 if bits is None else (1 << int(bits)) - 1
+    import torch
+    if torch.cuda.is_available():
+        from . import _hip
+        _hip.set_long_mask(LONG_HASH_MASK)
+
+
+def long_lo(h: int) -> int:
+    return (((fmix64(h) & LONG_HASH_MASK) << 8) & M64) | LONG_MARK
+
+
 def pack_key(b: bytes) -> tuple[int, int]:
     """(hi, lo) of a byte string."""
     n = len(b)
@@ -58,7 +79,7 @@ def pack_key(b: bytes) -> tuple[int, int]:
     if n <= PACK_MAX:
         lo = (int.from_bytes(b[8:15].ljust(7, b"\0"), "big") << 8) | n
     else:
-        lo = ((fmix64(long_hash(b)) << 8) & M64) | LONG_MARK
+        lo = long_lo(long_hash(b))
     return hi, lo
 
 
@@ -143,7 +164,7 @@ def span_keys(buf: np.ndarray, starts: np.ndarray, lens: np.ndarray) -> tuple[np
     lo[short] |= lens[short].astype(np.uint64)
     for i in np.flatnonzero(~short):
         s, ln = int(starts[i]), int(lens[i])
-        lo[i] = np.uint64(((fmix64(long_hash(bytes(buf[s:s + ln]))) << 8) & M64) | LONG_MARK)
+        lo[i] = np.uint64(long_lo(long_hash(bytes(buf[s:s + ln]))))
     return hi, lo
 
 

@@ -83,12 +83,20 @@ class HashTable:
 
     GPU: five HBM arrays + control words, filled by ``csrc/hip/hashtab.h``.
     CPU: pending arrays, reduced with ``np.unique`` at compaction.
+
+    ``src``: the byte source every rep word of the table indexes (set by the
+    owner: the map arena, the received shuffle buffer).  Long keys (>= 16
+    bytes) that match on (prefix, 56-bit hash) are compared byte for byte
+    through it, so colliding long keys are never merged (exact identity of the
+    reference's string keys, job.lua:83-97).  Without a source a long key is
+    identified by (prefix, hash) only.
     """
 
     def __init__(self, capacity: int, device="cpu", op: str = "sum"):
         self.device = torch.device(device)
         self.op = op
         self.cap = next_pow2(max(1024, int(capacity)))
+        self.src: torch.Tensor | None = None
         if self.device.type == "cuda":
             d = self.device
             self.tag = torch.zeros(self.cap, dtype=torch.int64, device=d)
@@ -107,6 +115,7 @@ class HashTable:
         return self.device.type == "cuda"
 
     def reset(self) -> None:
+        self.src = None
         if self.is_cuda:
             _hip.call("mr_table_reset", _hip.ptr(self.tag), _hip.ptr(self.lo), _hip.ptr(self.val), _hip.ptr(self.ctrl),
                       self.cap, _op_init(self.op), _hip.stream(self.device))
@@ -127,13 +136,17 @@ class HashTable:
 
     # -- inserts -------------------------------------------------------------
     def insert(self, hi: torch.Tensor, lo: torch.Tensor, val: torch.Tensor | None = None,
-               rep: torch.Tensor | None = None, rep_add: int = 0) -> None:
+               rep: torch.Tensor | None = None, rep_add: int = 0, src: torch.Tensor | None = None) -> None:
+        """Fold (key, value) rows in; rep words (+ ``rep_add``) index ``src``
+        (default: the table's own source)."""
         n = hi.numel()
         if n == 0:
             return
+        if src is not None:
+            self.src = src
         if self.is_cuda:
             _hip.call("mr_hash_agg", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), n, rep_add,
-                      OPS[self.op], *self._gtab(), self.cap, _hip.stream(self.device))
+                      OPS[self.op], *self._gtab(), self.cap, _hip.ptr(self.src), _hip.stream(self.device))
         else:
             v = _np(val).astype(np.int64) if val is not None else np.ones(n, np.int64)
             r = _u64(rep).copy() if rep is not None else np.zeros(n, np.uint64)
@@ -164,11 +177,17 @@ class HashTable:
         return self._ovf, self._ovf_counter
 
     def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, mode: int = 0,
-                      stamps: torch.Tensor | None = None) -> None:
+                      stamps: torch.Tensor | None = None, src: torch.Tensor | None = None) -> None:
         """Fused tokenize + exact key + combine of every whitespace token
-        (value 1): csrc/hip/wordcount3.hip.  ``mode`` = kernel config in the
-        low byte, ablation (timing only) in the high byte."""
+        (value 1): csrc/hip/wordcount3.hip.  ``text`` sits at byte
+        ``rep_base`` of the table's byte source ``src`` (default: ``text``
+        itself at 0).  ``mode`` = kernel config in the low byte, ablation
+        (timing only) in the high byte."""
         nbytes = text.numel()
+        if src is not None:
+            self.src = src
+        elif self.src is None and rep_base == 0:
+            self.src = text
         if nbytes == 0:
             return
         if self.is_cuda:
@@ -185,7 +204,8 @@ class HashTable:
                 np.minimum(lens, K.REP_LEN_MASK).astype(np.uint64)
             self._pending.append((hi, lo, np.ones(hi.size, np.int64), rep))
 
-    def insert_received(self, rec: torch.Tensor, recv_counts: torch.Tensor, W: int, rows: int | None = None) -> None:
+    def insert_received(self, rec: torch.Tensor, recv_counts: torch.Tensor, W: int, rows: int | None = None,
+                        src: torch.Tensor | None = None) -> None:
         """Fold all-to-all-received records into the table; ``recv_counts`` =
         the device count-exchange row [W, 3] (rows, key bytes, extra) per
         source.  ``rec``: int64 [n, 4] records (hi, lo, val, loc) whose key
@@ -195,12 +215,13 @@ class HashTable:
         whose rep words then index that same buffer.  One launch."""
         combined = rows is not None
         n = rows if combined else rec.shape[0]
+        self.src = rec if combined else src
         if n == 0:
             return
         if self.is_cuda:
             assert rec.is_contiguous() and recv_counts.is_contiguous()
             _hip.call("mr_insert_received", _hip.ptr(rec), n, _hip.ptr(recv_counts), W, *self._gtab(), self.cap,
-                      OPS[self.op], 1 if combined else 0, _hip.stream(self.device))
+                      OPS[self.op], 1 if combined else 0, _hip.ptr(self.src), _hip.stream(self.device))
             return
         assert not combined, "the combined layout is GPU-only"
         from .shuffle import absolute_reps
@@ -237,8 +258,19 @@ class HashTable:
         lo = np.concatenate([p[1] for p in self._pending])
         v = np.concatenate([p[2] for p in self._pending])
         r = np.concatenate([p[3] for p in self._pending])
-        keys = np.empty(hi.size, dtype=[("hi", np.uint64), ("lo", np.uint64)])
-        keys["hi"], keys["lo"] = hi, lo
+        keys = np.empty(hi.size, dtype=[("hi", np.uint64), ("lo", np.uint64), ("d", np.int64)])
+        keys["hi"], keys["lo"], keys["d"] = hi, lo, 0
+        long_ = (lo & np.uint64(0xFF)) == np.uint64(K.LONG_MARK)
+        if long_.any() and self.src is not None:
+            # exact identity of long keys: equal (prefix, hash) but different
+            # bytes get different ids (the device tables compare bytes)
+            sb = _np(self.src)
+            ids: dict = {}
+            d = keys["d"]
+            for i in np.flatnonzero(long_):
+                rr = int(r[i])
+                o, ln = rr >> K.REP_LEN_BITS, rr & K.REP_LEN_MASK
+                d[i] = ids.setdefault(sb[o:o + ln].tobytes(), len(ids) + 1)
         uk, first, inv = np.unique(keys, return_index=True, return_inverse=True)
         if self.op == "sum":
             agg = np.zeros(uk.size, np.int64)
@@ -356,7 +388,7 @@ def gather_key_bytes(hi, lo, rep, src, lengths: torch.Tensor | None = None, capa
         blob = torch.empty(max(nb, 1), dtype=torch.uint8, device=d)
         srcp = _hip.ptr(src) if src is not None else None
         _hip.call("mr_gather_key_bytes", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), _hip.ptr(off), n, srcp,
-                  _hip.ptr(blob), _hip.stream(d))
+                  _hip.ptr(blob), blob.numel(), _hip.stream(d))
         if capacity is None:
             blob = blob[:nb]
         return torch.cat([off, total]), blob
@@ -514,7 +546,8 @@ def sort_by_partition_key(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor
     (long keys sharing the 8-byte prefix compared bytewise on the device).
     ``bad`` (device int32): bit 0 = a run exceeded the fixup limit (caller must
     use the full multi-word sort); bit 1 = no ``src`` and a long-key prefix tie
-    exists (the host must check those keys bytewise).  CPU: lexsort (+bit 1).
+    exists (the host must check those keys bytewise); bit 2 = the radix sort's
+    look-back gave up (caller must re-sort).  CPU: lexsort (+bit 1).
     """
     n = hi.numel()
     if not hi.is_cuda or nparts > 256:
@@ -535,13 +568,38 @@ def sort_by_partition_key(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor
     bad = torch.zeros(1, dtype=torch.int32, device=d)
     _hip.call("mr_tie_fixup", _hip.ptr(c), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part2),
               n, _hip.ptr(bad), _hip.ptr(src) if src is not None else None, None, s)
+    err = sort_error_word(d)
+    if err is not None:  # bit 2: the sort's look-back gave up (order invalid)
+        bad.bitwise_or_((err != 0).to(torch.int32) * 4)
     return part2, hi, lo, val, rep, bad
 
 
 def sort_error(device) -> bool:
-    """True if a onesweep look-back gave up (result of that sort is invalid)."""
+    """True if a onesweep look-back of the last sort_keys call on ``device``
+    gave up (that sort's order is invalid).  Synchronises."""
     ws = _SORT_WS.get(torch.device(device))
     return bool(ws is not None and int(ws["small"][2112].item()) != 0)
+
+
+def sort_error_word(device) -> torch.Tensor | None:
+    """Device int32[1] error word of the last sort_keys call (no sync)."""
+    ws = _SORT_WS.get(torch.device(device))
+    return None if ws is None else ws["small"][2112:2113]
+
+
+def sort_keys_checked(words, bits=None, retries: int = 2, **kw):
+    """sort_keys that checks the look-back error word (one host sync) and
+    re-sorts on a give-up; raises after ``retries`` failed re-sorts."""
+    for attempt in range(retries + 1):
+        out = sort_keys(words, bits, **kw)
+        if not words[0].is_cuda or not sort_error(words[0].device):
+            return out
+    raise RuntimeError("radix sort: decoupled look-back gave up %d times" % (retries + 1))
+
+
+def debug_sort_fail(passes: int) -> None:
+    """Test knob: the next ``passes`` onesweep passes give up one look-back."""
+    _hip.call("mr_sort_debug_fail", int(passes))
 
 
 def bincount(ids: torch.Tensor, nbins: int) -> torch.Tensor:

@@ -598,7 +598,11 @@ class SPMDEngine:
     def _run_map(self, jobs, recs, j0, j1) -> None:
         ctx = devmod.DeviceMapContext.__new__(devmod.DeviceMapContext)
         ctx.device, ctx.op, ctx.table = self.device, self.op, self.table
-        ctx.sources, ctx.base, ctx.host_pairs = [], 0, []
+        ctx.arena, ctx.sources, ctx.base, ctx.host_pairs = None, [], 0, []
+        if self.device_input == "split":
+            # the staged splits ARE the key-byte source: the map reads them in
+            # place (ctx.base = offset of each mapped chunk in the arena)
+            ctx.sources = None
         ctx.emit = devmod.DeviceEmitter(ctx)
         self._ctx = ctx
         # the rank's whole staged input is ONE byte source (rep offsets index it)
@@ -615,6 +619,7 @@ class SPMDEngine:
                         # rep offsets relative to the arena start
                         base = data.data_ptr() - self.arena.data_ptr()
                         ctx.base = base
+                        ctx.arena = self.table.src = self.arena
                         self.dmap(keys if b - a > 1 else keys[0], data, ctx.emit)
                     else:
                         self.dmap(keys[0] if b - a == 1 else keys, data, ctx.emit)
@@ -738,7 +743,7 @@ class SPMDEngine:
             self.red_table = ops.HashTable(cap, device=self.device, op=self.op)
         else:
             self.red_table.reset()
-        self.red_table.insert(hi, lo, val, rep)
+        self.red_table.insert(hi, lo, val, rep, src=src)
         return self.red_table.compact()
 
     # ------------------------------------------------------------------------

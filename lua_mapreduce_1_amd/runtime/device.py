@@ -39,34 +39,55 @@ def default_device():
 
 
 class DeviceMapContext:
+    """State of one device map job: the hash table and ONE contiguous device
+    byte arena holding every key-byte source the job emitted from (input
+    texts, host-pair blobs, emitted key blobs).  Every rep word of the table
+    indexes that arena, so long keys are verified byte for byte on insert
+    (exact identity) and their bytes are materialised from it at the end."""
+
     def __init__(self, device=None, op: str = "sum", capacity: int = 1 << 20):
         self.device = torch.device(device) if device is not None else default_device()
         self.op = op
         self.capacity = capacity
         self.table = ops.HashTable(capacity, device=self.device, op=op)
-        self.sources: list[torch.Tensor] = []
+        self.arena: torch.Tensor | None = None
+        self.sources: list[torch.Tensor] = []  # (engine-owned arenas only: see SPMDEngine._run_map)
         self.base = 0
         self.host_pairs: list[tuple[bytes, int]] = []
         self.emit = DeviceEmitter(self)
 
-    def add_source(self, t: torch.Tensor) -> int:
+    def add_source(self, t: torch.Tensor) -> tuple[int, torch.Tensor]:
+        """Append ``t``'s bytes to the arena; returns (offset, arena view of
+        them).  The arena grows by doubling (offsets stay valid)."""
+        if self.sources is None:
+            raise RuntimeError("a map over engine-staged splits (device_input='split') emits keys whose bytes are "
+                               "in its input: words(), or pairs() with rep words relative to the mapped data")
+        n = t.numel()
+        need = self.base + n
+        if self.arena is None or self.arena.numel() < need:
+            grown = torch.empty(max(need, 2 * (self.arena.numel() if self.arena is not None else 0), 1 << 16),
+                                dtype=torch.uint8, device=self.device)
+            if self.arena is not None and self.base:
+                grown[:self.base].copy_(self.arena[:self.base])
+            self.arena = grown
         b = self.base
-        self.sources.append(t)
-        self.base += t.numel()
-        return b
+        view = self.arena[b:need]
+        if n:
+            view.copy_(t.reshape(-1), non_blocking=True)
+        self.base = need
+        self.table.src = self.arena
+        return b, view
 
     def source(self) -> torch.Tensor | None:
-        if not self.sources:
+        if self.arena is None:
             return None
-        if len(self.sources) == 1:
-            return self.sources[0]
-        return torch.cat(self.sources)
+        return self.arena[:self.base]
 
     def flush_host_pairs(self) -> None:
         if not self.host_pairs:
             return
         blob = b"".join(k for k, _ in self.host_pairs)
-        base = self.add_source(torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(self.device))
+        base, _ = self.add_source(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
         his, los, reps, off = [], [], [], 0
         for k, _ in self.host_pairs:
             h, l_ = K.pack_key(k)
@@ -76,7 +97,7 @@ class DeviceMapContext:
             off += len(k)
         t = lambda a: torch.from_numpy(np.array(a, dtype=np.uint64).view(np.int64)).to(self.device)  # noqa: E731
         vals = torch.tensor([v for _, v in self.host_pairs], dtype=torch.int64, device=self.device)
-        self.table.insert(t(his), t(los), vals, t(reps))
+        self.table.insert(t(his), t(los), vals, t(reps), src=self.arena)
         self.host_pairs = []
 
     def grow_and_retry(self, fn) -> None:
@@ -94,16 +115,27 @@ class DeviceEmitter:
         return self.ctx.device
 
     def words(self, text: torch.Tensor) -> None:
-        if text.device != self.ctx.device:
-            text = text.to(self.ctx.device, non_blocking=True)
-        base = self.ctx.add_source(text)
-        self.ctx.table.wordcount_map(text, rep_base=base)
+        """Every whitespace token of ``text`` with value 1 (fused kernel)."""
+        ctx = self.ctx
+        if ctx.arena is not None and ctx.sources is None:
+            # engine-owned arena (SPMDEngine._run_map): ``text`` already lives
+            # in it at byte ctx.base
+            ctx.table.wordcount_map(text, rep_base=ctx.base, src=ctx.arena)
+            ctx.base += text.numel()
+            return
+        base, view = ctx.add_source(text)
+        ctx.table.wordcount_map(view, rep_base=base, src=ctx.arena)
 
     def pairs(self, hi, lo, vals=None, rep=None, src: torch.Tensor | None = None) -> None:
+        """A batch of encoded (key, value) pairs; long keys' rep words index
+        ``src`` (appended to the job's arena)."""
+        ctx = self.ctx
         add = 0
         if src is not None:
-            add = self.ctx.add_source(src.to(self.ctx.device))
-        self.ctx.table.insert(hi, lo, vals, rep, rep_add=add)
+            add, _ = ctx.add_source(src)
+        elif ctx.sources is None:
+            add = ctx.base  # engine-staged input: rep words relative to the mapped data
+        ctx.table.insert(hi, lo, vals, rep, rep_add=add, src=ctx.arena)
 
     def __call__(self, key, value=1) -> None:
         if isinstance(key, str):
@@ -289,7 +321,7 @@ def finalize_table_device(table, n: int, src, nparts: int) -> dict:
     nb = int(_hip.lib().mr_tail_pack_bytes(n, nparts))
     packed = torch.empty(nb, dtype=torch.uint8, device=d)
     _hip.call("mr_tail_pack", _hip.ptr(val), _hip.ptr(off), n, _hip.ptr(pcount), nparts, _hip.ptr(bad),
-              _hip.ptr(packed), s)
+              _hip.ptr(ops.primitives.sort_error_word(d)), _hip.ptr(packed), s)
     hp = _POOL.get("pack", nb, torch.uint8)
     dma_to_host(hp, packed)
     est = _BLOB_EST.get(d)
@@ -413,6 +445,10 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
         else:
             ho = pend["ho"]
             nbytes = int(ho[n]) if n else 0
+        if nbytes > blob.numel() and not (flag0 := (f_bad if pend.get("fused") else int(pend["hbad"][0]))) & 4:
+            raise RuntimeError(f"key bytes ({nbytes}) exceed the blob capacity ({blob.numel()})")
+        if nbytes > blob.numel():
+            nbytes = blob.numel()  # a given-up sort's rows: discarded below (re-sort)
         if est is not None and nbytes > est:  # grew past the estimate: copy the rest
             hb = _POOL.get("blob", nbytes, torch.uint8)
             hb.copy_(blob[:nbytes])
@@ -422,13 +458,19 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
         _BLOB_EST[hi.device] = nbytes + nbytes // 16 + 4096
         hb = hb[:nbytes]
         flag = f_bad if pend.get("fused") else int(pend["hbad"][0])
-        if flag & 1:
-            # a tie run was too long for the fixup kernel: redo with the full sort
+        if flag & 5:
+            # bit 0: a tie run was too long for the fixup kernel; bit 2: the
+            # radix sort's decoupled look-back gave up (its order is invalid)
+            # -> redo with the full multi-word sort, checked (raises if the
+            # look-back keeps giving up)
+            if flag & 4:
+                import sys
+                sys.stderr.write("# warning: radix sort look-back gave up; re-sorting\n")
             ahi, alo, aval, arep = pend["args"]
             src = pend["src"]
             p2 = partition_of(ahi, alo, arep, src, nparts, partition_module)
-            perm = ops.sort_keys([p2.to(torch.int64), ahi, alo],
-                                 bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
+            perm = ops.sort_keys_checked([p2.to(torch.int64), ahi, alo],
+                                         bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
             return finalize(ahi[perm], alo[perm], aval[perm], arep[perm], src, nparts, partition_module,
                             part=p2[perm], _presorted=True, need_keys=need_keys)
         # offsets stay int32 when the blob is < 2 GiB (no host-side widening pass)
