@@ -262,8 +262,12 @@ class SPMDEngine:
         self.partmod = modules.load(self.params["partitionfn"])
         self.redmod = modules.load(self.params["reducefn"])
         self.finalmod = modules.load(self.params.get("finalfn")) if self.params.get("finalfn") else None
+        seen: set = set()
         for m in (self.taskfn, self.mapmod, self.partmod, self.redmod, self.finalmod):
-            modules.init_once(m, self.init_args)
+            # every engine is a new task: its modules' inits run with ITS init
+            # args (once per distinct init function), whatever earlier engines
+            # of this process did
+            modules.init_once(m, self.init_args, seen)
         self.op = modules.field(self.redmod, "device_reduce", "sum")
         spec = modules.field(self.partmod, "device_partition")
         self.nparts = int(self.params.get("num_partitions") or (spec[1] if spec else 0) or self.world)

@@ -55,8 +55,12 @@ class HostSPMDEngine(SPMDEngine):
         self.finalmod = modules.load(self.params.get("finalfn")) if self.params.get("finalfn") else None
         cname = self.params.get("combinerfn")
         self.combmod = modules.load(cname) if cname else None
+        seen: set = set()
         for m in (self.taskfn, self.mapmod, self.partmod, self.redmod, self.finalmod, self.combmod):
-            modules.init_once(m, self.init_args)
+            # every engine is a new task: its modules' inits run with ITS init
+            # args (once per distinct init function), whatever earlier engines
+            # of this process did
+            modules.init_once(m, self.init_args, seen)
         self.device_input = None
         self.iteration = 0
         self.finished = False

@@ -59,15 +59,19 @@ def field(mod, name: str, default=None):
     return v
 
 
-def init_once(mod, args) -> None:
+def init_once(mod, args, seen: set | None = None) -> None:
+    """Call the module's ``init(args)`` unless this init function already ran
+    (in ``seen``: one task's dedup set, job.lua:64-73; default: the process-wide
+    set, reset between tasks by :func:`reset`)."""
     f = field(mod, "init")
     if f is None:
         return
+    seen = _initialized if seen is None else seen
     key = id(f)
-    if key in _initialized:
+    if key in seen:
         return
     f(args)
-    _initialized.add(key)
+    seen.add(key)
 
 
 def reset() -> None:

@@ -238,11 +238,30 @@ def test_sort_giveup_in_fused_tail(gpu, sort_fail, monkeypatch, native_tail):
                                 init_args={"nsplits": len(splits), "num_reducers": 7}),
                            split_store=S.SplitStore(splits), device=gpu)
         res = eng.run_iteration()
-        return {k: v[0] for _n, c in eng.gather_results(res) for k, v in codec.iter_columnar(c)}
+        return [(k, v[0]) for _n, c in eng.gather_results(res) for k, v in codec.iter_columnar(c)]
 
     want = dict(Counter(w.decode() for s in splits for w in s.split()))
     sort_fail(1)
-    assert run() == want
+    got = run()
+    keys = [k for k, _ in got]
+    assert len(keys) == len(set(keys)), f"{len(keys) - len(set(keys))} duplicated keys, sum {sum(v for _, v in got)}"
+    assert dict(got) == want
     sort_fail(1000)
     with pytest.raises(RuntimeError, match="gave up"):
         run()
+
+
+def test_engines_in_one_process_init_their_own_args():
+    """Each engine is a new task: module inits run with its own init args
+    (an earlier engine's nsplits must not cut a later job short)."""
+    from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore
+    from lua_mapreduce_1_amd.utils.corpus import europarl_like
+    M = "lua_mapreduce_1_amd.models.wordcount"
+    for nsplits in (3, 7):
+        splits = europarl_like(seed=nsplits, lines=700 * nsplits, words=5000 * nsplits, vocab_size=2000,
+                               split_lines=700)
+        eng = SPMDEngine(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                              init_args={"nsplits": len(splits), "num_reducers": nsplits}),
+                         split_store=SplitStore(splits, pin=False), device="cpu")
+        res = eng.run_iteration()
+        assert res.total_value == 5000 * nsplits and eng.nparts == nsplits

@@ -1,4 +1,4 @@
-"""Debug: forced sort give-up in the fused tail; where do the values go wrong?"""
+"""Debug: forced sort give-up in the fused tail after the sort-only give-up test."""
 import sys
 from collections import Counter
 import numpy as np
@@ -10,31 +10,34 @@ from lua_mapreduce_1_amd.runtime import device as devmod, codec
 from lua_mapreduce_1_amd.utils.corpus import europarl_like
 
 gpu = torch.device("cuda", 0)
+mode = sys.argv[1]
+if "pre" in mode:
+    rng = np.random.default_rng(5)
+    w = torch.from_numpy(rng.integers(-2**63, 2**63 - 1, 300_000, dtype=np.int64))
+    ops.debug_sort_fail(1); ops.sort_keys([w.to(gpu)]); print("err", ops.sort_error(gpu))
+    ops.debug_sort_fail(1); ops.sort_keys_checked([w.to(gpu)])
+    ops.debug_sort_fail(100)
+    try:
+        ops.sort_keys_checked([w.to(gpu)], retries=2)
+    except RuntimeError as e:
+        print("raised", e)
+    ops.debug_sort_fail(0)
 splits = europarl_like(seed=4, lines=20_000, words=300_000, vocab_size=30_000, split_lines=2000)
 want = Counter(w.decode() for s in splits for w in s.split())
 M = "lua_mapreduce_1_amd.models.wordcount"
-
-def check(tag, cols):
-    got = {}
-    nb = cols["bounds"]
-    for p in range(len(nb) - 1):
-        for k, v in codec.iter_columnar(devmod.partition_slice(cols, p)):
-            got[k] = v[0]
-    bad = [(k, got.get(k), want[k]) for k in want if got.get(k) != want[k]]
-    print(tag, "n", len(got), "mismatch", len(bad), bad[:5], flush=True)
-
-orig_unpack = devmod._unpack_fused
-for mode in ("force_flag1", "fail1"):
-    eng = S.SPMDEngine(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
-                            init_args={"nsplits": len(splits), "num_reducers": 7}),
-                       split_store=S.SplitStore(splits), device=gpu)
-    if mode == "force_flag1":
-        def fake(pend):
-            v, o, c, b = orig_unpack(pend)
-            return v, o, c, b | 1
-        devmod._unpack_fused = fake
-    else:
-        devmod._unpack_fused = orig_unpack
-        ops.debug_sort_fail(1)
-    res = eng.run_iteration()
-    check(mode, res._cols)
+orig = devmod.finalize
+def spy(hi, lo, val, rep, src, nparts, pm=None, part=None, _presorted=False, need_keys=False):
+    torch.cuda.synchronize()
+    print("fallback finalize: n", hi.numel(), "val sum", int(val.sum()), "part sorted",
+          bool((part[1:] >= part[:-1]).all()), "keys sorted?", flush=True)
+    return orig(hi, lo, val, rep, src, nparts, pm, part, _presorted, need_keys)
+devmod.finalize = spy
+eng = S.SPMDEngine(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                        init_args={"nsplits": len(splits), "num_reducers": 7}),
+                   split_store=S.SplitStore(splits), device=gpu)
+if "fail" in mode:
+    ops.debug_sort_fail(1)
+res = eng.run_iteration()
+got = {k: v[0] for _n, c in eng.gather_results(res) for k, v in codec.iter_columnar(c)}
+bad = [(k, got.get(k), want[k]) for k in want if got.get(k) != want[k]]
+print(mode, "n", len(got), "mismatch", len(bad), bad[:4], flush=True)
