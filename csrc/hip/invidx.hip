@@ -96,7 +96,9 @@ __device__ u64 long_lo_global(const u8* text, u64 p0, u64 len) {
 }
 
 // LDS probe/claim; returns the local slot or -1 (table full / probe budget).
-__device__ __forceinline__ int lds_find_or_claim(Lds& L, u64 hi, u64 lo, u32 rep) {
+// A long key matched on (hi, lo) is compared byte for byte with the slot's
+// first occurrence (both in this chunk, kb = its first byte): exact identity.
+__device__ __forceinline__ int lds_find_or_claim(Lds& L, u64 hi, u64 lo, u32 rep, const u8* kb) {
   u64 h = hi ^ (lo * 0x9E3779B97F4A7C15ull);
   h ^= h >> 31;
   h *= 0xC2B2AE3D27D4EB4Full;
@@ -122,7 +124,10 @@ __device__ __forceinline__ int lds_find_or_claim(Lds& L, u64 hi, u64 lo, u32 rep
     if (cur == tag) {
       const u64 l = __hip_atomic_load(&L.lo[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (l == 0) continue;  // being published by its claimer
-      if (l == lo && L.hi[slot] == hi) return (int)slot;
+      if (l == lo && L.hi[slot] == hi &&
+          (!key_is_long(lo) || rep_bytes_equal(kb, make_rep(L.rep[slot] & 0xFFFFu, L.rep[slot] >> 16),
+                                               make_rep(rep & 0xFFFFu, rep >> 16))))
+        return (int)slot;
     }
     slot = (slot + 1) & (SLOTS - 1);
     ++probes;
@@ -282,7 +287,9 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
           lo = long_lo_global(text, gpos, len);
         }
         const u32 line = thread_line + __builtin_popcount(nlm & ((1u << i) - 1u));
-        int ls = len < 65536 ? lds_find_or_claim(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16)) : -1;
+        int ls = len < 65536 ? lds_find_or_claim(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16),
+                                                       text + chunk_begin)
+                         : -1;
         u32 ref;
         if (ls >= 0) {
           ref = (u32)ls;
@@ -519,7 +526,7 @@ int mr_ii_map(const void* text, u64 nbytes, u64 chunk, u64 rep_base, const void*
   g.rep = (u64*)rep;
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
-  g.src = nullptr;
+  g.src = (const u8*)text - rep_base;  // the vocabulary's rep words index the caller's byte source
   const u64 nb = (nbytes + chunk - 1) / chunk;
   hipLaunchKernelGGL(ii::ii_map_kernel, dim3((unsigned)nb), dim3(ii::T), 0, s, (const u8*)text, nbytes, chunk,
                      rep_base, (const u32*)chunk_line_base, g, doc_bits, (u64*)out, (unsigned long long*)out_counter,
@@ -604,9 +611,11 @@ __global__ void ii_insert_slots_kernel(GTab g, const u64* __restrict__ hi, const
 }  // namespace ii
 }  // namespace mr
 
+// src: the byte source of the rep words (received key bytes; null = no
+// long-key byte verification)
 extern "C" int mr_ii_insert_slots(void* tag, void* thi, void* tlo, void* val, void* trep, void* ctrl, u64 cap,
                                   const void* hi, const void* lo, const void* rep, u64 n, void* out_slot,
-                                  hipStream_t s) {
+                                  const void* src, hipStream_t s) {
   if (n == 0) return 0;
   GTab g;
   g.tag = (u64*)tag;
@@ -616,8 +625,43 @@ extern "C" int mr_ii_insert_slots(void* tag, void* thi, void* tlo, void* val, vo
   g.rep = (u64*)trep;
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
-  g.src = nullptr;
+  g.src = (const u8*)src;
   hipLaunchKernelGGL(ii::ii_insert_slots_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, g, (const u64*)hi,
                      (const u64*)lo, (const u64*)rep, n, (long long*)out_slot);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Segmented gather of posting lists into a new word order: output posting j
+// belongs to the word i with new_off[i] <= j < new_off[i+1] (binary search),
+// and comes from old_start[perm[i]] + (j - new_off[i]).  One thread per
+// posting: no per-word imbalance (a frequent word has millions of postings).
+namespace mr {
+namespace ii {
+__global__ void __launch_bounds__(256) ii_seg_gather_kernel(const u32* __restrict__ perm,
+                                                            const long long* __restrict__ old_start,
+                                                            const long long* __restrict__ new_off, u64 nw, u64 n,
+                                                            const int* __restrict__ src, int* __restrict__ dst) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+    u64 a = 0, b = nw;  // largest i with new_off[i] <= j
+    while (b - a > 1) {
+      const u64 m = (a + b) >> 1;
+      if ((u64)new_off[m] <= j) a = m;
+      else b = m;
+    }
+    const u64 w = clamp_row(perm[a], nw);
+    const u64 k = (u64)old_start[w] + (j - (u64)new_off[a]);
+    dst[j] = src[clamp_row(k, n)];
+  }
+}
+}  // namespace ii
+}  // namespace mr
+
+extern "C" int mr_ii_seg_gather(const void* perm, const void* old_start, const void* new_off, u64 nw, u64 n,
+                                const void* src, void* dst, hipStream_t s) {
+  if (n == 0 || nw == 0) return 0;
+  hipLaunchKernelGGL(ii::ii_seg_gather_kernel, dim3(grid_n(n, 256, 16384)), dim3(256), 0, s, (const u32*)perm,
+                     (const long long*)old_start, (const long long*)new_off, nw, n, (const int*)src, (int*)dst);
   return (int)hipGetLastError();
 }

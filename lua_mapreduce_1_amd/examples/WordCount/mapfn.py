@@ -1,7 +1,7 @@
 """WordCount mapfn (reference: examples/WordCount/mapfn.lua): whitespace tokens.
 
 ``device_mapfn`` is the GPU form: the file is staged to HBM and every token is
-counted by the fused tokenizer/combiner kernel (csrc/hip/wordcount.hip)."""
+counted by the fused tokenizer/combiner kernel (csrc/hip/wordcount3.hip)."""
 from lua_mapreduce_1_amd.ops import io as _io
 
 

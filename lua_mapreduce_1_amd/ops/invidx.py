@@ -57,10 +57,19 @@ class Vocab:
             self.table.reset()
 
     # -- CPU helpers --------------------------------------------------------------
-    def _assign_cpu(self, hi: np.ndarray, lo: np.ndarray, rep: np.ndarray) -> np.ndarray:
-        """Dense ids for (hi, lo) (first occurrence keeps its rep)."""
-        keys = np.empty(hi.size, dtype=[("h", "<u8"), ("l", "<u8")])
-        keys["h"], keys["l"] = hi, lo
+    def _assign_cpu(self, hi: np.ndarray, lo: np.ndarray, rep: np.ndarray, src=None) -> np.ndarray:
+        """Dense ids for (hi, lo) (first occurrence keeps its rep); long keys
+        that collide on (hi, lo) get different ids when their bytes differ."""
+        keys = np.empty(hi.size, dtype=[("h", "<u8"), ("l", "<u8"), ("d", "<i8")])
+        keys["h"], keys["l"], keys["d"] = hi, lo, 0
+        long_ = (lo & np.uint64(0xFF)) == np.uint64(K.LONG_MARK)
+        if long_.any() and src is not None:
+            sb = src.numpy() if isinstance(src, torch.Tensor) else np.asarray(src)
+            ids: dict = {}
+            ru = rep.view(np.uint64)
+            for i in np.flatnonzero(long_):
+                o, ln = int(ru[i]) >> K.REP_LEN_BITS, int(ru[i]) & K.REP_LEN_MASK
+                keys["d"][i] = ids.setdefault(sb[o:o + ln].tobytes(), len(ids) + 1)
         uk, first, inv = np.unique(keys, return_index=True, return_inverse=True)
         self.hi = _t64(uk["h"].copy())
         self.lo = _t64(uk["l"].copy())
@@ -98,7 +107,7 @@ def map_postings(text: torch.Tensor, vocab: Vocab, doc_bits: int, rep_base: int 
     hi, lo = K.span_keys(buf, starts, lens)
     rep = ((starts.astype(np.uint64) + np.uint64(rep_base)) << np.uint64(K.REP_LEN_BITS)) | \
         np.minimum(lens, K.REP_LEN_MASK).astype(np.uint64)
-    ids = vocab._assign_cpu(hi, lo, rep.view(np.int64))
+    ids = vocab._assign_cpu(hi, lo, rep.view(np.int64), buf)
     nl = np.flatnonzero(buf == 10)
     line = np.searchsorted(nl, starts, side="left").astype(np.int64)
     return torch.from_numpy((ids << doc_bits) | line)
@@ -216,15 +225,38 @@ def add_dest(keys: torch.Tensor, dest_of_id: torch.Tensor, doc_bits: int, id_bit
     return shift
 
 
-def insert_ids(vocab: Vocab, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor) -> torch.Tensor:
-    """Ids of (hi, lo) in ``vocab`` (inserting new words) -> int64."""
+def insert_ids(vocab: Vocab, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor,
+               src: torch.Tensor | None = None) -> torch.Tensor:
+    """Ids of (hi, lo) in ``vocab`` (inserting new words) -> int64.  ``src``:
+    the bytes the rep words index (exact identity of long keys)."""
     n = hi.numel()
     if hi.is_cuda:
         t = vocab.table
         out = torch.empty(n, dtype=torch.int64, device=hi.device)
         _hip.call("mr_ii_insert_slots", *t._gtab(), t.cap, _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), n,
-                  _hip.ptr(out), _hip.stream(hi.device))
+                  _hip.ptr(out), _hip.ptr(src), _hip.stream(hi.device))
         if vocab.overflowed:
             raise RuntimeError("inverted index reduce: vocabulary table overflow")
         return out
-    return torch.from_numpy(vocab._assign_cpu(_u64(hi), _u64(lo), rep.numpy()))
+    return torch.from_numpy(vocab._assign_cpu(_u64(hi), _u64(lo), rep.numpy(), src))
+
+
+def seg_gather(perm: torch.Tensor, old_start: torch.Tensor, new_off: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    """Posting lists reordered by a word permutation: word i of the output is
+    word perm[i] of the input (``old_start`` = input word starts, ``new_off`` =
+    output offsets, nw+1 entries).  int32 postings."""
+    nw = perm.numel()
+    n = src.numel()
+    if src.is_cuda:
+        out = torch.empty(n, dtype=torch.int32, device=src.device)
+        p32 = perm.to(torch.int32).contiguous()
+        _hip.call("mr_ii_seg_gather", _hip.ptr(p32), _hip.ptr(old_start.contiguous()), _hip.ptr(new_off.contiguous()),
+                  nw, n, _hip.ptr(src), _hip.ptr(out), _hip.stream(src.device))
+        return out
+    if nw == 0:
+        return src[:0].clone()
+    p = perm.long()
+    lens = (old_start[1:] - old_start[:-1])[p] if old_start.numel() == nw + 1 else None
+    idx = torch.cat([torch.arange(int(old_start[int(w)]), int(old_start[int(w)]) + int(ln))
+                     for w, ln in zip(p.tolist(), lens.tolist())]) if n else torch.zeros(0, dtype=torch.int64)
+    return src[idx]

@@ -211,6 +211,16 @@ def gather_objects(obj, dst: int = 0, group=None):
     return out
 
 
+def all_gather_object(obj, group=None) -> list:
+    """Every rank's ``obj`` (in rank order) on every rank."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return [obj]
+    _, world = world_info(group)
+    out = [None] * world
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
 def all_gather_tensor(t: torch.Tensor, group=None) -> torch.Tensor:
     """Concatenation of every rank's equally-shaped ``t`` along dim 0."""
     if not (dist.is_available() and dist.is_initialized()):

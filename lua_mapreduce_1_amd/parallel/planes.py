@@ -1,0 +1,558 @@
+"""List-valued and record-valued device data planes of the SPMD engine.
+
+The fold plane (``device_reduce`` = sum/min/max/count, parallel/spmd.py) keeps
+one int64 per key in an HBM hash table.  Two more reduce kinds make the same
+engine — same taskfn / device_mapfn / partition / reducefn / finalfn modules,
+same ``result.P<NN>`` layout, same job records and stats — run the other
+BASELINE workloads as MapReduce jobs:
+
+* :class:`ListPlane` (``device_reduce = "concat_unique" | "concat"``): the
+  reduce concatenates every value emitted for a key (reference reducers over
+  merged value lists, job.lua:260-284 / utils.lua:206-271) — the inverted
+  index.  The map turns each (key, value) into ONE 64-bit posting
+  ``word id << doc_bits | value`` (word ids = slots of an HBM vocabulary
+  table, csrc/hip/invidx.hip); one radix sort groups postings by key, a
+  fused unique drops repeats (``concat_unique``), and the lists come out as
+  (offsets, int32 values) per key, ordered by (partition, key) like every
+  result file.  At W > 1 the destination rank rides in the posting's top bits
+  and the shuffle is three ``all_to_all_single`` (words, key bytes, values).
+* :class:`RecordPlane` (``device_reduce = "identity"``): fixed-width records
+  (100-byte TeraSort rows, 10-byte keys) are moved, not folded — identity
+  map, range partitioner with sampled splitters (``device_partition =
+  ("range", R, None)``, TeraSort's total-order partitioner), identity reduce
+  = a per-rank radix sort of the received rows (csrc/hip/terasort.hip).
+
+Results stay in HBM (they can be ~the size of the input); ``partitions`` /
+``gather_results`` copy them to host memory on first use.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..ops import invidx as II
+from ..ops import terasort as TS
+from ..ops.keys import REP_LEN_BITS
+from ..runtime import device as devmod
+from ..runtime import modules
+from ..utils import STATUS
+from ..utils import trace
+from . import dist as D
+
+LIST_OPS = ("concat", "concat_unique")
+RECORD_OPS = ("identity",)
+
+
+def make_plane(eng):
+    if eng.op in LIST_OPS:
+        return ListPlane(eng)
+    if eng.op in RECORD_OPS:
+        return RecordPlane(eng)
+    return None
+
+
+def _bits(n: int) -> int:
+    return max(1, int(max(n, 1) - 1).bit_length())
+
+
+class DeviceResult:
+    """IterationResult whose per-partition columns live in HBM until first
+    use (``partitions`` downloads them)."""
+
+    def __init__(self):
+        self.result_names: dict[int, str] = {}
+        self.map_jobs: list = []
+        self.red_jobs: list = []
+        self.timings: dict[str, float] = {}
+        self.distinct_keys = 0
+        self.total_value = 0
+        self.failed_maps = 0
+        self.failed_reduces = 0
+        self.device = None  # device-resident columns (plane specific)
+        self._parts = None
+        self._materialize = None
+
+    @property
+    def partitions(self) -> dict[int, dict]:
+        if self._parts is None:
+            self._parts = self._materialize() if self._materialize is not None else {}
+        return self._parts
+
+
+def _records(eng, jobs, j0, j1, t0):
+    recs = eng._new_records(jobs, j0, j1)
+    for j in range(j0, j1):
+        recs[j].status, recs[j].started, recs[j].worker = STATUS.RUNNING, t0, eng.rank
+    return recs
+
+
+def _mark_written(recs, j0, j1, t0, t1, c0):
+    for j in range(j0, j1):
+        if recs[j].status != STATUS.FAILED:
+            recs[j].status = STATUS.WRITTEN
+        recs[j].written = t1
+        recs[j].real_time = (t1 - t0) / max(1, j1 - j0)
+        recs[j].cpu_time = (time.process_time() - c0) / max(1, j1 - j0)
+
+
+def _result_jobs(eng, res, counts: list[int], t1: float) -> None:
+    from .spmd import JobRecord
+    digits = len(str(max(eng.nparts - 1, 0)))
+    for p, c in enumerate(counts):
+        if c:
+            res.result_names[p] = ("%s.P%0" + str(digits) + "d") % (eng.result_ns, p)
+            r = JobRecord(p, {"result": res.result_names[p]})
+            r.status, r.started, r.written, r.worker = STATUS.WRITTEN, t1, time.time(), eng.rank
+            r.real_time = r.written - t1
+            res.red_jobs.append(r)
+
+
+# ---------------------------------------------------------------------------
+class ListEmitter:
+    """``emit`` of a list-plane map: ``emit.word_lines(text)`` emits every
+    whitespace token of the staged chunk with the global index of the line it
+    is on (the inverted index's (word, document) pairs)."""
+
+    def __init__(self, plane):
+        self.plane = plane
+        self.chunk = None  # (arena byte offset, line base relative to the rank's first line)
+
+    @property
+    def device(self):
+        return self.plane.eng.device
+
+    def word_lines(self, text: torch.Tensor) -> None:
+        self.plane._emit_word_lines(text, self.chunk)
+
+
+class ListPlane:
+    """``device_reduce = "concat_unique" | "concat"`` (see module docstring)."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.unique = eng.op == "concat_unique"
+        cap = int(eng.params.get("table_capacity") or 1 << 21)
+        self.vocab = II.Vocab(eng.device, cap)
+        self.rvocab = None
+        self.sink = None
+        self._lines = None
+        self._cpu_keys: list = []
+        self.emitter = ListEmitter(self)
+        if eng.device_input != "split":
+            raise ValueError("the list plane maps engine-staged splits (device_input = 'split')")
+
+    # -- global line numbering ------------------------------------------------
+    def line_offsets(self) -> np.ndarray:
+        """Global line index of every split's first line (all splits): this
+        rank counts the newlines of the splits it holds; one all-gather."""
+        if self._lines is None:
+            st = self.eng.splits
+            st.finish_loading()
+            i0, i1 = st.own
+            view = st.buffer.numpy() if st.buffer.device.type == "cpu" else st.buffer.cpu().numpy()
+            mine = [int(np.count_nonzero(view[st.region(i, i + 1)[0]:st.region(i, i + 1)[1]] == 10))
+                    for i in range(i0, i1)]
+            parts = D.all_gather_object((i0, mine), self.eng.group)
+            per = np.zeros(len(st), np.int64)
+            for a, counts in parts:
+                per[a:a + len(counts)] = counts
+            lo = np.zeros(len(st) + 1, np.int64)
+            np.cumsum(per, out=lo[1:])
+            self._lines = lo
+        return self._lines
+
+    # -- map ------------------------------------------------------------------
+    def _emit_word_lines(self, text: torch.Tensor, chunk) -> None:
+        eng = self.eng
+        base, line_base = chunk
+        arena = eng.arena
+        a = text.data_ptr() - arena.data_ptr()
+        if text.is_cuda:
+            II.map_postings_chunk(arena, a, a + text.numel(), line_base, self.vocab, self.doc_bits, self.sink)
+        else:
+            # CPU: the staged chunks are contiguous from the arena start; the
+            # whole span is mapped once after staging (one dense id space)
+            self._cpu_end = max(self._cpu_end, a + text.numel())
+
+    def _map(self, jobs, recs, j0, j1) -> torch.Tensor:
+        eng = self.eng
+        lines = self.line_offsets()
+        ids = eng._split_ids(jobs, j0, j1)
+        rank_l0 = int(lines[ids[0]]) if ids else 0
+        rank_lines = int(lines[ids[-1] + 1]) - rank_l0 if ids else 0
+        self.line_base = rank_l0
+        self.doc_bits = _bits(rank_lines + 1)
+        self.vocab.reset()
+        dmap = eng.dmap
+        if eng.device.type == "cuda":
+            a, b = eng.splits.region(ids[0], ids[-1] + 1) if ids else (0, 0)
+            if self.sink is None or self.sink.cap < (b - a) // 2 + 2:
+                self.sink = II.PostingSink(eng.device, b - a)
+            self.sink.reset()
+        else:
+            self._cpu_end = 0
+        for (ja, jb), data in eng._stage_chunks(jobs, j0, j1):
+            t0, c0 = time.time(), time.process_time()
+            sid = int(jobs[ja][1]["split"] if isinstance(jobs[ja][1], dict) else jobs[ja][1])
+            base = data.data_ptr() - eng.arena.data_ptr()
+            self.emitter.chunk = (base, int(lines[sid]) - rank_l0)
+            keys = [jobs[j][0] for j in range(ja, jb)]
+            for attempt in range(3):
+                try:
+                    dmap(keys if jb - ja > 1 else keys[0], data, self.emitter)
+                    break
+                except Exception:  # noqa: BLE001
+                    for j in range(ja, jb):
+                        recs[j].repetitions += 1
+                        recs[j].status = STATUS.BROKEN if attempt < 2 else STATUS.FAILED
+            _mark_written(recs, ja, jb, t0, time.time(), c0)
+        if eng.device.type == "cuda":
+            return self.sink.finish(self.vocab) if ids else torch.zeros(0, dtype=torch.int64, device=eng.device)
+        if not self._cpu_end:
+            return torch.zeros(0, dtype=torch.int64)
+        return II.map_postings(eng.arena[:self._cpu_end], self.vocab, self.doc_bits)
+
+    # -- sort / group ---------------------------------------------------------
+    def _group(self, keys: torch.Tensor, bits: int) -> torch.Tensor:
+        if self.unique:
+            return II.sort_unique(keys, bits)
+        if keys.is_cuda:
+            _, sk = ops.sort_keys_checked([keys], bits=[bits], return_keys=True, keys_only=True)
+            return sk
+        return torch.sort(keys).values
+
+    def run_iteration(self, prefetch_next, lookahead):
+        eng = self.eng
+        eng.iteration += 1
+        q = eng._seq
+        eng._seq += 1
+        eng._use(q)
+        res = DeviceResult()
+        T = res.timings
+        t_start = time.time()
+        jobs = eng._jobs()
+        j0, j1 = eng._assign(jobs)
+        t0 = time.time()
+        recs = _records(eng, jobs, j0, j1, t0)
+        res.map_jobs = recs
+        with trace.range("mr.list.map"):
+            keys = self._map(jobs, recs, j0, j1)
+        ahead = 0 if not (prefetch_next if prefetch_next is not None else eng.prefetch) else (
+            2 if lookahead is None else min(lookahead, 2))
+        if ahead:
+            eng._prefetch_ahead(jobs, j0, j1, q, ahead)
+        T["map"] = time.time() - t0
+        t1 = time.time()
+        vocab = self.vocab
+        src = self._src()
+        R = eng.nparts
+        W = eng.world
+        shuffle = W > 1 or eng.force_shuffle
+        bits = vocab.id_bits + self.doc_bits
+        dest = None
+        if shuffle:
+            vhi, vlo, vrep = vocab.arrays()
+            part, _ = ops.key_meta(vhi, vlo, vrep, src, nparts=R, want_len=False)
+            dest = (part.to(torch.int64) % W).to(torch.int32)
+            II.add_dest(keys, dest, self.doc_bits, vocab.id_bits)
+            bits += _bits(W)
+        if bits > 63:
+            raise ValueError(f"posting key needs {bits} bits (> 63): raise the vocabulary capacity bits or split "
+                             "the input")
+        with trace.range("mr.list.sort"):
+            ukeys = self._group(keys, bits)
+            wid, wstart, docs = II.split_words(ukeys, self.doc_bits, vocab.id_bits, self.line_base)
+            vhi, vlo, vrep = vocab.arrays()
+            hi, lo, rep = vhi[wid], vlo[wid], vrep[wid]
+        failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
+        if shuffle:
+            with trace.range("mr.list.shuffle"):
+                hi, lo, rep, src, wstart, docs, failed = self._shuffle(hi, lo, rep, src, wid, wstart, docs, dest,
+                                                                      failed)
+        T["shuffle"] = time.time() - t1
+        t2 = time.time()
+        with trace.range("mr.list.order"):
+            out = self._order(hi, lo, rep, src, wstart, docs, R)
+        counts = out["counts_host"]
+        _result_jobs(eng, res, counts, t1)
+        res.device = out
+        res.distinct_keys = int(out["hi"].numel())
+        res.total_value = int(out["docs"].numel())
+        res.failed_maps = failed
+        res._materialize = lambda o=out: _list_host(o, R)
+        T["reduce"] = time.time() - t2
+        T["iteration"] = time.time() - t_start
+        return res
+
+    def _src(self):
+        """The key-byte source of the map's vocabulary: the staged arena."""
+        eng = self.eng
+        return eng.arena if eng.arena is not None else torch.zeros(1, dtype=torch.uint8, device=eng.device)
+
+    def _shuffle(self, hi, lo, rep, text, wid, wstart, docs, dest, failed):
+        """Words + key bytes + posting lists to their owner (p % W): one count
+        exchange, three all_to_all_single; receivers merge the words of every
+        source in a second vocabulary and re-sort (word, line)."""
+        eng = self.eng
+        W = eng.world
+        d = hi.device
+        wdest = dest.to(torch.int64)[wid]
+        ndocs = wstart[1:] - wstart[:-1]
+        _, klen = ops.key_meta(hi, lo, rep, text, want_part=False)
+        koff, kblob = ops.gather_key_bytes(hi, lo, rep, text, lengths=klen)
+        cnt = torch.zeros(W, 3, dtype=torch.int64, device=d)
+        cnt[:, 0].index_add_(0, wdest, torch.ones_like(wdest))
+        cnt[:, 1].index_add_(0, wdest, klen.to(torch.int64))
+        cnt[:, 2].index_add_(0, wdest, ndocs)
+        # per destination: (words, key bytes, postings, this rank's failed maps)
+        xchg = torch.cat([cnt, torch.full((W, 1), failed, dtype=torch.int64, device=d)], 1).contiguous()
+        recv = D.exchange_counts(xchg.view(-1), eng.group).view(W, 4)
+        both = torch.cat([xchg, recv]).cpu().tolist()  # one host sync for every split size
+        send_c, recv_c = both[:W], both[W:]
+        failed_total = sum(r[3] for r in recv_c)
+        recs = torch.stack([hi, lo, klen.to(torch.int64), ndocs], 1)
+        rrecs = D.all_to_all_v(recs, [c[0] for c in send_c], [c[0] for c in recv_c], eng.group)
+        nbytes = sum(c[1] for c in send_c)
+        rblob = D.all_to_all_v(kblob[:nbytes], [c[1] for c in send_c], [c[1] for c in recv_c], eng.group)
+        rdocs = D.all_to_all_v(docs, [c[2] for c in send_c], [c[2] for c in recv_c], eng.group)
+        rhi, rlo = rrecs[:, 0].contiguous(), rrecs[:, 1].contiguous()
+        rlen, rnd = rrecs[:, 2].contiguous(), rrecs[:, 3].contiguous()
+        roff, _ = ops.exclusive_scan(rlen)
+        rrep = (roff << REP_LEN_BITS) | rlen
+        if self.rvocab is None:
+            self.rvocab = II.Vocab(d, int(eng.params.get("table_capacity") or 1 << 21))
+        rv = self.rvocab
+        rv.reset()
+        rid = II.insert_ids(rv, rhi, rlo, rrep, src=rblob)
+        pid = torch.repeat_interleave(rid, rnd, output_size=int(rdocs.numel()))
+        rkeys = (pid << 32) | rdocs.to(torch.int64)
+        sk = self._group(rkeys, rv.id_bits + 32)
+        wid2, wstart2, docs2 = II.split_words(sk, 32, rv.id_bits, 0)
+        vhi, vlo, vrep = rv.arrays()
+        return vhi[wid2], vlo[wid2], vrep[wid2], rblob, wstart2, docs2, failed_total
+
+    def _order(self, hi, lo, rep, src, wstart, docs, R: int) -> dict:
+        """Words in (partition, key) order with their posting lists: key
+        partition = exact FNV-1 mod R, one 3-word radix sort of the words, a
+        segmented gather of the lists; key bytes materialised."""
+        nw = hi.numel()
+        part, klen = ops.key_meta(hi, lo, rep, src, nparts=R)
+        if nw:
+            perm = ops.sort_keys_checked([part.to(torch.int64), hi, lo], bits=[max(8, _bits(R)), 64, 64]).long()
+        else:
+            perm = torch.zeros(0, dtype=torch.int64, device=hi.device)
+        hi, lo, rep, part, klen = hi[perm], lo[perm], rep[perm], part[perm], klen[perm]
+        lens = (wstart[1:] - wstart[:-1])[perm]
+        off, total = ops.exclusive_scan(lens)
+        new_off = torch.cat([off, total])
+        docs = II.seg_gather(perm, wstart, new_off, docs) if nw else docs[:0]
+        koff, kblob = ops.gather_key_bytes(hi, lo, rep, src, lengths=klen)
+        counts = ops.bincount(part, R) if nw else torch.zeros(R, dtype=torch.int64, device=hi.device)
+        return {"hi": hi, "lo": lo, "key_off": koff, "key_blob": kblob, "list_off": new_off, "docs": docs,
+                "counts_host": counts.cpu().tolist()}
+
+
+def _list_host(out: dict, R: int) -> dict[int, dict]:
+    hi = out["hi"].cpu().numpy().view(np.uint64)
+    lo = out["lo"].cpu().numpy().view(np.uint64)
+    koff = out["key_off"].cpu().numpy()
+    kblob = out["key_blob"].cpu().numpy()
+    loff = out["list_off"].cpu().numpy()
+    docs = out["docs"].cpu().numpy()
+    bounds = np.zeros(R + 1, np.int64)
+    np.cumsum(out["counts_host"], out=bounds[1:])
+    parts = {}
+    for p in range(R):
+        a, b = int(bounds[p]), int(bounds[p + 1])
+        if b <= a:
+            continue
+        idx = np.arange(a, b)
+        fix = devmod.fix_long_key_order(hi[a:b], lo[a:b], koff[a:b + 1], kblob)
+        if fix is not None:
+            idx = fix + a
+        kb = kblob.tobytes()
+        keys = [kb[koff[i]:koff[i + 1]] for i in idx]
+        lens = np.array([len(k) for k in keys], np.int64)
+        k_off = np.zeros(len(keys) + 1, np.int64)
+        np.cumsum(lens, out=k_off[1:])
+        l_lens = loff[idx + 1] - loff[idx]
+        l_off = np.zeros(len(idx) + 1, np.int64)
+        np.cumsum(l_lens, out=l_off[1:])
+        vals = np.concatenate([docs[loff[i]:loff[i + 1]] for i in idx]) if len(idx) else docs[:0]
+        parts[p] = {"key_off": k_off, "key_blob": np.frombuffer(b"".join(keys), np.uint8), "list_off": l_off,
+                    "list_val": vals, "val": l_lens}
+    return parts
+
+
+# ---------------------------------------------------------------------------
+class RecordStore:
+    """Input blocks of fixed-width records (uint8 [n, width] tensors, device
+    or host) — the record plane's analogue of SplitStore (a map job's value
+    names its block: ``{"block": i}``)."""
+
+    def __init__(self, blocks: list[torch.Tensor]):
+        self.blocks = list(blocks)
+
+    def __len__(self) -> int:
+        return len(self.blocks)
+
+    def size(self, i: int) -> int:
+        b = self.blocks[i]
+        return int(b.numel())
+
+    def block(self, i: int) -> torch.Tensor:
+        return self.blocks[i]
+
+
+class RecordEmitter:
+    """``emit`` of a record-plane map: ``emit.records(rec)`` emits every row
+    of a uint8 [n, 100] tensor (key = its first 10 bytes)."""
+
+    def __init__(self, plane):
+        self.plane = plane
+
+    @property
+    def device(self):
+        return self.plane.eng.device
+
+    def records(self, rec: torch.Tensor, key_bytes: int = TS.KEY) -> None:
+        if rec.dim() != 2 or rec.shape[1] != TS.REC or key_bytes != TS.KEY:
+            raise ValueError(f"the record plane moves {TS.REC}-byte rows with {TS.KEY}-byte keys "
+                             f"(got {tuple(rec.shape)}, key {key_bytes})")
+        if rec.device != self.plane.eng.device:
+            rec = rec.to(self.plane.eng.device, non_blocking=True)
+        self.plane._out.append(rec)
+
+
+class RecordPlane:
+    """``device_reduce = "identity"`` (see module docstring)."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        spec = modules.field(eng.partmod, "device_partition")
+        if not spec or spec[0] != "range":
+            raise ValueError("the record plane needs device_partition = ('range', R, splitters or None)")
+        self.splitters = None if len(spec) < 3 or spec[2] is None else torch.as_tensor(spec[2], dtype=torch.int64)
+        self.oversample = int(eng.params.get("oversample") or 1024)
+        self.seed = int(eng.params.get("sample_seed") or 0x7E5A)
+        self.emitter = RecordEmitter(self)
+        self._out: list = []
+
+    def _map(self, jobs, recs, j0, j1) -> torch.Tensor:
+        eng = self.eng
+        self._out = []
+        for j in range(j0, j1):
+            t0, c0 = time.time(), time.process_time()
+            v = jobs[j][1]
+            data = None
+            if eng.splits is not None:
+                data = eng.splits.block(int(v["block"] if isinstance(v, dict) else v))
+            for attempt in range(3):
+                n0 = len(self._out)
+                try:
+                    eng.dmap(jobs[j][0], data if data is not None else v, self.emitter)
+                    break
+                except Exception:  # noqa: BLE001
+                    del self._out[n0:]
+                    recs[j].repetitions += 1
+                    recs[j].status = STATUS.BROKEN if attempt < 2 else STATUS.FAILED
+            _mark_written(recs, j, j + 1, t0, time.time(), c0)
+        if not self._out:
+            return torch.zeros((0, TS.REC), dtype=torch.uint8, device=eng.device)
+        return self._out[0] if len(self._out) == 1 else torch.cat(self._out)
+
+    def _sample_splitters(self, hi: torch.Tensor, R: int) -> torch.Tensor:
+        """R-1 unsigned splitters (int64 bit patterns) from a sample of every
+        rank's keys (TeraSort's sampled total-order partitioner)."""
+        eng = self.eng
+        k = min(self.oversample * R, max(1, hi.numel()))
+        g = torch.Generator().manual_seed(self.seed * 7919 + eng.rank)
+        idx = torch.randint(0, max(1, hi.numel()), (k,), generator=g).to(hi.device)
+        samp = hi[idx] if hi.numel() else torch.zeros(k, dtype=torch.int64, device=hi.device)
+        allv = D.all_gather_tensor(samp, eng.group) if D.initialized() else samp
+        sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=allv.device)
+        srt = torch.sort(allv ^ sign).values ^ sign  # unsigned order of the bit patterns
+        m = srt.numel()
+        pick = torch.tensor([(m * j) // R for j in range(1, R)], dtype=torch.int64, device=srt.device)
+        return srt[pick].contiguous()
+
+    def _sort_perm(self, hi, lo):
+        perm = TS.sort_perm(hi, lo)
+        if hi.is_cuda and ops.sort_error(hi.device):
+            perm = ops.sort_keys_checked([hi, lo], bits=[64, 16])
+        return perm
+
+    def run_iteration(self, prefetch_next, lookahead):
+        eng = self.eng
+        eng.iteration += 1
+        eng._seq += 1
+        res = DeviceResult()
+        T = res.timings
+        t_start = time.time()
+        jobs = eng._jobs()
+        j0, j1 = eng._assign(jobs)
+        t0 = time.time()
+        recs = _records(eng, jobs, j0, j1, t0)
+        res.map_jobs = recs
+        with trace.range("mr.rec.map"):
+            rec = self._map(jobs, recs, j0, j1)
+        T["map"] = time.time() - t0
+        t1 = time.time()
+        R, W = eng.nparts, eng.world
+        failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
+        hi = None
+        sp = self.splitters
+        if R > 1 and sp is None:
+            hi, _ = TS.keys(rec)
+            sp = self._sample_splitters(hi, R)
+        elif sp is not None:
+            sp = sp.to(eng.device)
+        if W > 1 or eng.force_shuffle:
+            with trace.range("mr.rec.shuffle"):
+                if hi is None:
+                    hi, _ = TS.keys(rec)
+                part = TS.dest_of(hi, sp) if R > 1 else torch.zeros(hi.numel(), dtype=torch.int32, device=hi.device)
+                dest = (part.to(torch.int64) % W).to(torch.int32)
+                perm = ops.sort_keys_checked([dest.to(torch.int64)], bits=[max(8, _bits(W))])
+                packed = TS.gather(rec, perm)
+                counts = ops.bincount(dest, W)
+                # per destination: (rows, this rank's failed maps)
+                xchg = torch.stack([counts, torch.full((W,), failed, dtype=torch.int64, device=counts.device)],
+                                   1).contiguous()
+                recv = D.exchange_counts(xchg.view(-1), eng.group).view(W, 2)
+                both = torch.cat([xchg, recv]).cpu().tolist()
+                failed = sum(r[1] for r in both[W:])
+                rec = D.all_to_all_v(packed, [r[0] for r in both[:W]], [r[0] for r in both[W:]], eng.group)
+                del packed
+        T["shuffle"] = time.time() - t1
+        t2 = time.time()
+        with trace.range("mr.rec.sort"):
+            hi, lo = TS.keys(rec)
+            perm = self._sort_perm(hi, lo)
+            out = TS.gather(rec, perm)
+            if R > 1:
+                shi = hi[perm.long()]
+                pcount = ops.bincount(TS.dest_of(shi, sp), R)
+            else:
+                pcount = torch.tensor([out.shape[0]], dtype=torch.int64)
+        counts = pcount.cpu().tolist()
+        _result_jobs(eng, res, counts, t1)
+        res.device = {"records": out, "counts_host": counts, "splitters": sp}
+        res.distinct_keys = int(out.shape[0])
+        res.total_value = int(out.shape[0])
+        res.failed_maps = failed
+        res._materialize = lambda o=res.device: _record_host(o, R)
+        T["reduce"] = time.time() - t2
+        T["iteration"] = time.time() - t_start
+        return res
+
+
+def _record_host(out: dict, R: int) -> dict[int, dict]:
+    rec = out["records"].cpu().numpy()
+    bounds = np.zeros(R + 1, np.int64)
+    np.cumsum(out["counts_host"], out=bounds[1:])
+    return {p: {"records": rec[int(bounds[p]):int(bounds[p + 1])], "key_bytes": TS.KEY}
+            for p in range(R) if bounds[p + 1] > bounds[p]}

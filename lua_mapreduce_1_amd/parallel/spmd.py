@@ -279,7 +279,16 @@ class SPMDEngine:
         # one map table per input slot: with pipelining, iteration i+1 maps into
         # tables[1-s] while iteration i's shuffle/reduce still reads tables[s]
         self._table_capacity = table_capacity
-        self.tables: list = [ops.HashTable(table_capacity, device=self.device, op=self.op), None]
+        # list- and record-valued reduces run on their own data planes
+        # (parallel/planes.py); the fold plane below is the hash table
+        from . import planes
+        self.plane = None
+        self.tables: list = [None, None]
+        if self.op in planes.LIST_OPS + planes.RECORD_OPS:
+            self.plane_kind = "list" if self.op in planes.LIST_OPS else "records"
+        else:
+            self.plane_kind = "fold"
+            self.tables[0] = ops.HashTable(table_capacity, device=self.device, op=self.op)
         self.red_table: ops.HashTable | None = None
         # input arenas, used round-robin by iteration sequence number q: while
         # iteration q maps/reduces arenas[q % 3], the copies of q+1 and q+2
@@ -302,6 +311,8 @@ class SPMDEngine:
         self.force_shuffle = bool(self.params.get("force_shuffle", TUNABLES.force_shuffle))
         if self.force_shuffle and self.world == 1 and not D.initialized():
             raise RuntimeError("force_shuffle at world size 1 needs an initialised process group")
+        if self.plane_kind != "fold":
+            self.plane = planes.make_plane(self)
         # iteration pipelining (needs prefetch): the next iteration's map is
         # queued on the other slot's stream as soon as this map has finished,
         # and runs while this iteration shuffles, reduces and downloads
@@ -366,6 +377,8 @@ class SPMDEngine:
         if self.device_input == "file":
             import os
             return os.path.getsize(value) + 1
+        if self.device_input == "records" and self.splits is not None:
+            return self.splits.size(int(value["block"] if isinstance(value, dict) else value))
         return 1
 
     def _assign(self, jobs: list[tuple]) -> tuple[int, int]:
@@ -805,6 +818,8 @@ class SPMDEngine:
 
     def run_iteration(self, prefetch_next: bool | None = None, lookahead: int | None = None) -> IterationResult:
         with trace.range("mr.iteration"):
+            if self.plane is not None:
+                return self.plane.run_iteration(prefetch_next, lookahead)
             return self._run_iteration(prefetch_next, lookahead)
 
     def _new_records(self, jobs, j0: int, j1: int) -> list[JobRecord]:
@@ -1089,10 +1104,17 @@ class SPMDEngine:
             self._log("# Iteration %d\n" % (self.iteration + 1))
             res = self.run_iteration()
             self._log(self.stats_block(res))
-            gathered = self.gather_results(res)
             reply = None
-            if self.rank == 0 and self.finalmod is not None:
-                reply = modules.field(self.finalmod, "finalfn")(self.pairs(gathered))
+            dfin = modules.field(self.finalmod, "device_finalfn") if self.finalmod is not None else None
+            if dfin is not None:
+                # SPMD extension: every rank sees its own (device-resident)
+                # results, e.g. a collective validation of a 10 GB sort that
+                # must not be gathered to one host; rank 0's reply counts
+                reply = dfin(res, self)
+            else:
+                gathered = self.gather_results(res)
+                if self.rank == 0 and self.finalmod is not None:
+                    reply = modules.field(self.finalmod, "finalfn")(self.pairs(gathered))
             if self.world > 1:
                 reply = D.broadcast_object(reply, 0, self.group, self.device if self.device.type == "cuda" else None)
             if reply != "loop":

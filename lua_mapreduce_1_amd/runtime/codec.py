@@ -34,7 +34,10 @@ def _default(o):
 
 
 def encode_records(records: Iterable[tuple]) -> bytes:
-    pk = msgpack.Packer(use_bin_type=True, default=_default)
+    # keys from byte data are str with surrogate escapes (non-UTF-8 bytes,
+    # key_str): packed as such and decoded with the same handler, so any
+    # byte string round-trips (the reference's keys are arbitrary Lua strings)
+    pk = msgpack.Packer(use_bin_type=True, default=_default, unicode_errors="surrogateescape")
     out = [MAGIC_REC]
     for k, vals in records:
         out.append(pk.pack([k, list(vals)]))
@@ -89,8 +92,24 @@ def key_str(b: bytes) -> str:
 
 
 def iter_columnar(cols: dict) -> Iterator[tuple]:
+    """(key, values) pairs of a device result partition: one folded value per
+    key (``val``), a value list per key (``list_off`` / ``list_val``, the list
+    plane), or fixed-width records (``records`` with ``key_bytes``: key = the
+    record's key bytes, value = the rest of the record as bytes)."""
+    if "records" in cols:
+        rec = cols["records"]
+        kb = int(cols["key_bytes"])
+        for i in range(int(rec.shape[0])):
+            row = rec[i].tobytes()
+            yield key_str(row[:kb]), [row[kb:]]
+        return
     off = cols["key_off"]
     blob = cols["key_blob"].tobytes()
+    if "list_off" in cols:
+        lo, lv = cols["list_off"], cols["list_val"]
+        for i in range(int(lo.size) - 1):
+            yield key_str(blob[off[i]:off[i + 1]]), lv[lo[i]:lo[i + 1]].tolist()
+        return
     val = cols["val"]
     for i in range(int(val.size)):
         yield key_str(blob[off[i]:off[i + 1]]), [int(val[i])]

@@ -55,9 +55,17 @@ def reset_cache() -> None:
     modules.reset()
 
 
-def _use_device(task_tbl: dict | None, mod_map) -> bool:
+FOLD_OPS = ("sum", "min", "max", "count")
+
+
+def _use_device(task_tbl: dict | None, mod_map, mod_red=None) -> bool:
+    """The worker's device map plane folds int64 values in an HBM table; a
+    list- or record-valued reduce (device_reduce "concat*" / "identity", the
+    SPMD engine's planes) runs the host mapfn here."""
     want = (task_tbl or {}).get("device", "auto")
     if want in (False, "never", "host"):
+        return False
+    if mod_red is not None and modules.field(mod_red, "device_reduce", "sum") not in FOLD_OPS:
         return False
     return modules.field(mod_map, "device_mapfn") is not None
 
@@ -139,7 +147,7 @@ class job:  # noqa: N801
         if cmod is not None:
             modules.init_once(cmod, self.init_args)
         combiner = modules.field(cmod, "combinerfn") if cmod is not None else None
-        if _use_device(self.task_tbl, self.module):
+        if _use_device(self.task_tbl, self.module, cmod):
             return lambda: self._run_device_map(pmod, cmod)
         g = modules.field(self.module, "mapfn")
         map_key, map_value = self.get_pair()
@@ -258,7 +266,7 @@ class job:  # noqa: N801
             rstore, rbuilder = result_store(self.cnn, self.storage, self.path)
             rstore.remove_file(res_file)
             blobs = None
-            if dev_op is not None and filenames:
+            if dev_op in FOLD_OPS and filenames:
                 if self.storage == "gridfs":  # all inputs in one round trip per shard
                     blobs = [b or b"" for b in self.cnn.gridfs().get_many(filenames)]
                 else:
@@ -309,7 +317,7 @@ def _device_reduce(blobs: list[bytes], op: str) -> bytes:
     rep = torch.from_numpy(((offs << np.uint64(24)) | lens).view(np.int64)).to(d)
     src = torch.from_numpy(np.concatenate([c["key_blob"] for c in cols])).to(d)
     tab = dev.ops.HashTable(max(1024, 2 * n), device=d, op=op)
-    tab.insert(hi, lo, val, rep)
+    tab.insert(hi, lo, val, rep, src=src)  # long keys verified against their bytes
     uhi, ulo, uval, urep = tab.compact()
     out = dev.finalize(uhi, ulo, uval, urep, src, 1, None, part=torch.zeros(uhi.numel(), dtype=torch.int32,
                                                                               device=d), need_keys=True)

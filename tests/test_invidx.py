@@ -1,21 +1,26 @@
-"""Inverted-index build (BASELINE config "inverted-index build on the same corpus
-shape"): word -> sorted distinct line ids, diffed against a naive oracle on
-CPU (1 rank), over gloo (2 and 3 ranks, the RCCL shuffle path with host
-tensors) and on the GPU (HIP kernels; 1 rank and several ranks sharing it)."""
+"""Inverted index as a MapReduce job (examples/InvertedIndex; BASELINE config
+"inverted-index build on the same corpus shape"): word -> sorted distinct line
+numbers through the framework's own roles — the SPMD engine's list plane
+(parallel/planes.py) on CPU (1 rank), over gloo (3 ranks), on the GPU (HIP
+kernels; 1 rank, several ranks sharing it, the forced RCCL shuffle) and the
+server/worker roles (host mapfn/reducefn) — each diffed against a naive
+oracle."""
+import contextlib
+import io
 import os
 import socket
+import threading
 
 import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
 
-from lua_mapreduce_1_amd.parallel.invidx import InvertedIndexBuilder, naive_index
-from lua_mapreduce_1_amd.parallel.spmd import SplitStore
-from lua_mapreduce_1_amd.utils.corpus import europarl_like, tricky_text
+M = "lua_mapreduce_1_amd.examples.InvertedIndex"
 
 
 def _splits(seed=9):
+    from lua_mapreduce_1_amd.utils.corpus import europarl_like, tricky_text
     s = europarl_like(seed=seed, lines=3000, words=60000, vocab_size=3000, split_lines=500)
     s.append(tricky_text(np.random.default_rng(seed), 150_000))
     s.append(b"no trailing newline here")
@@ -24,12 +29,64 @@ def _splits(seed=9):
     return s
 
 
+def _engine(splits, device, nred=7, **extra):
+    from lua_mapreduce_1_amd import spmd
+    from lua_mapreduce_1_amd.parallel.spmd import SplitStore
+    params = dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                  init_args={"nsplits": len(splits), "num_reducers": nred}, **extra)
+    return spmd(params, device=device, split_store=SplitStore(splits, pin=torch.device(device).type == "cuda"))
+
+
+def _result():
+    import importlib
+    return importlib.import_module(M).RESULT
+
+
+def _naive(splits):
+    import importlib
+    return importlib.import_module(M).naive_index(splits)
+
+
 def test_cpu_single_rank_matches_oracle():
     splits = _splits()
-    sh = InvertedIndexBuilder(SplitStore(splits, pin=False), device="cpu").build()
-    exp = naive_index(splits)
-    assert sh.to_host() == exp
-    assert sh.num_postings == sum(len(v) for v in exp.values())
+    eng = _engine(splits, "cpu")
+    res = eng.run()
+    exp = _naive(splits)
+    assert _result() == exp
+    assert res.total_value == sum(len(v) for v in exp.values())
+    # result files named like every job's, keys in order inside each
+    for name, cols in eng.gather_results(res):
+        assert name.startswith("result.P")
+        from lua_mapreduce_1_amd.runtime import codec
+        keys = [k.encode("utf-8", "surrogateescape") for k, _ in codec.iter_columnar(cols)]
+        assert keys == sorted(keys)
+
+
+def test_server_worker_host_plane_matches_oracle(tmp_path):
+    """The same module through server + worker (host mapfn reads its split
+    file, reducefn = sorted distinct lines) — the reference deployment."""
+    import lua_mapreduce_1_amd as mr
+    from lua_mapreduce_1_amd.runtime import coordinator
+    splits = _splits()
+    files = []
+    for i, s in enumerate(splits):
+        p = tmp_path / f"s{i:03d}.txt"
+        p.write_bytes(s)
+        files.append(str(p))
+    cs = coordinator.start_local()
+    params = dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M, combinerfn=M, storage="gridfs",
+                  device="auto", init_args={"files": files, "num_reducers": 5})
+    s = mr.server.new(cs, "invidx_sw")
+    s.poll_sleep = 0.02
+    s.quiet = True
+    s.configure(params)
+    w = mr.worker.new(cs, "invidx_sw")
+    w.configure(verbose=False, poll_sleep=0.02, max_iter=2)
+    t = threading.Thread(target=w.execute, daemon=True)
+    t.start()
+    with contextlib.redirect_stdout(io.StringIO()):
+        s.loop()
+    assert _result() == _naive(splits)
 
 
 def _free_port():
@@ -40,79 +97,88 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, on_gpu=False):
+def _worker(rank, world, port, q, on_gpu=False, backend="gloo", force_shuffle=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
+    import datetime
     import torch.distributed as dist
     from lua_mapreduce_1_amd.parallel import dist as D
-    _, _, device = D.init_from_env(backend="gloo", use_gpu=on_gpu)
+    if force_shuffle:
+        dist.init_process_group(backend, rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}",
+                                timeout=datetime.timedelta(seconds=120),
+                                **({"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}))
+        device = torch.device("cuda", 0) if on_gpu else torch.device("cpu")
+    else:
+        _, _, device = D.init_from_env(backend=backend, use_gpu=on_gpu)
     splits = _splits()
-    b = InvertedIndexBuilder(SplitStore(splits, pin=on_gpu), device=device, num_reducers=7,
-                             capacity=1 << 16, recv_capacity=1 << 16)
-    sh = b.build()
-    own_ok = all(p % world == rank for p in sh.part.cpu().tolist())
-    shards = D.gather_objects(sh.to_host(), 0)
-    if rank == 0:
-        merged = {}
-        dup = False
-        for d in shards:
-            for k, v in d.items():
-                dup |= k in merged
-                merged[k] = v
-        q.put((merged == naive_index(splits), dup))
+    extra = {"table_capacity": 1 << 16}
+    if force_shuffle:
+        extra["force_shuffle"] = True
+    eng = _engine(splits, device, **extra)
+    res = eng.run()
+    own_ok = all(p % world == rank for p in res.result_names)
     oks = D.gather_objects(own_ok, 0)
     if rank == 0:
-        q.put(all(oks))
+        q.put((_result() == _naive(splits), all(oks)))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(world, on_gpu=False):
+def _run(world, **kw):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, on_gpu)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q), kwargs=kw) for r in range(world)]
     for p in procs:
         p.start()
-    same, dup = q.get(timeout=300)
-    owned = q.get(timeout=60)
+    same, owned = q.get(timeout=300)
     for p in procs:
         p.join(120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    assert same and not dup and owned
+    assert same and owned
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [3])
 def test_gloo_multi_rank_matches_oracle(world):
     _run(world)
+
+
+def test_gloo_forced_shuffle_one_rank():
+    _run(1, force_shuffle=True)
 
 
 @pytest.mark.gpu
 def test_gpu_single_rank_matches_oracle(gpu):
     splits = _splits()
-    b = InvertedIndexBuilder(SplitStore(splits, pin=True), device=gpu, capacity=1 << 16)
-    sh = b.build()
-    assert sh.docs.is_cuda
-    assert sh.to_host() == naive_index(splits)
-    # second build reuses the staged text and the (reset) table
-    assert b.build(stage=False).to_host() == naive_index(splits)
+    eng = _engine(splits, gpu, table_capacity=1 << 16)
+    res = eng.run()
+    assert res.device["docs"].is_cuda
+    assert _result() == _naive(splits)
+    # a second iteration on the same engine (tables reset, staging reused)
+    eng.finished = False
+    res = eng.run_iteration()
+    got = {k: v for _n, c in eng.gather_results(res) for k, v in __import__(
+        "lua_mapreduce_1_amd.runtime.codec", fromlist=["x"]).iter_columnar(c)}
+    assert got == _naive(splits)
 
 
 @pytest.mark.gpu
-def test_gpu_staged_pieces_and_prefetch(gpu):
-    """Split-aligned pieces mapped as their copies land (line ids continue
-    across pieces), and builds whose copies were prefetched into the other
-    arena during the previous build's sort."""
-    import torch
+def test_gpu_staged_chunks_and_prefetch(gpu):
+    """Small copy chunks mapped as their copies land (line numbers continue
+    across chunks), and iterations whose copies were prefetched during the
+    previous iteration's sort."""
+    from lua_mapreduce_1_amd.runtime import codec
     splits = _splits()
-    b = InvertedIndexBuilder(SplitStore(splits, pin=True), device=gpu, capacity=1 << 16)
-    b.pieces = b._plan_pieces(first_mb=0.01, big_mb=0.03)
-    b.events = [[torch.cuda.Event() for _ in b.pieces] for _ in range(2)]
-    assert len(b.pieces) >= 3
-    want = naive_index(splits)
+    eng = _engine(splits, gpu, table_capacity=1 << 16)
+    eng.chunk_bytes = [8 << 10, 16 << 10, 32 << 10]
+    eng.tail_bytes = [8 << 10]
+    eng.prefetch = True
+    want = _naive(splits)
     for i in range(4):
-        assert b.build(prefetch_next=i < 3).to_host() == want
-    assert b._prefetched is None
+        res = eng.run_iteration(prefetch_next=i < 3, lookahead=3 - i)
+        got = {k: v for _n, c in eng.gather_results(res) for k, v in codec.iter_columnar(c)}
+        assert got == want
+    assert not eng._inflight
 
 
 @pytest.mark.gpu
@@ -123,8 +189,8 @@ def test_gpu_long_lines_and_many_lines(gpu):
     long_line = b" ".join(words[i % 500] for i in rng.integers(0, 500, 30000)) + b"\n"
     many = b"".join(b"%s %s\n" % (words[i % 500], words[(i * 7) % 500]) for i in range(40000))
     splits = [long_line, many, long_line[:70000] + b"\n" + many[:50000]]
-    sh = InvertedIndexBuilder(SplitStore(splits, pin=True), device=gpu, capacity=1 << 14).build()
-    assert sh.to_host() == naive_index(splits)
+    _engine(splits, gpu, table_capacity=1 << 14).run()
+    assert _result() == _naive(splits)
 
 
 @pytest.mark.gpu
@@ -136,13 +202,20 @@ def test_gpu_dense_one_letter_tokens(gpu):
     lines = [b" ".join(letters[i] for i in rng.integers(0, len(letters), int(n))) + b"\n"
              for n in rng.integers(1, 3000, 120)]
     splits = [b"".join(lines[:60]), b"".join(lines[60:])]
-    sh = InvertedIndexBuilder(SplitStore(splits, pin=True), device=gpu, capacity=1 << 12).build()
-    assert sh.to_host() == naive_index(splits)
+    _engine(splits, gpu, table_capacity=1 << 12).run()
+    assert _result() == _naive(splits)
 
 
 @pytest.mark.gpu
 def test_gpu_multi_rank_on_one_gpu(gpu):
     _run(2, on_gpu=True)
+
+
+@pytest.mark.gpu
+def test_gpu_forced_shuffle_rccl(gpu):
+    """The list plane's three all_to_all_single on the RCCL backend (one-rank
+    nccl group, W>1 path forced)."""
+    _run(1, on_gpu=True, backend="nccl", force_shuffle=True)
 
 
 @pytest.mark.gpu
@@ -158,3 +231,19 @@ def test_gpu_sort_unique_matches_torch(gpu, n):
     assert torch.equal(got, torch.unique(keys))
     _, sk = sort_keys([keys.to(gpu)], bits=[40], return_keys=True, keys_only=True)
     assert torch.equal(sk.cpu(), torch.sort(keys).values)
+
+
+@pytest.mark.gpu
+def test_gpu_seg_gather_matches_cpu(gpu):
+    from lua_mapreduce_1_amd.ops import invidx as II
+    g = torch.Generator().manual_seed(3)
+    lens = torch.randint(0, 50, (2000,), generator=g)
+    lens[7] = 100_000  # one very frequent word
+    starts = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(lens, 0)])
+    docs = torch.randint(0, 1 << 30, (int(starts[-1]),), generator=g, dtype=torch.int32)
+    perm = torch.randperm(2000, generator=g)
+    nl = lens[perm]
+    noff = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(nl, 0)])
+    want = II.seg_gather(perm, starts, noff, docs)
+    got = II.seg_gather(perm.to(gpu), starts.to(gpu), noff.to(gpu), docs.to(gpu)).cpu()
+    assert torch.equal(got, want)

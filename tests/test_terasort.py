@@ -1,8 +1,10 @@
-"""TeraSort-style sort (BASELINE config "TeraSort-style 10 GB key/value sort"):
-generator, key extraction, splitter partitioning, all-to-all of 100-byte rows
-and the local radix sort — checked for global order and an order-independent
-record checksum on CPU, over gloo (2 and 4 ranks), and on the GPU (HIP kernels
-compared with the NumPy specification)."""
+"""TeraSort as a MapReduce job (examples/TeraSort; BASELINE config
+"TeraSort-style 10 GB key/value sort"): TeraGen map jobs, sampled range
+partitioner, all-to-all of 100-byte rows and the identity reduce's radix sort
+through the SPMD engine's record plane — checked for global order and an
+order-independent record checksum on CPU, over gloo (2 and 4 ranks, forced
+shuffle), on the GPU (HIP kernels vs the NumPy specification, forced RCCL
+shuffle) and through server/worker."""
 import os
 import socket
 
@@ -12,7 +14,6 @@ import torch
 import torch.multiprocessing as mp
 
 from lua_mapreduce_1_amd.ops import terasort as TS
-from lua_mapreduce_1_amd.parallel.terasort import TeraSort
 
 
 def test_generator_layout_and_keys():
@@ -27,15 +28,63 @@ def test_generator_layout_and_keys():
     assert torch.equal(TS.generate(20, 1010, 99), r[10:30])
 
 
-def test_cpu_single_rank_sort():
-    t = TeraSort(30000, device="cpu")
-    rec = t.generate()
-    cs = t.checksum_global(rec)
-    out = t.sort(rec)
-    v = t.validate(out, cs)
-    assert v["ok"], v
-    keys = [bytes(x[:10]) for x in out.numpy()]
-    assert keys == sorted(keys)
+M = "lua_mapreduce_1_amd.examples.TeraSort"
+
+
+def _engine(records, device, blocks=3, partitions=0, **extra):
+    from lua_mapreduce_1_amd import spmd
+    return spmd(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                     init_args={"records": records, "blocks": blocks, "partitions": partitions, "validate": True},
+                     **extra), device=device)
+
+
+def _validation():
+    import importlib
+    return importlib.import_module(M).VALIDATION
+
+
+@pytest.mark.parametrize("partitions", [1, 4])
+def test_cpu_single_rank_sort(partitions):
+    """TeraGen map jobs -> sampled range partitions -> identity reduce; the
+    gathered result files are globally sorted in file-name order."""
+    from lua_mapreduce_1_amd.runtime import codec
+    eng = _engine(30000, "cpu", partitions=partitions)
+    res = eng.run()
+    assert _validation()["ok"], _validation()
+    keys = [k.encode("utf-8", "surrogateescape") for _n, c in eng.gather_results(res)
+            for k, _v in codec.iter_columnar(c)]
+    assert len(keys) == 30000 and keys == sorted(keys)
+    assert len(res.result_names) == partitions
+
+
+def test_record_store_input_and_server_worker_host_plane():
+    """A caller-staged RecordStore input; and the same module through the
+    server/worker roles (host TeraGen map, uniform static splitters)."""
+    import contextlib
+    import io
+    import threading
+    import lua_mapreduce_1_amd as mr
+    from lua_mapreduce_1_amd import spmd
+    from lua_mapreduce_1_amd.parallel.planes import RecordStore
+    from lua_mapreduce_1_amd.runtime import coordinator
+    blocks = [TS.generate(4000, 0, 0x7E5A), TS.generate(3000, 4000, 0x7E5A)]
+    eng = spmd(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                    init_args={"records": 7000, "blocks": 2, "partitions": 3, "validate": True}),
+               device="cpu", split_store=RecordStore(blocks))
+    eng.run()
+    assert _validation()["ok"]
+    cs = coordinator.start_local()
+    s = mr.server.new(cs, "terasort_sw")
+    s.poll_sleep = 0.02
+    s.quiet = True
+    s.configure(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M, storage="gridfs", device="auto",
+                     init_args={"records": 3000, "blocks": 3, "partitions": 2}))
+    w = mr.worker.new(cs, "terasort_sw")
+    w.configure(verbose=False, poll_sleep=0.02, max_iter=2)
+    threading.Thread(target=w.execute, daemon=True).start()
+    with contextlib.redirect_stdout(io.StringIO()):
+        s.loop()
+    assert _validation() == {"records": 3000, "ok": True}
 
 
 def _free_port():
@@ -46,28 +95,35 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, on_gpu=False):
+def _worker(rank, world, port, q, on_gpu=False, backend="gloo", force_shuffle=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
+    import datetime
     import torch.distributed as dist
     from lua_mapreduce_1_amd.parallel import dist as D
-    _, _, device = D.init_from_env(backend="gloo", use_gpu=on_gpu)
-    t = TeraSort(40001, device=device, oversample=256)
-    rec = t.generate()
-    cs = t.checksum_global(rec)
-    out = t.sort(rec)
-    v = t.validate(out, cs)
+    if force_shuffle:
+        dist.init_process_group(backend, rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}",
+                                timeout=datetime.timedelta(seconds=120),
+                                **({"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}))
+        device = torch.device("cuda", 0) if on_gpu else torch.device("cpu")
+    else:
+        _, _, device = D.init_from_env(backend=backend, use_gpu=on_gpu)
+    extra = {"oversample": 256}
+    if force_shuffle:
+        extra["force_shuffle"] = True
+    eng = _engine(40001, device, blocks=max(world, 2), **extra)
+    eng.run()
     if rank == 0:
-        q.put(v)
+        q.put(_validation())
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(world, on_gpu=False):
+def _run(world, **kw):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, on_gpu)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q), kwargs=kw) for r in range(world)]
     for p in procs:
         p.start()
     v = q.get(timeout=300)
@@ -80,6 +136,10 @@ def _run(world, on_gpu=False):
 @pytest.mark.parametrize("world", [2, 4])
 def test_gloo_multi_rank_sort(world):
     _run(world)
+
+
+def test_gloo_forced_shuffle_one_rank():
+    _run(1, force_shuffle=True)
 
 
 @pytest.mark.gpu
@@ -98,13 +158,13 @@ def test_gpu_kernels_match_numpy(gpu):
 
 
 @pytest.mark.gpu
-def test_gpu_single_rank_sort(gpu):
-    t = TeraSort(300_007, device=gpu)
-    rec = t.generate()
-    cs = t.checksum_global(rec)
-    out = t.sort(rec)
-    v = t.validate(out, cs)
-    assert v["ok"], v
+@pytest.mark.parametrize("partitions", [1, 3])
+def test_gpu_single_rank_sort(gpu, partitions):
+    eng = _engine(300_007, gpu, blocks=2, partitions=partitions)
+    res = eng.run()
+    assert _validation()["ok"], _validation()
+    out = res.device["records"]
+    assert out.is_cuda
     k = out[:2000, :10].cpu().numpy()
     assert [bytes(x) for x in k] == sorted(bytes(x) for x in k)
 
@@ -112,6 +172,12 @@ def test_gpu_single_rank_sort(gpu):
 @pytest.mark.gpu
 def test_gpu_multi_rank_on_one_gpu(gpu):
     _run(2, on_gpu=True)
+
+
+@pytest.mark.gpu
+def test_gpu_forced_shuffle_rccl(gpu):
+    """The record plane's all_to_all_single of 100-byte rows on RCCL."""
+    _run(1, on_gpu=True, backend="nccl", force_shuffle=True)
 
 
 @pytest.mark.gpu

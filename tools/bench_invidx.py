@@ -1,9 +1,12 @@
 #!/usr/bin/env python
-"""Inverted-index build benchmark (BASELINE.json config "inverted-index build
-on the same corpus shape"): the 197-split Europarl-shaped corpus -> word ->
-sorted distinct line ids, resident in HBM.  One step = H2D of the rank's
-splits + map (tokenize, word ids, posting keys) + sort/unique + (N>1) RCCL
-shuffle + merge + key bytes.  Prints one JSON line (tokens/s, postings/s).
+"""Inverted-index benchmark (BASELINE.json config "inverted-index build on the
+same corpus shape") through the MapReduce API: the examples/InvertedIndex
+module (taskfn / device_mapfn / FNV partitionfn / concat_unique reducefn) on
+the SPMD engine's list plane.  Corpus = bench.py's Europarl-shaped 197 splits
+(each rank reads and pins only its own).  One step = one iteration: H2D of the
+rank's splits + map (tokenizer, vocabulary, posting keys) + sort/unique +
+(N>1) RCCL shuffle + merge + (partition, key) order + key bytes; the index
+stays in HBM.  Prints one JSON line (tokens/s, postings/s).
 
   python tools/bench_invidx.py [--steps K] [--warmup W] [--validate]
   (N>1: python -m torch.distributed.run --nproc-per-node N tools/bench_invidx.py)
@@ -16,16 +19,19 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from bench import load_corpus  # noqa: E402
+from bench import corpus_dir, ensure_corpus  # noqa: E402
+from lua_mapreduce_1_amd import spmd  # noqa: E402
 from lua_mapreduce_1_amd.parallel import dist as D  # noqa: E402
-from lua_mapreduce_1_amd.parallel.invidx import InvertedIndexBuilder, naive_index  # noqa: E402
 from lua_mapreduce_1_amd.parallel.spmd import SplitStore  # noqa: E402
 from lua_mapreduce_1_amd.utils import corpus  # noqa: E402
+
+M = "lua_mapreduce_1_amd.examples.InvertedIndex"
 
 
 def main() -> int:
@@ -37,33 +43,47 @@ def main() -> int:
     ap.add_argument("--validate", action="store_true", help="diff 1/8 of the splits against the naive oracle")
     args = ap.parse_args()
     rank, world, device = D.init_from_env()
-    splits = load_corpus(args.seed, rank, int(os.environ.get("LOCAL_RANK", 0)), world, device)
-    store = SplitStore(splits)
-    b = InvertedIndexBuilder(store, device=device, num_reducers=args.reducers)
-    # the next build's copies overlap this build's sort (two arenas); neither
-    # the last warm-up build nor the last timed one starts anything ahead, so
-    # every copy of the timed builds is inside the timed region
+    cdir = corpus_dir(args.seed, corpus.EUROPARL_LINES, corpus.EUROPARL_WORDS)
+    if int(os.environ.get("LOCAL_RANK", 0)) == 0:
+        ensure_corpus(cdir, args.seed, corpus.EUROPARL_LINES, corpus.EUROPARL_WORDS)
+    D.barrier(device=device)
+    off = np.load(os.path.join(cdir, "off.npy"))
+    store = SplitStore.from_blob(os.path.join(cdir, "blob.bin"), off, rank, world, pin=device.type == "cuda")
+    store.finish_loading()
+    params = dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                  init_args={"nsplits": len(store), "num_reducers": args.reducers, "quiet": True})
+    eng = spmd(params, device=device, split_store=store)
+    # the next iteration's copies overlap this iteration's sort (three
+    # arenas); neither the last warm-up step nor the last timed one starts
+    # anything ahead, so every copy of the timed steps is inside the region
+    eng.prefetch = True
     for w in range(args.warmup):
-        sh = b.build(prefetch_next=w < args.warmup - 1)
+        res = eng.run_iteration(prefetch_next=w < args.warmup - 1, lookahead=args.warmup - 1 - w)
     D.barrier(device=device)
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        sh = b.build(prefetch_next=i < args.steps - 1)
+        res = eng.run_iteration(prefetch_next=i < args.steps - 1, lookahead=args.steps - 1 - i)
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     D.barrier(device=device)
     ms = 1000.0 * D.all_reduce_max(time.perf_counter() - t0, device) / max(1, args.steps)
-    words = D.all_reduce_sum_int(sh.num_words, device)
-    postings = D.all_reduce_sum_int(sh.num_postings, device)
+    words = D.all_reduce_sum_int(res.distinct_keys, device)
+    postings = D.all_reduce_sum_int(res.total_value, device)
     ok = None
     if args.validate and world == 1:
-        sub = splits[:len(splits) // 8]
-        sb = InvertedIndexBuilder(SplitStore(sub), device=device, num_reducers=args.reducers)
-        ok = sb.build().to_host() == naive_index(sub)
+        import importlib
+        mod = importlib.import_module(M)
+        with open(os.path.join(cdir, "blob.bin"), "rb") as f:
+            blob = f.read(int(off[len(off) // 8]))
+        sub = [blob[off[i]:off[i + 1]] for i in range(len(off) // 8)]
+        e2 = spmd(dict(params, init_args={"nsplits": len(sub), "num_reducers": args.reducers}), device=device,
+                  split_store=SplitStore(sub))
+        e2.run()
+        ok = mod.RESULT == mod.naive_index(sub)
     if rank == 0:
-        print(f"# phases (last step, s): {b.timings}", file=sys.stderr)
+        print(f"# phases (last step, s): {res.timings}", file=sys.stderr)
         tokens = corpus.EUROPARL_WORDS
         print(json.dumps({
             "metric": "inverted-index build tokens/s (whole node), Europarl-v7-shaped 197 splits",
@@ -71,8 +91,8 @@ def main() -> int:
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong",
             "postings_per_s": postings / (ms / 1000.0), "distinct_words": words, "postings": postings,
             "validated_subset": ok, "data": "synthetic Europarl-v7-shaped corpus, host-pinned, staged every step",
-            "config": {"model": "inverted index (word -> sorted distinct line ids)", "parallelism": f"dp{world}",
-                       "num_reducers": args.reducers}}), flush=True)
+            "config": {"model": "examples/InvertedIndex (word -> sorted distinct line ids) on mr.spmd",
+                       "parallelism": f"dp{world}", "num_reducers": args.reducers}}), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -1,11 +1,15 @@
 #!/usr/bin/env python
-"""TeraSort-style benchmark (BASELINE.json config "TeraSort-style 10 GB
-key/value sort on 8xMI355X (radix sort + all-to-all)").
+"""TeraSort benchmark (BASELINE.json config "TeraSort-style 10 GB key/value
+sort on 8xMI355X (radix sort + all-to-all)") through the MapReduce API: the
+examples/TeraSort module (identity map, sampled range partitioner, identity
+reduce) on the SPMD engine's record plane.
 
-Records (100 B: 10 B key + 90 B value) are generated in HBM by the TeraGen
-analogue kernel (untimed); one timed step = splitter sampling + partition +
+Each rank's input block (100-byte records) is generated in HBM by the TeraGen
+kernel before timing and handed to the engine as a RecordStore; one timed step
+= one iteration: map (emit the block) + splitter sampling + partition +
 all-to-all of the rows (N>1) + local 80-bit radix sort + row gather, output
-resident in HBM.  Validation (global order + record checksum) after timing.
+resident in HBM.  Validation (global order + record checksum, collective
+device_finalfn) after timing.
 
   python tools/bench_terasort.py [--gb 10] [--steps K] [--warmup W]
   (N>1: python -m torch.distributed.run --nproc-per-node N tools/bench_terasort.py)
@@ -13,6 +17,7 @@ resident in HBM.  Validation (global order + record checksum) after timing.
 from __future__ import annotations
 
 import argparse
+import importlib
 import json
 import os
 import sys
@@ -22,8 +27,12 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from lua_mapreduce_1_amd import spmd  # noqa: E402
+from lua_mapreduce_1_amd.ops import terasort as TS  # noqa: E402
 from lua_mapreduce_1_amd.parallel import dist as D  # noqa: E402
-from lua_mapreduce_1_amd.parallel.terasort import TeraSort  # noqa: E402
+from lua_mapreduce_1_amd.parallel.planes import RecordStore  # noqa: E402
+
+M = "lua_mapreduce_1_amd.examples.TeraSort"
 
 
 def main() -> int:
@@ -34,33 +43,47 @@ def main() -> int:
     args = ap.parse_args()
     rank, world, device = D.init_from_env()
     total = int(args.gb * 1e9) // 100
-    t = TeraSort(total, device=device)
-    rec = t.generate()
-    cs = t.checksum_global(rec)
-    out = None
+    mod = importlib.import_module(M)
+    mod.init({"records": total, "blocks": world})
+    blocks = mod.blocks()
+    # every rank generates (only) its own block: block r is rank r's job
+    store = RecordStore([TS.generate(n, first, mod.SEED, device) if b == rank else torch.empty(0)
+                         for b, (first, n) in enumerate(blocks)])
+    for b, (first, n) in enumerate(blocks):
+        if b != rank:
+            store.blocks[b] = torch.empty((n, TS.REC), dtype=torch.uint8, device="meta")
+    params = dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                  init_args={"records": total, "blocks": world, "partitions": world})
+    eng = spmd(params, device=device, split_store=store)
     for _ in range(args.warmup):
-        out = t.sort(rec)
-        del out
+        res = eng.run_iteration()
+        del res
     D.barrier(device=device)
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = t.sort(rec)
+        res = eng.run_iteration()
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     D.barrier(device=device)
     ms = 1000.0 * D.all_reduce_max(time.perf_counter() - t0, device) / max(1, args.steps)
-    v = t.validate(out, cs)
+    timings = res.timings
+    del res
+    # validation iteration (not timed): input checksum in the map, collective check
+    mod.VALIDATE = True
+    mod._INPUT_CHECKSUM[0] = 0
+    res = eng.run_iteration()
+    ok = mod.device_finalfn(res, eng)
     if rank == 0:
-        print(f"# phases (last step, s): {t.timings}; validation {v}", file=sys.stderr)
+        print(f"# phases (last timed step, s): {timings}; validation {mod.VALIDATION}", file=sys.stderr)
         gbps = total * 100 / 1e9 / (ms / 1000.0)
         print(json.dumps({
             "metric": "TeraSort-style sort GB/s (whole node), 100-byte records",
             "value": gbps, "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms, "higher_is_better": True, "scaling": "strong", "records": total,
-            "valid": bool(v.get("ok")), "data": "synthetic TeraGen-style records generated in HBM (untimed)",
-            "config": {"model": "terasort (10-byte key, 90-byte value)", "total_gb": args.gb,
+            "valid": bool(ok), "data": "synthetic TeraGen-style records generated in HBM (untimed)",
+            "config": {"model": "examples/TeraSort (10-byte key, 90-byte value) on mr.spmd", "total_gb": args.gb,
                        "parallelism": f"dp{world}"}}), flush=True)
     if world > 1:
         import torch.distributed as dist
