@@ -418,6 +418,29 @@ def host_read(t: torch.Tensor) -> np.ndarray:
     return buf[:nb].numpy().view(_NP_DTYPE[t.dtype]).reshape(tuple(t.shape)).copy()
 
 
+def host_read_many(ts: list) -> list:
+    """Several small device tensors -> host numpy copies with ONE wait (the
+    downloads are queued back to back on the current stream)."""
+    if not ts or not ts[0].is_cuda:
+        return [t.detach().numpy().copy() for t in ts]
+    ts = [t.contiguous() for t in ts]
+    sizes = [t.numel() * t.element_size() for t in ts]
+    total = sum((n + 15) & ~15 for n in sizes)
+    d = ts[0].device
+    buf = _HOST_READ.get(d)
+    if buf is None or buf.numel() < total:
+        buf = torch.empty(max(total, 1 << 12), dtype=torch.uint8, pin_memory=True)
+        _HOST_READ[d] = buf
+    off = 0
+    views = []
+    for t, n in zip(ts, sizes):
+        _hip.call("mr_d2h_async", _hip.ptr(buf[off:off + n]), _hip.ptr(t), n, _hip.stream(d))
+        views.append((off, n, t))
+        off += (n + 15) & ~15
+    _hip.wait_stream(d)
+    return [buf[o:o + n].numpy().view(_NP_DTYPE[t.dtype]).reshape(tuple(t.shape)).copy() for o, n, t in views]
+
+
 _NP_DTYPE = {torch.int64: np.int64, torch.int32: np.int32, torch.uint8: np.uint8, torch.float32: np.float32,
              torch.float64: np.float64, torch.uint32: np.uint32, torch.int16: np.int16}
 

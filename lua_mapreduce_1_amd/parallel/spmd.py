@@ -215,6 +215,37 @@ class JobRecord:
         self.worker = -1
 
 
+class _DeviceTimer:
+    """Reusable HIP events (timing enabled) of one iteration slot: one before
+    the map, one after every map chunk's launches, and the shuffle/tail
+    boundaries.  Read after the iteration's final synchronisation."""
+
+    def __init__(self):
+        self._ev: list = []
+        self.n = 0
+        self.marks: dict[str, int] = {}
+
+    def _get(self, i: int):
+        while len(self._ev) <= i:
+            self._ev.append(torch.cuda.Event(enable_timing=True))
+        return self._ev[i]
+
+    def begin(self) -> None:
+        self.n = 0
+        self.marks = {}
+        self._get(0).record()
+
+    def mark(self, name: str | None = None) -> None:
+        """Event on the current stream after the work queued so far."""
+        self.n += 1
+        self._get(self.n).record()
+        if name is not None:
+            self.marks[name] = self.n
+
+    def ms(self, a: int, b: int) -> float:
+        return float(self._ev[a].elapsed_time(self._ev[b]))
+
+
 class IterationResult:
     def __init__(self):
         self._parts: dict[int, dict] | None = {}  # partition -> columnar host arrays (built on first use)
@@ -225,6 +256,8 @@ class IterationResult:
         self.timings: dict[str, float] = {}
         self.distinct_keys = 0
         self._vals = None
+        self.bytes_shuffled = 0     # payload bytes this rank sent in the all-to-all
+        self.bytes_shuffled_remote = 0  # ... to other ranks
 
     @property
     def partitions(self) -> dict[int, dict]:
@@ -327,6 +360,11 @@ class SPMDEngine:
         # rare multi-ms stalls) on the full single-GPU corpus, so it is opt-in
         self.use_graphs = TUNABLES.graphs
         self._tail_graphs: dict = {}
+        # per slot (pipelined iterations alternate): device event timers, the
+        # job ranges of the map chunks and their device error words
+        self._timers: list = [None, None]
+        self._chunks: list = [[], []]
+        self._errs: list = [None, None]
         self._tail_seen: set = set()
         self.iteration = 0
         self.finished = False
@@ -612,7 +650,31 @@ class SPMDEngine:
             for j in range(j0, j1):
                 yield (j, j + 1), jobs[j][1]
 
+    def _timer(self):
+        """The device timer of the current slot (None: timing off / CPU)."""
+        if not (TUNABLES.device_timing and self.device.type == "cuda") or self.use_graphs:
+            return None
+        t = self._timers[self.tslot]
+        if t is None:
+            t = self._timers[self.tslot] = _DeviceTimer()
+        return t
+
+    def _err_words(self, n: int) -> torch.Tensor:
+        """Per-chunk device error words of the current slot (zeroed here)."""
+        e = self._errs[self.tslot]
+        if e is None or e.numel() < n:
+            e = self._errs[self.tslot] = torch.zeros(max(64, 2 * n), dtype=torch.int32, device=self.device)
+        else:
+            e[:n].zero_()
+        return e
+
     def _run_map(self, jobs, recs, j0, j1) -> None:
+        """Issue the map of this rank's jobs [j0, j1), chunk by chunk as the
+        staged input lands.  A chunk = the jobs of one launch; its jobs share
+        a device error word (``emit.error_word()``) that device code sets to
+        report the chunk failed — checked after the map's synchronisation
+        (``_map_sync``), which re-runs it (BROKEN) or drops it (FAILED after
+        MAX_JOB_RETRIES attempts), like a host exception at launch time."""
         ctx = devmod.DeviceMapContext.__new__(devmod.DeviceMapContext)
         ctx.device, ctx.op, ctx.table = self.device, self.op, self.table
         ctx.arena, ctx.sources, ctx.base, ctx.host_pairs = None, [], 0, []
@@ -622,13 +684,26 @@ class SPMDEngine:
             ctx.sources = None
         ctx.emit = devmod.DeviceEmitter(ctx)
         self._ctx = ctx
+        timer = self._timer()
+        if timer is not None:
+            timer.begin()
+        chunks = self._chunks[self.tslot] = []
+        errs = self._err_words(j1 - j0 + 1) if self.device.type == "cuda" else None
+        fault = self._device_fault_spec()
         # the rank's whole staged input is ONE byte source (rep offsets index it)
         for (a, b), data in self._stage_chunks(jobs, j0, j1):
+            k = len(chunks)
+            chunks.append((a, b))
             t0 = time.time()
             c0 = time.process_time()
+            if all(recs[j].status == STATUS.FAILED for j in range(a, b)):
+                if timer is not None:
+                    timer.mark()
+                continue  # FAILED after MAX_JOB_RETRIES: left out of the results
             for j in range(a, b):
                 recs[j].status, recs[j].started, recs[j].worker = STATUS.RUNNING, t0, self.rank
             keys = [jobs[j][0] for j in range(a, b)]
+            ctx.err_word = errs[k:k + 1] if errs is not None else None
             done = False
             while not done:
                 try:
@@ -650,6 +725,13 @@ class SPMDEngine:
                         for j in range(a, b):
                             recs[j].status = STATUS.FAILED
                         done = True
+            if fault is not None and errs is not None and fault[0] in range(a, b) and fault[1] > 0:
+                # MR_SPMD_DEVICE_FAULT: a device-side write of the chunk's error
+                # word, as a kernel that detects bad input would do
+                fault[1] -= 1
+                errs[k:k + 1].fill_(1)
+            if timer is not None:
+                timer.mark()
             t1 = time.time()
             for j in range(a, b):
                 if recs[j].status != STATUS.FAILED:
@@ -658,6 +740,87 @@ class SPMDEngine:
                 recs[j].real_time = (t1 - t0) / (b - a)
                 recs[j].cpu_time = (time.process_time() - c0) / (b - a)
         ctx.flush_host_pairs()
+
+    def _device_fault_spec(self):
+        """``MR_SPMD_DEVICE_FAULT=<job index>:<times>``: the map chunk holding
+        that job reports a device-side failure in its first ``times`` runs
+        (fault injection).  State lives per engine."""
+        spec = os.environ.get("MR_SPMD_DEVICE_FAULT", "")
+        if not spec:
+            return None
+        if getattr(self, "_dev_fault", None) is None or self._dev_fault[2] != spec:
+            j, times = spec.split(":")
+            self._dev_fault = [int(j), int(times), spec]
+        return self._dev_fault
+
+    def _map_sync(self, jobs, recs, j0, j1):
+        """Synchronise the map phase: table fill + overflow + per-chunk device
+        error words in one download.  Failed chunks are BROKEN and the map is
+        re-run (FAILED chunks skipped); an overflowed table is regrown and the
+        map re-run.  Returns (occupied slots, overflowed)."""
+        while True:
+            errs = self._errs[self.tslot]
+            nch = len(self._chunks[self.tslot])
+            if errs is not None and nch:
+                c, e = ops.host_read_many([self.table.ctrl, errs[:nch]])
+                n_claimed = int(c[0]) + int(c[32::32].sum())
+                overflow = bool(c[1])
+            else:
+                n_claimed, overflow = self.table.stats()
+                e = None
+            bad = [k for k in range(nch) if e is not None and e[k]]
+            if bad:
+                for k in bad:
+                    a, b = self._chunks[self.tslot][k]
+                    if all(recs[j].status == STATUS.FAILED for j in range(a, b)):
+                        continue
+                    for j in range(a, b):
+                        recs[j].repetitions += 1
+                        recs[j].status = STATUS.BROKEN
+                        if recs[j].repetitions >= utils.MAX_JOB_RETRIES:
+                            recs[j].status = STATUS.FAILED
+                    sys.stderr.write("# map chunk of jobs %s..%s reported a device-side failure (attempt %d)\n" % (
+                        jobs[a][0], jobs[b - 1][0], recs[a].repetitions))
+                self.table.reset()
+                self._run_map(jobs, recs, j0, j1)
+                continue
+            if overflow or n_claimed > self.table.cap // 2:
+                # grow and redo this rank's map (results with an overflowed table are unusable)
+                self.table = ops.HashTable(ops.next_pow2(4 * max(n_claimed, 1)), device=self.device, op=self.op)
+                self._table_capacity = self.table.cap
+                self._run_map(jobs, recs, j0, j1)
+                continue
+            return n_claimed, overflow
+
+    def _device_spans(self, res, recs, j0: int, j1: int) -> None:
+        """Job records and timings from the slot's device events (after the
+        iteration's final synchronisation): each map job gets its chunk's
+        device span in proportion to its input bytes, each reduce job the
+        tail's span in proportion to its keys."""
+        timer = self._timers[self.tslot] if self._timer() is not None else None
+        if timer is None:
+            return
+        chunks = self._chunks[self.tslot]
+        T = res.timings
+        for k, (a, b) in enumerate(chunks):
+            span = timer.ms(k, k + 1) / 1000.0
+            w = [self._job_bytes(res.map_jobs[j].value) for j in range(a, b)] if self.device_input == "split" \
+                else [1] * (b - a)
+            tot = float(sum(w)) or 1.0
+            for j, x in zip(range(a, b), w):
+                res.map_jobs[j].real_time = span * x / tot
+        T["device_map"] = timer.ms(0, len(chunks)) / 1000.0 if chunks else 0.0
+        m = timer.marks
+        if "tail0" in m and "tail_end" in m:
+            s_end = m.get("shuffle_end", m["tail0"])
+            T["device_shuffle"] = timer.ms(m["tail0"], s_end) / 1000.0
+            T["device_tail"] = timer.ms(s_end, m["tail_end"]) / 1000.0
+            counts = res._cols["bounds"] if res._cols is not None else None
+            if counts is not None and res.red_jobs:
+                tot = float(counts[-1]) or 1.0
+                for r in res.red_jobs:
+                    p = int(r.key)
+                    r.real_time = (T["device_shuffle"] + T["device_tail"]) * float(counts[p + 1] - counts[p]) / tot
 
     # -- shuffle + reduce -------------------------------------------------------
     def _source(self) -> torch.Tensor | None:
@@ -690,6 +853,7 @@ class SPMDEngine:
             self._failed_total = sum(r[2] for r in recv_h)
             send_sz = [SH.seg_bytes(r[0], r[1]) for r in send_h]
             recv_sz = [SH.seg_bytes(r[0], r[1]) for r in recv_h]
+            self._shuffled = (sum(send_sz), sum(send_sz) - send_sz[self.rank])
             with trace.range("mr.all_to_all"):
                 rbuf = D.all_to_all_v(buf[:sum(send_sz)], send_sz, recv_sz, self.group)
             return rbuf, recv.view(W, 3), sum(r[0] for r in recv_h)
@@ -700,6 +864,8 @@ class SPMDEngine:
         self._failed_total = sum(r[2] for r in recv_h)
         send_rows, send_bytes = [r[0] for r in send_h], [r[1] for r in send_h]
         recv_rows, recv_bytes = [r[0] for r in recv_h], [r[1] for r in recv_h]
+        sent = [32 * r + b for r, b in zip(send_rows, send_bytes)]
+        self._shuffled = (sum(sent), sum(sent) - sent[self.rank])
         rrec = D.all_to_all_v(rec, send_rows, recv_rows, self.group)
         rblob = D.all_to_all_v(blob[:sum(send_bytes)], send_bytes, recv_bytes, self.group)
         rrep = SH.absolute_reps(rrec, recv_rows, recv_bytes)
@@ -895,15 +1061,10 @@ class SPMDEngine:
     def _finish_iteration(self, res, T, t_start, t0, jobs, recs, j0, j1, ahead, q) -> IterationResult:
         prefetch_next = ahead > 0
         trace.push("mr.map.wait")
-        n_claimed, overflow = self.table.stats()   # synchronises the map phase
+        n_claimed, overflow = self._map_sync(jobs, recs, j0, j1)  # synchronises the map phase
         trace.pop()
-        if overflow or n_claimed > self.table.cap // 2:
-            # grow and redo this rank's map (results with an overflowed table are unusable)
-            self.table = ops.HashTable(ops.next_pow2(4 * max(n_claimed, 1)), device=self.device, op=self.op)
-            self._table_capacity = self.table.cap
-            self._run_map(jobs, recs, j0, j1)
-            n_claimed, overflow = self.table.stats()
         T["map"] = time.time() - t0
+        timer = self._timer()
         pipelined = prefetch_next and self.pipeline and self._can_pipeline()
         # the next iteration's map is queued right after this iteration's first
         # tail kernels: those get the GPU first, and the host queues the map
@@ -916,6 +1077,8 @@ class SPMDEngine:
                 with trace.range("mr.map.issue_next"):
                     self._issue_next_map(jobs, j0, j1, q)
         t1 = time.time()
+        if timer is not None:
+            timer.mark("tail0")
         src = self._source()
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
         self._failed_total = failed
@@ -947,6 +1110,8 @@ class SPMDEngine:
                 src, rcounts, rows = self._shuffle(hi, lo, val, rep, src, part, failed, raw=True,
                                                   before_sync=issue_next_map)
                 n_red = self._reduce_insert_received(src, rcounts, rows)
+                if timer is not None:
+                    timer.mark("shuffle_end")
                 with trace.range("mr.tail_issue"):
                     pend = self._finalize_table(self.red_table, n_red, src)
             else:
@@ -958,6 +1123,8 @@ class SPMDEngine:
         t2 = time.time()
         if pend is None:
             pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
+        if timer is not None:
+            timer.mark("tail_end")
         issue_next_map()
         if _PREFETCH_LATE:
             self._prefetch_ahead(jobs, j0, j1, q, ahead)
@@ -978,6 +1145,8 @@ class SPMDEngine:
         T["reduce"] = time.time() - t2
         T["iteration"] = time.time() - t_start
         res.failed_maps = self._failed_total
+        res.bytes_shuffled, res.bytes_shuffled_remote = getattr(self, "_shuffled", (0, 0))
+        self._device_spans(res, recs, j0, j1)
         return res
 
     # ------------------------------------------------------------------------
@@ -1005,17 +1174,33 @@ class SPMDEngine:
         mr = sum(x.real_time for x in m)
         rr = sum(x.real_time for x in r)
         T = res.timings
+        # device spans (HIP events) when measured, else host times; the keys
+        # and their order are the reference's (server.lua:555-600)
+        dev = "device_map" in T
+        map_ct = T["device_map"] if dev else T["map"]
+        red_ct = (T.get("device_shuffle", 0.0) + T.get("device_tail", 0.0)) if dev else T["shuffle"] + T["reduce"]
         lines = [
             "#   Map sum(cpu_time)     %f" % ms, "#   Reduce sum(cpu_time)  %f" % rs,
             "# Sum(cpu_time)           %f" % (ms + rs), "#   Map sum(real_time)    %f" % mr,
             "#   Reduce sum(real_time) %f" % rr, "# Sum(real_time)          %f" % (mr + rr),
-            "# Sum(sys_time)           %f" % (mr + rr - ms - rs), "#   Map cluster time      %f" % T["map"],
-            "#   Reduce cluster time   %f" % (T["shuffle"] + T["reduce"]),
-            "# Cluster time            %f" % (T["map"] + T["shuffle"] + T["reduce"]),
+            "# Sum(sys_time)           %f" % (mr + rr - ms - rs), "#   Map cluster time      %f" % map_ct,
+            "#   Reduce cluster time   %f" % red_ct,
+            "# Cluster time            %f" % (map_ct + red_ct),
             "# Failed maps     %d" % getattr(res, "failed_maps", 0),
             "# Failed reduces  %d" % getattr(res, "failed_reduces", 0),
             "# Server time %f" % T["iteration"],
         ]
+        # SURVEY.md §5.5 additions: throughput, shuffle volume, device phases
+        vals = getattr(res, "total_value", 0)
+        if T["iteration"] > 0 and vals:
+            lines.append("# Values/s (server time) %.6g" % (vals / T["iteration"]))
+        lines.append("# Distinct keys %d" % getattr(res, "distinct_keys", 0))
+        if getattr(res, "bytes_shuffled", 0):
+            lines.append("# Bytes shuffled %d (to other ranks %d)" % (res.bytes_shuffled, res.bytes_shuffled_remote))
+        if dev:
+            lines.append("# Device spans ms: map (H2D + kernels) %.3f, shuffle %.3f, tail %.3f (%s)" % (
+                1e3 * T["device_map"], 1e3 * T.get("device_shuffle", 0.0), 1e3 * T.get("device_tail", 0.0),
+                "values are device-measured" if dev else "host"))
         return "\n".join(lines) + "\n"
 
     # -- checkpoint / resume and fault injection -------------------------------

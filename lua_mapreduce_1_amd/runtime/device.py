@@ -27,6 +27,9 @@ from ..ops import keys as K
 
 
 _HAS_GPU: bool | None = None
+# device map jobs run per device type (observability; tests check that the
+# worker's device plane really ran on the GPU)
+STATS: dict[str, int] = {}
 
 
 def default_device():
@@ -47,6 +50,7 @@ class DeviceMapContext:
 
     def __init__(self, device=None, op: str = "sum", capacity: int = 1 << 20):
         self.device = torch.device(device) if device is not None else default_device()
+        STATS["maps_" + self.device.type] = STATS.get("maps_" + self.device.type, 0) + 1
         self.op = op
         self.capacity = capacity
         self.table = ops.HashTable(capacity, device=self.device, op=op)
@@ -136,6 +140,13 @@ class DeviceEmitter:
         elif ctx.sources is None:
             add = ctx.base  # engine-staged input: rep words relative to the mapped data
         ctx.table.insert(hi, lo, vals, rep, rep_add=add, src=ctx.arena)
+
+    def error_word(self):
+        """The current map chunk's device error word (int32[1] on the
+        device; None off the SPMD engine / on CPU): device code that finds the
+        chunk's input bad writes it non-zero, and the engine re-runs the
+        chunk's jobs (BROKEN) or drops them (FAILED after MAX_JOB_RETRIES)."""
+        return getattr(self.ctx, "err_word", None)
 
     def __call__(self, key, value=1) -> None:
         if isinstance(key, str):

@@ -51,6 +51,9 @@ class Tunables:
     force_shuffle: bool = _knob("MR_FORCE_SHUFFLE", False,
                                 "SPMD: run the W>1 shuffle (pack, count exchange, all-to-all, receive insert) also "
                                 "at world size 1 (needs an initialised process group; tests RCCL on one GPU)")
+    device_timing: bool = _knob("MR_DEVICE_TIMING", True,
+                                "SPMD: HIP events around every map chunk, the shuffle and the tail; job records "
+                                "and the stats block report device spans instead of host issue times")
     numa_bind: bool = _knob("MR_NUMA_BIND", True, "pin each rank to the CPUs of its GPU's NUMA node")
     # -- diagnostics
     debug_checks: bool = _knob("MR_DEBUG_CHECKS", False, "extra host-side consistency checks (slow)")

@@ -1,0 +1,27 @@
+"""Server/worker WordCount with the device plane on the GPU (``device="auto"``
+on cuda:0: workers run device_mapfn through the HIP map kernel, reduce jobs
+merge the columnar partition files on the GPU), for every storage, diffed
+against the naive oracle — the GPU counterpart of test_e2e_wordcount.py."""
+import pytest
+
+from lua_mapreduce_1_amd.runtime import coordinator
+from lua_mapreduce_1_amd.runtime import device as devmod
+from test_e2e_wordcount import SCENARIOS, naive_output, run_job
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cs():
+    return coordinator.start_local()
+
+
+@pytest.mark.parametrize("storage", ["gridfs", "shared", "sshfs", "hbm"])
+@pytest.mark.parametrize("scenario", ["combiner_aci", "init_script"])
+def test_wordcount_device_plane_on_gpu(gpu, cs, storage, scenario):
+    before = devmod.STATS.get("maps_cuda", 0)
+    p = dict(SCENARIOS[scenario], storage=storage, device="auto")
+    got, s = run_job(cs, f"wcgpu_{storage}_{scenario}", p, nworkers=2)
+    assert got == naive_output()
+    assert s.last_stats["failed_map_jobs"] == 0 and s.last_stats["failed_red_jobs"] == 0
+    assert devmod.STATS.get("maps_cuda", 0) - before == 4  # every map job on the GPU
