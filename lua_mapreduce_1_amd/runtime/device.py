@@ -30,6 +30,11 @@ _HAS_GPU: bool | None = None
 # device map jobs run per device type (observability; tests check that the
 # worker's device plane really ran on the GPU)
 STATS: dict[str, int] = {}
+# finalize() results alias process-wide pinned buffers (_POOL) and the sort /
+# tail workspaces are per device: threads of one process that run device jobs
+# (several workers in one process) hold this lock around a job
+import threading as _threading  # noqa: E402
+PLANE_LOCK = _threading.RLock()
 
 
 def default_device():

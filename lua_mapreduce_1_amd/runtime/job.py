@@ -205,6 +205,12 @@ class job:  # noqa: N801
         self.cnn.gridfs().store_data(b"", INDEX_PREFIX + name + INDEX_SEP + utils.get_hostname())
 
     def _run_device_map(self, pmod, rmod):
+        # the device plane's pinned download buffers and workspaces are
+        # per-process: worker threads of one process take turns on the GPU
+        with dev.PLANE_LOCK:
+            return self._run_device_map_locked(pmod, rmod)
+
+    def _run_device_map_locked(self, pmod, rmod):
         clock1 = _time.process_time()
         map_key, map_value = self.get_pair()
         op = modules.field(rmod, "device_reduce", "sum") if rmod is not None else "sum"
@@ -275,7 +281,8 @@ class job:  # noqa: N801
                     blobs = None
             b = rbuilder()
             if blobs is not None:
-                b.append(_device_reduce(blobs, dev_op))
+                with dev.PLANE_LOCK:
+                    b.append(_device_reduce(blobs, dev_op))
             else:
                 recs = []
                 for k, v in utils.merge_iterator(fs, filenames, make_lines_iterator):
