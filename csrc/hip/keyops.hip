@@ -304,6 +304,31 @@ __global__ void gather_key_bytes_kernel(const u64* hi, const u64* lo, const u64*
   }
 }
 
+// Streaming map (input larger than the HBM arena ring): after a round, the
+// long keys whose rep words point into that round's arena slot
+// [lo_off, hi_off) of `buf` get their bytes copied to the persistent key heap
+// at the front of `buf` (bump allocator `heap[0]`, capacity heap_cap) and
+// their rep re-pointed there, so the slot can be refilled by a later round.
+// heap[1] is set when the heap is full (the host raises).
+__global__ void table_rehome_kernel(const u64* __restrict__ tag, const u64* __restrict__ lo, u64* __restrict__ rep,
+                                    u64 cap, u8* __restrict__ buf, u64 lo_off, u64 hi_off,
+                                    unsigned long long* __restrict__ heap, u64 heap_cap) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
+    if (tag[i] == 0 || !key_is_long(lo[i])) continue;
+    const u64 r = rep[i];
+    const u64 o = rep_off(r), n = rep_len(r);
+    if (o < lo_off || o >= hi_off) continue;
+    const unsigned long long d = atomicAdd(&heap[0], (unsigned long long)n);
+    if (d + n > heap_cap) {
+      atomicOr(&heap[1], 1ull);
+      continue;
+    }
+    for (u64 k = 0; k < n; ++k) buf[d + k] = buf[o + k];
+    rep[i] = make_rep(d, n);
+  }
+}
+
 // Reset a table in one launch: tag = lo = 0, val = init, ctrl = 0.
 __global__ void table_reset_kernel(u64* tag, u64* lo, long long* val, u32* ctrl, u64 cap, long long init) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
@@ -387,6 +412,13 @@ int mr_table_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* 
   hipLaunchKernelGGL(table_compact_kernel, dim3((unsigned)nb), dim3(256), 0, stream,
                      make_gtab(tag, hi, lo, val, rep, ctrl, cap), cap, (u64*)out_hi, (u64*)out_lo,
                      (long long*)out_val, (u64*)out_rep, (unsigned long long*)counter);
+  return (int)hipGetLastError();
+}
+
+int mr_table_rehome(const void* tag, const void* lo, void* rep, u64 cap, void* buf, u64 lo_off, u64 hi_off, void* heap,
+                    u64 heap_cap, hipStream_t stream) {
+  hipLaunchKernelGGL(table_rehome_kernel, dim3(grid_for(cap, 256)), dim3(256), 0, stream, (const u64*)tag,
+                     (const u64*)lo, (u64*)rep, cap, (u8*)buf, lo_off, hi_off, (unsigned long long*)heap, heap_cap);
   return (int)hipGetLastError();
 }
 

@@ -38,8 +38,11 @@ struct Lds {
   static constexpr int STAGED = TILE + HALO;
   static constexpr int TXT = PAD + STAGED + 32;
   static constexpr int WSW = STAGED / 32 + 2;
+  static constexpr int MAXTOK = T * 4;  // dense token list of a tile (~2.7 tokens per 16 B of text)
   u8 txt[TXT];
   u32 ws[WSW];
+  u16 tokpos[MAXTOK];
+  u32 wsum[T / 64];
   u64 tag[SLOTS];  // gtab_tag-style: a packed key of <= 7 bytes IS its tag
   u32 cnt[SLOTS];
   u32 rep[SLOTS];  // local offset (16 bits) | len (16 bits) << 16
@@ -156,7 +159,12 @@ __device__ __forceinline__ bool lds_insert(Lds<T, SLOTS>& L, u64 hi, u64 lo, u32
 }
 
 // T threads, SLOTS LDS slots, TPC tiles of T*16 bytes per workgroup chunk.
-template <int T, int SLOTS, int TPC>
+// DENSE: the tile's token starts are first compacted into an LDS list (block
+// prefix scan of per-thread start counts) and the tokens processed from that
+// list, lane i taking tokens i, i+T, ... — every lane busy in every
+// iteration, instead of each lane walking the 0..8 tokens that start in its
+// own 16 bytes (the wave ran as long as its busiest lane).
+template <int T, int SLOTS, int TPC, bool DENSE = false>
 __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text, u64 nbytes, u64 rep_base, GTab g,
                                                     Ovf ovf, int aligned, int ablate) {
   // ablate (timing only, the table is then incomplete): 1 = no flush to HBM,
@@ -210,67 +218,104 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
       q = load16(text, next + (u64)t * SEG, nbytes, aligned);
       if (t < NH) qh = load16(text, next + TILE + (u64)t * SEG, nbytes, aligned);
     }
+    // one token starting at tile offset p
+    auto process = [&](u32 p) {
+      u32 qq = p + 1;
+      u32 wd = L.ws[qq >> 5] >> (qq & 31);
+      u32 end;
+      if (wd) {
+        end = qq + __builtin_ctz(wd);
+      } else {
+        u32 k = (qq >> 5) + 1;
+        while (L.ws[k] == 0) ++k;
+        end = 32 * k + __builtin_ctz(L.ws[k]);
+      }
+      u64 len = end - p;
+      const u64 gpos = tile_base + p;
+      const u32 b = PAD + p;
+      const u32 a = b >> 2;
+      const u32 r8 = (b & 3u) * 8u;
+      const u32 x0 = txt32[a], x1 = txt32[a + 1], x2 = txt32[a + 2], x3 = txt32[a + 3], x4 = txt32[a + 4];
+      const u64 le_hi = (u64)funnel(x0, x1, r8) | ((u64)funnel(x1, x2, r8) << 32);
+      const u64 le_lo = (u64)funnel(x2, x3, r8) | ((u64)funnel(x3, x4, r8) << 32);
+      u64 hi = __builtin_bswap64(le_hi);
+      u64 lo;
+      if (end >= (u32)STAGED) {  // runs past the staged halo: measure from global memory
+        u64 pe = tile_base + STAGED;
+        while (pe < nbytes && !is_ws(text[pe])) ++pe;
+        len = pe - gpos;
+      }
+      if (len <= (u64)PACK_MAX) {
+        if (len < 8) hi &= ~0ull << (8 * (8 - len));
+        lo = len > 8 ? (__builtin_bswap64(le_lo) & (~0ull << (8 * (16 - len)))) : 0ull;
+        lo |= len;
+      } else {
+        lo = long_lo_global(text, gpos, len);
+      }
+      if (ablate == 2) {
+        if ((hi ^ lo) == 0x123456789ull) ovf.counter[1] = hi;  // keep the key live
+        return;
+      }
+      const bool ok = len < 65536 && lds_insert(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16),
+                                                 text + chunk_begin);
+      if (!ok) {
+        const u64 grep = make_rep(rep_base + gpos, len);
+        const unsigned long long idx = atomicAdd(ovf.counter, 1ull);
+        if (idx < ovf.cap) {
+          ovf.hi[idx] = hi;
+          ovf.lo[idx] = lo;
+          ovf.rep[idx] = grep;
+        } else {
+          claims += gtab_insert(g, hi, lo, 1, grep, OP_SUM) == 2;
+        }
+      }
+    };
     const u64 seg_base = tile_base + (u64)t * SEG;
+    u32 starts = 0;
     if (seg_base < chunk_end) {
       const u32 m = ws16[t];
       const u32 prev_ws = t ? ((ws16[t - 1] >> 15) & 1u) : (is_ws(L.txt[PAD - 1]) ? 1u : 0u);
-      u32 starts = (~m) & ((m << 1) | prev_ws) & 0xFFFFu;
+      starts = (~m) & ((m << 1) | prev_ws) & 0xFFFFu;
       const u64 lim_own = chunk_end - seg_base;
       if (lim_own < 16) starts &= (1u << lim_own) - 1u;
+    }
+    if constexpr (!DENSE) {
       while (starts) {
         const int i = __builtin_ctz(starts);
         starts &= starts - 1;
-        const u32 p = (u32)t * SEG + i;
-        u32 qq = p + 1;
-        u32 wd = L.ws[qq >> 5] >> (qq & 31);
-        u32 end;
-        if (wd) {
-          end = qq + __builtin_ctz(wd);
-        } else {
-          u32 k = (qq >> 5) + 1;
-          while (L.ws[k] == 0) ++k;
-          end = 32 * k + __builtin_ctz(L.ws[k]);
-        }
-        u64 len = end - p;
-        const u64 gpos = tile_base + p;
-        const u32 b = PAD + p;
-        const u32 a = b >> 2;
-        const u32 r8 = (b & 3u) * 8u;
-        const u32 x0 = txt32[a], x1 = txt32[a + 1], x2 = txt32[a + 2], x3 = txt32[a + 3], x4 = txt32[a + 4];
-        const u64 le_hi = (u64)funnel(x0, x1, r8) | ((u64)funnel(x1, x2, r8) << 32);
-        const u64 le_lo = (u64)funnel(x2, x3, r8) | ((u64)funnel(x3, x4, r8) << 32);
-        u64 hi = __builtin_bswap64(le_hi);
-        u64 lo;
-        if (end >= (u32)STAGED) {  // runs past the staged halo: measure from global memory
-          u64 pe = tile_base + STAGED;
-          while (pe < nbytes && !is_ws(text[pe])) ++pe;
-          len = pe - gpos;
-        }
-        if (len <= (u64)PACK_MAX) {
-          if (len < 8) hi &= ~0ull << (8 * (8 - len));
-          lo = len > 8 ? (__builtin_bswap64(le_lo) & (~0ull << (8 * (16 - len)))) : 0ull;
-          lo |= len;
-        } else {
-          lo = long_lo_global(text, gpos, len);
-        }
-        if (ablate == 2) {
-          if ((hi ^ lo) == 0x123456789ull) ovf.counter[1] = hi;  // keep the key live
-          continue;
-        }
-        const bool ok = len < 65536 && lds_insert(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16),
-                                                   text + chunk_begin);
-        if (!ok) {
-          const u64 grep = make_rep(rep_base + gpos, len);
-          const unsigned long long idx = atomicAdd(ovf.counter, 1ull);
-          if (idx < ovf.cap) {
-            ovf.hi[idx] = hi;
-            ovf.lo[idx] = lo;
-            ovf.rep[idx] = grep;
-          } else {
-            claims += gtab_insert(g, hi, lo, 1, grep, OP_SUM) == 2;
-          }
-        }
+        process((u32)t * SEG + i);
       }
+    } else {
+      // block exclusive scan of the per-thread token counts
+      constexpr int MAXTOK = L_t::MAXTOK;
+      const int lane = t & 63, wave = t >> 6;
+      const u32 c = __builtin_popcount(starts);
+      u32 incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const u32 v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      if (lane == 63) L.wsum[wave] = incl;
+      __syncthreads();
+      u32 base = 0, total = 0;
+#pragma unroll
+      for (int w = 0; w < T / 64; ++w) {
+        const u32 x = L.wsum[w];
+        base += w < wave ? x : 0u;
+        total += x;
+      }
+      u32 k = base + incl - c;
+      while (starts) {
+        const int i = __builtin_ctz(starts);
+        starts &= starts - 1;
+        if (k < (u32)MAXTOK) L.tokpos[k] = (u16)(t * SEG + i);
+        else process((u32)t * SEG + i);  // a tile denser than the list (one-letter words): in place
+        ++k;
+      }
+      __syncthreads();
+      const u32 ntok = total < (u32)MAXTOK ? total : (u32)MAXTOK;
+      for (u32 x = t; x < ntok; x += T) process(L.tokpos[x]);
     }
     __syncthreads();
   }
@@ -382,13 +427,14 @@ __global__ void __launch_bounds__(256) ovf_agg3_kernel(Ovf o, GTab g) {
   gtab_count_claims(g, claims);
 }
 
-template <int T, int SLOTS, int TPC>
+template <int T, int SLOTS, int TPC, bool DENSE = false>
 int launch(const u8* tx, u64 nbytes, u64 rep_base, const GTab& g, const Ovf& o, int aligned, int ablate,
            hipStream_t stream) {
+  static_assert(sizeof(Lds<T, SLOTS>) <= 160 * 1024, "LDS budget");
   constexpr u64 CHUNK = (u64)T * SEG * TPC;
   const u64 nblocks = (nbytes + CHUNK - 1) / CHUNK;
-  hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC>), dim3((unsigned)nblocks), dim3(T), 0, stream, tx, nbytes,
-                     rep_base, g, o, aligned, ablate);
+  hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC, DENSE>), dim3((unsigned)nblocks), dim3(T), 0, stream, tx,
+                     nbytes, rep_base, g, o, aligned, ablate);
   return 0;
 }
 
@@ -403,6 +449,7 @@ extern "C" {
 //         1 = 512 / 2048 / 2 (16 KiB)      2 = 1024 / 4096 / 1 (16 KiB, 1 per CU)
 //         3 = 256 / 1024 / 1 (4 KiB, 4 per CU)   4 = 256 / 2048 / 2 (8 KiB, 2 per CU)
 //         5 = 512 / 4096 / 2 (16 KiB, 1 per CU: v2's shape + prefetch)
+//         6..9 = configs 0, 1, 3, 2 with dense token lists
 int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, void* lo, void* val, void* rep,
                void* ctrl, u64 cap, void* ovf_hi, void* ovf_lo, void* ovf_rep, u64 ovf_cap, void* ovf_counter,
                int config, void* stamps, hipStream_t stream) {
@@ -428,6 +475,11 @@ int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, 
     case 3: v3::launch<256, 1024, 1>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
     case 4: v3::launch<256, 2048, 2>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
     case 5: v3::launch<512, 4096, 2>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
+    // dense token lists (see wc_map3_kernel)
+    case 6: v3::launch<512, 2048, 1, true>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
+    case 7: v3::launch<512, 2048, 2, true>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
+    case 8: v3::launch<256, 1024, 1, true>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
+    case 9: v3::launch<1024, 4096, 1, true>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
     default: return -1;
   }
   hipLaunchKernelGGL(v3::ovf_agg3_kernel, dim3(1024), dim3(256), 0, stream, o, g);

@@ -91,6 +91,7 @@ _SIGS = {
     "mr_tail_pack_bytes": [_u64, _u32],
     "mr_tail_ws_layout": [_u64, _u32, _u64, ctypes.POINTER(ctypes.c_uint64)],
     "mr_table_reset": [_p, _p, _p, _p, _u64, ctypes.c_longlong, _p],
+    "mr_table_rehome": [_p, _p, _p, _u64, _p, _u64, _u64, _p, _u64, _p],
     "mr_scan_partials_len": [_u64],
 }
 _RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout"}

@@ -176,7 +176,7 @@ class HashTable:
         self._ovf_next += 1
         return self._ovf, self._ovf_counter
 
-    def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, mode: int = 0,
+    def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, mode: int | None = None,
                       stamps: torch.Tensor | None = None, src: torch.Tensor | None = None) -> None:
         """Fused tokenize + exact key + combine of every whitespace token
         (value 1): csrc/hip/wordcount3.hip.  ``text`` sits at byte
@@ -190,6 +190,8 @@ class HashTable:
             self.src = text
         if nbytes == 0:
             return
+        if mode is None:
+            mode = TUNABLES.wc_config
         if self.is_cuda:
             assert text.dtype == torch.uint8 and text.is_contiguous()
             ovf, counter = self._overflow(nbytes)
@@ -228,6 +230,31 @@ class HashTable:
         rc = recv_counts.view(W, 3).tolist()
         rep = absolute_reps(rec, [r[0] for r in rc], [r[1] for r in rc])
         self.insert(rec[:, 0].contiguous(), rec[:, 1].contiguous(), rec[:, 2].contiguous(), rep)
+
+    def rehome_long_keys(self, buf: torch.Tensor, lo_off: int, hi_off: int, heap: torch.Tensor,
+                         heap_cap: int) -> None:
+        """Copy the bytes of long keys whose rep points into buf[lo_off:hi_off)
+        to the key heap at the front of ``buf`` (``heap`` = int64[2] bump
+        counter + full flag) and re-point their reps (streaming map rounds)."""
+        if self.is_cuda:
+            _hip.call("mr_table_rehome", _hip.ptr(self.tag), _hip.ptr(self.lo), _hip.ptr(self.rep), self.cap,
+                      _hip.ptr(buf), lo_off, hi_off, _hip.ptr(heap), heap_cap, _hip.stream(self.device))
+            return
+        b = _np(buf) if not buf.is_cuda else None
+        h = heap.numpy()
+        for k, (hi_, lo_, v, r) in enumerate(self._pending):
+            long_ = (lo_ & np.uint64(0xFF)) == np.uint64(K.LONG_MARK)
+            off = r >> np.uint64(K.REP_LEN_BITS)
+            sel = np.flatnonzero(long_ & (off >= np.uint64(lo_off)) & (off < np.uint64(hi_off)))
+            for i in sel:
+                o, n = int(r[i]) >> K.REP_LEN_BITS, int(r[i]) & K.REP_LEN_MASK
+                d = int(h[0])
+                if d + n > heap_cap:
+                    h[1] = 1
+                    continue
+                b[d:d + n] = b[o:o + n].copy()
+                h[0] = d + n
+                r[i] = np.uint64(K.make_rep(d, n))
 
     # -- state ---------------------------------------------------------------
     def stats(self) -> tuple[int, bool]:

@@ -191,6 +191,60 @@ def _engine_streams(device):
     return st[0], list(st[1])
 
 
+class WindowedSplitStore(SplitStore):
+    """Split files read on demand into a ring of two pinned windows (inputs
+    larger than host memory): the engine's streaming rounds
+    (``arena_cap_mb``) ask for one round of splits at a time
+    (:meth:`load_round`), the native loader reads them into the free window,
+    and the window is released once the round's host->HBM copies have
+    completed.  Offsets/sizes of every split are known up front (stat)."""
+
+    def __init__(self, paths: list[str], rank: int = 0, world: int = 1, window_mb: float = 256,
+                 pin: bool = True, threads: int = 8):
+        lens = [os.path.getsize(p) for p in paths]
+        self.paths = list(paths)
+        self.offsets = np.zeros(len(paths) + 1, dtype=np.int64)
+        np.cumsum(np.asarray(lens, dtype=np.int64) + 1, out=self.offsets[1:])
+        self.own = assign_contiguous([n + 1 for n in lens], rank, world)
+        self.base = int(self.offsets[self.own[0]])
+        self.window = int(window_mb * (1 << 20))
+        self.threads = threads
+        self._win = [torch.empty(self.window, dtype=torch.uint8, pin_memory=pin and torch.cuda.is_available())
+                     for _ in range(2)]
+        self._released = [None, None]
+        self._load = None
+        self.buffer = None  # no whole-share buffer: rounds only
+
+    def all_ready(self) -> bool:
+        return True
+
+    def wait_ready(self, i0: int, i1: int) -> None:
+        return None
+
+    def load_round(self, i0: int, i1: int, slot: int) -> torch.Tensor:
+        """Splits [i0, i1) (each followed by a newline) in window ``slot``;
+        waits until the window's previous copies have completed."""
+        ev = self._released[slot]
+        if ev is not None:
+            ev.synchronize()
+        nbytes = int(self.offsets[i1] - self.offsets[i0])
+        if nbytes > self.window:
+            raise ValueError(f"round of {nbytes} bytes exceeds the {self.window}-byte host window")
+        from ..ops import io as mio
+        w = self._win[slot]
+        lens = (self.offsets[i0 + 1:i1 + 1] - self.offsets[i0:i1] - 1).tolist()
+        ld = mio.AsyncLoad(self.paths[i0:i1], [0] * (i1 - i0), lens, self.offsets[i0:i1] - self.offsets[i0],
+                           [1] * (i1 - i0), w, threads=self.threads)
+        ld.wait()
+        return w[:nbytes]
+
+    def release(self, slot: int, event) -> None:
+        self._released[slot] = event
+
+    def line_offsets(self) -> np.ndarray:
+        raise ValueError("line numbering needs a store holding every split")
+
+
 def assign_contiguous(weights, rank: int, world: int) -> tuple[int, int]:
     """Contiguous block [j0, j1) of items for ``rank``, balanced by weight."""
     n = len(weights)
@@ -580,11 +634,132 @@ class SPMDEngine:
         self._issue_copies(plan)
         self._inflight[aslot] = self._arena_holds[aslot] = (ids[0], len(ids))
 
+    # -- streaming: inputs larger than the HBM arena ----------
+    def _arena_cap(self) -> int:
+        mb = self.params.get("arena_cap_mb", TUNABLES.arena_cap_mb)
+        return int(float(mb) * (1 << 20)) if mb else 0
+
+    def _streaming(self, ids) -> bool:
+        cap = self._arena_cap()
+        if not cap or not ids:
+            return False
+        a, b = self.splits.region(ids[0], ids[-1] + 1)
+        return b - a > cap
+
+    def _stage_streaming(self, jobs, j0, ids):
+        """Map a rank's input through a ring of two arena slots of the capped
+        size, in rounds of whole splits: round r+1's copies land while round r
+        maps; after a round the long keys it introduced move their bytes to a
+        persistent key heap at the front of the same buffer (the reference's
+        streaming reduce keeps only what it still needs, utils.lua:206-271),
+        so the slot can be refilled.  One buffer = one byte source for the
+        table's rep words: [key heap | slot 0 | slot 1]."""
+        A = self._arena_cap()
+        st = self.splits
+        sizes = [st.size(i) for i in ids]
+        if max(sizes) > A:
+            raise ValueError(f"a split of {max(sizes)} bytes does not fit the {A}-byte arena cap")
+        rounds, k0, acc = [], 0, 0
+        for k, sz in enumerate(sizes):
+            if acc + sz > A:
+                rounds.append((k0, k))
+                k0, acc = k, 0
+            acc += sz
+        rounds.append((k0, len(ids)))
+        a0, b0 = st.region(ids[0], ids[-1] + 1)
+        H = max(1 << 16, min(b0 - a0, int(TUNABLES.stream_heap_mb * (1 << 20))))
+        need = H + 2 * A
+        buf = getattr(self, "_stream_buf", None)
+        if buf is None or buf.numel() < need:
+            buf = self._stream_buf = torch.empty(need, dtype=torch.uint8, device=self.device)
+            self._stream_heap = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self._stream_H = H
+        self.arenas[self.slot] = buf
+        self._arena_holds.pop(self.slot, None)
+        heap = self._stream_heap
+        heap.zero_()
+        cs = self.copy_stream
+        host = st.buffer
+        piece = max(self.chunk_bytes[-1], 1)
+        plan = []  # per round: [(job range, buffer offset, host offset, bytes)]
+        for r, (k0, k1) in enumerate(rounds):
+            slot_off = H + (r % 2) * A
+            ra = st.region(ids[k0], ids[k0] + 1)[0]
+            pieces, k = [], k0
+            while k < k1:
+                e, acc = k, 0
+                while e < k1 and (e == k or acc + sizes[e] <= piece):
+                    acc += sizes[e]
+                    e += 1
+                pa = st.region(ids[k], ids[k] + 1)[0]
+                pieces.append(((j0 + k, j0 + e), slot_off + pa - ra, pa, acc, (ids[k], ids[e - 1] + 1)))
+                k = e
+            plan.append(pieces)
+        windowed = isinstance(st, WindowedSplitStore)
+
+        def host_of(r):
+            """Host bytes of round r (a window of a windowed store) and the
+            host offset of its first byte."""
+            k0, k1 = rounds[r]
+            if windowed:
+                return st.load_round(ids[k0], ids[k1 - 1] + 1, r % 2), st.region(ids[k0], ids[k0] + 1)[0]
+            return host, 0
+
+        if cs is None:  # CPU: copy, map, rehome round by round
+            for r, pieces in enumerate(plan):
+                h, hb = host_of(r)
+                for jr, off, ha, n, sp in pieces:
+                    st.wait_ready(*sp)
+                    buf[off:off + n].copy_(h[ha - hb:ha - hb + n])
+                    yield jr, buf[off:off + n]
+                self.table.rehome_long_keys(buf, H + (r % 2) * A, H + (r % 2) * A + A, heap, H)
+            return
+        from ..ops import _hip
+        cur = torch.cuda.current_stream(self.device)
+        evs = getattr(self, "_stream_events", None)
+        if evs is None:
+            evs = self._stream_events = {"gate": torch.cuda.Event(), "free": [torch.cuda.Event(), torch.cuda.Event()],
+                                         "piece": []}
+        sp_cs = _hip.stream_ptr(cs)
+
+        def issue(r):
+            pe = []
+            h, hb = host_of(r)
+            for jr, off, ha, n, sp in plan[r]:
+                st.wait_ready(*sp)
+                _hip.call("mr_memcpy_async", _hip.ptr(buf[off:off + n]), _hip.ptr(h[ha - hb:ha - hb + n]), n, 1,
+                          sp_cs)
+                ev = torch.cuda.Event()
+                ev.record(cs)
+                pe.append(ev)
+            if windowed:
+                st.release(r % 2, pe[-1])  # the window is free once its copies are done
+            return pe
+
+        # the buffer may still be read by the previous iteration's tail
+        evs["gate"].record(cur)
+        cs.wait_event(evs["gate"])
+        issued = {0: issue(0)}
+        if len(plan) > 1:
+            issued[1] = issue(1)
+        for r, pieces in enumerate(plan):
+            for (jr, off, ha, n, sp), ev in zip(pieces, issued.pop(r)):
+                cur.wait_event(ev)
+                yield jr, buf[off:off + n]
+            self.table.rehome_long_keys(buf, H + (r % 2) * A, H + (r % 2) * A + A, heap, H)
+            if r + 2 < len(plan):
+                evs["free"][r % 2].record(cur)  # slot r % 2 is free once round r's map and rehome ran
+                cs.wait_event(evs["free"][r % 2])
+                issued[r + 2] = issue(r + 2)
+
     def _stage_chunks(self, jobs, j0, j1):
         """Yield (job index range, device tensor) chunks, H2D overlapped with compute."""
         if self.device_input == "split":
             ids = self._split_ids(jobs, j0, j1)
             if not ids:
+                return
+            if self._streaming(ids):
+                yield from self._stage_streaming(jobs, j0, ids)
                 return
             cs = self.copy_stream
             key = (ids[0], len(ids))
@@ -768,6 +943,10 @@ class SPMDEngine:
             else:
                 n_claimed, overflow = self.table.stats()
                 e = None
+            sh = getattr(self, "_stream_heap", None)
+            if sh is not None and self.arena is getattr(self, "_stream_buf", None):
+                if int(ops.host_read(sh)[1]):
+                    raise RuntimeError("streaming map: the long-key heap is full (raise MR_STREAM_HEAP_MB)")
             bad = [k for k in range(nch) if e is not None and e[k]]
             if bad:
                 for k in bad:
@@ -962,7 +1141,7 @@ class SPMDEngine:
         return pend
 
     def _can_pipeline(self) -> bool:
-        return (self.copy_stream is not None and self.device_input == "split"
+        return (self.copy_stream is not None and self.device_input == "split" and not self._arena_cap()
                 and bool(modules.field(self.taskfn, "spmd_replicated_taskfn")))
 
     def _issue_next_map(self, jobs, j0, j1, q: int) -> None:

@@ -40,6 +40,14 @@ class Tunables:
     spmd_fault: str = _knob("MR_SPMD_FAULT", "",
                             "SPMD fault injection 'iteration:rank:raise|exit[:attempt]' at the start of that iteration")
     # -- device data plane
+    wc_config: int = _knob("MR_WC_CONFIG", 6,
+                           "word-count map kernel launch shape (csrc/hip/wordcount3.hip mr_wc_map3 config: "
+                           "0-5 per-lane token walks, 6-9 dense token lists)")
+    arena_cap_mb: float = _knob("MR_ARENA_CAP_MB", 0.0,
+                                "SPMD: cap of a rank's HBM input arena, MiB (0 = the rank's whole input); a larger "
+                                "input is mapped in rounds through a ring of two arenas of this size")
+    stream_heap_mb: float = _knob("MR_STREAM_HEAP_MB", 64.0,
+                                  "SPMD streaming rounds: HBM heap for the bytes of distinct long keys, MiB")
     fused_tail: bool = _knob("MR_FUSED_TAIL", True, "fused reduce-side tail kernels (tail.hip)")
     native_tail: bool = _knob("MR_NATIVE_TAIL", True, "queue the whole tail from one native call (mr_tail_run)")
     graphs: bool = _knob("MR_GRAPHS", False, "replay the W=1 tail as a hipGraph (stalls the copy stream: off)")

@@ -46,7 +46,7 @@ def test_wordcount_map_unaligned_and_chunks(gpu):
         assert _wc_dict(hi, lo, val, rep, tt) == _naive(text)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_wordcount_map3_configs_match_naive(gpu, cfg):
     """Every v3 launch shape (threads / LDS slots / tiles per chunk) on tricky
     bytes (long tokens crossing tiles, all whitespace kinds, NULs), aligned and

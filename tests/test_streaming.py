@@ -1,0 +1,100 @@
+"""Inputs larger than the HBM arena: with
+``arena_cap_mb`` a rank's splits are mapped in rounds through a ring of two
+capped arenas (round r+1's copies landing while round r maps) and the bytes of
+the long keys each round introduces move to a persistent key heap; with a
+WindowedSplitStore the host side is out of core too (split files read per
+round into two pinned windows).  Results must equal a naive count."""
+import os
+from collections import Counter
+
+import pytest
+
+from test_exactness import colliding_text
+
+M = "lua_mapreduce_1_amd.models.wordcount"
+
+
+def _splits():
+    from lua_mapreduce_1_amd.utils.corpus import europarl_like
+    return (europarl_like(seed=5, lines=24000, words=360000, vocab_size=4000, split_lines=500)
+            + [colliding_text(3 + i, ntok=2500, nlong=200) for i in range(3)])
+
+
+def _run(store, device, cap_mb=0.4, n=None):
+    from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine
+    from lua_mapreduce_1_amd.runtime import codec
+    eng = SPMDEngine(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M, arena_cap_mb=cap_mb,
+                          init_args={"nsplits": n or len(store), "num_reducers": 4}), split_store=store, device=device)
+    res = eng.run_iteration()
+    assert eng._streaming(eng._split_ids(eng._jobs(), 0, len(store)))
+    return {k: v[0] for _n, c in eng.gather_results(res) for k, v in codec.iter_columnar(c)}, eng
+
+
+def _want(splits):
+    return dict(Counter(w.decode("utf-8", "surrogateescape") for s in splits for w in s.split()))
+
+
+def _files(tmp_path, splits):
+    paths = []
+    for i, s in enumerate(splits):
+        p = tmp_path / f"s{i:03d}.txt"
+        p.write_bytes(s)
+        paths.append(str(p))
+    return paths
+
+
+@pytest.mark.parametrize("long_bits", [None, 3])
+def test_streaming_rounds_cpu(long_bits):
+    from lua_mapreduce_1_amd.ops import keys as K
+    from lua_mapreduce_1_amd.parallel.spmd import SplitStore
+    splits = _splits()
+    K.set_long_hash_bits(long_bits)
+    try:
+        got, _ = _run(SplitStore(splits, pin=False), "cpu")
+    finally:
+        K.set_long_hash_bits(None)
+    assert got == _want(splits)
+
+
+def test_windowed_out_of_core_cpu(tmp_path):
+    from lua_mapreduce_1_amd.parallel.spmd import WindowedSplitStore
+    splits = _splits()
+    st = WindowedSplitStore(_files(tmp_path, splits), window_mb=0.5, pin=False)
+    got, _ = _run(st, "cpu")
+    assert got == _want(splits)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("long_bits", [None, 3])
+def test_streaming_rounds_gpu(gpu, long_bits):
+    from lua_mapreduce_1_amd.ops import keys as K
+    from lua_mapreduce_1_amd.parallel.spmd import SplitStore
+    splits = _splits()
+    K.set_long_hash_bits(long_bits)
+    try:
+        got, eng = _run(SplitStore(splits), gpu)
+        assert eng.arena.is_cuda
+        # a second iteration reuses the ring and the (reset) heap
+        res = eng.run_iteration()
+    finally:
+        K.set_long_hash_bits(None)
+    assert got == _want(splits) and res.total_value == sum(_want(splits).values())
+
+
+@pytest.mark.gpu
+def test_windowed_out_of_core_gpu(gpu, tmp_path):
+    from lua_mapreduce_1_amd.parallel.spmd import WindowedSplitStore
+    splits = _splits()
+    st = WindowedSplitStore(_files(tmp_path, splits), window_mb=0.5)
+    got, _ = _run(st, gpu)
+    assert got == _want(splits)
+
+
+@pytest.mark.gpu
+def test_streaming_key_heap_full_raises(gpu, monkeypatch):
+    import dataclasses
+    from lua_mapreduce_1_amd.parallel import spmd as S
+    monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(S.TUNABLES, stream_heap_mb=0.07))
+    splits = [colliding_text(40 + i, ntok=20000, nlong=3000) for i in range(4)]
+    with pytest.raises(RuntimeError, match="heap is full"):
+        _run(S.SplitStore(splits), gpu, cap_mb=1.0)
