@@ -132,6 +132,21 @@ def ensure_corpus(d: str, seed: int, lines: int, words: int) -> None:
     print(f"# corpus generated in {time.time() - t0:.1f}s -> {d}", file=sys.stderr, flush=True)
 
 
+def load_corpus(seed: int = 1234, lines: int = 0, words: int = 0, *_unused) -> list:
+    """The synthetic corpus's splits as a list of bytes (generated and cached
+    as the benchmark does; 0 = the Europarl shape).  For tools/."""
+    import numpy as np
+    from lua_mapreduce_1_amd.utils import corpus
+    lines = lines or corpus.EUROPARL_LINES
+    words = words or corpus.EUROPARL_WORDS
+    d = corpus_dir(seed, lines, words)
+    ensure_corpus(d, seed, lines, words)
+    off = np.load(os.path.join(d, "off.npy"))
+    with open(os.path.join(d, "blob.bin"), "rb") as f:
+        blob = f.read()
+    return [blob[off[i]:off[i + 1]] for i in range(off.size - 1)]
+
+
 def truth_counts(d: str) -> dict:
     import numpy as np
     voff = np.load(os.path.join(d, "vocab_off.npy"))
