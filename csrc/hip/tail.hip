@@ -6,9 +6,10 @@
 //
 // The unfused tail was ~28 short launches; at small per-rank inputs (8-GPU
 // strong scaling) the drain/fill between dependent kernels dominated.  Here:
-//   tail_compact : table -> dense rows + FNV-1 partition + composite sort key
+//   compaction   : table -> dense rows + FNV-1 partition + composite sort key
 //                  (part << 56 | hi >> 8) + the 8 digit histograms of that key
-//                  (so the sort skips its histogram pass) + partition counts;
+//                  (so the sort skips its histogram pass) + partition counts
+//                  (mr_tail_compact: count / scatter / histogram launches);
 //   [onesweep passes, sort.hip]
 //   tail_gather  : rows reordered by the sort permutation + key lengths;
 //   [tie fix-up, scan, key-byte gather: existing kernels]
@@ -22,7 +23,6 @@ namespace mr {
 namespace tl {
 
 constexpr int T = 256;
-constexpr int ITEMS = 4;  // 4096-slot blocks left most CUs idle on a reduce-side table (64 blocks)
 
 __device__ __forceinline__ u32 key_fnv(u64 h, u64 l, u64 r, const u8* src, u32* len_out) {
   u32 f = FNV_OFFSET;
@@ -39,70 +39,104 @@ __device__ __forceinline__ u32 key_fnv(u64 h, u64 l, u64 r, const u8* src, u32* 
   return f;
 }
 
-__global__ void __launch_bounds__(T) tail_compact_kernel(GTab g, u64 cap, u32 nparts, const u8* __restrict__ src,
-                                                         u64* __restrict__ out_hi, u64* __restrict__ out_lo,
-                                                         long long* __restrict__ out_val, u64* __restrict__ out_rep,
-                                                         u32* __restrict__ out_part, u64* __restrict__ out_c,
-                                                         unsigned long long* __restrict__ counter,
-                                                         u32* __restrict__ ghist /*[8][256]*/,
-                                                         long long* __restrict__ pcount /*[nparts]*/) {
-  __shared__ u32 sh[T];
+// Compaction of a table's occupied slots into dense rows, in launches sized
+// for parallelism (one slot per thread; the first version gave each thread 4-16
+// slots and one block-wide scan, so a 1 M-slot table ran ONE wave per SIMD:
+// 50-73 us for 0.27 M keys, profiles/r2/tail):
+//   tail_count_kernel   : occupied slots per block -> bcount[block]
+//   tail_scatter_kernel : block base = sum of bcount[0..block) (read from L2),
+//                         wave ballots for the offsets inside the block, then
+//                         the row (partition, composite key) of each slot
+//   tail_hist_kernel    : the 8 digit histograms of the dense composite keys
+//                         (and partition counts)
+constexpr int CT = 512;  // compaction threads per block (one slot each)
+constexpr int HIST_BLOCKS = 64;
+
+__global__ void __launch_bounds__(CT) tail_count_kernel(const u64* __restrict__ tag, u64 cap, u32* __restrict__ bcount) {
+  __shared__ u32 wc[CT / 64];
+  const u64 i = (u64)blockIdx.x * CT + threadIdx.x;
+  const bool o = i < cap && tag[i] != 0;
+  const u64 m = __ballot(o);
+  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = (u32)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u32 c = 0;
+#pragma unroll
+    for (int w = 0; w < CT / 64; ++w) c += wc[w];
+    bcount[blockIdx.x] = c;
+  }
+}
+
+__global__ void __launch_bounds__(CT) tail_scatter_kernel(GTab g, u64 cap, u32 nparts, const u8* __restrict__ src,
+                                                          u64* __restrict__ out_hi, u64* __restrict__ out_lo,
+                                                          long long* __restrict__ out_val, u64* __restrict__ out_rep,
+                                                          u32* __restrict__ out_part, u64* __restrict__ out_c,
+                                                          unsigned long long* __restrict__ counter,
+                                                          const u32* __restrict__ bcount) {
+  __shared__ u32 red[CT / 64];
+  __shared__ u32 wc[CT / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  u32 acc = 0;
+  for (u32 j = t; j < blockIdx.x; j += CT) acc += bcount[j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  const u64 i = (u64)blockIdx.x * CT + t;
+  const bool occ = i < cap && g.tag[i] != 0;
+  const u64 m = __ballot(occ);
+  if (lane == 0) {
+    red[wave] = acc;
+    wc[wave] = (u32)__popcll(m);
+  }
+  __syncthreads();
+  u64 o = 0, mine = 0;
+#pragma unroll
+  for (int w = 0; w < CT / 64; ++w) {
+    o += red[w];
+    o += w < wave ? wc[w] : 0u;
+    mine += wc[w];
+  }
+  if (blockIdx.x == gridDim.x - 1 && t == 0) {
+    u64 tot = 0;
+#pragma unroll
+    for (int w = 0; w < CT / 64; ++w) tot += red[w];
+    *counter = tot + mine;  // number of rows
+  }
+  if (!occ) return;
+  o += (u64)__popcll(m & ((1ull << lane) - 1ull));
+  const u64 h = g.hi[i], l = g.lo[i], r = g.rep[i];
+  u32 len;
+  const u32 f = key_fnv(h, l, r, src, &len);
+  const u32 p = nparts ? f % nparts : f;
+  out_hi[o] = h;
+  out_lo[o] = l;
+  out_val[o] = g.val[i];
+  out_rep[o] = r;
+  out_part[o] = p;
+  out_c[o] = ((u64)p << 56) | (h >> 8);
+}
+
+// Digit histograms of the dense composite keys: LDS counts per block, then
+// one global atomic per non-empty bin (few blocks: at most HIST_BLOCKS x 2048
+// adds, each bin's chain HIST_BLOCKS long).  Digit 7 is the partition: its
+// totals also go to pcount.
+__global__ void __launch_bounds__(T) tail_hist_kernel(const u64* __restrict__ c, u64 n, u32* ghist, u32 nparts,
+                                                      long long* pcount) {
   __shared__ u32 hist[8][256];
-  __shared__ u32 pc[256];
-  __shared__ unsigned long long base;
   const int t = threadIdx.x;
 #pragma unroll
   for (int b = 0; b < 8; ++b) hist[b][t] = 0;
-  pc[t] = 0;
-  const u64 b0 = (u64)blockIdx.x * T * ITEMS;
-  u32 occ = 0, n = 0;
-#pragma unroll
-  for (int k = 0; k < ITEMS; ++k) {
-    const u64 i = b0 + (u64)k * T + t;
-    const bool o = i < cap && g.tag[i] != 0;
-    occ |= (o ? 1u : 0u) << k;
-    n += o ? 1u : 0u;
-  }
-  sh[t] = n;
   __syncthreads();
-  for (int o = 1; o < T; o <<= 1) {
-    const u32 y = t >= o ? sh[t - o] : 0u;
-    __syncthreads();
-    sh[t] += y;
-    __syncthreads();
-  }
-  if (t == T - 1) base = sh[T - 1] ? atomicAdd(counter, (unsigned long long)sh[T - 1]) : 0ull;
-  __syncthreads();
-  u64 o = base + sh[t] - n;
+  for (u64 i = (u64)blockIdx.x * T + t; i < n; i += (u64)gridDim.x * T) {
+    const u64 x = c[i];
 #pragma unroll
-  for (int k = 0; k < ITEMS; ++k) {
-    if (occ & (1u << k)) {
-      const u64 i = b0 + (u64)k * T + t;
-      const u64 h = g.hi[i], l = g.lo[i], r = g.rep[i];
-      u32 len;
-      const u32 f = key_fnv(h, l, r, src, &len);
-      const u32 p = nparts ? f % nparts : f;
-      const u64 c = ((u64)p << 56) | (h >> 8);
-      out_hi[o] = h;
-      out_lo[o] = l;
-      out_val[o] = g.val[i];
-      out_rep[o] = r;
-      out_part[o] = p;
-      out_c[o] = c;
-      // digit 7 of c is the partition: its histogram is pc (no second set of
-      // same-address LDS atomics on the few partition bins)
-#pragma unroll
-      for (int b = 0; b < 7; ++b) atomicAdd(&hist[b][(c >> (8 * b)) & 0xFF], 1u);
-      atomicAdd(&pc[p & 255], 1u);
-      ++o;
-    }
+    for (int b = 0; b < 8; ++b) atomicAdd(&hist[b][(x >> (8 * b)) & 0xFF], 1u);
   }
   __syncthreads();
 #pragma unroll
-  for (int b = 0; b < 7; ++b)
+  for (int b = 0; b < 8; ++b)
     if (hist[b][t]) atomicAdd(&ghist[b * 256 + t], hist[b][t]);
-  if (pc[t]) atomicAdd(&ghist[7 * 256 + t], pc[t]);
-  if ((u32)t < nparts && pc[t]) atomicAdd((unsigned long long*)&pcount[t], (unsigned long long)pc[t]);
+  if (pcount && (u32)t < nparts && hist[7][t])
+    atomicAdd((unsigned long long*)&pcount[t], (unsigned long long)hist[7][t]);
 }
 
 __global__ void tail_gather_kernel(const u32* __restrict__ perm, u64 n, const u64* __restrict__ hi,
@@ -154,10 +188,17 @@ extern "C" {
 
 u64 mr_tail_pack_bytes(u64 n, u32 nparts) { return 8 * n + (((4 * (n + 1)) + 7) & ~7ull) + 8 * (u64)nparts + 8; }
 
+// Bytes of the compaction scratch (`bhist`) of mr_tail_compact: per-block
+// slot counts.
+u64 mr_tail_bhist_bytes(u64 cap) { return ((cap + tl::CT - 1) / tl::CT * 4 + 255) & ~255ull; }
+
+// Occupied slots -> dense rows (+ partition, composite key).  With ghist: its
+// 8 digit histograms (+ partition counts into pcount); n = the number of
+// occupied slots (host-known: it sizes the histogram grid).
 int mr_tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, u32 nparts,
                     const void* src, void* out_hi, void* out_lo, void* out_val, void* out_rep, void* out_part,
-                    void* out_c, void* counter, void* ghist, void* pcount, hipStream_t s) {
-  if (nparts > 256) return -1;
+                    void* out_c, void* counter, void* ghist, void* pcount, void* bhist, u64 n, hipStream_t s) {
+  if (nparts > 256 || bhist == nullptr) return -1;
   GTab g;
   g.tag = (u64*)tag;
   g.hi = (u64*)hi;
@@ -167,13 +208,20 @@ int mr_tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* c
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
   g.src = nullptr;
-  const u64 nb = (cap + tl::T * tl::ITEMS - 1) / (tl::T * tl::ITEMS);
-  hipLaunchKernelGGL(tl::tail_compact_kernel, dim3((unsigned)nb), dim3(tl::T), 0, s, g, cap, nparts, (const u8*)src,
+  const u64 nb = (cap + tl::CT - 1) / tl::CT;
+  u32* bcount = (u32*)bhist;
+  hipLaunchKernelGGL(tl::tail_count_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, (const u64*)tag, cap, bcount);
+  hipLaunchKernelGGL(tl::tail_scatter_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, g, cap, nparts, (const u8*)src,
                      (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
-                     (unsigned long long*)counter, (u32*)ghist, (long long*)pcount);
+                     (unsigned long long*)counter, (const u32*)bcount);
+  if (ghist != nullptr && n > 0) {
+    u64 hb = (n + 4 * tl::T - 1) / (4 * tl::T);
+    if (hb > (u64)tl::HIST_BLOCKS) hb = tl::HIST_BLOCKS;
+    hipLaunchKernelGGL(tl::tail_hist_kernel, dim3((unsigned)hb), dim3(tl::T), 0, s, (const u64*)out_c, n, (u32*)ghist,
+                       nparts, (long long*)pcount);
+  }
   return (int)hipGetLastError();
 }
-
 int mr_tail_gather(const void* perm, u64 n, const void* hi, const void* lo, const void* val, const void* rep,
                    const void* part, void* o_hi, void* o_lo, void* o_val, void* o_rep, void* o_part, void* o_len,
                    hipStream_t s) {
@@ -221,19 +269,20 @@ int mr_d2h_async(void* host_dst, const void* src, u64 nbytes, hipStream_t s);
 enum TailBuf : int {
   TB_HI0, TB_LO0, TB_VAL0, TB_REP0, TB_C, TB_PART0, TB_ZERO /* counter|ghist|pcount|sort ctrs|err|bad */,
   TB_K0, TB_K1, TB_P0, TB_P1, TB_GRAN, TB_HI, TB_LO, TB_VAL, TB_REP, TB_PART, TB_LN, TB_OFF, TB_PARTIALS,
-  TB_BLOB, TB_PACKED, TB_COUNT
+  TB_BLOB, TB_PACKED, TB_BHIST, TB_COUNT
 };
 // TB_ZERO sub-layout (bytes): counter u64 @0 | ghist u32[2048] @8 | pcount i64[256] @8200 |
 // sort tile counters u32[64] @10248 | sort err u32 @10504 | bad u32 @10508
 constexpr u64 TZ_GHIST = 8, TZ_PCOUNT = 8200, TZ_TILES = 10248, TZ_ERR = 10504, TZ_BAD = 10508, TZ_BYTES = 10512;
 
-u64 mr_tail_ws_layout(u64 n, u32 nparts, u64 blob_cap, u64* off) {
+u64 mr_tail_ws_layout(u64 n, u32 nparts, u64 blob_cap, u64 cap, u64* off) {
   (void)nparts;
   const u64 m = n ? n : 1;
   const u64 tiles = mr_onesweep_tiles(m);
   const u64 sz[TB_COUNT] = {8 * m, 8 * m, 8 * m, 8 * m, 8 * m, 4 * m, TZ_BYTES, 8 * m, 8 * m, 4 * m, 4 * m,
                             tiles * 256 * 8, 8 * m, 8 * m, 8 * m, 8 * m, 4 * m, 8 * m, 8 * (m + 1),
-                            8 * mr_scan_partials_len(m), blob_cap ? blob_cap : 1, mr_tail_pack_bytes(m, 256)};
+                            8 * mr_scan_partials_len(m), blob_cap ? blob_cap : 1, mr_tail_pack_bytes(m, 256),
+                            mr_tail_bhist_bytes(cap)};
   u64 o = 0;
   for (int i = 0; i < TB_COUNT; ++i) {
     off[i] = o;
@@ -252,14 +301,14 @@ int mr_tail_run(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl,
                 hipStream_t s) {
   if (nparts > 256) return -1;
   u64 off[TB_COUNT];
-  mr_tail_ws_layout(n, nparts, blob_cap, off);
+  mr_tail_ws_layout(n, nparts, blob_cap, cap, off);
   u8* w = (u8*)ws;
   auto P = [&](int b) { return (void*)(w + off[b]); };
   u8* z = w + off[TB_ZERO];
   int rc = (int)hipMemsetAsync(z, 0, TZ_BYTES, s);
   if (rc) return rc;
   rc = mr_tail_compact(tag, hi, lo, val, rep, ctrl, cap, nparts, src, P(TB_HI0), P(TB_LO0), P(TB_VAL0), P(TB_REP0),
-                       P(TB_PART0), P(TB_C), z, z + TZ_GHIST, z + TZ_PCOUNT, s);
+                       P(TB_PART0), P(TB_C), z, z + TZ_GHIST, z + TZ_PCOUNT, P(TB_BHIST), n, s);
   if (rc) return rc;
   // 8 onesweep passes over the composite key (ghist from tail_compact)
   const void* kin = P(TB_C);

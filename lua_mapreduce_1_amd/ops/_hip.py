@@ -81,7 +81,8 @@ _SIGS = {
     "mr_ts_unsorted": [_p, _p, _u64, _p, _p],
     "mr_pack_by_dest": [_p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, ctypes.c_longlong, _p, _p, _i32, _p],
     "mr_fix_loc": [_p, _u64, _p, _p, _u32, _p, _p],
-    "mr_tail_compact": [_p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
+    "mr_tail_compact": [_p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _u64, _p],
+    "mr_tail_bhist_bytes": [_u64],
     "mr_tail_gather": [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "mr_tail_pack": [_p, _p, _u64, _p, _u32, _p, _p, _p, _p],
     "mr_sort_debug_fail": [_i32],
@@ -89,12 +90,13 @@ _SIGS = {
     "mr_set_long_mask_keyops": [_u64],
     "mr_set_long_mask_invidx": [_u64],
     "mr_tail_pack_bytes": [_u64, _u32],
-    "mr_tail_ws_layout": [_u64, _u32, _u64, ctypes.POINTER(ctypes.c_uint64)],
+    "mr_tail_ws_layout": [_u64, _u32, _u64, _u64, ctypes.POINTER(ctypes.c_uint64)],
     "mr_table_reset": [_p, _p, _p, _p, _u64, ctypes.c_longlong, _p],
     "mr_table_rehome": [_p, _p, _p, _u64, _p, _u64, _u64, _p, _u64, _p],
     "mr_scan_partials_len": [_u64],
 }
-_RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout"}
+_RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
+                "mr_tail_bhist_bytes"}
 
 
 def lib():

@@ -321,9 +321,10 @@ def finalize_table_device(table, n: int, src, nparts: int) -> dict:
     part0 = z(torch.int32)
     small = torch.zeros(1 + 2048 // 2 + nparts, dtype=torch.int64, device=d)  # counter | ghist (u32) | pcount
     counter, ghist, pcount = small[:1], small[1:1 + 1024].view(torch.int32), small[1 + 1024:]
+    bhist = torch.empty(int(_hip.lib().mr_tail_bhist_bytes(table.cap)), dtype=torch.uint8, device=d)
     _hip.call("mr_tail_compact", *table._gtab(), table.cap, nparts, _hip.ptr(src), _hip.ptr(hi0), _hip.ptr(lo0),
               _hip.ptr(val0), _hip.ptr(rep0), _hip.ptr(part0), _hip.ptr(c), _hip.ptr(counter), _hip.ptr(ghist),
-              _hip.ptr(pcount), s)
+              _hip.ptr(pcount), _hip.ptr(bhist), n, s)
     perm, cs = ops.sort_keys([c], return_keys=True, ghist=ghist)
     hi, lo, val, rep, ln = z(torch.int64), z(torch.int64), z(torch.int64), z(torch.int64), z(torch.int64)
     part = z(torch.int32)
@@ -354,22 +355,24 @@ def finalize_table_device(table, n: int, src, nparts: int) -> dict:
 
 _TAIL_WS: dict = {}  # device -> (workspace uint8 tensor, {layout key: (offsets, views)})
 _TB = {name: i for i, name in enumerate(
-    "HI0 LO0 VAL0 REP0 C PART0 ZERO K0 K1 P0 P1 GRAN HI LO VAL REP PART LN OFF PARTIALS BLOB PACKED".split())}
+    "HI0 LO0 VAL0 REP0 C PART0 ZERO K0 K1 P0 P1 GRAN HI LO VAL REP PART LN OFF PARTIALS BLOB PACKED BHIST".split())}
 
 
-def _tail_ws(d, n: int, nparts: int, blob_cap: int):
-    """Workspace of mr_tail_run (csrc/hip/tail.hip) and int64 views of the
-    buffers the host half reads, cached per (n, nparts, blob capacity)."""
+def _tail_ws(d, n: int, nparts: int, blob_cap: int, cap: int):
+    """Workspace of mr_tail_run (csrc/hip/tail.hip) for a table of ``cap``
+    slots and int64 views of the buffers the host half reads, cached per (n,
+    nparts, blob capacity, table capacity)."""
     import ctypes
     from ..ops import _hip
     lib = _hip.lib()
     offs = (ctypes.c_uint64 * len(_TB))()
-    need = int(lib.mr_tail_ws_layout(ctypes.c_uint64(n), ctypes.c_uint32(nparts), ctypes.c_uint64(blob_cap), offs))
+    need = int(lib.mr_tail_ws_layout(ctypes.c_uint64(n), ctypes.c_uint32(nparts), ctypes.c_uint64(blob_cap),
+                                     ctypes.c_uint64(cap), offs))
     ws, views = _TAIL_WS.get(d, (None, {}))
     if ws is None or ws.numel() < need:
         ws = torch.zeros(need + need // 4, dtype=torch.uint8, device=d)  # zeroed once: sort look-back granules
         views = {}
-    key = (n, nparts, blob_cap)
+    key = (n, nparts, blob_cap, cap)
     v = views.get(key)
     if v is None:
         o = list(offs)
@@ -402,12 +405,14 @@ def compact_partition(table, n: int, src, nparts: int):
               "part": torch.empty(c, dtype=torch.int32, device=d),
               "small": torch.empty(1 + 1024 + 256, dtype=torch.int64, device=d)}
         _CP_WS[d] = ws
+    nbh = int(_hip.lib().mr_tail_bhist_bytes(table.cap))
+    if ws.get("bhist") is None or ws["bhist"].numel() < nbh:
+        ws["bhist"] = torch.empty(nbh, dtype=torch.uint8, device=d)
     cols, part, small = ws["cols"], ws["part"], ws["small"]
-    small.zero_()
     hi, lo, val, rep, c = (cols[i, :n] for i in range(5))
     _hip.call("mr_tail_compact", *table._gtab(), table.cap, nparts, _hip.ptr(src), _hip.ptr(hi), _hip.ptr(lo),
               _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), _hip.ptr(c), _hip.ptr(small[:1]),
-              _hip.ptr(small[1:1025]), _hip.ptr(small[1025:]), _hip.stream(d))
+              None, None, _hip.ptr(ws["bhist"]), n, _hip.stream(d))  # no digit histograms on the send side
     return hi, lo, val, rep, part[:n]
 
 
@@ -418,7 +423,7 @@ def finalize_table_native(table, n: int, src, nparts: int) -> dict:
     from ..ops import _hip
     d = table.device
     cap = src.numel()
-    ws, v = _tail_ws(d, n, nparts, cap)
+    ws, v = _tail_ws(d, n, nparts, cap, table.cap)
     nb = int(_hip.lib().mr_tail_pack_bytes(n, nparts))
     hp = _POOL.get("pack", nb, torch.uint8)
     est = _BLOB_EST.get(d)
