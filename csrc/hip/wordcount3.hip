@@ -168,7 +168,9 @@ template <int T, int SLOTS, int TPC, bool DENSE = false>
 __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text, u64 nbytes, u64 rep_base, GTab g,
                                                     Ovf ovf, int aligned, int ablate) {
   // ablate (timing only, the table is then incomplete): 1 = no flush to HBM,
-  // 2 = tokenize + key packing only (no LDS combine, no flush)
+  // 2 = tokenize + key packing only (no LDS combine, no flush); flush variants:
+  // 3 = home-slot tag load only (no lo/hi loads), 4 = blind atomic adds to the
+  // home slots (no loads, no claims), 5 = the speculative loads only (no atomics)
   using L_t = Lds<T, SLOTS>;
   constexpr int TILE = L_t::TILE;
   constexpr int STAGED = L_t::STAGED;
@@ -320,7 +322,7 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
     __syncthreads();
   }
   if (stamp && t == 0) stamp[1] = wall_clock64();
-  if (ablate) return;
+  if (ablate == 1 || ablate == 2) return;
   // flush: each thread folds its PER slots.  The common case is a key already
   // in the HBM table at its home slot, so tag/lo/hi of every home slot are
   // loaded speculatively in ONE batch (one memory round trip instead of a
@@ -340,11 +342,17 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
     ktag[k] = gtab_tag(khi[k], klo[k]);
     kslot[k] = gtab_home(ktag[k], g.mask);
   }
+  if (ablate == 4) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (kcnt[k]) fold_value(&g.val[kslot[k]], (long long)kcnt[k], OP_SUM);
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (kcnt[k]) {
       gt[k] = ld_agent(&g.tag[kslot[k]]);
-      if (!gtab_tag_exact(ktag[k])) {
+      if (!gtab_tag_exact(ktag[k]) && ablate != 3) {
         gl[k] = ld_agent(&g.lo[kslot[k]]);
         gh[k] = ld_agent(&g.hi[kslot[k]]);
       } else {
@@ -352,6 +360,14 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
         gh[k] = khi[k];
       }
     }
+  }
+  if (ablate == 5) {
+    u64 x = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (kcnt[k]) x ^= gt[k] ^ gl[k] ^ gh[k];
+    if (x == 0x123456789ull) ovf.counter[1] = x;  // keep the loads live
+    return;
   }
   // new keys whose home slot is empty are claimed in a batch too: all CASes,
   // one wait, all payload stores, ONE vmcnt drain, all publishing stores
