@@ -673,12 +673,14 @@ int mr_copy_to_host(const void* src, void* host_dst, const void* nelem, u64 elem
   return (int)hipGetLastError();
 }
 
-// Device -> pinned-host download on stream s.  Default: shader stores over
-// PCIe (copy_to_host_kernel).  An SDMA download (hipMemcpyAsync) is queued
-// behind every host->device copy issued before it on ANY stream — the engine
-// is shared — so with the next iterations' input copies in flight a 1 MB
-// result download finished 2 ms late instead of after 0.1 ms
-// (tools/d2h_queue_probe.py, profiles/r1/d2h_queue_probe.log).  Mode 1 = SDMA.
+// Device -> pinned-host download on stream s.  Mode 1 (the framework's
+// default, MR_D2H=sdma): an SDMA copy (hipMemcpyAsync).  Mode 0 (MR_D2H=kernel):
+// shader stores over PCIe (copy_to_host_kernel), chosen in round 1 because an
+// SDMA download queued behind the next iterations' input copies finished 2 ms
+// late (tools/d2h_queue_probe.py, profiles/r1/d2h_queue_probe.log); with the
+// round-2 pipeline the host-staged bench is the same either way and the
+// HBM-resident one 0.19 ms faster with SDMA, whose downloads take no CU time
+// from the next map (profiles/r2/d2h_ab/).
 static int g_d2h_mode = 0;
 void mr_set_d2h_mode(int mode) { g_d2h_mode = mode; }
 

@@ -116,7 +116,7 @@ def lib():
         L.mr_set_d2h_mode.restype = None
         L.mr_host_alloc_coherent.argtypes = [_u64]
         L.mr_host_alloc_coherent.restype = _p
-        # downloads: shader stores by default, SDMA with MR_D2H=sdma (see sort.hip mr_d2h_async)
+        # downloads: SDMA by default, shader stores with MR_D2H=kernel (see sort.hip mr_d2h_async)
         L.mr_set_d2h_mode(1 if TUNABLES.d2h == "sdma" else 0)
         _LIB = L
     return _LIB

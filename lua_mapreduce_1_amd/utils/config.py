@@ -54,7 +54,10 @@ class Tunables:
     pipeline: bool = _knob("MR_PIPELINE", True, "bench/proxies: map of iteration i+1 overlaps the tail of i")
     prefetch_single: bool = _knob("MR_PREFETCH_SINGLE", True, "prefetched inputs: one DMA per iteration")
     prefetch_late: bool = _knob("MR_PREFETCH_LATE", False, "issue prefetches after the tail instead of first")
-    d2h: str = _knob("MR_D2H", "kernel", "downloads: 'kernel' (shader stores) or 'sdma' (queued behind H2D)")
+    d2h: str = _knob("MR_D2H", "sdma",
+                     "downloads: 'sdma' (DMA engine) or 'kernel' (shader stores into pinned memory: CU time that "
+                     "competes with the next map; resident bench 2.93 vs 2.74 ms, staged equal, "
+                     "profiles/r2/d2h_ab/)")
     spin_us: float = _knob("MR_SPIN_US", 2000.0, "host spin on completion words before hipStreamSynchronize, us")
     force_shuffle: bool = _knob("MR_FORCE_SHUFFLE", False,
                                 "SPMD: run the W>1 shuffle (pack, count exchange, all-to-all, receive insert) also "
