@@ -1239,15 +1239,15 @@ class SPMDEngine:
 
     def _finish_iteration(self, res, T, t_start, t0, jobs, recs, j0, j1, ahead, q) -> IterationResult:
         prefetch_next = ahead > 0
-        trace.push("mr.map.wait")
-        n_claimed, overflow = self._map_sync(jobs, recs, j0, j1)  # synchronises the map phase
-        trace.pop()
-        T["map"] = time.time() - t0
-        timer = self._timer()
         pipelined = prefetch_next and self.pipeline and self._can_pipeline()
-        # the next iteration's map is queued right after this iteration's first
-        # tail kernels: those get the GPU first, and the host queues the map
-        # while they run instead of in front of them
+        # When the next iteration's map is queued (MR_NEXT_MAP; "auto" =
+        # before_sync for HBM-resident input, after_tail otherwise): "after_tail"
+        # = right after this iteration's first tail kernels (W=1) / its count
+        # exchange (W>1), so those get the GPU first; "before_tail" = before
+        # the W=1 tail; "before_sync" = before this map's synchronisation, so
+        # with HBM-resident input two maps are queued back to back and the GPU
+        # never idles while the host syncs and issues (the tail's short kernels
+        # run beside the next map).
         next_map = [pipelined]
 
         def issue_next_map():
@@ -1255,6 +1255,16 @@ class SPMDEngine:
                 next_map[0] = False
                 with trace.range("mr.map.issue_next"):
                     self._issue_next_map(jobs, j0, j1, q)
+        when = TUNABLES.next_map
+        if when == "auto":
+            when = "before_sync" if self.resident else "after_tail"
+        if when == "before_sync":
+            issue_next_map()
+        trace.push("mr.map.wait")
+        n_claimed, overflow = self._map_sync(jobs, recs, j0, j1)  # synchronises the map phase
+        trace.pop()
+        T["map"] = time.time() - t0
+        timer = self._timer()
         t1 = time.time()
         if timer is not None:
             timer.mark("tail0")
@@ -1272,6 +1282,8 @@ class SPMDEngine:
             # -> downloads) is one replayed hipGraph once a table size repeats
             pend = self._graphed_tail(n_claimed, overflow, src)
         elif not sh and fused:
+            if when == "before_tail":
+                issue_next_map()
             pend = self._finalize_table(self.table, n_claimed, src)
             issue_next_map()
         elif sh and fused:
