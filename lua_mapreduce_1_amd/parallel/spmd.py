@@ -1144,17 +1144,21 @@ class SPMDEngine:
         return (self.copy_stream is not None and self.device_input == "split" and not self._arena_cap()
                 and bool(modules.field(self.taskfn, "spmd_replicated_taskfn")))
 
-    def _issue_next_map(self, jobs, j0, j1, q: int) -> None:
+    def _issue_next_map(self, jobs, j0, j1, q: int, gate=None) -> None:
         """Queue iteration q+1's map (same job list: the taskfn is pure) on its
         own arena, table and stream, then return to iteration q's.  Its table
         and stream were last used by iteration q-1, which has fully completed
-        (its results were downloaded)."""
+        (its results were downloaded).  ``gate``: an event the map (not the
+        table reset) waits for."""
         self._prefetch(jobs, j0, j1, q + 1)
         recs = self._new_records(jobs, j0, j1)
         self._use(q + 1)
         try:
-            with torch.cuda.stream(self.streams[self.tslot]):
+            st = self.streams[self.tslot]
+            with torch.cuda.stream(st):
                 self.table.reset()
+                if gate is not None:
+                    st.wait_event(gate)
                 t0 = time.time()
                 self._run_map(jobs, recs, j0, j1)
         finally:
@@ -1241,25 +1245,32 @@ class SPMDEngine:
         prefetch_next = ahead > 0
         pipelined = prefetch_next and self.pipeline and self._can_pipeline()
         # When the next iteration's map is queued (MR_NEXT_MAP; "auto" =
-        # before_sync for HBM-resident input, after_tail otherwise): "after_tail"
+        # chain for HBM-resident input, after_tail otherwise): "after_tail"
         # = right after this iteration's first tail kernels (W=1) / its count
         # exchange (W>1), so those get the GPU first; "before_tail" = before
         # the W=1 tail; "before_sync" = before this map's synchronisation, so
         # with HBM-resident input two maps are queued back to back and the GPU
         # never idles while the host syncs and issues (the tail's short kernels
-        # run beside the next map).
+        # run beside the next map); "chain" = the same, the next map gated on
+        # this one's completion (an event, no host round trip).
         next_map = [pipelined]
 
-        def issue_next_map():
+        def issue_next_map(gate=None):
             if next_map[0]:
                 next_map[0] = False
                 with trace.range("mr.map.issue_next"):
-                    self._issue_next_map(jobs, j0, j1, q)
+                    self._issue_next_map(jobs, j0, j1, q, gate)
         when = TUNABLES.next_map
         if when == "auto":
-            when = "before_sync" if self.resident else "after_tail"
-        if when == "before_sync":
-            issue_next_map()
+            when = "chain" if self.resident else "after_tail"
+        if when in ("before_sync", "chain") and next_map[0]:
+            gate = None
+            if when == "chain" and self.device.type == "cuda":
+                # "chain": the next map starts when this one ends (two maps
+                # sharing the GPU ran slower than one after the other)
+                gate = torch.cuda.Event()
+                gate.record()
+            issue_next_map(gate)
         trace.push("mr.map.wait")
         n_claimed, overflow = self._map_sync(jobs, recs, j0, j1)  # synchronises the map phase
         trace.pop()

@@ -55,9 +55,9 @@ class Tunables:
     next_map: str = _knob("MR_NEXT_MAP", "auto",
                           "pipelined iterations: when the next iteration's map is queued — 'after_tail' "
                           "(after this iteration's first tail kernels), 'before_tail', 'before_sync' "
-                          "(before this map's synchronisation), 'auto' = before_sync for HBM-resident input "
-                          "(bench 2.75 -> 2.50 ms), after_tail for host-staged input (5.30 vs 5.32-5.60 ms; "
-                          "profiles/r2/next_map/)")
+                          "(before this map's synchronisation), 'chain' (before the sync, gated on this map's "
+                          "completion by an event), 'auto' = chain for HBM-resident input, after_tail for "
+                          "host-staged input (profiles/r2/next_map/)")
     prefetch_single: bool = _knob("MR_PREFETCH_SINGLE", True, "prefetched inputs: one DMA per iteration")
     prefetch_late: bool = _knob("MR_PREFETCH_LATE", False, "issue prefetches after the tail instead of first")
     d2h: str = _knob("MR_D2H", "sdma",
