@@ -167,7 +167,8 @@ def sort_unique(keys: torch.Tensor, bits: int) -> torch.Tensor:
         s = _hip.stream(d)
         # keys-only radix sort (no permutation carried), then the fused
         # two-pass unique (per-tile head counts -> scan -> scatter)
-        _, sk = sort_keys([keys], bits=[bits], return_keys=True, keys_only=True)
+        # posting keys arrive in text order: a line's keys share their line digits
+        _, sk = sort_keys([keys], bits=[bits], return_keys=True, keys_only=True, runs=True)
         tiles = int(_hip.lib().mr_ii_unique_tiles(n))
         tc = torch.empty(tiles, dtype=torch.int32, device=d)
         _hip.call("mr_ii_unique_count", _hip.ptr(sk), n, _hip.ptr(tc), s)

@@ -76,6 +76,7 @@ _OVF_COUNTERS = 64
 _OVF_ENTRIES = 1 << 18
 _CTRL_SHARD0, _CTRL_STRIDE, _CTRL_SHARDS = 32, 32, 64  # csrc/hip/hashtab.h
 _CTRL_WORDS = _CTRL_SHARD0 + _CTRL_STRIDE * _CTRL_SHARDS
+_GHIST_RUNS = 0x100  # csrc/hip/sort.hip MR_GHIST_RUNS
 
 
 class HashTable:
@@ -503,7 +504,7 @@ def _sort_ws(d, n: int):
 
 def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None,
               return_keys: bool = False, ghist: torch.Tensor | None = None, from_bit: int = 0,
-              keys_only: bool = False):
+              keys_only: bool = False, runs: bool = False):
     """Stable permutation sorting rows by unsigned multi-word keys.
 
     ``words[0]`` is the most significant u64 word.  ``bits[j]`` limits the
@@ -514,8 +515,10 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None,
     (single word, GPU onesweep): only bits >= from_bit are sorted — rows equal
     in those bits keep their input order.  ``keys_only`` (single word, GPU
     onesweep): no permutation is carried (a third less traffic per pass);
-    returns ``(None, sorted keys)``.  GPU: LSD radix sort, one onesweep
-    launch per 8-bit digit (decoupled look-back, csrc/hip/sort.hip).
+    returns ``(None, sorted keys)``.  ``runs``: a hint that consecutive keys
+    share digits (e.g. posting keys in text order) — the digit histograms then
+    count each run once.  GPU: LSD radix sort, one onesweep launch per 8-bit
+    digit (decoupled look-back, csrc/hip/sort.hip).
     """
     n = words[0].numel()
     bits = bits or [64] * len(words)
@@ -558,7 +561,8 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None,
             else:
                 if pass_id:
                     ghist_ws.zero_()
-                _hip.call("mr_radix_ghist8", _hip.ptr(kin), n, _hip.ptr(ghist_ws), (nb + 7) // 8, s)
+                _hip.call("mr_radix_ghist8", _hip.ptr(kin), n, _hip.ptr(ghist_ws),
+                          (nb + 7) // 8 | (_GHIST_RUNS if runs else 0), s)
             ko = keys_only and len(words) == 1
             for shift in range(from_bit if len(words) == 1 else 0, nb, 8):
                 _EPOCH[0] = (_EPOCH[0] + 1) & 0xFFFFFF or 1

@@ -220,7 +220,7 @@ class ListPlane:
         if self.unique:
             return II.sort_unique(keys, bits)
         if keys.is_cuda:
-            _, sk = ops.sort_keys_checked([keys], bits=[bits], return_keys=True, keys_only=True)
+            _, sk = ops.sort_keys_checked([keys], bits=[bits], return_keys=True, keys_only=True, runs=True)
             return sk
         return torch.sort(keys).values
 

@@ -409,3 +409,32 @@ def test_h2d_pull_matches_copy(gpu):
     _hip.call("mr_h2d_pull", _hip.ptr(d), _hip.ptr(h), n, 512, _hip.stream(gpu))
     torch.cuda.synchronize()
     assert torch.equal(d.cpu(), h)
+
+
+@pytest.mark.parametrize("n,runs", [(1, True), (63, True), (64 * 1000 + 37, True), (3_000_001, True),
+                                    (3_000_001, False)])
+def test_radix_ghist8_matches_numpy(gpu, n, runs):
+    """Digit histograms (csrc/hip/sort.hip rs_ghist8_kernel, run-aggregated
+    per wave) against numpy: keys with long runs of equal digits (posting
+    keys in text order; runs crossing wave boundaries, a partial last wave)
+    and random keys."""
+    from lua_mapreduce_1_amd.ops import _hip
+    rng = np.random.default_rng(n)
+    if runs:
+        lens = rng.integers(1, 90, n // 3 + 2)
+        vals = rng.integers(0, 2**62, lens.size, dtype=np.int64)
+        k = np.repeat(vals, lens)[:n]
+        k[::7] ^= rng.integers(0, 256, k[::7].size)  # break some runs in the low digit only
+    else:
+        k = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64)
+    keys = torch.from_numpy(k).to(gpu)
+    for ndig in (8 | 0x100, 3 | 0x100, 8, 3):  # 0x100: run-aggregated (MR_GHIST_RUNS)
+        gh = torch.zeros(2048, dtype=torch.int32, device=gpu)
+        _hip.call("mr_radix_ghist8", _hip.ptr(keys), n, _hip.ptr(gh), ndig, _hip.stream(gpu))
+        ndig &= 0xFF
+        got = gh.cpu().numpy().reshape(8, 256)
+        ku = k.view(np.uint64)
+        for b in range(8):
+            want = np.bincount(((ku >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.int64), minlength=256) \
+                if b < ndig else np.zeros(256, np.int64)
+            assert np.array_equal(got[b], want), b
