@@ -632,27 +632,41 @@ extern "C" int mr_ii_insert_slots(void* tag, void* thi, void* tlo, void* val, vo
 }
 
 // ---------------------------------------------------------------------------
-// Segmented gather of posting lists into a new word order: output posting j
-// belongs to the word i with new_off[i] <= j < new_off[i+1] (binary search),
-// and comes from old_start[perm[i]] + (j - new_off[i]).  One thread per
-// posting: no per-word imbalance (a frequent word has millions of postings).
+// Segmented gather of posting lists into a new word order: word i of the
+// output is word perm[i] of the input (new_off: nw+1 output offsets).  Load
+// balanced by OUTPUT position: a block owns a fixed chunk of postings, finds
+// the word of its first posting with one binary search, then walks the words
+// that overlap its chunk, all threads copying each overlap (coalesced).  A
+// frequent word spans many blocks; a block spans many rare words.  (The first
+// version binary-searched the word of every posting: 19 dependent loads per
+// posting, 0.8 ms for 46 M postings.)
 namespace mr {
 namespace ii {
-__global__ void __launch_bounds__(256) ii_seg_gather_kernel(const u32* __restrict__ perm,
-                                                            const long long* __restrict__ old_start,
-                                                            const long long* __restrict__ new_off, u64 nw, u64 n,
-                                                            const int* __restrict__ src, int* __restrict__ dst) {
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
-    u64 a = 0, b = nw;  // largest i with new_off[i] <= j
+constexpr int SG_T = 256;
+constexpr u64 SG_CHUNK = 4096;
+__global__ void __launch_bounds__(SG_T) ii_seg_gather_kernel(const u32* __restrict__ perm,
+                                                             const long long* __restrict__ old_start,
+                                                             const long long* __restrict__ new_off, u64 nw, u64 n,
+                                                             const int* __restrict__ src, int* __restrict__ dst) {
+  __shared__ u64 s_w;
+  const u64 c0 = (u64)blockIdx.x * SG_CHUNK;
+  const u64 c1 = c0 + SG_CHUNK < n ? c0 + SG_CHUNK : n;
+  if (threadIdx.x == 0) {
+    u64 a = 0, b = nw;  // largest i with new_off[i] <= c0
     while (b - a > 1) {
       const u64 m = (a + b) >> 1;
-      if ((u64)new_off[m] <= j) a = m;
+      if ((u64)new_off[m] <= c0) a = m;
       else b = m;
     }
-    const u64 w = clamp_row(perm[a], nw);
-    const u64 k = (u64)old_start[w] + (j - (u64)new_off[a]);
-    dst[j] = src[clamp_row(k, n)];
+    s_w = a;
+  }
+  __syncthreads();
+  for (u64 w = s_w; w < nw; ++w) {
+    const u64 ws = (u64)new_off[w], we = (u64)new_off[w + 1];
+    if (ws >= c1) break;
+    const u64 a = ws > c0 ? ws : c0, b = we < c1 ? we : c1;
+    const u64 s0 = (u64)old_start[clamp_row(perm[w], nw)] + (a - ws);
+    for (u64 j = a + threadIdx.x; j < b; j += SG_T) dst[j] = src[clamp_row(s0 + (j - a), n)];
   }
 }
 }  // namespace ii
@@ -661,7 +675,8 @@ __global__ void __launch_bounds__(256) ii_seg_gather_kernel(const u32* __restric
 extern "C" int mr_ii_seg_gather(const void* perm, const void* old_start, const void* new_off, u64 nw, u64 n,
                                 const void* src, void* dst, hipStream_t s) {
   if (n == 0 || nw == 0) return 0;
-  hipLaunchKernelGGL(ii::ii_seg_gather_kernel, dim3(grid_n(n, 256, 16384)), dim3(256), 0, s, (const u32*)perm,
+  const u64 blocks = (n + ii::SG_CHUNK - 1) / ii::SG_CHUNK;
+  hipLaunchKernelGGL(ii::ii_seg_gather_kernel, dim3((unsigned)blocks), dim3(ii::SG_T), 0, s, (const u32*)perm,
                      (const long long*)old_start, (const long long*)new_off, nw, n, (const int*)src, (int*)dst);
   return (int)hipGetLastError();
 }
