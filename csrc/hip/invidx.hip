@@ -22,7 +22,13 @@
 //      vocabulary costs one HBM insert per distinct word, not per token;
 //      LDS misses (table 3/4 full) insert into HBM directly;
 //   4. newly claimed LDS slots get their global slot (one gtab_insert each);
-//   5. the tile's tokens are written with ONE atomic reservation per tile.
+//   5. the tile's tokens are written at their text-order positions: a token's
+//      output index = its chunk's token base (count_lines_tokens_kernel + an
+//      exclusive scan, before the launch) + the tokens before it in the chunk
+//      (block scans of per-thread token counts).  The posting array is thus in
+//      line order, and a STABLE radix sort of the word bits alone (sort_keys
+//      from_bit = doc_bits) yields (word, line) order: 3 passes for 21-bit word
+//      ids instead of 6 over (word, line).
 #include <hip/hip_runtime.h>
 #include "mr_common.h"
 #include "hashtab.h"
@@ -62,6 +68,7 @@ struct Lds {
   u32 tok_ref[MAX_TOK + 8];
   u16 tok_line[MAX_TOK + 8];  // line - the tile's first line (< TILE)
   u32 wave_nl[T / 64];
+  u32 wave_tok[T / 64];
   u32 ntok;
   u32 nclaimed;
   u32 tile_lines;
@@ -135,31 +142,51 @@ __device__ __forceinline__ int lds_find_or_claim(Lds& L, u64 hi, u64 lo, u32 rep
   return -1;
 }
 
-// Newlines per chunk (for the chunk line bases).
+// Newlines per chunk (for the chunk line bases) and, with out_tok, token
+// starts per chunk (a non-whitespace byte whose predecessor is whitespace or
+// the start of the text: exactly the tokens ii_map_kernel's chunk owns).
 __global__ void __launch_bounds__(256) count_newlines_kernel(const u8* __restrict__ text, u64 nbytes, u64 chunk,
-                                                             u32* __restrict__ out) {
+                                                             u32* __restrict__ out, u32* __restrict__ out_tok) {
   const u64 b0 = (u64)blockIdx.x * chunk;
   const u64 b1 = min(b0 + chunk, nbytes);
-  u32 c = 0;
+  u32 c = 0, ct = 0;
   for (u64 p = b0 + threadIdx.x * 16; p < b1; p += 256 * 16) {
     if (p + 16 <= b1 && ((uintptr_t)(text + p) & 15) == 0) {
       const uint4 q = *reinterpret_cast<const uint4*>(text + p);
       c += __builtin_popcount(mask16(q, 10u, false));
+      if (out_tok) {
+        const u32 m = mask16(q, 0, true);
+        const u32 prev = p == 0 ? 1u : (is_ws(text[p - 1]) ? 1u : 0u);
+        ct += __builtin_popcount(~m & ((m << 1) | prev) & 0xFFFFu);
+      }
     } else {
-      for (u64 k = p; k < min(p + 16, b1); ++k) c += text[k] == '\n';
+      for (u64 k = p; k < min(p + 16, b1); ++k) {
+        c += text[k] == '\n';
+        ct += !is_ws(text[k]) && (k == 0 || is_ws(text[k - 1]));
+      }
     }
   }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-  __shared__ u32 part[4];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    ct += __shfl_xor(ct, o);
+  }
+  __shared__ u32 part[4], tpart[4];
+  if ((threadIdx.x & 63) == 0) {
+    part[threadIdx.x >> 6] = c;
+    tpart[threadIdx.x >> 6] = ct;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) out[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+  if (threadIdx.x == 0) {
+    out[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+    if (out_tok) out_tok[blockIdx.x] = tpart[0] + tpart[1] + tpart[2] + tpart[3];
+  }
 }
 
 __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, u64 nbytes, u64 chunk_bytes,
-                                                   u64 rep_base, const u32* __restrict__ chunk_line_base, GTab g,
-                                                   u32 doc_bits, u64* __restrict__ out,
-                                                   unsigned long long* __restrict__ out_counter, u64 out_cap,
+                                                   u64 rep_base, const u32* __restrict__ chunk_line_base,
+                                                   const u32* __restrict__ chunk_tok_base, GTab g, u32 doc_bits,
+                                                   u64* __restrict__ out,
+                                                   const unsigned long long* __restrict__ out_counter, u64 out_cap,
                                                    u32* __restrict__ err) {
   __shared__ __attribute__((aligned(16))) Lds L;
   const int t = threadIdx.x;
@@ -180,6 +207,9 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
     L.ws[WSW - 1] = 0xFFFFFFFFu;
   }
   u32 line_base = chunk_line_base[blockIdx.x];
+  // this launch's first output slot (advanced after the launch) + the tokens
+  // of the chunks before this one
+  u64 tok_next = (u64)*out_counter + chunk_tok_base[blockIdx.x];
   u16* ws16 = reinterpret_cast<u16*>(L.ws);
   const u32* txt32 = reinterpret_cast<const u32*>(L.txt);
   const int aligned = ((uintptr_t)text & 15) == 0;
@@ -242,14 +272,34 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
       tile_nl += c;
     }
     const u32 thread_line = line_base + wbase + incl - mine;
-    // ---- 3. tokens of this thread's segment
+    // ---- 3. tokens of this thread's segment, at their text-order indices
     const u64 seg_base = tile_base + (u64)t * SEG;
+    u32 starts = 0;
     if (seg_base < chunk_end) {
       const u32 m = ws16[t];
       const u32 prev_ws = t ? ((ws16[t - 1] >> 15) & 1u) : (is_ws(L.txt[PAD - 1]) ? 1u : 0u);
-      u32 starts = (~m) & ((m << 1) | prev_ws) & 0xFFFFu;
+      starts = (~m) & ((m << 1) | prev_ws) & 0xFFFFu;
       const u64 lim_own = chunk_end - seg_base;
       if (lim_own < 16) starts &= (1u << lim_own) - 1u;
+    }
+    const u32 tmine = __builtin_popcount(starts);
+    u32 tincl = tmine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 v = __shfl_up(tincl, o);
+      if (lane >= o) tincl += v;
+    }
+    if (lane == 63) L.wave_tok[wave] = tincl;
+    __syncthreads();
+    u32 twbase = 0, tile_tok = 0;
+#pragma unroll
+    for (int w = 0; w < T / 64; ++w) {
+      const u32 c = L.wave_tok[w];
+      twbase += w < wave ? c : 0;
+      tile_tok += c;
+    }
+    u32 k = twbase + tincl - tmine;  // tile-relative index of this thread's first token
+    {
       while (starts) {
         const int i = __builtin_ctz(starts);
         starts &= starts - 1;
@@ -300,21 +350,21 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
           if (r == 0) gs = 0;  // table overflow: flagged in ctrl[1], host re-runs bigger
           ref = GFLAG | (u32)gs;
         }
-        const u32 k = __hip_atomic_fetch_add(&L.ntok, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (k < (u32)MAX_TOK) {
           L.tok_ref[k] = ref;
           L.tok_line[k] = (u16)(line - line_base);
-        } else {
+        } else {  // past the buffer (tiles of one-letter words): resolved and written here
           u64 gs = ref & ~GFLAG;
           if (!(ref & GFLAG)) {
             const int r = gtab_insert(g, hi, lo, 1, make_rep(rep_base + gpos, len), OP_SUM, &gs);
             claims += r == 2;
             if (r == 0) gs = 0;
           }
-          const unsigned long long o = atomicAdd(out_counter, 1ull);
+          const u64 o = tok_next + k;
           if (o < out_cap) out[o] = (gs << doc_bits) | (u64)line;
           else atomicOr(err, 1u);
         }
+        ++k;
       }
     }
     __syncthreads();
@@ -329,29 +379,21 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
         L.gslot[s] = rc ? (u32)gs : 0u;
       }
     }
-    if (t == 0) {
-      const u32 n = min(L.ntok, (u32)MAX_TOK);
-      const unsigned long long base = atomicAdd(out_counter, (unsigned long long)n);
-      L.out_base = base;
-      if (base + n > out_cap) atomicOr(err, 1u);
-    }
+    if (t == 0 && tok_next + tile_tok > out_cap) atomicOr(err, 1u);
     __syncthreads();
-    // ---- 5. write the tile's posting keys
+    // ---- 5. write the tile's posting keys (text order)
     {
-      const u32 n = min(L.ntok, (u32)MAX_TOK);
-      const unsigned long long base = L.out_base;
-      for (u32 k = t; k < n; k += T) {
-        const u32 ref = L.tok_ref[k];
+      const u32 n = min(tile_tok, (u32)MAX_TOK);
+      for (u32 j = t; j < n; j += T) {
+        const u32 ref = L.tok_ref[j];
         const u32 gs = (ref & GFLAG) ? (ref & ~GFLAG) : L.gslot[ref];
-        if (base + k < out_cap) out[base + k] = ((u64)gs << doc_bits) | (u64)(line_base + L.tok_line[k]);
+        if (tok_next + j < out_cap) out[tok_next + j] = ((u64)gs << doc_bits) | (u64)(line_base + L.tok_line[j]);
       }
     }
     line_base += tile_nl;
+    tok_next += tile_tok;
     __syncthreads();
-    if (t == 0) {
-      L.ntok = 0;
-      L.txt[PAD - 1] = L.txt[PAD + TILE - 1];
-    }
+    if (t == 0) L.txt[PAD - 1] = L.txt[PAD + TILE - 1];
     __syncthreads();
   }
   gtab_count_claims(g, claims);
@@ -505,17 +547,28 @@ extern "C" {
 
 int mr_ii_chunk_bytes() { return 32 * 1024; }
 
-int mr_count_newlines(const void* text, u64 nbytes, u64 chunk, void* out, hipStream_t s) {
+// Newlines (and, with out_tok, token starts) per chunk of `chunk` bytes.
+int mr_count_newlines(const void* text, u64 nbytes, u64 chunk, void* out, void* out_tok, hipStream_t s) {
   if (nbytes == 0) return 0;
   const u64 nb = (nbytes + chunk - 1) / chunk;
   hipLaunchKernelGGL(ii::count_newlines_kernel, dim3((unsigned)nb), dim3(256), 0, s, (const u8*)text, nbytes, chunk,
-                     (u32*)out);
+                     (u32*)out, (u32*)out_tok);
   return (int)hipGetLastError();
 }
 
-int mr_ii_map(const void* text, u64 nbytes, u64 chunk, u64 rep_base, const void* chunk_line_base, void* tag, void* hi,
-              void* lo, void* val, void* rep, void* ctrl, u64 cap, u32 doc_bits, void* out, void* out_counter,
-              u64 out_cap, void* err, hipStream_t s) {
+// *counter += *add (one thread): a posting sink's fill after a map launch.
+__global__ void ii_advance_kernel(unsigned long long* counter, const unsigned* add) { *counter += *add; }
+int mr_ii_advance(void* counter, const void* add, hipStream_t s) {
+  hipLaunchKernelGGL(ii_advance_kernel, dim3(1), dim3(1), 0, s, (unsigned long long*)counter, (const unsigned*)add);
+  return (int)hipGetLastError();
+}
+
+// chunk_tok_base: exclusive scan of the per-chunk token counts
+// (mr_count_newlines); postings land at *out_counter + their text-order index
+// (the caller advances *out_counter by the launch's token total afterwards).
+int mr_ii_map(const void* text, u64 nbytes, u64 chunk, u64 rep_base, const void* chunk_line_base,
+              const void* chunk_tok_base, void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap,
+              u32 doc_bits, void* out, void* out_counter, u64 out_cap, void* err, hipStream_t s) {
   if (nbytes == 0) return 0;
   if (chunk % ii::TILE) return -1;
   GTab g;
@@ -529,8 +582,8 @@ int mr_ii_map(const void* text, u64 nbytes, u64 chunk, u64 rep_base, const void*
   g.src = (const u8*)text - rep_base;  // the vocabulary's rep words index the caller's byte source
   const u64 nb = (nbytes + chunk - 1) / chunk;
   hipLaunchKernelGGL(ii::ii_map_kernel, dim3((unsigned)nb), dim3(ii::T), 0, s, (const u8*)text, nbytes, chunk,
-                     rep_base, (const u32*)chunk_line_base, g, doc_bits, (u64*)out, (unsigned long long*)out_counter,
-                     out_cap, (u32*)err);
+                     rep_base, (const u32*)chunk_line_base, (const u32*)chunk_tok_base, g, doc_bits, (u64*)out,
+                     (const unsigned long long*)out_counter, out_cap, (u32*)err);
   return (int)hipGetLastError();
 }
 

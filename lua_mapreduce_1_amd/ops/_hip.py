@@ -58,8 +58,9 @@ _SIGS = {
     "mr_mlp_sgd": [_p, _p, _p, _i32, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _i32, _i32,
                    _i32, _p],
     "mr_mlp_param_count": [_i32, _i32, _i32],
-    "mr_count_newlines": [_p, _u64, _u64, _p, _p],
-    "mr_ii_map": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _u64, _p, _p],
+    "mr_count_newlines": [_p, _u64, _u64, _p, _p, _p],
+    "mr_ii_map": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _u64, _p, _p],
+    "mr_ii_advance": [_p, _p, _p],
     "mr_ii_add_dest": [_p, _u64, _p, _u32, _u64, _u32, _p],
     "mr_ii_unique_flags": [_p, _u64, _p, _p],
     "mr_ii_compact": [_p, _p, _p, _u64, _p, _p],

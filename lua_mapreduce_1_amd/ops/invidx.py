@@ -78,24 +78,36 @@ class Vocab:
         return inv.astype(np.int64)
 
 
+def _chunk_bases(text: torch.Tensor, nbytes: int, s):
+    """Per map chunk: first line (exclusive scan of newline counts) and first
+    token (exclusive scan of token counts, + their total) — the map kernel
+    writes every posting at its text-order index."""
+    d = text.device
+    nchunks = max(1, (nbytes + CHUNK - 1) // CHUNK)
+    cnt = torch.empty((2, nchunks), dtype=torch.int32, device=d)
+    _hip.call("mr_count_newlines", _hip.ptr(text), nbytes, CHUNK, _hip.ptr(cnt[0]), _hip.ptr(cnt[1]), s)
+    lbase, _ = exclusive_scan(cnt[0])
+    tbase, ttot = exclusive_scan(cnt[1])
+    return lbase, tbase, ttot
+
+
 def map_postings(text: torch.Tensor, vocab: Vocab, doc_bits: int, rep_base: int = 0):
-    """Posting keys ``id << doc_bits | line`` of every token of ``text``
-    (unsorted on the GPU) -> int64 tensor.  ``line`` = newlines before the token."""
+    """Posting keys ``id << doc_bits | line`` of every token of ``text``, in
+    text order (so in line order) -> int64 tensor.  ``line`` = newlines before
+    the token."""
     nbytes = text.numel()
     if text.is_cuda:
         d = text.device
         s = _hip.stream(d)
-        nchunks = max(1, (nbytes + CHUNK - 1) // CHUNK)
-        cnt = torch.zeros(nchunks, dtype=torch.int32, device=d)
-        _hip.call("mr_count_newlines", _hip.ptr(text), nbytes, CHUNK, _hip.ptr(cnt), s)
-        base, _ = exclusive_scan(cnt)
+        base, tbase, ttot = _chunk_bases(text, nbytes, s)
         cap = nbytes // 2 + 2  # tokens are separated by >= 1 whitespace byte
         out = torch.empty(cap, dtype=torch.int64, device=d)
         counter = torch.zeros(1, dtype=torch.int64, device=d)
         err = torch.zeros(1, dtype=torch.int32, device=d)
         t = vocab.table
-        _hip.call("mr_ii_map", _hip.ptr(text), nbytes, CHUNK, rep_base, _hip.ptr(base), *t._gtab(), t.cap, doc_bits,
-                  _hip.ptr(out), _hip.ptr(counter), cap, _hip.ptr(err), s)
+        _hip.call("mr_ii_map", _hip.ptr(text), nbytes, CHUNK, rep_base, _hip.ptr(base), _hip.ptr(tbase), *t._gtab(),
+                  t.cap, doc_bits, _hip.ptr(out), _hip.ptr(counter), cap, _hip.ptr(err), s)
+        _hip.call("mr_ii_advance", _hip.ptr(counter), _hip.ptr(ttot), s)
         n, e = torch.cat([counter, err.to(torch.int64)]).tolist()
         if e:
             raise RuntimeError("inverted index map: posting buffer overflow")
@@ -138,27 +150,30 @@ class PostingSink:
 def map_postings_chunk(text: torch.Tensor, a: int, b: int, line_base: int, vocab: Vocab, doc_bits: int,
                        sink: PostingSink) -> None:
     """GPU: postings of text[a:b] (a split-aligned piece of a rank's text) into
-    ``sink``; ``line_base`` = newlines of the rank's text before byte a.  Line
-    ids come from the piece's own newline counts (one count + one scan launch)."""
+    ``sink`` after the postings already there, in text order (pieces are
+    mapped in text order, so the sink stays in line order); ``line_base`` =
+    newlines of the rank's text before byte a.  Line and token bases come from
+    the piece's own counts (one count launch, two scans)."""
     d = text.device
     s = _hip.stream(d)
     piece = text[a:b]
     nbytes = piece.numel()
     if nbytes == 0:
         return
-    nchunks = max(1, (nbytes + CHUNK - 1) // CHUNK)
-    cnt = torch.empty(nchunks, dtype=torch.int32, device=d)
-    _hip.call("mr_count_newlines", _hip.ptr(piece), nbytes, CHUNK, _hip.ptr(cnt), s)
-    base, _ = exclusive_scan(cnt)
+    base, tbase, ttot = _chunk_bases(piece, nbytes, s)
     if line_base:
         base.add_(line_base)
     t = vocab.table
-    _hip.call("mr_ii_map", _hip.ptr(piece), nbytes, CHUNK, a, _hip.ptr(base), *t._gtab(), t.cap, doc_bits,
-              _hip.ptr(sink.out), _hip.ptr(sink.ctrl[:1]), sink.cap, _hip.ptr(sink.ctrl[1:]), s)
+    _hip.call("mr_ii_map", _hip.ptr(piece), nbytes, CHUNK, a, _hip.ptr(base), _hip.ptr(tbase), *t._gtab(), t.cap,
+              doc_bits, _hip.ptr(sink.out), _hip.ptr(sink.ctrl[:1]), sink.cap, _hip.ptr(sink.ctrl[1:]), s)
+    _hip.call("mr_ii_advance", _hip.ptr(sink.ctrl[:1]), _hip.ptr(ttot), s)
 
 
-def sort_unique(keys: torch.Tensor, bits: int) -> torch.Tensor:
-    """Sorted distinct posting keys (keys < 2^bits, bits <= 63)."""
+def sort_unique(keys: torch.Tensor, bits: int, from_bit: int = 0) -> torch.Tensor:
+    """Sorted distinct posting keys (keys < 2^bits, bits <= 63).  ``from_bit``
+    (a multiple of 8): the keys are already in order of their bits below it
+    (postings in text order: line order), so a stable sort of the bits above
+    is enough."""
     n = keys.numel()
     if keys.is_cuda:
         if n == 0:
@@ -168,7 +183,7 @@ def sort_unique(keys: torch.Tensor, bits: int) -> torch.Tensor:
         # keys-only radix sort (no permutation carried), then the fused
         # two-pass unique (per-tile head counts -> scan -> scatter)
         # posting keys arrive in text order: a line's keys share their line digits
-        _, sk = sort_keys([keys], bits=[bits], return_keys=True, keys_only=True, runs=True)
+        _, sk = sort_keys([keys], bits=[bits], return_keys=True, keys_only=True, runs=True, from_bit=from_bit)
         tiles = int(_hip.lib().mr_ii_unique_tiles(n))
         tc = torch.empty(tiles, dtype=torch.int32, device=d)
         _hip.call("mr_ii_unique_count", _hip.ptr(sk), n, _hip.ptr(tc), s)

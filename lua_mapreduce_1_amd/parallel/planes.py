@@ -185,6 +185,11 @@ class ListPlane:
         rank_lines = int(lines[ids[-1] + 1]) - rank_l0 if ids else 0
         self.line_base = rank_l0
         self.doc_bits = _bits(rank_lines + 1)
+        if eng.device.type == "cuda":
+            # the device map writes postings in text (= line) order: the sort
+            # then orders only the word bits above doc_bits (sort_unique
+            # from_bit), which must be a digit boundary
+            self.doc_bits = (self.doc_bits + 7) // 8 * 8
         self.vocab.reset()
         dmap = eng.dmap
         if eng.device.type == "cuda":
@@ -216,11 +221,16 @@ class ListPlane:
         return II.map_postings(eng.arena[:self._cpu_end], self.vocab, self.doc_bits)
 
     # -- sort / group ---------------------------------------------------------
-    def _group(self, keys: torch.Tensor, bits: int) -> torch.Tensor:
+    def _group(self, keys: torch.Tensor, bits: int, from_bit: int = 0) -> torch.Tensor:
+        """Keys sorted (and made distinct for concat_unique); ``from_bit``
+        (GPU): the keys are already ordered by their bits below it."""
+        if not keys.is_cuda:
+            from_bit = 0
         if self.unique:
-            return II.sort_unique(keys, bits)
+            return II.sort_unique(keys, bits, from_bit)
         if keys.is_cuda:
-            _, sk = ops.sort_keys_checked([keys], bits=[bits], return_keys=True, keys_only=True, runs=True)
+            _, sk = ops.sort_keys_checked([keys], bits=[bits], return_keys=True, keys_only=True, runs=True,
+                                          from_bit=from_bit)
             return sk
         return torch.sort(keys).values
 
@@ -263,7 +273,7 @@ class ListPlane:
             raise ValueError(f"posting key needs {bits} bits (> 63): raise the vocabulary capacity bits or split "
                              "the input")
         with trace.range("mr.list.sort"):
-            ukeys = self._group(keys, bits)
+            ukeys = self._group(keys, bits, self.doc_bits)
             wid, wstart, docs = II.split_words(ukeys, self.doc_bits, vocab.id_bits, self.line_base)
             vhi, vlo, vrep = vocab.arrays()
             hi, lo, rep = vhi[wid], vlo[wid], vrep[wid]
@@ -329,7 +339,10 @@ class ListPlane:
         rid = II.insert_ids(rv, rhi, rlo, rrep, src=rblob)
         pid = torch.repeat_interleave(rid, rnd, output_size=int(rdocs.numel()))
         rkeys = (pid << 32) | rdocs.to(torch.int64)
-        sk = self._group(rkeys, rv.id_bits + 32)
+        # received in source-rank order, each source's lists sorted, and the
+        # ranks' line ranges increasing with the rank: every word's lines are
+        # already in order, so the sort orders the word bits only
+        sk = self._group(rkeys, rv.id_bits + 32, 32)
         wid2, wstart2, docs2 = II.split_words(sk, 32, rv.id_bits, 0)
         vhi, vlo, vrep = rv.arrays()
         return vhi[wid2], vlo[wid2], vrep[wid2], rblob, wstart2, docs2, failed_total
