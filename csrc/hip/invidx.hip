@@ -144,25 +144,31 @@ __device__ __forceinline__ int lds_find_or_claim(Lds& L, u64 hi, u64 lo, u32 rep
 
 // Newlines per chunk (for the chunk line bases) and, with out_tok, token
 // starts per chunk (a non-whitespace byte whose predecessor is whitespace or
-// the start of the text: exactly the tokens ii_map_kernel's chunk owns).
+// the start of the text: exactly the tokens ii_map_kernel's chunk owns).  Each
+// thread walks chunk/256 consecutive bytes, so the byte before a 16-byte
+// segment is the previous segment's last (one extra load per thread).
 __global__ void __launch_bounds__(256) count_newlines_kernel(const u8* __restrict__ text, u64 nbytes, u64 chunk,
                                                              u32* __restrict__ out, u32* __restrict__ out_tok) {
   const u64 b0 = (u64)blockIdx.x * chunk;
   const u64 b1 = min(b0 + chunk, nbytes);
+  const u64 per = chunk / 256;
+  const u64 p0 = b0 + threadIdx.x * per;
+  const u64 p1 = min(p0 + per, b1);
   u32 c = 0, ct = 0;
-  for (u64 p = b0 + threadIdx.x * 16; p < b1; p += 256 * 16) {
-    if (p + 16 <= b1 && ((uintptr_t)(text + p) & 15) == 0) {
+  u32 prev = (p0 == 0 || p0 >= b1) ? 1u : (is_ws(text[p0 - 1]) ? 1u : 0u);
+  for (u64 p = p0; p < p1; p += 16) {
+    if (p + 16 <= p1 && ((uintptr_t)(text + p) & 15) == 0) {
       const uint4 q = *reinterpret_cast<const uint4*>(text + p);
       c += __builtin_popcount(mask16(q, 10u, false));
-      if (out_tok) {
-        const u32 m = mask16(q, 0, true);
-        const u32 prev = p == 0 ? 1u : (is_ws(text[p - 1]) ? 1u : 0u);
-        ct += __builtin_popcount(~m & ((m << 1) | prev) & 0xFFFFu);
-      }
+      const u32 m = mask16(q, 0, true);
+      ct += __builtin_popcount(~m & ((m << 1) | prev) & 0xFFFFu);
+      prev = (m >> 15) & 1u;
     } else {
-      for (u64 k = p; k < min(p + 16, b1); ++k) {
+      for (u64 k = p; k < min(p + 16, p1); ++k) {
+        const u32 w = is_ws(text[k]) ? 1u : 0u;
         c += text[k] == '\n';
-        ct += !is_ws(text[k]) && (k == 0 || is_ws(text[k - 1]));
+        ct += (!w && prev) ? 1u : 0u;
+        prev = w;
       }
     }
   }
@@ -550,6 +556,7 @@ int mr_ii_chunk_bytes() { return 32 * 1024; }
 // Newlines (and, with out_tok, token starts) per chunk of `chunk` bytes.
 int mr_count_newlines(const void* text, u64 nbytes, u64 chunk, void* out, void* out_tok, hipStream_t s) {
   if (nbytes == 0) return 0;
+  if (chunk % 4096) return -1;  // 256 threads x whole 16-byte segments
   const u64 nb = (nbytes + chunk - 1) / chunk;
   hipLaunchKernelGGL(ii::count_newlines_kernel, dim3((unsigned)nb), dim3(256), 0, s, (const u8*)text, nbytes, chunk,
                      (u32*)out, (u32*)out_tok);

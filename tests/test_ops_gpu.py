@@ -246,9 +246,17 @@ def test_device_long_key_order_without_host_fix(gpu):
     assert got == words
 
 
-def test_spmd_prefetch_pipelined_iterations_match(gpu):
+@pytest.mark.parametrize("resident,next_map", [(False, "auto"), (True, "auto"), (True, "before_sync"),
+                                               (False, "before_tail")])
+def test_spmd_prefetch_pipelined_iterations_match(gpu, monkeypatch, resident, next_map):
     """Iterations whose input copies were prefetched into the other arena give
-    the same results as non-pipelined ones (and the counts stay exact)."""
+    the same results as non-pipelined ones (and the counts stay exact); also
+    with HBM-resident input and every MR_NEXT_MAP mode (auto = chain for
+    resident input: the next map queued before this map's sync, gated on its
+    completion)."""
+    import dataclasses
+    from lua_mapreduce_1_amd.parallel import spmd as S
+    monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(S.TUNABLES, next_map=next_map))
     from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore
     from lua_mapreduce_1_amd.utils.corpus import europarl_like
     M = "lua_mapreduce_1_amd.models.wordcount"
@@ -256,6 +264,7 @@ def test_spmd_prefetch_pipelined_iterations_match(gpu):
     params = dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
                   init_args={"nsplits": len(splits), "num_reducers": 10})
     eng = SPMDEngine(params, device=gpu, split_store=SplitStore(splits))
+    eng.resident = resident
     ref = eng.run_iteration()
     ref_total, ref_keys = ref.total_value, ref.distinct_keys
     from lua_mapreduce_1_amd.runtime import codec
