@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-2 checkpoint of the whole tree: smoke(), every GPU test, the default
+# 1-GPU bench, the resident bench, kernel stats of the default bench
+set -e
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/${1:-final}
+mkdir -p $OUT
+timeout -k 10 300 python -u __graft_entry__.py smoke > $OUT/smoke.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 300 python -u bench.py > $OUT/bench_default.log 2>&1
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > $OUT/bench_1gpu_20.log 2>&1
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --resident --no-cold > $OUT/bench_1gpu_resident.log 2>&1
+MR_FAST_EXIT=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 20 --warmup 3 > $OUT/prof_bench.log 2>&1
