@@ -47,7 +47,7 @@ __device__ __forceinline__ u64 gr_pack(u32 epoch, u64 flag, u64 count) {
 
 template <bool RUNS>
 __global__ void __launch_bounds__(RS_THREADS) rs_ghist8_kernel(const u64* keys, u64 n, u32* ghist /*[8][256]*/,
-                                                               int ndigits) {
+                                                               int d0, int ndigits) {
   // only the digits the sort will visit: a 16-bit word used to pay 6 extra
   // all-in-bin-0 (maximally contended) LDS atomics per key
   __shared__ u32 h[8][RS_BINS];
@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_ghist8_kernel(const u64* keys, 
       const u64 k = keys[i];
 #pragma unroll
       for (int b = 0; b < 8; ++b)
-        if (b < ndigits) atomicAdd(&h[b][(k >> (8 * b)) & 0xFF], 1u);
+        if (b >= d0 && b < ndigits) atomicAdd(&h[b][(k >> (8 * b)) & 0xFF], 1u);
     }
   }
   const int lane = t & 63;
@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_ghist8_kernel(const u64* keys, 
     const u32 nvalid = n - base < 64 ? (u32)(n - base) : 64u;
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
-      if (b < ndigits) {
+      if (b >= d0 && b < ndigits) {
         const u32 d = (u32)(k >> (8 * b)) & 0xFFu;
         const u32 prev = __shfl_up(d, 1);
         const bool head = valid && (lane == 0 || d != prev);
@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_ghist8_kernel(const u64* keys, 
   __syncthreads();
 #pragma unroll
   for (int b = 0; b < 8; ++b)
-    if (b < ndigits && h[b][t]) atomicAdd(&ghist[b * RS_BINS + t], h[b][t]);
+    if (b >= d0 && b < ndigits && h[b][t]) atomicAdd(&ghist[b * RS_BINS + t], h[b][t]);
 }
 
 // Inclusive scan of one value per thread over a 256-thread block: wave64
@@ -610,19 +610,22 @@ int mr_exclusive_scan_i64(const void* in, void* out, u64 n, void* partials, void
   return scan_impl<long long>((const long long*)in, (long long*)out, n, (long long*)partials, (long long*)total, s);
 }
 
-// Global histograms of all 8 digits of a u64 word (ghist: 2048 u32, zeroed by
-// caller).  ndigits | MR_GHIST_RUNS: the keys have runs of equal digits.
+// Global histograms of the digits [d0, ndigits) of a u64 word (ghist: 2048 u32,
+// zeroed by caller; digit b at ghist[256 b]).  Flags word: ndigits in bits
+// 0-7, MR_GHIST_RUNS (the keys have runs of equal digits), d0 in bits 16-23
+// (a sort of the bits >= from_bit needs no histograms below it).
 constexpr int MR_GHIST_RUNS = 0x100;
 int mr_radix_ghist8(const void* keys, u64 n, void* ghist, int ndigits, hipStream_t s) {
   if (n == 0) return 0;
   const bool runs = (ndigits & MR_GHIST_RUNS) != 0;
+  const int d0 = (ndigits >> 16) & 0xFF;
   ndigits &= 0xFF;
   if (runs)
     hipLaunchKernelGGL(rs_ghist8_kernel<true>, dim3(grid_n(n, RS_THREADS, 1024)), dim3(RS_THREADS), 0, s,
-                       (const u64*)keys, n, (u32*)ghist, ndigits);
+                       (const u64*)keys, n, (u32*)ghist, d0, ndigits);
   else
     hipLaunchKernelGGL(rs_ghist8_kernel<false>, dim3(grid_n(n, RS_THREADS, 1024)), dim3(RS_THREADS), 0, s,
-                       (const u64*)keys, n, (u32*)ghist, ndigits);
+                       (const u64*)keys, n, (u32*)ghist, d0, ndigits);
   return (int)hipGetLastError();
 }
 

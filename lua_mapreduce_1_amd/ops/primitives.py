@@ -561,8 +561,9 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None,
             else:
                 if pass_id:
                     ghist_ws.zero_()
+                d0 = from_bit // 8 if len(words) == 1 else 0  # digits below from_bit are not sorted
                 _hip.call("mr_radix_ghist8", _hip.ptr(kin), n, _hip.ptr(ghist_ws),
-                          (nb + 7) // 8 | (_GHIST_RUNS if runs else 0), s)
+                          (nb + 7) // 8 | (_GHIST_RUNS if runs else 0) | (d0 << 16), s)
             ko = keys_only and len(words) == 1
             for shift in range(from_bit if len(words) == 1 else 0, nb, 8):
                 _EPOCH[0] = (_EPOCH[0] + 1) & 0xFFFFFF or 1

@@ -437,13 +437,14 @@ def test_radix_ghist8_matches_numpy(gpu, n, runs):
     else:
         k = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64)
     keys = torch.from_numpy(k).to(gpu)
-    for ndig in (8 | 0x100, 3 | 0x100, 8, 3):  # 0x100: run-aggregated (MR_GHIST_RUNS)
+    # 0x100: run-aggregated (MR_GHIST_RUNS); bits 16-23: first digit
+    for flags in (8 | 0x100, 3 | 0x100, 8, 3, 8 | (4 << 16), 8 | 0x100 | (5 << 16)):
         gh = torch.zeros(2048, dtype=torch.int32, device=gpu)
-        _hip.call("mr_radix_ghist8", _hip.ptr(keys), n, _hip.ptr(gh), ndig, _hip.stream(gpu))
-        ndig &= 0xFF
+        _hip.call("mr_radix_ghist8", _hip.ptr(keys), n, _hip.ptr(gh), flags, _hip.stream(gpu))
+        ndig, d0 = flags & 0xFF, (flags >> 16) & 0xFF
         got = gh.cpu().numpy().reshape(8, 256)
         ku = k.view(np.uint64)
         for b in range(8):
             want = np.bincount(((ku >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.int64), minlength=256) \
-                if b < ndig else np.zeros(256, np.int64)
+                if d0 <= b < ndig else np.zeros(256, np.int64)
             assert np.array_equal(got[b], want), b
