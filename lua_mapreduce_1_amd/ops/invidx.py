@@ -169,11 +169,12 @@ def map_postings_chunk(text: torch.Tensor, a: int, b: int, line_base: int, vocab
     _hip.call("mr_ii_advance", _hip.ptr(sink.ctrl[:1]), _hip.ptr(ttot), s)
 
 
-def sort_unique(keys: torch.Tensor, bits: int, from_bit: int = 0) -> torch.Tensor:
+def sort_unique(keys: torch.Tensor, bits: int, from_bit: int = 0, runs: bool = False) -> torch.Tensor:
     """Sorted distinct posting keys (keys < 2^bits, bits <= 63).  ``from_bit``
     (a multiple of 8): the keys are already in order of their bits below it
     (postings in text order: line order), so a stable sort of the bits above
-    is enough."""
+    is enough.  ``runs``: consecutive keys share the sorted digits (a hint
+    for the digit histograms: word bits of text-order postings do not)."""
     n = keys.numel()
     if keys.is_cuda:
         if n == 0:
@@ -182,8 +183,7 @@ def sort_unique(keys: torch.Tensor, bits: int, from_bit: int = 0) -> torch.Tenso
         s = _hip.stream(d)
         # keys-only radix sort (no permutation carried), then the fused
         # two-pass unique (per-tile head counts -> scan -> scatter)
-        # posting keys arrive in text order: a line's keys share their line digits
-        _, sk = sort_keys([keys], bits=[bits], return_keys=True, keys_only=True, runs=True, from_bit=from_bit)
+        _, sk = sort_keys([keys], bits=[bits], return_keys=True, keys_only=True, runs=runs, from_bit=from_bit)
         tiles = int(_hip.lib().mr_ii_unique_tiles(n))
         tc = torch.empty(tiles, dtype=torch.int32, device=d)
         _hip.call("mr_ii_unique_count", _hip.ptr(sk), n, _hip.ptr(tc), s)

@@ -221,15 +221,16 @@ class ListPlane:
         return II.map_postings(eng.arena[:self._cpu_end], self.vocab, self.doc_bits)
 
     # -- sort / group ---------------------------------------------------------
-    def _group(self, keys: torch.Tensor, bits: int, from_bit: int = 0) -> torch.Tensor:
+    def _group(self, keys: torch.Tensor, bits: int, from_bit: int = 0, runs: bool = False) -> torch.Tensor:
         """Keys sorted (and made distinct for concat_unique); ``from_bit``
-        (GPU): the keys are already ordered by their bits below it."""
+        (GPU): the keys are already ordered by their bits below it; ``runs``:
+        consecutive keys share the sorted digits (histogram hint)."""
         if not keys.is_cuda:
             from_bit = 0
         if self.unique:
-            return II.sort_unique(keys, bits, from_bit)
+            return II.sort_unique(keys, bits, from_bit, runs)
         if keys.is_cuda:
-            _, sk = ops.sort_keys_checked([keys], bits=[bits], return_keys=True, keys_only=True, runs=True,
+            _, sk = ops.sort_keys_checked([keys], bits=[bits], return_keys=True, keys_only=True, runs=runs,
                                           from_bit=from_bit)
             return sk
         return torch.sort(keys).values
@@ -342,7 +343,7 @@ class ListPlane:
         # received in source-rank order, each source's lists sorted, and the
         # ranks' line ranges increasing with the rank: every word's lines are
         # already in order, so the sort orders the word bits only
-        sk = self._group(rkeys, rv.id_bits + 32, 32)
+        sk = self._group(rkeys, rv.id_bits + 32, 32, runs=True)  # one run of word bits per received list
         wid2, wstart2, docs2 = II.split_words(sk, 32, rv.id_bits, 0)
         vhi, vlo, vrep = rv.arrays()
         return vhi[wid2], vlo[wid2], vrep[wid2], rblob, wstart2, docs2, failed_total
