@@ -60,6 +60,7 @@ __device__ __forceinline__ void st_agent(u64* p, u64 v) {
 }
 
 __device__ __forceinline__ void fold_value(long long* p, long long v, int op) {
+  if (op == OP_NONE) return;
   if (op == OP_MIN) atomicMin(p, v);
   else if (op == OP_MAX) atomicMax(p, v);
   else atomicAdd((unsigned long long*)p, (unsigned long long)v);

@@ -21,7 +21,8 @@
 //   3. tokens probe a 4096-slot LDS table (exact 128-bit keys) — a chunk's
 //      vocabulary costs one HBM insert per distinct word, not per token;
 //      LDS misses (table 3/4 full) insert into HBM directly;
-//   4. newly claimed LDS slots get their global slot (one gtab_insert each);
+//   4. newly claimed LDS slots get their global slot (one gtab_insert each,
+//      OP_NONE: the vocabulary folds no value, so a present word costs a load);
 //   5. the tile's tokens are written at their text-order positions: a token's
 //      output index = its chunk's token base (count_lines_tokens_kernel + an
 //      exclusive scan, before the launch) + the tokens before it in the chunk
@@ -351,7 +352,7 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
           ref = (u32)ls;
         } else {
           u64 gs = 0;
-          const int r = gtab_insert(g, hi, lo, 1, make_rep(rep_base + gpos, len), OP_SUM, &gs);
+          const int r = gtab_insert(g, hi, lo, 1, make_rep(rep_base + gpos, len), OP_NONE, &gs);
           claims += r == 2;
           if (r == 0) gs = 0;  // table overflow: flagged in ctrl[1], host re-runs bigger
           ref = GFLAG | (u32)gs;
@@ -362,7 +363,7 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
         } else {  // past the buffer (tiles of one-letter words): resolved and written here
           u64 gs = ref & ~GFLAG;
           if (!(ref & GFLAG)) {
-            const int r = gtab_insert(g, hi, lo, 1, make_rep(rep_base + gpos, len), OP_SUM, &gs);
+            const int r = gtab_insert(g, hi, lo, 1, make_rep(rep_base + gpos, len), OP_NONE, &gs);
             claims += r == 2;
             if (r == 0) gs = 0;
           }
@@ -380,7 +381,7 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
         const u32 r = L.rep[s];
         u64 gs = 0;
         const int rc = gtab_insert(g, L.hi[s], L.lo[s], 1, make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16),
-                                   OP_SUM, &gs);
+                                   OP_NONE, &gs);
         claims += rc == 2;
         L.gslot[s] = rc ? (u32)gs : 0u;
       }
@@ -662,7 +663,7 @@ __global__ void ii_insert_slots_kernel(GTab g, const u64* __restrict__ hi, const
   u32 claims = 0;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     u64 s = 0;
-    const int r = gtab_insert(g, hi[i], lo[i], 1, rep[i], OP_SUM, &s);
+    const int r = gtab_insert(g, hi[i], lo[i], 1, rep[i], OP_NONE, &s);
     claims += r == 2;
     out_slot[i] = r ? (long long)s : -1;
   }

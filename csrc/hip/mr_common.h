@@ -129,6 +129,8 @@ MR_HD u64 rep_off(u64 rep) { return rep >> REP_LEN_BITS; }
 MR_HD u64 rep_len(u64 rep) { return rep & REP_LEN_MASK; }
 
 // Reduction operators for hash aggregation / reduce-by-key.
-enum ReduceOp : int { OP_SUM = 0, OP_MIN = 1, OP_MAX = 2, OP_COUNT = 3 };
+// OP_NONE: the table only maps keys to slots (a vocabulary: the inverted
+// index's word ids) — inserts fold nothing, so a hit costs one load, no atomic.
+enum ReduceOp : int { OP_SUM = 0, OP_MIN = 1, OP_MAX = 2, OP_COUNT = 3, OP_NONE = 4 };
 
 }  // namespace mr
