@@ -191,7 +191,8 @@ __global__ void __launch_bounds__(256) count_newlines_kernel(const u8* __restric
 
 __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, u64 nbytes, u64 chunk_bytes,
                                                    u64 rep_base, const u32* __restrict__ chunk_line_base,
-                                                   const u32* __restrict__ chunk_tok_base, GTab g, u32 doc_bits,
+                                                   const u32* __restrict__ chunk_tok_base,
+                                                   const u32* __restrict__ chunk_tok_count, GTab g, u32 doc_bits,
                                                    u64* __restrict__ out,
                                                    const unsigned long long* __restrict__ out_counter, u64 out_cap,
                                                    u32* __restrict__ err) {
@@ -217,6 +218,7 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
   // this launch's first output slot (advanced after the launch) + the tokens
   // of the chunks before this one
   u64 tok_next = (u64)*out_counter + chunk_tok_base[blockIdx.x];
+  const u64 tok_end = tok_next + chunk_tok_count[blockIdx.x];
   u16* ws16 = reinterpret_cast<u16*>(L.ws);
   const u32* txt32 = reinterpret_cast<const u32*>(L.txt);
   const int aligned = ((uintptr_t)text & 15) == 0;
@@ -403,6 +405,9 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
     if (t == 0) L.txt[PAD - 1] = L.txt[PAD + TILE - 1];
     __syncthreads();
   }
+  // the chunk's tokens must be exactly the ones the count kernel found (their
+  // output slots were reserved from those counts): bit 1 of err otherwise
+  if (t == 0 && tok_next != tok_end) atomicOr(err, 2u);
   gtab_count_claims(g, claims);
 }
 
@@ -575,8 +580,9 @@ int mr_ii_advance(void* counter, const void* add, hipStream_t s) {
 // (mr_count_newlines); postings land at *out_counter + their text-order index
 // (the caller advances *out_counter by the launch's token total afterwards).
 int mr_ii_map(const void* text, u64 nbytes, u64 chunk, u64 rep_base, const void* chunk_line_base,
-              const void* chunk_tok_base, void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap,
-              u32 doc_bits, void* out, void* out_counter, u64 out_cap, void* err, hipStream_t s) {
+              const void* chunk_tok_base, const void* chunk_tok_count, void* tag, void* hi, void* lo, void* val,
+              void* rep, void* ctrl, u64 cap, u32 doc_bits, void* out, void* out_counter, u64 out_cap, void* err,
+              hipStream_t s) {
   if (nbytes == 0) return 0;
   if (chunk % ii::TILE) return -1;
   GTab g;
@@ -590,7 +596,8 @@ int mr_ii_map(const void* text, u64 nbytes, u64 chunk, u64 rep_base, const void*
   g.src = (const u8*)text - rep_base;  // the vocabulary's rep words index the caller's byte source
   const u64 nb = (nbytes + chunk - 1) / chunk;
   hipLaunchKernelGGL(ii::ii_map_kernel, dim3((unsigned)nb), dim3(ii::T), 0, s, (const u8*)text, nbytes, chunk,
-                     rep_base, (const u32*)chunk_line_base, (const u32*)chunk_tok_base, g, doc_bits, (u64*)out,
+                     rep_base, (const u32*)chunk_line_base, (const u32*)chunk_tok_base,
+                     (const u32*)chunk_tok_count, g, doc_bits, (u64*)out,
                      (const unsigned long long*)out_counter, out_cap, (u32*)err);
   return (int)hipGetLastError();
 }

@@ -59,7 +59,7 @@ _SIGS = {
                    _i32, _p],
     "mr_mlp_param_count": [_i32, _i32, _i32],
     "mr_count_newlines": [_p, _u64, _u64, _p, _p, _p],
-    "mr_ii_map": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _u64, _p, _p],
+    "mr_ii_map": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _u64, _p, _p],
     "mr_ii_advance": [_p, _p, _p],
     "mr_ii_add_dest": [_p, _u64, _p, _u32, _u64, _u32, _p],
     "mr_ii_unique_flags": [_p, _u64, _p, _p],

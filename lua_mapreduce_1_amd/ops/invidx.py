@@ -88,7 +88,7 @@ def _chunk_bases(text: torch.Tensor, nbytes: int, s):
     _hip.call("mr_count_newlines", _hip.ptr(text), nbytes, CHUNK, _hip.ptr(cnt[0]), _hip.ptr(cnt[1]), s)
     lbase, _ = exclusive_scan(cnt[0])
     tbase, ttot = exclusive_scan(cnt[1])
-    return lbase, tbase, ttot
+    return lbase, tbase, ttot, cnt[1]
 
 
 def map_postings(text: torch.Tensor, vocab: Vocab, doc_bits: int, rep_base: int = 0):
@@ -99,16 +99,18 @@ def map_postings(text: torch.Tensor, vocab: Vocab, doc_bits: int, rep_base: int 
     if text.is_cuda:
         d = text.device
         s = _hip.stream(d)
-        base, tbase, ttot = _chunk_bases(text, nbytes, s)
+        base, tbase, ttot, tcnt = _chunk_bases(text, nbytes, s)
         cap = nbytes // 2 + 2  # tokens are separated by >= 1 whitespace byte
         out = torch.empty(cap, dtype=torch.int64, device=d)
         counter = torch.zeros(1, dtype=torch.int64, device=d)
         err = torch.zeros(1, dtype=torch.int32, device=d)
         t = vocab.table
-        _hip.call("mr_ii_map", _hip.ptr(text), nbytes, CHUNK, rep_base, _hip.ptr(base), _hip.ptr(tbase), *t._gtab(),
-                  t.cap, doc_bits, _hip.ptr(out), _hip.ptr(counter), cap, _hip.ptr(err), s)
+        _hip.call("mr_ii_map", _hip.ptr(text), nbytes, CHUNK, rep_base, _hip.ptr(base), _hip.ptr(tbase),
+                  _hip.ptr(tcnt), *t._gtab(), t.cap, doc_bits, _hip.ptr(out), _hip.ptr(counter), cap, _hip.ptr(err), s)
         _hip.call("mr_ii_advance", _hip.ptr(counter), _hip.ptr(ttot), s)
         n, e = torch.cat([counter, err.to(torch.int64)]).tolist()
+        if e & 2:
+            raise RuntimeError("inverted index map: a chunk's tokens differ from its reserved count")
         if e:
             raise RuntimeError("inverted index map: posting buffer overflow")
         if vocab.overflowed:
@@ -140,6 +142,8 @@ class PostingSink:
 
     def finish(self, vocab: "Vocab") -> torch.Tensor:
         n, e = self.ctrl.tolist()  # the one host synchronisation of the map phase
+        if e & 2:
+            raise RuntimeError("inverted index map: a chunk's tokens differ from its reserved count")
         if e:
             raise RuntimeError("inverted index map: posting buffer overflow")
         if vocab.overflowed:
@@ -160,12 +164,13 @@ def map_postings_chunk(text: torch.Tensor, a: int, b: int, line_base: int, vocab
     nbytes = piece.numel()
     if nbytes == 0:
         return
-    base, tbase, ttot = _chunk_bases(piece, nbytes, s)
+    base, tbase, ttot, tcnt = _chunk_bases(piece, nbytes, s)
     if line_base:
         base.add_(line_base)
     t = vocab.table
-    _hip.call("mr_ii_map", _hip.ptr(piece), nbytes, CHUNK, a, _hip.ptr(base), _hip.ptr(tbase), *t._gtab(), t.cap,
-              doc_bits, _hip.ptr(sink.out), _hip.ptr(sink.ctrl[:1]), sink.cap, _hip.ptr(sink.ctrl[1:]), s)
+    _hip.call("mr_ii_map", _hip.ptr(piece), nbytes, CHUNK, a, _hip.ptr(base), _hip.ptr(tbase), _hip.ptr(tcnt),
+              *t._gtab(), t.cap, doc_bits, _hip.ptr(sink.out), _hip.ptr(sink.ctrl[:1]), sink.cap,
+              _hip.ptr(sink.ctrl[1:]), s)
     _hip.call("mr_ii_advance", _hip.ptr(sink.ctrl[:1]), _hip.ptr(ttot), s)
 
 
