@@ -70,10 +70,7 @@ struct Lds {
   u16 tok_line[MAX_TOK + 8];  // line - the tile's first line (< TILE)
   u32 wave_nl[T / 64];
   u32 wave_tok[T / 64];
-  u32 ntok;
   u32 nclaimed;
-  u32 tile_lines;
-  unsigned long long out_base;
 };
 static_assert(sizeof(Lds) <= 160 * 1024, "LDS budget");
 
@@ -209,7 +206,6 @@ __global__ void __launch_bounds__(T) ii_map_kernel(const u8* __restrict__ text, 
   }
   if (t == 0) {
     L.nclaimed = 0;
-    L.ntok = 0;
     L.txt[PAD - 1] = chunk_begin > 0 ? text[chunk_begin - 1] : (u8)' ';
     L.ws[WSW - 2] = 0xFFFFFFFFu;
     L.ws[WSW - 1] = 0xFFFFFFFFu;
