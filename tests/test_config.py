@@ -7,11 +7,12 @@ from lua_mapreduce_1_amd.utils.config import Tunables
 
 def test_defaults_and_overrides():
     t = Tunables.from_env({})
-    assert t.default_sleep == 1.0 and t.force_shuffle is False and t.pipeline is True and t.d2h == "kernel"
+    assert t.default_sleep == 1.0 and t.force_shuffle is False and t.pipeline is True and t.d2h == "sdma"
+    assert t.next_map == "auto"
     o = Tunables.from_env({"MR_DEFAULT_SLEEP": "0.05", "MR_FORCE_SHUFFLE": "1", "MR_PIPELINE": "0",
-                           "MR_D2H": "sdma", "MR_ROCTX": "1", "MR_SPIN_US": "0"})
+                           "MR_D2H": "kernel", "MR_ROCTX": "1", "MR_SPIN_US": "0", "MR_NEXT_MAP": "chain"})
     assert o.default_sleep == 0.05 and o.force_shuffle is True and o.pipeline is False
-    assert o.d2h == "sdma" and o.roctx is True and o.spin_us == 0.0
+    assert o.d2h == "kernel" and o.roctx is True and o.spin_us == 0.0 and o.next_map == "chain"
 
 
 def test_every_knob_documented():
