@@ -117,9 +117,9 @@ __device__ __forceinline__ u32 block_scan_256(u32 v, u32* tmp) {
   return v + add;
 }
 
-// ROUNDS: tiles of 256 x ROUNDS keys.  16 (4096-key tiles) for large sorts;
-// 4 (1024-key tiles) below ONESWEEP_SMALL keys, where a pass is one tile's
-// latency and 4096-key tiles left most CUs idle (54k keys = 14 tiles).
+// ROUNDS: tiles of 256 x ROUNDS keys (onesweep_rounds below): 4 (1024-key
+// tiles) below ONESWEEP_SMALL keys, where a pass is one tile's latency and
+// 4096-key tiles left most CUs idle (54k keys = 14 tiles); 16 or more above.
 constexpr u64 ONESWEEP_SMALL = 1ull << 18;
 template <typename V, int ROUNDS>
 __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys_in, const V* vals_in, u64* keys_out,
@@ -598,6 +598,15 @@ static int scan_impl(const T* in, T* out, u64 n, T* partials, T* total, hipStrea
   return (int)hipGetLastError();
 }
 
+template <int ROUNDS>
+static void onesweep_launch(u32 nt, const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n,
+                            int shift, const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err,
+                            int iota, int debug_fail, hipStream_t s) {
+  hipLaunchKernelGGL((rs_onesweep_kernel<u32, ROUNDS>), dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
+                     (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
+                     (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota, debug_fail);
+}
+
 extern "C" {
 
 u64 mr_scan_partials_len(u64 n) { return (n + SC_TILE - 1) / SC_TILE + 1; }
@@ -643,8 +652,26 @@ int mr_sort_debug_fail(int passes) {
   return 0;
 }
 
+// Rounds (keys per thread) of a onesweep tile (256 threads): 4 up to
+// ONESWEEP_SMALL keys, 16 up to ONESWEEP_BIG, `g_big_rounds` above.  Larger
+// tiles mean fewer look-back chains and per-tile fixed costs: 100 M keys,
+// 0.97 ms per pass at 16 rounds, 0.82 ms at 24 (two workgroups per CU still
+// fit in LDS; tools/onesweep_rounds_ab.py, profiles/r2/onesweep/).  Mid-size
+// sorts (the word-count tail's ~10^5-10^6 keys) keep 16: there a pass is a
+// few tiles' latency, and bigger tiles are fewer and longer.
+constexpr u64 ONESWEEP_BIG = 1ull << 22;
+static int g_big_rounds = 24;
+int mr_sort_set_rounds(int rounds) {
+  if (rounds != 16 && rounds != 24 && rounds != 32) return -1;
+  g_big_rounds = rounds;
+  return 0;
+}
+
+static int onesweep_rounds(u64 n) { return n <= ONESWEEP_SMALL ? 4 : n < ONESWEEP_BIG ? RS_ROUNDS : g_big_rounds; }
+
 u64 mr_onesweep_tiles(u64 n) {
-  return n <= ONESWEEP_SMALL ? (n + RS_THREADS * 4 - 1) / (RS_THREADS * 4) : (n + RS_TILE - 1) / RS_TILE;
+  const u64 tile = (u64)RS_THREADS * (u64)onesweep_rounds(n);
+  return (n + tile - 1) / tile;
 }
 
 int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
@@ -657,14 +684,15 @@ int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_
   }
   if (n == 0) return 0;
   const u32 nt = (u32)mr_onesweep_tiles(n);
-  if (n <= ONESWEEP_SMALL) {
-    hipLaunchKernelGGL((rs_onesweep_kernel<u32, 4>), dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
-                       (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
-                       (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota, debug_fail);
-  } else {
-    hipLaunchKernelGGL((rs_onesweep_kernel<u32, RS_ROUNDS>), dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
-                       (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
-                       (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota, debug_fail);
+  switch (onesweep_rounds(n)) {
+    case 4: onesweep_launch<4>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
+                               epoch, err, iota, debug_fail, s); break;
+    case 24: onesweep_launch<24>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
+                                 epoch, err, iota, debug_fail, s); break;
+    case 32: onesweep_launch<32>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
+                                 epoch, err, iota, debug_fail, s); break;
+    default: onesweep_launch<RS_ROUNDS>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules,
+                                        tile_counter, epoch, err, iota, debug_fail, s);
   }
   return (int)hipGetLastError();
 }

@@ -87,6 +87,8 @@ _SIGS = {
     "mr_tail_gather": [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "mr_tail_pack": [_p, _p, _u64, _p, _u32, _p, _p, _p, _p],
     "mr_sort_debug_fail": [_i32],
+    "mr_sort_set_rounds": [_i32],
+    "mr_onesweep_tiles": [_u64],
     "mr_set_long_mask_wc3": [_u64],
     "mr_set_long_mask_keyops": [_u64],
     "mr_set_long_mask_invidx": [_u64],
@@ -97,7 +99,7 @@ _SIGS = {
     "mr_scan_partials_len": [_u64],
 }
 _RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
-                "mr_tail_bhist_bytes"}
+                "mr_tail_bhist_bytes", "mr_onesweep_tiles"}
 
 
 def lib():
@@ -119,6 +121,8 @@ def lib():
         L.mr_host_alloc_coherent.restype = _p
         # downloads: SDMA by default, shader stores with MR_D2H=kernel (see sort.hip mr_d2h_async)
         L.mr_set_d2h_mode(1 if TUNABLES.d2h == "sdma" else 0)
+        if L.mr_sort_set_rounds(TUNABLES.sort_rounds) != 0:
+            raise ValueError(f"MR_SORT_ROUNDS={TUNABLES.sort_rounds}: must be 16, 24 or 32")
         _LIB = L
     return _LIB
 

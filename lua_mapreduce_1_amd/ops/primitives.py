@@ -485,9 +485,10 @@ _SORT_WS: dict = {}
 
 
 def _onesweep_tiles(n: int) -> int:
-    """Tiles (= look-back granule rows) of one onesweep pass over n keys:
-    1024-key tiles up to 2^18 keys, 4096-key tiles above (csrc/hip/sort.hip)."""
-    return (n + 1023) // 1024 if n <= (1 << 18) else (n + 4095) // 4096
+    """Tiles (= look-back granule rows) of one onesweep pass over n keys
+    (csrc/hip/sort.hip mr_onesweep_tiles: 1024-key tiles up to 2^18 keys,
+    4096 up to 2^22, 256 x MR_SORT_ROUNDS above)."""
+    return int(_hip.lib().mr_onesweep_tiles(n))
 
 
 def _sort_ws(d, n: int):

@@ -43,6 +43,9 @@ class Tunables:
     wc_config: int = _knob("MR_WC_CONFIG", 6,
                            "word-count map kernel launch shape (csrc/hip/wordcount3.hip mr_wc_map3 config: "
                            "0-5 per-lane token walks, 6-9 dense token lists)")
+    sort_rounds: int = _knob("MR_SORT_ROUNDS", 24,
+                             "keys per thread of the onesweep radix tiles of sorts of >= 4 M keys (256 x rounds "
+                             "keys per tile; 16, 24 or 32)")
     arena_cap_mb: float = _knob("MR_ARENA_CAP_MB", 0.0,
                                 "SPMD: cap of a rank's HBM input arena, MiB (0 = the rank's whole input); a larger "
                                 "input is mapped in rounds through a ring of two arenas of this size")
