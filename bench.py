@@ -215,6 +215,7 @@ def main() -> int:
     # -- one cold iteration: split files on disk -> results in host memory ----
     cold_ms = None
     cold_tokens = None
+    table_cap = 1 << 20
     store = None
     if not args.no_cold:
         dropped = all(mio.drop_page_cache(p) for p in paths)
@@ -230,6 +231,7 @@ def main() -> int:
         D.barrier(device=device)
         cold_ms = 1000.0 * D.all_reduce_max(cold, device)
         cold_tokens = D.all_reduce_sum_int(res.total_value, device)
+        table_cap = eng._table_capacity  # sized from the cold map's distinct keys (MR_MAP_SPARSITY)
         del eng, res
         store.finish_loading()
     if store is None:
@@ -241,7 +243,7 @@ def main() -> int:
         store.finish_loading()
     total_bytes = int(store.offsets[-1])
 
-    eng = SPMDEngine(params, device=device, split_store=store, verbose=args.verbose)
+    eng = SPMDEngine(params, device=device, split_store=store, verbose=args.verbose, table_capacity=table_cap)
     # consecutive iterations are pipelined: the next iteration's input copies
     # start as soon as the HBM arena they fill is free (double-buffered), and
     # its map as soon as this map is done; neither the last warm-up step nor

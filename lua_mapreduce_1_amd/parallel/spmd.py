@@ -45,6 +45,8 @@ from . import dist as D
 
 
 N_ARENAS = 3
+# largest map table the sparsity rule asks for (2^25 slots = 1.3 GB of HBM)
+_MAX_SPARSE_CAP = 1 << 25
 _PREFETCH_LATE = TUNABLES.prefetch_late
 _PREFETCH_SINGLE = TUNABLES.prefetch_single
 
@@ -507,6 +509,18 @@ class SPMDEngine:
     def table(self, t: ops.HashTable) -> None:
         self.tables[self.tslot] = t
 
+    def _fresh_table(self) -> None:
+        """An empty map table for the map about to be issued: the slot's table
+        reset, or replaced by a larger one once an earlier map's distinct-key
+        count has raised the target capacity (``_map_sync``)."""
+        t = self.tables[self.tslot]
+        if t is not None and t.cap < self._table_capacity:
+            self.tables[self.tslot] = t = None
+        if t is None:
+            self.tables[self.tslot] = ops.HashTable(self._table_capacity, device=self.device, op=self.op)
+        else:
+            t.reset()
+
     def _use(self, q: int) -> None:
         """Make iteration q's arena, table and stream current."""
         self.slot, self.tslot = q % N_ARENAS, q % 2
@@ -869,6 +883,7 @@ class SPMDEngine:
         if timer is not None:
             timer.begin()
         chunks = self._chunks[self.tslot] = []
+        self._mapped_bytes = 0
         errs = self._err_words(j1 - j0 + 1) if self.device.type == "cuda" else None
         fault = self._device_fault_spec()
         # the rank's whole staged input is ONE byte source (rep offsets index it)
@@ -884,6 +899,8 @@ class SPMDEngine:
             for j in range(a, b):
                 recs[j].status, recs[j].started, recs[j].worker = STATUS.RUNNING, t0, self.rank
             keys = [jobs[j][0] for j in range(a, b)]
+            if isinstance(data, torch.Tensor):
+                self._mapped_bytes += data.numel()
             ctx.err_word = errs[k:k + 1] if errs is not None else None
             done = False
             while not done:
@@ -975,6 +992,16 @@ class SPMDEngine:
                 self._table_capacity = self.table.cap
                 self._run_map(jobs, recs, j0, j1)
                 continue
+            # a rank that maps a lot of input per iteration gets sparse tables
+            # for its next maps (MR_MAP_SPARSITY slots per distinct key): fewer
+            # probes, the flush's atomics and loads spread over more memory
+            # lines (full corpus: map 2.43 -> 2.06 ms from 2^20 to 2^23 slots).
+            # A small share keeps the table: the send-side compaction scans
+            # every slot, which cost more than the map saved at W = 8
+            # (profiles/r2/sparse/)
+            if getattr(self, "_mapped_bytes", 0) >= TUNABLES.map_sparse_min_mb * 2**20:
+                self._table_capacity = max(self._table_capacity, min(
+                    ops.next_pow2(TUNABLES.map_sparsity * max(n_claimed, 1)), _MAX_SPARSE_CAP))
             return n_claimed, overflow
 
     def _device_spans(self, res, recs, j0: int, j1: int) -> None:
@@ -1162,7 +1189,7 @@ class SPMDEngine:
         try:
             st = self.streams[self.tslot]
             with torch.cuda.stream(st):
-                self.table.reset()
+                self._fresh_table()
                 if gate is not None:
                     st.wait_event(gate)
                 t0 = time.time()
@@ -1223,7 +1250,7 @@ class SPMDEngine:
         with torch.cuda.stream(stream) if stream is not None else _nullctx():
             if pending is None:
                 with trace.range("mr.table_reset"):
-                    self.table.reset()
+                    self._fresh_table()
                 t0 = time.time()
                 with trace.range("mr.map.issue"):
                     self._run_map(jobs, recs, j0, j1)

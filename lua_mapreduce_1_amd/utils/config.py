@@ -43,6 +43,13 @@ class Tunables:
     wc_config: int = _knob("MR_WC_CONFIG", 6,
                            "word-count map kernel launch shape (csrc/hip/wordcount3.hip mr_wc_map3 config: "
                            "0-5 per-lane token walks, 6-9 dense token lists)")
+    map_sparsity: int = _knob("MR_MAP_SPARSITY", 8,
+                              "SPMD fold plane: after a map of at least MR_MAP_SPARSE_MIN_MB of input, later "
+                              "maps get a table of this many slots per distinct key (power of two); sparse "
+                              "tables probe less and spread the flush's atomics (tools/map_cap_ab.py)")
+    map_sparse_min_mb: float = _knob("MR_MAP_SPARSE_MIN_MB", 128.0,
+                                     "SPMD fold plane: input MiB per rank and iteration from which map tables "
+                                     "are made sparse (MR_MAP_SPARSITY)")
     sort_rounds: int = _knob("MR_SORT_ROUNDS", 24,
                              "keys per thread of the onesweep radix tiles of sorts of >= 4 M keys (256 x rounds "
                              "keys per tile; 16, 24 or 32)")
