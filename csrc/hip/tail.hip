@@ -44,9 +44,13 @@ __device__ __forceinline__ u32 key_fnv(u64 h, u64 l, u64 r, const u8* src, u32* 
 // slots and one block-wide scan, so a 1 M-slot table ran ONE wave per SIMD:
 // 50-73 us for 0.27 M keys, profiles/r2/tail):
 //   tail_count_kernel   : occupied slots per block -> bcount[block]
-//   tail_scatter_kernel : block base = sum of bcount[0..block) (read from L2),
-//                         wave ballots for the offsets inside the block, then
-//                         the row (partition, composite key) of each slot
+//   tail_bscan_kernel   : one block: bcount -> exclusive block bases, and the
+//                         row count (a per-block sum of its predecessors'
+//                         counts was quadratic in the capacity: 33 us at 2^20
+//                         slots, most of the scatter at 2^22-2^23)
+//   tail_scatter_kernel : block base from the scan, wave ballots for the
+//                         offsets inside the block, then the row (partition,
+//                         composite key) of each slot
 //   tail_hist_kernel    : the 8 digit histograms of the dense composite keys
 //                         (and partition counts)
 constexpr int CT = 512;  // compaction threads per block (one slot each)
@@ -67,40 +71,53 @@ __global__ void __launch_bounds__(CT) tail_count_kernel(const u64* __restrict__ 
   }
 }
 
+constexpr int BS = 1024;  // threads of the block-count scan
+__global__ void __launch_bounds__(BS) tail_bscan_kernel(u32* __restrict__ bcount, u64 nb,
+                                                        unsigned long long* __restrict__ counter) {
+  __shared__ u32 wsum[BS / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const u64 per = (nb + BS - 1) / BS;
+  const u64 a = (u64)t * per, b = a + per < nb ? a + per : nb;
+  u32 sum = 0;
+  for (u64 j = a; j < b; ++j) sum += bcount[j];
+  u32 incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  u32 base = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < BS / 64; ++w) {
+    base += w < wave ? wsum[w] : 0u;
+    total += wsum[w];
+  }
+  u32 run = base + incl - sum;
+  for (u64 j = a; j < b; ++j) {
+    const u32 c = bcount[j];
+    bcount[j] = run;
+    run += c;
+  }
+  if (t == 0) *counter = total;
+}
+
 __global__ void __launch_bounds__(CT) tail_scatter_kernel(GTab g, u64 cap, u32 nparts, const u8* __restrict__ src,
                                                           u64* __restrict__ out_hi, u64* __restrict__ out_lo,
                                                           long long* __restrict__ out_val, u64* __restrict__ out_rep,
                                                           u32* __restrict__ out_part, u64* __restrict__ out_c,
-                                                          unsigned long long* __restrict__ counter,
-                                                          const u32* __restrict__ bcount) {
-  __shared__ u32 red[CT / 64];
+                                                          const u32* __restrict__ bbase) {
   __shared__ u32 wc[CT / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  u32 acc = 0;
-  for (u32 j = t; j < blockIdx.x; j += CT) acc += bcount[j];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
   const u64 i = (u64)blockIdx.x * CT + t;
   const bool occ = i < cap && g.tag[i] != 0;
   const u64 m = __ballot(occ);
-  if (lane == 0) {
-    red[wave] = acc;
-    wc[wave] = (u32)__popcll(m);
-  }
+  if (lane == 0) wc[wave] = (u32)__popcll(m);
   __syncthreads();
-  u64 o = 0, mine = 0;
+  u64 o = bbase[blockIdx.x];
 #pragma unroll
-  for (int w = 0; w < CT / 64; ++w) {
-    o += red[w];
-    o += w < wave ? wc[w] : 0u;
-    mine += wc[w];
-  }
-  if (blockIdx.x == gridDim.x - 1 && t == 0) {
-    u64 tot = 0;
-#pragma unroll
-    for (int w = 0; w < CT / 64; ++w) tot += red[w];
-    *counter = tot + mine;  // number of rows
-  }
+  for (int w = 0; w < CT / 64; ++w) o += w < wave ? wc[w] : 0u;
   if (!occ) return;
   o += (u64)__popcll(m & ((1ull << lane) - 1ull));
   const u64 h = g.hi[i], l = g.lo[i], r = g.rep[i];
@@ -211,9 +228,10 @@ int mr_tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* c
   const u64 nb = (cap + tl::CT - 1) / tl::CT;
   u32* bcount = (u32*)bhist;
   hipLaunchKernelGGL(tl::tail_count_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, (const u64*)tag, cap, bcount);
+  hipLaunchKernelGGL(tl::tail_bscan_kernel, dim3(1), dim3(tl::BS), 0, s, bcount, nb, (unsigned long long*)counter);
   hipLaunchKernelGGL(tl::tail_scatter_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, g, cap, nparts, (const u8*)src,
                      (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
-                     (unsigned long long*)counter, (const u32*)bcount);
+                     (const u32*)bcount);
   if (ghist != nullptr && n > 0) {
     u64 hb = (n + 4 * tl::T - 1) / (4 * tl::T);
     if (hb > (u64)tl::HIST_BLOCKS) hb = tl::HIST_BLOCKS;
