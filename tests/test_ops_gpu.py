@@ -167,7 +167,7 @@ def test_hash_agg_pairs(gpu):
         assert ga == gb
 
 
-@pytest.mark.parametrize("n", [1, 4095, 4097, 100_000, 2_000_003])
+@pytest.mark.parametrize("n", [1, 4095, 4097, 100_000, 2_000_003, 4_500_007])
 def test_sort_onesweep(gpu, n):
     rng = np.random.default_rng(n)
     w0 = torch.from_numpy(rng.integers(0, 10, n).astype(np.int64))
@@ -246,6 +246,27 @@ def test_device_long_key_order_without_host_fix(gpu):
     assert got == words
 
 
+@pytest.mark.parametrize("rounds", [16, 24, 32])
+def test_sort_onesweep_large_tile_sizes(gpu, rounds):
+    """Sorts of >= 4 M keys with every instantiated tile size (MR_SORT_ROUNDS
+    keys per thread): permutation and sorted top bits equal the CPU sort's."""
+    from lua_mapreduce_1_amd.ops import _hip
+    from lua_mapreduce_1_amd.utils.config import TUNABLES
+    rng = np.random.default_rng(rounds)
+    n = (1 << 22) + 12_345
+    w = torch.from_numpy(rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64))
+    w[::7] = w[3]  # ties keep their input order (stability)
+    assert _hip.lib().mr_sort_set_rounds(rounds) == 0
+    try:
+        pg, kg = ops.sort_keys([w.to(gpu)], bits=[64], return_keys=True, from_bit=32)
+        assert not ops.sort_error(gpu)
+    finally:
+        _hip.lib().mr_sort_set_rounds(TUNABLES.sort_rounds)
+    pc = ops.sort_keys([w >> 32 & 0xFFFFFFFF], bits=[32])
+    assert torch.equal(pg.cpu().long(), pc)
+    assert torch.equal(kg.cpu(), w[pc])
+
+
 @pytest.mark.parametrize("resident,next_map", [(False, "auto"), (True, "auto"), (True, "before_sync"),
                                                (False, "before_tail")])
 def test_spmd_prefetch_pipelined_iterations_match(gpu, monkeypatch, resident, next_map):
@@ -253,10 +274,13 @@ def test_spmd_prefetch_pipelined_iterations_match(gpu, monkeypatch, resident, ne
     the same results as non-pipelined ones (and the counts stay exact); also
     with HBM-resident input and every MR_NEXT_MAP mode (auto = chain for
     resident input: the next map queued before this map's sync, gated on its
-    completion)."""
+    completion).  The first map grows the later maps' tables to the sparse
+    capacity (MR_MAP_SPARSE_MIN_MB=0, 64 slots per key: past the default
+    2^20), also while a map is queued ahead."""
     import dataclasses
     from lua_mapreduce_1_amd.parallel import spmd as S
-    monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(S.TUNABLES, next_map=next_map))
+    monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(S.TUNABLES, next_map=next_map, map_sparse_min_mb=0.0,
+                                                           map_sparsity=64))
     from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore
     from lua_mapreduce_1_amd.utils.corpus import europarl_like
     M = "lua_mapreduce_1_amd.models.wordcount"
@@ -284,6 +308,8 @@ def test_spmd_prefetch_pipelined_iterations_match(gpu, monkeypatch, resident, ne
         got = {k: v[0] for _n, cols in eng.gather_results(r) for k, v in codec.iter_columnar(cols)}
         assert got == want
     assert eng._pending is None and not eng._inflight
+    want_cap = ops.next_pow2(64 * ref_keys)
+    assert want_cap > 1 << 20 and all(t is not None and t.cap == want_cap for t in eng.tables)  # both slots grew
 
 
 @pytest.mark.parametrize("W", [1, 3, 8])
