@@ -72,7 +72,7 @@ _SIGS = {
     "mr_ii_insert_slots": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _p, _p],
     "mr_ii_seg_gather": [_p, _p, _p, _u64, _u64, _p, _p, _p],
     "mr_ts_gen": [_p, _u64, _u64, _u64, _p],
-    "mr_ts_keys": [_p, _u64, _p, _p, _p],
+    "mr_ts_keys": [_p, _u64, _p, _p, _p, _p],
     "mr_ts_dest": [_p, _u64, _p, _u32, _p, _p],
     "mr_ts_gather": [_p, _p, _u64, _p, _p],
     "mr_ts_checksum": [_p, _u64, _p, _p],

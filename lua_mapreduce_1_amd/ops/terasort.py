@@ -46,13 +46,16 @@ def generate(n: int, first: int, seed: int, device="cpu") -> torch.Tensor:
     return out
 
 
-def keys(rec: torch.Tensor):
-    """(hi, lo) int64 sort words of each record."""
+def keys(rec: torch.Tensor, ghist: torch.Tensor | None = None):
+    """(hi, lo) int64 sort words of each record.  ``ghist`` (GPU, a zeroed
+    int32 [2048]): also receives the digit histograms of hi's top 32 bits,
+    for :func:`sort_perm` (the sort then skips its histogram pass)."""
     n = rec.shape[0]
     if rec.is_cuda:
         hi = torch.empty(n, dtype=torch.int64, device=rec.device)
         lo = torch.empty(n, dtype=torch.int64, device=rec.device)
-        _hip.call("mr_ts_keys", _hip.ptr(rec), n, _hip.ptr(hi), _hip.ptr(lo), _hip.stream(rec.device))
+        _hip.call("mr_ts_keys", _hip.ptr(rec), n, _hip.ptr(hi), _hip.ptr(lo),
+                  _hip.ptr(ghist) if ghist is not None else None, _hip.stream(rec.device))
         return hi, lo
     a = rec.numpy()
     hi = np.ascontiguousarray(a[:, 0:8]).view(">u8").reshape(n).astype(np.uint64)
@@ -116,18 +119,19 @@ def unsorted_pairs(hi: torch.Tensor, lo: torch.Tensor) -> int:
     return int(np.count_nonzero((h[:-1] > h[1:]) | ((h[:-1] == h[1:]) & (lw[:-1] > lw[1:]))))
 
 
-def sort_perm(hi: torch.Tensor, lo: torch.Tensor) -> torch.Tensor:
+def sort_perm(hi: torch.Tensor, lo: torch.Tensor, ghist: torch.Tensor | None = None) -> torch.Tensor:
     """Permutation sorting rows by the 80-bit key (hi, lo).
 
     GPU: radix-sort the top 32 bits of hi (4 onesweep passes instead of 8)
     and order the runs of rows equal in those bits by (hi, lo) in a fix-up
     kernel — TeraGen keys are uniform, so ~2% of the rows sit in such a run,
     nearly all of length 2; a run longer than 64 (skewed keys) falls back to
-    the full (hi, lo) sort."""
+    the full (hi, lo) sort.  ``ghist``: the histograms :func:`keys` computed
+    along with hi (skips the sort's histogram pass)."""
     from .primitives import sort_keys
     if not hi.is_cuda:
         return sort_keys([hi, lo], bits=[64, 16])
-    perm, shi = sort_keys([hi], bits=[64], return_keys=True, from_bit=_TOP_FROM_BIT)
+    perm, shi = sort_keys([hi], bits=[64], return_keys=True, from_bit=_TOP_FROM_BIT, ghist=ghist)
     bad = torch.zeros(1, dtype=torch.int32, device=hi.device)
     _hip.call("mr_ts_tie_fixup2", _hip.ptr(shi), _hip.ptr(perm), _hip.ptr(lo), hi.numel(), _hip.ptr(bad),
               _TOP_FROM_BIT, _hip.stream(hi.device))

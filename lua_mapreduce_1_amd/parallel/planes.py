@@ -493,8 +493,8 @@ class RecordPlane:
         pick = torch.tensor([(m * j) // R for j in range(1, R)], dtype=torch.int64, device=srt.device)
         return srt[pick].contiguous()
 
-    def _sort_perm(self, hi, lo):
-        perm = TS.sort_perm(hi, lo)
+    def _sort_perm(self, hi, lo, ghist=None):
+        perm = TS.sort_perm(hi, lo, ghist)
         if hi.is_cuda and ops.sort_error(hi.device):
             perm = ops.sort_keys_checked([hi, lo], bits=[64, 16])
         return perm
@@ -544,8 +544,10 @@ class RecordPlane:
         T["shuffle"] = time.time() - t1
         t2 = time.time()
         with trace.range("mr.rec.sort"):
-            hi, lo = TS.keys(rec)
-            perm = self._sort_perm(hi, lo)
+            # the sort's digit histograms come out of the key extraction
+            gh = torch.zeros(2048, dtype=torch.int32, device=rec.device) if rec.is_cuda else None
+            hi, lo = TS.keys(rec, gh)
+            perm = self._sort_perm(hi, lo, gh)
             out = TS.gather(rec, perm)
             if R > 1:
                 shi = hi[perm.long()]

@@ -158,6 +158,23 @@ def test_gpu_kernels_match_numpy(gpu):
 
 
 @pytest.mark.gpu
+def test_gpu_keys_digit_histograms_feed_the_sort(gpu):
+    """Key extraction with histograms: digits 4..7 of hi equal numpy's counts
+    (digits 0..3 untouched), and the sort fed with them gives the same
+    permutation as the sort that computes its own."""
+    n = 3_000_017
+    rg = TS.generate(n, 5, 99, gpu)
+    gh = torch.zeros(2048, dtype=torch.int32, device=gpu)
+    hg, lg = TS.keys(rg, gh)
+    top = (hg.cpu().numpy().view(np.uint64) >> np.uint64(32)).astype(np.uint64)
+    want = np.zeros((8, 256), np.int64)
+    for b in range(4):
+        want[4 + b] = np.bincount(((top >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.int64), minlength=256)
+    assert np.array_equal(gh.cpu().numpy().reshape(8, 256), want)
+    assert torch.equal(TS.sort_perm(hg, lg, gh), TS.sort_perm(hg, lg))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("partitions", [1, 3])
 def test_gpu_single_rank_sort(gpu, partitions):
     eng = _engine(300_007, gpu, blocks=2, partitions=partitions)
