@@ -1,0 +1,39 @@
+"""Sparse map tables (parallel/spmd.py, MR_MAP_SPARSITY / MR_MAP_SPARSE_MIN_MB):
+after a map of a large enough share, the engine sizes the next maps' tables
+at `map_sparsity` slots per distinct key; the results stay those of the
+first iteration (CPU engine; the GPU path is covered by
+test_ops_gpu.py::test_spmd_prefetch_pipelined_iterations_match)."""
+import dataclasses
+
+from lua_mapreduce_1_amd.parallel import spmd as S
+from lua_mapreduce_1_amd.runtime import codec
+from lua_mapreduce_1_amd.utils.corpus import europarl_like
+
+M = "lua_mapreduce_1_amd.models.wordcount"
+
+
+def _run(monkeypatch, min_mb):
+    monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(S.TUNABLES, map_sparse_min_mb=min_mb, map_sparsity=64))
+    splits = europarl_like(seed=4, lines=4000, words=60_000, vocab_size=30_000, split_lines=500)
+    eng = S.SPMDEngine(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                            init_args={"nsplits": len(splits), "num_reducers": 4}),
+                       split_store=S.SplitStore(splits, pin=False), device="cpu", table_capacity=1 << 12)
+    out = []
+    for _ in range(3):
+        r = eng.run_iteration()
+        out.append({k: v[0] for _n, cols in eng.gather_results(r) for k, v in codec.iter_columnar(cols)})
+    return eng, out
+
+
+def test_tables_grow_after_a_large_map_and_results_stay_exact(monkeypatch):
+    eng, out = _run(monkeypatch, 0.0)
+    assert sum(out[0].values()) == 60_000
+    assert out[0] == out[1] == out[2]
+    assert eng._table_capacity >= 64 * len(out[0])
+    assert eng.table.cap == eng._table_capacity  # the table in use was replaced by a sparse one
+
+
+def test_small_shares_keep_their_table(monkeypatch):
+    eng, out = _run(monkeypatch, 1024.0)
+    assert out[0] == out[2]
+    assert eng._table_capacity < 64 * len(out[0])  # only the overflow regrowth, no sparsity
