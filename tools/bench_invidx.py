@@ -41,6 +41,7 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--reducers", type=int, default=10)
     ap.add_argument("--validate", action="store_true", help="diff 1/8 of the splits against the naive oracle")
+    ap.add_argument("--vocab-log2", type=int, default=0, help="vocabulary table capacity 2^k (0 = the plane's default)")
     args = ap.parse_args()
     rank, world, device = D.init_from_env()
     cdir = corpus_dir(args.seed, corpus.EUROPARL_LINES, corpus.EUROPARL_WORDS)
@@ -52,6 +53,8 @@ def main() -> int:
     store.finish_loading()
     params = dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
                   init_args={"nsplits": len(store), "num_reducers": args.reducers, "quiet": True})
+    if args.vocab_log2:
+        params["table_capacity"] = 1 << args.vocab_log2
     eng = spmd(params, device=device, split_store=store)
     # the next iteration's copies overlap this iteration's sort (three
     # arenas); neither the last warm-up step nor the last timed one starts
