@@ -10,7 +10,9 @@ from lua_mapreduce_1_amd.utils.corpus import europarl_like
 
 text = b"".join(europarl_like())
 dev = torch.frombuffer(bytearray(text), dtype=torch.uint8).cuda()
-tab = ops.HashTable(1 << 21, device="cuda")
+# MR_ABLATE_LOG2CAP: table capacity (default 2^21; the engine uses 2^22 for the full corpus, sparse tables)
+import os
+tab = ops.HashTable(1 << int(os.environ.get("MR_ABLATE_LOG2CAP", "21")), device="cuda")
 cfgs = [int(x) for x in sys.argv[1:]] or [0, 6, 1, 7, 3, 8, 2, 9]
 for c in cfgs:
     for mode, name in ((0, "full"), (1, "no-flush"), (2, "tokenize")):
