@@ -1,4 +1,5 @@
 #!/bin/bash
+# Staged bench with and without the cold file-to-result first iteration, twice each (profiles/r2/cold_ab/)
 set -e
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"

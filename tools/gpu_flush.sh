@@ -1,4 +1,5 @@
 #!/bin/bash
+# Map flush cost breakdown: timing-only ablate modes of config 6 (tools/wc_flush_ablate.py)
 set -e
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"

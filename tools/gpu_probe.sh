@@ -1,4 +1,5 @@
 #!/bin/bash
+# Map on a warm vs cold table at W = 8 and 1 shares, PMC counters of the tail compaction
 set -e
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"

@@ -1,3 +1,5 @@
+#!/bin/bash
+# Round-1 checkpoint: GPU tests, W = 8/4/2 proxies (shader and SDMA downloads), 1-GPU bench
 set -e
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1

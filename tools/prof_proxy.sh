@@ -1,4 +1,5 @@
 #!/bin/bash
+# One rank of an 8-rank job (tools/proxy_rank.py) vs one rank alone, kernel stats of the 8-rank share
 set -e
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"

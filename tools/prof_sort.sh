@@ -1,4 +1,5 @@
 #!/bin/bash
+# Radix sort passes on 100 M keys (tools/sort_passes.py) and their kernel stats
 set -e
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"

@@ -1,3 +1,6 @@
+"""CPU simulation on the synthetic Europarl token stream (6 M tokens): flush entries per token of the
+map kernel's per-chunk combine, and the share of them that belongs to the top-K words (the case for a
+static hot dictionary; profiles/r2/map_kernel/flush_simulation.txt)."""
 import numpy as np, sys
 sys.path.insert(0, '.')
 from lua_mapreduce_1_amd.utils import corpus as C

@@ -1,3 +1,6 @@
+"""CPU simulation of the map kernel's HBM flush count on the synthetic Europarl token stream: per-chunk
+combine at several chunk sizes, and persistent workgroup spans with a capped, evicting LDS table
+(profiles/r2/map_kernel/flush_simulation.txt)."""
 import numpy as np, sys
 sys.path.insert(0, '.')
 from lua_mapreduce_1_amd.utils import corpus as C
