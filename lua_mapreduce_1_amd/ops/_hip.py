@@ -119,6 +119,10 @@ def lib():
         L.mr_set_d2h_mode.restype = None
         L.mr_host_alloc_coherent.argtypes = [_u64]
         L.mr_host_alloc_coherent.restype = _p
+        L.mr_host_alloc.argtypes = [_u64]
+        L.mr_host_alloc.restype = _p
+        L.mr_host_free.argtypes = [_p]
+        L.mr_host_free.restype = _i32
         # downloads: SDMA by default, shader stores with MR_D2H=kernel (see sort.hip mr_d2h_async)
         L.mr_set_d2h_mode(1 if TUNABLES.d2h == "sdma" else 0)
         if L.mr_sort_set_rounds(TUNABLES.sort_rounds) != 0:

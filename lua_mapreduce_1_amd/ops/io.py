@@ -101,6 +101,26 @@ def drop_page_cache(path: str) -> bool:
     return host_lib().mrh_drop_cache(path.encode()) == 0
 
 
+def pinned_empty(nbytes: int) -> torch.Tensor:
+    """Uninitialised uint8 host tensor in pinned memory of exactly ``nbytes``
+    (csrc/hip/sort.hip mr_host_alloc).  torch's pinned allocator rounds a
+    request up to a power of two, and pinning is paid per page: the 291 MB
+    split buffer cost 22 ms as a 512 MB block (tools/cold_probe.py).  The
+    memory is freed when the last tensor viewing it is gone."""
+    import ctypes
+    import weakref
+    from . import _hip
+    n = max(int(nbytes), 1)
+    lib = _hip.lib()
+    ptr = lib.mr_host_alloc(n)
+    if not ptr:
+        return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    arr = (ctypes.c_uint8 * n).from_address(ptr)
+    f = weakref.finalize(arr, lib.mr_host_free, ptr)
+    f.atexit = False  # at interpreter exit the process releases it (the HIP runtime may be gone)
+    return torch.frombuffer(arr, dtype=torch.uint8)[:nbytes]
+
+
 def read_file_bytes(path: str) -> bytes:
     with open(path, "rb") as f:
         return f.read()

@@ -89,7 +89,11 @@ class SplitStore:
         self.own = (int(own[0]), int(own[1]))
         self.base = int(self.offsets[self.own[0]])
         nbytes = int(self.offsets[self.own[1]]) - self.base
-        self.buffer = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin and torch.cuda.is_available())
+        if pin and torch.cuda.is_available() and TUNABLES.pin_exact:
+            from ..ops import io as mio
+            self.buffer = mio.pinned_empty(nbytes)  # exact size: pinning is paid per page
+        else:
+            self.buffer = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin and torch.cuda.is_available())
         self._load = None
         self.paths = None
 

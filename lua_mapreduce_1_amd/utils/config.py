@@ -50,6 +50,9 @@ class Tunables:
     map_sparse_min_mb: float = _knob("MR_MAP_SPARSE_MIN_MB", 128.0,
                                      "SPMD fold plane: input MiB per rank and iteration from which map tables "
                                      "are made sparse (MR_MAP_SPARSITY)")
+    pin_exact: bool = _knob("MR_PIN_EXACT", True,
+                            "split buffers in exact-size pinned memory (mr_host_alloc) instead of torch's "
+                            "power-of-two pinned pool")
     sort_rounds: int = _knob("MR_SORT_ROUNDS", 24,
                              "keys per thread of the onesweep radix tiles of sorts of >= 4 M keys (256 x rounds "
                              "keys per tile; 16, 24 or 32)")

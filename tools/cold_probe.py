@@ -1,7 +1,8 @@
 """Where the cold first iteration's time goes on the host: pinned allocation
 of the rank's split buffer (torch caching host allocator, first and second
 time), and the native loader reading the split files with the page cache
-dropped into pinned vs pageable memory, with 8 / 16 / 32 reader threads.  Usage: python tools/cold_probe.py"""
+dropped into pinned (exact size, mr_host_alloc, or torch's power-of-two pool) vs pageable memory,
+with 8 / 16 / 32 reader threads.  Usage: python tools/cold_probe.py"""
 import os
 import sys
 import time
@@ -20,10 +21,11 @@ ensure_corpus(d, 1234, corpus.EUROPARL_LINES, corpus.EUROPARL_WORDS)
 paths = sorted(os.path.join(d, "files", f) for f in os.listdir(os.path.join(d, "files")))
 lens = np.array([os.path.getsize(p) for p in paths], dtype=np.int64)
 n = int(lens.sum() + len(paths))
-for label, pin, threads in (("pinned (first)", True, 8), ("pinned (again)", True, 8), ("pinned 16 thr", True, 16),
-                            ("pinned 32 thr", True, 32), ("pageable", False, 8)):
+for label, pin, threads in (("exact pinned", "exact", 8), ("torch pinned", True, 8), ("torch pinned again", True, 8),
+                            ("exact pinned 16 thr", "exact", 16), ("exact pinned 32 thr", "exact", 32),
+                            ("pageable", False, 8)):
     t0 = time.perf_counter()
-    buf = torch.empty(n, dtype=torch.uint8, pin_memory=pin)
+    buf = mio.pinned_empty(n) if pin == "exact" else torch.empty(n, dtype=torch.uint8, pin_memory=pin)
     t1 = time.perf_counter()
     for p in paths:
         mio.drop_page_cache(p)
@@ -34,7 +36,7 @@ for label, pin, threads in (("pinned (first)", True, 8), ("pinned (again)", True
                        buf, threads=threads)
     ld.wait()
     t3 = time.perf_counter()
-    print(f"{label:16s} alloc {1e3 * (t1 - t0):7.2f} ms  read {n / 1e6:.0f} MB cold {1e3 * (t3 - t2):7.2f} ms "
+    print(f"{label:20s} alloc {1e3 * (t1 - t0):7.2f} ms  read {n / 1e6:.0f} MB cold {1e3 * (t3 - t2):7.2f} ms "
           f"({n / (t3 - t2) / 1e9:.2f} GB/s)", flush=True)
     if not pin:
         del buf
