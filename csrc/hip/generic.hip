@@ -1,0 +1,322 @@
+// generic.hip — the general device MapReduce plane (parallel/generic.py):
+// arbitrary keys emitted by user device code, folded into typed value columns
+// or appended to per-key value lists.
+//
+// Reference semantics being served (/root/reference/mapreduce/job.lua:83-112):
+// ``emit(key, value)`` groups values by key; the reducer (or the combiner taken
+// from the reduce module, task.lua:325) folds each key's list.  On the device a
+// key is the 128-bit encoding of mr_common.h (exact for <= 15 bytes, prefix +
+// hash with byte verification beyond), located in one byte source by its rep
+// word; a key maps to a slot of an HBM open-addressing table (hashtab.h,
+// OP_NONE: no value in the table itself) and, per slot, either
+//   * K typed value columns (i64 / f64 / f32) folded with sum / min / max by
+//     native global atomics (gfx950 has global_atomic_{add,min,max}_f64 and
+//     add_f32; i64 min/max/add), or
+//   * one appended (slot, value) posting per emit (list mode: the reducer
+//     sees the whole value list, job.lua:98-106,264-284).
+//
+// Keys come either pre-encoded (hi, lo, rep) or as byte spans (start, len) of
+// a text buffer, packed here in the insert kernel (no intermediate key arrays).
+#include <hip/hip_runtime.h>
+#include "mr_common.h"
+#include "hashtab.h"
+
+MR_LONG_MASK_SYMBOL(generic)
+
+namespace mr {
+namespace ag {
+
+enum VType : int { VT_I64 = 0, VT_F64 = 1, VT_F32 = 2, VT_I32 = 3, VT_SCALAR = 4 };
+constexpr int MAXC = 8;
+
+// Column descriptors, passed by value (kernel argument).
+struct Cols {
+  int k;                       // value columns
+  int list;                    // 1: append (slot, value of column 0) postings instead of folding
+  const void* src[MAXC];       // per-row input values (null for a scalar)
+  int stype[MAXC];             // VType of src (VT_SCALAR: the constant sbits, in the dst type)
+  long long sbits[MAXC];
+  void* dst[MAXC];             // per-slot columns (fold) — or, list mode, dst[0] = posting values
+  int dtype[MAXC];             // VT_I64 / VT_F64 / VT_F32
+  int op[MAXC];                // OP_SUM / OP_MIN / OP_MAX
+  long long* post_slot;        // list mode: posting slot ids (sink)
+  u64 post_base;               // list mode: sink index of row 0
+};
+
+struct Keys {
+  const u64* hi;
+  const u64* lo;
+  const u64* rep;
+  u64 rep_add;                 // encoded keys: added to rep offsets
+  const u8* text;              // spans: key bytes = text[start, start + len)
+  const long long* starts;
+  const int* lens;
+  u64 rep_base;                // spans: rep offset of text[0] in the table's byte source
+};
+
+__device__ __forceinline__ long long rd_i64(const Cols& c, int j, u64 i) {
+  switch (c.stype[j]) {
+    case VT_I64: return ((const long long*)c.src[j])[i];
+    case VT_I32: return (long long)((const int*)c.src[j])[i];
+    case VT_F64: return (long long)((const double*)c.src[j])[i];
+    case VT_F32: return (long long)((const float*)c.src[j])[i];
+    default: return c.sbits[j];
+  }
+}
+
+__device__ __forceinline__ double rd_f64(const Cols& c, int j, u64 i) {
+  switch (c.stype[j]) {
+    case VT_I64: return (double)((const long long*)c.src[j])[i];
+    case VT_I32: return (double)((const int*)c.src[j])[i];
+    case VT_F64: return ((const double*)c.src[j])[i];
+    case VT_F32: return (double)((const float*)c.src[j])[i];
+    default: return __longlong_as_double(c.sbits[j]);
+  }
+}
+
+__device__ __forceinline__ float rd_f32(const Cols& c, int j, u64 i) {
+  switch (c.stype[j]) {
+    case VT_I64: return (float)((const long long*)c.src[j])[i];
+    case VT_I32: return (float)((const int*)c.src[j])[i];
+    case VT_F64: return (float)((const double*)c.src[j])[i];
+    case VT_F32: return ((const float*)c.src[j])[i];
+    default: return __int_as_float((int)c.sbits[j]);
+  }
+}
+
+__device__ __forceinline__ void fold_col(const Cols& c, int j, u64 i, u64 slot) {
+  const int op = c.op[j];
+  if (c.dtype[j] == VT_I64) {
+    long long* p = (long long*)c.dst[j] + slot;
+    const long long v = rd_i64(c, j, i);
+    if (op == OP_MIN) atomicMin(p, v);
+    else if (op == OP_MAX) atomicMax(p, v);
+    else atomicAdd((unsigned long long*)p, (unsigned long long)v);
+  } else if (c.dtype[j] == VT_F64) {
+    double* p = (double*)c.dst[j] + slot;
+    const double v = rd_f64(c, j, i);
+    if (op == OP_MIN) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (op == OP_MAX) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    float* p = (float*)c.dst[j] + slot;
+    const float v = rd_f32(c, j, i);
+    if (op == OP_MIN) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (op == OP_MAX) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// 128-bit key of text[s, s + len) (mr_common.h encoding; len >= 1).
+__device__ __forceinline__ void span_key(const u8* text, u64 s, u64 len, u64& hi, u64& lo) {
+  const u8* p = text + s;
+  hi = 0;
+  lo = 0;
+  const u64 k8 = len < 8 ? len : 8;
+  for (u64 k = 0; k < k8; ++k) hi |= (u64)p[k] << (56 - 8 * k);
+  if (len <= (u64)PACK_MAX) {
+    for (u64 k = 8; k < len; ++k) lo |= (u64)p[k] << (56 - 8 * (k - 8));
+    lo |= len;
+    return;
+  }
+  u64 h = long_hash_init(len);
+  for (u64 w = 0; w < len; w += 8) {
+    u64 word = 0;
+    const u64 n = (len - w) < 8 ? (len - w) : 8;
+    for (u64 j = 0; j < n; ++j) word |= (u64)p[w + j] << (8 * j);
+    h = long_hash_step(h, word);
+  }
+  lo = long_lo(h, mr_long_mask);
+}
+
+// One row per thread: key -> slot (insert or find), then fold the row's values
+// into the slot's columns, or append its posting.  Rows with an empty span
+// (len <= 0) are skipped (list mode: posting slot -1).  An insert that runs
+// out of probes sets the table's overflow flag; the host regrows and re-runs.
+__global__ void __launch_bounds__(256) agg_insert_kernel(GTab g, Keys ks, u64 n, Cols c) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  u32 claims = 0;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u64 hi = 0, lo = 0, rep = 0;
+    bool ok = true;
+    if (ks.text) {
+      const long long s = ks.starts[i];
+      const int len = ks.lens[i];
+      if (len <= 0 || s < 0) {
+        ok = false;
+      } else {
+        span_key(ks.text, (u64)s, (u64)len, hi, lo);
+        rep = make_rep(ks.rep_base + (u64)s, (u64)len);
+      }
+    } else {
+      hi = ks.hi[i];
+      lo = ks.lo[i];
+      rep = ks.rep ? ks.rep[i] + (ks.rep_add << REP_LEN_BITS) : 0;
+    }
+    u64 slot = 0;
+    int r = 0;
+    if (ok) {
+      r = gtab_insert(g, hi, lo, 0, rep, OP_NONE, &slot);
+      claims += r == 2;
+    }
+    if (c.list) {
+      c.post_slot[c.post_base + i] = r ? (long long)slot : -1;
+      ((long long*)c.dst[0])[c.post_base + i] =
+          c.dtype[0] == VT_F64 ? __double_as_longlong(rd_f64(c, 0, i)) : rd_i64(c, 0, i);
+    } else if (r) {
+      for (int j = 0; j < c.k; ++j) fold_col(c, j, i, slot);
+    }
+  }
+  gtab_count_claims(g, claims);
+}
+
+// Occupied slots -> dense (slot, hi, lo, rep).  One 256-thread block per 4096
+// slots: per-thread counts, LDS scan, one atomic per block for the base.
+constexpr int SC_ITEMS = 16;
+__global__ void __launch_bounds__(256) slot_compact_kernel(GTab g, u64 cap, long long* out_slot, u64* out_hi,
+                                                           u64* out_lo, u64* out_rep, unsigned long long* counter) {
+  __shared__ u32 sh[256];
+  __shared__ unsigned long long base;
+  const int t = threadIdx.x;
+  const u64 b0 = (u64)blockIdx.x * 256 * SC_ITEMS;
+  u32 occ = 0, n = 0;
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) {
+    const u64 i = b0 + (u64)k * 256 + t;
+    const bool o = i < cap && g.tag[i] != 0;
+    occ |= (o ? 1u : 0u) << k;
+    n += o ? 1u : 0u;
+  }
+  sh[t] = n;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const u32 y = t >= o ? sh[t - o] : 0u;
+    __syncthreads();
+    sh[t] += y;
+    __syncthreads();
+  }
+  if (t == 255) base = atomicAdd(counter, (unsigned long long)sh[255]);
+  __syncthreads();
+  u64 o = base + sh[t] - n;
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) {
+    if (occ & (1u << k)) {
+      const u64 i = b0 + (u64)k * 256 + t;
+      out_slot[o] = (long long)i;
+      out_hi[o] = g.hi[i];
+      out_lo[o] = g.lo[i];
+      out_rep[o] = g.rep[i];
+      ++o;
+    }
+  }
+}
+
+// Fill a typed column with its fold identity (sum 0, min +max, max -max).
+__global__ void col_fill_kernel(void* col, u64 n, long long bits, int width) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (width == 8) ((long long*)col)[i] = bits;
+    else ((int*)col)[i] = (int)bits;
+  }
+}
+
+}  // namespace ag
+}  // namespace mr
+
+using namespace mr;
+using namespace mr::ag;
+
+static inline unsigned ag_grid(u64 n, unsigned block, unsigned cap = 8192) {
+  u64 g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+static inline GTab ag_gtab(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, const void* src) {
+  GTab g;
+  g.tag = (u64*)tag;
+  g.hi = (u64*)hi;
+  g.lo = (u64*)lo;
+  g.val = (long long*)val;
+  g.rep = (u64*)rep;
+  g.ctrl = (u32*)ctrl;
+  g.mask = cap - 1;
+  g.src = (const u8*)src;
+  return g;
+}
+
+// Host-side mirror of Cols for ctypes (same field order, fixed arrays).
+struct ColsArg {
+  long long k, list;
+  const void* src[MAXC];
+  long long stype[MAXC];
+  long long sbits[MAXC];
+  void* dst[MAXC];
+  long long dtype[MAXC];
+  long long op[MAXC];
+  void* post_slot;
+  unsigned long long post_base;
+};
+
+static Cols to_cols(const ColsArg* a) {
+  Cols c;
+  c.k = (int)a->k;
+  c.list = (int)a->list;
+  for (int j = 0; j < MAXC; ++j) {
+    c.src[j] = a->src[j];
+    c.stype[j] = (int)a->stype[j];
+    c.sbits[j] = a->sbits[j];
+    c.dst[j] = a->dst[j];
+    c.dtype[j] = (int)a->dtype[j];
+    c.op[j] = (int)a->op[j];
+  }
+  c.post_slot = (long long*)a->post_slot;
+  c.post_base = a->post_base;
+  return c;
+}
+
+extern "C" {
+
+// Keys pre-encoded (hi, lo, rep + rep_add) — or, when `text` is given, byte
+// spans (starts int64, lens int32) of `text`, whose rep offsets are
+// rep_base + start.  `src`: the byte source every rep word of the table
+// indexes (long-key byte verification).
+int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void* ctrl, u64 cap, const void* src,
+                  const void* hi, const void* lo, const void* rep, u64 rep_add, const void* text, const void* starts,
+                  const void* lens, u64 rep_base, u64 n, const void* cols, hipStream_t stream) {
+  if (n == 0) return 0;
+  const ColsArg* a = (const ColsArg*)cols;
+  if (a->k < 0 || a->k > MAXC || (a->list && a->k != 1)) return -1;
+  Keys ks;
+  ks.hi = (const u64*)hi;
+  ks.lo = (const u64*)lo;
+  ks.rep = (const u64*)rep;
+  ks.rep_add = rep_add;
+  ks.text = (const u8*)text;
+  ks.starts = (const long long*)starts;
+  ks.lens = (const int*)lens;
+  ks.rep_base = rep_base;
+  if (!ks.text && (!ks.hi || !ks.lo)) return -2;
+  hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256)), dim3(256), 0, stream,
+                     ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
+  return (int)hipGetLastError();
+}
+
+int mr_slot_compact(void* tag, void* thi, void* tlo, void* tval, void* trep, void* ctrl, u64 cap, void* out_slot,
+                    void* out_hi, void* out_lo, void* out_rep, void* counter, hipStream_t stream) {
+  const u64 nb = (cap + 256 * SC_ITEMS - 1) / (256 * SC_ITEMS);
+  hipLaunchKernelGGL(slot_compact_kernel, dim3((unsigned)nb), dim3(256), 0, stream,
+                     ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, nullptr), cap, (long long*)out_slot,
+                     (u64*)out_hi, (u64*)out_lo, (u64*)out_rep, (unsigned long long*)counter);
+  return (int)hipGetLastError();
+}
+
+int mr_col_fill(void* col, u64 n, long long bits, int width, hipStream_t stream) {
+  if (n == 0) return 0;
+  if (width != 4 && width != 8) return -1;
+  hipLaunchKernelGGL(col_fill_kernel, dim3(ag_grid(n, 256)), dim3(256), 0, stream, col, n, bits, width);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

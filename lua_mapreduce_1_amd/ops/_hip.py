@@ -97,8 +97,18 @@ _SIGS = {
     "mr_table_reset": [_p, _p, _p, _p, _u64, ctypes.c_longlong, _p],
     "mr_table_rehome": [_p, _p, _p, _u64, _p, _u64, _u64, _p, _u64, _p],
     "mr_scan_partials_len": [_u64],
+    "mr_agg_insert": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _u64, _p, _p],
+    "mr_slot_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
+    "mr_col_fill": [_p, _u64, ctypes.c_longlong, _i32, _p],
+    "mr_set_long_mask_generic": [_u64],
+    "mr_text_tiles": [_u64],
+    "mr_text_count": [_p, _u64, _i32, _u32, _p, _p],
+    "mr_text_emit": [_p, _u64, _i32, _u32, _p, _u64, _p, _p, _p],
+    "mr_text_field": [_p, _p, _p, _u64, _u32, _i32, _p, _p, _p],
+    "mr_text_parse_f64": [_p, _p, _p, _u64, _p, _p, _p],
+    "mr_text_parse_i64": [_p, _p, _p, _u64, _p, _p, _p],
 }
-_RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
+_RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
                 "mr_tail_bhist_bytes", "mr_onesweep_tiles"}
 
 
@@ -131,7 +141,8 @@ def lib():
     return _LIB
 
 
-_LONG_MASK_SETTERS = ("mr_set_long_mask_wc3", "mr_set_long_mask_keyops", "mr_set_long_mask_invidx")
+_LONG_MASK_SETTERS = ("mr_set_long_mask_wc3", "mr_set_long_mask_keyops", "mr_set_long_mask_invidx",
+                      "mr_set_long_mask_generic")
 
 
 def set_long_mask(mask: int) -> None:

@@ -140,6 +140,14 @@ class PostingSink:
     def reset(self) -> None:
         self.ctrl.zero_()
 
+    def ctrl_snapshot(self) -> torch.Tensor:
+        """Posting count before a chunk's map (device copy, no sync)."""
+        return self.ctrl[:1].clone()
+
+    def ctrl_restore(self, snap: torch.Tensor) -> None:
+        """Drop the postings written since ``snap`` (a map attempt that raised)."""
+        self.ctrl[:1].copy_(snap)
+
     def finish(self, vocab: "Vocab") -> torch.Tensor:
         n, e = self.ctrl.tolist()  # the one host synchronisation of the map phase
         if e & 2:

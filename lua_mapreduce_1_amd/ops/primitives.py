@@ -17,6 +17,7 @@ Kernel inventory -> function here:
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import numpy as np
@@ -28,7 +29,10 @@ from ..utils.config import TUNABLES
 
 import os as _os
 
-OPS = {"sum": 0, "min": 1, "max": 2}
+# "count" folds like "sum" (a map emits 1 per occurrence, the reduce side sums
+# partial counts); "none": keys only (a vocabulary, or the general plane's
+# key -> slot table: csrc/hip/generic.hip)
+OPS = {"sum": 0, "min": 1, "max": 2, "count": 0, "none": 4}
 # MR_DEBUG_CHECKS=1: validate the offsets/indices a kernel will dereference
 # (with safe torch ops) before launching it, so a bad input raises in Python
 # instead of faulting the GPU.
@@ -52,7 +56,7 @@ _I64_MIN = -(1 << 63)
 
 
 def _op_init(op: str) -> int:
-    return {"sum": 0, "min": _I64_MAX, "max": _I64_MIN}[op]
+    return {"sum": 0, "count": 0, "none": 0, "min": _I64_MAX, "max": _I64_MIN}[op]
 
 
 def next_pow2(n: int) -> int:
@@ -154,6 +158,52 @@ class HashTable:
             if rep is not None and rep_add:
                 r = r + np.uint64(rep_add << K.REP_LEN_BITS)
             self._pending.append((_u64(hi).copy(), _u64(lo).copy(), v, r))
+
+    def insert_spans(self, text: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor, val=None, rep_base: int = 0,
+                     src: torch.Tensor | None = None) -> None:
+        """Fold the keys ``text[starts[i] : starts[i] + lens[i]]`` (empty spans
+        skipped) with values ``val`` (tensor, scalar, or None = 1); their rep
+        words are ``rep_base + start`` in the table's byte source (the
+        general plane's insert kernel, csrc/hip/generic.hip)."""
+        n = starts.numel()
+        if src is not None:
+            self.src = src
+        if n == 0:
+            return
+        if self.is_cuda:
+            from . import agg as A
+            a = A._ColsArg()
+            a.k, a.list = 1, 0
+            keep = []
+            if isinstance(val, torch.Tensor):
+                v = val.to(self.device)
+                if v.dtype not in A._VT:
+                    v = v.to(torch.float64 if v.is_floating_point() else torch.int64)
+                v = v.contiguous()
+                keep.append(v)
+                a.src[0], a.stype[0] = v.data_ptr(), A._VT[v.dtype]
+            else:
+                a.stype[0], a.sbits[0] = A._VT_SCALAR, int(1 if val is None else val)
+            a.dst[0], a.dtype[0], a.op[0] = self.val.data_ptr(), 0, OPS[self.op]
+            st = starts.to(torch.int64).contiguous()
+            ln = lens.to(torch.int32).contiguous()
+            _hip.call("mr_agg_insert", *self._gtab(), self.cap, _hip.ptr(self.src), None, None, None, 0,
+                      _hip.ptr(text), _hip.ptr(st), _hip.ptr(ln), rep_base, n, ctypes.byref(a),
+                      _hip.stream(self.device))
+            return
+        buf = _np(text)
+        st = _np(starts).astype(np.int64)
+        ln = _np(lens).astype(np.int64)
+        ok = (ln > 0) & (st >= 0)
+        st, ln = st[ok], ln[ok]
+        hi, lo = K.span_keys(buf, st, ln)
+        rep = ((st.astype(np.uint64) + np.uint64(rep_base)) << np.uint64(K.REP_LEN_BITS)) | \
+            np.minimum(ln, K.REP_LEN_MASK).astype(np.uint64)
+        if isinstance(val, torch.Tensor):
+            v = _np(val).astype(np.int64)[ok]
+        else:
+            v = np.full(st.size, 1 if val is None else int(val), np.int64)
+        self._pending.append((hi, lo, v, rep))
 
     def _overflow(self, nbytes: int):
         """Overflow entries (hi, lo, rep) of the map kernel: tokens that found
@@ -300,7 +350,7 @@ class HashTable:
                 o, ln = rr >> K.REP_LEN_BITS, rr & K.REP_LEN_MASK
                 d[i] = ids.setdefault(sb[o:o + ln].tobytes(), len(ids) + 1)
         uk, first, inv = np.unique(keys, return_index=True, return_inverse=True)
-        if self.op == "sum":
+        if self.op in ("sum", "count", "none"):
             agg = np.zeros(uk.size, np.int64)
             np.add.at(agg, inv, v)
         elif self.op == "min":

@@ -1,0 +1,175 @@
+"""Text scanning and parsing for user device map functions (HIP kernels in
+``csrc/hip/text.hip``; NumPy on CPU tensors — the executable specification).
+
+A ``device_mapfn`` picks its keys and values out of the staged input bytes
+with these plus ordinary torch ops, then hands them to ``emit.spans`` (see
+parallel/generic.py).  They replace the reference's Lua string functions in
+user map code: ``line:gmatch("[^%s]+")`` (examples/WordCount/mapfn.lua:5),
+``io.lines`` (mapfn.lua:4) and ``tonumber``.
+
+Every function returns tensors on the device of ``text``; positions are byte
+offsets into ``text`` (int64) and lengths are int32, in text order.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _hip
+from .keys import _WS_TABLE
+
+
+def _np(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().numpy()
+
+
+def _scan(text: torch.Tensor, mode: int, byte: int, want_len: bool):
+    n = text.numel()
+    d = text.device
+    if n == 0:
+        z = torch.zeros(0, dtype=torch.int64, device=d)
+        return z, (torch.zeros(0, dtype=torch.int32, device=d) if want_len else None)
+    if text.is_cuda:
+        from .primitives import exclusive_scan
+        assert text.dtype == torch.uint8 and text.is_contiguous()
+        s = _hip.stream(d)
+        tiles = int(_hip.lib().mr_text_tiles(n))
+        counts = torch.empty(tiles, dtype=torch.int64, device=d)
+        _hip.call("mr_text_count", _hip.ptr(text), n, mode, byte, _hip.ptr(counts), s)
+        off, total = exclusive_scan(counts)
+        m = int(total.item())
+        pos = torch.empty(m, dtype=torch.int64, device=d)
+        ln = torch.empty(m, dtype=torch.int32, device=d) if want_len else None
+        _hip.call("mr_text_emit", _hip.ptr(text), n, mode, byte, _hip.ptr(off), m, _hip.ptr(pos),
+                  _hip.ptr(ln) if ln is not None else None, s)
+        return pos, ln
+    b = _np(text)
+    if mode == 1:
+        return torch.from_numpy(np.flatnonzero(b == byte).astype(np.int64)), None
+    ws = _WS_TABLE[b]
+    d_ = np.diff((~ws).astype(np.int8), prepend=0, append=0)
+    starts = np.flatnonzero(d_ == 1).astype(np.int64)
+    ends = np.flatnonzero(d_ == -1).astype(np.int64)
+    return torch.from_numpy(starts), torch.from_numpy((ends - starts).astype(np.int32))
+
+
+def tokens(text: torch.Tensor):
+    """(starts int64, lens int32) of every whitespace token (maximal run of
+    bytes outside Lua's ``%s``), in text order."""
+    return _scan(text, 0, 0, True)
+
+
+def find_byte(text: torch.Tensor, byte: int) -> torch.Tensor:
+    """Positions (int64, ascending) of every byte equal to ``byte``."""
+    return _scan(text, 1, int(byte) & 0xFF, False)[0]
+
+
+def lines(text: torch.Tensor):
+    """(starts int64, lens int32) of every line (bytes between newlines, the
+    newline excluded; empty lines included; a final newline does not open an
+    empty last line)."""
+    n = text.numel()
+    nl = find_byte(text, 10)
+    d = text.device
+    zero = torch.zeros(1, dtype=torch.int64, device=d)
+    starts = torch.cat([zero, nl + 1])
+    ends = torch.cat([nl, torch.full((1,), n, dtype=torch.int64, device=d)])
+    if n == 0 or (nl.numel() and int(nl[-1]) == n - 1):
+        starts, ends = starts[:-1], ends[:-1]
+    return starts, (ends - starts).to(torch.int32)
+
+
+def line_index(text: torch.Tensor, positions: torch.Tensor, newlines: torch.Tensor | None = None) -> torch.Tensor:
+    """0-based line number of each byte position (int64)."""
+    nl = find_byte(text, 10) if newlines is None else newlines
+    return torch.searchsorted(nl, positions, right=False)
+
+
+def field(text: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor, sep: int | bytes, k: int):
+    """Span of field ``k`` (0-based) of each line given by (starts, lens),
+    fields separated by the byte ``sep``; a trailing ``\\r`` is dropped.  A
+    missing field has start -1 and length 0."""
+    if isinstance(sep, (bytes, str)):
+        sep = (sep.encode() if isinstance(sep, str) else sep)[0]
+    m = starts.numel()
+    d = text.device
+    if text.is_cuda:
+        st = starts.to(torch.int64).contiguous()
+        ln = lens.to(torch.int32).contiguous()
+        fs = torch.empty(m, dtype=torch.int64, device=d)
+        fl = torch.empty(m, dtype=torch.int32, device=d)
+        _hip.call("mr_text_field", _hip.ptr(text), _hip.ptr(st), _hip.ptr(ln), m, int(sep), int(k), _hip.ptr(fs),
+                  _hip.ptr(fl), _hip.stream(d))
+        return fs, fl
+    b = _np(text).tobytes()
+    fs = np.full(m, -1, np.int64)
+    fl = np.zeros(m, np.int32)
+    sb = bytes([sep])
+    for i, (s, n) in enumerate(zip(_np(starts).tolist(), _np(lens).tolist())):
+        line = b[s:s + n]
+        if line.endswith(b"\r"):
+            line = line[:-1]
+        if n <= 0:
+            continue
+        parts = line.split(sb)
+        if k < len(parts):
+            fs[i] = s + sum(len(p) + 1 for p in parts[:k])
+            fl[i] = len(parts[k])
+    return torch.from_numpy(fs), torch.from_numpy(fl)
+
+
+def _parse_host(b: bytes, s: int, n: int, kind):
+    if s < 0:
+        raise ValueError
+    tok = b[s:s + n].decode("ascii").strip(" \t\n\v\f\r")
+    if not tok:
+        raise ValueError
+    if kind is int:
+        if not (tok.lstrip("+-").isdigit()) or len(tok.lstrip("+-")) > 19:
+            raise ValueError
+        return int(tok)
+    if any(c not in "0123456789+-.eE" for c in tok):
+        raise ValueError
+    return float(tok)
+
+
+def _parse(text, starts, lens, kind, check: bool):
+    m = starts.numel()
+    d = text.device
+    dt = torch.float64 if kind is float else torch.int64
+    if text.is_cuda:
+        st = starts.to(torch.int64).contiguous()
+        ln = lens.to(torch.int32).contiguous()
+        out = torch.empty(m, dtype=dt, device=d)
+        err = torch.zeros(1, dtype=torch.int32, device=d)
+        name = "mr_text_parse_f64" if kind is float else "mr_text_parse_i64"
+        _hip.call(name, _hip.ptr(text), _hip.ptr(st), _hip.ptr(ln), m, _hip.ptr(out), _hip.ptr(err), _hip.stream(d))
+        if check and int(err.item()):
+            raise ValueError("malformed number in the parsed spans")
+        return out
+    b = _np(text).tobytes()
+    out = np.zeros(m, np.float64 if kind is float else np.int64)
+    bad = False
+    for i, (s, n) in enumerate(zip(_np(starts).tolist(), _np(lens).tolist())):
+        try:
+            out[i] = _parse_host(b, s, n, kind)
+        except (ValueError, UnicodeDecodeError):
+            out[i] = np.nan if kind is float else 0
+            bad = True
+    if check and bad:
+        raise ValueError("malformed number in the parsed spans")
+    return torch.from_numpy(out)
+
+
+def parse_f64(text: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor, check: bool = False) -> torch.Tensor:
+    """Decimal numbers of the spans as float64 (``[+-]digits[.digits][e[+-]digits]``
+    with surrounding whitespace): correctly rounded when the significant
+    digits fit 53 bits and the exponent is within +-22 (what Python's float()
+    gives), a few ulp off otherwise.  Malformed spans give NaN (``check``:
+    raise instead, one host synchronisation)."""
+    return _parse(text, starts, lens, float, check)
+
+
+def parse_i64(text: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor, check: bool = False) -> torch.Tensor:
+    """Decimal integers of the spans as int64 (malformed: 0, or raise with ``check``)."""
+    return _parse(text, starts, lens, int, check)

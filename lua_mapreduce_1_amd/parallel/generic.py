@@ -1,0 +1,678 @@
+"""General device MapReduce plane: any keys, typed folds, value lists, or the
+user's own reducefn — so a job that is not word count, word -> lines or
+TeraSort still runs its map, grouping and shuffle on the GPU.
+
+The reference's contract (/root/reference/mapreduce/job.lua:83-112,264-284):
+``mapfn`` emits (key, value) pairs, values are grouped per key, the combiner
+(taken from the reduce module, task.lua:325) and the reducer fold each key's
+list.  Here a ``device_mapfn(key, data, emit)`` picks keys and values out of
+the staged bytes with torch ops and ops/text.py, and emits them in batches:
+
+* ``emit.spans(starts, lens, *values, text=None)`` — key i = the bytes
+  ``text[starts[i] : starts[i] + lens[i]]`` (default ``text``: the staged
+  chunk being mapped); empty spans (len <= 0) are skipped;
+* ``emit.pairs(hi, lo, *values, rep=None, src=None)`` — keys already encoded
+  (ops/keys.py), long keys' bytes located by ``rep`` in ``src``;
+* ``emit.words(text=None, *values)`` — every whitespace token (value 1 by
+  default); ``emit.word_lines(text=None)`` — every token with the global
+  number of its line (the inverted index's pairs);
+* ``emit(key, *values)`` — one host pair (buffered, inserted in one batch).
+
+``values``: one tensor (one value per key) or Python number per input column.
+What happens to them is the reduce module's ``device_reduce``:
+
+* a column spec, ``"f64:sum"``, ``("f64:mean", "f64:max", "count")``, ...
+  (ops/agg.py) — each key's values are folded in place into typed columns
+  (native f64/f32/i64 atomics); the result of a key is the list of its
+  output columns, like a reducefn that emits several values;
+* ``"concat"`` / ``"concat_unique"`` — the key's values in emission order /
+  sorted and distinct (int64, or float64 with ``device_value_dtype = "f64"``
+  on the map module);
+* absent — the values are grouped on the device (list, emission order) and
+  the module's own ``reducefn(key, values, emit)`` runs on the host for each
+  key of the rank's partitions (the reduce job), skipping singleton lists
+  when the reducer declares all three ACI flags (job.lua:264-274).  Nothing
+  is folded with an op the user did not declare.
+
+Map-side grouping happens in ONE HBM table per rank (the combiner of
+job.lua:92-96 becomes the fold); the shuffle sends each key (with its folded
+columns or its value list) to the rank owning its partition ``p % W`` in one
+count exchange and three ``all_to_all_single``; the reduce side merges what
+it receives in a second table and orders the keys by (partition, key bytes).
+"""
+from __future__ import annotations
+
+import sys
+import time
+import traceback
+
+import numpy as np
+import torch
+
+from .. import ops, utils
+from ..ops import agg as A
+from ..ops import keys as K
+from ..ops import text as TX
+from ..runtime import codec
+from ..runtime import device as devmod
+from ..runtime import modules
+from ..utils import STATUS
+from ..utils import trace
+from . import dist as D
+
+
+def _bits(n: int) -> int:
+    return max(1, int(max(n, 1) - 1).bit_length())
+
+
+class NeedsHostMap(Exception):
+    """A device map called an emitter that this execution mode cannot run
+    (the caller runs the host ``mapfn`` instead)."""
+
+
+# ---------------------------------------------------------------------------
+class KeySource:
+    """The ONE byte source every rep word of an iteration's table indexes:
+    the engine's staged input arena (keys are spans of the input, read in
+    place), extended on demand by a copy of the arena followed by appended
+    bytes (host keys, spans of derived tensors)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.begin(None)
+
+    def begin(self, arena) -> None:
+        self.arena = arena
+        self.buf = None
+        self.used = arena.numel() if arena is not None else 0
+
+    def set_arena(self, arena) -> None:
+        if self.arena is None and self.buf is None and arena is not None:
+            self.begin(arena)
+
+    def _base(self):
+        return self.buf if self.buf is not None else self.arena
+
+    def offset_of(self, t: torch.Tensor) -> int | None:
+        """Byte offset of ``t`` inside the source (None: not a view of it)."""
+        b = self._base()
+        if b is None or t.device != b.device or t.dtype != torch.uint8:
+            return None
+        p = t.data_ptr() - b.data_ptr()
+        if 0 <= p and p + t.numel() <= self.used:
+            return p
+        return None
+
+    def add(self, t: torch.Tensor) -> tuple[int, torch.Tensor]:
+        """Append ``t``'s bytes; returns (offset, the source's view of them)."""
+        t = t.reshape(-1)
+        if t.dtype != torch.uint8:
+            raise TypeError("key bytes must be a uint8 tensor")
+        n = t.numel()
+        need = self.used + n
+        if self.buf is None or self.buf.numel() < need:
+            cap = max(need, 2 * (self.buf.numel() if self.buf is not None else 0), self.used + (1 << 16))
+            nb = torch.empty(cap, dtype=torch.uint8, device=self.device)
+            if self.buf is not None:
+                nb[:self.used].copy_(self.buf[:self.used])
+            elif self.arena is not None and self.used:
+                nb[:self.used].copy_(self.arena[:self.used])
+            self.buf = nb
+        off = self.used
+        if n:
+            self.buf[off:need].copy_(t, non_blocking=True)
+        self.used = need
+        return off, self.buf[off:need]
+
+    def locate(self, t: torch.Tensor) -> tuple[torch.Tensor, int]:
+        """(device view of t's bytes inside the source, its offset)."""
+        off = self.offset_of(t)
+        if off is not None:
+            return t, off
+        off, view = self.add(t)
+        return view, off
+
+    def source(self) -> torch.Tensor:
+        b = self._base()
+        if b is None:
+            return torch.zeros(1, dtype=torch.uint8, device=self.device)
+        return b[:max(self.used, 1)] if self.used else b[:1]
+
+
+class GenericEmitter:
+    """``emit`` of a general device map (see the module docstring)."""
+
+    def __init__(self, mapper: "GenericMap"):
+        self.m = mapper
+        self.chunk: torch.Tensor | None = None
+        self.line_base = None  # callable: global line number of the chunk's first byte
+        self.err_word = None
+
+    @property
+    def device(self):
+        return self.m.device
+
+    def _text(self, text):
+        t = self.chunk if text is None else text
+        if t is None:
+            raise ValueError("no staged chunk: pass text=")
+        if t.device != self.m.device:
+            t = t.to(self.m.device)
+        return t
+
+    def spans(self, starts, lens, *values, text=None) -> None:
+        t, base = self.m.src.locate(self._text(text))
+        self.m.insert(int(starts.numel()), values, text=t, starts=starts, lens=lens, rep_base=base)
+
+    def pairs(self, hi, lo, *values, rep=None, src=None) -> None:
+        add = 0
+        if src is not None:
+            _, add = self.m.src.locate(src if src.device == self.m.device else src.to(self.m.device))
+        elif rep is not None and self.chunk is not None:
+            add = self.m.src.offset_of(self.chunk) or 0  # rep words relative to the mapped chunk
+        self.m.insert(int(hi.numel()), values, hi=hi, lo=lo, rep=rep, rep_add=add)
+
+    def words(self, text=None, *values) -> None:
+        t = self._text(text)
+        st, ln = TX.tokens(t)
+        self.spans(st, ln, *values, text=t)
+
+    def word_lines(self, text=None) -> None:
+        """Every whitespace token of the chunk with the global (0-based)
+        number of the line it is on (needs split inputs: line numbers are
+        global over every split)."""
+        if self.line_base is None:
+            raise NeedsHostMap("word_lines needs the SPMD engine's global line numbering")
+        t = self._text(text)
+        st, ln = TX.tokens(t)
+        line = TX.line_index(t, st) + int(self.line_base(t))
+        self.spans(st, ln, line, text=t)
+
+    def records(self, *a, **k):
+        raise NeedsHostMap("emit.records needs the record plane (device_reduce = 'identity')")
+
+    def error_word(self):
+        return self.err_word
+
+    def __call__(self, key, *values) -> None:
+        if isinstance(key, str):
+            key = key.encode("utf-8", "surrogateescape")
+        elif not isinstance(key, bytes):
+            key = str(key).encode()
+        if not key:
+            return
+        self.m.host.append((key, values))
+
+
+class GenericMap:
+    """Map-side state of the general plane: the key -> columns / postings
+    table, the byte source of its rep words and the emitter."""
+
+    def __init__(self, device, capacity: int, phys: A.Physical | None, list_dtype: str = "i64"):
+        self.device = torch.device(device)
+        self.phys = phys
+        self.list_dtype = list_dtype
+        self.table = A.AggTable(capacity, self.device, phys.cols if phys is not None else None, list_dtype)
+        self.src = KeySource(self.device)
+        self.emit = GenericEmitter(self)
+        self.host: list = []
+        self.rows = 0
+
+    @property
+    def n_in(self) -> int:
+        return self.phys.n_in if self.phys is not None else 1
+
+    def begin(self, arena=None) -> None:
+        self.table.reset()
+        self.src.begin(arena)
+        self.host = []
+        self.rows = 0
+
+    def insert(self, n: int, values, **kw) -> None:
+        if n == 0:
+            return
+        if len(values) > self.n_in or (self.phys is not None and len(values) not in (0, self.n_in)):
+            raise ValueError(f"{len(values)} value columns emitted, the reduce expects {self.n_in}")
+        if self.phys is not None and not values:
+            values = (1,) * self.n_in
+        self.table.src = self.src.source()
+        self.table.insert(n, list(values), **kw)
+        self.rows += n
+
+    def flush_host(self) -> None:
+        if not self.host:
+            return
+        pairs, self.host = self.host, []
+        blob = b"".join(k for k, _ in pairs)
+        base, _ = self.src.add(torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(self.device))
+        his, los, reps, off = [], [], [], 0
+        for k, _ in pairs:
+            h, l_ = K.pack_key(k)
+            his.append(h)
+            los.append(l_)
+            reps.append(K.make_rep(base + off, len(k)))
+            off += len(k)
+        t64 = lambda a: torch.from_numpy(np.array(a, dtype=np.uint64).view(np.int64)).to(self.device)  # noqa: E731
+        k_in = max(len(v) for _, v in pairs) if self.phys is None else self.n_in
+        cols = []
+        for j in range(k_in):
+            col = [v[j] if j < len(v) else 1 for _, v in pairs]
+            isf = any(isinstance(x, float) for x in col)
+            cols.append(torch.tensor(col, dtype=torch.float64 if isf else torch.int64, device=self.device))
+        self.insert(len(pairs), tuple(cols), hi=t64(his), lo=t64(los), rep=t64(reps))
+
+
+# ---------------------------------------------------------------------------
+def _value_order_key(v: torch.Tensor, dtype: str) -> torch.Tensor:
+    """int64 whose unsigned order is the numeric order of the values (value
+    bit patterns: int64, or float64 when ``dtype`` is f64)."""
+    sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=v.device)
+    if dtype == "f64":
+        neg = v < 0
+        return torch.where(neg, ~v, v ^ sign)
+    return v ^ sign
+
+
+def order_fold(slot, hi, lo, rep, cols, src, nparts: int, partmod, phys: A.Physical, outputs: bool = True) -> dict:
+    """Keys of a folded table in (partition, key) order with their output
+    columns (``outputs=False``: the physical ones, e.g. a mean's sum and
+    count for a later merge), on the device: {hi, lo, key_off, key_blob,
+    cols, counts}."""
+    m = hi.numel()
+    d = hi.device
+    part = devmod.partition_of(hi, lo, rep, src, nparts, partmod) if m else torch.zeros(0, dtype=torch.int32, device=d)
+    if m:
+        perm = ops.sort_keys_checked([part.to(torch.int64), hi, lo], bits=[max(8, _bits(nparts)), 64, 64]).long()
+        hi, lo, rep, part = hi[perm], lo[perm], rep[perm], part[perm]
+        cols = [c[perm] for c in cols]
+    _, klen = ops.key_meta(hi, lo, rep, src, want_part=False)
+    koff, kblob = ops.gather_key_bytes(hi, lo, rep, src, lengths=klen)
+    counts = ops.bincount(part, nparts) if m else torch.zeros(nparts, dtype=torch.int64, device=d)
+    return {"hi": hi, "lo": lo, "key_off": koff, "key_blob": kblob, "cols": phys.outputs(cols) if outputs else cols,
+            "counts": counts}
+
+
+def order_lists(slot, hi, lo, rep, pslot, pval, src, nparts: int, partmod, unique: bool, dtype: str,
+                slot_space: int) -> dict:
+    """Keys in (partition, key) order with their value lists (emission order,
+    or sorted distinct with ``unique``): {hi, lo, key_off, key_blob,
+    list_off, list_val, counts}."""
+    m = hi.numel()
+    d = hi.device
+    part = devmod.partition_of(hi, lo, rep, src, nparts, partmod) if m else torch.zeros(0, dtype=torch.int32, device=d)
+    if m:
+        perm = ops.sort_keys_checked([part.to(torch.int64), hi, lo], bits=[max(8, _bits(nparts)), 64, 64]).long()
+        hi, lo, rep, part, slot = hi[perm], lo[perm], rep[perm], part[perm], slot[perm]
+    rank = torch.full((max(slot_space, 1),), -1, dtype=torch.int64, device=d)
+    rank[slot] = torch.arange(m, dtype=torch.int64, device=d)
+    keep = pslot >= 0
+    pr = rank[pslot.clamp(min=0)]
+    keep &= pr >= 0
+    pr, pv = pr[keep], pval[keep]
+    if pr.numel():
+        if unique:
+            pp = ops.sort_keys_checked([pr, _value_order_key(pv, dtype)], bits=[_bits(m), 64]).long()
+            pr, pv = pr[pp], pv[pp]
+            first = torch.ones(pr.numel(), dtype=torch.bool, device=d)
+            first[1:] = (pr[1:] != pr[:-1]) | (pv[1:] != pv[:-1])
+            pr, pv = pr[first], pv[first]
+        else:
+            pp = ops.sort_keys_checked([pr], bits=[_bits(m)]).long()  # stable: emission order per key
+            pr, pv = pr[pp], pv[pp]
+    nper = torch.bincount(pr, minlength=m)[:m] if m else torch.zeros(0, dtype=torch.int64, device=d)
+    loff = torch.zeros(m + 1, dtype=torch.int64, device=d)
+    if m:
+        loff[1:] = torch.cumsum(nper, 0)
+    _, klen = ops.key_meta(hi, lo, rep, src, want_part=False)
+    koff, kblob = ops.gather_key_bytes(hi, lo, rep, src, lengths=klen)
+    counts = ops.bincount(part, nparts) if m else torch.zeros(nparts, dtype=torch.int64, device=d)
+    return {"hi": hi, "lo": lo, "key_off": koff, "key_blob": kblob, "list_off": loff, "list_val": pv,
+            "counts": counts}
+
+
+def _np64(t):
+    return t.detach().cpu().numpy()
+
+
+def _np_cols(out: dict) -> list:
+    return [_np64(c) for c in out.get("cols", [])]
+
+
+def host_partitions(out: dict, nparts: int, dtype: str = "i64", reducefn=None, aci: bool = False) -> dict:
+    """Device result of :func:`order_fold` / :func:`order_lists` -> per
+    partition host columns (exact bytewise key order inside a partition),
+    with ``reducefn`` applied per key to list results (the host reduce)."""
+    hi = _np64(out["hi"]).view(np.uint64)
+    lo = _np64(out["lo"]).view(np.uint64)
+    koff = _np64(out["key_off"]).astype(np.int64)
+    kblob = _np64(out["key_blob"])
+    counts = _np64(out["counts"])
+    bounds = np.zeros(nparts + 1, np.int64)
+    np.cumsum(counts, out=bounds[1:])
+    cols = [_np64(c) for c in out.get("cols", [])]
+    is_list = "list_off" in out
+    if is_list:
+        loff = _np64(out["list_off"]).astype(np.int64)
+        lval = _np64(out["list_val"])
+        if dtype == "f64":
+            lval = lval.view(np.float64)
+    parts = {}
+    kb = kblob.tobytes()
+    for p in range(nparts):
+        a, b = int(bounds[p]), int(bounds[p + 1])
+        if b <= a:
+            continue
+        fix = devmod.fix_long_key_order(hi[a:b], lo[a:b], koff[a:b + 1], kblob) if b - a > 1 else None
+        idx = np.arange(a, b) if fix is None else fix + a
+        if fix is None:
+            k_off = koff[a:b + 1] - koff[a]
+            k_blob = kblob[koff[a]:koff[b]]
+        else:
+            lens = (koff[idx + 1] - koff[idx])
+            k_off = np.zeros(idx.size + 1, np.int64)
+            np.cumsum(lens, out=k_off[1:])
+            k_blob = np.frombuffer(b"".join(kb[koff[i]:koff[i + 1]] for i in idx), np.uint8)
+        part = {"key_off": k_off, "key_blob": k_blob, "hi": hi[idx], "lo": lo[idx]}
+        if is_list:
+            ln = loff[idx + 1] - loff[idx]
+            l_off = np.zeros(idx.size + 1, np.int64)
+            np.cumsum(ln, out=l_off[1:])
+            if fix is None:
+                l_val = lval[loff[a]:loff[b]]
+            else:
+                l_val = np.concatenate([lval[loff[i]:loff[i + 1]] for i in idx]) if idx.size else lval[:0]
+            part.update(list_off=l_off, list_val=l_val, val=ln)
+            if reducefn is not None:
+                pyv = []
+                for i in range(idx.size):
+                    key = codec.key_str(k_blob[k_off[i]:k_off[i + 1]].tobytes())
+                    values = l_val[l_off[i]:l_off[i + 1]].tolist()
+                    if aci and len(values) == 1:
+                        pyv.append(values)
+                        continue
+                    o: list = []
+                    reducefn(key, values, o.append)
+                    pyv.append(o)
+                part["py_vals"] = pyv
+        else:
+            part["cols"] = [c[idx] for c in cols]
+            part["val"] = part["cols"][0]
+        parts[p] = part
+    return parts
+
+
+# ---------------------------------------------------------------------------
+class GenericPlane:
+    """The SPMD engine's general plane (``device_reduce`` a column spec, a
+    list op with generic emits, or absent)."""
+
+    def __init__(self, eng):
+        from .planes import LIST_OPS
+        self.eng = eng
+        op = eng.op
+        self.host_reduce = op is None
+        self.unique = op == "concat_unique"
+        self.list_mode = op is None or op in LIST_OPS
+        self.dtype = str(modules.field(eng.mapmod, "device_value_dtype", "i64") or "i64")
+        if self.dtype not in ("i64", "f64"):
+            raise ValueError("device_value_dtype is 'i64' or 'f64'")
+        self.phys = None if self.list_mode else A.Physical(A.parse_spec(op))
+        self._cap = int(eng.params.get("table_capacity") or 1 << 16)
+        self.map = GenericMap(eng.device, self._cap, self.phys, self.dtype)
+        self.red = None
+        self._lines = None
+        if eng._arena_cap():
+            raise ValueError("the general device plane maps a rank's whole input at once (no arena_cap_mb / "
+                             "MR_ARENA_CAP_MB streaming)")
+        red = eng.redmod
+        self.reducefn = modules.field(red, "reducefn") if self.host_reduce else None
+        if self.host_reduce and self.reducefn is None:
+            raise ValueError("a reduce module without device_reduce needs a reducefn")
+        self.aci = all(bool(modules.field(red, f)) for f in
+                       ("associative_reducer", "commutative_reducer", "idempotent_reducer"))
+
+    # -- global line numbering (word_lines) ---------------------------------------
+    def _line_base(self):
+        eng = self.eng
+        st = eng.splits
+        if st is None:
+            return None
+        if self._lines is None:
+            from .planes import ListPlane
+            self._lines = ListPlane.line_offsets(self)  # same all-gather of per-split newline counts
+
+        def base(t):
+            a = t.data_ptr() - eng.arena.data_ptr()       # the chunk's offset in the rank's arena
+            rel = st.offsets - st.offsets[self._ids0]      # split i starts at rel[i] in the arena
+            i = int(np.searchsorted(rel, a, side="right")) - 1
+            inside = a - int(rel[i])
+            nl = int(torch.count_nonzero(eng.arena[a - inside:a] == 10)) if inside else 0
+            return int(self._lines[i]) + nl
+        return base
+
+    # -- map --------------------------------------------------------------------
+    def _map(self, jobs, recs, j0, j1) -> None:
+        eng = self.eng
+        mp = self.map
+        dmap = eng.dmap
+        if eng.device_input == "split" and j1 > j0:
+            ids = eng._split_ids(jobs, j0, j1)
+            self._ids0 = ids[0]
+        mp.emit.line_base = self._line_base() if eng.device_input == "split" else None
+        for _attempt in range(64):
+            mp.begin(None)
+            broken = []
+            for (a, b), data in eng._stage_chunks(jobs, j0, j1):
+                if all(recs[j].status == STATUS.FAILED for j in range(a, b)):
+                    continue
+                if eng.device_input == "split":
+                    mp.src.set_arena(eng.arena)
+                t0, c0 = time.time(), time.process_time()
+                for j in range(a, b):
+                    recs[j].status, recs[j].started, recs[j].worker = STATUS.RUNNING, t0, eng.rank
+                mp.emit.chunk = data if isinstance(data, torch.Tensor) and data.dtype == torch.uint8 else None
+                keys = [jobs[j][0] for j in range(a, b)]
+                try:
+                    dmap(keys if b - a > 1 else keys[0], data, mp.emit)
+                    mp.flush_host()
+                except NeedsHostMap:
+                    raise
+                except Exception:  # noqa: BLE001
+                    mp.host = []
+                    broken.append((a, b))
+                    sys.stderr.write("Error executing a job: %s\n" % traceback.format_exc())
+                t1 = time.time()
+                for j in range(a, b):
+                    if recs[j].status != STATUS.FAILED:
+                        recs[j].status = STATUS.WRITTEN
+                    recs[j].written = t1
+                    recs[j].real_time = (t1 - t0) / (b - a)
+                    recs[j].cpu_time = (time.process_time() - c0) / (b - a)
+            n, ovf = mp.table.stats()
+            if broken:
+                # a chunk whose map raised may have inserted part of its rows:
+                # redo the rank's map without it (BROKEN), or leave it out
+                # after MAX_JOB_RETRIES attempts (FAILED), server.lua:194-205
+                for a, b in broken:
+                    for j in range(a, b):
+                        recs[j].repetitions += 1
+                        recs[j].status = STATUS.FAILED if recs[j].repetitions >= utils.MAX_JOB_RETRIES \
+                            else STATUS.BROKEN
+                continue
+            if ovf or n > mp.table.cap // 2:
+                self._cap = ops.next_pow2(4 * max(n, 1))
+                mp.table = A.AggTable(self._cap, eng.device, self.phys.cols if self.phys is not None else None,
+                                      self.dtype)
+                continue
+            if n > mp.table.cap // 8 and self._cap < 4 * n:
+                self._cap = ops.next_pow2(4 * n)  # next iteration's table
+            return
+        raise RuntimeError("general plane: the map did not converge (table regrowth / retries)")
+
+    # -- shuffle ----------------------------------------------------------------
+    def _shuffle(self, keys: tuple, src, failed: int):
+        """Send every key (+ folded columns or value list) to rank p % W.
+        Returns the received (hi, lo, rep, payload, rblob, failed_total)."""
+        eng = self.eng
+        W, R = eng.world, eng.nparts
+        slot, hi, lo, rep = keys[:4]
+        d = hi.device
+        m = hi.numel()
+        part = devmod.partition_of(hi, lo, rep, src, R, eng.partmod) if m else torch.zeros(0, dtype=torch.int32,
+                                                                                           device=d)
+        dest = part.to(torch.int64) % W
+        kperm = ops.sort_keys_checked([dest], bits=[max(8, _bits(W))]).long() if m else torch.zeros(
+            0, dtype=torch.int64, device=d)
+        hi, lo, rep, dest, slot = hi[kperm], lo[kperm], rep[kperm], dest[kperm], slot[kperm]
+        _, klen = ops.key_meta(hi, lo, rep, src, want_part=False)
+        koff, kblob = ops.gather_key_bytes(hi, lo, rep, src, lengths=klen)
+        if self.list_mode:
+            pslot, pval = keys[4], keys[5]
+            pos = torch.full((max(self._slot_space(), 1),), -1, dtype=torch.int64, device=d)
+            pos[slot] = torch.arange(m, dtype=torch.int64, device=d)
+            pr = pos[pslot.clamp(min=0)]
+            ok = (pslot >= 0) & (pr >= 0)
+            pr, pv = pr[ok], pval[ok]
+            if pr.numel():
+                pp = ops.sort_keys_checked([pr], bits=[_bits(m)]).long()
+                pr, pv = pr[pp], pv[pp]
+            nv = torch.bincount(pr, minlength=m)[:m] if m else torch.zeros(0, dtype=torch.int64, device=d)
+            payload = [nv]
+            extra = pv
+        else:
+            cols = [c[kperm] for c in keys[4]]
+            payload = [c.view(torch.int64) if c.dtype == torch.float64 else
+                       (c.view(torch.int32).to(torch.int64) if c.dtype == torch.float32 else c) for c in cols]
+            nv = None
+            extra = None
+        cnt = torch.zeros(W, 4, dtype=torch.int64, device=d)
+        if m:
+            cnt[:, 0].index_add_(0, dest, torch.ones_like(dest))
+            cnt[:, 1].index_add_(0, dest, klen.to(torch.int64))
+            if nv is not None:
+                cnt[:, 2].index_add_(0, dest, nv)
+        cnt[:, 3] = failed
+        recv = D.exchange_counts(cnt.view(-1).contiguous(), eng.group).view(W, 4)
+        both = torch.cat([cnt, recv]).cpu().tolist()  # one host sync for every split size
+        send_c, recv_c = both[:W], both[W:]
+        failed_total = sum(r[3] for r in recv_c)
+        recs = torch.stack([hi, lo, klen.to(torch.int64)] + payload, 1) if m else torch.zeros(
+            (0, 3 + len(payload)), dtype=torch.int64, device=d)
+        rrecs = D.all_to_all_v(recs, [c[0] for c in send_c], [c[0] for c in recv_c], eng.group)
+        nbytes = sum(c[1] for c in send_c)
+        rblob = D.all_to_all_v(kblob[:nbytes], [c[1] for c in send_c], [c[1] for c in recv_c], eng.group)
+        rextra = None
+        if extra is not None:
+            rextra = D.all_to_all_v(extra, [c[2] for c in send_c], [c[2] for c in recv_c], eng.group)
+        sent = [32 * c[0] + c[1] + 8 * c[2] for c in send_c]
+        self._shuffled = (sum(sent), sum(sent) - sent[eng.rank])
+        rhi, rlo, rlen = rrecs[:, 0].contiguous(), rrecs[:, 1].contiguous(), rrecs[:, 2].contiguous()
+        roff, _ = ops.exclusive_scan(rlen)
+        rrep = (roff << K.REP_LEN_BITS) | rlen
+        if rblob.numel() == 0:
+            rblob = torch.zeros(1, dtype=torch.uint8, device=d)
+        rpay = [rrecs[:, 3 + j].contiguous() for j in range(len(payload))]
+        return rhi, rlo, rrep, rpay, rextra, rblob, failed_total
+
+    def _slot_space(self) -> int:
+        t = self.map.table
+        return t.cap if t.is_cuda else max(1, t.stats()[0])
+
+    def _merge_received(self, rhi, rlo, rrep, rpay, rextra, rblob):
+        """Received keys -> the reduce table (fold: merge the partial columns;
+        list: slot per received key, its values in source-rank order)."""
+        eng = self.eng
+        n = rhi.numel()
+        cap = ops.next_pow2(max(1 << 12, 2 * n))
+        for _ in range(8):
+            if self.list_mode:
+                rt = A.AggTable(cap, eng.device, None, "i64")
+                rt.src = rblob
+                rt.insert(n, [], hi=rhi, lo=rlo, rep=rrep)
+            else:
+                merge = [(dt, op, j) for j, (dt, op, _i) in enumerate(self.phys.cols)]
+                rt = A.AggTable(cap, eng.device, merge)
+                rt.src = rblob
+                vals = []
+                for (dt, _op, _i), c in zip(self.phys.cols, rpay):
+                    vals.append(c.view(torch.float64) if dt == "f64" else
+                                (c.to(torch.int32).view(torch.float32) if dt == "f32" else c))
+                rt.insert(n, vals, hi=rhi, lo=rlo, rep=rrep)
+            m, ovf = rt.stats()
+            if not ovf and m <= rt.cap // 2 + 1:
+                break
+            cap *= 4
+        else:
+            raise OverflowError("reduce table overflow")
+        self.red = rt
+        if self.list_mode:
+            slot, hi, lo, rep, kslot, _ = rt.postings()
+            nv = rpay[0]
+            pslot = torch.repeat_interleave(kslot, nv, output_size=int(rextra.numel()))
+            return (slot, hi, lo, rep, pslot, rextra), (rt.cap if rt.is_cuda else max(1, m))
+        slot, hi, lo, rep, cols = rt.compact((m, False))
+        return (slot, hi, lo, rep, cols), None
+
+    # -- one iteration --------------------------------------------------------------
+    def run_iteration(self, prefetch_next, lookahead):
+        from .planes import DeviceResult, _records, _result_jobs
+        eng = self.eng
+        eng.iteration += 1
+        q = eng._seq
+        eng._seq += 1
+        eng._use(q)
+        res = DeviceResult()
+        T = res.timings
+        t_start = time.time()
+        jobs = eng._jobs()
+        j0, j1 = eng._assign(jobs)
+        t0 = time.time()
+        recs = _records(eng, jobs, j0, j1, t0)
+        res.map_jobs = recs
+        with trace.range("mr.gen.map"):
+            self._map(jobs, recs, j0, j1)
+        T["map"] = time.time() - t0
+        t1 = time.time()
+        mp = self.map
+        src = mp.src.source()
+        R, W = eng.nparts, eng.world
+        failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
+        if self.list_mode:
+            keys = mp.table.postings()
+            space = self._slot_space()
+        else:
+            keys = mp.table.compact()
+            space = None
+        self._shuffled = (0, 0)
+        if W > 1 or eng.force_shuffle:
+            with trace.range("mr.gen.shuffle"):
+                rhi, rlo, rrep, rpay, rextra, rblob, failed = self._shuffle(keys, src, failed)
+                keys, space = self._merge_received(rhi, rlo, rrep, rpay, rextra, rblob)
+                src = rblob
+        T["shuffle"] = time.time() - t1
+        t2 = time.time()
+        with trace.range("mr.gen.order"):
+            if self.list_mode:
+                out = order_lists(*keys, src, R, eng.partmod, self.unique, self.dtype, space)
+            else:
+                out = order_fold(*keys, src, R, eng.partmod, self.phys)
+            counts = out["counts"].cpu().tolist()
+        _result_jobs(eng, res, counts, t1)
+        res.device = out
+        res.distinct_keys = int(out["hi"].numel())
+        res.total_value = mp.rows
+        res.failed_maps = failed
+        res.bytes_shuffled, res.bytes_shuffled_remote = self._shuffled
+        if self.host_reduce:
+            # the reduce jobs: the user's reducefn over each key's list
+            c0 = time.process_time()
+            parts = host_partitions(out, R, self.dtype, self.reducefn, self.aci)
+            res._parts = parts
+            cpu = time.process_time() - c0
+            for r in res.red_jobs:
+                r.cpu_time = cpu * len(parts.get(int(r.key), {}).get("py_vals", [])) / max(1, res.distinct_keys)
+        else:
+            res._materialize = lambda o=out: host_partitions(o, R, self.dtype)
+        T["reduce"] = time.time() - t2
+        T["iteration"] = time.time() - t_start
+        return res

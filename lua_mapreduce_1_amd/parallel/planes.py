@@ -42,16 +42,25 @@ from ..utils import STATUS
 from ..utils import trace
 from . import dist as D
 
+FOLD_OPS = ("sum", "min", "max", "count")
 LIST_OPS = ("concat", "concat_unique")
 RECORD_OPS = ("identity",)
 
 
 def make_plane(eng):
+    if eng.plane_kind == "generic":
+        from .generic import GenericPlane
+        return GenericPlane(eng)
     if eng.op in LIST_OPS:
         return ListPlane(eng)
     if eng.op in RECORD_OPS:
         return RecordPlane(eng)
     return None
+
+
+class _UseGeneric(Exception):
+    """A list-plane map emitted through a generic call (spans / pairs /
+    host pairs): the engine switches to the general plane."""
 
 
 def _bits(n: int) -> int:
@@ -126,6 +135,19 @@ class ListEmitter:
 
     def word_lines(self, text: torch.Tensor) -> None:
         self.plane._emit_word_lines(text, self.chunk)
+
+    # any other emit: the general plane (parallel/generic.py) runs this job
+    def spans(self, *a, **k):
+        raise _UseGeneric()
+
+    def pairs(self, *a, **k):
+        raise _UseGeneric()
+
+    def words(self, *a, **k):
+        raise _UseGeneric()
+
+    def __call__(self, *a, **k):
+        raise _UseGeneric()
 
 
 class ListPlane:
@@ -206,10 +228,15 @@ class ListPlane:
             self.emitter.chunk = (base, int(lines[sid]) - rank_l0)
             keys = [jobs[j][0] for j in range(ja, jb)]
             for attempt in range(3):
+                n0 = self.sink.ctrl_snapshot() if self.sink is not None and eng.device.type == "cuda" else None
                 try:
                     dmap(keys if jb - ja > 1 else keys[0], data, self.emitter)
                     break
+                except _UseGeneric:
+                    raise
                 except Exception:  # noqa: BLE001
+                    if n0 is not None:
+                        self.sink.ctrl_restore(n0)  # drop the postings of the failed attempt
                     for j in range(ja, jb):
                         recs[j].repetitions += 1
                         recs[j].status = STATUS.BROKEN if attempt < 2 else STATUS.FAILED
@@ -249,8 +276,18 @@ class ListPlane:
         t0 = time.time()
         recs = _records(eng, jobs, j0, j1, t0)
         res.map_jobs = recs
-        with trace.range("mr.list.map"):
-            keys = self._map(jobs, recs, j0, j1)
+        try:
+            with trace.range("mr.list.map"):
+                keys = self._map(jobs, recs, j0, j1)
+        except _UseGeneric:
+            # the map emits through generic calls: the general plane runs
+            # this engine from now on (this iteration is restarted there)
+            from .generic import GenericPlane
+            eng.iteration -= 1
+            eng._seq -= 1
+            eng.plane_kind = "generic"
+            eng.plane = GenericPlane(eng)
+            return eng.plane.run_iteration(prefetch_next, lookahead)
         ahead = 0 if not (prefetch_next if prefetch_next is not None else eng.prefetch) else (
             2 if lookahead is None else min(lookahead, 2))
         if ahead:

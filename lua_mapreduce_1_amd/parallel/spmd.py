@@ -367,7 +367,11 @@ class SPMDEngine:
             # args (once per distinct init function), whatever earlier engines
             # of this process did
             modules.init_once(m, self.init_args, seen)
-        self.op = modules.field(self.redmod, "device_reduce", "sum")
+        # the reduce module's device_reduce names what the device does with a
+        # key's values; WITHOUT one, nothing is folded with an op the user
+        # did not declare: values are grouped on the device and the module's
+        # reducefn runs per key (parallel/generic.py)
+        self.op = modules.field(self.redmod, "device_reduce", None)
         spec = modules.field(self.partmod, "device_partition")
         self.nparts = int(self.params.get("num_partitions") or (spec[1] if spec else 0) or self.world)
         self.device_input = modules.field(self.mapmod, "device_input")
@@ -381,13 +385,26 @@ class SPMDEngine:
         # list- and record-valued reduces run on their own data planes
         # (parallel/planes.py); the fold plane below is the hash table
         from . import planes
+        from ..ops import agg as _agg
         self.plane = None
         self.tables: list = [None, None]
-        if self.op in planes.LIST_OPS + planes.RECORD_OPS:
-            self.plane_kind = "list" if self.op in planes.LIST_OPS else "records"
-        else:
+        if self.op is None or _agg.is_column_spec(self.op) or (
+                self.params.get("plane") == "generic" and self.op not in planes.RECORD_OPS):
+            # (param plane="generic": the general plane also for fold / list
+            # ops, e.g. to check the fused planes against it)
+            self.plane_kind = "generic"
+        elif self.op in planes.LIST_OPS:
+            self.plane_kind = "list"
+        elif self.op in planes.RECORD_OPS:
+            self.plane_kind = "records"
+        elif self.op in planes.FOLD_OPS:
             self.plane_kind = "fold"
             self.tables[0] = ops.HashTable(table_capacity, device=self.device, op=self.op)
+        else:
+            known = planes.FOLD_OPS + planes.LIST_OPS + planes.RECORD_OPS
+            raise ValueError(f"unknown device_reduce {self.op!r}: one of {known}, a column spec such as "
+                             "'f64:sum' or ('f64:mean', 'count'), or none (the reducefn runs on the host over "
+                             "device-grouped values)")
         self.red_table: ops.HashTable | None = None
         # input arenas, used round-robin by iteration sequence number q: while
         # iteration q maps/reduces arenas[q % 3], the copies of q+1 and q+2
@@ -906,6 +923,7 @@ class SPMDEngine:
             if isinstance(data, torch.Tensor):
                 self._mapped_bytes += data.numel()
             ctx.err_word = errs[k:k + 1] if errs is not None else None
+            ctx.chunk = data if isinstance(data, torch.Tensor) else None
             done = False
             while not done:
                 try:

@@ -9,7 +9,8 @@ replace it:
 * ``MRK1`` — msgpack stream of ``[key, [values...]]`` records in key order
   (host plane: arbitrary Python keys/values from user map/reduce functions).
 * ``MRC1`` — columnar device format: u64 key words (hi, lo), int64 values and
-  the key bytes (offsets + blob), straight from HBM buffers (device plane).
+  the key bytes (offsets + blob), straight from HBM buffers (device plane);
+  ``MRC2`` the same with K typed value columns (the general plane's folds).
 """
 from __future__ import annotations
 
@@ -55,6 +56,8 @@ def decode_records(data: bytes) -> Iterator[tuple]:
         return iter(())
     if data[:4] == MAGIC_COL:
         return iter_columnar(decode_columnar(data))
+    if data[:4] == MAGIC_COL2:
+        return iter_columnar(decode_columns(data))
     if data[:4] != MAGIC_REC:
         raise ValueError("unknown intermediate file format")
     up = msgpack.Unpacker(use_list=False, raw=False, strict_map_key=False, unicode_errors="surrogateescape")
@@ -87,6 +90,47 @@ def decode_columnar(data: bytes) -> dict:
     return out
 
 
+# ---------------------------------------------------------------------------
+MAGIC_COL2 = b"MRC2"
+_DT_CODE = {np.dtype(np.int64): 0, np.dtype(np.float64): 1, np.dtype(np.float32): 2}
+_CODE_DT = {v: k for k, v in _DT_CODE.items()}
+
+
+def encode_columns(hi: np.ndarray, lo: np.ndarray, cols: list, key_off: np.ndarray, key_blob: np.ndarray) -> bytes:
+    """``MRC2``: keys + K typed value columns (int64 / float64 / float32),
+    the general plane's folds (parallel/generic.py)."""
+    n, nb, k = int(hi.size), int(key_blob.size), len(cols)
+    codes = bytes(_DT_CODE[np.asarray(c).dtype] for c in cols).ljust(8 * ((k + 7) // 8), b"\0")
+    parts = [MAGIC_COL2, struct.pack("<QQQ", n, nb, k), codes, np.ascontiguousarray(hi, np.uint64).tobytes(),
+             np.ascontiguousarray(lo, np.uint64).tobytes(), np.ascontiguousarray(key_off, np.int64).tobytes()]
+    parts += [np.ascontiguousarray(c).tobytes() for c in cols]
+    parts.append(np.ascontiguousarray(key_blob, np.uint8).tobytes())
+    return b"".join(parts)
+
+
+def decode_columns(data: bytes) -> dict:
+    if data[:4] != MAGIC_COL2:
+        raise ValueError("not an MRC2 file")
+    n, nb, k = struct.unpack("<QQQ", data[4:28])
+    p = 28
+    codes = data[p:p + k]
+    p += 8 * ((k + 7) // 8)
+    out = {}
+    for name, cnt in (("hi", n), ("lo", n)):
+        out[name] = np.frombuffer(data, dtype=np.uint64, count=cnt, offset=p)
+        p += 8 * cnt
+    out["key_off"] = np.frombuffer(data, dtype=np.int64, count=n + 1, offset=p)
+    p += 8 * (n + 1)
+    cols = []
+    for c in codes:
+        dt = _CODE_DT[c]
+        cols.append(np.frombuffer(data, dtype=dt, count=n, offset=p))
+        p += dt.itemsize * n
+    out["cols"] = cols
+    out["key_blob"] = np.frombuffer(data, dtype=np.uint8, count=nb, offset=p)
+    return out
+
+
 def key_str(b: bytes) -> str:
     return b.decode("utf-8", "surrogateescape")
 
@@ -105,6 +149,15 @@ def iter_columnar(cols: dict) -> Iterator[tuple]:
         return
     off = cols["key_off"]
     blob = cols["key_blob"].tobytes()
+    if "py_vals" in cols:  # a host reducefn's output per key (parallel/generic.py)
+        for i, v in enumerate(cols["py_vals"]):
+            yield key_str(blob[off[i]:off[i + 1]]), list(v)
+        return
+    if "cols" in cols:  # typed fold columns: one value per column
+        cs = cols["cols"]
+        for i in range(int(off.size) - 1):
+            yield key_str(blob[off[i]:off[i + 1]]), [c[i].item() for c in cs]
+        return
     if "list_off" in cols:
         lo, lv = cols["list_off"], cols["list_val"]
         for i in range(int(lo.size) - 1):

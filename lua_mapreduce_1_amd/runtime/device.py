@@ -6,12 +6,15 @@ Python dicts:
 
 * ``emit.words(text_u8)`` — every whitespace token of a byte tensor with value
   1, through the fused tokenize + exact-key + LDS-combine kernel (K1-K5);
+* ``emit.spans(starts, lens, vals=None, text=None)`` — keys = byte spans of
+  the staged chunk (or ``text``), e.g. CSV fields or n-grams picked with
+  ops/text.py and torch ops;
 * ``emit.pairs(hi, lo, vals, rep=None, src=None)`` — a batch of (key, value)
   pairs already encoded as 128-bit keys (ops.keys);
 * ``emit(key, value)`` — one host pair (buffered, inserted in one batch).
 
 Values are int64 and are folded at insert time with the reduce module's
-``device_reduce`` op (``"sum" | "min" | "max"``), i.e. the combiner of
+``device_reduce`` op (``"sum" | "min" | "max" | "count"``), i.e. the combiner of
 job.lua:92-96,198-202 runs inside the hash table.  Partitioning uses the
 partition module's ``device_partition = ("fnv1", N)`` (exact FNV-1 of the key
 bytes mod N, examples/WordCount/partitionfn.lua) or, failing that, the host
@@ -135,10 +138,33 @@ class DeviceEmitter:
         base, view = ctx.add_source(text)
         ctx.table.wordcount_map(view, rep_base=base, src=ctx.arena)
 
+    def spans(self, starts, lens, vals=None, text: torch.Tensor | None = None) -> None:
+        """Keys = the byte spans ``text[starts[i] : starts[i] + lens[i]]``
+        (default ``text``: the chunk being mapped; empty spans skipped) with
+        values ``vals`` (int64 tensor or number; ignored by ``count``)."""
+        ctx = self.ctx
+        t = text if text is not None else getattr(ctx, "chunk", None)
+        if t is None:
+            raise ValueError("emit.spans: no staged chunk, pass text=")
+        if t.device != ctx.device:
+            t = t.to(ctx.device)
+        if ctx.op == "count":
+            vals = None
+        if ctx.arena is not None and ctx.sources is None:
+            # engine-owned arena: the spans must lie in the staged input
+            base = t.data_ptr() - ctx.arena.data_ptr()
+            if not (0 <= base and base + t.numel() <= ctx.arena.numel()):
+                raise ValueError("emit.spans: with staged splits, text must be a view of the staged input")
+        else:
+            base, t = ctx.add_source(t)
+        ctx.table.insert_spans(t, starts, lens, vals, rep_base=base, src=ctx.arena)
+
     def pairs(self, hi, lo, vals=None, rep=None, src: torch.Tensor | None = None) -> None:
         """A batch of encoded (key, value) pairs; long keys' rep words index
         ``src`` (appended to the job's arena)."""
         ctx = self.ctx
+        if ctx.op == "count":
+            vals = None
         add = 0
         if src is not None:
             add, _ = ctx.add_source(src)
@@ -158,7 +184,7 @@ class DeviceEmitter:
             key = key.encode("utf-8", "surrogateescape")
         elif not isinstance(key, bytes):
             key = str(key).encode()
-        self.ctx.host_pairs.append((key, int(value)))
+        self.ctx.host_pairs.append((key, 1 if self.ctx.op == "count" else int(value)))
 
 
 # ---------------------------------------------------------------------------

@@ -56,18 +56,40 @@ def reset_cache() -> None:
 
 
 FOLD_OPS = ("sum", "min", "max", "count")
+LIST_OPS = ("concat", "concat_unique")
+
+
+def device_kind(task_tbl: dict | None, mod_map, mod_red=None) -> str | None:
+    """Which device map a worker runs for a map module with ``device_mapfn``
+    (None: the host ``mapfn``), from the reduce module's ``device_reduce``:
+
+    * ``"fold"`` — sum/min/max/count of int64 values in the HBM table
+      (runtime/device.py), columnar ``MRC1`` map outputs;
+    * ``"cols"`` — a typed column spec (ops/agg.py), ``MRC2`` outputs merged
+      by the device reduce;
+    * ``"list"`` — no device_reduce (or a concat op): values grouped per key
+      on the device, written as ``(key, [values])`` records that the reduce
+      job hands to the module's own reducefn (job.lua:264-284) — never a
+      fold the user did not declare;
+    * ``"identity"`` (the record plane) runs in SPMD mode only: host mapfn."""
+    want = (task_tbl or {}).get("device", "auto")
+    if want in (False, "never", "host"):
+        return None
+    if modules.field(mod_map, "device_mapfn") is None:
+        return None
+    op = modules.field(mod_red, "device_reduce", None) if mod_red is not None else None
+    if op in FOLD_OPS:
+        return "fold"
+    if op is None or op in LIST_OPS:
+        return "list"
+    from ..ops import agg as A
+    if A.is_column_spec(op):
+        return "cols"
+    return None
 
 
 def _use_device(task_tbl: dict | None, mod_map, mod_red=None) -> bool:
-    """The worker's device map plane folds int64 values in an HBM table; a
-    list- or record-valued reduce (device_reduce "concat*" / "identity", the
-    SPMD engine's planes) runs the host mapfn here."""
-    want = (task_tbl or {}).get("device", "auto")
-    if want in (False, "never", "host"):
-        return False
-    if mod_red is not None and modules.field(mod_red, "device_reduce", "sum") not in FOLD_OPS:
-        return False
-    return modules.field(mod_map, "device_mapfn") is not None
+    return device_kind(task_tbl, mod_map, mod_red) is not None
 
 
 class job:  # noqa: N801
@@ -147,8 +169,13 @@ class job:  # noqa: N801
         if cmod is not None:
             modules.init_once(cmod, self.init_args)
         combiner = modules.field(cmod, "combinerfn") if cmod is not None else None
-        if _use_device(self.task_tbl, self.module, cmod):
-            return lambda: self._run_device_map(pmod, cmod)
+        kind = device_kind(self.task_tbl, self.module, cmod)
+        host_run = self._host_map(combiner, partitioner)
+        if kind is not None:
+            return lambda: self._run_device_map(pmod, cmod, kind, host_run)
+        return host_run
+
+    def _host_map(self, combiner, partitioner):
         g = modules.field(self.module, "mapfn")
         map_key, map_value = self.get_pair()
 
@@ -204,16 +231,89 @@ class job:  # noqa: N801
         whatever the storage (sshfs files are only on the mapper's host)."""
         self.cnn.gridfs().store_data(b"", INDEX_PREFIX + name + INDEX_SEP + utils.get_hostname())
 
-    def _run_device_map(self, pmod, rmod):
+    def _run_device_map(self, pmod, rmod, kind: str = "fold", host_run=None):
         # the device plane's pinned download buffers and workspaces are
         # per-process: worker threads of one process take turns on the GPU
-        with dev.PLANE_LOCK:
-            return self._run_device_map_locked(pmod, rmod)
+        from ..parallel.generic import NeedsHostMap
+        try:
+            with dev.PLANE_LOCK:
+                if kind == "fold":
+                    return self._run_device_map_locked(pmod, rmod)
+                return self._run_generic_map(pmod, rmod, kind)
+        except NeedsHostMap:
+            # the device map needs an SPMD-only emitter (global line numbers,
+            # the record plane): the module's host mapfn does this job
+            if host_run is None or modules.field(self.module, "mapfn") is None:
+                raise
+            return host_run()
+
+    def _run_generic_map(self, pmod, rmod, kind: str):
+        """General device map of one job (parallel/generic.py): typed folds
+        (``MRC2`` partition files) or per-key value lists (``MRK1`` records
+        for the host reducefn)."""
+        from ..ops import agg as A
+        from ..parallel import generic as G
+        clock1 = _time.process_time()
+        map_key, map_value = self.get_pair()
+        spec = modules.field(rmod, "device_reduce", None) if rmod is not None else None
+        extra = self.task_tbl.get("extra") or {}
+        pspec = modules.field(pmod, "device_partition")
+        nparts = int(extra.get("num_partitions") or (pspec[1] if pspec else 0) or 1)
+        phys = A.Physical(A.parse_spec(spec)) if kind == "cols" else None
+        dtype = str(modules.field(self.module, "device_value_dtype", "i64") or "i64")
+        d = dev.default_device()
+        cap = int(extra.get("table_capacity") or 1 << 16)
+        fn = modules.field(self.module, "device_mapfn")
+        for _ in range(8):
+            gm = G.GenericMap(d, cap, phys, dtype)
+            gm.begin(None)
+            fn(map_key, map_value, gm.emit)
+            gm.flush_host()
+            n, ovf = gm.table.stats()
+            if not ovf and n <= gm.table.cap // 2 + 1:
+                break
+            cap = ops_next_pow2(4 * max(n, 1))
+        else:
+            raise OverflowError("device map table overflow")
+        self.mark_as_finished()
+        src = gm.src.source()
+        if kind == "cols":
+            out = G.order_fold(*gm.table.compact(), src, nparts, pmod, phys, outputs=False)
+        else:
+            space = gm.table.cap if gm.table.is_cuda else max(1, n)
+            out = G.order_lists(*gm.table.postings(), src, nparts, pmod, spec == "concat_unique", dtype, space)
+        parts = G.host_partitions(out, nparts, dtype)
+        host = utils.get_hostname()
+        outputs, index = [], []
+        for p, cols in sorted(parts.items()):
+            name = f"{self.path}/{self.results_ns}.P{p}.M{map_key}"
+            if kind == "cols":
+                blob = codec.encode_columns(cols["hi"], cols["lo"], cols["cols"], cols["key_off"], cols["key_blob"])
+            else:
+                blob = codec.encode_records(codec.iter_columnar(cols))
+            outputs.append((name, blob))
+            index.append((INDEX_PREFIX + name + INDEX_SEP + host, b""))
+        self._store_outputs(outputs, index)
+        elapsed = _time.process_time() - clock1
+        self.mark_as_written(elapsed)
+        return elapsed
+
+    def _store_outputs(self, outputs, index) -> None:
+        fs, make_builder, _ = fsmod.router(self.cnn, None, self.storage, self.path)
+        gfs = self.cnn.gridfs()
+        if self.storage == "gridfs":
+            gfs.store_many(outputs + index)
+        else:
+            for name, blob in outputs:
+                b = make_builder()
+                b.append(blob)
+                b.build(name)
+            gfs.store_many(index)
 
     def _run_device_map_locked(self, pmod, rmod):
         clock1 = _time.process_time()
         map_key, map_value = self.get_pair()
-        op = modules.field(rmod, "device_reduce", "sum") if rmod is not None else "sum"
+        op = modules.field(rmod, "device_reduce")  # device_kind() checked it is a fold op
         extra = self.task_tbl.get("extra") or {}
         spec = modules.field(pmod, "device_partition")
         nparts = int(extra.get("num_partitions") or (spec[1] if spec else 0) or 1)
@@ -272,17 +372,19 @@ class job:  # noqa: N801
             rstore, rbuilder = result_store(self.cnn, self.storage, self.path)
             rstore.remove_file(res_file)
             blobs = None
-            if dev_op in FOLD_OPS and filenames:
+            cols_op = dev_op is not None and dev_op not in FOLD_OPS and _is_cols(dev_op)
+            if (dev_op in FOLD_OPS or cols_op) and filenames:
                 if self.storage == "gridfs":  # all inputs in one round trip per shard
                     blobs = [b or b"" for b in self.cnn.gridfs().get_many(filenames)]
                 else:
                     blobs = [fsmod.read_blob(self.cnn, self.storage, self.path, n) for n in filenames]
-                if not all(b[:4] == codec.MAGIC_COL for b in blobs):
+                magic = codec.MAGIC_COL2 if cols_op else codec.MAGIC_COL
+                if not all(b[:4] == magic for b in blobs):
                     blobs = None
             b = rbuilder()
             if blobs is not None:
                 with dev.PLANE_LOCK:
-                    b.append(_device_reduce(blobs, dev_op))
+                    b.append(_device_reduce_cols(blobs, dev_op) if cols_op else _device_reduce(blobs, dev_op))
             else:
                 recs = []
                 for k, v in utils.merge_iterator(fs, filenames, make_lines_iterator):
@@ -329,6 +431,53 @@ def _device_reduce(blobs: list[bytes], op: str) -> bytes:
     out = dev.finalize(uhi, ulo, uval, urep, src, 1, None, part=torch.zeros(uhi.numel(), dtype=torch.int32,
                                                                               device=d), need_keys=True)
     return codec.encode_columnar(out["hi"], out["lo"], out["val"], out["key_off"], out["key_blob"])
+
+
+def _is_cols(op) -> bool:
+    from ..ops import agg as A
+    return A.is_column_spec(op)
+
+
+def ops_next_pow2(n: int) -> int:
+    return 1 << max(0, (int(n) - 1).bit_length())
+
+
+def _device_reduce_cols(blobs: list[bytes], spec) -> bytes:
+    """Merge ``MRC2`` partition files of a typed fold on the device: the
+    partial physical columns of every key are folded again (a mean's sums
+    and counts add up) and the output columns written."""
+    from ..ops import agg as A
+    from ..parallel import generic as G
+    phys = A.Physical(A.parse_spec(spec))
+    cols = [codec.decode_columns(b) for b in blobs]
+    d = dev.default_device()
+    n = sum(int(c["hi"].size) for c in cols)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(d)  # noqa: E731
+    hi = t(np.concatenate([c["hi"] for c in cols]).view(np.int64))
+    lo = t(np.concatenate([c["lo"] for c in cols]).view(np.int64))
+    bases = np.cumsum([0] + [int(c["key_blob"].size) for c in cols])[:-1]
+    offs = np.concatenate([c["key_off"][:-1] + b for c, b in zip(cols, bases)]).astype(np.uint64)
+    lens = np.concatenate([np.diff(c["key_off"]) for c in cols]).astype(np.uint64)
+    rep = t(((offs << np.uint64(24)) | lens).view(np.int64))
+    src = t(np.concatenate([c["key_blob"] for c in cols] + [np.zeros(1, np.uint8)]))
+    vals = [t(np.concatenate([c["cols"][j] for c in cols])) for j in range(len(phys.cols))]
+    merge = [(dt, op, j) for j, (dt, op, _i) in enumerate(phys.cols)]
+    cap = max(1024, 4 * n)
+    while True:
+        tab = A.AggTable(cap, d, merge)
+        tab.src = src
+        tab.insert(n, vals, hi=hi, lo=lo, rep=rep)
+        m, ovf = tab.stats()
+        if not ovf:
+            break
+        cap *= 4
+    out = G.order_fold(*tab.compact((m, False)), src, 1, None, phys)
+    part = G.host_partitions(out, 1).get(0)
+    if part is None:
+        return codec.encode_columns(np.zeros(0, np.uint64), np.zeros(0, np.uint64),
+                                    [np.zeros(0, c.dtype) for c in G._np_cols(out)], np.zeros(1, np.int64),
+                                    np.zeros(0, np.uint8))
+    return codec.encode_columns(part["hi"], part["lo"], part["cols"], part["key_off"], part["key_blob"])
 
 
 def result_store(cnn, storage: str, path: str):

@@ -140,3 +140,27 @@ def tricky_text(rng: np.random.Generator, nbytes: int) -> bytes:
         else:
             out += bytes([ws[int(rng.integers(0, 6))] for _ in range(int(rng.integers(1, 4)))])
     return bytes(out[:nbytes])
+
+
+def score_csv(seed: int = 7, lines: int = 100_000, vocab_size: int = 5_000, split_lines: int = 10_000,
+              long_frac: float = 0.01) -> list[bytes]:
+    """``word,score`` lines (a group-by-and-aggregate workload over a CSV
+    column): Zipf-distributed words (some longer than 15 bytes), scores with
+    three decimals in [-1000, 1000), split into pieces of ``split_lines``
+    lines (each ends with a newline)."""
+    rng = np.random.default_rng(seed)
+    vocab = make_vocab(vocab_size, rng, long_frac=long_frac)
+    vocab = [w.replace(b",", b";") for w in vocab]
+    cdf = np.cumsum(zipf_probs(vocab_size))
+    cdf[-1] = 1.0
+    tok = np.minimum(np.searchsorted(cdf, rng.random(lines), side="right"), vocab_size - 1)
+    milli = rng.integers(-1_000_000, 1_000_000, lines)
+    out = []
+    for s0 in range(0, lines, split_lines):
+        rows = []
+        for t, m in zip(tok[s0:s0 + split_lines], milli[s0:s0 + split_lines]):
+            sign = "-" if m < 0 else ""
+            a = abs(int(m))
+            rows.append(vocab[t] + (",%s%d.%03d\n" % (sign, a // 1000, a % 1000)).encode())
+        out.append(b"".join(rows))
+    return out

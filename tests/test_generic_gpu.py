@@ -1,0 +1,186 @@
+"""General device plane on the GPU (csrc/hip/generic.hip, text.hip): the
+kernels against their CPU specifications, and whole jobs (typed folds, int64
+lists, host reducefn, byte-span keys) against host oracles — at W = 1, with
+the RCCL shuffle forced on a one-rank nccl group, with three ranks sharing
+the GPU (gloo collectives), and in server/worker mode."""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from test_generic_plane import CASES, GM, SS, _free_port, close_lists, make_data, oracle, run_engine  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def test_text_tokens_lines_fields_gpu(gpu):
+    from lua_mapreduce_1_amd.ops import text as TX
+    from lua_mapreduce_1_amd.utils.corpus import tricky_text
+    rng = np.random.default_rng(11)
+    for n in (0, 1, 4095, 4096, 4097, 300_001):
+        b = tricky_text(rng, n)
+        for off in (0, 3):  # unaligned views too
+            hb = torch.frombuffer(bytearray(b"x" * off + b), dtype=torch.uint8)[off:]
+            db = torch.frombuffer(bytearray(b"x" * off + b), dtype=torch.uint8).to(gpu)[off:]
+            for f in (TX.tokens, TX.lines):
+                hs, hl = f(hb)
+                ds, dl = f(db)
+                assert torch.equal(hs, ds.cpu()) and torch.equal(hl, dl.cpu()), (f.__name__, n, off)
+            assert torch.equal(TX.find_byte(hb, 9), TX.find_byte(db, 9).cpu())
+            ls, ll = TX.lines(hb)
+            for k in (0, 1, 2):
+                hs, hl = TX.field(hb, ls, ll, ",", k)
+                ds, dl = TX.field(db, ls.to(gpu), ll.to(gpu), ",", k)
+                assert torch.equal(hs, ds.cpu()) and torch.equal(hl, dl.cpu())
+
+
+def test_text_parse_gpu_matches_python(gpu):
+    from lua_mapreduce_1_amd.ops import text as TX
+    rng = np.random.default_rng(5)
+    toks = []
+    for _ in range(20000):
+        r = rng.random()
+        if r < 0.4:
+            toks.append("%.3f" % rng.uniform(-1e6, 1e6))
+        elif r < 0.6:
+            toks.append("%d" % rng.integers(-10**15, 10**15))
+        elif r < 0.75:
+            toks.append("%.6e" % rng.uniform(-1e30, 1e30))
+        elif r < 0.85:
+            toks.append(" %.2f " % rng.uniform(-10, 10))
+        else:
+            toks.append(rng.choice(["abc", "", "1.2.3", "-", "1e", ".5", "5.", "+7", "0.000123", "00012"]))
+    data = ",".join(toks).encode()
+    t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    starts, lens, pos = [], [], 0
+    for s in toks:
+        starts.append(pos)
+        lens.append(len(s))
+        pos += len(s) + 1
+    st = torch.tensor(starts, dtype=torch.int64)
+    ln = torch.tensor(lens, dtype=torch.int32)
+    hv = TX.parse_f64(t, st, ln)
+    dv = TX.parse_f64(t.to(gpu), st.to(gpu), ln.to(gpu)).cpu()
+    for a, b, s in zip(hv.tolist(), dv.tolist(), toks):
+        if math.isnan(a):
+            assert math.isnan(b), s
+        elif "e" in s and abs(float(s)) > 1e22:
+            assert math.isclose(a, b, rel_tol=1e-14), s  # outside the exact fast path
+        else:
+            assert a == b, (s, a, b)  # correctly rounded: what Python's float() gives
+    hi = TX.parse_i64(t, st, ln)
+    di = TX.parse_i64(t.to(gpu), st.to(gpu), ln.to(gpu)).cpu()
+    assert torch.equal(hi, di)
+
+
+@pytest.mark.parametrize("dtype", ["i64", "f64", "f32"])
+def test_agg_table_folds_gpu(gpu, dtype):
+    """Typed sum/min/max folds of random (key, value) rows against numpy."""
+    from lua_mapreduce_1_amd.ops import agg as A
+    from lua_mapreduce_1_amd.ops import keys as K
+    rng = np.random.default_rng(3)
+    n, nk = 200_000, 5000
+    words = [("k%d" % i).encode() * (1 + i % 3) for i in range(nk)]  # some long keys
+    idx = rng.integers(0, nk, n)
+    blob = b"".join(words)
+    off = np.cumsum([0] + [len(w) for w in words])
+    starts = torch.from_numpy(off[:-1][idx].astype(np.int64))
+    lens = torch.from_numpy(np.array([len(w) for w in words], np.int32)[idx])
+    if dtype == "i64":
+        vals = torch.from_numpy(rng.integers(-10**12, 10**12, n))
+    else:
+        vals = torch.from_numpy(rng.uniform(-1e3, 1e3, n).astype(np.float64 if dtype == "f64" else np.float32))
+    cols = [(dtype, "sum", 0), (dtype, "min", 0), (dtype, "max", 0), ("i64", "sum", None)]
+    res = {}
+    for dev in ("cpu", gpu):
+        t = A.AggTable(1 << 14, dev, cols)
+        text = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+        t.src = text
+        t.insert(n, [vals.to(dev)], text=text, starts=starts.to(dev), lens=lens.to(dev), rep_base=0)
+        slot, hi, lo, rep, c = t.compact()
+        kb = __import__("lua_mapreduce_1_amd").ops.key_bytes_list(hi.cpu(), lo.cpu(), rep.cpu(), text.cpu())
+        res[str(dev)] = {k: [x[i].item() for x in c] for i, k in enumerate(kb)}
+    a, b = res["cpu"], res[str(gpu)]
+    assert set(a) == set(b) == set(words)
+    for k in a:
+        s0, s1 = a[k][0], b[k][0]
+        if dtype == "i64":
+            assert a[k] == b[k]
+        else:
+            tol = 1e-9 if dtype == "f64" else 1e-3
+            assert math.isclose(s0, s1, rel_tol=tol, abs_tol=tol) and a[k][1:] == b[k][1:]
+
+
+@pytest.mark.parametrize("which,mod,args", CASES, ids=["scores", "bigram", "max_host", "docs", "docs_concat",
+                                                       "mixed"])
+def test_generic_gpu_w1(gpu, which, mod, args):
+    splits = make_data(which)
+    eng, res, got = run_engine(mod, splits, gpu, args)
+    assert close_lists(got, oracle(which, args.get("mode"), splits))
+    assert eng.device.type == "cuda"
+
+
+def _rank(rank, world, port, q, which, mod, args, force_shuffle, backend):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import datetime
+    import torch.distributed as dist
+    from lua_mapreduce_1_amd.parallel import dist as D
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if force_shuffle:
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}",
+                                timeout=datetime.timedelta(seconds=120), **kw)
+    else:
+        D.init_from_env(backend="gloo", use_gpu=True)
+    splits = make_data(which)
+    eng, res, got = run_engine(mod, splits, dev, args, force_shuffle=force_shuffle)
+    if rank == 0:
+        q.put((close_lists(got, oracle(which, args.get("mode"), splits)), len(got)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _spawn(world, which, mod, args, force_shuffle=False, backend="gloo"):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, which, mod, args, force_shuffle, backend))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return q.get(timeout=5)
+
+
+@pytest.mark.parametrize("which,mod,args", [CASES[0], CASES[3], CASES[5]], ids=["scores", "docs", "mixed"])
+def test_generic_rccl_forced_shuffle(gpu, which, mod, args):
+    ok, n = _spawn(1, which, mod, args, force_shuffle=True, backend="nccl")
+    assert ok and n > 100
+
+
+@pytest.mark.parametrize("which,mod,args", [CASES[0], CASES[2], CASES[4]], ids=["scores", "max_host", "docs_concat"])
+def test_generic_three_ranks_one_gpu(gpu, which, mod, args):
+    ok, n = _spawn(3, which, mod, args)
+    assert ok and n > 100
+
+
+def test_generic_server_worker_gpu(gpu, tmp_path):
+    from lua_mapreduce_1_amd.runtime import coordinator
+    from test_generic_server_worker import job
+    cs = coordinator.start_local()
+    for which, mod, args in (CASES[0], CASES[1], CASES[2]):
+        got, exp, s = job(cs, tmp_path, which, mod, args, "device", db="gpu")
+        if "Bigram" in mod:
+            got = {k: [v] for k, v in got.items()}
+        assert close_lists(got, exp), mod
+        assert s.last_stats["failed_map_jobs"] == 0
