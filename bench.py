@@ -289,8 +289,10 @@ def main() -> int:
         per_key = got == truth_counts(cdir)
     if cdir is None:
         words = counted  # external files: the engine's own token count
+    block = eng.stats_block(last) if last is not None else ""  # a collective at W > 1: every rank
+    valid = True
     if rank == 0:
-        print(eng.stats_block(last), file=sys.stderr, end="")
+        print(block, file=sys.stderr, end="")
         print(f"# tokens counted {counted} (expected {words}), distinct words {distinct}, per-key match {per_key}, "
               f"bytes {total_bytes}, per-phase s: {last.timings}, cold first iteration ms {cold_ms} "
               f"(tokens {cold_tokens}, page cache dropped {not args.no_cold and dropped})",
@@ -319,7 +321,8 @@ def main() -> int:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    return 0
+    # a wrong answer is a failed run: the driver's exit code sees it
+    return 0 if valid else 3
 
 
 if __name__ == "__main__":

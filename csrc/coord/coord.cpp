@@ -448,25 +448,77 @@ class Store {
     return st;
   }
 
+  // Journal file: an 8-byte magic/version header, then records
+  // len | FNV-1a(body) | body.  A file with another header is refused (never
+  // truncated: it may be an older format or another program's file).  Replay
+  // stops at the first record that is short (a write torn by a crash: the
+  // tail is cut there) or whose checksum does not match; such a tail is kept
+  // as <path>.corrupt before the journal is cut back to the last intact
+  // record.  A length field larger than the bytes left is a torn tail (no
+  // allocation is made from it).
+  static constexpr char JMAGIC[8] = {'M', 'R', 'J', 'N', 'L', 0, 0, 2};
+
   bool open_journal(const char* path) {
     if (!path || !*path) return true;
     FILE* f = fopen(path, "rb");
     long good = 0;  // end of the last complete, intact record
+    long size = 0;
     if (f) {
+      fseek(f, 0, SEEK_END);
+      size = ftell(f);
+      fseek(f, 0, SEEK_SET);
+    }
+    if (f && size > 0) {
+      char magic[8];
+      if (fread(magic, 1, 8, f) != 8 || memcmp(magic, JMAGIC, 8) != 0) {
+        fclose(f);
+        fprintf(stderr, "coordinator: %s is not a journal of this format (header mismatch); refusing to use it\n",
+                path);
+        return false;
+      }
+      good = 8;
       replaying = true;
+      bool corrupt = false;
       for (;;) {
         uint32_t hdr[2];
-        if (fread(hdr, 4, 2, f) != 2) break;
+        const long at = ftell(f);
+        if (at == size) break;
+        if (fread(hdr, 4, 2, f) != 2) break;                 // torn header
+        if ((long)hdr[0] > size - at - 8) break;             // torn body (or a garbled length)
         std::string body(hdr[0], '\0');
         if (fread(&body[0], 1, hdr[0], f) != hdr[0]) break;
-        if (body_sum(body) != hdr[1]) break;
+        if (body_sum(body) != hdr[1]) {
+          corrupt = true;
+          break;
+        }
         Writer w;
         handle(body, w);
         good = ftell(f);
       }
       replaying = false;
+      if (good < size) {
+        // keep what is cut off for inspection (a checksum mismatch in the
+        // middle drops every later record from the replay)
+        std::string keep = std::string(path) + ".corrupt";
+        FILE* c = fopen(keep.c_str(), "wb");
+        if (c) {
+          fseek(f, good, SEEK_SET);
+          char buf[65536];
+          size_t k;
+          while ((k = fread(buf, 1, sizeof buf, f)) > 0) fwrite(buf, 1, k, c);
+          fclose(c);
+        }
+        fprintf(stderr, "coordinator: journal %s: %s at byte %ld of %ld, replayed the intact prefix (tail kept in %s)\n",
+                path, corrupt ? "checksum mismatch" : "torn record", good, size, keep.c_str());
+      }
       fclose(f);
       if (truncate(path, good) != 0) return false;
+    } else {
+      if (f) fclose(f);
+      FILE* n = fopen(path, "wb");
+      if (!n) return false;
+      fwrite(JMAGIC, 1, 8, n);
+      fclose(n);
     }
     journal = fopen(path, "ab");
     return journal != nullptr;

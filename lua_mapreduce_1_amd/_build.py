@@ -7,8 +7,12 @@
 * ``_lib/libmrcoord.so`` — the C++ coordinator (job table / control plane /
   blob store / persistent tables) in ``csrc/coord`` that replaces MongoDB
   (reference: mapreduce/cnn.lua, task.lua, persistent_table.lua, GridFS).
-* ``_lib/libmrhost.so`` — native host-side data path (multi-threaded split
-  loader into pinned memory, CPU word-count engine used as the non-GPU path).
+* ``_lib/libmrhost.so`` — native host-side input path: the multi-threaded
+  split loader that reads split files straight into pinned memory
+  (``csrc/host/loader.cpp``).
+
+``*_stress.cpp`` files are test harnesses (built under sanitizers by
+tests/test_native_sanitizers.py), not part of the libraries.
 
 Everything is compiled in-tree so the ``.so`` files travel with the repository
 snapshot to the GPU box (no JIT cache under ~/.cache).
@@ -75,7 +79,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
 def build_cxx(name: str, srcsub: str, target: str, extra: list[str] | None = None,
               force: bool = False, verbose: bool = False) -> str:
     srcdir = os.path.join(ROOT, "csrc", srcsub)
-    srcs = sorted(glob.glob(os.path.join(srcdir, "*.cpp")))
+    srcs = sorted(f for f in glob.glob(os.path.join(srcdir, "*.cpp")) if not f.endswith("_stress.cpp"))
     deps = srcs + sorted(glob.glob(os.path.join(srcdir, "*.h")))
     if not srcs:
         return ""

@@ -115,11 +115,12 @@ class SplitStore:
     def from_files(cls, paths: list[str], rank: int = 0, world: int = 1, pin: bool = True,
                    threads: int = 8) -> "SplitStore":
         """One split per file (the reference's split files, WordCountBig
-        taskfn.lua:6-10).  Sizes come from stat (+1 for the terminating
-        newline); only this rank's contiguous byte-balanced share is read."""
-        lens = [os.path.getsize(p) for p in paths]
-        pad = [1] * len(paths)
-        own = assign_contiguous([n + 1 for n in lens], rank, world)
+        taskfn.lua:6-10).  Sizes come from stat; a file that does not end in
+        a newline or a space is followed by one (the same rule as the
+        in-memory and blob stores, so line numbers agree); only this rank's
+        contiguous byte-balanced share is read."""
+        lens, pad = _file_pads(paths)
+        own = assign_contiguous([n + p for n, p in zip(lens, pad)], rank, world)
         self = cls._async(list(paths), [0] * len(paths), lens, pad, own, pin, threads)
         self.paths = list(paths)
         return self
@@ -207,11 +208,12 @@ class WindowedSplitStore(SplitStore):
 
     def __init__(self, paths: list[str], rank: int = 0, world: int = 1, window_mb: float = 256,
                  pin: bool = True, threads: int = 8):
-        lens = [os.path.getsize(p) for p in paths]
+        lens, pad = _file_pads(paths)
         self.paths = list(paths)
+        self._lens, self._pad = lens, pad
         self.offsets = np.zeros(len(paths) + 1, dtype=np.int64)
-        np.cumsum(np.asarray(lens, dtype=np.int64) + 1, out=self.offsets[1:])
-        self.own = assign_contiguous([n + 1 for n in lens], rank, world)
+        np.cumsum(np.asarray(lens, dtype=np.int64) + np.asarray(pad, dtype=np.int64), out=self.offsets[1:])
+        self.own = assign_contiguous([n + p for n, p in zip(lens, pad)], rank, world)
         self.base = int(self.offsets[self.own[0]])
         self.window = int(window_mb * (1 << 20))
         self.threads = threads
@@ -238,9 +240,8 @@ class WindowedSplitStore(SplitStore):
             raise ValueError(f"round of {nbytes} bytes exceeds the {self.window}-byte host window")
         from ..ops import io as mio
         w = self._win[slot]
-        lens = (self.offsets[i0 + 1:i1 + 1] - self.offsets[i0:i1] - 1).tolist()
-        ld = mio.AsyncLoad(self.paths[i0:i1], [0] * (i1 - i0), lens, self.offsets[i0:i1] - self.offsets[i0],
-                           [1] * (i1 - i0), w, threads=self.threads)
+        ld = mio.AsyncLoad(self.paths[i0:i1], [0] * (i1 - i0), self._lens[i0:i1], self.offsets[i0:i1] - self.offsets[i0],
+                           self._pad[i0:i1], w, threads=self.threads)
         ld.wait()
         return w[:nbytes]
 
@@ -249,6 +250,22 @@ class WindowedSplitStore(SplitStore):
 
     def line_offsets(self) -> np.ndarray:
         raise ValueError("line numbering needs a store holding every split")
+
+
+def _file_pads(paths) -> tuple[list[int], list[int]]:
+    """(sizes, pads): pad 1 when a file's last byte is not a newline or a
+    space (then a newline follows the split: tokens never straddle splits)."""
+    lens, pad = [], []
+    for p in paths:
+        n = os.path.getsize(p)
+        last = b""
+        if n:
+            with open(p, "rb") as f:
+                f.seek(n - 1)
+                last = f.read(1)
+        lens.append(n)
+        pad.append(0 if last in (b"\n", b" ") else 1)
+    return lens, pad
 
 
 def assign_contiguous(weights, rank: int, world: int) -> tuple[int, int]:
@@ -684,6 +701,9 @@ class SPMDEngine:
         cap = self._arena_cap()
         if not cap or not ids:
             return False
+        if self.plane_kind != "fold":
+            raise ValueError(f"arena_cap_mb / MR_ARENA_CAP_MB streaming is implemented for the fold plane only "
+                             f"(this job runs the {self.plane_kind} plane)")
         a, b = self.splits.region(ids[0], ids[-1] + 1)
         return b - a > cap
 
@@ -1423,19 +1443,47 @@ class SPMDEngine:
         for _name, cols in gathered:
             yield from codec.iter_columnar(cols)
 
-    def stats_block(self, res: IterationResult) -> str:
-        m = res.map_jobs
-        r = res.red_jobs
-        ms = sum(x.cpu_time for x in m)
-        rs = sum(x.cpu_time for x in r)
-        mr = sum(x.real_time for x in m)
-        rr = sum(x.real_time for x in r)
+    def global_stats(self, res) -> dict:
+        """The iteration's statistics over EVERY rank (server.lua:155-183,538-600
+        aggregates over all job documents): sums of the jobs' cpu/real times,
+        distinct keys, values and shuffled bytes; cluster times and server time
+        = the slowest rank's.  A collective at W > 1 (one all-gather of a
+        small vector): every rank must call it."""
         T = res.timings
-        # device spans (HIP events) when measured, else host times; the keys
-        # and their order are the reference's (server.lua:555-600)
         dev = "device_map" in T
-        map_ct = T["device_map"] if dev else T["map"]
-        red_ct = (T.get("device_shuffle", 0.0) + T.get("device_tail", 0.0)) if dev else T["shuffle"] + T["reduce"]
+        map_ct = T["device_map"] if dev else T.get("map", 0.0)
+        red_ct = (T.get("device_shuffle", 0.0) + T.get("device_tail", 0.0)) if dev else \
+            T.get("shuffle", 0.0) + T.get("reduce", 0.0)
+        # other ranks' map jobs are shared WAITING records with zero times:
+        # summing every record of this rank's list counts its own jobs only
+        vec = [sum(x.cpu_time for x in res.map_jobs), sum(x.cpu_time for x in res.red_jobs),
+               sum(x.real_time for x in res.map_jobs), sum(x.real_time for x in res.red_jobs),
+               float(getattr(res, "distinct_keys", 0)), float(getattr(res, "total_value", 0) or 0),
+               float(getattr(res, "bytes_shuffled", 0)), float(getattr(res, "bytes_shuffled_remote", 0)),
+               map_ct, red_ct, T.get("iteration", 0.0), T.get("device_map", 0.0), T.get("device_shuffle", 0.0),
+               T.get("device_tail", 0.0)]
+        nsum = 8
+        if self.world > 1:
+            dev_t = self.device if self.device.type == "cuda" and not D._is_gloo(self.group) else torch.device("cpu")
+            t = torch.tensor(vec, dtype=torch.float64, device=dev_t)
+            allv = D.all_gather_tensor(t.view(1, -1), self.group).view(self.world, -1).cpu().numpy()
+            vec = [float(allv[:, i].sum()) if i < nsum else float(allv[:, i].max()) for i in range(len(vec))]
+        keys = ("map_cpu", "red_cpu", "map_real", "red_real", "distinct_keys", "values", "bytes_shuffled",
+                "bytes_shuffled_remote", "map_cluster", "red_cluster", "server_time", "device_map",
+                "device_shuffle", "device_tail")
+        out = dict(zip(keys, vec))
+        out["device_spans"] = dev
+        out["failed_maps"] = getattr(res, "failed_maps", 0)  # global: rides on the count exchange
+        out["failed_reduces"] = getattr(res, "failed_reduces", 0)
+        out["ranks"] = self.world
+        return out
+
+    def stats_block(self, res: IterationResult) -> str:
+        """The reference's statistics block (server.lua:555-600 keys and
+        order) over every rank — a collective at W > 1 (global_stats)."""
+        g = self.global_stats(res)
+        ms, rs, mr, rr = g["map_cpu"], g["red_cpu"], g["map_real"], g["red_real"]
+        map_ct, red_ct = g["map_cluster"], g["red_cluster"]
         lines = [
             "#   Map sum(cpu_time)     %f" % ms, "#   Reduce sum(cpu_time)  %f" % rs,
             "# Sum(cpu_time)           %f" % (ms + rs), "#   Map sum(real_time)    %f" % mr,
@@ -1443,21 +1491,21 @@ class SPMDEngine:
             "# Sum(sys_time)           %f" % (mr + rr - ms - rs), "#   Map cluster time      %f" % map_ct,
             "#   Reduce cluster time   %f" % red_ct,
             "# Cluster time            %f" % (map_ct + red_ct),
-            "# Failed maps     %d" % getattr(res, "failed_maps", 0),
-            "# Failed reduces  %d" % getattr(res, "failed_reduces", 0),
-            "# Server time %f" % T["iteration"],
+            "# Failed maps     %d" % g["failed_maps"],
+            "# Failed reduces  %d" % g["failed_reduces"],
+            "# Server time %f" % g["server_time"],
         ]
         # SURVEY.md §5.5 additions: throughput, shuffle volume, device phases
-        vals = getattr(res, "total_value", 0)
-        if T["iteration"] > 0 and vals:
-            lines.append("# Values/s (server time) %.6g" % (vals / T["iteration"]))
-        lines.append("# Distinct keys %d" % getattr(res, "distinct_keys", 0))
-        if getattr(res, "bytes_shuffled", 0):
-            lines.append("# Bytes shuffled %d (to other ranks %d)" % (res.bytes_shuffled, res.bytes_shuffled_remote))
-        if dev:
-            lines.append("# Device spans ms: map (H2D + kernels) %.3f, shuffle %.3f, tail %.3f (%s)" % (
-                1e3 * T["device_map"], 1e3 * T.get("device_shuffle", 0.0), 1e3 * T.get("device_tail", 0.0),
-                "values are device-measured" if dev else "host"))
+        if g["server_time"] > 0 and g["values"]:
+            lines.append("# Values/s (server time) %.6g" % (g["values"] / g["server_time"]))
+        lines.append("# Distinct keys %d" % g["distinct_keys"])
+        if g["bytes_shuffled"]:
+            lines.append("# Bytes shuffled %d (to other ranks %d)" % (g["bytes_shuffled"], g["bytes_shuffled_remote"]))
+        if g["device_spans"]:
+            lines.append("# Device spans ms (slowest rank): map (H2D + kernels) %.3f, shuffle %.3f, tail %.3f" % (
+                1e3 * g["device_map"], 1e3 * g["device_shuffle"], 1e3 * g["device_tail"]))
+        if self.world > 1:
+            lines.append("# Ranks %d (sums over every rank's jobs; cluster times = slowest rank)" % self.world)
         return "\n".join(lines) + "\n"
 
     # -- checkpoint / resume and fault injection -------------------------------

@@ -29,13 +29,28 @@ _INTERN: dict = {}
 _limit = PRUNE_MIN
 
 
+def _calibrate_dead_refs() -> int:
+    """getrefcount of an entry nobody else references, measured in the same
+    comprehension shape _prune uses (the count includes the table's key and
+    value, the loop variable and the call's argument on CPython 3.10, but
+    interpreters differ: 3.14 borrows stack references and reports less)."""
+    probe: dict = {}
+    t = builtins_tuple([object()])
+    probe[t] = t
+    del t
+    return [sys.getrefcount(k) for k in probe][0]
+
+
+_DEAD_REFS = _calibrate_dead_refs()
+
+
 def _prune() -> None:
-    """Drop entries referenced only by the table (key and value are the same
-    object: 2 references, plus the loop variable and getrefcount's argument).
-    Outer tuples go first, so a pass repeats while it frees anything."""
+    """Drop entries referenced only by the table (reference count at most
+    the calibrated one of an unreferenced entry).  Outer tuples go first, so
+    a pass repeats while it frees anything."""
     global _limit
     while True:
-        dead = [k for k in _INTERN if sys.getrefcount(k) <= 4]
+        dead = [k for k in _INTERN if sys.getrefcount(k) <= _DEAD_REFS]
         for k in dead:
             del _INTERN[k]
         n = len(dead)
@@ -136,3 +151,7 @@ def utest() -> None:
     assert tuple.stats()[0] >= base + 10000
     del live
     assert tuple.stats()[0] <= base + 1
+    # an interned tuple held across a forced prune keeps its identity
+    held = tuple(["held", 1, [2, 3]])
+    _prune()
+    assert tuple(["held", 1, [2, 3]]) is held and held[2] is tuple(2, 3)

@@ -169,3 +169,32 @@ def test_journal_cut_mid_record_is_truncated_before_appending(tmp_path):
     assert c4.request("BLOB_GET", "jdb", "a")[1] == [b"first"]
     assert c4.request("BLOB_GET", "jdb", "b")[0] == 1  # not found
     assert os.path.getsize(journal) == good
+
+
+def test_journal_of_unknown_format_is_refused_not_truncated(tmp_path):
+    """a journal without this format's header (e.g. the round-1
+    len|body format) is refused, never cut to 0 bytes; a checksum mismatch
+    keeps the cut-off tail as <journal>.corrupt."""
+    journal = str(tmp_path / "old.journal")
+    old = (5).to_bytes(4, "little") + b"\x01\x00abc"
+    with open(journal, "wb") as f:
+        f.write(old)
+    with pytest.raises(Exception):
+        coordinator.start_local(journal=journal)
+    with open(journal, "rb") as f:
+        assert f.read() == old
+    j2 = str(tmp_path / "new.journal")
+    c1 = coordinator.Client(coordinator.start_local(journal=j2))
+    c1.request("BLOB_PUT", "jdb", "a", b"first")
+    good = os.path.getsize(j2)
+    c1.request("BLOB_PUT", "jdb", "b", b"second")
+    with open(j2, "r+b") as f:  # flip a byte of the second record's body
+        f.seek(good + 9)
+        b = f.read(1)
+        f.seek(good + 9)
+        f.write(bytes([b[0] ^ 0xFF]))
+    size = os.path.getsize(j2)
+    c2 = coordinator.Client(coordinator.start_local(journal=j2))
+    assert c2.request("BLOB_GET", "jdb", "a")[1] == [b"first"]
+    assert os.path.getsize(j2) == good
+    assert os.path.getsize(j2 + ".corrupt") == size - good

@@ -26,8 +26,9 @@ def test_text_tokens_lines_fields_gpu(gpu):
     for n in (0, 1, 4095, 4096, 4097, 300_001):
         b = tricky_text(rng, n)
         for off in (0, 3):  # unaligned views too
-            hb = torch.frombuffer(bytearray(b"x" * off + b), dtype=torch.uint8)[off:]
-            db = torch.frombuffer(bytearray(b"x" * off + b), dtype=torch.uint8).to(gpu)[off:]
+            full = torch.from_numpy(np.frombuffer(b"x" * off + b, dtype=np.uint8).copy())
+            hb = full[off:]
+            db = full.to(gpu)[off:]
             for f in (TX.tokens, TX.lines):
                 hs, hl = f(hb)
                 ds, dl = f(db)

@@ -62,6 +62,32 @@ def test_cpu_single_rank_matches_oracle():
         assert keys == sorted(keys)
 
 
+@pytest.mark.parametrize("windowed", [False, True])
+def test_split_files_number_lines_like_the_oracle(tmp_path, windowed):
+    """SplitStore.from_files (execute_spmd --split-glob) pads a
+    file with a newline only when it does not end in a newline or a space,
+    like the in-memory store and the oracle — a file ending in '\n' gains no
+    empty line, so later line ids do not shift."""
+    from lua_mapreduce_1_amd import spmd
+    from lua_mapreduce_1_amd.parallel.spmd import SplitStore, WindowedSplitStore
+    splits = _splits()
+    paths = []
+    for i, b in enumerate(splits):
+        p = tmp_path / f"s{i:03d}.txt"
+        p.write_bytes(b)
+        paths.append(str(p))
+    store = SplitStore.from_files(paths, pin=False)
+    assert len(store) == len(splits)
+    params = dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                  init_args={"nsplits": len(splits), "num_reducers": 5})
+    if windowed:
+        # the windowed store (inputs larger than host memory) has the same layout
+        ws = WindowedSplitStore(paths, window_mb=64)
+        assert ws.offsets.tolist() == store.offsets.tolist()
+    spmd(params, device="cpu", split_store=store).run()
+    assert _result() == _naive(splits)
+
+
 def test_server_worker_host_plane_matches_oracle(tmp_path):
     """The same module through server + worker (host mapfn reads its split
     file, reducefn = sorted distinct lines) — the reference deployment."""
