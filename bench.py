@@ -59,6 +59,9 @@ def parse_args(argv=None):
     ap.add_argument("--from-files", default=None, metavar="DIR",
                     help="corpus = the files in DIR (sorted; one split per file) instead of the synthetic one")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold file-to-result first iteration")
+    ap.add_argument("--force-shuffle", action="store_true",
+                    help="also time the W>1 data path (pack, count exchange, RCCL all_to_all_single, receive-side "
+                         "reduce) at one GPU: a one-rank nccl group, reported as force_shuffle_ms_per_step")
     # smaller corpora only for smoke tests of the harness (the headline number
     # is the full Europarl shape; a reduced one is flagged in "data"/"config")
     ap.add_argument("--lines", type=int, default=None)
@@ -191,6 +194,14 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     import torch.distributed as dist
     backend = dist.get_backend() if dist.is_initialized() else ("single-process-" + device.type)
+    if args.force_shuffle and world == 1 and not dist.is_initialized():
+        # a one-rank group, created before any other GPU work: the shuffle's
+        # collectives then run on RCCL (nccl backend) as at W > 1
+        import datetime
+        kw = {"device_id": device} if device.type == "cuda" else {}
+        dist.init_process_group("nccl" if device.type == "cuda" else "gloo", rank=0, world_size=1,
+                                init_method=f"tcp://127.0.0.1:{_free_port()}",
+                                timeout=datetime.timedelta(seconds=300), **kw)
     if world != args.gpus and rank == 0:
         print(f"# warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if device.type == "cuda":
@@ -279,6 +290,26 @@ def main() -> int:
     elapsed = D.all_reduce_max(elapsed, device)
     ms = 1000.0 * elapsed / max(1, args.steps)
 
+    fs_ms = fs_valid = None
+    if args.force_shuffle:
+        # the same steps with the W > 1 path forced at this world size
+        e2 = SPMDEngine(dict(params, force_shuffle=True), device=device, split_store=store, verbose=args.verbose,
+                        table_capacity=table_cap)
+        e2.prefetch, e2.resident, e2.pipeline = True, args.resident, TUNABLES.pipeline
+        for w in range(args.warmup):
+            e2.run_iteration(prefetch_next=w < args.warmup - 1, lookahead=args.warmup - 1 - w)
+        D.barrier(device=device)
+        sync()
+        t0 = time.perf_counter()
+        r2 = None
+        for i in range(args.steps):
+            r2 = e2.run_iteration(prefetch_next=i < args.steps - 1, lookahead=args.steps - 1 - i)
+        sync()
+        D.barrier(device=device)
+        fs_ms = 1000.0 * D.all_reduce_max(time.perf_counter() - t0, device) / max(1, args.steps)
+        fs_valid = r2 is not None and D.all_reduce_sum_int(r2.total_value, device) == words
+        del e2, r2
+
     # validation outside the timed region: every token counted exactly once,
     # and (synthetic corpus) every word's count equal to the generator's
     counted = D.all_reduce_sum_int(last.total_value, device) if last is not None else 0
@@ -297,7 +328,8 @@ def main() -> int:
               f"bytes {total_bytes}, per-phase s: {last.timings}, cold first iteration ms {cold_ms} "
               f"(tokens {cold_tokens}, page cache dropped {not args.no_cold and dropped})",
               file=sys.stderr, flush=True)
-        valid = counted == words and per_key is not False and (cold_tokens is None or cold_tokens == words)
+        valid = counted == words and per_key is not False and (cold_tokens is None or cold_tokens == words) and \
+            fs_valid is not False
         if not valid:
             print("# ERROR: result validation failed", file=sys.stderr, flush=True)
         value = words / (ms / 1000.0)
@@ -313,13 +345,16 @@ def main() -> int:
                         "this step's map/reduce)")),
             "backend": backend, "world": world,
             "cold_first_iteration_ms": cold_ms,
+            **({"force_shuffle_ms_per_step": fs_ms, "force_shuffle_valid": fs_valid,
+                "force_shuffle_backend": dist.get_backend() if dist.is_initialized() else None}
+               if args.force_shuffle else {}),
             "config": {"model": "wordcount (MapReduce: taskfn/mapfn/partitionfn/reducefn)", "global_batch": len(store),
                        "seq_len": 10000, "parallelism": f"dp{world}", "num_reducers": args.reducers,
                        "words": words, "bytes": total_bytes, "valid": valid, "per_key_valid": per_key,
                        "input": "hbm-resident" if args.resident else "host-staged-every-step"},
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     # a wrong answer is a failed run: the driver's exit code sees it
     return 0 if valid else 3

@@ -743,26 +743,14 @@ int mr_copy_to_host(const void* src, void* host_dst, const void* nelem, u64 elem
   return (int)hipGetLastError();
 }
 
-// Device -> pinned-host download on stream s.  Mode 1 (the framework's
-// default, MR_D2H=sdma): an SDMA copy (hipMemcpyAsync).  Mode 0 (MR_D2H=kernel):
-// shader stores over PCIe (copy_to_host_kernel), chosen in round 1 because an
-// SDMA download queued behind the next iterations' input copies finished 2 ms
-// late (tools/d2h_queue_probe.py, profiles/r1/d2h_queue_probe.log); with the
-// round-2 pipeline the host-staged bench is the same either way and the
-// HBM-resident one 0.19 ms faster with SDMA, whose downloads take no CU time
-// from the next map (profiles/r2/d2h_ab/).
-static int g_d2h_mode = 0;
-void mr_set_d2h_mode(int mode) { g_d2h_mode = mode; }
-
+// Device -> pinned-host download on stream s: an SDMA copy (hipMemcpyAsync),
+// which takes no CU time from the next iteration's map (the round-1 form,
+// shader stores over PCIe, measured 0.19 ms slower on the HBM-resident bench
+// and equal host-staged: profiles/r2/d2h_ab/; removed in round 3,
+// profiles/r3/pruned/).
 int mr_d2h_async(void* host_dst, const void* src, u64 nbytes, hipStream_t s) {
   if (nbytes == 0) return 0;
-  if (g_d2h_mode == 1) return (int)hipMemcpyAsync(host_dst, src, nbytes, hipMemcpyDeviceToHost, s);
-  void* dptr = nullptr;
-  if (hipHostGetDevicePointer(&dptr, host_dst, 0) != hipSuccess || dptr == nullptr) dptr = host_dst;
-  const u64 g = (nbytes + 16 * 256 - 1) / (16 * 256);
-  hipLaunchKernelGGL(copy_to_host_kernel, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s, (const u8*)src,
-                     (u8*)dptr, (const long long*)nullptr, (u64)1, nbytes);
-  return (int)hipGetLastError();
+  return (int)hipMemcpyAsync(host_dst, src, nbytes, hipMemcpyDeviceToHost, s);
 }
 
 // Host-visible completion flags.  A waiting host that sleeps in

@@ -33,7 +33,6 @@ _SIGS = {
     "mr_d2h_async": [_p, _p, _u64, _p],
     "mr_h2d_pull": [_p, _p, _u64, _i32, _p],
     "mr_signal_host": [_p, _u32, _p],
-    "mr_set_d2h_mode": [_i32],
     "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64, _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
     "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p, _p],
@@ -126,15 +125,12 @@ def lib():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = _u64 if name in _RESTYPE_U64 else _i32
-        L.mr_set_d2h_mode.restype = None
         L.mr_host_alloc_coherent.argtypes = [_u64]
         L.mr_host_alloc_coherent.restype = _p
         L.mr_host_alloc.argtypes = [_u64]
         L.mr_host_alloc.restype = _p
         L.mr_host_free.argtypes = [_p]
         L.mr_host_free.restype = _i32
-        # downloads: SDMA by default, shader stores with MR_D2H=kernel (see sort.hip mr_d2h_async)
-        L.mr_set_d2h_mode(1 if TUNABLES.d2h == "sdma" else 0)
         if L.mr_sort_set_rounds(TUNABLES.sort_rounds) != 0:
             raise ValueError(f"MR_SORT_ROUNDS={TUNABLES.sort_rounds}: must be 16, 24 or 32")
         _LIB = L

@@ -47,7 +47,6 @@ from . import dist as D
 N_ARENAS = 3
 # largest map table the sparsity rule asks for (2^25 slots = 1.3 GB of HBM)
 _MAX_SPARSE_CAP = 1 << 25
-_PREFETCH_LATE = TUNABLES.prefetch_late
 _PREFETCH_SINGLE = TUNABLES.prefetch_single
 
 
@@ -454,18 +453,11 @@ class SPMDEngine:
         self._rec_tmpl = None
         self.copy_stream, self.streams = _engine_streams(self.device)
         self._plans: dict = {}
-        import os as _os
-        # hipGraph replay of the device tail: measured (tools/proxy_rank.py) to
-        # save ~0.05 ms on small per-rank inputs but to cost ~0.25 ms (and show
-        # rare multi-ms stalls) on the full single-GPU corpus, so it is opt-in
-        self.use_graphs = TUNABLES.graphs
-        self._tail_graphs: dict = {}
         # per slot (pipelined iterations alternate): device event timers, the
         # job ranges of the map chunks and their device error words
         self._timers: list = [None, None]
         self._chunks: list = [[], []]
         self._errs: list = [None, None]
-        self._tail_seen: set = set()
         self.iteration = 0
         self.finished = False
         # iteration manifest: rank 0 records every iteration
@@ -888,7 +880,7 @@ class SPMDEngine:
 
     def _timer(self):
         """The device timer of the current slot (None: timing off / CPU)."""
-        if not (TUNABLES.device_timing and self.device.type == "cuda") or self.use_graphs:
+        if not (TUNABLES.device_timing and self.device.type == "cuda"):
             return None
         t = self._timers[self.tslot]
         if t is None:
@@ -1139,11 +1131,9 @@ class SPMDEngine:
                 and self.nparts <= 256 and TUNABLES.fused_tail)
 
     def _finalize_table(self, table, n: int, src) -> dict:
-        """The fused device tail of a table: one native call (mr_tail_run) by
-        default, the Python-sequenced launches with MR_NATIVE_TAIL=0."""
-        if TUNABLES.native_tail:
-            return devmod.finalize_table_native(table, n, src, self.nparts)
-        return devmod.finalize_table_device(table, n, src, self.nparts)
+        """The fused device tail of a table: every launch and download queued
+        by one native call (mr_tail_run, csrc/hip/tail.hip)."""
+        return devmod.finalize_table_native(table, n, src, self.nparts)
 
     def _reduce_insert_received(self, rbuf, recv_counts, rows: int) -> int:
         """Received records -> this rank's reduce table (one insert launch);
@@ -1184,37 +1174,6 @@ class SPMDEngine:
         return self.red_table.compact()
 
     # ------------------------------------------------------------------------
-    def _graph_tail_ok(self) -> bool:
-        return (self.use_graphs and self.device.type == "cuda" and self.partmod is not None
-                and getattr(self.partmod, "device_partition", None) is not None)
-
-    def _graphed_tail(self, n: int, overflow: bool, src):
-        """Device tail of a W=1 iteration as a hipGraph, captured the second
-        time the same (table fill, input) shows up and replayed afterwards —
-        the tail is ~25 short launches whose Python/launch overhead would
-        otherwise dominate small per-rank inputs."""
-        key = (n, src.data_ptr(), src.numel(), self.table.tag.data_ptr())
-        hit = self._tail_graphs.get(key)
-        if hit is not None:
-            g, pend = hit
-            g.replay()
-            return pend
-        if key not in self._tail_seen:
-            self._tail_seen.add(key)
-            hi, lo, val, rep = self.table.compact((n, overflow))
-            part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
-            return devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
-        if len(self._tail_graphs) >= 4:
-            self._tail_graphs.clear()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            hi, lo, val, rep = self.table.compact((n, overflow))
-            part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
-            pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
-        self._tail_graphs[key] = (g, pend)
-        g.replay()
-        return pend
-
     def _can_pipeline(self) -> bool:
         return (self.copy_stream is not None and self.device_input == "split" and not self._arena_cap()
                 and bool(modules.field(self.taskfn, "spmd_replicated_taskfn")))
@@ -1296,12 +1255,8 @@ class SPMDEngine:
                 t0 = time.time()
                 with trace.range("mr.map.issue"):
                     self._run_map(jobs, recs, j0, j1)
-            if ahead and not _PREFETCH_LATE:
+            if ahead:
                 self._prefetch_ahead(jobs, j0, j1, q, ahead)
-            elif ahead and (q + 1) % N_ARENAS not in self._inflight:
-                # nothing queued behind this iteration's copies: start q+1's
-                # now, or the copy engine idles through this map
-                self._prefetch(jobs, j0, j1, q + 1)
             return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, ahead, q)
 
     def _prefetch_ahead(self, jobs, j0, j1, q: int, ahead: int) -> None:
@@ -1319,15 +1274,14 @@ class SPMDEngine:
     def _finish_iteration(self, res, T, t_start, t0, jobs, recs, j0, j1, ahead, q) -> IterationResult:
         prefetch_next = ahead > 0
         pipelined = prefetch_next and self.pipeline and self._can_pipeline()
-        # When the next iteration's map is queued (MR_NEXT_MAP; "auto" =
-        # chain for HBM-resident input, after_tail otherwise): "after_tail"
-        # = right after this iteration's first tail kernels (W=1) / its count
-        # exchange (W>1), so those get the GPU first; "before_tail" = before
-        # the W=1 tail; "before_sync" = before this map's synchronisation, so
-        # with HBM-resident input two maps are queued back to back and the GPU
-        # never idles while the host syncs and issues (the tail's short kernels
-        # run beside the next map); "chain" = the same, the next map gated on
-        # this one's completion (an event, no host round trip).
+        # When the next iteration's map is queued: host-staged input —
+        # right after this iteration's tail kernels (W=1) / its count exchange
+        # (W>1), so those get the GPU first; HBM-resident input ("chain") —
+        # before this map's synchronisation, gated on its completion by an
+        # event, so two maps run back to back and the GPU never idles while
+        # the host syncs and issues (the tail's short kernels run beside the
+        # next map).  The other orders measured slower (profiles/r2/next_map/,
+        # removed in round 3: profiles/r3/pruned/).
         next_map = [pipelined]
 
         def issue_next_map(gate=None):
@@ -1335,14 +1289,11 @@ class SPMDEngine:
                 next_map[0] = False
                 with trace.range("mr.map.issue_next"):
                     self._issue_next_map(jobs, j0, j1, q, gate)
-        when = TUNABLES.next_map
-        if when == "auto":
-            when = "chain" if self.resident else "after_tail"
-        if when in ("before_sync", "chain") and next_map[0]:
+        if self.resident and next_map[0]:
             gate = None
-            if when == "chain" and self.device.type == "cuda":
-                # "chain": the next map starts when this one ends (two maps
-                # sharing the GPU ran slower than one after the other)
+            if self.device.type == "cuda":
+                # the next map starts when this one ends (two maps sharing the
+                # GPU ran slower than one after the other)
                 gate = torch.cuda.Event()
                 gate.record()
             issue_next_map(gate)
@@ -1363,13 +1314,7 @@ class SPMDEngine:
         # RCCL data path exercised on a single GPU: pack -> count exchange ->
         # all_to_all_single -> receive-side insert)
         sh = self.world > 1 or self.force_shuffle
-        if not sh and self._graph_tail_ok():
-            # the whole device tail (compact -> partition -> sort -> key bytes
-            # -> downloads) is one replayed hipGraph once a table size repeats
-            pend = self._graphed_tail(n_claimed, overflow, src)
-        elif not sh and fused:
-            if when == "before_tail":
-                issue_next_map()
+        if not sh and fused:
             pend = self._finalize_table(self.table, n_claimed, src)
             issue_next_map()
         elif sh and fused:
@@ -1403,8 +1348,6 @@ class SPMDEngine:
         if timer is not None:
             timer.mark("tail_end")
         issue_next_map()
-        if _PREFETCH_LATE:
-            self._prefetch_ahead(jobs, j0, j1, q, ahead)
 
         with trace.range("mr.finalize_host"):
             cols = devmod.finalize_host(pend, self.partmod)

@@ -332,53 +332,6 @@ def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, p
     return pend
 
 
-def finalize_table_device(table, n: int, src, nparts: int) -> dict:
-    """Fused device tail straight from an HBM hash table (csrc/hip/tail.hip):
-    compact + FNV partition + composite key + digit histograms in one kernel,
-    the composite onesweep sort (no histogram pass), one gather that also
-    yields key lengths, the exact-order tie fix-up, key bytes, and ONE packed
-    download of values/offsets/partition counts (+ the key-byte DMA).
-    ``n`` = occupied slots (table.stats()).  Requires nparts <= 256."""
-    from ..ops import _hip
-    d = table.device
-    s = _hip.stream(d)
-    z = lambda dt: torch.empty(n, dtype=dt, device=d)  # noqa: E731
-    hi0, lo0, val0, rep0, c = z(torch.int64), z(torch.int64), z(torch.int64), z(torch.int64), z(torch.int64)
-    part0 = z(torch.int32)
-    small = torch.zeros(1 + 2048 // 2 + nparts, dtype=torch.int64, device=d)  # counter | ghist (u32) | pcount
-    counter, ghist, pcount = small[:1], small[1:1 + 1024].view(torch.int32), small[1 + 1024:]
-    bhist = torch.empty(int(_hip.lib().mr_tail_bhist_bytes(table.cap)), dtype=torch.uint8, device=d)
-    _hip.call("mr_tail_compact", *table._gtab(), table.cap, nparts, _hip.ptr(src), _hip.ptr(hi0), _hip.ptr(lo0),
-              _hip.ptr(val0), _hip.ptr(rep0), _hip.ptr(part0), _hip.ptr(c), _hip.ptr(counter), _hip.ptr(ghist),
-              _hip.ptr(pcount), _hip.ptr(bhist), n, s)
-    perm, cs = ops.sort_keys([c], return_keys=True, ghist=ghist)
-    hi, lo, val, rep, ln = z(torch.int64), z(torch.int64), z(torch.int64), z(torch.int64), z(torch.int64)
-    part = z(torch.int32)
-    _hip.call("mr_tail_gather", _hip.ptr(perm), n, _hip.ptr(hi0), _hip.ptr(lo0), _hip.ptr(val0), _hip.ptr(rep0),
-              _hip.ptr(part0), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), _hip.ptr(ln), s)
-    bad = torch.zeros(1, dtype=torch.int32, device=d)
-    _hip.call("mr_tie_fixup", _hip.ptr(cs), _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part),
-              n, _hip.ptr(bad), _hip.ptr(src), _hip.ptr(ln), s)  # ln is permuted with the rows
-    cap = src.numel()
-    off, blob = ops.gather_key_bytes(hi, lo, rep, src, lengths=ln, capacity=cap)
-    nb = int(_hip.lib().mr_tail_pack_bytes(n, nparts))
-    packed = torch.empty(nb, dtype=torch.uint8, device=d)
-    _hip.call("mr_tail_pack", _hip.ptr(val), _hip.ptr(off), n, _hip.ptr(pcount), nparts, _hip.ptr(bad),
-              _hip.ptr(ops.primitives.sort_error_word(d)), _hip.ptr(packed), s)
-    hp = _POOL.get("pack", nb, torch.uint8)
-    dma_to_host(hp, packed)
-    est = _BLOB_EST.get(d)
-    if est is not None:
-        est = min(est, blob.numel())
-        hb = _POOL.get("blob", max(est, 1 << 16), torch.uint8)
-        dma_to_host(hb[:est], blob[:est])
-    else:
-        hb = _POOL.get("blob", max(1 << 20, 16 * n), torch.uint8)
-        ops.copy_to_host(blob, hb, off[n:])
-    return {"n": n, "nparts": nparts, "args": (hi0, lo0, val0, rep0), "src": src, "presorted": False, "hi": hi,
-            "lo": lo, "fused": True, "hp": hp, "off": off, "blob": blob, "est": est, "hb": hb}
-
-
 _TAIL_WS: dict = {}  # device -> (workspace uint8 tensor, {layout key: (offsets, views)})
 _TB = {name: i for i, name in enumerate(
     "HI0 LO0 VAL0 REP0 C PART0 ZERO K0 K1 P0 P1 GRAN HI LO VAL REP PART LN OFF PARTIALS BLOB PACKED BHIST".split())}
@@ -443,9 +396,14 @@ def compact_partition(table, n: int, src, nparts: int):
 
 
 def finalize_table_native(table, n: int, src, nparts: int) -> dict:
-    """finalize_table_device with every launch and download queued by ONE
-    native call (mr_tail_run): same kernels, same packed download, same
-    pending-state contract for finalize_host."""
+    """Fused device tail straight from an HBM hash table, every launch and
+    download queued by ONE native call (mr_tail_run, csrc/hip/tail.hip):
+    compact + FNV partition + composite key + digit histograms in one kernel,
+    the composite onesweep sort (no histogram pass), one gather that also
+    yields key lengths, the exact-order tie fix-up, key bytes, and ONE packed
+    download of values/offsets/partition counts (+ the key-byte DMA).  ``n``
+    = occupied slots (table.stats()).  Requires nparts <= 256; returns the
+    pending state for finalize_host."""
     from ..ops import _hip
     d = table.device
     cap = src.numel()

@@ -62,21 +62,8 @@ class Tunables:
     stream_heap_mb: float = _knob("MR_STREAM_HEAP_MB", 64.0,
                                   "SPMD streaming rounds: HBM heap for the bytes of distinct long keys, MiB")
     fused_tail: bool = _knob("MR_FUSED_TAIL", True, "fused reduce-side tail kernels (tail.hip)")
-    native_tail: bool = _knob("MR_NATIVE_TAIL", True, "queue the whole tail from one native call (mr_tail_run)")
-    graphs: bool = _knob("MR_GRAPHS", False, "replay the W=1 tail as a hipGraph (stalls the copy stream: off)")
     pipeline: bool = _knob("MR_PIPELINE", True, "bench/proxies: map of iteration i+1 overlaps the tail of i")
-    next_map: str = _knob("MR_NEXT_MAP", "auto",
-                          "pipelined iterations: when the next iteration's map is queued — 'after_tail' "
-                          "(after this iteration's first tail kernels), 'before_tail', 'before_sync' "
-                          "(before this map's synchronisation), 'chain' (before the sync, gated on this map's "
-                          "completion by an event), 'auto' = chain for HBM-resident input, after_tail for "
-                          "host-staged input (profiles/r2/next_map/)")
     prefetch_single: bool = _knob("MR_PREFETCH_SINGLE", True, "prefetched inputs: one DMA per iteration")
-    prefetch_late: bool = _knob("MR_PREFETCH_LATE", False, "issue prefetches after the tail instead of first")
-    d2h: str = _knob("MR_D2H", "sdma",
-                     "downloads: 'sdma' (DMA engine) or 'kernel' (shader stores into pinned memory: CU time that "
-                     "competes with the next map; resident bench 2.93 vs 2.74 ms, staged equal, "
-                     "profiles/r2/d2h_ab/)")
     spin_us: float = _knob("MR_SPIN_US", 2000.0, "host spin on completion words before hipStreamSynchronize, us")
     force_shuffle: bool = _knob("MR_FORCE_SHUFFLE", False,
                                 "SPMD: run the W>1 shuffle (pack, count exchange, all-to-all, receive insert) also "

@@ -267,20 +267,17 @@ def test_sort_onesweep_large_tile_sizes(gpu, rounds):
     assert torch.equal(kg.cpu(), w[pc])
 
 
-@pytest.mark.parametrize("resident,next_map", [(False, "auto"), (True, "auto"), (True, "before_sync"),
-                                               (False, "before_tail")])
-def test_spmd_prefetch_pipelined_iterations_match(gpu, monkeypatch, resident, next_map):
+@pytest.mark.parametrize("resident", [False, True])
+def test_spmd_prefetch_pipelined_iterations_match(gpu, monkeypatch, resident):
     """Iterations whose input copies were prefetched into the other arena give
     the same results as non-pipelined ones (and the counts stay exact); also
-    with HBM-resident input and every MR_NEXT_MAP mode (auto = chain for
-    resident input: the next map queued before this map's sync, gated on its
-    completion).  The first map grows the later maps' tables to the sparse
-    capacity (MR_MAP_SPARSE_MIN_MB=0, 64 slots per key: past the default
-    2^20), also while a map is queued ahead."""
+    with HBM-resident input (the next map queued before this map's sync,
+    gated on its completion).  The first map grows the later maps' tables to
+    the sparse capacity (MR_MAP_SPARSE_MIN_MB=0, 64 slots per key: past the
+    default 2^20), also while a map is queued ahead."""
     import dataclasses
     from lua_mapreduce_1_amd.parallel import spmd as S
-    monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(S.TUNABLES, next_map=next_map, map_sparse_min_mb=0.0,
-                                                           map_sparsity=64))
+    monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(S.TUNABLES, map_sparse_min_mb=0.0, map_sparsity=64))
     from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore
     from lua_mapreduce_1_amd.utils.corpus import europarl_like
     M = "lua_mapreduce_1_amd.models.wordcount"
