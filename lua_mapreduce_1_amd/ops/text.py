@@ -88,7 +88,8 @@ def line_index(text: torch.Tensor, positions: torch.Tensor, newlines: torch.Tens
 def field(text: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor, sep: int | bytes, k: int):
     """Span of field ``k`` (0-based) of each line given by (starts, lens),
     fields separated by the byte ``sep``; a trailing ``\\r`` is dropped.  A
-    missing field has start -1 and length 0."""
+    missing field (also every field of an empty line) has start -1 and
+    length 0."""
     if isinstance(sep, (bytes, str)):
         sep = (sep.encode() if isinstance(sep, str) else sep)[0]
     m = starts.numel()
@@ -106,11 +107,11 @@ def field(text: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor, sep: int
     fl = np.zeros(m, np.int32)
     sb = bytes([sep])
     for i, (s, n) in enumerate(zip(_np(starts).tolist(), _np(lens).tolist())):
-        line = b[s:s + n]
+        line = b[s:s + n] if n > 0 else b""
         if line.endswith(b"\r"):
             line = line[:-1]
-        if n <= 0:
-            continue
+        if not line:
+            continue  # an empty line has no fields
         parts = line.split(sb)
         if k < len(parts):
             fs[i] = s + sum(len(p) + 1 for p in parts[:k])
