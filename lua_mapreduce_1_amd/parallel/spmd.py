@@ -1133,7 +1133,7 @@ class SPMDEngine:
     def _finalize_table(self, table, n: int, src) -> dict:
         """The fused device tail of a table: every launch and download queued
         by one native call (mr_tail_run, csrc/hip/tail.hip)."""
-        return devmod.finalize_table_native(table, n, src, self.nparts)
+        return devmod.finalize_table_native(table, n, src, self.nparts, blob_cap=getattr(self, "_blob_cap", None))
 
     def _reduce_insert_received(self, rbuf, recv_counts, rows: int) -> int:
         """Received records -> this rank's reduce table (one insert launch);
@@ -1343,14 +1343,29 @@ class SPMDEngine:
             trace.pop()
         T["shuffle"] = time.time() - t1
         t2 = time.time()
-        if pend is None:
-            pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part)
+        unfused = pend is None
+        if unfused:
+            pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part,
+                                          blob_cap=getattr(self, "_blob_cap", None))
         if timer is not None:
             timer.mark("tail_end")
         issue_next_map()
 
         with trace.range("mr.finalize_host"):
-            cols = devmod.finalize_host(pend, self.partmod)
+            try:
+                cols = devmod.finalize_host(pend, self.partmod)
+            except devmod.BlobCapacityError as e:
+                # keys that overlap in the input (n-gram spans) need more key
+                # bytes than the input holds: redo the tail with room for them
+                # (remembered for the next iterations)
+                self._blob_cap = e.nbytes + e.nbytes // 8
+                if unfused:
+                    pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part,
+                                                  blob_cap=self._blob_cap)
+                else:
+                    pend = self._finalize_table(self.red_table if sh else self.table,
+                                                n_red if sh else n_claimed, src)
+                cols = devmod.finalize_host(pend, self.partmod)
         digits = len(str(max(self.nparts - 1, 0)))
         for p in range(self.nparts):
             if cols["bounds"][p + 1] > cols["bounds"][p]:

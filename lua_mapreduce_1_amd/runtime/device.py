@@ -288,11 +288,25 @@ def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: to
     stay valid until the next finalize() call (copy them to keep them longer).
     """
     pend = finalize_device(hi, lo, val, rep, src, nparts, partition_module, part, _presorted)
-    return finalize_host(pend, partition_module, need_keys)
+    try:
+        return finalize_host(pend, partition_module, need_keys)
+    except BlobCapacityError as e:  # keys overlapping in their source (n-gram spans)
+        pend = finalize_device(hi, lo, val, rep, src, nparts, partition_module, part, _presorted, blob_cap=e.nbytes)
+        return finalize_host(pend, partition_module, need_keys)
+
+
+class BlobCapacityError(RuntimeError):
+    """The key bytes of a result exceed the blob capacity the tail was given
+    (keys that overlap in their source, e.g. n-gram spans, can need more
+    bytes than the source holds): re-run the tail with ``blob_cap=nbytes``."""
+
+    def __init__(self, nbytes: int, cap: int):
+        super().__init__(f"key bytes ({nbytes}) exceed the blob capacity ({cap})")
+        self.nbytes = nbytes
 
 
 def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, part: torch.Tensor | None = None,
-                    _presorted: bool = False) -> dict:
+                    _presorted: bool = False, blob_cap: int | None = None) -> dict:
     """The device half of :func:`finalize`: every kernel and device->pinned
     copy, no host synchronisation (so it can be captured in a hipGraph once
     the pinned buffers exist).  Returns the pending state for finalize_host."""
@@ -311,8 +325,9 @@ def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, p
         counts = ops.bincount(part, nparts) if n else torch.zeros(nparts, dtype=torch.int64)
         pend.update(val=val, off=off, blob=blob, counts=counts)
         return pend
-    # blob capacity bound: distinct keys occupy disjoint bytes of their source
-    cap = src.numel() if src is not None else max(16 * n, 1)
+    # blob capacity bound: distinct words occupy disjoint bytes of their
+    # source (a caller whose keys overlap there passes blob_cap)
+    cap = max(src.numel() if src is not None else max(16 * n, 1), blob_cap or 0)
     off, blob = ops.gather_key_bytes(hi, lo, rep, src, capacity=cap)
     counts = ops.bincount(part, nparts) if n else torch.zeros(nparts, dtype=torch.int64, device=hi.device)
     hv = _to_host(val, "val")
@@ -395,7 +410,7 @@ def compact_partition(table, n: int, src, nparts: int):
     return hi, lo, val, rep, part[:n]
 
 
-def finalize_table_native(table, n: int, src, nparts: int) -> dict:
+def finalize_table_native(table, n: int, src, nparts: int, blob_cap: int | None = None) -> dict:
     """Fused device tail straight from an HBM hash table, every launch and
     download queued by ONE native call (mr_tail_run, csrc/hip/tail.hip):
     compact + FNV partition + composite key + digit histograms in one kernel,
@@ -406,7 +421,7 @@ def finalize_table_native(table, n: int, src, nparts: int) -> dict:
     pending state for finalize_host."""
     from ..ops import _hip
     d = table.device
-    cap = src.numel()
+    cap = max(src.numel(), blob_cap or 0)
     ws, v = _tail_ws(d, n, nparts, cap, table.cap)
     nb = int(_hip.lib().mr_tail_pack_bytes(n, nparts))
     hp = _POOL.get("pack", nb, torch.uint8)
@@ -451,7 +466,7 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
             ho = pend["ho"]
             nbytes = int(ho[n]) if n else 0
         if nbytes > blob.numel() and not (flag0 := (f_bad if pend.get("fused") else int(pend["hbad"][0]))) & 4:
-            raise RuntimeError(f"key bytes ({nbytes}) exceed the blob capacity ({blob.numel()})")
+            raise BlobCapacityError(nbytes, blob.numel())
         if nbytes > blob.numel():
             nbytes = blob.numel()  # a given-up sort's rows: discarded below (re-sort)
         if est is not None and nbytes > est:  # grew past the estimate: copy the rest
