@@ -466,6 +466,8 @@ class SPMDEngine:
         # resumes there instead of at iteration 1
         self.checkpoint_dir = self.params.get("checkpoint_dir") or TUNABLES.spmd_checkpoint or None
         self.resumed_from = 0
+        self.maps_restored = 0  # iterations whose map this rank restored from its checkpoint
+        self._restored_src = None
 
 
     # ------------------------------------------------------------------------
@@ -1070,6 +1072,9 @@ class SPMDEngine:
 
     # -- shuffle + reduce -------------------------------------------------------
     def _source(self) -> torch.Tensor | None:
+        restored = getattr(self, "_restored_src", None)
+        if restored is not None:
+            return restored  # a map output restored from its checkpoint: its own key bytes
         if self.device_input == "split":
             return self.arena
         return self._ctx.source()
@@ -1248,13 +1253,15 @@ class SPMDEngine:
             # warm-up step): the first timed step then launches on warm streams
             stream = self.streams[self.tslot] if self.pipeline and self._can_pipeline() else None
         res.map_jobs = recs
+        self._restored_src = None
         with torch.cuda.stream(stream) if stream is not None else _nullctx():
             if pending is None:
                 with trace.range("mr.table_reset"):
                     self._fresh_table()
                 t0 = time.time()
-                with trace.range("mr.map.issue"):
-                    self._run_map(jobs, recs, j0, j1)
+                if not self._restore_map(jobs, recs, j0, j1):
+                    with trace.range("mr.map.issue"):
+                        self._run_map(jobs, recs, j0, j1)
             if ahead:
                 self._prefetch_ahead(jobs, j0, j1, q, ahead)
             return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, ahead, q)
@@ -1298,8 +1305,13 @@ class SPMDEngine:
                 gate.record()
             issue_next_map(gate)
         trace.push("mr.map.wait")
-        n_claimed, overflow = self._map_sync(jobs, recs, j0, j1)  # synchronises the map phase
+        if self._restored_src is not None:
+            n_claimed, overflow = self.table.stats()
+        else:
+            n_claimed, overflow = self._map_sync(jobs, recs, j0, j1)  # synchronises the map phase
+            self._save_map(n_claimed, overflow)
         trace.pop()
+        self._maybe_inject_fault("shuffle")
         T["map"] = time.time() - t0
         timer = self._timer()
         t1 = time.time()
@@ -1467,6 +1479,80 @@ class SPMDEngine:
         return "\n".join(lines) + "\n"
 
     # -- checkpoint / resume and fault injection -------------------------------
+    def _map_ckpt_path(self, iteration: int | None = None) -> str | None:
+        """This rank's map output of an iteration (``checkpoint_dir`` only):
+        written after the map phase, so a relaunch after a failure later in
+        the iteration (shuffle, reduce, another rank's map) re-runs only the
+        maps that had not finished — this rank's block of splits is restored
+        instead of re-mapped (the reference keeps map outputs
+        until the reduce consumes them, job.lua:293, server.lua:475-481)."""
+        if not self.checkpoint_dir:
+            return None
+        import hashlib
+        import json
+        key = hashlib.sha1(json.dumps(self._manifest_key(), sort_keys=True, default=repr).encode()).hexdigest()[:12]
+        it = self.iteration if iteration is None else iteration
+        return os.path.join(self.checkpoint_dir, "%s.map.it%d.r%d.w%d.%s" % (self.result_ns, it, self.rank,
+                                                                           self.world, key))
+
+    def _save_map(self, n: int, overflow: bool) -> None:
+        path = self._map_ckpt_path()
+        if path is None or self.plane_kind != "fold" or overflow:
+            return
+        from ..runtime import codec
+        hi, lo, val, rep = self.table.compact((n, False))
+        _, ln = ops.key_meta(hi, lo, rep, self._source(), want_part=False)
+        off, blob = ops.gather_key_bytes(hi, lo, rep, self._source(), lengths=ln)
+        h = lambda t: t.detach().cpu().numpy()  # noqa: E731
+        data = codec.encode_columnar(h(hi).view(np.uint64), h(lo).view(np.uint64), h(val), h(off), h(blob))
+        os.makedirs(self.checkpoint_dir, exist_ok=True)
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(data)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+
+    def _restore_map(self, jobs, recs, j0: int, j1: int) -> bool:
+        """Load this rank's map output of the current iteration from its
+        checkpoint, if an earlier launch wrote it: the table is refilled from
+        the saved keys (their bytes become the tail's key source) and the
+        rank's map jobs are WRITTEN without running."""
+        path = self._map_ckpt_path()
+        if path is None or self.plane_kind != "fold" or not os.path.exists(path):
+            return False
+        from ..runtime import codec
+        with open(path, "rb") as f:
+            cols = codec.decode_columnar(f.read())
+        d = self.device
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(d)  # noqa: E731
+        koff = cols["key_off"].astype(np.int64)
+        lens = np.diff(koff).astype(np.uint64)
+        rep = t(((koff[:-1].astype(np.uint64)) << np.uint64(24)) | lens)
+        blob = torch.from_numpy(np.concatenate([cols["key_blob"], np.zeros(1, np.uint8)])).to(d)
+        self._restored_src = blob
+        n = int(cols["hi"].size)
+        if 2 * n > self.table.cap:
+            self.table = ops.HashTable(ops.next_pow2(4 * n), device=d, op=self.op)
+            self._table_capacity = self.table.cap
+        timer = self._timer()
+        if timer is not None:
+            timer.begin()
+        self.table.insert(t(cols["hi"]), t(cols["lo"]), t(cols["val"]), rep, src=blob)
+        self.maps_restored += 1
+        now = time.time()
+        for j in range(j0, j1):
+            recs[j].status, recs[j].started, recs[j].written, recs[j].worker = STATUS.WRITTEN, now, now, self.rank
+        self._chunks[self.tslot] = []
+        self._log("# rank %d: map of iteration %d restored from %s\n" % (self.rank, self.iteration, path))
+        sys.stderr.write("# rank %d: map of iteration %d restored from its checkpoint\n" % (self.rank, self.iteration))
+        return True
+
+    def _drop_map_ckpt(self, iteration: int) -> None:
+        path = self._map_ckpt_path(iteration)
+        if path is not None and os.path.exists(path):
+            os.remove(path)
+
     def _manifest_path(self) -> str | None:
         if not self.checkpoint_dir:
             return None
@@ -1516,25 +1602,30 @@ class SPMDEngine:
             os.fsync(f.fileno())
         os.replace(tmp, path)  # atomic: a crash leaves the old or the new manifest
 
-    def _maybe_inject_fault(self) -> None:
-        """``MR_SPMD_FAULT=<iteration>:<rank>:raise|exit[:<attempt>]``:
-        that rank fails at the start of that iteration — ``exit`` leaves its
-        peers blocked in a collective, as a lost GPU or node would."""
+    def _maybe_inject_fault(self, phase: str = "start") -> None:
+        """``MR_SPMD_FAULT=<iteration>:<rank>:raise|exit[:<attempt>[:<phase>]]``
+        (SURVEY.md §5.3): that rank fails in that iteration — at its start
+        (phase ``start``, the default) or after the map phase (``shuffle``:
+        every rank's map output of the iteration is already checkpointed) —
+        ``exit`` leaves its peers blocked in a collective, as a lost GPU or
+        node would."""
         spec = os.environ.get("MR_SPMD_FAULT", TUNABLES.spmd_fault)
         if not spec:
             return
         f = spec.split(":")
         it, rk, action = f[:3]
-        if int(it) != self.iteration + 1 or int(rk) != self.rank:
+        want_phase = f[4] if len(f) > 4 and f[4] else "start"
+        cur = self.iteration + 1 if phase == "start" else self.iteration
+        if want_phase != phase or int(it) != cur or int(rk) != self.rank:
             return
-        # optional 4th field: only in that torchrun attempt (0 = first launch)
-        if len(f) > 3 and int(f[3]) != int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")):
+        # optional 4th field: only in that torchrun attempt (0 = first launch; empty = any)
+        if len(f) > 3 and f[3] != "" and int(f[3]) != int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")):
             return
         if action == "exit":
-            sys.stderr.write("# injected fault: rank %d exits at iteration %d\n" % (self.rank, self.iteration + 1))
+            sys.stderr.write("# injected fault: rank %d exits in iteration %d (%s)\n" % (self.rank, cur, phase))
             sys.stderr.flush()
             os._exit(17)
-        raise RuntimeError("injected fault: rank %d at iteration %d" % (self.rank, self.iteration + 1))
+        raise RuntimeError("injected fault: rank %d in iteration %d (%s)" % (self.rank, cur, phase))
 
     def run(self) -> IterationResult:
         """Iterate until finalfn returns something other than "loop".  With a
@@ -1568,6 +1659,8 @@ class SPMDEngine:
             if reply != "loop":
                 self.finished = True
                 self._save_manifest(finished=True)
+                self._drop_map_ckpt(self.iteration)
                 return res
             self._save_manifest(finished=False)
+            self._drop_map_ckpt(self.iteration)  # the iteration is recorded: its map outputs are consumed
             self._log("# LOOP again\n")
