@@ -722,7 +722,8 @@ class SPMDEngine:
             acc += sz
         rounds.append((k0, len(ids)))
         a0, b0 = st.region(ids[0], ids[-1] + 1)
-        H = max(1 << 16, min(b0 - a0, int(TUNABLES.stream_heap_mb * (1 << 20))))
+        heap_mb = getattr(self, "_stream_heap_mb", TUNABLES.stream_heap_mb)
+        H = max(1 << 16, min(b0 - a0, int(heap_mb * (1 << 20))))
         need = H + 2 * A
         buf = getattr(self, "_stream_buf", None)
         if buf is None or buf.numel() < need:
@@ -1005,7 +1006,16 @@ class SPMDEngine:
             sh = getattr(self, "_stream_heap", None)
             if sh is not None and self.arena is getattr(self, "_stream_buf", None):
                 if int(ops.host_read(sh)[1]):
-                    raise RuntimeError("streaming map: the long-key heap is full (raise MR_STREAM_HEAP_MB)")
+                    # the key heap ran out: long keys of some round still point
+                    # into a ring slot that was refilled — redo the map with a
+                    # heap twice as large (kept for later iterations)
+                    cur = getattr(self, "_stream_heap_mb", TUNABLES.stream_heap_mb)
+                    self._stream_heap_mb = 2 * cur
+                    sys.stderr.write("# streaming map: long-key heap of %.0f MiB full, re-mapping with %.0f MiB\n" % (
+                        cur, 2 * cur))
+                    self.table.reset()
+                    self._run_map(jobs, recs, j0, j1)
+                    continue
             bad = [k for k in range(nch) if e is not None and e[k]]
             if bad:
                 for k in bad:

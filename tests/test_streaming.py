@@ -90,11 +90,15 @@ def test_windowed_out_of_core_gpu(gpu, tmp_path):
     assert got == _want(splits)
 
 
-@pytest.mark.gpu
-def test_streaming_key_heap_full_raises(gpu, monkeypatch):
+@pytest.mark.parametrize("on_gpu", [False, pytest.param(True, marks=pytest.mark.gpu)])
+def test_streaming_key_heap_grows(request, monkeypatch, on_gpu):
+    """A long-key heap too small for the input's distinct long keys is
+    doubled and the map re-run (it used to raise)."""
     import dataclasses
     from lua_mapreduce_1_amd.parallel import spmd as S
+    dev = request.getfixturevalue("gpu") if on_gpu else "cpu"
     monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(S.TUNABLES, stream_heap_mb=0.07))
     splits = [colliding_text(40 + i, ntok=20000, nlong=3000) for i in range(4)]
-    with pytest.raises(RuntimeError, match="heap is full"):
-        _run(S.SplitStore(splits), gpu, cap_mb=1.0)
+    got, eng = _run(S.SplitStore(splits, pin=on_gpu), dev, cap_mb=1.0)
+    assert got == _want(splits)
+    assert eng._stream_heap_mb > 0.07
