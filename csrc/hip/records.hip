@@ -1,0 +1,254 @@
+// records.hip — the record plane's kernels for rows of any width (gfx950):
+// fixed-width records moved, not folded (device_reduce = "identity";
+// parallel/planes.py RecordPlane), keyed by their first `kb` bytes (kb <= 16,
+// unsigned bytewise order = the reference's string key order, utils.lua:126).
+// TeraSort's 100-byte rows with 10-byte keys are one shape of it.
+//
+// The sort is a 32-bit radix sort of the key prefixes plus an exact fix-up:
+//   rec_keys32   : k32 = key bytes 0..3 big-endian, and the radix sort's digit
+//                  histograms of k32 in the same pass (no histogram pass);
+//   (sort.hip)   : 4 onesweep passes over (k32, u32 row) — u32 keys: 16 bytes
+//                  moved per row and pass instead of 24 with u64 keys;
+//   rec_tie_fixup: rows equal in k32 ordered by key bytes 4..kb-1 read from the
+//                  rows themselves (uniform keys: ~2 % of the rows sit in such
+//                  a run, almost all of length 2); a run longer than 64 sets
+//                  *bad and the caller sorts the full (hi, lo) key instead;
+//   rec_gather   : output row i = input row perm[i], 8 independent words per
+//                  thread in flight (the random 100-byte row reads touch 1.77
+//                  128-byte lines each on average: this is the bound).
+//   rec_keys     : full (hi, lo) key words (fallback sort, sampling, checks);
+//   rec_dest32   : range partition = number of splitters <= k32.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "mr_common.h"
+
+namespace mr {
+namespace rc {
+
+// Big-endian u32 of bytes [b, b+4) of a row, bytes at or past kb read as 0.
+__device__ __forceinline__ u32 be32(const u8* row, int b, int kb, bool words) {
+  if (words && b + 4 <= kb) return __builtin_bswap32(*reinterpret_cast<const u32*>(row + b));
+  u32 v = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v = (v << 8) | (b + j < kb ? (u32)row[b + j] : 0u);
+  return v;
+}
+
+__device__ __forceinline__ u64 be64(const u8* row, int b, int kb, bool words) {
+  return ((u64)be32(row, b, kb, words) << 32) | (u64)be32(row, b + 4, kb, words);
+}
+
+// k32 of every row (+ digit histograms of k32 into ghist[0..3][256] when
+// ghist is given: zeroed u32 [8][256]).  256 threads, grid-stride.
+__global__ void __launch_bounds__(256) rec_keys32_kernel(const u8* __restrict__ rec, u64 n, int rb, int kb,
+                                                         u32* __restrict__ k32, u32* __restrict__ ghist) {
+  __shared__ u32 h[4][256];
+  const int t = threadIdx.x;
+  if (ghist) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) h[b][t] = 0;
+    __syncthreads();
+  }
+  const bool words = (rb & 3) == 0;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + t; i < n; i += stride) {
+    const u32 k = be32(rec + i * (u64)rb, 0, kb, words);
+    k32[i] = k;
+    if (ghist) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 0xFFu], 1u);
+    }
+  }
+  if (ghist) {
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (h[b][t]) atomicAdd(&ghist[b * 256 + t], h[b][t]);
+  }
+}
+
+__global__ void rec_keys_kernel(const u8* __restrict__ rec, u64 n, int rb, int kb, u64* __restrict__ hi,
+                                u64* __restrict__ lo) {
+  const bool words = (rb & 3) == 0;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u8* row = rec + i * (u64)rb;
+    hi[i] = be64(row, 0, kb, words);
+    lo[i] = be64(row, 8, kb, words);
+  }
+}
+
+// The rest of a key after its 32-bit prefix: bytes 4..15 as (u64, u32).
+__device__ __forceinline__ void key_rest(const u8* row, int kb, bool words, u64& a, u32& b) {
+  a = be64(row, 4, kb, words);
+  b = be32(row, 12, kb, words);
+}
+
+// Runs of equal k32 in the sorted prefixes: insertion sort of the run's rows
+// by the rest of their keys (one thread per run; stable: the LSD sort left
+// equal keys in input order).
+__global__ void rec_tie_fixup_kernel(const u32* __restrict__ sk, u32* __restrict__ perm, const u8* __restrict__ rec,
+                                     u64 n, int rb, int kb, u32* __restrict__ bad) {
+  const bool words = (rb & 3) == 0;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += stride) {
+    const u32 h = sk[i];
+    if (sk[i + 1] != h || (i > 0 && sk[i - 1] == h)) continue;
+    u64 e = i + 2;
+    while (e < n && sk[e] == h && e - i <= 64) ++e;
+    if (e - i > 64) {
+      atomicOr(bad, 1u);
+      continue;
+    }
+    if (kb <= 4) continue;  // the prefix is the whole key
+    u64 ra[64];
+    u32 rb2[64];
+    u32 p[64];
+    const int m = (int)(e - i);
+    for (int a = 0; a < m; ++a) {
+      p[a] = perm[i + a];
+      key_rest(rec + (u64)clamp_row(p[a], n) * rb, kb, words, ra[a], rb2[a]);
+    }
+    for (int a = 1; a < m; ++a) {
+      const u64 ka = ra[a];
+      const u32 kb2 = rb2[a];
+      const u32 pa = p[a];
+      int b = a;
+      while (b > 0 && (ra[b - 1] > ka || (ra[b - 1] == ka && rb2[b - 1] > kb2))) {
+        ra[b] = ra[b - 1];
+        rb2[b] = rb2[b - 1];
+        p[b] = p[b - 1];
+        --b;
+      }
+      ra[b] = ka;
+      rb2[b] = kb2;
+      p[b] = pa;
+    }
+    for (int a = 0; a < m; ++a) perm[i + a] = p[a];
+  }
+}
+
+// Row gather, rows of W words (W > 0: compile-time width; W == 0: `words`
+// at run time), UNROLL independent words per thread: all permutation loads,
+// then all row loads, then all stores (tools/ts_gather_probe.py: 8 in flight).
+template <int W, int UNROLL>
+__global__ void __launch_bounds__(256) rec_gather_kernel(const u32* __restrict__ in, const u32* __restrict__ perm,
+                                                         u64 n, u32 words, u32* __restrict__ out) {
+  const u64 ww = W > 0 ? (u64)W : (u64)words;
+  const u64 nw = n * ww;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 w0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; w0 < nw; w0 += stride * UNROLL) {
+    u64 src[UNROLL];
+    u32 v[UNROLL];
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      const u64 w = w0 + (u64)k * stride;
+      const u64 r = w / ww;
+      const u64 j = w - r * ww;
+      src[k] = w < nw ? (u64)clamp_row(perm[r], n) * ww + j : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      const u64 w = w0 + (u64)k * stride;
+      v[k] = w < nw ? __builtin_nontemporal_load(in + src[k]) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      const u64 w = w0 + (u64)k * stride;
+      if (w < nw) __builtin_nontemporal_store(v[k], out + w);
+    }
+  }
+}
+
+// Rows whose width is not a multiple of 4 bytes: one byte per thread.
+__global__ void rec_gather_bytes_kernel(const u8* __restrict__ in, const u32* __restrict__ perm, u64 n, u64 rb,
+                                        u8* __restrict__ out) {
+  const u64 nb = n * rb;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 b = (u64)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += stride) {
+    const u64 r = b / rb;
+    out[b] = in[(u64)clamp_row(perm[r], n) * rb + (b - r * rb)];
+  }
+}
+
+__global__ void rec_dest32_kernel(const u32* __restrict__ k32, u64 n, const u32* __restrict__ split, u32 nsplit,
+                                  u32* __restrict__ dest) {
+  __shared__ u32 s[1024];
+  for (u32 k = threadIdx.x; k < nsplit; k += blockDim.x) s[k] = split[k];
+  __syncthreads();
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u32 h = k32[i];
+    u32 a = 0, b = nsplit;  // upper bound: first splitter > h
+    while (a < b) {
+      const u32 m = (a + b) >> 1;
+      if (s[m] <= h) a = m + 1;
+      else b = m;
+    }
+    dest[i] = a;
+  }
+}
+
+}  // namespace rc
+}  // namespace mr
+
+using namespace mr;
+
+static inline unsigned rc_grid(u64 n, unsigned cap = 8192) {
+  u64 g = (n + 255) / 256;
+  return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+extern "C" {
+
+// ghist: null, or a zeroed u32[8][256] that receives the digit histograms of k32
+int mr_rec_keys32(const void* rec, u64 n, int rb, int kb, void* k32, void* ghist, hipStream_t s) {
+  if (n == 0) return 0;
+  if (rb <= 0 || kb <= 0 || kb > rb || kb > 16) return -1;
+  hipLaunchKernelGGL(rc::rec_keys32_kernel, dim3(rc_grid(n, ghist ? 2048 : 8192)), dim3(256), 0, s, (const u8*)rec, n,
+                     rb, kb, (u32*)k32, (u32*)ghist);
+  return (int)hipGetLastError();
+}
+
+int mr_rec_keys(const void* rec, u64 n, int rb, int kb, void* hi, void* lo, hipStream_t s) {
+  if (n == 0) return 0;
+  if (rb <= 0 || kb <= 0 || kb > rb || kb > 16) return -1;
+  hipLaunchKernelGGL(rc::rec_keys_kernel, dim3(rc_grid(n)), dim3(256), 0, s, (const u8*)rec, n, rb, kb, (u64*)hi,
+                     (u64*)lo);
+  return (int)hipGetLastError();
+}
+
+int mr_rec_tie_fixup(const void* sk, void* perm, const void* rec, u64 n, int rb, int kb, void* bad, hipStream_t s) {
+  if (n < 2) return 0;
+  hipLaunchKernelGGL(rc::rec_tie_fixup_kernel, dim3(rc_grid(n)), dim3(256), 0, s, (const u32*)sk, (u32*)perm,
+                     (const u8*)rec, n, rb, kb, (u32*)bad);
+  return (int)hipGetLastError();
+}
+
+int mr_rec_gather(const void* in, const void* perm, u64 n, int rb, void* out, hipStream_t s) {
+  if (n == 0) return 0;
+  if (rb & 3) {
+    hipLaunchKernelGGL(rc::rec_gather_bytes_kernel, dim3(rc_grid(n * (u64)rb, 16384)), dim3(256), 0, s,
+                       (const u8*)in, (const u32*)perm, n, (u64)rb, (u8*)out);
+    return (int)hipGetLastError();
+  }
+  const u32 words = (u32)(rb >> 2);
+  const unsigned g = rc_grid(n * words, 16384);
+  if (words == 25)
+    hipLaunchKernelGGL((rc::rec_gather_kernel<25, 8>), dim3(g), dim3(256), 0, s, (const u32*)in, (const u32*)perm, n,
+                       words, (u32*)out);
+  else
+    hipLaunchKernelGGL((rc::rec_gather_kernel<0, 8>), dim3(g), dim3(256), 0, s, (const u32*)in, (const u32*)perm, n,
+                       words, (u32*)out);
+  return (int)hipGetLastError();
+}
+
+int mr_rec_dest32(const void* k32, u64 n, const void* split, u32 nsplit, void* dest, hipStream_t s) {
+  if (n == 0) return 0;
+  if (nsplit > 1024) return -1;
+  hipLaunchKernelGGL(rc::rec_dest32_kernel, dim3(rc_grid(n)), dim3(256), 0, s, (const u32*)k32, n, (const u32*)split,
+                     nsplit, (u32*)dest);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

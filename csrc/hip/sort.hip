@@ -121,8 +121,10 @@ __device__ __forceinline__ u32 block_scan_256(u32 v, u32* tmp) {
 // tiles) below ONESWEEP_SMALL keys, where a pass is one tile's latency and
 // 4096-key tiles left most CUs idle (54k keys = 14 tiles); 16 or more above.
 constexpr u64 ONESWEEP_SMALL = 1ull << 18;
-template <typename V, int ROUNDS>
-__global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys_in, const V* vals_in, u64* keys_out,
+// K: u64 keys, or u32 keys (TeraSort's 32-bit key prefixes: a third less
+// traffic per pass than u64 keys with u32 values).
+template <typename K, typename V, int ROUNDS>
+__global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const K* keys_in, const V* vals_in, K* keys_out,
                                                                  V* vals_out, u64 n, int shift, const u32* ghist,
                                                                  u64* granules, u32* tile_counter, u32 epoch,
                                                                  u32* err, int iota, int debug_fail) {
@@ -137,7 +139,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
   // placed in an LDS image of the tile in digit order and streamed out so
   // consecutive lanes write consecutive addresses of one digit run.
   constexpr int SUB = RS_TILE / RS_WAVES;  // keys per wave
-  __shared__ u64 sk[RS_TILE];
+  __shared__ K sk[RS_TILE];
   __shared__ V sv[RS_TILE];
   __shared__ u32 wc[RS_WAVES][RS_BINS];
   __shared__ u32 gout[RS_BINS];
@@ -175,7 +177,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
   const bool has_v = vals_in != nullptr || iota;
   // this wave's keys: tile[wave*SUB + r*64 + lane]
   const u64 w0 = t0 + (u64)wave * SUB;
-  u64 kr[RS_ROUNDS];
+  K kr[RS_ROUNDS];
   V vr[RS_ROUNDS];
 #pragma unroll
   for (int r = 0; r < RS_ROUNDS; ++r) {
@@ -267,7 +269,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const u64* keys
   __syncthreads();
   const u32 cnt = (u32)min((u64)RS_TILE, n - t0);
   for (u32 i = t; i < cnt; i += RS_THREADS) {
-    const u64 k = sk[i];
+    const K k = sk[i];
     const u32 pos = gout[(k >> shift) & 0xFF] + i;
     keys_out[pos] = k;
     if (has_v) vals_out[pos] = sv[i];
@@ -598,14 +600,19 @@ static int scan_impl(const T* in, T* out, u64 n, T* partials, T* total, hipStrea
   return (int)hipGetLastError();
 }
 
-template <int ROUNDS>
+template <typename K, int ROUNDS>
 static void onesweep_launch(u32 nt, const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n,
                             int shift, const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err,
                             int iota, int debug_fail, hipStream_t s) {
-  hipLaunchKernelGGL((rs_onesweep_kernel<u32, ROUNDS>), dim3(nt), dim3(RS_THREADS), 0, s, (const u64*)keys_in,
-                     (const u32*)vals_in, (u64*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
+  hipLaunchKernelGGL((rs_onesweep_kernel<K, u32, ROUNDS>), dim3(nt), dim3(RS_THREADS), 0, s, (const K*)keys_in,
+                     (const u32*)vals_in, (K*)keys_out, (u32*)vals_out, n, shift, (const u32*)ghist,
                      (u64*)granules, (u32*)tile_counter, epoch, (u32*)err, iota, debug_fail);
 }
+
+template <typename K>
+static int onesweep_pass(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
+                         const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
+                         int debug_fail, hipStream_t s);
 
 extern "C" {
 
@@ -674,27 +681,52 @@ u64 mr_onesweep_tiles(u64 n) {
   return (n + tile - 1) / tile;
 }
 
-int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
-                           const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
-                           hipStream_t s) {
-  int debug_fail = 0;
-  if (g_onesweep_debug_fail > 0 && mr_onesweep_tiles(n) > 1) {
-    debug_fail = 1;
-    --g_onesweep_debug_fail;
-  }
+}  // extern "C"
+
+template <typename K>
+static int onesweep_pass(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
+                         const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
+                         int debug_fail, hipStream_t s) {
   if (n == 0) return 0;
   const u32 nt = (u32)mr_onesweep_tiles(n);
   switch (onesweep_rounds(n)) {
-    case 4: onesweep_launch<4>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
-                               epoch, err, iota, debug_fail, s); break;
-    case 24: onesweep_launch<24>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
-                                 epoch, err, iota, debug_fail, s); break;
-    case 32: onesweep_launch<32>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
-                                 epoch, err, iota, debug_fail, s); break;
-    default: onesweep_launch<RS_ROUNDS>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules,
-                                        tile_counter, epoch, err, iota, debug_fail, s);
+    case 4: onesweep_launch<K, 4>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
+                                  epoch, err, iota, debug_fail, s); break;
+    case 24: onesweep_launch<K, 24>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules,
+                                    tile_counter, epoch, err, iota, debug_fail, s); break;
+    case 32: onesweep_launch<K, 32>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules,
+                                    tile_counter, epoch, err, iota, debug_fail, s); break;
+    default: onesweep_launch<K, RS_ROUNDS>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules,
+                                           tile_counter, epoch, err, iota, debug_fail, s);
   }
   return (int)hipGetLastError();
+}
+
+static int take_debug_fail(u64 n) {
+  if (g_onesweep_debug_fail > 0 && mr_onesweep_tiles(n) > 1) {
+    --g_onesweep_debug_fail;
+    return 1;
+  }
+  return 0;
+}
+
+extern "C" {
+
+int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
+                           const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
+                           hipStream_t s) {
+  const int debug_fail = take_debug_fail(n);
+  return onesweep_pass<u64>(keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter, epoch, err,
+                            iota, debug_fail, s);
+}
+
+// The same pass over u32 keys (shift 0..24).
+int mr_radix_onesweep_k32(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
+                          const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
+                          hipStream_t s) {
+  const int debug_fail = take_debug_fail(n);
+  return onesweep_pass<u32>(keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter, epoch, err,
+                            iota, debug_fail, s);
 }
 
 int mr_gather_u64(const void* src, const void* idx, void* dst, u64 n, hipStream_t s) {

@@ -96,6 +96,12 @@ _SIGS = {
     "mr_table_reset": [_p, _p, _p, _p, _u64, ctypes.c_longlong, _p],
     "mr_table_rehome": [_p, _p, _p, _u64, _p, _u64, _u64, _p, _u64, _p],
     "mr_scan_partials_len": [_u64],
+    "mr_radix_onesweep_k32": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p, _u32, _p, _i32, _p],
+    "mr_rec_keys32": [_p, _u64, _i32, _i32, _p, _p, _p],
+    "mr_rec_keys": [_p, _u64, _i32, _i32, _p, _p, _p],
+    "mr_rec_tie_fixup": [_p, _p, _p, _u64, _i32, _i32, _p, _p],
+    "mr_rec_gather": [_p, _p, _u64, _i32, _p, _p],
+    "mr_rec_dest32": [_p, _u64, _p, _u32, _p, _p],
     "mr_agg_insert": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _u64, _p, _p],
     "mr_slot_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
     "mr_col_fill": [_p, _u64, ctypes.c_longlong, _i32, _p],

@@ -641,6 +641,42 @@ def sort_keys(words: list[torch.Tensor], bits: list[int] | None = None,
     return (perm, words[0][perm]) if return_keys else perm
 
 
+def sort_keys32(k32: torch.Tensor, ghist: torch.Tensor | None = None, bits: int = 32):
+    """(permutation int32, sorted keys) of unsigned 32-bit keys (an int32
+    tensor of bit patterns), stable.  GPU: one onesweep pass over u32 keys
+    per 8-bit digit below ``bits`` (csrc/hip/sort.hip mr_radix_onesweep_k32);
+    ``ghist``: the keys' digit histograms in the [8][256] layout (digit b at
+    256 b), e.g. from records.keys32 — required on the GPU."""
+    n = k32.numel()
+    if not k32.is_cuda:
+        u = k32.numpy().view(np.uint32).astype(np.uint64)
+        if bits < 32:
+            u &= np.uint64((1 << bits) - 1)
+        perm = np.argsort(u, kind="stable").astype(np.int64)
+        return torch.from_numpy(perm), k32[torch.from_numpy(perm)]
+    d = k32.device
+    if n == 0:
+        return torch.zeros(0, dtype=torch.int32, device=d), k32[:0]
+    if ghist is None:
+        raise ValueError("sort_keys32 on the GPU needs the digit histograms (records.keys32 computes them)")
+    s = _hip.stream(d)
+    ws = _sort_ws(d, n)
+    small = ws["small"]
+    small[2048:].zero_()  # tile counters + error flag (the histograms are the caller's)
+    kbuf = [torch.empty(n, dtype=torch.int32, device=d) for _ in range(2)]
+    pbuf = [torch.empty(n, dtype=torch.int32, device=d) for _ in range(2)]
+    kin, pin = k32.contiguous(), None
+    for pass_id, shift in enumerate(range(0, bits, 8)):
+        _EPOCH[0] = (_EPOCH[0] + 1) & 0xFFFFFF or 1
+        kout = kbuf[0] if kin is not kbuf[0] else kbuf[1]
+        pout = pbuf[0] if pin is not pbuf[0] else pbuf[1]
+        _hip.call("mr_radix_onesweep_k32", _hip.ptr(kin), _hip.ptr(pin), _hip.ptr(kout), _hip.ptr(pout), n, shift,
+                  _hip.ptr(ghist[shift // 8 * 256:]), _hip.ptr(ws["granules"]), _hip.ptr(small[2048 + pass_id:]),
+                  _EPOCH[0], _hip.ptr(small[2112:]), 1 if pin is None else 0, s)
+        kin, pin = kout, pout
+    return pin, kin
+
+
 def sort_by_partition_key(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, val: torch.Tensor,
                           rep: torch.Tensor, nparts: int, src: torch.Tensor | None = None):
     """Rows ordered by (partition, key) -> (part, hi, lo, val, rep, bad).

@@ -1,0 +1,130 @@
+"""Fixed-width record primitives of the record plane (HIP kernels in
+``csrc/hip/records.hip``; NumPy on CPU tensors — the executable
+specification).  Rows are uint8 ``[n, rb]`` tensors keyed by their first
+``kb`` bytes (1 <= kb <= 16, kb <= rb), ordered bytewise (unsigned,
+big-endian) — TeraSort's 100-byte rows with 10-byte keys are one shape.
+
+The sort is a radix sort of the 32-bit key prefixes (4 passes over u32 keys
+and u32 row numbers) whose ties are ordered by the rest of the key read from
+the rows; skewed keys (runs of more than 64 equal prefixes) fall back to a
+sort of the full (hi, lo) key words.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _hip
+
+
+def _check(rec: torch.Tensor, kb: int) -> tuple[int, int]:
+    if rec.dim() != 2 or rec.dtype != torch.uint8:
+        raise ValueError("records are a uint8 [n, row_bytes] tensor")
+    rb = int(rec.shape[1])
+    if not (1 <= kb <= 16 and kb <= rb):
+        raise ValueError(f"key bytes must be 1..16 and at most the row width (got {kb} of {rb})")
+    return int(rec.shape[0]), rb
+
+
+def _host_keys(a: np.ndarray, kb: int) -> tuple[np.ndarray, np.ndarray]:
+    n = a.shape[0]
+    k = np.zeros((n, 16), np.uint8)
+    k[:, :kb] = a[:, :kb]
+    hi = np.ascontiguousarray(k[:, 0:8]).view(">u8").reshape(n).astype(np.uint64)
+    lo = np.ascontiguousarray(k[:, 8:16]).view(">u8").reshape(n).astype(np.uint64)
+    return hi, lo
+
+
+def keys32(rec: torch.Tensor, kb: int, ghist: torch.Tensor | None = None) -> torch.Tensor:
+    """Key bytes 0..3 big-endian (zero-padded) as the bit patterns of an
+    int32 tensor.  ``ghist`` (GPU: a zeroed int32 [2048]) also receives their
+    radix digit histograms ([8][256] layout, digits 0..3)."""
+    n, rb = _check(rec, kb)
+    if rec.is_cuda:
+        out = torch.empty(n, dtype=torch.int32, device=rec.device)
+        _hip.call("mr_rec_keys32", _hip.ptr(rec), n, rb, kb, _hip.ptr(out), _hip.ptr(ghist), _hip.stream(rec.device))
+        return out
+    hi, _ = _host_keys(rec.numpy(), kb)
+    return torch.from_numpy((hi >> np.uint64(32)).astype(np.uint32).view(np.int32))
+
+
+def keys(rec: torch.Tensor, kb: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """(hi, lo) int64 key words: key bytes 0..7 and 8..15 big-endian, zero-padded."""
+    n, rb = _check(rec, kb)
+    if rec.is_cuda:
+        hi = torch.empty(n, dtype=torch.int64, device=rec.device)
+        lo = torch.empty(n, dtype=torch.int64, device=rec.device)
+        _hip.call("mr_rec_keys", _hip.ptr(rec), n, rb, kb, _hip.ptr(hi), _hip.ptr(lo), _hip.stream(rec.device))
+        return hi, lo
+    hi, lo = _host_keys(rec.numpy(), kb)
+    return torch.from_numpy(hi.view(np.int64)), torch.from_numpy(lo.view(np.int64))
+
+
+def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: torch.Tensor | None = None):
+    """(permutation int32 (int64 on CPU), sorted 32-bit key prefixes) of the
+    rows in key order (stable).  GPU: pass ``k32``/``ghist`` from
+    :func:`keys32` to skip recomputing them."""
+    from .primitives import sort_error, sort_keys32, sort_keys_checked
+    n, rb = _check(rec, kb)
+    if not rec.is_cuda:
+        hi, lo = keys(rec, kb)
+        from .primitives import sort_keys
+        perm = sort_keys([hi, lo], bits=[64, 64])
+        return perm, keys32(rec, kb)[perm]
+    d = rec.device
+    if k32 is None or ghist is None:
+        ghist = torch.zeros(2048, dtype=torch.int32, device=d)
+        k32 = keys32(rec, kb, ghist)
+    perm, sk = sort_keys32(k32, ghist)
+    bad = torch.zeros(1, dtype=torch.int32, device=d)
+    _hip.call("mr_rec_tie_fixup", _hip.ptr(sk), _hip.ptr(perm), _hip.ptr(rec), n, rb, kb, _hip.ptr(bad),
+              _hip.stream(d))
+    if int(bad.item()) or sort_error(d):
+        # skewed keys (a prefix shared by more than 64 rows), or a given-up
+        # look-back: sort the full key words
+        hi, lo = keys(rec, kb)
+        perm = sort_keys_checked([hi, lo], bits=[64, 64])
+        sk = k32[perm.long()]
+    return perm, sk
+
+
+def gather(rec: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
+    """rec[perm] (rows)."""
+    n = perm.numel()
+    rb = int(rec.shape[1])
+    if rec.is_cuda:
+        out = torch.empty((n, rb), dtype=torch.uint8, device=rec.device)
+        p = perm if perm.dtype == torch.int32 else perm.to(torch.int32)
+        _hip.call("mr_rec_gather", _hip.ptr(rec), _hip.ptr(p.contiguous()), n, rb, _hip.ptr(out),
+                  _hip.stream(rec.device))
+        return out
+    return rec[perm.long()]
+
+
+def dest32(k32: torch.Tensor, splitters: torch.Tensor) -> torch.Tensor:
+    """Range partition: number of splitters <= the 32-bit key prefix (int32;
+    splitters: sorted unsigned 32-bit values as int32 bit patterns)."""
+    n = k32.numel()
+    if k32.is_cuda:
+        out = torch.empty(n, dtype=torch.int32, device=k32.device)
+        sp = splitters.to(device=k32.device, dtype=torch.int32).contiguous()
+        _hip.call("mr_rec_dest32", _hip.ptr(k32), n, _hip.ptr(sp), sp.numel(), _hip.ptr(out),
+                  _hip.stream(k32.device))
+        return out
+    h = k32.numpy().view(np.uint32)
+    s = splitters.numpy().astype(np.int32).view(np.uint32)
+    return torch.from_numpy(np.searchsorted(s, h, side="right").astype(np.int32))
+
+
+def unsorted_pairs(rec: torch.Tensor, kb: int) -> int:
+    """Adjacent rows out of key order (0 for a sorted block)."""
+    hi, lo = keys(rec, kb)
+    if hi.numel() < 2:
+        return 0
+    if rec.is_cuda:
+        sign = -(1 << 63)
+        a, b = hi ^ sign, lo ^ sign
+        bad = (a[:-1] > a[1:]) | ((a[:-1] == a[1:]) & (b[:-1] > b[1:]))
+        return int(bad.sum())
+    h, lw = hi.numpy().view(np.uint64), lo.numpy().view(np.uint64)
+    return int(np.count_nonzero((h[:-1] > h[1:]) | ((h[:-1] == h[1:]) & (lw[:-1] > lw[1:]))))

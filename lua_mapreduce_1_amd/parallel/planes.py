@@ -17,10 +17,11 @@ BASELINE workloads as MapReduce jobs:
   result file.  At W > 1 the destination rank rides in the posting's top bits
   and the shuffle is three ``all_to_all_single`` (words, key bytes, values).
 * :class:`RecordPlane` (``device_reduce = "identity"``): fixed-width records
-  (100-byte TeraSort rows, 10-byte keys) are moved, not folded — identity
-  map, range partitioner with sampled splitters (``device_partition =
-  ("range", R, None)``, TeraSort's total-order partitioner), identity reduce
-  = a per-rank radix sort of the received rows (csrc/hip/terasort.hip).
+  of any width keyed by up to 16 leading bytes (e.g. 100-byte TeraSort rows,
+  10-byte keys) are moved, not folded — identity map, range partitioner with
+  sampled splitters (``device_partition = ("range", R, None)``, TeraSort's
+  total-order partitioner), identity reduce = a per-rank radix sort of the
+  received rows (csrc/hip/records.hip).
 
 Results stay in HBM (they can be ~the size of the input); ``partitions`` /
 ``gather_results`` copy them to host memory on first use.
@@ -459,8 +460,10 @@ class RecordStore:
 
 
 class RecordEmitter:
-    """``emit`` of a record-plane map: ``emit.records(rec)`` emits every row
-    of a uint8 [n, 100] tensor (key = its first 10 bytes)."""
+    """``emit`` of a record-plane map: ``emit.records(rec, key_bytes)`` emits
+    every row of a uint8 ``[n, row_bytes]`` tensor, keyed by its first
+    ``key_bytes`` bytes (1..16; TeraSort: 100-byte rows, 10-byte keys).  Every
+    emit of a job uses one shape."""
 
     def __init__(self, plane):
         self.plane = plane
@@ -470,27 +473,51 @@ class RecordEmitter:
         return self.plane.eng.device
 
     def records(self, rec: torch.Tensor, key_bytes: int = TS.KEY) -> None:
-        if rec.dim() != 2 or rec.shape[1] != TS.REC or key_bytes != TS.KEY:
-            raise ValueError(f"the record plane moves {TS.REC}-byte rows with {TS.KEY}-byte keys "
-                             f"(got {tuple(rec.shape)}, key {key_bytes})")
-        if rec.device != self.plane.eng.device:
-            rec = rec.to(self.plane.eng.device, non_blocking=True)
-        self.plane._out.append(rec)
+        pl = self.plane
+        if rec.dim() != 2 or rec.dtype != torch.uint8:
+            raise ValueError("emit.records takes a uint8 [n, row_bytes] tensor")
+        shape = (int(rec.shape[1]), int(key_bytes))
+        if not (1 <= shape[1] <= 16 and shape[1] <= shape[0]):
+            raise ValueError(f"key_bytes must be 1..16 and at most the row width (got {shape[1]} of {shape[0]})")
+        if pl.shape is None:
+            pl.shape = shape
+        elif pl.shape != shape:
+            raise ValueError(f"records of one job share a shape: {pl.shape} (row, key bytes) vs {shape}")
+        if rec.device != pl.eng.device:
+            rec = rec.to(pl.eng.device, non_blocking=True)
+        pl._out.append(rec)
+
+
+def _bits32(x) -> int:
+    """A splitter as a 32-bit key prefix: an int < 2^32, or the first 4 key bytes."""
+    if isinstance(x, (bytes, bytearray)):
+        return int.from_bytes(bytes(x[:4]).ljust(4, b"\0"), "big")
+    x = int(x)
+    if not 0 <= x < 1 << 32:
+        raise ValueError("range splitters are 32-bit key prefixes (ints < 2^32) or key bytes")
+    return x
 
 
 class RecordPlane:
-    """``device_reduce = "identity"`` (see module docstring)."""
+    """``device_reduce = "identity"`` (see module docstring): rows of any
+    width, range-partitioned by their 32-bit key prefix (splitters sampled
+    from every rank's keys, or given), sorted by key on the receiving rank
+    (ops/records.py: 32-bit radix sort + exact tie fix-up + row gather)."""
 
     def __init__(self, eng):
         self.eng = eng
         spec = modules.field(eng.partmod, "device_partition")
         if not spec or spec[0] != "range":
             raise ValueError("the record plane needs device_partition = ('range', R, splitters or None)")
-        self.splitters = None if len(spec) < 3 or spec[2] is None else torch.as_tensor(spec[2], dtype=torch.int64)
+        self.splitters = None
+        if len(spec) > 2 and spec[2] is not None:
+            sp = sorted(_bits32(x) for x in spec[2])
+            self.splitters = torch.tensor(np.array(sp, dtype=np.uint32).view(np.int32))
         self.oversample = int(eng.params.get("oversample") or 1024)
         self.seed = int(eng.params.get("sample_seed") or 0x7E5A)
         self.emitter = RecordEmitter(self)
         self._out: list = []
+        self.shape = None  # (row bytes, key bytes) of the emitted records
 
     def _map(self, jobs, recs, j0, j1) -> torch.Tensor:
         eng = self.eng
@@ -511,32 +538,38 @@ class RecordPlane:
                     recs[j].repetitions += 1
                     recs[j].status = STATUS.BROKEN if attempt < 2 else STATUS.FAILED
             _mark_written(recs, j, j + 1, t0, time.time(), c0)
+        if self.shape is None:  # nothing emitted on this rank: agree on the shape with the others
+            shapes = D.all_gather_object(None, eng.group) if D.initialized() and eng.world > 1 else []
+            self.shape = next((x for x in shapes if x is not None), (TS.REC, TS.KEY))
+        elif D.initialized() and eng.world > 1:
+            D.all_gather_object(self.shape, eng.group)
         if not self._out:
-            return torch.zeros((0, TS.REC), dtype=torch.uint8, device=eng.device)
+            return torch.zeros((0, self.shape[0]), dtype=torch.uint8, device=eng.device)
         return self._out[0] if len(self._out) == 1 else torch.cat(self._out)
 
-    def _sample_splitters(self, hi: torch.Tensor, R: int) -> torch.Tensor:
-        """R-1 unsigned splitters (int64 bit patterns) from a sample of every
-        rank's keys (TeraSort's sampled total-order partitioner)."""
+    def _sample_splitters(self, k32: torch.Tensor, R: int) -> torch.Tensor:
+        """R-1 splitters (32-bit key prefixes, unsigned, as int32 bit
+        patterns) from a sample of every rank's keys (TeraSort's sampled
+        total-order partitioner)."""
         eng = self.eng
-        k = min(self.oversample * R, max(1, hi.numel()))
+        # the same sample size on every rank (all_gather), drawn with
+        # replacement; a rank without rows contributes -1s, dropped below
+        k = self.oversample * R
         g = torch.Generator().manual_seed(self.seed * 7919 + eng.rank)
-        idx = torch.randint(0, max(1, hi.numel()), (k,), generator=g).to(hi.device)
-        samp = hi[idx] if hi.numel() else torch.zeros(k, dtype=torch.int64, device=hi.device)
+        idx = torch.randint(0, max(1, k32.numel()), (k,), generator=g).to(k32.device)
+        samp = (k32[idx].to(torch.int64) & 0xFFFFFFFF) if k32.numel() else torch.full((k,), -1, dtype=torch.int64,
+                                                                                    device=k32.device)
         allv = D.all_gather_tensor(samp, eng.group) if D.initialized() else samp
-        sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=allv.device)
-        srt = torch.sort(allv ^ sign).values ^ sign  # unsigned order of the bit patterns
+        allv = allv[allv >= 0]
+        if allv.numel() == 0:
+            allv = torch.zeros(1, dtype=torch.int64, device=k32.device)
+        srt = torch.sort(allv).values  # non-negative: unsigned order
         m = srt.numel()
         pick = torch.tensor([(m * j) // R for j in range(1, R)], dtype=torch.int64, device=srt.device)
-        return srt[pick].contiguous()
-
-    def _sort_perm(self, hi, lo, ghist=None):
-        perm = TS.sort_perm(hi, lo, ghist)
-        if hi.is_cuda and ops.sort_error(hi.device):
-            perm = ops.sort_keys_checked([hi, lo], bits=[64, 16])
-        return perm
+        return srt[pick].to(torch.int32).contiguous()
 
     def run_iteration(self, prefetch_next, lookahead):
+        from ..ops import records as RC
         eng = self.eng
         eng.iteration += 1
         eng._seq += 1
@@ -548,27 +581,30 @@ class RecordPlane:
         t0 = time.time()
         recs = _records(eng, jobs, j0, j1, t0)
         res.map_jobs = recs
+        self.shape = None
         with trace.range("mr.rec.map"):
             rec = self._map(jobs, recs, j0, j1)
+        kb = self.shape[1]
         T["map"] = time.time() - t0
         t1 = time.time()
         R, W = eng.nparts, eng.world
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
-        hi = None
+        k32 = None
         sp = self.splitters
         if R > 1 and sp is None:
-            hi, _ = TS.keys(rec)
-            sp = self._sample_splitters(hi, R)
+            k32 = RC.keys32(rec, kb)
+            sp = self._sample_splitters(k32, R)
         elif sp is not None:
             sp = sp.to(eng.device)
         if W > 1 or eng.force_shuffle:
             with trace.range("mr.rec.shuffle"):
-                if hi is None:
-                    hi, _ = TS.keys(rec)
-                part = TS.dest_of(hi, sp) if R > 1 else torch.zeros(hi.numel(), dtype=torch.int32, device=hi.device)
+                if k32 is None:
+                    k32 = RC.keys32(rec, kb)
+                part = RC.dest32(k32, sp) if R > 1 else torch.zeros(k32.numel(), dtype=torch.int32,
+                                                                     device=k32.device)
                 dest = (part.to(torch.int64) % W).to(torch.int32)
                 perm = ops.sort_keys_checked([dest.to(torch.int64)], bits=[max(8, _bits(W))])
-                packed = TS.gather(rec, perm)
+                packed = RC.gather(rec, perm)
                 counts = ops.bincount(dest, W)
                 # per destination: (rows, this rank's failed maps)
                 xchg = torch.stack([counts, torch.full((W,), failed, dtype=torch.int64, device=counts.device)],
@@ -583,17 +619,16 @@ class RecordPlane:
         with trace.range("mr.rec.sort"):
             # the sort's digit histograms come out of the key extraction
             gh = torch.zeros(2048, dtype=torch.int32, device=rec.device) if rec.is_cuda else None
-            hi, lo = TS.keys(rec, gh)
-            perm = self._sort_perm(hi, lo, gh)
-            out = TS.gather(rec, perm)
+            k32 = RC.keys32(rec, kb, gh)
+            perm, sk = RC.sort(rec, kb, k32, gh)
+            out = RC.gather(rec, perm)
             if R > 1:
-                shi = hi[perm.long()]
-                pcount = ops.bincount(TS.dest_of(shi, sp), R)
+                pcount = ops.bincount(RC.dest32(sk, sp), R)
             else:
                 pcount = torch.tensor([out.shape[0]], dtype=torch.int64)
         counts = pcount.cpu().tolist()
         _result_jobs(eng, res, counts, t1)
-        res.device = {"records": out, "counts_host": counts, "splitters": sp}
+        res.device = {"records": out, "counts_host": counts, "splitters": sp, "key_bytes": kb}
         res.distinct_keys = int(out.shape[0])
         res.total_value = int(out.shape[0])
         res.failed_maps = failed
@@ -607,5 +642,5 @@ def _record_host(out: dict, R: int) -> dict[int, dict]:
     rec = out["records"].cpu().numpy()
     bounds = np.zeros(R + 1, np.int64)
     np.cumsum(out["counts_host"], out=bounds[1:])
-    return {p: {"records": rec[int(bounds[p]):int(bounds[p + 1])], "key_bytes": TS.KEY}
+    return {p: {"records": rec[int(bounds[p]):int(bounds[p + 1])], "key_bytes": out.get("key_bytes", TS.KEY)}
             for p in range(R) if bounds[p + 1] > bounds[p]}

@@ -1,0 +1,134 @@
+"""The record plane for rows of any width (record widths as
+parameters): 64-byte rows with 16-byte keys, 37-byte rows (not a multiple of
+4) with 5-byte keys, TeraSort's 100/10, and skewed keys (the full-key
+fallback of the 32-bit prefix sort) — W = 1, forced shuffle and gloo W = 3 on
+CPU; the GPU kernels against the CPU specification in test_records_gpu."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+M = "rec_modules"
+SHAPES = [dict(rb=64, kb=16), dict(rb=37, kb=5), dict(rb=100, kb=10), dict(rb=24, kb=3, skew=True)]
+IDS = ["64x16", "37x5", "100x10", "24x3-skew"]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def expected(args):
+    import importlib
+    mod = importlib.import_module(M)
+    mod.init(dict(args, rows=args.get("rows", 10000)))
+    rows = np.concatenate([mod.block_rows(b) for b in range(mod.BLOCKS)])
+    return rows, mod.KB
+
+
+def check(got_rows: np.ndarray, args) -> bool:
+    rows, kb = expected(args)
+    if got_rows.shape != rows.shape:
+        return False
+    keys = [bytes(r[:kb]) for r in got_rows]
+    if keys != sorted(keys):
+        return False
+    a = np.sort(rows.view(np.dtype((np.void, rows.shape[1]))).ravel())
+    b = np.sort(got_rows.view(np.dtype((np.void, rows.shape[1]))).ravel())
+    return bool(np.array_equal(a, b))
+
+
+def run_engine(args, device, **params):
+    from lua_mapreduce_1_amd import spmd
+    eng = spmd(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, init_args=dict(args), **params), device=device)
+    res = eng.run_iteration()
+    parts = eng.gather_results(res)
+    rows = np.concatenate([c["records"] for _n, c in parts]) if parts else None
+    return eng, res, rows
+
+
+@pytest.mark.parametrize("args", SHAPES, ids=IDS)
+def test_records_any_width_cpu(args):
+    eng, res, rows = run_engine(args, torch.device("cpu"))
+    assert eng.plane_kind == "records" and check(rows, args)
+    assert len(res.result_names) == (4 if not args.get("skew") else len(res.result_names))
+
+
+def test_records_shape_must_agree():
+    from lua_mapreduce_1_amd.parallel.planes import RecordEmitter
+
+    class P:
+        shape = None
+        _out: list = []
+
+        class eng:
+            device = torch.device("cpu")
+    e = RecordEmitter(P)
+    e.records(torch.zeros((3, 8), dtype=torch.uint8), 4)
+    with pytest.raises(ValueError):
+        e.records(torch.zeros((3, 9), dtype=torch.uint8), 4)
+    with pytest.raises(ValueError):
+        RecordEmitter(type("Q", (), {"shape": None, "_out": [], "eng": P.eng})).records(
+            torch.zeros((3, 8), dtype=torch.uint8), 9)
+
+
+def _rank(rank, world, port, q, args, force_shuffle):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import datetime
+    import torch.distributed as dist
+    from lua_mapreduce_1_amd.parallel import dist as D
+    if force_shuffle:
+        dist.init_process_group("gloo", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}",
+                                timeout=datetime.timedelta(seconds=120))
+    else:
+        D.init_from_env(backend="gloo", use_gpu=False)
+    _eng, _res, rows = run_engine(args, torch.device("cpu"), force_shuffle=force_shuffle)
+    if rank == 0:
+        q.put(check(rows, args))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,force", [(3, False), (1, True)], ids=["gloo3", "forced1"])
+@pytest.mark.parametrize("args", [SHAPES[1], SHAPES[3]], ids=["37x5", "24x3-skew"])
+def test_records_multi_rank_cpu(args, world, force):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, args, force)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5)
+
+
+# -- GPU kernels vs the CPU specification ---------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", SHAPES, ids=IDS)
+def test_records_any_width_gpu(gpu, args):
+    from lua_mapreduce_1_amd.ops import records as RC
+    rows, kb = expected(dict(args, rows=300_000))
+    h = torch.from_numpy(rows)
+    d = h.to(gpu)
+    assert torch.equal(RC.keys32(d, kb).cpu(), RC.keys32(h, kb))
+    hh, hl = RC.keys(h, kb)
+    dh, dl = RC.keys(d, kb)
+    assert torch.equal(dh.cpu(), hh) and torch.equal(dl.cpu(), hl)
+    perm, _ = RC.sort(d, kb)
+    out = RC.gather(d, perm).cpu().numpy()
+    assert check(out, dict(args, rows=300_000))
+    ref = torch.from_numpy(np.lexsort((hl.numpy().view(np.uint64), hh.numpy().view(np.uint64))))
+    assert torch.equal(RC.gather(d, ref.to(gpu)).cpu(), h[ref])  # the gather itself
+    eng, res, got = run_engine(dict(args, rows=200_000), gpu)
+    assert check(got, dict(args, rows=200_000))

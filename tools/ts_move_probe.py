@@ -18,6 +18,8 @@ if not os.path.exists(SO):
 L = ctypes.CDLL(SO)
 for f in ("probe_copy",):
     getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+L.probe_bucket.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
+                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 for f in ("probe_gather", "probe_scatter"):
     getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
 
@@ -63,3 +65,21 @@ for win_mb in (8, 40, 160):
     t = timeit(lambda: L.probe_gather(P(rec), P(pw), n, P(out), s))
     print(f"gather_w{win_mb:<4d}{t:7.3f} ms  {2 * gb / t:6.2f} TB/s (perm random inside {win_mb} MB windows)",
           flush=True)
+
+# MSD bucket pass: rows into 2^b bucket regions of capacity n/2^b * 1.05
+del perm, inv
+for bbits in (4, 6, 8):
+    nb = 1 << bbits
+    bcap = int(n / nb * 1.05) + 4096
+    big = torch.empty(nb * bcap * 25, dtype=torch.int32, device=dev)
+    keys = torch.empty(nb * bcap, dtype=torch.int32, device=dev)
+    cur = torch.zeros(nb, dtype=torch.int64, device=dev)
+
+    def run():
+        cur.zero_()
+        L.probe_bucket(P(rec), n, bbits, bcap, P(cur), P(big), P(keys), s)
+    t = timeit(run)
+    ok = int(cur.sum()) == n and int(cur.max()) <= bcap
+    print(f"bucket{nb:<5d}{t:7.3f} ms  {2 * gb / t:6.2f} TB/s (rows read in order, written to {nb} bucket "
+          f"regions, + keys) {'ok' if ok else 'OVERFLOW'}", flush=True)
+    del big, keys
