@@ -219,17 +219,13 @@ def test_sort_giveup_detected_and_resorted(gpu, sort_fail):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("native_tail", [True, False])
-def test_sort_giveup_in_fused_tail(gpu, sort_fail, monkeypatch, native_tail):
+def test_sort_giveup_in_fused_tail(gpu, sort_fail):
     """The fused device tail packs the sort error into the 'bad' word (bit 2):
     the host re-sorts (one forced give-up: exact results) or raises (give-ups
     that do not stop)."""
     from lua_mapreduce_1_amd.parallel import spmd as S
     from lua_mapreduce_1_amd.runtime import codec
-    from lua_mapreduce_1_amd.utils.config import TUNABLES
     from lua_mapreduce_1_amd.utils.corpus import europarl_like
-    import dataclasses
-    monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(TUNABLES, native_tail=native_tail))
     splits = europarl_like(seed=4, lines=20_000, words=300_000, vocab_size=30_000, split_lines=2000)
     M = "lua_mapreduce_1_amd.models.wordcount"
 

@@ -88,7 +88,7 @@ def main() -> int:
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
-    return 0
+    return 0 if ok else 3
 
 
 if __name__ == "__main__":
