@@ -28,6 +28,7 @@ Results stay in HBM (they can be ~the size of the input); ``partitions`` /
 """
 from __future__ import annotations
 
+import sys
 import time
 
 import numpy as np
@@ -41,6 +42,7 @@ from ..runtime import device as devmod
 from ..runtime import modules
 from ..utils import STATUS
 from ..utils import trace
+from ..utils.config import TUNABLES
 from . import dist as D
 
 FOLD_OPS = ("sum", "min", "max", "count")
@@ -57,6 +59,11 @@ def make_plane(eng):
     if eng.op in RECORD_OPS:
         return RecordPlane(eng)
     return None
+
+
+class _HeapFull(Exception):
+    """A streamed list map's long-key heap ran out (the map re-runs with a
+    larger heap)."""
 
 
 class _UseGeneric(Exception):
@@ -163,6 +170,10 @@ class ListPlane:
         self.sink = None
         self._lines = None
         self._cpu_keys: list = []
+        self._cpu_text = None
+        self._round_keys: list = []
+        self._cpu_parts: list = []
+        self.streamed = False
         self.emitter = ListEmitter(self)
         if eng.device_input != "split":
             raise ValueError("the list plane maps engine-staged splits (device_input = 'split')")
@@ -173,11 +184,8 @@ class ListPlane:
         rank counts the newlines of the splits it holds; one all-gather."""
         if self._lines is None:
             st = self.eng.splits
-            st.finish_loading()
             i0, i1 = st.own
-            view = st.buffer.numpy() if st.buffer.device.type == "cpu" else st.buffer.cpu().numpy()
-            mine = [int(np.count_nonzero(view[st.region(i, i + 1)[0]:st.region(i, i + 1)[1]] == 10))
-                    for i in range(i0, i1)]
+            mine = st.newline_counts(i0, i1)
             parts = D.all_gather_object((i0, mine), self.eng.group)
             per = np.zeros(len(st), np.int64)
             for a, counts in parts:
@@ -201,6 +209,39 @@ class ListPlane:
             self._cpu_end = max(self._cpu_end, a + text.numel())
 
     def _map(self, jobs, recs, j0, j1) -> torch.Tensor:
+        """Postings of the rank's splits.  A rank input larger than
+        ``arena_cap_mb`` streams through the engine's two capped ring slots
+        (SpmdEngine._stage_streaming): each round's postings are grouped as
+        the round ends (stream_round_end) and the vocabulary's long words
+        move to the key heap, so the slot can be refilled; a full heap
+        doubles and the map re-runs."""
+        while True:
+            try:
+                return self._map_once(jobs, recs, j0, j1)
+            except _HeapFull:
+                eng = self.eng
+                cur = getattr(eng, "_stream_heap_mb", TUNABLES.stream_heap_mb)
+                eng._stream_heap_mb = 2 * cur
+                sys.stderr.write("# streaming list map: long-key heap of %.0f MiB full, re-mapping with %.0f MiB\n"
+                                 % (cur, 2 * cur))
+
+    def stream_round_end(self, buf, lo: int, hi: int, heap, H: int) -> None:
+        if not buf.is_cuda:
+            # CPU: keep the round's text; the whole rank text is mapped at
+            # the end (one dense id space, ops/invidx.py Vocab._assign_cpu)
+            if self._cpu_end > lo:
+                self._cpu_parts.append(buf[lo:self._cpu_end].clone())
+            self._cpu_end = 0
+            return
+        k = self.sink.finish(self.vocab)  # one synchronisation per round
+        if k.numel():
+            self._round_keys.append(self._group(k, self.vocab.id_bits + self.doc_bits, self.doc_bits))
+        self.sink.reset()
+        self.vocab.table.rehome_long_keys(buf, lo, hi, heap, H)
+        if int(ops.host_read(heap)[1]):
+            raise _HeapFull()
+
+    def _map_once(self, jobs, recs, j0, j1) -> torch.Tensor:
         eng = self.eng
         lines = self.line_offsets()
         ids = eng._split_ids(jobs, j0, j1)
@@ -215,10 +256,13 @@ class ListPlane:
             self.doc_bits = (self.doc_bits + 7) // 8 * 8
         self.vocab.reset()
         dmap = eng.dmap
+        self.streamed = bool(ids) and eng._streaming(ids)
+        self._round_keys, self._cpu_parts, self._cpu_text = [], [], None
         if eng.device.type == "cuda":
             a, b = eng.splits.region(ids[0], ids[-1] + 1) if ids else (0, 0)
-            if self.sink is None or self.sink.cap < (b - a) // 2 + 2:
-                self.sink = II.PostingSink(eng.device, b - a)
+            nb = eng._arena_cap() if self.streamed else b - a
+            if self.sink is None or self.sink.cap < nb // 2 + 2:
+                self.sink = II.PostingSink(eng.device, nb)
             self.sink.reset()
         else:
             self._cpu_end = 0
@@ -243,7 +287,20 @@ class ListPlane:
                         recs[j].status = STATUS.BROKEN if attempt < 2 else STATUS.FAILED
             _mark_written(recs, ja, jb, t0, time.time(), c0)
         if eng.device.type == "cuda":
+            if self.streamed:
+                # every round's (word, line) groups, rounds in line order: a
+                # stable sort of the word bits merges them (run_iteration)
+                keys = torch.cat(self._round_keys) if self._round_keys else torch.zeros(
+                    0, dtype=torch.int64, device=eng.device)
+                self._round_keys = []
+                return keys
             return self.sink.finish(self.vocab) if ids else torch.zeros(0, dtype=torch.int64, device=eng.device)
+        if self.streamed:
+            if not self._cpu_parts:
+                return torch.zeros(0, dtype=torch.int64)
+            self._cpu_text = torch.cat(self._cpu_parts)
+            self._cpu_parts = []
+            return II.map_postings(self._cpu_text, self.vocab, self.doc_bits)
         if not self._cpu_end:
             return torch.zeros(0, dtype=torch.int64)
         return II.map_postings(eng.arena[:self._cpu_end], self.vocab, self.doc_bits)
@@ -312,7 +369,7 @@ class ListPlane:
             raise ValueError(f"posting key needs {bits} bits (> 63): raise the vocabulary capacity bits or split "
                              "the input")
         with trace.range("mr.list.sort"):
-            ukeys = self._group(keys, bits, self.doc_bits)
+            ukeys = self._group(keys, bits, self.doc_bits, runs=self.streamed)
             wid, wstart, docs = II.split_words(ukeys, self.doc_bits, vocab.id_bits, self.line_base)
             vhi, vlo, vrep = vocab.arrays()
             hi, lo, rep = vhi[wid], vlo[wid], vrep[wid]
@@ -337,8 +394,11 @@ class ListPlane:
         return res
 
     def _src(self):
-        """The key-byte source of the map's vocabulary: the staged arena."""
+        """The key-byte source of the map's vocabulary: the staged arena
+        (streamed on the CPU: the rounds' text)."""
         eng = self.eng
+        if self._cpu_text is not None:
+            return self._cpu_text
         return eng.arena if eng.arena is not None else torch.zeros(1, dtype=torch.uint8, device=eng.device)
 
     def _shuffle(self, hi, lo, rep, text, wid, wstart, docs, dest, failed):

@@ -163,20 +163,15 @@ class SplitStore:
             self._load.wait()
             self._load = None
 
-    def line_offsets(self) -> np.ndarray:
-        """Cumulative newline counts at split boundaries (global line ids;
-        needs every split in this store)."""
-        lo = getattr(self, "_line_offsets", None)
-        if lo is None:
-            self.finish_loading()
-            if self.own != (0, len(self)):
-                raise ValueError("line_offsets needs a store holding every split")
-            view = self.buffer.numpy()
-            per = [int(np.count_nonzero(view[self.offsets[i]:self.offsets[i + 1]] == 10)) for i in range(len(self))]
-            lo = np.zeros(len(self) + 1, dtype=np.int64)
-            np.cumsum(per, out=lo[1:])
-            self._line_offsets = lo
-        return lo
+    def newline_counts(self, i0: int, i1: int) -> list[int]:
+        """Newlines of each owned split [i0, i1) (its padding newline included)."""
+        self.finish_loading()
+        view = self.buffer.numpy() if self.buffer.device.type == "cpu" else self.buffer.cpu().numpy()
+        out = []
+        for i in range(i0, i1):
+            a, b = self.region(i, i + 1)
+            out.append(int(np.count_nonzero(view[a:b] == 10)))
+        return out
 
 
 _STREAMS: dict = {}
@@ -247,8 +242,20 @@ class WindowedSplitStore(SplitStore):
     def release(self, slot: int, event) -> None:
         self._released[slot] = event
 
-    def line_offsets(self) -> np.ndarray:
-        raise ValueError("line numbering needs a store holding every split")
+    def newline_counts(self, i0: int, i1: int) -> list[int]:
+        """Newlines of each split [i0, i1) (its padding newline included),
+        counted by reading the files in 16 MiB blocks."""
+        out = []
+        for i in range(i0, i1):
+            n = 0
+            with open(self.paths[i], "rb") as f:
+                while True:
+                    b = f.read(16 << 20)
+                    if not b:
+                        break
+                    n += b.count(b"\n")
+            out.append(n + int(self._pad[i]))
+        return out
 
 
 def _file_pads(paths) -> tuple[list[int], list[int]]:
@@ -695,9 +702,10 @@ class SPMDEngine:
         cap = self._arena_cap()
         if not cap or not ids:
             return False
-        if self.plane_kind != "fold":
-            raise ValueError(f"arena_cap_mb / MR_ARENA_CAP_MB streaming is implemented for the fold plane only "
-                             f"(this job runs the {self.plane_kind} plane)")
+        if self.plane_kind not in ("fold", "list"):
+            raise ValueError(f"arena_cap_mb / MR_ARENA_CAP_MB streaming is implemented for the fold and list "
+                             f"planes (this job runs the {self.plane_kind} plane; the record plane spills "
+                             f"with record_cap_mb)")
         a, b = self.splits.region(ids[0], ids[-1] + 1)
         return b - a > cap
 
@@ -768,7 +776,7 @@ class SPMDEngine:
                     st.wait_ready(*sp)
                     buf[off:off + n].copy_(h[ha - hb:ha - hb + n])
                     yield jr, buf[off:off + n]
-                self.table.rehome_long_keys(buf, H + (r % 2) * A, H + (r % 2) * A + A, heap, H)
+                self._round_end(buf, H + (r % 2) * A, H + (r % 2) * A + A, heap, H)
             return
         from ..ops import _hip
         cur = torch.cuda.current_stream(self.device)
@@ -802,11 +810,21 @@ class SPMDEngine:
             for (jr, off, ha, n, sp), ev in zip(pieces, issued.pop(r)):
                 cur.wait_event(ev)
                 yield jr, buf[off:off + n]
-            self.table.rehome_long_keys(buf, H + (r % 2) * A, H + (r % 2) * A + A, heap, H)
+            self._round_end(buf, H + (r % 2) * A, H + (r % 2) * A + A, heap, H)
             if r + 2 < len(plan):
                 evs["free"][r % 2].record(cur)  # slot r % 2 is free once round r's map and rehome ran
                 cs.wait_event(evs["free"][r % 2])
                 issued[r + 2] = issue(r + 2)
+
+    def _round_end(self, buf, lo: int, hi: int, heap, H: int) -> None:
+        """After a streamed round: the fold plane moves the long keys the
+        round introduced to the key heap; the list plane also groups the
+        round's postings (ListPlane.stream_round_end)."""
+        hook = getattr(self.plane, "stream_round_end", None) if self.plane is not None else None
+        if hook is not None:
+            hook(buf, lo, hi, heap, H)
+        else:
+            self.table.rehome_long_keys(buf, lo, hi, heap, H)
 
     def _stage_chunks(self, jobs, j0, j1):
         """Yield (job index range, device tensor) chunks, H2D overlapped with compute."""
@@ -1632,10 +1650,10 @@ class SPMDEngine:
         if len(f) > 3 and f[3] != "" and int(f[3]) != int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")):
             return
         if action == "exit":
-            sys.stderr.write("# injected fault: rank %d exits in iteration %d (%s)\n" % (self.rank, cur, phase))
+            sys.stderr.write("# injected fault: rank %d exits at iteration %d (%s)\n" % (self.rank, cur, phase))
             sys.stderr.flush()
             os._exit(17)
-        raise RuntimeError("injected fault: rank %d in iteration %d (%s)" % (self.rank, cur, phase))
+        raise RuntimeError("injected fault: rank %d at iteration %d (%s)" % (self.rank, cur, phase))
 
     def run(self) -> IterationResult:
         """Iterate until finalfn returns something other than "loop".  With a

@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${1:-r3_check}
 mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_generic_gpu.py tests/test_records.py -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_new.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_streaming.py tests/test_ops_gpu.py tests/test_exactness.py -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_new.log 2>&1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 timeout -k 10 300 python -u __graft_entry__.py smoke > $OUT/smoke.log 2>&1
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --force-shuffle > $OUT/bench_staged_fs.log 2>&1
