@@ -543,9 +543,7 @@ class RecordEmitter:
             pl.shape = shape
         elif pl.shape != shape:
             raise ValueError(f"records of one job share a shape: {pl.shape} (row, key bytes) vs {shape}")
-        if rec.device != pl.eng.device:
-            rec = rec.to(pl.eng.device, non_blocking=True)
-        pl._out.append(rec)
+        pl._take(rec)
 
 
 def _bits32(x) -> int:
@@ -579,9 +577,30 @@ class RecordPlane:
         self._out: list = []
         self.shape = None  # (row bytes, key bytes) of the emitted records
 
+    # -- spill tier: a rank's rows beyond ``record_cap_mb`` live in host memory
+    def _cap(self) -> int:
+        mb = self.eng.params.get("record_cap_mb", TUNABLES.record_cap_mb)
+        return int(float(mb) * (1 << 20)) if mb else 0
+
+    def _take(self, rec: torch.Tensor) -> None:
+        """Keep an emitted block: on the device until the rank's rows pass
+        the cap, then every block (the earlier ones too) in host memory."""
+        dev = self.eng.device
+        cap = self._cap()
+        self._bytes += rec.numel()
+        if cap and not self._spilled and self._bytes > cap:
+            self._spilled = True
+            self._out = [_to_host(r) for r in self._out]
+        if self._spilled:
+            self._out.append(_to_host(rec))
+        else:
+            self._out.append(rec if rec.device == dev else rec.to(dev, non_blocking=True))
+
     def _map(self, jobs, recs, j0, j1) -> torch.Tensor:
         eng = self.eng
         self._out = []
+        self._bytes = 0
+        self._spilled = False
         for j in range(j0, j1):
             t0, c0 = time.time(), time.process_time()
             v = jobs[j][1]
@@ -603,22 +622,34 @@ class RecordPlane:
             self.shape = next((x for x in shapes if x is not None), (TS.REC, TS.KEY))
         elif D.initialized() and eng.world > 1:
             D.all_gather_object(self.shape, eng.group)
+        # every rank takes the same path (the shuffle of the spilled path
+        # runs in rounds): spill when any rank spilled
+        if D.initialized() and eng.world > 1:
+            self._spilled = D.all_reduce_max(float(self._spilled), eng.device) > 0
+            if self._spilled:
+                self._out = [_to_host(r) for r in self._out]
+        if self._spilled:
+            return None
         if not self._out:
             return torch.zeros((0, self.shape[0]), dtype=torch.uint8, device=eng.device)
         return self._out[0] if len(self._out) == 1 else torch.cat(self._out)
 
-    def _sample_splitters(self, k32: torch.Tensor, R: int) -> torch.Tensor:
+    def _sample_splitters(self, k32: torch.Tensor | None, R: int, host_rows: list | None = None) -> torch.Tensor:
         """R-1 splitters (32-bit key prefixes, unsigned, as int32 bit
         patterns) from a sample of every rank's keys (TeraSort's sampled
-        total-order partitioner)."""
+        total-order partitioner).  ``host_rows``: the sample is drawn from
+        spilled blocks instead."""
         eng = self.eng
         # the same sample size on every rank (all_gather), drawn with
         # replacement; a rank without rows contributes -1s, dropped below
         k = self.oversample * R
         g = torch.Generator().manual_seed(self.seed * 7919 + eng.rank)
-        idx = torch.randint(0, max(1, k32.numel()), (k,), generator=g).to(k32.device)
-        samp = (k32[idx].to(torch.int64) & 0xFFFFFFFF) if k32.numel() else torch.full((k,), -1, dtype=torch.int64,
-                                                                                    device=k32.device)
+        if host_rows is not None:
+            samp = _host_sample32(host_rows, self.shape[1], k, g).to(eng.device)
+        else:
+            idx = torch.randint(0, max(1, k32.numel()), (k,), generator=g).to(k32.device)
+            samp = (k32[idx].to(torch.int64) & 0xFFFFFFFF) if k32.numel() else torch.full(
+                (k,), -1, dtype=torch.int64, device=k32.device)
         allv = D.all_gather_tensor(samp, eng.group) if D.initialized() else samp
         allv = allv[allv >= 0]
         if allv.numel() == 0:
@@ -627,6 +658,127 @@ class RecordPlane:
         m = srt.numel()
         pick = torch.tensor([(m * j) // R for j in range(1, R)], dtype=torch.int64, device=srt.device)
         return srt[pick].to(torch.int32).contiguous()
+
+    # -- spilled rows: external sort ------------------------------------------
+    def _run_spilled(self, failed: int, T: dict, t1: float):
+        """Rows beyond the HBM cap (``record_cap_mb``), kept in host memory:
+        splitters from a host sample; at W > 1 a shuffle in rounds of at most
+        the cap (every rank runs the same number of rounds), received rows
+        back to host memory; then an external sort of the rank's rows
+        (_external_sort).  The reference's reduce streams merged runs from
+        storage the same way (utils.lua:206-271)."""
+        eng = self.eng
+        R, W = eng.nparts, eng.world
+        rb = self.shape[0]
+        cap = max(self._cap(), rb)
+        blocks, self._out = self._out, []
+        sp = self.splitters
+        if R > 1 and sp is None:
+            sp = self._sample_splitters(None, R, host_rows=blocks)
+        elif sp is not None:
+            sp = sp.to(eng.device)
+        if W > 1 or eng.force_shuffle:
+            blocks, failed = self._shuffle_rounds(blocks, sp, cap, failed)
+        T["shuffle"] = time.time() - t1
+        t2 = time.time()
+        out, counts = self._external_sort(blocks, sp, cap)
+        T["reduce"] = time.time() - t2
+        return out, counts, sp, failed
+
+    def _device_rows(self, pieces: list) -> torch.Tensor:
+        dev = self.eng.device
+        if not pieces:
+            return torch.zeros((0, self.shape[0]), dtype=torch.uint8, device=dev)
+        return torch.cat([p.to(dev, non_blocking=True) for p in pieces])
+
+    def _shuffle_rounds(self, blocks: list, sp, cap: int, failed: int):
+        from ..ops import records as RC
+        eng = self.eng
+        R, W = eng.nparts, eng.world
+        kb = self.shape[1]
+        rounds = _host_rounds(blocks, cap)
+        nr = int(D.all_reduce_max(float(len(rounds)), eng.device)) if D.initialized() and W > 1 else len(rounds)
+        got, failed_total = [], 0
+        for r in range(nr):
+            rec = self._device_rows(rounds[r] if r < len(rounds) else [])
+            k32 = RC.keys32(rec, kb)
+            part = RC.dest32(k32, sp) if R > 1 else torch.zeros(k32.numel(), dtype=torch.int32, device=k32.device)
+            dest = (part.to(torch.int64) % W).to(torch.int32)
+            perm = ops.sort_keys_checked([dest.to(torch.int64)], bits=[max(8, _bits(W))])
+            packed = RC.gather(rec, perm)
+            del rec
+            counts = ops.bincount(dest, W)
+            # per destination: (rows, this rank's failed maps — first round only)
+            xchg = torch.stack([counts, torch.full((W,), failed if r == 0 else 0, dtype=torch.int64,
+                                                   device=counts.device)], 1).contiguous()
+            recv = D.exchange_counts(xchg.view(-1), eng.group).view(W, 2)
+            both = torch.cat([xchg, recv]).cpu().tolist()
+            failed_total += sum(x[1] for x in both[W:])
+            rrec = D.all_to_all_v(packed, [x[0] for x in both[:W]], [x[0] for x in both[W:]], eng.group)
+            del packed
+            if rrec.shape[0]:
+                got.append(_to_host(rrec))
+        return got, failed_total
+
+    def _external_sort(self, blocks: list, sp, cap: int):
+        """Host rows -> one host array in key order + rows per partition.
+        Rows that fit the cap are sorted in one go; otherwise a bucket pass
+        moves every round's rows to sub-range buckets of their 32-bit key
+        prefix (sub-splitters from a local sample, sized so that a bucket
+        fills about half the cap; equal prefixes share a bucket) and each
+        bucket is sorted on the device and written at its place."""
+        from ..ops import records as RC
+        eng = self.eng
+        dev = eng.device
+        R = eng.nparts
+        rb, kb = self.shape
+        n = sum(int(b.shape[0]) for b in blocks)
+        counts = np.zeros(max(R, 1), np.int64)
+        out = torch.empty((n, rb), dtype=torch.uint8, pin_memory=dev.type == "cuda")
+
+        def sort_into(pieces, pos):
+            rec = self._device_rows(pieces)
+            m = int(rec.shape[0])
+            if not m:
+                return pos
+            gh = torch.zeros(2048, dtype=torch.int32, device=dev) if rec.is_cuda else None
+            k32 = RC.keys32(rec, kb, gh)
+            perm, sk = RC.sort(rec, kb, k32, gh)
+            out[pos:pos + m].copy_(RC.gather(rec, perm))
+            if R > 1:
+                counts[:] += ops.bincount(RC.dest32(sk, sp), R).cpu().numpy()
+            else:
+                counts[0] += m
+            return pos + m
+
+        if n * rb <= cap:
+            sort_into(blocks, 0)
+            return out, counts.tolist()
+        nb = -(-n * rb // max(rb, cap // 2))
+        g = torch.Generator().manual_seed(self.seed * 104729 + eng.rank)
+        samp = np.sort(_host_sample32(blocks, kb, 64 * nb, g).numpy())
+        m = samp.size
+        sub = np.unique(samp[[(m * j) // nb for j in range(1, nb)]]).astype(np.uint32)
+        sub_t = torch.from_numpy(sub.view(np.int32).copy()).to(dev)
+        B = sub.size + 1
+        buckets: list = [[] for _ in range(B)]
+        for pieces in _host_rounds(blocks, cap):
+            rec = self._device_rows(pieces)
+            b = RC.dest32(RC.keys32(rec, kb), sub_t)
+            perm = ops.sort_keys_checked([b.to(torch.int64)], bits=[max(8, _bits(B))])
+            host = _to_host(RC.gather(rec, perm))
+            del rec
+            off = 0
+            for j, c in enumerate(ops.bincount(b, B).cpu().tolist()):
+                if c:
+                    buckets[j].append(host[off:off + c])
+                    off += c
+        del blocks
+        pos = 0
+        for j in range(B):
+            pos = sort_into(buckets[j], pos)
+            buckets[j] = None  # release the bucket's host rows
+        return out, counts.tolist()
 
     def run_iteration(self, prefetch_next, lookahead):
         from ..ops import records as RC
@@ -649,6 +801,16 @@ class RecordPlane:
         t1 = time.time()
         R, W = eng.nparts, eng.world
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
+        if rec is None:
+            with trace.range("mr.rec.spilled"):
+                out, counts, sp, failed = self._run_spilled(failed, T, t1)
+            _result_jobs(eng, res, counts, t1)
+            res.device = {"records": out, "counts_host": counts, "splitters": sp, "key_bytes": kb, "spilled": True}
+            res.distinct_keys = res.total_value = int(out.shape[0])
+            res.failed_maps = failed
+            res._materialize = lambda o=res.device: _record_host(o, R)
+            T["iteration"] = time.time() - t_start
+            return res
         k32 = None
         sp = self.splitters
         if R > 1 and sp is None:
@@ -696,6 +858,55 @@ class RecordPlane:
         T["reduce"] = time.time() - t2
         T["iteration"] = time.time() - t_start
         return res
+
+
+def _to_host(t: torch.Tensor) -> torch.Tensor:
+    """A block in (pinned, when a GPU is present) host memory."""
+    if t.device.type == "cpu":
+        return t
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t)
+    return h
+
+
+def _host_sample32(blocks: list, kb: int, k: int, g) -> torch.Tensor:
+    """``k`` 32-bit key prefixes (int64, unsigned values) of rows drawn with
+    replacement from host blocks (-1s when there are no rows)."""
+    sizes = np.array([int(b.shape[0]) for b in blocks], np.int64)
+    n = int(sizes.sum())
+    if n == 0:
+        return torch.full((k,), -1, dtype=torch.int64)
+    idx = torch.randint(0, n, (k,), generator=g).numpy()
+    starts = np.concatenate([[0], np.cumsum(sizes)])
+    which = np.searchsorted(starts, idx, side="right") - 1
+    kk = min(kb, 4)
+    pref = np.zeros((k, 4), np.uint8)
+    for bi in np.unique(which):
+        sel = np.flatnonzero(which == bi)
+        a = blocks[bi].numpy()
+        pref[sel, :kk] = a[idx[sel] - starts[bi], :kk]
+    return torch.from_numpy(pref.view(">u4").reshape(k).astype(np.int64))
+
+
+def _host_rounds(blocks: list, cap: int) -> list:
+    """Host blocks cut into row ranges of at most ``cap`` bytes each (a row
+    wider than the cap is one round)."""
+    out, cur, acc = [], [], 0
+    for b in blocks:
+        n, w = int(b.shape[0]), int(b.shape[1])
+        per = max(1, cap // max(1, w))
+        i = 0
+        while i < n:
+            take = min(n - i, max(1, (cap - acc) // max(1, w)) if acc else per)
+            cur.append(b[i:i + take])
+            acc += take * w
+            i += take
+            if acc + w > cap:
+                out.append(cur)
+                cur, acc = [], 0
+    if cur:
+        out.append(cur)
+    return out
 
 
 def _record_host(out: dict, R: int) -> dict[int, dict]:

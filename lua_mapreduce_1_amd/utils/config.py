@@ -61,6 +61,9 @@ class Tunables:
                                 "input is mapped in rounds through a ring of two arenas of this size")
     stream_heap_mb: float = _knob("MR_STREAM_HEAP_MB", 64.0,
                                   "SPMD streaming rounds: HBM heap for the bytes of distinct long keys, MiB")
+    record_cap_mb: float = _knob("MR_RECORD_CAP_MB", 0.0,
+                                 "SPMD record plane: HBM budget for a rank's rows, MiB (0 = unbounded); more rows "
+                                 "spill to host memory and are sorted externally (bucket pass + per-bucket sorts)")
     fused_tail: bool = _knob("MR_FUSED_TAIL", True, "fused reduce-side tail kernels (tail.hip)")
     pipeline: bool = _knob("MR_PIPELINE", True, "bench/proxies: map of iteration i+1 overlaps the tail of i")
     prefetch_single: bool = _knob("MR_PREFETCH_SINGLE", True, "prefetched inputs: one DMA per iteration")

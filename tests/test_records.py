@@ -68,6 +68,7 @@ def test_records_shape_must_agree():
     class P:
         shape = None
         _out: list = []
+        _take = staticmethod(lambda rec: None)
 
         class eng:
             device = torch.device("cpu")
@@ -76,11 +77,12 @@ def test_records_shape_must_agree():
     with pytest.raises(ValueError):
         e.records(torch.zeros((3, 9), dtype=torch.uint8), 4)
     with pytest.raises(ValueError):
-        RecordEmitter(type("Q", (), {"shape": None, "_out": [], "eng": P.eng})).records(
+        RecordEmitter(type("Q", (), {"shape": None, "_out": [], "_take": staticmethod(lambda r: None),
+                                     "eng": P.eng})).records(
             torch.zeros((3, 8), dtype=torch.uint8), 9)
 
 
-def _rank(rank, world, port, q, args, force_shuffle):
+def _rank(rank, world, port, q, args, force_shuffle, extra=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import datetime
@@ -91,9 +93,9 @@ def _rank(rank, world, port, q, args, force_shuffle):
                                 timeout=datetime.timedelta(seconds=120))
     else:
         D.init_from_env(backend="gloo", use_gpu=False)
-    _eng, _res, rows = run_engine(args, torch.device("cpu"), force_shuffle=force_shuffle)
+    eng, _res, rows = run_engine(args, torch.device("cpu"), force_shuffle=force_shuffle, **(extra or {}))
     if rank == 0:
-        q.put(check(rows, args))
+        q.put(check(rows, args) and (not extra or eng.plane._spilled))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -111,6 +113,53 @@ def test_records_multi_rank_cpu(args, world, force):
         p.join(240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5)
+
+
+# -- spill tier: rows beyond the HBM cap -------------------------
+SPILL = [dict(rb=64, kb=16, rows=20000), dict(rb=37, kb=5, rows=20000), dict(rb=24, kb=3, skew=True, rows=20000)]
+SPILL_IDS = ["64x16", "37x5", "24x3-skew"]
+
+
+@pytest.mark.parametrize("args", SPILL, ids=SPILL_IDS)
+def test_records_spill_external_sort_cpu(args):
+    """1.3 MB of rows under a 0.1 MB cap: spilled to host, bucket pass,
+    per-bucket sorts; the output equals a sort of the input."""
+    eng, res, rows = run_engine(args, torch.device("cpu"), record_cap_mb=0.1)
+    assert eng.plane._spilled and res.device["spilled"]
+    assert check(rows, args)
+
+
+@pytest.mark.parametrize("world,force", [(3, False), (1, True)], ids=["gloo3", "forced1"])
+def test_records_spill_multi_rank_cpu(world, force):
+    args = SPILL[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, args, force, {"record_cap_mb": 0.05}))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5)
+
+
+def test_host_rounds_cover_every_row():
+    from lua_mapreduce_1_amd.parallel.planes import _host_rounds
+    blocks = [torch.arange(n * 7, dtype=torch.int64).to(torch.uint8).view(n, 7) for n in (5, 0, 13, 1, 40)]
+    rounds = _host_rounds(blocks, 50)
+    assert all(sum(p.numel() for p in r) <= 50 for r in rounds)
+    assert torch.equal(torch.cat([p for r in rounds for p in r]), torch.cat(blocks))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", SPILL, ids=SPILL_IDS)
+def test_records_spill_external_sort_gpu(gpu, args):
+    a = dict(args, rows=200_000)
+    eng, res, rows = run_engine(a, gpu, record_cap_mb=1.0)
+    assert eng.plane._spilled and res.device["spilled"]
+    assert check(rows, a)
 
 
 # -- GPU kernels vs the CPU specification ---------------------------------------
