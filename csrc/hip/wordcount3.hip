@@ -1,23 +1,21 @@
 // wordcount3.hip — third-generation fused word-count map kernel (gfx950).
 //
-// Same contract as wc_map2_kernel (wordcount2.hip; reference hot loops K1-K5:
-// examples/WordCount/mapfn.lua:4-7, job.lua:83-97, job.lua:92-96): tokenize a
+// Same contract as the reference's hot loops K1-K5
+// (examples/WordCount/mapfn.lua:4-7, job.lua:83-97, job.lua:92-96): tokenize a
 // byte stream on Lua-%s whitespace, build exact 128-bit keys, combine in an LDS
 // hash table, fold each workgroup's distinct words into the HBM table.
 //
-// What v2's ablation showed (tools/wc_ablate2.py, full corpus, 16 KiB chunks):
-// tokenize 0.90 ms + LDS combine 0.90 ms + flush to HBM 1.47 ms = 3.40 ms.  The
-// kernel ran ONE 512-thread workgroup per CU (112 KiB LDS table): every phase's
-// latency was exposed — the HBM load of each tile (no other workgroup to
-// overlap it) and the flush's chain of dependent global atomics (~1,600
-// distinct words per chunk; device atomics execute at the memory side at
-// ~24 G/s chip-wide, tools/probe/atomic_probe.hip).  v3 therefore:
-//   * sizes the LDS table so several workgroups share a CU (the flush of one
-//     overlaps the tokenizing of another): T threads, SLOTS slots, TPC tiles per
-//     chunk are template parameters (ablated in tools/wc_ablate2.py);
-//   * prefetches the next tile's bytes into registers before the token loop of
-//     the current tile (the HBM latency of a tile hides behind the LDS work);
-//   * reads the halo with the same 16-byte loads as the body (no byte loops).
+// One launch shape: 512 threads, 2048 LDS slots, one 8 KiB tile per
+// workgroup (two workgroups per CU, so one's flush to HBM overlaps the other's
+// tokenizing), dense token lists.  The other shapes and the timing-only
+// ablation modes measured in rounds 1-2 (profiles/r2/map_kernel/, the
+// per-workgroup phase stamps of profiles/r1/map_v3/) are archived as
+// profiles/r3/pruned/map_configs/wc_map3_configs.patch.
+//
+// The map is bound by memory-side atomics: the flush folds ~0.63
+// (workgroup, distinct word) entries per token, one device-scope atomic add
+// each, and device atomics execute at the memory side at ~24 G/s chip-wide
+// (profiles/r3/map_pmc/README.md: TCC_EA0_ATOMIC = flush entries).
 #include <hip/hip_runtime.h>
 #include "mr_common.h"
 #include "hashtab.h"
@@ -57,7 +55,6 @@ struct Ovf {
   u64* rep;
   u64 cap;
   unsigned long long* counter;
-  u64* stamps;  // optional per-workgroup phase timestamps (tools/wc_stamps.py), 4 per workgroup
 };
 
 __device__ __forceinline__ u32 ws_mask_word(u32 w) {
@@ -159,18 +156,14 @@ __device__ __forceinline__ bool lds_insert(Lds<T, SLOTS>& L, u64 hi, u64 lo, u32
 }
 
 // T threads, SLOTS LDS slots, TPC tiles of T*16 bytes per workgroup chunk.
-// DENSE: the tile's token starts are first compacted into an LDS list (block
-// prefix scan of per-thread start counts) and the tokens processed from that
-// list, lane i taking tokens i, i+T, ... — every lane busy in every
-// iteration, instead of each lane walking the 0..8 tokens that start in its
-// own 16 bytes (the wave ran as long as its busiest lane).
-template <int T, int SLOTS, int TPC, bool DENSE = false>
+// The tile's token starts are first compacted into an LDS list (block prefix
+// scan of per-thread start counts) and the tokens processed from that list,
+// lane i taking tokens i, i+T, ... — every lane busy in every iteration,
+// instead of each lane walking the 0..8 tokens that start in its own 16 bytes
+// (the wave would run as long as its busiest lane).
+template <int T, int SLOTS, int TPC>
 __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text, u64 nbytes, u64 rep_base, GTab g,
-                                                    Ovf ovf, int aligned, int ablate) {
-  // ablate (timing only, the table is then incomplete): 1 = no flush to HBM,
-  // 2 = tokenize + key packing only (no LDS combine, no flush); flush variants:
-  // 3 = home-slot tag load only (no lo/hi loads), 4 = blind atomic adds to the
-  // home slots (no loads, no claims), 5 = the speculative loads only (no atomics)
+                                                    Ovf ovf, int aligned) {
   using L_t = Lds<T, SLOTS>;
   constexpr int TILE = L_t::TILE;
   constexpr int STAGED = L_t::STAGED;
@@ -181,8 +174,6 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
   const u64 chunk_begin = (u64)blockIdx.x * CHUNK;
   if (chunk_begin >= nbytes) return;
   const u64 chunk_end = min(chunk_begin + CHUNK, nbytes);
-  u64* stamp = ovf.stamps ? ovf.stamps + 4 * (u64)blockIdx.x : nullptr;
-  if (stamp && t == 0) stamp[0] = wall_clock64();
   for (int s = t; s < SLOTS; s += T) {
     L.tag[s] = 0;
     L.cnt[s] = 0;
@@ -254,10 +245,6 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
       } else {
         lo = long_lo_global(text, gpos, len);
       }
-      if (ablate == 2) {
-        if ((hi ^ lo) == 0x123456789ull) ovf.counter[1] = hi;  // keep the key live
-        return;
-      }
       const bool ok = len < 65536 && lds_insert(L, hi, lo, (u32)(gpos - chunk_begin) | ((u32)len << 16),
                                                  text + chunk_begin);
       if (!ok) {
@@ -281,13 +268,7 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
       const u64 lim_own = chunk_end - seg_base;
       if (lim_own < 16) starts &= (1u << lim_own) - 1u;
     }
-    if constexpr (!DENSE) {
-      while (starts) {
-        const int i = __builtin_ctz(starts);
-        starts &= starts - 1;
-        process((u32)t * SEG + i);
-      }
-    } else {
+    {
       // block exclusive scan of the per-thread token counts
       constexpr int MAXTOK = L_t::MAXTOK;
       const int lane = t & 63, wave = t >> 6;
@@ -321,8 +302,6 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
     }
     __syncthreads();
   }
-  if (stamp && t == 0) stamp[1] = wall_clock64();
-  if (ablate == 1 || ablate == 2) return;
   // flush: each thread folds its PER slots.  The common case is a key already
   // in the HBM table at its home slot, so tag/lo/hi of every home slot are
   // loaded speculatively in ONE batch (one memory round trip instead of a
@@ -342,17 +321,11 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
     ktag[k] = gtab_tag(khi[k], klo[k]);
     kslot[k] = gtab_home(ktag[k], g.mask);
   }
-  if (ablate == 4) {
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-      if (kcnt[k]) fold_value(&g.val[kslot[k]], (long long)kcnt[k], OP_SUM);
-    return;
-  }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (kcnt[k]) {
       gt[k] = ld_agent(&g.tag[kslot[k]]);
-      if (!gtab_tag_exact(ktag[k]) && ablate != 3) {
+      if (!gtab_tag_exact(ktag[k])) {
         gl[k] = ld_agent(&g.lo[kslot[k]]);
         gh[k] = ld_agent(&g.hi[kslot[k]]);
       } else {
@@ -360,14 +333,6 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
         gh[k] = khi[k];
       }
     }
-  }
-  if (ablate == 5) {
-    u64 x = 0;
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-      if (kcnt[k]) x ^= gt[k] ^ gl[k] ^ gh[k];
-    if (x == 0x123456789ull) ovf.counter[1] = x;  // keep the loads live
-    return;
   }
   // new keys whose home slot is empty are claimed in a batch too: all CASes,
   // one wait, all payload stores, ONE vmcnt drain, all publishing stores
@@ -419,18 +384,6 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
                           make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16), OP_SUM) == 2;
   }
   gtab_count_claims(g, claims);
-  if (stamp) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-      stamp[2] = wall_clock64();
-      u32 xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      u32 cu;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(cu));
-      stamp[3] = ((u64)xcc << 32) | cu;
-    }
-  }
 }
 
 __global__ void __launch_bounds__(256) ovf_agg3_kernel(Ovf o, GTab g) {
@@ -443,16 +396,8 @@ __global__ void __launch_bounds__(256) ovf_agg3_kernel(Ovf o, GTab g) {
   gtab_count_claims(g, claims);
 }
 
-template <int T, int SLOTS, int TPC, bool DENSE = false>
-int launch(const u8* tx, u64 nbytes, u64 rep_base, const GTab& g, const Ovf& o, int aligned, int ablate,
-           hipStream_t stream) {
-  static_assert(sizeof(Lds<T, SLOTS>) <= 160 * 1024, "LDS budget");
-  constexpr u64 CHUNK = (u64)T * SEG * TPC;
-  const u64 nblocks = (nbytes + CHUNK - 1) / CHUNK;
-  hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC, DENSE>), dim3((unsigned)nblocks), dim3(T), 0, stream, tx,
-                     nbytes, rep_base, g, o, aligned, ablate);
-  return 0;
-}
+constexpr int MAP_T = 512, MAP_SLOTS = 2048, MAP_TPC = 1;
+static_assert(sizeof(Lds<MAP_T, MAP_SLOTS>) <= 80 * 1024, "two workgroups per CU");
 
 }  // namespace v3
 }  // namespace mr
@@ -461,14 +406,9 @@ using namespace mr;
 
 extern "C" {
 
-// config: 0 = 512 threads / 2048 slots / 1 tile (8 KiB chunks, 2 workgroups per CU)
-//         1 = 512 / 2048 / 2 (16 KiB)      2 = 1024 / 4096 / 1 (16 KiB, 1 per CU)
-//         3 = 256 / 1024 / 1 (4 KiB, 4 per CU)   4 = 256 / 2048 / 2 (8 KiB, 2 per CU)
-//         5 = 512 / 4096 / 2 (16 KiB, 1 per CU: v2's shape + prefetch)
-//         6..9 = configs 0, 1, 3, 2 with dense token lists
 int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, void* lo, void* val, void* rep,
                void* ctrl, u64 cap, void* ovf_hi, void* ovf_lo, void* ovf_rep, u64 ovf_cap, void* ovf_counter,
-               int config, void* stamps, hipStream_t stream) {
+               hipStream_t stream) {
   if (nbytes == 0) return 0;
   GTab g;
   g.tag = (u64*)tag;
@@ -479,25 +419,12 @@ int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, 
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
   g.src = (const u8*)text - rep_base;  // every rep word of this table indexes the caller's byte source
-  v3::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter, (u64*)stamps};
+  v3::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter};
   const int aligned = ((uintptr_t)text & 15) == 0;
-  const u8* tx = (const u8*)text;
-  const int ablate = config >> 8;  // ablation modes ride in the high bits of config
-  config &= 0xFF;
-  switch (config) {
-    case 0: v3::launch<512, 2048, 1>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
-    case 1: v3::launch<512, 2048, 2>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
-    case 2: v3::launch<1024, 4096, 1>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
-    case 3: v3::launch<256, 1024, 1>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
-    case 4: v3::launch<256, 2048, 2>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
-    case 5: v3::launch<512, 4096, 2>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
-    // dense token lists (see wc_map3_kernel)
-    case 6: v3::launch<512, 2048, 1, true>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
-    case 7: v3::launch<512, 2048, 2, true>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
-    case 8: v3::launch<256, 1024, 1, true>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
-    case 9: v3::launch<1024, 4096, 1, true>(tx, nbytes, rep_base, g, o, aligned, ablate, stream); break;
-    default: return -1;
-  }
+  constexpr u64 CHUNK = (u64)v3::MAP_T * v3::SEG * v3::MAP_TPC;
+  const u64 nblocks = (nbytes + CHUNK - 1) / CHUNK;
+  hipLaunchKernelGGL((v3::wc_map3_kernel<v3::MAP_T, v3::MAP_SLOTS, v3::MAP_TPC>), dim3((unsigned)nblocks),
+                     dim3(v3::MAP_T), 0, stream, (const u8*)text, nbytes, rep_base, g, o, aligned);
   hipLaunchKernelGGL(v3::ovf_agg3_kernel, dim3(1024), dim3(256), 0, stream, o, g);
   return (int)hipGetLastError();
 }

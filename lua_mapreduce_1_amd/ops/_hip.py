@@ -27,7 +27,7 @@ _p = ctypes.c_void_p
 
 _SIGS = {
     "mr_count_tokens": [_p, _u64, _u64, _p, _p],
-    "mr_wc_map3": [_p, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _i32, _p, _p],
+    "mr_wc_map3": [_p, _u64, _u64, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _p],
     "mr_insert_received": [_p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p, _u64, _i32, _i32, _p, _p],
     "mr_memcpy_async": [_p, _p, _u64, _i32, _p],
     "mr_d2h_async": [_p, _p, _u64, _p],

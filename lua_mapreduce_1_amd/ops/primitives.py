@@ -227,13 +227,11 @@ class HashTable:
         self._ovf_next += 1
         return self._ovf, self._ovf_counter
 
-    def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, mode: int | None = None,
-                      stamps: torch.Tensor | None = None, src: torch.Tensor | None = None) -> None:
+    def wordcount_map(self, text: torch.Tensor, rep_base: int = 0, src: torch.Tensor | None = None) -> None:
         """Fused tokenize + exact key + combine of every whitespace token
         (value 1): csrc/hip/wordcount3.hip.  ``text`` sits at byte
         ``rep_base`` of the table's byte source ``src`` (default: ``text``
-        itself at 0).  ``mode`` = kernel config in the low byte, ablation
-        (timing only) in the high byte."""
+        itself at 0)."""
         nbytes = text.numel()
         if src is not None:
             self.src = src
@@ -241,14 +239,12 @@ class HashTable:
             self.src = text
         if nbytes == 0:
             return
-        if mode is None:
-            mode = TUNABLES.wc_config
         if self.is_cuda:
             assert text.dtype == torch.uint8 and text.is_contiguous()
             ovf, counter = self._overflow(nbytes)
             _hip.call("mr_wc_map3", _hip.ptr(text), nbytes, rep_base, *self._gtab(), self.cap,
                       _hip.ptr(ovf[0]), _hip.ptr(ovf[1]), _hip.ptr(ovf[2]), ovf[0].numel(), _hip.ptr(counter),
-                      mode, _hip.ptr(stamps) if stamps is not None else None, _hip.stream(self.device))
+                      _hip.stream(self.device))
         else:
             buf = _np(text)
             starts, lens = K.token_spans(buf)

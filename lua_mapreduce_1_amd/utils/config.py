@@ -38,11 +38,9 @@ class Tunables:
     coll_timeout: float = _knob("MR_COLL_TIMEOUT", 600.0,
                                 "collective timeout, s: a hung or dead rank fails its peers' collectives")
     spmd_fault: str = _knob("MR_SPMD_FAULT", "",
-                            "SPMD fault injection 'iteration:rank:raise|exit[:attempt]' at the start of that iteration")
+                            "SPMD fault injection 'iteration:rank:raise|exit[:attempt[:start|shuffle]]': that rank "
+                            "fails at the start of that iteration or after its map phase")
     # -- device data plane
-    wc_config: int = _knob("MR_WC_CONFIG", 6,
-                           "word-count map kernel launch shape (csrc/hip/wordcount3.hip mr_wc_map3 config: "
-                           "0-5 per-lane token walks, 6-9 dense token lists)")
     map_sparsity: int = _knob("MR_MAP_SPARSITY", 8,
                               "SPMD fold plane: after a map of at least MR_MAP_SPARSE_MIN_MB of input, later "
                               "maps get a table of this many slots per distinct key (power of two); sparse "

@@ -46,20 +46,19 @@ def test_wordcount_map_unaligned_and_chunks(gpu):
         assert _wc_dict(hi, lo, val, rep, tt) == _naive(text)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
-def test_wordcount_map3_configs_match_naive(gpu, cfg):
-    """Every v3 launch shape (threads / LDS slots / tiles per chunk) on tricky
-    bytes (long tokens crossing tiles, all whitespace kinds, NULs), aligned and
-    misaligned, in several launches into one table (per-launch overflow
-    counters), plus a tiny table that forces the overflow path."""
-    rng = np.random.default_rng(100 + cfg)
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_wordcount_map3_launches_match_naive(gpu, seed):
+    """The map kernel on tricky bytes (long tokens crossing tiles, all
+    whitespace kinds, NULs), aligned and misaligned, in several launches into
+    one table (per-launch overflow counters)."""
+    rng = np.random.default_rng(100 + seed)
     text = tricky_text(rng, 700_001)
     base = torch.frombuffer(bytearray(b"x" + text), dtype=torch.uint8).to(gpu)
     for t in (base[1:].contiguous(), base[1:]):
         tab = ops.HashTable(1 << 16, device=gpu)
         cut = [0, 12_345, 400_000, len(text)]
         for a, b in zip(cut[:-1], cut[1:]):  # a token cut by a launch boundary counts as two
-            tab.wordcount_map(t[a:b], rep_base=a, mode=cfg)
+            tab.wordcount_map(t[a:b], rep_base=a)
         hi, lo, val, rep = tab.compact()
         got = _wc_dict(hi, lo, val, rep, t)
         want = {}
