@@ -33,6 +33,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <set>
 #include <string>
@@ -47,6 +48,11 @@ enum Op : uint16_t {
   TASK_GET = 10, TASK_SET = 11, TASK_DROP = 12,
   JOB_INSERT = 20, JOB_REMOVE_STATUS = 21, JOB_FAIL_BROKEN = 22, JOB_COUNT = 23, JOB_CLAIM = 24,
   JOB_UPDATE = 25, JOB_GET = 26, JOB_LIST = 27, JOB_DROP = 28, JOB_STATS = 29, JOB_EXPIRE = 30,
+  // long polls: JOB_CLAIM_WAIT = wait_ms + JOB_CLAIM's args, blocks (up to
+  // wait_ms) until a job can be claimed or the task document changes;
+  // WAIT_CHANGE since, wait_ms -> the database's mutation count once it
+  // differs from `since` (or at the timeout)
+  JOB_CLAIM_WAIT = 31, WAIT_CHANGE = 32,
   ERR_INSERT = 40, ERR_TAKE = 41,
   BLOB_PUT = 50, BLOB_GET = 51, BLOB_LIST = 52, BLOB_DEL = 53,
   // batched forms (one round trip for all outputs of a job, all inputs of a
@@ -62,7 +68,8 @@ enum Status : int { WAITING = 0, RUNNING = 1, BROKEN = 2, FINISHED = 3, WRITTEN 
 bool is_mutating(uint16_t op) {
   switch (op) {
     case TASK_SET: case TASK_DROP: case JOB_INSERT: case JOB_REMOVE_STATUS: case JOB_FAIL_BROKEN:
-    case JOB_CLAIM: case JOB_UPDATE: case JOB_DROP: case JOB_EXPIRE: case ERR_INSERT: case ERR_TAKE:
+    case JOB_CLAIM: case JOB_CLAIM_WAIT: case JOB_UPDATE: case JOB_DROP: case JOB_EXPIRE: case ERR_INSERT:
+    case ERR_TAKE:
     case BLOB_PUT: case BLOB_DEL: case BLOB_PUT_MANY: case BLOB_DEL_MANY: case PT_OPEN: case PT_UPDATE: case PT_LOCK: case PT_UNLOCK: case PT_DROP:
     case DB_DROP:
       return true;
@@ -150,6 +157,10 @@ class Store {
   std::map<std::string, Db> dbs;
   FILE* journal = nullptr;
   bool replaying = false;
+  std::condition_variable cv;
+  std::map<std::string, uint64_t> ver;   // per database: mutations so far
+  std::map<std::string, uint64_t> tver;  // per database: task-document changes
+  bool unchanged = false;  // set by a mutating op that found nothing to change (wakes no long poll)
 
   // Executes one request; returns status (0 ok, 1 "not found / false", <0 error).
   int exec(uint16_t op, Reader& r, Writer& w) {
@@ -158,6 +169,11 @@ class Store {
     switch (op) {
       case PING: w.str("pong"); return 0;
       case TASK_GET: {
+        // the database's mutation count rides along as field "_ver" (also
+        // when there is no task): a long poll from that count waits for
+        // whatever changes after this read
+        w.str("_ver");
+        w.i((long long)ver[dbname]);
         if (!db.has_task) return 1;
         for (auto& kv : db.task) { w.str(kv.first); w.str(kv.second); }
         return 0;
@@ -189,6 +205,7 @@ class Store {
           else ++it;
         }
         w.i(n);
+        unchanged = n == 0;
         return 0;
       }
       case JOB_FAIL_BROKEN: {
@@ -198,6 +215,7 @@ class Store {
         for (auto& kv : c.jobs)
           if (kv.second.status == BROKEN && kv.second.repetitions >= maxrep) { kv.second.status = FAILED; ++n; }
         w.i(n);
+        unchanged = n == 0;
         return 0;
       }
       case JOB_COUNT: {
@@ -210,6 +228,9 @@ class Store {
         w.i(n);
         return 0;
       }
+      case JOB_CLAIM_WAIT:
+        r.str();  // wait_ms (the waiting is done by handle())
+        [[fallthrough]];
       case JOB_CLAIM: {
         // args: coll, worker, tmpname, time, claimable status mask, [ids...]
         Collection& c = db.colls[r.str()];
@@ -306,6 +327,7 @@ class Store {
           }
         }
         w.i(n);
+        unchanged = n == 0;
         return 0;
       }
       case ERR_INSERT: {
@@ -314,6 +336,7 @@ class Store {
         return 0;
       }
       case ERR_TAKE: {
+        unchanged = db.errors.empty();
         for (auto& e : db.errors) { w.str(e.first); w.str(e.second); }
         db.errors.clear();
         return 0;
@@ -436,15 +459,70 @@ class Store {
     fflush(journal);
   }
 
+  // Long polls: every mutation of a database bumps its count and wakes the
+  // waiters (one condition variable for the store; waits are short and few:
+  // one per idle worker and one for the server's monitor).
+
+  static std::string db_of(const std::string& body) {
+    Reader r{body.data() + 2, body.data() + body.size()};
+    return r.str();
+  }
+
+  // A claim that found nothing: wait for a mutation of the database and claim
+  // again, until the deadline; a change of the task document ends the wait
+  // (the worker re-reads the task: the phase may have changed).
+  int claim_wait(const std::string& body, Writer& w, std::unique_lock<std::mutex>& g) {
+    Reader r{body.data() + 2, body.data() + body.size()};
+    const std::string db = r.str();
+    const double ms = to_d(r.str());
+    if (!r.ok || !(ms > 0)) return 1;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds((long long)(ms * 1000.0));
+    const uint64_t tv = tver[db];
+    uint64_t v = ver[db];
+    for (;;) {
+      if (!cv.wait_until(g, deadline, [&] { return ver[db] != v; })) return 1;
+      if (tver[db] != tv) return 1;
+      v = ver[db];
+      Reader r2{body.data() + 2, body.data() + body.size()};
+      Writer w2;
+      const int st = exec(JOB_CLAIM_WAIT, r2, w2);
+      if (st != 1) {
+        w = std::move(w2);
+        return st;
+      }
+    }
+  }
+
+  int wait_change(Reader& r, Writer& w, std::unique_lock<std::mutex>& g) {
+    const std::string db = r.str();
+    const uint64_t since = (uint64_t)to_ll(r.str());
+    const double ms = to_d(r.str());
+    if (!r.ok) return -1;
+    if (ms > 0)
+      cv.wait_until(g, std::chrono::steady_clock::now() + std::chrono::microseconds((long long)(ms * 1000.0)),
+                    [&] { return ver[db] != since; });
+    w.i((long long)ver[db]);
+    return 0;
+  }
+
   int handle(const std::string& body, Writer& w) {
     if (body.size() < 2) return -1;
     uint16_t op;
     memcpy(&op, body.data(), 2);
     Reader r{body.data() + 2, body.data() + body.size()};
-    std::lock_guard<std::mutex> g(mu);
+    std::unique_lock<std::mutex> g(mu);
+    if (op == WAIT_CHANGE) return replaying ? 0 : wait_change(r, w, g);
+    unchanged = false;
     int st = exec(op, r, w);
     if (!r.ok) return -1;
+    if (op == JOB_CLAIM_WAIT && st == 1 && !replaying) st = claim_wait(body, w, g);
     if (is_mutating(op) && st >= 0) log(body);
+    if (is_mutating(op) && st == 0 && !unchanged) {  // (a claim that found nothing wakes nobody)
+      const std::string db = db_of(body);
+      ++ver[db];
+      if (op == TASK_SET || op == TASK_DROP || op == DB_DROP) ++tver[db];
+      cv.notify_all();
+    }
     return st;
   }
 

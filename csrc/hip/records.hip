@@ -67,6 +67,63 @@ __global__ void __launch_bounds__(256) rec_keys32_kernel(const u8* __restrict__ 
   }
 }
 
+// k32 (+ histograms) of rows of rb <= KT_MAXRB bytes, rb a multiple of 4:
+// each workgroup streams a tile of 256 whole rows into LDS with coalesced
+// 16-byte loads, then thread t takes row t's key from LDS.  A strided 4-byte
+// load per row (rec_keys32_kernel) makes one memory request per row; the tile
+// reads the same lines as full-width streaming requests.
+constexpr int KT_ROWS = 256, KT_MAXRB = 160;
+
+__global__ void __launch_bounds__(256) rec_keys32_tile_kernel(const u8* __restrict__ rec, u64 n, int rb, int kb,
+                                                              u32* __restrict__ k32, u32* __restrict__ ghist,
+                                                              int vec16) {
+  __shared__ __attribute__((aligned(16))) uint4 buf[KT_ROWS * KT_MAXRB / 16];
+  __shared__ u32 h[4][256];
+  const int t = threadIdx.x;
+  if (ghist) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) h[b][t] = 0;
+  }
+  u32* buf32 = reinterpret_cast<u32*>(buf);
+  const u8* buf8 = reinterpret_cast<const u8*>(buf);
+  const u64 ntiles = (n + KT_ROWS - 1) / KT_ROWS;
+  for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const u64 r0 = tile * KT_ROWS;
+    const u32 rows = (u32)min((u64)KT_ROWS, n - r0);
+    const u32 nwords = rows * (u32)(rb >> 2);
+    const u8* src = rec + r0 * (u64)rb;
+    __syncthreads();  // the previous tile's keys have been read
+    u32 w0 = 0;
+    if (vec16) {
+      const u32 nq = nwords >> 2;
+      const uint4* s4 = reinterpret_cast<const uint4*>(src);
+      for (u32 q = t; q < nq; q += KT_ROWS) {
+        typedef u32 v4u __attribute__((ext_vector_type(4)));
+        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s4 + q));
+        buf[q] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      w0 = nq << 2;
+    }
+    const u32* s32 = reinterpret_cast<const u32*>(src);
+    for (u32 w = w0 + t; w < nwords; w += KT_ROWS) buf32[w] = __builtin_nontemporal_load(s32 + w);
+    __syncthreads();
+    if ((u32)t < rows) {
+      const u32 k = be32(buf8 + (u32)t * (u32)rb, 0, kb, true);
+      k32[r0 + t] = k;
+      if (ghist) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 0xFFu], 1u);
+      }
+    }
+  }
+  if (ghist) {
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (h[b][t]) atomicAdd(&ghist[b * 256 + t], h[b][t]);
+  }
+}
+
 __global__ void rec_keys_kernel(const u8* __restrict__ rec, u64 n, int rb, int kb, u64* __restrict__ hi,
                                 u64* __restrict__ lo) {
   const bool words = (rb & 3) == 0;
@@ -203,6 +260,23 @@ extern "C" {
 
 // ghist: null, or a zeroed u32[8][256] that receives the digit histograms of k32
 int mr_rec_keys32(const void* rec, u64 n, int rb, int kb, void* k32, void* ghist, hipStream_t s) {
+  if (n == 0) return 0;
+  if (rb <= 0 || kb <= 0 || kb > rb || kb > 16) return -1;
+  if ((rb & 3) == 0 && rb <= rc::KT_MAXRB && ((uintptr_t)rec & 3) == 0) {
+    const u64 tiles = (n + rc::KT_ROWS - 1) / rc::KT_ROWS;
+    const unsigned g = (unsigned)(tiles < 4096 ? tiles : 4096);
+    const int vec16 = ((uintptr_t)rec & 15) == 0 && ((rb * rc::KT_ROWS) & 15) == 0;
+    hipLaunchKernelGGL(rc::rec_keys32_tile_kernel, dim3(g), dim3(256), 0, s, (const u8*)rec, n, rb, kb, (u32*)k32,
+                       (u32*)ghist, vec16);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL(rc::rec_keys32_kernel, dim3(rc_grid(n, ghist ? 2048 : 8192)), dim3(256), 0, s, (const u8*)rec, n,
+                     rb, kb, (u32*)k32, (u32*)ghist);
+  return (int)hipGetLastError();
+}
+
+// the per-row strided form (any width), for A/B against the tiled one
+int mr_rec_keys32_strided(const void* rec, u64 n, int rb, int kb, void* k32, void* ghist, hipStream_t s) {
   if (n == 0) return 0;
   if (rb <= 0 || kb <= 0 || kb > rb || kb > 16) return -1;
   hipLaunchKernelGGL(rc::rec_keys32_kernel, dim3(rc_grid(n, ghist ? 2048 : 8192)), dim3(256), 0, s, (const u8*)rec, n,

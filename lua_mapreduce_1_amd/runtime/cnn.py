@@ -179,6 +179,13 @@ class cnn:  # noqa: N801
         return [{"_id": i // 2, "worker": f[i].decode(), "msg": f[i + 1].decode("utf-8", "replace")}
                 for i in range(0, len(f), 2)]
 
+    def wait_change(self, since: int, timeout: float) -> int:
+        """Block until the database has changed since mutation count ``since``
+        (returned by an earlier call; -1 = return the current count now) or
+        ``timeout`` seconds pass; returns the current mutation count."""
+        _, f = self.connect().request("WAIT_CHANGE", self.dbname, since, max(0.0, timeout) * 1000.0)
+        return int(f[0])
+
     def remove_errors(self, ids) -> None:
         # errors are removed atomically by get_errors (ERR_TAKE)
         return None
@@ -241,11 +248,19 @@ class JobCollection:
     def count(self, *statuses: int) -> int:
         return int(self.c.request("JOB_COUNT", self.db, self.ns, status_mask(*statuses))[1][0])
 
-    def claim(self, worker: str, tmpname: str, t: float, statuses=(0, 2), only_ids=None) -> dict | None:
+    def claim(self, worker: str, tmpname: str, t: float, statuses=(0, 2), only_ids=None,
+              wait: float = 0.0) -> dict | None:
+        """Claim one job atomically.  ``wait`` > 0 (seconds): a long poll —
+        when nothing is claimable the coordinator holds the request until a
+        job can be claimed, the task document changes, or ``wait`` expires."""
         ids = list(only_ids) if only_ids else []
         if only_ids is not None and not ids:
             return None
-        st, f = self.c.request("JOB_CLAIM", self.db, self.ns, worker, tmpname, t, status_mask(*statuses), *ids)
+        if wait > 0:
+            st, f = self.c.request("JOB_CLAIM_WAIT", self.db, wait * 1000.0, self.ns, worker, tmpname, t,
+                                   status_mask(*statuses), *ids)
+        else:
+            st, f = self.c.request("JOB_CLAIM", self.db, self.ns, worker, tmpname, t, status_mask(*statuses), *ids)
         return decode_jobs(f)[0] if st == 0 else None
 
     def update(self, job_id: str, guard_tmpname: str = "", **fields) -> dict | None:

@@ -21,7 +21,7 @@ DEFAULT_PORT = 27027
 
 OP = dict(PING=1, TASK_GET=10, TASK_SET=11, TASK_DROP=12, JOB_INSERT=20, JOB_REMOVE_STATUS=21,
           JOB_FAIL_BROKEN=22, JOB_COUNT=23, JOB_CLAIM=24, JOB_UPDATE=25, JOB_GET=26, JOB_LIST=27, JOB_DROP=28,
-          JOB_STATS=29, JOB_EXPIRE=30, ERR_INSERT=40, ERR_TAKE=41, BLOB_PUT=50, BLOB_GET=51, BLOB_LIST=52,
+          JOB_STATS=29, JOB_EXPIRE=30, JOB_CLAIM_WAIT=31, WAIT_CHANGE=32, ERR_INSERT=40, ERR_TAKE=41, BLOB_PUT=50, BLOB_GET=51, BLOB_LIST=52,
           BLOB_DEL=53, BLOB_PUT_MANY=54, BLOB_GET_MANY=55, BLOB_DEL_MANY=56, PT_OPEN=60, PT_UPDATE=61,
           PT_LOCK=62, PT_UNLOCK=63, PT_DROP=64, DB_DROP=70, COLLECTIONS=71, SHUTDOWN=99)
 

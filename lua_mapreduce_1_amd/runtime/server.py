@@ -20,6 +20,7 @@ import re
 import sys
 
 from .. import utils
+from ..utils.config import TUNABLES
 from ..utils import STATUS, TASK_STATUS
 from ..utils.tuple import tuple as tuple_
 from . import codec, fs as fsmod, modules
@@ -101,6 +102,15 @@ class server:  # noqa: N801
         self.configured = True
 
     # ------------------------------------------------------------------------
+    def _pause(self) -> None:
+        """Between two monitor passes: a long poll that returns as soon as a
+        worker changes something (a claim, a written job, an error), at most
+        one poll period (MR_LONG_POLL; else a plain sleep)."""
+        if TUNABLES.long_poll:
+            self._ver = self.cnn.wait_change(getattr(self, "_ver", -1), self.poll_sleep)
+        else:
+            utils.sleep(self.poll_sleep)
+
     def _monitor(self, ns: str):
         jobs = self.cnn.jobs(ns)
         n = jobs.count()
@@ -237,14 +247,14 @@ class server:  # noqa: N801
                 step, map_count = self._prepare_map()
                 self._log("# \t Map execution, size= %d\n" % map_count)
                 for _ in step:
-                    utils.sleep(self.poll_sleep)
+                    self._pause()
             map_count = self.cnn.jobs(self.task.get_map_jobs_ns()).count()
             self._log("# \t Preparing Reduce\n")
             step, _ = self._prepare_reduce()
             red_count = self.cnn.jobs(self.task.get_red_jobs_ns()).count()
             self._log("# \t Reduce execution, num_files= %d  size= %d\n" % (red_count * map_count, red_count))
             for _ in step:
-                utils.sleep(self.poll_sleep)
+                self._pause()
             end_time = utils.time()
             total_time = end_time - start_time
             self.task.insert_finished_time(end_time)

@@ -34,6 +34,8 @@ class task:  # noqa: N801
     count_idle_iterations = 0
 
     def __init__(self, cnn):
+        self.claimed_or_waited = False
+        self.version = -1
         self.cnn = cnn
         dbname = cnn.get_dbname()
         self.ns = dbname + ".task"
@@ -92,8 +94,11 @@ class task:  # noqa: N801
 
     def update(self) -> None:
         st, f = self.cnn.connect().request("TASK_GET", self.cnn.get_dbname())
+        tbl = {f[i].decode(): json.loads(f[i + 1]) for i in range(0, len(f), 2)}
+        # the coordinator's mutation count at this read (long polls wait for
+        # a change after it)
+        self.version = int(tbl.pop("_ver", -1))
         if st == 0:
-            tbl = {f[i].decode(): json.loads(f[i + 1]) for i in range(0, len(f), 2)}
             self._set_status_local(tbl.get("status"), tbl)
         else:
             self.tbl = None
@@ -172,13 +177,18 @@ class task:  # noqa: N801
         cls.cache_inv_map_ids = set()
 
     # -- job claim -------------------------------------------------------------
-    def take_next_job(self, tmpname: str, worker_name: str | None = None):
-        """Returns (task_status, job | None)."""
+    def take_next_job(self, tmpname: str, worker_name: str | None = None, wait: float = 0.0):
+        """Returns (task_status, job | None).  ``wait`` > 0: the last claim
+        is a long poll of up to ``wait`` seconds (``claimed_or_waited`` tells
+        the caller whether a claim was made at all: not while the task is in
+        WAIT or FINISHED)."""
         from .job import job  # local import (job imports task-level helpers)
 
+        self.claimed_or_waited = False
         status = self.get_task_status()
         if status in (TASK_STATUS.WAIT, TASK_STATUS.FINISHED):
             return status, None
+        self.claimed_or_waited = True
         jobs = self.cnn.jobs(self.get_jobs_ns())
         worker = worker_name or utils.get_hostname()
         t = utils.time()
@@ -191,9 +201,9 @@ class task:  # noqa: N801
                 cls.count_idle_iterations += 1
                 if cls.count_idle_iterations <= utils.MAX_IDLE_COUNT:
                     claim_kwargs = {"statuses": (STATUS.BROKEN,)}
-                job_tbl = jobs.claim(worker, tmpname_summary(tmpname), t, **claim_kwargs)
+                job_tbl = jobs.claim(worker, tmpname_summary(tmpname), t, wait=wait, **claim_kwargs)
         else:
-            job_tbl = jobs.claim(worker, tmpname_summary(tmpname), t, **claim_kwargs)
+            job_tbl = jobs.claim(worker, tmpname_summary(tmpname), t, wait=wait, **claim_kwargs)
         if job_tbl is None:
             return TASK_STATUS.WAIT, None
         type(self).count_idle_iterations = 0

@@ -123,10 +123,11 @@ class worker:  # noqa: N801
         iter_sleep = self.poll_sleep
         ntasks = 0
         job_done = False
+        long_poll = TUNABLES.long_poll
         while it < self.max_iter and ntasks < self.max_tasks and not self._stop.is_set():
             while not self._stop.is_set():
                 task.update()
-                status, j = task.take_next_job(self.tmpname, self.name)
+                status, j = task.take_next_job(self.tmpname, self.name, wait=self.poll_sleep if long_poll else 0.0)
                 self.current_job = j
                 if j is not None:
                     if not job_done:
@@ -143,7 +144,12 @@ class worker:  # noqa: N801
                         break
                     self._print("# \t Running, waiting for new jobs...")
                     self.cnn.flush_pending_inserts(0)
-                    utils.sleep(self.poll_sleep)
+                    if not long_poll:
+                        utils.sleep(self.poll_sleep)
+                    elif not task.claimed_or_waited:
+                        # the task is not claimable yet (server preparing a phase): wait for a
+                        # change after the task read
+                        self.cnn.wait_change(task.version, self.poll_sleep)
                 if task.finished():
                     break
             self.cnn.flush_pending_inserts()
@@ -158,7 +164,10 @@ class worker:  # noqa: N801
             if ntasks < self.max_tasks:
                 self._print("# WAITING...\tntasks: %d/%d\tit: %d/%d\tsleep: %.1f" %
                             (ntasks, self.max_tasks, it, self.max_iter, iter_sleep))
-                utils.sleep(iter_sleep)
+                if long_poll:  # the next task wakes the worker at once
+                    self.cnn.wait_change(task.version, iter_sleep)
+                else:
+                    utils.sleep(iter_sleep)
                 iter_sleep = min(self.max_sleep, iter_sleep * 1.5)
             it += 1
 

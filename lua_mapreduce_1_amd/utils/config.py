@@ -29,6 +29,9 @@ def _knob(env: str, default, doc: str):
 class Tunables:
     # -- reference constants (utils.lua:24-56) that are tunable here
     default_sleep: float = _knob("MR_DEFAULT_SLEEP", 1.0, "poll period of server and workers, s (utils.lua:28)")
+    long_poll: bool = _knob("MR_LONG_POLL", True,
+                            "server/worker: wait for coordinator changes (long-poll claims, change waits) instead "
+                            "of sleeping a poll period; the poll period becomes the longest wait")
     job_lease: float = _knob("MR_JOB_LEASE", 120.0,
                              "a RUNNING job whose worker stopped heart-beating this long is re-queued, s (new)")
     fault: str = _knob("MR_FAULT", "",
