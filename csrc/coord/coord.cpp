@@ -185,15 +185,22 @@ class Store {
       }
       case TASK_DROP: db.task.clear(); db.has_task = false; return 0;
       case JOB_INSERT: {
+        // one or more (id, value, creation time) triples: a batch is one round trip
         Collection& c = db.colls[r.str()];
-        Job j;
-        j.id = r.str(); j.value = r.str(); j.creation_time = to_d(r.str());
-        if (!r.ok) return -1;
-        if (c.jobs.count(j.id)) return 1;  // duplicate key (reference relied on mongo rejection)
-        j.seq = c.next_seq++;
-        c.order[j.seq] = j.id;
-        c.jobs[j.id] = j;
-        return 0;
+        int st = 0;
+        do {
+          Job j;
+          j.id = r.str(); j.value = r.str(); j.creation_time = to_d(r.str());
+          if (!r.ok) return -1;
+          if (c.jobs.count(j.id)) {  // duplicate key (reference relied on mongo rejection)
+            st = 1;
+            continue;
+          }
+          j.seq = c.next_seq++;
+          c.order[j.seq] = j.id;
+          c.jobs[j.id] = j;
+        } while (r.more());
+        return st;
       }
       case JOB_REMOVE_STATUS: {
         Collection& c = db.colls[r.str()];

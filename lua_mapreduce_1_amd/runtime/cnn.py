@@ -213,10 +213,14 @@ class cnn:  # noqa: N801
         self.pending_callbacks = {}
 
     def _insert_batch(self, ns: str, docs: list[dict]) -> None:
+        """Insert documents in requests of up to 4096 jobs each (duplicates
+        are skipped, as a unique index would reject them)."""
         c = self.connect()
-        for d in docs:
-            c.request("JOB_INSERT", self.dbname, ns, d["_id"], json.dumps(d.get("value")),
-                      d.get("creation_time", utils.time()))
+        for a in range(0, len(docs), 4096):
+            fields = []
+            for d in docs[a:a + 4096]:
+                fields += [d["_id"], json.dumps(d.get("value")), d.get("creation_time", utils.time())]
+            c.request("JOB_INSERT", self.dbname, ns, *fields)
 
     # -- job collections (the <db>.map_jobs / <db>.red_jobs namespaces) -------
     def jobs(self, ns: str) -> "JobCollection":
