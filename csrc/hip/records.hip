@@ -9,10 +9,12 @@
 //                  histograms of k32 in the same pass (no histogram pass);
 //   (sort.hip)   : 4 onesweep passes over (k32, u32 row) — u32 keys: 16 bytes
 //                  moved per row and pass instead of 24 with u64 keys;
-//   rec_tie_fixup: rows equal in k32 ordered by key bytes 4..kb-1 read from the
+//   rec_tie_*    : rows equal in k32 ordered by key bytes 4..kb-1 read from the
 //                  rows themselves (uniform keys: ~2 % of the rows sit in such
-//                  a run, almost all of length 2); a run longer than 64 sets
-//                  *bad and the caller sorts the full (hi, lo) key instead;
+//                  a run, almost all of length 2: swapped in registers; longer
+//                  runs listed and insertion-sorted by a second kernel); a run
+//                  longer than 64 sets *bad and the caller sorts the full
+//                  (hi, lo) key instead;
 //   rec_gather   : output row i = input row perm[i], 8 independent words per
 //                  thread in flight (the random 100-byte row reads touch 1.77
 //                  128-byte lines each on average: this is the bound).
@@ -67,63 +69,6 @@ __global__ void __launch_bounds__(256) rec_keys32_kernel(const u8* __restrict__ 
   }
 }
 
-// k32 (+ histograms) of rows of rb <= KT_MAXRB bytes, rb a multiple of 4:
-// each workgroup streams a tile of 256 whole rows into LDS with coalesced
-// 16-byte loads, then thread t takes row t's key from LDS.  A strided 4-byte
-// load per row (rec_keys32_kernel) makes one memory request per row; the tile
-// reads the same lines as full-width streaming requests.
-constexpr int KT_ROWS = 256, KT_MAXRB = 160;
-
-__global__ void __launch_bounds__(256) rec_keys32_tile_kernel(const u8* __restrict__ rec, u64 n, int rb, int kb,
-                                                              u32* __restrict__ k32, u32* __restrict__ ghist,
-                                                              int vec16) {
-  __shared__ __attribute__((aligned(16))) uint4 buf[KT_ROWS * KT_MAXRB / 16];
-  __shared__ u32 h[4][256];
-  const int t = threadIdx.x;
-  if (ghist) {
-#pragma unroll
-    for (int b = 0; b < 4; ++b) h[b][t] = 0;
-  }
-  u32* buf32 = reinterpret_cast<u32*>(buf);
-  const u8* buf8 = reinterpret_cast<const u8*>(buf);
-  const u64 ntiles = (n + KT_ROWS - 1) / KT_ROWS;
-  for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const u64 r0 = tile * KT_ROWS;
-    const u32 rows = (u32)min((u64)KT_ROWS, n - r0);
-    const u32 nwords = rows * (u32)(rb >> 2);
-    const u8* src = rec + r0 * (u64)rb;
-    __syncthreads();  // the previous tile's keys have been read
-    u32 w0 = 0;
-    if (vec16) {
-      const u32 nq = nwords >> 2;
-      const uint4* s4 = reinterpret_cast<const uint4*>(src);
-      for (u32 q = t; q < nq; q += KT_ROWS) {
-        typedef u32 v4u __attribute__((ext_vector_type(4)));
-        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s4 + q));
-        buf[q] = make_uint4(v.x, v.y, v.z, v.w);
-      }
-      w0 = nq << 2;
-    }
-    const u32* s32 = reinterpret_cast<const u32*>(src);
-    for (u32 w = w0 + t; w < nwords; w += KT_ROWS) buf32[w] = __builtin_nontemporal_load(s32 + w);
-    __syncthreads();
-    if ((u32)t < rows) {
-      const u32 k = be32(buf8 + (u32)t * (u32)rb, 0, kb, true);
-      k32[r0 + t] = k;
-      if (ghist) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 0xFFu], 1u);
-      }
-    }
-  }
-  if (ghist) {
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      if (h[b][t]) atomicAdd(&ghist[b * 256 + t], h[b][t]);
-  }
-}
-
 __global__ void rec_keys_kernel(const u8* __restrict__ rec, u64 n, int rb, int kb, u64* __restrict__ hi,
                                 u64* __restrict__ lo) {
   const bool words = (rb & 3) == 0;
@@ -141,26 +86,63 @@ __device__ __forceinline__ void key_rest(const u8* row, int kb, bool words, u64&
   b = be32(row, 12, kb, words);
 }
 
-// Runs of equal k32 in the sorted prefixes: insertion sort of the run's rows
-// by the rest of their keys (one thread per run; stable: the LSD sort left
-// equal keys in input order).
-__global__ void rec_tie_fixup_kernel(const u32* __restrict__ sk, u32* __restrict__ perm, const u8* __restrict__ rec,
-                                     u64 n, int rb, int kb, u32* __restrict__ bad) {
+// Runs of equal k32 in the sorted prefixes, ordered by the rest of their keys
+// (bytes 4..kb-1 read from the rows; stable: the LSD sort left equal keys in
+// input order).  Uniform keys: ~2 % of the rows sit in a run, almost all of
+// length 2 — rec_tie_pairs_kernel swaps those in registers and appends the
+// start of every longer run to a list; rec_tie_runs_kernel sorts the listed
+// runs (insertion sort, one thread per run).  A run longer than 64 sets *bad
+// and the caller sorts the full (hi, lo) key instead.
+constexpr int TIE_MAX = 64;
+
+__global__ void __launch_bounds__(256) rec_tie_pairs_kernel(const u32* __restrict__ sk, u32* __restrict__ perm,
+                                                            const u8* __restrict__ rec, u64 n, int rb, int kb,
+                                                            u32* __restrict__ bad, u64* __restrict__ runs,
+                                                            unsigned long long* __restrict__ nruns, u64 runs_cap) {
   const bool words = (rb & 3) == 0;
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += stride) {
     const u32 h = sk[i];
     if (sk[i + 1] != h || (i > 0 && sk[i - 1] == h)) continue;
+    if (kb <= 4) continue;  // the prefix is the whole key
+    if (i + 2 < n && sk[i + 2] == h) {  // a run of 3 or more
+      const unsigned long long k = atomicAdd(nruns, 1ull);
+      if (k < runs_cap) runs[k] = i;
+      else atomicOr(bad, 1u);
+      continue;
+    }
+    const u32 p0 = perm[i], p1 = perm[i + 1];
+    u64 a0, a1;
+    u32 b0, b1;
+    key_rest(rec + (u64)clamp_row(p0, n) * rb, kb, words, a0, b0);
+    key_rest(rec + (u64)clamp_row(p1, n) * rb, kb, words, a1, b1);
+    if (a0 > a1 || (a0 == a1 && b0 > b1)) {
+      perm[i] = p1;
+      perm[i + 1] = p0;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64) rec_tie_runs_kernel(const u32* __restrict__ sk, u32* __restrict__ perm,
+                                                          const u8* __restrict__ rec, u64 n, int rb, int kb,
+                                                          u32* __restrict__ bad, const u64* __restrict__ runs,
+                                                          const unsigned long long* __restrict__ nruns,
+                                                          u64 runs_cap) {
+  const bool words = (rb & 3) == 0;
+  const u64 m_runs = min((u64)*nruns, runs_cap);
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x; x < m_runs; x += stride) {
+    const u64 i = runs[x];
+    const u32 h = sk[i];
     u64 e = i + 2;
-    while (e < n && sk[e] == h && e - i <= 64) ++e;
-    if (e - i > 64) {
+    while (e < n && sk[e] == h && e - i <= TIE_MAX) ++e;
+    if (e - i > TIE_MAX) {
       atomicOr(bad, 1u);
       continue;
     }
-    if (kb <= 4) continue;  // the prefix is the whole key
-    u64 ra[64];
-    u32 rb2[64];
-    u32 p[64];
+    u64 ra[TIE_MAX];
+    u32 rb2[TIE_MAX];
+    u32 p[TIE_MAX];
     const int m = (int)(e - i);
     for (int a = 0; a < m; ++a) {
       p[a] = perm[i + a];
@@ -262,23 +244,6 @@ extern "C" {
 int mr_rec_keys32(const void* rec, u64 n, int rb, int kb, void* k32, void* ghist, hipStream_t s) {
   if (n == 0) return 0;
   if (rb <= 0 || kb <= 0 || kb > rb || kb > 16) return -1;
-  if ((rb & 3) == 0 && rb <= rc::KT_MAXRB && ((uintptr_t)rec & 3) == 0) {
-    const u64 tiles = (n + rc::KT_ROWS - 1) / rc::KT_ROWS;
-    const unsigned g = (unsigned)(tiles < 4096 ? tiles : 4096);
-    const int vec16 = ((uintptr_t)rec & 15) == 0 && ((rb * rc::KT_ROWS) & 15) == 0;
-    hipLaunchKernelGGL(rc::rec_keys32_tile_kernel, dim3(g), dim3(256), 0, s, (const u8*)rec, n, rb, kb, (u32*)k32,
-                       (u32*)ghist, vec16);
-    return (int)hipGetLastError();
-  }
-  hipLaunchKernelGGL(rc::rec_keys32_kernel, dim3(rc_grid(n, ghist ? 2048 : 8192)), dim3(256), 0, s, (const u8*)rec, n,
-                     rb, kb, (u32*)k32, (u32*)ghist);
-  return (int)hipGetLastError();
-}
-
-// the per-row strided form (any width), for A/B against the tiled one
-int mr_rec_keys32_strided(const void* rec, u64 n, int rb, int kb, void* k32, void* ghist, hipStream_t s) {
-  if (n == 0) return 0;
-  if (rb <= 0 || kb <= 0 || kb > rb || kb > 16) return -1;
   hipLaunchKernelGGL(rc::rec_keys32_kernel, dim3(rc_grid(n, ghist ? 2048 : 8192)), dim3(256), 0, s, (const u8*)rec, n,
                      rb, kb, (u32*)k32, (u32*)ghist);
   return (int)hipGetLastError();
@@ -292,10 +257,16 @@ int mr_rec_keys(const void* rec, u64 n, int rb, int kb, void* hi, void* lo, hipS
   return (int)hipGetLastError();
 }
 
-int mr_rec_tie_fixup(const void* sk, void* perm, const void* rec, u64 n, int rb, int kb, void* bad, hipStream_t s) {
+// ws: u64 scratch of 1 + ws_cap words (a run counter, then run starts)
+int mr_rec_tie_fixup(const void* sk, void* perm, const void* rec, u64 n, int rb, int kb, void* bad, void* ws,
+                     u64 ws_cap, hipStream_t s) {
   if (n < 2) return 0;
-  hipLaunchKernelGGL(rc::rec_tie_fixup_kernel, dim3(rc_grid(n)), dim3(256), 0, s, (const u32*)sk, (u32*)perm,
-                     (const u8*)rec, n, rb, kb, (u32*)bad);
+  u64* w = (u64*)ws;
+  hipMemsetAsync(w, 0, sizeof(u64), s);
+  hipLaunchKernelGGL(rc::rec_tie_pairs_kernel, dim3(rc_grid(n)), dim3(256), 0, s, (const u32*)sk, (u32*)perm,
+                     (const u8*)rec, n, rb, kb, (u32*)bad, w + 1, (unsigned long long*)w, ws_cap);
+  hipLaunchKernelGGL(rc::rec_tie_runs_kernel, dim3(256), dim3(64), 0, s, (const u32*)sk, (u32*)perm, (const u8*)rec,
+                     n, rb, kb, (u32*)bad, (const u64*)(w + 1), (const unsigned long long*)w, ws_cap);
   return (int)hipGetLastError();
 }
 

@@ -60,6 +60,17 @@ def keys(rec: torch.Tensor, kb: int) -> tuple[torch.Tensor, torch.Tensor]:
     return torch.from_numpy(hi.view(np.int64)), torch.from_numpy(lo.view(np.int64))
 
 
+_TIE_WS: dict = {}
+
+
+def _tie_ws(d, cap: int) -> torch.Tensor:
+    """Scratch of the tie fix-up (a run counter + run starts), per device."""
+    w = _TIE_WS.get(d)
+    if w is None or w.numel() < cap + 1:
+        w = _TIE_WS[d] = torch.empty(cap + 1, dtype=torch.int64, device=d)
+    return w
+
+
 def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: torch.Tensor | None = None):
     """(permutation int32 (int64 on CPU), sorted 32-bit key prefixes) of the
     rows in key order (stable).  GPU: pass ``k32``/``ghist`` from
@@ -77,8 +88,10 @@ def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: tor
         k32 = keys32(rec, kb, ghist)
     perm, sk = sort_keys32(k32, ghist)
     bad = torch.zeros(1, dtype=torch.int32, device=d)
+    cap = max(1024, n // 256)
+    ws = _tie_ws(d, cap)
     _hip.call("mr_rec_tie_fixup", _hip.ptr(sk), _hip.ptr(perm), _hip.ptr(rec), n, rb, kb, _hip.ptr(bad),
-              _hip.stream(d))
+              _hip.ptr(ws), cap, _hip.stream(d))
     if int(bad.item()) or sort_error(d):
         # skewed keys (a prefix shared by more than 64 rows), or a given-up
         # look-back: sort the full key words

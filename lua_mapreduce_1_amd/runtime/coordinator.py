@@ -107,18 +107,26 @@ class Client:
             finally:
                 self._sock = None
 
-    def _recv(self, n: int) -> bytes:
-        buf = bytearray()
-        while len(buf) < n:
-            chunk = self._sock.recv(n - len(buf))
-            if not chunk:
+    def _recv(self, n: int) -> bytearray:
+        """Exactly n bytes, received straight into one buffer."""
+        buf = bytearray(n)
+        mv = memoryview(buf)
+        got = 0
+        while got < n:
+            k = self._sock.recv_into(mv[got:], n - got)
+            if not k:
                 raise ConnectionError("coordinator closed the connection")
-            buf += chunk
-        return bytes(buf)
+            got += k
+        return buf
 
     def request(self, op: str, *fields) -> tuple[int, list[bytes]]:
-        body = struct.pack("<H", OP[op]) + b"".join(struct.pack("<I", len(b)) + b for b in map(_enc, fields))
-        msg = struct.pack("<I", len(body)) + body
+        parts = [b"", struct.pack("<H", OP[op])]
+        for b in map(_enc, fields):
+            parts.append(struct.pack("<I", len(b)))
+            parts.append(b)
+        body_len = sum(len(x) for x in parts)
+        parts[0] = struct.pack("<I", body_len)
+        msg = b"".join(parts)
         with self._lock:
             for attempt in (0, 1):  # reconnect once (cnn.lua:34-39 auto-reconnect)
                 try:
@@ -132,11 +140,13 @@ class Client:
                     self.close()
                     if attempt:
                         raise
-        (status,) = struct.unpack("<i", data[:4])
+        (status,) = struct.unpack_from("<i", data, 0)
         out, p = [], 4
-        while p < len(data):
-            (ln,) = struct.unpack("<I", data[p:p + 4])
-            out.append(data[p + 4:p + 4 + ln])
+        mv = memoryview(data)
+        end = len(data)
+        while p < end:
+            (ln,) = struct.unpack_from("<I", data, p)
+            out.append(bytes(mv[p + 4:p + 4 + ln]))
             p += 4 + ln
         if status < 0:
             raise CoordError(f"coordinator error {status} on {op}")

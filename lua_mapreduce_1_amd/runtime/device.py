@@ -49,6 +49,9 @@ def default_device():
     return torch.device("cpu")
 
 
+_CTX_CACHE: dict = {}
+
+
 class DeviceMapContext:
     """State of one device map job: the hash table and ONE contiguous device
     byte arena holding every key-byte source the job emitted from (input
@@ -67,6 +70,27 @@ class DeviceMapContext:
         self.base = 0
         self.host_pairs: list[tuple[bytes, int]] = []
         self.emit = DeviceEmitter(self)
+
+    @classmethod
+    def for_job(cls, op: str = "sum", capacity: int = 1 << 20, device=None) -> "DeviceMapContext":
+        """A worker's device map context, kept across its jobs: the HBM table
+        (reset, one kernel) and the byte arena are reused instead of being
+        allocated and cleared per job.  Callers hold PLANE_LOCK."""
+        d = torch.device(device) if device is not None else default_device()
+        key = (str(d), op, int(capacity))
+        ctx = _CTX_CACHE.get(key)
+        if ctx is None:
+            if len(_CTX_CACHE) >= 4:
+                _CTX_CACHE.clear()
+            ctx = _CTX_CACHE[key] = cls(d, op, capacity)
+        else:
+            STATS["maps_" + d.type] = STATS.get("maps_" + d.type, 0) + 1
+            ctx.table.reset()
+            ctx.base = 0
+            ctx.sources = []
+            ctx.host_pairs = []
+            ctx.table.src = ctx.arena
+        return ctx
 
     def add_source(self, t: torch.Tensor) -> tuple[int, torch.Tensor]:
         """Append ``t``'s bytes to the arena; returns (offset, arena view of

@@ -317,7 +317,7 @@ class job:  # noqa: N801
         extra = self.task_tbl.get("extra") or {}
         spec = modules.field(pmod, "device_partition")
         nparts = int(extra.get("num_partitions") or (spec[1] if spec else 0) or 1)
-        ctx = dev.DeviceMapContext(op=op, capacity=int(extra.get("table_capacity") or 1 << 20))
+        ctx = dev.DeviceMapContext.for_job(op=op, capacity=int(extra.get("table_capacity") or 1 << 20))
         modules.field(self.module, "device_mapfn")(map_key, map_value, ctx.emit)
         ctx.flush_host_pairs()
         self.mark_as_finished()
