@@ -99,6 +99,7 @@ _SIGS = {
     "mr_radix_onesweep_k32": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p, _u32, _p, _i32, _p],
     "mr_rec_keys32": [_p, _u64, _i32, _i32, _p, _p, _p],
     "mr_rec_keys": [_p, _u64, _i32, _i32, _p, _p, _p],
+    "mr_rec_gather_rows": [_p, _p, _u64, _i32, _p, _p],
     "mr_rec_tie_fixup": [_p, _p, _p, _u64, _i32, _i32, _p, _p, _u64, _p],
     "mr_rec_gather": [_p, _p, _u64, _i32, _p, _p],
     "mr_rec_dest32": [_p, _u64, _p, _u32, _p, _p],
