@@ -72,12 +72,7 @@ _SIGS = {
     "mr_ii_seg_gather": [_p, _p, _p, _u64, _u64, _p, _p, _p],
     "mr_ts_gen": [_p, _u64, _u64, _u64, _p],
     "mr_ts_keys": [_p, _u64, _p, _p, _p, _p],
-    "mr_ts_dest": [_p, _u64, _p, _u32, _p, _p],
-    "mr_ts_gather": [_p, _p, _u64, _p, _p],
     "mr_ts_checksum": [_p, _u64, _p, _p],
-    "mr_ts_tie_fixup": [_p, _p, _p, _u64, _p, _p],
-    "mr_ts_gather_mode": [_p, _p, _u64, _p, _i32, _i32, _p],
-    "mr_ts_tie_fixup2": [_p, _p, _p, _u64, _p, _i32, _p],
     "mr_ts_unsorted": [_p, _p, _u64, _p, _p],
     "mr_pack_by_dest": [_p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, ctypes.c_longlong, _p, _p, _i32, _p],
     "mr_fix_loc": [_p, _u64, _p, _p, _u32, _p, _p],

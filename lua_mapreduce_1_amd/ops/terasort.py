@@ -1,5 +1,7 @@
 """TeraSort record primitives (HIP kernels in ``csrc/hip/terasort.hip``; NumPy
-on CPU tensors — the CPU path is the executable specification).
+on CPU tensors — the CPU path is the executable specification): the TeraGen
+analogue and the checks of a sorted output (full keys, checksum, order).  The
+sort itself is the record plane's (ops/records.py).
 
 Records: 100 bytes = 10-byte key + 90-byte value, row-major uint8 tensors of
 shape [n, 100].  Sort order: unsigned bytewise on the key = (hi, lo) with
@@ -47,9 +49,9 @@ def generate(n: int, first: int, seed: int, device="cpu") -> torch.Tensor:
 
 
 def keys(rec: torch.Tensor, ghist: torch.Tensor | None = None):
-    """(hi, lo) int64 sort words of each record.  ``ghist`` (GPU, a zeroed
-    int32 [2048]): also receives the digit histograms of hi's top 32 bits,
-    for :func:`sort_perm` (the sort then skips its histogram pass)."""
+    """(hi, lo) int64 sort words of each record (validation: order checks).
+    ``ghist`` (GPU, a zeroed int32 [2048]): also receives the digit
+    histograms of hi's top 32 bits."""
     n = rec.shape[0]
     if rec.is_cuda:
         hi = torch.empty(n, dtype=torch.int64, device=rec.device)
@@ -61,30 +63,6 @@ def keys(rec: torch.Tensor, ghist: torch.Tensor | None = None):
     hi = np.ascontiguousarray(a[:, 0:8]).view(">u8").reshape(n).astype(np.uint64)
     lo = a[:, 8].astype(np.uint64) << np.uint64(8) | a[:, 9].astype(np.uint64)
     return torch.from_numpy(hi.view(np.int64)), torch.from_numpy(lo.view(np.int64))
-
-
-def dest_of(hi: torch.Tensor, splitters: torch.Tensor) -> torch.Tensor:
-    """Number of splitters <= hi (unsigned), int32."""
-    if hi.is_cuda:
-        out = torch.empty(hi.numel(), dtype=torch.int32, device=hi.device)
-        sp = splitters.to(hi.device).contiguous()
-        _hip.call("mr_ts_dest", _hip.ptr(hi), hi.numel(), _hip.ptr(sp), sp.numel(), _hip.ptr(out),
-                  _hip.stream(hi.device))
-        return out
-    h = hi.numpy().view(np.uint64)
-    s = splitters.numpy().view(np.uint64)
-    return torch.from_numpy(np.searchsorted(s, h, side="right").astype(np.int32))
-
-
-def gather(rec: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
-    """rec[perm] (rows)."""
-    n = perm.numel()
-    if rec.is_cuda:
-        out = torch.empty((n, REC), dtype=torch.uint8, device=rec.device)
-        p = perm if perm.dtype == torch.int32 else perm.to(torch.int32)
-        _hip.call("mr_ts_gather", _hip.ptr(rec), _hip.ptr(p.contiguous()), n, _hip.ptr(out), _hip.stream(rec.device))
-        return out
-    return rec[perm.long()]
 
 
 def checksum(rec: torch.Tensor) -> int:
@@ -119,25 +97,3 @@ def unsorted_pairs(hi: torch.Tensor, lo: torch.Tensor) -> int:
     return int(np.count_nonzero((h[:-1] > h[1:]) | ((h[:-1] == h[1:]) & (lw[:-1] > lw[1:]))))
 
 
-def sort_perm(hi: torch.Tensor, lo: torch.Tensor, ghist: torch.Tensor | None = None) -> torch.Tensor:
-    """Permutation sorting rows by the 80-bit key (hi, lo).
-
-    GPU: radix-sort the top 32 bits of hi (4 onesweep passes instead of 8)
-    and order the runs of rows equal in those bits by (hi, lo) in a fix-up
-    kernel — TeraGen keys are uniform, so ~2% of the rows sit in such a run,
-    nearly all of length 2; a run longer than 64 (skewed keys) falls back to
-    the full (hi, lo) sort.  ``ghist``: the histograms :func:`keys` computed
-    along with hi (skips the sort's histogram pass)."""
-    from .primitives import sort_keys
-    if not hi.is_cuda:
-        return sort_keys([hi, lo], bits=[64, 16])
-    perm, shi = sort_keys([hi], bits=[64], return_keys=True, from_bit=_TOP_FROM_BIT, ghist=ghist)
-    bad = torch.zeros(1, dtype=torch.int32, device=hi.device)
-    _hip.call("mr_ts_tie_fixup2", _hip.ptr(shi), _hip.ptr(perm), _hip.ptr(lo), hi.numel(), _hip.ptr(bad),
-              _TOP_FROM_BIT, _hip.stream(hi.device))
-    if int(bad.item()):
-        return sort_keys([hi, lo], bits=[64, 16])
-    return perm
-
-
-_TOP_FROM_BIT = 32
