@@ -174,6 +174,7 @@ class ListPlane:
         self._round_keys: list = []
         self._cpu_parts: list = []
         self.streamed = False
+        self._after_issue = None
         self.emitter = ListEmitter(self)
         if eng.device_input != "split":
             raise ValueError("the list plane maps engine-staged splits (device_input = 'split')")
@@ -286,6 +287,11 @@ class ListPlane:
                         recs[j].repetitions += 1
                         recs[j].status = STATUS.BROKEN if attempt < 2 else STATUS.FAILED
             _mark_written(recs, ja, jb, t0, time.time(), c0)
+        if self._after_issue is not None:
+            # the next iterations' copies queue right behind this map's (the
+            # finish below waits for the map): the copy engine never idles
+            self._after_issue()
+            self._after_issue = None
         if eng.device.type == "cuda":
             if self.streamed:
                 # every round's (word, line) groups, rounds in line order: a
@@ -334,6 +340,9 @@ class ListPlane:
         t0 = time.time()
         recs = _records(eng, jobs, j0, j1, t0)
         res.map_jobs = recs
+        ahead = 0 if not (prefetch_next if prefetch_next is not None else eng.prefetch) else (
+            2 if lookahead is None else min(lookahead, 2))
+        self._after_issue = (lambda: eng._prefetch_ahead(jobs, j0, j1, q, ahead)) if ahead else None
         try:
             with trace.range("mr.list.map"):
                 keys = self._map(jobs, recs, j0, j1)
@@ -341,15 +350,15 @@ class ListPlane:
             # the map emits through generic calls: the general plane runs
             # this engine from now on (this iteration is restarted there)
             from .generic import GenericPlane
+            self._after_issue = None
             eng.iteration -= 1
             eng._seq -= 1
             eng.plane_kind = "generic"
             eng.plane = GenericPlane(eng)
             return eng.plane.run_iteration(prefetch_next, lookahead)
-        ahead = 0 if not (prefetch_next if prefetch_next is not None else eng.prefetch) else (
-            2 if lookahead is None else min(lookahead, 2))
-        if ahead:
-            eng._prefetch_ahead(jobs, j0, j1, q, ahead)
+        if self._after_issue is not None:  # (a map that raised before issuing everything)
+            self._after_issue()
+            self._after_issue = None
         T["map"] = time.time() - t0
         t1 = time.time()
         vocab = self.vocab
