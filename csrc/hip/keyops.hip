@@ -369,6 +369,34 @@ static inline int grid_for(u64 n, int block, int maxg = 8192) {
   return (int)g;
 }
 
+// Word k of every key: its bytes [8k, 8k+8) big-endian, zero past the end
+// (word 0 = hi; packed keys keep bytes 8..14 in lo's top 7 bytes; long keys
+// read their bytes from src).  The columns of an exact bytewise key sort
+// (with the key length as the least significant column: a prefix sorts
+// first), for key sets whose long keys share long prefixes.
+__global__ void key_word_kernel(const u64* __restrict__ hi, const u64* __restrict__ lo, const u64* __restrict__ rep,
+                                const u8* __restrict__ src, u64 n, u32 k, u64* __restrict__ out) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 l = lo[i];
+    u64 w = 0;
+    if (k == 0) {
+      w = hi[i];
+    } else if (!key_is_long(l)) {
+      w = k == 1 ? (l & ~0xFFull) : 0ull;
+    } else {
+      const u64 r = rep[i];
+      const u64 off = rep_off(r), len = rep_len(r);
+#pragma unroll
+      for (u32 j = 0; j < 8; ++j) {
+        const u64 b = 8ull * k + j;
+        w = (w << 8) | (b < len ? (u64)src[off + b] : 0ull);
+      }
+    }
+    out[i] = w;
+  }
+}
+
 extern "C" {
 
 int mr_count_tokens(const void* text, u64 nbytes, u64 chunk_bytes, void* counter, hipStream_t stream) {
@@ -425,6 +453,14 @@ int mr_table_rehome(const void* tag, const void* lo, void* rep, u64 cap, void* b
 int mr_table_reset(void* tag, void* lo, void* val, void* ctrl, u64 cap, long long init, hipStream_t stream) {
   hipLaunchKernelGGL(table_reset_kernel, dim3(grid_for(cap, 256)), dim3(256), 0, stream, (u64*)tag, (u64*)lo,
                      (long long*)val, (u32*)ctrl, cap, init);
+  return (int)hipGetLastError();
+}
+
+int mr_key_word(const void* hi, const void* lo, const void* rep, const void* src, u64 n, u32 k, void* out,
+                hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(key_word_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)hi, (const u64*)lo,
+                     (const u64*)rep, (const u8*)src, n, k, (u64*)out);
   return (int)hipGetLastError();
 }
 

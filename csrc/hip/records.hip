@@ -199,61 +199,6 @@ __global__ void __launch_bounds__(256) rec_gather_kernel(const u32* __restrict__
   }
 }
 
-// Row gather, one row per lane (RB bytes, RB % 4 == 0): the lane reads the
-// 16-byte-aligned span holding its row with NQ 16-byte loads, writes the row's
-// words into its wave's LDS slab (row stride RB/4 words, odd for RB = 100:
-// no bank conflicts), and the wave then writes its 64 consecutive output rows
-// (a 16-byte-aligned region when 64 * RB is a multiple of 16) with coalesced
-// 16-byte stores.
-template <int RB>
-__global__ void __launch_bounds__(256) rec_gather_rows_kernel(const u8* __restrict__ in, const u32* __restrict__ perm,
-                                                              u64 n, u8* __restrict__ out) {
-  constexpr int W = RB / 4;
-  constexpr int NQ = (12 + RB + 15) / 16;
-  static_assert(RB % 4 == 0 && (64 * RB) % 16 == 0, "row shape");
-  __shared__ __attribute__((aligned(16))) u32 slab[4][64 * W];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  u32* my = slab[wave];
-  const u64 total = n * (u64)RB;
-  for (u64 base = ((u64)blockIdx.x * 4 + wave) * 64; base < n; base += (u64)gridDim.x * 4 * 64) {
-    const u64 row = base + lane;
-    if (row < n) {
-      const u64 src = (u64)clamp_row(perm[row], n) * RB;
-      const u64 a = src & ~15ull;
-      const int sh = (int)((src & 15) >> 2);
-      u32 w[NQ * 4];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (a + 16 * (u64)q < total) {
-          typedef u32 v4u __attribute__((ext_vector_type(4)));
-          const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + a) + q);
-          v = make_uint4(x.x, x.y, x.z, x.w);
-        }
-        w[4 * q] = v.x;
-        w[4 * q + 1] = v.y;
-        w[4 * q + 2] = v.z;
-        w[4 * q + 3] = v.w;
-      }
-#pragma unroll
-      for (int k = 0; k < W; ++k)
-        my[lane * W + k] = sh == 0 ? w[k] : sh == 1 ? w[k + 1] : sh == 2 ? w[k + 2] : w[k + 3];
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's slab writes are done
-    __builtin_amdgcn_wave_barrier();
-    const u64 rows = min((u64)64, n - base);
-    const u32 nq = (u32)(rows * RB / 16);
-    typedef u32 v4u __attribute__((ext_vector_type(4)));
-    v4u* o = reinterpret_cast<v4u*>(out + base * RB);
-    const v4u* l4 = reinterpret_cast<const v4u*>(my);
-    for (u32 j = lane; j < nq; j += 64) __builtin_nontemporal_store(l4[j], o + j);
-    const u32 nw = (u32)(rows * RB / 4);
-    u32* o32 = reinterpret_cast<u32*>(out + base * RB);
-    for (u32 j = nq * 4 + lane; j < nw; j += 64) o32[j] = my[j];
-    __builtin_amdgcn_wave_barrier();  // the slab is rewritten by the next group
-  }
-}
-
 // Rows whose width is not a multiple of 4 bytes: one byte per thread.
 __global__ void rec_gather_bytes_kernel(const u8* __restrict__ in, const u32* __restrict__ perm, u64 n, u64 rb,
                                         u8* __restrict__ out) {
@@ -340,17 +285,6 @@ int mr_rec_gather(const void* in, const void* perm, u64 n, int rb, void* out, hi
   else
     hipLaunchKernelGGL((rc::rec_gather_kernel<0, 8>), dim3(g), dim3(256), 0, s, (const u32*)in, (const u32*)perm, n,
                        words, (u32*)out);
-  return (int)hipGetLastError();
-}
-
-// A/B candidate: the one-row-per-lane gather (100-byte rows only)
-int mr_rec_gather_rows(const void* in, const void* perm, u64 n, int rb, void* out, hipStream_t s) {
-  if (n == 0) return 0;
-  if (rb != 100 || ((uintptr_t)in & 15) || ((uintptr_t)out & 15)) return -1;
-  const u64 groups = (n + 63) / 64;
-  const unsigned g = (unsigned)min((groups + 3) / 4, (u64)8192);
-  hipLaunchKernelGGL((rc::rec_gather_rows_kernel<100>), dim3(g), dim3(256), 0, s, (const u8*)in, (const u32*)perm, n,
-                     (u8*)out);
   return (int)hipGetLastError();
 }
 

@@ -37,6 +37,7 @@ _SIGS = {
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
     "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p, _p],
     "mr_table_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
+    "mr_key_word": [_p, _p, _p, _p, _u64, _u32, _p, _p],
     "mr_key_meta": [_p, _p, _p, _u64, _p, _u32, _p, _p, _p],
     "mr_gather_key_bytes": [_p, _p, _p, _p, _u64, _p, _p, _u64, _p],
     "mr_exclusive_scan_u32": [_p, _p, _u64, _p, _p, _p],
@@ -94,7 +95,6 @@ _SIGS = {
     "mr_radix_onesweep_k32": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p, _u32, _p, _i32, _p],
     "mr_rec_keys32": [_p, _u64, _i32, _i32, _p, _p, _p],
     "mr_rec_keys": [_p, _u64, _i32, _i32, _p, _p, _p],
-    "mr_rec_gather_rows": [_p, _p, _u64, _i32, _p, _p],
     "mr_rec_tie_fixup": [_p, _p, _p, _u64, _i32, _i32, _p, _p, _u64, _p],
     "mr_rec_gather": [_p, _p, _u64, _i32, _p, _p],
     "mr_rec_dest32": [_p, _u64, _p, _u32, _p, _p],

@@ -725,6 +725,45 @@ def sort_error_word(device) -> torch.Tensor | None:
     return None if ws is None else ws["small"][2112:2113]
 
 
+EXACT_MAX_WORDS = 32  # keys up to 256 bytes get the device's exact order
+
+
+def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor,
+                   src: torch.Tensor | None, nparts: int) -> torch.Tensor | None:
+    """Stable permutation ordering rows by (partition, exact key bytes) on the
+    device, for key sets the (partition, hi, lo) sort plus the tie fix-up
+    cannot order (long keys — whose lo is a hash — in long runs of a shared
+    8-byte prefix, e.g. n-grams): an LSD sort of the key as 8-byte words
+    (mr_key_word; zero-padded) with the key length as the least significant
+    column, in stages of at most 6 columns (each stage stable, permutations
+    composed).  None when a key is longer than 8 * EXACT_MAX_WORDS bytes (the
+    caller orders on the host)."""
+    n = hi.numel()
+    d = hi.device
+    if n == 0:
+        return torch.zeros(0, dtype=torch.int64, device=d)
+    _, klen = key_meta(hi, lo, rep, src, want_part=False)
+    max_len = int(klen.max())
+    nw = max(1, (max_len + 7) // 8)
+    if nw > EXACT_MAX_WORDS:
+        return None
+    s = _hip.stream(d)
+    cols = [part.to(torch.int64)]
+    for k in range(nw):
+        w = torch.empty(n, dtype=torch.int64, device=d)
+        _hip.call("mr_key_word", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), _hip.ptr(src), n, k, _hip.ptr(w), s)
+        cols.append(w)
+    cols.append(klen.to(torch.int64))
+    bits = [max(8, int(max(nparts, 1) - 1).bit_length())] + [64] * nw + [max(8, max_len.bit_length())]
+    perm = None
+    for end in range(len(cols), 0, -6):  # least significant stage first
+        a = max(0, end - 6)
+        grp = [c if perm is None else c[perm] for c in cols[a:end]]
+        p = sort_keys_checked(grp, bits=bits[a:end]).long()
+        perm = p if perm is None else perm[p]
+    return perm
+
+
 def sort_keys_checked(words, bits=None, retries: int = 2, **kw):
     """sort_keys that checks the look-back error word (one host sync) and
     re-sorts on a give-up; raises after ``retries`` failed re-sorts."""

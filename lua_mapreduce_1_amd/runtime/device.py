@@ -302,7 +302,7 @@ def _to_host(t: torch.Tensor, name: str) -> torch.Tensor:
 
 
 def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: torch.Tensor | None = None,
-             _presorted: bool = False, need_keys: bool = False):
+             _presorted: bool = False, need_keys: bool = False, _exact: bool = False):
     """Partition, sort by (partition, key) and materialise key bytes.
 
     Returns a dict of host numpy arrays: hi, lo, val, key_off, key_blob and
@@ -312,6 +312,7 @@ def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: to
     stay valid until the next finalize() call (copy them to keep them longer).
     """
     pend = finalize_device(hi, lo, val, rep, src, nparts, partition_module, part, _presorted)
+    pend["exact"] = _exact
     try:
         return finalize_host(pend, partition_module, need_keys)
     except BlobCapacityError as e:  # keys overlapping in their source (n-gram spans)
@@ -513,16 +514,21 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
             ahi, alo, aval, arep = pend["args"]
             src = pend["src"]
             p2 = partition_of(ahi, alo, arep, src, nparts, partition_module)
-            perm = ops.sort_keys_checked([p2.to(torch.int64), ahi, alo],
-                                         bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
+            # exact bytewise order on the device (long keys compared by their
+            # bytes); the host fix-up is left for keys past its length limit
+            perm = ops.exact_key_perm(p2, ahi, alo, arep, src, nparts) if src is not None else None
+            exact = perm is not None
+            if perm is None:
+                perm = ops.sort_keys_checked([p2.to(torch.int64), ahi, alo],
+                                             bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
             return finalize(ahi[perm], alo[perm], aval[perm], arep[perm], src, nparts, partition_module,
-                            part=p2[perm], _presorted=True, need_keys=need_keys)
+                            part=p2[perm], _presorted=True, need_keys=need_keys, _exact=exact)
         # offsets stay int32 when the blob is < 2 GiB (no host-side widening pass)
         if pend.get("fused"):
             h_val, h_off, h_blob, h_counts = f_val, f_off, hb.numpy(), f_counts
         else:
             h_val, h_off, h_blob, h_counts = pend["hv"].numpy(), ho.numpy(), hb.numpy(), pend["hc"].numpy()
-        need_fix = bool(flag & 2) or pend["presorted"]
+        need_fix = bool(flag & 2) or (pend["presorted"] and not pend.get("exact"))
         h_hi = hi.cpu().numpy().view(np.uint64) if (need_fix or need_keys) else None
         h_lo = lo.cpu().numpy().view(np.uint64) if (need_fix or need_keys) else None
     else:

@@ -466,3 +466,38 @@ def test_radix_ghist8_matches_numpy(gpu, n, runs):
             want = np.bincount(((ku >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.int64), minlength=256) \
                 if d0 <= b < ndig else np.zeros(256, np.int64)
             assert np.array_equal(got[b], want), b
+
+
+@pytest.mark.parametrize("nparts", [1, 7])
+def test_tail_orders_long_runs_of_a_shared_prefix_exactly(gpu, nparts):
+    """Keys that share their first 8 bytes in runs far longer than the tie
+    fix-up handles (n-gram-like: one long prefix, many suffixes, long keys
+    among them): the tail falls back to the exact device order (key words +
+    length), no host sort — result keys are in bytewise order in every
+    partition with their counts."""
+    from lua_mapreduce_1_amd.runtime import device as dv
+    rng = np.random.default_rng(nparts)
+    words = set()
+    while len(words) < 6000:
+        k = int(rng.integers(0, 24))
+        words.add(b"sharedpx" + bytes(rng.integers(97, 100, k).astype(np.uint8)))
+    words = sorted(words)
+    reps = rng.integers(1, 4, len(words))
+    toks = [w for w, r in zip(words, reps) for _ in range(int(r))]
+    rng.shuffle(toks)
+    text = b" ".join(toks) + b"\n"
+    t = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(gpu)
+    tab = ops.HashTable(1 << 15, device=gpu)
+    tab.wordcount_map(t)
+    n, _ = tab.stats()
+    c = dv.finalize_host(dv.finalize_table_native(tab, n, t, nparts))
+    kb = c["key_blob"].tobytes()
+    ko = np.asarray(c["key_off"], np.int64)
+    want = dict(zip(words, reps.tolist()))
+    got = {}
+    for p in range(nparts):
+        a, b = int(c["bounds"][p]), int(c["bounds"][p + 1])
+        keys = [kb[ko[i]:ko[i + 1]] for i in range(a, b)]
+        assert keys == sorted(keys)
+        got.update(zip(keys, c["val"][a:b].tolist()))
+    assert got == want
