@@ -150,8 +150,15 @@ def set_long_mask(mask: int) -> None:
         call(name, mask)
 
 
+_AVAILABLE: list = []
+
+
 def available() -> bool:
-    return torch.cuda.is_available()
+    """torch.cuda.is_available(), asked once (each call costs milliseconds
+    on this stack)."""
+    if not _AVAILABLE:
+        _AVAILABLE.append(torch.cuda.is_available())
+    return _AVAILABLE[0]
 
 
 def ptr(t):

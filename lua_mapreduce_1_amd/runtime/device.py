@@ -270,7 +270,7 @@ class _PinnedPool:
     def get(self, name: str, n: int, dtype) -> torch.Tensor:
         b = self.bufs.get(name)
         if b is None or b.numel() < n or b.dtype != dtype:
-            b = torch.empty(max(n, 1024) * 5 // 4, dtype=dtype, pin_memory=torch.cuda.is_available())
+            b = torch.empty(max(n, 1024) * 5 // 4, dtype=dtype, pin_memory=default_device().type == "cuda")
             self.bufs[name] = b
         return b[:n]
 
@@ -462,6 +462,29 @@ def finalize_table_native(table, n: int, src, nparts: int, blob_cap: int | None 
               _hip.ptr(hb), est_arg, hb.numel(), _hip.stream(d))
     return {"n": n, "nparts": nparts, "args": v["args"], "src": src, "presorted": False, "hi": v["hi"], "lo": v["lo"],
             "fused": True, "hp": hp, "off": v["off"], "blob": v["blob"], "est": est, "hb": hb}
+
+
+def finalize_table(table, src, nparts: int, partition_module=None, need_keys: bool = False) -> dict:
+    """HBM table -> host result columns (a worker's map tail): the fused
+    native tail (one call: compact, FNV partition, sort, key bytes, one
+    download) when the partition is the device FNV-1 of ``nparts`` <= 256
+    partitions, else compaction + :func:`finalize`.  An overflowed table
+    raises OverflowError."""
+    n, ovf = table.stats()
+    if ovf:
+        raise OverflowError("device map table overflow")
+    spec = getattr(partition_module, "device_partition", None) if partition_module is not None else ("fnv1", nparts)
+    if (table.is_cuda and src is not None and spec is not None and spec[0] == "fnv1" and int(spec[1]) == nparts
+            and 0 < nparts <= 256 and n > 0):
+        cap = None
+        for _ in range(4):
+            try:
+                return finalize_host(finalize_table_native(table, n, src, nparts, blob_cap=cap), partition_module,
+                                     need_keys)
+            except BlobCapacityError as e:
+                cap = e.nbytes + e.nbytes // 4 + 4096
+    hi, lo, val, rep = table.compact((n, ovf))
+    return finalize(hi, lo, val, rep, src, nparts, partition_module, need_keys=need_keys)
 
 
 def _unpack_fused(pend: dict):

@@ -321,8 +321,7 @@ class job:  # noqa: N801
         modules.field(self.module, "device_mapfn")(map_key, map_value, ctx.emit)
         ctx.flush_host_pairs()
         self.mark_as_finished()
-        hi, lo, val, rep = ctx.table.compact()
-        cols = dev.finalize(hi, lo, val, rep, ctx.source(), nparts, pmod, need_keys=True)
+        cols = dev.finalize_table(ctx.table, ctx.source(), nparts, pmod, need_keys=True)
         fs, make_builder, _ = fsmod.router(self.cnn, None, self.storage, self.path)
         # every storage's build replaces an existing file (BLOB_PUT overwrites,
         # file builders rename over), so the reference's remove-before-build
