@@ -38,8 +38,8 @@ M = "lua_mapreduce_1_amd.examples.TeraSort"
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gb", type=float, default=10.0, help="total data size (1 GB = 1e9 bytes)")
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2, help="untimed iterations (two: the double-buffered 10 GB outputs are both allocated before timing)")
     args = ap.parse_args()
     rank, world, device = D.init_from_env()
     total = int(args.gb * 1e9) // 100
