@@ -302,7 +302,7 @@ def _to_host(t: torch.Tensor, name: str) -> torch.Tensor:
 
 
 def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: torch.Tensor | None = None,
-             _presorted: bool = False, need_keys: bool = False, _exact: bool = False):
+             _presorted: bool = False, need_keys: bool = False, _exact: bool = False, blob_cap: int | None = None):
     """Partition, sort by (partition, key) and materialise key bytes.
 
     Returns a dict of host numpy arrays: hi, lo, val, key_off, key_blob and
@@ -311,7 +311,7 @@ def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: to
     with a single synchronisation.  NOTE: the arrays alias the pinned pool and
     stay valid until the next finalize() call (copy them to keep them longer).
     """
-    pend = finalize_device(hi, lo, val, rep, src, nparts, partition_module, part, _presorted)
+    pend = finalize_device(hi, lo, val, rep, src, nparts, partition_module, part, _presorted, blob_cap=blob_cap)
     pend["exact"] = _exact
     try:
         return finalize_host(pend, partition_module, need_keys)
@@ -545,7 +545,8 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
                 perm = ops.sort_keys_checked([p2.to(torch.int64), ahi, alo],
                                              bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
             return finalize(ahi[perm], alo[perm], aval[perm], arep[perm], src, nparts, partition_module,
-                            part=p2[perm], _presorted=True, need_keys=need_keys, _exact=exact)
+                            part=p2[perm], _presorted=True, need_keys=need_keys, _exact=exact,
+                            blob_cap=max(int(blob.numel()), nbytes))
         # offsets stay int32 when the blob is < 2 GiB (no host-side widening pass)
         if pend.get("fused"):
             h_val, h_off, h_blob, h_counts = f_val, f_off, hb.numpy(), f_counts
