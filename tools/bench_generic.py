@@ -76,11 +76,15 @@ def run_job(name: str, mod_name: str, store, nbytes: int, check_splits: list[byt
                     init_args={"nsplits": len(store), "num_reducers": 10, "quiet": True}), device=device,
                split_store=store)
     ms, res = _time(eng, args.steps, args.warmup, device)
-    ok = _check(mod_name, check_splits, device)
-    return {"metric": f"{name} {unit}/s (general device plane, mr.spmd)", "value": units / (ms / 1000.0),
-            "unit": f"{unit}/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
-            "bytes": int(nbytes), "GB_per_s": nbytes / (ms / 1000.0) / 1e9, "distinct_keys": res.distinct_keys,
-            "total_value": res.total_value, "oracle_subset_ok": ok, "timings_last_step": res.timings}
+    # read the result before the check runs another engine (result columns
+    # alias the process's pinned download buffers until the next tail)
+    out = {"metric": f"{name} {unit}/s (general device plane, mr.spmd)", "value": units / (ms / 1000.0),
+           "unit": f"{unit}/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+           "bytes": int(nbytes), "GB_per_s": nbytes / (ms / 1000.0) / 1e9, "distinct_keys": res.distinct_keys,
+           "total_value": res.total_value, "timings_last_step": res.timings}
+    del res
+    out["oracle_subset_ok"] = _check(mod_name, check_splits, device)
+    return out
 
 
 def main() -> int:
