@@ -348,17 +348,33 @@ class IterationResult:
         self.bytes_shuffled = 0     # payload bytes this rank sent in the all-to-all
         self.bytes_shuffled_remote = 0  # ... to other ranks
 
+    def _fresh(self) -> None:
+        """The result columns of the fold plane alias the process's pinned
+        download buffers (no copy per iteration); a later tail — the next
+        iteration, or another engine — overwrites them.  Reading them after
+        that raises instead of returning another iteration's data."""
+        g = getattr(self, "_gen", None)
+        if g is not None and g != devmod.pool_generation() and self._parts is None:
+            raise RuntimeError("this iteration's result columns were overwritten by a later device tail: read "
+                               "them (partitions, gather_results, total_value) before the next iteration runs")
+
     @property
     def partitions(self) -> dict[int, dict]:
         if self._parts is None:
-            self._parts = {p: devmod.partition_slice(self._cols, p) for p in self.result_names}
+            self._fresh()
+            # copies: the partitions outlive the pinned buffers they came from
+            self._parts = {p: {k: (None if v is None else np.array(v)) for k, v in
+                               devmod.partition_slice(self._cols, p).items()} for p in self.result_names}
         return self._parts
 
     @property
     def total_value(self) -> int:
         """Sum of all reduced values of this rank (computed on first use)."""
-        v = self._vals
-        return int(v.sum()) if v is not None and v.size else 0
+        if getattr(self, "_total", None) is None:
+            self._fresh()
+            v = self._vals
+            self._total = int(v.sum()) if v is not None and v.size else 0
+        return self._total
 
 
 class SPMDEngine:
@@ -1417,6 +1433,7 @@ class SPMDEngine:
         res.distinct_keys = int(cols["val"].size)
         res._vals = cols["val"]
         res._cols, res._parts = cols, None
+        res._gen = devmod.pool_generation()
         T["reduce"] = time.time() - t2
         T["iteration"] = time.time() - t_start
         res.failed_maps = self._failed_total

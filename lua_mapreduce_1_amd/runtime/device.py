@@ -262,10 +262,13 @@ def fix_long_key_order(hi: np.ndarray, lo: np.ndarray, off: np.ndarray, blob: np
 
 
 class _PinnedPool:
-    """Reusable pinned host buffers for device -> host result copies."""
+    """Reusable pinned host buffers for device -> host result copies.
+    ``gen`` counts the downloads into them (finalize_host): a result whose
+    columns alias the pool is stale once ``gen`` has moved on."""
 
     def __init__(self):
         self.bufs: dict[str, torch.Tensor] = {}
+        self.gen = 0
 
     def get(self, name: str, n: int, dtype) -> torch.Tensor:
         b = self.bufs.get(name)
@@ -499,8 +502,13 @@ def _unpack_fused(pend: dict):
     return val, off, counts, bad
 
 
+def pool_generation() -> int:
+    return _POOL.gen
+
+
 def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) -> dict:
     """The host half of :func:`finalize`: one synchronisation, then numpy."""
+    _POOL.gen += 1
     n, nparts = pend["n"], pend["nparts"]
     hi, lo = pend["hi"], pend["lo"]
     if hi.is_cuda:
