@@ -290,6 +290,14 @@ def main() -> int:
     elapsed = D.all_reduce_max(elapsed, device)
     ms = 1000.0 * elapsed / max(1, args.steps)
 
+    # validation outside the timed region: every token counted exactly once,
+    # and (synthetic corpus) every word's count equal to the generator's (read
+    # before any other engine runs: result columns live in the pinned
+    # download buffers until the next tail)
+    counted = D.all_reduce_sum_int(last.total_value, device) if last is not None else 0
+    distinct = D.all_reduce_sum_int(last.distinct_keys, device) if last is not None else 0
+    got = result_counts(eng, last) if last is not None else {}
+
     fs_ms = fs_valid = None
     if args.force_shuffle:
         # the same steps with the W > 1 path forced at this world size
@@ -310,11 +318,6 @@ def main() -> int:
         fs_valid = r2 is not None and D.all_reduce_sum_int(r2.total_value, device) == words
         del e2, r2
 
-    # validation outside the timed region: every token counted exactly once,
-    # and (synthetic corpus) every word's count equal to the generator's
-    counted = D.all_reduce_sum_int(last.total_value, device) if last is not None else 0
-    distinct = D.all_reduce_sum_int(last.distinct_keys, device) if last is not None else 0
-    got = result_counts(eng, last) if last is not None else {}
     per_key = None
     if rank == 0 and cdir is not None:
         per_key = got == truth_counts(cdir)

@@ -1433,7 +1433,7 @@ class SPMDEngine:
         res.distinct_keys = int(cols["val"].size)
         res._vals = cols["val"]
         res._cols, res._parts = cols, None
-        res._gen = devmod.pool_generation()
+        res._gen = devmod.pool_generation() if self.device.type == "cuda" else None
         T["reduce"] = time.time() - t2
         T["iteration"] = time.time() - t_start
         res.failed_maps = self._failed_total
