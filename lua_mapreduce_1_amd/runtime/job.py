@@ -423,13 +423,26 @@ def _device_reduce(blobs: list[bytes], op: str) -> bytes:
     offs = np.concatenate([c["key_off"][:-1] + b for c, b in zip(cols, bases)]).astype(np.uint64)
     lens = np.concatenate([np.diff(c["key_off"]) for c in cols]).astype(np.uint64)
     rep = torch.from_numpy(((offs << np.uint64(24)) | lens).view(np.int64)).to(d)
-    src = torch.from_numpy(np.concatenate([c["key_blob"] for c in cols])).to(d)
-    tab = dev.ops.HashTable(max(1024, 2 * n), device=d, op=op)
+    src = torch.from_numpy(np.concatenate([c["key_blob"] for c in cols] + [np.zeros(1, np.uint8)])).to(d)
+    tab = _reduce_table(d, op, 2 * n)
     tab.insert(hi, lo, val, rep, src=src)  # long keys verified against their bytes
-    uhi, ulo, uval, urep = tab.compact()
-    out = dev.finalize(uhi, ulo, uval, urep, src, 1, None, part=torch.zeros(uhi.numel(), dtype=torch.int32,
-                                                                              device=d), need_keys=True)
+    out = dev.finalize_table(tab, src, 1, None, need_keys=True)  # one partition: the job's own
     return codec.encode_columnar(out["hi"], out["lo"], out["val"], out["key_off"], out["key_blob"])
+
+
+_RED_TABLES: dict = {}
+
+
+def _reduce_table(d, op: str, need: int):
+    """A worker's reduce hash table, kept across its jobs (reset, regrown when
+    a job needs more slots)."""
+    key = (str(d), op)
+    t = _RED_TABLES.get(key)
+    if t is None or t.cap < need:
+        t = _RED_TABLES[key] = dev.ops.HashTable(max(1024, need), device=d, op=op)
+    else:
+        t.reset()
+    return t
 
 
 def _is_cols(op) -> bool:

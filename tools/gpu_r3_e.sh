@@ -6,6 +6,8 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${1:-r3_e}
 mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --force-shuffle > $OUT/bench_fs.log 2>&1
 timeout -k 10 300 python -u tools/debug_exact_order.py 30 > $OUT/exact_order.log 2>&1
 timeout -k 10 400 python -u tools/bench_generic.py > $OUT/generic.log 2>&1 || true
 for n in 1 4 8; do
