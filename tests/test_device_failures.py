@@ -38,7 +38,7 @@ def test_transient_device_failure_is_retried(gpu, monkeypatch):
     monkeypatch.setenv("MR_SPMD_DEVICE_FAULT", "5:1")
     eng = _engine(gpu, splits)
     res = eng.run_iteration()
-    assert len(eng._chunks[eng.tslot]) > 3  # several launches
+    # (the re-run may map everything in one launch: its copies have landed)
     assert _counts(eng, res) == dict(Counter(w.decode() for s in splits for w in s.split()))
     assert res.map_jobs[5].repetitions == 1 and res.map_jobs[5].status == STATUS.WRITTEN
     assert res.failed_maps == 0
