@@ -52,6 +52,26 @@ def default_device():
 _CTX_CACHE: dict = {}
 
 
+def warm_worker(op: str = "sum", capacity: int = 1 << 20) -> None:
+    """Bring up a worker's GPU device plane before its first job: the HIP
+    context and kernel library, the map context (table + arena) that
+    :meth:`DeviceMapContext.for_job` hands out, the reduce table, the sort
+    and tail workspaces and the pinned download buffers (a tiny map + tail).
+    A no-op without a GPU."""
+    d = default_device()
+    if d.type != "cuda":
+        return
+    from ..ops import _hip
+    _hip.lib()
+    ctx = DeviceMapContext.for_job(op, capacity, d)
+    ctx.emit.words(torch.frombuffer(bytearray(b"warm up the device plane\n"), dtype=torch.uint8).to(d))
+    finalize_table(ctx.table, ctx.source(), 1, None, need_keys=True)
+    STATS["maps_cuda"] = max(0, STATS.get("maps_cuda", 0) - 1)  # (not a job)
+    from . import job as job_mod
+    job_mod._reduce_table(d, op, 1 << 21)
+    torch.cuda.synchronize(d)
+
+
 class DeviceMapContext:
     """State of one device map job: the hash table and ONE contiguous device
     byte arena holding every key-byte source the job emitted from (input

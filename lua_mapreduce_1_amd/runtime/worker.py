@@ -179,6 +179,12 @@ class worker:  # noqa: N801
         failed: set = set()
         if self._gpu_slot is None:  # before any job touches the GPU
             self._gpu_slot = gpu_slots.place_worker(self.gpu)
+        if self.gpu != "none":
+            # a persistent worker brings up its device plane once, before it
+            # claims anything (HIP context, kernel library, the map context
+            # and reduce table it reuses across jobs), not inside its first job
+            from . import device as dev_mod
+            dev_mod.warm_worker()
         self._start_heartbeat()
         try:
             while True:
