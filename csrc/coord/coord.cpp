@@ -104,7 +104,10 @@ struct Db {
   bool has_task = false;
   std::map<std::string, Collection> colls;
   std::vector<std::pair<std::string, std::string>> errors;
-  std::map<std::string, std::string> blobs;
+  // blob bodies are shared and immutable: a read references them (the reply
+  // is written after the store lock is released) and a write builds them
+  // before taking it, so large blobs are never copied under the lock
+  std::map<std::string, std::shared_ptr<const std::string>> blobs;
   std::map<std::string, PTable> ptables;  // key: doc + "\x1f" + name
 };
 
@@ -127,6 +130,18 @@ struct Reader {
 
 struct Writer {
   std::string buf;
+  // blob bodies referenced by the reply: (offset in buf where the body goes, body)
+  std::vector<std::pair<size_t, std::shared_ptr<const std::string>>> refs;
+  void blob(std::shared_ptr<const std::string> p) {
+    uint32_t n = (uint32_t)p->size();
+    buf.append((const char*)&n, 4);
+    refs.emplace_back(buf.size(), std::move(p));
+  }
+  size_t size() const {
+    size_t n = buf.size();
+    for (auto& r : refs) n += r.second->size();
+    return n;
+  }
   void str(const std::string& s) {
     uint32_t n = (uint32_t)s.size();
     buf.append((const char*)&n, 4);
@@ -348,11 +363,15 @@ class Store {
         db.errors.clear();
         return 0;
       }
-      case BLOB_PUT: { std::string n = r.str(); db.blobs[n] = r.str(); return r.ok ? 0 : -1; }
+      case BLOB_PUT: {
+        std::string n = r.str();
+        db.blobs[n] = std::make_shared<const std::string>(r.str());
+        return r.ok ? 0 : -1;
+      }
       case BLOB_GET: {
         auto it = db.blobs.find(r.str());
         if (it == db.blobs.end()) return 1;
-        w.str(it->second);
+        w.blob(it->second);
         return 0;
       }
       case BLOB_LIST: {
@@ -360,7 +379,7 @@ class Store {
         for (auto it = db.blobs.lower_bound(prefix); it != db.blobs.end(); ++it) {
           if (it->first.compare(0, prefix.size(), prefix) != 0) break;
           w.str(it->first);
-          w.i((long long)it->second.size());
+          w.i((long long)it->second->size());
         }
         return 0;
       }
@@ -370,7 +389,7 @@ class Store {
           std::string n = r.str();
           std::string d = r.str();
           if (!r.ok) return -1;
-          db.blobs[n] = std::move(d);
+          db.blobs[n] = std::make_shared<const std::string>(std::move(d));
         }
         return r.ok ? 0 : -1;
       }
@@ -382,7 +401,7 @@ class Store {
             w.str(std::string());
           } else {
             w.i(1);
-            w.str(it->second);
+            w.blob(it->second);
           }
         }
         return r.ok ? 0 : -1;
@@ -512,10 +531,32 @@ class Store {
     return 0;
   }
 
+  // BLOB_PUT / BLOB_PUT_MANY with the bodies built before the lock is taken
+  int put_blobs(uint16_t op, const std::string& body, Writer& w) {
+    Reader r{body.data() + 2, body.data() + body.size()};
+    const std::string dbname = r.str();
+    std::vector<std::pair<std::string, std::shared_ptr<const std::string>>> items;
+    do {
+      std::string n = r.str();
+      std::string d = r.str();
+      if (!r.ok) return -1;
+      items.emplace_back(std::move(n), std::make_shared<const std::string>(std::move(d)));
+    } while (op == BLOB_PUT_MANY && r.more());
+    std::unique_lock<std::mutex> g(mu);
+    Db& db = dbs[dbname];
+    for (auto& it : items) db.blobs[it.first] = std::move(it.second);
+    log(body);
+    ++ver[dbname];
+    cv.notify_all();
+    (void)w;
+    return 0;
+  }
+
   int handle(const std::string& body, Writer& w) {
     if (body.size() < 2) return -1;
     uint16_t op;
     memcpy(&op, body.data(), 2);
+    if ((op == BLOB_PUT || op == BLOB_PUT_MANY) && !replaying) return put_blobs(op, body, w);
     Reader r{body.data() + 2, body.data() + body.size()};
     std::unique_lock<std::mutex> g(mu);
     if (op == WAIT_CHANGE) return replaying ? 0 : wait_change(r, w, g);
@@ -659,12 +700,29 @@ struct Server {
       if (n >= 2) memcpy(&op, body.data(), 2);
       Writer w;
       int st = store.handle(body, w);
-      uint32_t rn = (uint32_t)(4 + w.buf.size());
+      uint32_t rn = (uint32_t)(4 + w.size());
       std::string out;
       out.append((const char*)&rn, 4);
       out.append((const char*)&st, 4);
-      out.append(w.buf);
-      if (!write_full(fd, out.data(), out.size())) break;
+      bool ok = true;
+      if (w.refs.empty()) {
+        out.append(w.buf);
+        ok = write_full(fd, out.data(), out.size());
+      } else {  // referenced blob bodies go straight from the store (no copy, no lock)
+        size_t at = 0;
+        for (auto& ref : w.refs) {
+          out.append(w.buf, at, ref.first - at);
+          at = ref.first;
+          if (!(ok = write_full(fd, out.data(), out.size()))) break;
+          out.clear();
+          if (!(ok = write_full(fd, ref.second->data(), ref.second->size()))) break;
+        }
+        if (ok) {
+          out.append(w.buf, at, std::string::npos);
+          ok = write_full(fd, out.data(), out.size());
+        }
+      }
+      if (!ok) break;
       if (op == SHUTDOWN) { stop = true; ::shutdown(listen_fd, SHUT_RDWR); break; }
     }
     ::close(fd);
