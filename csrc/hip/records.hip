@@ -95,30 +95,50 @@ __device__ __forceinline__ void key_rest(const u8* row, int kb, bool words, u64&
 // and the caller sorts the full (hi, lo) key instead.
 constexpr int TIE_MAX = 64;
 
+// One thread per 4 consecutive prefixes (one 16-byte load + the two after
+// and the one before): a run start is a prefix equal to the next and
+// different from the previous.
 __global__ void __launch_bounds__(256) rec_tie_pairs_kernel(const u32* __restrict__ sk, u32* __restrict__ perm,
                                                             const u8* __restrict__ rec, u64 n, int rb, int kb,
                                                             u32* __restrict__ bad, u64* __restrict__ runs,
                                                             unsigned long long* __restrict__ nruns, u64 runs_cap) {
+  if (kb <= 4) return;  // the prefix is the whole key
   const bool words = (rb & 3) == 0;
   const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += stride) {
-    const u32 h = sk[i];
-    if (sk[i + 1] != h || (i > 0 && sk[i - 1] == h)) continue;
-    if (kb <= 4) continue;  // the prefix is the whole key
-    if (i + 2 < n && sk[i + 2] == h) {  // a run of 3 or more
-      const unsigned long long k = atomicAdd(nruns, 1ull);
-      if (k < runs_cap) runs[k] = i;
-      else atomicOr(bad, 1u);
-      continue;
+  for (u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x; 4 * g < n; g += stride) {
+    const u64 i0 = 4 * g;
+    u32 v[7];  // sk[i0 - 1 .. i0 + 5]
+    if (i0 + 4 <= n && (((uintptr_t)sk & 15) == 0)) {
+      const uint4 q = *reinterpret_cast<const uint4*>(sk + i0);
+      v[1] = q.x; v[2] = q.y; v[3] = q.z; v[4] = q.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[1 + j] = i0 + j < n ? sk[i0 + j] : 0u;
     }
-    const u32 p0 = perm[i], p1 = perm[i + 1];
-    u64 a0, a1;
-    u32 b0, b1;
-    key_rest(rec + (u64)clamp_row(p0, n) * rb, kb, words, a0, b0);
-    key_rest(rec + (u64)clamp_row(p1, n) * rb, kb, words, a1, b1);
-    if (a0 > a1 || (a0 == a1 && b0 > b1)) {
-      perm[i] = p1;
-      perm[i + 1] = p0;
+    v[0] = i0 > 0 ? sk[i0 - 1] : ~v[1];
+    v[5] = i0 + 4 < n ? sk[i0 + 4] : 0u;
+    v[6] = i0 + 5 < n ? sk[i0 + 5] : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u64 i = i0 + j;
+      if (i + 1 >= n) break;
+      const u32 h = v[1 + j];
+      if (v[2 + j] != h || v[j] == h) continue;  // not the start of a run
+      if (i + 2 < n && v[3 + j] == h) {          // a run of 3 or more
+        const unsigned long long k = atomicAdd(nruns, 1ull);
+        if (k < runs_cap) runs[k] = i;
+        else atomicOr(bad, 1u);
+        continue;
+      }
+      const u32 p0 = perm[i], p1 = perm[i + 1];
+      u64 a0, a1;
+      u32 b0, b1;
+      key_rest(rec + (u64)clamp_row(p0, n) * rb, kb, words, a0, b0);
+      key_rest(rec + (u64)clamp_row(p1, n) * rb, kb, words, a1, b1);
+      if (a0 > a1 || (a0 == a1 && b0 > b1)) {
+        perm[i] = p1;
+        perm[i + 1] = p0;
+      }
     }
   }
 }
@@ -263,7 +283,7 @@ int mr_rec_tie_fixup(const void* sk, void* perm, const void* rec, u64 n, int rb,
   if (n < 2) return 0;
   u64* w = (u64*)ws;
   (void)hipMemsetAsync(w, 0, sizeof(u64), s);
-  hipLaunchKernelGGL(rc::rec_tie_pairs_kernel, dim3(rc_grid(n)), dim3(256), 0, s, (const u32*)sk, (u32*)perm,
+  hipLaunchKernelGGL(rc::rec_tie_pairs_kernel, dim3(rc_grid((n + 3) / 4)), dim3(256), 0, s, (const u32*)sk, (u32*)perm,
                      (const u8*)rec, n, rb, kb, (u32*)bad, w + 1, (unsigned long long*)w, ws_cap);
   hipLaunchKernelGGL(rc::rec_tie_runs_kernel, dim3(256), dim3(64), 0, s, (const u32*)sk, (u32*)perm, (const u8*)rec,
                      n, rb, kb, (u32*)bad, (const u64*)(w + 1), (const unsigned long long*)w, ws_cap);
