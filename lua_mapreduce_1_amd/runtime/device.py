@@ -62,14 +62,15 @@ def warm_worker(op: str = "sum", capacity: int = 1 << 20) -> None:
     if d.type != "cuda":
         return
     from ..ops import _hip
-    _hip.lib()
-    ctx = DeviceMapContext.for_job(op, capacity, d)
-    ctx.emit.words(torch.frombuffer(bytearray(b"warm up the device plane\n"), dtype=torch.uint8).to(d))
-    finalize_table(ctx.table, ctx.source(), 1, None, need_keys=True)
-    STATS["maps_cuda"] = max(0, STATS.get("maps_cuda", 0) - 1)  # (not a job)
     from . import job as job_mod
-    job_mod._reduce_table(d, op, 1 << 21)
-    torch.cuda.synchronize(d)
+    with PLANE_LOCK:  # (worker threads of one process share the plane's buffers)
+        _hip.lib()
+        ctx = DeviceMapContext.for_job(op, capacity, d)
+        ctx.emit.words(torch.frombuffer(bytearray(b"warm up the device plane\n"), dtype=torch.uint8).to(d))
+        finalize_table(ctx.table, ctx.source(), 1, None, need_keys=True)
+        STATS["maps_cuda"] = max(0, STATS.get("maps_cuda", 0) - 1)  # (not a job)
+        job_mod._reduce_table(d, op, 1 << 21)
+        torch.cuda.synchronize(d)
 
 
 class DeviceMapContext:
