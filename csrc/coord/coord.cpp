@@ -485,6 +485,9 @@ class Store {
     fflush(journal);
   }
 
+  // (Deadlines are on system_clock: a condition-variable wait on it is a
+  // pthread_cond_timedwait, which ThreadSanitizer understands; steady_clock
+  // waits go through pthread_cond_clockwait, which it does not intercept.)
   // Long polls: every mutation of a database bumps its count and wakes the
   // waiters (one condition variable for the store; waits are short and few:
   // one per idle worker and one for the server's monitor).
@@ -502,7 +505,7 @@ class Store {
     const std::string db = r.str();
     const double ms = to_d(r.str());
     if (!r.ok || !(ms > 0)) return 1;
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds((long long)(ms * 1000.0));
+    const auto deadline = std::chrono::system_clock::now() + std::chrono::microseconds((long long)(ms * 1000.0));
     const uint64_t tv = tver[db];
     uint64_t v = ver[db];
     for (;;) {
@@ -525,7 +528,7 @@ class Store {
     const double ms = to_d(r.str());
     if (!r.ok) return -1;
     if (ms > 0)
-      cv.wait_until(g, std::chrono::steady_clock::now() + std::chrono::microseconds((long long)(ms * 1000.0)),
+      cv.wait_until(g, std::chrono::system_clock::now() + std::chrono::microseconds((long long)(ms * 1000.0)),
                     [&] { return ver[db] != since; });
     w.i((long long)ver[db]);
     return 0;

@@ -86,7 +86,25 @@ struct Conn {
   }
 };
 
-enum : uint16_t { JOB_INSERT = 20, JOB_CLAIM = 24, PT_OPEN = 60, PT_LOCK = 62, PT_UNLOCK = 63 };
+enum : uint16_t {
+  JOB_INSERT = 20, JOB_CLAIM = 24, JOB_CLAIM_WAIT = 31, BLOB_PUT_MANY = 54, BLOB_GET_MANY = 55, BLOB_DEL_MANY = 56,
+  PT_OPEN = 60, PT_LOCK = 62, PT_UNLOCK = 63
+};
+
+// A blob body whose every byte is a function of (writer, version): a reader
+// can tell a torn or mixed body from an intact one.
+std::string body_of(int t, int k, size_t n) {
+  std::string b(n, '\0');
+  for (size_t i = 0; i < n; ++i) b[i] = (char)((t * 131 + k * 7 + (int)(i % 251)) & 0xFF);
+  b.replace(0, 8, std::to_string(1000 + t).substr(0, 4) + std::to_string(1000 + k % 9000).substr(0, 4));
+  return b;
+}
+
+bool intact(const std::string& b) {
+  if (b.size() < 8) return false;
+  const int t = atoi(b.substr(0, 4).c_str()) - 1000, k = atoi(b.substr(4, 4).c_str()) - 1000;
+  return b == body_of(t, k, b.size());
+}
 
 }  // namespace
 
@@ -156,11 +174,74 @@ int main(int argc, char** argv) {
       }
     });
   for (auto& x : th) x.join();
+  th.clear();
   if (max_inside.load() != 1 || sections.load() != (long)T * K) {
     fprintf(stderr, "lock check failed: max %ld holders at once, %ld sections\n", max_inside.load(),
             sections.load());
     return 1;
   }
-  printf("coord_stress ok: %d threads, %d jobs claimed once each, %ld locked sections\n", T, N, sections.load());
+  // --- blobs: concurrent batched puts / gets / deletes of 64 KiB bodies, one
+  // name shared by every thread (its body must always be one writer's intact
+  // version: bodies are swapped in whole, never copied under a reader)
+  std::atomic<int> blob_bad{0};
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      Conn c(port);
+      std::vector<std::string> out;
+      for (int k = 0; k < 60; ++k) {
+        const std::string own = "own." + std::to_string(t) + "." + std::to_string(k);
+        const std::string mine = body_of(t, k, 65536);
+        c.req(BLOB_PUT_MANY, {"stress", own, mine, "shared", body_of(t, k, 32768 + 4096 * (k % 8))});
+        if (c.req(BLOB_GET_MANY, {"stress", own, "shared"}, &out) != 0 || out.size() != 4 || out[0] != "1" ||
+            out[1] != mine || out[2] != "1" || !intact(out[3]))
+          blob_bad.fetch_add(1);
+        if (k % 3 == 2) c.req(BLOB_DEL_MANY, {"stress", own});
+      }
+    });
+  for (auto& x : th) x.join();
+  th.clear();
+  if (blob_bad.load()) {
+    fprintf(stderr, "blob check failed: %d bad reads\n", blob_bad.load());
+    return 1;
+  }
+  // --- long-poll claims: claimers block in JOB_CLAIM_WAIT while one thread
+  // inserts jobs one at a time; every job is claimed exactly once and the
+  // claimers return once the inserter is done and the queue stays empty
+  const int N2 = 400;
+  std::vector<std::atomic<int>> seen2(N2);
+  for (auto& x : seen2) x = 0;
+  std::atomic<bool> inserting{true};
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      Conn c(port);
+      std::vector<std::string> out;
+      const std::string worker = "lp" + std::to_string(t);
+      for (;;) {
+        const int st = c.req(JOB_CLAIM_WAIT, {"stress", "50", "lp_jobs", worker, worker + "-tmp", "1.0", "1"}, &out);
+        if (st == 0) {
+          seen2[atoi(out.at(0).c_str())].fetch_add(1);
+        } else if (!inserting.load()) {
+          break;
+        }
+      }
+    });
+  {
+    Conn c(port);
+    for (int i = 0; i < N2; ++i) {
+      c.req(JOB_INSERT, {"stress", "lp_jobs", std::to_string(i), "{}", "0"});
+      if (i % 50 == 0) usleep(2000);
+    }
+    usleep(100000);  // every job claimable before the claimers may stop
+    inserting = false;
+  }
+  for (auto& x : th) x.join();
+  int bad2 = 0;
+  for (int i = 0; i < N2; ++i) bad2 += seen2[i].load() != 1;
+  if (bad2) {
+    fprintf(stderr, "long-poll claim check failed: %d jobs not claimed exactly once\n", bad2);
+    return 1;
+  }
+  printf("coord_stress ok: %d threads, %d jobs claimed once each, %ld locked sections, blobs intact, %d long-poll "
+         "claims\n", T, N, sections.load(), N2);
   return 0;
 }

@@ -5,7 +5,10 @@ together with a multi-threaded stress client (csrc/coord/coord_stress.cpp)
 under ThreadSanitizer and under AddressSanitizer + UndefinedBehaviorSanitizer:
 concurrent atomic job claims must hand every job out exactly once (the
 reference's update-then-find claim could not guarantee that), persistent-table
-locks must be exclusive, and neither sanitizer may report anything."""
+locks must be exclusive, concurrent batched blob puts/gets/deletes must only
+ever read intact bodies (they are swapped in whole outside the store lock),
+long-poll claims must also hand every job out exactly once, and neither
+sanitizer may report anything."""
 import os
 import shutil
 import subprocess
