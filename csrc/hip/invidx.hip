@@ -540,6 +540,127 @@ __global__ void ii_word_heads_kernel(const u64* __restrict__ keys, const u32* __
   }
 }
 
+// Sorted posting keys -> word lists in one count + one scatter pass (replaces
+// unique scatter + split + a device-wide scan of per-posting head flags + the
+// head write: four passes over n keys).  Per 4096-key tile: kept postings
+// (all, or the distinct ones for concat_unique) and word heads (the word part
+// key >> doc_bits differs from the previous key's; a head is always kept) are
+// counted; after a scan of the two small tile-count arrays the scatter writes
+// every kept posting's doc id at its rank and every word's (slot, start).
+__device__ __forceinline__ void gw_flags(u64 k, u64 prev, bool first, int unique, u32 doc_bits, bool& keep,
+                                         bool& head) {
+  keep = first || !unique || k != prev;
+  head = first || (k >> doc_bits) != (prev >> doc_bits);
+}
+
+__global__ void __launch_bounds__(UQ_T) gw_count_kernel(const u64* __restrict__ keys, u64 n, u32 doc_bits, int unique,
+                                                        u32* __restrict__ tc /* [2][tiles] */, u64 tiles) {
+  const int t = threadIdx.x, lane = t & 63;
+  const u64 tile0 = (u64)blockIdx.x * UQ_TILE;
+  u32 ck = 0, ch = 0;
+#pragma unroll 4
+  for (int r = 0; r < UQ_ITEMS; ++r) {
+    const u64 i = tile0 + (u64)r * UQ_T + t;
+    const u64 k = i < n ? keys[i] : 0;
+    u64 prev = __shfl_up(k, 1);
+    if (lane == 0) prev = (i > 0 && i - 1 < n) ? keys[i - 1] : ~k;
+    if (i < n) {
+      bool keep, head;
+      gw_flags(k, prev, i == 0, unique, doc_bits, keep, head);
+      ck += keep ? 1u : 0u;
+      ch += head ? 1u : 0u;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    ck += __shfl_xor(ck, o);
+    ch += __shfl_xor(ch, o);
+  }
+  __shared__ u32 w[2][UQ_T / 64];
+  if (lane == 0) {
+    w[0][t >> 6] = ck;
+    w[1][t >> 6] = ch;
+  }
+  __syncthreads();
+  if (t == 0) {
+    tc[blockIdx.x] = w[0][0] + w[0][1] + w[0][2] + w[0][3];
+    tc[tiles + blockIdx.x] = w[1][0] + w[1][1] + w[1][2] + w[1][3];
+  }
+}
+
+__device__ __forceinline__ u32 block_excl_256(u32 c, u32* w /* [4] */, u32& total) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  u32 incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) w[wave] = incl;
+  __syncthreads();
+  u32 base = 0;
+  total = 0;
+#pragma unroll
+  for (int x = 0; x < UQ_T / 64; ++x) {
+    base += x < wave ? w[x] : 0u;
+    total += w[x];
+  }
+  return base + incl - c;
+}
+
+__global__ void __launch_bounds__(UQ_T) gw_scatter_kernel(const u64* __restrict__ keys, u64 n, u32 doc_bits,
+                                                          long long doc_base, u64 slot_mask, int unique,
+                                                          const u32* __restrict__ off /* [2][tiles] */, u64 tiles,
+                                                          int* __restrict__ doc, long long* __restrict__ word_slot,
+                                                          long long* __restrict__ word_start) {
+  __shared__ u64 sk[UQ_TILE + 1];  // sk[0] = the key before the tile
+  __shared__ int sd[UQ_TILE];
+  __shared__ u32 w[2][UQ_T / 64];
+  const int t = threadIdx.x;
+  const u64 tile0 = (u64)blockIdx.x * UQ_TILE;
+#pragma unroll 4
+  for (int r = 0; r < UQ_ITEMS; ++r) {
+    const u64 i = tile0 + (u64)r * UQ_T + t;
+    sk[1 + r * UQ_T + t] = i < n ? keys[i] : 0;
+  }
+  if (t == 0) sk[0] = tile0 > 0 ? keys[tile0 - 1] : ~keys[0];
+  __syncthreads();
+  u64 k[UQ_ITEMS];
+  u32 mk = 0, mh = 0;
+  {
+    u64 prev = sk[t * UQ_ITEMS];
+#pragma unroll
+    for (int j = 0; j < UQ_ITEMS; ++j) {
+      k[j] = sk[1 + t * UQ_ITEMS + j];
+      const u64 i = tile0 + (u64)t * UQ_ITEMS + j;
+      if (i < n) {
+        bool keep, head;
+        gw_flags(k[j], prev, i == 0, unique, doc_bits, keep, head);
+        mk |= (keep ? 1u : 0u) << j;
+        mh |= (head ? 1u : 0u) << j;
+      }
+      prev = k[j];
+    }
+  }
+  u32 tk, th;
+  u32 ok = block_excl_256(__builtin_popcount(mk), w[0], tk);
+  u32 oh = block_excl_256(__builtin_popcount(mh), w[1], th);
+  const u64 base_k = off[blockIdx.x], base_h = off[tiles + blockIdx.x];
+  const u64 dm = (1ull << doc_bits) - 1;
+#pragma unroll
+  for (int j = 0; j < UQ_ITEMS; ++j) {
+    if (mk & (1u << j)) {
+      if (mh & (1u << j)) {
+        word_slot[base_h + oh] = (long long)((k[j] >> doc_bits) & slot_mask);
+        word_start[base_h + oh] = (long long)(base_k + ok);
+        ++oh;
+      }
+      sd[ok++] = (int)((long long)(k[j] & dm) + doc_base);
+    }
+  }
+  __syncthreads();
+  for (u32 x = t; x < tk; x += UQ_T) doc[base_k + x] = sd[x];
+}
+
 }  // namespace ii
 }  // namespace mr
 
@@ -649,6 +770,27 @@ int mr_ii_word_heads(const void* keys, const void* wflag, const void* wpos, u64 
   if (n == 0) return 0;
   hipLaunchKernelGGL(ii::ii_word_heads_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)keys,
                      (const u32*)wflag, (const u32*)wpos, n, doc_bits, slot_mask, (long long*)word_slot,
+                     (long long*)word_start);
+  return (int)hipGetLastError();
+}
+
+// word grouping of sorted posting keys: pass 1 fills tc[2][mr_ii_unique_tiles(n)]
+int mr_ii_group_count(const void* keys, u64 n, u32 doc_bits, int unique, void* tc, hipStream_t s) {
+  if (n == 0) return 0;
+  const u64 tiles = mr_ii_unique_tiles(n);
+  hipLaunchKernelGGL(ii::gw_count_kernel, dim3((unsigned)tiles), dim3(ii::UQ_T), 0, s, (const u64*)keys, n, doc_bits,
+                     unique, (u32*)tc, tiles);
+  return (int)hipGetLastError();
+}
+
+// pass 2 (after an exclusive scan of tc into off): doc ids of the kept postings,
+// (slot, start) of every word
+int mr_ii_group_scatter(const void* keys, u64 n, u32 doc_bits, long long doc_base, u64 slot_mask, int unique,
+                        const void* off, void* doc, void* word_slot, void* word_start, hipStream_t s) {
+  if (n == 0) return 0;
+  const u64 tiles = mr_ii_unique_tiles(n);
+  hipLaunchKernelGGL(ii::gw_scatter_kernel, dim3((unsigned)tiles), dim3(ii::UQ_T), 0, s, (const u64*)keys, n,
+                     doc_bits, doc_base, slot_mask, unique, (const u32*)off, tiles, (int*)doc, (long long*)word_slot,
                      (long long*)word_start);
   return (int)hipGetLastError();
 }

@@ -67,6 +67,8 @@ _SIGS = {
     "mr_ii_unique_tiles": [_u64],
     "mr_ii_unique_count": [_p, _u64, _p, _p],
     "mr_ii_unique_scatter": [_p, _u64, _p, _p, _p],
+    "mr_ii_group_count": [_p, _u64, _u32, _i32, _p, _p],
+    "mr_ii_group_scatter": [_p, _u64, _u32, ctypes.c_longlong, _u64, _i32, _p, _p, _p, _p, _p],
     "mr_ii_split": [_p, _u64, _u32, ctypes.c_longlong, _p, _p, _p],
     "mr_ii_word_heads": [_p, _p, _p, _u64, _u32, _u64, _p, _p, _p],
     "mr_ii_insert_slots": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _p, _p],

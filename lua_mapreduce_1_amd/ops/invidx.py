@@ -208,6 +208,35 @@ def sort_unique(keys: torch.Tensor, bits: int, from_bit: int = 0, runs: bool = F
     return torch.unique(keys)
 
 
+def group_words(keys: torch.Tensor, doc_bits: int, id_bits: int, doc_base: int = 0, unique: bool = True):
+    """Sorted posting keys -> (word ids int64[nw], word starts int64[nw+1],
+    docs int32[m]): :func:`split_words` of the distinct keys (``unique``) or
+    of all of them.  GPU: one count pass + one scatter pass over the keys
+    (csrc/hip/invidx.hip gw_*), no per-posting flag arrays."""
+    n = keys.numel()
+    if not keys.is_cuda:
+        return split_words(torch.unique(keys) if unique else keys, doc_bits, id_bits, doc_base)
+    d = keys.device
+    if n == 0:
+        z = torch.zeros(0, dtype=torch.int64, device=d)
+        return z, torch.zeros(1, dtype=torch.int64, device=d), torch.zeros(0, dtype=torch.int32, device=d)
+    s = _hip.stream(d)
+    tiles = int(_hip.lib().mr_ii_unique_tiles(n))
+    tc = torch.empty(2 * tiles, dtype=torch.int32, device=d)
+    _hip.call("mr_ii_group_count", _hip.ptr(keys), n, doc_bits, 1 if unique else 0, _hip.ptr(tc), s)
+    ok, nk = exclusive_scan(tc[:tiles])
+    oh, nh = exclusive_scan(tc[tiles:])
+    off = torch.cat([ok, oh]).contiguous()
+    m, nw = (int(x) for x in torch.stack([nk.reshape(()), nh.reshape(())]).tolist())  # one synchronisation
+    docs = torch.empty(m, dtype=torch.int32, device=d)
+    wid = torch.empty(nw, dtype=torch.int64, device=d)
+    wstart = torch.empty(nw + 1, dtype=torch.int64, device=d)
+    wstart[nw:].fill_(m)
+    _hip.call("mr_ii_group_scatter", _hip.ptr(keys), n, doc_bits, int(doc_base), (1 << id_bits) - 1,
+              1 if unique else 0, _hip.ptr(off), _hip.ptr(docs), _hip.ptr(wid), _hip.ptr(wstart), s)
+    return wid, wstart, docs
+
+
 def split_words(ukeys: torch.Tensor, doc_bits: int, id_bits: int, doc_base: int = 0):
     """Sorted unique posting keys -> (word ids int64[nw], word starts
     int64[nw+1], docs int32[n]).  Words are runs of equal ``key >> doc_bits``

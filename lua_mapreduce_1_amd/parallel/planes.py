@@ -312,6 +312,19 @@ class ListPlane:
         return II.map_postings(eng.arena[:self._cpu_end], self.vocab, self.doc_bits)
 
     # -- sort / group ---------------------------------------------------------
+    def _words(self, keys: torch.Tensor, bits: int, from_bit: int, doc_bits: int, id_bits: int, doc_base: int,
+               runs: bool = False):
+        """Posting keys -> (word ids, word starts, docs): sorted (stable, by
+        the bits from ``from_bit``), then grouped by word (distinct postings
+        for concat_unique) — on the GPU one keys-only sort and the fused
+        count/scatter of ops/invidx.group_words."""
+        if keys.is_cuda:
+            if keys.numel():
+                _, keys = ops.sort_keys_checked([keys], bits=[bits], return_keys=True, keys_only=True, runs=runs,
+                                                from_bit=from_bit)
+            return II.group_words(keys, doc_bits, id_bits, doc_base, unique=self.unique)
+        return II.split_words(self._group(keys, bits, from_bit, runs), doc_bits, id_bits, doc_base)
+
     def _group(self, keys: torch.Tensor, bits: int, from_bit: int = 0, runs: bool = False) -> torch.Tensor:
         """Keys sorted (and made distinct for concat_unique); ``from_bit``
         (GPU): the keys are already ordered by their bits below it; ``runs``:
@@ -378,8 +391,8 @@ class ListPlane:
             raise ValueError(f"posting key needs {bits} bits (> 63): raise the vocabulary capacity bits or split "
                              "the input")
         with trace.range("mr.list.sort"):
-            ukeys = self._group(keys, bits, self.doc_bits, runs=self.streamed)
-            wid, wstart, docs = II.split_words(ukeys, self.doc_bits, vocab.id_bits, self.line_base)
+            wid, wstart, docs = self._words(keys, bits, self.doc_bits, self.doc_bits, vocab.id_bits, self.line_base,
+                                            runs=self.streamed)
             vhi, vlo, vrep = vocab.arrays()
             hi, lo, rep = vhi[wid], vlo[wid], vrep[wid]
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
@@ -450,8 +463,8 @@ class ListPlane:
         # received in source-rank order, each source's lists sorted, and the
         # ranks' line ranges increasing with the rank: every word's lines are
         # already in order, so the sort orders the word bits only
-        sk = self._group(rkeys, rv.id_bits + 32, 32, runs=True)  # one run of word bits per received list
-        wid2, wstart2, docs2 = II.split_words(sk, 32, rv.id_bits, 0)
+        # one run of word bits per received list
+        wid2, wstart2, docs2 = self._words(rkeys, rv.id_bits + 32, 32, 32, rv.id_bits, 0, runs=True)
         vhi, vlo, vrep = rv.arrays()
         return vhi[wid2], vlo[wid2], vrep[wid2], rblob, wstart2, docs2, failed_total
 
