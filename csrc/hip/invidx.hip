@@ -418,20 +418,6 @@ __global__ void ii_add_dest_kernel(u64* __restrict__ keys, u64 n, const u32* __r
 }
 
 // Unique sorted keys -> keep flags (1 at i if i == 0 or key[i] != key[i-1]).
-__global__ void ii_unique_flags_kernel(const u64* __restrict__ keys, u64 n, u32* __restrict__ flags) {
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
-}
-
-// Scatter kept keys: out[pos[i]] = keys[i] where flags[i].
-__global__ void ii_compact_kernel(const u64* __restrict__ keys, const u32* __restrict__ flags,
-                                  const u32* __restrict__ pos, u64 n, u64* __restrict__ out) {
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    if (flags[i]) out[pos[i]] = keys[i];
-}
-
 // Fused "sorted keys -> distinct keys" (replaces flags + 3-launch scan +
 // compact, which wrote and re-read two n-word arrays): uq_count_kernel counts
 // the run heads of each 4096-key tile, the tile counts are scanned, and
@@ -510,34 +496,6 @@ __global__ void __launch_bounds__(UQ_T) uq_scatter_kernel(const u64* __restrict_
   __syncthreads();
   const u64 ob = tile_off[blockIdx.x];
   for (u32 x = t; x < total; x += UQ_T) out[ob + x] = sk[x];
-}
-
-// Split unique posting keys into word boundaries and doc ids:
-//   wflag[i] = 1 if the word part (key >> doc_bits) differs from key[i-1]'s;
-//   doc[i]   = (key & doc_mask) + doc_base.
-__global__ void ii_split_kernel(const u64* __restrict__ keys, u64 n, u32 doc_bits, long long doc_base,
-                                u32* __restrict__ wflag, int* __restrict__ doc) {
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  const u64 dm = (1ull << doc_bits) - 1;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const u64 k = keys[i];
-    wflag[i] = (i == 0 || (k >> doc_bits) != (keys[i - 1] >> doc_bits)) ? 1u : 0u;
-    doc[i] = (int)((long long)(k & dm) + doc_base);
-  }
-}
-
-// Word heads -> per-word (slot, start): wid = wpos[i] at heads.
-__global__ void ii_word_heads_kernel(const u64* __restrict__ keys, const u32* __restrict__ wflag,
-                                     const u32* __restrict__ wpos, u64 n, u32 doc_bits, u64 slot_mask,
-                                     long long* __restrict__ word_slot, long long* __restrict__ word_start) {
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    if (wflag[i]) {
-      const u32 w = wpos[i];
-      word_slot[w] = (long long)((keys[i] >> doc_bits) & slot_mask);
-      word_start[w] = (long long)i;
-    }
-  }
 }
 
 // Sorted posting keys -> word lists in one count + one scatter pass (replaces
@@ -726,13 +684,6 @@ int mr_ii_add_dest(void* keys, u64 n, const void* dest, u32 doc_bits, u64 slot_m
   return (int)hipGetLastError();
 }
 
-int mr_ii_unique_flags(const void* keys, u64 n, void* flags, hipStream_t s) {
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(ii::ii_unique_flags_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)keys, n,
-                     (u32*)flags);
-  return (int)hipGetLastError();
-}
-
 u64 mr_ii_unique_tiles(u64 n) { return (n + ii::UQ_TILE - 1) / ii::UQ_TILE; }
 
 // pass 1: per-tile head counts into tc[mr_ii_unique_tiles(n)]
@@ -748,29 +699,6 @@ int mr_ii_unique_scatter(const void* keys, u64 n, const void* tile_off, void* ou
   if (n == 0) return 0;
   hipLaunchKernelGGL(ii::uq_scatter_kernel, dim3((unsigned)mr_ii_unique_tiles(n)), dim3(ii::UQ_T), 0, s,
                      (const u64*)keys, n, (const u32*)tile_off, (u64*)out);
-  return (int)hipGetLastError();
-}
-
-int mr_ii_compact(const void* keys, const void* flags, const void* pos, u64 n, void* out, hipStream_t s) {
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(ii::ii_compact_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)keys,
-                     (const u32*)flags, (const u32*)pos, n, (u64*)out);
-  return (int)hipGetLastError();
-}
-
-int mr_ii_split(const void* keys, u64 n, u32 doc_bits, long long doc_base, void* wflag, void* doc, hipStream_t s) {
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(ii::ii_split_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)keys, n, doc_bits,
-                     doc_base, (u32*)wflag, (int*)doc);
-  return (int)hipGetLastError();
-}
-
-int mr_ii_word_heads(const void* keys, const void* wflag, const void* wpos, u64 n, u32 doc_bits, u64 slot_mask,
-                     void* word_slot, void* word_start, hipStream_t s) {
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(ii::ii_word_heads_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, (const u64*)keys,
-                     (const u32*)wflag, (const u32*)wpos, n, doc_bits, slot_mask, (long long*)word_slot,
-                     (long long*)word_start);
   return (int)hipGetLastError();
 }
 

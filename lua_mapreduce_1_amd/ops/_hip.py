@@ -62,15 +62,11 @@ _SIGS = {
     "mr_ii_map": [_p, _u64, _u64, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _u64, _p, _p],
     "mr_ii_advance": [_p, _p, _p],
     "mr_ii_add_dest": [_p, _u64, _p, _u32, _u64, _u32, _p],
-    "mr_ii_unique_flags": [_p, _u64, _p, _p],
-    "mr_ii_compact": [_p, _p, _p, _u64, _p, _p],
     "mr_ii_unique_tiles": [_u64],
     "mr_ii_unique_count": [_p, _u64, _p, _p],
     "mr_ii_unique_scatter": [_p, _u64, _p, _p, _p],
     "mr_ii_group_count": [_p, _u64, _u32, _i32, _p, _p],
     "mr_ii_group_scatter": [_p, _u64, _u32, ctypes.c_longlong, _u64, _i32, _p, _p, _p, _p, _p],
-    "mr_ii_split": [_p, _u64, _u32, ctypes.c_longlong, _p, _p, _p],
-    "mr_ii_word_heads": [_p, _p, _p, _u64, _u32, _u64, _p, _p, _p],
     "mr_ii_insert_slots": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _p, _p],
     "mr_ii_seg_gather": [_p, _p, _p, _u64, _u64, _p, _p, _p],
     "mr_ts_gen": [_p, _u64, _u64, _u64, _p],

@@ -240,26 +240,10 @@ def group_words(keys: torch.Tensor, doc_bits: int, id_bits: int, doc_base: int =
 def split_words(ukeys: torch.Tensor, doc_bits: int, id_bits: int, doc_base: int = 0):
     """Sorted unique posting keys -> (word ids int64[nw], word starts
     int64[nw+1], docs int32[n]).  Words are runs of equal ``key >> doc_bits``
-    (destination bits included, so a word never spans two destinations)."""
+    (destination bits included, so a word never spans two destinations).
+    CPU; the GPU groups sorted keys with :func:`group_words`."""
     n = ukeys.numel()
     id_mask = (1 << id_bits) - 1
-    if ukeys.is_cuda:
-        d = ukeys.device
-        s = _hip.stream(d)
-        if n == 0:
-            z = torch.zeros(0, dtype=torch.int64, device=d)
-            return z, torch.zeros(1, dtype=torch.int64, device=d), torch.zeros(0, dtype=torch.int32, device=d)
-        wflag = torch.empty(n, dtype=torch.int32, device=d)
-        docs = torch.empty(n, dtype=torch.int32, device=d)
-        _hip.call("mr_ii_split", _hip.ptr(ukeys), n, doc_bits, int(doc_base), _hip.ptr(wflag), _hip.ptr(docs), s)
-        wpos, total = exclusive_scan(wflag)
-        nw = int(total.item())
-        wid = torch.empty(nw, dtype=torch.int64, device=d)
-        wstart = torch.empty(nw + 1, dtype=torch.int64, device=d)
-        wstart[nw:].fill_(n)
-        _hip.call("mr_ii_word_heads", _hip.ptr(ukeys), _hip.ptr(wflag), _hip.ptr(wpos), n, doc_bits, id_mask,
-                  _hip.ptr(wid), _hip.ptr(wstart), s)
-        return wid, wstart, docs
     wk = ukeys >> doc_bits
     flags = torch.ones(n, dtype=torch.bool)
     if n > 1:
