@@ -10,8 +10,9 @@
 // where word_slot is the word's slot in the HBM hash table (a dense key id),
 // doc the line index and dest the owning rank (added after the map).  A radix
 // sort of those keys groups by destination, then word, then document — exactly
-// the shuffle + k-way merge of the reference — and adjacent duplicates (a word
-// repeated in one line) are dropped by a compaction.
+// the shuffle + k-way merge of the reference — and one count + scatter pass
+// (gw_*) drops adjacent duplicates (a word repeated in one line) and cuts the
+// sorted postings into per-word lists.
 //
 // ii_map_kernel (one 512-thread workgroup per chunk, 8 KiB tiles):
 //   1. stage the tile + halo into LDS with a whitespace bitmap and a newline
