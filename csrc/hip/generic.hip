@@ -18,6 +18,7 @@
 // Keys come either pre-encoded (hi, lo, rep) or as byte spans (start, len) of
 // a text buffer, packed here in the insert kernel (no intermediate key arrays).
 #include <hip/hip_runtime.h>
+#include <climits>
 #include "mr_common.h"
 #include "hashtab.h"
 
@@ -211,6 +212,158 @@ __global__ void __launch_bounds__(256) slot_compact_kernel(GTab g, u64 cap, long
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fold mode with an LDS combine (skewed keys: a Zipf-hot key would otherwise
+// take one memory-side atomic per row, all on the same address).  A block
+// takes CB_ROWS consecutive rows: keys of <= 15 bytes are combined in a
+// CB_SLOTS-slot LDS table whose per-slot partial columns are folded with LDS
+// atomics (f32 columns accumulate in f64); the block then inserts each of its
+// distinct keys into the HBM table once and folds the partials with one
+// global atomic per column.  Long keys (prefix + hash, verified by bytes in
+// the global table) and rows past the LDS table's load limit take the direct
+// per-row path of agg_insert_kernel.
+constexpr int CB_T = 256, CB_ITEMS = 16, CB_ROWS = CB_T * CB_ITEMS, CB_SLOTS = 1024;
+constexpr int CB_LIMIT = CB_SLOTS * 3 / 4, CB_PROBES = 32;
+
+__device__ __forceinline__ long long cb_identity(int dtype, int op) {
+  if (dtype == VT_I64) return op == OP_MIN ? LLONG_MAX : (op == OP_MAX ? LLONG_MIN : 0ll);
+  return __double_as_longlong(op == OP_MIN ? __builtin_inf() : (op == OP_MAX ? -__builtin_inf() : 0.0));
+}
+
+__device__ __forceinline__ void cb_lds_fold(long long* acc, const Cols& c, int j, u64 i) {
+  const int op = c.op[j];
+  if (c.dtype[j] == VT_I64) {
+    const long long v = rd_i64(c, j, i);
+    if (op == OP_MIN) atomicMin(acc, v);
+    else if (op == OP_MAX) atomicMax(acc, v);
+    else atomicAdd((unsigned long long*)acc, (unsigned long long)v);
+  } else {
+    double* p = (double*)acc;
+    const double v = c.dtype[j] == VT_F64 ? rd_f64(c, j, i) : (double)rd_f32(c, j, i);
+    if (op == OP_MIN) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else if (op == OP_MAX) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+// One block partial (bits in the LDS accumulator's representation) into slot.
+__device__ __forceinline__ void cb_global_fold(const Cols& c, int j, u64 slot, long long bits) {
+  const int op = c.op[j];
+  if (c.dtype[j] == VT_I64) {
+    long long* p = (long long*)c.dst[j] + slot;
+    if (op == OP_MIN) atomicMin(p, bits);
+    else if (op == OP_MAX) atomicMax(p, bits);
+    else atomicAdd((unsigned long long*)p, (unsigned long long)bits);
+  } else if (c.dtype[j] == VT_F64) {
+    double* p = (double*)c.dst[j] + slot;
+    const double v = __longlong_as_double(bits);
+    if (op == OP_MIN) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (op == OP_MAX) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    float* p = (float*)c.dst[j] + slot;
+    const float v = (float)__longlong_as_double(bits);
+    if (op == OP_MIN) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (op == OP_MAX) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// LDS slot of a packed key (claimed if absent), or -1 (table at its limit).
+// A key of <= 7 bytes is its own tag (one LDS read on a hit); longer packed
+// keys use a hashed tag plus the (hi, lo) published by the claimer (lo last).
+__device__ __forceinline__ int cb_slot(u64* tag, u64* khi, u64* klo, u64* krep, u32* nclaimed, u64 hi, u64 lo,
+                                       u64 rep) {
+  u64 h = hi ^ (lo * 0x9E3779B97F4A7C15ull);
+  h ^= h >> 31;
+  h *= 0xC2B2AE3D27D4EB4Full;
+  h ^= h >> 29;
+  const bool exact = (lo - 1 < 7) && (hi & 0xFFull) == 0;
+  const u64 t = exact ? (hi | lo) : ((h & ~0xFFull) | 0x80ull);
+  u32 s = (u32)(h >> 40) & (CB_SLOTS - 1);
+  for (int probes = 0; probes < CB_PROBES;) {
+    u64 cur = __hip_atomic_load(&tag[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == 0) {
+      if (__hip_atomic_load(nclaimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (u32)CB_LIMIT) return -1;
+      u64 expected = 0;
+      if (__hip_atomic_compare_exchange_strong(&tag[s], &expected, t, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        khi[s] = hi;
+        krep[s] = rep;
+        __hip_atomic_fetch_add(nclaimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&klo[s], lo, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return (int)s;
+      }
+      cur = expected;
+    }
+    if (cur == t) {
+      if (exact) return (int)s;
+      const u64 l = __hip_atomic_load(&klo[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (l == 0) continue;  // the claimer has not published yet: re-read this slot
+      if (l == lo && khi[s] == hi) return (int)s;
+    }
+    s = (s + 1) & (CB_SLOTS - 1);
+    ++probes;
+  }
+  return -1;
+}
+
+__global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 n, Cols c) {
+  extern __shared__ __attribute__((aligned(16))) u64 lds[];
+  u64* tag = lds;
+  u64* khi = tag + CB_SLOTS;
+  u64* klo = khi + CB_SLOTS;
+  u64* krep = klo + CB_SLOTS;
+  long long* acc = (long long*)(krep + CB_SLOTS);  // [c.k][CB_SLOTS]
+  __shared__ u32 nclaimed;
+  const int t = threadIdx.x;
+  for (int s = t; s < CB_SLOTS; s += CB_T) {
+    tag[s] = 0;
+    klo[s] = 0;
+    for (int j = 0; j < c.k; ++j) acc[j * CB_SLOTS + s] = cb_identity(c.dtype[j], c.op[j]);
+  }
+  if (t == 0) nclaimed = 0;
+  __syncthreads();
+  u32 claims = 0;
+  const u64 r0 = (u64)blockIdx.x * CB_ROWS;
+  for (int it = 0; it < CB_ITEMS; ++it) {
+    const u64 i = r0 + (u64)it * CB_T + t;
+    if (i >= n) break;
+    u64 hi = 0, lo = 0, rep = 0;
+    if (ks.text) {
+      const long long st = ks.starts[i];
+      const int len = ks.lens[i];
+      if (len <= 0 || st < 0) continue;
+      span_key(ks.text, (u64)st, (u64)len, hi, lo);
+      rep = make_rep(ks.rep_base + (u64)st, (u64)len);
+    } else {
+      hi = ks.hi[i];
+      lo = ks.lo[i];
+      rep = ks.rep ? ks.rep[i] + (ks.rep_add << REP_LEN_BITS) : 0;
+    }
+    const int s = key_is_long(lo) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, hi, lo, rep);
+    if (s >= 0) {
+      for (int j = 0; j < c.k; ++j) cb_lds_fold(&acc[j * CB_SLOTS + s], c, j, i);
+    } else {
+      u64 slot = 0;
+      const int r = gtab_insert(g, hi, lo, 0, rep, OP_NONE, &slot);
+      claims += r == 2;
+      if (r)
+        for (int j = 0; j < c.k; ++j) fold_col(c, j, i, slot);
+    }
+  }
+  __syncthreads();
+  for (int s = t; s < CB_SLOTS; s += CB_T) {
+    if (!tag[s]) continue;
+    u64 slot = 0;
+    const int r = gtab_insert(g, khi[s], klo[s], 0, krep[s], OP_NONE, &slot);
+    claims += r == 2;
+    if (r)
+      for (int j = 0; j < c.k; ++j) cb_global_fold(c, j, slot, acc[j * CB_SLOTS + s]);
+  }
+  gtab_count_claims(g, claims);
+}
+
 // Fill a typed column with its fold identity (sum 0, min +max, max -max).
 __global__ void col_fill_kernel(void* col, u64 n, long long bits, int width) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
@@ -298,6 +451,19 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
   ks.lens = (const int*)lens;
   ks.rep_base = rep_base;
   if (!ks.text && (!ks.hi || !ks.lo)) return -2;
+  if (!a->list && a->k > 0 && n >= (u64)CB_ROWS) {
+    const size_t lds = (size_t)CB_SLOTS * (4 + (size_t)a->k) * sizeof(u64);
+    static bool lds_attr = false;  // dynamic LDS above 64 KiB (k > 4 columns) must be allowed once
+    if (!lds_attr) {
+      (void)hipFuncSetAttribute((const void*)agg_combine_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)((size_t)CB_SLOTS * (4 + MAXC) * sizeof(u64)));
+      lds_attr = true;
+    }
+    const u64 nb = (n + CB_ROWS - 1) / CB_ROWS;
+    hipLaunchKernelGGL(agg_combine_kernel, dim3((unsigned)nb), dim3(CB_T), lds, stream,
+                       ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256)), dim3(256), 0, stream,
                      ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
   return (int)hipGetLastError();

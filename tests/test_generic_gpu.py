@@ -80,15 +80,18 @@ def test_text_parse_gpu_matches_python(gpu):
     assert torch.equal(hi, di)
 
 
+@pytest.mark.parametrize("skew", [False, True], ids=["uniform", "zipf"])
 @pytest.mark.parametrize("dtype", ["i64", "f64", "f32"])
-def test_agg_table_folds_gpu(gpu, dtype):
-    """Typed sum/min/max folds of random (key, value) rows against numpy."""
+def test_agg_table_folds_gpu(gpu, dtype, skew):
+    """Typed sum/min/max folds of random (key, value) rows against numpy:
+    uniform keys (the LDS combine fills up, most rows fold straight into the
+    HBM table) and Zipf keys (hot keys combined in LDS)."""
     from lua_mapreduce_1_amd.ops import agg as A
     from lua_mapreduce_1_amd.ops import keys as K
     rng = np.random.default_rng(3)
     n, nk = 200_000, 5000
     words = [("k%d" % i).encode() * (1 + i % 3) for i in range(nk)]  # some long keys
-    idx = rng.integers(0, nk, n)
+    idx = (np.minimum(rng.zipf(1.3, n), nk) - 1) if skew else rng.integers(0, nk, n)
     blob = b"".join(words)
     off = np.cumsum([0] + [len(w) for w in words])
     starts = torch.from_numpy(off[:-1][idx].astype(np.int64))
@@ -108,7 +111,7 @@ def test_agg_table_folds_gpu(gpu, dtype):
         kb = __import__("lua_mapreduce_1_amd").ops.key_bytes_list(hi.cpu(), lo.cpu(), rep.cpu(), text.cpu())
         res[str(dev)] = {k: [x[i].item() for x in c] for i, k in enumerate(kb)}
     a, b = res["cpu"], res[str(gpu)]
-    assert set(a) == set(b) == set(words)
+    assert set(a) == set(b) == set(words[i] for i in np.unique(idx))
     for k in a:
         s0, s1 = a[k][0], b[k][0]
         if dtype == "i64":
