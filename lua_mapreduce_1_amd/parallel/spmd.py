@@ -1181,8 +1181,15 @@ class SPMDEngine:
 
     def _finalize_table(self, table, n: int, src) -> dict:
         """The fused device tail of a table: every launch and download queued
-        by one native call (mr_tail_run, csrc/hip/tail.hip)."""
-        return devmod.finalize_table_native(table, n, src, self.nparts, blob_cap=getattr(self, "_blob_cap", None))
+        by one native call (mr_tail_run, csrc/hip/tail.hip) — or, once a tail
+        of this engine had to fall back to the exact key order (long keys in
+        long runs of a shared prefix, e.g. n-grams), that order directly
+        (the fused tie fix-up would fail the same way every iteration)."""
+        cap = getattr(self, "_blob_cap", None)
+        if getattr(self, "_exact_tail", False):
+            hi, lo, val, rep = table.compact((n, False))
+            return devmod.finalize_exact_device(hi, lo, val, rep, src, self.nparts, self.partmod, blob_cap=cap)
+        return devmod.finalize_table_native(table, n, src, self.nparts, blob_cap=cap)
 
     def _reduce_insert_received(self, rbuf, recv_counts, rows: int) -> int:
         """Received records -> this rank's reduce table (one insert launch);
@@ -1422,6 +1429,8 @@ class SPMDEngine:
                     pend = self._finalize_table(self.red_table if sh else self.table,
                                                 n_red if sh else n_claimed, src)
                 cols = devmod.finalize_host(pend, self.partmod)
+        if cols.get("exact_fallback"):
+            self._exact_tail = True  # later iterations go straight to the exact order
         digits = len(str(max(self.nparts - 1, 0)))
         for p in range(self.nparts):
             if cols["bounds"][p + 1] > cols["bounds"][p]:

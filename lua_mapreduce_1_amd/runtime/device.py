@@ -488,6 +488,24 @@ def finalize_table_native(table, n: int, src, nparts: int, blob_cap: int | None 
             "fused": True, "hp": hp, "off": v["off"], "blob": v["blob"], "est": est, "hb": hb}
 
 
+def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=None,
+                          blob_cap: int | None = None) -> dict:
+    """The device half of a tail ordered exactly by key bytes from the start
+    (ops.exact_key_perm) — for key sets whose fused tail falls back every time.
+    Keys past the exact sort's length limit get the (partition, hi, lo) sort
+    and the host fix-up instead."""
+    part = partition_of(hi, lo, rep, src, nparts, partition_module)
+    perm = ops.exact_key_perm(part, hi, lo, rep, src, nparts) if src is not None else None
+    exact = perm is not None
+    if perm is None:
+        perm = ops.sort_keys_checked([part.to(torch.int64), hi, lo],
+                                     bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
+    pend = finalize_device(hi[perm], lo[perm], val[perm], rep[perm], src, nparts, partition_module, part=part[perm],
+                           _presorted=True, blob_cap=blob_cap)
+    pend["exact"] = exact
+    return pend
+
+
 def finalize_table(table, src, nparts: int, partition_module=None, need_keys: bool = False) -> dict:
     """HBM table -> host result columns (a worker's map tail): the fused
     native tail (one call: compact, FNV partition, sort, key bytes, one
@@ -573,9 +591,11 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
             if perm is None:
                 perm = ops.sort_keys_checked([p2.to(torch.int64), ahi, alo],
                                              bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
-            return finalize(ahi[perm], alo[perm], aval[perm], arep[perm], src, nparts, partition_module,
-                            part=p2[perm], _presorted=True, need_keys=need_keys, _exact=exact,
-                            blob_cap=max(int(blob.numel()), nbytes))
+            out = finalize(ahi[perm], alo[perm], aval[perm], arep[perm], src, nparts, partition_module,
+                           part=p2[perm], _presorted=True, need_keys=need_keys, _exact=exact,
+                           blob_cap=max(int(blob.numel()), nbytes))
+            out["exact_fallback"] = exact
+            return out
         # offsets stay int32 when the blob is < 2 GiB (no host-side widening pass)
         if pend.get("fused"):
             h_val, h_off, h_blob, h_counts = f_val, f_off, hb.numpy(), f_counts
