@@ -143,6 +143,93 @@ __global__ void __launch_bounds__(256) rec_tie_pairs_kernel(const u32* __restric
   }
 }
 
+// The same fix-up in two streaming-friendly steps (the single kernel above
+// waits on a dependent perm -> row load chain in every wave that holds a
+// pair, ~0.56 ms per 100 M rows): rec_tie_scan_kernel only reads the sorted
+// prefixes and keeps each block's run starts (TS_POS positions per block, at
+// most TS_CAP starts, in LDS, then in the block's own segment — no global
+// atomics); rec_tie_fix_kernel then gives every listed run a thread of its
+// own, so all the random loads are independent.  Runs of 3 or more go to the
+// run list of rec_tie_runs_kernel as before.
+constexpr int TS_POS = 4096;
+constexpr int TS_CAP = 1024;
+
+__global__ void __launch_bounds__(256) rec_tie_scan_kernel(const u32* __restrict__ sk, u64 n,
+                                                           u32* __restrict__ counts, u32* __restrict__ seg,
+                                                           u32* __restrict__ bad) {
+  __shared__ u32 cnt;
+  __shared__ u32 list[TS_CAP];
+  const u32 t = threadIdx.x;
+  if (t == 0) cnt = 0;
+  __syncthreads();
+  const u64 base = (u64)blockIdx.x * TS_POS;
+  const bool al = (((uintptr_t)sk & 15) == 0);
+#pragma unroll
+  for (int it = 0; it < TS_POS / 1024; ++it) {
+    const u64 i0 = base + (u64)it * 1024 + 4ull * t;
+    if (i0 >= n) break;
+    u32 v[7];  // sk[i0 - 1 .. i0 + 5]
+    if (i0 + 4 <= n && al) {
+      const uint4 q = *reinterpret_cast<const uint4*>(sk + i0);
+      v[1] = q.x; v[2] = q.y; v[3] = q.z; v[4] = q.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[1 + j] = i0 + j < n ? sk[i0 + j] : 0u;
+    }
+    v[0] = i0 > 0 ? sk[i0 - 1] : ~v[1];
+    v[5] = i0 + 4 < n ? sk[i0 + 4] : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u64 i = i0 + j;
+      if (i + 1 >= n) break;
+      const u32 h = v[1 + j];
+      if (v[2 + j] == h && v[j] != h) {  // the start of a run
+        const u32 k = atomicAdd(&cnt, 1u);
+        if (k < (u32)TS_CAP) list[k] = (u32)(i - base);
+      }
+    }
+  }
+  __syncthreads();
+  const u32 m = cnt;
+  const u32 keep = m < (u32)TS_CAP ? m : (u32)TS_CAP;
+  if (t == 0) {
+    counts[blockIdx.x] = keep;
+    if (m > (u32)TS_CAP) atomicOr(bad, 1u);  // > 1/4 of the rows start a tie run: full-key sort
+  }
+  for (u32 k = t; k < keep; k += 256) seg[(u64)blockIdx.x * TS_CAP + k] = list[k];
+}
+
+__global__ void __launch_bounds__(256) rec_tie_fix_kernel(const u32* __restrict__ sk, u32* __restrict__ perm,
+                                                          const u8* __restrict__ rec, u64 n, int rb, int kb,
+                                                          const u32* __restrict__ counts,
+                                                          const u32* __restrict__ seg, u32* __restrict__ bad,
+                                                          u64* __restrict__ runs,
+                                                          unsigned long long* __restrict__ nruns, u64 runs_cap) {
+  const bool words = (rb & 3) == 0;
+  const u32 m = counts[blockIdx.x];
+  const u64 base = (u64)blockIdx.x * TS_POS;
+  for (u32 k = threadIdx.x; k < m; k += 256) {
+    const u64 i = base + seg[(u64)blockIdx.x * TS_CAP + k];
+    if (i + 1 >= n) continue;
+    const u32 h = sk[i];
+    if (i + 2 < n && sk[i + 2] == h) {  // a run of 3 or more
+      const unsigned long long x = atomicAdd(nruns, 1ull);
+      if (x < runs_cap) runs[x] = i;
+      else atomicOr(bad, 1u);
+      continue;
+    }
+    const u32 p0 = perm[i], p1 = perm[i + 1];
+    u64 a0, a1;
+    u32 b0, b1;
+    key_rest(rec + (u64)clamp_row(p0, n) * rb, kb, words, a0, b0);
+    key_rest(rec + (u64)clamp_row(p1, n) * rb, kb, words, a1, b1);
+    if (a0 > a1 || (a0 == a1 && b0 > b1)) {
+      perm[i] = p1;
+      perm[i + 1] = p0;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(64) rec_tie_runs_kernel(const u32* __restrict__ sk, u32* __restrict__ perm,
                                                           const u8* __restrict__ rec, u64 n, int rb, int kb,
                                                           u32* __restrict__ bad, const u64* __restrict__ runs,
@@ -191,8 +278,9 @@ __global__ void __launch_bounds__(64) rec_tie_runs_kernel(const u32* __restrict_
 // at run time), UNROLL independent words per thread: all permutation loads,
 // then all row loads, then all stores (tools/ts_gather_probe.py: 8 in flight).
 template <int W, int UNROLL>
-__global__ void __launch_bounds__(256) rec_gather_kernel(const u32* __restrict__ in, const u32* __restrict__ perm,
-                                                         u64 n, u32 words, u32* __restrict__ out) {
+__global__ void __launch_bounds__(256) rec_gather_kernel(const u32* __restrict__ in, u64 nin,
+                                                         const u32* __restrict__ perm, u64 n, u32 words,
+                                                         u32* __restrict__ out) {
   const u64 ww = W > 0 ? (u64)W : (u64)words;
   const u64 nw = n * ww;
   const u64 stride = (u64)gridDim.x * blockDim.x;
@@ -204,7 +292,7 @@ __global__ void __launch_bounds__(256) rec_gather_kernel(const u32* __restrict__
       const u64 w = w0 + (u64)k * stride;
       const u64 r = w / ww;
       const u64 j = w - r * ww;
-      src[k] = w < nw ? (u64)clamp_row(perm[r], n) * ww + j : 0u;
+      src[k] = w < nw ? (u64)clamp_row(perm[r], nin) * ww + j : 0u;
     }
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
@@ -219,14 +307,98 @@ __global__ void __launch_bounds__(256) rec_gather_kernel(const u32* __restrict__
   }
 }
 
+// Row gather through LDS with 16-byte accesses on both sides, for rows of rb
+// bytes (rb % 4 == 0, 16 <= rb <= 244) and 16-byte aligned buffers.  A row
+// starts 0/4/8/12 bytes into an aligned 16-byte chunk, so C = ceil((rb + 12) /
+// 16) aligned chunks cover it whatever its position: the block loads the C
+// chunks of each of its R rows (one dwordx4 per lane, all independent),
+// keeps them in LDS as an image of the aligned source with each row's start
+// offset, and writes its R output rows — R * rb bytes, contiguous and 16-byte
+// aligned — as dwordx4 stores assembled from that image.  The dword form
+// (rec_gather_kernel) issues 4x the vector-memory instructions for the same
+// bytes; the windowed-permutation probe (profiles/r3/check1/ts_move.log: 8 MB
+// windows no faster than random rows) says instructions, not DRAM, bound it.
+template <int C, int R>
+__global__ void __launch_bounds__(256) rec_gather16_kernel(const u8* __restrict__ in, u64 nin,
+                                                           const u32* __restrict__ perm, u64 n, u32 rb,
+                                                           u8* __restrict__ out) {
+  typedef u32 v4u __attribute__((ext_vector_type(4)));
+  __shared__ v4u img[R * C];
+  __shared__ u32 mis[R];
+  constexpr int PER = (R * C + 255) / 256;
+  const u32 t = threadIdx.x;
+  const u64 in_bytes = nin * (u64)rb;
+  const u64 nbatch = (n + R - 1) / R;
+  const float inv_rb = 1.0f / (float)rb;
+  const u32* img32 = reinterpret_cast<const u32*>(img);
+  for (u64 b = blockIdx.x; b < nbatch; b += gridDim.x) {
+    const u64 r0 = b * (u64)R;
+    const u32 rows = (u32)min((u64)R, n - r0);
+    v4u v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const u32 idx = t + 256u * k;
+      const u32 row = idx / C, c = idx - row * C;
+      v[k] = v4u{0u, 0u, 0u, 0u};
+      if (idx < (u32)(R * C) && row < rows) {
+        const u64 sb = (u64)clamp_row(perm[r0 + row], nin) * rb;
+        const u64 a = (sb & ~15ull) + 16ull * c;
+        if (a + 16 <= in_bytes) {
+          v[k] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + a));
+        } else {  // the chunk that runs past the buffer's end (in_bytes % 16 != 0)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (a + 4 * j < in_bytes) v[k][j] = *reinterpret_cast<const u32*>(in + a + 4 * j);
+        }
+        if (c == 0) mis[row] = (u32)(sb & 15);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const u32 idx = t + 256u * k;
+      if (idx < (u32)(R * C)) img[idx] = v[k];
+    }
+    __syncthreads();
+    const u32 obytes = rows * rb;  // < 2^16 for R <= 256, rb <= 244
+    u8* ob = out + r0 * rb;
+    const u32 nch = obytes >> 4;
+    for (u32 oc = t; oc < nch + 1; oc += 256) {
+      const u32 byte0 = oc * 16u;
+      if (byte0 >= obytes) break;
+      u32 row = (u32)((float)byte0 * inv_rb);  // exact after the corrections (byte0 < 2^24)
+      if (row * rb > byte0) --row;
+      if ((row + 1) * rb <= byte0) ++row;
+      const u32 off = byte0 - row * rb;
+      u32 w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        u32 rr = row, oo = off + 4u * j;
+        if (oo >= rb) {
+          ++rr;
+          oo -= rb;
+        }
+        w[j] = rr < rows ? img32[(rr * (u32)C * 16u + mis[rr] + oo) >> 2] : 0u;
+      }
+      if (oc < nch) {
+        __builtin_nontemporal_store(v4u{w[0], w[1], w[2], w[3]}, reinterpret_cast<v4u*>(ob + byte0));
+      } else {  // the batch's last partial chunk (rows * rb % 16 != 0): dwords
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (byte0 + 4u * j < obytes) *reinterpret_cast<u32*>(ob + byte0 + 4u * j) = w[j];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Rows whose width is not a multiple of 4 bytes: one byte per thread.
-__global__ void rec_gather_bytes_kernel(const u8* __restrict__ in, const u32* __restrict__ perm, u64 n, u64 rb,
-                                        u8* __restrict__ out) {
+__global__ void rec_gather_bytes_kernel(const u8* __restrict__ in, u64 nin, const u32* __restrict__ perm, u64 n,
+                                        u64 rb, u8* __restrict__ out) {
   const u64 nb = n * rb;
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 b = (u64)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += stride) {
     const u64 r = b / rb;
-    out[b] = in[(u64)clamp_row(perm[r], n) * rb + (b - r * rb)];
+    out[b] = in[(u64)clamp_row(perm[r], nin) * rb + (b - r * rb)];
   }
 }
 
@@ -258,6 +430,15 @@ static inline unsigned rc_grid(u64 n, unsigned cap = 8192) {
   return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
+template <int C>
+static void launch_gather16(const void* in, u64 nin, const void* perm, u64 n, int rb, void* out, hipStream_t s) {
+  constexpr int R = C <= 8 ? 256 : 128;
+  const u64 nb = (n + R - 1) / R;
+  const unsigned g = (unsigned)(nb < 65536 ? nb : 65536);
+  hipLaunchKernelGGL((rc::rec_gather16_kernel<C, R>), dim3(g), dim3(256), 0, s, (const u8*)in, nin, (const u32*)perm,
+                     n, (u32)rb, (u8*)out);
+}
+
 extern "C" {
 
 // ghist: null, or a zeroed u32[8][256] that receives the digit histograms of k32
@@ -278,33 +459,78 @@ int mr_rec_keys(const void* rec, u64 n, int rb, int kb, void* hi, void* lo, hipS
 }
 
 // ws: u64 scratch of 1 + ws_cap words (a run counter, then run starts)
+// ws: u64 scratch of mr_rec_tie_ws_words(n, ws_cap) words: a run counter,
+// ws_cap run starts (runs of 3+), then the scan's per-block counts and
+// segments (u32).  mode 1: the single-kernel fix-up (A/B probes).
+u64 mr_rec_tie_ws_words(u64 n, u64 ws_cap) {
+  const u64 g = (n + rc::TS_POS - 1) / rc::TS_POS;
+  return 1 + ws_cap + (g + g * rc::TS_CAP + 1) / 2 + 1;
+}
+
 int mr_rec_tie_fixup(const void* sk, void* perm, const void* rec, u64 n, int rb, int kb, void* bad, void* ws,
-                     u64 ws_cap, hipStream_t s) {
-  if (n < 2) return 0;
+                     u64 ws_cap, int mode, hipStream_t s) {
+  if (n < 2 || kb <= 4) return 0;  // kb <= 4: the prefix is the whole key
   u64* w = (u64*)ws;
   (void)hipMemsetAsync(w, 0, sizeof(u64), s);
-  hipLaunchKernelGGL(rc::rec_tie_pairs_kernel, dim3(rc_grid((n + 3) / 4)), dim3(256), 0, s, (const u32*)sk, (u32*)perm,
-                     (const u8*)rec, n, rb, kb, (u32*)bad, w + 1, (unsigned long long*)w, ws_cap);
+  if (mode == 1) {
+    hipLaunchKernelGGL(rc::rec_tie_pairs_kernel, dim3(rc_grid((n + 3) / 4)), dim3(256), 0, s, (const u32*)sk,
+                       (u32*)perm, (const u8*)rec, n, rb, kb, (u32*)bad, w + 1, (unsigned long long*)w, ws_cap);
+  } else {
+    const u64 g = (n + rc::TS_POS - 1) / rc::TS_POS;
+    if (g > 0x7FFFFFFFull) return -1;
+    u32* counts = reinterpret_cast<u32*>(w + 1 + ws_cap);
+    u32* seg = counts + g;
+    hipLaunchKernelGGL(rc::rec_tie_scan_kernel, dim3((unsigned)g), dim3(256), 0, s, (const u32*)sk, n, counts, seg,
+                       (u32*)bad);
+    hipLaunchKernelGGL(rc::rec_tie_fix_kernel, dim3((unsigned)g), dim3(256), 0, s, (const u32*)sk, (u32*)perm,
+                       (const u8*)rec, n, rb, kb, (const u32*)counts, (const u32*)seg, (u32*)bad, w + 1,
+                       (unsigned long long*)w, ws_cap);
+  }
   hipLaunchKernelGGL(rc::rec_tie_runs_kernel, dim3(256), dim3(64), 0, s, (const u32*)sk, (u32*)perm, (const u8*)rec,
                      n, rb, kb, (u32*)bad, (const u64*)(w + 1), (const unsigned long long*)w, ws_cap);
   return (int)hipGetLastError();
 }
 
-int mr_rec_gather(const void* in, const void* perm, u64 n, int rb, void* out, hipStream_t s) {
+// nin: rows of `in` (permutation entries >= nin read row 0).  mode: 0 = the
+// 16-byte LDS-staged gather where the shape allows it, 1 = the dword gather
+// (A/B probes and tests of both paths).
+int mr_rec_gather(const void* in, u64 nin, const void* perm, u64 n, int rb, void* out, int mode, hipStream_t s) {
   if (n == 0) return 0;
+  if (nin == 0) return -1;
   if (rb & 3) {
     hipLaunchKernelGGL(rc::rec_gather_bytes_kernel, dim3(rc_grid(n * (u64)rb, 16384)), dim3(256), 0, s,
-                       (const u8*)in, (const u32*)perm, n, (u64)rb, (u8*)out);
+                       (const u8*)in, nin, (const u32*)perm, n, (u64)rb, (u8*)out);
+    return (int)hipGetLastError();
+  }
+  const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+  if (mode == 0 && aligned && rb >= 16 && rb <= 244) {
+    switch ((rb + 27) / 16) {
+      case 2: launch_gather16<2>(in, nin, perm, n, rb, out, s); break;
+      case 3: launch_gather16<3>(in, nin, perm, n, rb, out, s); break;
+      case 4: launch_gather16<4>(in, nin, perm, n, rb, out, s); break;
+      case 5: launch_gather16<5>(in, nin, perm, n, rb, out, s); break;
+      case 6: launch_gather16<6>(in, nin, perm, n, rb, out, s); break;
+      case 7: launch_gather16<7>(in, nin, perm, n, rb, out, s); break;
+      case 8: launch_gather16<8>(in, nin, perm, n, rb, out, s); break;
+      case 9: launch_gather16<9>(in, nin, perm, n, rb, out, s); break;
+      case 10: launch_gather16<10>(in, nin, perm, n, rb, out, s); break;
+      case 11: launch_gather16<11>(in, nin, perm, n, rb, out, s); break;
+      case 12: launch_gather16<12>(in, nin, perm, n, rb, out, s); break;
+      case 13: launch_gather16<13>(in, nin, perm, n, rb, out, s); break;
+      case 14: launch_gather16<14>(in, nin, perm, n, rb, out, s); break;
+      case 15: launch_gather16<15>(in, nin, perm, n, rb, out, s); break;
+      default: launch_gather16<16>(in, nin, perm, n, rb, out, s); break;
+    }
     return (int)hipGetLastError();
   }
   const u32 words = (u32)(rb >> 2);
   const unsigned g = rc_grid(n * words, 16384);
   if (words == 25)
-    hipLaunchKernelGGL((rc::rec_gather_kernel<25, 8>), dim3(g), dim3(256), 0, s, (const u32*)in, (const u32*)perm, n,
-                       words, (u32*)out);
+    hipLaunchKernelGGL((rc::rec_gather_kernel<25, 8>), dim3(g), dim3(256), 0, s, (const u32*)in, nin,
+                       (const u32*)perm, n, words, (u32*)out);
   else
-    hipLaunchKernelGGL((rc::rec_gather_kernel<0, 8>), dim3(g), dim3(256), 0, s, (const u32*)in, (const u32*)perm, n,
-                       words, (u32*)out);
+    hipLaunchKernelGGL((rc::rec_gather_kernel<0, 8>), dim3(g), dim3(256), 0, s, (const u32*)in, nin,
+                       (const u32*)perm, n, words, (u32*)out);
   return (int)hipGetLastError();
 }
 

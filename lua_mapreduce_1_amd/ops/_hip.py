@@ -93,8 +93,8 @@ _SIGS = {
     "mr_radix_onesweep_k32": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p, _u32, _p, _i32, _p],
     "mr_rec_keys32": [_p, _u64, _i32, _i32, _p, _p, _p],
     "mr_rec_keys": [_p, _u64, _i32, _i32, _p, _p, _p],
-    "mr_rec_tie_fixup": [_p, _p, _p, _u64, _i32, _i32, _p, _p, _u64, _p],
-    "mr_rec_gather": [_p, _p, _u64, _i32, _p, _p],
+    "mr_rec_tie_fixup": [_p, _p, _p, _u64, _i32, _i32, _p, _p, _u64, _i32, _p],
+    "mr_rec_gather": [_p, _u64, _p, _u64, _i32, _p, _i32, _p],
     "mr_rec_dest32": [_p, _u64, _p, _u32, _p, _p],
     "mr_agg_insert": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _u64, _p, _p],
     "mr_slot_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
@@ -106,9 +106,10 @@ _SIGS = {
     "mr_text_field": [_p, _p, _p, _u64, _u32, _i32, _p, _p, _p],
     "mr_text_parse_f64": [_p, _p, _p, _u64, _p, _p, _p],
     "mr_text_parse_i64": [_p, _p, _p, _u64, _p, _p, _p],
+    "mr_rec_tie_ws_words": [_u64, _u64],
 }
 _RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
-                "mr_tail_bhist_bytes", "mr_onesweep_tiles"}
+                "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words"}
 
 
 def lib():

@@ -728,40 +728,83 @@ def sort_error_word(device) -> torch.Tensor | None:
 EXACT_MAX_WORDS = 32  # keys up to 256 bytes get the device's exact order
 
 
+def key_word(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.Tensor | None,
+             k: int) -> torch.Tensor:
+    """Bytes [8k, 8k+8) of every key as a big-endian int64 word, zero padded
+    past the key's end (so unsigned word order is byte order)."""
+    n = hi.numel()
+    if hi.is_cuda:
+        d = hi.device
+        w = torch.empty(n, dtype=torch.int64, device=d)
+        if n:
+            _hip.call("mr_key_word", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), _hip.ptr(src), n, k, _hip.ptr(w),
+                      _hip.stream(d))
+        return w
+    out = np.zeros(n, np.uint64)
+    for i, b in enumerate(key_bytes_list(hi, lo, rep, src)):
+        out[i] = int.from_bytes(b[8 * k:8 * k + 8].ljust(8, b"\0"), "big")
+    return torch.from_numpy(out.view(np.int64))
+
+
 def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor,
                    src: torch.Tensor | None, nparts: int) -> torch.Tensor | None:
     """Stable permutation ordering rows by (partition, exact key bytes) on the
     device, for key sets the (partition, hi, lo) sort plus the tie fix-up
     cannot order (long keys — whose lo is a hash — in long runs of a shared
-    8-byte prefix, e.g. n-grams): an LSD sort of the key as 8-byte words
-    (mr_key_word; zero-padded) with the key length as the least significant
-    column, in stages of at most 6 columns (each stage stable, permutations
-    composed).  None when a key is longer than 8 * EXACT_MAX_WORDS bytes (the
-    caller orders on the host)."""
+    8-byte prefix, e.g. n-grams).
+
+    MSD refinement over 16-byte windows of the key (mr_key_word; zero padded):
+    round 0 sorts every row by (partition, bytes 0-15, min(len, 16)); a key of
+    at most 16 bytes is then placed exactly (a shorter key that is a prefix of a
+    longer one sorts first through the length column).  Only rows that still
+    tie — long keys sharing their first 16 bytes — go to the next round, which
+    sorts them by (tie group, bytes 16-31, min(len, 32)) in place inside their
+    groups, and so on.  Each round is a stable LSD radix sort, so rows of one
+    key set keep their input order where they tie.  None when a key is longer
+    than 8 * EXACT_MAX_WORDS bytes (the caller orders on the host)."""
     n = hi.numel()
     d = hi.device
     if n == 0:
         return torch.zeros(0, dtype=torch.int64, device=d)
     _, klen = key_meta(hi, lo, rep, src, want_part=False)
+    klen = klen.to(torch.int64)
     max_len = int(klen.max())
-    nw = max(1, (max_len + 7) // 8)
-    if nw > EXACT_MAX_WORDS:
+    if (max_len + 7) // 8 > EXACT_MAX_WORDS:
         return None
-    s = _hip.stream(d)
-    cols = [part.to(torch.int64)]
-    for k in range(nw):
-        w = torch.empty(n, dtype=torch.int64, device=d)
-        _hip.call("mr_key_word", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), _hip.ptr(src), n, k, _hip.ptr(w), s)
-        cols.append(w)
-    cols.append(klen.to(torch.int64))
-    bits = [max(8, int(max(nparts, 1) - 1).bit_length())] + [64] * nw + [max(8, max_len.bit_length())]
-    perm = None
-    for end in range(len(cols), 0, -6):  # least significant stage first
-        a = max(0, end - 6)
-        grp = [c if perm is None else c[perm] for c in cols[a:end]]
-        p = sort_keys_checked(grp, bits=bits[a:end]).long()
-        perm = p if perm is None else perm[p]
-    return perm
+    pbits = max(8, int(max(nparts, 1) - 1).bit_length())
+    w1 = key_word(hi, lo, rep, src, 1)
+    lc = klen.clamp(max=16)
+    cols = [part.to(torch.int64), hi, w1, lc]
+    perm = sort_keys_checked(cols, bits=[pbits, 64, 64, 8]).long()
+    if max_len <= 16:
+        return perm
+    scols = [c[perm] for c in cols]
+    pos = torch.arange(n, dtype=torch.int64, device=d)
+    cap = 16
+    while True:
+        # ties: adjacent rows equal in every column whose keys go on past cap
+        same = scols[-1][1:] == cap
+        for c in scols:
+            same &= c[1:] == c[:-1]
+        if not bool(same.any()):
+            return perm
+        member = torch.zeros(pos.numel(), dtype=torch.bool, device=d)
+        member[1:] |= same
+        member[:-1] |= same
+        head = torch.ones(pos.numel(), dtype=torch.int64, device=d)
+        head[1:] = (~same).to(torch.int64)
+        grp = torch.cumsum(head, 0)[member]
+        grp = grp - grp[:1]
+        pos = pos[member]
+        rows = perm[pos]
+        k = cap // 8
+        rh, rl, rr = hi[rows], lo[rows], rep[rows]
+        cap += 16
+        cols = [grp, key_word(rh, rl, rr, src, k), key_word(rh, rl, rr, src, k + 1), klen[rows].clamp(max=cap)]
+        gbits = max(8, int(grp[-1]).bit_length())
+        sub = sort_keys_checked(cols, bits=[gbits, 64, 64, max(8, cap.bit_length())]).long()
+        perm[pos] = rows[sub]  # a group's rows stay inside its positions (grp is the major column)
+        scols = [c[sub] for c in cols]
 
 
 def sort_keys_checked(words, bits=None, retries: int = 2, **kw):

@@ -63,18 +63,21 @@ def keys(rec: torch.Tensor, kb: int) -> tuple[torch.Tensor, torch.Tensor]:
 _TIE_WS: dict = {}
 
 
-def _tie_ws(d, cap: int) -> torch.Tensor:
-    """Scratch of the tie fix-up (a run counter + run starts), per device."""
+def _tie_ws(d, words: int) -> torch.Tensor:
+    """Scratch of the tie fix-up (a run counter, run starts, the scan's
+    per-block run lists), per device."""
     w = _TIE_WS.get(d)
-    if w is None or w.numel() < cap + 1:
-        w = _TIE_WS[d] = torch.empty(cap + 1, dtype=torch.int64, device=d)
+    if w is None or w.numel() < words:
+        w = _TIE_WS[d] = torch.empty(words, dtype=torch.int64, device=d)
     return w
 
 
-def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: torch.Tensor | None = None):
+def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: torch.Tensor | None = None,
+         tie_mode: int = 0):
     """(permutation int32 (int64 on CPU), sorted 32-bit key prefixes) of the
     rows in key order (stable).  GPU: pass ``k32``/``ghist`` from
-    :func:`keys32` to skip recomputing them."""
+    :func:`keys32` to skip recomputing them; ``tie_mode=1`` takes the
+    single-kernel tie fix-up (A/B probes, tests)."""
     from .primitives import sort_error, sort_keys32, sort_keys_checked
     n, rb = _check(rec, kb)
     if not rec.is_cuda:
@@ -89,9 +92,9 @@ def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: tor
     perm, sk = sort_keys32(k32, ghist)
     bad = torch.zeros(1, dtype=torch.int32, device=d)
     cap = max(1024, n // 256)
-    ws = _tie_ws(d, cap)
+    ws = _tie_ws(d, int(_hip.lib().mr_rec_tie_ws_words(n, cap)))
     _hip.call("mr_rec_tie_fixup", _hip.ptr(sk), _hip.ptr(perm), _hip.ptr(rec), n, rb, kb, _hip.ptr(bad),
-              _hip.ptr(ws), cap, _hip.stream(d))
+              _hip.ptr(ws), cap, int(tie_mode), _hip.stream(d))
     if int(bad.item()) or sort_error(d):
         # skewed keys (a prefix shared by more than 64 rows), or a given-up
         # look-back: sort the full key words
@@ -101,15 +104,21 @@ def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: tor
     return perm, sk
 
 
-def gather(rec: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
-    """rec[perm] (rows)."""
+def gather(rec: torch.Tensor, perm: torch.Tensor, mode: int = 0) -> torch.Tensor:
+    """rec[perm] (rows).  GPU: 16-byte LDS-staged row gather for rows of
+    16-244 bytes (a multiple of 4) in 16-byte aligned buffers, else the dword
+    (or byte) gather; ``mode=1`` forces the dword gather (A/B probes, tests)."""
     n = perm.numel()
     rb = int(rec.shape[1])
     if rec.is_cuda:
         out = torch.empty((n, rb), dtype=torch.uint8, device=rec.device)
+        if n == 0:
+            return out
+        if rec.shape[0] == 0:
+            raise IndexError("gather from an empty record block")
         p = perm if perm.dtype == torch.int32 else perm.to(torch.int32)
-        _hip.call("mr_rec_gather", _hip.ptr(rec), _hip.ptr(p.contiguous()), n, rb, _hip.ptr(out),
-                  _hip.stream(rec.device))
+        _hip.call("mr_rec_gather", _hip.ptr(rec), int(rec.shape[0]), _hip.ptr(p.contiguous()), n, rb, _hip.ptr(out),
+                  int(mode), _hip.stream(rec.device))
         return out
     return rec[perm.long()]
 

@@ -1,0 +1,72 @@
+"""ops.exact_key_perm: (partition, exact key bytes) order of mixed packed and
+long keys — n-gram-like keys that share long prefixes, keys that are prefixes
+of others, NUL and control bytes at the 15/16-byte boundary — against Python's
+bytes order.  CPU (key words from the host helper) and GPU (mr_key_word +
+onesweep rounds)."""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from lua_mapreduce_1_amd import ops
+from lua_mapreduce_1_amd.ops import keys as K
+
+
+def _key_set(seed: int, n: int) -> list[bytes]:
+    rng = random.Random(seed)
+    stems = [b"of the ", b"in the european ", b"the commission and the council ", b"x" * 15, b"abcdefghijklmnop"]
+    out = set()
+    while len(out) < n:
+        r = rng.random()
+        if r < 0.5:
+            k = rng.choice(stems) + bytes(rng.choice(b"abcdefgh \t") for _ in range(rng.randrange(0, 40)))
+        elif r < 0.7:
+            k = rng.choice(stems)[:rng.randrange(1, 17)] + bytes(rng.choice(b"\x00\x01\x09z") for _ in
+                                                                  range(rng.randrange(0, 4)))
+        else:
+            k = bytes(rng.randrange(1, 256) for _ in range(rng.randrange(1, 70)))
+        if k:
+            out.add(k)
+    return sorted(out, key=lambda _: rng.random())
+
+
+def _columns(keys: list[bytes]):
+    src = np.frombuffer(b"".join(keys), np.uint8).copy()
+    hi, lo, rep = [], [], []
+    off = 0
+    for k in keys:
+        h, l_ = K.pack_key(k)
+        hi.append(h)
+        lo.append(l_)
+        rep.append(K.make_rep(off, len(k)))
+        off += len(k)
+    t = lambda v: torch.from_numpy(np.array(v, dtype=np.uint64).view(np.int64))  # noqa: E731
+    return t(hi), t(lo), t(rep), torch.from_numpy(src)
+
+
+def _check(keys, nparts, device):
+    hi, lo, rep, src = _columns(keys)
+    part = torch.tensor([K.fnv1(k) % nparts for k in keys], dtype=torch.int32)
+    if device is not None:
+        hi, lo, rep, src, part = (x.to(device) for x in (hi, lo, rep, src, part))
+    perm = ops.exact_key_perm(part, hi, lo, rep, src, nparts)
+    got = [(int(part[i]), keys[i]) for i in perm.cpu().tolist()]
+    assert got == sorted((int(p), k) for p, k in zip(part.cpu().tolist(), keys))
+
+
+@pytest.mark.parametrize("nparts", [1, 10])
+def test_exact_key_perm_cpu(nparts):
+    _check(_key_set(1, 3000), nparts, None)
+
+
+def test_exact_key_perm_short_only_cpu():
+    _check([b"b", b"a", b"ab", b"a\x00", b"a\x00\x00", b"zz" * 7, b"zz" * 8], 1, None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nparts", [1, 10, 256])
+def test_exact_key_perm_gpu(gpu, nparts):
+    _check(_key_set(2, 200_000), nparts, gpu)

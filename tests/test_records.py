@@ -181,3 +181,29 @@ def test_records_any_width_gpu(gpu, args):
     assert torch.equal(RC.gather(d, ref.to(gpu)).cpu(), h[ref])  # the gather itself
     eng, res, got = run_engine(dict(args, rows=200_000), gpu)
     assert check(got, dict(args, rows=200_000))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rb", [4, 12, 16, 20, 24, 36, 37, 64, 100, 116, 128, 132, 244, 248])
+def test_record_gather_widths_gpu(gpu, rb):
+    """records.gather (16-byte LDS-staged path for 16 <= rb <= 244, rb % 4 == 0;
+    dword / byte gathers otherwise and with mode=1) against torch indexing:
+    row counts that are not a multiple of the 256-row batch, repeated and
+    reversed rows, a permutation longer than the input."""
+    from lua_mapreduce_1_amd.ops import records as RC
+    g = torch.Generator().manual_seed(rb)
+    nin = 70_001
+    rec = torch.randint(0, 256, (nin, rb), dtype=torch.uint8, generator=g)
+    d = rec.to(gpu)
+    perms = [torch.randperm(nin, generator=g), torch.arange(nin - 1, -1, -1),
+             torch.randint(0, nin, (nin + 517,), generator=g), torch.randint(0, nin, (255,), generator=g)]
+    for p in perms:
+        want = rec[p]
+        for mode in (0, 1):
+            got = RC.gather(d, p.to(torch.int32).to(gpu), mode=mode).cpu()
+            assert torch.equal(got, want), (rb, mode, p.numel())
+    # a view whose base is not 16-byte aligned takes the dword path
+    if rb % 4 == 0 and nin > 2:
+        flat = d.view(-1)[4:4 + (nin - 1) * rb].view(nin - 1, rb)
+        p = torch.randperm(nin - 1, generator=g)
+        assert torch.equal(RC.gather(flat, p.to(gpu)).cpu(), rec.view(-1)[4:4 + (nin - 1) * rb].view(nin - 1, rb)[p])

@@ -189,15 +189,19 @@ def _rows16(hi: np.ndarray, lo: np.ndarray) -> torch.Tensor:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["uniform", "pairs", "runs", "runs_over_cap", "skewed"])
-def test_gpu_record_sort_tie_paths(gpu, case):
+@pytest.mark.parametrize("tie_mode", [0, 1])
+@pytest.mark.parametrize("case", ["uniform", "pairs", "runs", "runs_over_cap", "dense_pairs", "skewed"])
+def test_gpu_record_sort_tie_paths(gpu, case, tie_mode):
     """The record sort radix-sorts the 32-bit key prefixes and fixes runs of
     equal prefixes from the rows: pairs in registers (uniform, pairs), runs
     of 3..64 listed for the second kernel (runs), more listed runs than the
     list holds and runs longer than 64 (full-key fallback): all exact and
-    stable."""
+    stable.  tie_mode 0: scan + per-run fix kernels (a block whose segment
+    overflows — dense_pairs: half the rows start a run — takes the full-key
+    sort); 1: the single-kernel fix-up."""
     from lua_mapreduce_1_amd.ops import records as RC
-    g = np.random.default_rng({"uniform": 1, "pairs": 2, "runs": 3, "runs_over_cap": 4, "skewed": 5}[case])
+    g = np.random.default_rng({"uniform": 1, "pairs": 2, "runs": 3, "runs_over_cap": 4, "dense_pairs": 6,
+                               "skewed": 5}[case])
     n = 1_000_000
     hi = g.integers(0, 2**63, n, dtype=np.int64).view(np.uint64) * np.uint64(2) + g.integers(0, 2, n).astype(np.uint64)
     low = hi & np.uint64(0xFFFFFFFF)
@@ -212,11 +216,14 @@ def test_gpu_record_sort_tie_paths(gpu, case):
     elif case == "runs_over_cap":  # every prefix shared by ~8 rows: more runs than the list holds
         top = g.integers(0, n // 8, n).astype(np.uint64) << np.uint64(32)
         hi = top | low
+    elif case == "dense_pairs":  # every prefix shared by exactly two rows
+        top = g.permutation(np.repeat(np.arange(n // 2, dtype=np.uint64), 2)) << np.uint64(32)
+        hi = top | low
     elif case == "skewed":
         hi = (np.uint64(7) << np.uint64(32)) | (hi & np.uint64(0xFFFF))
     lo = g.integers(0, 1 << 16, n).astype(np.uint64)
     rows = _rows16(hi, lo)
-    perm, _ = RC.sort(rows.to(gpu), 16)
+    perm, _ = RC.sort(rows.to(gpu), 16, tie_mode=tie_mode)
     perm = perm.cpu().numpy().astype(np.int64)
     want = np.lexsort((np.arange(n), lo, hi))  # stable: ties in input order
     assert np.array_equal(perm, want)
