@@ -53,7 +53,25 @@ __global__ void __launch_bounds__(256) rec_keys32_kernel(const u8* __restrict__ 
   }
   const bool words = (rb & 3) == 0;
   const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + t; i < n; i += stride) {
+  // KU rows per thread and trip with every key load issued before the first
+  // is used: one 4-byte load per 100-byte row touches a new line for every
+  // lane, so the pass is bound by how many of those misses are in flight
+  constexpr int KU = 8;
+  u64 i0 = (u64)blockIdx.x * blockDim.x + t;
+  for (; i0 + (KU - 1) * stride < n; i0 += KU * stride) {
+    u32 k[KU];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) k[u] = be32(rec + (i0 + u * stride) * (u64)rb, 0, kb, words);
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      k32[i0 + u * stride] = k[u];
+      if (ghist) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) atomicAdd(&h[b][(k[u] >> (8 * b)) & 0xFFu], 1u);
+      }
+    }
+  }
+  for (u64 i = i0; i < n; i += stride) {
     const u32 k = be32(rec + i * (u64)rb, 0, kb, words);
     k32[i] = k;
     if (ghist) {

@@ -747,7 +747,7 @@ def key_word(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.T
 
 
 def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor,
-                   src: torch.Tensor | None, nparts: int) -> torch.Tensor | None:
+                   src: torch.Tensor | None, nparts: int, klen: torch.Tensor | None = None) -> torch.Tensor | None:
     """Stable permutation ordering rows by (partition, exact key bytes) on the
     device, for key sets the (partition, hi, lo) sort plus the tie fix-up
     cannot order (long keys — whose lo is a hash — in long runs of a shared
@@ -761,12 +761,14 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     sorts them by (tie group, bytes 16-31, min(len, 32)) in place inside their
     groups, and so on.  Each round is a stable LSD radix sort, so rows of one
     key set keep their input order where they tie.  None when a key is longer
-    than 8 * EXACT_MAX_WORDS bytes (the caller orders on the host)."""
+    than 8 * EXACT_MAX_WORDS bytes (the caller orders on the host).
+    ``klen``: the keys' lengths when the caller has them (key_meta)."""
     n = hi.numel()
     d = hi.device
     if n == 0:
         return torch.zeros(0, dtype=torch.int64, device=d)
-    _, klen = key_meta(hi, lo, rep, src, want_part=False)
+    if klen is None:
+        _, klen = key_meta(hi, lo, rep, src, want_part=False)
     klen = klen.to(torch.int64)
     max_len = int(klen.max())
     if (max_len + 7) // 8 > EXACT_MAX_WORDS:

@@ -355,7 +355,8 @@ class BlobCapacityError(RuntimeError):
 
 
 def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, part: torch.Tensor | None = None,
-                    _presorted: bool = False, blob_cap: int | None = None) -> dict:
+                    _presorted: bool = False, blob_cap: int | None = None,
+                    lengths: torch.Tensor | None = None) -> dict:
     """The device half of :func:`finalize`: every kernel and device->pinned
     copy, no host synchronisation (so it can be captured in a hipGraph once
     the pinned buffers exist).  Returns the pending state for finalize_host."""
@@ -377,7 +378,7 @@ def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, p
     # blob capacity bound: distinct words occupy disjoint bytes of their
     # source (a caller whose keys overlap there passes blob_cap)
     cap = max(src.numel() if src is not None else max(16 * n, 1), blob_cap or 0)
-    off, blob = ops.gather_key_bytes(hi, lo, rep, src, capacity=cap)
+    off, blob = ops.gather_key_bytes(hi, lo, rep, src, lengths=lengths if _presorted else None, capacity=cap)
     counts = ops.bincount(part, nparts) if n else torch.zeros(nparts, dtype=torch.int64, device=hi.device)
     hv = _to_host(val, "val")
     ho = _to_host(off.to(torch.int32), "off32") if cap < 2**31 else _to_host(off, "off64")
@@ -493,15 +494,33 @@ def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=N
     """The device half of a tail ordered exactly by key bytes from the start
     (ops.exact_key_perm) — for key sets whose fused tail falls back every time.
     Keys past the exact sort's length limit get the (partition, hi, lo) sort
-    and the host fix-up instead."""
-    part = partition_of(hi, lo, rep, src, nparts, partition_module)
-    perm = ops.exact_key_perm(part, hi, lo, rep, src, nparts) if src is not None else None
+    and the host fix-up instead.  Partitions and key lengths come from one
+    key_meta pass (device FNV-1 partitions); the rows and their lengths are
+    reordered by one gather launch."""
+    spec = getattr(partition_module, "device_partition", None) if partition_module is not None else ("fnv1", nparts)
+    klen = None
+    if hi.is_cuda and spec is not None and spec[0] == "fnv1" and int(spec[1]) == nparts:
+        part, klen = ops.key_meta(hi, lo, rep, src, nparts=nparts)
+    else:
+        part = partition_of(hi, lo, rep, src, nparts, partition_module)
+    perm = ops.exact_key_perm(part, hi, lo, rep, src, nparts, klen=klen) if src is not None else None
     exact = perm is not None
     if perm is None:
         perm = ops.sort_keys_checked([part.to(torch.int64), hi, lo],
                                      bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
-    pend = finalize_device(hi[perm], lo[perm], val[perm], rep[perm], src, nparts, partition_module, part=part[perm],
-                           _presorted=True, blob_cap=blob_cap)
+    if hi.is_cuda and klen is not None:
+        from ..ops import _hip
+        n = hi.numel()
+        cols = [torch.empty(n, dtype=torch.int64, device=hi.device) for _ in range(5)]
+        spart = torch.empty(n, dtype=torch.int32, device=hi.device)
+        _hip.call("mr_gather_cols", _hip.ptr(perm.to(torch.int32)), n, _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val),
+                  _hip.ptr(rep), _hip.ptr(klen), _hip.ptr(part.to(torch.int32).contiguous()),
+                  *[_hip.ptr(c) for c in cols], _hip.ptr(spart), _hip.stream(hi.device))
+        pend = finalize_device(*cols[:4], src, nparts, partition_module, part=spart, _presorted=True,
+                               blob_cap=blob_cap, lengths=cols[4])
+    else:
+        pend = finalize_device(hi[perm], lo[perm], val[perm], rep[perm], src, nparts, partition_module,
+                               part=part[perm], _presorted=True, blob_cap=blob_cap)
     pend["exact"] = exact
     return pend
 
