@@ -222,7 +222,11 @@ __global__ void __launch_bounds__(256) slot_compact_kernel(GTab g, u64 cap, long
 // global atomic per column.  Long keys (prefix + hash, verified by bytes in
 // the global table) and rows past the LDS table's load limit take the direct
 // per-row path of agg_insert_kernel.
-constexpr int CB_T = 256, CB_ITEMS = 16, CB_ROWS = CB_T * CB_ITEMS, CB_SLOTS = 1024;
+// 512 threads per block: with 4 value columns the block's LDS (64 KiB) allows
+// two blocks per CU, and 16 waves hide the per-row load chains better than 8
+// (CSV group-by 5.49 -> 5.13 ms per step, bigram unchanged;
+// profiles/r3/check7/generic_combine_block_ab.txt).
+constexpr int CB_T = 512, CB_ROWS = 4096, CB_SLOTS = 1024;
 constexpr int CB_LIMIT = CB_SLOTS * 3 / 4, CB_PROBES = 32;
 
 __device__ __forceinline__ long long cb_identity(int dtype, int op) {
@@ -309,6 +313,7 @@ __device__ __forceinline__ int cb_slot(u64* tag, u64* khi, u64* klo, u64* krep, 
 }
 
 __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 n, Cols c) {
+  constexpr int CB_ITEMS = CB_ROWS / CB_T;
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
   u64* tag = lds;
   u64* khi = tag + CB_SLOTS;

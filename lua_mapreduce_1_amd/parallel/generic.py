@@ -500,7 +500,7 @@ class GenericPlane:
                             else STATUS.BROKEN
                 continue
             if ovf or n > mp.table.cap // 2:
-                self._cap = ops.next_pow2(4 * max(n, 1))
+                self._cap = ops.next_pow2((16 if ovf else 4) * max(n, 1))  # overflowed: the count is a lower bound
                 mp.table = A.AggTable(self._cap, eng.device, self.phys.cols if self.phys is not None else None,
                                       self.dtype)
                 continue

@@ -1067,8 +1067,12 @@ class SPMDEngine:
                 self._run_map(jobs, recs, j0, j1)
                 continue
             if overflow or n_claimed > self.table.cap // 2:
-                # grow and redo this rank's map (results with an overflowed table are unusable)
-                self.table = ops.HashTable(ops.next_pow2(4 * max(n_claimed, 1)), device=self.device, op=self.op)
+                # grow and redo this rank's map (results with an overflowed table
+                # are unusable; after an overflow the key count is unknown — it
+                # is at least the capacity — so the table grows 16x, else 4x
+                # the count)
+                grow = 16 if overflow else 4
+                self.table = ops.HashTable(ops.next_pow2(grow * max(n_claimed, 1)), device=self.device, op=self.op)
                 self._table_capacity = self.table.cap
                 self._run_map(jobs, recs, j0, j1)
                 continue
