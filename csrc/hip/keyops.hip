@@ -397,6 +397,80 @@ __global__ void key_word_kernel(const u64* __restrict__ hi, const u64* __restric
   }
 }
 
+// Exact key order after the (partition, bytes 0-15, min(len, 16)) sort of
+// ops.exact_key_perm: only long keys sharing their first 16 bytes can still
+// be out of order.  exact_hash_kernel gives every row a 64-bit hash of its
+// sort columns; on those hashes in sorted order, exact_fix_kernel finds each
+// run of equal hashes (one thread per run start) and insertion-sorts the run
+// by the full key: (partition, bytes 0-15, and for two long keys their bytes
+// from 16 on and their lengths; else min(len, 16)) — the order the columns
+// give, refined, so a run that only collides on the hash stays sorted too.
+// Runs longer than EX_RUN set *bad (the caller refines in rounds instead).
+constexpr int EX_RUN = 64;
+
+__global__ void exact_hash_kernel(const int* __restrict__ part, const u64* __restrict__ hi, const u64* __restrict__ w1,
+                                  const long long* __restrict__ klen, u64 n, u64* __restrict__ out) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 lc = klen[i] < 16 ? (u64)klen[i] : 16ull;
+    out[i] = fmix64((u64)(unsigned)part[i] * 0x9E3779B97F4A7C15ull ^ fmix64(hi[i] ^ fmix64(w1[i] + lc)));
+  }
+}
+
+// a < b in the exact key order (rows of one partition run)
+__device__ bool exact_less(const int* part, const u64* hi, const u64* w1, const long long* klen, const u64* rep,
+                           const u8* src, u32 a, u32 b) {
+  if (part[a] != part[b]) return (unsigned)part[a] < (unsigned)part[b];
+  if (hi[a] != hi[b]) return hi[a] < hi[b];
+  if (w1[a] != w1[b]) return w1[a] < w1[b];
+  const u64 la = (u64)klen[a], lb = (u64)klen[b];
+  if (la < 16 || lb < 16) return la < lb;  // bytes 0-15 equal: the shorter key is a prefix
+  const u64 oa = rep_off(rep[a]), ob = rep_off(rep[b]);
+  const u64 m = la < lb ? la : lb;
+  for (u64 i = 16; i < m; i += 16) {
+    u32 x[16], y[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      x[j] = i + j < m ? src[oa + i + j] : 0u;
+      y[j] = i + j < m ? src[ob + i + j] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (x[j] != y[j]) return x[j] < y[j];
+  }
+  return la < lb;
+}
+
+__global__ void exact_fix_kernel(const u64* __restrict__ sh, u32* __restrict__ perm, u64 n,
+                                 const int* __restrict__ part, const u64* __restrict__ hi, const u64* __restrict__ w1,
+                                 const long long* __restrict__ klen, const u64* __restrict__ rep,
+                                 const u8* __restrict__ src, u32* __restrict__ bad) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += stride) {
+    const u64 h = sh[i];
+    if (sh[i + 1] != h || (i > 0 && sh[i - 1] == h)) continue;  // not a run start
+    u64 e = i + 2;
+    while (e < n && sh[e] == h && e - i <= (u64)EX_RUN) ++e;
+    if (e - i > (u64)EX_RUN) {
+      atomicOr(bad, 1u);
+      continue;
+    }
+    u32 r[EX_RUN];
+    const int m = (int)(e - i);
+    for (int a = 0; a < m; ++a) r[a] = perm[i + a];
+    for (int a = 1; a < m; ++a) {
+      const u32 x = r[a];
+      int b = a;
+      while (b > 0 && exact_less(part, hi, w1, klen, rep, src, x, r[b - 1])) {
+        r[b] = r[b - 1];
+        --b;
+      }
+      r[b] = x;
+    }
+    for (int a = 0; a < m; ++a) perm[i + a] = r[a];
+  }
+}
+
 extern "C" {
 
 int mr_count_tokens(const void* text, u64 nbytes, u64 chunk_bytes, void* counter, hipStream_t stream) {
@@ -477,6 +551,23 @@ int mr_gather_key_bytes(const void* hi, const void* lo, const void* rep, const v
   if (n == 0) return 0;
   hipLaunchKernelGGL(gather_key_bytes_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)hi,
                      (const u64*)lo, (const u64*)rep, (const long long*)off, n, (const u8*)src, (u8*)dst, dst_cap);
+  return (int)hipGetLastError();
+}
+
+int mr_exact_hash(const void* part, const void* hi, const void* w1, const void* klen, u64 n, void* out,
+                  hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(exact_hash_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const int*)part,
+                     (const u64*)hi, (const u64*)w1, (const long long*)klen, n, (u64*)out);
+  return (int)hipGetLastError();
+}
+
+int mr_exact_fix(const void* sh, void* perm, u64 n, const void* part, const void* hi, const void* w1,
+                 const void* klen, const void* rep, const void* src, void* bad, hipStream_t stream) {
+  if (n < 2) return 0;
+  hipLaunchKernelGGL(exact_fix_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)sh, (u32*)perm, n,
+                     (const int*)part, (const u64*)hi, (const u64*)w1, (const long long*)klen, (const u64*)rep,
+                     (const u8*)src, (u32*)bad);
   return (int)hipGetLastError();
 }
 

@@ -107,6 +107,8 @@ _SIGS = {
     "mr_text_parse_f64": [_p, _p, _p, _u64, _p, _p, _p],
     "mr_text_parse_i64": [_p, _p, _p, _u64, _p, _p, _p],
     "mr_rec_tie_ws_words": [_u64, _u64],
+    "mr_exact_hash": [_p, _p, _p, _p, _u64, _p, _p],
+    "mr_exact_fix": [_p, _p, _u64, _p, _p, _p, _p, _p, _p, _p, _p],
 }
 _RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
                 "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words"}

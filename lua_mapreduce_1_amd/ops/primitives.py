@@ -777,9 +777,26 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     w1 = key_word(hi, lo, rep, src, 1)
     lc = klen.clamp(max=16)
     cols = [part.to(torch.int64), hi, w1, lc]
-    perm = sort_keys_checked(cols, bits=[pbits, 64, 64, 8]).long()
+    p32 = sort_keys_checked(cols, bits=[pbits, 64, 64, 8])
     if max_len <= 16:
-        return perm
+        return p32.long()
+    if hi.is_cuda:
+        # runs of rows equal in the sort columns (long keys sharing 16 bytes),
+        # found through a hash of the columns in sorted order and insertion-
+        # sorted by their full bytes, one thread per run (mr_exact_fix); runs
+        # longer than its limit go to the refinement rounds below
+        s = _hip.stream(d)
+        part32 = part.to(torch.int32).contiguous()
+        h = torch.empty(n, dtype=torch.int64, device=d)
+        _hip.call("mr_exact_hash", _hip.ptr(part32), _hip.ptr(hi), _hip.ptr(w1), _hip.ptr(klen), n, _hip.ptr(h), s)
+        sh = torch.empty(n, dtype=torch.int64, device=d)
+        _hip.call("mr_gather_u64", _hip.ptr(h), _hip.ptr(p32), _hip.ptr(sh), n, s)
+        bad = torch.zeros(1, dtype=torch.int32, device=d)
+        _hip.call("mr_exact_fix", _hip.ptr(sh), _hip.ptr(p32), n, _hip.ptr(part32), _hip.ptr(hi), _hip.ptr(w1),
+                  _hip.ptr(klen), _hip.ptr(rep), _hip.ptr(src), _hip.ptr(bad), s)
+        if not int(bad.item()):
+            return p32.long()
+    perm = p32.long()
     scols = [c[perm] for c in cols]
     pos = torch.arange(n, dtype=torch.int64, device=d)
     cap = 16

@@ -417,7 +417,7 @@ class GenericPlane:
         if self.dtype not in ("i64", "f64"):
             raise ValueError("device_value_dtype is 'i64' or 'f64'")
         self.phys = None if self.list_mode else A.Physical(A.parse_spec(op))
-        self._cap = int(eng.params.get("table_capacity") or 1 << 16)
+        self._cap = self._cap0 = int(eng.params.get("table_capacity") or 1 << 16)
         self.map = GenericMap(eng.device, self._cap, self.phys, self.dtype)
         self.red = None
         self._lines = None
@@ -459,6 +459,10 @@ class GenericPlane:
             ids = eng._split_ids(jobs, j0, j1)
             self._ids0 = ids[0]
         mp.emit.line_base = self._line_base() if eng.device_input == "split" else None
+        if mp.table.cap != ops.next_pow2(max(1024, self._cap)) and mp.table.is_cuda:
+            # the capacity target moved since this table was made (grown, or fitted)
+            mp.table = A.AggTable(self._cap, eng.device, self.phys.cols if self.phys is not None else None,
+                                  self.dtype)
         for _attempt in range(64):
             mp.begin(None)
             broken = []
@@ -504,8 +508,11 @@ class GenericPlane:
                 mp.table = A.AggTable(self._cap, eng.device, self.phys.cols if self.phys is not None else None,
                                       self.dtype)
                 continue
-            if n > mp.table.cap // 8 and self._cap < 4 * n:
-                self._cap = ops.next_pow2(4 * n)  # next iteration's table
+            fit = max(ops.next_pow2(2 * max(n, 1)), self._cap0)  # load 1/4 - 1/2
+            if n > mp.table.cap // 8 and self._cap < fit:
+                self._cap = fit  # next iteration's table
+            elif mp.table.cap > 16 * fit:
+                self._cap = fit  # grown 16x past an overflow: the next maps get a fitted table
             return
         raise RuntimeError("general plane: the map did not converge (table regrowth / retries)")
 

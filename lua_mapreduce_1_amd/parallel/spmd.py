@@ -421,6 +421,7 @@ class SPMDEngine:
         # one map table per input slot: with pipelining, iteration i+1 maps into
         # tables[1-s] while iteration i's shuffle/reduce still reads tables[s]
         self._table_capacity = table_capacity
+        self._initial_capacity = table_capacity
         # list- and record-valued reduces run on their own data planes
         # (parallel/planes.py); the fold plane below is the hash table
         from . import planes
@@ -569,8 +570,8 @@ class SPMDEngine:
         reset, or replaced by a larger one once an earlier map's distinct-key
         count has raised the target capacity (``_map_sync``)."""
         t = self.tables[self.tslot]
-        if t is not None and t.cap < self._table_capacity:
-            self.tables[self.tslot] = t = None
+        if t is not None and (t.cap < self._table_capacity or t.cap > 4 * self._table_capacity):
+            self.tables[self.tslot] = t = None  # grown, or far too large (every tail scans each slot)
         if t is None:
             self.tables[self.tslot] = ops.HashTable(self._table_capacity, device=self.device, op=self.op)
         else:
@@ -1086,6 +1087,14 @@ class SPMDEngine:
             if getattr(self, "_mapped_bytes", 0) >= TUNABLES.map_sparse_min_mb * 2**20:
                 self._table_capacity = max(self._table_capacity, min(
                     ops.next_pow2(TUNABLES.map_sparsity * max(n_claimed, 1)), _MAX_SPARSE_CAP))
+            # a table grown 16x after an overflow can end far above the key
+            # count: the next maps get one sized for it (load 1/4 - 1/2; the
+            # tail's compaction reads every slot's line of every column)
+            fit = max(ops.next_pow2(2 * max(n_claimed, 1)), self._initial_capacity,
+                      min(ops.next_pow2(TUNABLES.map_sparsity * max(n_claimed, 1)), _MAX_SPARSE_CAP)
+                      if getattr(self, "_mapped_bytes", 0) >= TUNABLES.map_sparse_min_mb * 2**20 else 0)
+            if self._table_capacity > 4 * fit:
+                self._table_capacity = fit
             return n_claimed, overflow
 
     def _device_spans(self, res, recs, j0: int, j1: int) -> None:

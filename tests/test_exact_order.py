@@ -33,6 +33,19 @@ def _key_set(seed: int, n: int) -> list[bytes]:
     return sorted(out, key=lambda _: rng.random())
 
 
+def _short_runs(seed: int, groups: int) -> list[bytes]:
+    """Long keys in groups of 1-6 sharing their first 16 bytes (runs the
+    one-kernel fix sorts), plus short keys that are prefixes of them."""
+    rng = random.Random(seed)
+    out = set()
+    for _ in range(groups):
+        pre = bytes(rng.randrange(1, 256) for _ in range(16))
+        for _ in range(rng.randrange(1, 7)):
+            out.add(pre + bytes(rng.randrange(0, 256) for _ in range(rng.randrange(0, 30))))
+        out.add(pre[:rng.randrange(1, 16)])
+    return sorted(out, key=lambda _: rng.random())
+
+
 def _columns(keys: list[bytes]):
     src = np.frombuffer(b"".join(keys), np.uint8).copy()
     hi, lo, rep = [], [], []
@@ -66,7 +79,19 @@ def test_exact_key_perm_short_only_cpu():
     _check([b"b", b"a", b"ab", b"a\x00", b"a\x00\x00", b"zz" * 7, b"zz" * 8], 1, None)
 
 
+def test_exact_key_perm_short_runs_cpu():
+    _check(_short_runs(3, 300), 4, None)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("nparts", [1, 10, 256])
 def test_exact_key_perm_gpu(gpu, nparts):
+    """Long runs of a shared 16-byte prefix: the refinement rounds."""
     _check(_key_set(2, 200_000), nparts, gpu)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nparts", [1, 10])
+def test_exact_key_perm_short_runs_gpu(gpu, nparts):
+    """Runs of at most 6 keys sharing 16 bytes: one fix kernel (mr_exact_fix)."""
+    _check(_short_runs(4, 40_000), nparts, gpu)

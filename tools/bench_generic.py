@@ -39,12 +39,17 @@ from lua_mapreduce_1_amd.utils import corpus  # noqa: E402
 
 
 def _time(eng, steps: int, warmup: int, device) -> float:
-    for _ in range(warmup):
-        eng.run_iteration()
+    """bench.py's schedule: input copies of the next iteration prefetched and
+    its map pipelined (where the plane supports it), but neither the last
+    warm-up step nor the last timed step starts work for the one after it."""
+    from lua_mapreduce_1_amd.utils.config import TUNABLES
+    eng.prefetch, eng.pipeline = True, TUNABLES.pipeline
+    for w in range(warmup):
+        eng.run_iteration(prefetch_next=w < warmup - 1, lookahead=warmup - 1 - w)
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        res = eng.run_iteration()
+    for k in range(steps):
+        res = eng.run_iteration(prefetch_next=k < steps - 1, lookahead=steps - 1 - k)
     torch.cuda.synchronize(device)
     return (time.perf_counter() - t0) * 1000.0 / steps, res
 
