@@ -511,8 +511,8 @@ class GenericPlane:
             fit = max(ops.next_pow2(2 * max(n, 1)), self._cap0)  # load 1/4 - 1/2
             if n > mp.table.cap // 8 and self._cap < fit:
                 self._cap = fit  # next iteration's table
-            elif mp.table.cap > 16 * fit:
-                self._cap = fit  # grown 16x past an overflow: the next maps get a fitted table
+            elif mp.table.cap >= 4 * fit:
+                self._cap = fit  # grown past the key count (16x after an overflow): fitted for the next maps
             return
         raise RuntimeError("general plane: the map did not converge (table regrowth / retries)")
 

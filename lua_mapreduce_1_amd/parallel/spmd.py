@@ -570,7 +570,7 @@ class SPMDEngine:
         reset, or replaced by a larger one once an earlier map's distinct-key
         count has raised the target capacity (``_map_sync``)."""
         t = self.tables[self.tslot]
-        if t is not None and (t.cap < self._table_capacity or t.cap > 4 * self._table_capacity):
+        if t is not None and (t.cap < self._table_capacity or t.cap >= 4 * self._table_capacity):
             self.tables[self.tslot] = t = None  # grown, or far too large (every tail scans each slot)
         if t is None:
             self.tables[self.tslot] = ops.HashTable(self._table_capacity, device=self.device, op=self.op)
@@ -1093,7 +1093,7 @@ class SPMDEngine:
             fit = max(ops.next_pow2(2 * max(n_claimed, 1)), self._initial_capacity,
                       min(ops.next_pow2(TUNABLES.map_sparsity * max(n_claimed, 1)), _MAX_SPARSE_CAP)
                       if getattr(self, "_mapped_bytes", 0) >= TUNABLES.map_sparse_min_mb * 2**20 else 0)
-            if self._table_capacity > 4 * fit:
+            if self._table_capacity >= 4 * fit:
                 self._table_capacity = fit
             return n_claimed, overflow
 
