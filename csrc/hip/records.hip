@@ -11,13 +11,17 @@
 //                  moved per row and pass instead of 24 with u64 keys;
 //   rec_tie_*    : rows equal in k32 ordered by key bytes 4..kb-1 read from the
 //                  rows themselves (uniform keys: ~2 % of the rows sit in such
-//                  a run, almost all of length 2: swapped in registers; longer
-//                  runs listed and insertion-sorted by a second kernel); a run
-//                  longer than 64 sets *bad and the caller sorts the full
-//                  (hi, lo) key instead;
-//   rec_gather   : output row i = input row perm[i], 8 independent words per
-//                  thread in flight (the random 100-byte row reads touch 1.77
-//                  128-byte lines each on average: this is the bound).
+//                  a run, almost all of length 2): a streaming scan lists each
+//                  block's run starts, one thread per listed pair swaps it,
+//                  longer runs are insertion-sorted by a third kernel; a run
+//                  longer than 64 (or a block with too many runs) sets *bad and
+//                  the caller sorts the full (hi, lo) key instead;
+//   rec_gather16 : output row i = input row perm[i] with 16-byte loads and
+//                  stores through LDS (rows of 16-244 bytes, a multiple of 4);
+//                  rec_gather (one word per lane) and rec_gather_bytes for the
+//                  other widths.  The random row reads touch 1.75 128-byte
+//                  lines per 100-byte row: the gather runs near the HBM rate
+//                  on those lines.
 //   rec_keys     : full (hi, lo) key words (fallback sort, sampling, checks);
 //   rec_dest32   : range partition = number of splitters <= k32.
 #include <hip/hip_runtime.h>
@@ -53,25 +57,10 @@ __global__ void __launch_bounds__(256) rec_keys32_kernel(const u8* __restrict__ 
   }
   const bool words = (rb & 3) == 0;
   const u64 stride = (u64)gridDim.x * blockDim.x;
-  // KU rows per thread and trip with every key load issued before the first
-  // is used: one 4-byte load per 100-byte row touches a new line for every
-  // lane, so the pass is bound by how many of those misses are in flight
-  constexpr int KU = 8;
-  u64 i0 = (u64)blockIdx.x * blockDim.x + t;
-  for (; i0 + (KU - 1) * stride < n; i0 += KU * stride) {
-    u32 k[KU];
-#pragma unroll
-    for (int u = 0; u < KU; ++u) k[u] = be32(rec + (i0 + u * stride) * (u64)rb, 0, kb, words);
-#pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      k32[i0 + u * stride] = k[u];
-      if (ghist) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) atomicAdd(&h[b][(k[u] >> (8 * b)) & 0xFFu], 1u);
-      }
-    }
-  }
-  for (u64 i = i0; i < n; i += stride) {
+  // one 4-byte load per 100-byte row: the pass reads every line of the rows
+  // (2.0 ms per 10 GB, ~5 TB/s; 8 loads in flight per thread measured no
+  // faster, profiles/r3/check7/ts_ab_box2.log)
+  for (u64 i = (u64)blockIdx.x * blockDim.x + t; i < n; i += stride) {
     const u32 k = be32(rec + i * (u64)rb, 0, kb, words);
     k32[i] = k;
     if (ghist) {
