@@ -96,63 +96,15 @@ __device__ __forceinline__ void key_rest(const u8* row, int kb, bool words, u64&
 // Runs of equal k32 in the sorted prefixes, ordered by the rest of their keys
 // (bytes 4..kb-1 read from the rows; stable: the LSD sort left equal keys in
 // input order).  Uniform keys: ~2 % of the rows sit in a run, almost all of
-// length 2 — rec_tie_pairs_kernel swaps those in registers and appends the
-// start of every longer run to a list; rec_tie_runs_kernel sorts the listed
-// runs (insertion sort, one thread per run).  A run longer than 64 sets *bad
-// and the caller sorts the full (hi, lo) key instead.
+// length 2 — rec_tie_fix_kernel swaps those and appends the start of every
+// longer run to a list; rec_tie_runs_kernel sorts the listed runs (insertion
+// sort, one thread per run).  A run longer than 64 sets *bad and the caller
+// sorts the full (hi, lo) key instead.
 constexpr int TIE_MAX = 64;
 
-// One thread per 4 consecutive prefixes (one 16-byte load + the two after
-// and the one before): a run start is a prefix equal to the next and
-// different from the previous.
-__global__ void __launch_bounds__(256) rec_tie_pairs_kernel(const u32* __restrict__ sk, u32* __restrict__ perm,
-                                                            const u8* __restrict__ rec, u64 n, int rb, int kb,
-                                                            u32* __restrict__ bad, u64* __restrict__ runs,
-                                                            unsigned long long* __restrict__ nruns, u64 runs_cap) {
-  if (kb <= 4) return;  // the prefix is the whole key
-  const bool words = (rb & 3) == 0;
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x; 4 * g < n; g += stride) {
-    const u64 i0 = 4 * g;
-    u32 v[7];  // sk[i0 - 1 .. i0 + 5]
-    if (i0 + 4 <= n && (((uintptr_t)sk & 15) == 0)) {
-      const uint4 q = *reinterpret_cast<const uint4*>(sk + i0);
-      v[1] = q.x; v[2] = q.y; v[3] = q.z; v[4] = q.w;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[1 + j] = i0 + j < n ? sk[i0 + j] : 0u;
-    }
-    v[0] = i0 > 0 ? sk[i0 - 1] : ~v[1];
-    v[5] = i0 + 4 < n ? sk[i0 + 4] : 0u;
-    v[6] = i0 + 5 < n ? sk[i0 + 5] : 0u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u64 i = i0 + j;
-      if (i + 1 >= n) break;
-      const u32 h = v[1 + j];
-      if (v[2 + j] != h || v[j] == h) continue;  // not the start of a run
-      if (i + 2 < n && v[3 + j] == h) {          // a run of 3 or more
-        const unsigned long long k = atomicAdd(nruns, 1ull);
-        if (k < runs_cap) runs[k] = i;
-        else atomicOr(bad, 1u);
-        continue;
-      }
-      const u32 p0 = perm[i], p1 = perm[i + 1];
-      u64 a0, a1;
-      u32 b0, b1;
-      key_rest(rec + (u64)clamp_row(p0, n) * rb, kb, words, a0, b0);
-      key_rest(rec + (u64)clamp_row(p1, n) * rb, kb, words, a1, b1);
-      if (a0 > a1 || (a0 == a1 && b0 > b1)) {
-        perm[i] = p1;
-        perm[i + 1] = p0;
-      }
-    }
-  }
-}
-
-// The same fix-up in two streaming-friendly steps (the single kernel above
-// waits on a dependent perm -> row load chain in every wave that holds a
-// pair, ~0.56 ms per 100 M rows): rec_tie_scan_kernel only reads the sorted
+// Two streaming-friendly steps (a single kernel that swapped pairs where it
+// found them waited on a dependent perm -> row load chain in every wave that
+// held a pair: 0.56 ms per 100 M rows against 0.24): rec_tie_scan_kernel only reads the sorted
 // prefixes and keeps each block's run starts (TS_POS positions per block, at
 // most TS_CAP starts, in LDS, then in the block's own segment — no global
 // atomics); rec_tie_fix_kernel then gives every listed run a thread of its
@@ -468,31 +420,26 @@ int mr_rec_keys(const void* rec, u64 n, int rb, int kb, void* hi, void* lo, hipS
 // ws: u64 scratch of 1 + ws_cap words (a run counter, then run starts)
 // ws: u64 scratch of mr_rec_tie_ws_words(n, ws_cap) words: a run counter,
 // ws_cap run starts (runs of 3+), then the scan's per-block counts and
-// segments (u32).  mode 1: the single-kernel fix-up (A/B probes).
+// segments (u32).
 u64 mr_rec_tie_ws_words(u64 n, u64 ws_cap) {
   const u64 g = (n + rc::TS_POS - 1) / rc::TS_POS;
   return 1 + ws_cap + (g + g * rc::TS_CAP + 1) / 2 + 1;
 }
 
 int mr_rec_tie_fixup(const void* sk, void* perm, const void* rec, u64 n, int rb, int kb, void* bad, void* ws,
-                     u64 ws_cap, int mode, hipStream_t s) {
+                     u64 ws_cap, hipStream_t s) {
   if (n < 2 || kb <= 4) return 0;  // kb <= 4: the prefix is the whole key
   u64* w = (u64*)ws;
   (void)hipMemsetAsync(w, 0, sizeof(u64), s);
-  if (mode == 1) {
-    hipLaunchKernelGGL(rc::rec_tie_pairs_kernel, dim3(rc_grid((n + 3) / 4)), dim3(256), 0, s, (const u32*)sk,
-                       (u32*)perm, (const u8*)rec, n, rb, kb, (u32*)bad, w + 1, (unsigned long long*)w, ws_cap);
-  } else {
-    const u64 g = (n + rc::TS_POS - 1) / rc::TS_POS;
-    if (g > 0x7FFFFFFFull) return -1;
-    u32* counts = reinterpret_cast<u32*>(w + 1 + ws_cap);
-    u32* seg = counts + g;
-    hipLaunchKernelGGL(rc::rec_tie_scan_kernel, dim3((unsigned)g), dim3(256), 0, s, (const u32*)sk, n, counts, seg,
-                       (u32*)bad);
-    hipLaunchKernelGGL(rc::rec_tie_fix_kernel, dim3((unsigned)g), dim3(256), 0, s, (const u32*)sk, (u32*)perm,
-                       (const u8*)rec, n, rb, kb, (const u32*)counts, (const u32*)seg, (u32*)bad, w + 1,
-                       (unsigned long long*)w, ws_cap);
-  }
+  const u64 g = (n + rc::TS_POS - 1) / rc::TS_POS;
+  if (g > 0x7FFFFFFFull) return -1;
+  u32* counts = reinterpret_cast<u32*>(w + 1 + ws_cap);
+  u32* seg = counts + g;
+  hipLaunchKernelGGL(rc::rec_tie_scan_kernel, dim3((unsigned)g), dim3(256), 0, s, (const u32*)sk, n, counts, seg,
+                     (u32*)bad);
+  hipLaunchKernelGGL(rc::rec_tie_fix_kernel, dim3((unsigned)g), dim3(256), 0, s, (const u32*)sk, (u32*)perm,
+                     (const u8*)rec, n, rb, kb, (const u32*)counts, (const u32*)seg, (u32*)bad, w + 1,
+                     (unsigned long long*)w, ws_cap);
   hipLaunchKernelGGL(rc::rec_tie_runs_kernel, dim3(256), dim3(64), 0, s, (const u32*)sk, (u32*)perm, (const u8*)rec,
                      n, rb, kb, (u32*)bad, (const u64*)(w + 1), (const unsigned long long*)w, ws_cap);
   return (int)hipGetLastError();

@@ -666,19 +666,37 @@ int mr_sort_debug_fail(int passes) {
 // fit in LDS; tools/onesweep_rounds_ab.py, profiles/r2/onesweep/).  Mid-size
 // sorts (the word-count tail's ~10^5-10^6 keys) keep 16: there a pass is a
 // few tiles' latency, and bigger tiles are fewer and longer.
+// u32 keys (the record plane's 32-bit prefixes) take 8 bytes of LDS per key
+// with their u32 values instead of 12, so their tiles can be larger: 100 M
+// keys, 4 passes, 2.98 ms at 24 rounds, 2.62 at 32 (two workgroups per CU;
+// tools/ts_ab.py, profiles/r3/check8/sort_rounds_ab.log).
 constexpr u64 ONESWEEP_BIG = 1ull << 22;
 static int g_big_rounds = 24;
+static int g_big_rounds32 = 32;
 int mr_sort_set_rounds(int rounds) {
   if (rounds != 16 && rounds != 24 && rounds != 32) return -1;
   g_big_rounds = rounds;
   return 0;
 }
+int mr_sort_set_rounds32(int rounds) {
+  if (rounds != 16 && rounds != 24 && rounds != 32 && rounds != 40 && rounds != 48) return -1;
+  g_big_rounds32 = rounds;
+  return 0;
+}
 
-static int onesweep_rounds(u64 n) { return n <= ONESWEEP_SMALL ? 4 : n < ONESWEEP_BIG ? RS_ROUNDS : g_big_rounds; }
+static int onesweep_rounds(u64 n, int key_bytes) {
+  return n <= ONESWEEP_SMALL ? 4 : n < ONESWEEP_BIG ? RS_ROUNDS : (key_bytes == 4 ? g_big_rounds32 : g_big_rounds);
+}
 
-u64 mr_onesweep_tiles(u64 n) {
-  const u64 tile = (u64)RS_THREADS * (u64)onesweep_rounds(n);
+static u64 onesweep_tiles_of(u64 n, int key_bytes) {
+  const u64 tile = (u64)RS_THREADS * (u64)onesweep_rounds(n, key_bytes);
   return (n + tile - 1) / tile;
+}
+
+// look-back granule rows a pass over n keys of either key width may use
+u64 mr_onesweep_tiles(u64 n) {
+  const u64 a = onesweep_tiles_of(n, 8), b = onesweep_tiles_of(n, 4);
+  return a > b ? a : b;
 }
 
 }  // extern "C"
@@ -688,14 +706,24 @@ static int onesweep_pass(const void* keys_in, const void* vals_in, void* keys_ou
                          const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
                          int debug_fail, hipStream_t s) {
   if (n == 0) return 0;
-  const u32 nt = (u32)mr_onesweep_tiles(n);
-  switch (onesweep_rounds(n)) {
+  const u32 nt = (u32)onesweep_tiles_of(n, (int)sizeof(K));
+  switch (onesweep_rounds(n, (int)sizeof(K))) {
     case 4: onesweep_launch<K, 4>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
                                   epoch, err, iota, debug_fail, s); break;
     case 24: onesweep_launch<K, 24>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules,
                                     tile_counter, epoch, err, iota, debug_fail, s); break;
     case 32: onesweep_launch<K, 32>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules,
                                     tile_counter, epoch, err, iota, debug_fail, s); break;
+    case 40:
+      if constexpr (sizeof(K) == 4)
+        onesweep_launch<K, 40>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
+                               epoch, err, iota, debug_fail, s);
+      break;
+    case 48:
+      if constexpr (sizeof(K) == 4)
+        onesweep_launch<K, 48>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
+                               epoch, err, iota, debug_fail, s);
+      break;
     default: onesweep_launch<K, RS_ROUNDS>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules,
                                            tile_counter, epoch, err, iota, debug_fail, s);
   }

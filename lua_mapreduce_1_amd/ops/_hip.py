@@ -81,6 +81,7 @@ _SIGS = {
     "mr_tail_pack": [_p, _p, _u64, _p, _u32, _p, _p, _p, _p],
     "mr_sort_debug_fail": [_i32],
     "mr_sort_set_rounds": [_i32],
+    "mr_sort_set_rounds32": [_i32],
     "mr_onesweep_tiles": [_u64],
     "mr_set_long_mask_wc3": [_u64],
     "mr_set_long_mask_keyops": [_u64],
@@ -93,7 +94,7 @@ _SIGS = {
     "mr_radix_onesweep_k32": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p, _u32, _p, _i32, _p],
     "mr_rec_keys32": [_p, _u64, _i32, _i32, _p, _p, _p],
     "mr_rec_keys": [_p, _u64, _i32, _i32, _p, _p, _p],
-    "mr_rec_tie_fixup": [_p, _p, _p, _u64, _i32, _i32, _p, _p, _u64, _i32, _p],
+    "mr_rec_tie_fixup": [_p, _p, _p, _u64, _i32, _i32, _p, _p, _u64, _p],
     "mr_rec_gather": [_p, _u64, _p, _u64, _i32, _p, _i32, _p],
     "mr_rec_dest32": [_p, _u64, _p, _u32, _p, _p],
     "mr_agg_insert": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _u64, _p, _p],

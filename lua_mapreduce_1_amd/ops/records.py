@@ -72,12 +72,10 @@ def _tie_ws(d, words: int) -> torch.Tensor:
     return w
 
 
-def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: torch.Tensor | None = None,
-         tie_mode: int = 0):
+def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: torch.Tensor | None = None):
     """(permutation int32 (int64 on CPU), sorted 32-bit key prefixes) of the
     rows in key order (stable).  GPU: pass ``k32``/``ghist`` from
-    :func:`keys32` to skip recomputing them; ``tie_mode=1`` takes the
-    single-kernel tie fix-up (A/B probes, tests)."""
+    :func:`keys32` to skip recomputing them."""
     from .primitives import sort_error, sort_keys32, sort_keys_checked
     n, rb = _check(rec, kb)
     if not rec.is_cuda:
@@ -94,7 +92,7 @@ def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: tor
     cap = max(1024, n // 256)
     ws = _tie_ws(d, int(_hip.lib().mr_rec_tie_ws_words(n, cap)))
     _hip.call("mr_rec_tie_fixup", _hip.ptr(sk), _hip.ptr(perm), _hip.ptr(rec), n, rb, kb, _hip.ptr(bad),
-              _hip.ptr(ws), cap, int(tie_mode), _hip.stream(d))
+              _hip.ptr(ws), cap, _hip.stream(d))
     if int(bad.item()) or sort_error(d):
         # skewed keys (a prefix shared by more than 64 rows), or a given-up
         # look-back: sort the full key words

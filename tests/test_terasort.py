@@ -189,16 +189,14 @@ def _rows16(hi: np.ndarray, lo: np.ndarray) -> torch.Tensor:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tie_mode", [0, 1])
 @pytest.mark.parametrize("case", ["uniform", "pairs", "runs", "runs_over_cap", "dense_pairs", "skewed"])
-def test_gpu_record_sort_tie_paths(gpu, case, tie_mode):
+def test_gpu_record_sort_tie_paths(gpu, case):
     """The record sort radix-sorts the 32-bit key prefixes and fixes runs of
     equal prefixes from the rows: pairs in registers (uniform, pairs), runs
     of 3..64 listed for the second kernel (runs), more listed runs than the
     list holds and runs longer than 64 (full-key fallback): all exact and
-    stable.  tie_mode 0: scan + per-run fix kernels (a block whose segment
-    overflows — dense_pairs: half the rows start a run — takes the full-key
-    sort); 1: the single-kernel fix-up."""
+    stable.  A block whose run list overflows (dense_pairs: half the rows
+    start a run) takes the full-key sort."""
     from lua_mapreduce_1_amd.ops import records as RC
     g = np.random.default_rng({"uniform": 1, "pairs": 2, "runs": 3, "runs_over_cap": 4, "dense_pairs": 6,
                                "skewed": 5}[case])
@@ -223,7 +221,7 @@ def test_gpu_record_sort_tie_paths(gpu, case, tie_mode):
         hi = (np.uint64(7) << np.uint64(32)) | (hi & np.uint64(0xFFFF))
     lo = g.integers(0, 1 << 16, n).astype(np.uint64)
     rows = _rows16(hi, lo)
-    perm, _ = RC.sort(rows.to(gpu), 16, tie_mode=tie_mode)
+    perm, _ = RC.sort(rows.to(gpu), 16)
     perm = perm.cpu().numpy().astype(np.int64)
     want = np.lexsort((np.arange(n), lo, hi))  # stable: ties in input order
     assert np.array_equal(perm, want)

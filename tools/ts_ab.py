@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """A/B of the record plane's TeraSort kernels on 10 GB (100 M x 100-byte rows
 generated in HBM): the row gather (16-byte LDS-staged vs the dword gather)
-and the tie fix-up (scan + per-run fix vs the single kernel), each checked
-equal to the other and timed with HIP events (median of --reps).
+and the onesweep tile size of the u32-key sort passes, each checked equal to
+the default and timed with HIP events (median of --reps).
 
     python tools/ts_ab.py [--rows 100000000] [--reps 5]
 """
@@ -46,10 +46,12 @@ def main() -> int:
     res = {"rows": a.rows}
     res["keys32_ms"] = timed(lambda: RC.keys32(rec, TS.KEY, torch.zeros(2048, dtype=torch.int32, device=d)), a.reps)
     perms = {}
-    for mode in (0, 1):
-        res[f"sort_tie{mode}_ms"] = timed(lambda m=mode: perms.__setitem__(m, RC.sort(rec, TS.KEY, k32, gh,
-                                                                                       tie_mode=m)[0]), a.reps)
-    res["tie_modes_equal"] = bool(torch.equal(perms[0], perms[1]))
+    res["sort_ms"] = timed(lambda: perms.__setitem__(0, RC.sort(rec, TS.KEY, k32, gh)[0]), a.reps)
+    from lua_mapreduce_1_amd.ops import _hip
+    for r in (24, 40, 48, 32):  # onesweep keys per thread of the u32-key passes (32 = the default, restored last)
+        assert _hip.lib().mr_sort_set_rounds32(r) == 0
+        res[f"sort_rounds{r}_ms"] = timed(lambda: RC.sort(rec, TS.KEY, k32, gh), a.reps)
+        res[f"sort_rounds{r}_equal"] = bool(torch.equal(RC.sort(rec, TS.KEY, k32, gh)[0], perms[0]))
     perm = perms[0]
     outs = {}
     for mode in (0, 1):
@@ -58,7 +60,7 @@ def main() -> int:
     outs.clear()
     res["order_ok"] = RC.unsorted_pairs(RC.gather(rec, perm), TS.KEY) == 0
     print(json.dumps(res), flush=True)
-    ok = res["tie_modes_equal"] and res["gather_modes_equal"] and res["order_ok"]
+    ok = res["gather_modes_equal"] and res["order_ok"] and all(v for k, v in res.items() if k.endswith("_equal"))
     return 0 if ok else 1
 
 
