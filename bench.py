@@ -192,6 +192,13 @@ def main() -> int:
     words = args.words or corpus.EUROPARL_WORDS
     rank, world, device = D.init_from_env()
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if device.type == "cuda":
+        # host buffers (pinned splits, downloads) on the GPU's own socket
+        from lua_mapreduce_1_amd.utils import numa
+        nb = numa.bind_to_gpu(device.index or 0)
+        if args.verbose or rank == 0:
+            print(f"# rank {rank}: GPU {nb['pci']} on NUMA node {nb['node']}, {nb['cpus']} CPUs bound",
+                  file=sys.stderr, flush=True)
     import torch.distributed as dist
     backend = dist.get_backend() if dist.is_initialized() else ("single-process-" + device.type)
     if args.force_shuffle and world == 1 and not dist.is_initialized():

@@ -59,6 +59,9 @@ def main(argv=None) -> int:
 
     use_gpu = a.device == "auto" and torch.cuda.is_available()
     rank, world, device = D.init_from_env(use_gpu=use_gpu)
+    if device.type == "cuda":
+        from ..utils import numa
+        numa.bind_to_gpu(device.index or 0)  # pinned split buffers on the GPU's socket
     n = modules.normalize
     params = {"taskfn": n(a.taskfn), "mapfn": n(a.mapfn), "partitionfn": n(a.partitionfn),
               "reducefn": n(a.reducefn), "finalfn": n(finalfn) if finalfn else None,

@@ -51,6 +51,9 @@ class Tunables:
     map_sparse_min_mb: float = _knob("MR_MAP_SPARSE_MIN_MB", 128.0,
                                      "SPMD fold plane: input MiB per rank and iteration from which map tables "
                                      "are made sparse (MR_MAP_SPARSITY)")
+    numa_bind: bool = _knob("MR_NUMA_BIND", True,
+                            "SPMD ranks (bench.py, execute_spmd): restrict the rank's CPU threads to the NUMA "
+                            "node of its GPU before pinned buffers are allocated (utils/numa.py)")
     pin_exact: bool = _knob("MR_PIN_EXACT", True,
                             "split buffers in exact-size pinned memory (mr_host_alloc) instead of torch's "
                             "power-of-two pinned pool")
