@@ -5,6 +5,8 @@ first iteration (CPU engine; the GPU path is covered by
 test_ops_gpu.py::test_spmd_prefetch_pipelined_iterations_match)."""
 import dataclasses
 
+import pytest
+
 from lua_mapreduce_1_amd.parallel import spmd as S
 from lua_mapreduce_1_amd.runtime import codec
 from lua_mapreduce_1_amd.utils.corpus import europarl_like
@@ -37,3 +39,28 @@ def test_small_shares_keep_their_table(monkeypatch):
     eng, out = _run(monkeypatch, 1024.0)
     assert out[0] == out[2]
     assert eng._table_capacity < 64 * len(out[0])  # only the overflow regrowth, no sparsity
+
+
+@pytest.mark.gpu
+def test_overflowed_table_is_fitted_for_later_maps_gpu(gpu):
+    """A first map that overflows its table (6 k keys, 4 k slots) re-runs in a
+    table grown 16x; the later maps get one fitted to the key count
+    (2 slots per key, power of two), and every iteration's counts are exact."""
+    splits = europarl_like(seed=5, lines=8000, words=200_000, vocab_size=6_000, split_lines=1000)
+    eng = S.SPMDEngine(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                            init_args={"nsplits": len(splits), "num_reducers": 4}),
+                       split_store=S.SplitStore(splits), device=gpu, table_capacity=1 << 12)
+    want = {}
+    for s in splits:
+        for w in s.split():
+            want[w.decode()] = want.get(w.decode(), 0) + 1
+    caps = []
+    for _ in range(3):
+        r = eng.run_iteration()
+        got = {k: v[0] for _n, cols in eng.gather_results(r) for k, v in codec.iter_columnar(cols)}
+        assert got == want
+        caps.append(eng.table.cap)
+    if len(want) <= 1 << 12:
+        pytest.skip("corpus too small to overflow")
+    assert caps[0] == 16 << 12  # grown 16x after the overflow
+    assert caps[2] == 1 << (2 * len(want) - 1).bit_length()  # fitted: next_pow2(2 n)
