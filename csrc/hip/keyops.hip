@@ -266,18 +266,18 @@ __global__ void key_meta_kernel(const u64* hi, const u64* lo, const u64* rep, u6
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const u64 h = hi[i], l = lo[i];
+    const bool lng = key_is_long(l);
+    const u64 len = lng ? rep_len(rep[i]) : packed_len(l);
+    if (out_len) out_len[i] = (long long)len;
+    if (!out_part) continue;  // lengths only: no key bytes read
     u32 f = FNV_OFFSET;
-    u64 len;
-    if (!key_is_long(l)) {
-      len = packed_len(l);
+    if (!lng) {
       for (u32 k = 0; k < len; ++k) f = fnv1_step(f, packed_byte(h, l, k));
     } else {
-      len = rep_len(rep[i]);
       const u8* p = src + rep_off(rep[i]);
       for (u64 k = 0; k < len; ++k) f = fnv1_step(f, p[k]);
     }
-    if (out_part) out_part[i] = nparts ? f % nparts : f;
-    if (out_len) out_len[i] = (long long)len;
+    out_part[i] = nparts ? f % nparts : f;
   }
 }
 

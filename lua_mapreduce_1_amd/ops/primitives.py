@@ -747,7 +747,8 @@ def key_word(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.T
 
 
 def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor,
-                   src: torch.Tensor | None, nparts: int, klen: torch.Tensor | None = None) -> torch.Tensor | None:
+                   src: torch.Tensor | None, nparts: int, klen: torch.Tensor | None = None,
+                   with_part: bool = False):
     """Stable permutation ordering rows by (partition, exact key bytes) on the
     device, for key sets the (partition, hi, lo) sort plus the tie fix-up
     cannot order (long keys — whose lo is a hash — in long runs of a shared
@@ -762,11 +763,14 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     groups, and so on.  Each round is a stable LSD radix sort, so rows of one
     key set keep their input order where they tie.  None when a key is longer
     than 8 * EXACT_MAX_WORDS bytes (the caller orders on the host).
-    ``klen``: the keys' lengths when the caller has them (key_meta)."""
+    ``klen``: the keys' lengths when the caller has them (key_meta).
+    ``with_part``: return (perm, partitions in the new order as int64) —
+    the sort's major word, so no gather is needed for it."""
     n = hi.numel()
     d = hi.device
     if n == 0:
-        return torch.zeros(0, dtype=torch.int64, device=d)
+        z = torch.zeros(0, dtype=torch.int64, device=d)
+        return (z, z.clone()) if with_part else z
     if klen is None:
         _, klen = key_meta(hi, lo, rep, src, want_part=False)
     klen = klen.to(torch.int64)
@@ -777,9 +781,11 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     w1 = key_word(hi, lo, rep, src, 1)
     lc = klen.clamp(max=16)
     cols = [part.to(torch.int64), hi, w1, lc]
-    p32 = sort_keys_checked(cols, bits=[pbits, 64, 64, 8])
+    p32, spart = sort_keys_checked(cols, bits=[pbits, 64, 64, 8], return_keys=True)
+    # every later step reorders rows only inside runs of one partition
+    done = (lambda p: (p, spart)) if with_part else (lambda p: p)  # noqa: E731
     if max_len <= 16:
-        return p32.long()
+        return done(p32.long())
     if hi.is_cuda:
         # runs of rows equal in the sort columns (long keys sharing 16 bytes),
         # found through a hash of the columns in sorted order and insertion-
@@ -795,7 +801,7 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
         _hip.call("mr_exact_fix", _hip.ptr(sh), _hip.ptr(p32), n, _hip.ptr(part32), _hip.ptr(hi), _hip.ptr(w1),
                   _hip.ptr(klen), _hip.ptr(rep), _hip.ptr(src), _hip.ptr(bad), s)
         if not int(bad.item()):
-            return p32.long()
+            return done(p32.long())
     perm = p32.long()
     scols = [c[perm] for c in cols]
     pos = torch.arange(n, dtype=torch.int64, device=d)
@@ -806,7 +812,7 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
         for c in scols:
             same &= c[1:] == c[:-1]
         if not bool(same.any()):
-            return perm
+            return done(perm)
         member = torch.zeros(pos.numel(), dtype=torch.bool, device=d)
         member[1:] |= same
         member[:-1] |= same

@@ -503,21 +503,26 @@ def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=N
         part, klen = ops.key_meta(hi, lo, rep, src, nparts=nparts)
     else:
         part = partition_of(hi, lo, rep, src, nparts, partition_module)
-    perm = ops.exact_key_perm(part, hi, lo, rep, src, nparts, klen=klen) if src is not None else None
-    exact = perm is not None
-    if perm is None:
+    got = ops.exact_key_perm(part, hi, lo, rep, src, nparts, klen=klen, with_part=True) if src is not None else None
+    exact = got is not None
+    spart = None
+    if got is None:
         perm = ops.sort_keys_checked([part.to(torch.int64), hi, lo],
                                      bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
-    if hi.is_cuda and klen is not None:
+    else:
+        perm, spart = got
+    if hi.is_cuda and spart is not None:
+        # one gather launch for the four key/value columns; the partitions
+        # come sorted from the sort and the lengths from (lo, rep) of the
+        # gathered rows (no key bytes read)
         from ..ops import _hip
         n = hi.numel()
-        cols = [torch.empty(n, dtype=torch.int64, device=hi.device) for _ in range(5)]
-        spart = torch.empty(n, dtype=torch.int32, device=hi.device)
+        cols = [torch.empty(n, dtype=torch.int64, device=hi.device) for _ in range(4)]
         _hip.call("mr_gather_cols", _hip.ptr(perm.to(torch.int32)), n, _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val),
-                  _hip.ptr(rep), _hip.ptr(klen), _hip.ptr(part.to(torch.int32).contiguous()),
-                  *[_hip.ptr(c) for c in cols], _hip.ptr(spart), _hip.stream(hi.device))
-        pend = finalize_device(*cols[:4], src, nparts, partition_module, part=spart, _presorted=True,
-                               blob_cap=blob_cap, lengths=cols[4])
+                  _hip.ptr(rep), None, None, *[_hip.ptr(c) for c in cols], None, None, _hip.stream(hi.device))
+        _, slen = ops.key_meta(cols[0], cols[1], cols[3], src, want_part=False)
+        pend = finalize_device(*cols, src, nparts, partition_module, part=spart.to(torch.int32), _presorted=True,
+                               blob_cap=blob_cap, lengths=slen)
     else:
         pend = finalize_device(hi[perm], lo[perm], val[perm], rep[perm], src, nparts, partition_module,
                                part=part[perm], _presorted=True, blob_cap=blob_cap)
