@@ -95,3 +95,12 @@ def test_exact_key_perm_gpu(gpu, nparts):
 def test_exact_key_perm_short_runs_gpu(gpu, nparts):
     """Runs of at most 6 keys sharing 16 bytes: one fix kernel (mr_exact_fix)."""
     _check(_short_runs(4, 40_000), nparts, gpu)
+
+
+def test_exact_key_perm_returns_sorted_partitions_cpu():
+    keys = _short_runs(5, 200)
+    hi, lo, rep, src = _columns(keys)
+    part = torch.tensor([K.fnv1(k) % 7 for k in keys], dtype=torch.int32)
+    perm, spart = ops.exact_key_perm(part, hi, lo, rep, src, 7, with_part=True)
+    assert torch.equal(spart, part.to(torch.int64)[perm])
+    assert torch.equal(perm, ops.exact_key_perm(part, hi, lo, rep, src, 7))
