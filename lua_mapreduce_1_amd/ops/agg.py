@@ -302,6 +302,30 @@ class AggTable:
         self._pending.append((h, lw, r, cols, ok))
         self.npost += n if self.list_mode else 0
 
+    def rehome_long_keys(self, buf: torch.Tensor, lo_off: int, hi_off: int, heap: torch.Tensor,
+                         heap_cap: int) -> None:
+        """Streaming map rounds: the bytes of the long keys whose rep points
+        into buf[lo_off:hi_off) move to the key heap at the front of ``buf``
+        (``heap`` = int64[2] bump counter + full flag) and their reps follow
+        (HashTable.rehome_long_keys for the GPU key table)."""
+        if self.is_cuda:
+            self.keys.rehome_long_keys(buf, lo_off, hi_off, heap, heap_cap)
+            return
+        b = _np(buf)
+        h = heap.numpy()
+        for hi_, lo_, r, _cols, ok in self._pending:
+            long_ = ok & ((lo_ & np.uint64(0xFF)) == np.uint64(K.LONG_MARK))
+            off = r >> np.uint64(K.REP_LEN_BITS)
+            for i in np.flatnonzero(long_ & (off >= np.uint64(lo_off)) & (off < np.uint64(hi_off))):
+                o, n = int(r[i]) >> K.REP_LEN_BITS, int(r[i]) & K.REP_LEN_MASK
+                d = int(h[0])
+                if d + n > heap_cap:
+                    h[1] = 1
+                    continue
+                b[d:d + n] = b[o:o + n].copy()
+                h[0] = d + n
+                r[i] = np.uint64(K.make_rep(d, n))
+
     # -- state -----------------------------------------------------------------
     def stats(self) -> tuple[int, bool]:
         if self.is_cuda:

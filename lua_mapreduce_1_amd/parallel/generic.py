@@ -58,6 +58,7 @@ from ..runtime import device as devmod
 from ..runtime import modules
 from ..utils import STATUS
 from ..utils import trace
+from ..utils.config import TUNABLES
 from . import dist as D
 
 
@@ -70,6 +71,11 @@ class NeedsHostMap(Exception):
     (the caller runs the host ``mapfn`` instead)."""
 
 
+class StreamedSourceError(ValueError):
+    """A streamed map (arena_cap_mb) emitted keys that are not spans of its
+    staged input (raised to the caller, not treated as a failing job)."""
+
+
 # ---------------------------------------------------------------------------
 class KeySource:
     """The ONE byte source every rep word of an iteration's table indexes:
@@ -80,6 +86,8 @@ class KeySource:
     def __init__(self, device):
         self.device = torch.device(device)
         self.begin(None)
+
+    fixed = False  # a streamed map: the source is the engine's ring buffer, nothing may be appended
 
     def begin(self, arena) -> None:
         self.arena = arena
@@ -108,6 +116,9 @@ class KeySource:
         t = t.reshape(-1)
         if t.dtype != torch.uint8:
             raise TypeError("key bytes must be a uint8 tensor")
+        if self.fixed:
+            raise StreamedSourceError("a streamed general-plane map (arena_cap_mb) emits spans of its staged input "
+                                      "only (no host keys or spans of other tensors)")
         n = t.numel()
         need = self.used + n
         if self.buf is None or self.buf.numel() < need:
@@ -421,9 +432,6 @@ class GenericPlane:
         self.map = GenericMap(eng.device, self._cap, self.phys, self.dtype)
         self.red = None
         self._lines = None
-        if eng._arena_cap():
-            raise ValueError("the general device plane maps a rank's whole input at once (no arena_cap_mb / "
-                             "MR_ARENA_CAP_MB streaming)")
         red = eng.redmod
         self.reducefn = modules.field(red, "reducefn") if self.host_reduce else None
         if self.host_reduce and self.reducefn is None:
@@ -451,20 +459,32 @@ class GenericPlane:
         return base
 
     # -- map --------------------------------------------------------------------
+    def stream_round_end(self, buf, lo: int, hi: int, heap, H: int) -> None:
+        """After a streamed round (SPMDEngine._stage_streaming): the long keys
+        the round introduced move their bytes to the key heap at the front of
+        the ring buffer, so the round's slot can be refilled (a full heap is
+        seen after the map, which then re-runs with a larger one)."""
+        self.map.table.rehome_long_keys(buf, lo, hi, heap, H)
+
     def _map(self, jobs, recs, j0, j1) -> None:
         eng = self.eng
         mp = self.map
         dmap = eng.dmap
+        streamed = False
         if eng.device_input == "split" and j1 > j0:
             ids = eng._split_ids(jobs, j0, j1)
             self._ids0 = ids[0]
-        mp.emit.line_base = self._line_base() if eng.device_input == "split" else None
+            streamed = eng._streaming(ids)
+        # streamed rounds reuse ring slots: keys are spans of the staged input
+        # (rehomed after each round), global line numbers are not available
+        mp.emit.line_base = self._line_base() if eng.device_input == "split" and not streamed else None
         if mp.table.cap != ops.next_pow2(max(1024, self._cap)) and mp.table.is_cuda:
             # the capacity target moved since this table was made (grown, or fitted)
             mp.table = A.AggTable(self._cap, eng.device, self.phys.cols if self.phys is not None else None,
                                   self.dtype)
         for _attempt in range(64):
             mp.begin(None)
+            mp.src.fixed = streamed
             broken = []
             for (a, b), data in eng._stage_chunks(jobs, j0, j1):
                 if all(recs[j].status == STATUS.FAILED for j in range(a, b)):
@@ -479,7 +499,7 @@ class GenericPlane:
                 try:
                     dmap(keys if b - a > 1 else keys[0], data, mp.emit)
                     mp.flush_host()
-                except NeedsHostMap:
+                except (NeedsHostMap, StreamedSourceError):
                     raise
                 except Exception:  # noqa: BLE001
                     mp.host = []
@@ -493,6 +513,14 @@ class GenericPlane:
                     recs[j].real_time = (t1 - t0) / (b - a)
                     recs[j].cpu_time = (time.process_time() - c0) / (b - a)
             n, ovf = mp.table.stats()
+            if streamed and int(ops.host_read(eng._stream_heap)[1]):
+                # the key heap ran out: some long keys still point into a ring
+                # slot that was refilled — re-map with a heap twice as large
+                cur = getattr(eng, "_stream_heap_mb", TUNABLES.stream_heap_mb)
+                eng._stream_heap_mb = 2 * cur
+                sys.stderr.write("# streaming general map: long-key heap of %.0f MiB full, re-mapping with %.0f MiB\n"
+                                 % (cur, 2 * cur))
+                continue
             if broken:
                 # a chunk whose map raised may have inserted part of its rows:
                 # redo the rank's map without it (BROKEN), or leave it out

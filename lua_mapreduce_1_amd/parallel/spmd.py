@@ -719,10 +719,10 @@ class SPMDEngine:
         cap = self._arena_cap()
         if not cap or not ids:
             return False
-        if self.plane_kind not in ("fold", "list"):
-            raise ValueError(f"arena_cap_mb / MR_ARENA_CAP_MB streaming is implemented for the fold and list "
-                             f"planes (this job runs the {self.plane_kind} plane; the record plane spills "
-                             f"with record_cap_mb)")
+        if self.plane_kind not in ("fold", "list", "generic"):
+            raise ValueError(f"arena_cap_mb / MR_ARENA_CAP_MB streaming is implemented for the fold, list and "
+                             f"general planes (this job runs the {self.plane_kind} plane, which spills with "
+                             f"record_cap_mb)")
         a, b = self.splits.region(ids[0], ids[-1] + 1)
         return b - a > cap
 

@@ -209,3 +209,58 @@ def test_generic_gloo_w3(which, mod, args):
 def test_generic_forced_shuffle_w1(which, mod, args):
     ok, owned, n, _ = _spawn(1, which, mod, args, force_shuffle=True)
     assert ok and n > 100
+
+
+def _long_text():
+    from test_exactness import colliding_text
+    return [colliding_text(11 + i, ntok=2000, nlong=150) for i in range(2)]
+
+
+STREAM_CASES = [("scores", SS, {}), ("text", GM, {"mode": "max_host"}), ("text", GM, {"mode": "docs"}),
+                ("text", GM, {"mode": "docs_concat"})]
+
+
+@pytest.mark.parametrize("which,mod,args", STREAM_CASES, ids=["scores", "max_host", "docs", "docs_concat"])
+def test_generic_streams_rounds_cpu(which, mod, args):
+    """arena_cap_mb on the general plane: the rank's splits are mapped in
+    rounds through the two capped ring slots, long keys moving to the key heap
+    after each round; results equal the whole-input oracle."""
+    splits = make_data(which) + (_long_text() if which == "text" else [])
+    eng, res, got = run_engine(mod, splits, torch.device("cpu"), args, arena_cap_mb=0.06)
+    assert eng.plane_kind == "generic"
+    assert eng._streaming(eng._split_ids(eng._jobs(), 0, len(splits)))
+    assert close_lists(got, oracle(which, args.get("mode"), splits))
+    assert res.failed_maps == 0
+
+
+def test_generic_streamed_host_keys_raise_cpu():
+    with pytest.raises(ValueError, match="streamed general-plane map"):
+        run_engine(GM, make_data("text"), torch.device("cpu"), {"mode": "mixed"}, arena_cap_mb=0.06)
+
+
+@pytest.mark.parametrize("on_gpu", [False, pytest.param(True, marks=pytest.mark.gpu)])
+def test_generic_stream_heap_grows(request, monkeypatch, on_gpu):
+    """A long-key heap too small for the rounds' long keys doubles and the
+    general map re-runs; the value lists stay exact."""
+    import dataclasses
+    from test_exactness import colliding_text
+    from lua_mapreduce_1_amd.parallel import generic as G
+    from lua_mapreduce_1_amd.parallel import spmd as S
+    dev = request.getfixturevalue("gpu") if on_gpu else torch.device("cpu")
+    monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(S.TUNABLES, stream_heap_mb=0.07))
+    monkeypatch.setattr(G, "TUNABLES", dataclasses.replace(G.TUNABLES, stream_heap_mb=0.07))
+    splits = [colliding_text(90 + i, ntok=20000, nlong=3000) for i in range(4)]
+    cap = max(len(s) for s in splits) + 1
+    eng, res, got = run_engine(GM, splits, dev, {"mode": "docs"}, arena_cap_mb=cap / (1 << 20))
+    assert close_lists(got, oracle("text", "docs", splits))
+    assert eng._stream_heap_mb > 0.07
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which,mod,args", STREAM_CASES, ids=["scores", "max_host", "docs", "docs_concat"])
+def test_generic_streams_rounds_gpu(gpu, which, mod, args):
+    splits = make_data(which) + (_long_text() if which == "text" else [])
+    eng, res, got = run_engine(mod, splits, gpu, args, arena_cap_mb=0.06)
+    assert eng._streaming(eng._split_ids(eng._jobs(), 0, len(splits)))
+    assert close_lists(got, oracle(which, args.get("mode"), splits))
+    assert res.failed_maps == 0
