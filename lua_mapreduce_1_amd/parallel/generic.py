@@ -478,7 +478,9 @@ class GenericPlane:
         # streamed rounds reuse ring slots: keys are spans of the staged input
         # (rehomed after each round), global line numbers are not available
         mp.emit.line_base = self._line_base() if eng.device_input == "split" and not streamed else None
-        if mp.table.cap != ops.next_pow2(max(1024, self._cap)) and mp.table.is_cuda:
+        if getattr(self, "_table_restored", False) or (mp.table.cap != ops.next_pow2(max(1024, self._cap))
+                                                          and mp.table.is_cuda):
+            self._table_restored = False
             # the capacity target moved since this table was made (grown, or fitted)
             mp.table = A.AggTable(self._cap, eng.device, self.phys.cols if self.phys is not None else None,
                                   self.dtype)
@@ -543,6 +545,93 @@ class GenericPlane:
                 self._cap = fit  # grown past the key count (16x after an overflow): fitted for the next maps
             return
         raise RuntimeError("general plane: the map did not converge (table regrowth / retries)")
+
+    # -- map checkpoints (split-level restart) ------------------------
+    def _save_map(self) -> None:
+        """This rank's map output of the iteration -> ``checkpoint_dir``
+        (data-only .npz: key words, key bytes, and the physical fold columns or
+        the value lists), so a relaunch after a failure later in the iteration
+        restores it instead of re-mapping the rank's splits (the fold plane's
+        SPMDEngine._save_map for the general plane)."""
+        eng = self.eng
+        path = eng._map_ckpt_path()
+        if path is None:
+            return
+        import os
+        mp = self.map
+        src = mp.src.source()
+        if self.list_mode:
+            slot, hi, lo, rep, pslot, pval = mp.table.postings()
+        else:
+            slot, hi, lo, rep, cols = mp.table.compact()
+        _, ln = ops.key_meta(hi, lo, rep, src, want_part=False)
+        off, blob = ops.gather_key_bytes(hi, lo, rep, src, lengths=ln)
+        arrs = {"hi": hi, "lo": lo, "off": off, "blob": blob,
+                "rows": torch.tensor([mp.rows], dtype=torch.int64)}
+        if self.list_mode:
+            m = hi.numel()
+            pos = torch.full((max(self._slot_space(), int(slot.max()) + 1 if m else 1),), -1, dtype=torch.int64,
+                             device=slot.device)
+            pos[slot] = torch.arange(m, dtype=torch.int64, device=slot.device)
+            kidx = pos[pslot.clamp(min=0)]
+            keep = (pslot >= 0) & (kidx >= 0)
+            arrs["pkey"], arrs["pval"] = kidx[keep], pval[keep]
+        else:
+            for j, c in enumerate(cols):
+                arrs[f"col{j}"] = c
+        os.makedirs(eng.checkpoint_dir, exist_ok=True)
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            np.savez(f, **{k: v.detach().cpu().numpy() for k, v in arrs.items()})
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+
+    def _restore_map(self, recs, j0: int, j1: int) -> bool:
+        """Refill the map table from this rank's checkpoint of the iteration,
+        if an earlier launch wrote it (the saved keys' bytes become the key
+        source); the rank's map jobs are WRITTEN without running."""
+        eng = self.eng
+        path = eng._map_ckpt_path()
+        import os
+        if path is None or not os.path.exists(path):
+            return False
+        with np.load(path, allow_pickle=False) as z:
+            a = {k: z[k] for k in z.files}
+        d = eng.device
+        t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(d)  # noqa: E731
+        koff = a["off"].astype(np.int64)
+        lens = np.diff(koff).astype(np.uint64)
+        rep = t((((koff[:-1].astype(np.uint64)) << np.uint64(K.REP_LEN_BITS)) | lens).view(np.int64))
+        blob = t(np.concatenate([a["blob"], np.zeros(1, np.uint8)]))
+        hi, lo = t(a["hi"].view(np.int64)), t(a["lo"].view(np.int64))
+        m = hi.numel()
+        mp = self.map
+        mp.begin(None)
+        mp.src.begin(blob)
+        cap = ops.next_pow2(max(1 << 12, 4 * m, self._cap))
+        if self.list_mode:
+            mp.table = A.AggTable(cap, d, None, self.dtype)
+            mp.table.src = blob
+            kidx = t(a["pkey"])
+            pv = t(a["pval"].view(np.int64))
+            if self.dtype == "f64":
+                pv = pv.view(torch.float64)
+            mp.table.insert(int(kidx.numel()), [pv], hi=hi[kidx], lo=lo[kidx], rep=rep[kidx])
+        else:
+            # the saved physical columns are folded 1:1 (the receive side's merge spec)
+            merge = [(dt, op, j) for j, (dt, op, _i) in enumerate(self.phys.cols)]
+            mp.table = A.AggTable(cap, d, merge)
+            mp.table.src = blob
+            mp.table.insert(m, [t(a[f"col{j}"]) for j in range(len(merge))], hi=hi, lo=lo, rep=rep)
+        self._table_restored = True  # the next map gets a regular table again
+        mp.rows = int(a["rows"][0])
+        now = time.time()
+        for j in range(j0, j1):
+            recs[j].status, recs[j].started, recs[j].written, recs[j].worker = STATUS.WRITTEN, now, now, eng.rank
+        eng.maps_restored += 1
+        sys.stderr.write("# rank %d: map of iteration %d restored from its checkpoint\n" % (eng.rank, eng.iteration))
+        return True
 
     # -- shuffle ----------------------------------------------------------------
     def _shuffle(self, keys: tuple, src, failed: int):
@@ -665,7 +754,10 @@ class GenericPlane:
         recs = _records(eng, jobs, j0, j1, t0)
         res.map_jobs = recs
         with trace.range("mr.gen.map"):
-            self._map(jobs, recs, j0, j1)
+            if not self._restore_map(recs, j0, j1):
+                self._map(jobs, recs, j0, j1)
+                self._save_map()
+        eng._maybe_inject_fault("shuffle")
         T["map"] = time.time() - t0
         t1 = time.time()
         mp = self.map

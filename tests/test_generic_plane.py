@@ -264,3 +264,55 @@ def test_generic_streams_rounds_gpu(gpu, which, mod, args):
     assert eng._streaming(eng._split_ids(eng._jobs(), 0, len(splits)))
     assert close_lists(got, oracle(which, args.get("mode"), splits))
     assert res.failed_maps == 0
+
+
+# -- split-level restart on the general plane ------------------
+def _restart_rank(rank, world, port, q, which, mod, args, ckpt, fault):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), MR_SPMD_FAULT=fault)
+    import torch.distributed as dist
+    from lua_mapreduce_1_amd.parallel import dist as D
+    D.init_from_env(backend="gloo", use_gpu=False, timeout_s=30)
+    splits = make_data(which)
+    eng, res, got = run_engine(mod, splits, torch.device("cpu"), args, checkpoint_dir=ckpt)
+    if rank == 0:
+        q.put((eng.maps_restored, close_lists(got, oracle(which, args.get("mode"), splits))))
+    else:
+        q.put((eng.maps_restored, None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _restart_launch(world, which, mod, args, ckpt, fault, expect_fail):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_restart_rank, args=(r, world, port, q, which, mod, args, ckpt, fault))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240 if not expect_fail else 120)
+        if p.is_alive():
+            p.terminate()
+            p.join(10)
+    if expect_fail:
+        return [p.exitcode for p in procs], None
+    return [p.exitcode for p in procs], [q.get(timeout=5) for _ in range(world)]
+
+
+@pytest.mark.parametrize("which,mod,args", [CASES[0], CASES[3]], ids=["scores", "docs"])
+def test_generic_restart_restores_map_outputs(tmp_path, which, mod, args):
+    """Rank 1 dies after the map phase of iteration 1 (``1:1:exit::shuffle``):
+    both ranks had checkpointed their map outputs (typed fold columns / value
+    lists); the relaunch restores them instead of re-mapping, and the results
+    equal the oracle."""
+    ckpt = str(tmp_path / "ckpt")
+    codes, _ = _restart_launch(2, which, mod, args, ckpt, "1:1:exit::shuffle", expect_fail=True)
+    assert codes[1] == 17 and codes[0] != 0, codes
+    assert len([f for f in os.listdir(ckpt) if ".map.it1." in f]) == 2
+    codes, out = _restart_launch(2, which, mod, args, ckpt, "", expect_fail=False)
+    assert codes == [0, 0], codes
+    assert sorted(o[0] for o in out) == [1, 1]
+    assert [o[1] for o in out if o[1] is not None] == [True]
+    assert not [f for f in os.listdir(ckpt) if ".map." in f]  # consumed checkpoints are removed
