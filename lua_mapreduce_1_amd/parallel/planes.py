@@ -618,12 +618,52 @@ class RecordPlane:
         else:
             self._out.append(rec if rec.device == dev else rec.to(dev, non_blocking=True))
 
+    # -- map checkpoints (split-level restart) ------------------------
+    def _save_rows(self) -> None:
+        """This rank's mapped rows -> ``checkpoint_dir`` (data-only .npz), so a
+        relaunch after a failure later in the iteration restores them instead
+        of re-running the rank's map jobs."""
+        eng = self.eng
+        path = eng._map_ckpt_path()
+        if path is None or self.shape is None:
+            return
+        import os
+        rows = torch.cat([r.cpu() for r in self._out]) if self._out else torch.zeros((0, self.shape[0]),
+                                                                                     dtype=torch.uint8)
+        os.makedirs(eng.checkpoint_dir, exist_ok=True)
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            np.savez(f, rows=rows.numpy(), key_bytes=np.array([self.shape[1]], np.int64))
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+
+    def _restore_rows(self, recs, j0: int, j1: int) -> bool:
+        eng = self.eng
+        path = eng._map_ckpt_path()
+        import os
+        if path is None or not os.path.exists(path):
+            return False
+        with np.load(path, allow_pickle=False) as z:
+            rows, kb = z["rows"], int(z["key_bytes"][0])
+        if rows.shape[0]:
+            self.emitter.records(torch.from_numpy(rows).to(eng.device), kb)  # the emitter's spill rule applies
+        else:
+            self.shape = (int(rows.shape[1]), kb)
+        now = time.time()
+        for j in range(j0, j1):
+            recs[j].status, recs[j].started, recs[j].written, recs[j].worker = STATUS.WRITTEN, now, now, eng.rank
+        eng.maps_restored += 1
+        sys.stderr.write("# rank %d: rows of iteration %d restored from the checkpoint\n" % (eng.rank, eng.iteration))
+        return True
+
     def _map(self, jobs, recs, j0, j1) -> torch.Tensor:
         eng = self.eng
         self._out = []
         self._bytes = 0
         self._spilled = False
-        for j in range(j0, j1):
+        restored = self._restore_rows(recs, j0, j1)
+        for j in range(j0, j0 if restored else j1):
             t0, c0 = time.time(), time.process_time()
             v = jobs[j][1]
             data = None
@@ -639,6 +679,8 @@ class RecordPlane:
                     recs[j].repetitions += 1
                     recs[j].status = STATUS.BROKEN if attempt < 2 else STATUS.FAILED
             _mark_written(recs, j, j + 1, t0, time.time(), c0)
+        if not restored:
+            self._save_rows()
         if self.shape is None:  # nothing emitted on this rank: agree on the shape with the others
             shapes = D.all_gather_object(None, eng.group) if D.initialized() and eng.world > 1 else []
             self.shape = next((x for x in shapes if x is not None), (TS.REC, TS.KEY))
@@ -818,6 +860,7 @@ class RecordPlane:
         self.shape = None
         with trace.range("mr.rec.map"):
             rec = self._map(jobs, recs, j0, j1)
+        eng._maybe_inject_fault("shuffle")
         kb = self.shape[1]
         T["map"] = time.time() - t0
         t1 = time.time()
