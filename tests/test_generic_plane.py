@@ -316,3 +316,27 @@ def test_generic_restart_restores_map_outputs(tmp_path, which, mod, args):
     assert sorted(o[0] for o in out) == [1, 1]
     assert [o[1] for o in out if o[1] is not None] == [True]
     assert not [f for f in os.listdir(ckpt) if ".map." in f]  # consumed checkpoints are removed
+
+
+def _restart_gpu_proc(q, which, mod, args, ckpt, fault):
+    os.environ["MR_SPMD_FAULT"] = fault
+    splits = make_data(which)
+    eng, res, got = run_engine(mod, splits, torch.device("cuda", 0), args, checkpoint_dir=ckpt)
+    q.put((eng.maps_restored, close_lists(got, oracle(which, args.get("mode"), splits))))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which,mod,args", [CASES[0], CASES[3]], ids=["scores", "docs"])
+def test_generic_restart_restores_map_outputs_gpu(gpu, tmp_path, which, mod, args):
+    """One rank on the GPU exits after its map phase; the relaunch restores
+    the saved map output into a fresh device table and the results are exact."""
+    ckpt = str(tmp_path / "ckpt")
+    ctx = mp.get_context("spawn")
+    for fault, want_code in (("1:0:exit::shuffle", 17), ("", 0)):
+        q = ctx.Queue()
+        p = ctx.Process(target=_restart_gpu_proc, args=(q, which, mod, args, ckpt, fault))
+        p.start()
+        p.join(180)
+        assert p.exitcode == want_code, p.exitcode
+    restored, ok = q.get(timeout=5)
+    assert restored == 1 and ok
