@@ -248,3 +248,24 @@ def test_records_restart_restores_rows(tmp_path):
     codes, out = launch("", False)
     assert codes == [0, 0], codes
     assert [o[1] for o in out] == [1, 1] and out[0][2] is True
+
+
+def _restart_gpu_proc(q, args, ckpt, fault):
+    os.environ["MR_SPMD_FAULT"] = fault
+    eng, _res, rows = run_engine(args, torch.device("cuda", 0), checkpoint_dir=ckpt)
+    q.put((eng.maps_restored, check(rows, args)))
+
+
+@pytest.mark.gpu
+def test_records_restart_restores_rows_gpu(gpu, tmp_path):
+    ckpt = str(tmp_path / "ckpt")
+    args = dict(SHAPES[2], rows=50_000)
+    ctx = mp.get_context("spawn")
+    for fault, want_code in (("1:0:exit::shuffle", 17), ("", 0)):
+        q = ctx.Queue()
+        p = ctx.Process(target=_restart_gpu_proc, args=(q, args, ckpt, fault))
+        p.start()
+        p.join(180)
+        assert p.exitcode == want_code, p.exitcode
+    restored, ok = q.get(timeout=5)
+    assert restored == 1 and ok
