@@ -158,6 +158,16 @@ class ListEmitter:
         raise _UseGeneric()
 
 
+class _SavedVocab:
+    """The word arrays of a restored list-plane map (``Vocab.arrays()``)."""
+
+    def __init__(self, hi, lo, rep, id_bits: int):
+        self.hi, self.lo, self.rep, self.id_bits = hi, lo, rep, id_bits
+
+    def arrays(self):
+        return self.hi, self.lo, self.rep
+
+
 class ListPlane:
     """``device_reduce = "concat_unique" | "concat"`` (see module docstring)."""
 
@@ -175,6 +185,7 @@ class ListPlane:
         self._cpu_parts: list = []
         self.streamed = False
         self._after_issue = None
+        self._restored = None  # (vocabulary arrays, key-byte source) of a restored map
         self.emitter = ListEmitter(self)
         if eng.device_input != "split":
             raise ValueError("the list plane maps engine-staged splits (device_input = 'split')")
@@ -311,6 +322,68 @@ class ListPlane:
             return torch.zeros(0, dtype=torch.int64)
         return II.map_postings(eng.arena[:self._cpu_end], self.vocab, self.doc_bits)
 
+    # -- map checkpoints (split-level restart) ------------------------
+    def _save_map(self, keys: torch.Tensor) -> None:
+        """This rank's postings of the iteration -> ``checkpoint_dir`` (data-only
+        .npz: the posting keys ``id << doc_bits | line``, the words their ids
+        name with their key bytes, the line numbering), so a relaunch after a
+        failure later in the iteration restores them instead of re-mapping
+        the rank's splits."""
+        eng = self.eng
+        path = eng._map_ckpt_path()
+        if path is None:
+            return
+        import os
+        vhi, vlo, vrep = self.vocab.arrays()
+        ids = torch.unique((keys >> self.doc_bits) & ((1 << self.vocab.id_bits) - 1)) if keys.numel() else keys[:0]
+        src = self._src()
+        hi, lo, rep = vhi[ids], vlo[ids], vrep[ids]
+        if ids.numel():
+            off, blob = ops.gather_key_bytes(hi, lo, rep, src)
+        else:
+            off, blob = torch.zeros(1, dtype=torch.int64), torch.zeros(0, dtype=torch.uint8)
+        meta = torch.tensor([self.vocab.id_bits, self.doc_bits, self.line_base, int(self.streamed)])
+        arrs = {"keys": keys, "ids": ids, "hi": hi, "lo": lo, "off": off, "blob": blob, "meta": meta}
+        os.makedirs(eng.checkpoint_dir, exist_ok=True)
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            np.savez(f, **{k: v.detach().cpu().numpy() for k, v in arrs.items()})
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+
+    def _restore_map(self, recs, j0: int, j1: int) -> torch.Tensor | None:
+        """The postings of this rank's checkpoint of the iteration, if an
+        earlier launch wrote it: the words are put back under their ids (the
+        saved key bytes become the key source) and the rank's map jobs are
+        WRITTEN without running."""
+        eng = self.eng
+        path = eng._map_ckpt_path()
+        import os
+        if path is None or not os.path.exists(path):
+            return None
+        with np.load(path, allow_pickle=False) as z:
+            a = {k: z[k] for k in z.files}
+        id_bits, self.doc_bits, self.line_base, streamed = (int(x) for x in a["meta"])
+        self.streamed = bool(streamed)
+        koff = a["off"].astype(np.int64)
+        lens = np.diff(koff).astype(np.uint64)
+        ids = a["ids"].astype(np.int64)
+        words = np.zeros((3, 1 << id_bits), np.int64)  # hi, lo, rep by word id
+        words[0, ids], words[1, ids] = a["hi"], a["lo"]
+        words[2, ids] = ((koff[:-1].astype(np.uint64) << np.uint64(REP_LEN_BITS)) | lens).view(np.int64)
+        d = eng.device
+        t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(d)  # noqa: E731
+        self._restored = (_SavedVocab(t(words[0]), t(words[1]), t(words[2]), id_bits),
+                          t(np.concatenate([a["blob"], np.zeros(1, np.uint8)])))
+        now = time.time()
+        for j in range(j0, j1):
+            recs[j].status, recs[j].started, recs[j].written, recs[j].worker = STATUS.WRITTEN, now, now, eng.rank
+        eng.maps_restored += 1
+        sys.stderr.write("# rank %d: postings of iteration %d restored from the checkpoint\n"
+                         % (eng.rank, eng.iteration))
+        return t(a["keys"])
+
     # -- sort / group ---------------------------------------------------------
     def _words(self, keys: torch.Tensor, bits: int, from_bit: int, doc_bits: int, id_bits: int, doc_base: int,
                runs: bool = False):
@@ -356,9 +429,14 @@ class ListPlane:
         ahead = 0 if not (prefetch_next if prefetch_next is not None else eng.prefetch) else (
             2 if lookahead is None else min(lookahead, 2))
         self._after_issue = (lambda: eng._prefetch_ahead(jobs, j0, j1, q, ahead)) if ahead else None
+        self._restored = None
         try:
             with trace.range("mr.list.map"):
-                keys = self._map(jobs, recs, j0, j1)
+                self.line_offsets()  # (a collective: every rank, restored or not)
+                keys = self._restore_map(recs, j0, j1)
+                if keys is None:
+                    keys = self._map(jobs, recs, j0, j1)
+                    self._save_map(keys)
         except _UseGeneric:
             # the map emits through generic calls: the general plane runs
             # this engine from now on (this iteration is restarted there)
@@ -372,9 +450,10 @@ class ListPlane:
         if self._after_issue is not None:  # (a map that raised before issuing everything)
             self._after_issue()
             self._after_issue = None
+        eng._maybe_inject_fault("shuffle")
         T["map"] = time.time() - t0
         t1 = time.time()
-        vocab = self.vocab
+        vocab = self._restored[0] if self._restored is not None else self.vocab
         src = self._src()
         R = eng.nparts
         W = eng.world
@@ -419,6 +498,8 @@ class ListPlane:
         """The key-byte source of the map's vocabulary: the staged arena
         (streamed on the CPU: the rounds' text)."""
         eng = self.eng
+        if self._restored is not None:
+            return self._restored[1]
         if self._cpu_text is not None:
             return self._cpu_text
         return eng.arena if eng.arena is not None else torch.zeros(1, dtype=torch.uint8, device=eng.device)
