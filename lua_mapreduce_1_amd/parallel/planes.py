@@ -328,7 +328,8 @@ class ListPlane:
         .npz: the posting keys ``id << doc_bits | line``, the words their ids
         name with their key bytes, the line numbering), so a relaunch after a
         failure later in the iteration restores them instead of re-mapping
-        the rank's splits."""
+        the rank's splits (the reference keeps map outputs until the reduce
+        consumes them: job.lua:293, server.lua:475-481)."""
         eng = self.eng
         path = eng._map_ckpt_path()
         if path is None:
