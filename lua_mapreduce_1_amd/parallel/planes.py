@@ -364,6 +364,10 @@ class ListPlane:
         if path is None or not os.path.exists(path):
             return None
         with np.load(path, allow_pickle=False) as z:
+            if "meta" not in z.files:
+                # another plane's map output: this map emits through generic
+                # calls, so it moves to the general plane, which restores it
+                return None
             a = {k: z[k] for k in z.files}
         id_bits, self.doc_bits, self.line_base, streamed = (int(x) for x in a["meta"])
         self.streamed = bool(streamed)
