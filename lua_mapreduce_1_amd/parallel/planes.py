@@ -555,13 +555,18 @@ class ListPlane:
         return vhi[wid2], vlo[wid2], vrep[wid2], rblob, wstart2, docs2, failed_total
 
     def _order(self, hi, lo, rep, src, wstart, docs, R: int) -> dict:
-        """Words in (partition, key) order with their posting lists: key
-        partition = exact FNV-1 mod R, one 3-word radix sort of the words, a
-        segmented gather of the lists; key bytes materialised."""
+        """Words in (partition, exact key bytes) order with their posting
+        lists: key partition = exact FNV-1 mod R, the words sorted by
+        ops.exact_key_perm (long words sharing a prefix placed by their bytes,
+        not their hash), a segmented gather of the lists; key bytes
+        materialised."""
         nw = hi.numel()
         part, klen = ops.key_meta(hi, lo, rep, src, nparts=R)
         if nw:
-            perm = ops.sort_keys_checked([part.to(torch.int64), hi, lo], bits=[max(8, _bits(R)), 64, 64]).long()
+            perm = ops.exact_key_perm(part, hi, lo, rep, src, R, klen=klen)
+            if perm is None:  # a word past the exact sort's length limit: the host fix-up orders it
+                perm = ops.sort_keys_checked([part.to(torch.int64), hi, lo], bits=[max(8, _bits(R)), 64, 64])
+            perm = perm.long()
         else:
             perm = torch.zeros(0, dtype=torch.int64, device=hi.device)
         hi, lo, rep, part, klen = hi[perm], lo[perm], rep[perm], part[perm], klen[perm]

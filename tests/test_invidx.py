@@ -359,3 +359,40 @@ def test_list_restart_restores_postings_gpu(gpu, tmp_path):
         assert p.exitcode == want_code, p.exitcode
     restored, ok = q.get(timeout=5)
     assert restored == 1 and ok
+
+
+def _device_order_ok(res, R):
+    """res.device (the list plane's device result) holds every partition's
+    words in exact bytewise order, long words sharing a prefix included."""
+    out = res.device
+    koff = out["key_off"].cpu().numpy()
+    blob = out["key_blob"].cpu().numpy().tobytes()
+    counts = out["counts_host"]
+    a = 0
+    for c in counts:
+        keys = [blob[koff[i]:koff[i + 1]] for i in range(a, a + c)]
+        if keys != sorted(keys):
+            return False
+        a += c
+    return a == len(koff) - 1
+
+
+def _long_prefix_splits():
+    import numpy as np
+    rng = np.random.default_rng(5)
+    words = [b"sharedprefix_" + bytes(rng.integers(97, 123, size=int(rng.integers(1, 12))).astype(np.uint8))
+             for _ in range(400)] + [b"sharedprefix_", b"short", b"a"]
+    lines = [b" ".join(words[int(i)] for i in rng.integers(0, len(words), size=12)) for _ in range(3000)]
+    return [b"\n".join(lines[i:i + 500]) + b"\n" for i in range(0, 3000, 500)]
+
+
+@pytest.mark.parametrize("on_gpu", [False, pytest.param(True, marks=pytest.mark.gpu)])
+def test_device_result_in_exact_key_order(request, on_gpu):
+    dev = request.getfixturevalue("gpu") if on_gpu else "cpu"
+    splits = _long_prefix_splits()
+    eng = _engine(splits, dev, nred=3, **({"table_capacity": 1 << 16} if on_gpu else {}))
+    res = eng.run_iteration()
+    assert _device_order_ok(res, 3)
+    from lua_mapreduce_1_amd.runtime import codec
+    got = {k: v for _n, c in eng.gather_results(res) for k, v in codec.iter_columnar(c)}
+    assert got == _naive(splits)
