@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(256) rec_gather_kernel(const u32* __restrict__
 // (rec_gather_kernel) issues 4x the vector-memory instructions for the same
 // bytes; the windowed-permutation probe (profiles/r3/check1/ts_move.log: 8 MB
 // windows no faster than random rows) says instructions, not DRAM, bound it.
-template <int C, int R>
+template <int C, int R, bool PIPE>
 __global__ void __launch_bounds__(256) rec_gather16_kernel(const u8* __restrict__ in, u64 nin,
                                                            const u32* __restrict__ perm, u64 n, u32 rb,
                                                            u8* __restrict__ out) {
@@ -290,17 +290,22 @@ __global__ void __launch_bounds__(256) rec_gather16_kernel(const u8* __restrict_
   const u64 nbatch = (n + R - 1) / R;
   const float inv_rb = 1.0f / (float)rb;
   const u32* img32 = reinterpret_cast<const u32*>(img);
-  for (u64 b = blockIdx.x; b < nbatch; b += gridDim.x) {
-    const u64 r0 = b * (u64)R;
-    const u32 rows = (u32)min((u64)R, n - r0);
-    v4u v[PER];
+  // PIPE: the next batch's row loads are issued before this batch's stores
+  // (its offsets kept in registers until the LDS image is free), so a block
+  // keeps loads in flight through its store phase
+  v4u v[PER];
+  u32 mv[PER];
+  auto load = [&](u64 bb) {
+    const u64 q0 = bb * (u64)R;
+    const u32 qrows = (u32)min((u64)R, n - q0);
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const u32 idx = t + 256u * k;
       const u32 row = idx / C, c = idx - row * C;
       v[k] = v4u{0u, 0u, 0u, 0u};
-      if (idx < (u32)(R * C) && row < rows) {
-        const u64 sb = (u64)clamp_row(perm[r0 + row], nin) * rb;
+      mv[k] = 0xFFFFFFFFu;
+      if (idx < (u32)(R * C) && row < qrows) {
+        const u64 sb = (u64)clamp_row(perm[q0 + row], nin) * rb;
         const u64 a = (sb & ~15ull) + 16ull * c;
         if (a + 16 <= in_bytes) {
           v[k] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + a));
@@ -309,15 +314,23 @@ __global__ void __launch_bounds__(256) rec_gather16_kernel(const u8* __restrict_
           for (int j = 0; j < 4; ++j)
             if (a + 4 * j < in_bytes) v[k][j] = *reinterpret_cast<const u32*>(in + a + 4 * j);
         }
-        if (c == 0) mis[row] = (u32)(sb & 15);
+        if (c == 0) mv[k] = (u32)(sb & 15);
       }
     }
+  };
+  if (PIPE && (u64)blockIdx.x < nbatch) load(blockIdx.x);
+  for (u64 b = blockIdx.x; b < nbatch; b += gridDim.x) {
+    const u64 r0 = b * (u64)R;
+    const u32 rows = (u32)min((u64)R, n - r0);
+    if (!PIPE) load(b);
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const u32 idx = t + 256u * k;
       if (idx < (u32)(R * C)) img[idx] = v[k];
+      if (mv[k] != 0xFFFFFFFFu) mis[idx / C] = mv[k];
     }
     __syncthreads();
+    if (PIPE && b + gridDim.x < nbatch) load(b + gridDim.x);
     const u32 obytes = rows * rb;  // < 2^16 for R <= 256, rb <= 244
     u8* ob = out + r0 * rb;
     const u32 nch = obytes >> 4;
@@ -389,13 +402,23 @@ static inline unsigned rc_grid(u64 n, unsigned cap = 8192) {
   return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
-template <int C>
-static void launch_gather16(const void* in, u64 nin, const void* perm, u64 n, int rb, void* out, hipStream_t s) {
+template <int C, bool PIPE>
+static void launch_gather16_t(const void* in, u64 nin, const void* perm, u64 n, int rb, void* out, hipStream_t s) {
   constexpr int R = C <= 8 ? 256 : 128;
   const u64 nb = (n + R - 1) / R;
   const unsigned g = (unsigned)(nb < 65536 ? nb : 65536);
-  hipLaunchKernelGGL((rc::rec_gather16_kernel<C, R>), dim3(g), dim3(256), 0, s, (const u8*)in, nin, (const u32*)perm,
-                     n, (u32)rb, (u8*)out);
+  hipLaunchKernelGGL((rc::rec_gather16_kernel<C, R, PIPE>), dim3(g), dim3(256), 0, s, (const u8*)in, nin,
+                     (const u32*)perm, n, (u32)rb, (u8*)out);
+}
+
+static bool g_gather_pipe = true;  // mr_rec_gather mode 2 forces the unpipelined form (A/B)
+
+template <int C>
+static void launch_gather16(const void* in, u64 nin, const void* perm, u64 n, int rb, void* out, hipStream_t s) {
+  if (g_gather_pipe)
+    launch_gather16_t<C, true>(in, nin, perm, n, rb, out, s);
+  else
+    launch_gather16_t<C, false>(in, nin, perm, n, rb, out, s);
 }
 
 extern "C" {
@@ -457,6 +480,8 @@ int mr_rec_gather(const void* in, u64 nin, const void* perm, u64 n, int rb, void
     return (int)hipGetLastError();
   }
   const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+  g_gather_pipe = mode != 2;
+  if (mode == 2) mode = 0;
   if (mode == 0 && aligned && rb >= 16 && rb <= 244) {
     switch ((rb + 27) / 16) {
       case 2: launch_gather16<2>(in, nin, perm, n, rb, out, s); break;
