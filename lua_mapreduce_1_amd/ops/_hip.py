@@ -110,6 +110,7 @@ _SIGS = {
     "mr_rec_tie_ws_words": [_u64, _u64],
     "mr_exact_hash": [_p, _p, _p, _p, _u64, _p, _p],
     "mr_exact_fix": [_p, _p, _u64, _p, _p, _p, _p, _p, _p, _p, _p],
+    "mr_seg_reduce": [_p, _u64, _p, _u64, _i32, _i32, _p, _p],
 }
 _RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
                 "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words"}

@@ -52,6 +52,7 @@ import torch
 from .. import ops, utils
 from ..ops import agg as A
 from ..ops import keys as K
+from ..ops import segments as S
 from ..ops import text as TX
 from ..runtime import codec
 from ..runtime import device as devmod
@@ -60,6 +61,7 @@ from ..utils import STATUS
 from ..utils import trace
 from ..utils.config import TUNABLES
 from . import dist as D
+from . import reducers as RD
 
 
 def _bits(n: int) -> int:
@@ -219,7 +221,8 @@ class GenericMap:
     """Map-side state of the general plane: the key -> columns / postings
     table, the byte source of its rep words and the emitter."""
 
-    def __init__(self, device, capacity: int, phys: A.Physical | None, list_dtype: str = "i64"):
+    def __init__(self, device, capacity: int, phys: A.Physical | None, list_dtype: str = "i64",
+                 reducers: "RD.ListReducers | None" = None, combine_at: int = 0):
         self.device = torch.device(device)
         self.phys = phys
         self.list_dtype = list_dtype
@@ -228,6 +231,12 @@ class GenericMap:
         self.emit = GenericEmitter(self)
         self.host: list = []
         self.rows = 0
+        # list mode with a combiner: the table's postings are combined
+        # whenever they pass combine_at (the batched MAX_MAP_RESULT,
+        # job.lua:92-96) and once more at the end of the map (job.lua:198-202)
+        self.reducers = reducers if (reducers is not None and reducers.has_combiner and phys is None) else None
+        self.combine_at = int(combine_at or TUNABLES.combine_postings)
+        self.combines = 0
 
     @property
     def n_in(self) -> int:
@@ -249,6 +258,36 @@ class GenericMap:
         self.table.src = self.src.source()
         self.table.insert(n, list(values), **kw)
         self.rows += n
+        if self.reducers is not None and self.table.npost >= self.combine_at:
+            self.combine()
+
+    def combine(self) -> bool:
+        """Run the reduce module's combiner over every key's list and rebuild
+        the table from the combined postings (same capacity, same key
+        source).  False (nothing done) when the table overflowed: the map is
+        re-run with a larger one anyway."""
+        t = self.table
+        if self.reducers is None or t.npost == 0:
+            return False
+        m, ovf = t.stats()
+        if ovf or m > t.cap // 2 + 1:
+            return False
+        slot, hi, lo, rep, pslot, pval = t.postings()
+        m = int(hi.numel())
+        space = t.cap if t.is_cuda else max(1, m)
+        src = self.src.source()
+        off, val = RD.lists_of_postings(slot, pslot, pval, m, space)
+        noff, nval = self.reducers.combine(RD.KeyBatch(hi, lo, rep, src), off, val)
+        nt = A.AggTable(t.cap, self.device, None, self.list_dtype)
+        nt.src = src
+        n = int(nval.numel())
+        if n:
+            kid = S.ids(noff, n)
+            v = nval.view(torch.float64) if self.list_dtype == "f64" else nval
+            nt.insert(n, [v], hi=hi[kid], lo=lo[kid], rep=rep[kid])
+        self.table = nt
+        self.combines += 1
+        return True
 
     def flush_host(self) -> None:
         if not self.host:
@@ -292,15 +331,28 @@ def order_fold(slot, hi, lo, rep, cols, src, nparts: int, partmod, phys: A.Physi
     m = hi.numel()
     d = hi.device
     part = devmod.partition_of(hi, lo, rep, src, nparts, partmod) if m else torch.zeros(0, dtype=torch.int32, device=d)
+    exact = True
     if m:
-        perm = ops.sort_keys_checked([part.to(torch.int64), hi, lo], bits=[max(8, _bits(nparts)), 64, 64]).long()
+        perm, exact = _key_order(part, hi, lo, rep, src, nparts)
         hi, lo, rep, part = hi[perm], lo[perm], rep[perm], part[perm]
         cols = [c[perm] for c in cols]
     _, klen = ops.key_meta(hi, lo, rep, src, want_part=False)
     koff, kblob = ops.gather_key_bytes(hi, lo, rep, src, lengths=klen)
     counts = ops.bincount(part, nparts) if m else torch.zeros(nparts, dtype=torch.int64, device=d)
     return {"hi": hi, "lo": lo, "key_off": koff, "key_blob": kblob, "cols": phys.outputs(cols) if outputs else cols,
-            "counts": counts}
+            "counts": counts, "exact": exact}
+
+
+def _key_order(part, hi, lo, rep, src, nparts: int):
+    """(permutation into (partition, exact key bytes) order, True) on the
+    device (ops.exact_key_perm: long keys sharing a prefix are placed by
+    their bytes, not their hash) — or, for a key past the exact sort's length
+    limit, the (partition, hi, lo) order and False (host_partitions then
+    fixes the order of long keys sharing an 8-byte prefix)."""
+    perm = ops.exact_key_perm(part, hi, lo, rep, src, nparts) if src is not None else None
+    if perm is not None:
+        return perm.long(), True
+    return ops.sort_keys_checked([part.to(torch.int64), hi, lo], bits=[max(8, _bits(nparts)), 64, 64]).long(), False
 
 
 def order_lists(slot, hi, lo, rep, pslot, pval, src, nparts: int, partmod, unique: bool, dtype: str,
@@ -311,8 +363,9 @@ def order_lists(slot, hi, lo, rep, pslot, pval, src, nparts: int, partmod, uniqu
     m = hi.numel()
     d = hi.device
     part = devmod.partition_of(hi, lo, rep, src, nparts, partmod) if m else torch.zeros(0, dtype=torch.int32, device=d)
+    exact = True
     if m:
-        perm = ops.sort_keys_checked([part.to(torch.int64), hi, lo], bits=[max(8, _bits(nparts)), 64, 64]).long()
+        perm, exact = _key_order(part, hi, lo, rep, src, nparts)
         hi, lo, rep, part, slot = hi[perm], lo[perm], rep[perm], part[perm], slot[perm]
     rank = torch.full((max(slot_space, 1),), -1, dtype=torch.int64, device=d)
     rank[slot] = torch.arange(m, dtype=torch.int64, device=d)
@@ -338,7 +391,7 @@ def order_lists(slot, hi, lo, rep, pslot, pval, src, nparts: int, partmod, uniqu
     koff, kblob = ops.gather_key_bytes(hi, lo, rep, src, lengths=klen)
     counts = ops.bincount(part, nparts) if m else torch.zeros(nparts, dtype=torch.int64, device=d)
     return {"hi": hi, "lo": lo, "key_off": koff, "key_blob": kblob, "list_off": loff, "list_val": pv,
-            "counts": counts}
+            "counts": counts, "exact": exact}
 
 
 def _np64(t):
@@ -365,15 +418,16 @@ def host_partitions(out: dict, nparts: int, dtype: str = "i64", reducefn=None, a
     if is_list:
         loff = _np64(out["list_off"]).astype(np.int64)
         lval = _np64(out["list_val"])
-        if dtype == "f64":
+        if dtype == "f64" and not out.get("list_typed"):
             lval = lval.view(np.float64)
     parts = {}
     kb = kblob.tobytes()
+    exact = bool(out.get("exact", False))
     for p in range(nparts):
         a, b = int(bounds[p]), int(bounds[p + 1])
         if b <= a:
             continue
-        fix = devmod.fix_long_key_order(hi[a:b], lo[a:b], koff[a:b + 1], kblob) if b - a > 1 else None
+        fix = devmod.fix_long_key_order(hi[a:b], lo[a:b], koff[a:b + 1], kblob) if b - a > 1 and not exact else None
         idx = np.arange(a, b) if fix is None else fix + a
         if fix is None:
             k_off = koff[a:b + 1] - koff[a]
@@ -394,22 +448,33 @@ def host_partitions(out: dict, nparts: int, dtype: str = "i64", reducefn=None, a
                 l_val = np.concatenate([lval[loff[i]:loff[i + 1]] for i in idx]) if idx.size else lval[:0]
             part.update(list_off=l_off, list_val=l_val, val=ln)
             if reducefn is not None:
-                pyv = []
-                for i in range(idx.size):
-                    key = codec.key_str(k_blob[k_off[i]:k_off[i + 1]].tobytes())
-                    values = l_val[l_off[i]:l_off[i + 1]].tolist()
-                    if aci and len(values) == 1:
-                        pyv.append(values)
-                        continue
-                    o: list = []
-                    reducefn(key, values, o.append)
-                    pyv.append(o)
-                part["py_vals"] = pyv
+                part["py_vals"] = _host_reduce(reducefn, aci, k_off, k_blob, l_off, l_val)
         else:
             part["cols"] = [c[idx] for c in cols]
             part["val"] = part["cols"][0]
         parts[p] = part
     return parts
+
+
+def _host_reduce(reducefn, aci: bool, k_off, k_blob, l_off, l_val) -> list:
+    """The last resort: the user's reducefn per key over downloaded lists
+    (job.lua:264-284; singleton lists skip it under the three ACI flags).
+    One host conversion of the partition's values and key bytes, then a
+    slice per key."""
+    vals = l_val.tolist()
+    kb = k_blob.tobytes()
+    ko = k_off.tolist()
+    lo = l_off.tolist()
+    out = []
+    for i in range(len(ko) - 1):
+        values = vals[lo[i]:lo[i + 1]]
+        if aci and len(values) == 1:
+            out.append(values)
+            continue
+        o: list = []
+        reducefn(codec.key_str(kb[ko[i]:ko[i + 1]]), values, o.append)
+        out.append(o)
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -429,15 +494,16 @@ class GenericPlane:
             raise ValueError("device_value_dtype is 'i64' or 'f64'")
         self.phys = None if self.list_mode else A.Physical(A.parse_spec(op))
         self._cap = self._cap0 = int(eng.params.get("table_capacity") or 1 << 16)
-        self.map = GenericMap(eng.device, self._cap, self.phys, self.dtype)
+        red = eng.redmod
+        # no device_reduce: the module's own combiner / reducer over the
+        # device-grouped lists (batched device hooks, or per key on the host)
+        self.reducers = RD.ListReducers(red, self.dtype) if self.host_reduce else None
+        self.reducefn = self.reducers.reducefn if self.host_reduce else None
+        self.aci = self.reducers.aci if self.host_reduce else False
+        self.map = GenericMap(eng.device, self._cap, self.phys, self.dtype, self.reducers,
+                              int(eng.params.get("combine_postings") or 0))
         self.red = None
         self._lines = None
-        red = eng.redmod
-        self.reducefn = modules.field(red, "reducefn") if self.host_reduce else None
-        if self.host_reduce and self.reducefn is None:
-            raise ValueError("a reduce module without device_reduce needs a reducefn")
-        self.aci = all(bool(modules.field(red, f)) for f in
-                       ("associative_reducer", "commutative_reducer", "idempotent_reducer"))
 
     # -- global line numbering (word_lines) ---------------------------------------
     def _line_base(self):
@@ -689,6 +755,7 @@ class GenericPlane:
         if extra is not None:
             rextra = D.all_to_all_v(extra, [c[2] for c in send_c], [c[2] for c in recv_c], eng.group)
         sent = [32 * c[0] + c[1] + 8 * c[2] for c in send_c]
+        self._nvals_shipped = sum(c[2] for c in send_c) if self.list_mode else sum(c[0] for c in send_c)
         self._shuffled = (sum(sent), sum(sent) - sent[eng.rank])
         rhi, rlo, rlen = rrecs[:, 0].contiguous(), rrecs[:, 1].contiguous(), rrecs[:, 2].contiguous()
         roff, _ = ops.exclusive_scan(rlen)
@@ -756,6 +823,7 @@ class GenericPlane:
         with trace.range("mr.gen.map"):
             if not self._restore_map(recs, j0, j1):
                 self._map(jobs, recs, j0, j1)
+                self.map.combine()  # the end-of-map combiner (job.lua:198-202); no-op without one
                 self._save_map()
         eng._maybe_inject_fault("shuffle")
         T["map"] = time.time() - t0
@@ -771,6 +839,8 @@ class GenericPlane:
             keys = mp.table.compact()
             space = None
         self._shuffled = (0, 0)
+        self._nvals_shipped = 0
+        res.distinct_keys_map = int(keys[1].numel())
         if W > 1 or eng.force_shuffle:
             with trace.range("mr.gen.shuffle"):
                 rhi, rlo, rrep, rpay, rextra, rblob, failed = self._shuffle(keys, src, failed)
@@ -790,7 +860,16 @@ class GenericPlane:
         res.total_value = mp.rows
         res.failed_maps = failed
         res.bytes_shuffled, res.bytes_shuffled_remote = self._shuffled
-        if self.host_reduce:
+        if self.host_reduce and self.reducers.device_reduce:
+            # the reduce jobs, batched: device_reducefn over every key's list
+            with trace.range("mr.gen.reduce"):
+                keys = RD.KeyBatch(out["hi"], out["lo"], key_off=out["key_off"], key_blob=out["key_blob"])
+                red = self.reducers.reduce_device(keys, out["list_off"], out["list_val"])
+            out = {k: v for k, v in out.items() if k not in ("list_off", "list_val")}
+            out.update(red)
+            res.device = out
+            res._materialize = lambda o=out: host_partitions(o, R, self.dtype)
+        elif self.host_reduce:
             # the reduce jobs: the user's reducefn over each key's list
             c0 = time.process_time()
             parts = host_partitions(out, R, self.dtype, self.reducefn, self.aci)

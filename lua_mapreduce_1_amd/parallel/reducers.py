@@ -1,0 +1,309 @@
+"""The reduce module's combiner and reducer over value lists grouped on the
+device — batched on the GPU when the module says how, per key on the host
+otherwise.
+
+Reference contract (/root/reference/mapreduce/job.lua:83-112,198-202,264-284,
+task.lua:325): the combiner is the *reduce* module's ``combinerfn``; it runs
+map-side on a key's value list whenever the list passes ``MAX_MAP_RESULT``
+values and once more per key (with more than one value) at the end of the
+map, and its emitted values replace the list; the reducer then runs per key
+over the merged lists (skipping singleton lists when the module declares the
+three ACI flags).  The general device plane (parallel/generic.py) groups a
+rank's values per key in HBM, so here both run over ALL of a rank's lists at
+once, in CSR form (``off`` [m + 1], ``val`` [n]):
+
+* ``device_combinerfn(keys, off, val)`` / ``device_reducefn(keys, off, val)``
+  — batched torch code (ops/segments.py has the segmented folds, sorts,
+  top-k and quantiles); ``keys`` is a :class:`KeyBatch`, ``val`` int64 or
+  float64 (the map module's ``device_value_dtype``).  The return value is
+  one value per key (a tensor [m]), several (a tuple of tensors [m], or a
+  tensor [m, k]) or a variable number (:class:`ValueLists`).  A module whose
+  ``combinerfn`` IS its ``reducefn`` (WordCount's reducefn2) uses
+  ``device_reducefn`` as its device combiner too;
+* otherwise the host ``combinerfn`` / ``reducefn`` run per key over the
+  downloaded lists (the last resort: Python per key).
+
+The map-side combine keeps a rank's postings bounded
+(:data:`~lua_mapreduce_1_amd.utils.config.Tunables.combine_postings`, the
+batched form of ``MAX_MAP_RESULT``) and is applied once more before the
+shuffle, so a key ships at most its combined values from each rank.
+"""
+from __future__ import annotations
+
+from typing import NamedTuple
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..ops import segments as S
+from ..runtime import codec, modules
+
+
+class ValueLists(NamedTuple):
+    """A batched reducer's variable-length output: key i emits
+    ``val[off[i]:off[i + 1]]``."""
+    off: torch.Tensor
+    val: torch.Tensor
+
+
+class KeyBatch:
+    """The keys of a batch of value lists: their 128-bit words (``hi``,
+    ``lo``, ops/keys.py) and — materialised on first use — their bytes as a
+    CSR pair (``key_off`` [m + 1], ``key_blob``)."""
+
+    def __init__(self, hi, lo, rep=None, src=None, key_off=None, key_blob=None):
+        self.hi, self.lo, self._rep, self._src = hi, lo, rep, src
+        self._off, self._blob = key_off, key_blob
+
+    def __len__(self) -> int:
+        return int(self.hi.numel())
+
+    @property
+    def device(self):
+        return self.hi.device
+
+    def _materialize(self) -> None:
+        if self._off is None:
+            _, ln = ops.key_meta(self.hi, self.lo, self._rep, self._src, want_part=False)
+            self._off, self._blob = ops.gather_key_bytes(self.hi, self.lo, self._rep, self._src, lengths=ln)
+
+    @property
+    def key_off(self) -> torch.Tensor:
+        self._materialize()
+        return self._off
+
+    @property
+    def key_blob(self) -> torch.Tensor:
+        self._materialize()
+        return self._blob
+
+    def strings(self) -> list[str]:
+        """The keys as Python strings (host copy)."""
+        off = self.key_off.cpu().numpy()
+        blob = self.key_blob.cpu().numpy().tobytes()
+        return [codec.key_str(blob[off[i]:off[i + 1]]) for i in range(len(self))]
+
+
+# ---------------------------------------------------------------------------
+def lists_of_postings(slot, pslot, pval, m: int, space: int):
+    """A table's postings (key slot, value; emission order) -> the keys' value
+    lists in CSR form, key i = the i-th entry of ``slot`` (emission order
+    inside a list): (off [m + 1], val)."""
+    d = slot.device
+    if m == 0:
+        return torch.zeros(1, dtype=torch.int64, device=d), pval[:0]
+    pos = torch.full((max(space, 1),), -1, dtype=torch.int64, device=d)
+    pos[slot] = torch.arange(m, dtype=torch.int64, device=d)
+    pr = pos[pslot.clamp(min=0)]
+    ok = (pslot >= 0) & (pr >= 0)
+    pr, pv = pr[ok], pval[ok]
+    if pr.numel():
+        pp = ops.sort_keys_checked([pr], bits=[max(1, int(m - 1).bit_length())]).long()  # stable
+        pr, pv = pr[pp], pv[pp]
+    nv = torch.bincount(pr, minlength=m)[:m]
+    return S.from_lengths(nv), pv
+
+
+def splice(off, val, noff, nval, keep_old):
+    """Per key: the old list where ``keep_old`` else the new one -> (off, val)."""
+    d = off.device
+    lo_, ln = S.lengths(off), S.lengths(noff)
+    lens = torch.where(keep_old, lo_, ln)
+    roff = S.from_lengths(lens)
+    total = int(roff[-1]) if lens.numel() else 0
+    if total == 0:
+        return roff, val[:0]
+    seg = S.ids(roff, total)
+    j = torch.arange(total, dtype=torch.int64, device=d) - roff[seg]
+    old = keep_old[seg]
+    a = val[(off[seg] + j).clamp(max=max(val.numel() - 1, 0))] if val.numel() else torch.zeros_like(j)
+    b = nval[(noff[seg] + j).clamp(max=max(nval.numel() - 1, 0))] if nval.numel() else torch.zeros_like(j)
+    return roff, torch.where(old, a, b)
+
+
+def _typed(bits: torch.Tensor, dtype: str) -> torch.Tensor:
+    return bits.view(torch.float64) if dtype == "f64" else bits
+
+
+def _bits(t: torch.Tensor) -> torch.Tensor:
+    return t.view(torch.int64) if t.dtype == torch.float64 else t
+
+
+def _to_list_dtype(v: torch.Tensor, dtype: str, who: str) -> torch.Tensor:
+    """A combiner's values in the list dtype (int64 bits of the i64 / f64
+    values the lists hold)."""
+    if dtype == "f64":
+        return v.to(torch.float64).contiguous()
+    if v.is_floating_point():
+        r = v.round()
+        if v.numel() and not bool(torch.equal(r, v)):
+            raise TypeError(f"{who} emitted non-integral values into int64 value lists (declare "
+                            "device_value_dtype = 'f64' on the map module)")
+        v = r
+    return v.to(torch.int64).contiguous()
+
+
+def as_lists(out, m: int, who: str):
+    """A batched reducer's return value -> (off, val) CSR."""
+    d = None
+    if isinstance(out, ValueLists) or (isinstance(out, dict) and "off" in out):
+        off, val = (out.off, out.val) if isinstance(out, ValueLists) else (out["off"], out["val"])
+        if off.numel() != m + 1:
+            raise ValueError(f"{who}: {off.numel()} list offsets for {m} keys (want m + 1)")
+        return off.to(torch.int64), val
+    if isinstance(out, torch.Tensor):
+        if out.dim() == 1:
+            out = out.reshape(m, 1) if out.numel() == m else None
+        elif out.dim() != 2 or out.shape[0] != m:
+            out = None
+        if out is None:
+            raise ValueError(f"{who}: a tensor result needs one row per key ({m})")
+        cols = out
+    elif isinstance(out, (tuple, list)) and out and all(isinstance(c, torch.Tensor) for c in out):
+        if any(c.numel() != m for c in out):
+            raise ValueError(f"{who}: every returned column needs one value per key ({m})")
+        dt = torch.float64 if any(c.is_floating_point() for c in out) else torch.int64
+        cols = torch.stack([c.reshape(-1).to(dt) for c in out], 1)
+    else:
+        raise TypeError(f"{who} must return a tensor [m], a tuple of tensors [m], a tensor [m, k] or "
+                        f"ValueLists(off, val) (got {type(out).__name__})")
+    d = cols.device
+    k = cols.shape[1]
+    off = torch.arange(m + 1, dtype=torch.int64, device=d) * k
+    return off, cols.reshape(-1)
+
+
+# ---------------------------------------------------------------------------
+class ListReducers:
+    """The combiner / reducer of a reduce module without ``device_reduce``,
+    for value lists of ``dtype`` (``"i64"`` | ``"f64"``)."""
+
+    def __init__(self, redmod, dtype: str = "i64"):
+        f = modules.field
+        self.dtype = dtype
+        self.reducefn = f(redmod, "reducefn")
+        self.combinerfn = f(redmod, "combinerfn")
+        self.device_reducefn = f(redmod, "device_reducefn")
+        dc = f(redmod, "device_combinerfn")
+        if dc is None and self.device_reducefn is not None and self.combinerfn is not None \
+                and self.combinerfn is self.reducefn:
+            dc = self.device_reducefn  # the combiner is the reducer: so is its batched form
+        self.device_combinerfn = dc
+        if self.reducefn is None and self.device_reducefn is None:
+            raise ValueError("a reduce module without device_reduce needs a reducefn (or a device_reducefn)")
+        self.aci = all(bool(f(redmod, x)) for x in ("associative_reducer", "commutative_reducer",
+                                                    "idempotent_reducer"))
+
+    @property
+    def has_combiner(self) -> bool:
+        return self.combinerfn is not None or self.device_combinerfn is not None
+
+    @property
+    def device_reduce(self) -> bool:
+        return self.device_reducefn is not None
+
+    # -- the combiner (map side) ---------------------------------------------
+    def combine(self, keys: KeyBatch, off: torch.Tensor, val: torch.Tensor):
+        """Every key's list with more than one value -> the combiner's values
+        (job.lua:198-202); singleton lists are kept.  ``val``: int64 bits of
+        the lists' values.  Returns (off, val) in the same form."""
+        m = off.numel() - 1
+        multi = S.lengths(off) > 1
+        if m == 0:
+            return off, val
+        if self.device_combinerfn is not None:
+            out = self.device_combinerfn(keys, off, _typed(val, self.dtype))
+            noff, nval = as_lists(out, m, "device_combinerfn")
+            nval = _bits(_to_list_dtype(nval, self.dtype, "device_combinerfn"))
+            return splice(off, val, noff, nval, ~multi)
+        return self._host_lists(self.combinerfn, keys, off, val, multi, "combinerfn")
+
+    def _host_lists(self, fn, keys: KeyBatch, off, val, sel, who: str):
+        """Per selected key on the host: fn(key, values, emit) replaces the
+        list (the reference's per-key call)."""
+        d = off.device
+        o = off.cpu().numpy()
+        v = _typed(val, self.dtype).cpu().numpy()
+        pick = np.flatnonzero(sel.cpu().numpy())
+        if pick.size == 0:
+            return off, val
+        names = keys.strings()
+        lens = np.diff(o)
+        outs = []
+        for i in pick:
+            acc: list = []
+            fn(names[i], v[o[i]:o[i + 1]].tolist(), acc.append)
+            outs.append(acc)
+        new_lens = lens.copy()
+        new_lens[pick] = [len(a) for a in outs]
+        flat = [x for a in outs for x in a]
+        npdt = np.float64 if self.dtype == "f64" else np.int64
+        try:
+            arr = np.asarray(flat, dtype=np.float64 if self.dtype == "f64" else None)
+        except (TypeError, ValueError) as e:
+            raise TypeError(f"{who} emitted values that are not numbers: {e}") from None
+        if arr.size and arr.dtype != npdt:
+            if self.dtype == "i64" and arr.dtype.kind == "f" and np.all(np.floor(arr) == arr):
+                arr = arr.astype(np.int64)
+            elif self.dtype == "i64" and arr.dtype.kind in "iub":
+                arr = arr.astype(np.int64)
+            else:
+                raise TypeError(f"{who} emitted {arr.dtype} values into {self.dtype} value lists (declare "
+                                "device_value_dtype = 'f64' on the map module for real values)")
+        arr = arr.astype(npdt, copy=False)
+        noff = np.zeros(lens.size + 1, np.int64)
+        np.cumsum(new_lens, out=noff[1:])
+        res = np.empty(int(noff[-1]), npdt)
+        keep = np.ones(lens.size, bool)
+        keep[pick] = False
+        ki = np.flatnonzero(keep & (lens > 0))
+        if ki.size:
+            src_idx = np.repeat(o[:-1][ki], lens[ki]) + _ranks(lens[ki])
+            dst_idx = np.repeat(noff[:-1][ki], lens[ki]) + _ranks(lens[ki])
+            res[dst_idx] = v[src_idx]
+        if pick.size and arr.size:
+            nl = new_lens[pick]
+            dst_idx = np.repeat(noff[:-1][pick], nl) + _ranks(nl)
+            res[dst_idx] = arr
+        t = torch.from_numpy(res).to(d)
+        return torch.from_numpy(noff).to(d), _bits(t)
+
+    # -- the reducer (reduce side) ---------------------------------------------
+    def reduce_device(self, keys: KeyBatch, off: torch.Tensor, val: torch.Tensor) -> dict:
+        """The batched reducer over every key's list -> result columns
+        ({"cols": [...]}) or lists ({"list_off", "list_val"}), on the device.
+        With the three ACI flags a singleton list is its own result
+        (job.lua:264-274) — applied to single-column and list results."""
+        m = off.numel() - 1
+        out = self.device_reducefn(keys, off, _typed(val, self.dtype))
+        single = S.lengths(off) == 1
+        if isinstance(out, ValueLists) or (isinstance(out, dict) and "off" in out):
+            noff, nval = as_lists(out, m, "device_reducefn")
+            if self.aci:
+                noff, nval = splice(off, _typed(val, self.dtype).to(nval.dtype), noff, nval, single)
+            return {"list_off": noff, "list_val": nval, "list_typed": True}
+        if isinstance(out, torch.Tensor) and out.dim() == 2:
+            cols = [out[:, j] for j in range(out.shape[1])]
+        elif isinstance(out, torch.Tensor):
+            cols = [out]
+        else:
+            as_lists(out, m, "device_reducefn")  # validates the shape / type
+            cols = list(out)
+        cols = [c.reshape(-1) for c in cols]
+        if any(c.numel() != m for c in cols):
+            raise ValueError(f"device_reducefn: every returned column needs one value per key ({m})")
+        if self.aci and len(cols) == 1 and m:
+            c = cols[0]
+            cols = [torch.where(single, S.first(off, _typed(val, self.dtype)).to(c.dtype), c)]
+        return {"cols": cols}
+
+
+def _ranks(lens: np.ndarray) -> np.ndarray:
+    """0, 1, .., lens[0]-1, 0, 1, .., lens[1]-1, ..."""
+    total = int(lens.sum())
+    if total == 0:
+        return np.zeros(0, np.int64)
+    starts = np.zeros(lens.size, np.int64)
+    np.cumsum(lens[:-1], out=starts[1:])
+    return np.arange(total, dtype=np.int64) - np.repeat(starts, lens)

@@ -264,8 +264,15 @@ class job:  # noqa: N801
         d = dev.default_device()
         cap = int(extra.get("table_capacity") or 1 << 16)
         fn = modules.field(self.module, "device_mapfn")
+        # no device_reduce: the reduce module's combiner runs over the job's
+        # device-grouped lists (batched, or per key on the host) before the
+        # partition files are written (job.lua:92-96,198-202)
+        reducers = None
+        if kind == "list" and spec is None and rmod is not None:
+            from ..parallel import reducers as RD
+            reducers = RD.ListReducers(rmod, dtype)
         for _ in range(8):
-            gm = G.GenericMap(d, cap, phys, dtype)
+            gm = G.GenericMap(d, cap, phys, dtype, reducers, int(extra.get("combine_postings") or 0))
             gm.begin(None)
             fn(map_key, map_value, gm.emit)
             gm.flush_host()
@@ -275,6 +282,9 @@ class job:  # noqa: N801
             cap = ops_next_pow2(4 * max(n, 1))
         else:
             raise OverflowError("device map table overflow")
+        gm.combine()
+        n = gm.table.stats()[0]
+        dev.STATS["maps_" + d.type] = dev.STATS.get("maps_" + d.type, 0) + 1
         self.mark_as_finished()
         src = gm.src.source()
         if kind == "cols":
@@ -356,6 +366,7 @@ class job:  # noqa: N801
         aci = all(bool(modules.field(self.module, f)) for f in
                   ("associative_reducer", "commutative_reducer", "idempotent_reducer"))
         dev_op = modules.field(self.module, "device_reduce")
+        dev_reducefn = modules.field(self.module, "device_reducefn") if dev_op is None else None
         part_key, value = self.get_pair()
 
         def run():
@@ -385,13 +396,20 @@ class job:  # noqa: N801
                 with dev.PLANE_LOCK:
                     b.append(_device_reduce_cols(blobs, dev_op) if cols_op else _device_reduce(blobs, dev_op))
             else:
-                recs = []
-                for k, v in utils.merge_iterator(fs, filenames, make_lines_iterator):
-                    if not aci or len(v) > 1:
-                        out = []
-                        g(k, v, out.append)
-                        v = [tuple_(x) for x in out]
-                    recs.append((k, v))
+                merged = utils.merge_iterator(fs, filenames, make_lines_iterator)
+                recs = None
+                if dev_reducefn is not None:
+                    merged = list(merged)
+                    with dev.PLANE_LOCK:
+                        recs = _device_reduce_lists(merged, self.module)
+                if recs is None:
+                    recs = []
+                    for k, v in merged:
+                        if not aci or len(v) > 1:
+                            out = []
+                            g(k, v, out.append)
+                            v = [tuple_(x) for x in out]
+                        recs.append((k, v))
                 b.append(codec.encode_records(recs))
             b.build(res_file)
             elapsed = _time.process_time() - clock1
@@ -490,6 +508,41 @@ def _device_reduce_cols(blobs: list[bytes], spec) -> bytes:
                                     [np.zeros(0, c.dtype) for c in G._np_cols(out)], np.zeros(1, np.int64),
                                     np.zeros(0, np.uint8))
     return codec.encode_columns(part["hi"], part["lo"], part["cols"], part["key_off"], part["key_blob"])
+
+
+def _device_reduce_lists(merged: list, rmod) -> list | None:
+    """A reduce job's merged (key, values) lists through the module's
+    batched ``device_reducefn`` (parallel/reducers.py) — None when a value
+    is not a number (the per-key host reducefn then runs)."""
+    from ..parallel import reducers as RD
+    from ..parallel.generic import host_partitions
+    if not merged:
+        return []
+    flat = [x for _, v in merged for x in v]
+    if not all(isinstance(x, (int, float)) and not isinstance(x, bool) for x in flat):
+        return None
+    isf = any(isinstance(x, float) for x in flat)
+    dtype = "f64" if isf else "i64"
+    d = dev.default_device()
+    lens = np.array([len(v) for _, v in merged], np.int64)
+    off = np.zeros(lens.size + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    val = torch.from_numpy(np.asarray(flat, np.float64 if isf else np.int64)).to(d)
+    kb = [k.encode("utf-8", "surrogateescape") if isinstance(k, str) else str(k).encode() for k, _ in merged]
+    koff = np.zeros(len(kb) + 1, np.int64)
+    np.cumsum([len(k) for k in kb], out=koff[1:])
+    blob = np.frombuffer(b"".join(kb), np.uint8) if koff[-1] else np.zeros(0, np.uint8)
+    keys = RD.KeyBatch(torch.zeros(len(kb), dtype=torch.int64, device=d),
+                       torch.zeros(len(kb), dtype=torch.int64, device=d),
+                       key_off=torch.from_numpy(koff).to(d), key_blob=torch.from_numpy(blob.copy()).to(d))
+    red = RD.ListReducers(rmod, dtype)
+    bits = val.view(torch.int64) if isf else val
+    out = red.reduce_device(keys, torch.from_numpy(off).to(d), bits)
+    out.update(hi=keys.hi, lo=keys.lo, key_off=keys.key_off, key_blob=keys.key_blob, exact=True,
+               counts=torch.tensor([len(kb)], dtype=torch.int64))
+    part = host_partitions(out, 1, dtype).get(0)
+    ks = [k for k, _ in merged]
+    return [(k, list(v)) for k, (_kk, v) in zip(ks, codec.iter_columnar(part))]
 
 
 def result_store(cnn, storage: str, path: str):

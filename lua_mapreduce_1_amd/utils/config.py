@@ -78,7 +78,10 @@ class Tunables:
     device_timing: bool = _knob("MR_DEVICE_TIMING", True,
                                 "SPMD: HIP events around every map chunk, the shuffle and the tail; job records "
                                 "and the stats block report device spans instead of host issue times")
-    numa_bind: bool = _knob("MR_NUMA_BIND", True, "pin each rank to the CPUs of its GPU's NUMA node")
+    combine_postings: int = _knob("MR_COMBINE_POSTINGS", 1 << 26,
+                                  "general plane, list mode with a combiner: a rank's map table runs the "
+                                  "reduce module's combiner over its value lists whenever it holds this many "
+                                  "postings (the batched MAX_MAP_RESULT of job.lua:92-96; bounds map memory)")
     # -- diagnostics
     debug_checks: bool = _knob("MR_DEBUG_CHECKS", False, "extra host-side consistency checks (slow)")
     roctx: bool = _knob("MR_ROCTX", False, "roctx ranges around every phase (rocprofv3 --marker-trace)")

@@ -1,0 +1,159 @@
+"""The reduce module's combiner and batched reducers on the general device
+plane (parallel/reducers.py, ops/segments.py) — reference contract:
+/root/reference/mapreduce/job.lua:92-96 (combine past MAX_MAP_RESULT),
+:198-202 (combine at the end of the map), :264-284 (reduce per key),
+task.lua:325 (the combiner comes from the reduce module).
+
+CPU tensors here (world size 1, forced shuffle, gloo W = 3); the GPU variants
+(incl. a hot key of > 10 M values) are in test_combiner_gpu.py."""
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from test_generic_plane import _free_port, close_lists, make_data, run_engine  # noqa: E402
+
+CM = "comb_modules"
+
+
+def _oracle(splits, mode, hot=0):
+    import comb_modules
+    return comb_modules.oracle(splits, mode, hot)
+
+
+# -- ops/segments.py against NumPy / Python ----------------------------------------
+def _rand_csr(seed, m=300, hot=5000):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 6, m)
+    lens[rng.integers(0, m, 3)] = hot  # a few hot keys
+    lens[:4] = 0                       # empty lists at the front
+    off = np.zeros(m + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    val = rng.integers(-1000, 1000, int(off[-1]))
+    return off, val
+
+
+def test_segment_ops_cpu():
+    from lua_mapreduce_1_amd.ops import segments as S
+    off, val = _rand_csr(0)
+    o, v = torch.from_numpy(off), torch.from_numpy(val)
+    lists = [val[off[i]:off[i + 1]] for i in range(off.size - 1)]
+    assert S.sum(o, v).tolist() == [int(x.sum()) for x in lists]
+    assert S.min(o, v, empty=0).tolist() == [int(x.min()) if x.size else 0 for x in lists]
+    assert S.max(o, v, empty=0).tolist() == [int(x.max()) if x.size else 0 for x in lists]
+    assert S.count(o).tolist() == [x.size for x in lists]
+    med = S.median(o, v).tolist()
+    for a, x in zip(med, lists):
+        assert (np.isnan(a) and x.size == 0) or a == float(np.median(x))
+    assert S.nunique(o, v).tolist() == [len(set(x.tolist())) for x in lists]
+    to, tv = S.topk(o, v, 3)
+    got = [tv[to[i]:to[i + 1]].tolist() for i in range(len(lists))]
+    assert got == [sorted(x.tolist(), reverse=True)[:3] for x in lists]
+    fo = torch.from_numpy(off)
+    fv = torch.from_numpy(val.astype(np.float64) / 7)
+    assert np.allclose(S.mean(fo, fv).numpy()[off[1:] > off[:-1]],
+                       [x.mean() / 7 for x in lists if x.size])
+
+
+def test_splice_and_as_lists():
+    from lua_mapreduce_1_amd.parallel import reducers as RD
+    off = torch.tensor([0, 2, 3, 6])
+    val = torch.tensor([1, 2, 3, 4, 5, 6])
+    noff, nval = RD.as_lists((torch.tensor([10, 20, 30]), torch.tensor([11, 21, 31])), 3, "t")
+    assert noff.tolist() == [0, 2, 4, 6] and nval.tolist() == [10, 11, 20, 21, 30, 31]
+    roff, rval = RD.splice(off, val, noff, nval, torch.tensor([False, True, False]))
+    assert roff.tolist() == [0, 2, 3, 5] and rval.tolist() == [10, 11, 3, 30, 31]
+    with pytest.raises(ValueError):
+        RD.as_lists(torch.tensor([1, 2]), 3, "t")
+    with pytest.raises(TypeError):
+        RD.as_lists("x", 3, "t")
+
+
+# -- the SPMD general plane -----------------------------------------------------------
+@pytest.mark.parametrize("mode", ["host", "device", "topk", "median"])
+def test_combiner_modes_cpu_w1(mode):
+    import comb_modules
+    splits = make_data("text")
+    comb_modules.CALLS.update(combinerfn=0, reducefn=0)
+    eng, res, got = run_engine(CM, splits, torch.device("cpu"), {"mode": mode})
+    assert eng.plane_kind == "generic"
+    assert close_lists(got, _oracle(splits, mode))
+    mp = eng.plane.map
+    if mode == "median":
+        assert mp.reducers is None and mp.combines == 0  # no combinerfn: lists are shipped whole
+    else:
+        assert mp.combines == 1
+        # the combined table holds ONE value per key (sum) / at most 3 (top-k)
+        per_key = 3 if mode == "topk" else 1
+        assert mp.table.npost <= per_key * res.distinct_keys
+    if mode in ("device", "topk", "median"):
+        assert comb_modules.CALLS["reducefn"] == 0  # batched on the device: no per-key host call
+
+
+def test_reducefn2_wordcount_ships_combined_values_gloo_w3():
+    """WordCount mapfn + the general reducer (host combiner): at W = 3 every
+    rank ships at most one value per distinct key of its map, not one per
+    word."""
+    ok, n, shipped, words, distinct = _spawn(3, "host")
+    assert ok and n > 100
+    assert shipped <= distinct  # values shipped over all ranks <= sum of per-rank distinct keys
+    assert shipped < words // 4
+
+
+@pytest.mark.parametrize("mode", ["device", "topk", "median"])
+def test_batched_reducers_gloo_w3(mode):
+    ok, n, shipped, words, distinct = _spawn(3, mode)
+    assert ok and n > 100
+
+
+def test_hot_key_bounded_cpu():
+    """One key with 4 x 600 k values and a combine threshold of 2^18
+    postings: the map table is combined every time it fills (the batched
+    MAX_MAP_RESULT), so it never holds more than threshold + one emit."""
+    splits = make_data("text")
+    hot = 600_000
+    t0 = time.time()
+    eng, res, got = run_engine(CM, splits, torch.device("cpu"), {"mode": "hot", "hot": hot},
+                               combine_postings=1 << 18)
+    dt = time.time() - t0
+    assert close_lists(got, _oracle(splits, "hot", hot))
+    assert eng.plane.map.combines >= (hot * len(splits)) // ((1 << 18) + hot)
+    assert dt < 120
+
+
+# -- multi-rank (gloo) -------------------------------------------------------------------
+def _rank(rank, world, port, q, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from lua_mapreduce_1_amd.parallel import dist as D
+    D.init_from_env(backend="gloo", use_gpu=False)
+    splits = make_data("text")
+    eng, res, got = run_engine(CM, splits, torch.device("cpu"), {"mode": mode})
+    # values shipped by this rank (8 bytes each) and its distinct keys
+    st = torch.tensor([eng.plane._nvals_shipped, res.distinct_keys_map], dtype=torch.int64)
+    dist.all_reduce(st)
+    if rank == 0:
+        words = sum(len(s.split()) for s in splits)
+        q.put((close_lists(got, _oracle(splits, mode)), len(got), int(st[0]), words, int(st[1])))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _spawn(world, mode):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, mode)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return q.get(timeout=5)

@@ -17,7 +17,7 @@ def cs():
 
 
 @pytest.mark.parametrize("storage", ["gridfs", "shared", "sshfs", "hbm"])
-@pytest.mark.parametrize("scenario", ["combiner_aci", "init_script"])
+@pytest.mark.parametrize("scenario", list(SCENARIOS))
 def test_wordcount_device_plane_on_gpu(gpu, cs, storage, scenario):
     before = devmod.STATS.get("maps_cuda", 0)
     p = dict(SCENARIOS[scenario], storage=storage, device="auto")

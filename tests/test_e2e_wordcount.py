@@ -26,6 +26,10 @@ SCENARIOS = {
     "general_reducer": dict(taskfn=W + ".taskfn", mapfn=W + ".mapfn", partitionfn=W + ".partitionfn",
                             reducefn=W + ".reducefn2", finalfn=W + ".finalfn"),
     "init_script": dict(taskfn=W, mapfn=W, partitionfn=W, reducefn=W, finalfn=W, combinerfn=W),
+    # reducefn2 plus its batched device form (device_reducefn): combiner and
+    # reduce jobs fold every key's list at once on the device
+    "general_reducer_device": dict(taskfn=W + ".taskfn", mapfn=W + ".mapfn", partitionfn=W + ".partitionfn",
+                                   reducefn=W + ".reducefn3", finalfn=W + ".finalfn"),
 }
 
 
