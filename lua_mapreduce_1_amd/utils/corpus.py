@@ -53,10 +53,16 @@ def zipf_probs(size: int, s: float = 1.05, q: float = 2.7) -> np.ndarray:
 
 
 def europarl_like(seed: int = 1234, lines: int = EUROPARL_LINES, words: int = EUROPARL_WORDS,
-                  split_lines: int = EUROPARL_SPLIT_LINES, vocab_size: int = 300_000, return_counts: bool = False):
+                  split_lines: int = EUROPARL_SPLIT_LINES, vocab_size: int = 300_000, return_counts: bool = False,
+                  return_bigrams: bool = False):
     """List of split byte strings (each ends with a newline); with
     ``return_counts`` also the vocabulary and every word's exact number of
-    occurrences (the per-key ground truth of a word count)."""
+    occurrences (the per-key ground truth of a word count); with
+    ``return_bigrams`` (implies the vocabulary) also the distinct bigrams of
+    the corpus as sorted codes ``first * vocab_size + second`` (word ids of
+    two consecutive tokens of one line) and their counts."""
+    return_counts = return_counts or return_bigrams
+    bigram_codes = []
     rng = np.random.default_rng(seed)
     vocab = make_vocab(vocab_size, rng)
     vlen = np.array([len(w) for w in vocab], dtype=np.int64)
@@ -86,6 +92,11 @@ def europarl_like(seed: int = 1234, lines: int = EUROPARL_LINES, words: int = EU
         tok = np.minimum(tok, vocab_size - 1)
         if return_counts:
             counts += np.bincount(tok, minlength=vocab_size)
+        if return_bigrams and nt > 1:
+            same_line = np.ones(nt - 1, bool)
+            same_line[np.cumsum(lw)[:-1] - 1] = False  # token i is the last of its line
+            c = tok[:-1] * np.int64(vocab_size) + tok[1:]
+            bigram_codes.append(c[same_line])
         tl = vlen[tok]
         # separator after each token: space, or newline at end of line
         sep = np.full(nt, ord(" "), dtype=np.uint8)
@@ -100,6 +111,10 @@ def europarl_like(seed: int = 1234, lines: int = EUROPARL_LINES, words: int = EU
         buf[isw] = vbytes[voff[tok[ti[isw]]] + ci[isw]]
         buf[~isw] = sep
         splits.append(buf.tobytes())
+    if return_bigrams:
+        codes, ccount = np.unique(np.concatenate(bigram_codes) if bigram_codes else np.zeros(0, np.int64),
+                                  return_counts=True)
+        return splits, vocab, counts, (codes, ccount)
     if return_counts:
         return splits, vocab, counts
     return splits
@@ -143,11 +158,13 @@ def tricky_text(rng: np.random.Generator, nbytes: int) -> bytes:
 
 
 def score_csv(seed: int = 7, lines: int = 100_000, vocab_size: int = 5_000, split_lines: int = 10_000,
-              long_frac: float = 0.01) -> list[bytes]:
+              long_frac: float = 0.01, return_truth: bool = False):
     """``word,score`` lines (a group-by-and-aggregate workload over a CSV
     column): Zipf-distributed words (some longer than 15 bytes), scores with
     three decimals in [-1000, 1000), split into pieces of ``split_lines``
-    lines (each ends with a newline)."""
+    lines (each ends with a newline).  With ``return_truth`` also
+    ``{word: [mean, max, count]}`` of every word that occurs (exact: the
+    scores are integers of milli-units)."""
     rng = np.random.default_rng(seed)
     vocab = make_vocab(vocab_size, rng, long_frac=long_frac)
     vocab = [w.replace(b",", b";") for w in vocab]
@@ -163,4 +180,14 @@ def score_csv(seed: int = 7, lines: int = 100_000, vocab_size: int = 5_000, spli
             a = abs(int(m))
             rows.append(vocab[t] + (",%s%d.%03d\n" % (sign, a // 1000, a % 1000)).encode())
         out.append(b"".join(rows))
-    return out
+    if not return_truth:
+        return out
+    cnt = np.bincount(tok, minlength=vocab_size)
+    tot = np.bincount(tok, weights=milli.astype(np.float64), minlength=vocab_size)
+    mx = np.full(vocab_size, np.iinfo(np.int64).min, np.int64)
+    np.maximum.at(mx, tok, milli)
+    truth = {}
+    for i in np.flatnonzero(cnt):
+        w = vocab[i].decode("utf-8", "surrogateescape")
+        truth[w] = [tot[i] / 1000.0 / cnt[i], mx[i] / 1000.0, int(cnt[i])]
+    return out, truth
