@@ -578,19 +578,71 @@ class Store {
   }
 
   // Journal file: an 8-byte magic/version header, then records
-  // len | FNV-1a(body) | body.  A file with another header is refused (never
-  // truncated: it may be an older format or another program's file).  Replay
-  // stops at the first record that is short (a write torn by a crash: the
-  // tail is cut there) or whose checksum does not match; such a tail is kept
-  // as <path>.corrupt before the journal is cut back to the last intact
-  // record.  A length field larger than the bytes left is a torn tail (no
-  // allocation is made from it).
+  // len | FNV-1a(body) | body.  Replay stops at the first record that is short
+  // (a write torn by a crash: the tail is cut there) or whose checksum does
+  // not match; such a tail is kept as <path>.corrupt before the journal is
+  // cut back to the last intact record.  A length field larger than the bytes
+  // left is a torn tail (no allocation is made from it).  A file without the
+  // header whose first record is intact is a journal of the previous build
+  // (the same records, no header): it is replayed and rewritten with the
+  // header (in place, through a temporary file and a rename).  Any other
+  // file is refused (never truncated: it may be another program's).
   static constexpr char JMAGIC[8] = {'M', 'R', 'J', 'N', 'L', 0, 0, 2};
+
+  // Replays the records from the current position; returns the end of the
+  // last intact record.
+  long replay_records(FILE* f, long size, bool& corrupt) {
+    long good = ftell(f);
+    corrupt = false;
+    replaying = true;
+    for (;;) {
+      uint32_t hdr[2];
+      const long at = ftell(f);
+      if (at == size) break;
+      if (fread(hdr, 4, 2, f) != 2) break;                 // torn header
+      if ((long)hdr[0] > size - at - 8) break;             // torn body (or a garbled length)
+      std::string body(hdr[0], '\0');
+      if (fread(&body[0], 1, hdr[0], f) != hdr[0]) break;
+      if (body_sum(body) != hdr[1]) {
+        corrupt = true;
+        break;
+      }
+      Writer w;
+      handle(body, w);
+      good = ftell(f);
+    }
+    replaying = false;
+    return good;
+  }
+
+  // The first record of a headerless file is intact (a legacy journal).
+  static bool legacy_journal(FILE* f, long size) {
+    uint32_t hdr[2];
+    fseek(f, 0, SEEK_SET);
+    if (size < 8 || fread(hdr, 4, 2, f) != 2 || (long)hdr[0] > size - 8) return false;
+    std::string body(hdr[0], '\0');
+    if (hdr[0] && fread(&body[0], 1, hdr[0], f) != hdr[0]) return false;
+    fseek(f, 0, SEEK_SET);
+    return body_sum(body) == hdr[1];
+  }
+
+  static void keep_tail(FILE* f, const char* path, long good, long size, bool corrupt) {
+    std::string keep = std::string(path) + ".corrupt";
+    FILE* c = fopen(keep.c_str(), "wb");
+    if (c) {
+      fseek(f, good, SEEK_SET);
+      char buf[65536];
+      size_t k;
+      while ((k = fread(buf, 1, sizeof buf, f)) > 0) fwrite(buf, 1, k, c);
+      fclose(c);
+    }
+    fprintf(stderr, "coordinator: journal %s: %s at byte %ld of %ld, replayed the intact prefix (tail kept in %s)\n",
+            path, corrupt ? "checksum mismatch" : "torn record", good, size, keep.c_str());
+  }
 
   bool open_journal(const char* path) {
     if (!path || !*path) return true;
     FILE* f = fopen(path, "rb");
-    long good = 0;  // end of the last complete, intact record
     long size = 0;
     if (f) {
       fseek(f, 0, SEEK_END);
@@ -599,49 +651,44 @@ class Store {
     }
     if (f && size > 0) {
       char magic[8];
-      if (fread(magic, 1, 8, f) != 8 || memcmp(magic, JMAGIC, 8) != 0) {
-        fclose(f);
-        fprintf(stderr, "coordinator: %s is not a journal of this format (header mismatch); refusing to use it\n",
-                path);
-        return false;
-      }
-      good = 8;
-      replaying = true;
       bool corrupt = false;
-      for (;;) {
-        uint32_t hdr[2];
-        const long at = ftell(f);
-        if (at == size) break;
-        if (fread(hdr, 4, 2, f) != 2) break;                 // torn header
-        if ((long)hdr[0] > size - at - 8) break;             // torn body (or a garbled length)
-        std::string body(hdr[0], '\0');
-        if (fread(&body[0], 1, hdr[0], f) != hdr[0]) break;
-        if (body_sum(body) != hdr[1]) {
-          corrupt = true;
-          break;
+      if (fread(magic, 1, 8, f) != 8 || memcmp(magic, JMAGIC, 8) != 0) {
+        if (!legacy_journal(f, size)) {
+          fclose(f);
+          fprintf(stderr, "coordinator: %s is not a journal of this format (header mismatch); refusing to use it\n",
+                  path);
+          return false;
         }
-        Writer w;
-        handle(body, w);
-        good = ftell(f);
-      }
-      replaying = false;
-      if (good < size) {
-        // keep what is cut off for inspection (a checksum mismatch in the
-        // middle drops every later record from the replay)
-        std::string keep = std::string(path) + ".corrupt";
-        FILE* c = fopen(keep.c_str(), "wb");
-        if (c) {
-          fseek(f, good, SEEK_SET);
-          char buf[65536];
-          size_t k;
-          while ((k = fread(buf, 1, sizeof buf, f)) > 0) fwrite(buf, 1, k, c);
-          fclose(c);
+        // a journal of the previous build: replay it, then rewrite it with
+        // the header (the old file is replaced only once the new one is whole)
+        const long good = replay_records(f, size, corrupt);
+        if (good < size) keep_tail(f, path, good, size, corrupt);
+        std::string tmp = std::string(path) + ".upgrade";
+        FILE* n = fopen(tmp.c_str(), "wb");
+        if (!n) {
+          fclose(f);
+          return false;
         }
-        fprintf(stderr, "coordinator: journal %s: %s at byte %ld of %ld, replayed the intact prefix (tail kept in %s)\n",
-                path, corrupt ? "checksum mismatch" : "torn record", good, size, keep.c_str());
+        fwrite(JMAGIC, 1, 8, n);
+        fseek(f, 0, SEEK_SET);
+        char buf[65536];
+        long left = good;
+        while (left > 0) {
+          size_t k = fread(buf, 1, (size_t)(left < (long)sizeof buf ? left : (long)sizeof buf), f);
+          if (k == 0) break;
+          fwrite(buf, 1, k, n);
+          left -= (long)k;
+        }
+        fclose(f);
+        if (fflush(n) != 0 || fclose(n) != 0 || left != 0 || rename(tmp.c_str(), path) != 0) return false;
+        fprintf(stderr, "coordinator: journal %s upgraded from the headerless format (%ld bytes replayed)\n", path,
+                good);
+      } else {
+        const long good = replay_records(f, size, corrupt);
+        if (good < size) keep_tail(f, path, good, size, corrupt);
+        fclose(f);
+        if (truncate(path, good) != 0) return false;
       }
-      fclose(f);
-      if (truncate(path, good) != 0) return false;
     } else {
       if (f) fclose(f);
       FILE* n = fopen(path, "wb");

@@ -39,10 +39,10 @@ def init(args):
 
 def _file_lines(path: str) -> int:
     """Lines of a file as the split store numbers them (a file that does not
-    end in whitespace gets a terminating newline)."""
+    end in a newline gets a terminating one)."""
     with open(path, "rb") as f:
         data = f.read()
-    return data.count(b"\n") + (0 if (data and data[-1:] in (b"\n", b" ")) else 1)
+    return data.count(b"\n") + (0 if data[-1:] == b"\n" else 1)
 
 
 def taskfn(emit):
@@ -68,7 +68,7 @@ def device_mapfn(keys, data, emit):
 def mapfn(key, value, emit):
     with open(value["file"], "rb") as f:
         data = f.read()
-    if not (data and data[-1:] in (b"\n", b" ")):
+    if data[-1:] != b"\n":
         data += b"\n"
     for n, line in enumerate(data.split(b"\n")):
         for w in line.split():
@@ -111,11 +111,11 @@ def finalfn(pairs_iterator):
 
 def naive_index(splits: list[bytes]) -> dict:
     """Oracle: word -> sorted distinct global line numbers (split-store layout:
-    a split that does not end in whitespace is followed by a newline)."""
+    a split that does not end in a newline is followed by one)."""
     out: dict = {}
     line = 0
     for s in splits:
-        if not (s and s[-1:] in (b"\n", b" ")):
+        if s[-1:] != b"\n":
             s = s + b"\n"
         pieces = s.split(b"\n")
         for n, ln in enumerate(pieces):

@@ -104,13 +104,21 @@ class KeySource:
         return self.buf if self.buf is not None else self.arena
 
     def offset_of(self, t: torch.Tensor) -> int | None:
-        """Byte offset of ``t`` inside the source (None: not a view of it)."""
-        b = self._base()
-        if b is None or t.device != b.device or t.dtype != torch.uint8:
+        """Byte offset of ``t`` inside the source (None: not a view of it).
+        Once bytes were appended the source is a copy ``buf`` whose first
+        ``arena.numel()`` bytes mirror the arena at the same offsets, so a
+        view of the arena keeps its arena offset."""
+        if t.dtype != torch.uint8:
             return None
-        p = t.data_ptr() - b.data_ptr()
-        if 0 <= p and p + t.numel() <= self.used:
-            return p
+        for b, lim in ((self.buf, self.used), (self.arena, self.arena.numel() if self.arena is not None else 0)):
+            if b is None or t.device != b.device:
+                continue
+            p = t.data_ptr() - b.data_ptr()
+            if 0 <= p and p + t.numel() <= lim:
+                if b is self.arena and self.buf is not None and t.numel():
+                    # staged after the copy was taken: refresh its mirror
+                    self.buf[p:p + t.numel()].copy_(t.reshape(-1), non_blocking=True)
+                return p
         return None
 
     def add(self, t: torch.Tensor) -> tuple[int, torch.Tensor]:
@@ -182,7 +190,10 @@ class GenericEmitter:
         if src is not None:
             _, add = self.m.src.locate(src if src.device == self.m.device else src.to(self.m.device))
         elif rep is not None and self.chunk is not None:
-            add = self.m.src.offset_of(self.chunk) or 0  # rep words relative to the mapped chunk
+            add = self.m.src.offset_of(self.chunk)  # rep words relative to the mapped chunk
+            if add is None:
+                raise ValueError("emit.pairs(rep=...): the mapped chunk is not part of the key source; pass src= "
+                                 "(the tensor the rep words index)")
         self.m.insert(int(hi.numel()), values, hi=hi, lo=lo, rep=rep, rep_add=add)
 
     def words(self, text=None, *values) -> None:
@@ -613,7 +624,7 @@ class GenericPlane:
         raise RuntimeError("general plane: the map did not converge (table regrowth / retries)")
 
     # -- map checkpoints (split-level restart) ------------------------
-    def _save_map(self) -> None:
+    def _save_map(self, recs=None, j0: int = 0, j1: int = 0) -> None:
         """This rank's map output of the iteration -> ``checkpoint_dir``
         (data-only .npz: key words, key bytes, and the physical fold columns or
         the value lists), so a relaunch after a failure later in the iteration
@@ -624,6 +635,8 @@ class GenericPlane:
         if path is None:
             return
         import os
+        if recs is not None:
+            eng._save_job_status(recs, j0, j1)
         mp = self.map
         src = mp.src.source()
         if self.list_mode:
@@ -692,9 +705,7 @@ class GenericPlane:
             mp.table.insert(m, [t(a[f"col{j}"]) for j in range(len(merge))], hi=hi, lo=lo, rep=rep)
         self._table_restored = True  # the next map gets a regular table again
         mp.rows = int(a["rows"][0])
-        now = time.time()
-        for j in range(j0, j1):
-            recs[j].status, recs[j].started, recs[j].written, recs[j].worker = STATUS.WRITTEN, now, now, eng.rank
+        eng._restore_job_status(recs, j0, j1)
         eng.maps_restored += 1
         sys.stderr.write("# rank %d: map of iteration %d restored from its checkpoint\n" % (eng.rank, eng.iteration))
         return True
@@ -824,7 +835,7 @@ class GenericPlane:
             if not self._restore_map(recs, j0, j1):
                 self._map(jobs, recs, j0, j1)
                 self.map.combine()  # the end-of-map combiner (job.lua:198-202); no-op without one
-                self._save_map()
+                self._save_map(recs, j0, j1)
         eng._maybe_inject_fault("shuffle")
         T["map"] = time.time() - t0
         t1 = time.time()

@@ -323,7 +323,7 @@ class ListPlane:
         return II.map_postings(eng.arena[:self._cpu_end], self.vocab, self.doc_bits)
 
     # -- map checkpoints (split-level restart) ------------------------
-    def _save_map(self, keys: torch.Tensor) -> None:
+    def _save_map(self, keys: torch.Tensor, recs=None, j0: int = 0, j1: int = 0) -> None:
         """This rank's postings of the iteration -> ``checkpoint_dir`` (data-only
         .npz: the posting keys ``id << doc_bits | line``, the words their ids
         name with their key bytes, the line numbering), so a relaunch after a
@@ -335,6 +335,8 @@ class ListPlane:
         if path is None:
             return
         import os
+        if recs is not None:
+            eng._save_job_status(recs, j0, j1)
         vhi, vlo, vrep = self.vocab.arrays()
         ids = torch.unique((keys >> self.doc_bits) & ((1 << self.vocab.id_bits) - 1)) if keys.numel() else keys[:0]
         src = self._src()
@@ -381,9 +383,7 @@ class ListPlane:
         t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(d)  # noqa: E731
         self._restored = (_SavedVocab(t(words[0]), t(words[1]), t(words[2]), id_bits),
                           t(np.concatenate([a["blob"], np.zeros(1, np.uint8)])))
-        now = time.time()
-        for j in range(j0, j1):
-            recs[j].status, recs[j].started, recs[j].written, recs[j].worker = STATUS.WRITTEN, now, now, eng.rank
+        eng._restore_job_status(recs, j0, j1)
         eng.maps_restored += 1
         sys.stderr.write("# rank %d: postings of iteration %d restored from the checkpoint\n"
                          % (eng.rank, eng.iteration))
@@ -441,7 +441,7 @@ class ListPlane:
                 keys = self._restore_map(recs, j0, j1)
                 if keys is None:
                     keys = self._map(jobs, recs, j0, j1)
-                    self._save_map(keys)
+                    self._save_map(keys, recs, j0, j1)
         except _UseGeneric:
             # the map emits through generic calls: the general plane runs
             # this engine from now on (this iteration is restarted there)
@@ -710,7 +710,7 @@ class RecordPlane:
             self._out.append(rec if rec.device == dev else rec.to(dev, non_blocking=True))
 
     # -- map checkpoints (split-level restart) ------------------------
-    def _save_rows(self) -> None:
+    def _save_rows(self, recs=None, j0: int = 0, j1: int = 0) -> None:
         """This rank's mapped rows -> ``checkpoint_dir`` (data-only .npz), so a
         relaunch after a failure later in the iteration restores them instead
         of re-running the rank's map jobs."""
@@ -719,12 +719,20 @@ class RecordPlane:
         if path is None or self.shape is None:
             return
         import os
-        rows = torch.cat([r.cpu() for r in self._out]) if self._out else torch.zeros((0, self.shape[0]),
-                                                                                     dtype=torch.uint8)
+        import zipfile
+        if recs is not None:
+            eng._save_job_status(recs, j0, j1)
         os.makedirs(eng.checkpoint_dir, exist_ok=True)
         tmp = path + ".tmp"
+        # one .npz member per emitted block, written one at a time (host
+        # memory: one block, not a concatenation of all of them — ADVICE r3)
         with open(tmp, "wb") as f:
-            np.savez(f, rows=rows.numpy(), key_bytes=np.array([self.shape[1]], np.int64))
+            with zipfile.ZipFile(f, "w", allowZip64=True) as zf:
+                for i, r in enumerate(self._out):
+                    with zf.open("rows%d.npy" % i, "w", force_zip64=True) as fh:
+                        np.lib.format.write_array(fh, np.ascontiguousarray(r.cpu().numpy()))
+                with zf.open("shape.npy", "w") as fh:
+                    np.lib.format.write_array(fh, np.array([self.shape[0], self.shape[1], len(self._out)], np.int64))
             f.flush()
             os.fsync(f.fileno())
         os.replace(tmp, path)
@@ -735,15 +743,20 @@ class RecordPlane:
         import os
         if path is None or not os.path.exists(path):
             return False
+        cap = self._cap()
         with np.load(path, allow_pickle=False) as z:
-            rows, kb = z["rows"], int(z["key_bytes"][0])
-        if rows.shape[0]:
-            self.emitter.records(torch.from_numpy(rows).to(eng.device), kb)  # the emitter's spill rule applies
-        else:
-            self.shape = (int(rows.shape[1]), kb)
-        now = time.time()
-        for j in range(j0, j1):
-            recs[j].status, recs[j].started, recs[j].written, recs[j].worker = STATUS.WRITTEN, now, now, eng.rank
+            rb, kb, nblocks = (int(x) for x in z["shape"])
+            # block by block from host memory, each at most the HBM cap: the
+            # emitter's spill rule keeps rows past the cap on the host
+            for i in range(nblocks):
+                rows = z["rows%d" % i]
+                step = max(1, cap // max(rb, 1)) if cap else max(1, rows.shape[0])
+                for a in range(0, rows.shape[0], step):
+                    self.emitter.records(torch.from_numpy(rows[a:a + step]), kb)
+                del rows
+        if self.shape is None:
+            self.shape = (rb, kb)
+        eng._restore_job_status(recs, j0, j1)
         eng.maps_restored += 1
         sys.stderr.write("# rank %d: rows of iteration %d restored from the checkpoint\n" % (eng.rank, eng.iteration))
         return True
@@ -771,7 +784,7 @@ class RecordPlane:
                     recs[j].status = STATUS.BROKEN if attempt < 2 else STATUS.FAILED
             _mark_written(recs, j, j + 1, t0, time.time(), c0)
         if not restored:
-            self._save_rows()
+            self._save_rows(recs, j0, j1)
         if self.shape is None:  # nothing emitted on this rank: agree on the shape with the others
             shapes = D.all_gather_object(None, eng.group) if D.initialized() and eng.world > 1 else []
             self.shape = next((x for x in shapes if x is not None), (TS.REC, TS.KEY))

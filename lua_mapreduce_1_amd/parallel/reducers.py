@@ -101,8 +101,8 @@ def lists_of_postings(slot, pslot, pval, m: int, space: int):
     if pr.numel():
         pp = ops.sort_keys_checked([pr], bits=[max(1, int(m - 1).bit_length())]).long()  # stable
         pr, pv = pr[pp], pv[pp]
-    nv = torch.bincount(pr, minlength=m)[:m]
-    return S.from_lengths(nv), pv
+    # list boundaries of the sorted key indices (no atomics: hot keys are free)
+    return torch.searchsorted(pr, torch.arange(m + 1, dtype=torch.int64, device=d)), pv
 
 
 def splice(off, val, noff, nval, keep_old):

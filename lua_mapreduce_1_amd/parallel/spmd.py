@@ -73,7 +73,7 @@ class SplitStore:
 
     def __init__(self, splits: list[bytes] | None = None, pin: bool = True):
         splits = splits or []
-        sizes = [len(s) + (0 if (s and s[-1:] in (b"\n", b" ")) else 1) for s in splits]
+        sizes = [len(s) + (0 if s[-1:] == b"\n" else 1) for s in splits]
         self._layout(sizes, (0, len(splits)), pin)
         view = self.buffer.numpy()
         for i, s in enumerate(splits):
@@ -115,7 +115,7 @@ class SplitStore:
                    threads: int = 8) -> "SplitStore":
         """One split per file (the reference's split files, WordCountBig
         taskfn.lua:6-10).  Sizes come from stat; a file that does not end in
-        a newline or a space is followed by one (the same rule as the
+        a newline is followed by one (the same rule as the
         in-memory and blob stores, so line numbers agree); only this rank's
         contiguous byte-balanced share is read."""
         lens, pad = _file_pads(paths)
@@ -134,7 +134,7 @@ class SplitStore:
         mm = np.memmap(path, dtype=np.uint8, mode="r") if offsets[-1] else None
         last = [int(mm[o - 1]) if n else 0 for o, n in zip(offsets[1:], lens)] if mm is not None else []
         del mm
-        pad = [0 if (n and b in (10, 32)) else 1 for n, b in zip(lens, last)]
+        pad = [0 if (n and b == 10) else 1 for n, b in zip(lens, last)]
         own = assign_contiguous((lens + np.asarray(pad, dtype=np.int64)).tolist(), rank, world)
         return cls._async([path] * len(lens), offsets[:-1], lens, pad, own, pin, threads)
 
@@ -259,8 +259,9 @@ class WindowedSplitStore(SplitStore):
 
 
 def _file_pads(paths) -> tuple[list[int], list[int]]:
-    """(sizes, pads): pad 1 when a file's last byte is not a newline or a
-    space (then a newline follows the split: tokens never straddle splits)."""
+    """(sizes, pads): pad 1 when a file's last byte is not a newline (then a
+    newline follows the split: tokens never straddle splits, and the next
+    split's first line gets its own global line number)."""
     lens, pad = [], []
     for p in paths:
         n = os.path.getsize(p)
@@ -270,7 +271,7 @@ def _file_pads(paths) -> tuple[list[int], list[int]]:
                 f.seek(n - 1)
                 last = f.read(1)
         lens.append(n)
-        pad.append(0 if last in (b"\n", b" ") else 1)
+        pad.append(0 if last == b"\n" else 1)
     return lens, pad
 
 
@@ -1373,7 +1374,7 @@ class SPMDEngine:
             n_claimed, overflow = self.table.stats()
         else:
             n_claimed, overflow = self._map_sync(jobs, recs, j0, j1)  # synchronises the map phase
-            self._save_map(n_claimed, overflow)
+            self._save_map(n_claimed, overflow, recs, j0, j1)
         trace.pop()
         self._maybe_inject_fault("shuffle")
         T["map"] = time.time() - t0
@@ -1562,10 +1563,53 @@ class SPMDEngine:
         return os.path.join(self.checkpoint_dir, "%s.map.it%d.r%d.w%d.%s" % (self.result_ns, it, self.rank,
                                                                            self.world, key))
 
-    def _save_map(self, n: int, overflow: bool) -> None:
+    def _save_job_status(self, recs, j0: int, j1: int) -> None:
+        """Next to a map checkpoint: the jobs of this rank's block that did
+        not end WRITTEN (FAILED / BROKEN, with their repetitions), written
+        before the checkpoint itself — a restore then reports the same failed
+        maps as the run that wrote it (a failed job stays FAILED,
+        server.lua:194-205)."""
+        path = self._map_ckpt_path()
+        if path is None:
+            return
+        import json
+        bad = {str(j): [int(recs[j].status), int(recs[j].repetitions)] for j in range(j0, j1)
+               if recs[j].status in (STATUS.FAILED, STATUS.BROKEN)}
+        if not bad:
+            if os.path.exists(path + ".jobs.json"):
+                os.remove(path + ".jobs.json")  # a stale record of an earlier launch
+            return
+        os.makedirs(self.checkpoint_dir, exist_ok=True)
+        tmp = path + ".jobs.json.tmp"
+        with open(tmp, "w") as f:
+            json.dump(bad, f)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path + ".jobs.json")
+
+    def _restore_job_status(self, recs, j0: int, j1: int) -> None:
+        """The rank's map jobs after a restore: WRITTEN, except those its
+        checkpoint recorded as failed."""
+        import json
+        now = time.time()
+        for j in range(j0, j1):
+            recs[j].status, recs[j].started, recs[j].written, recs[j].worker = STATUS.WRITTEN, now, now, self.rank
+        path = self._map_ckpt_path()
+        if path is None or not os.path.exists(path + ".jobs.json"):
+            return
+        with open(path + ".jobs.json") as f:
+            bad = json.load(f)
+        for j, (st, reps) in bad.items():
+            j = int(j)
+            if j0 <= j < j1:
+                recs[j].status, recs[j].repetitions = st, reps
+
+    def _save_map(self, n: int, overflow: bool, recs=None, j0: int = 0, j1: int = 0) -> None:
         path = self._map_ckpt_path()
         if path is None or self.plane_kind != "fold" or overflow:
             return
+        if recs is not None:
+            self._save_job_status(recs, j0, j1)
         from ..runtime import codec
         hi, lo, val, rep = self.table.compact((n, False))
         _, ln = ops.key_meta(hi, lo, rep, self._source(), want_part=False)
@@ -1607,9 +1651,7 @@ class SPMDEngine:
             timer.begin()
         self.table.insert(t(cols["hi"]), t(cols["lo"]), t(cols["val"]), rep, src=blob)
         self.maps_restored += 1
-        now = time.time()
-        for j in range(j0, j1):
-            recs[j].status, recs[j].started, recs[j].written, recs[j].worker = STATUS.WRITTEN, now, now, self.rank
+        self._restore_job_status(recs, j0, j1)
         self._chunks[self.tslot] = []
         self._log("# rank %d: map of iteration %d restored from %s\n" % (self.rank, self.iteration, path))
         sys.stderr.write("# rank %d: map of iteration %d restored from its checkpoint\n" % (self.rank, self.iteration))
@@ -1617,8 +1659,9 @@ class SPMDEngine:
 
     def _drop_map_ckpt(self, iteration: int) -> None:
         path = self._map_ckpt_path(iteration)
-        if path is not None and os.path.exists(path):
-            os.remove(path)
+        for p in (path, path + ".jobs.json") if path is not None else ():
+            if os.path.exists(p):
+                os.remove(p)
 
     def _manifest_path(self) -> str | None:
         if not self.checkpoint_dir:

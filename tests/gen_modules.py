@@ -40,7 +40,7 @@ def init(args):
     NUM_REDUCERS = int(args.get("num_reducers", NUM_REDUCERS))
     device_partition = ("fnv1", NUM_REDUCERS)
     device_reduce = {"max_host": None, "docs": "concat_unique", "docs_concat": "concat",
-                     "mixed": ("i64:sum", "max")}[MODE]
+                     "mixed": ("i64:sum", "max"), "pairs_host": "i64:sum"}[MODE]
 
 
 def taskfn(emit):
@@ -71,6 +71,15 @@ def device_mapfn(key, data, emit):
     if not hasattr(data, "data_ptr"):  # server/worker: the job's file
         from lua_mapreduce_1_amd.ops import io as _io
         data = _io.load_file(data["file"], emit.device)
+    if MODE == "pairs_host":
+        # a host pair first (the key source becomes a copy of the arena), then
+        # pre-encoded keys whose rep words are relative to the mapped chunk
+        # (chunk offsets must survive the copy)
+        from lua_mapreduce_1_amd import ops
+        emit("__host_key__", 1)
+        hi, lo, rep = ops.tokenize(data)
+        emit.pairs(hi, lo, 1, rep=rep)
+        return
     st, ln, val = _token_values(data)
     if MODE == "mixed":
         emit.spans(st, ln, val, val, text=data)

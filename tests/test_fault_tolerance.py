@@ -198,3 +198,26 @@ def test_journal_of_unknown_format_is_refused_not_truncated(tmp_path):
     assert c2.request("BLOB_GET", "jdb", "a")[1] == [b"first"]
     assert os.path.getsize(j2) == good
     assert os.path.getsize(j2 + ".corrupt") == size - good
+
+
+def test_headerless_journal_of_previous_build_is_upgraded(tmp_path):
+    """a journal written by the previous build (the same intact
+    records, no header) is replayed and rewritten with the header, so a
+    coordinator upgraded in place recovers its task and job state."""
+    j = str(tmp_path / "coord.journal")
+    c1 = coordinator.Client(coordinator.start_local(journal=j))
+    c1.request("BLOB_PUT", "jdb", "a", b"first")
+    c1.request("BLOB_PUT", "jdb", "b", b"second")
+    with open(j, "rb") as f:
+        data = f.read()
+    legacy = str(tmp_path / "legacy.journal")
+    with open(legacy, "wb") as f:
+        f.write(data[8:])  # the records without the header
+    c2 = coordinator.Client(coordinator.start_local(journal=legacy))
+    assert c2.request("BLOB_GET", "jdb", "a")[1] == [b"first"]
+    assert c2.request("BLOB_GET", "jdb", "b")[1] == [b"second"]
+    c2.request("BLOB_PUT", "jdb", "c", b"third")
+    with open(legacy, "rb") as f:
+        assert f.read(8) == data[:8]  # now in the current format
+    c3 = coordinator.Client(coordinator.start_local(journal=legacy))
+    assert c3.request("BLOB_GET", "jdb", "c")[1] == [b"third"]

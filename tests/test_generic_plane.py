@@ -125,6 +125,34 @@ def test_list_plane_switches_to_generic_on_spans():
     assert got == oracle("text", "docs", splits)
 
 
+def test_pairs_rep_after_host_keys_many_chunks():
+    """emit(host key) then emit.pairs(rep=...) in every one of many staged
+    chunks: long keys of later chunks still point at their own bytes."""
+    from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore
+    from lua_mapreduce_1_amd.runtime import codec
+    from lua_mapreduce_1_amd.utils.corpus import europarl_like
+    splits = europarl_like(seed=13, lines=2000, words=20000, vocab_size=900, split_lines=100)
+    splits = [s.replace(b" of ", b" extraordinarily_long_word_of_many_bytes ") for s in splits]
+    eng = SPMDEngine(dict(taskfn=GM, mapfn=GM, partitionfn=GM, reducefn=GM, finalfn=None,
+                          init_args={"mode": "pairs_host", "nsplits": len(splits)}),
+                     split_store=SplitStore(splits, pin=False), device=torch.device("cpu"))
+    eng.chunk_bytes = [8 << 10]
+    eng.tail_bytes = [8 << 10]
+    res = eng.run()
+    got = {}
+    for _n, cols in eng.gather_results(res):
+        for k, v in codec.iter_columnar(cols):
+            got[k] = v[0]
+    exp = {}
+    for s in splits:
+        for w in s.split():
+            exp[w.decode()] = exp.get(w.decode(), 0) + 1
+    nchunks = len(eng._chunks[0]) if eng._chunks[0] else None
+    exp["__host_key__"] = got.get("__host_key__")
+    assert got == exp
+    assert got["__host_key__"] > 1, nchunks  # several chunks were mapped
+
+
 def test_column_spec_parsing():
     from lua_mapreduce_1_amd.ops import agg as A
     assert [repr(c) for c in A.parse_spec(("f64:mean", "max", "count", "sum:f32"))] == [

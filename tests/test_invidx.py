@@ -65,9 +65,10 @@ def test_cpu_single_rank_matches_oracle():
 @pytest.mark.parametrize("windowed", [False, True])
 def test_split_files_number_lines_like_the_oracle(tmp_path, windowed):
     """SplitStore.from_files (execute_spmd --split-glob) pads a
-    file with a newline only when it does not end in a newline or a space,
-    like the in-memory store and the oracle — a file ending in '\n' gains no
-    empty line, so later line ids do not shift."""
+    file with a newline only when it does not end in a newline, like the
+    in-memory store and the oracle — a file ending in '\n' gains no empty
+    line, so later line ids do not shift; one ending in a space does (ADVICE
+    r3: its last line and the next file's first line are different lines)."""
     from lua_mapreduce_1_amd import spmd
     from lua_mapreduce_1_amd.parallel.spmd import SplitStore, WindowedSplitStore
     splits = _splits()
@@ -86,6 +87,25 @@ def test_split_files_number_lines_like_the_oracle(tmp_path, windowed):
         assert ws.offsets.tolist() == store.offsets.tolist()
     spmd(params, device="cpu", split_store=store).run()
     assert _result() == _naive(splits)
+
+
+def test_trailing_space_file_ends_its_line(tmp_path):
+    """A split ending in a space is followed by a newline: the next split's
+    first line is a new global line."""
+    from lua_mapreduce_1_amd import spmd
+    from lua_mapreduce_1_amd.parallel.spmd import SplitStore
+    splits = [b"alpha beta ", b"gamma\ndelta ", b"eps"]
+    assert _naive(splits) == {"alpha": [0], "beta": [0], "gamma": [1], "delta": [2], "eps": [3]}
+    paths = []
+    for i, b in enumerate(splits):
+        p = tmp_path / f"t{i}.txt"
+        p.write_bytes(b)
+        paths.append(str(p))
+    for store in (SplitStore(splits, pin=False), SplitStore.from_files(paths, pin=False)):
+        params = dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                      init_args={"nsplits": len(splits), "num_reducers": 3})
+        spmd(params, device="cpu", split_store=store).run()
+        assert _result() == _naive(splits)
 
 
 def test_server_worker_host_plane_matches_oracle(tmp_path):
