@@ -782,7 +782,10 @@ constexpr u64 SG_CHUNK = 4096;
 __global__ void __launch_bounds__(SG_T) ii_seg_gather_kernel(const u32* __restrict__ perm,
                                                              const long long* __restrict__ old_start,
                                                              const long long* __restrict__ new_off, u64 nw, u64 n,
+                                                             u64 nw_in, u64 n_src,
                                                              const int* __restrict__ src, int* __restrict__ dst) {
+  // n: output postings; nw_in / n_src: words / postings of the input lists
+  // (a reduce round gathers a subset of the words: nw < nw_in, n < n_src)
   __shared__ u64 s_w;
   const u64 c0 = (u64)blockIdx.x * SG_CHUNK;
   const u64 c1 = c0 + SG_CHUNK < n ? c0 + SG_CHUNK : n;
@@ -800,18 +803,19 @@ __global__ void __launch_bounds__(SG_T) ii_seg_gather_kernel(const u32* __restri
     const u64 ws = (u64)new_off[w], we = (u64)new_off[w + 1];
     if (ws >= c1) break;
     const u64 a = ws > c0 ? ws : c0, b = we < c1 ? we : c1;
-    const u64 s0 = (u64)old_start[clamp_row(perm[w], nw)] + (a - ws);
-    for (u64 j = a + threadIdx.x; j < b; j += SG_T) dst[j] = src[clamp_row(s0 + (j - a), n)];
+    const u64 s0 = (u64)old_start[clamp_row(perm[w], nw_in)] + (a - ws);
+    for (u64 j = a + threadIdx.x; j < b; j += SG_T) dst[j] = src[clamp_row(s0 + (j - a), n_src)];
   }
 }
 }  // namespace ii
 }  // namespace mr
 
 extern "C" int mr_ii_seg_gather(const void* perm, const void* old_start, const void* new_off, u64 nw, u64 n,
-                                const void* src, void* dst, hipStream_t s) {
+                                u64 nw_in, u64 n_src, const void* src, void* dst, hipStream_t s) {
   if (n == 0 || nw == 0) return 0;
   const u64 blocks = (n + ii::SG_CHUNK - 1) / ii::SG_CHUNK;
   hipLaunchKernelGGL(ii::ii_seg_gather_kernel, dim3((unsigned)blocks), dim3(ii::SG_T), 0, s, (const u32*)perm,
-                     (const long long*)old_start, (const long long*)new_off, nw, n, (const int*)src, (int*)dst);
+                     (const long long*)old_start, (const long long*)new_off, nw, n, nw_in, n_src, (const int*)src,
+                     (int*)dst);
   return (int)hipGetLastError();
 }

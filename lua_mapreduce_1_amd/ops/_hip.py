@@ -68,7 +68,7 @@ _SIGS = {
     "mr_ii_group_count": [_p, _u64, _u32, _i32, _p, _p],
     "mr_ii_group_scatter": [_p, _u64, _u32, ctypes.c_longlong, _u64, _i32, _p, _p, _p, _p, _p],
     "mr_ii_insert_slots": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _p, _p, _p],
-    "mr_ii_seg_gather": [_p, _p, _p, _u64, _u64, _p, _p, _p],
+    "mr_ii_seg_gather": [_p, _p, _p, _u64, _u64, _u64, _u64, _p, _p, _p],
     "mr_ts_gen": [_p, _u64, _u64, _u64, _p],
     "mr_ts_keys": [_p, _u64, _p, _p, _p, _p],
     "mr_ts_checksum": [_p, _u64, _p, _p],
@@ -111,6 +111,7 @@ _SIGS = {
     "mr_exact_hash": [_p, _p, _p, _p, _u64, _p, _p],
     "mr_exact_fix": [_p, _p, _u64, _p, _p, _p, _p, _p, _p, _p, _p],
     "mr_seg_reduce": [_p, _u64, _p, _u64, _i32, _i32, _p, _p],
+    "mr_wc_map3_set_config": [_i32],
 }
 _RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
                 "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words"}
@@ -138,6 +139,8 @@ def lib():
         L.mr_host_free.restype = _i32
         if L.mr_sort_set_rounds(TUNABLES.sort_rounds) != 0:
             raise ValueError(f"MR_SORT_ROUNDS={TUNABLES.sort_rounds}: must be 16, 24 or 32")
+        if L.mr_wc_map3_set_config(TUNABLES.wc_map_config) != 0:
+            raise ValueError(f"MR_WC_MAP_CONFIG={TUNABLES.wc_map_config}: must be 0..3")
         _LIB = L
     return _LIB
 

@@ -285,20 +285,24 @@ def insert_ids(vocab: Vocab, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tens
 
 def seg_gather(perm: torch.Tensor, old_start: torch.Tensor, new_off: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
     """Posting lists reordered by a word permutation: word i of the output is
-    word perm[i] of the input (``old_start`` = input word starts, ``new_off`` =
-    output offsets, nw+1 entries).  int32 postings."""
+    word perm[i] of the input (``old_start`` = input word starts, nw_in+1
+    entries; ``new_off`` = output offsets, nw+1 entries).  ``perm`` may select
+    a subset of the words (a reduce round): the output then holds only their
+    lists.  int32 postings."""
     nw = perm.numel()
-    n = src.numel()
+    nw_in = old_start.numel() - 1
+    n_src = src.numel()
+    n = n_src if nw == nw_in else (int(new_off[-1]) if nw else 0)
     if src.is_cuda:
         out = torch.empty(n, dtype=torch.int32, device=src.device)
         p32 = perm.to(torch.int32).contiguous()
         _hip.call("mr_ii_seg_gather", _hip.ptr(p32), _hip.ptr(old_start.contiguous()), _hip.ptr(new_off.contiguous()),
-                  nw, n, _hip.ptr(src), _hip.ptr(out), _hip.stream(src.device))
+                  nw, n, nw_in, n_src, _hip.ptr(src), _hip.ptr(out), _hip.stream(src.device))
         return out
-    if nw == 0:
+    if nw == 0 or n == 0:
         return src[:0].clone()
     p = perm.long()
-    lens = (old_start[1:] - old_start[:-1])[p] if old_start.numel() == nw + 1 else None
+    lens = (old_start[1:] - old_start[:-1])[p]
     idx = torch.cat([torch.arange(int(old_start[int(w)]), int(old_start[int(w)]) + int(ln))
-                     for w, ln in zip(p.tolist(), lens.tolist())]) if n else torch.zeros(0, dtype=torch.int64)
+                     for w, ln in zip(p.tolist(), lens.tolist())])
     return src[idx]

@@ -815,9 +815,72 @@ class GenericPlane:
         slot, hi, lo, rep, cols = rt.compact((m, False))
         return (slot, hi, lo, rep, cols), None
 
+    # -- order + reduce (one round, or the rank's partitions in rounds) ---------------
+    def _order(self, keys: tuple, src, space):
+        eng = self.eng
+        if self.list_mode:
+            return order_lists(*keys, src, eng.nparts, eng.partmod, self.unique, self.dtype, space)
+        return order_fold(*keys, src, eng.nparts, eng.partmod, self.phys)
+
+    def _reduce(self, out: dict):
+        """The reduce jobs over an ordered result: (device result, None), or
+        (None, host partitions) when the module's reducefn ran on the host."""
+        R = self.eng.nparts
+        if self.host_reduce and self.reducers.device_reduce:
+            # batched: device_reducefn over every key's list
+            with trace.range("mr.gen.reduce"):
+                keys = RD.KeyBatch(out["hi"], out["lo"], key_off=out["key_off"], key_blob=out["key_blob"])
+                red = self.reducers.reduce_device(keys, out["list_off"], out["list_val"])
+            out = {k: v for k, v in out.items() if k not in ("list_off", "list_val")}
+            out.update(red)
+            return out, None
+        if self.host_reduce:
+            # the last resort: the user's reducefn per key on the host
+            return None, host_partitions(out, R, self.dtype, self.reducefn, self.aci)
+        return out, None
+
+    def _reduce_groups(self, keys: tuple, src, space):
+        """(partition of every key, rounds of partitions) for a reduce under
+        reduce_cap_mb — volumes from the key lengths and value counts."""
+        from .planes import partition_volumes, reduce_cap_bytes, round_groups
+        eng = self.eng
+        R = eng.nparts
+        hi, lo, rep = keys[1], keys[2], keys[3]
+        part, klen = (ops.key_meta(hi, lo, rep, src, nparts=R) if self._fnv_parts() else
+                      (devmod.partition_of(hi, lo, rep, src, R, eng.partmod),
+                       ops.key_meta(hi, lo, rep, src, want_part=False)[1]))
+        if self.list_mode:
+            slot, pslot = keys[0], keys[4]
+            m = hi.numel()
+            pos = torch.full((max(int(space), 1),), -1, dtype=torch.int64, device=hi.device)
+            pos[slot] = torch.arange(m, dtype=torch.int64, device=hi.device)
+            pr = pos[pslot.clamp(min=0)]
+            pr = pr[(pslot >= 0) & (pr >= 0)]
+            nv = torch.bincount(pr, minlength=m)[:m] if m else torch.zeros(0, dtype=torch.int64, device=hi.device)
+        else:
+            nv = torch.full_like(klen, len(keys[4]), dtype=torch.int64)
+        vol = partition_volumes(part, klen, nv, R)
+        return part, round_groups(vol, reduce_cap_bytes(eng))
+
+    def _fnv_parts(self) -> bool:
+        spec = getattr(self.eng.partmod, "device_partition", None) if self.eng.partmod is not None else None
+        return spec is not None and spec[0] == "fnv1" and int(spec[1]) == self.eng.nparts
+
+    def _select(self, keys: tuple, space, part, grp: list[int]):
+        """The keys (and their values) of partitions ``grp``."""
+        km = torch.isin(part.to(torch.int64), torch.tensor(grp, dtype=torch.int64, device=part.device))
+        if not self.list_mode:
+            slot, hi, lo, rep, cols = keys
+            return (slot[km], hi[km], lo[km], rep[km], [c[km] for c in cols]), space
+        slot, hi, lo, rep, pslot, pval = keys
+        sel = torch.zeros(max(int(space), 1), dtype=torch.bool, device=slot.device)
+        sel[slot[km]] = True
+        pm = (pslot >= 0) & sel[pslot.clamp(min=0)]
+        return (slot[km], hi[km], lo[km], rep[km], pslot[pm], pval[pm]), space
+
     # -- one iteration --------------------------------------------------------------
     def run_iteration(self, prefetch_next, lookahead):
-        from .planes import DeviceResult, _records, _result_jobs
+        from .planes import DeviceResult, _records, _result_jobs, reduce_cap_bytes
         eng = self.eng
         eng.iteration += 1
         q = eng._seq
@@ -859,37 +922,50 @@ class GenericPlane:
                 src = rblob
         T["shuffle"] = time.time() - t1
         t2 = time.time()
-        with trace.range("mr.gen.order"):
-            if self.list_mode:
-                out = order_lists(*keys, src, R, eng.partmod, self.unique, self.dtype, space)
-            else:
-                out = order_fold(*keys, src, R, eng.partmod, self.phys)
-            counts = out["counts"].cpu().tolist()
-        _result_jobs(eng, res, counts, t1)
-        res.device = out
-        res.distinct_keys = int(out["hi"].numel())
         res.total_value = mp.rows
         res.failed_maps = failed
         res.bytes_shuffled, res.bytes_shuffled_remote = self._shuffled
-        if self.host_reduce and self.reducers.device_reduce:
-            # the reduce jobs, batched: device_reducefn over every key's list
-            with trace.range("mr.gen.reduce"):
-                keys = RD.KeyBatch(out["hi"], out["lo"], key_off=out["key_off"], key_blob=out["key_blob"])
-                red = self.reducers.reduce_device(keys, out["list_off"], out["list_val"])
-            out = {k: v for k, v in out.items() if k not in ("list_off", "list_val")}
-            out.update(red)
-            res.device = out
-            res._materialize = lambda o=out: host_partitions(o, R, self.dtype)
-        elif self.host_reduce:
-            # the reduce jobs: the user's reducefn over each key's list
-            c0 = time.process_time()
-            parts = host_partitions(out, R, self.dtype, self.reducefn, self.aci)
+        groups = self._reduce_groups(keys, src, space) if reduce_cap_bytes(eng) else None
+        c0 = time.process_time()
+        if groups is not None and len(groups[1]) > 1:
+            # reduce-side out-of-core (the reference's reduce streams its
+            # inputs, utils.lua:133-271): the rank's partitions in rounds of at
+            # most reduce_cap_mb, each ordered and reduced on the device and
+            # moved to host memory before the next
+            part, rounds = groups
+            parts, counts, nk = {}, [0] * R, 0
+            for grp in rounds:
+                sub, sub_space = self._select(keys, space, part, grp)
+                with trace.range("mr.gen.order"):
+                    out = self._order(sub, src, sub_space)
+                counts = [a + b for a, b in zip(counts, out["counts"].cpu().tolist())]
+                nk += int(out["hi"].numel())
+                dev_out, got = self._reduce(out)
+                parts.update(got if got is not None else host_partitions(dev_out, R, self.dtype))
+                del out, dev_out, sub
+            self.reduce_rounds = len(rounds)
+            _result_jobs(eng, res, counts, t1)
+            res.device = None
             res._parts = parts
+            res.distinct_keys = nk
+        else:
+            with trace.range("mr.gen.order"):
+                out = self._order(keys, src, space)
+                counts = out["counts"].cpu().tolist()
+            self.reduce_rounds = 1
+            _result_jobs(eng, res, counts, t1)
+            res.distinct_keys = int(out["hi"].numel())
+            dev_out, parts = self._reduce(out)
+            res.device = dev_out
+            if parts is not None:
+                res._parts = parts
+            else:
+                res._materialize = lambda o=dev_out: host_partitions(o, R, self.dtype)
+        if self.host_reduce and not self.reducers.device_reduce:
             cpu = time.process_time() - c0
+            parts = res._parts or {}
             for r in res.red_jobs:
                 r.cpu_time = cpu * len(parts.get(int(r.key), {}).get("py_vals", [])) / max(1, res.distinct_keys)
-        else:
-            res._materialize = lambda o=out: host_partitions(o, R, self.dtype)
         T["reduce"] = time.time() - t2
         T["iteration"] = time.time() - t_start
         return res

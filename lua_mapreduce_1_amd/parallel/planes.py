@@ -99,6 +99,43 @@ class DeviceResult:
         return self._parts
 
 
+def reduce_cap_bytes(eng) -> int:
+    mb = eng.params.get("reduce_cap_mb", TUNABLES.reduce_cap_mb)
+    return int(float(mb) * (1 << 20)) if mb else 0
+
+
+def round_groups(vol: np.ndarray, cap: int) -> list[list[int]]:
+    """Partitions (those with data) packed in order into rounds of at most
+    ``cap`` bytes each (a partition larger than the cap is a round of its
+    own: a partition's keys are ordered together)."""
+    groups: list[list[int]] = []
+    cur: list[int] = []
+    acc = 0
+    for p in np.flatnonzero(vol > 0).tolist():
+        v = int(vol[p])
+        if cur and acc + v > cap:
+            groups.append(cur)
+            cur, acc = [], 0
+        cur.append(p)
+        acc += v
+    if cur:
+        groups.append(cur)
+    return groups
+
+
+def partition_volumes(part: torch.Tensor, klen: torch.Tensor, nvals: torch.Tensor | None, R: int,
+                      val_bytes: int = 8) -> np.ndarray:
+    """Bytes a reduce round holds per partition: per key its words and key
+    bytes (32 + len), plus ``val_bytes`` per value (one host read)."""
+    w = klen.to(torch.int64) + 32
+    if nvals is not None:
+        w = w + val_bytes * nvals.to(torch.int64)
+    vol = torch.zeros(R, dtype=torch.int64, device=part.device)
+    if part.numel():
+        vol.index_add_(0, part.to(torch.int64), w)
+    return vol.cpu().numpy()
+
+
 def _records(eng, jobs, j0, j1, t0):
     recs = eng._new_records(jobs, j0, j1)
     for j in range(j0, j1):
@@ -487,14 +524,42 @@ class ListPlane:
         T["shuffle"] = time.time() - t1
         t2 = time.time()
         with trace.range("mr.list.order"):
-            out = self._order(hi, lo, rep, src, wstart, docs, R)
-        counts = out["counts_host"]
+            groups = None
+            cap = reduce_cap_bytes(eng)
+            if cap:
+                part, klen = ops.key_meta(hi, lo, rep, src, nparts=R)
+                vol = partition_volumes(part, klen, wstart[1:] - wstart[:-1], R)
+                groups = round_groups(vol, cap)
+            if groups is not None and len(groups) > 1:
+                # reduce-side out-of-core (reference: the reduce streams its
+                # inputs, utils.lua:133-271): partitions in rounds, each round
+                # ordered on the device and moved to host memory
+                parts, counts, nk, nd = {}, [0] * R, 0, 0
+                for grp in groups:
+                    sel = torch.nonzero(torch.isin(part, torch.tensor(grp, dtype=part.dtype, device=part.device)))
+                    out = self._order(hi, lo, rep, src, wstart, docs, R, sel=sel.view(-1))
+                    parts.update(_list_host(out, R))
+                    counts = [a + b for a, b in zip(counts, out["counts_host"])]
+                    nk += int(out["hi"].numel())
+                    nd += int(out["docs"].numel())
+                    del out
+                self.reduce_rounds = len(groups)
+                out = None
+            else:
+                out = self._order(hi, lo, rep, src, wstart, docs, R)
+                counts = out["counts_host"]
+                self.reduce_rounds = 1
         _result_jobs(eng, res, counts, t1)
-        res.device = out
-        res.distinct_keys = int(out["hi"].numel())
-        res.total_value = int(out["docs"].numel())
         res.failed_maps = failed
-        res._materialize = lambda o=out: _list_host(o, R)
+        if out is None:
+            res.device = None
+            res._parts = parts
+            res.distinct_keys, res.total_value = nk, nd
+        else:
+            res.device = out
+            res.distinct_keys = int(out["hi"].numel())
+            res.total_value = int(out["docs"].numel())
+            res._materialize = lambda o=out: _list_host(o, R)
         T["reduce"] = time.time() - t2
         T["iteration"] = time.time() - t_start
         return res
@@ -554,12 +619,16 @@ class ListPlane:
         vhi, vlo, vrep = rv.arrays()
         return vhi[wid2], vlo[wid2], vrep[wid2], rblob, wstart2, docs2, failed_total
 
-    def _order(self, hi, lo, rep, src, wstart, docs, R: int) -> dict:
+    def _order(self, hi, lo, rep, src, wstart, docs, R: int, sel: torch.Tensor | None = None) -> dict:
         """Words in (partition, exact key bytes) order with their posting
         lists: key partition = exact FNV-1 mod R, the words sorted by
         ops.exact_key_perm (long words sharing a prefix placed by their bytes,
         not their hash), a segmented gather of the lists; key bytes
         materialised."""
+        gsel = None
+        if sel is not None:  # a reduce round: only these words (indices into hi/lo/rep and the lists)
+            gsel = sel.to(torch.int64)
+            hi, lo, rep = hi[gsel], lo[gsel], rep[gsel]
         nw = hi.numel()
         part, klen = ops.key_meta(hi, lo, rep, src, nparts=R)
         if nw:
@@ -570,10 +639,11 @@ class ListPlane:
         else:
             perm = torch.zeros(0, dtype=torch.int64, device=hi.device)
         hi, lo, rep, part, klen = hi[perm], lo[perm], rep[perm], part[perm], klen[perm]
-        lens = (wstart[1:] - wstart[:-1])[perm]
+        gperm = perm if gsel is None else gsel[perm]  # rows of the full lists
+        lens = (wstart[1:] - wstart[:-1])[gperm]
         off, total = ops.exclusive_scan(lens)
         new_off = torch.cat([off, total])
-        docs = II.seg_gather(perm, wstart, new_off, docs) if nw else docs[:0]
+        docs = II.seg_gather(gperm, wstart, new_off, docs) if nw else docs[:0]
         koff, kblob = ops.gather_key_bytes(hi, lo, rep, src, lengths=klen)
         counts = ops.bincount(part, R) if nw else torch.zeros(R, dtype=torch.int64, device=hi.device)
         return {"hi": hi, "lo": lo, "key_off": koff, "key_blob": kblob, "list_off": new_off, "docs": docs,

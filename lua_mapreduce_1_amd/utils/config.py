@@ -60,6 +60,10 @@ class Tunables:
     sort_rounds: int = _knob("MR_SORT_ROUNDS", 24,
                              "keys per thread of the onesweep radix tiles of sorts of >= 4 M keys (256 x rounds "
                              "keys per tile; 16, 24 or 32)")
+    wc_map_config: int = _knob("MR_WC_MAP_CONFIG", 0,
+                               "word-count map kernel shape (csrc/hip/wordcount3.hip): 0 = 512 threads, 2048 LDS "
+                               "slots, 8 KiB spans, two workgroups per CU; 1 / 2 = 4096 slots over 32 / 64 KiB, one "
+                               "workgroup per CU; 3 = 1024 threads, 4096 slots, 32 KiB")
     arena_cap_mb: float = _knob("MR_ARENA_CAP_MB", 0.0,
                                 "SPMD: cap of a rank's HBM input arena, MiB (0 = the rank's whole input); a larger "
                                 "input is mapped in rounds through a ring of two arenas of this size")
@@ -68,6 +72,10 @@ class Tunables:
     record_cap_mb: float = _knob("MR_RECORD_CAP_MB", 0.0,
                                  "SPMD record plane: HBM budget for a rank's rows, MiB (0 = unbounded); more rows "
                                  "spill to host memory and are sorted externally (bucket pass + per-bucket sorts)")
+    reduce_cap_mb: float = _knob("MR_REDUCE_CAP_MB", 0.0,
+                                 "SPMD list / general planes: HBM budget of one reduce round, MiB (0 = one round); "
+                                 "a rank's partitions are ordered and reduced in rounds of at most this many key "
+                                 "and value bytes, each round's result moved to host memory")
     fused_tail: bool = _knob("MR_FUSED_TAIL", True, "fused reduce-side tail kernels (tail.hip)")
     pipeline: bool = _knob("MR_PIPELINE", True, "bench/proxies: map of iteration i+1 overlaps the tail of i")
     prefetch_single: bool = _knob("MR_PREFETCH_SINGLE", True, "prefetched inputs: one DMA per iteration")

@@ -105,7 +105,32 @@ def _generic_cols(R, device):
     return res, lambda: close_lists(got, importlib.import_module(SS).naive(splits))
 
 
-PLANES = {"fold": _fold, "list": _list, "records": _records, "generic": _generic, "generic_cols": _generic_cols}
+def _list_rounds(R, device):
+    """The list plane with reduce rounds (reduce_cap_mb) after the shuffle."""
+    import importlib
+    from lua_mapreduce_1_amd import spmd
+    from lua_mapreduce_1_amd.parallel.spmd import SplitStore
+    M = "lua_mapreduce_1_amd.examples.InvertedIndex"
+    splits = _text()
+    eng = spmd(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M, reduce_cap_mb=0.01,
+                    init_args={"nsplits": len(splits), "num_reducers": R}, table_capacity=1 << 14),
+               device=device, split_store=SplitStore(splits, pin=False))
+    res = eng.run()
+    mod = importlib.import_module(M)
+    return res, lambda: mod.RESULT == mod.naive_index(splits)
+
+
+def _generic_rounds(R, device):
+    from test_generic_plane import close_lists, run_engine
+    import comb_modules
+    splits = _text()
+    eng, res, got = run_engine("comb_modules", splits, device, {"mode": "topk", "num_reducers": R},
+                               reduce_cap_mb=0.01)
+    return res, lambda: close_lists(got, comb_modules.oracle(splits, "topk"))
+
+
+PLANES = {"fold": _fold, "list": _list, "records": _records, "generic": _generic, "generic_cols": _generic_cols,
+          "list_rounds": _list_rounds, "generic_rounds": _generic_rounds}
 
 
 def _rank(rank, world, port, q, plane):
