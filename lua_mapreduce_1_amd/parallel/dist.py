@@ -24,50 +24,6 @@ def env_world() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
-def gpu_numa_cpus(device) -> list[int] | None:
-    """CPUs of the NUMA node the GPU's PCIe root sits on (None if unknown).
-
-    The map phase streams every input byte host -> HBM over the GPU's own PCIe
-    link; pinned staging buffers on the far socket would cross the inter-socket
-    fabric (8 ranks x ~55 GB/s on a 2-socket node)."""
-    try:
-        p = torch.cuda.get_device_properties(device)
-        dom, bus, dev = getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", None), getattr(p, "pci_device_id", 0)
-        if bus is None:
-            return None
-        with open(f"/sys/bus/pci/devices/{dom:04x}:{bus:02x}:{dev:02x}.0/numa_node") as f:
-            node = int(f.read().strip())
-        if node < 0:
-            return None
-        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
-            spec = f.read().strip()
-    except (OSError, ValueError, RuntimeError, AttributeError):
-        return None
-    cpus: list[int] = []
-    for part in spec.split(","):
-        if "-" in part:
-            a, b = part.split("-")
-            cpus.extend(range(int(a), int(b) + 1))
-        elif part:
-            cpus.append(int(part))
-    return cpus or None
-
-
-def bind_to_gpu_numa(device) -> list[int] | None:
-    """Pin this process to its GPU's NUMA node (before pinned buffers are
-    allocated, so their pages are node-local).  ``MR_NUMA_BIND=0`` disables."""
-    if not TUNABLES.numa_bind or not hasattr(os, "sched_setaffinity"):
-        return None
-    cpus = gpu_numa_cpus(device)
-    if not cpus:
-        return None
-    allowed = os.sched_getaffinity(0)
-    use = [c for c in cpus if c in allowed]
-    if use and set(use) != allowed:
-        os.sched_setaffinity(0, use)
-    return use or None
-
-
 def init_from_env(backend: str | None = None, timeout_s: float | None = None, use_gpu: bool | None = None):
     """Initialise the default group from torchrun's env (no-op for WORLD_SIZE=1).
 
@@ -88,7 +44,8 @@ def init_from_env(backend: str | None = None, timeout_s: float | None = None, us
     device = torch.device("cuda", local) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
-        bind_to_gpu_numa(device)
+        from ..utils import numa
+        numa.bind_to_gpu(device.index or 0)  # pinned buffers allocated later land on the GPU's socket
     if world > 1 and not dist.is_initialized():
         # more ranks than GPUs (a rehearsal on a 1-GPU box): RCCL refuses two
         # ranks on one device, so such a job runs its collectives over gloo

@@ -10,8 +10,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 HEAD = """# tools/ — benchmarks, probes and profiling scripts
 
-Everything that produced a file under `profiles/` is here. `gpu_*.sh` and `prof_*.sh` are the `gpurun` command
-scripts (each step under its own `timeout`); the Python tools run on one GPU unless noted. Generated from each
+Benchmarks and probes behind the files under `profiles/`. `prof_*.sh` are `gpurun` command scripts; the one-shot
+checkpoint scripts of rounds 1-3 are archived in `profiles/scripts/`. The Python tools run on one GPU unless noted. Generated from each
 file's docstring or header comment by `tools/gen_tools_readme.py`.
 
 | File | What it does |
