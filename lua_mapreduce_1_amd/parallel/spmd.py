@@ -42,12 +42,12 @@ from ..runtime import modules
 from ..utils import STATUS
 from ..utils import trace
 from . import dist as D
+from .checkpoint import CheckpointMixin
+from .splits import SplitStore, WindowedSplitStore, _file_pads, assign_contiguous  # noqa: F401  (public here too)
+from .staging import N_ARENAS, StagingMixin
 
-
-N_ARENAS = 3
 # largest map table the sparsity rule asks for (2^25 slots = 1.3 GB of HBM)
 _MAX_SPARSE_CAP = 1 << 25
-_PREFETCH_SINGLE = TUNABLES.prefetch_single
 
 
 class _nullctx:
@@ -56,122 +56,6 @@ class _nullctx:
 
     def __exit__(self, *exc):
         return False
-
-
-class SplitStore:
-    """Host-resident input splits in ONE pinned buffer (the page-cache analogue
-    of the reference's split files).  Every split is followed by a newline so
-    tokens never straddle two splits.
-
-    ``offsets`` are global (every split's padded size is known to every rank,
-    for the byte-balanced job assignment); the buffer holds only the owned
-    splits ``own = (i0, i1)`` — a rank pins and reads just its share
-    (:meth:`from_files` / :meth:`from_blob` with ``rank, world``).  Those two
-    fill the buffer asynchronously with the native loader (ops/io.py);
-    :meth:`wait_ready` blocks until a range of splits has landed, so the
-    engine's host->HBM copies start while later splits are still being read."""
-
-    def __init__(self, splits: list[bytes] | None = None, pin: bool = True):
-        splits = splits or []
-        sizes = [len(s) + (0 if s[-1:] == b"\n" else 1) for s in splits]
-        self._layout(sizes, (0, len(splits)), pin)
-        view = self.buffer.numpy()
-        for i, s in enumerate(splits):
-            a = int(self.offsets[i])
-            view[a:a + len(s)] = np.frombuffer(s, dtype=np.uint8)
-            if sizes[i] > len(s):
-                view[a + len(s)] = 10
-
-    def _layout(self, sizes, own, pin: bool) -> None:
-        self.offsets = np.zeros(len(sizes) + 1, dtype=np.int64)
-        np.cumsum(np.asarray(sizes, dtype=np.int64), out=self.offsets[1:])
-        self.own = (int(own[0]), int(own[1]))
-        self.base = int(self.offsets[self.own[0]])
-        nbytes = int(self.offsets[self.own[1]]) - self.base
-        if pin and torch.cuda.is_available() and TUNABLES.pin_exact:
-            from ..ops import io as mio
-            self.buffer = mio.pinned_empty(nbytes)  # exact size: pinning is paid per page
-        else:
-            self.buffer = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin and torch.cuda.is_available())
-        self._load = None
-        self.paths = None
-
-    @classmethod
-    def _async(cls, paths, file_off, lens, pad, own, pin: bool, threads: int) -> "SplitStore":
-        self = cls.__new__(cls)
-        sizes = np.asarray(lens, dtype=np.int64) + np.asarray(pad, dtype=np.int64)
-        self._layout(sizes, own, pin)
-        i0, i1 = self.own
-        if i1 > i0:
-            from ..ops import io as mio
-            dst_off = self.offsets[i0:i1] - self.base
-            self._load = mio.AsyncLoad([paths[i] for i in range(i0, i1)], np.asarray(file_off)[i0:i1],
-                                       np.asarray(lens)[i0:i1], dst_off, np.asarray(pad)[i0:i1], self.buffer,
-                                       threads=threads)
-        return self
-
-    @classmethod
-    def from_files(cls, paths: list[str], rank: int = 0, world: int = 1, pin: bool = True,
-                   threads: int = 8) -> "SplitStore":
-        """One split per file (the reference's split files, WordCountBig
-        taskfn.lua:6-10).  Sizes come from stat; a file that does not end in
-        a newline is followed by one (the same rule as the
-        in-memory and blob stores, so line numbers agree); only this rank's
-        contiguous byte-balanced share is read."""
-        lens, pad = _file_pads(paths)
-        own = assign_contiguous([n + p for n, p in zip(lens, pad)], rank, world)
-        self = cls._async(list(paths), [0] * len(paths), lens, pad, own, pin, threads)
-        self.paths = list(paths)
-        return self
-
-    @classmethod
-    def from_blob(cls, path: str, offsets, rank: int = 0, world: int = 1, pin: bool = True,
-                  threads: int = 8) -> "SplitStore":
-        """Splits stored back to back in one file, split i at bytes
-        ``[offsets[i], offsets[i+1])`` (the benchmark's corpus cache)."""
-        offsets = np.asarray(offsets, dtype=np.int64)
-        lens = offsets[1:] - offsets[:-1]
-        mm = np.memmap(path, dtype=np.uint8, mode="r") if offsets[-1] else None
-        last = [int(mm[o - 1]) if n else 0 for o, n in zip(offsets[1:], lens)] if mm is not None else []
-        del mm
-        pad = [0 if (n and b == 10) else 1 for n, b in zip(lens, last)]
-        own = assign_contiguous((lens + np.asarray(pad, dtype=np.int64)).tolist(), rank, world)
-        return cls._async([path] * len(lens), offsets[:-1], lens, pad, own, pin, threads)
-
-    def __len__(self) -> int:
-        return len(self.offsets) - 1
-
-    def size(self, i: int) -> int:
-        return int(self.offsets[i + 1] - self.offsets[i])
-
-    def region(self, i0: int, i1: int) -> tuple[int, int]:
-        """Byte range of splits [i0, i1) in :attr:`buffer` (owned splits only)."""
-        if i0 < i1 and not (self.own[0] <= i0 and i1 <= self.own[1]):
-            raise ValueError(f"splits [{i0}, {i1}) are not held by this store (own {self.own})")
-        return int(self.offsets[i0]) - self.base, int(self.offsets[i1]) - self.base
-
-    def all_ready(self) -> bool:
-        return self._load is None or self._load.done() == self._load.n
-
-    def wait_ready(self, i0: int, i1: int) -> None:
-        """Block until splits [i0, i1) are in the buffer."""
-        if self._load is not None and i1 > i0:
-            self._load.wait_jobs(i0 - self.own[0], i1 - self.own[0])
-
-    def finish_loading(self) -> None:
-        if self._load is not None:
-            self._load.wait()
-            self._load = None
-
-    def newline_counts(self, i0: int, i1: int) -> list[int]:
-        """Newlines of each owned split [i0, i1) (its padding newline included)."""
-        self.finish_loading()
-        view = self.buffer.numpy() if self.buffer.device.type == "cpu" else self.buffer.cpu().numpy()
-        out = []
-        for i in range(i0, i1):
-            a, b = self.region(i, i + 1)
-            out.append(int(np.count_nonzero(view[a:b] == 10)))
-        return out
 
 
 _STREAMS: dict = {}
@@ -190,101 +74,6 @@ def _engine_streams(device):
     if st is None:
         st = _STREAMS[device] = (torch.cuda.Stream(device), [torch.cuda.Stream(device), torch.cuda.Stream(device)])
     return st[0], list(st[1])
-
-
-class WindowedSplitStore(SplitStore):
-    """Split files read on demand into a ring of two pinned windows (inputs
-    larger than host memory): the engine's streaming rounds
-    (``arena_cap_mb``) ask for one round of splits at a time
-    (:meth:`load_round`), the native loader reads them into the free window,
-    and the window is released once the round's host->HBM copies have
-    completed.  Offsets/sizes of every split are known up front (stat)."""
-
-    def __init__(self, paths: list[str], rank: int = 0, world: int = 1, window_mb: float = 256,
-                 pin: bool = True, threads: int = 8):
-        lens, pad = _file_pads(paths)
-        self.paths = list(paths)
-        self._lens, self._pad = lens, pad
-        self.offsets = np.zeros(len(paths) + 1, dtype=np.int64)
-        np.cumsum(np.asarray(lens, dtype=np.int64) + np.asarray(pad, dtype=np.int64), out=self.offsets[1:])
-        self.own = assign_contiguous([n + p for n, p in zip(lens, pad)], rank, world)
-        self.base = int(self.offsets[self.own[0]])
-        self.window = int(window_mb * (1 << 20))
-        self.threads = threads
-        self._win = [torch.empty(self.window, dtype=torch.uint8, pin_memory=pin and torch.cuda.is_available())
-                     for _ in range(2)]
-        self._released = [None, None]
-        self._load = None
-        self.buffer = None  # no whole-share buffer: rounds only
-
-    def all_ready(self) -> bool:
-        return True
-
-    def wait_ready(self, i0: int, i1: int) -> None:
-        return None
-
-    def load_round(self, i0: int, i1: int, slot: int) -> torch.Tensor:
-        """Splits [i0, i1) (each followed by a newline) in window ``slot``;
-        waits until the window's previous copies have completed."""
-        ev = self._released[slot]
-        if ev is not None:
-            ev.synchronize()
-        nbytes = int(self.offsets[i1] - self.offsets[i0])
-        if nbytes > self.window:
-            raise ValueError(f"round of {nbytes} bytes exceeds the {self.window}-byte host window")
-        from ..ops import io as mio
-        w = self._win[slot]
-        ld = mio.AsyncLoad(self.paths[i0:i1], [0] * (i1 - i0), self._lens[i0:i1], self.offsets[i0:i1] - self.offsets[i0],
-                           self._pad[i0:i1], w, threads=self.threads)
-        ld.wait()
-        return w[:nbytes]
-
-    def release(self, slot: int, event) -> None:
-        self._released[slot] = event
-
-    def newline_counts(self, i0: int, i1: int) -> list[int]:
-        """Newlines of each split [i0, i1) (its padding newline included),
-        counted by reading the files in 16 MiB blocks."""
-        out = []
-        for i in range(i0, i1):
-            n = 0
-            with open(self.paths[i], "rb") as f:
-                while True:
-                    b = f.read(16 << 20)
-                    if not b:
-                        break
-                    n += b.count(b"\n")
-            out.append(n + int(self._pad[i]))
-        return out
-
-
-def _file_pads(paths) -> tuple[list[int], list[int]]:
-    """(sizes, pads): pad 1 when a file's last byte is not a newline (then a
-    newline follows the split: tokens never straddle splits, and the next
-    split's first line gets its own global line number)."""
-    lens, pad = [], []
-    for p in paths:
-        n = os.path.getsize(p)
-        last = b""
-        if n:
-            with open(p, "rb") as f:
-                f.seek(n - 1)
-                last = f.read(1)
-        lens.append(n)
-        pad.append(0 if last == b"\n" else 1)
-    return lens, pad
-
-
-def assign_contiguous(weights, rank: int, world: int) -> tuple[int, int]:
-    """Contiguous block [j0, j1) of items for ``rank``, balanced by weight."""
-    n = len(weights)
-    if world == 1:
-        return 0, n
-    c = np.concatenate([[0.0], np.cumsum(np.asarray(weights, dtype=np.float64))])
-    tot = c[-1]
-    cuts = [int(np.searchsorted(c, tot * r / world, side="left")) for r in range(world + 1)]
-    cuts[0], cuts[-1] = 0, n
-    return cuts[rank], max(cuts[rank], cuts[rank + 1])
 
 
 class JobRecord:
@@ -378,7 +167,7 @@ class IterationResult:
         return self._total
 
 
-class SPMDEngine:
+class SPMDEngine(StagingMixin, CheckpointMixin):
     def __init__(self, params: dict, group=None, device=None, split_store: SplitStore | None = None,
                  chunk_mb: tuple = (2, 8, 32), verbose: bool = False, table_capacity: int = 1 << 20,
                  tail_mb: tuple = (8, 2)):
@@ -581,341 +370,6 @@ class SPMDEngine:
     def _use(self, q: int) -> None:
         """Make iteration q's arena, table and stream current."""
         self.slot, self.tslot = q % N_ARENAS, q % 2
-
-    def _plan_chunks(self, ids: list[int], slot: int, single: bool = False):
-        """Chunking of a contiguous split range (cached per range): boundaries
-        at split boundaries, sizes ramping up (the first copy is exposed), big
-        in the middle, ramping down at the end (the last kernel is exposed) —
-        also for small per-rank inputs.  Returns (split bounds, arena views,
-        pinned host views, reusable events)."""
-        a, b = self.splits.region(ids[0], ids[-1] + 1)
-        nbytes = b - a
-        if self.arenas[slot] is None or self.arenas[slot].numel() < nbytes:
-            self.arenas[slot] = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-            self._arena_holds.pop(slot, None)
-            self._plans = {k: v for k, v in self._plans.items() if k[2] != slot}
-
-        arena = self.arenas[slot]
-        offs = self.splits.offsets
-        sizes = []
-        rem = nbytes
-        up = list(self.chunk_bytes[:-1])
-        big = self.chunk_bytes[-1]
-        tail = list(self.tail_bytes)
-        if single:  # prefetched copies: landed long before the map, one DMA is enough
-            up, big, tail = [], max(nbytes, 1), []
-        ts = sum(tail)
-        while up and rem > up[0] + ts:
-            sizes.append(up.pop(0))
-            rem -= sizes[-1]
-        while rem > big + ts:
-            sizes.append(big)
-            rem -= big
-        if rem > ts:
-            sizes.append(rem - ts)
-            rem = ts
-        for t in tail:
-            if rem <= 0:
-                break
-            sizes.append(min(t, rem))
-            rem -= sizes[-1]
-        rel = offs[ids[0]:ids[-1] + 2] - offs[ids[0]]
-        bidx = np.searchsorted(rel, np.cumsum(sizes), side="left")
-        bounds = sorted({0, len(ids)} | {min(int(x), len(ids)) for x in bidx})
-        host = self.splits.buffer
-        views, host_views, events = [], [], []
-        for i in range(len(bounds) - 1):
-            ca, cb = self.splits.region(ids[0] + bounds[i], ids[0] + bounds[i + 1])
-            views.append(arena[ca - a:cb - a])
-            host_views.append(host[ca:cb])
-            events.append(torch.cuda.Event() if self.copy_stream is not None else None)
-        return bounds, views, host_views, events, ids[0]
-
-    def _get_plan(self, ids: list[int], slot: int, single: bool = False):
-        key = (ids[0], len(ids), slot, single)
-        plan = self._plans.get(key)
-        if plan is None and self.copy_stream is not None and self._can_pipeline() and self.prime_plans and not getattr(
-                self, "_priming", False):
-            # a pure taskfn maps the same splits every iteration: build (and
-            # prime) both copy plans of every arena now, so that no plan is
-            # first used — and primed — inside a later, timed iteration
-            self._priming = True
-            try:
-                for sl in range(N_ARENAS):
-                    for sg in (False, True):
-                        self._get_plan(ids, sl, sg)
-            finally:
-                self._priming = False
-            return self._plans[key]
-        if plan is None:
-            plan = self._plan_chunks(ids, slot, single)
-            self._plans[key] = plan
-            if self.copy_stream is not None and self.prime_plans:
-                # the first two rounds of a plan's copies behind a cross-stream
-                # wait each stalled the host 5-7 ms inside hipMemcpyAsync (a
-                # one-time runtime set-up, tools/first_iter.py): take that hit
-                # here, once per plan, not in an iteration's copy issue
-                for _ in range(2):
-                    self._issue_copies(plan, wait_for=torch.cuda.current_stream(self.device))
-                    self.copy_stream.synchronize()
-        return plan
-
-    def _issue_copies(self, plan, wait_for=None) -> None:
-        bounds, views, host_views, events, id0 = plan
-        streaming = not self.splits.all_ready()
-        cs = self.copy_stream
-        if wait_for is not None:
-            # the arena may still be read by earlier work (a reused event: a
-            # fresh one per iteration grows the runtime's event/signal pool)
-            ev0 = self._copy_gate_event()
-            ev0.record(wait_for)
-            cs.wait_event(ev0)
-        from ..ops import _hip
-        sp = _hip.stream_ptr(cs)
-        for i, (dst, src, ev) in enumerate(zip(views, host_views, events)):
-            if streaming:  # the native loader is still reading: copy each chunk once it has landed
-                self.splits.wait_ready(id0 + bounds[i], id0 + bounds[i + 1])
-            # direct hipMemcpyAsync (pinned -> HBM) instead of copy_: no
-            # host-allocator event bookkeeping per chunk (it stalled the host)
-            _hip.call("mr_memcpy_async", _hip.ptr(dst), _hip.ptr(src), dst.numel(), 1, sp)
-            ev.record(cs)
-
-    def _copy_gate_event(self):
-        ev0 = getattr(self, "_copy_gate", None)
-        if ev0 is None:
-            ev0 = self._copy_gate = torch.cuda.Event()
-        return ev0
-
-    def _split_ids(self, jobs, j0, j1):
-        ids = [int(v["split"] if isinstance(v, dict) else v) for _, v in jobs[j0:j1]]
-        if ids and ids != list(range(ids[0], ids[0] + len(ids))):
-            raise ValueError("split jobs of a rank must be contiguous splits")
-        return ids
-
-    def _prefetch(self, jobs, j0, j1, q: int) -> None:
-        """Start iteration q's host->HBM copies (same splits: the taskfn is
-        pure) into its arena now, so the copy engine keeps streaming while
-        earlier iterations map, reduce and finalize.  Only for a pure taskfn
-        and split inputs; a mismatching plan is re-copied when q runs."""
-        if not self._can_pipeline():
-            return
-        aslot = q % N_ARENAS
-        ids = self._split_ids(jobs, j0, j1)
-        if not ids or aslot in self._inflight:
-            return
-        if self.resident and self._arena_holds.get(aslot) == (ids[0], len(ids)):
-            return  # HBM-resident input: the arena still holds these splits
-        plan = self._get_plan(ids, aslot, single=_PREFETCH_SINGLE)
-        # arenas[aslot] was last read by iteration q - N_ARENAS, which has
-        # completed (its finalize synchronised): no stream dependency needed
-        self._issue_copies(plan)
-        self._inflight[aslot] = self._arena_holds[aslot] = (ids[0], len(ids))
-
-    # -- streaming: inputs larger than the HBM arena (SURVEY.md §5.7) ----------
-    def _arena_cap(self) -> int:
-        mb = self.params.get("arena_cap_mb", TUNABLES.arena_cap_mb)
-        return int(float(mb) * (1 << 20)) if mb else 0
-
-    def _streaming(self, ids) -> bool:
-        cap = self._arena_cap()
-        if not cap or not ids:
-            return False
-        if self.plane_kind not in ("fold", "list", "generic"):
-            raise ValueError(f"arena_cap_mb / MR_ARENA_CAP_MB streaming is implemented for the fold, list and "
-                             f"general planes (this job runs the {self.plane_kind} plane, which spills with "
-                             f"record_cap_mb)")
-        a, b = self.splits.region(ids[0], ids[-1] + 1)
-        return b - a > cap
-
-    def _stage_streaming(self, jobs, j0, ids):
-        """Map a rank's input through a ring of two arena slots of the capped
-        size, in rounds of whole splits: round r+1's copies land while round r
-        maps; after a round the long keys it introduced move their bytes to a
-        persistent key heap at the front of the same buffer (the reference's
-        streaming reduce keeps only what it still needs, utils.lua:206-271),
-        so the slot can be refilled.  One buffer = one byte source for the
-        table's rep words: [key heap | slot 0 | slot 1]."""
-        A = self._arena_cap()
-        st = self.splits
-        sizes = [st.size(i) for i in ids]
-        if max(sizes) > A:
-            raise ValueError(f"a split of {max(sizes)} bytes does not fit the {A}-byte arena cap")
-        rounds, k0, acc = [], 0, 0
-        for k, sz in enumerate(sizes):
-            if acc + sz > A:
-                rounds.append((k0, k))
-                k0, acc = k, 0
-            acc += sz
-        rounds.append((k0, len(ids)))
-        a0, b0 = st.region(ids[0], ids[-1] + 1)
-        heap_mb = getattr(self, "_stream_heap_mb", TUNABLES.stream_heap_mb)
-        H = max(1 << 16, min(b0 - a0, int(heap_mb * (1 << 20))))
-        need = H + 2 * A
-        buf = getattr(self, "_stream_buf", None)
-        if buf is None or buf.numel() < need:
-            buf = self._stream_buf = torch.empty(need, dtype=torch.uint8, device=self.device)
-            self._stream_heap = torch.zeros(2, dtype=torch.int64, device=self.device)
-        self._stream_H = H
-        self.arenas[self.slot] = buf
-        self._arena_holds.pop(self.slot, None)
-        heap = self._stream_heap
-        heap.zero_()
-        cs = self.copy_stream
-        host = st.buffer
-        piece = max(self.chunk_bytes[-1], 1)
-        plan = []  # per round: [(job range, buffer offset, host offset, bytes)]
-        for r, (k0, k1) in enumerate(rounds):
-            slot_off = H + (r % 2) * A
-            ra = st.region(ids[k0], ids[k0] + 1)[0]
-            pieces, k = [], k0
-            while k < k1:
-                e, acc = k, 0
-                while e < k1 and (e == k or acc + sizes[e] <= piece):
-                    acc += sizes[e]
-                    e += 1
-                pa = st.region(ids[k], ids[k] + 1)[0]
-                pieces.append(((j0 + k, j0 + e), slot_off + pa - ra, pa, acc, (ids[k], ids[e - 1] + 1)))
-                k = e
-            plan.append(pieces)
-        windowed = isinstance(st, WindowedSplitStore)
-
-        def host_of(r):
-            """Host bytes of round r (a window of a windowed store) and the
-            host offset of its first byte."""
-            k0, k1 = rounds[r]
-            if windowed:
-                return st.load_round(ids[k0], ids[k1 - 1] + 1, r % 2), st.region(ids[k0], ids[k0] + 1)[0]
-            return host, 0
-
-        if cs is None:  # CPU: copy, map, rehome round by round
-            for r, pieces in enumerate(plan):
-                h, hb = host_of(r)
-                for jr, off, ha, n, sp in pieces:
-                    st.wait_ready(*sp)
-                    buf[off:off + n].copy_(h[ha - hb:ha - hb + n])
-                    yield jr, buf[off:off + n]
-                self._round_end(buf, H + (r % 2) * A, H + (r % 2) * A + A, heap, H)
-            return
-        from ..ops import _hip
-        cur = torch.cuda.current_stream(self.device)
-        evs = getattr(self, "_stream_events", None)
-        if evs is None:
-            evs = self._stream_events = {"gate": torch.cuda.Event(), "free": [torch.cuda.Event(), torch.cuda.Event()],
-                                         "piece": []}
-        sp_cs = _hip.stream_ptr(cs)
-
-        def issue(r):
-            pe = []
-            h, hb = host_of(r)
-            for jr, off, ha, n, sp in plan[r]:
-                st.wait_ready(*sp)
-                _hip.call("mr_memcpy_async", _hip.ptr(buf[off:off + n]), _hip.ptr(h[ha - hb:ha - hb + n]), n, 1,
-                          sp_cs)
-                ev = torch.cuda.Event()
-                ev.record(cs)
-                pe.append(ev)
-            if windowed:
-                st.release(r % 2, pe[-1])  # the window is free once its copies are done
-            return pe
-
-        # the buffer may still be read by the previous iteration's tail
-        evs["gate"].record(cur)
-        cs.wait_event(evs["gate"])
-        issued = {0: issue(0)}
-        if len(plan) > 1:
-            issued[1] = issue(1)
-        for r, pieces in enumerate(plan):
-            for (jr, off, ha, n, sp), ev in zip(pieces, issued.pop(r)):
-                cur.wait_event(ev)
-                yield jr, buf[off:off + n]
-            self._round_end(buf, H + (r % 2) * A, H + (r % 2) * A + A, heap, H)
-            if r + 2 < len(plan):
-                evs["free"][r % 2].record(cur)  # slot r % 2 is free once round r's map and rehome ran
-                cs.wait_event(evs["free"][r % 2])
-                issued[r + 2] = issue(r + 2)
-
-    def _round_end(self, buf, lo: int, hi: int, heap, H: int) -> None:
-        """After a streamed round: the fold plane moves the long keys the
-        round introduced to the key heap; the list plane also groups the
-        round's postings (ListPlane.stream_round_end)."""
-        hook = getattr(self.plane, "stream_round_end", None) if self.plane is not None else None
-        if hook is not None:
-            hook(buf, lo, hi, heap, H)
-        else:
-            self.table.rehome_long_keys(buf, lo, hi, heap, H)
-
-    def _stage_chunks(self, jobs, j0, j1):
-        """Yield (job index range, device tensor) chunks, H2D overlapped with compute."""
-        if self.device_input == "split":
-            ids = self._split_ids(jobs, j0, j1)
-            if not ids:
-                return
-            if self._streaming(ids):
-                yield from self._stage_streaming(jobs, j0, ids)
-                return
-            cs = self.copy_stream
-            key = (ids[0], len(ids))
-            prefetched = cs is not None and self._inflight.pop(self.slot, None) == key
-            if self.resident and not prefetched and self._arena_holds.get(self.slot) == key:
-                # HBM-resident input: these splits were copied into this arena by
-                # an earlier, completed iteration — map them in place
-                a, b = self.splits.region(ids[0], ids[-1] + 1)
-                yield (j0, j0 + len(ids)), self.arena[:b - a]
-                return
-            plan = self._get_plan(ids, self.slot, single=prefetched and _PREFETCH_SINGLE)
-            bounds, views, host_views, events, _ = plan
-            if cs is not None and not prefetched and not self.splits.all_ready():
-                # input still being read from files (cold start): each chunk is
-                # copied as soon as its splits have landed and mapped right
-                # behind its copy, so file reads, PCIe and the map overlap
-                cur = torch.cuda.current_stream(self.device)
-                with trace.range("mr.copies"):
-                    gate = self._copy_gate_event()
-                    gate.record(cur)
-                    cs.wait_event(gate)
-                from ..ops import _hip
-                sp = _hip.stream_ptr(cs)
-                for i in range(len(views)):
-                    self.splits.wait_ready(ids[0] + bounds[i], ids[0] + bounds[i + 1])
-                    _hip.call("mr_memcpy_async", _hip.ptr(views[i]), _hip.ptr(host_views[i]), views[i].numel(), 1, sp)
-                    events[i].record(cs)
-                    cur.wait_event(events[i])
-                    yield (j0 + bounds[i], j0 + bounds[i + 1]), views[i]
-                self._arena_holds[self.slot] = key
-                return
-            if cs is not None:
-                cur = torch.cuda.current_stream(self.device)
-                if not prefetched:
-                    with trace.range("mr.copies"):
-                        self._issue_copies(plan, wait_for=cur)
-                    self._arena_holds[self.slot] = key
-                # chunks whose copies have already landed (prefetched during the
-                # previous iteration's tail) are mapped by ONE launch: a launch's
-                # ramp-up and drain cost more than its chunking saves
-                done = 0
-                while done < len(events) and events[done].query():
-                    done += 1
-                i0 = 0
-                if done >= 2:
-                    a0 = views[0].data_ptr() - self.arena.data_ptr()
-                    nb = sum(v.numel() for v in views[:done])
-                    yield (j0 + bounds[0], j0 + bounds[done]), self.arena[a0:a0 + nb]
-                    i0 = done
-                for i in range(i0, len(views)):
-                    cur.wait_event(events[i])
-                    yield (j0 + bounds[i], j0 + bounds[i + 1]), views[i]
-            else:
-                for i, (dst, src) in enumerate(zip(views, host_views)):
-                    self.splits.wait_ready(ids[0] + bounds[i], ids[0] + bounds[i + 1])
-                    dst.copy_(src)
-                    yield (j0 + bounds[i], j0 + bounds[i + 1]), dst
-        elif self.device_input == "file":
-            from ..ops import io as mio
-            for j in range(j0, j1):
-                yield (j, j + 1), mio.load_file(jobs[j][1], self.device)
-        else:
-            for j in range(j0, j1):
-                yield (j, j + 1), jobs[j][1]
 
     def _timer(self):
         """The device timer of the current slot (None: timing off / CPU)."""
@@ -1545,197 +999,6 @@ class SPMDEngine:
         if self.world > 1:
             lines.append("# Ranks %d (sums over every rank's jobs; cluster times = slowest rank)" % self.world)
         return "\n".join(lines) + "\n"
-
-    # -- checkpoint / resume and fault injection -------------------------------
-    def _map_ckpt_path(self, iteration: int | None = None) -> str | None:
-        """This rank's map output of an iteration (``checkpoint_dir`` only):
-        written after the map phase, so a relaunch after a failure later in
-        the iteration (shuffle, reduce, another rank's map) re-runs only the
-        maps that had not finished — this rank's block of splits is restored
-        instead of re-mapped (the reference keeps map outputs
-        until the reduce consumes them, job.lua:293, server.lua:475-481)."""
-        if not self.checkpoint_dir:
-            return None
-        import hashlib
-        import json
-        key = hashlib.sha1(json.dumps(self._manifest_key(), sort_keys=True, default=repr).encode()).hexdigest()[:12]
-        it = self.iteration if iteration is None else iteration
-        return os.path.join(self.checkpoint_dir, "%s.map.it%d.r%d.w%d.%s" % (self.result_ns, it, self.rank,
-                                                                           self.world, key))
-
-    def _save_job_status(self, recs, j0: int, j1: int) -> None:
-        """Next to a map checkpoint: the jobs of this rank's block that did
-        not end WRITTEN (FAILED / BROKEN, with their repetitions), written
-        before the checkpoint itself — a restore then reports the same failed
-        maps as the run that wrote it (a failed job stays FAILED,
-        server.lua:194-205)."""
-        path = self._map_ckpt_path()
-        if path is None:
-            return
-        import json
-        bad = {str(j): [int(recs[j].status), int(recs[j].repetitions)] for j in range(j0, j1)
-               if recs[j].status in (STATUS.FAILED, STATUS.BROKEN)}
-        if not bad:
-            if os.path.exists(path + ".jobs.json"):
-                os.remove(path + ".jobs.json")  # a stale record of an earlier launch
-            return
-        os.makedirs(self.checkpoint_dir, exist_ok=True)
-        tmp = path + ".jobs.json.tmp"
-        with open(tmp, "w") as f:
-            json.dump(bad, f)
-            f.flush()
-            os.fsync(f.fileno())
-        os.replace(tmp, path + ".jobs.json")
-
-    def _restore_job_status(self, recs, j0: int, j1: int) -> None:
-        """The rank's map jobs after a restore: WRITTEN, except those its
-        checkpoint recorded as failed."""
-        import json
-        now = time.time()
-        for j in range(j0, j1):
-            recs[j].status, recs[j].started, recs[j].written, recs[j].worker = STATUS.WRITTEN, now, now, self.rank
-        path = self._map_ckpt_path()
-        if path is None or not os.path.exists(path + ".jobs.json"):
-            return
-        with open(path + ".jobs.json") as f:
-            bad = json.load(f)
-        for j, (st, reps) in bad.items():
-            j = int(j)
-            if j0 <= j < j1:
-                recs[j].status, recs[j].repetitions = st, reps
-
-    def _save_map(self, n: int, overflow: bool, recs=None, j0: int = 0, j1: int = 0) -> None:
-        path = self._map_ckpt_path()
-        if path is None or self.plane_kind != "fold" or overflow:
-            return
-        if recs is not None:
-            self._save_job_status(recs, j0, j1)
-        from ..runtime import codec
-        hi, lo, val, rep = self.table.compact((n, False))
-        _, ln = ops.key_meta(hi, lo, rep, self._source(), want_part=False)
-        off, blob = ops.gather_key_bytes(hi, lo, rep, self._source(), lengths=ln)
-        h = lambda t: t.detach().cpu().numpy()  # noqa: E731
-        data = codec.encode_columnar(h(hi).view(np.uint64), h(lo).view(np.uint64), h(val), h(off), h(blob))
-        os.makedirs(self.checkpoint_dir, exist_ok=True)
-        tmp = path + ".tmp"
-        with open(tmp, "wb") as f:
-            f.write(data)
-            f.flush()
-            os.fsync(f.fileno())
-        os.replace(tmp, path)
-
-    def _restore_map(self, jobs, recs, j0: int, j1: int) -> bool:
-        """Load this rank's map output of the current iteration from its
-        checkpoint, if an earlier launch wrote it: the table is refilled from
-        the saved keys (their bytes become the tail's key source) and the
-        rank's map jobs are WRITTEN without running."""
-        path = self._map_ckpt_path()
-        if path is None or self.plane_kind != "fold" or not os.path.exists(path):
-            return False
-        from ..runtime import codec
-        with open(path, "rb") as f:
-            cols = codec.decode_columnar(f.read())
-        d = self.device
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(d)  # noqa: E731
-        koff = cols["key_off"].astype(np.int64)
-        lens = np.diff(koff).astype(np.uint64)
-        rep = t(((koff[:-1].astype(np.uint64)) << np.uint64(24)) | lens)
-        blob = torch.from_numpy(np.concatenate([cols["key_blob"], np.zeros(1, np.uint8)])).to(d)
-        self._restored_src = blob
-        n = int(cols["hi"].size)
-        if 2 * n > self.table.cap:
-            self.table = ops.HashTable(ops.next_pow2(4 * n), device=d, op=self.op)
-            self._table_capacity = self.table.cap
-        timer = self._timer()
-        if timer is not None:
-            timer.begin()
-        self.table.insert(t(cols["hi"]), t(cols["lo"]), t(cols["val"]), rep, src=blob)
-        self.maps_restored += 1
-        self._restore_job_status(recs, j0, j1)
-        self._chunks[self.tslot] = []
-        self._log("# rank %d: map of iteration %d restored from %s\n" % (self.rank, self.iteration, path))
-        sys.stderr.write("# rank %d: map of iteration %d restored from its checkpoint\n" % (self.rank, self.iteration))
-        return True
-
-    def _drop_map_ckpt(self, iteration: int) -> None:
-        path = self._map_ckpt_path(iteration)
-        for p in (path, path + ".jobs.json") if path is not None else ():
-            if os.path.exists(p):
-                os.remove(p)
-
-    def _manifest_path(self) -> str | None:
-        if not self.checkpoint_dir:
-            return None
-        return os.path.join(self.checkpoint_dir, "%s.spmd.json" % self.result_ns)
-
-    def _manifest_key(self) -> dict:
-        """Identity of the job a manifest belongs to: a relaunch with other
-        modules, partition count or init args starts from scratch."""
-        import hashlib
-        import json
-        p = self.params
-        try:
-            args = json.dumps(p.get("init_args"), sort_keys=True, default=repr)
-        except (TypeError, ValueError):
-            args = repr(p.get("init_args"))
-        return {k: p.get(k) for k in ("taskfn", "mapfn", "partitionfn", "reducefn", "finalfn", "combinerfn",
-                                      "num_partitions")} | {
-            "world": self.world, "init_args": hashlib.sha1(args.encode()).hexdigest()}
-
-    def _load_manifest(self) -> int:
-        """Iterations already finished by an earlier launch of this same task
-        (server.lua:469-502 restart semantics: an unfinished task resumes, a
-        FINISHED one starts again from scratch).  Rank 0 decides, all agree."""
-        start = 0
-        path = self._manifest_path()
-        if self.rank == 0 and path and os.path.exists(path):
-            import json
-            with open(path) as f:
-                m = json.load(f)
-            if m.get("key") == self._manifest_key() and not m.get("finished"):
-                start = int(m.get("iteration", 0))
-        if self.world > 1:
-            start = D.broadcast_object(start, 0, self.group, self.device if self.device.type == "cuda" else None)
-        return start
-
-    def _save_manifest(self, finished: bool) -> None:
-        path = self._manifest_path()
-        if self.rank != 0 or not path:
-            return
-        import json
-        os.makedirs(self.checkpoint_dir, exist_ok=True)
-        tmp = path + ".tmp"
-        with open(tmp, "w") as f:
-            json.dump({"key": self._manifest_key(), "iteration": self.iteration, "finished": finished,
-                       "time": time.time()}, f)
-            f.flush()
-            os.fsync(f.fileno())
-        os.replace(tmp, path)  # atomic: a crash leaves the old or the new manifest
-
-    def _maybe_inject_fault(self, phase: str = "start") -> None:
-        """``MR_SPMD_FAULT=<iteration>:<rank>:raise|exit[:<attempt>[:<phase>]]``
-        (SURVEY.md §5.3): that rank fails in that iteration — at its start
-        (phase ``start``, the default) or after the map phase (``shuffle``:
-        every rank's map output of the iteration is already checkpointed) —
-        ``exit`` leaves its peers blocked in a collective, as a lost GPU or
-        node would."""
-        spec = os.environ.get("MR_SPMD_FAULT", TUNABLES.spmd_fault)
-        if not spec:
-            return
-        f = spec.split(":")
-        it, rk, action = f[:3]
-        want_phase = f[4] if len(f) > 4 and f[4] else "start"
-        cur = self.iteration + 1 if phase == "start" else self.iteration
-        if want_phase != phase or int(it) != cur or int(rk) != self.rank:
-            return
-        # optional 4th field: only in that torchrun attempt (0 = first launch; empty = any)
-        if len(f) > 3 and f[3] != "" and int(f[3]) != int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")):
-            return
-        if action == "exit":
-            sys.stderr.write("# injected fault: rank %d exits at iteration %d (%s)\n" % (self.rank, cur, phase))
-            sys.stderr.flush()
-            os._exit(17)
-        raise RuntimeError("injected fault: rank %d at iteration %d (%s)" % (self.rank, cur, phase))
 
     def run(self) -> IterationResult:
         """Iterate until finalfn returns something other than "loop".  With a

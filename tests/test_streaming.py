@@ -98,6 +98,8 @@ def test_streaming_key_heap_grows(request, monkeypatch, on_gpu):
     from lua_mapreduce_1_amd.parallel import spmd as S
     dev = request.getfixturevalue("gpu") if on_gpu else "cpu"
     monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(S.TUNABLES, stream_heap_mb=0.07))
+    from lua_mapreduce_1_amd.parallel import staging as _ST
+    monkeypatch.setattr(_ST, "TUNABLES", dataclasses.replace(_ST.TUNABLES, stream_heap_mb=0.07))
     splits = [colliding_text(40 + i, ntok=20000, nlong=3000) for i in range(4)]
     got, eng = _run(S.SplitStore(splits, pin=on_gpu), dev, cap_mb=1.0)
     assert got == _want(splits)
@@ -152,6 +154,8 @@ def test_list_plane_stream_heap_grows(request, monkeypatch, on_gpu):
     from lua_mapreduce_1_amd.parallel import spmd as S
     dev = request.getfixturevalue("gpu") if on_gpu else "cpu"
     monkeypatch.setattr(S, "TUNABLES", dataclasses.replace(S.TUNABLES, stream_heap_mb=0.07))
+    from lua_mapreduce_1_amd.parallel import staging as _ST
+    monkeypatch.setattr(_ST, "TUNABLES", dataclasses.replace(_ST.TUNABLES, stream_heap_mb=0.07))
     monkeypatch.setattr(P, "TUNABLES", dataclasses.replace(P.TUNABLES, stream_heap_mb=0.07))
     splits = [colliding_text(80 + i, ntok=20000, nlong=3000) for i in range(4)]
     cap = max(len(s) for s in splits) + 1
