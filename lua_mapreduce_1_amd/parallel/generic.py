@@ -258,6 +258,7 @@ class GenericMap:
         self.src.begin(arena)
         self.host = []
         self.rows = 0
+        self.combines = 0
 
     def insert(self, n: int, values, **kw) -> None:
         if n == 0:

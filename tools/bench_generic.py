@@ -168,6 +168,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--jobs", default="bigram,scores")
     ap.add_argument("--score-lines", type=int, default=8_000_000)
+    ap.add_argument("--wc-reducers", default="reducefn3,reducefn2",
+                    help="wc_general: the WordCount reduce modules to run")
     ap.add_argument("--validate", action="store_true",
                     help="check every key of the last timed step against the generator's ground truth")
     args = ap.parse_args()
@@ -216,7 +218,7 @@ def main() -> int:
         store.finish_loading()
         tc = {k.decode("utf-8", "surrogateescape"): v for k, v in truth_counts(cdir).items()}
         W = "lua_mapreduce_1_amd.models.wordcount"
-        for red in ("reducefn3", "reducefn2"):
+        for red in args.wc_reducers.split(","):
             a = argparse.Namespace(**vars(args))
             if red == "reducefn2":  # per-key Python combiner + reducer: seconds per step
                 a.steps, a.warmup = min(args.steps, 2), 1
