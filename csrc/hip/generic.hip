@@ -108,25 +108,31 @@ __device__ __forceinline__ void fold_col(const Cols& c, int j, u64 i, u64 slot) 
   }
 }
 
+// Little-endian word of the bytes p[0, min(8, avail)) (avail >= 1), the rest
+// zero: at most two ALIGNED 8-byte loads, each of a word that holds at least
+// one of the wanted bytes (an aligned word never crosses a page, so nothing
+// past the buffer's last valid byte's page is touched) — instead of one
+// dependent byte load per key byte (profiles/r4/kstats: the span inserts).
+__device__ __forceinline__ u64 le_bytes(const u8* p, u64 avail) {
+  const uintptr_t a = (uintptr_t)p;
+  const u64* w = reinterpret_cast<const u64*>(a & ~(uintptr_t)7);
+  const u32 off = (u32)(a & 7);
+  u64 x = w[0] >> (8 * off);
+  if (off && avail > 8 - off) x |= w[1] << (64 - 8 * off);
+  if (avail < 8) x &= (1ull << (8 * avail)) - 1;
+  return x;
+}
+
 // 128-bit key of text[s, s + len) (mr_common.h encoding; len >= 1).
 __device__ __forceinline__ void span_key(const u8* text, u64 s, u64 len, u64& hi, u64& lo) {
   const u8* p = text + s;
-  hi = 0;
-  lo = 0;
-  const u64 k8 = len < 8 ? len : 8;
-  for (u64 k = 0; k < k8; ++k) hi |= (u64)p[k] << (56 - 8 * k);
+  hi = __builtin_bswap64(le_bytes(p, len));
   if (len <= (u64)PACK_MAX) {
-    for (u64 k = 8; k < len; ++k) lo |= (u64)p[k] << (56 - 8 * (k - 8));
-    lo |= len;
+    lo = (len > 8 ? __builtin_bswap64(le_bytes(p + 8, len - 8)) : 0ull) | len;
     return;
   }
   u64 h = long_hash_init(len);
-  for (u64 w = 0; w < len; w += 8) {
-    u64 word = 0;
-    const u64 n = (len - w) < 8 ? (len - w) : 8;
-    for (u64 j = 0; j < n; ++j) word |= (u64)p[w + j] << (8 * j);
-    h = long_hash_step(h, word);
-  }
+  for (u64 w = 0; w < len; w += 8) h = long_hash_step(h, le_bytes(p + w, len - w));
   lo = long_lo(h, mr_long_mask);
 }
 
@@ -171,43 +177,53 @@ __global__ void __launch_bounds__(256) agg_insert_kernel(GTab g, Keys ks, u64 n,
   gtab_count_claims(g, claims);
 }
 
-// Occupied slots -> dense (slot, hi, lo, rep).  One 256-thread block per 4096
-// slots: per-thread counts, LDS scan, one atomic per block for the base.
+// Occupied slots -> dense (slot, hi, lo, rep), in slot order: slots ranked
+// k-major inside the block (b0 + k*256 + t), so the lanes of a wave write
+// consecutive rows for each k (ballot + popcount per (k, wave), a 64-entry
+// scan in LDS, one atomic per block for its base).
 constexpr int SC_ITEMS = 16;
 __global__ void __launch_bounds__(256) slot_compact_kernel(GTab g, u64 cap, long long* out_slot, u64* out_hi,
                                                            u64* out_lo, u64* out_rep, unsigned long long* counter) {
-  __shared__ u32 sh[256];
+  constexpr int NW = 256 / 64;
+  __shared__ u32 wc[SC_ITEMS * NW];
   __shared__ unsigned long long base;
   const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
   const u64 b0 = (u64)blockIdx.x * 256 * SC_ITEMS;
-  u32 occ = 0, n = 0;
+  u32 occ = 0;
+  u32 rank[SC_ITEMS];
 #pragma unroll
   for (int k = 0; k < SC_ITEMS; ++k) {
     const u64 i = b0 + (u64)k * 256 + t;
     const bool o = i < cap && g.tag[i] != 0;
     occ |= (o ? 1u : 0u) << k;
-    n += o ? 1u : 0u;
+    const unsigned long long m = __ballot(o);
+    rank[k] = (u32)__popcll(m & below);
+    if (lane == 0) wc[k * NW + wave] = (u32)__popcll(m);
   }
-  sh[t] = n;
   __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {
-    const u32 y = t >= o ? sh[t - o] : 0u;
-    __syncthreads();
-    sh[t] += y;
-    __syncthreads();
+  if (t < 64) {
+    const u32 c = t < SC_ITEMS * NW ? wc[t] : 0u;
+    u32 incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    if (t < SC_ITEMS * NW) wc[t] = incl - c;
+    if (t == 63) base = atomicAdd(counter, (unsigned long long)incl);
   }
-  if (t == 255) base = atomicAdd(counter, (unsigned long long)sh[255]);
   __syncthreads();
-  u64 o = base + sh[t] - n;
 #pragma unroll
   for (int k = 0; k < SC_ITEMS; ++k) {
     if (occ & (1u << k)) {
       const u64 i = b0 + (u64)k * 256 + t;
+      const u64 o = base + wc[k * NW + wave] + rank[k];
       out_slot[o] = (long long)i;
       out_hi[o] = g.hi[i];
       out_lo[o] = g.lo[i];
       out_rep[o] = g.rep[i];
-      ++o;
     }
   }
 }
@@ -331,21 +347,44 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
   __syncthreads();
   u32 claims = 0;
   const u64 r0 = (u64)blockIdx.x * CB_ROWS;
+  // phase 1: the keys of all of this thread's rows, their loads issued
+  // together (span starts/lengths, then the key words: independent chains,
+  // so the row loop below does not wait a memory round trip per row)
+  u64 khi_r[CB_ITEMS], klo_r[CB_ITEMS], krep_r[CB_ITEMS];
+  u32 ok = 0;
+  if (ks.text) {
+    long long st_r[CB_ITEMS];
+    int len_r[CB_ITEMS];
+#pragma unroll
+    for (int it = 0; it < CB_ITEMS; ++it) {
+      const u64 i = r0 + (u64)it * CB_T + t;
+      st_r[it] = i < n ? ks.starts[i] : -1;
+      len_r[it] = i < n ? ks.lens[i] : 0;
+    }
+#pragma unroll
+    for (int it = 0; it < CB_ITEMS; ++it) {
+      khi_r[it] = klo_r[it] = krep_r[it] = 0;
+      if (len_r[it] > 0 && st_r[it] >= 0) {
+        span_key(ks.text, (u64)st_r[it], (u64)len_r[it], khi_r[it], klo_r[it]);
+        krep_r[it] = make_rep(ks.rep_base + (u64)st_r[it], (u64)len_r[it]);
+        ok |= 1u << it;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int it = 0; it < CB_ITEMS; ++it) {
+      const u64 i = r0 + (u64)it * CB_T + t;
+      khi_r[it] = i < n ? ks.hi[i] : 0;
+      klo_r[it] = i < n ? ks.lo[i] : 0;
+      krep_r[it] = (i < n && ks.rep) ? ks.rep[i] + (ks.rep_add << REP_LEN_BITS) : 0;
+      if (i < n) ok |= 1u << it;
+    }
+  }
+#pragma unroll
   for (int it = 0; it < CB_ITEMS; ++it) {
     const u64 i = r0 + (u64)it * CB_T + t;
-    if (i >= n) break;
-    u64 hi = 0, lo = 0, rep = 0;
-    if (ks.text) {
-      const long long st = ks.starts[i];
-      const int len = ks.lens[i];
-      if (len <= 0 || st < 0) continue;
-      span_key(ks.text, (u64)st, (u64)len, hi, lo);
-      rep = make_rep(ks.rep_base + (u64)st, (u64)len);
-    } else {
-      hi = ks.hi[i];
-      lo = ks.lo[i];
-      rep = ks.rep ? ks.rep[i] + (ks.rep_add << REP_LEN_BITS) : 0;
-    }
+    if (!(ok & (1u << it))) continue;
+    const u64 hi = khi_r[it], lo = klo_r[it], rep = krep_r[it];
     const int s = key_is_long(lo) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, hi, lo, rep);
     if (s >= 0) {
       for (int j = 0; j < c.k; ++j) cb_lds_fold(&acc[j * CB_SLOTS + s], c, j, i);

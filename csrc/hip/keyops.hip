@@ -220,42 +220,86 @@ __global__ void hash_agg_kernel(const u64* hi, const u64* lo, const long long* v
 // per block for the output base (a per-wave atomic on one counter serialised
 // ~3e4 same-address atomics: 0.4 ms for a 2M-slot table).
 constexpr int CP_ITEMS = 16;
+// Occupied slots -> dense rows, in slot order.  The block's CP_ITEMS x 256
+// slots are ranked k-major (slot b0 + k*256 + t), so for each k the lanes of a
+// wave write CONSECUTIVE rows: one ballot + popcount per (k, wave), a 64-entry
+// scan of the (k, wave) counts in LDS, one atomic per block for its base.
+// (The first version gave each thread a run of its own and wrote it lane by
+// lane: every store of a wave hit a different line.)  ``out_aos`` (optional):
+// the rows also as 32-byte records {hi, lo, val, rep}, so a later gather by a
+// permutation reads one sector per row instead of one per column.
 __global__ void __launch_bounds__(256) table_compact_kernel(GTab g, u64 cap, u64* out_hi, u64* out_lo,
                                                             long long* out_val, u64* out_rep,
-                                                            unsigned long long* counter) {
-  __shared__ u32 sh[256];
+                                                            unsigned long long* counter, u64* out_aos) {
+  constexpr int NW = 256 / 64;
+  __shared__ u32 wc[CP_ITEMS * NW];
   __shared__ unsigned long long base;
   const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
   const u64 b0 = (u64)blockIdx.x * 256 * CP_ITEMS;
-  u32 occ = 0, n = 0;
+  u32 occ = 0;
+  u32 rank[CP_ITEMS];
 #pragma unroll
   for (int k = 0; k < CP_ITEMS; ++k) {
     const u64 i = b0 + (u64)k * 256 + t;
     const bool o = i < cap && g.tag[i] != 0;
     occ |= (o ? 1u : 0u) << k;
-    n += o ? 1u : 0u;
+    const unsigned long long m = __ballot(o);
+    rank[k] = (u32)__popcll(m & below);
+    if (lane == 0) wc[k * NW + wave] = (u32)__popcll(m);
   }
-  sh[t] = n;
   __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {
-    const u32 y = t >= o ? sh[t - o] : 0u;
-    __syncthreads();
-    sh[t] += y;
-    __syncthreads();
+  if (t < 64) {
+    // exclusive scan of the CP_ITEMS * NW (k-major) counts by one wave
+    const u32 c = t < CP_ITEMS * NW ? wc[t] : 0u;
+    u32 incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    if (t < CP_ITEMS * NW) wc[t] = incl - c;
+    if (t == 63) base = atomicAdd(counter, (unsigned long long)incl);
   }
-  if (t == 255) base = atomicAdd(counter, (unsigned long long)sh[255]);
   __syncthreads();
-  u64 o = base + sh[t] - n;
 #pragma unroll
   for (int k = 0; k < CP_ITEMS; ++k) {
     if (occ & (1u << k)) {
       const u64 i = b0 + (u64)k * 256 + t;
-      out_hi[o] = g.hi[i];
-      out_lo[o] = g.lo[i];
-      out_val[o] = g.val[i];
-      out_rep[o] = g.rep[i];
-      ++o;
+      const u64 o = base + wc[k * NW + wave] + rank[k];
+      const u64 h = g.hi[i], l = g.lo[i], r = g.rep[i];
+      const long long v = g.val[i];
+      out_hi[o] = h;
+      out_lo[o] = l;
+      out_val[o] = v;
+      out_rep[o] = r;
+      if (out_aos) {
+        typedef u64 v2u __attribute__((ext_vector_type(2)));
+        v2u* q = reinterpret_cast<v2u*>(out_aos + 4 * o);
+        q[0] = v2u{h, l};
+        q[1] = v2u{(u64)v, r};
+      }
     }
+  }
+}
+
+// Rows of 32-byte records {hi, lo, val, rep} gathered by an int32 permutation
+// into four columns (two 16-byte loads per row from one 32-byte record).
+__global__ void __launch_bounds__(256) gather_aos4_kernel(const u32* __restrict__ perm, u64 n,
+                                                          const u64* __restrict__ aos, u64* o0, u64* o1, u64* o2,
+                                                          u64* o3) {
+  typedef u64 v2u __attribute__((ext_vector_type(2)));
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u64 j = perm[i];
+    j = j < n ? j : n - 1;
+    const v2u* q = reinterpret_cast<const v2u*>(aos + 4 * j);
+    const v2u a = q[0], b = q[1];
+    o0[i] = a.x;
+    o1[i] = a.y;
+    o2[i] = b.x;
+    o3[i] = b.y;
   }
 }
 
@@ -509,11 +553,21 @@ int mr_hash_agg(const void* hi, const void* lo, const void* val, const void* rep
 }
 
 int mr_table_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, void* out_hi,
-                     void* out_lo, void* out_val, void* out_rep, void* counter, hipStream_t stream) {
+                     void* out_lo, void* out_val, void* out_rep, void* counter, void* out_aos, hipStream_t stream) {
   const u64 nb = (cap + 256 * CP_ITEMS - 1) / (256 * CP_ITEMS);
   hipLaunchKernelGGL(table_compact_kernel, dim3((unsigned)nb), dim3(256), 0, stream,
                      make_gtab(tag, hi, lo, val, rep, ctrl, cap), cap, (u64*)out_hi, (u64*)out_lo,
-                     (long long*)out_val, (u64*)out_rep, (unsigned long long*)counter);
+                     (long long*)out_val, (u64*)out_rep, (unsigned long long*)counter, (u64*)out_aos);
+  return (int)hipGetLastError();
+}
+
+// out[c][i] = aos[perm[i]].c for the four columns {hi, lo, val, rep}
+int mr_gather_aos4(const void* perm, u64 n, const void* aos, void* o0, void* o1, void* o2, void* o3,
+                   hipStream_t stream) {
+  if (n == 0) return 0;
+  const u64 g = (n + 255) / 256;
+  hipLaunchKernelGGL(gather_aos4_kernel, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, stream,
+                     (const u32*)perm, n, (const u64*)aos, (u64*)o0, (u64*)o1, (u64*)o2, (u64*)o3);
   return (int)hipGetLastError();
 }
 

@@ -402,9 +402,8 @@ static inline unsigned rc_grid(u64 n, unsigned cap = 8192) {
   return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
-template <int C, bool PIPE>
+template <int C, int R, bool PIPE>
 static void launch_gather16_t(const void* in, u64 nin, const void* perm, u64 n, int rb, void* out, hipStream_t s) {
-  constexpr int R = C <= 8 ? 256 : 128;
   const u64 nb = (n + R - 1) / R;
   const unsigned g = (unsigned)(nb < 65536 ? nb : 65536);
   hipLaunchKernelGGL((rc::rec_gather16_kernel<C, R, PIPE>), dim3(g), dim3(256), 0, s, (const u8*)in, nin,
@@ -412,13 +411,23 @@ static void launch_gather16_t(const void* in, u64 nin, const void* perm, u64 n, 
 }
 
 static bool g_gather_pipe = true;  // mr_rec_gather mode 2 forces the unpipelined form (A/B)
+// rows per workgroup batch (mr_rec_gather_set_rows): 256 (LDS image of 28 KiB
+// for 100-byte rows: 5 workgroups = 20 waves per CU) or 128 (14 KiB: the CU
+// fills to 8 waves per SIMD, more row loads in flight)
+static int g_gather_rows = 256;
 
 template <int C>
 static void launch_gather16(const void* in, u64 nin, const void* perm, u64 n, int rb, void* out, hipStream_t s) {
+  constexpr int RD = C <= 8 ? 256 : 128;
+  if (g_gather_rows == 128 && RD == 256) {
+    if (g_gather_pipe) launch_gather16_t<C, 128, true>(in, nin, perm, n, rb, out, s);
+    else launch_gather16_t<C, 128, false>(in, nin, perm, n, rb, out, s);
+    return;
+  }
   if (g_gather_pipe)
-    launch_gather16_t<C, true>(in, nin, perm, n, rb, out, s);
+    launch_gather16_t<C, RD, true>(in, nin, perm, n, rb, out, s);
   else
-    launch_gather16_t<C, false>(in, nin, perm, n, rb, out, s);
+    launch_gather16_t<C, RD, false>(in, nin, perm, n, rb, out, s);
 }
 
 extern "C" {
@@ -471,6 +480,12 @@ int mr_rec_tie_fixup(const void* sk, void* perm, const void* rec, u64 n, int rb,
 // nin: rows of `in` (permutation entries >= nin read row 0).  mode: 0 = the
 // 16-byte LDS-staged gather where the shape allows it, 1 = the dword gather
 // (A/B probes and tests of both paths).
+int mr_rec_gather_set_rows(int rows) {
+  if (rows != 128 && rows != 256) return -1;
+  g_gather_rows = rows;
+  return 0;
+}
+
 int mr_rec_gather(const void* in, u64 nin, const void* perm, u64 n, int rb, void* out, int mode, hipStream_t s) {
   if (n == 0) return 0;
   if (nin == 0) return -1;

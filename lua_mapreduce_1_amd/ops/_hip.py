@@ -36,7 +36,9 @@ _SIGS = {
     "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64, _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
     "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p, _p],
-    "mr_table_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
+    "mr_table_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p, _p],
+    "mr_gather_aos4": [_p, _u64, _p, _p, _p, _p, _p, _p],
+    "mr_rec_gather_set_rows": [_i32],
     "mr_key_word": [_p, _p, _p, _p, _u64, _u32, _p, _p],
     "mr_key_meta": [_p, _p, _p, _u64, _p, _u32, _p, _p, _p],
     "mr_gather_key_bytes": [_p, _p, _p, _p, _u64, _p, _p, _u64, _p],
@@ -141,6 +143,8 @@ def lib():
             raise ValueError(f"MR_SORT_ROUNDS={TUNABLES.sort_rounds}: must be 16, 24 or 32")
         if L.mr_wc_map3_set_config(TUNABLES.wc_map_config) != 0:
             raise ValueError(f"MR_WC_MAP_CONFIG={TUNABLES.wc_map_config}: must be 0..3")
+        if L.mr_rec_gather_set_rows(TUNABLES.rec_gather_rows) != 0:
+            raise ValueError(f"MR_REC_GATHER_ROWS={TUNABLES.rec_gather_rows}: must be 128 or 256")
         _LIB = L
     return _LIB
 

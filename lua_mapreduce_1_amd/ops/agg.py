@@ -109,17 +109,20 @@ class Physical:
         self.specs = specs
         self.cols: list[tuple[str, str, int | None]] = []
         self.out: list[tuple] = []  # per output: ("col", j) | ("mean", j_sum, j_cnt)
+
+        def col(c) -> int:
+            # one physical column per distinct (dtype, op, input): a mean and
+            # a count share their count (one atomic fewer per row)
+            if c not in self.cols:
+                self.cols.append(c)
+            return self.cols.index(c)
         for i, s in enumerate(specs):
             if s.op == "mean":
-                self.cols.append(("f64", "sum", i))
-                self.cols.append(("i64", "sum", None))
-                self.out.append(("mean", len(self.cols) - 2, len(self.cols) - 1))
+                self.out.append(("mean", col(("f64", "sum", i)), col(("i64", "sum", None))))
             elif s.op == "count":
-                self.cols.append(("i64", "sum", None))
-                self.out.append(("col", len(self.cols) - 1))
+                self.out.append(("col", col(("i64", "sum", None))))
             else:
-                self.cols.append((s.dtype, s.op, i))
-                self.out.append(("col", len(self.cols) - 1))
+                self.out.append(("col", col((s.dtype, s.op, i))))
         if len(self.cols) > MAXC:
             raise ValueError(f"at most {MAXC} physical columns (means count twice)")
 

@@ -311,23 +311,26 @@ class HashTable:
             return int(c[0]) + int(c[_CTRL_SHARD0::_CTRL_STRIDE].sum()), bool(c[1])
         return sum(p[0].size for p in self._pending), False
 
-    def compact(self, known_stats: tuple[int, bool] | None = None):
-        """Dense (hi, lo, val, rep) of all occupied slots (unsorted on GPU).
+    def compact(self, known_stats: tuple[int, bool] | None = None, aos: bool = False):
+        """Dense (hi, lo, val, rep) of all occupied slots (slot order on GPU).
         ``known_stats``: the (n, overflow) of a stats() call made since the last
-        insert (saves a second host synchronisation)."""
+        insert (saves a second host synchronisation).  ``aos``: also the rows
+        as int64 [n, 4] records for :func:`gather_aos4` (a fifth value; None
+        on CPU)."""
         if self.is_cuda:
             n, ovf = known_stats if known_stats is not None else self.stats()
             if ovf:
                 raise OverflowError("hash table overflow")
             d = self.device
             out = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(4)]
+            rec = torch.empty((n, 4), dtype=torch.int64, device=d) if aos else None
             counter = torch.zeros(1, dtype=torch.int64, device=d)
             _hip.call("mr_table_compact", *self._gtab(), self.cap, *[_hip.ptr(o) for o in out],
-                      _hip.ptr(counter), _hip.stream(d))
-            return tuple(out)
+                      _hip.ptr(counter), _hip.ptr(rec), _hip.stream(d))
+            return tuple(out) + ((rec,) if aos else ())
         if not self._pending:
             z = torch.zeros(0, dtype=torch.int64)
-            return z, z.clone(), z.clone(), z.clone()
+            return (z, z.clone(), z.clone(), z.clone()) + ((None,) if aos else ())
         hi = np.concatenate([p[0] for p in self._pending])
         lo = np.concatenate([p[1] for p in self._pending])
         v = np.concatenate([p[2] for p in self._pending])
@@ -355,7 +358,20 @@ class HashTable:
         else:
             agg = np.full(uk.size, _I64_MIN, np.int64)
             np.maximum.at(agg, inv, v)
-        return (_t64(uk["hi"].copy()), _t64(uk["lo"].copy()), torch.from_numpy(agg), _t64(r[first]))
+        return (_t64(uk["hi"].copy()), _t64(uk["lo"].copy()), torch.from_numpy(agg), _t64(r[first])) + \
+            ((None,) if aos else ())
+
+
+def gather_aos4(perm: torch.Tensor, aos: torch.Tensor):
+    """(hi, lo, val, rep) of the 32-byte records ``aos[perm]`` (GPU: one
+    launch, one 32-byte record read per row instead of one line per column)."""
+    n = perm.numel()
+    d = aos.device
+    out = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(4)]
+    if n:
+        _hip.call("mr_gather_aos4", _hip.ptr(perm.to(torch.int32).contiguous()), n, _hip.ptr(aos),
+                  *[_hip.ptr(o) for o in out], _hip.stream(d))
+    return tuple(out)
 
 
 # ---------------------------------------------------------------------------

@@ -655,8 +655,9 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         (the fused tie fix-up would fail the same way every iteration)."""
         cap = getattr(self, "_blob_cap", None)
         if getattr(self, "_exact_tail", False):
-            hi, lo, val, rep = table.compact((n, False))
-            return devmod.finalize_exact_device(hi, lo, val, rep, src, self.nparts, self.partmod, blob_cap=cap)
+            hi, lo, val, rep, aos = table.compact((n, False), aos=True)
+            return devmod.finalize_exact_device(hi, lo, val, rep, src, self.nparts, self.partmod, blob_cap=cap,
+                                                aos=aos)
         return devmod.finalize_table_native(table, n, src, self.nparts, blob_cap=cap)
 
     def _reduce_insert_received(self, rbuf, recv_counts, rows: int) -> int:

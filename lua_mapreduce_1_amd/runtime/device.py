@@ -490,13 +490,15 @@ def finalize_table_native(table, n: int, src, nparts: int, blob_cap: int | None 
 
 
 def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=None,
-                          blob_cap: int | None = None) -> dict:
+                          blob_cap: int | None = None, aos: torch.Tensor | None = None) -> dict:
     """The device half of a tail ordered exactly by key bytes from the start
     (ops.exact_key_perm) — for key sets whose fused tail falls back every time.
     Keys past the exact sort's length limit get the (partition, hi, lo) sort
     and the host fix-up instead.  Partitions and key lengths come from one
     key_meta pass (device FNV-1 partitions); the rows and their lengths are
-    reordered by one gather launch."""
+    reordered by one gather launch (from the 32-byte row records ``aos`` of
+    the compaction when given: one record read per row instead of one line
+    per column)."""
     spec = getattr(partition_module, "device_partition", None) if partition_module is not None else ("fnv1", nparts)
     klen = None
     if hi.is_cuda and spec is not None and spec[0] == "fnv1" and int(spec[1]) == nparts:
@@ -517,9 +519,13 @@ def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=N
         # gathered rows (no key bytes read)
         from ..ops import _hip
         n = hi.numel()
-        cols = [torch.empty(n, dtype=torch.int64, device=hi.device) for _ in range(4)]
-        _hip.call("mr_gather_cols", _hip.ptr(perm.to(torch.int32)), n, _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val),
-                  _hip.ptr(rep), None, None, *[_hip.ptr(c) for c in cols], None, None, _hip.stream(hi.device))
+        if aos is not None:
+            cols = list(ops.gather_aos4(perm, aos))
+        else:
+            cols = [torch.empty(n, dtype=torch.int64, device=hi.device) for _ in range(4)]
+            _hip.call("mr_gather_cols", _hip.ptr(perm.to(torch.int32)), n, _hip.ptr(hi), _hip.ptr(lo),
+                      _hip.ptr(val), _hip.ptr(rep), None, None, *[_hip.ptr(c) for c in cols], None, None,
+                      _hip.stream(hi.device))
         _, slen = ops.key_meta(cols[0], cols[1], cols[3], src, want_part=False)
         pend = finalize_device(*cols, src, nparts, partition_module, part=spart.to(torch.int32), _presorted=True,
                                blob_cap=blob_cap, lengths=slen)

@@ -64,6 +64,9 @@ class Tunables:
                                "word-count map kernel shape (csrc/hip/wordcount3.hip): 0 = 512 threads, 2048 LDS "
                                "slots, 8 KiB spans, two workgroups per CU; 1 / 2 = 4096 slots over 32 / 64 KiB, one "
                                "workgroup per CU; 3 = 1024 threads, 4096 slots, 32 KiB")
+    rec_gather_rows: int = _knob("MR_REC_GATHER_ROWS", 256,
+                                 "record plane: rows per workgroup batch of the 16-byte row gather (256, or 128: "
+                                 "half the LDS image, more workgroups per CU)")
     arena_cap_mb: float = _knob("MR_ARENA_CAP_MB", 0.0,
                                 "SPMD: cap of a rank's HBM input arena, MiB (0 = the rank's whole input); a larger "
                                 "input is mapped in rounds through a ring of two arenas of this size")

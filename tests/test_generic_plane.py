@@ -160,7 +160,8 @@ def test_column_spec_parsing():
     assert A.is_column_spec("f64:sum") and A.is_column_spec(("sum", "max"))
     assert not A.is_column_spec("sum") and not A.is_column_spec("concat") and not A.is_column_spec(None)
     ph = A.Physical(A.parse_spec(("f64:mean", "count")))
-    assert ph.cols == [("f64", "sum", 0), ("i64", "sum", None), ("i64", "sum", None)]
+    assert ph.cols == [("f64", "sum", 0), ("i64", "sum", None)]  # the mean and the count share the count
+    assert ph.out == [("mean", 0, 1), ("col", 1)]
     with pytest.raises(ValueError):
         A.parse_spec("f64:median")
 
