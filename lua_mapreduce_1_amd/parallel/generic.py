@@ -209,7 +209,7 @@ class GenericEmitter:
             raise NeedsHostMap("word_lines needs the SPMD engine's global line numbering")
         t = self._text(text)
         st, ln = TX.tokens(t)
-        line = TX.line_index(t, st) + int(self.line_base(t))
+        line = TX.line_index(t, st) + self.line_base(t)  # an int, or a device scalar
         self.spans(st, ln, line, text=t)
 
     def records(self, *a, **k):
@@ -532,8 +532,11 @@ class GenericPlane:
             rel = st.offsets - st.offsets[self._ids0]      # split i starts at rel[i] in the arena
             i = int(np.searchsorted(rel, a, side="right")) - 1
             inside = a - int(rel[i])
-            nl = int(torch.count_nonzero(eng.arena[a - inside:a] == 10)) if inside else 0
-            return int(self._lines[i]) + nl
+            if not inside:
+                return int(self._lines[i])
+            # newlines of the split before the chunk: counted on the device and
+            # added there (no host synchronisation per chunk)
+            return torch.count_nonzero(eng.arena[a - inside:a] == 10) + int(self._lines[i])
         return base
 
     # -- map --------------------------------------------------------------------
