@@ -67,6 +67,9 @@ class Tunables:
     rec_gather_rows: int = _knob("MR_REC_GATHER_ROWS", 256,
                                  "record plane: rows per workgroup batch of the 16-byte row gather (256, or 128: "
                                  "half the LDS image, more workgroups per CU)")
+    rec_scatter: bool = _knob("MR_REC_SCATTER", False,
+                              "record plane: apply a full row permutation as a scatter through its inverse "
+                              "(coalesced row reads) instead of the gather (random row reads)")
     arena_cap_mb: float = _knob("MR_ARENA_CAP_MB", 0.0,
                                 "SPMD: cap of a rank's HBM input arena, MiB (0 = the rank's whole input); a larger "
                                 "input is mapped in rounds through a ring of two arenas of this size")
