@@ -408,6 +408,52 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
   gtab_count_claims(g, claims);
 }
 
+// Sort-based pre-combine of byte-span rows (AggTable._insert_sorted): the
+// 128-bit key of every span and a 32-bit sort key — a hash of the key for
+// short keys (<= 15 bytes: exact (hi, lo)), all ones for long keys and empty
+// spans (they sort last and take the direct insert) — plus the sort's digit
+// histograms ([4][256] u32, LDS-combined) and the number of short rows.
+// Equal keys share a hash, so they end up adjacent after the sort; colliding
+// keys may interleave, which only splits their partial folds (the table
+// merges partials of one key).
+__global__ void __launch_bounds__(256) span_prep_kernel(const u8* __restrict__ text, const long long* __restrict__ starts,
+                                                        const int* __restrict__ lens, u64 n, u64* __restrict__ out_hi,
+                                                        u64* __restrict__ out_lo, u32* __restrict__ k32,
+                                                        u32* __restrict__ ghist, unsigned long long* __restrict__ nshort) {
+  __shared__ u32 h[4][256];
+  __shared__ u32 bcnt;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) h[b][t] = 0;
+  if (t == 0) bcnt = 0;
+  __syncthreads();
+  u32 cnt = 0;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + t; i < n; i += stride) {
+    const long long s = starts[i];
+    const int len = lens[i];
+    u64 hi = 0, lo = 0;
+    u32 k = 0xFFFFFFFFu;
+    if (len > 0 && s >= 0 && len <= PACK_MAX) {
+      span_key(text, (u64)s, (u64)len, hi, lo);
+      const u32 x = (u32)(fmix64(hi ^ fmix64(lo + 0x9E3779B97F4A7C15ull)) >> 32);
+      k = x == 0xFFFFFFFFu ? 0xFFFFFFFEu : x;
+      ++cnt;
+    }
+    out_hi[i] = hi;
+    out_lo[i] = lo;
+    k32[i] = k;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 0xFFu], 1u);
+  }
+  if (cnt) atomicAdd(&bcnt, cnt);
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    if (h[b][t]) atomicAdd(&ghist[b * 256 + t], h[b][t]);
+  if (t == 0 && bcnt) atomicAdd(nshort, (unsigned long long)bcnt);  // the block's short rows
+}
+
 // Fill a typed column with its fold identity (sum 0, min +max, max -max).
 __global__ void col_fill_kernel(void* col, u64 n, long long bits, int width) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
@@ -510,6 +556,16 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
   }
   hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256)), dim3(256), 0, stream,
                      ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
+  return (int)hipGetLastError();
+}
+
+// ghist: zeroed u32 [8][256] (the first 4 rows are filled); nshort: zeroed u64
+int mr_span_prep(const void* text, const void* starts, const void* lens, u64 n, void* hi, void* lo, void* k32,
+                 void* ghist, void* nshort, hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(span_prep_kernel, dim3(ag_grid(n, 256, 2048)), dim3(256), 0, stream, (const u8*)text,
+                     (const long long*)starts, (const int*)lens, n, (u64*)hi, (u64*)lo, (u32*)k32, (u32*)ghist,
+                     (unsigned long long*)nshort);
   return (int)hipGetLastError();
 }
 

@@ -80,14 +80,19 @@ def test_text_parse_gpu_matches_python(gpu):
     assert torch.equal(hi, di)
 
 
+@pytest.mark.parametrize("sort", [False, True], ids=["rows", "sorted"])
 @pytest.mark.parametrize("skew", [False, True], ids=["uniform", "zipf"])
 @pytest.mark.parametrize("dtype", ["i64", "f64", "f32"])
-def test_agg_table_folds_gpu(gpu, dtype, skew):
+def test_agg_table_folds_gpu(gpu, dtype, skew, sort, monkeypatch):
     """Typed sum/min/max folds of random (key, value) rows against numpy:
     uniform keys (the LDS combine fills up, most rows fold straight into the
-    HBM table) and Zipf keys (hot keys combined in LDS)."""
+    HBM table) and Zipf keys (hot keys combined in LDS) — through the per-row
+    insert and through the sort-based pre-combine (MR_AGG_SORT_MIN), with
+    long keys and empty spans mixed in."""
+    import dataclasses
     from lua_mapreduce_1_amd.ops import agg as A
     from lua_mapreduce_1_amd.ops import keys as K
+    monkeypatch.setattr(A, "TUNABLES", dataclasses.replace(A.TUNABLES, agg_sort_min=1 if sort else 0))
     rng = np.random.default_rng(3)
     n, nk = 200_000, 5000
     words = [("k%d" % i).encode() * (1 + i % 3) for i in range(nk)]  # some long keys
@@ -96,6 +101,7 @@ def test_agg_table_folds_gpu(gpu, dtype, skew):
     off = np.cumsum([0] + [len(w) for w in words])
     starts = torch.from_numpy(off[:-1][idx].astype(np.int64))
     lens = torch.from_numpy(np.array([len(w) for w in words], np.int32)[idx])
+    lens[::97] = 0  # empty spans are skipped
     if dtype == "i64":
         vals = torch.from_numpy(rng.integers(-10**12, 10**12, n))
     else:
@@ -111,7 +117,7 @@ def test_agg_table_folds_gpu(gpu, dtype, skew):
         kb = __import__("lua_mapreduce_1_amd").ops.key_bytes_list(hi.cpu(), lo.cpu(), rep.cpu(), text.cpu())
         res[str(dev)] = {k: [x[i].item() for x in c] for i, k in enumerate(kb)}
     a, b = res["cpu"], res[str(gpu)]
-    assert set(a) == set(b) == set(words[i] for i in np.unique(idx))
+    assert set(a) == set(b) == set(words[i] for i in np.unique(idx[lens.numpy() > 0]))
     for k in a:
         s0, s1 = a[k][0], b[k][0]
         if dtype == "i64":
@@ -119,6 +125,16 @@ def test_agg_table_folds_gpu(gpu, dtype, skew):
         else:
             tol = 1e-9 if dtype == "f64" else 1e-3
             assert math.isclose(s0, s1, rel_tol=tol, abs_tol=tol) and a[k][1:] == b[k][1:]
+
+
+def test_scores_sorted_precombine_gpu(gpu, monkeypatch):
+    """The CSV group-by job with every span batch pre-combined by the sort."""
+    import dataclasses
+    from lua_mapreduce_1_amd.ops import agg as A
+    monkeypatch.setattr(A, "TUNABLES", dataclasses.replace(A.TUNABLES, agg_sort_min=1))
+    splits = make_data("scores")
+    eng, res, got = run_engine(SS, splits, gpu, {})
+    assert close_lists(got, oracle("scores", None, splits))
 
 
 @pytest.mark.parametrize("which,mod,args", CASES, ids=["scores", "bigram", "max_host", "docs", "docs_concat",
