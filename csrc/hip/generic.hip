@@ -328,8 +328,13 @@ __device__ __forceinline__ int cb_slot(u64* tag, u64* khi, u64* klo, u64* krep, 
   return -1;
 }
 
-__global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 n, Cols c) {
+// rows: rows per block (a multiple of CB_T, at most CB_ROWS): small batches get
+// smaller blocks so the launch still covers the chip (a 2-8 MiB CSV chunk at
+// 4096 rows per block ran 37-150 blocks on 256 CUs, 72 % of wave cycles
+// waiting: profiles/r4/general/csv_pmc/)
+__global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 n, Cols c, u32 rows) {
   constexpr int CB_ITEMS = CB_ROWS / CB_T;
+  const int items = (int)(rows / CB_T);
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
   u64* tag = lds;
   u64* khi = tag + CB_SLOTS;
@@ -346,7 +351,7 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
   if (t == 0) nclaimed = 0;
   __syncthreads();
   u32 claims = 0;
-  const u64 r0 = (u64)blockIdx.x * CB_ROWS;
+  const u64 r0 = (u64)blockIdx.x * rows;
   // phase 1: the keys of all of this thread's rows, their loads issued
   // together (span starts/lengths, then the key words: independent chains,
   // so the row loop below does not wait a memory round trip per row)
@@ -358,8 +363,9 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
 #pragma unroll
     for (int it = 0; it < CB_ITEMS; ++it) {
       const u64 i = r0 + (u64)it * CB_T + t;
-      st_r[it] = i < n ? ks.starts[i] : -1;
-      len_r[it] = i < n ? ks.lens[i] : 0;
+      const bool in = it < items && i < n;
+      st_r[it] = in ? ks.starts[i] : -1;
+      len_r[it] = in ? ks.lens[i] : 0;
     }
 #pragma unroll
     for (int it = 0; it < CB_ITEMS; ++it) {
@@ -374,10 +380,11 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
 #pragma unroll
     for (int it = 0; it < CB_ITEMS; ++it) {
       const u64 i = r0 + (u64)it * CB_T + t;
-      khi_r[it] = i < n ? ks.hi[i] : 0;
-      klo_r[it] = i < n ? ks.lo[i] : 0;
-      krep_r[it] = (i < n && ks.rep) ? ks.rep[i] + (ks.rep_add << REP_LEN_BITS) : 0;
-      if (i < n) ok |= 1u << it;
+      const bool in = it < items && i < n;
+      khi_r[it] = in ? ks.hi[i] : 0;
+      klo_r[it] = in ? ks.lo[i] : 0;
+      krep_r[it] = (in && ks.rep) ? ks.rep[i] + (ks.rep_add << REP_LEN_BITS) : 0;
+      if (in) ok |= 1u << it;
     }
   }
 #pragma unroll
@@ -500,6 +507,7 @@ struct ColsArg {
   long long op[MAXC];
   void* post_slot;
   unsigned long long post_base;
+  long long rows_only;  // 1: one row per thread (distinct keys: an LDS combine has nothing to fold)
 };
 
 static Cols to_cols(const ColsArg* a) {
@@ -541,7 +549,7 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
   ks.lens = (const int*)lens;
   ks.rep_base = rep_base;
   if (!ks.text && (!ks.hi || !ks.lo)) return -2;
-  if (!a->list && a->k > 0 && n >= (u64)CB_ROWS) {
+  if (!a->list && !a->rows_only && a->k > 0 && n >= (u64)CB_ROWS) {
     const size_t lds = (size_t)CB_SLOTS * (4 + (size_t)a->k) * sizeof(u64);
     static bool lds_attr = false;  // dynamic LDS above 64 KiB (k > 4 columns) must be allowed once
     if (!lds_attr) {
@@ -549,9 +557,12 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
                                 (int)((size_t)CB_SLOTS * (4 + MAXC) * sizeof(u64)));
       lds_attr = true;
     }
-    const u64 nb = (n + CB_ROWS - 1) / CB_ROWS;
+    // rows per block: 4096, or fewer (down to 512) so the grid has >= 1024 blocks
+    u32 rows = (u32)CB_ROWS;
+    while (rows > (u32)CB_T && (n + rows - 1) / rows < 1024) rows >>= 1;
+    const u64 nb = (n + rows - 1) / rows;
     hipLaunchKernelGGL(agg_combine_kernel, dim3((unsigned)nb), dim3(CB_T), lds, stream,
-                       ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
+                       ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256)), dim3(256), 0, stream,

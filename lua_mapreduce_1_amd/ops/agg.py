@@ -159,7 +159,8 @@ class _ColsArg(ctypes.Structure):
     _fields_ = [("k", ctypes.c_longlong), ("list", ctypes.c_longlong), ("src", ctypes.c_void_p * MAXC),
                 ("stype", ctypes.c_longlong * MAXC), ("sbits", ctypes.c_longlong * MAXC),
                 ("dst", ctypes.c_void_p * MAXC), ("dtype", ctypes.c_longlong * MAXC),
-                ("op", ctypes.c_longlong * MAXC), ("post_slot", ctypes.c_void_p), ("post_base", ctypes.c_ulonglong)]
+                ("op", ctypes.c_longlong * MAXC), ("post_slot", ctypes.c_void_p), ("post_base", ctypes.c_ulonglong),
+                ("rows_only", ctypes.c_longlong)]
 
 
 def _scalar_bits(v, dtype: str) -> int:
@@ -421,6 +422,7 @@ class AggTable:
         """m distinct keys with one partial fold per physical column."""
         keep: list = []
         a = self._cols_arg([(p, dt) for p, (dt, _op, _i) in zip(partial, self.cols_spec)], m, keep)
+        a.rows_only = 1  # distinct keys: one per thread over the whole chip, no LDS combine
         t = self.keys
         _hip.call("mr_agg_insert", *t._gtab(), t.cap, _hip.ptr(self.src), _hip.ptr(hi.contiguous()),
                   _hip.ptr(lo.contiguous()), _hip.ptr(rep.contiguous()), 0, None, None, None, 0, m, ctypes.byref(a),

@@ -67,7 +67,7 @@ class Tunables:
     rec_gather_rows: int = _knob("MR_REC_GATHER_ROWS", 256,
                                  "record plane: rows per workgroup batch of the 16-byte row gather (256, or 128: "
                                  "half the LDS image, more workgroups per CU)")
-    agg_sort_min: int = _knob("MR_AGG_SORT_MIN", 1 << 20,
+    agg_sort_min: int = _knob("MR_AGG_SORT_MIN", 0,
                               "general plane, typed folds on the GPU: byte-span batches of at least this many rows "
                               "are pre-combined by a hash sort + segmented folds before the table insert (0 = "
                               "never; smaller batches hash every row into the table with an LDS combine)")
