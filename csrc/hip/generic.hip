@@ -21,6 +21,7 @@
 #include <climits>
 #include "mr_common.h"
 #include "hashtab.h"
+#include "text_parse.h"
 
 MR_LONG_MASK_SYMBOL(generic)
 
@@ -461,6 +462,225 @@ __global__ void __launch_bounds__(256) span_prep_kernel(const u8* __restrict__ t
   if (t == 0 && bcnt) atomicAdd(nshort, (unsigned long long)bcnt);  // the block's short rows
 }
 
+// ---------------------------------------------------------------------------
+// Fused CSV fold (emit.csv): lines -> fields -> decimal parse -> LDS combine
+// -> HBM table, in one kernel that reads the text once — instead of the op
+// chain lines / field / field / parse / mask / insert (six launches and five
+// intermediate arrays per chunk).  Line and field rules are text.hip's
+// (ops/text.py is the specification): a line starts at byte 0 or after a
+// '\n'; a trailing '\r' is not part of the line's last field; a missing key
+// or value field, an empty key, or a value that does not parse drops the row.
+// Each block takes `tiles` consecutive 8 KiB tiles: per tile the line starts
+// are found from a newline mask of 16 bytes per thread and compacted by a
+// block scan, then processed lane per line; a line belongs to the tile of
+// its first byte (its bytes past the tile are read from global memory).
+constexpr int CV_SEG = 16, CV_TILE = CB_T * CV_SEG;  // 8 KiB tiles, 512 threads
+constexpr int CV_MAXV = 4;                          // value inputs of a fused CSV fold
+
+// the value of input i (0..3) among four registers (no register-array indexing)
+__device__ __forceinline__ double pick(double v0, double v1, double v2, double v3, int i) {
+  return i == 0 ? v0 : (i == 1 ? v1 : (i == 2 ? v2 : v3));
+}
+
+struct CsvSpec {
+  int sep;
+  int kf;              // key field
+  int nin;             // input (value) columns
+  int vf[MAXC];        // per input column: its field, or -1 = the constant 1
+  int pin[MAXC];       // per physical column: its input column, or -1 = the scalar c.sbits
+};
+
+__device__ __forceinline__ double scalar_of(const Cols& c, int j) {
+  return c.dtype[j] == VT_I64 ? (double)c.sbits[j] : __longlong_as_double(c.sbits[j]);
+}
+
+__device__ __forceinline__ void cv_lds_fold(long long* acc, int dtype, int op, double v) {
+  if (dtype == VT_I64) {
+    const long long x = (long long)v;
+    if (op == OP_MIN) atomicMin(acc, x);
+    else if (op == OP_MAX) atomicMax(acc, x);
+    else atomicAdd((unsigned long long*)acc, (unsigned long long)x);
+  } else {
+    double* p = (double*)acc;
+    const double x = dtype == VT_F32 ? (double)(float)v : v;
+    if (op == OP_MIN) __hip_atomic_fetch_min(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else if (op == OP_MAX) __hip_atomic_fetch_max(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else __hip_atomic_fetch_add(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+__device__ __forceinline__ void cv_global_fold(const Cols& c, int j, u64 slot, double v) {
+  const int op = c.op[j];
+  if (c.dtype[j] == VT_I64) {
+    long long* p = (long long*)c.dst[j] + slot;
+    const long long x = (long long)v;
+    if (op == OP_MIN) atomicMin(p, x);
+    else if (op == OP_MAX) atomicMax(p, x);
+    else atomicAdd((unsigned long long*)p, (unsigned long long)x);
+  } else if (c.dtype[j] == VT_F64) {
+    double* p = (double*)c.dst[j] + slot;
+    if (op == OP_MIN) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (op == OP_MAX) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    float* p = (float*)c.dst[j] + slot;
+    const float x = (float)v;
+    if (op == OP_MIN) __hip_atomic_fetch_min(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (op == OP_MAX) __hip_atomic_fetch_max(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_fetch_add(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ void __launch_bounds__(CB_T) __attribute__((amdgpu_waves_per_eu(4, 8))) csv_fold_kernel(GTab g, const u8* __restrict__ text, u64 n, u64 rep_base,
+                                                        CsvSpec sp, Cols c, u32 tiles,
+                                                        unsigned long long* __restrict__ rows_out) {
+  extern __shared__ __attribute__((aligned(16))) u64 lds[];
+  u64* tag = lds;
+  u64* khi = tag + CB_SLOTS;
+  u64* klo = khi + CB_SLOTS;
+  u64* krep = klo + CB_SLOTS;
+  long long* acc = (long long*)(krep + CB_SLOTS);  // [c.k][CB_SLOTS]
+  __shared__ u16 lpos[CV_TILE];
+  __shared__ u32 wsum[CB_T / 64];
+  __shared__ u32 nclaimed, nrows;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  for (int q = t; q < CB_SLOTS; q += CB_T) {
+    tag[q] = 0;
+    klo[q] = 0;
+    for (int j = 0; j < c.k; ++j) acc[j * CB_SLOTS + q] = cb_identity(c.dtype[j], c.op[j]);
+  }
+  if (t == 0) nclaimed = nrows = 0;
+  __syncthreads();
+  u32 claims = 0, myrows = 0;
+  const u64 b0 = (u64)blockIdx.x * tiles * (u64)CV_TILE;
+  for (u32 tt = 0; tt < tiles; ++tt) {
+    const u64 tile = b0 + (u64)tt * CV_TILE;
+    if (tile >= n) break;  // (uniform across the block)
+    const u64 gpos = tile + (u64)t * CV_SEG;
+    u32 starts = 0;
+    if (gpos < n) {
+      u32 nlm = 0;
+      if (gpos + CV_SEG <= n && (((uintptr_t)(text + gpos)) & 15) == 0) {
+        const uint4 q = *reinterpret_cast<const uint4*>(text + gpos);
+        const u32 w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int i = 0; i < CV_SEG; ++i) nlm |= (((w[i >> 2] >> (8 * (i & 3))) & 0xFFu) == 10u ? 1u : 0u) << i;
+      } else {
+#pragma unroll
+        for (int i = 0; i < CV_SEG; ++i) nlm |= (gpos + i < n && text[gpos + i] == 10 ? 1u : 0u) << i;
+      }
+      const u32 prev = (gpos == 0 || text[gpos - 1] == 10) ? 1u : 0u;
+      starts = ((nlm << 1) | prev) & 0xFFFFu;
+      const u64 lim = n - gpos;
+      if (lim < (u64)CV_SEG) starts &= (1u << lim) - 1u;
+    }
+    // block exclusive scan of the line-start counts -> lpos (tile offsets)
+    const u32 cnt = (u32)__builtin_popcount(starts);
+    u32 incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    u32 base = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < CB_T / 64; ++w) {
+      const u32 x = wsum[w];
+      base += w < wave ? x : 0u;
+      total += x;
+    }
+    u32 k = base + incl - cnt;
+    while (starts) {
+      const int i = __builtin_ctz(starts);
+      starts &= starts - 1;
+      lpos[k++] = (u16)(t * CV_SEG + i);
+    }
+    __syncthreads();
+    for (u32 x = t; x < total; x += CB_T) {
+      const u64 ls = tile + lpos[x];
+      // the line's end, then its fields (a trailing '\r' is dropped)
+      u64 le = ls;
+      while (le < n && text[le] != 10) ++le;
+      if (le > ls && text[le - 1] == 13) --le;
+      int f = 0;
+      u64 fs = ls, ks = 0;
+      int klen = -1;
+      double v0 = 1.0, v1 = 1.0, v2 = 1.0, v3 = 1.0;  // inputs without a field stay 1
+      u32 got = 0;  // bit j: input j's field was seen and parsed
+      bool bad = false;
+      for (u64 p = ls;; ++p) {
+        if (p == le || text[p] == (u8)sp.sep) {
+          const int flen = (int)(p - fs);
+          if (f == sp.kf) {
+            ks = fs;
+            klen = flen;
+          }
+          u32 hit = 0;  // the inputs this field feeds (one parse for all of them)
+#pragma unroll
+          for (int j = 0; j < CV_MAXV; ++j) hit |= (j < sp.nin && sp.vf[j] == f ? 1u : 0u) << j;
+          if (hit) {
+            bool b = false;
+            const double v = tx::parse_f64(text + fs, flen, b);
+            bad |= b;
+            got |= hit;
+            if (hit & 1u) v0 = v;
+            if (hit & 2u) v1 = v;
+            if (hit & 4u) v2 = v;
+            if (hit & 8u) v3 = v;
+          }
+          if (p == le) break;
+          ++f;
+          fs = p + 1;
+        }
+      }
+      // every field-valued input present and numeric, a non-empty key
+      u32 need = 0;
+#pragma unroll
+      for (int j = 0; j < CV_MAXV; ++j)
+        if (j < sp.nin && sp.vf[j] >= 0) need |= 1u << j;
+      if (bad || klen <= 0 || (got & need) != need) continue;
+      ++myrows;
+      u64 hi, lo;
+      span_key(text, ks, (u64)klen, hi, lo);
+      const u64 rep = make_rep(rep_base + ks, (u64)klen);
+      const int q = key_is_long(lo) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, hi, lo, rep);
+      if (q >= 0) {
+        for (int j = 0; j < c.k; ++j) {
+          const int i = sp.pin[j];
+          const double v = i >= 0 ? pick(v0, v1, v2, v3, i) : scalar_of(c, j);
+          cv_lds_fold(&acc[j * CB_SLOTS + q], c.dtype[j], c.op[j], v);
+        }
+      } else {
+        u64 slot = 0;
+        const int r = gtab_insert(g, hi, lo, 0, rep, OP_NONE, &slot);
+        claims += r == 2;
+        if (r)
+          for (int j = 0; j < c.k; ++j) {
+            const int i = sp.pin[j];
+            const double v = i >= 0 ? pick(v0, v1, v2, v3, i) : scalar_of(c, j);
+            cv_global_fold(c, j, slot, v);
+          }
+      }
+    }
+    __syncthreads();
+  }
+  if (myrows) atomicAdd(&nrows, myrows);
+  __syncthreads();
+  if (t == 0 && nrows) atomicAdd(rows_out, (unsigned long long)nrows);
+  for (int q = t; q < CB_SLOTS; q += CB_T) {
+    if (!tag[q]) continue;
+    u64 slot = 0;
+    const int r = gtab_insert(g, khi[q], klo[q], 0, krep[q], OP_NONE, &slot);
+    claims += r == 2;
+    if (r)
+      for (int j = 0; j < c.k; ++j) cb_global_fold(c, j, slot, acc[j * CB_SLOTS + q]);
+  }
+  gtab_count_claims(g, claims);
+}
+
 // Fill a typed column with its fold identity (sum 0, min +max, max -max).
 __global__ void col_fill_kernel(void* col, u64 n, long long bits, int width) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
@@ -567,6 +787,48 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
   }
   hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256)), dim3(256), 0, stream,
                      ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
+  return (int)hipGetLastError();
+}
+
+// Host-side mirror of CsvSpec.
+struct CsvArg {
+  long long sep, kf, nin;
+  long long vf[MAXC];
+  long long pin[MAXC];
+};
+
+// The fused CSV fold of text[0, n) into a fold-mode table (see csv_fold_kernel);
+// rows_out (u64, device): += rows folded.
+int mr_csv_fold(void* tag, void* thi, void* tlo, void* tval, void* trep, void* ctrl, u64 cap, const void* src,
+                const void* text, u64 n, u64 rep_base, const void* spec, const void* cols, void* rows_out,
+                hipStream_t stream) {
+  if (n == 0) return 0;
+  const ColsArg* a = (const ColsArg*)cols;
+  const CsvArg* sa = (const CsvArg*)spec;
+  if (a->list || a->k < 1 || a->k > MAXC || sa->nin < 0 || sa->nin > CV_MAXV) return -1;
+  CsvSpec sp;
+  sp.sep = (int)sa->sep;
+  sp.kf = (int)sa->kf;
+  sp.nin = (int)sa->nin;
+  for (int j = 0; j < MAXC; ++j) {
+    sp.vf[j] = (int)sa->vf[j];
+    sp.pin[j] = (int)sa->pin[j];
+    if (j < a->k && sp.pin[j] >= sp.nin) return -1;
+  }
+  const size_t lds = (size_t)CB_SLOTS * (4 + (size_t)a->k) * sizeof(u64);
+  static bool lds_attr = false;
+  if (!lds_attr) {
+    (void)hipFuncSetAttribute((const void*)csv_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)((size_t)CB_SLOTS * (4 + MAXC) * sizeof(u64)));
+    lds_attr = true;
+  }
+  const u64 ntiles = (n + CV_TILE - 1) / CV_TILE;
+  u32 tiles = 4;  // 32 KiB per block, fewer when that leaves the chip short of blocks
+  while (tiles > 1 && (ntiles + tiles - 1) / tiles < 1024) tiles >>= 1;
+  const u64 nb = (ntiles + tiles - 1) / tiles;
+  hipLaunchKernelGGL(csv_fold_kernel, dim3((unsigned)nb), dim3(CB_T), lds, stream,
+                     ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), (const u8*)text, n, rep_base, sp, to_cols(a),
+                     tiles, (unsigned long long*)rows_out);
   return (int)hipGetLastError();
 }
 

@@ -1,7 +1,8 @@
 """Group-by on a CSV column with float aggregates, as a MapReduce job: input
 lines ``word,score``; result per word = [mean score, max score, count].  The
-device map finds the fields and parses the scores on the GPU (ops/text.py)
-and emits (word span, score, score, 1); the reduce module's
+device map emits every line as (word span, score, score, 1) with
+``emit.csv`` (one fused GPU kernel: line and field split, decimal parse and
+the LDS-combined typed fold; specified by ops/text.py csv_rows); the reduce module's
 ``device_reduce = ("f64:mean", "f64:max", "count")`` folds them in typed
 columns of the general plane (native f64 atomics; a mean is kept as a sum
 and a count and divided when results are read).  The host ``reducefn``
@@ -43,20 +44,16 @@ device_input = "split"
 
 
 def device_mapfn(key, value, emit):
-    import torch
-    from lua_mapreduce_1_amd.ops import text as TX
     if hasattr(value, "data_ptr"):
         data = value
     else:
         from lua_mapreduce_1_amd.ops import io as _io
         data = _io.load_file(value["file"] if isinstance(value, dict) else value, emit.device)
-    ls, ll = TX.lines(data)
-    ks, kl = TX.field(data, ls, ll, b",", 0)
-    vs, vl = TX.field(data, ls, ll, b",", 1)
-    score = TX.parse_f64(data, vs, vl)
-    ok = (vs >= 0) & ~torch.isnan(score)
-    kl = torch.where(ok, kl, torch.zeros_like(kl))  # rows without a valid score emit nothing
-    emit.spans(ks, kl, score, score, 1, text=data)
+    # key = field 0, inputs (score, score, 1); rows without a valid score
+    # emit nothing.  On the GPU one fused kernel (lines, fields, parse, the
+    # LDS-combined fold); its specification is the ops/text.py chain
+    # TX.csv_rows (lines -> field -> parse_f64).
+    emit.csv(data, key=0, values=(1, 1, None), sep=",")
 
 
 def _rows(data: bytes):

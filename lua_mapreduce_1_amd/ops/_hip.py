@@ -41,6 +41,7 @@ _SIGS = {
     "mr_rec_gather_set_rows": [_i32],
     "mr_rec_scatter": [_p, _p, _u64, _i32, _p, _p, _p],
     "mr_span_prep": [_p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
+    "mr_csv_fold": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _u64, _u64, _p, _p, _p, _p],
     "mr_key_word": [_p, _p, _p, _p, _u64, _u32, _p, _p],
     "mr_key_meta": [_p, _p, _p, _u64, _p, _u32, _p, _p, _p],
     "mr_gather_key_bytes": [_p, _p, _p, _p, _u64, _p, _p, _u64, _p],

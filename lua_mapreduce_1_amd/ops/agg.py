@@ -163,6 +163,14 @@ class _ColsArg(ctypes.Structure):
                 ("rows_only", ctypes.c_longlong)]
 
 
+class _CsvArg(ctypes.Structure):
+    _fields_ = [("sep", ctypes.c_longlong), ("kf", ctypes.c_longlong), ("nin", ctypes.c_longlong),
+                ("vf", ctypes.c_longlong * MAXC), ("pin", ctypes.c_longlong * MAXC)]
+
+
+CSV_MAXV = 4  # value inputs of the fused CSV fold (csrc/hip/generic.hip CV_MAXV)
+
+
 def _scalar_bits(v, dtype: str) -> int:
     if dtype == "i64":
         return int(v)
@@ -395,6 +403,32 @@ class AggTable:
             for v, dt in vals:
                 rest_vals.append((g_in[id(v)][ns:] if isinstance(v, torch.Tensor) else v, dt))
             self._insert_rows(n - ns, rest_vals, text, g_st[ns:].contiguous(), sln[ns:].contiguous(), rep_base)
+
+    def insert_csv(self, text: torch.Tensor, rep_base: int, key: int, values, sep: int,
+                   rows_out: torch.Tensor) -> None:
+        """Fold mode on the GPU: every line of ``text`` -> key = field ``key``,
+        input i = the number in field ``values[i]`` (None: the constant 1),
+        folded by the fused kernel (mr_csv_fold: lines, fields, parse and the
+        LDS-combined insert in one pass over the bytes); rows with a missing
+        or empty key or a value that does not parse are dropped.
+        ``rows_out`` (int64 [1], device) += the rows folded."""
+        if not self.is_cuda or self.list_mode:
+            raise ValueError("insert_csv: a fold-mode table on the GPU")
+        if len(values) > CSV_MAXV or max([key] + [v for v in values if v is not None]) >= 1 << 20:
+            raise ValueError(f"insert_csv: at most {CSV_MAXV} value fields")
+        sa = _CsvArg()
+        sa.sep, sa.kf, sa.nin = int(sep) & 0xFF, int(key), len(values)
+        for i, v in enumerate(values):
+            sa.vf[i] = -1 if v is None else int(v)
+        keep: list = []
+        vals = []
+        for j, (dt, _op, i) in enumerate(self.cols_spec):
+            sa.pin[j] = -1 if i is None else int(i)
+            vals.append((1 if i is None else 0.0, dt))  # field inputs: no source array (the kernel parses)
+        a = self._cols_arg(vals, 0, keep)
+        t = self.keys
+        _hip.call("mr_csv_fold", *t._gtab(), t.cap, _hip.ptr(self.src), _hip.ptr(text), text.numel(), rep_base,
+                  ctypes.byref(sa), ctypes.byref(a), _hip.ptr(rows_out), _hip.stream(self.device))
 
     def _cols_arg(self, vals: list, n: int, keep: list):
         a = _ColsArg()

@@ -174,3 +174,29 @@ def parse_f64(text: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor, chec
 def parse_i64(text: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor, check: bool = False) -> torch.Tensor:
     """Decimal integers of the spans as int64 (malformed: 0, or raise with ``check``)."""
     return _parse(text, starts, lens, int, check)
+
+
+def csv_rows(text: torch.Tensor, key: int = 0, values=(1,), sep: str | int = ","):
+    """The rows of a CSV-like text as the general plane's ``emit.csv`` folds
+    them: (key starts, key lens, [one tensor or the constant 1 per value
+    input]) — key = field ``key`` of each line, input i = the number in field
+    ``values[i]`` (None: the constant 1).  A row with a missing key or value
+    field or a value that does not parse gets key length 0 (emit skips it).
+    The specification of the fused kernel (csrc/hip/generic.hip mr_csv_fold)."""
+    sep = sep if isinstance(sep, int) else ord(sep)
+    ls, ll = lines(text)
+    ks, kl = field(text, ls, ll, sep, key)
+    ok = ks >= 0
+    cols, cache = [], {}
+    for v in values:
+        if v is None:
+            cols.append(1)
+            continue
+        if v not in cache:
+            fs, fl = field(text, ls, ll, sep, v)
+            x = parse_f64(text, fs, fl)
+            ok &= (fs >= 0) & ~torch.isnan(x)
+            cache[v] = x
+        cols.append(cache[v])
+    kl = torch.where(ok, kl, torch.zeros_like(kl))
+    return ks, kl, cols

@@ -196,6 +196,16 @@ class GenericEmitter:
                                  "(the tensor the rep words index)")
         self.m.insert(int(hi.numel()), values, hi=hi, lo=lo, rep=rep, rep_add=add)
 
+    def csv(self, text=None, key: int = 0, values=(1,), sep=",") -> None:
+        """Every line of the chunk (or ``text``) as one row: key = field
+        ``key`` (``sep``-separated, 0-based), value input i = the number in
+        field ``values[i]`` (None: the constant 1); rows whose key is missing
+        or empty or whose value fields do not parse are dropped.  Typed folds
+        on the GPU run one fused kernel (lines, fields, parse and the
+        LDS-combined insert); otherwise the ops/text.py chain."""
+        t = self._text(text)
+        self.m.insert_csv(t, int(key), tuple(values), sep if isinstance(sep, int) else ord(sep))
+
     def words(self, text=None, *values) -> None:
         t = self._text(text)
         st, ln = TX.tokens(t)
@@ -241,6 +251,7 @@ class GenericMap:
         self.src = KeySource(self.device)
         self.emit = GenericEmitter(self)
         self.host: list = []
+        self._rows_dev = None
         self.rows = 0
         # list mode with a combiner: the table's postings are combined
         # whenever they pass combine_at (the batched MAX_MAP_RESULT,
@@ -272,6 +283,34 @@ class GenericMap:
         self.rows += n
         if self.reducers is not None and self.table.npost >= self.combine_at:
             self.combine()
+
+    def insert_csv(self, text: torch.Tensor, key: int, values: tuple, sep: int) -> None:
+        fused = (self.phys is not None and self.table.is_cuda and len(values) <= A.CSV_MAXV
+                 and len(values) == self.n_in)
+        if not fused:
+            ks, kl, cols = TX.csv_rows(text, key, values, sep)
+            t, base = self.src.locate(text)
+            self.insert(int(ks.numel()), tuple(cols), text=t, starts=ks, lens=kl, rep_base=base)
+            return
+        t, base = self.src.locate(text)
+        if self._rows_dev is None:
+            self._rows_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.table.src = self.src.source()
+        self.table.insert_csv(t, base, key, values, sep, self._rows_dev)
+
+    @property
+    def rows(self) -> int:
+        """Rows emitted into the table (the fused CSV fold counts its rows on
+        the device: read here, once per iteration)."""
+        if self._rows_dev is not None:
+            self._rows += int(self._rows_dev.item())
+            self._rows_dev = None
+        return self._rows
+
+    @rows.setter
+    def rows(self, v: int) -> None:
+        self._rows = int(v)
+        self._rows_dev = None
 
     def combine(self) -> bool:
         """Run the reduce module's combiner over every key's list and rebuild
