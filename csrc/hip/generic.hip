@@ -533,7 +533,7 @@ __device__ __forceinline__ void cv_global_fold(const Cols& c, int j, u64 slot, d
 
 __global__ void __launch_bounds__(CB_T) __attribute__((amdgpu_waves_per_eu(4, 8))) csv_fold_kernel(GTab g, const u8* __restrict__ text, u64 n, u64 rep_base,
                                                         CsvSpec sp, Cols c, u32 tiles,
-                                                        unsigned long long* __restrict__ rows_out) {
+                                                        unsigned long long* __restrict__ rows_out, int mode) {
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
   u64* tag = lds;
   u64* khi = tag + CB_SLOTS;
@@ -643,10 +643,11 @@ __global__ void __launch_bounds__(CB_T) __attribute__((amdgpu_waves_per_eu(4, 8)
         if (j < sp.nin && sp.vf[j] >= 0) need |= 1u << j;
       if (bad || klen <= 0 || (got & need) != need) continue;
       ++myrows;
+      if (mode == 1) continue;  // (ablation: parse only)
       u64 hi, lo;
       span_key(text, ks, (u64)klen, hi, lo);
       const u64 rep = make_rep(rep_base + ks, (u64)klen);
-      const int q = key_is_long(lo) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, hi, lo, rep);
+      const int q = (key_is_long(lo) || mode == 2) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, hi, lo, rep);
       if (q >= 0) {
         for (int j = 0; j < c.k; ++j) {
           const int i = sp.pin[j];
@@ -790,6 +791,8 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
   return (int)hipGetLastError();
 }
 
+static int g_csv_tiles = 0, g_csv_mode = 0;
+
 // Host-side mirror of CsvSpec.
 struct CsvArg {
   long long sep, kf, nin;
@@ -825,11 +828,21 @@ int mr_csv_fold(void* tag, void* thi, void* tlo, void* tval, void* trep, void* c
   const u64 ntiles = (n + CV_TILE - 1) / CV_TILE;
   u32 tiles = 4;  // 32 KiB per block, fewer when that leaves the chip short of blocks
   while (tiles > 1 && (ntiles + tiles - 1) / tiles < 1024) tiles >>= 1;
+  if (g_csv_tiles > 0) tiles = (u32)g_csv_tiles;
   const u64 nb = (ntiles + tiles - 1) / tiles;
   hipLaunchKernelGGL(csv_fold_kernel, dim3((unsigned)nb), dim3(CB_T), lds, stream,
                      ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), (const u8*)text, n, rep_base, sp, to_cols(a),
-                     tiles, (unsigned long long*)rows_out);
+                     tiles, (unsigned long long*)rows_out, g_csv_mode);
   return (int)hipGetLastError();
+}
+
+// Launch knobs of mr_csv_fold: tiles per block (0 = auto) and an ablation
+// mode (0 = normal, 1 = parse only, 2 = no LDS combine).
+int mr_csv_set_config(int tiles, int mode) {
+  if (tiles < 0 || tiles > 64 || mode < 0 || mode > 2) return -1;
+  g_csv_tiles = tiles;
+  g_csv_mode = mode;
+  return 0;
 }
 
 // ghist: zeroed u32 [8][256] (the first 4 rows are filled); nshort: zeroed u64

@@ -64,6 +64,12 @@ class Tunables:
                                "word-count map kernel shape (csrc/hip/wordcount3.hip): 0 = 512 threads, 2048 LDS "
                                "slots, 8 KiB spans, two workgroups per CU; 1 / 2 = 4096 slots over 32 / 64 KiB, one "
                                "workgroup per CU; 3 = 1024 threads, 4096 slots, 32 KiB")
+    csv_tiles: int = _knob("MR_CSV_TILES", 0,
+                           "fused CSV fold (emit.csv): 8 KiB tiles per workgroup (0 = auto: up to 4 while the "
+                           "launch keeps >= 1024 workgroups)")
+    csv_mode: int = _knob("MR_CSV_MODE", 0,
+                          "fused CSV fold ablation: 0 = normal, 1 = parse only (no insert: wrong results), 2 = no "
+                          "LDS combine")
     rec_gather_rows: int = _knob("MR_REC_GATHER_ROWS", 256,
                                  "record plane: rows per workgroup batch of the 16-byte row gather (256, or 128: "
                                  "half the LDS image, more workgroups per CU)")
