@@ -43,6 +43,9 @@ struct Cols {
   int op[MAXC];                // OP_SUM / OP_MIN / OP_MAX
   long long* post_slot;        // list mode: posting slot ids (sink)
   u64 post_base;               // list mode: sink index of row 0
+  u32 cs;                      // slot stride of the dst columns in elements (1: one array per
+                               // column; 4/8: one row of 8-byte columns per slot, so a key's
+                               // folds hit one cache line)
 };
 
 struct Keys {
@@ -89,19 +92,19 @@ __device__ __forceinline__ float rd_f32(const Cols& c, int j, u64 i) {
 __device__ __forceinline__ void fold_col(const Cols& c, int j, u64 i, u64 slot) {
   const int op = c.op[j];
   if (c.dtype[j] == VT_I64) {
-    long long* p = (long long*)c.dst[j] + slot;
+    long long* p = (long long*)c.dst[j] + slot * c.cs;
     const long long v = rd_i64(c, j, i);
     if (op == OP_MIN) atomicMin(p, v);
     else if (op == OP_MAX) atomicMax(p, v);
     else atomicAdd((unsigned long long*)p, (unsigned long long)v);
   } else if (c.dtype[j] == VT_F64) {
-    double* p = (double*)c.dst[j] + slot;
+    double* p = (double*)c.dst[j] + slot * c.cs;
     const double v = rd_f64(c, j, i);
     if (op == OP_MIN) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else if (op == OP_MAX) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
-    float* p = (float*)c.dst[j] + slot;
+    float* p = (float*)c.dst[j] + slot * c.cs;
     const float v = rd_f32(c, j, i);
     if (op == OP_MIN) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else if (op == OP_MAX) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -271,18 +274,18 @@ __device__ __forceinline__ void cb_lds_fold(long long* acc, const Cols& c, int j
 __device__ __forceinline__ void cb_global_fold(const Cols& c, int j, u64 slot, long long bits) {
   const int op = c.op[j];
   if (c.dtype[j] == VT_I64) {
-    long long* p = (long long*)c.dst[j] + slot;
+    long long* p = (long long*)c.dst[j] + slot * c.cs;
     if (op == OP_MIN) atomicMin(p, bits);
     else if (op == OP_MAX) atomicMax(p, bits);
     else atomicAdd((unsigned long long*)p, (unsigned long long)bits);
   } else if (c.dtype[j] == VT_F64) {
-    double* p = (double*)c.dst[j] + slot;
+    double* p = (double*)c.dst[j] + slot * c.cs;
     const double v = __longlong_as_double(bits);
     if (op == OP_MIN) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else if (op == OP_MAX) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
-    float* p = (float*)c.dst[j] + slot;
+    float* p = (float*)c.dst[j] + slot * c.cs;
     const float v = (float)__longlong_as_double(bits);
     if (op == OP_MIN) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else if (op == OP_MAX) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -512,18 +515,18 @@ __device__ __forceinline__ void cv_lds_fold(long long* acc, int dtype, int op, d
 __device__ __forceinline__ void cv_global_fold(const Cols& c, int j, u64 slot, double v) {
   const int op = c.op[j];
   if (c.dtype[j] == VT_I64) {
-    long long* p = (long long*)c.dst[j] + slot;
+    long long* p = (long long*)c.dst[j] + slot * c.cs;
     const long long x = (long long)v;
     if (op == OP_MIN) atomicMin(p, x);
     else if (op == OP_MAX) atomicMax(p, x);
     else atomicAdd((unsigned long long*)p, (unsigned long long)x);
   } else if (c.dtype[j] == VT_F64) {
-    double* p = (double*)c.dst[j] + slot;
+    double* p = (double*)c.dst[j] + slot * c.cs;
     if (op == OP_MIN) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else if (op == OP_MAX) __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
-    float* p = (float*)c.dst[j] + slot;
+    float* p = (float*)c.dst[j] + slot * c.cs;
     const float x = (float)v;
     if (op == OP_MIN) __hip_atomic_fetch_min(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else if (op == OP_MAX) __hip_atomic_fetch_max(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -531,18 +534,40 @@ __device__ __forceinline__ void cv_global_fold(const Cols& c, int j, u64 slot, d
   }
 }
 
-__global__ void __launch_bounds__(CB_T) __attribute__((amdgpu_waves_per_eu(4, 8))) csv_fold_kernel(GTab g, const u8* __restrict__ text, u64 n, u64 rep_base,
-                                                        CsvSpec sp, Cols c, u32 tiles,
-                                                        unsigned long long* __restrict__ rows_out, int mode) {
+// First set bit of a tile bit mask (1 bit per byte, u32 words) at a position
+// in [from, to), or `to`.
+__device__ __forceinline__ u32 cv_next_bit(const u32* w, u32 from, u32 to) {
+  u32 i = from;
+  while (i < to) {
+    const u32 m = w[i >> 5] >> (i & 31);
+    if (m) {
+      const u32 p = i + (u32)__builtin_ctz(m);
+      return p < to ? p : to;
+    }
+    i = (i | 31) + 1;
+  }
+  return to;
+}
+
+constexpr int CV_LP = 4096;  // line starts ranked per pass (a tile of shorter lines takes two passes)
+
+__global__ void __launch_bounds__(CB_T) __attribute__((amdgpu_waves_per_eu(4, 8)))
+csv_fold_kernel(GTab g, const u8* __restrict__ text, u64 n, u64 rep_base, CsvSpec sp, Cols c, u32 tiles,
+                unsigned long long* __restrict__ rows_out, int mode) {
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
   u64* tag = lds;
   u64* khi = tag + CB_SLOTS;
   u64* klo = khi + CB_SLOTS;
   u64* krep = klo + CB_SLOTS;
   long long* acc = (long long*)(krep + CB_SLOTS);  // [c.k][CB_SLOTS]
-  __shared__ u16 lpos[CV_TILE];
+  // the tile's bytes and its newline / separator bit masks: the per-line walks
+  // below read LDS (a byte-serial walk through global memory was latency-bound)
+  __shared__ __attribute__((aligned(16))) u64 tb64[CV_TILE / 8 + 2];
+  __shared__ u32 nlw[CV_TILE / 32 + 1], spw[CV_TILE / 32 + 1];
+  __shared__ u16 lpos[CV_LP];
   __shared__ u32 wsum[CB_T / 64];
   __shared__ u32 nclaimed, nrows;
+  const u8* tb = (const u8*)tb64;
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
   for (int q = t; q < CB_SLOTS; q += CB_T) {
@@ -550,32 +575,64 @@ __global__ void __launch_bounds__(CB_T) __attribute__((amdgpu_waves_per_eu(4, 8)
     klo[q] = 0;
     for (int j = 0; j < c.k; ++j) acc[j * CB_SLOTS + q] = cb_identity(c.dtype[j], c.op[j]);
   }
-  if (t == 0) nclaimed = nrows = 0;
+  if (t == 0) {
+    nclaimed = nrows = 0;
+    nlw[CV_TILE / 32] = spw[CV_TILE / 32] = 0;
+    tb64[CV_TILE / 8] = tb64[CV_TILE / 8 + 1] = 0;
+  }
+  int maxf = sp.kf;
+#pragma unroll
+  for (int j = 0; j < CV_MAXV; ++j)
+    if (j < sp.nin && sp.vf[j] > maxf) maxf = sp.vf[j];
+  u32 need = 0;  // inputs read from a field
+#pragma unroll
+  for (int j = 0; j < CV_MAXV; ++j)
+    if (j < sp.nin && sp.vf[j] >= 0) need |= 1u << j;
+  const u8 sep = (u8)sp.sep;
   __syncthreads();
   u32 claims = 0, myrows = 0;
   const u64 b0 = (u64)blockIdx.x * tiles * (u64)CV_TILE;
   for (u32 tt = 0; tt < tiles; ++tt) {
     const u64 tile = b0 + (u64)tt * CV_TILE;
     if (tile >= n) break;  // (uniform across the block)
+    const u64 tend = n - tile < (u64)CV_TILE ? n : tile + CV_TILE;  // bytes [tile, tend) are in LDS
+    const u32 tlen = (u32)(tend - tile);
     const u64 gpos = tile + (u64)t * CV_SEG;
-    u32 starts = 0;
-    if (gpos < n) {
-      u32 nlm = 0;
-      if (gpos + CV_SEG <= n && (((uintptr_t)(text + gpos)) & 15) == 0) {
-        const uint4 q = *reinterpret_cast<const uint4*>(text + gpos);
-        const u32 w[4] = {q.x, q.y, q.z, q.w};
+    u32 starts = 0, nlm = 0, spm = 0;
+    uint4 q = make_uint4(0u, 0u, 0u, 0u);
+    if (gpos + CV_SEG <= n && (((uintptr_t)(text + gpos)) & 15) == 0) {
+      q = *reinterpret_cast<const uint4*>(text + gpos);
+    } else if (gpos < n) {
+      u32 w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int i = 0; i < CV_SEG; ++i) nlm |= (((w[i >> 2] >> (8 * (i & 3))) & 0xFFu) == 10u ? 1u : 0u) << i;
-      } else {
+      for (int i = 0; i < CV_SEG; ++i)
+        if (gpos + i < n) w[i >> 2] |= (u32)text[gpos + i] << (8 * (i & 3));
+      q = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    reinterpret_cast<uint4*>(tb64)[t] = q;
+    {
+      const u32 w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-        for (int i = 0; i < CV_SEG; ++i) nlm |= (gpos + i < n && text[gpos + i] == 10 ? 1u : 0u) << i;
+      for (int i = 0; i < CV_SEG; ++i) {
+        const u32 ch = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        nlm |= (ch == 10u ? 1u : 0u) << i;
+        spm |= (ch == (u32)sep ? 1u : 0u) << i;
       }
+    }
+    if (gpos < n) {
       const u32 prev = (gpos == 0 || text[gpos - 1] == 10) ? 1u : 0u;
       starts = ((nlm << 1) | prev) & 0xFFFFu;
       const u64 lim = n - gpos;
-      if (lim < (u64)CV_SEG) starts &= (1u << lim) - 1u;
+      if (lim < (u64)CV_SEG) {
+        const u32 keep = (1u << lim) - 1u;
+        starts &= keep;
+        nlm &= keep;
+        spm &= keep;
+      }
     }
-    // block exclusive scan of the line-start counts -> lpos (tile offsets)
+    reinterpret_cast<u16*>(nlw)[t] = (u16)nlm;
+    reinterpret_cast<u16*>(spw)[t] = (u16)spm;
+    // block exclusive scan of the line-start counts
     const u32 cnt = (u32)__builtin_popcount(starts);
     u32 incl = cnt;
 #pragma unroll
@@ -592,38 +649,60 @@ __global__ void __launch_bounds__(CB_T) __attribute__((amdgpu_waves_per_eu(4, 8)
       base += w < wave ? x : 0u;
       total += x;
     }
-    u32 k = base + incl - cnt;
-    while (starts) {
-      const int i = __builtin_ctz(starts);
-      starts &= starts - 1;
-      lpos[k++] = (u16)(t * CV_SEG + i);
-    }
-    __syncthreads();
-    for (u32 x = t; x < total; x += CB_T) {
-      const u64 ls = tile + lpos[x];
-      // the line's end, then its fields (a trailing '\r' is dropped)
-      u64 le = ls;
-      while (le < n && text[le] != 10) ++le;
-      if (le > ls && text[le - 1] == 13) --le;
-      int f = 0;
-      u64 fs = ls, ks = 0;
-      int klen = -1;
-      double v0 = 1.0, v1 = 1.0, v2 = 1.0, v3 = 1.0;  // inputs without a field stay 1
-      u32 got = 0;  // bit j: input j's field was seen and parsed
-      bool bad = false;
-      for (u64 p = ls;; ++p) {
-        if (p == le || text[p] == (u8)sp.sep) {
-          const int flen = (int)(p - fs);
+    const u32 kx = base + incl - cnt;
+    for (u32 p0 = 0; p0 < total; p0 += CV_LP) {  // (uniform)
+      {
+        u32 k = kx, st = starts;
+        while (st) {
+          const int i = __builtin_ctz(st);
+          st &= st - 1;
+          if (k >= p0 && k < p0 + CV_LP) lpos[k - p0] = (u16)(t * CV_SEG + i);
+          ++k;
+        }
+      }
+      __syncthreads();
+      const u32 cntp = total - p0 < (u32)CV_LP ? total - p0 : (u32)CV_LP;
+      for (u32 x = t; x < cntp; x += CB_T) {
+        const u32 rs = lpos[x];  // tile offset of the line start
+        // line end: the next newline (LDS mask), past the tile through global memory
+        u32 re = cv_next_bit(nlw, rs, tlen);
+        u64 le = tile + re;
+        if (re == tlen) {
+          while (le < n && text[le] != 10) ++le;
+        }
+        if (le > tile + rs) {
+          const u64 l1 = le - 1;
+          if ((l1 < tend ? tb[l1 - tile] : text[l1]) == 13) --le;
+        }
+        int klen = -1;
+        u64 ks = 0;
+        double v0 = 1.0, v1 = 1.0, v2 = 1.0, v3 = 1.0;  // inputs without a field stay 1
+        u32 got = 0;
+        bool bad = false;
+        u64 fs = tile + rs;
+        for (int f = 0; f <= maxf; ++f) {
+          // the field's end: the next separator before the line end
+          const u64 lim = le < tend ? le : tend;
+          u64 fe;
+          if (fs < lim) {
+            fe = tile + cv_next_bit(spw, (u32)(fs - tile), (u32)(lim - tile));
+          } else {
+            fe = fs;
+          }
+          if (fe >= lim && fe < le) {  // the field runs past the tile
+            while (fe < le && text[fe] != sep) ++fe;
+          }
+          const int flen = (int)(fe - fs);
           if (f == sp.kf) {
             ks = fs;
             klen = flen;
           }
-          u32 hit = 0;  // the inputs this field feeds (one parse for all of them)
+          u32 hit = 0;
 #pragma unroll
           for (int j = 0; j < CV_MAXV; ++j) hit |= (j < sp.nin && sp.vf[j] == f ? 1u : 0u) << j;
           if (hit) {
             bool b = false;
-            const double v = tx::parse_f64(text + fs, flen, b);
+            const double v = fe <= tend ? tx::parse_f64(tb + (fs - tile), flen, b) : tx::parse_f64(text + fs, flen, b);
             bad |= b;
             got |= hit;
             if (hit & 1u) v0 = v;
@@ -631,42 +710,38 @@ __global__ void __launch_bounds__(CB_T) __attribute__((amdgpu_waves_per_eu(4, 8)
             if (hit & 4u) v2 = v;
             if (hit & 8u) v3 = v;
           }
-          if (p == le) break;
-          ++f;
-          fs = p + 1;
+          if (fe >= le) break;
+          fs = fe + 1;
         }
-      }
-      // every field-valued input present and numeric, a non-empty key
-      u32 need = 0;
-#pragma unroll
-      for (int j = 0; j < CV_MAXV; ++j)
-        if (j < sp.nin && sp.vf[j] >= 0) need |= 1u << j;
-      if (bad || klen <= 0 || (got & need) != need) continue;
-      ++myrows;
-      if (mode == 1) continue;  // (ablation: parse only)
-      u64 hi, lo;
-      span_key(text, ks, (u64)klen, hi, lo);
-      const u64 rep = make_rep(rep_base + ks, (u64)klen);
-      const int q = (key_is_long(lo) || mode == 2) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, hi, lo, rep);
-      if (q >= 0) {
-        for (int j = 0; j < c.k; ++j) {
-          const int i = sp.pin[j];
-          const double v = i >= 0 ? pick(v0, v1, v2, v3, i) : scalar_of(c, j);
-          cv_lds_fold(&acc[j * CB_SLOTS + q], c.dtype[j], c.op[j], v);
-        }
-      } else {
-        u64 slot = 0;
-        const int r = gtab_insert(g, hi, lo, 0, rep, OP_NONE, &slot);
-        claims += r == 2;
-        if (r)
+        if (bad || klen <= 0 || (got & need) != need) continue;
+        ++myrows;
+        if (mode == 1) continue;  // (ablation: parse only)
+        u64 hi, lo;
+        if (ks + (u64)klen <= tend) span_key(tb, ks - tile, (u64)klen, hi, lo);
+        else span_key(text, ks, (u64)klen, hi, lo);
+        const u64 rep = make_rep(rep_base + ks, (u64)klen);
+        const int sl = (key_is_long(lo) || mode == 2) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, hi, lo, rep);
+        if (sl >= 0) {
           for (int j = 0; j < c.k; ++j) {
             const int i = sp.pin[j];
             const double v = i >= 0 ? pick(v0, v1, v2, v3, i) : scalar_of(c, j);
-            cv_global_fold(c, j, slot, v);
+            cv_lds_fold(&acc[j * CB_SLOTS + sl], c.dtype[j], c.op[j], v);
           }
+        } else {
+          u64 slot = 0;
+          const int r = gtab_insert(g, hi, lo, 0, rep, OP_NONE, &slot);
+          claims += r == 2;
+          if (r)
+            for (int j = 0; j < c.k; ++j) {
+              const int i = sp.pin[j];
+              const double v = i >= 0 ? pick(v0, v1, v2, v3, i) : scalar_of(c, j);
+              cv_global_fold(c, j, slot, v);
+            }
+        }
       }
+      __syncthreads();
     }
-    __syncthreads();
+    __syncthreads();  // (a tile without line starts: wsum and the LDS tile are rewritten next)
   }
   if (myrows) atomicAdd(&nrows, myrows);
   __syncthreads();
@@ -729,6 +804,7 @@ struct ColsArg {
   void* post_slot;
   unsigned long long post_base;
   long long rows_only;  // 1: one row per thread (distinct keys: an LDS combine has nothing to fold)
+  long long cstride;    // slot stride of the dst columns (elements; 0 = 1)
 };
 
 static Cols to_cols(const ColsArg* a) {
@@ -745,6 +821,7 @@ static Cols to_cols(const ColsArg* a) {
   }
   c.post_slot = (long long*)a->post_slot;
   c.post_base = a->post_base;
+  c.cs = a->cstride > 0 ? (u32)a->cstride : 1u;
   return c;
 }
 

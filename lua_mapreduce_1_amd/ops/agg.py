@@ -160,7 +160,7 @@ class _ColsArg(ctypes.Structure):
                 ("stype", ctypes.c_longlong * MAXC), ("sbits", ctypes.c_longlong * MAXC),
                 ("dst", ctypes.c_void_p * MAXC), ("dtype", ctypes.c_longlong * MAXC),
                 ("op", ctypes.c_longlong * MAXC), ("post_slot", ctypes.c_void_p), ("post_base", ctypes.c_ulonglong),
-                ("rows_only", ctypes.c_longlong)]
+                ("rows_only", ctypes.c_longlong), ("cstride", ctypes.c_longlong)]
 
 
 class _CsvArg(ctypes.Structure):
@@ -193,15 +193,28 @@ class AggTable:
         self.list_dtype = list_dtype
         self.src: torch.Tensor | None = None
         self.cap = next_pow2(max(1024, int(capacity)))
+        self.cstride = 1
         if self.is_cuda:
             self.keys = HashTable(self.cap, self.device, op="none")
-            self.cols = [] if self.list_mode else [torch.empty(self.cap, dtype=DTYPES[dt], device=self.device)
-                                                   for dt, _op, _i in cols]
+            self.cols = [] if self.list_mode else self._alloc_cols(cols)
             self._fill_cols()
             self.post_slot = self.post_val = None
         else:
             self._pending: list = []
         self.npost = 0
+
+    def _alloc_cols(self, cols: list) -> list:
+        """The physical columns on the GPU.  With more than one column, all
+        of 8 bytes, they are one row per slot (4 or 8 words: a row never
+        straddles a 64-byte line), so the folds of a key touch one line of
+        memory instead of one per column (MR_AGG_ROWS); otherwise one array
+        per column."""
+        k = len(cols)
+        if TUNABLES.agg_rows and k > 1 and all(dt in ("i64", "f64") for dt, _op, _i in cols):
+            self.cstride = 4 if k <= 4 else 8
+            buf = torch.empty(self.cap, self.cstride, dtype=torch.int64, device=self.device)
+            return [buf[:, j].view(DTYPES[dt]) for j, (dt, _op, _i) in enumerate(cols)]
+        return [torch.empty(self.cap, dtype=DTYPES[dt], device=self.device) for dt, _op, _i in cols]
 
     @property
     def is_cuda(self) -> bool:
@@ -254,6 +267,7 @@ class AggTable:
             a = _ColsArg()
             a.k = len(vals)
             a.list = 1 if self.list_mode else 0
+            a.cstride = 1 if self.list_mode else self.cstride
             keep = []
             for j, (v, dt) in enumerate(vals):
                 if isinstance(v, torch.Tensor):
@@ -434,6 +448,7 @@ class AggTable:
         a = _ColsArg()
         a.k = len(vals)
         a.list = 0
+        a.cstride = self.cstride
         for j, (v, dt) in enumerate(vals):
             if isinstance(v, torch.Tensor):
                 if v.numel() != n:

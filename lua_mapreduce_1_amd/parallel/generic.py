@@ -42,6 +42,7 @@ it receives in a second table and orders the keys by (partition, key bytes).
 """
 from __future__ import annotations
 
+import contextlib
 import sys
 import time
 import traceback
@@ -586,10 +587,16 @@ class GenericPlane:
         seen after the map, which then re-runs with a larger one)."""
         self.map.table.rehome_long_keys(buf, lo, hi, heap, H)
 
-    def _map(self, jobs, recs, j0, j1) -> None:
+    def _issue_ahead(self) -> None:
+        f, self._after_issue = getattr(self, "_after_issue", None), None
+        if f is not None:
+            f()
+
+    def _map_prelude(self, jobs, j0, j1) -> bool:
+        """Line numbering and table capacity for a map about to be issued;
+        returns whether its input streams through the capped arenas."""
         eng = self.eng
         mp = self.map
-        dmap = eng.dmap
         streamed = False
         if eng.device_input == "split" and j1 > j0:
             ids = eng._split_ids(jobs, j0, j1)
@@ -604,36 +611,62 @@ class GenericPlane:
             # the capacity target moved since this table was made (grown, or fitted)
             mp.table = A.AggTable(self._cap, eng.device, self.phys.cols if self.phys is not None else None,
                                   self.dtype)
+        return streamed
+
+    def _map_chunks(self, jobs, recs, j0, j1, streamed: bool) -> list:
+        """Issue one attempt of the map: every staged chunk through the
+        module's device_mapfn (kernels queued, no synchronisation); returns
+        the job ranges whose map raised."""
+        eng = self.eng
+        mp = self.map
+        dmap = eng.dmap
+        mp.begin(None)
+        mp.src.fixed = streamed
+        broken = []
+        for (a, b), data in eng._stage_chunks(jobs, j0, j1):
+            if all(recs[j].status == STATUS.FAILED for j in range(a, b)):
+                continue
+            if eng.device_input == "split":
+                mp.src.set_arena(eng.arena)
+            t0, c0 = time.time(), time.process_time()
+            for j in range(a, b):
+                recs[j].status, recs[j].started, recs[j].worker = STATUS.RUNNING, t0, eng.rank
+            mp.emit.chunk = data if isinstance(data, torch.Tensor) and data.dtype == torch.uint8 else None
+            keys = [jobs[j][0] for j in range(a, b)]
+            try:
+                dmap(keys if b - a > 1 else keys[0], data, mp.emit)
+                mp.flush_host()
+            except (NeedsHostMap, StreamedSourceError):
+                raise
+            except Exception:  # noqa: BLE001
+                mp.host = []
+                broken.append((a, b))
+                sys.stderr.write("Error executing a job: %s\n" % traceback.format_exc())
+            t1 = time.time()
+            for j in range(a, b):
+                if recs[j].status != STATUS.FAILED:
+                    recs[j].status = STATUS.WRITTEN
+                recs[j].written = t1
+                recs[j].real_time = (t1 - t0) / (b - a)
+                recs[j].cpu_time = (time.process_time() - c0) / (b - a)
+        return broken
+
+    def _map(self, jobs, recs, j0, j1, issued: tuple | None = None) -> None:
+        """The rank's map: issue, synchronise, and re-run on a full table, a
+        raising job (BROKEN / FAILED) or a full streaming key heap.
+        ``issued``: (streamed, broken) of a first attempt already queued (the
+        map the previous iteration issued ahead)."""
+        eng = self.eng
+        streamed = issued[0] if issued is not None else self._map_prelude(jobs, j0, j1)
         for _attempt in range(64):
-            mp.begin(None)
-            mp.src.fixed = streamed
-            broken = []
-            for (a, b), data in eng._stage_chunks(jobs, j0, j1):
-                if all(recs[j].status == STATUS.FAILED for j in range(a, b)):
-                    continue
-                if eng.device_input == "split":
-                    mp.src.set_arena(eng.arena)
-                t0, c0 = time.time(), time.process_time()
-                for j in range(a, b):
-                    recs[j].status, recs[j].started, recs[j].worker = STATUS.RUNNING, t0, eng.rank
-                mp.emit.chunk = data if isinstance(data, torch.Tensor) and data.dtype == torch.uint8 else None
-                keys = [jobs[j][0] for j in range(a, b)]
-                try:
-                    dmap(keys if b - a > 1 else keys[0], data, mp.emit)
-                    mp.flush_host()
-                except (NeedsHostMap, StreamedSourceError):
-                    raise
-                except Exception:  # noqa: BLE001
-                    mp.host = []
-                    broken.append((a, b))
-                    sys.stderr.write("Error executing a job: %s\n" % traceback.format_exc())
-                t1 = time.time()
-                for j in range(a, b):
-                    if recs[j].status != STATUS.FAILED:
-                        recs[j].status = STATUS.WRITTEN
-                    recs[j].written = t1
-                    recs[j].real_time = (t1 - t0) / (b - a)
-                    recs[j].cpu_time = (time.process_time() - c0) / (b - a)
+            mp = self.map
+            if issued is not None and _attempt == 0:
+                broken = issued[1]
+            else:
+                if _attempt:
+                    self._map_prelude(jobs, j0, j1)  # (a regrown table)
+                broken = self._map_chunks(jobs, recs, j0, j1, streamed)
+            self._issue_ahead()  # (before the map's first synchronisation)
             n, ovf = mp.table.stats()
             if streamed and int(ops.host_read(eng._stream_heap)[1]):
                 # the key heap ran out: some long keys still point into a ring
@@ -665,6 +698,48 @@ class GenericPlane:
                 self._cap = fit  # grown past the key count (16x after an overflow): fitted for the next maps
             return
         raise RuntimeError("general plane: the map did not converge (table regrowth / retries)")
+
+    # -- pipelined iterations ---------------------------------------------------------
+    def _pipelined(self) -> bool:
+        """Iteration q+1's map is issued while iteration q reduces (its own
+        map state and stream): GPU tables, split inputs prefetched by a pure
+        taskfn, no map checkpoints, no streaming."""
+        eng = self.eng
+        return (bool(eng.pipeline) and eng.device.type == "cuda" and eng._can_pipeline()
+                and eng._map_ckpt_path() is None and bool(eng.streams))
+
+    def _map_of(self, q: int) -> "GenericMap":
+        """The map state of iteration q when iterations are pipelined (two,
+        alternating: the next map fills one while this one is reduced)."""
+        if getattr(self, "_maps", None) is None:
+            self._maps = [self.map, None]
+        m = self._maps[q % 2]
+        if m is None:
+            m = self._maps[q % 2] = GenericMap(self.eng.device, self._cap, self.phys, self.dtype, self.reducers,
+                                               int(self.eng.params.get("combine_postings") or 0))
+        return m
+
+    def _issue_next_map(self, jobs, j0, j1, q: int) -> None:
+        """Queue iteration q+1's map (same jobs: the taskfn is pure) on its
+        own stream and map state; run_iteration(q+1) synchronises it."""
+        from .planes import _records
+        eng = self.eng
+        eng._prefetch(jobs, j0, j1, q + 1)
+        cur = self.map
+        eng._use(q + 1)
+        try:
+            with torch.cuda.stream(eng.streams[eng.tslot]):
+                self.map = self._map_of(q + 1)
+                t0 = time.time()
+                recs = _records(eng, jobs, j0, j1, t0)
+                streamed = self._map_prelude(jobs, j0, j1)
+                broken = self._map_chunks(jobs, recs, j0, j1, streamed)
+                nxt = self.map
+        finally:
+            self.map = cur
+            eng._use(q)
+        self._pending = {"q": q + 1, "jobs": jobs, "recs": recs, "j0": j0, "j1": j1, "t0": t0, "map": nxt,
+                         "issued": (streamed, broken)}
 
     # -- map checkpoints (split-level restart, SURVEY.md §5.4) ------------------------
     def _save_map(self, recs=None, j0: int = 0, j1: int = 0) -> None:
@@ -923,25 +998,62 @@ class GenericPlane:
 
     # -- one iteration --------------------------------------------------------------
     def run_iteration(self, prefetch_next, lookahead):
-        from .planes import DeviceResult, _records, _result_jobs, reduce_cap_bytes
         eng = self.eng
         eng.iteration += 1
         q = eng._seq
         eng._seq += 1
         eng._use(q)
+        pend, self._pending = getattr(self, "_pending", None), None
+        if pend is not None and pend["q"] != q:
+            pend = None
+        pipe = self._pipelined()
+        stream = eng.streams[eng.tslot] if (pipe or pend is not None) else None
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            return self._iteration(q, prefetch_next, lookahead, pend, pipe)
+
+    def _iteration(self, q, prefetch_next, lookahead, pend, pipe):
+        from .planes import DeviceResult, _records, _result_jobs, reduce_cap_bytes
+        eng = self.eng
         res = DeviceResult()
         T = res.timings
         t_start = time.time()
-        jobs = eng._jobs()
-        j0, j1 = eng._assign(jobs)
-        t0 = time.time()
-        recs = _records(eng, jobs, j0, j1, t0)
+        if pend is not None:  # this iteration's map was queued by the previous one
+            jobs, recs, j0, j1, t0 = pend["jobs"], pend["recs"], pend["j0"], pend["j1"], pend["t0"]
+            self.map = pend["map"]
+        else:
+            jobs = eng._jobs()
+            j0, j1 = eng._assign(jobs)
+            t0 = time.time()
+            recs = _records(eng, jobs, j0, j1, t0)
+            if pipe:
+                self.map = self._map_of(q)
         res.map_jobs = recs
+        # the next iterations' input copies (pure taskfn, split inputs) queue
+        # right behind this map's, so the copy engine streams while this
+        # iteration reduces: its arena was last read by iteration q - 2 or
+        # earlier, whose key bytes were gathered (and synchronised) by its order
+        ahead = 0 if not (prefetch_next if prefetch_next is not None else eng.prefetch) else (
+            2 if lookahead is None else min(lookahead, 2))
+        self._after_issue = (lambda: eng._prefetch_ahead(jobs, j0, j1, q, ahead)) if ahead else None
+        # iteration q+1's map is queued once this iteration's order is (it runs
+        # on its own stream while this one's tail and downloads finish)
+        next_map = [pipe and ahead > 0]
+
+        def issue_next_map():
+            if next_map[0]:
+                next_map[0] = False
+                with trace.range("mr.gen.issue_next"):
+                    self._issue_next_map(jobs, j0, j1, q)
         with trace.range("mr.gen.map"):
-            if not self._restore_map(recs, j0, j1):
+            if pend is not None:
+                self._map(jobs, recs, j0, j1, issued=pend["issued"])
+                self.map.combine()
+                self._save_map(recs, j0, j1)
+            elif not self._restore_map(recs, j0, j1):
                 self._map(jobs, recs, j0, j1)
                 self.map.combine()  # the end-of-map combiner (job.lua:198-202); no-op without one
                 self._save_map(recs, j0, j1)
+            self._issue_ahead()
         eng._maybe_inject_fault("shuffle")
         T["map"] = time.time() - t0
         t1 = time.time()
@@ -977,6 +1089,7 @@ class GenericPlane:
             # moved to host memory before the next
             part, rounds = groups
             parts, counts, nk = {}, [0] * R, 0
+            issue_next_map()
             for grp in rounds:
                 sub, sub_space = self._select(keys, space, part, grp)
                 with trace.range("mr.gen.order"):
@@ -994,6 +1107,7 @@ class GenericPlane:
         else:
             with trace.range("mr.gen.order"):
                 out = self._order(keys, src, space)
+                issue_next_map()
                 counts = out["counts"].cpu().tolist()
             self.reduce_rounds = 1
             _result_jobs(eng, res, counts, t1)

@@ -64,6 +64,10 @@ class Tunables:
                                "word-count map kernel shape (csrc/hip/wordcount3.hip): 0 = 512 threads, 2048 LDS "
                                "slots, 8 KiB spans, two workgroups per CU; 1 / 2 = 4096 slots over 32 / 64 KiB, one "
                                "workgroup per CU; 3 = 1024 threads, 4096 slots, 32 KiB")
+    agg_rows: bool = _knob("MR_AGG_ROWS", False,
+                           "general plane, typed folds on the GPU: the 8-byte physical columns of a table as one "
+                           "row per slot (a key's folds touch one cache line) instead of one array per column; measured "
+                           "equal or slower on the CSV group-by, profiles/r4/general/csv_ab/)")
     csv_tiles: int = _knob("MR_CSV_TILES", 0,
                            "fused CSV fold (emit.csv): 8 KiB tiles per workgroup (0 = auto: up to 4 while the "
                            "launch keeps >= 1024 workgroups)")
