@@ -22,79 +22,168 @@ constexpr int T = 256;
 constexpr int SEG = 16;
 constexpr u64 TILE = (u64)T * SEG;  // 4096 bytes per workgroup
 
-// Bit i of the result: an item starts at byte g + i (mode 0: token start,
-// mode 1: byte == c).  Bytes past n are whitespace / not c.
-__device__ __forceinline__ u32 item_mask(const u8* __restrict__ text, u64 n, u64 g, int mode, u32 c) {
-  u32 b[SEG];
+// One thread's 16 bytes (bytes past n read as whitespace, not c): item mask
+// (bit i: an item starts at byte g + i; mode 0: token start, mode 1: byte ==
+// c), whitespace mask and newline mask.
+struct SegMasks {
+  u32 item, ws, nl;
+};
+
+__device__ __forceinline__ SegMasks seg_masks(const u8* __restrict__ text, u64 n, u64 g, int mode, u32 c) {
+  u32 w[4] = {0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u};
   if (g + SEG <= n && (((uintptr_t)(text + g)) & 15) == 0) {
     const uint4 q = *reinterpret_cast<const uint4*>(text + g);
-    const u32 w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int i = 0; i < SEG; ++i) b[i] = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+    w[0] = q.x;
+    w[1] = q.y;
+    w[2] = q.z;
+    w[3] = q.w;
   } else {
 #pragma unroll
-    for (int i = 0; i < SEG; ++i) b[i] = g + i < n ? (u32)text[g + i] : 32u;
+    for (int i = 0; i < SEG; ++i)
+      if (g + i < n) w[i >> 2] = (w[i >> 2] & ~(0xFFu << (8 * (i & 3)))) | ((u32)text[g + i] << (8 * (i & 3)));
   }
-  u32 m = 0;
-  if (mode == 1) {
+  SegMasks r{0u, 0u, 0u};
 #pragma unroll
-    for (int i = 0; i < SEG; ++i) m |= (b[i] == c && g + i < n ? 1u : 0u) << i;
-    return m;
+  for (int i = 0; i < SEG; ++i) {
+    const u32 b = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+    const bool in = g + i < n;
+    r.ws |= (is_ws(b) ? 1u : 0u) << i;
+    r.nl |= (b == 10u && in ? 1u : 0u) << i;
+    if (mode == 1) r.item |= (b == c && in ? 1u : 0u) << i;
   }
-  u32 ws = 0;
-#pragma unroll
-  for (int i = 0; i < SEG; ++i) ws |= (is_ws(b[i]) ? 1u : 0u) << i;
-  const u32 prev_ws = (g == 0 || is_ws(text[g - 1])) ? 1u : 0u;
-  return (~ws) & ((ws << 1) | prev_ws) & 0xFFFFu;
+  if (mode == 0) {
+    const u32 prev_ws = (g == 0 || is_ws(text[g - 1])) ? 1u : 0u;
+    r.item = (~r.ws) & ((r.ws << 1) | prev_ws) & 0xFFFFu;
+  }
+  return r;
 }
 
+// Per tile: the number of items, and (line_counts != null) of newlines.
 __global__ void __launch_bounds__(T) text_count_kernel(const u8* __restrict__ text, u64 n, int mode, u32 c,
-                                                      long long* __restrict__ tile_counts) {
-  __shared__ u32 wsum[T / 64];
+                                                      long long* __restrict__ tile_counts,
+                                                      long long* __restrict__ line_counts) {
+  __shared__ u32 wsum[T / 64], nsum[T / 64];
   const u64 g = (u64)blockIdx.x * TILE + (u64)threadIdx.x * SEG;
-  u32 cnt = g < n ? (u32)__builtin_popcount(item_mask(text, n, g, mode, c)) : 0u;
+  u32 cnt = 0, nlc = 0;
+  if (g < n) {
+    const SegMasks m = seg_masks(text, n, g, mode, c);
+    cnt = (u32)__builtin_popcount(m.item);
+    nlc = (u32)__builtin_popcount(m.nl);
+  }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o);
+    nlc += __shfl_xor(nlc, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    wsum[threadIdx.x >> 6] = cnt;
+    nsum[threadIdx.x >> 6] = nlc;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    u32 s = 0;
+    u32 s = 0, q = 0;
 #pragma unroll
-    for (int w = 0; w < T / 64; ++w) s += wsum[w];
+    for (int w = 0; w < T / 64; ++w) {
+      s += wsum[w];
+      q += nsum[w];
+    }
     tile_counts[blockIdx.x] = (long long)s;
+    if (line_counts) line_counts[blockIdx.x] = (long long)q;
   }
 }
+
+// Items of a tile in text order at tile_off[tile] + rank: positions, token
+// lengths (out_len) and 0-based line numbers (out_line, from the newline
+// counts' exclusive scan line_off).  Token ends come from the tile's
+// whitespace masks in LDS (a token past the tile continues through global
+// memory); a tile's items are ranked by a wave64 scan and staged in LDS, then
+// written out coalesced.
+constexpr int TE_MAX = (int)TILE / 2 + 1;  // items per tile: tokens are >= 1 byte apart
 
 __global__ void __launch_bounds__(T) text_emit_kernel(const u8* __restrict__ text, u64 n, int mode, u32 c,
                                                      const long long* __restrict__ tile_off, u64 cap,
-                                                     long long* __restrict__ out_pos, int* __restrict__ out_len) {
-  __shared__ u32 sh[T];
+                                                     long long* __restrict__ out_pos, int* __restrict__ out_len,
+                                                     const long long* __restrict__ line_off,
+                                                     long long* __restrict__ out_line) {
+  __shared__ u16 wsm[T + 1];
+  __shared__ u16 ipos[TILE];        // tile offsets of the items (mode 1 may have TILE of them)
+  __shared__ u32 ilen[TE_MAX];      // token lengths (mode 0)
+  __shared__ u16 iline[TILE];       // newlines of the tile before each item
+  __shared__ u32 wsum[T / 64], nsum[T / 64];
   const int t = threadIdx.x;
-  const u64 g = (u64)blockIdx.x * TILE + (u64)t * SEG;
-  u32 m = g < n ? item_mask(text, n, g, mode, c) : 0u;
-  const u32 cnt = (u32)__builtin_popcount(m);
-  sh[t] = cnt;
-  __syncthreads();
-  for (int o = 1; o < T; o <<= 1) {
-    const u32 y = t >= o ? sh[t - o] : 0u;
-    __syncthreads();
-    sh[t] += y;
-    __syncthreads();
+  const int lane = t & 63, wave = t >> 6;
+  const u64 tile = (u64)blockIdx.x * TILE;
+  const u64 g = tile + (u64)t * SEG;
+  SegMasks m{0u, 0u, 0u};
+  if (g < n) m = seg_masks(text, n, g, mode, c);
+  else m.ws = 0xFFFFu;
+  wsm[t] = (u16)m.ws;
+  if (t == 0) wsm[T] = 0;  // (past the tile: not whitespace -> continue in global memory)
+  const u32 cnt = (u32)__builtin_popcount(m.item);
+  const u32 nlc = (u32)__builtin_popcount(m.nl);
+  u32 ci = cnt, ni = nlc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 a = __shfl_up(ci, o), b = __shfl_up(ni, o);
+    if (lane >= o) {
+      ci += a;
+      ni += b;
+    }
   }
-  u64 k = (u64)tile_off[blockIdx.x] + sh[t] - cnt;
-  while (m) {
-    const int i = __builtin_ctz(m);
-    m &= m - 1;
-    const u64 p = g + i;
-    if (k < cap) {
-      out_pos[k] = (long long)p;
-      if (out_len) {
-        u64 e = p + 1;
-        while (e < n && !is_ws(text[e])) ++e;
-        out_len[k] = (int)(e - p);
+  if (lane == 63) {
+    wsum[wave] = ci;
+    nsum[wave] = ni;
+  }
+  __syncthreads();
+  u32 cb = 0, nb = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < T / 64; ++w) {
+    cb += w < wave ? wsum[w] : 0u;
+    nb += w < wave ? nsum[w] : 0u;
+    total += wsum[w];
+  }
+  u32 k = cb + ci - cnt;         // this thread's first item rank in the tile
+  const u32 nl0 = nb + ni - nlc;  // newlines of the tile before this segment
+  u32 it = m.item;
+  while (it) {
+    const int i = __builtin_ctz(it);
+    it &= it - 1;
+    ipos[k] = (u16)(t * SEG + i);
+    if (out_line) iline[k] = (u16)(nl0 + (u32)__builtin_popcount(m.nl & ((1u << i) - 1u)));
+    if (out_len) {
+      // the token's end: the next whitespace byte (own mask, then the next
+      // segments' masks in LDS, then global memory past the tile)
+      u32 rest = (m.ws >> (i + 1)) << (i + 1);
+      u32 e;
+      if (rest) {
+        e = t * SEG + (u32)__builtin_ctz(rest);
+      } else {
+        int s2 = t + 1;
+        e = (u32)TILE;
+        for (; s2 < T; ++s2) {
+          const u32 w2 = wsm[s2];
+          if (w2) {
+            e = (u32)s2 * SEG + (u32)__builtin_ctz(w2);
+            break;
+          }
+        }
       }
+      u64 ge = tile + e;
+      if (e == (u32)TILE)
+        while (ge < n && !is_ws(text[ge])) ++ge;
+      ilen[k] = (u32)(ge - (tile + t * SEG + i));
     }
     ++k;
+  }
+  __syncthreads();
+  const u64 k0 = (u64)tile_off[blockIdx.x];
+  const long long lb = out_line ? line_off[blockIdx.x] : 0;
+  for (u32 x = t; x < total; x += T) {
+    const u64 q = k0 + x;
+    if (q >= cap) break;
+    out_pos[q] = (long long)(tile + ipos[x]);
+    if (out_len) out_len[q] = (int)ilen[x];
+    if (out_line) out_line[q] = lb + (long long)iline[x];
   }
 }
 
@@ -187,18 +276,24 @@ extern "C" {
 
 u64 mr_text_tiles(u64 n) { return (n + TILE - 1) / TILE; }
 
-int mr_text_count(const void* text, u64 n, int mode, u32 c, void* tile_counts, hipStream_t s) {
+// line_counts (optional): per-tile newline counts (for mr_text_emit's line numbers)
+int mr_text_count(const void* text, u64 n, int mode, u32 c, void* tile_counts, void* line_counts, hipStream_t s) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(text_count_kernel, dim3((unsigned)mr_text_tiles(n)), dim3(T), 0, s, (const u8*)text, n, mode, c,
-                     (long long*)tile_counts);
+                     (long long*)tile_counts, (long long*)line_counts);
   return (int)hipGetLastError();
 }
 
+// out_len (mode 0) and out_line (with line_off = exclusive scan of the newline
+// counts) are optional.
 int mr_text_emit(const void* text, u64 n, int mode, u32 c, const void* tile_off, u64 cap, void* out_pos,
-                 void* out_len, hipStream_t s) {
+                 void* out_len, const void* line_off, void* out_line, hipStream_t s) {
   if (n == 0) return 0;
+  if (out_len && mode != 0) return -1;
+  if (out_line && !line_off) return -1;
   hipLaunchKernelGGL(text_emit_kernel, dim3((unsigned)mr_text_tiles(n)), dim3(T), 0, s, (const u8*)text, n, mode, c,
-                     (const long long*)tile_off, cap, (long long*)out_pos, (int*)out_len);
+                     (const long long*)tile_off, cap, (long long*)out_pos, (int*)out_len,
+                     (const long long*)line_off, (long long*)out_line);
   return (int)hipGetLastError();
 }
 

@@ -57,10 +57,9 @@ def device_mapfn(key, value, emit):
     import torch
     from lua_mapreduce_1_amd.ops import text as TX
     data = _data(value, emit)
-    st, ln = TX.tokens(data)
+    st, ln, line = TX.tokens(data, lines=True)  # tokens and their line numbers in one pass
     if st.numel() < 2:
         return
-    line = TX.line_index(data, st)
     start = st[:-1]
     end = st[1:] + ln[1:].to(torch.int64)
     same_line = line[1:] == line[:-1]

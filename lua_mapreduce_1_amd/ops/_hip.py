@@ -107,8 +107,8 @@ _SIGS = {
     "mr_col_fill": [_p, _u64, ctypes.c_longlong, _i32, _p],
     "mr_set_long_mask_generic": [_u64],
     "mr_text_tiles": [_u64],
-    "mr_text_count": [_p, _u64, _i32, _u32, _p, _p],
-    "mr_text_emit": [_p, _u64, _i32, _u32, _p, _u64, _p, _p, _p],
+    "mr_text_count": [_p, _u64, _i32, _u32, _p, _p, _p],
+    "mr_text_emit": [_p, _u64, _i32, _u32, _p, _u64, _p, _p, _p, _p, _p],
     "mr_text_field": [_p, _p, _p, _u64, _u32, _i32, _p, _p, _p],
     "mr_text_parse_f64": [_p, _p, _p, _u64, _p, _p, _p],
     "mr_text_parse_i64": [_p, _p, _p, _u64, _p, _p, _p],

@@ -23,40 +23,53 @@ def _np(t: torch.Tensor) -> np.ndarray:
     return t.detach().cpu().numpy()
 
 
-def _scan(text: torch.Tensor, mode: int, byte: int, want_len: bool):
+def _scan(text: torch.Tensor, mode: int, byte: int, want_len: bool, want_line: bool = False):
+    """(positions, lengths | None, line numbers | None) of the items."""
     n = text.numel()
     d = text.device
     if n == 0:
         z = torch.zeros(0, dtype=torch.int64, device=d)
-        return z, (torch.zeros(0, dtype=torch.int32, device=d) if want_len else None)
+        return z, (torch.zeros(0, dtype=torch.int32, device=d) if want_len else None), (z.clone() if want_line else None)
     if text.is_cuda:
         from .primitives import exclusive_scan
         assert text.dtype == torch.uint8 and text.is_contiguous()
         s = _hip.stream(d)
         tiles = int(_hip.lib().mr_text_tiles(n))
         counts = torch.empty(tiles, dtype=torch.int64, device=d)
-        _hip.call("mr_text_count", _hip.ptr(text), n, mode, byte, _hip.ptr(counts), s)
+        nls = torch.empty(tiles, dtype=torch.int64, device=d) if want_line else None
+        _hip.call("mr_text_count", _hip.ptr(text), n, mode, byte, _hip.ptr(counts), _hip.ptr(nls), s)
         off, total = exclusive_scan(counts)
+        loff = exclusive_scan(nls)[0] if want_line else None
         m = int(total.item())
         pos = torch.empty(m, dtype=torch.int64, device=d)
         ln = torch.empty(m, dtype=torch.int32, device=d) if want_len else None
-        _hip.call("mr_text_emit", _hip.ptr(text), n, mode, byte, _hip.ptr(off), m, _hip.ptr(pos),
-                  _hip.ptr(ln) if ln is not None else None, s)
-        return pos, ln
+        line = torch.empty(m, dtype=torch.int64, device=d) if want_line else None
+        _hip.call("mr_text_emit", _hip.ptr(text), n, mode, byte, _hip.ptr(off), m, _hip.ptr(pos), _hip.ptr(ln),
+                  _hip.ptr(loff), _hip.ptr(line), s)
+        return pos, ln, line
     b = _np(text)
     if mode == 1:
-        return torch.from_numpy(np.flatnonzero(b == byte).astype(np.int64)), None
-    ws = _WS_TABLE[b]
-    d_ = np.diff((~ws).astype(np.int8), prepend=0, append=0)
-    starts = np.flatnonzero(d_ == 1).astype(np.int64)
-    ends = np.flatnonzero(d_ == -1).astype(np.int64)
-    return torch.from_numpy(starts), torch.from_numpy((ends - starts).astype(np.int32))
+        pos = np.flatnonzero(b == byte).astype(np.int64)
+        ln = None
+    else:
+        ws = _WS_TABLE[b]
+        d_ = np.diff((~ws).astype(np.int8), prepend=0, append=0)
+        pos = np.flatnonzero(d_ == 1).astype(np.int64)
+        ends = np.flatnonzero(d_ == -1).astype(np.int64)
+        ln = torch.from_numpy((ends - pos).astype(np.int32))
+    line = None
+    if want_line:  # newlines strictly before each position
+        line = torch.from_numpy(np.searchsorted(np.flatnonzero(b == 10), pos, side="left").astype(np.int64))
+    return torch.from_numpy(pos), ln, line
 
 
-def tokens(text: torch.Tensor):
+def tokens(text: torch.Tensor, lines: bool = False):
     """(starts int64, lens int32) of every whitespace token (maximal run of
-    bytes outside Lua's ``%s``), in text order."""
-    return _scan(text, 0, 0, True)
+    bytes outside Lua's ``%s``), in text order; with ``lines=True`` also the
+    0-based line number of each token (int64; = ``line_index(text, starts)``,
+    from the same pass over the bytes)."""
+    st, ln, line = _scan(text, 0, 0, True, lines)
+    return (st, ln, line) if lines else (st, ln)
 
 
 def find_byte(text: torch.Tensor, byte: int) -> torch.Tensor:

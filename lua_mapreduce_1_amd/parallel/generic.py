@@ -219,8 +219,8 @@ class GenericEmitter:
         if self.line_base is None:
             raise NeedsHostMap("word_lines needs the SPMD engine's global line numbering")
         t = self._text(text)
-        st, ln = TX.tokens(t)
-        line = TX.line_index(t, st) + self.line_base(t)  # an int, or a device scalar
+        st, ln, line = TX.tokens(t, lines=True)
+        line = line + self.line_base(t)  # an int, or a device scalar
         self.spans(st, ln, line, text=t)
 
     def records(self, *a, **k):

@@ -50,11 +50,10 @@ def taskfn(emit):
 
 def _token_values(data: torch.Tensor):
     from lua_mapreduce_1_amd.ops import text as TX
-    st, ln = TX.tokens(data)
+    st, ln, line = TX.tokens(data, lines=True)
     n = st.numel()
     if n == 0:
         return st, ln, st
-    line = TX.line_index(data, st)
     nxt = torch.zeros(n, dtype=torch.int64, device=data.device)
     if n > 1:
         same = line[1:] == line[:-1]

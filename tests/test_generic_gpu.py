@@ -34,11 +34,31 @@ def test_text_tokens_lines_fields_gpu(gpu):
                 ds, dl = f(db)
                 assert torch.equal(hs, ds.cpu()) and torch.equal(hl, dl.cpu()), (f.__name__, n, off)
             assert torch.equal(TX.find_byte(hb, 9), TX.find_byte(db, 9).cpu())
+            hs, hl, hn = TX.tokens(hb, lines=True)
+            ds, dl, dn = TX.tokens(db, lines=True)
+            assert torch.equal(hn, dn.cpu()) and torch.equal(hs, ds.cpu()) and torch.equal(hl, dl.cpu())
+            assert torch.equal(dn.cpu(), TX.line_index(hb, hs))
             ls, ll = TX.lines(hb)
             for k in (0, 1, 2):
                 hs, hl = TX.field(hb, ls, ll, ",", k)
                 ds, dl = TX.field(db, ls.to(gpu), ll.to(gpu), ",", k)
                 assert torch.equal(hs, ds.cpu()) and torch.equal(hl, dl.cpu())
+
+
+def test_text_scan_dense_and_long_gpu(gpu):
+    """Tiles full of items (every byte a newline / a one-byte token every other
+    byte) and tokens longer than several 4 KiB tiles, against the CPU scans."""
+    from lua_mapreduce_1_amd.ops import text as TX
+    cases = [b"\n" * 9000, b"a " * 5000 + b"b", b"x" * 20000 + b" y\n" + b"z" * 9000,
+             b"\n".join(b"w%d %s" % (i, b"q" * (i % 97)) for i in range(3000))]
+    for b in cases:
+        hb = torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy())
+        db = hb.to(gpu)
+        assert torch.equal(TX.find_byte(hb, 10), TX.find_byte(db, 10).cpu())
+        h = TX.tokens(hb, lines=True)
+        d = TX.tokens(db, lines=True)
+        for x, y in zip(h, d):
+            assert torch.equal(x, y.cpu())
 
 
 def test_text_parse_gpu_matches_python(gpu):
