@@ -268,6 +268,7 @@ class AggTable:
             a.k = len(vals)
             a.list = 1 if self.list_mode else 0
             a.cstride = 1 if self.list_mode else self.cstride
+            a.rows_only = 1 if TUNABLES.agg_direct else 0
             keep = []
             for j, (v, dt) in enumerate(vals):
                 if isinstance(v, torch.Tensor):

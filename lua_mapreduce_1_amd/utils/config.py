@@ -68,6 +68,13 @@ class Tunables:
                            "general plane, typed folds on the GPU: the 8-byte physical columns of a table as one "
                            "row per slot (a key's folds touch one cache line) instead of one array per column; measured "
                            "equal or slower on the CSV group-by, profiles/r4/general/csv_ab/)")
+    agg_direct: bool = _knob("MR_AGG_DIRECT", False,
+                             "byte-span / encoded-key inserts (fold and general planes): one row per thread straight "
+                             "into the HBM table, no LDS combine (for key sets with few repeats per block)")
+    d2h_blocks: int = _knob("MR_D2H_BLOCKS", 0,
+                            "result downloads (device -> pinned host): 0 = hipMemcpyAsync (run as a ~512-workgroup "
+                            "blit kernel on this image), N = our copy kernel on N workgroups (fewer CU slots held "
+                            "while the next map runs beside it)")
     csv_tiles: int = _knob("MR_CSV_TILES", 0,
                            "fused CSV fold (emit.csv): 8 KiB tiles per workgroup (0 = auto: up to 4 while the "
                            "launch keeps >= 1024 workgroups)")
