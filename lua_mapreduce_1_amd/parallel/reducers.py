@@ -93,16 +93,18 @@ def lists_of_postings(slot, pslot, pval, m: int, space: int):
     d = slot.device
     if m == 0:
         return torch.zeros(1, dtype=torch.int64, device=d), pval[:0]
-    pos = torch.full((max(space, 1),), -1, dtype=torch.int64, device=d)
+    pos = torch.full((max(space, 1),), m, dtype=torch.int64, device=d)
     pos[slot] = torch.arange(m, dtype=torch.int64, device=d)
-    pr = pos[pslot.clamp(min=0)]
-    ok = (pslot >= 0) & (pr >= 0)
-    pr, pv = pr[ok], pval[ok]
+    # dropped rows (slot -1) and postings of keys not listed take key index m:
+    # the stable sort puts them after every list (no compaction pass)
+    pr = torch.where(pslot >= 0, pos[pslot.clamp(min=0)], torch.full_like(pslot, m))
+    pv = pval
     if pr.numel():
-        pp = ops.sort_keys_checked([pr], bits=[max(1, int(m - 1).bit_length())]).long()  # stable
+        pp = ops.sort_keys_checked([pr], bits=[max(1, int(m).bit_length())]).long()  # stable
         pr, pv = pr[pp], pv[pp]
     # list boundaries of the sorted key indices (no atomics: hot keys are free)
-    return torch.searchsorted(pr, torch.arange(m + 1, dtype=torch.int64, device=d)), pv
+    off = torch.searchsorted(pr, torch.arange(m + 1, dtype=torch.int64, device=d))
+    return off, pv[:int(off[-1])]  # (the sorted-last postings of no key dropped)
 
 
 def splice(off, val, noff, nval, keep_old):

@@ -157,3 +157,16 @@ def _spawn(world, mode):
         p.join(300)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     return q.get(timeout=5)
+
+
+def test_lists_of_postings_drops_unlisted():
+    """Postings of dropped rows (slot -1) and of slots not listed go nowhere;
+    each listed key's values keep their emission order."""
+    import torch
+    from lua_mapreduce_1_amd.parallel import reducers as RD
+    slot = torch.tensor([7, 2, 5])                     # key i lives in slot[i]
+    pslot = torch.tensor([2, -1, 7, 5, 2, 9, -1, 7, 2])  # slot 9: not a listed key
+    pval = torch.tensor([10, 11, 12, 13, 14, 15, 16, 17, 18])
+    off, val = RD.lists_of_postings(slot, pslot, pval, 3, 16)
+    assert off.tolist() == [0, 2, 5, 6]
+    assert val.tolist() == [12, 17, 10, 14, 18, 13]
