@@ -1,12 +1,14 @@
 #!/usr/bin/env python
-"""Throughput of the general device plane (parallel/generic.py) through the
-MapReduce API on mr.spmd:
+"""Throughput of user device maps that pick their own keys (byte spans,
+``ops/text.py``) through the MapReduce API on mr.spmd — the general plane
+(parallel/generic.py: typed folds, value lists) and, for an int64 ``sum``,
+the fold plane:
 
 * bigram: examples/Bigram (byte-span keys = two consecutive tokens of a
   line, int64 sum) over bench.py's Europarl-shaped corpus (197 splits,
   291 MB, ~47 M bigrams);
 * scores: examples/ScoreStats (CSV ``word,score``: field split + decimal
-  parse on the GPU, typed f64 mean / f64 max / count folds) over a generated
+  parse in one fused kernel, typed f64 mean / f64 max / count folds) over a generated
   CSV (``--score-lines`` lines).
 
 * wc_general: word count with the reference's GENERAL reducer contract
@@ -106,7 +108,7 @@ def run_job(name: str, mod_name: str, store, nbytes: int, check_splits: list[byt
     ms, res = _time(eng, args.steps, args.warmup, device)
     # read the result before the check runs another engine (result columns
     # alias the process's pinned download buffers until the next tail)
-    out = {"metric": f"{name} {unit}/s (general device plane, mr.spmd)", "value": units / (ms / 1000.0),
+    out = {"metric": f"{name} {unit}/s (device_mapfn with span emits, mr.spmd)", "value": units / (ms / 1000.0),
            "unit": f"{unit}/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
            "bytes": int(nbytes), "GB_per_s": nbytes / (ms / 1000.0) / 1e9, "distinct_keys": res.distinct_keys,
            "total_value": res.total_value, "timings_last_step": res.timings}
