@@ -224,3 +224,51 @@ def test_generic_server_worker_gpu(gpu, tmp_path):
             got = {k: [v] for k, v in got.items()}
         assert close_lists(got, exp), mod
         assert s.last_stats["failed_map_jobs"] == 0
+
+
+def _rank_pipe(rank, world, port, q, which, mod, args):
+    """A rank of a pipelined W-rank run (gloo over GPU tensors, one GPU):
+    three iterations with prefetched inputs and the next map queued early."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from lua_mapreduce_1_amd.parallel import dist as D
+    from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore
+    from lua_mapreduce_1_amd.runtime import codec
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    D.init_from_env(backend="gloo", use_gpu=True)
+    splits = make_data(which)
+    init = dict(args, nsplits=len(splits))
+    eng = SPMDEngine(dict(taskfn=mod, mapfn=mod, partitionfn=mod, reducefn=mod, finalfn=None, init_args=init),
+                     split_store=SplitStore(splits, pin=True), device=dev)
+    eng.prefetch, eng.pipeline = True, True
+    oks = []
+    steps = 3
+    for k in range(steps):
+        res = eng.run_iteration(prefetch_next=k < steps - 1, lookahead=steps - 1 - k)
+        got = {}
+        for _n, cols in eng.gather_results(res):
+            for key, v in codec.iter_columnar(cols):
+                got[key] = list(v)
+        if rank == 0:
+            oks.append(close_lists(got, oracle(which, args.get("mode"), splits)))
+    if rank == 0:
+        q.put((all(oks), getattr(eng.plane, "_maps", [None, None])[1] is not None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("which,mod,args", [CASES[0], CASES[4]], ids=["scores", "docs_concat"])
+def test_generic_three_ranks_pipelined(gpu, which, mod, args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_pipe, args=(r, 3, port, q, which, mod, args)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    ok, piped = q.get(timeout=5)
+    assert ok and piped
