@@ -332,6 +332,48 @@ __device__ __forceinline__ int cb_slot(u64* tag, u64* khi, u64* klo, u64* krep, 
   return -1;
 }
 
+// The keys of a thread's rows r0 + it * CB_T + threadIdx.x (it < items), their
+// loads issued together (span starts/lengths, then the key words: independent
+// chains, so the row loop after it does not wait a memory round trip per
+// row); returns the mask of rows with a key.
+template <int ITEMS>
+__device__ __forceinline__ u32 cb_row_keys(const Keys& ks, u64 r0, int items, u64 n, u64 (&khi_r)[ITEMS],
+                                           u64 (&klo_r)[ITEMS], u64 (&krep_r)[ITEMS]) {
+  const int t = threadIdx.x;
+  u32 ok = 0;
+  if (ks.text) {
+    long long st_r[ITEMS];
+    int len_r[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+      const u64 i = r0 + (u64)it * CB_T + t;
+      const bool in = it < items && i < n;
+      st_r[it] = in ? ks.starts[i] : -1;
+      len_r[it] = in ? ks.lens[i] : 0;
+    }
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+      khi_r[it] = klo_r[it] = krep_r[it] = 0;
+      if (len_r[it] > 0 && st_r[it] >= 0) {
+        span_key(ks.text, (u64)st_r[it], (u64)len_r[it], khi_r[it], klo_r[it]);
+        krep_r[it] = make_rep(ks.rep_base + (u64)st_r[it], (u64)len_r[it]);
+        ok |= 1u << it;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+      const u64 i = r0 + (u64)it * CB_T + t;
+      const bool in = it < items && i < n;
+      khi_r[it] = in ? ks.hi[i] : 0;
+      klo_r[it] = in ? ks.lo[i] : 0;
+      krep_r[it] = (in && ks.rep) ? ks.rep[i] + (ks.rep_add << REP_LEN_BITS) : 0;
+      if (in) ok |= 1u << it;
+    }
+  }
+  return ok;
+}
+
 // rows: rows per block (a multiple of CB_T, at most CB_ROWS): small batches get
 // smaller blocks so the launch still covers the chip (a 2-8 MiB CSV chunk at
 // 4096 rows per block ran 37-150 blocks on 256 CUs, 72 % of wave cycles
@@ -356,41 +398,8 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
   __syncthreads();
   u32 claims = 0;
   const u64 r0 = (u64)blockIdx.x * rows;
-  // phase 1: the keys of all of this thread's rows, their loads issued
-  // together (span starts/lengths, then the key words: independent chains,
-  // so the row loop below does not wait a memory round trip per row)
   u64 khi_r[CB_ITEMS], klo_r[CB_ITEMS], krep_r[CB_ITEMS];
-  u32 ok = 0;
-  if (ks.text) {
-    long long st_r[CB_ITEMS];
-    int len_r[CB_ITEMS];
-#pragma unroll
-    for (int it = 0; it < CB_ITEMS; ++it) {
-      const u64 i = r0 + (u64)it * CB_T + t;
-      const bool in = it < items && i < n;
-      st_r[it] = in ? ks.starts[i] : -1;
-      len_r[it] = in ? ks.lens[i] : 0;
-    }
-#pragma unroll
-    for (int it = 0; it < CB_ITEMS; ++it) {
-      khi_r[it] = klo_r[it] = krep_r[it] = 0;
-      if (len_r[it] > 0 && st_r[it] >= 0) {
-        span_key(ks.text, (u64)st_r[it], (u64)len_r[it], khi_r[it], klo_r[it]);
-        krep_r[it] = make_rep(ks.rep_base + (u64)st_r[it], (u64)len_r[it]);
-        ok |= 1u << it;
-      }
-    }
-  } else {
-#pragma unroll
-    for (int it = 0; it < CB_ITEMS; ++it) {
-      const u64 i = r0 + (u64)it * CB_T + t;
-      const bool in = it < items && i < n;
-      khi_r[it] = in ? ks.hi[i] : 0;
-      klo_r[it] = in ? ks.lo[i] : 0;
-      krep_r[it] = (in && ks.rep) ? ks.rep[i] + (ks.rep_add << REP_LEN_BITS) : 0;
-      if (in) ok |= 1u << it;
-    }
-  }
+  const u32 ok = cb_row_keys<CB_ITEMS>(ks, r0, items, n, khi_r, klo_r, krep_r);
 #pragma unroll
   for (int it = 0; it < CB_ITEMS; ++it) {
     const u64 i = r0 + (u64)it * CB_T + t;
@@ -415,6 +424,70 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
     claims += r == 2;
     if (r)
       for (int j = 0; j < c.k; ++j) cb_global_fold(c, j, slot, acc[j * CB_SLOTS + s]);
+  }
+  gtab_count_claims(g, claims);
+}
+
+// List mode (postings: one (slot, value) per row, in row order), rows of a
+// block resolved through an LDS key -> global-slot cache: the block's rows
+// claim LDS slots (cb_slot), each distinct key of the block is inserted into
+// the HBM table ONCE, and every row then writes its posting with its key's
+// slot — a Zipf vocabulary's hot keys no longer probe the HBM table per row
+// (agg_insert_kernel did).  Keys the cache cannot hold (full, long keys) take
+// the direct insert.
+__global__ void __launch_bounds__(CB_T) list_combine_kernel(GTab g, Keys ks, u64 n, Cols c, u32 rows) {
+  constexpr int CB_ITEMS = CB_ROWS / CB_T;
+  const int items = (int)(rows / CB_T);
+  extern __shared__ __attribute__((aligned(16))) u64 lds[];
+  u64* tag = lds;
+  u64* khi = tag + CB_SLOTS;
+  u64* klo = khi + CB_SLOTS;
+  u64* krep = klo + CB_SLOTS;
+  long long* gslot = (long long*)(krep + CB_SLOTS);  // global slot of each cached key (-1: overflow)
+  __shared__ u32 nclaimed;
+  const int t = threadIdx.x;
+  for (int s = t; s < CB_SLOTS; s += CB_T) {
+    tag[s] = 0;
+    klo[s] = 0;
+  }
+  if (t == 0) nclaimed = 0;
+  __syncthreads();
+  u32 claims = 0;
+  const u64 r0 = (u64)blockIdx.x * rows;
+  u64 khi_r[CB_ITEMS], klo_r[CB_ITEMS], krep_r[CB_ITEMS];
+  const u32 ok = cb_row_keys<CB_ITEMS>(ks, r0, items, n, khi_r, klo_r, krep_r);
+  int s_r[CB_ITEMS];
+#pragma unroll
+  for (int it = 0; it < CB_ITEMS; ++it) {
+    s_r[it] = -1;
+    if (ok & (1u << it))
+      s_r[it] = key_is_long(klo_r[it]) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, khi_r[it], klo_r[it], krep_r[it]);
+  }
+  __syncthreads();
+  for (int s = t; s < CB_SLOTS; s += CB_T) {
+    if (!tag[s]) continue;
+    u64 slot = 0;
+    const int r = gtab_insert(g, khi[s], klo[s], 0, krep[s], OP_NONE, &slot);
+    claims += r == 2;
+    gslot[s] = r ? (long long)slot : -1ll;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < CB_ITEMS; ++it) {
+    const u64 i = r0 + (u64)it * CB_T + t;
+    if (it >= items || i >= n) continue;
+    long long slot = -1;
+    if (s_r[it] >= 0) {
+      slot = gslot[s_r[it]];
+    } else if (ok & (1u << it)) {
+      u64 sl = 0;
+      const int r = gtab_insert(g, khi_r[it], klo_r[it], 0, krep_r[it], OP_NONE, &sl);
+      claims += r == 2;
+      slot = r ? (long long)sl : -1ll;
+    }
+    c.post_slot[c.post_base + i] = slot;
+    ((long long*)c.dst[0])[c.post_base + i] =
+        c.dtype[0] == VT_F64 ? __double_as_longlong(rd_f64(c, 0, i)) : rd_i64(c, 0, i);
   }
   gtab_count_claims(g, claims);
 }
@@ -860,6 +933,15 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
     while (rows > (u32)CB_T && (n + rows - 1) / rows < 1024) rows >>= 1;
     const u64 nb = (n + rows - 1) / rows;
     hipLaunchKernelGGL(agg_combine_kernel, dim3((unsigned)nb), dim3(CB_T), lds, stream,
+                       ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
+    return (int)hipGetLastError();
+  }
+  if (a->list && !a->rows_only && n >= (u64)CB_ROWS) {
+    const size_t lds = (size_t)CB_SLOTS * 5 * sizeof(u64);
+    u32 rows = (u32)CB_ROWS;
+    while (rows > (u32)CB_T && (n + rows - 1) / rows < 1024) rows >>= 1;
+    const u64 nb = (n + rows - 1) / rows;
+    hipLaunchKernelGGL(list_combine_kernel, dim3((unsigned)nb), dim3(CB_T), lds, stream,
                        ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
     return (int)hipGetLastError();
   }

@@ -28,6 +28,7 @@ Results stay in HBM (they can be ~the size of the input); ``partitions`` /
 """
 from __future__ import annotations
 
+import contextlib
 import sys
 import time
 
@@ -223,6 +224,9 @@ class ListPlane:
         self.streamed = False
         self._after_issue = None
         self._restored = None  # (vocabulary arrays, key-byte source) of a restored map
+        self._vocab_cap = cap
+        self._states = None    # pipelined iterations: (vocabulary, posting sink) per iteration parity
+        self._pending = None   # the next iteration's map, queued by this one
         self.emitter = ListEmitter(self)
         if eng.device_input != "split":
             raise ValueError("the list plane maps engine-staged splits (device_input = 'split')")
@@ -291,6 +295,11 @@ class ListPlane:
             raise _HeapFull()
 
     def _map_once(self, jobs, recs, j0, j1) -> torch.Tensor:
+        return self._map_finish(self._map_issue(jobs, recs, j0, j1))
+
+    def _map_issue(self, jobs, recs, j0, j1) -> list:
+        """Queue the rank's map (every staged chunk through device_mapfn);
+        returns its split ids for _map_finish."""
         eng = self.eng
         lines = self.line_offsets()
         ids = eng._split_ids(jobs, j0, j1)
@@ -340,6 +349,11 @@ class ListPlane:
             # finish below waits for the map): the copy engine never idles
             self._after_issue()
             self._after_issue = None
+        return ids
+
+    def _map_finish(self, ids: list) -> torch.Tensor:
+        """The posting keys of a queued map (one synchronisation)."""
+        eng = self.eng
         if eng.device.type == "cuda":
             if self.streamed:
                 # every round's (word, line) groups, rounds in line order: a
@@ -454,19 +468,76 @@ class ListPlane:
             return sk
         return torch.sort(keys).values
 
+    # -- pipelined iterations ---------------------------------------------------
+    def _pipelined(self) -> bool:
+        """Iteration q+1's map is queued (own stream, vocabulary and posting
+        sink) as soon as iteration q's postings are out: GPU, split inputs
+        prefetched by a pure taskfn, no map checkpoints, no streaming."""
+        eng = self.eng
+        return (bool(eng.pipeline) and eng.device.type == "cuda" and eng._can_pipeline()
+                and eng._map_ckpt_path() is None and bool(eng.streams))
+
+    def _use_state(self, q: int) -> None:
+        """Make iteration q's vocabulary and posting sink current."""
+        if self._states is None:
+            self._states = [(self.vocab, self.sink), None]
+        st = self._states[q % 2]
+        if st is None:
+            st = self._states[q % 2] = (II.Vocab(self.eng.device, self._vocab_cap), None)
+        self.vocab, self.sink = st
+
+    def _keep_state(self, q: int) -> None:
+        self._states[q % 2] = (self.vocab, self.sink)  # (the map may have grown its sink)
+
+    def _issue_next_map(self, jobs, j0, j1, q: int) -> None:
+        """Queue iteration q+1's map (same jobs: the taskfn is pure) on its
+        own stream, vocabulary and sink; run_iteration(q+1) finishes it."""
+        eng = self.eng
+        eng._prefetch(jobs, j0, j1, q + 1)
+        cur = (self.vocab, self.sink)
+        eng._use(q + 1)
+        try:
+            with torch.cuda.stream(eng.streams[eng.tslot]):
+                self._use_state(q + 1)
+                t0 = time.time()
+                recs = _records(eng, jobs, j0, j1, t0)
+                ids = self._map_issue(jobs, recs, j0, j1)
+                self._keep_state(q + 1)
+            self._pending = {"q": q + 1, "jobs": jobs, "recs": recs, "j0": j0, "j1": j1, "t0": t0, "ids": ids}
+        except _UseGeneric:
+            self._pending = None  # (the next iteration re-runs its map and switches planes there)
+        finally:
+            self.vocab, self.sink = cur
+            eng._use(q)
+
     def run_iteration(self, prefetch_next, lookahead):
         eng = self.eng
         eng.iteration += 1
         q = eng._seq
         eng._seq += 1
         eng._use(q)
+        pend, self._pending = self._pending, None
+        if pend is not None and pend["q"] != q:
+            pend = None
+        pipe = self._pipelined()
+        stream = eng.streams[eng.tslot] if (pipe or pend is not None) else None
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            return self._iteration(q, prefetch_next, lookahead, pend, pipe)
+
+    def _iteration(self, q, prefetch_next, lookahead, pend, pipe):
+        eng = self.eng
         res = DeviceResult()
         T = res.timings
         t_start = time.time()
-        jobs = eng._jobs()
-        j0, j1 = eng._assign(jobs)
-        t0 = time.time()
-        recs = _records(eng, jobs, j0, j1, t0)
+        if pend is not None:  # this iteration's map was queued by the previous one
+            jobs, recs, j0, j1, t0 = pend["jobs"], pend["recs"], pend["j0"], pend["j1"], pend["t0"]
+        else:
+            jobs = eng._jobs()
+            j0, j1 = eng._assign(jobs)
+            t0 = time.time()
+            recs = _records(eng, jobs, j0, j1, t0)
+        if pipe or pend is not None:
+            self._use_state(q)
         res.map_jobs = recs
         ahead = 0 if not (prefetch_next if prefetch_next is not None else eng.prefetch) else (
             2 if lookahead is None else min(lookahead, 2))
@@ -475,10 +546,16 @@ class ListPlane:
         try:
             with trace.range("mr.list.map"):
                 self.line_offsets()  # (a collective: every rank, restored or not)
-                keys = self._restore_map(recs, j0, j1)
-                if keys is None:
-                    keys = self._map(jobs, recs, j0, j1)
-                    self._save_map(keys, recs, j0, j1)
+                if pend is not None:
+                    if self._after_issue is not None:
+                        self._after_issue()
+                        self._after_issue = None
+                    keys = self._map_finish(pend["ids"])
+                else:
+                    keys = self._restore_map(recs, j0, j1)
+                    if keys is None:
+                        keys = self._map(jobs, recs, j0, j1)
+                        self._save_map(keys, recs, j0, j1)
         except _UseGeneric:
             # the map emits through generic calls: the general plane runs
             # this engine from now on (this iteration is restarted there)
@@ -492,6 +569,11 @@ class ListPlane:
         if self._after_issue is not None:  # (a map that raised before issuing everything)
             self._after_issue()
             self._after_issue = None
+        if pipe or pend is not None:
+            self._keep_state(q)
+        if pipe and ahead and self._restored is None:
+            with trace.range("mr.list.issue_next"):
+                self._issue_next_map(jobs, j0, j1, q)
         eng._maybe_inject_fault("shuffle")
         T["map"] = time.time() - t0
         t1 = time.time()

@@ -209,22 +209,25 @@ def test_gpu_single_rank_matches_oracle(gpu):
 
 
 @pytest.mark.gpu
-def test_gpu_staged_chunks_and_prefetch(gpu):
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_gpu_staged_chunks_and_prefetch(gpu, pipeline):
     """Small copy chunks mapped as their copies land (line numbers continue
     across chunks), and iterations whose copies were prefetched during the
-    previous iteration's sort."""
+    previous iteration's sort — with ``pipeline`` also each next iteration's
+    map queued (own stream, vocabulary and sink) while this one is ordered."""
     from lua_mapreduce_1_amd.runtime import codec
     splits = _splits()
     eng = _engine(splits, gpu, table_capacity=1 << 16)
     eng.chunk_bytes = [8 << 10, 16 << 10, 32 << 10]
     eng.tail_bytes = [8 << 10]
-    eng.prefetch = True
+    eng.prefetch, eng.pipeline = True, pipeline
     want = _naive(splits)
     for i in range(4):
         res = eng.run_iteration(prefetch_next=i < 3, lookahead=3 - i)
         got = {k: v for _n, c in eng.gather_results(res) for k, v in codec.iter_columnar(c)}
         assert got == want
     assert not eng._inflight
+    assert (eng.plane._states is not None and eng.plane._states[1] is not None) == pipeline
 
 
 @pytest.mark.gpu
