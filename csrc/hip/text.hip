@@ -92,6 +92,56 @@ __global__ void __launch_bounds__(T) text_count_kernel(const u8* __restrict__ te
   }
 }
 
+// First position in [from, to) whose bit is set (want = 1) or clear (want =
+// 0) in a tile bit mask (u32 words, bit i of word w = byte 32 w + i), or `to`.
+template <int WANT>
+__device__ __forceinline__ u32 tile_next_bit(const u32* w, u32 from, u32 to) {
+  u32 i = from;
+  while (i < to) {
+    const u32 word = WANT ? w[i >> 5] : ~w[i >> 5];
+    const u32 m = word >> (i & 31);
+    if (m) {
+      const u32 p = i + (u32)__builtin_ctz(m);
+      return p < to ? p : to;
+    }
+    i = (i | 31) + 1;
+  }
+  return to;
+}
+
+// End (exclusive, global) of the n-gram whose first token ends at global
+// position e: grams - 1 more tokens on the same line, each after a run of
+// whitespace that holds no newline; -1 when the line ends first.  Bytes of
+// the tile [tile, tile + TILE) are read from its LDS masks, later bytes from
+// global memory.
+__device__ __forceinline__ long long ngram_end(const u8* __restrict__ text, u64 n, u64 tile, const u32* wsw,
+                                               const u32* nlw, u64 e, int grams) {
+  for (int g = 1; g < grams; ++g) {
+    // the next token's start: skip whitespace, but not a newline
+    u64 q = e;
+    if (q < tile + TILE) {
+      const u32 r = tile_next_bit<0>(wsw, (u32)(q - tile), (u32)TILE);
+      const u32 nl = tile_next_bit<1>(nlw, (u32)(q - tile), r);
+      if (nl < r) return -1;
+      q = tile + r;
+    }
+    if (q >= tile + TILE) {
+      while (q < n && is_ws(text[q])) {
+        if (text[q] == 10) return -1;
+        ++q;
+      }
+    }
+    if (q >= n) return -1;
+    // its end
+    u64 f = q;
+    if (f < tile + TILE) f = tile + tile_next_bit<1>(wsw, (u32)(f - tile), (u32)TILE);
+    if (f >= tile + TILE)
+      while (f < n && !is_ws(text[f])) ++f;
+    e = f;
+  }
+  return (long long)e;
+}
+
 // Items of a tile in text order at tile_off[tile] + rank: positions, token
 // lengths (out_len) and 0-based line numbers (out_line, from the newline
 // counts' exclusive scan line_off).  Token ends come from the tile's
@@ -105,7 +155,8 @@ __global__ void __launch_bounds__(T) text_emit_kernel(const u8* __restrict__ tex
                                                      long long* __restrict__ out_pos, int* __restrict__ out_len,
                                                      const long long* __restrict__ line_off,
                                                      long long* __restrict__ out_line) {
-  __shared__ u16 wsm[T + 1];
+  __shared__ __attribute__((aligned(4))) u16 wsm[T + 2];
+  __shared__ __attribute__((aligned(4))) u16 nlm[T];   // newline masks (n-grams stop at line ends)
   __shared__ u16 ipos[TILE];        // tile offsets of the items (mode 1 may have TILE of them)
   __shared__ u32 ilen[TE_MAX];      // token lengths (mode 0)
   __shared__ u16 iline[TILE];       // newlines of the tile before each item
@@ -118,7 +169,8 @@ __global__ void __launch_bounds__(T) text_emit_kernel(const u8* __restrict__ tex
   if (g < n) m = seg_masks(text, n, g, mode, c);
   else m.ws = 0xFFFFu;
   wsm[t] = (u16)m.ws;
-  if (t == 0) wsm[T] = 0;  // (past the tile: not whitespace -> continue in global memory)
+  nlm[t] = (u16)m.nl;
+  if (t == 0) wsm[T] = wsm[T + 1] = 0;
   const u32 cnt = (u32)__builtin_popcount(m.item);
   const u32 nlc = (u32)__builtin_popcount(m.nl);
   u32 ci = cnt, ni = nlc;
@@ -171,7 +223,13 @@ __global__ void __launch_bounds__(T) text_emit_kernel(const u8* __restrict__ tex
       u64 ge = tile + e;
       if (e == (u32)TILE)
         while (ge < n && !is_ws(text[ge])) ++ge;
-      ilen[k] = (u32)(ge - (tile + t * SEG + i));
+      const u64 gs = tile + t * SEG + i;
+      if (c >= 2) {  // n-gram spans (c tokens of one line) instead of token lengths; 0: none
+        const long long ne = ngram_end(text, n, tile, (const u32*)wsm, (const u32*)nlm, ge, (int)c);
+        ilen[k] = ne < 0 ? 0u : (u32)((u64)ne - gs);
+      } else {
+        ilen[k] = (u32)(ge - gs);
+      }
     }
     ++k;
   }
@@ -286,10 +344,13 @@ int mr_text_count(const void* text, u64 n, int mode, u32 c, void* tile_counts, v
 
 // out_len (mode 0) and out_line (with line_off = exclusive scan of the newline
 // counts) are optional.
+// mode 0 with c >= 2: out_len = the span of the c-token n-gram starting at each
+// token (0: fewer than c tokens left on its line) instead of its length.
 int mr_text_emit(const void* text, u64 n, int mode, u32 c, const void* tile_off, u64 cap, void* out_pos,
                  void* out_len, const void* line_off, void* out_line, hipStream_t s) {
   if (n == 0) return 0;
   if (out_len && mode != 0) return -1;
+  if (mode == 0 && c > 64) return -1;
   if (out_line && !line_off) return -1;
   hipLaunchKernelGGL(text_emit_kernel, dim3((unsigned)mr_text_tiles(n)), dim3(T), 0, s, (const u8*)text, n, mode, c,
                      (const long long*)tile_off, cap, (long long*)out_pos, (int*)out_len,

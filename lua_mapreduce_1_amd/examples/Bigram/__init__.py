@@ -2,7 +2,7 @@
 tokens on one line -> number of occurrences.  The key of a pair is the byte
 span from the first token's start to the second token's end (``"w1 w2"``
 for single-spaced text), so keys are not tokens of the input: the device map
-picks them with ops/text.py and torch ops and emits byte spans
+picks them with ops/text.py (``ngrams``) and emits byte spans
 (``emit.spans``), which the int64 fold plane sums like word counts.  One
 module holds every function, like the reference's single-module WordCount
 (/root/reference/mapreduce/examples/WordCount/init.lua).
@@ -54,16 +54,14 @@ def _data(value, emit):
 
 
 def device_mapfn(key, value, emit):
-    import torch
     from lua_mapreduce_1_amd.ops import text as TX
     data = _data(value, emit)
-    st, ln, line = TX.tokens(data, lines=True)  # tokens and their line numbers in one pass
-    if st.numel() < 2:
-        return
-    start = st[:-1]
-    end = st[1:] + ln[1:].to(torch.int64)
-    same_line = line[1:] == line[:-1]
-    emit.spans(start, torch.where(same_line, end - start, torch.zeros_like(start)).to(torch.int32), text=data)
+    # every token with the span to the end of the next token on its line
+    # (length 0 at a line's last token: emit.spans skips it) — one pass over
+    # the bytes; the same as tokens(lines=True) + torch ops pairing token i
+    # with token i+1 where both lines agree (see ops/text.py ngrams)
+    st, ln = TX.ngrams(data, 2)
+    emit.spans(st, ln, text=data)
 
 
 def bigrams(data: bytes):

@@ -268,7 +268,9 @@ class AggTable:
             a.k = len(vals)
             a.list = 1 if self.list_mode else 0
             a.cstride = 1 if self.list_mode else self.cstride
-            a.rows_only = 1 if TUNABLES.agg_direct else 0
+            # list mode: one row per thread unless MR_LIST_CACHE (the LDS key ->
+            # slot cache measured 1.1 ms slower on the reducefn3 word count)
+            a.rows_only = 1 if (TUNABLES.agg_direct or (self.list_mode and not TUNABLES.list_cache)) else 0
             keep = []
             for j, (v, dt) in enumerate(vals):
                 if isinstance(v, torch.Tensor):

@@ -72,6 +72,32 @@ def tokens(text: torch.Tensor, lines: bool = False):
     return (st, ln, line) if lines else (st, ln)
 
 
+def ngrams(text: torch.Tensor, n: int = 2):
+    """(starts int64, lens int32) of the n-gram starting at every whitespace
+    token: the byte span from the token's start to the end of the (n-1)-th
+    token after it on the same line (a newline ends an n-gram; other
+    whitespace between the tokens is part of the span); lens 0 where fewer
+    than n tokens are left on the line (``emit.spans`` skips those).  One
+    pass over the bytes on the GPU (the token scan's kernel, spans from the
+    tile's whitespace / newline masks)."""
+    n = int(n)
+    if not 1 <= n <= 64:
+        raise ValueError("ngrams: 1 <= n <= 64")
+    if n == 1:
+        return tokens(text)
+    if text.is_cuda and text.numel():
+        st, ln, _ = _scan(text, 0, n, True)
+        return st, ln
+    st, ln, line = _scan(text, 0, 0, True, True)
+    m = st.numel()
+    out = torch.zeros(m, dtype=torch.int32)
+    if m >= n:
+        end = st[n - 1:] + ln[n - 1:].to(torch.int64)
+        same = line[n - 1:] == line[:m - n + 1]
+        out[:m - n + 1] = torch.where(same, end - st[:m - n + 1], torch.zeros_like(end)).to(torch.int32)
+    return st, out
+
+
 def find_byte(text: torch.Tensor, byte: int) -> torch.Tensor:
     """Positions (int64, ascending) of every byte equal to ``byte``."""
     return _scan(text, 1, int(byte) & 0xFF, False)[0]

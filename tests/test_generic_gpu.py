@@ -61,6 +61,24 @@ def test_text_scan_dense_and_long_gpu(gpu):
             assert torch.equal(x, y.cpu())
 
 
+def test_text_ngrams_gpu(gpu):
+    """n-gram spans on the GPU (token scan kernel, tile masks, global memory
+    past the tile) against the CPU form, on tricky text and on tokens and
+    whitespace runs that cross 4 KiB tiles."""
+    from lua_mapreduce_1_amd.ops import text as TX
+    from lua_mapreduce_1_amd.utils.corpus import tricky_text
+    rng = np.random.default_rng(7)
+    cases = [tricky_text(rng, k) for k in (1, 4095, 4097, 200_003)]
+    cases += [b"a" * 5000 + b" " * 5000 + b"b\n c", b"x " * 3000 + b"\n" * 10 + b"y z", b"p\r\nq r\t\ts"]
+    for b in cases:
+        hb = torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy())
+        db = hb.to(gpu)
+        for n in (2, 3, 5):
+            hs, hl = TX.ngrams(hb, n)
+            ds, dl = TX.ngrams(db, n)
+            assert torch.equal(hs, ds.cpu()) and torch.equal(hl, dl.cpu()), (len(b), n)
+
+
 def test_text_parse_gpu_matches_python(gpu):
     from lua_mapreduce_1_amd.ops import text as TX
     rng = np.random.default_rng(5)

@@ -19,3 +19,8 @@ timeout -k 10 200 python3 tools/bench_invidx.py --validate > $OUT/invidx_bench.l
 echo "invidx $(grep -o '"ms_per_step": [0-9.]*' $OUT/invidx_bench.log)"
 MR_PIPELINE=0 timeout -k 10 200 python3 tools/bench_invidx.py --validate > $OUT/invidx_bench_nopipe.log 2>&1 || exit $?
 echo "invidx no-pipeline $(grep -o '"ms_per_step": [0-9.]*' $OUT/invidx_bench_nopipe.log)"
+# n-gram spans in one pass: their GPU tests, then the bigram bench
+timeout -k 10 300 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_generic_gpu.py \
+  -k "ngrams or tokens or generic_gpu_w1" > $OUT/ngram_tests.log 2>&1 || exit $?
+timeout -k 10 300 python3 tools/bench_generic.py --jobs bigram --steps 8 --warmup 2 --validate > $OUT/bigram.log 2>&1 || exit $?
+echo "bigram $(grep -o '"ms_per_step": [0-9.]*\|"validated_full": [a-z]*' $OUT/bigram.log | paste -sd' ')"
