@@ -115,3 +115,24 @@ def test_generic_pipelined_iterations_gpu(gpu, which):
         assert close_lists(_gather(eng, res), exp), k
         assert res.failed_maps == 0
     assert getattr(eng.plane, "_maps", [None, None])[1] is not None  # the pipelined path ran
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_text_edge_cases(dev):
+    """Empty text, one token, text of only separators / newlines: tokens,
+    n-grams and CSV rows agree with the definitions (no rows, no spans)."""
+    from lua_mapreduce_1_amd.ops import text as TX
+    if dev == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    for b in (b"", b"x", b"\n\n\n", b" \t ", b",,,\n,,\n", b"a,1"):
+        t = torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev) if b else torch.zeros(0, dtype=torch.uint8,
+                                                                                           device=dev)
+        st, ln = TX.tokens(t)
+        toks = [b[s:s + n] for s, n in zip(st.tolist(), ln.tolist())]
+        assert toks == b.split()
+        st, ln = TX.ngrams(t, 2)
+        grams = [b[s:s + n] for s, n in zip(st.tolist(), ln.tolist()) if n]
+        assert grams == []  # no line of these holds two tokens
+        ks, kl, cols = TX.csv_rows(t, 0, (1,), ",")
+        keys = [b[s:s + n] for s, n in zip(ks.tolist(), kl.tolist()) if n]
+        assert keys == ([b"a"] if b == b"a,1" else [])
