@@ -530,7 +530,11 @@ __global__ void copy_to_host_kernel(const u8* src, u8* dst, const long long* nel
   for (u64 i = tid; i < nv; i += stride)
     reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
   for (u64 i = nv * 16 + tid; i < nb; i += stride) dst[i] = src[i];
-  __threadfence_system();
+  // one system-scope release per workgroup, not per thread (a per-thread
+  // fence wrote back L2 16 K times per launch and slowed the kernels beside
+  // the copy); the host reads only after the stream's completion signal
+  __syncthreads();
+  if (threadIdx.x == 0) __threadfence_system();
 }
 
 }  // namespace mr
