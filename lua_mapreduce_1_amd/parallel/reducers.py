@@ -86,6 +86,20 @@ class KeyBatch:
 
 
 # ---------------------------------------------------------------------------
+def _take(v: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
+    """v[perm] for 8-byte values (GPU: mr_gather_u64 with the sort's int32
+    permutation; torch's index kernel was a quarter of the general reducer's
+    kernel time, profiles/r4/final_profiles/)."""
+    if not v.is_cuda or v.element_size() != 8:
+        return v[perm.long()]
+    from ..ops import _hip
+    src = v.contiguous().view(torch.int64)
+    out = torch.empty_like(src)
+    p32 = perm.to(torch.int32).contiguous()
+    _hip.call("mr_gather_u64", _hip.ptr(src), _hip.ptr(p32), _hip.ptr(out), src.numel(), _hip.stream(v.device))
+    return out.view(v.dtype)
+
+
 def lists_of_postings(slot, pslot, pval, m: int, space: int):
     """A table's postings (key slot, value; emission order) -> the keys' value
     lists in CSR form, key i = the i-th entry of ``slot`` (emission order
@@ -100,8 +114,10 @@ def lists_of_postings(slot, pslot, pval, m: int, space: int):
     pr = torch.where(pslot >= 0, pos[pslot.clamp(min=0)], torch.full_like(pslot, m))
     pv = pval
     if pr.numel():
-        pp = ops.sort_keys_checked([pr], bits=[max(1, int(m).bit_length())]).long()  # stable
-        pr, pv = pr[pp], pv[pp]
+        # stable; the sort hands back its sorted keys (no gather of them) and
+        # the values follow the permutation through one u64 gather kernel
+        pp, pr = ops.sort_keys_checked([pr], bits=[max(1, int(m).bit_length())], return_keys=True)
+        pv = _take(pv, pp)
     # list boundaries of the sorted key indices (no atomics: hot keys are free)
     off = torch.searchsorted(pr, torch.arange(m + 1, dtype=torch.int64, device=d))
     return off, pv[:int(off[-1])]  # (the sorted-last postings of no key dropped)
