@@ -336,7 +336,7 @@ __device__ __forceinline__ int cb_slot(u64* tag, u64* khi, u64* klo, u64* krep, 
 // loads issued together (span starts/lengths, then the key words: independent
 // chains, so the row loop after it does not wait a memory round trip per
 // row); returns the mask of rows with a key.
-template <int ITEMS>
+template <int ITEMS, int STRIDE = CB_T>
 __device__ __forceinline__ u32 cb_row_keys(const Keys& ks, u64 r0, int items, u64 n, u64 (&khi_r)[ITEMS],
                                            u64 (&klo_r)[ITEMS], u64 (&krep_r)[ITEMS]) {
   const int t = threadIdx.x;
@@ -346,7 +346,7 @@ __device__ __forceinline__ u32 cb_row_keys(const Keys& ks, u64 r0, int items, u6
     int len_r[ITEMS];
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
-      const u64 i = r0 + (u64)it * CB_T + t;
+      const u64 i = r0 + (u64)it * STRIDE + t;
       const bool in = it < items && i < n;
       st_r[it] = in ? ks.starts[i] : -1;
       len_r[it] = in ? ks.lens[i] : 0;
@@ -363,7 +363,7 @@ __device__ __forceinline__ u32 cb_row_keys(const Keys& ks, u64 r0, int items, u6
   } else {
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
-      const u64 i = r0 + (u64)it * CB_T + t;
+      const u64 i = r0 + (u64)it * STRIDE + t;
       const bool in = it < items && i < n;
       khi_r[it] = in ? ks.hi[i] : 0;
       klo_r[it] = in ? ks.lo[i] : 0;
@@ -424,6 +424,53 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
     claims += r == 2;
     if (r)
       for (int j = 0; j < c.k; ++j) cb_global_fold(c, j, slot, acc[j * CB_SLOTS + s]);
+  }
+  gtab_count_claims(g, claims);
+}
+
+// List mode, one row per thread-item (LR_ITEMS rows per thread, strided by the
+// block): the rows' span and key loads are issued together, then the home
+// slot's tag of every row; a row whose key is a short exact tag found at its
+// home slot (a sparse table: most rows) takes that slot with no further
+// memory round trip, the others the full insert.  Each row then writes its
+// posting (slot, value) at its row index.
+constexpr int LR_T = 256, LR_ITEMS = 8;
+__global__ void __launch_bounds__(LR_T) list_rows_kernel(GTab g, Keys ks, u64 n, Cols c) {
+  const int t = threadIdx.x;
+  u32 claims = 0;
+  for (u64 r0 = (u64)blockIdx.x * (LR_T * LR_ITEMS); r0 < n; r0 += (u64)gridDim.x * (LR_T * LR_ITEMS)) {
+    u64 khi_r[LR_ITEMS], klo_r[LR_ITEMS], krep_r[LR_ITEMS];
+    const u32 ok = cb_row_keys<LR_ITEMS, LR_T>(ks, r0, LR_ITEMS, n, khi_r, klo_r, krep_r);
+    u64 home[LR_ITEMS], seen[LR_ITEMS];
+#pragma unroll
+    for (int it = 0; it < LR_ITEMS; ++it) {
+      home[it] = 0;
+      seen[it] = 0;
+      if (ok & (1u << it)) {
+        home[it] = gtab_home(gtab_tag(khi_r[it], klo_r[it]), g.mask);
+        seen[it] = ld_agent(&g.tag[home[it]]);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < LR_ITEMS; ++it) {
+      const u64 i = r0 + (u64)it * LR_T + t;
+      if (i >= n) continue;
+      long long slot = -1;
+      if (ok & (1u << it)) {
+        const u64 tag = gtab_tag(khi_r[it], klo_r[it]);
+        if (seen[it] == tag && gtab_tag_exact(tag)) {
+          slot = (long long)home[it];
+        } else {
+          u64 sl = 0;
+          const int r = gtab_insert(g, khi_r[it], klo_r[it], 0, krep_r[it], OP_NONE, &sl);
+          claims += r == 2;
+          slot = r ? (long long)sl : -1ll;
+        }
+      }
+      c.post_slot[c.post_base + i] = slot;
+      ((long long*)c.dst[0])[c.post_base + i] =
+          c.dtype[0] == VT_F64 ? __double_as_longlong(rd_f64(c, 0, i)) : rd_i64(c, 0, i);
+    }
   }
   gtab_count_claims(g, claims);
 }
@@ -934,6 +981,13 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
     const u64 nb = (n + rows - 1) / rows;
     hipLaunchKernelGGL(agg_combine_kernel, dim3((unsigned)nb), dim3(CB_T), lds, stream,
                        ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
+    return (int)hipGetLastError();
+  }
+  if (a->list && a->rows_only == 1) {  // (2: the one-row-per-thread kernel below, for A/B)
+    u64 g = (n + LR_T * LR_ITEMS - 1) / (LR_T * LR_ITEMS);
+    if (g > 16384) g = 16384;
+    hipLaunchKernelGGL(list_rows_kernel, dim3((unsigned)g), dim3(LR_T), 0, stream,
+                       ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
     return (int)hipGetLastError();
   }
   if (a->list && !a->rows_only && n >= (u64)CB_ROWS) {

@@ -161,10 +161,34 @@ __global__ void __launch_bounds__(THREADS) seg_reduce_kernel(const long long* __
   }
 }
 
+// Key index of each posting: pos[pslot[i]] for a posting of a listed slot,
+// `none` for a dropped row (pslot < 0) or a slot past the table (one pass in
+// place of torch's clamp + gather + where).
+__global__ void posting_keys_kernel(const long long* __restrict__ pos, long long space,
+                                    const long long* __restrict__ pslot, long long n, long long none,
+                                    long long* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const long long s = pslot[i];
+    out[i] = (s >= 0 && s < space) ? pos[s] : none;
+  }
+}
+
 }  // namespace seg
 }  // namespace mr
 
 extern "C" {
+
+int mr_posting_keys(const void* pos, long long space, const void* pslot, long long n, long long none, void* out,
+                    hipStream_t stream) {
+  using namespace mr::seg;
+  if (n <= 0) return 0;
+  long long g = (n + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(posting_keys_kernel, dim3((unsigned)g), dim3(256), 0, stream, (const long long*)pos, space,
+                     (const long long*)pslot, n, none, (long long*)out);
+  return (int)hipGetLastError();
+}
 
 // out[s] = fold of val[off[s] .. off[s+1]) for s < m (out pre-filled with the
 // fold's identity by the caller; empty segments keep it).  vtype: 0 int64,

@@ -271,6 +271,8 @@ class AggTable:
             # list mode: one row per thread unless MR_LIST_CACHE (the LDS key ->
             # slot cache measured 1.1 ms slower on the reducefn3 word count)
             a.rows_only = 1 if (TUNABLES.agg_direct or (self.list_mode and not TUNABLES.list_cache)) else 0
+            if self.list_mode and a.rows_only and not TUNABLES.list_rows:
+                a.rows_only = 2  # the plain one-row-per-thread insert (A/B)
             keep = []
             for j, (v, dt) in enumerate(vals):
                 if isinstance(v, torch.Tensor):

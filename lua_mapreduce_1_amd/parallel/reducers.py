@@ -111,7 +111,14 @@ def lists_of_postings(slot, pslot, pval, m: int, space: int):
     pos[slot] = torch.arange(m, dtype=torch.int64, device=d)
     # dropped rows (slot -1) and postings of keys not listed take key index m:
     # the stable sort puts them after every list (no compaction pass)
-    pr = torch.where(pslot >= 0, pos[pslot.clamp(min=0)], torch.full_like(pslot, m))
+    if pslot.is_cuda:
+        from ..ops import _hip
+        ps = pslot.to(torch.int64).contiguous()
+        pr = torch.empty_like(ps)
+        _hip.call("mr_posting_keys", _hip.ptr(pos), pos.numel(), _hip.ptr(ps), ps.numel(), m, _hip.ptr(pr),
+                  _hip.stream(d))
+    else:
+        pr = torch.where(pslot >= 0, pos[pslot.clamp(min=0)], torch.full_like(pslot, m))
     pv = pval
     if pr.numel():
         # stable; the sort hands back its sorted keys (no gather of them) and
