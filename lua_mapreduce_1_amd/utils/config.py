@@ -80,10 +80,14 @@ class Tunables:
                              "an LDS key -> slot cache (one HBM insert per distinct key of a block) instead of one "
                              "HBM probe per row; measured 9.6 vs 8.5 ms on the reducefn3 word count "
                              "(profiles/r4/general/list_ab/)")
-    list_rows: bool = _knob("MR_LIST_ROWS", True,
-                            "general plane, value lists on the GPU: 8 rows per thread with their key loads and "
-                            "home-slot tag loads issued together (a short key found at its home slot needs no "
-                            "further round trip); 0 = one row per thread")
+    list_rows: bool = _knob("MR_LIST_ROWS", False,
+                            "general plane, value lists on the GPU: 6 rows per thread with their key loads and "
+                            "home-slot probes issued together (a key found at its home slot needs no "
+                            "further round trip); off: one row per thread (measured 7.37 vs 7.0 ms with 8 rows "
+                            "per thread, profiles/r4/general/list_rows_ab/)")
+    flush_probe: bool = _knob("MR_FLUSH_PROBE", True,
+                              "LDS-combined inserts (general plane, CSV fold): a thread's flushed keys probe their "
+                              "home slots together before any falls back to the full insert")
     csv_tiles: int = _knob("MR_CSV_TILES", 0,
                            "fused CSV fold (emit.csv): 8 KiB tiles per workgroup (0 = auto: up to 4 while the "
                            "launch keeps >= 1024 workgroups)")
