@@ -85,9 +85,10 @@ class Tunables:
                             "home-slot probes issued together (a key found at its home slot needs no "
                             "further round trip); off: one row per thread (measured 7.37 vs 7.0 ms with 8 rows "
                             "per thread, profiles/r4/general/list_rows_ab/)")
-    flush_probe: bool = _knob("MR_FLUSH_PROBE", True,
+    flush_probe: bool = _knob("MR_FLUSH_PROBE", False,
                               "LDS-combined inserts (general plane, CSV fold): a thread's flushed keys probe their "
-                              "home slots together before any falls back to the full insert")
+                              "home slots together before any falls back to the full insert (measured neutral: "
+                              "CSV 2.455 vs 2.443 ms, bigram 23.3 vs 23.3, profiles/r4/general/flush_ab/)")
     csv_tiles: int = _knob("MR_CSV_TILES", 0,
                            "fused CSV fold (emit.csv): 8 KiB tiles per workgroup (0 = auto: up to 4 while the "
                            "launch keeps >= 1024 workgroups)")
