@@ -143,7 +143,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, on_gpu=False, backend="gloo", force_shuffle=False):
+def _worker(rank, world, port, q, on_gpu=False, backend="gloo", force_shuffle=False, pipelined=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import datetime
@@ -161,6 +161,24 @@ def _worker(rank, world, port, q, on_gpu=False, backend="gloo", force_shuffle=Fa
     if force_shuffle:
         extra["force_shuffle"] = True
     eng = _engine(splits, device, **extra)
+    if pipelined:
+        # three iterations with prefetched inputs and each next map queued
+        # early (own stream, vocabulary and sink), every result checked
+        from lua_mapreduce_1_amd.runtime import codec
+        eng.prefetch, eng.pipeline = True, True
+        want, same = _naive(splits), True
+        for i in range(3):
+            res = eng.run_iteration(prefetch_next=i < 2, lookahead=2 - i)
+            parts = eng.gather_results(res)
+            if rank == 0:
+                same &= {k: v for _n, c in parts for k, v in codec.iter_columnar(c)} == want
+        own_ok = all(p % world == rank for p in res.result_names) and eng.plane._states[1] is not None
+        oks = D.gather_objects(own_ok, 0)
+        if rank == 0:
+            q.put((same, all(oks)))
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     res = eng.run()
     own_ok = all(p % world == rank for p in res.result_names)
     oks = D.gather_objects(own_ok, 0)
@@ -258,6 +276,12 @@ def test_gpu_dense_one_letter_tokens(gpu):
 @pytest.mark.gpu
 def test_gpu_multi_rank_on_one_gpu(gpu):
     _run(2, on_gpu=True)
+
+
+@pytest.mark.gpu
+def test_gpu_multi_rank_pipelined(gpu):
+    """Two ranks sharing the GPU (gloo) running pipelined list-plane iterations."""
+    _run(2, on_gpu=True, pipelined=True)
 
 
 @pytest.mark.gpu
