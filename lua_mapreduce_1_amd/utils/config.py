@@ -102,6 +102,9 @@ class Tunables:
                               "general plane, typed folds on the GPU: byte-span batches of at least this many rows "
                               "are pre-combined by a hash sort + segmented folds before the table insert (0 = "
                               "never; smaller batches hash every row into the table with an LDS combine)")
+    rec_glds: bool = _knob("MR_REC_GLDS", False,
+                           "record plane: row gather staged by LDS-DMA loads (global_load_lds_dwordx4) into two "
+                           "LDS images instead of register-staged 16-byte loads")
     rec_scatter: bool = _knob("MR_REC_SCATTER", False,
                               "record plane: apply a full row permutation as a scatter through its inverse "
                               "(coalesced row reads) instead of the gather (random row reads)")
