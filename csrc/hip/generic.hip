@@ -332,59 +332,6 @@ __device__ __forceinline__ int cb_slot(u64* tag, u64* khi, u64* klo, u64* krep, 
   return -1;
 }
 
-// Speculative home-slot probe: the (tag, lo, hi) words of a key's home slot,
-// loaded together so several keys' probes are in flight at once.  home_hit:
-// the key is at its home slot — a short key by its exact tag, a longer packed
-// key by tag, lo and hi (slots are claimed once and hi is published before lo,
-// so a matching triple is final); long keys (byte-verified) never hit here.
-// A miss takes the full gtab_insert.
-__device__ __forceinline__ void home_load(const GTab& g, u64 hi, u64 lo, u64& home, u64& st, u64& sl, u64& sh) {
-  home = gtab_home(gtab_tag(hi, lo), g.mask);
-  st = ld_agent(&g.tag[home]);
-  sl = ld_agent(&g.lo[home]);
-  sh = ld_agent(&g.hi[home]);
-}
-
-__device__ __forceinline__ bool home_hit(u64 hi, u64 lo, u64 st, u64 sl, u64 sh) {
-  const u64 tag = gtab_tag(hi, lo);
-  if (st != tag) return false;
-  if (gtab_tag_exact(tag)) return true;
-  return !key_is_long(lo) && sl == lo && sh == hi;
-}
-
-// Flush of an LDS combine table: each thread's claimed slots probe their home
-// slots together, then fold there (hit) or through gtab_insert (miss).
-// (spec = 0: no probes, every slot through gtab_insert — the A/B form)
-__device__ __forceinline__ u32 cb_flush(const GTab& g, const Cols& c, const u64* tag, const u64* khi, const u64* klo,
-                                        const u64* krep, const long long* acc, int spec) {
-  constexpr int FL = CB_SLOTS / CB_T;
-  const int t = threadIdx.x;
-  u64 hm[FL], st[FL], sl[FL], sh[FL];
-#pragma unroll
-  for (int f = 0; f < FL; ++f) {
-    const int s = t + f * CB_T;
-    hm[f] = st[f] = sl[f] = sh[f] = 0;
-    if (spec && tag[s]) home_load(g, khi[s], klo[s], hm[f], st[f], sl[f], sh[f]);
-  }
-  u32 claims = 0;
-#pragma unroll
-  for (int f = 0; f < FL; ++f) {
-    const int s = t + f * CB_T;
-    if (!tag[s]) continue;
-    u64 slot = 0;
-    int r = 1;
-    if (spec && home_hit(khi[s], klo[s], st[f], sl[f], sh[f])) {
-      slot = hm[f];
-    } else {
-      r = gtab_insert(g, khi[s], klo[s], 0, krep[s], OP_NONE, &slot);
-      claims += r == 2;
-    }
-    if (r)
-      for (int j = 0; j < c.k; ++j) cb_global_fold(c, j, slot, acc[j * CB_SLOTS + s]);
-  }
-  return claims;
-}
-
 // The keys of a thread's rows r0 + it * CB_T + threadIdx.x (it < items), their
 // loads issued together (span starts/lengths, then the key words: independent
 // chains, so the row loop after it does not wait a memory round trip per
@@ -431,7 +378,7 @@ __device__ __forceinline__ u32 cb_row_keys(const Keys& ks, u64 r0, int items, u6
 // smaller blocks so the launch still covers the chip (a 2-8 MiB CSV chunk at
 // 4096 rows per block ran 37-150 blocks on 256 CUs, 72 % of wave cycles
 // waiting: profiles/r4/general/csv_pmc/)
-__global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 n, Cols c, u32 rows, int probe) {
+__global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 n, Cols c, u32 rows) {
   constexpr int CB_ITEMS = CB_ROWS / CB_T;
   const int items = (int)(rows / CB_T);
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
@@ -470,112 +417,13 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
     }
   }
   __syncthreads();
-  claims += cb_flush(g, c, tag, khi, klo, krep, acc, probe);
-  gtab_count_claims(g, claims);
-}
-
-// List mode, one row per thread-item (LR_ITEMS rows per thread, strided by the
-// block): the rows' span and key loads are issued together, then every row's
-// home-slot probe (home_load); a row whose key sits at its home slot (a
-// sparse table: most rows) takes that slot with no further memory round trip,
-// the others the full insert.  Each row then writes its
-// posting (slot, value) at its row index.
-constexpr int LR_T = 256, LR_ITEMS = 6;
-__global__ void __launch_bounds__(LR_T) list_rows_kernel(GTab g, Keys ks, u64 n, Cols c) {
-  const int t = threadIdx.x;
-  u32 claims = 0;
-  for (u64 r0 = (u64)blockIdx.x * (LR_T * LR_ITEMS); r0 < n; r0 += (u64)gridDim.x * (LR_T * LR_ITEMS)) {
-    u64 khi_r[LR_ITEMS], klo_r[LR_ITEMS], krep_r[LR_ITEMS];
-    const u32 ok = cb_row_keys<LR_ITEMS, LR_T>(ks, r0, LR_ITEMS, n, khi_r, klo_r, krep_r);
-    u64 home[LR_ITEMS], st[LR_ITEMS], sl[LR_ITEMS], sh[LR_ITEMS];
-#pragma unroll
-    for (int it = 0; it < LR_ITEMS; ++it) {
-      home[it] = st[it] = sl[it] = sh[it] = 0;
-      if (ok & (1u << it)) home_load(g, khi_r[it], klo_r[it], home[it], st[it], sl[it], sh[it]);
-    }
-#pragma unroll
-    for (int it = 0; it < LR_ITEMS; ++it) {
-      const u64 i = r0 + (u64)it * LR_T + t;
-      if (i >= n) continue;
-      long long slot = -1;
-      if (ok & (1u << it)) {
-        if (home_hit(khi_r[it], klo_r[it], st[it], sl[it], sh[it])) {
-          slot = (long long)home[it];
-        } else {
-          u64 sl = 0;
-          const int r = gtab_insert(g, khi_r[it], klo_r[it], 0, krep_r[it], OP_NONE, &sl);
-          claims += r == 2;
-          slot = r ? (long long)sl : -1ll;
-        }
-      }
-      c.post_slot[c.post_base + i] = slot;
-      ((long long*)c.dst[0])[c.post_base + i] =
-          c.dtype[0] == VT_F64 ? __double_as_longlong(rd_f64(c, 0, i)) : rd_i64(c, 0, i);
-    }
-  }
-  gtab_count_claims(g, claims);
-}
-
-// List mode (postings: one (slot, value) per row, in row order), rows of a
-// block resolved through an LDS key -> global-slot cache: the block's rows
-// claim LDS slots (cb_slot), each distinct key of the block is inserted into
-// the HBM table ONCE, and every row then writes its posting with its key's
-// slot — a Zipf vocabulary's hot keys no longer probe the HBM table per row
-// (agg_insert_kernel did).  Keys the cache cannot hold (full, long keys) take
-// the direct insert.
-__global__ void __launch_bounds__(CB_T) list_combine_kernel(GTab g, Keys ks, u64 n, Cols c, u32 rows) {
-  constexpr int CB_ITEMS = CB_ROWS / CB_T;
-  const int items = (int)(rows / CB_T);
-  extern __shared__ __attribute__((aligned(16))) u64 lds[];
-  u64* tag = lds;
-  u64* khi = tag + CB_SLOTS;
-  u64* klo = khi + CB_SLOTS;
-  u64* krep = klo + CB_SLOTS;
-  long long* gslot = (long long*)(krep + CB_SLOTS);  // global slot of each cached key (-1: overflow)
-  __shared__ u32 nclaimed;
-  const int t = threadIdx.x;
-  for (int s = t; s < CB_SLOTS; s += CB_T) {
-    tag[s] = 0;
-    klo[s] = 0;
-  }
-  if (t == 0) nclaimed = 0;
-  __syncthreads();
-  u32 claims = 0;
-  const u64 r0 = (u64)blockIdx.x * rows;
-  u64 khi_r[CB_ITEMS], klo_r[CB_ITEMS], krep_r[CB_ITEMS];
-  const u32 ok = cb_row_keys<CB_ITEMS>(ks, r0, items, n, khi_r, klo_r, krep_r);
-  int s_r[CB_ITEMS];
-#pragma unroll
-  for (int it = 0; it < CB_ITEMS; ++it) {
-    s_r[it] = -1;
-    if (ok & (1u << it))
-      s_r[it] = key_is_long(klo_r[it]) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, khi_r[it], klo_r[it], krep_r[it]);
-  }
-  __syncthreads();
   for (int s = t; s < CB_SLOTS; s += CB_T) {
     if (!tag[s]) continue;
     u64 slot = 0;
     const int r = gtab_insert(g, khi[s], klo[s], 0, krep[s], OP_NONE, &slot);
     claims += r == 2;
-    gslot[s] = r ? (long long)slot : -1ll;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int it = 0; it < CB_ITEMS; ++it) {
-    const u64 i = r0 + (u64)it * CB_T + t;
-    if (it >= items || i >= n) continue;
-    long long slot = -1;
-    if (s_r[it] >= 0) {
-      slot = gslot[s_r[it]];
-    } else if (ok & (1u << it)) {
-      u64 sl = 0;
-      const int r = gtab_insert(g, khi_r[it], klo_r[it], 0, krep_r[it], OP_NONE, &sl);
-      claims += r == 2;
-      slot = r ? (long long)sl : -1ll;
-    }
-    c.post_slot[c.post_base + i] = slot;
-    ((long long*)c.dst[0])[c.post_base + i] =
-        c.dtype[0] == VT_F64 ? __double_as_longlong(rd_f64(c, 0, i)) : rd_i64(c, 0, i);
+    if (r)
+      for (int j = 0; j < c.k; ++j) cb_global_fold(c, j, slot, acc[j * CB_SLOTS + s]);
   }
   gtab_count_claims(g, claims);
 }
@@ -714,7 +562,7 @@ constexpr int CV_LP = 4096;  // line starts ranked per pass (a tile of shorter l
 
 __global__ void __launch_bounds__(CB_T) __attribute__((amdgpu_waves_per_eu(4, 8)))
 csv_fold_kernel(GTab g, const u8* __restrict__ text, u64 n, u64 rep_base, CsvSpec sp, Cols c, u32 tiles,
-                unsigned long long* __restrict__ rows_out, int mode, int probe) {
+                unsigned long long* __restrict__ rows_out, int mode) {
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
   u64* tag = lds;
   u64* khi = tag + CB_SLOTS;
@@ -907,7 +755,14 @@ csv_fold_kernel(GTab g, const u8* __restrict__ text, u64 n, u64 rep_base, CsvSpe
   if (myrows) atomicAdd(&nrows, myrows);
   __syncthreads();
   if (t == 0 && nrows) atomicAdd(rows_out, (unsigned long long)nrows);
-  claims += cb_flush(g, c, tag, khi, klo, krep, acc, probe);
+  for (int s = t; s < CB_SLOTS; s += CB_T) {
+    if (!tag[s]) continue;
+    u64 slot = 0;
+    const int r = gtab_insert(g, khi[s], klo[s], 0, krep[s], OP_NONE, &slot);
+    claims += r == 2;
+    if (r)
+      for (int j = 0; j < c.k; ++j) cb_global_fold(c, j, slot, acc[j * CB_SLOTS + s]);
+  }
   gtab_count_claims(g, claims);
 }
 
@@ -985,15 +840,6 @@ extern "C" {
 // spans (starts int64, lens int32) of `text`, whose rep offsets are
 // rep_base + start.  `src`: the byte source every rep word of the table
 // indexes (long-key byte verification).
-// LDS-table flushes probe the home slots of all of a thread's keys at once
-// (cb_flush); 0 = every key through gtab_insert (A/B)
-static int g_flush_probe = 0;
-
-int mr_agg_set_flush_probe(int on) {
-  g_flush_probe = on ? 1 : 0;
-  return 0;
-}
-
 int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void* ctrl, u64 cap, const void* src,
                   const void* hi, const void* lo, const void* rep, u64 rep_add, const void* text, const void* starts,
                   const void* lens, u64 rep_base, u64 n, const void* cols, hipStream_t stream) {
@@ -1023,22 +869,6 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
     while (rows > (u32)CB_T && (n + rows - 1) / rows < 1024) rows >>= 1;
     const u64 nb = (n + rows - 1) / rows;
     hipLaunchKernelGGL(agg_combine_kernel, dim3((unsigned)nb), dim3(CB_T), lds, stream,
-                       ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows, g_flush_probe);
-    return (int)hipGetLastError();
-  }
-  if (a->list && a->rows_only == 1) {  // (2: the one-row-per-thread kernel below, for A/B)
-    u64 g = (n + LR_T * LR_ITEMS - 1) / (LR_T * LR_ITEMS);
-    if (g > 16384) g = 16384;
-    hipLaunchKernelGGL(list_rows_kernel, dim3((unsigned)g), dim3(LR_T), 0, stream,
-                       ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
-    return (int)hipGetLastError();
-  }
-  if (a->list && !a->rows_only && n >= (u64)CB_ROWS) {
-    const size_t lds = (size_t)CB_SLOTS * 5 * sizeof(u64);
-    u32 rows = (u32)CB_ROWS;
-    while (rows > (u32)CB_T && (n + rows - 1) / rows < 1024) rows >>= 1;
-    const u64 nb = (n + rows - 1) / rows;
-    hipLaunchKernelGGL(list_combine_kernel, dim3((unsigned)nb), dim3(CB_T), lds, stream,
                        ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
     return (int)hipGetLastError();
   }
@@ -1088,7 +918,7 @@ int mr_csv_fold(void* tag, void* thi, void* tlo, void* tval, void* trep, void* c
   const u64 nb = (ntiles + tiles - 1) / tiles;
   hipLaunchKernelGGL(csv_fold_kernel, dim3((unsigned)nb), dim3(CB_T), lds, stream,
                      ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), (const u8*)text, n, rep_base, sp, to_cols(a),
-                     tiles, (unsigned long long*)rows_out, g_csv_mode, g_flush_probe);
+                     tiles, (unsigned long long*)rows_out, g_csv_mode);
   return (int)hipGetLastError();
 }
 

@@ -807,32 +807,13 @@ int mr_copy_to_host(const void* src, void* host_dst, const void* nelem, u64 elem
   return (int)hipGetLastError();
 }
 
-// Device -> pinned-host download on stream s: an SDMA copy (hipMemcpyAsync),
-// which takes no CU time from the next iteration's map (the round-1 form,
-// shader stores over PCIe, measured 0.19 ms slower on the HBM-resident bench
-// and equal host-staged: profiles/r2/d2h_ab/; removed in round 3,
-// profiles/r3/pruned/).
-// On this image the runtime executes such copies as blit kernels
-// (__amd_rocclr_copyBuffer, ~512 workgroups whose waves wait on PCIe): a
-// large download then holds CU slots of the next map running beside it.
-// g_d2h_blocks > 0 copies with our own kernel on that many workgroups instead.
-static int g_d2h_blocks = 0;
-
-int mr_d2h_set_blocks(int blocks) {
-  if (blocks < 0 || blocks > 8192) return -1;
-  g_d2h_blocks = blocks;
-  return 0;
-}
-
+// Device -> pinned-host download on stream s (hipMemcpyAsync; this image's
+// runtime runs it as a blit kernel).  Shader stores of our own measured slower
+// twice: round 1 (0.19 ms on the HBM-resident bench, profiles/r2/d2h_ab/) and
+// round 4 on 16-256 workgroups (bigram 26.2-27.9 vs 23.2-23.7 ms,
+// profiles/r4/general/bigram_ab/, profiles/r4/rehearse/; profiles/r4/pruned/).
 int mr_d2h_async(void* host_dst, const void* src, u64 nbytes, hipStream_t s) {
   if (nbytes == 0) return 0;
-  if (g_d2h_blocks > 0) {
-    void* dptr = nullptr;
-    if (hipHostGetDevicePointer(&dptr, host_dst, 0) != hipSuccess || dptr == nullptr) dptr = host_dst;
-    hipLaunchKernelGGL(copy_to_host_kernel, dim3(g_d2h_blocks), dim3(256), 0, s, (const u8*)src, (u8*)dptr,
-                       (const long long*)nullptr, (u64)1, nbytes);
-    return (int)hipGetLastError();
-  }
   return (int)hipMemcpyAsync(host_dst, src, nbytes, hipMemcpyDeviceToHost, s);
 }
 

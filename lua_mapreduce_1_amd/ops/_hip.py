@@ -119,8 +119,6 @@ _SIGS = {
     "mr_posting_keys": [_p, ctypes.c_longlong, _p, ctypes.c_longlong, ctypes.c_longlong, _p, _p],
     "mr_wc_map3_set_config": [_i32],
     "mr_csv_set_config": [_i32, _i32],
-    "mr_d2h_set_blocks": [_i32],
-    "mr_agg_set_flush_probe": [_i32],
 }
 _RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
                 "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words"}
@@ -150,9 +148,6 @@ def lib():
             raise ValueError(f"MR_SORT_ROUNDS={TUNABLES.sort_rounds}: must be 16, 24 or 32")
         if L.mr_wc_map3_set_config(TUNABLES.wc_map_config) != 0:
             raise ValueError(f"MR_WC_MAP_CONFIG={TUNABLES.wc_map_config}: must be 0..3")
-        L.mr_agg_set_flush_probe(1 if TUNABLES.flush_probe else 0)
-        if L.mr_d2h_set_blocks(TUNABLES.d2h_blocks) != 0:
-            raise ValueError(f"MR_D2H_BLOCKS={TUNABLES.d2h_blocks}: 0..8192")
         if L.mr_csv_set_config(TUNABLES.csv_tiles, TUNABLES.csv_mode) != 0:
             raise ValueError(f"MR_CSV_TILES={TUNABLES.csv_tiles} / MR_CSV_MODE={TUNABLES.csv_mode}: 0..64 / 0..2")
         if L.mr_rec_gather_set_rows(TUNABLES.rec_gather_rows) != 0:

@@ -193,28 +193,16 @@ class AggTable:
         self.list_dtype = list_dtype
         self.src: torch.Tensor | None = None
         self.cap = next_pow2(max(1024, int(capacity)))
-        self.cstride = 1
+        self.cstride = 1  # slot stride of the value columns (one array per column)
         if self.is_cuda:
             self.keys = HashTable(self.cap, self.device, op="none")
-            self.cols = [] if self.list_mode else self._alloc_cols(cols)
+            self.cols = [] if self.list_mode else [torch.empty(self.cap, dtype=DTYPES[dt], device=self.device)
+                                                   for dt, _op, _i in cols]
             self._fill_cols()
             self.post_slot = self.post_val = None
         else:
             self._pending: list = []
         self.npost = 0
-
-    def _alloc_cols(self, cols: list) -> list:
-        """The physical columns on the GPU.  With more than one column, all
-        of 8 bytes, they are one row per slot (4 or 8 words: a row never
-        straddles a 64-byte line), so the folds of a key touch one line of
-        memory instead of one per column (MR_AGG_ROWS); otherwise one array
-        per column."""
-        k = len(cols)
-        if TUNABLES.agg_rows and k > 1 and all(dt in ("i64", "f64") for dt, _op, _i in cols):
-            self.cstride = 4 if k <= 4 else 8
-            buf = torch.empty(self.cap, self.cstride, dtype=torch.int64, device=self.device)
-            return [buf[:, j].view(DTYPES[dt]) for j, (dt, _op, _i) in enumerate(cols)]
-        return [torch.empty(self.cap, dtype=DTYPES[dt], device=self.device) for dt, _op, _i in cols]
 
     @property
     def is_cuda(self) -> bool:
@@ -268,11 +256,9 @@ class AggTable:
             a.k = len(vals)
             a.list = 1 if self.list_mode else 0
             a.cstride = 1 if self.list_mode else self.cstride
-            # list mode: one row per thread unless MR_LIST_CACHE (the LDS key ->
-            # slot cache measured 1.1 ms slower on the reducefn3 word count)
-            a.rows_only = 1 if (TUNABLES.agg_direct or (self.list_mode and not TUNABLES.list_cache)) else 0
-            if self.list_mode and a.rows_only and not TUNABLES.list_rows:
-                a.rows_only = 2  # the plain one-row-per-thread insert (A/B)
+            # (list mode: one row per thread; an LDS key -> slot cache and batched
+            # rows per thread measured slower, profiles/r4/pruned/)
+            a.rows_only = 1 if TUNABLES.agg_direct else 0
             keep = []
             for j, (v, dt) in enumerate(vals):
                 if isinstance(v, torch.Tensor):

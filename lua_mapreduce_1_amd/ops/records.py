@@ -109,13 +109,11 @@ def gather(rec: torch.Tensor, perm: torch.Tensor, mode: int | None = None) -> to
     (or byte) gather; ``mode=1`` forces the dword gather (A/B probes, tests);
     ``mode=3`` (default with ``MR_REC_SCATTER=1``): a full permutation is
     applied as a scatter through its inverse (coalesced row reads, dword
-    stores to the destinations); ``mode=4`` (default with ``MR_REC_GLDS=1``):
-    the row chunks are moved global -> LDS by LDS-DMA loads into two images
-    (the next batch's loads in flight while this one is stored)."""
+    stores to the destinations)."""
     n = perm.numel()
     rb = int(rec.shape[1])
     if mode is None:
-        mode = 3 if TUNABLES.rec_scatter else (4 if TUNABLES.rec_glds else 0)
+        mode = 3 if TUNABLES.rec_scatter else 0
     if rec.is_cuda:
         out = torch.empty((n, rb), dtype=torch.uint8, device=rec.device)
         if n == 0:

@@ -64,31 +64,9 @@ class Tunables:
                                "word-count map kernel shape (csrc/hip/wordcount3.hip): 0 = 512 threads, 2048 LDS "
                                "slots, 8 KiB spans, two workgroups per CU; 1 / 2 = 4096 slots over 32 / 64 KiB, one "
                                "workgroup per CU; 3 = 1024 threads, 4096 slots, 32 KiB")
-    agg_rows: bool = _knob("MR_AGG_ROWS", False,
-                           "general plane, typed folds on the GPU: the 8-byte physical columns of a table as one "
-                           "row per slot (a key's folds touch one cache line) instead of one array per column; measured "
-                           "equal or slower on the CSV group-by, profiles/r4/general/csv_ab/)")
     agg_direct: bool = _knob("MR_AGG_DIRECT", False,
                              "byte-span / encoded-key inserts (fold and general planes): one row per thread straight "
                              "into the HBM table, no LDS combine (for key sets with few repeats per block)")
-    d2h_blocks: int = _knob("MR_D2H_BLOCKS", 0,
-                            "result downloads (device -> pinned host): 0 = hipMemcpyAsync (run as a ~512-workgroup "
-                            "blit kernel on this image), N = our copy kernel on N workgroups (fewer CU slots held "
-                            "while the next map runs beside it)")
-    list_cache: bool = _knob("MR_LIST_CACHE", False,
-                             "general plane, value lists on the GPU: rows resolve their key's table slot through "
-                             "an LDS key -> slot cache (one HBM insert per distinct key of a block) instead of one "
-                             "HBM probe per row; measured 9.6 vs 8.5 ms on the reducefn3 word count "
-                             "(profiles/r4/general/list_ab/)")
-    list_rows: bool = _knob("MR_LIST_ROWS", False,
-                            "general plane, value lists on the GPU: 6 rows per thread with their key loads and "
-                            "home-slot probes issued together (a key found at its home slot needs no "
-                            "further round trip); off: one row per thread (measured 7.37 vs 7.0 ms with 8 rows "
-                            "per thread, profiles/r4/general/list_rows_ab/)")
-    flush_probe: bool = _knob("MR_FLUSH_PROBE", False,
-                              "LDS-combined inserts (general plane, CSV fold): a thread's flushed keys probe their "
-                              "home slots together before any falls back to the full insert (measured neutral: "
-                              "CSV 2.455 vs 2.443 ms, bigram 23.3 vs 23.3, profiles/r4/general/flush_ab/)")
     csv_tiles: int = _knob("MR_CSV_TILES", 0,
                            "fused CSV fold (emit.csv): 8 KiB tiles per workgroup (0 = auto: up to 4 while the "
                            "launch keeps >= 1024 workgroups)")
@@ -102,9 +80,6 @@ class Tunables:
                               "general plane, typed folds on the GPU: byte-span batches of at least this many rows "
                               "are pre-combined by a hash sort + segmented folds before the table insert (0 = "
                               "never; smaller batches hash every row into the table with an LDS combine)")
-    rec_glds: bool = _knob("MR_REC_GLDS", False,
-                           "record plane: row gather staged by LDS-DMA loads (global_load_lds_dwordx4) into two "
-                           "LDS images instead of register-staged 16-byte loads")
     rec_scatter: bool = _knob("MR_REC_SCATTER", False,
                               "record plane: apply a full row permutation as a scatter through its inverse "
                               "(coalesced row reads) instead of the gather (random row reads)")

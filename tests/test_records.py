@@ -283,18 +283,3 @@ def test_row_scatter_equals_gather_gpu(gpu, rb):
     perm = torch.randperm(n, generator=g).to(torch.int32).to(gpu)
     assert torch.equal(RC.gather(rec, perm, mode=3), RC.gather(rec, perm, mode=0))
     assert torch.equal(RC.gather(rec, perm, mode=3).cpu(), rec.cpu()[perm.cpu().long()])
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("rb", [100, 64, 24, 244, 16, 36])
-@pytest.mark.parametrize("n", [100_000, 1_000, 37])
-def test_row_gather_lds_dma_gpu(gpu, rb, n):
-    """The LDS-DMA staged row gather (MR_REC_GLDS, mode 4) moves the same
-    bytes as the register-staged one, for partial batches and subsets."""
-    from lua_mapreduce_1_amd.ops import records as RC
-    g = torch.Generator().manual_seed(rb + n)
-    rec = torch.randint(0, 256, (n + 16, rb), dtype=torch.uint8, generator=g).to(gpu)  # n+16 rows: nin*rb % 16 == 0
-    perm = torch.randint(0, n + 16, (n,), generator=g).to(torch.int32).to(gpu)
-    want = rec.cpu()[perm.cpu().long()]
-    assert torch.equal(RC.gather(rec, perm, mode=4).cpu(), want)
-    assert torch.equal(RC.gather(rec, perm, mode=0).cpu(), want)
