@@ -162,16 +162,31 @@ __global__ void __launch_bounds__(THREADS) seg_reduce_kernel(const long long* __
 }
 
 // Key index of each posting: pos[pslot[i]] for a posting of a listed slot,
-// `none` for a dropped row (pslot < 0) or a slot past the table (one pass in
-// place of torch's clamp + gather + where).
-__global__ void posting_keys_kernel(const long long* __restrict__ pos, long long space,
-                                    const long long* __restrict__ pslot, long long n, long long none,
-                                    long long* __restrict__ out) {
+// `none` for a dropped row (pslot < 0) or a slot past the table, as u32 (one
+// pass in place of torch's clamp + gather + where), plus the radix sort's
+// digit histograms of those u32 keys ([8][256] layout, the first 4 rows;
+// LDS-combined per block) so the stable u32 sort needs no histogram pass.
+__global__ void __launch_bounds__(256) posting_keys_kernel(const long long* __restrict__ pos, long long space,
+                                                          const long long* __restrict__ pslot, long long n,
+                                                          unsigned none, unsigned* __restrict__ out,
+                                                          unsigned* __restrict__ ghist) {
+  __shared__ unsigned h[4][256];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) h[b][t] = 0;
+  __syncthreads();
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + t; i < n; i += stride) {
     const long long s = pslot[i];
-    out[i] = (s >= 0 && s < space) ? pos[s] : none;
+    const unsigned k = (s >= 0 && s < space) ? (unsigned)pos[s] : none;
+    out[i] = k;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 0xFFu], 1u);
   }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    if (h[b][t]) atomicAdd(&ghist[b * 256 + t], h[b][t]);
 }
 
 }  // namespace seg
@@ -179,14 +194,16 @@ __global__ void posting_keys_kernel(const long long* __restrict__ pos, long long
 
 extern "C" {
 
+// ghist: zeroed u32[8][256] (rows 0-3 are filled)
 int mr_posting_keys(const void* pos, long long space, const void* pslot, long long n, long long none, void* out,
-                    hipStream_t stream) {
+                    void* ghist, hipStream_t stream) {
   using namespace mr::seg;
   if (n <= 0) return 0;
+  if (none < 0 || none > 0xFFFFFFFFll || !ghist) return -1;
   long long g = (n + 255) / 256;
-  if (g > 16384) g = 16384;
+  if (g > 4096) g = 4096;
   hipLaunchKernelGGL(posting_keys_kernel, dim3((unsigned)g), dim3(256), 0, stream, (const long long*)pos, space,
-                     (const long long*)pslot, n, none, (long long*)out);
+                     (const long long*)pslot, n, (unsigned)none, (unsigned*)out, (unsigned*)ghist);
   return (int)hipGetLastError();
 }
 

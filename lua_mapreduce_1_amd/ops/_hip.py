@@ -116,7 +116,7 @@ _SIGS = {
     "mr_exact_hash": [_p, _p, _p, _p, _u64, _p, _p],
     "mr_exact_fix": [_p, _p, _u64, _p, _p, _p, _p, _p, _p, _p, _p],
     "mr_seg_reduce": [_p, _u64, _p, _u64, _i32, _i32, _p, _p],
-    "mr_posting_keys": [_p, ctypes.c_longlong, _p, ctypes.c_longlong, ctypes.c_longlong, _p, _p],
+    "mr_posting_keys": [_p, ctypes.c_longlong, _p, ctypes.c_longlong, ctypes.c_longlong, _p, _p, _p],
     "mr_wc_map3_set_config": [_i32],
     "mr_csv_set_config": [_i32, _i32],
 }
