@@ -12,8 +12,8 @@
 //   claim:   CAS tag 0 -> gtab_tag(hi,lo)           (relaxed, agent); for keys of <= 7
 //            bytes the tag IS the key (mr_common.h) and a tag match is final
 //   publish: sc1 stores of hi, rep ; fold value ; s_waitcnt vmcnt(0) ; sc1 store lo
-//   lookup:  tag match -> load lo (relaxed); lo==0 => not yet published, retry;
-//            lo match -> load hi; on mismatch re-check after an acquire fence;
+//   lookup:  tag match -> load lo and hi (relaxed); lo==0 => not yet published, retry;
+//            lo match -> compare hi; on mismatch re-check after an acquire fence;
 //            a long key (lo low byte 0xFF) must also match byte for byte
 //            through the rep words (exact identity, mr_common.h) — keys that
 //            collide on (prefix, hash) take separate slots.
@@ -104,10 +104,12 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
       return 1;
     }
     if (cur == tag) {
+      // lo and hi in one round trip: an hi read ahead of lo's publication is
+      // caught by the acquire + re-read below, as an early hi always was
       const u64 l = ld_agent(&t.lo[slot]);
+      u64 h = ld_agent(&t.hi[slot]);
       if (l == 0) continue;  // claimed but not yet published: re-read this slot
       if (l == lo) {
-        u64 h = ld_agent(&t.hi[slot]);
         if (h != hi) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           h = ld_agent(&t.hi[slot]);
