@@ -19,6 +19,7 @@
 // a text buffer, packed here in the insert kernel (no intermediate key arrays).
 #include <hip/hip_runtime.h>
 #include <climits>
+#include <cstdlib>
 #include "mr_common.h"
 #include "hashtab.h"
 #include "text_parse.h"
@@ -872,7 +873,15 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
                        ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256)), dim3(256), 0, stream,
+  static const unsigned ins_cap = [] {
+    // workgroup cap of the per-row insert: one row per thread up to 16 M rows
+    // (the insert is probe-latency-bound; 65536 vs 8192 vs 2048 workgroups:
+    // reducefn3 6.57-6.62 vs 6.60-6.91 vs 6.73-6.76 ms, profiles/r4/agg_grid_ab)
+    const char* e = getenv("MR_AGG_INSERT_GRID");
+    const long v = e ? atol(e) : 0;
+    return v >= 256 ? (unsigned)v : 65536u;
+  }();
+  hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256, ins_cap)), dim3(256), 0, stream,
                      ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
   return (int)hipGetLastError();
 }
