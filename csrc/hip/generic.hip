@@ -429,52 +429,6 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
   gtab_count_claims(g, claims);
 }
 
-// Sort-based pre-combine of byte-span rows (AggTable._insert_sorted): the
-// 128-bit key of every span and a 32-bit sort key — a hash of the key for
-// short keys (<= 15 bytes: exact (hi, lo)), all ones for long keys and empty
-// spans (they sort last and take the direct insert) — plus the sort's digit
-// histograms ([4][256] u32, LDS-combined) and the number of short rows.
-// Equal keys share a hash, so they end up adjacent after the sort; colliding
-// keys may interleave, which only splits their partial folds (the table
-// merges partials of one key).
-__global__ void __launch_bounds__(256) span_prep_kernel(const u8* __restrict__ text, const long long* __restrict__ starts,
-                                                        const int* __restrict__ lens, u64 n, u64* __restrict__ out_hi,
-                                                        u64* __restrict__ out_lo, u32* __restrict__ k32,
-                                                        u32* __restrict__ ghist, unsigned long long* __restrict__ nshort) {
-  __shared__ u32 h[4][256];
-  __shared__ u32 bcnt;
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int b = 0; b < 4; ++b) h[b][t] = 0;
-  if (t == 0) bcnt = 0;
-  __syncthreads();
-  u32 cnt = 0;
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + t; i < n; i += stride) {
-    const long long s = starts[i];
-    const int len = lens[i];
-    u64 hi = 0, lo = 0;
-    u32 k = 0xFFFFFFFFu;
-    if (len > 0 && s >= 0 && len <= PACK_MAX) {
-      span_key(text, (u64)s, (u64)len, hi, lo);
-      const u32 x = (u32)(fmix64(hi ^ fmix64(lo + 0x9E3779B97F4A7C15ull)) >> 32);
-      k = x == 0xFFFFFFFFu ? 0xFFFFFFFEu : x;
-      ++cnt;
-    }
-    out_hi[i] = hi;
-    out_lo[i] = lo;
-    k32[i] = k;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 0xFFu], 1u);
-  }
-  if (cnt) atomicAdd(&bcnt, cnt);
-  __syncthreads();
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-    if (h[b][t]) atomicAdd(&ghist[b * 256 + t], h[b][t]);
-  if (t == 0 && bcnt) atomicAdd(nshort, (unsigned long long)bcnt);  // the block's short rows
-}
-
 // ---------------------------------------------------------------------------
 // Fused CSV fold (emit.csv): lines -> fields -> decimal parse -> LDS combine
 // -> HBM table, in one kernel that reads the text once — instead of the op
@@ -835,7 +789,19 @@ static Cols to_cols(const ColsArg* a) {
   return c;
 }
 
+// workgroup cap of the per-row insert: one row per thread up to 16 M rows
+// (the insert is probe-latency-bound; 65536 vs 8192 vs 2048 workgroups:
+// reducefn3 6.57-6.62 vs 6.60-6.91 vs 6.73-6.76 ms, profiles/r4/agg_grid_ab);
+// set from Tunables.agg_insert_grid (MR_AGG_INSERT_GRID) by the binding
+static unsigned g_ins_cap = 65536u;
+
 extern "C" {
+
+int mr_agg_set_insert_grid(int cap) {
+  if (cap < 256) return -1;
+  g_ins_cap = (unsigned)cap;
+  return 0;
+}
 
 // Keys pre-encoded (hi, lo, rep + rep_add) — or, when `text` is given, byte
 // spans (starts int64, lens int32) of `text`, whose rep offsets are
@@ -873,15 +839,7 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
                        ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
     return (int)hipGetLastError();
   }
-  static const unsigned ins_cap = [] {
-    // workgroup cap of the per-row insert: one row per thread up to 16 M rows
-    // (the insert is probe-latency-bound; 65536 vs 8192 vs 2048 workgroups:
-    // reducefn3 6.57-6.62 vs 6.60-6.91 vs 6.73-6.76 ms, profiles/r4/agg_grid_ab)
-    const char* e = getenv("MR_AGG_INSERT_GRID");
-    const long v = e ? atol(e) : 0;
-    return v >= 256 ? (unsigned)v : 65536u;
-  }();
-  hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256, ins_cap)), dim3(256), 0, stream,
+  hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256, g_ins_cap)), dim3(256), 0, stream,
                      ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
   return (int)hipGetLastError();
 }
@@ -941,15 +899,6 @@ int mr_csv_set_config(int tiles, int mode) {
 }
 
 // ghist: zeroed u32 [8][256] (the first 4 rows are filled); nshort: zeroed u64
-int mr_span_prep(const void* text, const void* starts, const void* lens, u64 n, void* hi, void* lo, void* k32,
-                 void* ghist, void* nshort, hipStream_t stream) {
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(span_prep_kernel, dim3(ag_grid(n, 256, 2048)), dim3(256), 0, stream, (const u8*)text,
-                     (const long long*)starts, (const int*)lens, n, (u64*)hi, (u64*)lo, (u32*)k32, (u32*)ghist,
-                     (unsigned long long*)nshort);
-  return (int)hipGetLastError();
-}
-
 int mr_slot_compact(void* tag, void* thi, void* tlo, void* tval, void* trep, void* ctrl, u64 cap, void* out_slot,
                     void* out_hi, void* out_lo, void* out_rep, void* counter, hipStream_t stream) {
   const u64 nb = (cap + 256 * SC_ITEMS - 1) / (256 * SC_ITEMS);

@@ -363,64 +363,6 @@ __global__ void __launch_bounds__(256) rec_gather16_kernel(const u8* __restrict_
   }
 }
 
-// The inverse of a permutation: inv[perm[i]] = i (n rows; perm a bijection).
-__global__ void rec_invert_kernel(const u32* __restrict__ perm, u64 n, u32* __restrict__ inv) {
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) inv[clamp_row(perm[i], n)] = (u32)i;
-}
-
-// out[inv[j]] = in[j] for rows of rb bytes (rb % 4 == 0): the row permutation
-// as a SCATTER.  The gather (rec_gather16_kernel) waits on a random 100-byte
-// read per row (84 % of its wave cycles, profiles/r3/ts_pmc/); here every
-// block reads R consecutive input rows with coalesced 16-byte loads into LDS
-// and writes each row to its destination with dword stores — 4-byte lanes of
-// one row side by side, so a row is one store instruction over its lines —
-// and stores do not stall the wave.  R * rb <= 16 KiB.
-template <int R>
-__global__ void __launch_bounds__(256) rec_scatter_kernel(const u8* __restrict__ in, u64 n, const u32* __restrict__ inv,
-                                                          u32 rb, u8* __restrict__ out) {
-  typedef u32 v4u __attribute__((ext_vector_type(4)));
-  extern __shared__ __attribute__((aligned(16))) v4u img[];  // ceil((R * rb + 12) / 16) chunks
-  __shared__ u32 dst[R];
-  const u32 t = threadIdx.x;
-  const u32 W = rb >> 2;  // dwords per row
-  const u64 nbatch = (n + R - 1) / R;
-  u32* img32 = reinterpret_cast<u32*>(img);
-  for (u64 b = blockIdx.x; b < nbatch; b += gridDim.x) {
-    const u64 r0 = b * (u64)R;
-    const u32 rows = (u32)min((u64)R, n - r0);
-    const u64 byte0 = r0 * rb;           // 4-byte aligned
-    const u64 a0 = byte0 & ~15ull;        // first aligned chunk
-    const u32 lead = (u32)(byte0 - a0);   // 0, 4, 8 or 12
-    const u64 nbytes = (u64)rows * rb;
-    const u64 in_end = n * (u64)rb;
-    const u32 nch = (u32)((lead + nbytes + 15) >> 4);
-    for (u32 c = t; c < nch; c += 256) {
-      const u64 a = a0 + 16ull * c;
-      v4u v;
-      if (a + 16 <= in_end) {
-        v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + a));
-      } else {
-        v = v4u{0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (a + 4 * j < in_end) v[j] = *reinterpret_cast<const u32*>(in + a + 4 * j);
-      }
-      img[c] = v;
-    }
-    for (u32 r = t; r < rows; r += 256) dst[r] = inv[r0 + r];
-    __syncthreads();
-    const u32 nw = rows * W;
-    const u32 l4 = lead >> 2;
-    for (u32 k = t; k < nw; k += 256) {
-      const u32 row = k / W, w = k - row * W;
-      const u64 d = (u64)clamp_row(dst[row], n);
-      reinterpret_cast<u32*>(out)[d * W + w] = img32[l4 + k];
-    }
-    __syncthreads();
-  }
-}
-
 // Rows whose width is not a multiple of 4 bytes: one byte per thread.
 __global__ void rec_gather_bytes_kernel(const u8* __restrict__ in, u64 nin, const u32* __restrict__ perm, u64 n,
                                         u64 rb, u8* __restrict__ out) {
@@ -538,21 +480,6 @@ int mr_rec_tie_fixup(const void* sk, void* perm, const void* rec, u64 n, int rb,
 // nin: rows of `in` (permutation entries >= nin read row 0).  mode: 0 = the
 // 16-byte LDS-staged gather where the shape allows it, 1 = the dword gather
 // (A/B probes and tests of both paths).
-// out[i] = in[perm[i]] for a full permutation of n rows (rb % 4 == 0,
-// rb <= 244, 16-byte aligned input), as a scatter through the inverse
-// permutation (ws: u32 [n]).  -1 when the shape does not fit it.
-int mr_rec_scatter(const void* in, const void* perm, u64 n, int rb, void* out, void* ws, hipStream_t s) {
-  if (n == 0) return 0;
-  if ((rb & 3) || rb < 4 || rb > 244 || ((uintptr_t)in & 15) || ((uintptr_t)out & 3)) return -1;
-  hipLaunchKernelGGL(rc::rec_invert_kernel, dim3(rc_grid(n, 16384)), dim3(256), 0, s, (const u32*)perm, n, (u32*)ws);
-  constexpr int R = 128;
-  const u64 nb = (n + R - 1) / R;
-  const size_t lds = (((size_t)R * rb + 12 + 15) / 16) * 16;
-  hipLaunchKernelGGL((rc::rec_scatter_kernel<R>), dim3((unsigned)(nb < 65536 ? nb : 65536)), dim3(256), lds, s,
-                     (const u8*)in, n, (const u32*)ws, (u32)rb, (u8*)out);
-  return (int)hipGetLastError();
-}
-
 int mr_rec_gather_set_rows(int rows) {
   if (rows != 128 && rows != 256) return -1;
   g_gather_rows = rows;

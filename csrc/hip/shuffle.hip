@@ -30,7 +30,9 @@ __device__ __forceinline__ u32 key_len(u64 lo, u64 rep) { return key_is_long(lo)
 
 __global__ void __launch_bounds__(T) pk_count_kernel(const u64* __restrict__ lo, const u64* __restrict__ rep,
                                                      const u32* __restrict__ part, u64 n, u32 W,
-                                                     unsigned long long* __restrict__ cnt /*[2W]*/) {
+                                                     unsigned long long* __restrict__ cnt /*[2W]*/,
+                                                     const unsigned long long* __restrict__ n_dev) {
+  if (n_dev && *n_dev < n) n = *n_dev;
   __shared__ u32 rc[MAXW];
   __shared__ unsigned long long bc[MAXW];
   for (u32 d = threadIdx.x; d < W; d += T) {
@@ -61,10 +63,22 @@ __host__ __device__ __forceinline__ u64 seg_bytes(u64 rows, u64 bytes) { return 
 // Separate layout: records in one array, key bytes in another.  Combined
 // layout: ONE buffer of per-destination segments [records | key bytes], so
 // the payload is a single all_to_all_single.
+//
+// Status (the W > 1 single-sync iteration): the map's completion checks ride
+// on the count exchange instead of a host read before it.  If the map table
+// overflowed (*ovf), a map chunk set its error word (errs[0..nerr)) or the
+// compaction found more rows than its bound (*n_dev > n_cap), extra gets
+// STATUS_REDO added: every rank sees it in the exchanged counts and the
+// exchange is redone after the flagged rank fixed its map.
+constexpr long long STATUS_REDO = 1ll << 40;
 __global__ void pk_scan_kernel(const unsigned long long* __restrict__ cnt, u32 W, unsigned long long* __restrict__ start,
                                unsigned long long* __restrict__ cursor, long long* __restrict__ xchg, long long extra,
-                               int combined) {
+                               int combined, const u32* __restrict__ ovf, const int* __restrict__ errs, u32 nerr,
+                               const unsigned long long* __restrict__ n_dev, u64 n_cap) {
   if (threadIdx.x != 0) return;
+  bool redo = (ovf && *ovf) || (n_dev && *n_dev > n_cap);
+  for (u32 k = 0; errs && k < nerr; ++k) redo |= errs[k] != 0;
+  if (redo) extra += STATUS_REDO;
   unsigned long long r = 0, b = 0;
   for (u32 d = 0; d < W; ++d) {
     if (combined) {
@@ -92,7 +106,9 @@ __global__ void __launch_bounds__(T) pk_scatter_kernel(const u64* __restrict__ h
                                                        const unsigned long long* __restrict__ start,
                                                        unsigned long long* __restrict__ cursor,
                                                        u8* __restrict__ rec /*records, byte-addressed*/,
-                                                       u8* __restrict__ blob) {
+                                                       u8* __restrict__ blob,
+                                                       const unsigned long long* __restrict__ n_dev) {
+  if (n_dev && *n_dev < n) n = *n_dev;
   __shared__ u32 rc[MAXW];
   __shared__ u32 bc[MAXW];
   __shared__ unsigned long long rbase[MAXW];
@@ -215,9 +231,12 @@ extern "C" {
 // ws: 6*W u64 (cnt[2W], start[2W], cursor[2W]); xchg: 3*W int64 (device)
 // combined != 0: rec == blob == one buffer of per-destination [records | key
 // bytes] segments (mr_pack_seg_bytes), sent with a single all-to-all.
+// n_dev (may be null): the row count on the device, n then being a bound
+// (rows [0, min(n, *n_dev)) are packed); ovf / errs / n_dev: the status
+// folded into the exchanged extra column (pk_scan_kernel).
 int mr_pack_by_dest(const void* hi, const void* lo, const void* val, const void* rep, const void* part, u64 n, u32 W,
                     const void* src, void* ws, void* xchg, long long extra, void* rec, void* blob, int combined,
-                    hipStream_t s) {
+                    const void* n_dev, const void* ovf, const void* errs, u32 nerr, hipStream_t s) {
   if (W == 0 || W > (u32)pk::MAXW) return -1;
   unsigned long long* cnt = (unsigned long long*)ws;
   unsigned long long* start = cnt + 2 * W;
@@ -225,17 +244,18 @@ int mr_pack_by_dest(const void* hi, const void* lo, const void* val, const void*
   hipMemsetAsync(cnt, 0, 2 * W * sizeof(unsigned long long), s);
   if (n) {
     hipLaunchKernelGGL(pk::pk_count_kernel, dim3(pk_grid(n, 1024)), dim3(pk::T), 0, s, (const u64*)lo,
-                       (const u64*)rep, (const u32*)part, n, W, cnt);
+                       (const u64*)rep, (const u32*)part, n, W, cnt, (const unsigned long long*)n_dev);
   }
   hipLaunchKernelGGL(pk::pk_scan_kernel, dim3(1), dim3(64), 0, s, (const unsigned long long*)cnt, W, start, cursor,
-                     (long long*)xchg, extra, combined);
+                     (long long*)xchg, extra, combined, (const u32*)ovf, (const int*)errs, nerr,
+                     (const unsigned long long*)n_dev, n);
   if (n) {
     // one record per thread (the per-block reservation needs every key of the
     // block in flight at once): grid = ceil(n / 256), not capped
     const u64 g = (n + pk::T - 1) / pk::T;
     hipLaunchKernelGGL(pk::pk_scatter_kernel, dim3((unsigned)g), dim3(pk::T), 0, s, (const u64*)hi, (const u64*)lo,
                        (const long long*)val, (const u64*)rep, (const u32*)part, n, W, (const u8*)src,
-                       (const unsigned long long*)start, cursor, (u8*)rec, (u8*)blob);
+                       (const unsigned long long*)start, cursor, (u8*)rec, (u8*)blob, (const unsigned long long*)n_dev);
   }
   return (int)hipGetLastError();
 }

@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(CT) tail_scatter_kernel(GTab g, u64 cap, u32 n
                                                           u64* __restrict__ out_hi, u64* __restrict__ out_lo,
                                                           long long* __restrict__ out_val, u64* __restrict__ out_rep,
                                                           u32* __restrict__ out_part, u64* __restrict__ out_c,
-                                                          const u32* __restrict__ bbase) {
+                                                          const u32* __restrict__ bbase, u64 out_cap) {
   __shared__ u32 wc[CT / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const u64 i = (u64)blockIdx.x * CT + t;
@@ -120,6 +120,7 @@ __global__ void __launch_bounds__(CT) tail_scatter_kernel(GTab g, u64 cap, u32 n
   for (int w = 0; w < CT / 64; ++w) o += w < wave ? wc[w] : 0u;
   if (!occ) return;
   o += (u64)__popcll(m & ((1ull << lane) - 1ull));
+  if (o >= out_cap) return;  // more rows than the caller's bound: flagged by tail_pad_kernel / the host
   const u64 h = g.hi[i], l = g.lo[i], r = g.rep[i];
   u32 len;
   const u32 f = key_fnv(h, l, r, src, &len);
@@ -130,6 +131,36 @@ __global__ void __launch_bounds__(CT) tail_scatter_kernel(GTab g, u64 cap, u32 n
   out_rep[o] = r;
   out_part[o] = p;
   out_c[o] = ((u64)p << 56) | (h >> 8);
+}
+
+// Rows [n, bound) of a compaction launched for a row BOUND instead of the
+// host-known count (the W > 1 reduce tail: the count is never downloaded
+// before the tail is queued).  They become sentinels that sort after every
+// real row — composite key 0xFF << 56 | row, i.e. partition digit 0xFF, which
+// no real row has when nparts <= 255, and distinct, so no tie run — with an
+// empty key (hi = lo = 0: length 0) and a zero value.  The host takes the real
+// count from the partition counts.  bad |= 8: the table had more rows than the
+// bound (re-run with the count); bad |= 16: the table overflowed.
+__global__ void tail_pad_kernel(const unsigned long long* __restrict__ counter, u64 bound, u64* __restrict__ out_hi,
+                                u64* __restrict__ out_lo, long long* __restrict__ out_val, u64* __restrict__ out_rep,
+                                u32* __restrict__ out_part, u64* __restrict__ out_c, const u32* __restrict__ ovf,
+                                u32* __restrict__ bad) {
+  const u64 n = *counter;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  const u64 i0 = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 == 0) {
+    u32 b = n > bound ? 8u : 0u;
+    if (ovf && *ovf) b |= 16u;
+    if (b) atomicOr(bad, b);
+  }
+  for (u64 i = n + i0; i < bound; i += stride) {
+    out_hi[i] = 0;
+    out_lo[i] = 0;
+    out_val[i] = 0;
+    out_rep[i] = 0;
+    out_part[i] = 0xFFu;
+    out_c[i] = (0xFFull << 56) | i;
+  }
 }
 
 // Digit histograms of the dense composite keys: LDS counts per block, then
@@ -212,10 +243,15 @@ u64 mr_tail_bhist_bytes(u64 cap) { return ((cap + tl::CT - 1) / tl::CT * 4 + 255
 // Occupied slots -> dense rows (+ partition, composite key).  With ghist: its
 // 8 digit histograms (+ partition counts into pcount); n = the number of
 // occupied slots (host-known: it sizes the histogram grid).
+// out_cap: rows the outputs hold (slots past it are dropped; the count in
+// `counter` still says how many there were).  pad != 0: n is a row BOUND, the
+// rows [count, n) become sentinels (tail_pad_kernel; nparts <= 255) and the
+// histograms cover all n rows; `bad` gets the bound / overflow flags.
 int mr_tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, u32 nparts,
                     const void* src, void* out_hi, void* out_lo, void* out_val, void* out_rep, void* out_part,
-                    void* out_c, void* counter, void* ghist, void* pcount, void* bhist, u64 n, hipStream_t s) {
-  if (nparts > 256 || bhist == nullptr) return -1;
+                    void* out_c, void* counter, void* ghist, void* pcount, void* bhist, u64 n, u64 out_cap, int pad,
+                    void* bad, hipStream_t s) {
+  if (nparts > 256 || bhist == nullptr || (pad && (nparts > 255 || bad == nullptr))) return -1;
   GTab g;
   g.tag = (u64*)tag;
   g.hi = (u64*)hi;
@@ -231,7 +267,14 @@ int mr_tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* c
   hipLaunchKernelGGL(tl::tail_bscan_kernel, dim3(1), dim3(tl::BS), 0, s, bcount, nb, (unsigned long long*)counter);
   hipLaunchKernelGGL(tl::tail_scatter_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, g, cap, nparts, (const u8*)src,
                      (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
-                     (const u32*)bcount);
+                     (const u32*)bcount, out_cap);
+  if (pad && n > 0) {
+    u64 pb = (n + 255) / 256;
+    if (pb > 1024) pb = 1024;
+    hipLaunchKernelGGL(tl::tail_pad_kernel, dim3((unsigned)pb), dim3(256), 0, s, (const unsigned long long*)counter, n,
+                       (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
+                       (const u32*)ctrl + 1, (u32*)bad);
+  }
   if (ghist != nullptr && n > 0) {
     u64 hb = (n + 4 * tl::T - 1) / (4 * tl::T);
     if (hb > (u64)tl::HIST_BLOCKS) hb = tl::HIST_BLOCKS;
@@ -314,10 +357,13 @@ static u32 g_tail_epoch = 0;
 // n = occupied slots of the table; src = the key-byte source (map arena or the
 // received blob); hp / hb = pinned host buffers of the packed columns and the
 // key bytes; est >= 0: DMA min(est, hb_cap) key bytes, else a device-sized copy.
+// padded != 0: n is a row bound, not the count (tail_pad_kernel): the host
+// learns the count from the downloaded partition counts, and bits 3/4 of the
+// downloaded flag word if the bound was too small / the table overflowed.
 int mr_tail_run(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, u64 n, u32 nparts,
-                const void* src, void* ws, u64 blob_cap, void* hp, void* hb, long long est, u64 hb_cap,
+                const void* src, void* ws, u64 blob_cap, void* hp, void* hb, long long est, u64 hb_cap, int padded,
                 hipStream_t s) {
-  if (nparts > 256) return -1;
+  if (nparts > 256 || (padded && nparts > 255)) return -1;
   u64 off[TB_COUNT];
   mr_tail_ws_layout(n, nparts, blob_cap, cap, off);
   u8* w = (u8*)ws;
@@ -326,7 +372,8 @@ int mr_tail_run(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl,
   int rc = (int)hipMemsetAsync(z, 0, TZ_BYTES, s);
   if (rc) return rc;
   rc = mr_tail_compact(tag, hi, lo, val, rep, ctrl, cap, nparts, src, P(TB_HI0), P(TB_LO0), P(TB_VAL0), P(TB_REP0),
-                       P(TB_PART0), P(TB_C), z, z + TZ_GHIST, z + TZ_PCOUNT, P(TB_BHIST), n, s);
+                       P(TB_PART0), P(TB_C), z, z + TZ_GHIST, z + TZ_PCOUNT, P(TB_BHIST), n, n, padded,
+                       z + TZ_BAD, s);
   if (rc) return rc;
   // 8 onesweep passes over the composite key (ghist from tail_compact)
   const void* kin = P(TB_C);

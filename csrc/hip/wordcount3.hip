@@ -398,18 +398,9 @@ __global__ void __launch_bounds__(256) ovf_agg3_kernel(Ovf o, GTab g) {
 
 constexpr int MAP_T = 512, MAP_SLOTS = 2048, MAP_TPC = 1;
 static_assert(sizeof(Lds<MAP_T, MAP_SLOTS>) <= 80 * 1024, "two workgroups per CU");
-// Wider combine spans: one workgroup per CU holds a 4096-slot
-// LDS table (gfx950: 160 KiB of LDS per CU) over 32-64 KiB of text, so more of
-// a word's occurrences meet in LDS before the flush (0.46 instead of 0.63
-// flushed entries per token in the round-3 simulation) at the price of no
-// second workgroup to overlap a flush with.
-static_assert(sizeof(Lds<512, 4096>) <= 160 * 1024, "4096 slots: one workgroup per CU");
-static_assert(sizeof(Lds<1024, 4096>) <= 160 * 1024, "4096 slots x 1024 threads: one workgroup per CU");
-
-// launch shapes: 0 = <512, 2048, 1> (8 KiB spans, two workgroups per CU),
-// 1 = <512, 4096, 4> (32 KiB), 2 = <512, 4096, 8> (64 KiB), 3 = <1024, 4096, 2>
-// (32 KiB, 16 waves per CU)
-static int g_map_cfg = 0;
+// (Wider combine spans — 4096 LDS slots over 32/64 KiB, one workgroup per CU —
+// cut the flush's atomics by 18 % but ran 3.40 vs 2.04 ms; removed in round 5,
+// archived in profiles/r5/pruned/, numbers in profiles/r4/map_shapes/.)
 
 template <int T, int SLOTS, int TPC>
 static void launch_map3(const u8* text, u64 nbytes, u64 rep_base, const GTab& g, const Ovf& o, int aligned,
@@ -443,21 +434,9 @@ int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, 
   v3::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter};
   const int aligned = ((uintptr_t)text & 15) == 0;
   const u8* t = (const u8*)text;
-  switch (v3::g_map_cfg) {
-    case 1: v3::launch_map3<512, 4096, 4>(t, nbytes, rep_base, g, o, aligned, stream); break;
-    case 2: v3::launch_map3<512, 4096, 8>(t, nbytes, rep_base, g, o, aligned, stream); break;
-    case 3: v3::launch_map3<1024, 4096, 2>(t, nbytes, rep_base, g, o, aligned, stream); break;
-    default: v3::launch_map3<v3::MAP_T, v3::MAP_SLOTS, v3::MAP_TPC>(t, nbytes, rep_base, g, o, aligned, stream);
-  }
+  v3::launch_map3<v3::MAP_T, v3::MAP_SLOTS, v3::MAP_TPC>(t, nbytes, rep_base, g, o, aligned, stream);
   hipLaunchKernelGGL(v3::ovf_agg3_kernel, dim3(1024), dim3(256), 0, stream, o, g);
   return (int)hipGetLastError();
-}
-
-// The map kernel's launch shape (see v3::g_map_cfg); -1 on an unknown one.
-int mr_wc_map3_set_config(int cfg) {
-  if (cfg < 0 || cfg > 3) return -1;
-  v3::g_map_cfg = cfg;
-  return 0;
 }
 
 }  // extern "C"

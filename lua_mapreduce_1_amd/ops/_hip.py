@@ -33,14 +33,13 @@ _SIGS = {
     "mr_d2h_async": [_p, _p, _u64, _p],
     "mr_h2d_pull": [_p, _p, _u64, _i32, _p],
     "mr_signal_host": [_p, _u32, _p],
-    "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64, _p],
+    "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64, _i32,
+                    _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
     "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p, _p],
     "mr_table_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p, _p],
     "mr_gather_aos4": [_p, _u64, _p, _p, _p, _p, _p, _p],
     "mr_rec_gather_set_rows": [_i32],
-    "mr_rec_scatter": [_p, _p, _u64, _i32, _p, _p, _p],
-    "mr_span_prep": [_p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
     "mr_csv_fold": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _u64, _u64, _p, _p, _p, _p],
     "mr_key_word": [_p, _p, _p, _p, _u64, _u32, _p, _p],
     "mr_key_meta": [_p, _p, _p, _u64, _p, _u32, _p, _p, _p],
@@ -78,9 +77,11 @@ _SIGS = {
     "mr_ts_keys": [_p, _u64, _p, _p, _p, _p],
     "mr_ts_checksum": [_p, _u64, _p, _p],
     "mr_ts_unsorted": [_p, _p, _u64, _p, _p],
-    "mr_pack_by_dest": [_p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, ctypes.c_longlong, _p, _p, _i32, _p],
+    "mr_pack_by_dest": [_p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, ctypes.c_longlong, _p, _p, _i32, _p, _p, _p,
+                        _u32, _p],
     "mr_fix_loc": [_p, _u64, _p, _p, _u32, _p, _p],
-    "mr_tail_compact": [_p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _u64, _p],
+    "mr_tail_compact": [_p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _u64, _u64,
+                        _i32, _p, _p],
     "mr_tail_bhist_bytes": [_u64],
     "mr_tail_gather": [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "mr_tail_pack": [_p, _p, _u64, _p, _u32, _p, _p, _p, _p],
@@ -117,8 +118,8 @@ _SIGS = {
     "mr_exact_fix": [_p, _p, _u64, _p, _p, _p, _p, _p, _p, _p, _p],
     "mr_seg_reduce": [_p, _u64, _p, _u64, _i32, _i32, _p, _p],
     "mr_posting_keys": [_p, ctypes.c_longlong, _p, ctypes.c_longlong, ctypes.c_longlong, _p, _p, _p],
-    "mr_wc_map3_set_config": [_i32],
     "mr_csv_set_config": [_i32, _i32],
+    "mr_agg_set_insert_grid": [_i32],
 }
 _RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
                 "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words"}
@@ -146,10 +147,10 @@ def lib():
         L.mr_host_free.restype = _i32
         if L.mr_sort_set_rounds(TUNABLES.sort_rounds) != 0:
             raise ValueError(f"MR_SORT_ROUNDS={TUNABLES.sort_rounds}: must be 16, 24 or 32")
-        if L.mr_wc_map3_set_config(TUNABLES.wc_map_config) != 0:
-            raise ValueError(f"MR_WC_MAP_CONFIG={TUNABLES.wc_map_config}: must be 0..3")
         if L.mr_csv_set_config(TUNABLES.csv_tiles, TUNABLES.csv_mode) != 0:
             raise ValueError(f"MR_CSV_TILES={TUNABLES.csv_tiles} / MR_CSV_MODE={TUNABLES.csv_mode}: 0..64 / 0..2")
+        if L.mr_agg_set_insert_grid(TUNABLES.agg_insert_grid) != 0:
+            raise ValueError(f"MR_AGG_INSERT_GRID={TUNABLES.agg_insert_grid}: must be >= 256")
         if L.mr_rec_gather_set_rows(TUNABLES.rec_gather_rows) != 0:
             raise ValueError(f"MR_REC_GATHER_ROWS={TUNABLES.rec_gather_rows}: must be 128 or 256")
         _LIB = L
@@ -252,6 +253,7 @@ def wait_stream(device=None) -> None:
     hipStreamSynchronize (which also reports a failed kernel).
     ``MR_SPIN_US=0``: always hipStreamSynchronize."""
     global _FLAGS
+    WAITS[0] += 1
     if SPIN_S <= 0:
         torch.cuda.current_stream(device).synchronize()
         return
@@ -280,4 +282,5 @@ def wait_stream(device=None) -> None:
         WAIT_LOG.append((t_a, time.perf_counter(), bool(w[k] == seq)))
 
 
+WAITS = [0]  # host waits on a stream so far (tests count them per iteration)
 WAIT_LOG = [] if TUNABLES.wait_log else None  # (start, end, flag seen) of each wait_stream

@@ -26,7 +26,6 @@ import torch
 from . import _hip
 from . import keys as K
 from .primitives import HashTable, _np, _t64, _u64, next_pow2
-from ..utils.config import TUNABLES
 
 DTYPES = {"i64": torch.int64, "f64": torch.float64, "f32": torch.float32}
 _VT = {torch.int64: 0, torch.float64: 1, torch.float32: 2, torch.int32: 3}
@@ -257,8 +256,10 @@ class AggTable:
             a.list = 1 if self.list_mode else 0
             a.cstride = 1 if self.list_mode else self.cstride
             # (list mode: one row per thread; an LDS key -> slot cache and batched
-            # rows per thread measured slower, profiles/r4/pruned/)
-            a.rows_only = 1 if TUNABLES.agg_direct else 0
+            # rows per thread measured slower, profiles/r4/pruned/; a direct
+            # per-row insert without the LDS combine and a sort-based
+            # pre-combine lost too, profiles/r5/pruned/)
+            a.rows_only = 0
             keep = []
             for j, (v, dt) in enumerate(vals):
                 if isinstance(v, torch.Tensor):
@@ -285,9 +286,6 @@ class AggTable:
                 a.post_slot = self.post_slot.data_ptr()
                 a.post_base = self.npost
             t = self.keys
-            if (text is not None and not self.list_mode and n >= TUNABLES.agg_sort_min > 0):
-                self._insert_sorted(n, vals, text, starts, lens, rep_base)
-                return
             if text is not None:
                 st = starts.to(torch.int64).contiguous()
                 ln = lens.to(torch.int32).contiguous()
@@ -322,92 +320,6 @@ class AggTable:
             cols.append(_np(v).astype(npdt) if isinstance(v, torch.Tensor) else np.full(n, v, npdt))
         self._pending.append((h, lw, r, cols, ok))
         self.npost += n if self.list_mode else 0
-
-    def _insert_sorted(self, n: int, vals: list, text, starts, lens, rep_base: int) -> None:
-        """Fold mode, many byte-span rows (GPU): pre-combine by sorting instead
-        of hashing each row into the table.  Rows are ordered by a 32-bit hash
-        of their (exact, <= 15-byte) key — 4 onesweep passes over u32 keys —
-        so equal keys are adjacent; each run's partial columns are folded by
-        segmented reductions (ops/segments.py) and only the runs' keys are
-        inserted, one table insert per distinct key of the batch instead of
-        one per row (the per-row inserts of a Zipf vocabulary's tail were the
-        CSV group-by's bound, profiles/r4/kstats).  Long keys and empty spans
-        sort last and take the per-row insert."""
-        from . import segments as SG
-        from .primitives import exclusive_scan, sort_keys32
-        d = self.device
-        s = _hip.stream(d)
-        st = starts.to(torch.int64).contiguous()
-        ln = lens.to(torch.int32).contiguous()
-        hi = torch.empty(n, dtype=torch.int64, device=d)
-        lo = torch.empty(n, dtype=torch.int64, device=d)
-        k32 = torch.empty(n, dtype=torch.int32, device=d)
-        ghist = torch.zeros(2048, dtype=torch.int32, device=d)
-        nsh = torch.zeros(1, dtype=torch.int64, device=d)
-        _hip.call("mr_span_prep", _hip.ptr(text), _hip.ptr(st), _hip.ptr(ln), n, _hip.ptr(hi), _hip.ptr(lo),
-                  _hip.ptr(k32), _hip.ptr(ghist), _hip.ptr(nsh), s)
-        perm, _ = sort_keys32(k32, ghist=ghist)
-        # gather the rows' columns in sorted order: keys, spans, value inputs
-        tens = {}
-        for v, _dt in vals:
-            if isinstance(v, torch.Tensor) and id(v) not in tens:
-                tens[id(v)] = v
-        inputs = []
-        for v in tens.values():
-            if v.device != d:
-                v = v.to(d)
-            if v.dtype == torch.float32:
-                v = v.to(torch.float64)
-            elif v.dtype == torch.int32:
-                v = v.to(torch.int64)
-            inputs.append(v.contiguous())
-        words = [hi, lo, st] + [v.view(torch.int64) if v.dtype == torch.float64 else v for v in inputs]
-        outs = [torch.empty(n, dtype=torch.int64, device=d) for _ in words]
-        sln = torch.empty(n, dtype=torch.int32, device=d)
-        for c0 in range(0, len(words), 5):
-            ws, os_ = words[c0:c0 + 5], outs[c0:c0 + 5]
-            ws = ws + [None] * (5 - len(ws))
-            os_ = os_ + [None] * (5 - len(os_))
-            q = ln if c0 == 0 else None
-            _hip.call("mr_gather_cols", _hip.ptr(perm), n, *[_hip.ptr(w) for w in ws], _hip.ptr(q),
-                      *[_hip.ptr(o) for o in os_], _hip.ptr(sln if q is not None else None), s)
-        g_hi, g_lo, g_st = outs[0], outs[1], outs[2]
-        g_in = {}
-        for (key, v), o in zip(tens.items(), outs[3:]):
-            g_in[key] = o.view(torch.float64) if (v.dtype in (torch.float64, torch.float32)) else o
-        ns = int(nsh.item())
-        if ns:
-            heads = torch.empty(ns, dtype=torch.int32, device=d)
-            _hip.call("mr_segment_heads", _hip.ptr(g_hi), _hip.ptr(g_lo), ns, _hip.ptr(heads), s)
-            seg, total = exclusive_scan(heads)
-            m = int(total.item())
-            uhi, ulo, start = (torch.empty(m, dtype=torch.int64, device=d) for _ in range(3))
-            _hip.call("mr_segment_keys", _hip.ptr(seg), _hip.ptr(heads), _hip.ptr(g_hi), _hip.ptr(g_lo), None, ns,
-                      _hip.ptr(uhi), _hip.ptr(ulo), None, _hip.ptr(start), s)
-            off = torch.cat([start, torch.tensor([ns], dtype=torch.int64, device=d)])
-            cnt = SG.lengths(off)
-            urep = ((g_st[start] + rep_base) << K.REP_LEN_BITS) | sln[start].to(torch.int64)
-            partial = []
-            for (v, dt), (_dt, op, _i) in zip(vals, self.cols_spec):
-                if isinstance(v, torch.Tensor):
-                    col = g_in[id(v)][:ns]
-                    if dt in ("f64", "f32") and col.dtype != torch.float64:
-                        col = col.to(torch.float64)
-                    elif dt == "i64" and col.dtype == torch.float64:
-                        col = col.to(torch.int64)  # per-row truncation, as the row insert does
-                    partial.append(SG.reduce(off, col, op))
-                elif op == "sum":
-                    partial.append(cnt.to(torch.float64) * float(v) if dt != "i64" else cnt * int(v))
-                else:
-                    partial.append(torch.full((m,), float(v) if dt != "i64" else int(v),
-                                              dtype=torch.float64 if dt != "i64" else torch.int64, device=d))
-            self._insert_partials(m, partial, uhi, ulo, urep)
-        if ns < n:
-            # long keys and empty spans: the per-row insert
-            rest_vals = []
-            for v, dt in vals:
-                rest_vals.append((g_in[id(v)][ns:] if isinstance(v, torch.Tensor) else v, dt))
-            self._insert_rows(n - ns, rest_vals, text, g_st[ns:].contiguous(), sln[ns:].contiguous(), rep_base)
 
     def insert_csv(self, text: torch.Tensor, rep_base: int, key: int, values, sep: int,
                    rows_out: torch.Tensor) -> None:
@@ -457,27 +369,6 @@ class AggTable:
             a.op[j] = _OPC[self.cols_spec[j][1]]
             a.dst[j] = self.cols[j].data_ptr()
         return a
-
-    def _insert_partials(self, m: int, partial: list, hi, lo, rep) -> None:
-        """m distinct keys with one partial fold per physical column."""
-        keep: list = []
-        a = self._cols_arg([(p, dt) for p, (dt, _op, _i) in zip(partial, self.cols_spec)], m, keep)
-        a.rows_only = 1  # distinct keys: one per thread over the whole chip, no LDS combine
-        t = self.keys
-        _hip.call("mr_agg_insert", *t._gtab(), t.cap, _hip.ptr(self.src), _hip.ptr(hi.contiguous()),
-                  _hip.ptr(lo.contiguous()), _hip.ptr(rep.contiguous()), 0, None, None, None, 0, m, ctypes.byref(a),
-                  _hip.stream(self.device))
-
-    def _insert_rows(self, n: int, vals: list, text, starts, lens, rep_base: int) -> None:
-        """Per-row insert of byte spans (the kernel's direct / LDS-combine path)."""
-        keep: list = []
-        a = self._cols_arg(vals, n, keep)
-        t = self.keys
-        st = starts.to(torch.int64).contiguous()
-        ln = lens.to(torch.int32).contiguous()
-        keep += [st, ln]
-        _hip.call("mr_agg_insert", *t._gtab(), t.cap, _hip.ptr(self.src), None, None, None, 0,
-                  _hip.ptr(text), _hip.ptr(st), _hip.ptr(ln), rep_base, n, ctypes.byref(a), _hip.stream(self.device))
 
     def rehome_long_keys(self, buf: torch.Tensor, lo_off: int, hi_off: int, heap: torch.Tensor,
                          heap_cap: int) -> None:

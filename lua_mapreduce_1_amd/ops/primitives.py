@@ -185,7 +185,6 @@ class HashTable:
             else:
                 a.stype[0], a.sbits[0] = A._VT_SCALAR, int(1 if val is None else val)
             a.dst[0], a.dtype[0], a.op[0] = self.val.data_ptr(), 0, OPS[self.op]
-            a.rows_only = 1 if TUNABLES.agg_direct else 0
             st = starts.to(torch.int64).contiguous()
             ln = lens.to(torch.int32).contiguous()
             _hip.call("mr_agg_insert", *self._gtab(), self.cap, _hip.ptr(self.src), None, None, None, 0,

@@ -15,7 +15,6 @@ import numpy as np
 import torch
 
 from . import _hip
-from ..utils.config import TUNABLES
 
 
 def _check(rec: torch.Tensor, kb: int) -> tuple[int, int]:
@@ -103,31 +102,20 @@ def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: tor
     return perm, sk
 
 
-def gather(rec: torch.Tensor, perm: torch.Tensor, mode: int | None = None) -> torch.Tensor:
+def gather(rec: torch.Tensor, perm: torch.Tensor, mode: int = 0) -> torch.Tensor:
     """rec[perm] (rows).  GPU: 16-byte LDS-staged row gather for rows of
     16-244 bytes (a multiple of 4) in 16-byte aligned buffers, else the dword
-    (or byte) gather; ``mode=1`` forces the dword gather (A/B probes, tests);
-    ``mode=3`` (default with ``MR_REC_SCATTER=1``): a full permutation is
-    applied as a scatter through its inverse (coalesced row reads, dword
-    stores to the destinations)."""
+    (or byte) gather; ``mode=1`` forces the dword gather (A/B probes, tests).
+    (A scatter through the inverse permutation lost: 16.6 vs 10.1 ms per
+    10 GB, removed in round 5, profiles/r5/pruned/.)"""
     n = perm.numel()
     rb = int(rec.shape[1])
-    if mode is None:
-        mode = 3 if TUNABLES.rec_scatter else 0
     if rec.is_cuda:
         out = torch.empty((n, rb), dtype=torch.uint8, device=rec.device)
         if n == 0:
             return out
         if rec.shape[0] == 0:
             raise IndexError("gather from an empty record block")
-        if mode == 3:
-            if n == rec.shape[0] and rec.is_contiguous():
-                p = perm if perm.dtype == torch.int32 else perm.to(torch.int32)
-                ws = torch.empty(n, dtype=torch.int32, device=rec.device)
-                if _hip.lib().mr_rec_scatter(_hip.ptr(rec), _hip.ptr(p.contiguous()), n, rb, _hip.ptr(out),
-                                             _hip.ptr(ws), _hip.stream(rec.device)) == 0:
-                    return out
-            mode = 0
         p = perm if perm.dtype == torch.int32 else perm.to(torch.int32)
         _hip.call("mr_rec_gather", _hip.ptr(rec), int(rec.shape[0]), _hip.ptr(p.contiguous()), n, rb, _hip.ptr(out),
                   int(mode), _hip.stream(rec.device))

@@ -31,7 +31,7 @@ def pack_by_dest(hi, lo, val, rep, part, W: int, src, extra: int = 0, blob_capac
         xchg = torch.empty(3 * W, dtype=torch.int64, device=d)
         _hip.call("mr_pack_by_dest", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), n, W,
                   _hip.ptr(src) if src is not None else None, _hip.ptr(ws), _hip.ptr(xchg), int(extra),
-                  _hip.ptr(rec), _hip.ptr(blob), 0, _hip.stream(d))
+                  _hip.ptr(rec), _hip.ptr(blob), 0, None, None, None, 0, _hip.stream(d))
         return rec, blob, xchg
     dest = (part.numpy().astype(np.int64) % W)
     order = np.argsort(dest, kind="stable")
@@ -59,11 +59,19 @@ def seg_bytes(rows: int, nbytes: int) -> int:
     return 32 * rows + ((nbytes + 7) & ~7)
 
 
-def pack_by_dest_combined(hi, lo, val, rep, part, W: int, src, extra: int = 0):
+STATUS_REDO = 1 << 40  # csrc/hip/shuffle.hip: added to the exchanged extra column by a rank that must redo its map
+
+
+def pack_by_dest_combined(hi, lo, val, rep, part, W: int, src, extra: int = 0, n_dev=None, status=None):
     """GPU: ONE uint8 buffer of per-destination segments [records (32 B:
     hi, lo, val, loc) | key bytes, padded to 8] + the count-exchange row
     [records, bytes, extra] per destination; destination d's segment is
     seg_bytes(rows_d, bytes_d) long, so the payload is a single all-to-all.
+    ``n_dev``: the row count as a device int64 (the columns then hold a
+    bound of rows, not the count: nothing is read on the host).
+    ``status`` = (table ctrl, chunk error words): a rank whose map table
+    overflowed, whose map reported a device error or whose rows exceed the
+    bound adds STATUS_REDO to its exchanged extra column.
     -> (buf uint8, xchg int64 [3W])."""
     assert hi.is_cuda
     n = hi.numel()
@@ -72,9 +80,16 @@ def pack_by_dest_combined(hi, lo, val, rep, part, W: int, src, extra: int = 0):
     cap = 32 * n + ((src.numel() if src is not None else 0) + 16 * n) + 8 * W
     ws, buf = _combined_bufs(d, W, cap)
     xchg = torch.empty(3 * W, dtype=torch.int64, device=d)
+    ovf = errs = None
+    nerr = 0
+    if status is not None:
+        ctrl, ew = status
+        ovf = _hip.ptr(ctrl[1:2])
+        if ew is not None and ew.numel():
+            errs, nerr = _hip.ptr(ew), int(ew.numel())
     _hip.call("mr_pack_by_dest", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), n, W,
               _hip.ptr(src) if src is not None else None, _hip.ptr(ws), _hip.ptr(xchg), int(extra),
-              _hip.ptr(buf), _hip.ptr(buf), 1, _hip.stream(d))
+              _hip.ptr(buf), _hip.ptr(buf), 1, _hip.ptr(n_dev), ovf, errs, nerr, _hip.stream(d))
     return buf, xchg
 
 

@@ -123,6 +123,27 @@ def all_to_all_v(payload: torch.Tensor, send_counts: list[int], recv_counts: lis
     return out
 
 
+def all_to_all_bytes(payloads: list, device=None, group=None) -> list:
+    """payloads[d] (bytes) goes to rank d; returns the byte strings every rank
+    sent here, in rank order.  Two collectives whatever the world size: the
+    int64 byte counts, then ONE uint8 all_to_all_single of the concatenated
+    payloads (on the device for RCCL, on the host for gloo).  Every payload
+    carries one pad byte, so no rank sends or receives an empty tensor."""
+    rank, world = world_info(group)
+    dev = _coll_device(torch.device(device) if device is not None else torch.device("cpu"), group)
+    send = [len(b) + 1 for b in payloads]
+    counts = torch.tensor(send, dtype=torch.int64)
+    recv = exchange_counts(counts.to(dev), group).cpu().tolist()
+    blob = b"".join(b + b"\0" for b in payloads)
+    buf = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+    out = all_to_all_v(buf, send, recv, group).cpu().numpy().tobytes()
+    res, o = [], 0
+    for n in recv:
+        res.append(out[o:o + n - 1])
+        o += n
+    return res
+
+
 def barrier(group=None, device=None) -> None:
     if dist.is_available() and dist.is_initialized():
         if device is not None and torch.device(device).type == "cuda" and not _is_gloo(group):

@@ -259,6 +259,11 @@ class GenericMap:
         # job.lua:92-96) and once more at the end of the map (job.lua:198-202)
         self.reducers = reducers if (reducers is not None and reducers.has_combiner and phys is None) else None
         self.combine_at = int(combine_at or TUNABLES.combine_postings)
+        # the next combine runs when the postings pass this: after a combine
+        # (or a refused one) it moves to twice what is left, so a combiner
+        # that cannot shrink the table (many distinct keys, a dedup or top-k
+        # combiner) runs O(log n) times per map, not once per emit call
+        self._next_combine = self.combine_at
         self.combines = 0
 
     @property
@@ -282,8 +287,9 @@ class GenericMap:
         self.table.src = self.src.source()
         self.table.insert(n, list(values), **kw)
         self.rows += n
-        if self.reducers is not None and self.table.npost >= self.combine_at:
+        if self.reducers is not None and self.table.npost >= self._next_combine:
             self.combine()
+            self._next_combine = max(self.combine_at, 2 * self.table.npost)
 
     def insert_csv(self, text: torch.Tensor, key: int, values: tuple, sep: int) -> None:
         fused = (self.phys is not None and self.table.is_cuda and len(values) <= A.CSV_MAXV
@@ -322,7 +328,7 @@ class GenericMap:
         if self.reducers is None or t.npost == 0:
             return False
         m, ovf = t.stats()
-        if ovf or m > t.cap // 2 + 1:
+        if ovf or (t.is_cuda and m > t.cap // 2 + 1):  # (CPU stats count rows: no capacity to respect)
             return False
         slot, hi, lo, rep, pslot, pval = t.postings()
         m = int(hi.numel())

@@ -532,25 +532,32 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                 self._table_capacity = self.table.cap
                 self._run_map(jobs, recs, j0, j1)
                 continue
-            # a rank that maps a lot of input per iteration gets sparse tables
-            # for its next maps (MR_MAP_SPARSITY slots per distinct key): fewer
-            # probes, the flush's atomics and loads spread over more memory
-            # lines (full corpus: map 2.43 -> 2.06 ms from 2^20 to 2^23 slots).
-            # A small share keeps the table: the send-side compaction scans
-            # every slot, which cost more than the map saved at W = 8
-            # (profiles/r2/sparse/)
-            if getattr(self, "_mapped_bytes", 0) >= TUNABLES.map_sparse_min_mb * 2**20:
-                self._table_capacity = max(self._table_capacity, min(
-                    ops.next_pow2(TUNABLES.map_sparsity * max(n_claimed, 1)), _MAX_SPARSE_CAP))
-            # a table grown 16x after an overflow can end far above the key
-            # count: the next maps get one sized for it (load 1/4 - 1/2; the
-            # tail's compaction reads every slot's line of every column)
-            fit = max(ops.next_pow2(2 * max(n_claimed, 1)), self._initial_capacity,
-                      min(ops.next_pow2(TUNABLES.map_sparsity * max(n_claimed, 1)), _MAX_SPARSE_CAP)
-                      if getattr(self, "_mapped_bytes", 0) >= TUNABLES.map_sparse_min_mb * 2**20 else 0)
-            if self._table_capacity >= 4 * fit:
-                self._table_capacity = fit
+            self._adapt_capacity(n_claimed)
             return n_claimed, overflow
+
+    def _adapt_capacity(self, n_claimed: int) -> None:
+        """The map table capacity of the next maps, from this map's key count."""
+        # a rank that maps a lot of input per iteration gets sparse tables
+        # for its next maps (MR_MAP_SPARSITY slots per distinct key): fewer
+        # probes, the flush's atomics and loads spread over more memory
+        # lines (full corpus: map 2.43 -> 2.06 ms from 2^20 to 2^23 slots).
+        # A small share keeps the table: the send-side compaction scans
+        # every slot, which cost more than the map saved at W = 8
+        # (profiles/r2/sparse/)
+        big = getattr(self, "_mapped_bytes", 0) >= TUNABLES.map_sparse_min_mb * 2**20
+        if n_claimed > self.table.cap // 2:
+            # more than half full (still exact): the next maps get room
+            self._table_capacity = max(self._table_capacity, ops.next_pow2(4 * n_claimed))
+        if big:
+            self._table_capacity = max(self._table_capacity, min(
+                ops.next_pow2(TUNABLES.map_sparsity * max(n_claimed, 1)), _MAX_SPARSE_CAP))
+        # a table grown 16x after an overflow can end far above the key
+        # count: the next maps get one sized for it (load 1/4 - 1/2; the
+        # tail's compaction reads every slot's line of every column)
+        fit = max(ops.next_pow2(2 * max(n_claimed, 1)), self._initial_capacity,
+                  min(ops.next_pow2(TUNABLES.map_sparsity * max(n_claimed, 1)), _MAX_SPARSE_CAP) if big else 0)
+        if self._table_capacity >= 4 * fit:
+            self._table_capacity = fit
 
     def _device_spans(self, res, recs, j0: int, j1: int) -> None:
         """Job records and timings from the slot's device events (after the
@@ -647,7 +654,7 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         return (self.device.type == "cuda" and spec is not None and spec[0] == "fnv1"
                 and self.nparts <= 256 and TUNABLES.fused_tail)
 
-    def _finalize_table(self, table, n: int, src) -> dict:
+    def _finalize_table(self, table, n: int, src, padded: bool = False) -> dict:
         """The fused device tail of a table: every launch and download queued
         by one native call (mr_tail_run, csrc/hip/tail.hip) — or, once a tail
         of this engine had to fall back to the exact key order (long keys in
@@ -658,7 +665,121 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
             hi, lo, val, rep, aos = table.compact((n, False), aos=True)
             return devmod.finalize_exact_device(hi, lo, val, rep, src, self.nparts, self.partmod, blob_cap=cap,
                                                 aos=aos)
-        return devmod.finalize_table_native(table, n, src, self.nparts, blob_cap=cap)
+        return devmod.finalize_table_native(table, n, src, self.nparts, blob_cap=cap, padded=padded)
+
+    # -- the W > 1 iteration with two host waits ------------------------------
+    def _single_sync_ok(self, sh: bool, fused: bool) -> bool:
+        """The fold plane's W > 1 iteration waits on the device only for the
+        count exchange and the result download: the map's completion checks
+        (table overflow, chunk error words) ride on the count exchange, and
+        the reduce table's key count is never read before the tail is queued
+        (the tail runs for a row bound; finalize_table_native(padded=True)).
+        Not for restored or checkpointed maps (they need the key count
+        first), streamed inputs or more than 255 partitions."""
+        return (sh and fused and TUNABLES.single_sync and self.nparts <= 255 and self._restored_src is None
+                and not self.checkpoint_dir and not self._arena_cap())
+
+    def _send_bound(self) -> int:
+        """Rows the send-side compaction is launched for: the table's slots on
+        a first map, else the last map's key count plus a quarter (rounded, so
+        the workspaces keep their shape); a map with more keys is flagged by
+        the compaction and redone with its count."""
+        est = getattr(self, "_send_est", None)
+        if est is None:
+            return self.table.cap
+        b = est + est // 4 + 4096
+        return min(self.table.cap, (b + 0xFFFF) & ~0xFFFF)
+
+    def _exchange_single_sync(self, jobs, recs, j0: int, j1: int, before_sync):
+        """Compaction, pack and count exchange queued straight behind the
+        map's launches; ONE host wait downloads the exchanged counts together
+        with this rank's map checks.  A rank whose map overflowed, reported a
+        device error or outgrew the compaction's bound adds STATUS_REDO to its
+        exchanged extra column; every rank sees it and the exchange is redone
+        after that rank fixed its map (the map re-run of _map_sync).  Returns
+        (received buffer, recv counts [W, 3] on the device, received rows,
+        map key count)."""
+        from ..ops import shuffle as SH
+        W = self.world
+        while True:
+            src = self._source()
+            failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
+            bound = self._send_bound()
+            with trace.range("mr.compact"):
+                hi, lo, val, rep, part, cnt = devmod.compact_partition(self.table, bound, src, self.nparts, bound=True)
+            nch = len(self._chunks[self.tslot])
+            errs = self._errs[self.tslot][:nch] if nch and self._errs[self.tslot] is not None else None
+            with trace.range("mr.pack"):
+                buf, xchg = SH.pack_by_dest_combined(hi, lo, val, rep, part, W, src, extra=failed, n_dev=cnt,
+                                                     status=(self.table.ctrl, errs))
+            with trace.range("mr.count_exchange"):
+                recv = D.exchange_counts(xchg, self.group)
+            if before_sync is not None:
+                before_sync()  # the next iteration's map: queued before this wait
+                before_sync = None
+            with trace.range("mr.count_sync"):
+                got = ops.host_read_many([xchg, recv, self.table.ctrl, cnt] + ([errs] if errs is not None else []))
+            send_h, recv_h = got[0].reshape(W, 3).tolist(), got[1].reshape(W, 3).tolist()
+            c = got[2]
+            overflow = bool(c[1])
+            n_claimed = int(got[3][0])
+            e = got[4] if errs is not None else None
+            if not any(r[2] >= SH.STATUS_REDO for r in recv_h):
+                break
+            # a redo: this rank fixes what it flagged, every rank exchanges again
+            self._send_est = n_claimed
+            bad = [k for k in range(nch) if e is not None and e[k]]
+            if bad:
+                self._mark_broken(jobs, recs, bad)
+                self.table.reset()
+                self._run_map(jobs, recs, j0, j1)
+            elif overflow:
+                self.table = ops.HashTable(ops.next_pow2(16 * max(n_claimed, 1)), device=self.device, op=self.op)
+                self._table_capacity = self.table.cap
+                self._run_map(jobs, recs, j0, j1)
+        self._send_est = n_claimed
+        self._adapt_capacity(n_claimed)
+        self._failed_total = sum(r[2] & (SH.STATUS_REDO - 1) for r in recv_h)
+        send_sz = [SH.seg_bytes(r[0], r[1]) for r in send_h]
+        recv_sz = [SH.seg_bytes(r[0], r[1]) for r in recv_h]
+        self._shuffled = (sum(send_sz), sum(send_sz) - send_sz[self.rank])
+        with trace.range("mr.all_to_all"):
+            rbuf = D.all_to_all_v(buf[:sum(send_sz)], send_sz, recv_sz, self.group)
+        return rbuf, recv.view(W, 3), sum(r[0] for r in recv_h), n_claimed
+
+    def _mark_broken(self, jobs, recs, bad_chunks) -> None:
+        """Chunks whose device error word was set: BROKEN (FAILED after
+        MAX_JOB_RETRIES attempts), to be re-run (server.lua:194-205)."""
+        for k in bad_chunks:
+            a, b = self._chunks[self.tslot][k]
+            if all(recs[j].status == STATUS.FAILED for j in range(a, b)):
+                continue
+            for j in range(a, b):
+                recs[j].repetitions += 1
+                recs[j].status = STATUS.BROKEN
+                if recs[j].repetitions >= utils.MAX_JOB_RETRIES:
+                    recs[j].status = STATUS.FAILED
+            sys.stderr.write("# map chunk of jobs %s..%s reported a device-side failure (attempt %d)\n" % (
+                jobs[a][0], jobs[b - 1][0], recs[a].repetitions))
+
+    def _reduce_insert_bound(self, rbuf, recv_counts, rows: int) -> int:
+        """Received records -> the reduce table WITHOUT reading its key count:
+        the table is sized from the previous iteration's distinct keys (or the
+        received rows), and the returned row bound — at most the received
+        rows — launches the padded tail, which flags a table that overflowed
+        or outgrew the bound (TailBoundError: _retry_tail)."""
+        guess = getattr(self, "_red_distinct", None)
+        want = 2 * (guess + guess // 4) if guess is not None else 2 * rows
+        cap = ops.next_pow2(max(1 << 16, min(2 * rows, want)))
+        if self.red_table is None or self.red_table.cap != cap:
+            self.red_table = ops.HashTable(cap, device=self.device, op=self.op)
+        else:
+            self.red_table.reset()
+        self.red_table.insert_received(rbuf, recv_counts, self.world, rows=rows)
+        if guess is None:
+            return max(rows, 1)
+        b = guess + guess // 4 + 4096
+        return max(1, min(rows, (b + 0xFFFF) & ~0xFFFF))
 
     def _reduce_insert_received(self, rbuf, recv_counts, rows: int) -> int:
         """Received records -> this rank's reduce table (one insert launch);
@@ -824,13 +945,20 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                 gate = torch.cuda.Event()
                 gate.record()
             issue_next_map(gate)
-        trace.push("mr.map.wait")
-        if self._restored_src is not None:
-            n_claimed, overflow = self.table.stats()
-        else:
-            n_claimed, overflow = self._map_sync(jobs, recs, j0, j1)  # synchronises the map phase
-            self._save_map(n_claimed, overflow, recs, j0, j1)
-        trace.pop()
+        fused = self._fused_tail_ok()
+        # the shuffle runs at W > 1, or at W = 1 with MR_FORCE_SHUFFLE (the
+        # RCCL data path exercised on a single GPU: pack -> count exchange ->
+        # all_to_all_single -> receive-side insert)
+        sh = self.world > 1 or self.force_shuffle
+        single = self._single_sync_ok(sh, fused)
+        if not single:
+            trace.push("mr.map.wait")
+            if self._restored_src is not None:
+                n_claimed, overflow = self.table.stats()
+            else:
+                n_claimed, overflow = self._map_sync(jobs, recs, j0, j1)  # synchronises the map phase
+                self._save_map(n_claimed, overflow, recs, j0, j1)
+            trace.pop()
         self._maybe_inject_fault("shuffle")
         T["map"] = time.time() - t0
         timer = self._timer()
@@ -841,12 +969,24 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
         self._failed_total = failed
         pend = None
-        fused = self._fused_tail_ok()
-        # the shuffle runs at W > 1, or at W = 1 with MR_FORCE_SHUFFLE (the
-        # RCCL data path exercised on a single GPU: pack -> count exchange ->
-        # all_to_all_single -> receive-side insert)
-        sh = self.world > 1 or self.force_shuffle
-        if not sh and fused:
+        padded = False
+        if single:
+            # two host waits per iteration: the count exchange (with the map's
+            # checks) and the result download
+            trace.push("mr.shuffle_reduce")
+            src, rcounts, rows, n_claimed = self._exchange_single_sync(jobs, recs, j0, j1, issue_next_map)
+            T["map"] = time.time() - t0
+            if getattr(self, "_exact_tail", False):
+                n_red = self._reduce_insert_received(src, rcounts, rows)
+            else:
+                n_red = self._reduce_insert_bound(src, rcounts, rows)
+                padded = True
+            if timer is not None:
+                timer.mark("shuffle_end")
+            with trace.range("mr.tail_issue"):
+                pend = self._finalize_table(self.red_table, n_red, src, padded=padded)
+            trace.pop()
+        elif not sh and fused:
             pend = self._finalize_table(self.table, n_claimed, src)
             issue_next_map()
         elif sh and fused:
@@ -858,7 +998,7 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         else:
             hi, lo, val, rep = self.table.compact((n_claimed, overflow))
             part = devmod.partition_of(hi, lo, rep, src, self.nparts, self.partmod)
-        if sh:
+        if sh and not single:
             trace.push("mr.shuffle_reduce")
             if fused:
                 src, rcounts, rows = self._shuffle(hi, lo, val, rep, src, part, failed, raw=True,
@@ -884,20 +1024,36 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         issue_next_map()
 
         with trace.range("mr.finalize_host"):
-            try:
-                cols = devmod.finalize_host(pend, self.partmod)
-            except devmod.BlobCapacityError as e:
-                # keys that overlap in the input (n-gram spans) need more key
-                # bytes than the input holds: redo the tail with room for them
-                # (remembered for the next iterations)
-                self._blob_cap = e.nbytes + e.nbytes // 8
-                if unfused:
-                    pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part,
-                                                  blob_cap=self._blob_cap)
-                else:
-                    pend = self._finalize_table(self.red_table if sh else self.table,
-                                                n_red if sh else n_claimed, src)
-                cols = devmod.finalize_host(pend, self.partmod)
+            for attempt in range(4):
+                try:
+                    cols = devmod.finalize_host(pend, self.partmod)
+                    break
+                except devmod.TailBoundError as e:
+                    # the padded tail's bound was too small or its table
+                    # overflowed (reduce_insert_bound guessed from the last
+                    # iteration): refill with the synchronised sizing and re-run
+                    # the tail with the count
+                    if e.overflow:
+                        self._red_distinct = None
+                    n_red = self._reduce_insert_received(src, rcounts, rows) if e.overflow else \
+                        self.red_table.stats()[0]
+                    padded = False
+                    pend = self._finalize_table(self.red_table, n_red, src)
+                except devmod.BlobCapacityError as e:
+                    # keys that overlap in the input (n-gram spans) need more key
+                    # bytes than the input holds: redo the tail with room for them
+                    # (remembered for the next iterations)
+                    if attempt == 3:
+                        raise
+                    self._blob_cap = e.nbytes + e.nbytes // 8
+                    if unfused:
+                        pend = devmod.finalize_device(hi, lo, val, rep, src, self.nparts, self.partmod, part=part,
+                                                      blob_cap=self._blob_cap)
+                    else:
+                        pend = self._finalize_table(self.red_table if sh else self.table,
+                                                    n_red if sh else n_claimed, src, padded=padded)
+        if padded:
+            self._red_distinct = int(cols["val"].size)
         if cols.get("exact_fallback"):
             self._exact_tail = True  # later iterations go straight to the exact order
         digits = len(str(max(self.nparts - 1, 0)))

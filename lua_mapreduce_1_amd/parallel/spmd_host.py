@@ -27,10 +27,8 @@ import sys
 import time
 import traceback
 
-import torch.distributed as tdist
-
 from .. import utils
-from ..runtime import modules
+from ..runtime import codec, modules
 from ..utils import STATUS
 from ..utils.tuple import tuple as tuple_
 from . import dist as D
@@ -142,24 +140,8 @@ class HostSPMDEngine(SPMDEngine):
             r.cpu_time, r.real_time = time.process_time() - c0, r.written - r.started
             res.map_jobs.append(r)
         t_map = time.time()
-        # shuffle: partition p -> rank p % W (one object all-to-all)
         if self.world > 1:
-            send = [dict() for _ in range(self.world)]
-            for p, kv in local.items():
-                send[p % self.world][p] = kv
-            recv = [None] * self.world
-            for src in range(self.world):  # scatter from every rank in turn (gloo and RCCL both)
-                out = [None]
-                tdist.scatter_object_list(out, send if self.rank == src else None, src=src, group=self.group)
-                recv[src] = out[0]
-            mine: dict = {}
-            for piece in recv:  # rank order = job order: values stay in job order
-                for p, kv in piece.items():
-                    dst = mine.setdefault(p, {})
-                    for k, v in kv.items():
-                        dst.setdefault(k, []).extend(v)
-            local = mine
-            failed = D.all_reduce_sum_int(failed, self.device)
+            local, failed = self._shuffle_host(local, failed)
         t_shuf = time.time()
         red = modules.field(self.redmod, "reducefn")
         aci = all(bool(modules.field(self.redmod, f)) for f in
@@ -206,6 +188,33 @@ class HostSPMDEngine(SPMDEngine):
         t_end = time.time()
         T.update(map=t_map - t_start, shuffle=t_shuf - t_map, reduce=t_end - t_shuf, iteration=t_end - t_start)
         return res
+
+    def _shuffle_host(self, local: dict, failed: int):
+        """Partition p -> rank p % W.  Each destination's partitions are
+        serialised once (data-only MRK1 records, runtime/codec.py, with the
+        failed-map count riding along) and exchanged by ONE byte all-to-all
+        (the reference moves map_results.P<p>.M<m> files through GridFS / scp
+        / a shared FS, fs.lua:141-181).  Returns (this rank's partitions,
+        job-wide failed maps)."""
+        send = [[(-1, [failed])] for _ in range(self.world)]
+        for p, kv in local.items():
+            send[p % self.world].append((p, list(kv.items())))
+        recv = D.all_to_all_bytes([codec.encode_records(r) for r in send], self.device, self.group)
+        mine: dict = {}
+        failed = 0
+        for piece in recv:  # rank order = job order: values stay in job order
+            for p, kv in codec.decode_records(piece):
+                if p < 0:
+                    failed += int(kv[0])
+                    continue
+                dst = mine.setdefault(p, {})
+                for k, v in kv:  # (msgpack arrays come back as tuples: hashable, equal by value)
+                    lst = dst.get(k)
+                    if lst is None:
+                        dst[k] = list(v)
+                    else:
+                        lst.extend(v)
+        return mine, failed
 
     @staticmethod
     def _reduce_partition(kv: dict, red, aci: bool) -> list:

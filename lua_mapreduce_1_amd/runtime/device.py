@@ -344,6 +344,16 @@ def finalize(hi, lo, val, rep, src, nparts: int, partition_module=None, part: to
         return finalize_host(pend, partition_module, need_keys)
 
 
+class TailBoundError(RuntimeError):
+    """A padded tail (finalize_table_native(padded=True)) was launched for
+    fewer rows than its table holds, or its table overflowed: re-run it with
+    the table's count (``overflow``: grow and refill the table first)."""
+
+    def __init__(self, overflow: bool):
+        super().__init__("reduce table overflowed" if overflow else "reduce tail row bound too small")
+        self.overflow = overflow
+
+
 class BlobCapacityError(RuntimeError):
     """The key bytes of a result exceed the blob capacity the tail was given
     (keys that overlap in their source, e.g. n-gram spans, can need more
@@ -434,11 +444,16 @@ def _tail_ws(d, n: int, nparts: int, blob_cap: int, cap: int):
 _CP_WS: dict = {}
 
 
-def compact_partition(table, n: int, src, nparts: int):
+def compact_partition(table, n: int, src, nparts: int, bound: bool = False):
     """Occupied slots of a table -> dense (hi, lo, val, rep) + exact FNV-1
     partition (int32), in ONE kernel (tail_compact; its composite sort key and
     digit histograms are by-products).  The send side of the shuffle; buffers
-    are reused across iterations (valid until the next call)."""
+    are reused across iterations (valid until the next call).
+
+    ``bound=True``: ``n`` is a bound on the rows, not their count (which is
+    then never read on the host before the shuffle): rows past it are
+    dropped, and the count comes back as a sixth value, a device int64[1]
+    (it exceeds ``n`` when rows were dropped)."""
     from ..ops import _hip
     d = table.device
     ws = _CP_WS.get(d)
@@ -456,11 +471,14 @@ def compact_partition(table, n: int, src, nparts: int):
     hi, lo, val, rep, c = (cols[i, :n] for i in range(5))
     _hip.call("mr_tail_compact", *table._gtab(), table.cap, nparts, _hip.ptr(src), _hip.ptr(hi), _hip.ptr(lo),
               _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), _hip.ptr(c), _hip.ptr(small[:1]),
-              None, None, _hip.ptr(ws["bhist"]), n, _hip.stream(d))  # no digit histograms on the send side
+              None, None, _hip.ptr(ws["bhist"]), n, n, 0, None, _hip.stream(d))  # no digit histograms here
+    if bound:
+        return hi, lo, val, rep, part[:n], small[:1]
     return hi, lo, val, rep, part[:n]
 
 
-def finalize_table_native(table, n: int, src, nparts: int, blob_cap: int | None = None) -> dict:
+def finalize_table_native(table, n: int, src, nparts: int, blob_cap: int | None = None,
+                          padded: bool = False) -> dict:
     """Fused device tail straight from an HBM hash table, every launch and
     download queued by ONE native call (mr_tail_run, csrc/hip/tail.hip):
     compact + FNV partition + composite key + digit histograms in one kernel,
@@ -468,7 +486,13 @@ def finalize_table_native(table, n: int, src, nparts: int, blob_cap: int | None 
     yields key lengths, the exact-order tie fix-up, key bytes, and ONE packed
     download of values/offsets/partition counts (+ the key-byte DMA).  ``n``
     = occupied slots (table.stats()).  Requires nparts <= 256; returns the
-    pending state for finalize_host."""
+    pending state for finalize_host.
+
+    ``padded=True``: ``n`` is a BOUND on the occupied slots (nparts <= 255),
+    so nothing is read before the tail is queued: the rows past the count are
+    sentinels sorted last, finalize_host takes the count from the partition
+    counts, and raises :class:`TailBoundError` if the bound was too small or
+    the table overflowed (the caller re-runs with the count)."""
     from ..ops import _hip
     d = table.device
     cap = max(src.numel(), blob_cap or 0)
@@ -484,9 +508,9 @@ def finalize_table_native(table, n: int, src, nparts: int, blob_cap: int | None 
         hb = _POOL.get("blob", max(1 << 20, 16 * n), torch.uint8)
         est_arg = -1
     _hip.call("mr_tail_run", *table._gtab(), table.cap, n, nparts, _hip.ptr(src), _hip.ptr(ws), cap, _hip.ptr(hp),
-              _hip.ptr(hb), est_arg, hb.numel(), _hip.stream(d))
+              _hip.ptr(hb), est_arg, hb.numel(), 1 if padded else 0, _hip.stream(d))
     return {"n": n, "nparts": nparts, "args": v["args"], "src": src, "presorted": False, "hi": v["hi"], "lo": v["lo"],
-            "fused": True, "hp": hp, "off": v["off"], "blob": v["blob"], "est": est, "hb": hb}
+            "fused": True, "hp": hp, "off": v["off"], "blob": v["blob"], "est": est, "hb": hb, "padded": padded}
 
 
 def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=None,
@@ -586,6 +610,15 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
         hb, est, blob = pend["hb"], pend["est"], pend["blob"]
         if pend.get("fused"):
             f_val, f_off, f_counts, f_bad = _unpack_fused(pend)
+            if pend.get("padded"):
+                if f_bad & 24:
+                    raise TailBoundError(bool(f_bad & 16))
+                # the real rows: their count from the partition counts (the
+                # sentinel rows past it sort last and have empty keys)
+                n = int(f_counts.sum())
+                f_val, f_off = f_val[:n], f_off[:n + 1]
+                hi, lo = hi[:n], lo[:n]
+                pend = dict(pend, n=n, args=tuple(a[:n] for a in pend["args"]))
             nbytes = int(f_off[n]) if n else 0
         else:
             ho = pend["ho"]

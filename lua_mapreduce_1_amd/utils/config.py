@@ -60,29 +60,18 @@ class Tunables:
     sort_rounds: int = _knob("MR_SORT_ROUNDS", 24,
                              "keys per thread of the onesweep radix tiles of sorts of >= 4 M keys (256 x rounds "
                              "keys per tile; 16, 24 or 32)")
-    wc_map_config: int = _knob("MR_WC_MAP_CONFIG", 0,
-                               "word-count map kernel shape (csrc/hip/wordcount3.hip): 0 = 512 threads, 2048 LDS "
-                               "slots, 8 KiB spans, two workgroups per CU; 1 / 2 = 4096 slots over 32 / 64 KiB, one "
-                               "workgroup per CU; 3 = 1024 threads, 4096 slots, 32 KiB")
-    agg_direct: bool = _knob("MR_AGG_DIRECT", False,
-                             "byte-span / encoded-key inserts (fold and general planes): one row per thread straight "
-                             "into the HBM table, no LDS combine (for key sets with few repeats per block)")
     csv_tiles: int = _knob("MR_CSV_TILES", 0,
                            "fused CSV fold (emit.csv): 8 KiB tiles per workgroup (0 = auto: up to 4 while the "
                            "launch keeps >= 1024 workgroups)")
     csv_mode: int = _knob("MR_CSV_MODE", 0,
                           "fused CSV fold ablation: 0 = normal, 1 = parse only (no insert: wrong results), 2 = no "
                           "LDS combine")
+    agg_insert_grid: int = _knob("MR_AGG_INSERT_GRID", 65536,
+                                 "general plane: workgroup cap of the per-row table insert (>= 256; one row per "
+                                 "thread up to 16 M rows, profiles/r4/agg_grid_ab)")
     rec_gather_rows: int = _knob("MR_REC_GATHER_ROWS", 256,
                                  "record plane: rows per workgroup batch of the 16-byte row gather (256, or 128: "
                                  "half the LDS image, more workgroups per CU)")
-    agg_sort_min: int = _knob("MR_AGG_SORT_MIN", 0,
-                              "general plane, typed folds on the GPU: byte-span batches of at least this many rows "
-                              "are pre-combined by a hash sort + segmented folds before the table insert (0 = "
-                              "never; smaller batches hash every row into the table with an LDS combine)")
-    rec_scatter: bool = _knob("MR_REC_SCATTER", False,
-                              "record plane: apply a full row permutation as a scatter through its inverse "
-                              "(coalesced row reads) instead of the gather (random row reads)")
     arena_cap_mb: float = _knob("MR_ARENA_CAP_MB", 0.0,
                                 "SPMD: cap of a rank's HBM input arena, MiB (0 = the rank's whole input); a larger "
                                 "input is mapped in rounds through a ring of two arenas of this size")
@@ -96,6 +85,10 @@ class Tunables:
                                  "a rank's partitions are ordered and reduced in rounds of at most this many key "
                                  "and value bytes, each round's result moved to host memory")
     fused_tail: bool = _knob("MR_FUSED_TAIL", True, "fused reduce-side tail kernels (tail.hip)")
+    single_sync: bool = _knob("MR_SINGLE_SYNC", True,
+                              "SPMD fold plane at W > 1: the map's checks ride on the count exchange and the reduce "
+                              "tail is launched for a row bound, so an iteration waits on the device twice (count "
+                              "exchange, result download) instead of four times")
     pipeline: bool = _knob("MR_PIPELINE", True, "bench/proxies: map of iteration i+1 overlaps the tail of i")
     prefetch_single: bool = _knob("MR_PREFETCH_SINGLE", True, "prefetched inputs: one DMA per iteration")
     spin_us: float = _knob("MR_SPIN_US", 2000.0, "host spin on completion words before hipStreamSynchronize, us")

@@ -170,3 +170,20 @@ def test_lists_of_postings_drops_unlisted():
     off, val = RD.lists_of_postings(slot, pslot, pval, 3, 16)
     assert off.tolist() == [0, 2, 5, 6]
     assert val.tolist() == [12, 17, 10, 14, 18, 13]
+
+
+def test_combine_trigger_backs_off_cpu():
+    """A combiner that cannot bring the table under the threshold (many
+    distinct keys, up to 3 values kept per key) must not run on every emit
+    call after the first combine: the trigger moves to twice the postings
+    left, so the combines stay logarithmic in the rows."""
+    import math
+    splits = make_data("text")
+    eng, res, got = run_engine(CM, splits, torch.device("cpu"), {"mode": "topk"}, combine_postings=64)
+    assert close_lists(got, _oracle(splits, "topk"))
+    mp = eng.plane.map
+    rows = max(mp.rows, 1)
+    assert mp.table.npost > 64  # the combined table stays above the threshold
+    assert 1 <= mp.combines <= 2 * math.ceil(math.log2(rows / 64)) + 2, (mp.combines, rows)
+    # one emit call per split: the old trigger combined after every one of them
+    assert mp.combines < len(splits) - 2, (mp.combines, len(splits))

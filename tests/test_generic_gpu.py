@@ -118,19 +118,14 @@ def test_text_parse_gpu_matches_python(gpu):
     assert torch.equal(hi, di)
 
 
-@pytest.mark.parametrize("sort", [False, True], ids=["rows", "sorted"])
 @pytest.mark.parametrize("skew", [False, True], ids=["uniform", "zipf"])
 @pytest.mark.parametrize("dtype", ["i64", "f64", "f32"])
-def test_agg_table_folds_gpu(gpu, dtype, skew, sort, monkeypatch):
+def test_agg_table_folds_gpu(gpu, dtype, skew):
     """Typed sum/min/max folds of random (key, value) rows against numpy:
     uniform keys (the LDS combine fills up, most rows fold straight into the
-    HBM table) and Zipf keys (hot keys combined in LDS) — through the per-row
-    insert and through the sort-based pre-combine (MR_AGG_SORT_MIN), with
-    long keys and empty spans mixed in."""
-    import dataclasses
+    HBM table) and Zipf keys (hot keys combined in LDS), with long keys and
+    empty spans mixed in."""
     from lua_mapreduce_1_amd.ops import agg as A
-    from lua_mapreduce_1_amd.ops import keys as K
-    monkeypatch.setattr(A, "TUNABLES", dataclasses.replace(A.TUNABLES, agg_sort_min=1 if sort else 0))
     rng = np.random.default_rng(3)
     n, nk = 200_000, 5000
     words = [("k%d" % i).encode() * (1 + i % 3) for i in range(nk)]  # some long keys
@@ -163,16 +158,6 @@ def test_agg_table_folds_gpu(gpu, dtype, skew, sort, monkeypatch):
         else:
             tol = 1e-9 if dtype == "f64" else 1e-3
             assert math.isclose(s0, s1, rel_tol=tol, abs_tol=tol) and a[k][1:] == b[k][1:]
-
-
-def test_scores_sorted_precombine_gpu(gpu, monkeypatch):
-    """The CSV group-by job with every span batch pre-combined by the sort."""
-    import dataclasses
-    from lua_mapreduce_1_amd.ops import agg as A
-    monkeypatch.setattr(A, "TUNABLES", dataclasses.replace(A.TUNABLES, agg_sort_min=1))
-    splits = make_data("scores")
-    eng, res, got = run_engine(SS, splits, gpu, {})
-    assert close_lists(got, oracle("scores", None, splits))
 
 
 @pytest.mark.parametrize("which,mod,args", CASES, ids=["scores", "bigram", "max_host", "docs", "docs_concat",

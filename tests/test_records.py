@@ -273,13 +273,13 @@ def test_records_restart_restores_rows_gpu(gpu, tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("rb", [100, 64, 24, 244, 8])
-def test_row_scatter_equals_gather_gpu(gpu, rb):
-    """The scatter form of a full row permutation (MR_REC_SCATTER) moves the
-    same bytes as the gather."""
+def test_row_gathers_equal_gpu(gpu, rb):
+    """The 16-byte LDS-staged row gather and the dword gather move the same
+    bytes as a host gather of a full row permutation."""
     from lua_mapreduce_1_amd.ops import records as RC
     n = 100_003
     g = torch.Generator().manual_seed(rb)
     rec = torch.randint(0, 256, (n, rb), dtype=torch.uint8, generator=g).to(gpu)
     perm = torch.randperm(n, generator=g).to(torch.int32).to(gpu)
-    assert torch.equal(RC.gather(rec, perm, mode=3), RC.gather(rec, perm, mode=0))
-    assert torch.equal(RC.gather(rec, perm, mode=3).cpu(), rec.cpu()[perm.cpu().long()])
+    assert torch.equal(RC.gather(rec, perm, mode=1), RC.gather(rec, perm, mode=0))
+    assert torch.equal(RC.gather(rec, perm, mode=0).cpu(), rec.cpu()[perm.cpu().long()])

@@ -133,3 +133,69 @@ def test_spmd_forced_shuffle_rccl_one_gpu(pipelined):
     nccl backend, device buffers) on the single GPU of the box: a one-rank
     nccl group with the W>1 path forced, checked against the naive count."""
     _run(1, on_gpu=True, backend="nccl", force_shuffle=True, pipelined=pipelined)
+
+
+def _single_sync_worker(port, q, mode):
+    """One-rank nccl group, W>1 path forced, pipelined iterations: host waits
+    per iteration and every iteration's result against the naive count."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    if mode == "device_error":
+        os.environ["MR_SPMD_DEVICE_FAULT"] = "3:1"  # the chunk of job 3 fails once (device error word)
+    import datetime
+    import torch
+    import torch.distributed as dist
+    from lua_mapreduce_1_amd.ops import _hip
+    from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore
+    from lua_mapreduce_1_amd.runtime import codec
+    from lua_mapreduce_1_amd.utils.corpus import europarl_like
+    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}",
+                            timeout=datetime.timedelta(seconds=120), device_id=torch.device("cuda", 0))
+    splits = europarl_like(seed=9, lines=12_000, words=200_000, vocab_size=8_000, split_lines=1000)
+    naive = {}
+    for s in splits:
+        for w in s.split():
+            naive[w.decode()] = naive.get(w.decode(), 0) + 1
+    store = SplitStore(splits, pin=True)
+    eng = SPMDEngine(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M,
+                          init_args={"nsplits": len(splits), "num_reducers": 7}, force_shuffle=True),
+                     split_store=store, device=torch.device("cuda", 0),
+                     table_capacity=1024 if mode == "map_overflow" else 1 << 20)
+    eng.prefetch = eng.pipeline = True
+    waits, ok = [], []
+    n_it = 6
+    for i in range(n_it):
+        if i == 3 and mode == "send_bound":
+            eng._send_est = 100      # the compaction's bound is too small: flagged, exchange redone
+        if i == 3 and mode == "red_bound":
+            eng._red_distinct = 100  # the padded tail's bound is too small: TailBoundError, tail re-run
+        w0 = _hip.WAITS[0]
+        res = eng.run_iteration(prefetch_next=i < n_it - 1, lookahead=2)
+        got = {}
+        for _n, cols in eng.gather_results(res):
+            for k, v in codec.iter_columnar(cols):
+                got[k] = got.get(k, 0) + v[0]
+        waits.append(_hip.WAITS[0] - w0)
+        ok.append(got == naive)
+    q.put((ok, waits, eng._single_sync_ok(True, True)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["steady", "send_bound", "red_bound", "map_overflow", "device_error"])
+def test_single_sync_iteration_rccl_one_gpu(mode):
+    """a W>1 fold-plane iteration waits on the device twice
+    (count exchange with the map's checks; result download), every result
+    exact; the redo paths (send bound, reduce bound, map overflow, device
+    error word) stay exact and only add waits to the iteration they hit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_single_sync_worker, args=(_free_port(), q, mode))
+    p.start()
+    p.join(300)
+    assert p.exitcode == 0
+    ok, waits, single = q.get(timeout=5)
+    assert single and all(ok), (ok, waits)
+    steady = [w for i, w in enumerate(waits) if i >= 1 and not (mode != "steady" and i == 3)]
+    if mode in ("map_overflow", "device_error"):
+        steady = waits[4:]
+    assert max(steady) <= 2, waits

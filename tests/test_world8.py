@@ -129,7 +129,19 @@ def _generic_rounds(R, device):
     return res, lambda: close_lists(got, comb_modules.oracle(splits, "topk"))
 
 
-PLANES = {"fold": _fold, "list": _list, "records": _records, "generic": _generic, "generic_cols": _generic_cols,
+def _host(R, device):
+    """The host plane (plain mapfn, no device_mapfn): the reference's tuple
+    keys and values through the SPMD engine's host shuffle."""
+    from lua_mapreduce_1_amd import spmd
+    import host_modules as H
+    M = "host_modules"
+    eng = spmd(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, finalfn=M, init_args={"num_reducers": R}),
+               device=device)
+    res = eng.run()
+    return res, lambda: H.RESULT == H.naive(H._SPLITS)
+
+
+PLANES = {"host": _host, "fold": _fold, "list": _list, "records": _records, "generic": _generic, "generic_cols": _generic_cols,
           "list_rounds": _list_rounds, "generic_rounds": _generic_rounds}
 
 

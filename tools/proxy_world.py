@@ -71,6 +71,19 @@ def main() -> int:
         t_hot = time.perf_counter() + float(os.environ["MR_HOT_CPU"]) * 1e-3
         while time.perf_counter() < t_hot:
             pass
+    copy_ev = []
+    if os.environ.get("MR_COPY_TIMELINE"):
+        # diagnosis: timing events around every iteration's input copies on
+        # the copy stream -> copy durations and the copy engine's idle gaps
+        orig = eng._issue_copies
+
+        def issue(plan, wait_for=None):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(eng.copy_stream)
+            orig(plan, wait_for)
+            e1.record(eng.copy_stream)
+            copy_ev.append((e0, e1, time.perf_counter()))
+        eng._issue_copies = issue
     per = []
     prof = None
     if os.environ.get("MR_CPROFILE"):
@@ -115,6 +128,16 @@ def main() -> int:
             print(f"-- host timeline of timed iteration {k} ({1e6 * (b - a):.1f} us)", file=sys.stderr)
             for name, s0, s1 in sorted((e for e in trace.LOG if a <= e[1] <= b), key=lambda e: e[1]):
                 print(f"   {1e6 * (s0 - a):8.1f} +{1e6 * (s1 - s0):7.1f}  {name}", file=sys.stderr)
+    if copy_ev:
+        c = copy_ev[-30:]
+        dur = [round(a.elapsed_time(b), 3) for a, b, _ in c]
+        gap = [round(c[i][1].elapsed_time(c[i + 1][0]), 3) for i in range(len(c) - 1)]
+        per_it = [round(c[i][0].elapsed_time(c[i + 1][0]), 3) for i in range(len(c) - 1)]
+        print(f"copies (last {len(c)}): duration ms {dur}", file=sys.stderr)
+        print(f"copy engine idle gap ms {gap}", file=sys.stderr)
+        print(f"copy start-to-start ms {per_it}", file=sys.stderr)
+        print(f"host issue spacing ms {[round(1e3 * (c[i + 1][2] - c[i][2]), 3) for i in range(len(c) - 1)]}",
+              file=sys.stderr)
     seq = [round(x, 2) for x in per]
     per.sort()
     print(json.dumps({"world": W, "ms_per_step": ms, "median": per[len(per) // 2], "min": per[0], "seq": seq,
