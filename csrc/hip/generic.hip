@@ -35,11 +35,11 @@ constexpr int MAXC = 8;
 // Column descriptors, passed by value (kernel argument).
 struct Cols {
   int k;                       // value columns
-  int list;                    // 1: append (slot, value of column 0) postings instead of folding
+  int list;                    // 1: append (slot, value row of the k columns) postings instead of folding
   const void* src[MAXC];       // per-row input values (null for a scalar)
   int stype[MAXC];             // VType of src (VT_SCALAR: the constant sbits, in the dst type)
   long long sbits[MAXC];
-  void* dst[MAXC];             // per-slot columns (fold) — or, list mode, dst[0] = posting values
+  void* dst[MAXC];             // per-slot columns (fold) — or, list mode, dst[0] = posting value rows [n][k]
   int dtype[MAXC];             // VT_I64 / VT_F64 / VT_F32
   int op[MAXC];                // OP_SUM / OP_MIN / OP_MAX
   long long* post_slot;        // list mode: posting slot ids (sink)
@@ -172,9 +172,12 @@ __global__ void __launch_bounds__(256) agg_insert_kernel(GTab g, Keys ks, u64 n,
       claims += r == 2;
     }
     if (c.list) {
+      // a posting = the key's slot + a value row of k 8-byte words (int64 /
+      // float64 bits; byte-string values are span words of the byte source)
       c.post_slot[c.post_base + i] = r ? (long long)slot : -1;
-      ((long long*)c.dst[0])[c.post_base + i] =
-          c.dtype[0] == VT_F64 ? __double_as_longlong(rd_f64(c, 0, i)) : rd_i64(c, 0, i);
+      long long* row = (long long*)c.dst[0] + (c.post_base + i) * (u64)c.k;
+      for (int j = 0; j < c.k; ++j)
+        row[j] = c.dtype[j] == VT_F64 ? __double_as_longlong(rd_f64(c, j, i)) : rd_i64(c, j, i);
     } else if (r) {
       for (int j = 0; j < c.k; ++j) fold_col(c, j, i, slot);
     }
@@ -812,7 +815,7 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
                   const void* lens, u64 rep_base, u64 n, const void* cols, hipStream_t stream) {
   if (n == 0) return 0;
   const ColsArg* a = (const ColsArg*)cols;
-  if (a->k < 0 || a->k > MAXC || (a->list && a->k != 1)) return -1;
+  if (a->k < 0 || a->k > MAXC || (a->list && a->k < 1)) return -1;
   Keys ks;
   ks.hi = (const u64*)hi;
   ks.lo = (const u64*)lo;

@@ -424,7 +424,7 @@ __global__ void key_word_kernel(const u64* __restrict__ hi, const u64* __restric
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const u64 l = lo[i];
     u64 w = 0;
-    if (k == 0) {
+    if (k == 0 && hi != nullptr) {
       w = hi[i];
     } else if (!key_is_long(l)) {
       w = k == 1 ? (l & ~0xFFull) : 0ull;

@@ -71,7 +71,9 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
             print(" ".join(cmd))
         _run(cmd)
     tmp = HIP_LIB + ".tmp"
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
+    # libhsa-runtime64: the ROCr copy API of the SDMA downloads (csrc/hip/sdma.hip)
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs +
+         ["-L/opt/rocm/lib", "-lhsa-runtime64"])
     os.replace(tmp, HIP_LIB)
     return HIP_LIB
 

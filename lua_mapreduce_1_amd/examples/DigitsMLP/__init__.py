@@ -1,10 +1,18 @@
 """Iterative MapReduce training of the digits MLP — the reference's APRIL-ANN
 example (/root/reference/mapreduce/examples/APRIL-ANN/{init,common,server,
-worker}.lua) in the server/worker form.  One module provides every function
-(pass it as taskfn, mapfn, partitionfn, reducefn and finalfn).
+worker}.lua).  One module provides every function (pass it as taskfn, mapfn,
+partitionfn, reducefn and finalfn), in two execution forms:
 
-``init_args = [connection_string, data, max_epochs?]`` where ``data`` is a
-digits.png-shaped file or ``"synthetic"``.
+* server/worker — ``init_args = [connection_string, data, max_epochs?]``
+  (``data``: a digits.png-shaped file or ``"synthetic"``): the reference's
+  shape, described below;
+* SPMD on the device data plane — ``init_args = {"data": ..., "max_epochs":
+  ...}`` through ``execute_spmd.py`` / ``lua_mapreduce_1_amd.spmd``: the map
+  jobs' gradients are emitted as fp32 tensors per weight name into the
+  tensor plane (``device_reduce = "tensor_sum"``, parallel/tensor_plane.py),
+  reduced by ONE RCCL reduce-scatter by weight-name partition and one
+  all-gather, and ``device_finalfn`` steps the replicated model on every rank
+  — no gradient bytes through the host (``HISTORY`` keeps the epochs).
 
 * ``init``: opens the persistent table ``conf`` and, if there is no model (or the
   previous run finished), creates one and checkpoints it to the coordinator's
@@ -46,6 +54,12 @@ conf = None
 _data_cache: dict = {}
 _trainer = None
 _trainer_version = None
+# SPMD form: replicated per rank (trainer, epoch, stopping rule, history)
+SPMD = False
+HISTORY: list = []
+_spmd: dict = {}
+device_reduce = "tensor_sum"   # the SPMD tensor plane; a server/worker run takes the host mapfn
+spmd_replicated_taskfn = True
 
 
 def _device():
@@ -91,7 +105,16 @@ def _dataset(value):
 
 
 def init(arg):
-    global CONN, DATA, MAX_EPOCHS, conf
+    global CONN, DATA, MAX_EPOCHS, conf, SPMD, HISTORY
+    if isinstance(arg, dict):
+        # SPMD form: every rank holds the (identical) model; nothing shared
+        SPMD = True
+        DATA = arg.get("data", DATA) or "synthetic"
+        MAX_EPOCHS = int(arg["max_epochs"]) if arg.get("max_epochs") else None
+        HISTORY = []
+        _spmd.clear()
+        return
+    SPMD = False
     arg = list(arg or [])
     if arg:
         CONN = arg[0]
@@ -116,9 +139,59 @@ def init(arg):
 
 
 def taskfn(emit):
-    conf.update()
+    if not SPMD:
+        conf.update()
     for j in range(1, T.HYPER["jobs_per_iteration"] + 1):
         emit(j, DATA)
+
+
+# -- SPMD form: the tensor plane ------------------------------------------------------
+def device_tensor_layout() -> dict:
+    """Keys and sizes of the tensor plane: one fp32 gradient per weight name
+    and [loss, correct, count] under TR_LOSS (common.lua:95-103)."""
+    lay = {name: getattr(M.LAYOUT, name).stop - getattr(M.LAYOUT, name).start for name in M.WEIGHT_NAMES}
+    lay[TR_LOSS_KEY] = 3
+    return lay
+
+
+def _spmd_trainer(device) -> T.DigitsTrainer:
+    tr = _spmd.get("trainer")
+    if tr is None:
+        hyper = {"max_epochs": MAX_EPOCHS} if MAX_EPOCHS else None
+        tr = _spmd["trainer"] = T.DigitsTrainer(device, _dataset(DATA), hyper)
+        _spmd["epoch"] = 0
+    return tr
+
+
+def device_mapfn(key, value, emit):
+    """The gradient of map job ``key``'s bunch (the fused MFMA kernel on a
+    GPU) into the tensor plane, per weight name (common.lua:85-104)."""
+    tr = _spmd_trainer(emit.device)
+    tr.compute_gradients(tr.bunch_indices(_spmd["epoch"] + 1, [key]))
+    for name in M.WEIGHT_NAMES:
+        emit.tensor(name, tr.grads[getattr(M.LAYOUT, name)])
+    emit.tensor(TR_LOSS_KEY, tr.buf[-3:])
+
+
+def device_finalfn(res, engine):
+    """Every rank: the summed gradients (res.tensors, device) -> 1/sqrt(N)
+    smoothing + SGD step, validation, stopping rule (common.lua:144-202);
+    the same on every rank, so the replicated model stays identical."""
+    tr = _spmd_trainer(engine.device)
+    grads = tr.grads  # (free after the map: the flat gradient the SGD kernel reads)
+    for name in M.WEIGHT_NAMES:
+        grads[getattr(M.LAYOUT, name)].copy_(res.tensors[name])
+    loss, correct, count = res.tensors[TR_LOSS_KEY].tolist()  # 3 floats: the stopping rule's input
+    tr.apply(grads, count)
+    va_loss, va_acc = tr.validate()
+    tr_loss = loss / max(count, 1.0)
+    go = tr.stop.update(tr_loss, va_loss)
+    _spmd["epoch"] += 1
+    HISTORY.append({"epoch": _spmd["epoch"], "tr_loss": tr_loss, "va_loss": va_loss, "va_acc": va_acc,
+                    "tr_acc": correct / max(count, 1.0)})
+    if engine.rank == 0 and engine.verbose:
+        print(tr.stop.state_string(), flush=True)
+    return "loop" if go else True
 
 
 def mapfn(key, value, emit):

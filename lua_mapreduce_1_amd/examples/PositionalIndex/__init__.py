@@ -1,0 +1,112 @@
+"""Positional inverted index as a MapReduce job: word -> sorted distinct
+(line, position) pairs — a tuple value per posting.
+
+The reference wraps every emitted value in ``tuple(value)``
+(/root/reference/mapreduce/job.lua:84) and serialises tables into its
+intermediate files (utils.lua:100-120); a positional index emits a
+(document, position) table per word.  Here the map module declares its value
+row, ``device_value_dtype = ("i64", "i64")``, and the device map emits both
+columns as tensors (parallel/values.py); the postings are grouped, shuffled
+and sorted per key on the device (``device_reduce = "concat_unique"``: sorted
+by (line, position), duplicates dropped).
+
+* ``taskfn``: one map job per split (``device_input = "split"``);
+* map: every whitespace token -> (word, (global line, index of the token in
+  its line)); device form through ``ops/text.py`` tokens + the plane's global
+  line numbering, host form over the split's text;
+* partition: exact FNV-1 of the word mod R;
+* reduce: the sorted distinct (line, position) pairs (also the combiner).
+"""
+from __future__ import annotations
+
+import torch
+
+NUM_REDUCERS = 10
+NSPLITS = 8
+SPLITS: list = []   # host form: the split texts (init {"splits": [...]})
+RESULT: dict = {}
+device_input = "split"
+spmd_replicated_taskfn = True
+device_value_dtype = ("i64", "i64")
+device_reduce = "concat_unique"
+device_partition = ("fnv1", NUM_REDUCERS)
+
+
+def init(args):
+    global NUM_REDUCERS, NSPLITS, SPLITS, device_partition
+    args = args or {}
+    NUM_REDUCERS = int(args.get("num_reducers", NUM_REDUCERS))
+    SPLITS = list(args.get("splits") or [])
+    NSPLITS = int(args.get("nsplits", len(SPLITS) or NSPLITS))
+    device_partition = ("fnv1", NUM_REDUCERS)
+
+
+def taskfn(emit):
+    for i in range(NSPLITS):
+        emit(i + 1, {"split": i})
+
+
+def token_positions(line: torch.Tensor) -> torch.Tensor:
+    """Index of every token inside its line, for tokens in text order with
+    their (non-decreasing) line numbers."""
+    idx = torch.arange(line.numel(), dtype=torch.int64, device=line.device)
+    return idx - torch.searchsorted(line, line)
+
+
+def device_mapfn(keys, data, emit):
+    from lua_mapreduce_1_amd.ops import text as TX
+    st, ln, line = TX.tokens(data, lines=True)
+    pos = token_positions(line)
+    if emit.line_base is None:
+        raise RuntimeError("PositionalIndex needs the SPMD engine's global line numbering (split inputs)")
+    emit.spans(st, ln, line + emit.line_base(data), pos)
+
+
+def mapfn(key, value, emit):
+    """Host form: the split's text from init {"splits": [...]} and the global
+    number of its first line (job value {"split": i, "line0": L})."""
+    s = SPLITS[value["split"]]
+    if s[-1:] != b"\n":
+        s += b"\n"
+    for n, text in enumerate(s.split(b"\n")):
+        for p, w in enumerate(text.split()):
+            emit(w.decode("utf-8", "surrogateescape"), (value.get("line0", 0) + n, p))
+
+
+def partitionfn(key):
+    h = 2166136261
+    for c in key.encode("utf-8", "surrogateescape"):
+        h = ((h * 16777619) & 0xFFFFFFFF) ^ c
+    return h % NUM_REDUCERS
+
+
+def reducefn(key, values, emit):
+    for v in sorted(set(tuple(v) for v in values)):
+        emit(v)
+
+
+combinerfn = reducefn
+associative_reducer = True
+commutative_reducer = True
+idempotent_reducer = True
+
+
+def finalfn(pairs):
+    global RESULT
+    RESULT = {k: [tuple(v) for v in vs] for k, vs in pairs}
+    return True
+
+
+def naive(splits: list[bytes]) -> dict:
+    """Oracle: word -> sorted distinct (global line, position in line)."""
+    out: dict = {}
+    line = 0
+    for s in splits:
+        if s[-1:] != b"\n":
+            s = s + b"\n"
+        pieces = s.split(b"\n")
+        for n, text in enumerate(pieces):
+            for p, w in enumerate(text.split()):
+                out.setdefault(w.decode("utf-8", "surrogateescape"), set()).add((line + n, p))
+        line += len(pieces) - 1
+    return {k: sorted(v) for k, v in out.items()}

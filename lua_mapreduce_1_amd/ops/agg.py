@@ -185,11 +185,15 @@ class AggTable:
     values of ``list_dtype``).  ``src``: the byte source every rep word
     indexes (set by the owner before inserting long keys)."""
 
-    def __init__(self, capacity: int, device, cols: list | None = None, list_dtype: str = "i64"):
+    def __init__(self, capacity: int, device, cols: list | None = None, list_dtype="i64"):
+        from ..parallel.values import spec_of
         self.device = torch.device(device)
         self.cols_spec = cols
         self.list_mode = cols is None
-        self.list_dtype = list_dtype
+        # list mode: a posting's value row (parallel/values.py: numbers,
+        # tuples, byte-string span words); list_dtype the legacy scalar name
+        self.vspec = spec_of(list_dtype)
+        self.list_dtype = self.vspec.dtype
         self.src: torch.Tensor | None = None
         self.cap = next_pow2(max(1024, int(capacity)))
         self.cstride = 1  # slot stride of the value columns (one array per column)
@@ -224,8 +228,16 @@ class AggTable:
     def _values(self, values, n: int) -> list:
         """Per physical column (src tensor | None, scalar bits)."""
         if self.list_mode:
-            v = values[0] if values else 1
-            return [(v, self.list_dtype)]
+            sp = self.vspec
+            if len(values) > sp.width:
+                raise ValueError(f"{len(values)} value columns emitted, the value lists hold {sp}")
+            out = []
+            for j, dt in enumerate(sp.cols):
+                if j >= len(values) and dt == "bytes":
+                    raise ValueError(f"value column {j} ({sp}) is a byte string: emit it (ByteSpans)")
+                # byte columns arrive as int64 span words (GenericEmitter)
+                out.append((values[j] if j < len(values) else 1, "i64" if dt == "bytes" else dt))
+            return out
         out = []
         for dt, _op, i in self.cols_spec:
             v = 1 if i is None else values[i]
@@ -234,12 +246,13 @@ class AggTable:
 
     def _grow_posts(self, need: int) -> None:
         if self.post_slot is None or self.post_slot.numel() < need:
+            k = self.vspec.width
             cap = max(need, 2 * (self.post_slot.numel() if self.post_slot is not None else 0), 1 << 16)
             ns = torch.empty(cap, dtype=torch.int64, device=self.device)
-            nv = torch.empty(cap, dtype=torch.int64, device=self.device)
+            nv = torch.empty(cap * k, dtype=torch.int64, device=self.device)  # value rows [cap][k]
             if self.post_slot is not None and self.npost:
                 ns[:self.npost].copy_(self.post_slot[:self.npost])
-                nv[:self.npost].copy_(self.post_val[:self.npost])
+                nv[:self.npost * k].copy_(self.post_val[:self.npost * k])
             self.post_slot, self.post_val = ns, nv
 
     def insert(self, n: int, values, hi=None, lo=None, rep=None, rep_add: int = 0, text=None, starts=None,
@@ -461,13 +474,16 @@ class AggTable:
         if self.is_cuda:
             slot, hi, lo, rep, _ = self.compact()
             n = self.npost
+            sp = self.vspec
             if n == 0:
                 z = torch.zeros(0, dtype=torch.int64, device=self.device)
-                return slot, hi, lo, rep, z, z.clone()
-            return slot, hi, lo, rep, self.post_slot[:n], self.post_val[:n]
+                return slot, hi, lo, rep, z, sp.storage(z.clone())
+            return slot, hi, lo, rep, self.post_slot[:n], sp.storage(self.post_val[:n * sp.width])
         h, lw, r, inv, cols = self._cpu_ids()
-        vals = cols[0] if cols else np.zeros(0, np.int64)
-        if vals.dtype == np.float64:
-            vals = vals.view(np.int64)
+        sp = self.vspec
+        bits = [c.view(np.int64) if c.dtype == np.float64 else c.astype(np.int64, copy=False) for c in cols or []]
+        if not bits:
+            bits = [np.zeros(0, np.int64)] * sp.width
+        vals = bits[0] if sp.scalar else np.stack(bits, 1)
         return (torch.arange(h.size, dtype=torch.int64), _t64(h), _t64(lw), _t64(r), torch.from_numpy(inv),
-                torch.from_numpy(vals.astype(np.int64, copy=False)))
+                torch.from_numpy(np.ascontiguousarray(vals)))

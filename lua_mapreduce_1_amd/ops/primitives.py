@@ -747,10 +747,14 @@ EXACT_MAX_WORDS = 32  # keys up to 256 bytes get the device's exact order
 def key_word(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.Tensor | None,
              k: int) -> torch.Tensor:
     """Bytes [8k, 8k+8) of every key as a big-endian int64 word, zero padded
-    past the key's end (so unsigned word order is byte order)."""
-    n = hi.numel()
-    if hi.is_cuda:
-        d = hi.device
+    past the key's end (so unsigned word order is byte order).  ``hi`` None:
+    word 0 of long keys read from their bytes too (spans with no key words,
+    e.g. byte-string values)."""
+    n = lo.numel()
+    if hi is None and not lo.is_cuda:
+        hi = torch.zeros_like(lo)
+    if lo.is_cuda:
+        d = lo.device
         w = torch.empty(n, dtype=torch.int64, device=d)
         if n:
             _hip.call("mr_key_word", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), _hip.ptr(src), n, k, _hip.ptr(w),

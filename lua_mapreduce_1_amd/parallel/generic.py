@@ -26,8 +26,8 @@ What happens to them is the reduce module's ``device_reduce``:
   (native f64/f32/i64 atomics); the result of a key is the list of its
   output columns, like a reducefn that emits several values;
 * ``"concat"`` / ``"concat_unique"`` — the key's values in emission order /
-  sorted and distinct (int64, or float64 with ``device_value_dtype = "f64"``
-  on the map module);
+  sorted and distinct (int64, float64, a k-tuple of numbers or a byte string,
+  as the map module's ``device_value_dtype`` declares: parallel/values.py);
 * absent — the values are grouped on the device (list, emission order) and
   the module's own ``reducefn(key, values, emit)`` runs on the host for each
   key of the rank's partitions (the reduce job), skipping singleton lists
@@ -53,6 +53,7 @@ import torch
 from .. import ops, utils
 from ..ops import agg as A
 from ..ops import keys as K
+from ..ops import primitives as P
 from ..ops import segments as S
 from ..ops import text as TX
 from ..runtime import codec
@@ -63,6 +64,7 @@ from ..utils import trace
 from ..utils.config import TUNABLES
 from . import dist as D
 from . import reducers as RD
+from . import values as VL
 
 
 def _bits(n: int) -> int:
@@ -186,6 +188,12 @@ class GenericEmitter:
         t, base = self.m.src.locate(self._text(text))
         self.m.insert(int(starts.numel()), values, text=t, starts=starts, lens=lens, rep_base=base)
 
+    def bytes(self, starts, lens, text=None) -> VL.ByteSpans:
+        """A byte-string value column for ``spans`` / ``pairs``: value i =
+        ``text[starts[i] : starts[i] + lens[i]]`` (default ``text``: the
+        chunk being mapped); needs ``device_value_dtype`` "bytes" there."""
+        return VL.ByteSpans(starts, lens, self._text(text) if text is not None else None)
+
     def pairs(self, hi, lo, *values, rep=None, src=None) -> None:
         add = 0
         if src is not None:
@@ -243,12 +251,13 @@ class GenericMap:
     """Map-side state of the general plane: the key -> columns / postings
     table, the byte source of its rep words and the emitter."""
 
-    def __init__(self, device, capacity: int, phys: A.Physical | None, list_dtype: str = "i64",
+    def __init__(self, device, capacity: int, phys: A.Physical | None, list_dtype="i64",
                  reducers: "RD.ListReducers | None" = None, combine_at: int = 0):
         self.device = torch.device(device)
         self.phys = phys
-        self.list_dtype = list_dtype
-        self.table = A.AggTable(capacity, self.device, phys.cols if phys is not None else None, list_dtype)
+        self.vspec = VL.spec_of(list_dtype)  # list mode: the value row of a posting
+        self.list_dtype = self.vspec.dtype
+        self.table = A.AggTable(capacity, self.device, phys.cols if phys is not None else None, self.vspec)
         self.src = KeySource(self.device)
         self.emit = GenericEmitter(self)
         self.host: list = []
@@ -268,7 +277,28 @@ class GenericMap:
 
     @property
     def n_in(self) -> int:
-        return self.phys.n_in if self.phys is not None else 1
+        return self.phys.n_in if self.phys is not None else self.vspec.width
+
+    def _byte_words(self, v):
+        """An emitted ByteSpans value column -> span words into the key
+        source (the value text located there like key text)."""
+        if not isinstance(v, VL.ByteSpans):
+            return v
+        if self.phys is not None:
+            raise TypeError("byte-string values go to value lists (no device_reduce, or concat): a typed fold "
+                            "folds numbers")
+        text = v.text if v.text is not None else self.emit._text(None)
+        _, base = self.src.locate(text)
+        return VL.span_words(v.starts.to(self.device), v.lens.to(self.device), base)
+
+    def add_bytes(self, data) -> int:
+        """Append bytes (a uint8 tensor or bytes) to the key source; returns
+        their offset (byte-string values made by a combiner or host emits)."""
+        if not isinstance(data, torch.Tensor):
+            data = torch.frombuffer(bytearray(data), dtype=torch.uint8) if len(data) else \
+                torch.zeros(0, dtype=torch.uint8)
+        off, _ = self.src.add(data.to(self.device))
+        return off
 
     def begin(self, arena=None) -> None:
         self.table.reset()
@@ -284,6 +314,8 @@ class GenericMap:
             raise ValueError(f"{len(values)} value columns emitted, the reduce expects {self.n_in}")
         if self.phys is not None and not values:
             values = (1,) * self.n_in
+        if self.vspec.has_bytes:
+            values = tuple(self._byte_words(v) for v in values)
         self.table.src = self.src.source()
         self.table.insert(n, list(values), **kw)
         self.rows += n
@@ -335,17 +367,24 @@ class GenericMap:
         space = t.cap if t.is_cuda else max(1, m)
         src = self.src.source()
         off, val = RD.lists_of_postings(slot, pslot, pval, m, space)
-        noff, nval = self.reducers.combine(RD.KeyBatch(hi, lo, rep, src), off, val)
-        nt = A.AggTable(t.cap, self.device, None, self.list_dtype)
-        nt.src = src
-        n = int(nval.numel())
+        noff, nval = self.reducers.combine(RD.KeyBatch(hi, lo, rep, src), off, val, src=src,
+                                           add_bytes=self.add_bytes)
+        nt = A.AggTable(t.cap, self.device, None, self.vspec)
+        nt.src = self.src.source()  # (a combiner may have appended byte values)
+        n = int(noff[-1]) if noff.numel() else 0
         if n:
             kid = S.ids(noff, n)
-            v = nval.view(torch.float64) if self.list_dtype == "f64" else nval
-            nt.insert(n, [v], hi=hi[kid], lo=lo[kid], rep=rep[kid])
+            nt.insert(n, self._value_cols(nval), hi=hi[kid], lo=lo[kid], rep=rep[kid])
         self.table = nt
         self.combines += 1
         return True
+
+    def _value_cols(self, bits: torch.Tensor) -> list:
+        """Stored value bits [n] / [n, k] -> the insert's value columns
+        (float64 tensors for f64 columns: the kernel converts by type)."""
+        rows = self.vspec.rows(bits)
+        return [rows[:, j].contiguous().view(torch.float64) if dt == "f64" else rows[:, j].contiguous()
+                for j, dt in enumerate(self.vspec.cols)]
 
     def flush_host(self) -> None:
         if not self.host:
@@ -361,6 +400,14 @@ class GenericMap:
             reps.append(K.make_rep(base + off, len(k)))
             off += len(k)
         t64 = lambda a: torch.from_numpy(np.array(a, dtype=np.uint64).view(np.int64)).to(self.device)  # noqa: E731
+        if self.phys is None and not self.vspec.scalar:
+            # tuples / byte strings: one value row per pair (strings appended
+            # to the key source as span words)
+            vals = [v if len(v) != 1 else v[0] for _, v in pairs]
+            bits = VL.host_bits(vals, self.vspec, self.add_bytes, "emit")
+            cols = self._value_cols(torch.from_numpy(bits).to(self.device))
+            self.insert(len(pairs), tuple(cols), hi=t64(his), lo=t64(los), rep=t64(reps))
+            return
         k_in = max(len(v) for _, v in pairs) if self.phys is None else self.n_in
         cols = []
         for j in range(k_in):
@@ -413,11 +460,16 @@ def _key_order(part, hi, lo, rep, src, nparts: int):
     return ops.sort_keys_checked([part.to(torch.int64), hi, lo], bits=[max(8, _bits(nparts)), 64, 64]).long(), False
 
 
-def order_lists(slot, hi, lo, rep, pslot, pval, src, nparts: int, partmod, unique: bool, dtype: str,
-                slot_space: int) -> dict:
+def order_lists(slot, hi, lo, rep, pslot, pval, src, nparts: int, partmod, unique: bool, dtype,
+                slot_space: int, vsrc=None) -> dict:
     """Keys in (partition, key) order with their value lists (emission order,
     or sorted distinct with ``unique``): {hi, lo, key_off, key_blob,
-    list_off, list_val, counts}."""
+    list_off, list_val, counts} — or, for tuple / byte-string values
+    (parallel/values.py), ``list_cols`` (one typed tensor per number column,
+    a ByteValues per byte column, in posting order) instead of ``list_val``.
+    ``vsrc``: the byte source of byte-string values (default ``src``)."""
+    spec = VL.spec_of(dtype)
+    vsrc = src if vsrc is None else vsrc
     m = hi.numel()
     d = hi.device
     part = devmod.partition_of(hi, lo, rep, src, nparts, partmod) if m else torch.zeros(0, dtype=torch.int32, device=d)
@@ -433,11 +485,7 @@ def order_lists(slot, hi, lo, rep, pslot, pval, src, nparts: int, partmod, uniqu
     pr, pv = pr[keep], pval[keep]
     if pr.numel():
         if unique:
-            pp = ops.sort_keys_checked([pr, _value_order_key(pv, dtype)], bits=[_bits(m), 64]).long()
-            pr, pv = pr[pp], pv[pp]
-            first = torch.ones(pr.numel(), dtype=torch.bool, device=d)
-            first[1:] = (pr[1:] != pr[:-1]) | (pv[1:] != pv[:-1])
-            pr, pv = pr[first], pv[first]
+            pr, pv = _unique_values(pr, pv, spec, m, vsrc)
         else:
             pp = ops.sort_keys_checked([pr], bits=[_bits(m)]).long()  # stable: emission order per key
             pr, pv = pr[pp], pv[pp]
@@ -448,8 +496,62 @@ def order_lists(slot, hi, lo, rep, pslot, pval, src, nparts: int, partmod, uniqu
     _, klen = ops.key_meta(hi, lo, rep, src, want_part=False)
     koff, kblob = ops.gather_key_bytes(hi, lo, rep, src, lengths=klen)
     counts = ops.bincount(part, nparts) if m else torch.zeros(nparts, dtype=torch.int64, device=d)
-    return {"hi": hi, "lo": lo, "key_off": koff, "key_blob": kblob, "list_off": loff, "list_val": pv,
-            "counts": counts, "exact": exact}
+    out = {"hi": hi, "lo": lo, "key_off": koff, "key_blob": kblob, "list_off": loff, "counts": counts,
+           "exact": exact}
+    if spec.scalar:
+        out["list_val"] = pv
+    else:
+        out["list_cols"] = list(_user_cols(pv, spec, vsrc))
+    return out
+
+
+def _user_cols(bits, spec: VL.ValueSpec, vsrc):
+    """Stored value rows -> per column: a typed tensor, or ByteValues."""
+    rows = spec.rows(bits)
+    for j, dt in enumerate(spec.cols):
+        col = rows[:, j].contiguous()
+        yield VL.byte_values(col, vsrc) if dt == "bytes" else (col.view(torch.float64) if dt == "f64" else col)
+
+
+def _unique_values(pr, pv, spec: VL.ValueSpec, m: int, vsrc):
+    """Postings sorted by (key, value) with duplicates of a key's value
+    dropped: numbers (scalars or tuples) in numeric order, one byte-string
+    column in exact byte order (ops.exact_key_perm over the value bytes)."""
+    d = pr.device
+    if spec.scalar:
+        pp = ops.sort_keys_checked([pr, _value_order_key(pv, spec.cols[0])], bits=[_bits(m), 64]).long()
+        pr, pv = pr[pp], pv[pp]
+        first = torch.ones(pr.numel(), dtype=torch.bool, device=d)
+        first[1:] = (pr[1:] != pr[:-1]) | (pv[1:] != pv[:-1])
+        return pr[first], pv[first]
+    rows = spec.rows(pv)
+    if spec.has_bytes:
+        if spec.width != 1:
+            raise ValueError("concat_unique: byte-string values are compared alone (device_value_dtype 'bytes'), "
+                             "not inside tuples")
+        w = rows[:, 0].contiguous()
+        n = w.numel()
+        z = torch.zeros(n, dtype=torch.int64, device=d)
+        mark = torch.full((n,), 0xFF, dtype=torch.int64, device=d)
+        vh = P.key_word(None, mark, w, vsrc, 0)  # the value's first 8 bytes (the key encoding's hi)
+        pp = ops.exact_key_perm(pr, vh, mark, w, vsrc, max(m, 1))
+        if pp is None:
+            raise ValueError("concat_unique: a byte-string value is longer than the exact sort handles")
+        pr, w, vh = pr[pp], w[pp], vh[pp]
+        ln = VL.word_lengths(w)
+        same = (pr[1:] == pr[:-1]) & (ln[1:] == ln[:-1]) & (vh[1:] == vh[:-1])
+        for k in range(1, (int(ln.max()) + 7) // 8 if n else 0):
+            wk = P.key_word(z, mark, w, vsrc, k)
+            same &= wk[1:] == wk[:-1]
+        first = torch.ones(n, dtype=torch.bool, device=d)
+        first[1:] = ~same
+        return pr[first], spec.storage(w[first].reshape(-1, 1))
+    words = VL.order_words(rows, spec)
+    pp = ops.sort_keys_checked([pr] + words, bits=[_bits(m)] + [64] * len(words)).long()
+    pr, rows = pr[pp], rows[pp]
+    first = torch.ones(pr.numel(), dtype=torch.bool, device=d)
+    first[1:] = (pr[1:] != pr[:-1]) | (rows[1:] != rows[:-1]).any(1)
+    return pr[first], spec.storage(rows[first])
 
 
 def _np64(t):
@@ -460,7 +562,52 @@ def _np_cols(out: dict) -> list:
     return [_np64(c) for c in out.get("cols", [])]
 
 
-def host_partitions(out: dict, nparts: int, dtype: str = "i64", reducefn=None, aci: bool = False) -> dict:
+def _host_list_cols(out: dict) -> list:
+    """``list_cols`` on the host: numpy arrays, (off, blob) per byte column."""
+    cols = []
+    for c in out["list_cols"]:
+        if isinstance(c, (VL.ByteValues, tuple)) and not isinstance(c, torch.Tensor):
+            cols.append((_np64(c[0]).astype(np.int64), _np64(c[1])))
+        else:
+            cols.append(_np64(c))
+    return cols
+
+
+def _take_cols(cols: list, idx: np.ndarray) -> list:
+    """Postings ``idx`` of host list columns (byte columns re-packed)."""
+    out = []
+    for c in cols:
+        if isinstance(c, tuple):
+            off, blob = c
+            lens = off[idx + 1] - off[idx]
+            noff = np.zeros(idx.size + 1, np.int64)
+            np.cumsum(lens, out=noff[1:])
+            if idx.size and np.all(np.diff(idx) == 1):
+                nb = blob[off[idx[0]]:off[idx[-1] + 1]]
+            else:
+                b = blob.tobytes()
+                nb = np.frombuffer(b"".join(b[off[i]:off[i + 1]] for i in idx), np.uint8)
+            out.append((noff, nb))
+        else:
+            out.append(c[idx])
+    return out
+
+
+def host_values(cols: list) -> list:
+    """Host list columns -> one Python value per posting: a number or a str
+    (one column), or a tuple of them."""
+    py = []
+    for c in cols:
+        if isinstance(c, tuple):
+            off, blob = c
+            b = blob.tobytes()
+            py.append([codec.key_str(b[off[i]:off[i + 1]]) for i in range(off.size - 1)])
+        else:
+            py.append(c.tolist())
+    return py[0] if len(py) == 1 else list(zip(*py))
+
+
+def host_partitions(out: dict, nparts: int, dtype="i64", reducefn=None, aci: bool = False) -> dict:
     """Device result of :func:`order_fold` / :func:`order_lists` -> per
     partition host columns (exact bytewise key order inside a partition),
     with ``reducefn`` applied per key to list results (the host reduce)."""
@@ -473,11 +620,15 @@ def host_partitions(out: dict, nparts: int, dtype: str = "i64", reducefn=None, a
     np.cumsum(counts, out=bounds[1:])
     cols = [_np64(c) for c in out.get("cols", [])]
     is_list = "list_off" in out
+    lcols = None
     if is_list:
         loff = _np64(out["list_off"]).astype(np.int64)
-        lval = _np64(out["list_val"])
-        if dtype == "f64" and not out.get("list_typed"):
-            lval = lval.view(np.float64)
+        if "list_cols" in out:  # tuple / byte-string values (parallel/values.py)
+            lcols = _host_list_cols(out)
+        else:
+            lval = _np64(out["list_val"])
+            if VL.spec_of(dtype).dtype == "f64" and not out.get("list_typed"):
+                lval = lval.view(np.float64)
     parts = {}
     kb = kblob.tobytes()
     exact = bool(out.get("exact", False))
@@ -500,13 +651,22 @@ def host_partitions(out: dict, nparts: int, dtype: str = "i64", reducefn=None, a
             ln = loff[idx + 1] - loff[idx]
             l_off = np.zeros(idx.size + 1, np.int64)
             np.cumsum(ln, out=l_off[1:])
-            if fix is None:
-                l_val = lval[loff[a]:loff[b]]
+            if lcols is not None:
+                pidx = np.arange(loff[a], loff[b]) if fix is None else (
+                    np.concatenate([np.arange(loff[i], loff[i + 1]) for i in idx]) if idx.size else
+                    np.zeros(0, np.int64))
+                l_cols = _take_cols(lcols, pidx)
+                part.update(list_off=l_off, list_cols=l_cols, val=ln)
+                if reducefn is not None:
+                    part["py_vals"] = _host_reduce(reducefn, aci, k_off, k_blob, l_off, None, host_values(l_cols))
             else:
-                l_val = np.concatenate([lval[loff[i]:loff[i + 1]] for i in idx]) if idx.size else lval[:0]
-            part.update(list_off=l_off, list_val=l_val, val=ln)
-            if reducefn is not None:
-                part["py_vals"] = _host_reduce(reducefn, aci, k_off, k_blob, l_off, l_val)
+                if fix is None:
+                    l_val = lval[loff[a]:loff[b]]
+                else:
+                    l_val = np.concatenate([lval[loff[i]:loff[i + 1]] for i in idx]) if idx.size else lval[:0]
+                part.update(list_off=l_off, list_val=l_val, val=ln)
+                if reducefn is not None:
+                    part["py_vals"] = _host_reduce(reducefn, aci, k_off, k_blob, l_off, l_val)
         else:
             part["cols"] = [c[idx] for c in cols]
             part["val"] = part["cols"][0]
@@ -514,12 +674,13 @@ def host_partitions(out: dict, nparts: int, dtype: str = "i64", reducefn=None, a
     return parts
 
 
-def _host_reduce(reducefn, aci: bool, k_off, k_blob, l_off, l_val) -> list:
+def _host_reduce(reducefn, aci: bool, k_off, k_blob, l_off, l_val, vals: list | None = None) -> list:
     """The last resort: the user's reducefn per key over downloaded lists
     (job.lua:264-284; singleton lists skip it under the three ACI flags).
     One host conversion of the partition's values and key bytes, then a
-    slice per key."""
-    vals = l_val.tolist()
+    slice per key (``vals``: the values already as Python objects)."""
+    if vals is None:
+        vals = l_val.tolist()
     kb = k_blob.tobytes()
     ko = k_off.tolist()
     lo = l_off.tolist()
@@ -547,9 +708,13 @@ class GenericPlane:
         self.host_reduce = op is None
         self.unique = op == "concat_unique"
         self.list_mode = op is None or op in LIST_OPS
-        self.dtype = str(modules.field(eng.mapmod, "device_value_dtype", "i64") or "i64")
-        if self.dtype not in ("i64", "f64"):
-            raise ValueError("device_value_dtype is 'i64' or 'f64'")
+        # the value row of a posting (parallel/values.py): a number, a tuple
+        # of numbers or byte strings
+        self.vspec = VL.spec_of(modules.field(eng.mapmod, "device_value_dtype", "i64") or "i64")
+        self.dtype = self.vspec if not self.vspec.scalar else self.vspec.dtype
+        if not self.list_mode and not self.vspec.scalar:
+            raise ValueError(f"device_value_dtype {self.vspec}: tuple and byte-string values go to value lists "
+                             "(no device_reduce, 'concat' or 'concat_unique'), not to typed folds")
         self.phys = None if self.list_mode else A.Physical(A.parse_spec(op))
         self._cap = self._cap0 = int(eng.params.get("table_capacity") or 1 << 16)
         red = eng.redmod
@@ -779,6 +944,9 @@ class GenericPlane:
             kidx = pos[pslot.clamp(min=0)]
             keep = (pslot >= 0) & (kidx >= 0)
             arrs["pkey"], arrs["pval"] = kidx[keep], pval[keep]
+            if self.vspec.has_bytes:  # byte-string values: their bytes too (row-major over the byte columns)
+                arrs["vb_off"], arrs["vb_blob"] = VL.gather_bytes(
+                    self.vspec.rows(arrs["pval"])[:, self.vspec.bytes_cols], src)
         else:
             for j, c in enumerate(cols):
                 arrs[f"col{j}"] = c
@@ -814,13 +982,20 @@ class GenericPlane:
         mp.src.begin(blob)
         cap = ops.next_pow2(max(1 << 12, 4 * m, self._cap))
         if self.list_mode:
-            mp.table = A.AggTable(cap, d, None, self.dtype)
-            mp.table.src = blob
+            mp.table = A.AggTable(cap, d, None, self.vspec)
             kidx = t(a["pkey"])
             pv = t(a["pval"].view(np.int64))
-            if self.dtype == "f64":
-                pv = pv.view(torch.float64)
-            mp.table.insert(int(kidx.numel()), [pv], hi=hi[kidx], lo=lo[kidx], rep=rep[kidx])
+            if self.vspec.has_bytes:
+                # the saved value bytes appended to the key source; the span
+                # words re-pointed at them
+                base = mp.add_bytes(t(a["vb_blob"]))
+                rows = self.vspec.rows(pv).clone()
+                voff = t(a["vb_off"][:-1].astype(np.int64)).reshape(-1, len(self.vspec.bytes_cols))
+                rows[:, self.vspec.bytes_cols] = VL.span_words(
+                    voff, VL.word_lengths(rows[:, self.vspec.bytes_cols]), base)
+                pv = self.vspec.storage(rows)
+            mp.table.src = mp.src.source()
+            mp.table.insert(int(kidx.numel()), mp._value_cols(pv), hi=hi[kidx], lo=lo[kidx], rep=rep[kidx])
         else:
             # the saved physical columns are folded 1:1 (the receive side's merge spec)
             merge = [(dt, op, j) for j, (dt, op, _i) in enumerate(self.phys.cols)]
@@ -864,20 +1039,28 @@ class GenericPlane:
             nv = torch.bincount(pr, minlength=m)[:m] if m else torch.zeros(0, dtype=torch.int64, device=d)
             payload = [nv]
             extra = pv
+            if self.vspec.has_bytes:
+                # byte-string values: their bytes follow the postings (row-
+                # major over the byte columns) in one more all-to-all
+                bw = self.vspec.rows(pv)[:, self.vspec.bytes_cols]
+                vb_off, vb_blob = VL.gather_bytes(bw, src)
+                vlen = VL.word_lengths(bw).sum(1)
         else:
             cols = [c[kperm] for c in keys[4]]
             payload = [c.view(torch.int64) if c.dtype == torch.float64 else
                        (c.view(torch.int32).to(torch.int64) if c.dtype == torch.float32 else c) for c in cols]
             nv = None
             extra = None
-        cnt = torch.zeros(W, 4, dtype=torch.int64, device=d)
+        cnt = torch.zeros(W, 5, dtype=torch.int64, device=d)
         if m:
             cnt[:, 0].index_add_(0, dest, torch.ones_like(dest))
             cnt[:, 1].index_add_(0, dest, klen.to(torch.int64))
             if nv is not None:
                 cnt[:, 2].index_add_(0, dest, nv)
+            if extra is not None and self.vspec.has_bytes and pr.numel():
+                cnt[:, 4].index_add_(0, dest[pr], vlen)
         cnt[:, 3] = failed
-        recv = D.exchange_counts(cnt.view(-1).contiguous(), eng.group).view(W, 4)
+        recv = D.exchange_counts(cnt.view(-1).contiguous(), eng.group).view(W, 5)
         both = torch.cat([cnt, recv]).cpu().tolist()  # one host sync for every split size
         send_c, recv_c = both[:W], both[W:]
         failed_total = sum(r[3] for r in recv_c)
@@ -887,9 +1070,19 @@ class GenericPlane:
         nbytes = sum(c[1] for c in send_c)
         rblob = D.all_to_all_v(kblob[:nbytes], [c[1] for c in send_c], [c[1] for c in recv_c], eng.group)
         rextra = None
+        self._rvsrc = None
         if extra is not None:
             rextra = D.all_to_all_v(extra, [c[2] for c in send_c], [c[2] for c in recv_c], eng.group)
-        sent = [32 * c[0] + c[1] + 8 * c[2] for c in send_c]
+            if self.vspec.has_bytes:
+                nvb = sum(c[4] for c in send_c)
+                rvb = D.all_to_all_v(vb_blob[:nvb], [c[4] for c in send_c], [c[4] for c in recv_c], eng.group)
+                # received span words index the sender's source: re-point
+                # them at the received value bytes (same row-major order)
+                rows = self.vspec.rows(rextra).clone()
+                rows[:, self.vspec.bytes_cols] = VL.words_of_lengths(VL.word_lengths(rows[:, self.vspec.bytes_cols]))
+                rextra = self.vspec.storage(rows)
+                self._rvsrc = rvb if rvb.numel() else torch.zeros(1, dtype=torch.uint8, device=d)
+        sent = [32 * c[0] + c[1] + 8 * self.vspec.width * c[2] + c[4] for c in send_c]
         self._nvals_shipped = sum(c[2] for c in send_c) if self.list_mode else sum(c[0] for c in send_c)
         self._shuffled = (sum(sent), sum(sent) - sent[eng.rank])
         rhi, rlo, rlen = rrecs[:, 0].contiguous(), rrecs[:, 1].contiguous(), rrecs[:, 2].contiguous()
@@ -934,16 +1127,16 @@ class GenericPlane:
         if self.list_mode:
             slot, hi, lo, rep, kslot, _ = rt.postings()
             nv = rpay[0]
-            pslot = torch.repeat_interleave(kslot, nv, output_size=int(rextra.numel()))
+            pslot = torch.repeat_interleave(kslot, nv, output_size=int(rextra.shape[0]))
             return (slot, hi, lo, rep, pslot, rextra), (rt.cap if rt.is_cuda else max(1, m))
         slot, hi, lo, rep, cols = rt.compact((m, False))
         return (slot, hi, lo, rep, cols), None
 
     # -- order + reduce (one round, or the rank's partitions in rounds) ---------------
-    def _order(self, keys: tuple, src, space):
+    def _order(self, keys: tuple, src, space, vsrc=None):
         eng = self.eng
         if self.list_mode:
-            return order_lists(*keys, src, eng.nparts, eng.partmod, self.unique, self.dtype, space)
+            return order_lists(*keys, src, eng.nparts, eng.partmod, self.unique, self.vspec, space, vsrc=vsrc)
         return order_fold(*keys, src, eng.nparts, eng.partmod, self.phys)
 
     def _reduce(self, out: dict):
@@ -954,13 +1147,16 @@ class GenericPlane:
             # batched: device_reducefn over every key's list
             with trace.range("mr.gen.reduce"):
                 keys = RD.KeyBatch(out["hi"], out["lo"], key_off=out["key_off"], key_blob=out["key_blob"])
-                red = self.reducers.reduce_device(keys, out["list_off"], out["list_val"])
-            out = {k: v for k, v in out.items() if k not in ("list_off", "list_val")}
+                if "list_cols" in out:
+                    red = self.reducers.reduce_device_cols(keys, out["list_off"], out["list_cols"])
+                else:
+                    red = self.reducers.reduce_device(keys, out["list_off"], out["list_val"])
+            out = {k: v for k, v in out.items() if k not in ("list_off", "list_val", "list_cols")}
             out.update(red)
             return out, None
         if self.host_reduce:
             # the last resort: the user's reducefn per key on the host
-            return None, host_partitions(out, R, self.dtype, self.reducefn, self.aci)
+            return None, host_partitions(out, R, self.vspec, self.reducefn, self.aci)
         return out, None
 
     def _reduce_groups(self, keys: tuple, src, space):
@@ -1076,11 +1272,13 @@ class GenericPlane:
         self._shuffled = (0, 0)
         self._nvals_shipped = 0
         res.distinct_keys_map = int(keys[1].numel())
+        vsrc = src  # byte-string values: spans of the key source until the shuffle moves them
         if W > 1 or eng.force_shuffle:
             with trace.range("mr.gen.shuffle"):
                 rhi, rlo, rrep, rpay, rextra, rblob, failed = self._shuffle(keys, src, failed)
                 keys, space = self._merge_received(rhi, rlo, rrep, rpay, rextra, rblob)
                 src = rblob
+                vsrc = self._rvsrc if self._rvsrc is not None else rblob
         T["shuffle"] = time.time() - t1
         t2 = time.time()
         res.total_value = mp.rows
@@ -1099,11 +1297,11 @@ class GenericPlane:
             for grp in rounds:
                 sub, sub_space = self._select(keys, space, part, grp)
                 with trace.range("mr.gen.order"):
-                    out = self._order(sub, src, sub_space)
+                    out = self._order(sub, src, sub_space, vsrc)
                 counts = [a + b for a, b in zip(counts, out["counts"].cpu().tolist())]
                 nk += int(out["hi"].numel())
                 dev_out, got = self._reduce(out)
-                parts.update(got if got is not None else host_partitions(dev_out, R, self.dtype))
+                parts.update(got if got is not None else host_partitions(dev_out, R, self.vspec))
                 del out, dev_out, sub
             self.reduce_rounds = len(rounds)
             _result_jobs(eng, res, counts, t1)
@@ -1112,7 +1310,7 @@ class GenericPlane:
             res.distinct_keys = nk
         else:
             with trace.range("mr.gen.order"):
-                out = self._order(keys, src, space)
+                out = self._order(keys, src, space, vsrc)
                 issue_next_map()
                 counts = out["counts"].cpu().tolist()
             self.reduce_rounds = 1
@@ -1123,7 +1321,7 @@ class GenericPlane:
             if parts is not None:
                 res._parts = parts
             else:
-                res._materialize = lambda o=dev_out: host_partitions(o, R, self.dtype)
+                res._materialize = lambda o=dev_out: host_partitions(o, R, self.vspec)
         if self.host_reduce and not self.reducers.device_reduce:
             cpu = time.process_time() - c0
             parts = res._parts or {}

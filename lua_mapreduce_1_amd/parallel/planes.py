@@ -52,6 +52,9 @@ RECORD_OPS = ("identity",)
 
 
 def make_plane(eng):
+    if eng.plane_kind == "tensor":
+        from .tensor_plane import TensorPlane
+        return TensorPlane(eng)
     if eng.plane_kind == "generic":
         from .generic import GenericPlane
         return GenericPlane(eng)
@@ -191,6 +194,16 @@ class ListEmitter:
 
     def words(self, *a, **k):
         raise _UseGeneric()
+
+    def bytes(self, *a, **k):
+        raise _UseGeneric()
+
+    def csv(self, *a, **k):
+        raise _UseGeneric()
+
+    @property
+    def line_base(self):
+        raise _UseGeneric()  # (a map computing its own line numbers: the general plane has them)
 
     def __call__(self, *a, **k):
         raise _UseGeneric()

@@ -38,6 +38,7 @@ import torch
 from .. import ops
 from ..ops import segments as S
 from ..runtime import codec, modules
+from . import values as VL
 
 
 class ValueLists(NamedTuple):
@@ -89,8 +90,9 @@ class KeyBatch:
 def _take(v: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
     """v[perm] for 8-byte values (GPU: mr_gather_u64 with the sort's int32
     permutation; torch's index kernel was a quarter of the general reducer's
-    kernel time, profiles/r4/final_profiles/)."""
-    if not v.is_cuda or v.element_size() != 8:
+    kernel time, profiles/r4/final_profiles/).  Rows of tuple values ([n, k]):
+    v[perm] by rows."""
+    if not v.is_cuda or v.element_size() != 8 or v.dim() != 1:
         return v[perm.long()]
     from ..ops import _hip
     src = v.contiguous().view(torch.int64)
@@ -153,9 +155,12 @@ def splice(off, val, noff, nval, keep_old):
     seg = S.ids(roff, total)
     j = torch.arange(total, dtype=torch.int64, device=d) - roff[seg]
     old = keep_old[seg]
-    a = val[(off[seg] + j).clamp(max=max(val.numel() - 1, 0))] if val.numel() else torch.zeros_like(j)
-    b = nval[(noff[seg] + j).clamp(max=max(nval.numel() - 1, 0))] if nval.numel() else torch.zeros_like(j)
-    return roff, torch.where(old, a, b)
+    shape = (total,) + tuple(val.shape[1:])
+    a = val[(off[seg] + j).clamp(max=max(val.shape[0] - 1, 0))] if val.numel() else \
+        torch.zeros(shape, dtype=val.dtype, device=d)
+    b = nval[(noff[seg] + j).clamp(max=max(nval.shape[0] - 1, 0))] if nval.numel() else torch.zeros_like(a)
+    b = b.to(a.dtype)
+    return roff, torch.where(old.unsqueeze(1) if a.dim() == 2 else old, a, b)
 
 
 def _typed(bits: torch.Tensor, dtype: str) -> torch.Tensor:
@@ -213,11 +218,13 @@ def as_lists(out, m: int, who: str):
 # ---------------------------------------------------------------------------
 class ListReducers:
     """The combiner / reducer of a reduce module without ``device_reduce``,
-    for value lists of ``dtype`` (``"i64"`` | ``"f64"``)."""
+    for value lists of ``dtype`` (``"i64"`` | ``"f64"``, or a
+    parallel/values.py spec: tuples, byte strings)."""
 
-    def __init__(self, redmod, dtype: str = "i64"):
+    def __init__(self, redmod, dtype="i64"):
         f = modules.field
-        self.dtype = dtype
+        self.spec = VL.spec_of(dtype)
+        self.dtype = self.spec.dtype
         self.reducefn = f(redmod, "reducefn")
         self.combinerfn = f(redmod, "combinerfn")
         self.device_reducefn = f(redmod, "device_reducefn")
@@ -240,14 +247,22 @@ class ListReducers:
         return self.device_reducefn is not None
 
     # -- the combiner (map side) ---------------------------------------------
-    def combine(self, keys: KeyBatch, off: torch.Tensor, val: torch.Tensor):
+    def combine(self, keys: KeyBatch, off: torch.Tensor, val: torch.Tensor, src=None, add_bytes=None):
         """Every key's list with more than one value -> the combiner's values
         (job.lua:198-202); singleton lists are kept.  ``val``: int64 bits of
-        the lists' values.  Returns (off, val) in the same form."""
+        the lists' values (rows [n, k] for tuple / byte values, whose bytes
+        are spans of ``src``; new byte values go through ``add_bytes``).
+        Returns (off, val) in the same form."""
         m = off.numel() - 1
         multi = S.lengths(off) > 1
         if m == 0:
             return off, val
+        if not self.spec.scalar:
+            if self.device_combinerfn is not None:
+                out = self.device_combinerfn(keys, off, VL.to_user(val, self.spec, src))
+                noff, nval = self._spec_lists(out, m, "device_combinerfn", add_bytes)
+                return splice(off, val, noff, nval, ~multi)
+            return self._host_lists_spec(self.combinerfn, keys, off, val, multi, src, add_bytes, "combinerfn")
         if self.device_combinerfn is not None:
             out = self.device_combinerfn(keys, off, _typed(val, self.dtype))
             noff, nval = as_lists(out, m, "device_combinerfn")
@@ -304,6 +319,93 @@ class ListReducers:
             res[dst_idx] = arr
         t = torch.from_numpy(res).to(d)
         return torch.from_numpy(noff).to(d), _bits(t)
+
+    def _spec_lists(self, out, m: int, who: str, add_bytes):
+        """A batched hook's ValueLists over tuple / byte values -> (off, bits)."""
+        if not isinstance(out, ValueLists):
+            raise TypeError(f"{who} over {self.spec} values must return ValueLists(off, values)")
+        off = out.off.to(torch.int64)
+        if off.numel() != m + 1:
+            raise ValueError(f"{who}: {off.numel()} list offsets for {m} keys (want m + 1)")
+        n = int(off[-1]) if m else 0
+        return off, VL.from_user(out.val, self.spec, n, add_bytes, who)
+
+    def _host_lists_spec(self, fn, keys: KeyBatch, off, val, sel, src, add_bytes, who: str):
+        """Per selected key on the host over tuple / byte values (the
+        reference's per-key combiner call, job.lua:92-96,198-202)."""
+        d = off.device
+        o = off.cpu().numpy()
+        pick = np.flatnonzero(sel.cpu().numpy())
+        if pick.size == 0:
+            return off, val
+        rows = self.spec.rows(val)
+        csr = {}
+        for j in self.spec.bytes_cols:
+            bo, bb = VL.gather_bytes(rows[:, j], src)
+            csr[j] = (bo.cpu().numpy(), bb.cpu().numpy())
+        py = VL.host_columns(rows.cpu().numpy(), self.spec, csr)
+        names = keys.strings()
+        lens = np.diff(o)
+        outs = []
+        for i in pick:
+            acc: list = []
+            fn(names[i], py[o[i]:o[i + 1]], acc.append)
+            outs.append(acc)
+        new_lens = lens.copy()
+        new_lens[pick] = [len(a) for a in outs]
+        noff = np.zeros(lens.size + 1, np.int64)
+        np.cumsum(new_lens, out=noff[1:])
+        flat = [x for a in outs for x in a]
+        nb = VL.host_bits(flat, self.spec, add_bytes, who).reshape(-1, self.spec.width)
+        res = np.zeros((int(noff[-1]), self.spec.width), np.int64)
+        keep = np.ones(lens.size, bool)
+        keep[pick] = False
+        ki = np.flatnonzero(keep & (lens > 0))
+        host_rows = rows.cpu().numpy()
+        if ki.size:
+            src_idx = np.repeat(o[:-1][ki], lens[ki]) + _ranks(lens[ki])
+            dst_idx = np.repeat(noff[:-1][ki], lens[ki]) + _ranks(lens[ki])
+            res[dst_idx] = host_rows[src_idx]
+        if pick.size and nb.size:
+            nl = new_lens[pick]
+            dst_idx = np.repeat(noff[:-1][pick], nl) + _ranks(nl)
+            res[dst_idx] = nb
+        return torch.from_numpy(noff).to(d), self.spec.storage(torch.from_numpy(res).to(d))
+
+    # -- the reducer (reduce side) ---------------------------------------------
+    def reduce_device_cols(self, keys: KeyBatch, off: torch.Tensor, cols: list) -> dict:
+        """The batched reducer over tuple / byte-string value lists (``cols``:
+        a typed tensor per number column, ByteValues per byte column, as
+        order_lists gives them) -> result columns or lists."""
+        m = off.numel() - 1
+        spec = self.spec
+        if spec.width == 1:
+            val = cols[0]  # one byte-string column: its ByteValues
+        elif not spec.has_bytes and len(set(spec.cols)) == 1:
+            val = torch.stack(cols, 1)
+        else:
+            val = tuple(cols)
+        out = self.device_reducefn(keys, off, val)
+        if isinstance(out, ValueLists):
+            noff = out.off.to(torch.int64)
+            if noff.numel() != m + 1:
+                raise ValueError(f"device_reducefn: {noff.numel()} list offsets for {m} keys (want m + 1)")
+            v = out.val
+            if isinstance(v, torch.Tensor) and v.dim() == 1:
+                return {"list_off": noff, "list_val": v, "list_typed": True}
+            lc = [v[:, j] for j in range(v.shape[1])] if isinstance(v, torch.Tensor) else list(v)
+            return {"list_off": noff, "list_cols": lc}
+        if isinstance(out, torch.Tensor) and out.dim() == 2:
+            rc = [out[:, j] for j in range(out.shape[1])]
+        elif isinstance(out, torch.Tensor):
+            rc = [out]
+        else:
+            as_lists(out, m, "device_reducefn")  # validates the shape / type
+            rc = list(out)
+        rc = [c.reshape(-1) for c in rc]
+        if any(c.numel() != m for c in rc):
+            raise ValueError(f"device_reducefn: every returned column needs one value per key ({m})")
+        return {"cols": rc}
 
     # -- the reducer (reduce side) ---------------------------------------------
     def reduce_device(self, keys: KeyBatch, off: torch.Tensor, val: torch.Tensor) -> dict:

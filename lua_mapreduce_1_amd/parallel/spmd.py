@@ -50,6 +50,11 @@ from .staging import N_ARENAS, StagingMixin
 _MAX_SPARSE_CAP = 1 << 25
 
 
+def _tensor_ops() -> tuple:
+    from .tensor_plane import TENSOR_OPS
+    return TENSOR_OPS
+
+
 class _nullctx:
     def __enter__(self):
         return None
@@ -230,8 +235,10 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         elif self.op in planes.FOLD_OPS:
             self.plane_kind = "fold"
             self.tables[0] = ops.HashTable(table_capacity, device=self.device, op=self.op)
+        elif self.op in _tensor_ops():
+            self.plane_kind = "tensor"  # dense fp32 vectors per key (parallel/tensor_plane.py)
         else:
-            known = planes.FOLD_OPS + planes.LIST_OPS + planes.RECORD_OPS
+            known = planes.FOLD_OPS + planes.LIST_OPS + planes.RECORD_OPS + _tensor_ops()
             raise ValueError(f"unknown device_reduce {self.op!r}: one of {known}, a column spec such as "
                              "'f64:sum' or ('f64:mean', 'count'), or none (the reducefn runs on the host over "
                              "device-grouped values)")
@@ -1090,6 +1097,10 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
     def pairs(self, gathered):
         from ..runtime import codec
         for _name, cols in gathered:
+            if "keys" in cols and "values" in cols:  # the tensor plane: (key, [array])
+                for k, v in zip(cols["keys"], cols["values"]):
+                    yield k, [v]
+                continue
             yield from codec.iter_columnar(cols)
 
     def global_stats(self, res) -> dict:

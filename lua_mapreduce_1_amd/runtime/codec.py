@@ -158,6 +158,19 @@ def iter_columnar(cols: dict) -> Iterator[tuple]:
         for i in range(int(off.size) - 1):
             yield key_str(blob[off[i]:off[i + 1]]), [c[i].item() for c in cs]
         return
+    if "list_cols" in cols:  # tuple / byte-string values (parallel/values.py): (off, blob) per byte column
+        lo = cols["list_off"]
+        py = []
+        for c in cols["list_cols"]:
+            if isinstance(c, tuple):
+                o, b = c[0], c[1].tobytes()
+                py.append([key_str(b[o[i]:o[i + 1]]) for i in range(len(o) - 1)])
+            else:
+                py.append(c.tolist())
+        vals = py[0] if len(py) == 1 else list(zip(*py))
+        for i in range(int(lo.size) - 1):
+            yield key_str(blob[off[i]:off[i + 1]]), vals[lo[i]:lo[i + 1]]
+        return
     if "list_off" in cols:
         lo, lv = cols["list_off"], cols["list_val"]
         for i in range(int(lo.size) - 1):

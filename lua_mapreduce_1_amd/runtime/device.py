@@ -303,18 +303,55 @@ _POOL = _PinnedPool()
 _BLOB_EST: dict = {}  # device -> expected key-blob bytes of the next finalize()
 
 
+_SDMA: dict = {}  # device -> [(dst, src, nbytes)] downloads deferred to flush_downloads
+
+
+def _sdma_ok() -> bool:
+    ok = _SDMA.get("ok")
+    if ok is None:
+        from ..ops import _hip
+        ok = _SDMA["ok"] = bool(_hip.lib().mr_sdma_available())
+    return ok
+
+
 def dma_to_host(dst: torch.Tensor, src: torch.Tensor) -> None:
     """Queue a device -> pinned-host download of ``src`` into ``dst`` on the
-    current stream (mr_d2h_async: shader stores, so it is not queued behind
-    the input copies of later iterations on the shared SDMA engine; and not
-    torch's non_blocking copy_, which also records an event for the pinned
-    block in its host allocator on every call — that event pool's growth
-    stalled the host for ~5 ms now and then)."""
+    current stream (hipMemcpyAsync; not torch's non_blocking copy_, which
+    also records an event for the pinned block in its host allocator on
+    every call — that event pool's growth stalled the host for ~5 ms now and
+    then).  A download of at least ``MR_SDMA_MIN_MB`` is deferred instead: the
+    runtime would run it as a blit kernel on the CUs, beside the next
+    iteration's map; :func:`flush_downloads` (after the stream wait that
+    precedes every read of the results) moves it on the SDMA engines."""
     from ..ops import _hip
+    from ..utils.config import TUNABLES
     assert src.is_contiguous() and dst.is_contiguous() and dst.numel() * dst.element_size() >= \
         src.numel() * src.element_size()
-    _hip.call("mr_d2h_async", _hip.ptr(dst), _hip.ptr(src), src.numel() * src.element_size(),
-              _hip.stream(src.device))
+    nb = src.numel() * src.element_size()
+    if TUNABLES.sdma_min_mb > 0 and nb >= TUNABLES.sdma_min_mb * (1 << 20) and _sdma_ok():
+        _SDMA.setdefault(src.device, []).append((dst, src, nb))
+        return
+    _hip.call("mr_d2h_async", _hip.ptr(dst), _hip.ptr(src), nb, _hip.stream(src.device))
+
+
+def flush_downloads(device) -> None:
+    """Run the downloads deferred by :func:`dma_to_host` on the SDMA engines
+    and wait for them (call after waiting for the stream that produced
+    them)."""
+    pend = _SDMA.pop(device, None)
+    if not pend:
+        return
+    import ctypes
+    from ..ops import _hip
+    n = len(pend)
+    dsts = (ctypes.c_void_p * n)(*[t[0].data_ptr() for t in pend])
+    srcs = (ctypes.c_void_p * n)(*[t[1].data_ptr() for t in pend])
+    sizes = (ctypes.c_uint64 * n)(*[t[2] for t in pend])
+    rc = _hip.lib().mr_sdma_d2h(dsts, srcs, sizes, n)
+    if rc < 0:
+        raise RuntimeError("device -> host download failed (SDMA and hipMemcpy)")
+    if rc == 1:
+        _SDMA["ok"] = False  # the SDMA path failed once: plain runtime copies from now on
 
 
 def _to_host(t: torch.Tensor, name: str) -> torch.Tensor:
@@ -607,6 +644,7 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
     if hi.is_cuda:
         from ..ops import _hip
         _hip.wait_stream(hi.device)
+        flush_downloads(hi.device)  # large downloads: on the SDMA engines, now that their data is produced
         hb, est, blob = pend["hb"], pend["est"], pend["blob"]
         if pend.get("fused"):
             f_val, f_off, f_counts, f_bad = _unpack_fused(pend)

@@ -260,7 +260,8 @@ class job:  # noqa: N801
         pspec = modules.field(pmod, "device_partition")
         nparts = int(extra.get("num_partitions") or (pspec[1] if pspec else 0) or 1)
         phys = A.Physical(A.parse_spec(spec)) if kind == "cols" else None
-        dtype = str(modules.field(self.module, "device_value_dtype", "i64") or "i64")
+        from ..parallel import values as VL
+        dtype = VL.spec_of(modules.field(self.module, "device_value_dtype", "i64") or "i64")
         d = dev.default_device()
         cap = int(extra.get("table_capacity") or 1 << 16)
         fn = modules.field(self.module, "device_mapfn")

@@ -91,6 +91,10 @@ class Tunables:
                               "exchange, result download) instead of four times")
     pipeline: bool = _knob("MR_PIPELINE", True, "bench/proxies: map of iteration i+1 overlaps the tail of i")
     prefetch_single: bool = _knob("MR_PREFETCH_SINGLE", True, "prefetched inputs: one DMA per iteration")
+    sdma_min_mb: float = _knob("MR_SDMA_MIN_MB", 8.0,
+                               "result downloads of at least this many MiB go over the SDMA copy engines (ROCr copy "
+                               "API, csrc/hip/sdma.hip) after the tail's kernels, not as a runtime blit kernel on "
+                               "the CUs beside the next map (0 = never)")
     spin_us: float = _knob("MR_SPIN_US", 2000.0, "host spin on completion words before hipStreamSynchronize, us")
     force_shuffle: bool = _knob("MR_FORCE_SHUFFLE", False,
                                 "SPMD: run the W>1 shuffle (pack, count exchange, all-to-all, receive insert) also "

@@ -141,7 +141,28 @@ def _host(R, device):
     return res, lambda: H.RESULT == H.naive(H._SPLITS)
 
 
-PLANES = {"host": _host, "fold": _fold, "list": _list, "records": _records, "generic": _generic, "generic_cols": _generic_cols,
+def _value_rows(mod, splits, R, device):
+    """Tuple values (PositionalIndex) / byte-string values (SourceIndex) on
+    the general plane's value lists."""
+    import importlib
+    from test_generic_plane import run_engine
+    eng, res, got = run_engine(mod, splits, device, {"num_reducers": R})
+    exp = importlib.import_module(mod).naive(splits)
+    if mod.endswith("PositionalIndex"):
+        got = {k: [tuple(v) for v in vs] for k, vs in got.items()}
+    return res, lambda: got == exp
+
+
+def _positional(R, device):
+    return _value_rows("lua_mapreduce_1_amd.examples.PositionalIndex", _text(), R, device)
+
+
+def _sources(R, device):
+    from lua_mapreduce_1_amd.examples import SourceIndex
+    return _value_rows("lua_mapreduce_1_amd.examples.SourceIndex", SourceIndex.corpus(seed=4, lines=4000), R, device)
+
+
+PLANES = {"host": _host, "positional": _positional, "sources": _sources, "fold": _fold, "list": _list, "records": _records, "generic": _generic, "generic_cols": _generic_cols,
           "list_rounds": _list_rounds, "generic_rounds": _generic_rounds}
 
 
