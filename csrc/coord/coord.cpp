@@ -19,6 +19,7 @@
 // Wire format (little endian): request = u32 body_len | u16 op | fields,
 // response = u32 body_len | i32 status | fields; field = u32 len | bytes.
 #include <arpa/inet.h>
+#include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
@@ -680,7 +681,18 @@ class Store {
           left -= (long)k;
         }
         fclose(f);
-        if (fflush(n) != 0 || fclose(n) != 0 || left != 0 || rename(tmp.c_str(), path) != 0) return false;
+        // durable before it replaces the only copy of the state: the new file
+        // synced, the old one kept as <path>.legacy (a hard link) until the
+        // upgraded journal has been reopened, the directory entry synced
+        // (a power loss right after the rename could otherwise
+        // leave an empty journal, read as a fresh one)
+        const bool synced = fflush(n) == 0 && fsync(fileno(n)) == 0;
+        if (fclose(n) != 0 || !synced || left != 0) return false;
+        legacy = std::string(path) + ".legacy";
+        unlink(legacy.c_str());
+        if (link(path, legacy.c_str()) != 0) legacy.clear();
+        if (rename(tmp.c_str(), path) != 0) return false;
+        sync_dir(path);
         fprintf(stderr, "coordinator: journal %s upgraded from the headerless format (%ld bytes replayed)\n", path,
                 good);
       } else {
@@ -697,7 +709,24 @@ class Store {
       fclose(n);
     }
     journal = fopen(path, "ab");
+    if (journal != nullptr && !legacy.empty()) {
+      unlink(legacy.c_str());  // the upgraded journal is in use: the old copy can go
+      legacy.clear();
+    }
     return journal != nullptr;
+  }
+
+  std::string legacy;  // the pre-upgrade journal, kept until the upgraded one is reopened
+
+  static void sync_dir(const char* path) {
+    std::string d(path);
+    const size_t k = d.find_last_of('/');
+    d = k == std::string::npos ? std::string(".") : (k == 0 ? std::string("/") : d.substr(0, k));
+    const int fd = ::open(d.c_str(), O_RDONLY | O_DIRECTORY);
+    if (fd >= 0) {
+      fsync(fd);
+      ::close(fd);
+    }
   }
 };
 

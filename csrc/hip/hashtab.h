@@ -104,8 +104,15 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
       return 1;
     }
     if (cur == tag) {
-      // lo and hi in one round trip: an hi read ahead of lo's publication is
-      // caught by the acquire + re-read below, as an early hi always was
+      // lo and hi in one round trip (profiles/r4/probe_lohi/).  The hi load is
+      // not ordered after the lo load, so it may return the slot's value from
+      // before the claimer published (a previous key of this slot: reset does
+      // not clear hi).  A stale hi that MISMATCHES is re-read after the acquire
+      // fence below; a stale hi that happens to EQUAL ours is accepted without
+      // one — which needs the claimer's key to share our 56-bit tag (a hash of
+      // hi and lo) and our lo while differing in hi, i.e. a 56-bit collision of
+      // two keys' (hi, lo) hashes, ~2^-56 per probe pair.  Keys of <= 7 bytes
+      // (exact tags) never get here; long keys still compare bytes.
       const u64 l = ld_agent(&t.lo[slot]);
       u64 h = ld_agent(&t.hi[slot]);
       if (l == 0) continue;  // claimed but not yet published: re-read this slot

@@ -331,8 +331,24 @@ class AggTable:
         for v, dt in vals:
             npdt = {"i64": np.int64, "f64": np.float64, "f32": np.float32}[dt]
             cols.append(_np(v).astype(npdt) if isinstance(v, torch.Tensor) else np.full(n, v, npdt))
-        self._pending.append((h, lw, r, cols, ok))
+        self._pending.append((h, lw, r, cols, ok, ok))
         self.npost += n if self.list_mode else 0
+
+    def insert_keys(self, hi, lo, rep) -> None:
+        """List mode: keys with NO posting (a key whose combiner emitted
+        nothing keeps its place, like the reference's ``return k,{}`` line of
+        an emptied list, job.lua:198-214): the key is in the table, its list
+        is empty."""
+        n = int(hi.numel())
+        if n == 0:
+            return
+        if self.is_cuda:
+            self.keys.insert(hi.contiguous(), lo.contiguous(), torch.zeros(n, dtype=torch.int64, device=self.device),
+                             rep.contiguous(), src=self.src)
+            return
+        k = self.vspec.width
+        self._pending.append((_u64(hi).copy(), _u64(lo).copy(), _u64(rep).copy(), [np.zeros(n, np.int64)] * k,
+                              np.ones(n, bool), np.zeros(n, bool)))
 
     def insert_csv(self, text: torch.Tensor, rep_base: int, key: int, values, sep: int,
                    rows_out: torch.Tensor) -> None:
@@ -394,7 +410,7 @@ class AggTable:
             return
         b = _np(buf)
         h = heap.numpy()
-        for hi_, lo_, r, _cols, ok in self._pending:
+        for hi_, lo_, r, _cols, ok, _post in self._pending:
             long_ = ok & ((lo_ & np.uint64(0xFF)) == np.uint64(K.LONG_MARK))
             off = r >> np.uint64(K.REP_LEN_BITS)
             for i in np.flatnonzero(long_ & (off >= np.uint64(lo_off)) & (off < np.uint64(hi_off))):
@@ -480,6 +496,10 @@ class AggTable:
                 return slot, hi, lo, rep, z, sp.storage(z.clone())
             return slot, hi, lo, rep, self.post_slot[:n], sp.storage(self.post_val[:n * sp.width])
         h, lw, r, inv, cols = self._cpu_ids()
+        if any(not p[5].all() for p in self._pending):
+            # key-only rows (insert_keys): in the key set, no posting
+            post = np.concatenate([p[5] for p in self._pending])[np.concatenate([p[4] for p in self._pending])]
+            inv = np.where(post, inv, -1)
         sp = self.vspec
         bits = [c.view(np.int64) if c.dtype == np.float64 else c.astype(np.int64, copy=False) for c in cols or []]
         if not bits:

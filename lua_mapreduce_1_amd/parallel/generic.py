@@ -375,6 +375,12 @@ class GenericMap:
         if n:
             kid = S.ids(noff, n)
             nt.insert(n, self._value_cols(nval), hi=hi[kid], lo=lo[kid], rep=rep[kid])
+        empty = S.lengths(noff) == 0
+        if bool(empty.any()):
+            # a key whose combiner emitted nothing stays, with an empty list:
+            # the reference still writes it (`return k,{}`, job.lua:198-214),
+            # so its reducer runs over whatever the other maps sent
+            nt.insert_keys(hi[empty], lo[empty], rep[empty])
         self.table = nt
         self.combines += 1
         return True

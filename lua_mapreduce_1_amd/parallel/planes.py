@@ -910,11 +910,21 @@ class RecordPlane:
             return False
         cap = self._cap()
         with np.load(path, allow_pickle=False) as z:
-            rb, kb, nblocks = (int(x) for x in z["shape"])
+            if "shape" in z.files:
+                rb, kb, nblocks = (int(x) for x in z["shape"])
+                names = ["rows%d" % i for i in range(nblocks)]
+            elif "rows" in z.files and "key_bytes" in z.files:
+                # a checkpoint of the round-3 format (one `rows` array + `key_bytes`)
+                kb = int(np.asarray(z["key_bytes"]).reshape(-1)[0])
+                rb = int(z["rows"].shape[1])
+                names = ["rows"]
+            else:
+                sys.stderr.write("# rank %d: map checkpoint %s has an unknown format: re-mapping\n" % (eng.rank, path))
+                return False
             # block by block from host memory, each at most the HBM cap: the
             # emitter's spill rule keeps rows past the cap on the host
-            for i in range(nblocks):
-                rows = z["rows%d" % i]
+            for name in names:
+                rows = z[name]
                 step = max(1, cap // max(rb, 1)) if cap else max(1, rows.shape[0])
                 for a in range(0, rows.shape[0], step):
                     self.emitter.records(torch.from_numpy(rows[a:a + step]), kb)

@@ -219,5 +219,7 @@ def test_headerless_journal_of_previous_build_is_upgraded(tmp_path):
     c2.request("BLOB_PUT", "jdb", "c", b"third")
     with open(legacy, "rb") as f:
         assert f.read(8) == data[:8]  # now in the current format
+    # the pre-upgrade copy (<path>.legacy) is gone once the upgraded journal is in use
+    assert not os.path.exists(legacy + ".legacy") and not os.path.exists(legacy + ".upgrade")
     c3 = coordinator.Client(coordinator.start_local(journal=legacy))
     assert c3.request("BLOB_GET", "jdb", "c")[1] == [b"third"]

@@ -283,3 +283,32 @@ def test_row_gathers_equal_gpu(gpu, rb):
     perm = torch.randperm(n, generator=g).to(torch.int32).to(gpu)
     assert torch.equal(RC.gather(rec, perm, mode=1), RC.gather(rec, perm, mode=0))
     assert torch.equal(RC.gather(rec, perm, mode=0).cpu(), rec.cpu()[perm.cpu().long()])
+
+
+@pytest.mark.parametrize("fmt", ["legacy", "unknown"])
+def test_records_checkpoint_formats(tmp_path, fmt):
+    """a map checkpoint of the round-3 format (one ``rows`` array +
+    ``key_bytes``) is restored; a file of an unknown format is ignored and the
+    map re-runs — a relaunch never dies on KeyError('shape')."""
+    ckpt = str(tmp_path / "ckpt")
+    args = dict(SHAPES[0], rows=6000)
+    eng, _res, rows = run_engine(args, torch.device("cpu"), checkpoint_dir=ckpt)
+    assert check(rows, args)
+    # iteration 2 of a new engine on the same checkpoint dir: plant its map checkpoint
+    from lua_mapreduce_1_amd import spmd
+    eng2 = spmd(dict(taskfn=M, mapfn=M, partitionfn=M, reducefn=M, init_args=dict(args), checkpoint_dir=ckpt),
+                device=torch.device("cpu"))
+    eng2.iteration = 0
+    eng2.iteration += 1
+    path = eng2._map_ckpt_path()
+    eng2.iteration -= 1
+    want, kb = expected(args)
+    with open(path, "wb") as f:
+        if fmt == "legacy":
+            np.savez(f, rows=want, key_bytes=np.array([kb], np.int64))
+        else:
+            np.savez(f, something=np.zeros(3))
+    res = eng2.run_iteration()
+    got = np.concatenate([c["records"] for _n, c in eng2.gather_results(res)])
+    assert check(got, args)
+    assert eng2.maps_restored == (1 if fmt == "legacy" else 0)
