@@ -23,7 +23,8 @@ import torch
 
 NUM_REDUCERS = 10
 NSPLITS = 8
-SPLITS: list = []   # host form: the split texts (init {"splits": [...]})
+SPLITS: list = []
+FILES: list = []    # server/worker form: one map job per file (init {"files": [...]})
 RESULT: dict = {}
 device_input = "split"
 spmd_replicated_taskfn = True
@@ -33,17 +34,43 @@ device_partition = ("fnv1", NUM_REDUCERS)
 
 
 def init(args):
-    global NUM_REDUCERS, NSPLITS, SPLITS, device_partition
+    global NUM_REDUCERS, NSPLITS, SPLITS, FILES, device_partition
     args = args or {}
     NUM_REDUCERS = int(args.get("num_reducers", NUM_REDUCERS))
     SPLITS = list(args.get("splits") or [])
-    NSPLITS = int(args.get("nsplits", len(SPLITS) or NSPLITS))
+    FILES = list(args.get("files") or [])
+    NSPLITS = int(args.get("nsplits", len(FILES) or len(SPLITS) or NSPLITS))
     device_partition = ("fnv1", NUM_REDUCERS)
 
 
+def _file_lines(path: str) -> int:
+    with open(path, "rb") as f:
+        data = f.read()
+    return data.count(b"\n") + (0 if data[-1:] == b"\n" else 1)
+
+
 def taskfn(emit):
+    line0 = 0
     for i in range(NSPLITS):
-        emit(i + 1, {"split": i})
+        if FILES:
+            emit(i + 1, {"split": i, "file": FILES[i], "line0": line0})
+            line0 += _file_lines(FILES[i])
+        else:
+            emit(i + 1, {"split": i})
+
+
+def _data(value, emit):
+    if hasattr(value, "data_ptr"):
+        return value  # SPMD: the staged split(s)
+    from lua_mapreduce_1_amd.ops import io as _io
+    return _io.load_file(value["file"], emit.device)  # a worker's job: its file
+
+
+def _text(value) -> bytes:
+    if isinstance(value, dict) and value.get("file"):
+        with open(value["file"], "rb") as f:
+            return f.read()
+    return SPLITS[value["split"]]
 
 
 def token_positions(line: torch.Tensor) -> torch.Tensor:
@@ -53,19 +80,24 @@ def token_positions(line: torch.Tensor) -> torch.Tensor:
     return idx - torch.searchsorted(line, line)
 
 
-def device_mapfn(keys, data, emit):
+def device_mapfn(keys, value, emit):
     from lua_mapreduce_1_amd.ops import text as TX
+    data = _data(value, emit)
     st, ln, line = TX.tokens(data, lines=True)
     pos = token_positions(line)
-    if emit.line_base is None:
-        raise RuntimeError("PositionalIndex needs the SPMD engine's global line numbering (split inputs)")
-    emit.spans(st, ln, line + emit.line_base(data), pos)
+    if isinstance(value, dict):
+        base = int(value.get("line0", 0))  # a worker's file: the global number of its first line
+    elif getattr(emit, "line_base", None) is not None:
+        base = emit.line_base(data)        # SPMD: the plane's global line numbering
+    else:
+        raise RuntimeError("PositionalIndex needs global line numbers (split inputs or file jobs with line0)")
+    emit.spans(st, ln, line + base, pos, text=data)
 
 
 def mapfn(key, value, emit):
     """Host form: the split's text from init {"splits": [...]} and the global
     number of its first line (job value {"split": i, "line0": L})."""
-    s = SPLITS[value["split"]]
+    s = _text(value)
     if s[-1:] != b"\n":
         s += b"\n"
     for n, text in enumerate(s.split(b"\n")):

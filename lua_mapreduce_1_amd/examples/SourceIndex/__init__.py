@@ -25,6 +25,7 @@ import torch
 NUM_REDUCERS = 10
 NSPLITS = 8
 SPLITS: list = []
+FILES: list = []    # server/worker (and host-plane) form: one map job per file
 RESULT: dict = {}
 device_input = "split"
 spmd_replicated_taskfn = True
@@ -34,17 +35,43 @@ device_partition = ("fnv1", NUM_REDUCERS)
 
 
 def init(args):
-    global NUM_REDUCERS, NSPLITS, SPLITS, device_partition
+    global NUM_REDUCERS, NSPLITS, SPLITS, FILES, device_partition
     args = args or {}
     NUM_REDUCERS = int(args.get("num_reducers", NUM_REDUCERS))
     SPLITS = list(args.get("splits") or [])
-    NSPLITS = int(args.get("nsplits", len(SPLITS) or NSPLITS))
+    FILES = list(args.get("files") or [])
+    NSPLITS = int(args.get("nsplits", len(FILES) or len(SPLITS) or NSPLITS))
     device_partition = ("fnv1", NUM_REDUCERS)
 
 
+def _file_lines(path: str) -> int:
+    with open(path, "rb") as f:
+        data = f.read()
+    return data.count(b"\n") + (0 if data[-1:] == b"\n" else 1)
+
+
 def taskfn(emit):
+    line0 = 0
     for i in range(NSPLITS):
-        emit(i + 1, {"split": i})
+        if FILES:
+            emit(i + 1, {"split": i, "file": FILES[i], "line0": line0})
+            line0 += _file_lines(FILES[i])
+        else:
+            emit(i + 1, {"split": i})
+
+
+def _data(value, emit):
+    if hasattr(value, "data_ptr"):
+        return value  # SPMD: the staged split(s)
+    from lua_mapreduce_1_amd.ops import io as _io
+    return _io.load_file(value["file"], emit.device)  # a worker's job: its file
+
+
+def _text(value) -> bytes:
+    if isinstance(value, dict) and value.get("file"):
+        with open(value["file"], "rb") as f:
+            return f.read()
+    return SPLITS[value["split"]]
 
 
 def line_sources(data: torch.Tensor):
@@ -67,17 +94,18 @@ def line_sources(data: torch.Tensor):
     return starts, lens, name_end
 
 
-def device_mapfn(keys, data, emit):
+def device_mapfn(keys, value, emit):
     from lua_mapreduce_1_amd.ops import text as TX
+    data = _data(value, emit)
     st, ln, line = TX.tokens(data, lines=True)
     s0, sl, name_end = line_sources(data)
     keep = st > name_end[line]  # the text after the tab (the name itself is no word of it)
     st, ln, line = st[keep], ln[keep], line[keep]
-    emit.spans(st, ln, emit.bytes(s0[line], sl[line]))
+    emit.spans(st, ln, emit.bytes(s0[line], sl[line], text=data), text=data)
 
 
 def mapfn(key, value, emit):
-    s = SPLITS[value["split"]]
+    s = _text(value)
     for text in s.split(b"\n"):
         name, tab, rest = text.partition(b"\t")
         if not tab:

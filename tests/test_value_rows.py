@@ -180,3 +180,31 @@ def test_device_reducefn_over_bytes_cpu(monkeypatch):
                 k = w.decode()
                 occ[k] = occ.get(k, 0) + len(name)
     assert got == {k: [v] for k, v in occ.items()}
+
+
+# -- the reference's deployment shape (server + workers over the coordinator) ---------
+@pytest.mark.parametrize("plane", ["host", "device"])
+@pytest.mark.parametrize("which", ["pi", "si"])
+def test_value_rows_server_worker(tmp_path, which, plane):
+    """Both examples through server/worker: the host plane (MRK1 records of
+    tuples / strings) and the device map (value rows written as records for
+    the reduce jobs), diffed against the oracles."""
+    import importlib
+    from lua_mapreduce_1_amd.runtime import coordinator
+    from test_e2e_wordcount import run_job
+    mod = PI if which == "pi" else SI
+    splits = (pi_data() if which == "pi" else si_data())[:4]
+    files = []
+    for i, s in enumerate(splits):
+        p = tmp_path / f"split{i}.txt"
+        p.write_bytes(s)
+        files.append(str(p))
+    cs = coordinator.start_local()
+    params = dict(taskfn=mod, mapfn=mod, partitionfn=mod, reducefn=mod, finalfn=mod,
+                  init_args={"files": files, "num_reducers": 5}, storage="gridfs",
+                  device="auto" if plane == "device" else "host")
+    _, s = run_job(cs, f"vr_{which}_{plane}", params, nworkers=2)
+    m = importlib.import_module(mod)
+    got = _pi_got(m.RESULT) if which == "pi" else m.RESULT
+    assert got == m.naive(splits)
+    assert s.last_stats["failed_map_jobs"] == 0 and s.last_stats["failed_red_jobs"] == 0
