@@ -120,6 +120,7 @@ _SIGS = {
     "mr_posting_keys": [_p, ctypes.c_longlong, _p, ctypes.c_longlong, ctypes.c_longlong, _p, _p, _p],
     "mr_csv_set_config": [_i32, _i32],
     "mr_agg_set_insert_grid": [_i32],
+    "mr_agg_set_l1_probe": [_i32],
     "mr_sdma_available": [],
     "mr_sort11_set_rounds": [_i32],
     "mr_sort11_tiles": [_u64],
@@ -159,6 +160,7 @@ def lib():
             raise ValueError(f"MR_SORT11_ROUNDS={TUNABLES.sort11_rounds}: must be 8, 16, 24 or 32")
         if L.mr_agg_set_insert_grid(TUNABLES.agg_insert_grid) != 0:
             raise ValueError(f"MR_AGG_INSERT_GRID={TUNABLES.agg_insert_grid}: must be >= 256")
+        L.mr_agg_set_l1_probe(1 if TUNABLES.agg_l1_probe else 0)
         if L.mr_rec_gather_set_rows(TUNABLES.rec_gather_rows) != 0:
             raise ValueError(f"MR_REC_GATHER_ROWS={TUNABLES.rec_gather_rows}: must be 128 or 256")
         _LIB = L

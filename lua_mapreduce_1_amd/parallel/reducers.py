@@ -38,7 +38,9 @@ import torch
 from .. import ops
 from ..ops import segments as S
 from ..runtime import codec, modules
+from . import recognize as RZ
 from . import values as VL
+from ..utils.config import TUNABLES
 
 
 class ValueLists(NamedTuple):
@@ -229,6 +231,14 @@ class ListReducers:
         self.combinerfn = f(redmod, "combinerfn")
         self.device_reducefn = f(redmod, "device_reducefn")
         dc = f(redmod, "device_combinerfn")
+        # a host reducer / combiner that is exactly sum / min / max of its
+        # values runs batched on the device (parallel/recognize.py)
+        self.recognized = {}
+        if TUNABLES.recognize_reducers and self.spec.scalar and self.spec.dtype in ("i64", "f64"):
+            if self.device_reducefn is None:
+                self.device_reducefn = self._recognized("reducefn", self.reducefn)
+            if dc is None and self.combinerfn is not None and self.combinerfn is not self.reducefn:
+                dc = self._recognized("combinerfn", self.combinerfn)
         if dc is None and self.device_reducefn is not None and self.combinerfn is not None \
                 and self.combinerfn is self.reducefn:
             dc = self.device_reducefn  # the combiner is the reducer: so is its batched form
@@ -237,6 +247,13 @@ class ListReducers:
             raise ValueError("a reduce module without device_reduce needs a reducefn (or a device_reducefn)")
         self.aci = all(bool(f(redmod, x)) for x in ("associative_reducer", "commutative_reducer",
                                                     "idempotent_reducer"))
+
+    def _recognized(self, name: str, fn):
+        op = RZ.recognize(fn)
+        fold = RZ.device_fold(op, self.spec.dtype) if op else None
+        if fold is not None:
+            self.recognized[name] = op
+        return fold
 
     @property
     def has_combiner(self) -> bool:

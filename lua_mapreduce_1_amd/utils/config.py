@@ -73,6 +73,13 @@ class Tunables:
     agg_insert_grid: int = _knob("MR_AGG_INSERT_GRID", 65536,
                                  "general plane: workgroup cap of the per-row table insert (>= 256; one row per "
                                  "thread up to 16 M rows, profiles/r4/agg_grid_ab)")
+    recognize_reducers: bool = _knob("MR_RECOGNIZE_REDUCERS", True,
+                                     "general plane: a host reducefn / combinerfn that is exactly emit(sum|min|max("
+                                     "values)) (or the accumulate loop) runs batched on the device "
+                                     "(parallel/recognize.py)")
+    agg_l1_probe: bool = _knob("MR_AGG_L1_PROBE", False,
+                               "general plane: the per-row table insert probes with plain (vector-L1 cached) "
+                               "loads, falling back to agent loads on a stale read (hashtab.h gtab_insert<true>)")
     rec_gather_rows: int = _knob("MR_REC_GATHER_ROWS", 256,
                                  "record plane: rows per workgroup batch of the 16-byte row gather (256, or 128: "
                                  "half the LDS image, more workgroups per CU)")
