@@ -206,6 +206,19 @@ class AggTable:
         else:
             self._pending: list = []
         self.npost = 0
+        # Run-length postings (list mode on the GPU, one scalar value column):
+        # while every row inserted so far carries the SAME constant value (a
+        # word count's emit(word, 1)), a key's list is that constant repeated,
+        # so the table keeps a per-slot COUNT (an LDS-combined fold) instead
+        # of one (slot, value) posting per row — no posting writes, no posting
+        # sort and gather before the combiner.  The first row with another
+        # value expands the counts into postings (every earlier row precedes
+        # it, so each list's emission order is kept) and the table continues
+        # as plain list mode.
+        from ..utils.config import TUNABLES
+        self._runs = self.is_cuda and self.list_mode and self.vspec.scalar and TUNABLES.const_runs
+        self.run_bits: int | None = None  # the constant's value bits (None: no row yet)
+        self._run_count: torch.Tensor | None = None
 
     @property
     def is_cuda(self) -> bool:
@@ -221,8 +234,65 @@ class AggTable:
         if self.is_cuda:
             self.keys.reset()
             self._fill_cols()
+            from ..utils.config import TUNABLES
+            self._runs = self.list_mode and self.vspec.scalar and TUNABLES.const_runs
+            if self.run_bits is not None and self._run_count is not None:
+                self._run_count.zero_()
+            self.run_bits = None
         else:
             self._pending = []
+
+    # -- run-length postings ---------------------------------------------------
+    @property
+    def runs(self) -> bool:
+        """True while the postings are held as per-slot counts of one constant."""
+        return self._runs and self.run_bits is not None
+
+    def _run_insert(self, vals: list) -> bool:
+        """Whether this insert's rows can be counted (run-length form): one
+        scalar value equal to every earlier row's.  Leaves the run form
+        (expanding it) when not."""
+        if not self._runs:
+            return False
+        v, dt = vals[0]
+        if len(vals) == 1 and not isinstance(v, torch.Tensor):
+            bits = _scalar_bits(v, dt)
+            if self.run_bits is None or self.run_bits == bits:
+                if self._run_count is None:
+                    self._run_count = torch.zeros(self.cap, dtype=torch.int64, device=self.device)
+                self.run_bits = bits
+                return True
+        self.expand_runs()
+        return False
+
+    def expand_runs(self) -> None:
+        """Counts -> explicit postings (slot, constant); plain list mode from here."""
+        if not self._runs:
+            return
+        self._runs = False
+        if self.run_bits is None:
+            return  # nothing counted yet
+        slot, _hi, _lo, _rep, _ = self.compact()
+        cnt = self._run_count[slot]
+        n = int(cnt.sum())
+        self.npost = 0
+        self._grow_posts(n)
+        if n:
+            self.post_slot[:n] = torch.repeat_interleave(slot, cnt, output_size=n)
+            self.post_val[:n].fill_(self.run_bits)
+        self.npost = n
+
+    def run_lists(self, known: tuple[int, bool] | None = None):
+        """Run-length form: (slot, hi, lo, rep) of every key and its list in
+        CSR form (off [m + 1], val: the constant repeated) — what
+        parallel/reducers.lists_of_postings builds from explicit postings,
+        without the sort."""
+        slot, hi, lo, rep, _ = self.compact(known)
+        cnt = self._run_count[slot]
+        off = torch.zeros(slot.numel() + 1, dtype=torch.int64, device=self.device)
+        torch.cumsum(cnt, 0, out=off[1:])
+        n = int(off[-1]) if slot.numel() else 0
+        return slot, hi, lo, rep, off, torch.full((n,), self.run_bits, dtype=torch.int64, device=self.device)  # value bits
 
     # -- inserts ---------------------------------------------------------------
     def _values(self, values, n: int) -> list:
@@ -263,6 +333,14 @@ class AggTable:
         if n == 0:
             return
         vals = self._values(values, n)
+        if self.is_cuda and self.list_mode and self._run_insert(vals):
+            a = _ColsArg()  # the rows' key counts: a fold (LDS-combined) into the run-count column
+            a.k, a.list, a.cstride, a.rows_only = 1, 0, 1, 0
+            a.stype[0], a.sbits[0], a.dtype[0], a.op[0] = _VT_SCALAR, 1, _VT[torch.int64], _OPC["sum"]
+            a.dst[0] = self._run_count.data_ptr()
+            self._agg_insert(a, n, [], hi, lo, rep, rep_add, text, starts, lens, rep_base)
+            self.npost += n
+            return
         if self.is_cuda:
             a = _ColsArg()
             a.k = len(vals)
@@ -298,18 +376,7 @@ class AggTable:
                 a.dst[0] = self.post_val.data_ptr()
                 a.post_slot = self.post_slot.data_ptr()
                 a.post_base = self.npost
-            t = self.keys
-            if text is not None:
-                st = starts.to(torch.int64).contiguous()
-                ln = lens.to(torch.int32).contiguous()
-                keep += [st, ln]
-                _hip.call("mr_agg_insert", *t._gtab(), t.cap, _hip.ptr(self.src), None, None, None, 0,
-                          _hip.ptr(text), _hip.ptr(st), _hip.ptr(ln), rep_base, n, ctypes.byref(a),
-                          _hip.stream(self.device))
-            else:
-                _hip.call("mr_agg_insert", *t._gtab(), t.cap, _hip.ptr(self.src), _hip.ptr(hi.contiguous()),
-                          _hip.ptr(lo.contiguous()), _hip.ptr(rep.contiguous()) if rep is not None else None,
-                          rep_add, None, None, None, 0, n, ctypes.byref(a), _hip.stream(self.device))
+            self._agg_insert(a, n, keep, hi, lo, rep, rep_add, text, starts, lens, rep_base)
             self.npost += n if self.list_mode else 0
             return
         # CPU: pending rows, folded at compaction
@@ -333,6 +400,20 @@ class AggTable:
             cols.append(_np(v).astype(npdt) if isinstance(v, torch.Tensor) else np.full(n, v, npdt))
         self._pending.append((h, lw, r, cols, ok, ok))
         self.npost += n if self.list_mode else 0
+
+    def _agg_insert(self, a, n: int, keep: list, hi, lo, rep, rep_add, text, starts, lens, rep_base) -> None:
+        t = self.keys
+        if text is not None:
+            st = starts.to(torch.int64).contiguous()
+            ln = lens.to(torch.int32).contiguous()
+            keep += [st, ln]
+            _hip.call("mr_agg_insert", *t._gtab(), t.cap, _hip.ptr(self.src), None, None, None, 0,
+                      _hip.ptr(text), _hip.ptr(st), _hip.ptr(ln), rep_base, n, ctypes.byref(a),
+                      _hip.stream(self.device))
+        else:
+            _hip.call("mr_agg_insert", *t._gtab(), t.cap, _hip.ptr(self.src), _hip.ptr(hi.contiguous()),
+                      _hip.ptr(lo.contiguous()), _hip.ptr(rep.contiguous()) if rep is not None else None,
+                      rep_add, None, None, None, 0, n, ctypes.byref(a), _hip.stream(self.device))
 
     def insert_keys(self, hi, lo, rep) -> None:
         """List mode: keys with NO posting (a key whose combiner emitted
@@ -488,6 +569,7 @@ class AggTable:
         """List mode: (slot, hi, lo, rep) of every key and the (posting slot,
         posting value) pairs in emission order (slot -1: dropped row)."""
         if self.is_cuda:
+            self.expand_runs()
             slot, hi, lo, rep, _ = self.compact()
             n = self.npost
             sp = self.vspec

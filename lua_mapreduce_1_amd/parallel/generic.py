@@ -362,11 +362,14 @@ class GenericMap:
         m, ovf = t.stats()
         if ovf or (t.is_cuda and m > t.cap // 2 + 1):  # (CPU stats count rows: no capacity to respect)
             return False
-        slot, hi, lo, rep, pslot, pval = t.postings()
-        m = int(hi.numel())
-        space = t.cap if t.is_cuda else max(1, m)
         src = self.src.source()
-        off, val = RD.lists_of_postings(slot, pslot, pval, m, space)
+        if t.runs:  # run-length postings: the lists straight from the per-key counts
+            slot, hi, lo, rep, off, val = t.run_lists((m, ovf))
+        else:
+            slot, hi, lo, rep, pslot, pval = t.postings()
+            m = int(hi.numel())
+            space = t.cap if t.is_cuda else max(1, m)
+            off, val = RD.lists_of_postings(slot, pslot, pval, m, space)
         noff, nval = self.reducers.combine(RD.KeyBatch(hi, lo, rep, src), off, val, src=src,
                                            add_bytes=self.add_bytes)
         nt = A.AggTable(t.cap, self.device, None, self.vspec)

@@ -77,6 +77,10 @@ class Tunables:
                                      "general plane: a host reducefn / combinerfn that is exactly emit(sum|min|max("
                                      "values)) (or the accumulate loop) runs batched on the device "
                                      "(parallel/recognize.py)")
+    const_runs: bool = _knob("MR_CONST_RUNS", True,
+                             "general plane, value lists on the GPU: rows that all carry one constant value are "
+                             "counted per key (run-length postings) until a row with another value arrives "
+                             "(ops/agg.py AggTable.runs)")
     agg_l1_probe: bool = _knob("MR_AGG_L1_PROBE", False,
                                "general plane: the per-row table insert probes with plain (vector-L1 cached) "
                                "loads, falling back to agent loads on a stale read (hashtab.h gtab_insert<true>)")

@@ -160,6 +160,62 @@ def test_agg_table_folds_gpu(gpu, dtype, skew):
             assert math.isclose(s0, s1, rel_tol=tol, abs_tol=tol) and a[k][1:] == b[k][1:]
 
 
+def _lists_of(t, text):
+    """A list-mode table's key -> value list (emission order), through the
+    run-length form when the table holds one."""
+    from lua_mapreduce_1_amd import ops
+    from lua_mapreduce_1_amd.parallel import reducers as RD
+    if t.runs:
+        slot, hi, lo, rep, off, val = t.run_lists()
+    else:
+        slot, hi, lo, rep, ps, pv = t.postings()
+        off, val = RD.lists_of_postings(slot, ps, pv, int(hi.numel()), t.cap)
+    kb = ops.key_bytes_list(hi.cpu(), lo.cpu(), rep.cpu(), text.cpu())
+    off, val = off.cpu().tolist(), val.cpu().tolist()
+    return {k: val[off[i]:off[i + 1]] for i, k in enumerate(kb)}
+
+
+@pytest.mark.parametrize("n", [3000, 200_000])
+def test_const_runs_gpu(gpu, monkeypatch, n):
+    """Run-length postings (AggTable.runs): constant-valued rows counted per
+    key give the same lists as explicit postings, also after a row with
+    another value expands them (the constants keep their place before it),
+    with empty spans and long keys mixed in; small batches take the per-row
+    insert, large ones the LDS-combined fold."""
+    import dataclasses
+    from lua_mapreduce_1_amd.ops import agg as A
+    from lua_mapreduce_1_amd.utils import config
+    rng = np.random.default_rng(5)
+    nk = 3000
+    words = [("w%d" % i).encode() * (1 + i % 4) for i in range(nk)]
+    idx = np.minimum(rng.zipf(1.3, n), nk) - 1
+    blob = b"".join(words)
+    off = np.cumsum([0] + [len(w) for w in words])
+    starts = torch.from_numpy(off[:-1][idx].astype(np.int64)).to(gpu)
+    lens = torch.from_numpy(np.array([len(w) for w in words], np.int32)[idx])
+    lens[::89] = 0
+    lens = lens.to(gpu)
+    text = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(gpu)
+    vals = torch.from_numpy(rng.integers(-50, 50, n)).to(gpu)
+    out = {}
+    for runs in (True, False):
+        monkeypatch.setattr(config, "TUNABLES", dataclasses.replace(config.TUNABLES, const_runs=runs))
+        t = A.AggTable(1 << 13, gpu, None, "i64")
+        t.src = text
+        t.insert(n, [], text=text, starts=starts, lens=lens, rep_base=0)        # constant 1
+        t.insert(n // 2, [1], text=text, starts=starts[:n // 2], lens=lens[:n // 2], rep_base=0)
+        assert t.runs == runs
+        first = _lists_of(t, text)
+        t.insert(n, [vals], text=text, starts=starts, lens=lens, rep_base=0)    # expands the runs
+        assert not t.runs
+        t.insert(n // 3, [7], text=text, starts=starts[:n // 3], lens=lens[:n // 3], rep_base=0)
+        out[runs] = (first, _lists_of(t, text))
+    assert out[True][0] == out[False][0] and out[True][1] == out[False][1]
+    assert all(set(v) == {1} for v in out[True][0].values())
+    t.reset()
+    assert t.npost == 0
+
+
 @pytest.mark.parametrize("which,mod,args", CASES, ids=["scores", "bigram", "max_host", "docs", "docs_concat",
                                                        "mixed"])
 def test_generic_gpu_w1(gpu, which, mod, args):

@@ -117,6 +117,7 @@ def run_job(name: str, mod_name: str, store, nbytes: int, check_splits: list[byt
         out["combines_last_step"] = mp.combines
         out["values_after_combine"] = int(mp.table.npost)
         out["values_emitted"] = int(mp.rows)
+        out["recognized_folds"] = dict(mp.reducers.recognized)
     if args.validate and truth is not None:
         t0 = time.time()
         out["validated_full"] = bool(truth(result_pairs(eng, res)))
@@ -222,8 +223,9 @@ def main() -> int:
         W = "lua_mapreduce_1_amd.models.wordcount"
         for red in args.wc_reducers.split(","):
             a = argparse.Namespace(**vars(args))
-            if red == "reducefn2":  # per-key Python combiner + reducer: seconds per step
-                a.steps, a.warmup = min(args.steps, 2), 1
+            from lua_mapreduce_1_amd.utils.config import TUNABLES
+            if red == "reducefn2" and not TUNABLES.recognize_reducers:
+                a.steps, a.warmup = min(args.steps, 2), 1  # per-key Python combiner + reducer: seconds per step
             out = run_job(f"word count, general reducer {red}", W, store, int(off[-1]), None,
                           corpus.EUROPARL_WORDS, "words", a, device,
                           params={"reducefn": "lua_mapreduce_1_amd.examples.WordCount." + red},
