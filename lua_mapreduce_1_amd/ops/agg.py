@@ -185,7 +185,7 @@ class AggTable:
     values of ``list_dtype``).  ``src``: the byte source every rep word
     indexes (set by the owner before inserting long keys)."""
 
-    def __init__(self, capacity: int, device, cols: list | None = None, list_dtype="i64"):
+    def __init__(self, capacity: int, device, cols: list | None = None, list_dtype="i64", runs: bool = False):
         from ..parallel.values import spec_of
         self.device = torch.device(device)
         self.cols_spec = cols
@@ -214,9 +214,12 @@ class AggTable:
         # sort and gather before the combiner.  The first row with another
         # value expands the counts into postings (every earlier row precedes
         # it, so each list's emission order is kept) and the table continues
-        # as plain list mode.
+        # as plain list mode.  Opt-in (``runs``): expanded postings keep each
+        # list's order but not the rows' global order, which a caller pairing
+        # postings with its input rows (the shuffle's receive table) needs.
         from ..utils.config import TUNABLES
-        self._runs = self.is_cuda and self.list_mode and self.vspec.scalar and TUNABLES.const_runs
+        self._runs_opt = bool(runs)
+        self._runs = self._runs_opt and self.is_cuda and self.list_mode and self.vspec.scalar and TUNABLES.const_runs
         self.run_bits: int | None = None  # the constant's value bits (None: no row yet)
         self._run_count: torch.Tensor | None = None
 
@@ -235,7 +238,7 @@ class AggTable:
             self.keys.reset()
             self._fill_cols()
             from ..utils.config import TUNABLES
-            self._runs = self.list_mode and self.vspec.scalar and TUNABLES.const_runs
+            self._runs = self._runs_opt and self.list_mode and self.vspec.scalar and TUNABLES.const_runs
             if self.run_bits is not None and self._run_count is not None:
                 self._run_count.zero_()
             self.run_bits = None
@@ -567,7 +570,8 @@ class AggTable:
 
     def postings(self):
         """List mode: (slot, hi, lo, rep) of every key and the (posting slot,
-        posting value) pairs in emission order (slot -1: dropped row)."""
+        posting value) pairs in emission order (slot -1: dropped row) — for a
+        table that counted runs, each key's postings in order, keys grouped."""
         if self.is_cuda:
             self.expand_runs()
             slot, hi, lo, rep, _ = self.compact()

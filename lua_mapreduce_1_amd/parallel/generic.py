@@ -257,7 +257,7 @@ class GenericMap:
         self.phys = phys
         self.vspec = VL.spec_of(list_dtype)  # list mode: the value row of a posting
         self.list_dtype = self.vspec.dtype
-        self.table = A.AggTable(capacity, self.device, phys.cols if phys is not None else None, self.vspec)
+        self.table = self.new_table(capacity)
         self.src = KeySource(self.device)
         self.emit = GenericEmitter(self)
         self.host: list = []
@@ -274,6 +274,12 @@ class GenericMap:
         # combiner) runs O(log n) times per map, not once per emit call
         self._next_combine = self.combine_at
         self.combines = 0
+
+    def new_table(self, capacity: int) -> A.AggTable:
+        """The map's key table: typed fold columns, or value lists (run-length
+        postings while the values are one constant, ops/agg.py)."""
+        return A.AggTable(capacity, self.device, self.phys.cols if self.phys is not None else None, self.vspec,
+                          runs=True)
 
     @property
     def n_in(self) -> int:
@@ -372,7 +378,7 @@ class GenericMap:
             off, val = RD.lists_of_postings(slot, pslot, pval, m, space)
         noff, nval = self.reducers.combine(RD.KeyBatch(hi, lo, rep, src), off, val, src=src,
                                            add_bytes=self.add_bytes)
-        nt = A.AggTable(t.cap, self.device, None, self.vspec)
+        nt = self.new_table(t.cap)
         nt.src = self.src.source()  # (a combiner may have appended byte values)
         n = int(noff[-1]) if noff.numel() else 0
         if n:
@@ -789,8 +795,7 @@ class GenericPlane:
                                                           and mp.table.is_cuda):
             self._table_restored = False
             # the capacity target moved since this table was made (grown, or fitted)
-            mp.table = A.AggTable(self._cap, eng.device, self.phys.cols if self.phys is not None else None,
-                                  self.dtype)
+            mp.table = mp.new_table(self._cap)
         return streamed
 
     def _map_chunks(self, jobs, recs, j0, j1, streamed: bool) -> list:
@@ -868,8 +873,7 @@ class GenericPlane:
                 continue
             if ovf or n > mp.table.cap // 2:
                 self._cap = ops.next_pow2((16 if ovf else 4) * max(n, 1))  # overflowed: the count is a lower bound
-                mp.table = A.AggTable(self._cap, eng.device, self.phys.cols if self.phys is not None else None,
-                                      self.dtype)
+                mp.table = mp.new_table(self._cap)
                 continue
             fit = max(ops.next_pow2(2 * max(n, 1)), self._cap0)  # load 1/4 - 1/2
             if n > mp.table.cap // 8 and self._cap < fit:
@@ -991,7 +995,7 @@ class GenericPlane:
         mp.src.begin(blob)
         cap = ops.next_pow2(max(1 << 12, 4 * m, self._cap))
         if self.list_mode:
-            mp.table = A.AggTable(cap, d, None, self.vspec)
+            mp.table = mp.new_table(cap)
             kidx = t(a["pkey"])
             pv = t(a["pval"].view(np.int64))
             if self.vspec.has_bytes:

@@ -200,7 +200,7 @@ def test_const_runs_gpu(gpu, monkeypatch, n):
     out = {}
     for runs in (True, False):
         monkeypatch.setattr(config, "TUNABLES", dataclasses.replace(config.TUNABLES, const_runs=runs))
-        t = A.AggTable(1 << 13, gpu, None, "i64")
+        t = A.AggTable(1 << 13, gpu, None, "i64", runs=True)
         t.src = text
         t.insert(n, [], text=text, starts=starts, lens=lens, rep_base=0)        # constant 1
         t.insert(n // 2, [1], text=text, starts=starts[:n // 2], lens=lens[:n // 2], rep_base=0)
