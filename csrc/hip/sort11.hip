@@ -21,6 +21,13 @@ constexpr int T = 256;
 constexpr int WAVES = T / 64;
 constexpr int BINS = 2048;
 constexpr int BPT = BINS / T;  // bins per thread
+// LDS bin arrays are padded by one word per 8 bins: thread t's bins t*8..t*8+7
+// sit at t*9..t*9+7, so the 64 lanes of a wave walking "their j-th bin" hit 64
+// different banks (unpadded, a stride of 8 words: 8 lanes per bank, 8-way
+// conflicts on every per-thread histogram, scan and offset access)
+constexpr int PBINS = BINS + BINS / BPT;
+static_assert(BPT == 8, "pb() pads one word per 8 bins");
+__device__ __forceinline__ u32 pb(u32 b) { return b + (b >> 3); }
 constexpr u64 GR_AGG = 1ull, GR_INC = 2ull;
 
 __device__ __forceinline__ u64 gr_pack(u32 epoch, u64 flag, u64 count) {
@@ -69,8 +76,8 @@ __global__ void __launch_bounds__(T) onesweep11_kernel(const u32* keys_in, const
   constexpr int SUB = TILE / WAVES;
   __shared__ u32 sk[TILE];
   __shared__ u32 sv[TILE];
-  __shared__ u32 wc[WAVES][BINS];
-  __shared__ u32 gout[BINS];
+  __shared__ u32 wc[WAVES][PBINS];
+  __shared__ u32 gout[PBINS];
   __shared__ u32 wsum[WAVES];
   __shared__ u32 sh_tile;
   __shared__ u32 sh_uniform;
@@ -81,7 +88,7 @@ __global__ void __launch_bounds__(T) onesweep11_kernel(const u32* keys_in, const
     sh_tile = atomicAdd(tile_counter, 1u);
     sh_uniform = 0;
   }
-  for (int i = t; i < WAVES * BINS; i += T) (&wc[0][0])[i] = 0;
+  for (int i = t; i < WAVES * PBINS; i += T) (&wc[0][0])[i] = 0;
   u32 gcnt[BPT];
   u32 gsum = 0;
 #pragma unroll
@@ -128,17 +135,17 @@ __global__ void __launch_bounds__(T) onesweep11_kernel(const u32* keys_in, const
       const unsigned long long m = __ballot((d >> b) & 1u);
       peers &= ((d >> b) & 1u) ? m : ~m;
     }
-    const u32 before = valid ? mywc[d] : 0u;
+    const u32 before = valid ? mywc[pb(d)] : 0u;
     myrank[r] = before + (u32)__popcll(peers & below);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): every lane read its counter before the leader updates it
-    if (valid && (peers & below) == 0) mywc[d] = before + (u32)__popcll(peers);
+    if (valid && (peers & below) == 0) mywc[pb(d)] = before + (u32)__popcll(peers);
   }
   __syncthreads();
   u32 mine[BPT];
   u32 msum = 0;
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
-    const int b = t * BPT + j;
+    const int b = t * (BPT + 1) + j;  // pb(t * BPT + j)
     u32 c = 0;
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) c += wc[w][b];
@@ -156,7 +163,7 @@ __global__ void __launch_bounds__(T) onesweep11_kernel(const u32* keys_in, const
     u32 off = lex, goff = gex;
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
-      const int b = t * BPT + j;
+      const int b = t * (BPT + 1) + j;  // pb(t * BPT + j)
       lbase[j] = off;
       gbase[j] = goff;
       u32 o = off;
@@ -176,7 +183,7 @@ __global__ void __launch_bounds__(T) onesweep11_kernel(const u32* keys_in, const
     const u64 i = w0 + (u64)r * 64 + lane;
     if (i < n) {
       const u32 d = (kr[r] >> shift) & mask;
-      const u32 pos = mywc[d] + myrank[r];
+      const u32 pos = mywc[pb(d)] + myrank[r];
       sk[pos] = kr[r];
       sv[pos] = vr[r];
     }
@@ -219,12 +226,12 @@ __global__ void __launch_bounds__(T) onesweep11_kernel(const u32* keys_in, const
       __hip_atomic_store(&G[j], gr_pack(epoch, GR_INC, excl[j] + mine[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #pragma unroll
-  for (int j = 0; j < BPT; ++j) gout[t * BPT + j] = gbase[j] + (u32)excl[j] - lbase[j];
+  for (int j = 0; j < BPT; ++j) gout[t * (BPT + 1) + j] = gbase[j] + (u32)excl[j] - lbase[j];
   __syncthreads();
   const u32 cnt = (u32)min((u64)TILE, n - t0);
   for (u32 i = t; i < cnt; i += T) {
     const u32 k = sk[i];
-    const u32 pos = gout[(k >> shift) & mask] + i;
+    const u32 pos = gout[pb((k >> shift) & mask)] + i;
     keys_out[pos] = k;
     vals_out[pos] = sv[i];
   }
