@@ -285,6 +285,10 @@ class AggTable:
             self.post_val[:n].fill_(self.run_bits)
         self.npost = n
 
+    def run_count(self, slot: torch.Tensor) -> torch.Tensor:
+        """Run-length form: the rows counted for each key slot."""
+        return self._run_count[slot]
+
     def run_lists(self, known: tuple[int, bool] | None = None):
         """Run-length form: (slot, hi, lo, rep) of every key and its list in
         CSR form (off [m + 1], val: the constant repeated) — what

@@ -369,6 +369,8 @@ class GenericMap:
         if ovf or (t.is_cuda and m > t.cap // 2 + 1):  # (CPU stats count rows: no capacity to respect)
             return False
         src = self.src.source()
+        if t.runs and self.reducers.combiner_fold is not None:
+            return self._combine_runs(t, (m, ovf))
         if t.runs:  # run-length postings: the lists straight from the per-key counts
             slot, hi, lo, rep, off, val = t.run_lists((m, ovf))
         else:
@@ -390,6 +392,28 @@ class GenericMap:
             # the reference still writes it (`return k,{}`, job.lua:198-214),
             # so its reducer runs over whatever the other maps sent
             nt.insert_keys(hi[empty], lo[empty], rep[empty])
+        self.table = nt
+        self.combines += 1
+        return True
+
+    def _combine_runs(self, t, known) -> bool:
+        """A recognised fold combiner over run-length postings: key i's list
+        is the constant c repeated cnt[i] times, so its combined value is
+        c * cnt[i] (sum, int64) or c (min / max) — singleton lists unchanged,
+        keys with an empty list kept empty — without materialising the lists."""
+        slot, hi, lo, rep, _ = t.compact(known)
+        cnt = t.run_count(slot)
+        has = cnt > 0
+        c = torch.tensor(t.run_bits, dtype=torch.int64, device=self.device)
+        nval = (c * cnt[has]) if self.reducers.combiner_fold == "sum" else c.expand(int(has.sum())).clone()
+        nt = self.new_table(t.cap)
+        nt.src = self.src.source()
+        n = int(nval.numel())
+        if n:
+            nt.insert(n, self._value_cols(nval), hi=hi[has], lo=lo[has], rep=rep[has])
+        if not bool(has.all()):
+            e = ~has
+            nt.insert_keys(hi[e], lo[e], rep[e])
         self.table = nt
         self.combines += 1
         return True

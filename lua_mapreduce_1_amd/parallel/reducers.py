@@ -243,6 +243,10 @@ class ListReducers:
                 and self.combinerfn is self.reducefn:
             dc = self.device_reducefn  # the combiner is the reducer: so is its batched form
         self.device_combinerfn = dc
+        # 'sum' / 'min' / 'max' when the device combiner is a recognised fold:
+        # lists of one repeated constant then combine without being built
+        # (GenericMap.combine over run-length postings)
+        self.combiner_fold = getattr(dc, "recognized", None)
         if self.reducefn is None and self.device_reducefn is None:
             raise ValueError("a reduce module without device_reduce needs a reducefn (or a device_reducefn)")
         self.aci = all(bool(f(redmod, x)) for x in ("associative_reducer", "commutative_reducer",
