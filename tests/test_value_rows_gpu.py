@@ -80,7 +80,9 @@ def test_device_reducefn_over_bytes_gpu(gpu, monkeypatch):
         return S.count(off)
     monkeypatch.setattr(m, "device_reducefn", device_reducefn, raising=False)
     monkeypatch.setattr(m, "device_reduce", None)
-    monkeypatch.setattr(m, "combinerfn", m.reducefn)  # host combiner over str values, then the device reducer
+    def combinerfn(key, values, emit):  # host combiner over str values (NOT the reducer: device_reducefn
+        m.reducefn(key, values, emit)    # is not its batched form), then the device reducer
+    monkeypatch.setattr(m, "combinerfn", combinerfn)
     splits = si_data()
     eng, res, got = run_engine(SI, splits, gpu, {"num_reducers": 5})
     exp = m.naive(splits)
