@@ -846,6 +846,56 @@ void* mr_host_alloc_coherent(u64 nbytes) {
   return p;
 }
 
+// Small device buffers -> one mapped pinned host buffer, then the host
+// flag, in ONE single-workgroup launch (instead of a blit per buffer plus the
+// signal kernel: the W > 1 iteration downloads five small tensors at its count
+// exchange).  Every thread's stores are vector stores of its own words, each
+// followed by a system-scope fence before the barrier; then one lane stores the
+// flag with release semantics at system scope.
+struct SmallD2H {
+  const void* src[8];
+  unsigned long long bytes[8];
+  unsigned long long off[8];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) small_d2h_kernel(SmallD2H c, u8* dst, unsigned int* flag, unsigned int seq) {
+  for (int j = 0; j < c.n; ++j) {
+    const u64 nb = c.bytes[j];
+    u8* d = dst + c.off[j];
+    if ((nb & 3) == 0) {
+      const u32* s = (const u32*)c.src[j];
+      for (u64 i = threadIdx.x; i < nb / 4; i += blockDim.x) ((u32*)d)[i] = s[i];
+    } else {
+      const u8* s = (const u8*)c.src[j];
+      for (u64 i = threadIdx.x; i < nb; i += blockDim.x) d[i] = s[i];
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// n (<= 8) device buffers srcs[i] of bytes[i] bytes -> host_dst + offs[i]
+// (host_dst: mapped pinned memory, offsets 4-byte aligned), then flag = seq.
+int mr_small_d2h(const void* const* srcs, const u64* bytes, const u64* offs, int n, void* host_dst, void* flag_host,
+                 unsigned int seq, hipStream_t s) {
+  if (n < 0 || n > 8) return -1;
+  void* dp = nullptr;
+  void* fp = nullptr;
+  if (hipHostGetDevicePointer(&dp, host_dst, 0) != hipSuccess || dp == nullptr) return -2;
+  if (hipHostGetDevicePointer(&fp, flag_host, 0) != hipSuccess || fp == nullptr) return -2;
+  SmallD2H c;
+  c.n = n;
+  for (int i = 0; i < 8; ++i) {
+    c.src[i] = i < n ? srcs[i] : nullptr;
+    c.bytes[i] = i < n ? bytes[i] : 0;
+    c.off[i] = i < n ? offs[i] : 0;
+  }
+  hipLaunchKernelGGL(small_d2h_kernel, dim3(1), dim3(256), 0, s, c, (u8*)dp, (unsigned int*)fp, seq);
+  return (int)hipGetLastError();
+}
+
 int mr_signal_host(void* flag_host, unsigned int seq, hipStream_t s) {
   void* dp = nullptr;
   if (hipHostGetDevicePointer(&dp, flag_host, 0) != hipSuccess || dp == nullptr) return -1;

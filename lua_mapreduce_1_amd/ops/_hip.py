@@ -121,6 +121,7 @@ _SIGS = {
     "mr_csv_set_config": [_i32, _i32],
     "mr_agg_set_insert_grid": [_i32],
     "mr_agg_set_l1_probe": [_i32],
+    "mr_small_d2h": [_p, _p, _p, _i32, _p, _p, _u32, _p],
     "mr_sdma_available": [],
     "mr_sort11_set_rounds": [_i32],
     "mr_sort11_tiles": [_u64],
@@ -262,11 +263,20 @@ def wait_stream(device=None) -> None:
     wake-up.  After ``MR_SPIN_US`` (2000) of spinning, falls back to
     hipStreamSynchronize (which also reports a failed kernel).
     ``MR_SPIN_US=0``: always hipStreamSynchronize."""
-    global _FLAGS
-    WAITS[0] += 1
     if SPIN_S <= 0:
+        WAITS[0] += 1
         torch.cuda.current_stream(device).synchronize()
         return
+    flag, k, seq = next_signal(device)
+    call("mr_signal_host", flag, seq, stream(device))
+    spin(k, seq, device)
+
+
+def next_signal(device=None):
+    """(flag address, slot, sequence number) for a completion signal queued
+    on the current stream: the caller's kernel stores ``seq`` there (the
+    signal kernel, or a download that signals itself: mr_small_d2h)."""
+    global _FLAGS
     if _FLAGS is None:
         _FLAGS = _HostFlags()
     F = _FLAGS
@@ -275,21 +285,31 @@ def wait_stream(device=None) -> None:
     if k is None:
         k = F.slot[sp.value] = len(F.slot) % F.nslots
     F.seq = (F.seq + 1) & 0x7FFFFFFF or 1
-    seq = F.seq
-    call("mr_signal_host", ctypes.c_void_p(F.base + 4 * k), seq, sp)
-    w = F.words
+    return ctypes.c_void_p(F.base + 4 * k), k, F.seq
+
+
+def _done(w: int, seq: int) -> bool:
+    # signals of one stream complete in order: a later one seen means ours is done
+    return ((int(w) - seq) & 0x7FFFFFFF) < 0x40000000
+
+
+def spin(k: int, seq: int, device=None) -> None:
+    """Host wait for the signal (slot k, seq): spin on the word, then after
+    MR_SPIN_US fall back to synchronising the current stream."""
+    WAITS[0] += 1
+    w = _FLAGS.words
     if WAIT_LOG is not None:
         t_a = time.perf_counter()
-    if w[k] != seq:
+    if not _done(w[k], seq):
         t_end = time.perf_counter() + SPIN_S
         n = 0
-        while w[k] != seq:
+        while not _done(w[k], seq):
             n += 1
             if (n & 255) == 0 and time.perf_counter() > t_end:
                 torch.cuda.current_stream(device).synchronize()
                 break
     if WAIT_LOG is not None:
-        WAIT_LOG.append((t_a, time.perf_counter(), bool(w[k] == seq)))
+        WAIT_LOG.append((t_a, time.perf_counter(), _done(w[k], seq)))
 
 
 WAITS = [0]  # host waits on a stream so far (tests count them per iteration)

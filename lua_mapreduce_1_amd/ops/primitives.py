@@ -508,6 +508,58 @@ def host_read(t: torch.Tensor) -> np.ndarray:
     return buf[:nb].numpy().view(_NP_DTYPE[t.dtype]).reshape(tuple(t.shape)).copy()
 
 
+class HostRead:
+    """Small device tensors queued for download (host_read_begin); wait()
+    returns their host copies.  Up to 8 tensors of <= 64 KiB in total go in
+    one launch that also signals the host (mr_small_d2h); the host work done
+    between begin and wait overlaps the download."""
+
+    def __init__(self, ts: list):
+        self.ts = [t.contiguous() for t in ts]
+        self.views = None
+        self.sig = None
+        if not self.ts or not self.ts[0].is_cuda:
+            return
+        d = self.ts[0].device
+        self.device = d
+        sizes = [t.numel() * t.element_size() for t in self.ts]
+        total = sum((n + 15) & ~15 for n in sizes)
+        if len(self.ts) > 8 or total > (1 << 16) or _hip.SPIN_S <= 0:
+            return  # host_read_many's blits + wait
+        buf = _SMALL_READ.get(d)
+        if buf is None:
+            p = _hip.lib().mr_host_alloc(1 << 16)
+            if not p:
+                raise RuntimeError("hipHostMalloc of the small-download buffer failed")
+            buf = _SMALL_READ[d] = (p, np.ctypeslib.as_array((ctypes.c_uint8 * (1 << 16)).from_address(p)))
+        offs, off = [], 0
+        for n in sizes:
+            offs.append(off)
+            off += (n + 15) & ~15
+        srcs = (ctypes.c_void_p * 8)(*[t.data_ptr() for t in self.ts])
+        nb = (ctypes.c_uint64 * 8)(*sizes)
+        of = (ctypes.c_uint64 * 8)(*offs)
+        flag, k, seq = _hip.next_signal(d)
+        _hip.call("mr_small_d2h", srcs, nb, of, len(self.ts), ctypes.c_void_p(buf[0]), flag, seq, _hip.stream(d))
+        self.sig = (k, seq)
+        self.views = [(buf[1], o, n, t) for o, n, t in zip(offs, sizes, self.ts)]
+
+    def wait(self) -> list:
+        if self.sig is None:
+            return host_read_many(self.ts)
+        _hip.spin(*self.sig, self.device)
+        return [a[o:o + n].view(_NP_DTYPE[t.dtype]).reshape(tuple(t.shape)).copy() for a, o, n, t in self.views]
+
+
+_SMALL_READ: dict = {}
+
+
+def host_read_begin(ts: list) -> HostRead:
+    """Queue the download of small device tensors on the current stream;
+    ``.wait()`` returns them as numpy arrays (one host wait)."""
+    return HostRead(ts)
+
+
 def host_read_many(ts: list) -> list:
     """Several small device tensors -> host numpy copies with ONE wait (the
     downloads are queued back to back on the current stream)."""

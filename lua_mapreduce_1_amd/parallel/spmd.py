@@ -721,11 +721,14 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                                                      status=(self.table.ctrl, errs))
             with trace.range("mr.count_exchange"):
                 recv = D.exchange_counts(xchg, self.group)
+                # the download (one launch that signals the host) is queued
+                # before the next map is issued, so it runs during that
+                rd = ops.host_read_begin([xchg, recv, self.table.ctrl[:2], cnt] + ([errs] if errs is not None else []))
             if before_sync is not None:
                 before_sync()  # the next iteration's map: queued before this wait
                 before_sync = None
             with trace.range("mr.count_sync"):
-                got = ops.host_read_many([xchg, recv, self.table.ctrl, cnt] + ([errs] if errs is not None else []))
+                got = rd.wait()
             send_h, recv_h = got[0].reshape(W, 3).tolist(), got[1].reshape(W, 3).tolist()
             c = got[2]
             overflow = bool(c[1])

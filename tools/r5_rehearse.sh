@@ -13,3 +13,5 @@ timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 > $OUT/bench_1gpu.log 2
 for ss in 1 0 1; do
   MR_SINGLE_SYNC=$ss timeout -k 10 200 python -u tools/proxy_world.py --world 8 --steps 40 >> $OUT/proxy_w8_ss$ss.log 2>&1 || exit $?
 done
+MR_HOST_TIMELINE=1 timeout -k 10 200 python -u tools/proxy_world.py --world 8 --steps 40 > $OUT/proxy_w8_hosttl.log 2>&1 || exit $?
+MR_COPY_TIMELINE=1 timeout -k 10 200 python -u tools/proxy_world.py --world 8 --steps 40 > $OUT/proxy_w8_copytl.log 2>&1 || exit $?
