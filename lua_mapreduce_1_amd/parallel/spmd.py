@@ -81,6 +81,21 @@ def _engine_streams(device):
     return st[0], list(st[1])
 
 
+def _post_stream(device):
+    """The high-priority stream a W > 1 iteration's post-map work (compaction,
+    pack, count exchange, receive-side insert, tail) runs on, so its short
+    latency-bound kernels are dispatched ahead of the next iteration's map
+    that runs beside them (Tunables.post_stream); None when off."""
+    if device.type != "cuda" or not TUNABLES.post_stream:
+        return None
+    key = (device, "post")
+    ps = _STREAMS.get(key)
+    if ps is None:
+        _least, greatest = torch.cuda.Stream.priority_range()
+        ps = _STREAMS[key] = torch.cuda.Stream(device, priority=greatest)
+    return ps
+
+
 class JobRecord:
     __slots__ = ("key", "value", "status", "repetitions", "started", "written", "cpu_time", "real_time", "worker")
 
@@ -915,7 +930,12 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                         self._run_map(jobs, recs, j0, j1)
             if ahead:
                 self._prefetch_ahead(jobs, j0, j1, q, ahead)
-            return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, ahead, q)
+            cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+            try:
+                return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, ahead, q)
+            finally:
+                if cur is not None:
+                    torch.cuda.set_stream(cur)  # (_finish_iteration may move to the post stream)
 
     def _prefetch_ahead(self, jobs, j0, j1, q: int, ahead: int) -> None:
         """Copies of iterations q+1..q+ahead (their arenas are free: iterations
@@ -984,6 +1004,15 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
             # two host waits per iteration: the count exchange (with the map's
             # checks) and the result download
             trace.push("mr.shuffle_reduce")
+            ps = _post_stream(self.device)
+            if ps is not None:
+                # from here on (through the result download) on the
+                # high-priority stream, behind this iteration's map; the
+                # caller restores the current stream
+                ev = torch.cuda.Event()
+                ev.record()
+                ps.wait_event(ev)
+                torch.cuda.set_stream(ps)
             src, rcounts, rows, n_claimed = self._exchange_single_sync(jobs, recs, j0, j1, issue_next_map)
             T["map"] = time.time() - t0
             if getattr(self, "_exact_tail", False):
