@@ -123,13 +123,9 @@ _SIGS = {
     "mr_agg_set_l1_probe": [_i32],
     "mr_small_d2h": [_p, _p, _p, _i32, _p, _p, _u32, _p],
     "mr_sdma_available": [],
-    "mr_sort11_set_rounds": [_i32],
-    "mr_sort11_tiles": [_u64],
-    "mr_hist11": [_p, _u64, _p, _p],
-    "mr_radix_onesweep11": [_p, _p, _p, _p, _u64, _i32, _u32, _p, _p, _p, _u32, _p, _i32, _p],
     "mr_sdma_d2h": [_p, _p, _p, _i32],
 }
-_RESTYPE_U64 = {"mr_sort11_tiles", "mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
+_RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
                 "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words"}
 
 
@@ -157,8 +153,6 @@ def lib():
             raise ValueError(f"MR_SORT_ROUNDS={TUNABLES.sort_rounds}: must be 16, 24 or 32")
         if L.mr_csv_set_config(TUNABLES.csv_tiles, TUNABLES.csv_mode) != 0:
             raise ValueError(f"MR_CSV_TILES={TUNABLES.csv_tiles} / MR_CSV_MODE={TUNABLES.csv_mode}: 0..64 / 0..2")
-        if L.mr_sort11_set_rounds(TUNABLES.sort11_rounds) != 0:
-            raise ValueError(f"MR_SORT11_ROUNDS={TUNABLES.sort11_rounds}: must be 8, 16, 24 or 32")
         if L.mr_agg_set_insert_grid(TUNABLES.agg_insert_grid) != 0:
             raise ValueError(f"MR_AGG_INSERT_GRID={TUNABLES.agg_insert_grid}: must be >= 256")
         L.mr_agg_set_l1_probe(1 if TUNABLES.agg_l1_probe else 0)

@@ -607,7 +607,6 @@ def _onesweep_tiles(n: int) -> int:
 
 def _sort_ws(d, n: int):
     """Per-device workspace for the onesweep sort (grown, never shrunk)."""
-    _LAST11.pop(d, None)  # an 8-bit sort: sort_error reads this workspace's error word
     tiles = _onesweep_tiles(n)
     ws = _SORT_WS.get(d)
     if ws is None or ws["tiles"] < tiles:
@@ -722,8 +721,6 @@ def sort_keys32(k32: torch.Tensor, ghist: torch.Tensor | None = None, bits: int 
     d = k32.device
     if n == 0:
         return torch.zeros(0, dtype=torch.int32, device=d), k32[:0]
-    if TUNABLES.sort32_digit_bits == 11 and bits == 32 and n >= (1 << 20):
-        return _sort_keys32_11(k32)
     if ghist is None:
         raise ValueError("sort_keys32 on the GPU needs the digit histograms (records.keys32 computes them)")
     s = _hip.stream(d)
@@ -744,45 +741,6 @@ def sort_keys32(k32: torch.Tensor, ghist: torch.Tensor | None = None, bits: int 
     return pin, kin
 
 
-_SORT11_WS: dict = {}
-
-
-def _sort_keys32_11(k32: torch.Tensor):
-    """sort_keys32 in THREE onesweep passes of 11 + 11 + 10 bits
-    (csrc/hip/sort11.hip; ``MR_SORT32_DIGIT_BITS=11``): its own histogram
-    pass ([3][2048] bins), 2048 look-back granules per tile."""
-    n = k32.numel()
-    d = k32.device
-    s = _hip.stream(d)
-    lib = _hip.lib()
-    tiles = int(lib.mr_sort11_tiles(n))
-    ws = _SORT11_WS.get(d)
-    if ws is None or ws["tiles"] < tiles:
-        ws = {"tiles": tiles, "granules": torch.zeros(tiles * 2048, dtype=torch.int64, device=d),
-              "small": torch.zeros(3 * 2048 + 64 + 1, dtype=torch.int32, device=d)}
-        _SORT11_WS[d] = ws
-    small = ws["small"]
-    small.zero_()
-    _hip.call("mr_hist11", _hip.ptr(k32), n, _hip.ptr(small[:3 * 2048]), s)
-    kbuf = [torch.empty(n, dtype=torch.int32, device=d) for _ in range(2)]
-    pbuf = [torch.empty(n, dtype=torch.int32, device=d) for _ in range(2)]
-    kin, pin = k32.contiguous(), None
-    for pass_id, (shift, mask) in enumerate(((0, 0x7FF), (11, 0x7FF), (22, 0x3FF))):
-        _EPOCH[0] = (_EPOCH[0] + 1) & 0xFFFFFF or 1
-        kout = kbuf[0] if kin is not kbuf[0] else kbuf[1]
-        pout = pbuf[0] if pin is not pbuf[0] else pbuf[1]
-        _hip.call("mr_radix_onesweep11", _hip.ptr(kin), _hip.ptr(pin), _hip.ptr(kout), _hip.ptr(pout), n, shift, mask,
-                  _hip.ptr(small[pass_id * 2048:(pass_id + 1) * 2048]), _hip.ptr(ws["granules"]),
-                  _hip.ptr(small[3 * 2048 + pass_id:]), _EPOCH[0], _hip.ptr(small[3 * 2048 + 64:]),
-                  1 if pin is None else 0, s)
-        kin, pin = kout, pout
-    _SORT11_ERR[d] = small[3 * 2048 + 64:]
-    _LAST11[d] = True
-    return pin, kin
-
-
-_SORT11_ERR: dict = {}
-_LAST11: dict = {}  # device -> the last u32 sort took the 11-bit passes (sort_error reads its error word)
 
 
 def sort_by_partition_key(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, val: torch.Tensor,
@@ -828,8 +786,6 @@ def sort_error(device) -> bool:
     """True if a onesweep look-back of the last sort_keys call on ``device``
     gave up (that sort's order is invalid).  Synchronises."""
     d = torch.device(device)
-    if _LAST11.get(d):
-        return bool(int(_SORT11_ERR[d].item()) != 0)
     ws = _SORT_WS.get(d)
     return bool(ws is not None and int(ws["small"][2112].item()) != 0)
 
@@ -837,8 +793,6 @@ def sort_error(device) -> bool:
 def sort_error_word(device) -> torch.Tensor | None:
     """Device int32[1] error word of the last sort_keys call (no sync)."""
     d = torch.device(device)
-    if _LAST11.get(d):
-        return _SORT11_ERR[d][:1]
     ws = _SORT_WS.get(d)
     return None if ws is None else ws["small"][2112:2113]
 

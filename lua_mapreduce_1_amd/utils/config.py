@@ -60,10 +60,6 @@ class Tunables:
     sort_rounds: int = _knob("MR_SORT_ROUNDS", 24,
                              "keys per thread of the onesweep radix tiles of sorts of >= 4 M keys (256 x rounds "
                              "keys per tile; 16, 24 or 32)")
-    sort32_digit_bits: int = _knob("MR_SORT32_DIGIT_BITS", 8,
-                                   "radix digit of the u32 prefix sorts of >= 1 M keys (record plane): 8 (four onesweep "
-                                   "passes, sort.hip) or 11 (three passes of 11 + 11 + 10 bits, sort11.hip)")
-    sort11_rounds: int = _knob("MR_SORT11_ROUNDS", 16, "keys per thread of the 11-bit onesweep tiles (8/16/24/32)")
     csv_tiles: int = _knob("MR_CSV_TILES", 0,
                            "fused CSV fold (emit.csv): 8 KiB tiles per workgroup (0 = auto: up to 4 while the "
                            "launch keeps >= 1024 workgroups)")

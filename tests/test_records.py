@@ -314,29 +314,3 @@ def test_records_checkpoint_formats(tmp_path, fmt):
     assert eng2.maps_restored == (1 if fmt == "legacy" else 0)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("rounds", [8, 16, 32])
-def test_sort11_passes_gpu(gpu, rounds, monkeypatch):
-    """The 11-bit onesweep (three passes of 11 + 11 + 10 bits,
-    csrc/hip/sort11.hip) gives the same stable permutation as a host stable
-    sort of the u32 keys (uniform and skewed keys)."""
-    import dataclasses
-    from lua_mapreduce_1_amd.ops import _hip
-    from lua_mapreduce_1_amd.ops import primitives as P
-    assert _hip.lib().mr_sort11_set_rounds(rounds) == 0
-    try:
-        monkeypatch.setattr(P, "TUNABLES", dataclasses.replace(P.TUNABLES, sort32_digit_bits=11))
-        g = torch.Generator().manual_seed(rounds)
-        for skew in (False, True):
-            n = 3_000_017
-            k = torch.randint(0, 2**32, (n,), generator=g, dtype=torch.int64)
-            if skew:
-                k = k & 0xFFF0000F  # few distinct middle digits, long runs of equal digits
-            k32 = (k - (1 << 32) * (k >= 2**31).to(torch.int64)).to(torch.int32)
-            perm, sk = P.sort_keys32(k32.to(gpu), None)
-            assert not P.sort_error(gpu)
-            want = np.argsort(k.numpy().astype(np.uint64), kind="stable")
-            assert np.array_equal(perm.long().cpu().numpy(), want)
-            assert torch.equal(sk.cpu(), k32[torch.from_numpy(want)])
-    finally:
-        _hip.lib().mr_sort11_set_rounds(16)
