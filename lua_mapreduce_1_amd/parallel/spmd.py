@@ -81,19 +81,53 @@ def _engine_streams(device):
     return st[0], list(st[1])
 
 
-def _post_stream(device):
-    """The high-priority stream a W > 1 iteration's post-map work (compaction,
-    pack, count exchange, receive-side insert, tail) runs on, so its short
-    latency-bound kernels are dispatched ahead of the next iteration's map
-    that runs beside them (Tunables.post_stream); None when off."""
-    if device.type != "cuda" or not TUNABLES.post_stream:
+def _cu_masks(ncu: int, k: int) -> tuple[list[int], list[int]]:
+    """(rest, reserved) CU masks (u32 words) reserving k of ncu CUs, spread
+    evenly over the 8 XCDs whether CU ids run XCD by XCD or interleave across
+    them: in each block of 32 ids, block x reserves the ids whose residue mod 8
+    is one of k/32 residues starting at x."""
+    per = max(1, min(8, k // 32))
+    words = (ncu + 31) // 32
+    rest, res = [0] * words, [0] * words
+    for i in range(ncu):
+        x = (i // 32) % 8
+        if (i % 8) in {(x + j * (8 // per)) % 8 for j in range(per)}:
+            res[i // 32] |= 1 << (i % 32)
+        else:
+            rest[i // 32] |= 1 << (i % 32)
+    return rest, res
+
+
+def _masked_streams(device):
+    """W > 1 with Tunables.post_cus > 0: ([two map streams], post stream) —
+    the post-map chain (compaction, pack, count exchange, receive-side
+    insert, tail) on post_cus CUs of its own, the maps on the others, so
+    neither waits for the other's workgroups to leave a CU (csrc/hip/streams.hip);
+    None when off or unavailable."""
+    k = int(TUNABLES.post_cus)
+    if device.type != "cuda" or k <= 0:
         return None
-    key = (device, "post")
-    ps = _STREAMS.get(key)
-    if ps is None:
-        _least, greatest = torch.cuda.Stream.priority_range()
-        ps = _STREAMS[key] = torch.cuda.Stream(device, priority=greatest)
-    return ps
+    key = (device, "masked", k)
+    st = _STREAMS.get(key)
+    if st is None:
+        import ctypes
+        from ..ops import _hip
+        lib = _hip.lib()
+        with torch.cuda.device(device):
+            ncu = lib.mr_device_cus()
+            if ncu <= 2 * k:
+                return None
+            rest, res = _cu_masks(ncu, k)
+            handles = []
+            for m in (rest, rest, res):
+                arr = (ctypes.c_uint32 * len(m))(*m)
+                h = lib.mr_stream_cumask(arr, len(m))
+                if not h:
+                    return None
+                handles.append(h)
+        ss = [torch.cuda.ExternalStream(h, device=device) for h in handles]
+        st = _STREAMS[key] = (ss[:2], ss[2])
+    return list(st[0]), st[1]
 
 
 class JobRecord:
@@ -288,6 +322,11 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         self._pending = None
         self._rec_tmpl = None
         self.copy_stream, self.streams = _engine_streams(self.device)
+        self.post_stream = None
+        if self.world > 1 or self.force_shuffle:
+            ms = _masked_streams(self.device)
+            if ms is not None:
+                self.streams, self.post_stream = ms
         self._plans: dict = {}
         # per slot (pipelined iterations alternate): device event timers, the
         # job ranges of the map chunks and their device error words
@@ -1004,7 +1043,7 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
             # two host waits per iteration: the count exchange (with the map's
             # checks) and the result download
             trace.push("mr.shuffle_reduce")
-            ps = _post_stream(self.device)
+            ps = self.post_stream
             if ps is not None:
                 # from here on (through the result download) on the
                 # high-priority stream, behind this iteration's map; the

@@ -73,10 +73,10 @@ class Tunables:
                                      "general plane: a host reducefn / combinerfn that is exactly emit(sum|min|max("
                                      "values)) (or the accumulate loop) runs batched on the device "
                                      "(parallel/recognize.py)")
-    post_stream: bool = _knob("MR_POST_STREAM", True,
-                              "SPMD W > 1: the post-map work of an iteration (compaction, pack, count exchange, "
-                              "receive-side insert, tail) runs on a high-priority stream, ahead of the next "
-                              "iteration's map beside it")
+    post_cus: int = _knob("MR_POST_CUS", 32,
+                          "SPMD W > 1: CUs reserved for the post-map work of an iteration (compaction, pack, count "
+                          "exchange, receive-side insert, tail), the maps running on the others (CU-masked "
+                          "streams, csrc/hip/streams.hip); 0 = every stream on every CU")
     const_runs: bool = _knob("MR_CONST_RUNS", True,
                              "general plane, value lists on the GPU: rows that all carry one constant value are "
                              "counted per key (run-length postings) until a row with another value arrives "
