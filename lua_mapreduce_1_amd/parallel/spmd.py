@@ -1052,7 +1052,11 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                 ev.record()
                 ps.wait_event(ev)
                 torch.cuda.set_stream(ps)
-            src, rcounts, rows, n_claimed = self._exchange_single_sync(jobs, recs, j0, j1, issue_next_map)
+            # MR_SERIAL_MAP: the next map waits for this iteration's tail (queued
+            # after it, gated on its end) instead of running beside it
+            serial = TUNABLES.serial_map
+            src, rcounts, rows, n_claimed = self._exchange_single_sync(jobs, recs, j0, j1,
+                                                                       None if serial else issue_next_map)
             T["map"] = time.time() - t0
             if getattr(self, "_exact_tail", False):
                 n_red = self._reduce_insert_received(src, rcounts, rows)
@@ -1099,6 +1103,10 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                                           blob_cap=getattr(self, "_blob_cap", None))
         if timer is not None:
             timer.mark("tail_end")
+        if single and TUNABLES.serial_map and next_map[0] and self.device.type == "cuda":
+            gate = torch.cuda.Event()
+            gate.record()
+            issue_next_map(gate)
         issue_next_map()
 
         with trace.range("mr.finalize_host"):
