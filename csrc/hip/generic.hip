@@ -145,7 +145,6 @@ __device__ __forceinline__ void span_key(const u8* text, u64 s, u64 len, u64& hi
 // into the slot's columns, or append its posting.  Rows with an empty span
 // (len <= 0) are skipped (list mode: posting slot -1).  An insert that runs
 // out of probes sets the table's overflow flag; the host regrows and re-runs.
-template <bool L1>
 __global__ void __launch_bounds__(256) agg_insert_kernel(GTab g, Keys ks, u64 n, Cols c) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   u32 claims = 0;
@@ -169,7 +168,7 @@ __global__ void __launch_bounds__(256) agg_insert_kernel(GTab g, Keys ks, u64 n,
     u64 slot = 0;
     int r = 0;
     if (ok) {
-      r = gtab_insert<L1>(g, hi, lo, 0, rep, OP_NONE, &slot);
+      r = gtab_insert(g, hi, lo, 0, rep, OP_NONE, &slot);
       claims += r == 2;
     }
     if (c.list) {
@@ -798,20 +797,12 @@ static Cols to_cols(const ColsArg* a) {
 // reducefn3 6.57-6.62 vs 6.60-6.91 vs 6.73-6.76 ms, profiles/r4/agg_grid_ab);
 // set from Tunables.agg_insert_grid (MR_AGG_INSERT_GRID) by the binding
 static unsigned g_ins_cap = 65536u;
-// 1: the per-row insert probes through the vector L1 (gtab_insert<true>);
-// set from Tunables.agg_l1_probe (MR_AGG_L1_PROBE)
-static int g_l1_probe = 0;
 
 extern "C" {
 
 int mr_agg_set_insert_grid(int cap) {
   if (cap < 256) return -1;
   g_ins_cap = (unsigned)cap;
-  return 0;
-}
-
-int mr_agg_set_l1_probe(int on) {
-  g_l1_probe = on ? 1 : 0;
   return 0;
 }
 
@@ -851,12 +842,8 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
                        ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
     return (int)hipGetLastError();
   }
-  if (g_l1_probe)
-    hipLaunchKernelGGL(agg_insert_kernel<true>, dim3(ag_grid(n, 256, g_ins_cap)), dim3(256), 0, stream,
-                       ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
-  else
-    hipLaunchKernelGGL(agg_insert_kernel<false>, dim3(ag_grid(n, 256, g_ins_cap)), dim3(256), 0, stream,
-                       ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
+  hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256, g_ins_cap)), dim3(256), 0, stream,
+                     ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a));
   return (int)hipGetLastError();
 }
 

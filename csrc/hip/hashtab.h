@@ -72,15 +72,6 @@ __device__ __forceinline__ void fold_value(long long* p, long long v, int op) {
 // (optional) receives the key's slot index — a dense-ish key id.  Callers count
 // claims locally and publish them with gtab_count_claims (one atomic per wave:
 // a same-address atomic per claim serialised ~3e5 adds in the map kernel).
-//
-// L1 = true: the probe's tag / lo / hi loads are plain (vector-L1 cached: a
-// Zipf vocabulary's hot keys hit the CU's L1 instead of an L2 round trip per
-// row).  A plain load can only be stale in the safe direction: a tag read as 0
-// goes to the CAS, which returns the slot's real tag; a lo read as 0 is
-// re-read with an agent (L1-bypassing) load; a hi that mismatches is re-read
-// after the acquire fence as before.  (Tags and lo only ever go 0 -> final
-// within a launch, and the L1 is invalidated at every launch.)
-template <bool L1 = false>
 __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long long v, u64 rep, int op,
                                            u64* out_slot = nullptr) {
   const u64 tag = gtab_tag(hi, lo);
@@ -88,7 +79,7 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
   u64 slot = gtab_home(tag, t.mask);
   u32 probes = 0;
   while (probes < GTAB_MAX_PROBES) {
-    u64 cur = L1 ? t.tag[slot] : ld_agent(&t.tag[slot]);
+    u64 cur = ld_agent(&t.tag[slot]);
     if (cur == 0) {
       u64 expected = 0;
       if (__hip_atomic_compare_exchange_strong(&t.tag[slot], &expected, tag, __ATOMIC_RELAXED,
@@ -122,12 +113,8 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
       // hi and lo) and our lo while differing in hi, i.e. a 56-bit collision of
       // two keys' (hi, lo) hashes, ~2^-56 per probe pair.  Keys of <= 7 bytes
       // (exact tags) never get here; long keys still compare bytes.
-      u64 l = L1 ? t.lo[slot] : ld_agent(&t.lo[slot]);
-      u64 h = L1 ? t.hi[slot] : ld_agent(&t.hi[slot]);
-      if (L1 && l == 0) {
-        l = ld_agent(&t.lo[slot]);
-        h = ld_agent(&t.hi[slot]);
-      }
+      const u64 l = ld_agent(&t.lo[slot]);
+      u64 h = ld_agent(&t.hi[slot]);
       if (l == 0) continue;  // claimed but not yet published: re-read this slot
       if (l == lo) {
         if (h != hi) {

@@ -120,7 +120,6 @@ _SIGS = {
     "mr_posting_keys": [_p, ctypes.c_longlong, _p, ctypes.c_longlong, ctypes.c_longlong, _p, _p, _p],
     "mr_csv_set_config": [_i32, _i32],
     "mr_agg_set_insert_grid": [_i32],
-    "mr_agg_set_l1_probe": [_i32],
     "mr_small_d2h": [_p, _p, _p, _i32, _p, _p, _u32, _p],
     "mr_device_cus": [],
     "mr_stream_cumask": [_p, _u32],
@@ -159,7 +158,6 @@ def lib():
             raise ValueError(f"MR_CSV_TILES={TUNABLES.csv_tiles} / MR_CSV_MODE={TUNABLES.csv_mode}: 0..64 / 0..2")
         if L.mr_agg_set_insert_grid(TUNABLES.agg_insert_grid) != 0:
             raise ValueError(f"MR_AGG_INSERT_GRID={TUNABLES.agg_insert_grid}: must be >= 256")
-        L.mr_agg_set_l1_probe(1 if TUNABLES.agg_l1_probe else 0)
         if L.mr_rec_gather_set_rows(TUNABLES.rec_gather_rows) != 0:
             raise ValueError(f"MR_REC_GATHER_ROWS={TUNABLES.rec_gather_rows}: must be 128 or 256")
         _LIB = L

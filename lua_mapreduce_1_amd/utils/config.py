@@ -84,9 +84,6 @@ class Tunables:
                              "general plane, value lists on the GPU: rows that all carry one constant value are "
                              "counted per key (run-length postings) until a row with another value arrives "
                              "(ops/agg.py AggTable.runs)")
-    agg_l1_probe: bool = _knob("MR_AGG_L1_PROBE", False,
-                               "general plane: the per-row table insert probes with plain (vector-L1 cached) "
-                               "loads, falling back to agent loads on a stale read (hashtab.h gtab_insert<true>)")
     rec_gather_rows: int = _knob("MR_REC_GATHER_ROWS", 256,
                                  "record plane: rows per workgroup batch of the 16-byte row gather (256, or 128: "
                                  "half the LDS image, more workgroups per CU)")
