@@ -121,9 +121,6 @@ _SIGS = {
     "mr_csv_set_config": [_i32, _i32],
     "mr_agg_set_insert_grid": [_i32],
     "mr_small_d2h": [_p, _p, _p, _i32, _p, _p, _u32, _p],
-    "mr_device_cus": [],
-    "mr_stream_cumask": [_p, _u32],
-    "mr_stream_destroy": [_p],
     "mr_sdma_available": [],
     "mr_sdma_d2h": [_p, _p, _p, _i32],
 }
@@ -149,7 +146,6 @@ def lib():
         L.mr_host_alloc_coherent.restype = _p
         L.mr_host_alloc.argtypes = [_u64]
         L.mr_host_alloc.restype = _p
-        L.mr_stream_cumask.restype = _p
         L.mr_host_free.argtypes = [_p]
         L.mr_host_free.restype = _i32
         if L.mr_sort_set_rounds(TUNABLES.sort_rounds) != 0:

@@ -81,55 +81,6 @@ def _engine_streams(device):
     return st[0], list(st[1])
 
 
-def _cu_masks(ncu: int, k: int) -> tuple[list[int], list[int]]:
-    """(rest, reserved) CU masks (u32 words) reserving k of ncu CUs, spread
-    evenly over the 8 XCDs whether CU ids run XCD by XCD or interleave across
-    them: in each block of 32 ids, block x reserves the ids whose residue mod 8
-    is one of k/32 residues starting at x."""
-    per = max(1, min(8, k // 32))
-    words = (ncu + 31) // 32
-    rest, res = [0] * words, [0] * words
-    for i in range(ncu):
-        x = (i // 32) % 8
-        if (i % 8) in {(x + j * (8 // per)) % 8 for j in range(per)}:
-            res[i // 32] |= 1 << (i % 32)
-        else:
-            rest[i // 32] |= 1 << (i % 32)
-    return rest, res
-
-
-def _masked_streams(device):
-    """W > 1 with Tunables.post_cus > 0: ([two map streams], post stream) —
-    the post-map chain (compaction, pack, count exchange, receive-side
-    insert, tail) on post_cus CUs of its own, the maps on the others, so
-    neither waits for the other's workgroups to leave a CU (csrc/hip/streams.hip);
-    None when off or unavailable."""
-    k = int(TUNABLES.post_cus)
-    if device.type != "cuda" or k <= 0:
-        return None
-    key = (device, "masked", k)
-    st = _STREAMS.get(key)
-    if st is None:
-        import ctypes
-        from ..ops import _hip
-        lib = _hip.lib()
-        with torch.cuda.device(device):
-            ncu = lib.mr_device_cus()
-            if ncu <= 2 * k:
-                return None
-            rest, res = _cu_masks(ncu, k)
-            handles = []
-            for m in (rest, rest, res):
-                arr = (ctypes.c_uint32 * len(m))(*m)
-                h = lib.mr_stream_cumask(arr, len(m))
-                if not h:
-                    return None
-                handles.append(h)
-        ss = [torch.cuda.ExternalStream(h, device=device) for h in handles]
-        st = _STREAMS[key] = (ss[:2], ss[2])
-    return list(st[0]), st[1]
-
-
 class JobRecord:
     __slots__ = ("key", "value", "status", "repetitions", "started", "written", "cpu_time", "real_time", "worker")
 
@@ -322,11 +273,6 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         self._pending = None
         self._rec_tmpl = None
         self.copy_stream, self.streams = _engine_streams(self.device)
-        self.post_stream = None
-        if self.world > 1 or self.force_shuffle:
-            ms = _masked_streams(self.device)
-            if ms is not None:
-                self.streams, self.post_stream = ms
         self._plans: dict = {}
         # per slot (pipelined iterations alternate): device event timers, the
         # job ranges of the map chunks and their device error words
@@ -969,12 +915,7 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                         self._run_map(jobs, recs, j0, j1)
             if ahead:
                 self._prefetch_ahead(jobs, j0, j1, q, ahead)
-            cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
-            try:
-                return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, ahead, q)
-            finally:
-                if cur is not None:
-                    torch.cuda.set_stream(cur)  # (_finish_iteration may move to the post stream)
+            return self._finish_iteration(res, T, t_start, t0, jobs, recs, j0, j1, ahead, q)
 
     def _prefetch_ahead(self, jobs, j0, j1, q: int, ahead: int) -> None:
         """Copies of iterations q+1..q+ahead (their arenas are free: iterations
@@ -1043,20 +984,7 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
             # two host waits per iteration: the count exchange (with the map's
             # checks) and the result download
             trace.push("mr.shuffle_reduce")
-            ps = self.post_stream
-            if ps is not None:
-                # from here on (through the result download) on the
-                # high-priority stream, behind this iteration's map; the
-                # caller restores the current stream
-                ev = torch.cuda.Event()
-                ev.record()
-                ps.wait_event(ev)
-                torch.cuda.set_stream(ps)
-            # MR_SERIAL_MAP: the next map waits for this iteration's tail (queued
-            # after it, gated on its end) instead of running beside it
-            serial = TUNABLES.serial_map
-            src, rcounts, rows, n_claimed = self._exchange_single_sync(jobs, recs, j0, j1,
-                                                                       None if serial else issue_next_map)
+            src, rcounts, rows, n_claimed = self._exchange_single_sync(jobs, recs, j0, j1, issue_next_map)
             T["map"] = time.time() - t0
             if getattr(self, "_exact_tail", False):
                 n_red = self._reduce_insert_received(src, rcounts, rows)
@@ -1103,10 +1031,6 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                                           blob_cap=getattr(self, "_blob_cap", None))
         if timer is not None:
             timer.mark("tail_end")
-        if single and TUNABLES.serial_map and next_map[0] and self.device.type == "cuda":
-            gate = torch.cuda.Event()
-            gate.record()
-            issue_next_map(gate)
         issue_next_map()
 
         with trace.range("mr.finalize_host"):

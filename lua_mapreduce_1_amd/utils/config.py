@@ -73,13 +73,6 @@ class Tunables:
                                      "general plane: a host reducefn / combinerfn that is exactly emit(sum|min|max("
                                      "values)) (or the accumulate loop) runs batched on the device "
                                      "(parallel/recognize.py)")
-    post_cus: int = _knob("MR_POST_CUS", 0,
-                          "SPMD W > 1: CUs reserved for the post-map work of an iteration (compaction, pack, count "
-                          "exchange, receive-side insert, tail), the maps running on the others (CU-masked "
-                          "streams, csrc/hip/streams.hip); 0 = every stream on every CU")
-    serial_map: bool = _knob("MR_SERIAL_MAP", False,
-                             "SPMD W > 1 (single sync): the next iteration's map is gated on this iteration's tail "
-                             "instead of running beside its post-map chain")
     const_runs: bool = _knob("MR_CONST_RUNS", True,
                              "general plane, value lists on the GPU: rows that all carry one constant value are "
                              "counted per key (run-length postings) until a row with another value arrives "
