@@ -688,14 +688,16 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
 
     def _send_bound(self) -> int:
         """Rows the send-side compaction is launched for: the table's slots on
-        a first map, else the last map's key count plus a quarter (rounded, so
-        the workspaces keep their shape); a map with more keys is flagged by
-        the compaction and redone with its count."""
+        a first map, else the last map's key count plus a quarter (rounded to
+        4096 rows, so the workspaces keep their shape across iterations; the
+        round-4 rounding to 64 K had the W = 8 reduce tail sort 131 K rows for
+        54 K keys); a map with more keys is flagged by the compaction and
+        redone with its count."""
         est = getattr(self, "_send_est", None)
         if est is None:
             return self.table.cap
         b = est + est // 4 + 4096
-        return min(self.table.cap, (b + 0xFFFF) & ~0xFFFF)
+        return min(self.table.cap, (b + 0xFFF) & ~0xFFF)
 
     def _exchange_single_sync(self, jobs, recs, j0: int, j1: int, before_sync):
         """Compaction, pack and count exchange queued straight behind the
@@ -789,7 +791,7 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         if guess is None:
             return max(rows, 1)
         b = guess + guess // 4 + 4096
-        return max(1, min(rows, (b + 0xFFFF) & ~0xFFFF))
+        return max(1, min(rows, (b + 0xFFF) & ~0xFFF))
 
     def _reduce_insert_received(self, rbuf, recv_counts, rows: int) -> int:
         """Received records -> this rank's reduce table (one insert launch);
