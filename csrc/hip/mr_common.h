@@ -136,6 +136,23 @@ MR_HD u64 make_rep(u64 off, u64 len) { return (off << REP_LEN_BITS) | (len < REP
 MR_HD u64 rep_off(u64 rep) { return rep >> REP_LEN_BITS; }
 MR_HD u64 rep_len(u64 rep) { return rep & REP_LEN_MASK; }
 
+// FNV-1 of a table key's bytes (packed in (hi, lo), or at rep in src for a
+// long key) and its length.
+MR_HD u32 key_fnv(u64 h, u64 l, u64 r, const u8* src, u32* len_out) {
+  u32 f = FNV_OFFSET;
+  u32 len;
+  if (!key_is_long(l)) {
+    len = packed_len(l);
+    for (u32 k = 0; k < len; ++k) f = fnv1_step(f, packed_byte(h, l, k));
+  } else {
+    len = (u32)rep_len(r);
+    const u8* p = src + rep_off(r);
+    for (u32 k = 0; k < len; ++k) f = fnv1_step(f, p[k]);
+  }
+  *len_out = len;
+  return f;
+}
+
 // Reduction operators for hash aggregation / reduce-by-key.
 // OP_NONE: the table only maps keys to slots (a vocabulary: the inverted
 // index's word ids) — inserts fold nothing, so a hit costs one load, no atomic.

@@ -150,6 +150,136 @@ __global__ void __launch_bounds__(T) pk_scatter_kernel(const u64* __restrict__ h
   }
 }
 
+// ---------------------------------------------------------------------------
+// Send side straight from the map's hash table (the W > 1 single-sync
+// iteration): three launches instead of the compaction's three plus the
+// pack's four, and no dense intermediate columns.
+//   cp_count   : per table block (one slot per thread), per destination, the
+//                rows and key bytes of its occupied slots -> bcnt[block][2W]
+//   cp_scan    : one workgroup: per (destination, rows | bytes) column, the
+//                exclusive prefix over the blocks (one wave per column),
+//                segment starts, the count-exchange row and the status
+//                (table overflow, chunk errors, send buffer too small)
+//   cp_scatter : each slot again -> its record + key bytes at the block's
+//                base in its destination's segment (LDS-atomic ranks inside
+//                the block: order inside a segment is irrelevant, the
+//                receiver re-aggregates by key)
+constexpr int CP = 512;  // table slots per block
+
+__device__ __forceinline__ bool cp_slot(const GTab& g, u64 cap, u64 i, u32 nparts, u32 W, const u8* src, u64& h,
+                                        u64& l, u64& r, u32& d, u32& len) {
+  if (i >= cap || g.tag[i] == 0) return false;
+  h = g.hi[i];
+  l = g.lo[i];
+  r = g.rep[i];
+  const u32 f = key_fnv(h, l, r, src, &len);
+  d = (nparts ? f % nparts : f) % W;
+  return true;
+}
+
+__global__ void __launch_bounds__(CP) cp_count_kernel(GTab g, u64 cap, u32 nparts, u32 W, const u8* __restrict__ src,
+                                                      u32* __restrict__ bcnt) {
+  __shared__ u32 rc[MAXW], bc[MAXW];
+  for (u32 k = threadIdx.x; k < W; k += CP) rc[k] = bc[k] = 0;
+  __syncthreads();
+  u64 h, l, r;
+  u32 d, len;
+  if (cp_slot(g, cap, (u64)blockIdx.x * CP + threadIdx.x, nparts, W, src, h, l, r, d, len)) {
+    atomicAdd(&rc[d], 1u);
+    atomicAdd(&bc[d], len);
+  }
+  __syncthreads();
+  u32* out = bcnt + (u64)blockIdx.x * 2 * W;
+  for (u32 k = threadIdx.x; k < W; k += CP) {
+    out[k] = rc[k];
+    out[W + k] = bc[k];
+  }
+}
+
+// One workgroup of 1024 threads; column c of bcnt ([nb][2W]) is scanned by
+// waves c, c + 16, ... (one wave per column at a time).  rows_out: the table's occupied slots (the map's key count).
+constexpr int CS = 1024;
+__global__ void __launch_bounds__(CS) cp_scan_kernel(u32* __restrict__ bcnt, u64 nb, u32 W,
+                                                     unsigned long long* __restrict__ start, long long* __restrict__ xchg,
+                                                     long long extra, const u32* __restrict__ ovf,
+                                                     const int* __restrict__ errs, u32 nerr,
+                                                     unsigned long long* __restrict__ rows_out, u64 buf_cap) {
+  __shared__ unsigned long long tot[2 * MAXW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const u32 C = 2 * W;
+  const u64 per = (nb + 63) / 64;  // blocks per lane
+  for (u32 c = wave; c < C; c += CS / 64) {
+    const u64 a = (u64)lane * per, b = a + per < nb ? a + per : nb;
+    unsigned long long sum = 0;
+    for (u64 j = a; j < b; ++j) sum += bcnt[j * C + c];
+    unsigned long long incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    unsigned long long run = incl - sum;
+    for (u64 j = a; j < b; ++j) {
+      const u32 x = bcnt[j * C + c];
+      bcnt[j * C + c] = (u32)run;  // exclusive base of block j in column c
+      run += x;
+    }
+    if (lane == 63) tot[c] = incl;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  bool redo = ovf && *ovf;
+  for (u32 k = 0; errs && k < nerr; ++k) redo |= errs[k] != 0;
+  unsigned long long off = 0, rows = 0;
+  for (u32 d = 0; d < W; ++d) {
+    start[d] = off;                 // destination d's records
+    start[W + d] = off + 32 * tot[d];  // and its key bytes
+    off += seg_bytes(tot[d], tot[W + d]);
+    rows += tot[d];
+  }
+  redo |= off > buf_cap;  // the send buffer (sized from the row bound) is too small
+  for (u32 d = 0; d < W; ++d) {
+    xchg[3 * d] = (long long)tot[d];
+    xchg[3 * d + 1] = (long long)tot[W + d];
+    xchg[3 * d + 2] = extra + (redo ? STATUS_REDO : 0);
+  }
+  *rows_out = rows;
+}
+
+__global__ void __launch_bounds__(CP) cp_scatter_kernel(GTab g, u64 cap, u32 nparts, u32 W, const u8* __restrict__ src,
+                                                        const u32* __restrict__ bcnt,
+                                                        const unsigned long long* __restrict__ start, u8* __restrict__ buf,
+                                                        u64 buf_cap) {
+  __shared__ u32 rc[MAXW], bc[MAXW];
+  for (u32 k = threadIdx.x; k < W; k += CP) rc[k] = bc[k] = 0;
+  __syncthreads();
+  u64 h = 0, l = 0, r = 0;
+  u32 d = 0, len = 0, rpos = 0, bpos = 0;
+  const bool live = cp_slot(g, cap, (u64)blockIdx.x * CP + threadIdx.x, nparts, W, src, h, l, r, d, len);
+  if (live) {
+    rpos = atomicAdd(&rc[d], 1u);
+    bpos = atomicAdd(&bc[d], len);
+  }
+  if (!live) return;  // (no barrier below)
+  const u32* base = bcnt + (u64)blockIdx.x * 2 * W;
+  const u64 ro = start[d] + 32 * ((u64)base[d] + rpos);
+  const u64 boff = (u64)base[W + d] + bpos;  // inside destination d's byte segment
+  const u64 bo = start[W + d] + boff;
+  if (ro + 32 > buf_cap || bo + len > buf_cap) return;  // too small: flagged by cp_scan, the exchange is redone
+  u64* rr = reinterpret_cast<u64*>(buf + ro);
+  rr[0] = h;
+  rr[1] = l;
+  rr[2] = (u64)g.val[blockIdx.x * (u64)CP + threadIdx.x];
+  rr[3] = make_rep(boff, len);
+  u8* out = buf + bo;
+  if (!key_is_long(l)) {
+    for (u32 k = 0; k < len; ++k) out[k] = (u8)packed_byte(h, l, k);
+  } else {
+    const u8* p = src + rep_off(r);
+    for (u32 k = 0; k < len; ++k) out[k] = p[k];
+  }
+}
+
 // Received records from source s carry offsets relative to s's byte segment;
 // make them absolute: loc += byte_start(s) << 24, s found from the record
 // prefix counts (rstart[W+1] / bstart[W] on the device).
@@ -257,6 +387,42 @@ int mr_pack_by_dest(const void* hi, const void* lo, const void* val, const void*
                        (const long long*)val, (const u64*)rep, (const u32*)part, n, W, (const u8*)src,
                        (const unsigned long long*)start, cursor, (u8*)rec, (u8*)blob, (const unsigned long long*)n_dev);
   }
+  return (int)hipGetLastError();
+}
+
+// The send side from the map's table in three launches (cp_* above): ws =
+// u32 [nb][2W] block counts (nb = ceil(cap / 512)) + 4W u64; buf (buf_cap
+// bytes) receives the per-destination segments [records | key bytes];
+// xchg = the count-exchange row [W][3]; rows_out (u64, device) = the table's
+// occupied slots.  extra gets STATUS_REDO when the table overflowed, a chunk
+// error word is set or the segments do not fit buf.
+u64 mr_compact_pack_ws_bytes(u64 cap, u32 W) {
+  const u64 nb = (cap + pk::CP - 1) / pk::CP;
+  return ((nb * 2 * W * 4 + 255) & ~255ull) + 2 * (u64)W * 8;
+}
+
+int mr_compact_pack(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, u32 nparts, u32 W,
+                    const void* src, void* ws, void* buf, u64 buf_cap, void* xchg, long long extra, const void* errs,
+                    u32 nerr, void* rows_out, hipStream_t s) {
+  if (W == 0 || W > (u32)pk::MAXW || cap == 0) return -1;
+  GTab g;
+  g.tag = (u64*)tag;
+  g.hi = (u64*)hi;
+  g.lo = (u64*)lo;
+  g.val = (long long*)val;
+  g.rep = (u64*)rep;
+  g.ctrl = (u32*)ctrl;
+  g.mask = cap - 1;
+  g.src = (const u8*)src;
+  const u64 nb = (cap + pk::CP - 1) / pk::CP;
+  u32* bcnt = (u32*)ws;
+  unsigned long long* start = (unsigned long long*)((u8*)ws + ((nb * 2 * W * 4 + 255) & ~255ull));
+  hipLaunchKernelGGL(pk::cp_count_kernel, dim3((unsigned)nb), dim3(pk::CP), 0, s, g, cap, nparts, W, (const u8*)src,
+                     bcnt);
+  hipLaunchKernelGGL(pk::cp_scan_kernel, dim3(1), dim3(pk::CS), 0, s, bcnt, nb, W, start, (long long*)xchg, extra,
+                     (const u32*)ctrl + 1, (const int*)errs, nerr, (unsigned long long*)rows_out, buf_cap);
+  hipLaunchKernelGGL(pk::cp_scatter_kernel, dim3((unsigned)nb), dim3(pk::CP), 0, s, g, cap, nparts, W, (const u8*)src,
+                     (const u32*)bcnt, (const unsigned long long*)start, (u8*)buf, buf_cap);
   return (int)hipGetLastError();
 }
 

@@ -24,20 +24,6 @@ namespace tl {
 
 constexpr int T = 256;
 
-__device__ __forceinline__ u32 key_fnv(u64 h, u64 l, u64 r, const u8* src, u32* len_out) {
-  u32 f = FNV_OFFSET;
-  u32 len;
-  if (!key_is_long(l)) {
-    len = packed_len(l);
-    for (u32 k = 0; k < len; ++k) f = fnv1_step(f, packed_byte(h, l, k));
-  } else {
-    len = (u32)rep_len(r);
-    const u8* p = src + rep_off(r);
-    for (u32 k = 0; k < len; ++k) f = fnv1_step(f, p[k]);
-  }
-  *len_out = len;
-  return f;
-}
 
 // Compaction of a table's occupied slots into dense rows, in launches sized
 // for parallelism (one slot per thread; the first version gave each thread 4-16

@@ -121,10 +121,13 @@ _SIGS = {
     "mr_csv_set_config": [_i32, _i32],
     "mr_agg_set_insert_grid": [_i32],
     "mr_small_d2h": [_p, _p, _p, _i32, _p, _p, _u32, _p],
+    "mr_compact_pack_ws_bytes": [_u64, _u32],
+    "mr_compact_pack": [_p, _p, _p, _p, _p, _p, _u64, _u32, _u32, _p, _p, _p, _u64, _p, ctypes.c_longlong, _p, _u32,
+                        _p, _p],
     "mr_sdma_available": [],
     "mr_sdma_d2h": [_p, _p, _p, _i32],
 }
-_RESTYPE_U64 = {"mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
+_RESTYPE_U64 = {"mr_compact_pack_ws_bytes", "mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
                 "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words"}
 
 

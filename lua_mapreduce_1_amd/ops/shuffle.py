@@ -93,6 +93,37 @@ def pack_by_dest_combined(hi, lo, val, rep, part, W: int, src, extra: int = 0, n
     return buf, xchg
 
 
+def compact_pack(table, src, nparts: int, W: int, bound: int, extra: int = 0, errs=None, cap_bytes: int | None = None):
+    """The W > 1 single-sync send side straight from the map's hash table
+    (csrc/hip/shuffle.hip mr_compact_pack: three launches, no dense
+    columns): every occupied slot -> its destination (FNV-1 partition of the
+    key bytes, mod W) -> one uint8 buffer of per-destination segments
+    [records (32 B) | key bytes], sized for ``bound`` rows; plus the
+    count-exchange row and the table's key count on the device.  A rank
+    whose table overflowed, whose chunk error words are set (``errs``) or
+    whose segments outgrow the buffer adds STATUS_REDO to its exchanged
+    extra column.  ``cap_bytes`` (tests): the buffer capacity the kernels
+    assume, instead of the bound's.  -> (buf uint8, xchg int64 [3W], rows
+    int64 [1])."""
+    d = table.device
+    lib = _hip.lib()
+    cap = 32 * bound + (src.numel() if src is not None else 0) + 16 * bound + 8 * W
+    ws, buf = _combined_bufs(d, W, cap)
+    ncap = buf.numel() if cap_bytes is None else min(int(cap_bytes), buf.numel())
+    nws = int(lib.mr_compact_pack_ws_bytes(table.cap, W))
+    cw = _CP_WS.get(d)
+    if cw is None or cw.numel() < nws:
+        cw = _CP_WS[d] = torch.empty(nws + nws // 4, dtype=torch.uint8, device=d)
+    xchg = torch.empty(3 * W, dtype=torch.int64, device=d)
+    rows = torch.empty(1, dtype=torch.int64, device=d)
+    e, ne = (_hip.ptr(errs), int(errs.numel())) if errs is not None and errs.numel() else (None, 0)
+    _hip.call("mr_compact_pack", *table._gtab(), table.cap, nparts, W, _hip.ptr(src) if src is not None else None,
+              _hip.ptr(cw), _hip.ptr(buf), ncap, _hip.ptr(xchg), int(extra), e, ne, _hip.ptr(rows),
+              _hip.stream(d))
+    return buf, xchg, rows
+
+
+_CP_WS: dict = {}
 _COMBINED: dict = {}
 
 

@@ -714,13 +714,13 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
             src = self._source()
             failed = sum(1 for r in recs[j0:j1] if r.status == STATUS.FAILED)
             bound = self._send_bound()
-            with trace.range("mr.compact"):
-                hi, lo, val, rep, part, cnt = devmod.compact_partition(self.table, bound, src, self.nparts, bound=True)
             nch = len(self._chunks[self.tslot])
             errs = self._errs[self.tslot][:nch] if nch and self._errs[self.tslot] is not None else None
-            with trace.range("mr.pack"):
-                buf, xchg = SH.pack_by_dest_combined(hi, lo, val, rep, part, W, src, extra=failed, n_dev=cnt,
-                                                     status=(self.table.ctrl, errs))
+            with trace.range("mr.compact_pack"):
+                # table -> per-destination segments in three launches (no dense columns)
+                buf, xchg, cnt = SH.compact_pack(self.table, src, self.nparts, W, bound, extra=failed, errs=errs,
+                                                 cap_bytes=getattr(self, "_send_cap_test", None))
+                self._send_cap_test = None  # (a test's one-shot: a send buffer too small)
             with trace.range("mr.count_exchange"):
                 recv = D.exchange_counts(xchg, self.group)
                 # the download (one launch that signals the host) is queued

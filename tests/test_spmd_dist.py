@@ -166,6 +166,7 @@ def _single_sync_worker(port, q, mode):
     for i in range(n_it):
         if i == 3 and mode == "send_bound":
             eng._send_est = 100      # the compaction's bound is too small: flagged, exchange redone
+            eng._send_cap_test = 4096  # and its send buffer (the bound sizes it with room to spare)
         if i == 3 and mode == "red_bound":
             eng._red_distinct = 100  # the padded tail's bound is too small: TailBoundError, tail re-run
         w0 = _hip.WAITS[0]
