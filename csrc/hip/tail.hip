@@ -42,8 +42,14 @@ constexpr int T = 256;
 constexpr int CT = 512;  // compaction threads per block (one slot each)
 constexpr int HIST_BLOCKS = 64;
 
-__global__ void __launch_bounds__(CT) tail_count_kernel(const u64* __restrict__ tag, u64 cap, u32* __restrict__ bcount) {
+// zero (optional): the tail's zeroed scratch (histograms, tile counters,
+// flags), cleared by block 0 here instead of by a separate memset launch
+// (everything that uses it runs after this kernel)
+__global__ void __launch_bounds__(CT) tail_count_kernel(const u64* __restrict__ tag, u64 cap, u32* __restrict__ bcount,
+                                                        u32* __restrict__ zero, u32 zwords) {
   __shared__ u32 wc[CT / 64];
+  if (zero && blockIdx.x == 0)
+    for (u32 k = threadIdx.x; k < zwords; k += CT) zero[k] = 0u;
   const u64 i = (u64)blockIdx.x * CT + threadIdx.x;
   const bool o = i < cap && tag[i] != 0;
   const u64 m = __ballot(o);
@@ -173,6 +179,51 @@ __global__ void __launch_bounds__(T) tail_hist_kernel(const u64* __restrict__ c,
     atomicAdd((unsigned long long*)&pcount[t], (unsigned long long)hist[7][t]);
 }
 
+// Padded mode (a row BOUND): tail_pad_kernel and tail_hist_kernel in one
+// launch — the sentinel rows [count, bound) are written and their composite
+// keys histogrammed with the real ones (one launch less in the W > 1 tail).
+__global__ void __launch_bounds__(T) tail_padhist_kernel(const unsigned long long* __restrict__ counter, u64 bound,
+                                                         u64* __restrict__ out_hi, u64* __restrict__ out_lo,
+                                                         long long* __restrict__ out_val, u64* __restrict__ out_rep,
+                                                         u32* __restrict__ out_part, u64* __restrict__ out_c,
+                                                         const u32* __restrict__ ovf, u32* __restrict__ bad,
+                                                         u32* ghist, u32 nparts, long long* pcount) {
+  __shared__ u32 hist[8][256];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) hist[b][t] = 0;
+  const u64 cnt = *counter;
+  const u64 n = cnt < bound ? cnt : bound;
+  if (blockIdx.x == 0 && t == 0) {
+    u32 b = cnt > bound ? 8u : 0u;
+    if (ovf && *ovf) b |= 16u;
+    if (b) atomicOr(bad, b);
+  }
+  __syncthreads();
+  for (u64 i = (u64)blockIdx.x * T + t; i < bound; i += (u64)gridDim.x * T) {
+    u64 x;
+    if (i < n) {
+      x = out_c[i];
+    } else {
+      x = (0xFFull << 56) | i;
+      out_hi[i] = 0;
+      out_lo[i] = 0;
+      out_val[i] = 0;
+      out_rep[i] = 0;
+      out_part[i] = 0xFFu;
+      out_c[i] = x;
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) atomicAdd(&hist[b][(x >> (8 * b)) & 0xFF], 1u);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+    if (hist[b][t]) atomicAdd(&ghist[b * 256 + t], hist[b][t]);
+  if (pcount && (u32)t < nparts && hist[7][t])
+    atomicAdd((unsigned long long*)&pcount[t], (unsigned long long)hist[7][t]);
+}
+
 __global__ void tail_gather_kernel(const u32* __restrict__ perm, u64 n, const u64* __restrict__ hi,
                                    const u64* __restrict__ lo, const long long* __restrict__ val,
                                    const u64* __restrict__ rep, const u32* __restrict__ part, u64* __restrict__ o_hi,
@@ -233,10 +284,25 @@ u64 mr_tail_bhist_bytes(u64 cap) { return ((cap + tl::CT - 1) / tl::CT * 4 + 255
 // `counter` still says how many there were).  pad != 0: n is a row BOUND, the
 // rows [count, n) become sentinels (tail_pad_kernel; nparts <= 255) and the
 // histograms cover all n rows; `bad` gets the bound / overflow flags.
+static int tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, u32 nparts,
+                        const void* src, void* out_hi, void* out_lo, void* out_val, void* out_rep, void* out_part,
+                        void* out_c, void* counter, void* ghist, void* pcount, void* bhist, u64 n, u64 out_cap, int pad,
+                        void* bad, void* zero, u32 zbytes, hipStream_t s);
+
 int mr_tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, u32 nparts,
                     const void* src, void* out_hi, void* out_lo, void* out_val, void* out_rep, void* out_part,
                     void* out_c, void* counter, void* ghist, void* pcount, void* bhist, u64 n, u64 out_cap, int pad,
                     void* bad, hipStream_t s) {
+  return tail_compact(tag, hi, lo, val, rep, ctrl, cap, nparts, src, out_hi, out_lo, out_val, out_rep, out_part, out_c,
+                      counter, ghist, pcount, bhist, n, out_cap, pad, bad, nullptr, 0, s);
+}
+
+}  // extern "C"
+
+static int tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, u32 nparts,
+                        const void* src, void* out_hi, void* out_lo, void* out_val, void* out_rep, void* out_part,
+                        void* out_c, void* counter, void* ghist, void* pcount, void* bhist, u64 n, u64 out_cap, int pad,
+                        void* bad, void* zero, u32 zbytes, hipStream_t s) {
   if (nparts > 256 || bhist == nullptr || (pad && (nparts > 255 || bad == nullptr))) return -1;
   GTab g;
   g.tag = (u64*)tag;
@@ -249,11 +315,20 @@ int mr_tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* c
   g.src = nullptr;
   const u64 nb = (cap + tl::CT - 1) / tl::CT;
   u32* bcount = (u32*)bhist;
-  hipLaunchKernelGGL(tl::tail_count_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, (const u64*)tag, cap, bcount);
+  hipLaunchKernelGGL(tl::tail_count_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, (const u64*)tag, cap, bcount,
+                     (u32*)zero, zbytes / 4);
   hipLaunchKernelGGL(tl::tail_bscan_kernel, dim3(1), dim3(tl::BS), 0, s, bcount, nb, (unsigned long long*)counter);
   hipLaunchKernelGGL(tl::tail_scatter_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, g, cap, nparts, (const u8*)src,
                      (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
                      (const u32*)bcount, out_cap);
+  if (pad && n > 0 && ghist != nullptr) {
+    u64 hb = (n + 4 * tl::T - 1) / (4 * tl::T);
+    if (hb > (u64)tl::HIST_BLOCKS) hb = tl::HIST_BLOCKS;
+    hipLaunchKernelGGL(tl::tail_padhist_kernel, dim3((unsigned)hb), dim3(tl::T), 0, s, (const unsigned long long*)counter,
+                       n, (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
+                       (const u32*)ctrl + 1, (u32*)bad, (u32*)ghist, nparts, (long long*)pcount);
+    return (int)hipGetLastError();
+  }
   if (pad && n > 0) {
     u64 pb = (n + 255) / 256;
     if (pb > 1024) pb = 1024;
@@ -269,6 +344,9 @@ int mr_tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* c
   }
   return (int)hipGetLastError();
 }
+
+extern "C" {
+
 int mr_tail_gather(const void* perm, u64 n, const void* hi, const void* lo, const void* val, const void* rep,
                    const void* part, void* o_hi, void* o_lo, void* o_val, void* o_rep, void* o_part, void* o_len,
                    hipStream_t s) {
@@ -355,11 +433,10 @@ int mr_tail_run(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl,
   u8* w = (u8*)ws;
   auto P = [&](int b) { return (void*)(w + off[b]); };
   u8* z = w + off[TB_ZERO];
-  int rc = (int)hipMemsetAsync(z, 0, TZ_BYTES, s);
-  if (rc) return rc;
-  rc = mr_tail_compact(tag, hi, lo, val, rep, ctrl, cap, nparts, src, P(TB_HI0), P(TB_LO0), P(TB_VAL0), P(TB_REP0),
-                       P(TB_PART0), P(TB_C), z, z + TZ_GHIST, z + TZ_PCOUNT, P(TB_BHIST), n, n, padded,
-                       z + TZ_BAD, s);
+  // (the zeroed scratch z is cleared by the compaction's first kernel)
+  int rc = tail_compact(tag, hi, lo, val, rep, ctrl, cap, nparts, src, P(TB_HI0), P(TB_LO0), P(TB_VAL0), P(TB_REP0),
+                        P(TB_PART0), P(TB_C), z, z + TZ_GHIST, z + TZ_PCOUNT, P(TB_BHIST), n, n, padded, z + TZ_BAD,
+                        z, (u32)TZ_BYTES, s);
   if (rc) return rc;
   // 8 onesweep passes over the composite key (ghist from tail_compact)
   const void* kin = P(TB_C);

@@ -783,8 +783,11 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         guess = getattr(self, "_red_distinct", None)
         want = 2 * (guess + guess // 4) if guess is not None else 2 * rows
         cap = ops.next_pow2(max(1 << 16, min(2 * rows, want)))
+        ev, self._red_reset_ev = getattr(self, "_red_reset_ev", None), None
         if self.red_table is None or self.red_table.cap != cap:
             self.red_table = ops.HashTable(cap, device=self.device, op=self.op)
+        elif ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)  # reset after the last tail (off this chain)
         else:
             self.red_table.reset()
         self.red_table.insert_received(rbuf, recv_counts, self.world, rows=rows)
@@ -1066,6 +1069,13 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                                                     n_red if sh else n_claimed, src, padded=padded)
         if padded:
             self._red_distinct = int(cols["val"].size)
+            if self.device.type == "cuda":
+                # the reduce table is cleared now, while the host reads the
+                # results and issues the next iteration, instead of at the
+                # head of the next iteration's post-map chain
+                self.red_table.reset()
+                self._red_reset_ev = torch.cuda.Event()
+                self._red_reset_ev.record()
         if cols.get("exact_fallback"):
             self._exact_tail = True  # later iterations go straight to the exact order
         digits = len(str(max(self.nparts - 1, 0)))
