@@ -106,7 +106,7 @@ def test_sort_keys_matches_lexsort(gpu):
 
 def test_scan_and_bincount(gpu):
     rng = np.random.default_rng(4)
-    for n in (1, 4095, 4096, 70_001, 3_000_000):
+    for n in (1, 4095, 4096, 16_385, 70_001, 131_072, 131_073, 3_000_000):  # small, mid (one launch), large
         x = torch.from_numpy(rng.integers(0, 50, n).astype(np.int64))
         o, tot = ops.exclusive_scan(x.to(gpu))
         oc, tc = ops.exclusive_scan(x)
