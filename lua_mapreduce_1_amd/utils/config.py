@@ -57,6 +57,9 @@ class Tunables:
     pin_exact: bool = _knob("MR_PIN_EXACT", True,
                             "split buffers in exact-size pinned memory (mr_host_alloc) instead of torch's "
                             "power-of-two pinned pool")
+    sort_small_rounds: int = _knob("MR_SORT_SMALL_ROUNDS", 4,
+                                   "keys per thread of the onesweep tiles of sorts of <= 2^18 keys (4, 8 or 16: "
+                                   "1024- to 4096-key tiles; fewer tiles, a shorter look-back chain)")
     sort_rounds: int = _knob("MR_SORT_ROUNDS", 24,
                              "keys per thread of the onesweep radix tiles of sorts of >= 4 M keys (256 x rounds "
                              "keys per tile; 16, 24 or 32)")
