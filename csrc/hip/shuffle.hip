@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(T) pk_scatter_kernel(const u64* __restrict__ h
 // Send side straight from the map's hash table (the W > 1 single-sync
 // iteration): three launches instead of the compaction's three plus the
 // pack's four, and no dense intermediate columns.
-//   cp_count   : per table block (one slot per thread), per destination, the
+//   cp_count   : per table block (4096 slots, 8 per thread), per destination, the
 //                rows and key bytes of its occupied slots -> bcnt[2W][block]
 //   cp_scan    : one workgroup: per (destination, rows | bytes) column, the
 //                exclusive prefix over the blocks (one wave per column),
@@ -164,7 +164,8 @@ __global__ void __launch_bounds__(T) pk_scatter_kernel(const u64* __restrict__ h
 //                base in its destination's segment (LDS-atomic ranks inside
 //                the block: order inside a segment is irrelevant, the
 //                receiver re-aggregates by key)
-constexpr int CP = 512;  // table slots per block
+constexpr int CP = 512;       // threads per block
+constexpr int CP_PER = 8;     // table slots per thread: 4096 per block, so the block-count scan stays short
 
 __device__ __forceinline__ bool cp_slot(const GTab& g, u64 cap, u64 i, u32 nparts, u32 W, const u8* src, u64& h,
                                         u64& l, u64& r, u32& d, u32& len) {
@@ -182,11 +183,15 @@ __global__ void __launch_bounds__(CP) cp_count_kernel(GTab g, u64 cap, u32 npart
   __shared__ u32 rc[MAXW], bc[MAXW];
   for (u32 k = threadIdx.x; k < W; k += CP) rc[k] = bc[k] = 0;
   __syncthreads();
-  u64 h, l, r;
-  u32 d, len;
-  if (cp_slot(g, cap, (u64)blockIdx.x * CP + threadIdx.x, nparts, W, src, h, l, r, d, len)) {
-    atomicAdd(&rc[d], 1u);
-    atomicAdd(&bc[d], len);
+  const u64 i0 = (u64)blockIdx.x * CP * CP_PER + threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < CP_PER; ++it) {
+    u64 h, l, r;
+    u32 d, len;
+    if (cp_slot(g, cap, i0 + (u64)it * CP, nparts, W, src, h, l, r, d, len)) {
+      atomicAdd(&rc[d], 1u);
+      atomicAdd(&bc[d], len);
+    }
   }
   __syncthreads();
   const u64 nb = gridDim.x;  // column-major [2W][nb]: a column's blocks are contiguous for the scan
@@ -199,7 +204,7 @@ __global__ void __launch_bounds__(CP) cp_count_kernel(GTab g, u64 cap, u32 npart
 // One workgroup of 1024 threads; column c of bcnt ([2W][nb], column-major)
 // is scanned by one wave (waves c, c + 16, ...): lane l owns the blocks
 // [l * per, (l + 1) * per), read 8 at a time with their loads issued together
-// (a dependent load per block cost ~1 us each: 56 us per scan at nb = 2048).
+// (with 512-slot blocks, nb = 2048, this scan took 56 us; 4096-slot blocks keep nb, and it, small).
 // rows_out: the table's occupied slots (the map's key count).
 constexpr int CS = 1024;
 constexpr int CS_U = 8;
@@ -269,30 +274,31 @@ __global__ void __launch_bounds__(CP) cp_scatter_kernel(GTab g, u64 cap, u32 npa
   __shared__ u32 rc[MAXW], bc[MAXW];
   for (u32 k = threadIdx.x; k < W; k += CP) rc[k] = bc[k] = 0;
   __syncthreads();
-  u64 h = 0, l = 0, r = 0;
-  u32 d = 0, len = 0, rpos = 0, bpos = 0;
-  const bool live = cp_slot(g, cap, (u64)blockIdx.x * CP + threadIdx.x, nparts, W, src, h, l, r, d, len);
-  if (live) {
-    rpos = atomicAdd(&rc[d], 1u);
-    bpos = atomicAdd(&bc[d], len);
-  }
-  if (!live) return;  // (no barrier below)
   const u64 nb = gridDim.x;
-  const u64 ro = start[d] + 32 * ((u64)bcnt[(u64)d * nb + blockIdx.x] + rpos);
-  const u64 boff = (u64)bcnt[(u64)(W + d) * nb + blockIdx.x] + bpos;  // inside destination d's byte segment
-  const u64 bo = start[W + d] + boff;
-  if (ro + 32 > buf_cap || bo + len > buf_cap) return;  // too small: flagged by cp_scan, the exchange is redone
-  u64* rr = reinterpret_cast<u64*>(buf + ro);
-  rr[0] = h;
-  rr[1] = l;
-  rr[2] = (u64)g.val[blockIdx.x * (u64)CP + threadIdx.x];
-  rr[3] = make_rep(boff, len);
-  u8* out = buf + bo;
-  if (!key_is_long(l)) {
-    for (u32 k = 0; k < len; ++k) out[k] = (u8)packed_byte(h, l, k);
-  } else {
-    const u8* p = src + rep_off(r);
-    for (u32 k = 0; k < len; ++k) out[k] = p[k];
+  const u64 i0 = (u64)blockIdx.x * CP * CP_PER + threadIdx.x;
+  for (int it = 0; it < CP_PER; ++it) {
+    const u64 i = i0 + (u64)it * CP;
+    u64 h = 0, l = 0, r = 0;
+    u32 d = 0, len = 0;
+    if (!cp_slot(g, cap, i, nparts, W, src, h, l, r, d, len)) continue;
+    const u32 rpos = atomicAdd(&rc[d], 1u);
+    const u32 bpos = atomicAdd(&bc[d], len);
+    const u64 ro = start[d] + 32 * ((u64)bcnt[(u64)d * nb + blockIdx.x] + rpos);
+    const u64 boff = (u64)bcnt[(u64)(W + d) * nb + blockIdx.x] + bpos;  // inside destination d's byte segment
+    const u64 bo = start[W + d] + boff;
+    if (ro + 32 > buf_cap || bo + len > buf_cap) continue;  // too small: flagged by cp_scan, the exchange is redone
+    u64* rr = reinterpret_cast<u64*>(buf + ro);
+    rr[0] = h;
+    rr[1] = l;
+    rr[2] = (u64)g.val[i];
+    rr[3] = make_rep(boff, len);
+    u8* out = buf + bo;
+    if (!key_is_long(l)) {
+      for (u32 k = 0; k < len; ++k) out[k] = (u8)packed_byte(h, l, k);
+    } else {
+      const u8* p = src + rep_off(r);
+      for (u32 k = 0; k < len; ++k) out[k] = p[k];
+    }
   }
 }
 
@@ -407,13 +413,13 @@ int mr_pack_by_dest(const void* hi, const void* lo, const void* val, const void*
 }
 
 // The send side from the map's table in three launches (cp_* above): ws =
-// u32 [nb][2W] block counts (nb = ceil(cap / 512)) + 4W u64; buf (buf_cap
+// u32 [2W][nb] block counts (nb = ceil(cap / 4096)) + 2W u64; buf (buf_cap
 // bytes) receives the per-destination segments [records | key bytes];
 // xchg = the count-exchange row [W][3]; rows_out (u64, device) = the table's
 // occupied slots.  extra gets STATUS_REDO when the table overflowed, a chunk
 // error word is set or the segments do not fit buf.
 u64 mr_compact_pack_ws_bytes(u64 cap, u32 W) {
-  const u64 nb = (cap + pk::CP - 1) / pk::CP;
+  const u64 nb = (cap + pk::CP * pk::CP_PER - 1) / (pk::CP * pk::CP_PER);
   return ((nb * 2 * W * 4 + 255) & ~255ull) + 2 * (u64)W * 8;
 }
 
@@ -430,7 +436,7 @@ int mr_compact_pack(void* tag, void* hi, void* lo, void* val, void* rep, void* c
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
   g.src = (const u8*)src;
-  const u64 nb = (cap + pk::CP - 1) / pk::CP;
+  const u64 nb = (cap + pk::CP * pk::CP_PER - 1) / (pk::CP * pk::CP_PER);
   u32* bcnt = (u32*)ws;
   unsigned long long* start = (unsigned long long*)((u8*)ws + ((nb * 2 * W * 4 + 255) & ~255ull));
   hipLaunchKernelGGL(pk::cp_count_kernel, dim3((unsigned)nb), dim3(pk::CP), 0, s, g, cap, nparts, W, (const u8*)src,

@@ -590,62 +590,11 @@ __global__ void __launch_bounds__(SS_THREADS) scan_small_kernel(const T* in, T* 
   if (t == 0 && total) *total = all;
 }
 
-// single-launch exclusive scan for mid-size arrays (<= 1024 * SM_MAX elements,
-// e.g. the W > 1 tail's ~10^5 key lengths, which took three launches): each
-// thread's contiguous elements are read in batches of SS_ITEMS with their
-// loads issued together, summed, block-scanned, then re-read and written.
-constexpr int SM_MAX = 128;
-template <typename T>
-__global__ void __launch_bounds__(SS_THREADS) scan_mid_kernel(const T* in, T* out, u64 n, T* total) {
-  __shared__ T sh[SS_THREADS / 64];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const u64 per = (n + SS_THREADS - 1) / SS_THREADS;  // <= SM_MAX
-  const u64 b = (u64)t * per, e = b + per < n ? b + per : n;
-  T s = 0;
-  for (u64 j = b; j < e; j += SS_ITEMS) {
-    T v[SS_ITEMS];
-#pragma unroll
-    for (int k = 0; k < SS_ITEMS; ++k) v[k] = j + k < e ? in[j + k] : (T)0;
-#pragma unroll
-    for (int k = 0; k < SS_ITEMS; ++k) s += v[k];
-  }
-  T incl = s;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const T y = __shfl_up(incl, o);
-    if (lane >= o) incl += y;
-  }
-  if (lane == 63) sh[wave] = incl;
-  __syncthreads();
-  T before = 0, all = 0;
-#pragma unroll
-  for (int w = 0; w < SS_THREADS / 64; ++w) {
-    before += w < wave ? sh[w] : (T)0;
-    all += sh[w];
-  }
-  T off = before + incl - s;
-  for (u64 j = b; j < e; j += SS_ITEMS) {
-    T v[SS_ITEMS];
-#pragma unroll
-    for (int k = 0; k < SS_ITEMS; ++k) v[k] = j + k < e ? in[j + k] : (T)0;
-#pragma unroll
-    for (int k = 0; k < SS_ITEMS; ++k) {
-      if (j + k < e) out[j + k] = off;
-      off += v[k];
-    }
-  }
-  if (t == 0 && total) *total = all;
-}
-
 template <typename T>
 static int scan_impl(const T* in, T* out, u64 n, T* partials, T* total, hipStream_t s) {
   if (n == 0) return 0;
   if (n <= (u64)SS_THREADS * SS_ITEMS) {
     hipLaunchKernelGGL(scan_small_kernel<T>, dim3(1), dim3(SS_THREADS), 0, s, in, out, n, total);
-    return (int)hipGetLastError();
-  }
-  if (n <= (u64)SS_THREADS * SM_MAX) {
-    hipLaunchKernelGGL(scan_mid_kernel<T>, dim3(1), dim3(SS_THREADS), 0, s, in, out, n, total);
     return (int)hipGetLastError();
   }
   const u64 nt = (n + SC_TILE - 1) / SC_TILE;
