@@ -57,6 +57,9 @@ class Tunables:
     pin_exact: bool = _knob("MR_PIN_EXACT", True,
                             "split buffers in exact-size pinned memory (mr_host_alloc) instead of torch's "
                             "power-of-two pinned pool")
+    map_slots: int = _knob("MR_MAP_SLOTS", 2048,
+                           "word-count map: LDS slots of a workgroup's combine table (2048: 77.5 KiB, or 1024: "
+                           "45.5 KiB, leaving LDS on every CU for kernels running beside the map)")
     sort_small_rounds: int = _knob("MR_SORT_SMALL_ROUNDS", 4,
                                    "keys per thread of the onesweep tiles of sorts of <= 2^18 keys (4, 8 or 16: "
                                    "1024- to 4096-key tiles; fewer tiles, a shorter look-back chain)")
