@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(T) pk_scatter_kernel(const u64* __restrict__ h
 //                the block: order inside a segment is irrelevant, the
 //                receiver re-aggregates by key)
 constexpr int CP = 512;       // threads per block
-constexpr int CP_PER = 8;     // table slots per thread: 4096 per block, so the block-count scan stays short
+constexpr int CP_PER = 1;     // table slots per thread (8: 4096-slot blocks ran cp_count / cp_scatter 2x slower)
 
 __device__ __forceinline__ bool cp_slot(const GTab& g, u64 cap, u64 i, u32 nparts, u32 W, const u8* src, u64& h,
                                         u64& l, u64& r, u32& d, u32& len) {
@@ -201,51 +201,66 @@ __global__ void __launch_bounds__(CP) cp_count_kernel(GTab g, u64 cap, u32 npart
   }
 }
 
-// One workgroup of 1024 threads; column c of bcnt ([2W][nb], column-major)
-// is scanned by one wave (waves c, c + 16, ...): lane l owns the blocks
-// [l * per, (l + 1) * per), read 8 at a time with their loads issued together
-// (with 512-slot blocks, nb = 2048, this scan took 56 us; 4096-slot blocks keep nb, and it, small).
+// One workgroup of 1024 threads scans every column of bcnt ([2W][nb],
+// column-major) at once: thread t owns the blocks [t * per, (t + 1) * per)
+// of 16 columns per pass (its loads independent), a wave scan per column in
+// registers, wave totals through LDS.  (One wave per column, each lane
+// walking nb / 64 blocks, took 55 us at nb = 2048.)
 // rows_out: the table's occupied slots (the map's key count).
 constexpr int CS = 1024;
-constexpr int CS_U = 8;
+constexpr int CS_G = 16;  // columns per pass
 __global__ void __launch_bounds__(CS) cp_scan_kernel(u32* __restrict__ bcnt, u64 nb, u32 W,
                                                      unsigned long long* __restrict__ start, long long* __restrict__ xchg,
                                                      long long extra, const u32* __restrict__ ovf,
                                                      const int* __restrict__ errs, u32 nerr,
                                                      unsigned long long* __restrict__ rows_out, u64 buf_cap) {
   __shared__ unsigned long long tot[2 * MAXW];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ unsigned long long wt[CS / 64][CS_G];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const u32 C = 2 * W;
-  const u64 per = (nb + 63) / 64;  // blocks per lane
-  for (u32 c = wave; c < C; c += CS / 64) {
-    u32* col = bcnt + (u64)c * nb;
-    const u64 a = (u64)lane * per, b = a + per < nb ? a + per : nb;
-    unsigned long long sum = 0;
-    for (u64 j = a; j < b; j += CS_U) {
-      u32 v[CS_U];
+  const u64 per = (nb + CS - 1) / CS;
+  const u64 a = (u64)t * per < nb ? (u64)t * per : nb, b = a + per < nb ? a + per : nb;
+  for (u32 c0 = 0; c0 < C; c0 += CS_G) {
+    unsigned long long sum[CS_G], incl[CS_G];
 #pragma unroll
-      for (int u = 0; u < CS_U; ++u) v[u] = j + u < b ? col[j + u] : 0u;
-#pragma unroll
-      for (int u = 0; u < CS_U; ++u) sum += v[u];
+    for (int g = 0; g < CS_G; ++g) {
+      sum[g] = 0;
+      if (c0 + g < C) {
+        const u32* col = bcnt + (u64)(c0 + g) * nb;
+        for (u64 j = a; j < b; ++j) sum[g] += col[j];
+      }
+      incl[g] = sum[g];
     }
-    unsigned long long incl = sum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      const unsigned long long y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
-    }
-    unsigned long long run = incl - sum;
-    for (u64 j = a; j < b; j += CS_U) {
-      u32 v[CS_U];
 #pragma unroll
-      for (int u = 0; u < CS_U; ++u) v[u] = j + u < b ? col[j + u] : 0u;
-#pragma unroll
-      for (int u = 0; u < CS_U; ++u) {
-        if (j + u < b) col[j + u] = (u32)run;  // exclusive base of block j + u in column c
-        run += v[u];
+      for (int g = 0; g < CS_G; ++g) {
+        const unsigned long long y = __shfl_up(incl[g], o);
+        if (lane >= o) incl[g] += y;
       }
     }
-    if (lane == 63) tot[c] = incl;
+    if (lane == 63)
+#pragma unroll
+      for (int g = 0; g < CS_G; ++g) wt[wave][g] = incl[g];
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < CS_G; ++g) {
+      if (c0 + g >= C) continue;
+      unsigned long long before = 0, all = 0;
+      for (int w = 0; w < CS / 64; ++w) {
+        before += w < wave ? wt[w][g] : 0ull;
+        all += wt[w][g];
+      }
+      unsigned long long run = before + incl[g] - sum[g];
+      u32* col = bcnt + (u64)(c0 + g) * nb;
+      for (u64 j = a; j < b; ++j) {
+        const u32 x = col[j];
+        col[j] = (u32)run;  // exclusive base of block j in column c0 + g
+        run += x;
+      }
+      if (t == 0) tot[c0 + g] = all;
+    }
+    __syncthreads();  // (wt is rewritten by the next pass)
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
