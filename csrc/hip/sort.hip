@@ -688,20 +688,11 @@ int mr_sort_set_rounds32(int rounds) {
   return 0;
 }
 
-// Rounds of the small sorts (<= ONESWEEP_SMALL keys): 4 (1024-key tiles), or 8
-// / 16 (Tunables.sort_small_rounds, MR_SORT_SMALL_ROUNDS): fewer tiles shorten
-// the look-back chain a small pass is bound by (the W > 1 tail sorts ~10^5
-// keys per rank in 8 passes).
-static int g_small_rounds = 4;
-int mr_sort_set_small_rounds(int rounds) {
-  if (rounds != 4 && rounds != 8 && rounds != 16) return -1;
-  g_small_rounds = rounds;
-  return 0;
-}
-
+// (small sorts: 1024-key tiles; 2048 / 4096 measured slower for the W > 1
+// tail's ~10^5 keys, 0.711 / 0.717 vs 0.706 ms per W = 8 proxy step,
+// profiles/r5/proxy/)
 static int onesweep_rounds(u64 n, int key_bytes) {
-  return n <= ONESWEEP_SMALL ? g_small_rounds
-                             : n < ONESWEEP_BIG ? RS_ROUNDS : (key_bytes == 4 ? g_big_rounds32 : g_big_rounds);
+  return n <= ONESWEEP_SMALL ? 4 : n < ONESWEEP_BIG ? RS_ROUNDS : (key_bytes == 4 ? g_big_rounds32 : g_big_rounds);
 }
 
 static u64 onesweep_tiles_of(u64 n, int key_bytes) {
@@ -725,8 +716,6 @@ static int onesweep_pass(const void* keys_in, const void* vals_in, void* keys_ou
   const u32 nt = (u32)onesweep_tiles_of(n, (int)sizeof(K));
   switch (onesweep_rounds(n, (int)sizeof(K))) {
     case 4: onesweep_launch<K, 4>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
-                                  epoch, err, iota, debug_fail, s); break;
-    case 8: onesweep_launch<K, 8>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules, tile_counter,
                                   epoch, err, iota, debug_fail, s); break;
     case 24: onesweep_launch<K, 24>(nt, keys_in, vals_in, keys_out, vals_out, n, shift, ghist, granules,
                                     tile_counter, epoch, err, iota, debug_fail, s); break;

@@ -60,9 +60,6 @@ class Tunables:
     map_slots: int = _knob("MR_MAP_SLOTS", 2048,
                            "word-count map: LDS slots of a workgroup's combine table (2048: 77.5 KiB, or 1024: "
                            "45.5 KiB, leaving LDS on every CU for kernels running beside the map)")
-    sort_small_rounds: int = _knob("MR_SORT_SMALL_ROUNDS", 4,
-                                   "keys per thread of the onesweep tiles of sorts of <= 2^18 keys (4, 8 or 16: "
-                                   "1024- to 4096-key tiles; fewer tiles, a shorter look-back chain)")
     sort_rounds: int = _knob("MR_SORT_ROUNDS", 24,
                              "keys per thread of the onesweep radix tiles of sorts of >= 4 M keys (256 x rounds "
                              "keys per tile; 16, 24 or 32)")
