@@ -396,6 +396,9 @@ __global__ void __launch_bounds__(256) ovf_agg3_kernel(Ovf o, GTab g) {
   gtab_count_claims(g, claims);
 }
 
+// (1024 slots, 45.5 KiB, would leave LDS on every CU for the W > 1 post-map
+// kernels beside the map, but overflowed the table: resident map 4.25 vs
+// 2.29 ms per step, W = 8 proxy 0.96 vs 0.71 ms; profiles/r5/proxy/slots/)
 constexpr int MAP_T = 512, MAP_SLOTS = 2048, MAP_TPC = 1;
 static_assert(sizeof(Lds<MAP_T, MAP_SLOTS>) <= 80 * 1024, "two workgroups per CU");
 // (Wider combine spans — 4096 LDS slots over 32/64 KiB, one workgroup per CU —
@@ -416,20 +419,7 @@ static void launch_map3(const u8* text, u64 nbytes, u64 rep_base, const GTab& g,
 
 using namespace mr;
 
-// LDS slots of the map's per-workgroup table (Tunables.map_slots): 2048
-// (77.5 KiB of LDS, two workgroups per CU: 5 KiB of a CU's LDS left), or 1024
-// (45.5 KiB: ~70 KiB left, so the W > 1 post-map kernels that run beside the
-// next map — sort passes 17 KiB, receive-side insert 25 KiB — find room on
-// every CU instead of waiting for a map workgroup to retire).
-static int g_map_slots = 2048;
-
 extern "C" {
-
-int mr_wc_map3_set_slots(int slots) {
-  if (slots != 1024 && slots != 2048) return -1;
-  g_map_slots = slots;
-  return 0;
-}
 
 int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, void* lo, void* val, void* rep,
                void* ctrl, u64 cap, void* ovf_hi, void* ovf_lo, void* ovf_rep, u64 ovf_cap, void* ovf_counter,
@@ -447,10 +437,7 @@ int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, 
   v3::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter};
   const int aligned = ((uintptr_t)text & 15) == 0;
   const u8* t = (const u8*)text;
-  if (g_map_slots == 1024)
-    v3::launch_map3<v3::MAP_T, 1024, v3::MAP_TPC>(t, nbytes, rep_base, g, o, aligned, stream);
-  else
-    v3::launch_map3<v3::MAP_T, v3::MAP_SLOTS, v3::MAP_TPC>(t, nbytes, rep_base, g, o, aligned, stream);
+  v3::launch_map3<v3::MAP_T, v3::MAP_SLOTS, v3::MAP_TPC>(t, nbytes, rep_base, g, o, aligned, stream);
   hipLaunchKernelGGL(v3::ovf_agg3_kernel, dim3(1024), dim3(256), 0, stream, o, g);
   return (int)hipGetLastError();
 }

@@ -122,7 +122,6 @@ _SIGS = {
     "mr_agg_set_insert_grid": [_i32],
     "mr_small_d2h": [_p, _p, _p, _i32, _p, _p, _u32, _p],
     "mr_compact_pack_ws_bytes": [_u64, _u32],
-    "mr_wc_map3_set_slots": [_i32],
     "mr_compact_pack": [_p, _p, _p, _p, _p, _p, _u64, _u32, _u32, _p, _p, _p, _u64, _p, ctypes.c_longlong, _p, _u32,
                         _p, _p],
     "mr_sdma_available": [],
@@ -156,8 +155,6 @@ def lib():
             raise ValueError(f"MR_SORT_ROUNDS={TUNABLES.sort_rounds}: must be 16, 24 or 32")
         if L.mr_csv_set_config(TUNABLES.csv_tiles, TUNABLES.csv_mode) != 0:
             raise ValueError(f"MR_CSV_TILES={TUNABLES.csv_tiles} / MR_CSV_MODE={TUNABLES.csv_mode}: 0..64 / 0..2")
-        if L.mr_wc_map3_set_slots(TUNABLES.map_slots) != 0:
-            raise ValueError(f"MR_MAP_SLOTS={TUNABLES.map_slots}: must be 1024 or 2048")
         if L.mr_agg_set_insert_grid(TUNABLES.agg_insert_grid) != 0:
             raise ValueError(f"MR_AGG_INSERT_GRID={TUNABLES.agg_insert_grid}: must be >= 256")
         if L.mr_rec_gather_set_rows(TUNABLES.rec_gather_rows) != 0:

@@ -57,9 +57,6 @@ class Tunables:
     pin_exact: bool = _knob("MR_PIN_EXACT", True,
                             "split buffers in exact-size pinned memory (mr_host_alloc) instead of torch's "
                             "power-of-two pinned pool")
-    map_slots: int = _knob("MR_MAP_SLOTS", 2048,
-                           "word-count map: LDS slots of a workgroup's combine table (2048: 77.5 KiB, or 1024: "
-                           "45.5 KiB, leaving LDS on every CU for kernels running beside the map)")
     sort_rounds: int = _knob("MR_SORT_ROUNDS", 24,
                              "keys per thread of the onesweep radix tiles of sorts of >= 4 M keys (256 x rounds "
                              "keys per tile; 16, 24 or 32)")
