@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(CS) cp_scan_kernel(u32* __restrict__ bcnt, u64
                                                      long long extra, const u32* __restrict__ ovf,
                                                      const int* __restrict__ errs, u32 nerr,
                                                      unsigned long long* __restrict__ rows_out, u64 buf_cap) {
-  __shared__ unsigned long long tot[2 * MAXW];
+  extern __shared__ unsigned long long tot[];  // [2W], sized at launch (LDS kept small: see pk_insert_received)
   __shared__ unsigned long long wt[CS / 64][CS_G];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const u32 C = 2 * W;
@@ -344,9 +344,13 @@ constexpr int MAXW_RECV = 1024;
 __global__ void __launch_bounds__(256) pk_insert_received_kernel(const u8* __restrict__ rec, u64 n,
                                                                  const long long* __restrict__ recv, u32 W, GTab g,
                                                                  int op, int combined) {
-  __shared__ long long rstart[MAXW_RECV + 1];   // first row of source k
-  __shared__ long long rbyte[MAXW_RECV + 1];    // byte offset of source k's records
-  __shared__ long long bstart[MAXW_RECV + 1];   // byte offset of source k's key bytes
+  // LDS sized by W at launch (3 (W + 1) words: ~200 B at W = 8, not the 24 KiB
+  // of MAXW_RECV-sized arrays): the insert then fits beside the next map's
+  // workgroups (77.5 KiB each, two per CU) instead of waiting for one to retire
+  extern __shared__ long long pk_lds[];
+  long long* rstart = pk_lds;              // first row of source k
+  long long* rbyte = rstart + (W + 1);     // byte offset of source k's records
+  long long* bstart = rbyte + (W + 1);     // byte offset of source k's key bytes
   if (threadIdx.x == 0) {  // W is small (ranks of one job): a serial prefix sum
     long long r = 0, b = 0, seg = 0;
     for (u32 k = 0; k < W; ++k) {
@@ -456,7 +460,8 @@ int mr_compact_pack(void* tag, void* hi, void* lo, void* val, void* rep, void* c
   unsigned long long* start = (unsigned long long*)((u8*)ws + ((nb * 2 * W * 4 + 255) & ~255ull));
   hipLaunchKernelGGL(pk::cp_count_kernel, dim3((unsigned)nb), dim3(pk::CP), 0, s, g, cap, nparts, W, (const u8*)src,
                      bcnt);
-  hipLaunchKernelGGL(pk::cp_scan_kernel, dim3(1), dim3(pk::CS), 0, s, bcnt, nb, W, start, (long long*)xchg, extra,
+  hipLaunchKernelGGL(pk::cp_scan_kernel, dim3(1), dim3(pk::CS), 2 * W * sizeof(unsigned long long), s, bcnt, nb, W,
+                     start, (long long*)xchg, extra,
                      (const u32*)ctrl + 1, (const int*)errs, nerr, (unsigned long long*)rows_out, buf_cap);
   hipLaunchKernelGGL(pk::cp_scatter_kernel, dim3((unsigned)nb), dim3(pk::CP), 0, s, g, cap, nparts, W, (const u8*)src,
                      (const u32*)bcnt, (const unsigned long long*)start, (u8*)buf, buf_cap);
@@ -478,8 +483,8 @@ int mr_insert_received(const void* rec, u64 n, const void* recv, u32 W, void* ta
   g.ctrl = (u32*)ctrl;
   g.mask = cap - 1;
   g.src = (const u8*)(combined ? rec : src);
-  hipLaunchKernelGGL(pk::pk_insert_received_kernel, dim3(pk_grid(n, 2048)), dim3(256), 0, s, (const u8*)rec, n,
-                     (const long long*)recv, W, g, op, combined);
+  hipLaunchKernelGGL(pk::pk_insert_received_kernel, dim3(pk_grid(n, 2048)), dim3(256),
+                     3 * (W + 1) * sizeof(long long), s, (const u8*)rec, n, (const long long*)recv, W, g, op, combined);
   return (int)hipGetLastError();
 }
 

@@ -182,16 +182,21 @@ __global__ void __launch_bounds__(T) tail_hist_kernel(const u64* __restrict__ c,
 // Padded mode (a row BOUND): tail_pad_kernel and tail_hist_kernel in one
 // launch — the sentinel rows [count, bound) are written and their composite
 // keys histogrammed with the real ones (one launch less in the W > 1 tail).
+// The block histograms are 16-bit counters, two per LDS word (4 KiB instead
+// of 8: the kernel then fits beside the next map's workgroups, which leave
+// 5 KiB of a CU's LDS), so a block may count at most 65535 rows (the caller
+// checks).
 __global__ void __launch_bounds__(T) tail_padhist_kernel(const unsigned long long* __restrict__ counter, u64 bound,
                                                          u64* __restrict__ out_hi, u64* __restrict__ out_lo,
                                                          long long* __restrict__ out_val, u64* __restrict__ out_rep,
                                                          u32* __restrict__ out_part, u64* __restrict__ out_c,
                                                          const u32* __restrict__ ovf, u32* __restrict__ bad,
                                                          u32* ghist, u32 nparts, long long* pcount) {
-  __shared__ u32 hist[8][256];
+  __shared__ u32 hist[8][128];  // digit b, bin k: 16 bits at (k & 1) * 16 of word k >> 1
   const int t = threadIdx.x;
+  if (t < 128)
 #pragma unroll
-  for (int b = 0; b < 8; ++b) hist[b][t] = 0;
+    for (int b = 0; b < 8; ++b) hist[b][t] = 0;
   const u64 cnt = *counter;
   const u64 n = cnt < bound ? cnt : bound;
   if (blockIdx.x == 0 && t == 0) {
@@ -214,14 +219,19 @@ __global__ void __launch_bounds__(T) tail_padhist_kernel(const unsigned long lon
       out_c[i] = x;
     }
 #pragma unroll
-    for (int b = 0; b < 8; ++b) atomicAdd(&hist[b][(x >> (8 * b)) & 0xFF], 1u);
+    for (int b = 0; b < 8; ++b) {
+      const u32 k = (u32)(x >> (8 * b)) & 0xFFu;
+      atomicAdd(&hist[b][k >> 1], 1u << (16 * (k & 1u)));
+    }
   }
   __syncthreads();
+  const u32 sh = 16 * (t & 1);
 #pragma unroll
-  for (int b = 0; b < 8; ++b)
-    if (hist[b][t]) atomicAdd(&ghist[b * 256 + t], hist[b][t]);
-  if (pcount && (u32)t < nparts && hist[7][t])
-    atomicAdd((unsigned long long*)&pcount[t], (unsigned long long)hist[7][t]);
+  for (int b = 0; b < 8; ++b) {
+    const u32 c = (hist[b][t >> 1] >> sh) & 0xFFFFu;
+    if (c) atomicAdd(&ghist[b * 256 + t], c);
+    if (b == 7 && pcount && (u32)t < nparts && c) atomicAdd((unsigned long long*)&pcount[t], (unsigned long long)c);
+  }
 }
 
 __global__ void tail_gather_kernel(const u32* __restrict__ perm, u64 n, const u64* __restrict__ hi,
@@ -321,9 +331,9 @@ static int tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, voi
   hipLaunchKernelGGL(tl::tail_scatter_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, g, cap, nparts, (const u8*)src,
                      (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
                      (const u32*)bcount, out_cap);
-  if (pad && n > 0 && ghist != nullptr) {
+  if (pad && n > 0 && ghist != nullptr && n <= (u64)tl::HIST_BLOCKS * 65535u) {
     u64 hb = (n + 4 * tl::T - 1) / (4 * tl::T);
-    if (hb > (u64)tl::HIST_BLOCKS) hb = tl::HIST_BLOCKS;
+    if (hb > (u64)tl::HIST_BLOCKS) hb = tl::HIST_BLOCKS;  // (<= 65535 rows per block: 16-bit counters)
     hipLaunchKernelGGL(tl::tail_padhist_kernel, dim3((unsigned)hb), dim3(tl::T), 0, s, (const unsigned long long*)counter,
                        n, (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
                        (const u32*)ctrl + 1, (u32*)bad, (u32*)ghist, nparts, (long long*)pcount);
