@@ -203,12 +203,14 @@ __global__ void __launch_bounds__(CP) cp_count_kernel(GTab g, u64 cap, u32 npart
 
 // One workgroup of 1024 threads scans every column of bcnt ([2W][nb],
 // column-major) at once: thread t owns the blocks [t * per, (t + 1) * per)
-// of 16 columns per pass (its loads independent), a wave scan per column in
-// registers, wave totals through LDS.  (One wave per column, each lane
-// walking nb / 64 blocks, took 55 us at nb = 2048.)
+// of 16 columns per pass; the counts of a chunk of CS_K blocks of all 16
+// columns are loaded into registers together (64 independent loads), summed,
+// wave-scanned per column, and written back as bases from the same registers.
+// (A per-block load-then-add loop waited out each load: 50-56 us at nb = 2048.)
 // rows_out: the table's occupied slots (the map's key count).
 constexpr int CS = 1024;
 constexpr int CS_G = 16;  // columns per pass
+constexpr int CS_K = 4;   // blocks per thread per chunk
 __global__ void __launch_bounds__(CS) cp_scan_kernel(u32* __restrict__ bcnt, u64 nb, u32 W,
                                                      unsigned long long* __restrict__ start, long long* __restrict__ xchg,
                                                      long long extra, const u32* __restrict__ ovf,
@@ -216,51 +218,64 @@ __global__ void __launch_bounds__(CS) cp_scan_kernel(u32* __restrict__ bcnt, u64
                                                      unsigned long long* __restrict__ rows_out, u64 buf_cap) {
   extern __shared__ unsigned long long tot[];  // [2W], sized at launch (LDS kept small: see pk_insert_received)
   __shared__ unsigned long long wt[CS / 64][CS_G];
+  __shared__ unsigned long long carry[CS_G];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const u32 C = 2 * W;
-  const u64 per = (nb + CS - 1) / CS;
-  const u64 a = (u64)t * per < nb ? (u64)t * per : nb, b = a + per < nb ? a + per : nb;
+  const u64 nchunk = (nb + (u64)CS * CS_K - 1) / ((u64)CS * CS_K);  // chunks of CS * CS_K blocks
   for (u32 c0 = 0; c0 < C; c0 += CS_G) {
-    unsigned long long sum[CS_G], incl[CS_G];
-#pragma unroll
-    for (int g = 0; g < CS_G; ++g) {
-      sum[g] = 0;
-      if (c0 + g < C) {
-        const u32* col = bcnt + (u64)(c0 + g) * nb;
-        for (u64 j = a; j < b; ++j) sum[g] += col[j];
-      }
-      incl[g] = sum[g];
-    }
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
+    if (t < CS_G) carry[t] = 0;
+    __syncthreads();
+    for (u64 ch = 0; ch < nchunk; ++ch) {
+      const u64 a = ch * CS * CS_K + (u64)t * CS_K;  // this thread's first block of the chunk
+      u32 v[CS_G][CS_K];
+      unsigned long long sum[CS_G], incl[CS_G];
 #pragma unroll
       for (int g = 0; g < CS_G; ++g) {
-        const unsigned long long y = __shfl_up(incl[g], o);
-        if (lane >= o) incl[g] += y;
-      }
-    }
-    if (lane == 63)
+        const bool colok = c0 + g < C;
+        const u32* col = bcnt + (u64)(c0 + g) * nb;
 #pragma unroll
-      for (int g = 0; g < CS_G; ++g) wt[wave][g] = incl[g];
-    __syncthreads();
+        for (int k = 0; k < CS_K; ++k) v[g][k] = (colok && a + k < nb) ? col[a + k] : 0u;
+      }
 #pragma unroll
-    for (int g = 0; g < CS_G; ++g) {
-      if (c0 + g >= C) continue;
-      unsigned long long before = 0, all = 0;
-      for (int w = 0; w < CS / 64; ++w) {
-        before += w < wave ? wt[w][g] : 0ull;
-        all += wt[w][g];
+      for (int g = 0; g < CS_G; ++g) {
+        sum[g] = 0;
+#pragma unroll
+        for (int k = 0; k < CS_K; ++k) sum[g] += v[g][k];
+        incl[g] = sum[g];
       }
-      unsigned long long run = before + incl[g] - sum[g];
-      u32* col = bcnt + (u64)(c0 + g) * nb;
-      for (u64 j = a; j < b; ++j) {
-        const u32 x = col[j];
-        col[j] = (u32)run;  // exclusive base of block j in column c0 + g
-        run += x;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+        for (int g = 0; g < CS_G; ++g) {
+          const unsigned long long y = __shfl_up(incl[g], o);
+          if (lane >= o) incl[g] += y;
+        }
       }
-      if (t == 0) tot[c0 + g] = all;
+      if (lane == 63)
+#pragma unroll
+        for (int g = 0; g < CS_G; ++g) wt[wave][g] = incl[g];
+      __syncthreads();
+#pragma unroll
+      for (int g = 0; g < CS_G; ++g) {
+        if (c0 + g >= C) continue;
+        unsigned long long before = carry[g], all = 0;
+        for (int w = 0; w < CS / 64; ++w) {
+          before += w < wave ? wt[w][g] : 0ull;
+          all += wt[w][g];
+        }
+        unsigned long long run = before + incl[g] - sum[g];
+        u32* col = bcnt + (u64)(c0 + g) * nb;
+#pragma unroll
+        for (int k = 0; k < CS_K; ++k) {
+          if (a + k < nb) col[a + k] = (u32)run;  // exclusive base of block a + k in column c0 + g
+          run += v[g][k];
+        }
+        if (t == 0) tot[c0 + g] = carry[g] + all;
+      }
+      __syncthreads();  // every thread read carry and wt
+      if (t < CS_G && c0 + t < C) carry[t] = tot[c0 + t];
+      __syncthreads();
     }
-    __syncthreads();  // (wt is rewritten by the next pass)
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
