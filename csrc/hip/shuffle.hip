@@ -201,108 +201,88 @@ __global__ void __launch_bounds__(CP) cp_count_kernel(GTab g, u64 cap, u32 npart
   }
 }
 
-// One workgroup of 1024 threads scans every column of bcnt ([2W][nb],
-// column-major) at once: thread t owns the blocks [t * per, (t + 1) * per)
-// of 16 columns per pass; the counts of a chunk of CS_K blocks of all 16
-// columns are loaded into registers together (64 independent loads), summed,
-// wave-scanned per column, and written back as bases from the same registers.
-// (A per-block load-then-add loop waited out each load: 50-56 us at nb = 2048.)
-// rows_out: the table's occupied slots (the map's key count).
-constexpr int CS = 1024;
-constexpr int CS_G = 16;  // columns per pass
-constexpr int CS_K = 4;   // blocks per thread per chunk
-__global__ void __launch_bounds__(CS) cp_scan_kernel(u32* __restrict__ bcnt, u64 nb, u32 W,
-                                                     unsigned long long* __restrict__ start, long long* __restrict__ xchg,
-                                                     long long extra, const u32* __restrict__ ovf,
-                                                     const int* __restrict__ errs, u32 nerr,
-                                                     unsigned long long* __restrict__ rows_out, u64 buf_cap) {
-  extern __shared__ unsigned long long tot[];  // [2W], sized at launch (LDS kept small: see pk_insert_received)
-  __shared__ unsigned long long wt[CS / 64][CS_G];
-  __shared__ unsigned long long carry[CS_G];
+// One workgroup per column of bcnt ([2W][nb], column-major): the exclusive
+// prefix of the column over the blocks, written back in place, and the
+// column's total into coltot[c].  Thread t owns the blocks
+// [t * per, (t + 1) * per), read CS_K at a time with their loads issued
+// together.  (A single 1024-thread workgroup for all columns took 50-63 us:
+// it waited for a CU beside the map's workgroups and walked its blocks
+// serially.)
+constexpr int CS = 256;
+constexpr int CS_K = 8;
+__global__ void __launch_bounds__(CS) cp_scan_kernel(u32* __restrict__ bcnt, u64 nb,
+                                                     unsigned long long* __restrict__ coltot) {
+  __shared__ unsigned long long ws[CS / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const u32 C = 2 * W;
-  const u64 nchunk = (nb + (u64)CS * CS_K - 1) / ((u64)CS * CS_K);  // chunks of CS * CS_K blocks
-  for (u32 c0 = 0; c0 < C; c0 += CS_G) {
-    if (t < CS_G) carry[t] = 0;
-    __syncthreads();
-    for (u64 ch = 0; ch < nchunk; ++ch) {
-      const u64 a = ch * CS * CS_K + (u64)t * CS_K;  // this thread's first block of the chunk
-      u32 v[CS_G][CS_K];
-      unsigned long long sum[CS_G], incl[CS_G];
+  u32* col = bcnt + (u64)blockIdx.x * nb;
+  const u64 per = (nb + CS - 1) / CS;
+  const u64 a = (u64)t * per < nb ? (u64)t * per : nb, b = a + per < nb ? a + per : nb;
+  unsigned long long sum = 0;
+  for (u64 j = a; j < b; j += CS_K) {
+    u32 v[CS_K];
 #pragma unroll
-      for (int g = 0; g < CS_G; ++g) {
-        const bool colok = c0 + g < C;
-        const u32* col = bcnt + (u64)(c0 + g) * nb;
+    for (int k = 0; k < CS_K; ++k) v[k] = j + k < b ? col[j + k] : 0u;
 #pragma unroll
-        for (int k = 0; k < CS_K; ++k) v[g][k] = (colok && a + k < nb) ? col[a + k] : 0u;
-      }
+    for (int k = 0; k < CS_K; ++k) sum += v[k];
+  }
+  unsigned long long incl = sum;
 #pragma unroll
-      for (int g = 0; g < CS_G; ++g) {
-        sum[g] = 0;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) ws[wave] = incl;
+  __syncthreads();
+  unsigned long long run = incl - sum, all = 0;
 #pragma unroll
-        for (int k = 0; k < CS_K; ++k) sum[g] += v[g][k];
-        incl[g] = sum[g];
-      }
+  for (int w = 0; w < CS / 64; ++w) {
+    run += w < wave ? ws[w] : 0ull;
+    all += ws[w];
+  }
+  for (u64 j = a; j < b; j += CS_K) {
+    u32 v[CS_K];
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
+    for (int k = 0; k < CS_K; ++k) v[k] = j + k < b ? col[j + k] : 0u;
 #pragma unroll
-        for (int g = 0; g < CS_G; ++g) {
-          const unsigned long long y = __shfl_up(incl[g], o);
-          if (lane >= o) incl[g] += y;
-        }
-      }
-      if (lane == 63)
-#pragma unroll
-        for (int g = 0; g < CS_G; ++g) wt[wave][g] = incl[g];
-      __syncthreads();
-#pragma unroll
-      for (int g = 0; g < CS_G; ++g) {
-        if (c0 + g >= C) continue;
-        unsigned long long before = carry[g], all = 0;
-        for (int w = 0; w < CS / 64; ++w) {
-          before += w < wave ? wt[w][g] : 0ull;
-          all += wt[w][g];
-        }
-        unsigned long long run = before + incl[g] - sum[g];
-        u32* col = bcnt + (u64)(c0 + g) * nb;
-#pragma unroll
-        for (int k = 0; k < CS_K; ++k) {
-          if (a + k < nb) col[a + k] = (u32)run;  // exclusive base of block a + k in column c0 + g
-          run += v[g][k];
-        }
-        if (t == 0) tot[c0 + g] = carry[g] + all;
-      }
-      __syncthreads();  // every thread read carry and wt
-      if (t < CS_G && c0 + t < C) carry[t] = tot[c0 + t];
-      __syncthreads();
+    for (int k = 0; k < CS_K; ++k) {
+      if (j + k < b) col[j + k] = (u32)run;  // exclusive base of block j + k
+      run += v[k];
     }
   }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  bool redo = ovf && *ovf;
-  for (u32 k = 0; errs && k < nerr; ++k) redo |= errs[k] != 0;
-  unsigned long long off = 0, rows = 0;
-  for (u32 d = 0; d < W; ++d) {
-    start[d] = off;                 // destination d's records
-    start[W + d] = off + 32 * tot[d];  // and its key bytes
-    off += seg_bytes(tot[d], tot[W + d]);
-    rows += tot[d];
-  }
-  redo |= off > buf_cap;  // the send buffer (sized from the row bound) is too small
-  for (u32 d = 0; d < W; ++d) {
-    xchg[3 * d] = (long long)tot[d];
-    xchg[3 * d + 1] = (long long)tot[W + d];
-    xchg[3 * d + 2] = extra + (redo ? STATUS_REDO : 0);
-  }
-  *rows_out = rows;
+  if (t == 0) coltot[blockIdx.x] = all;
 }
 
 __global__ void __launch_bounds__(CP) cp_scatter_kernel(GTab g, u64 cap, u32 nparts, u32 W, const u8* __restrict__ src,
                                                         const u32* __restrict__ bcnt,
-                                                        const unsigned long long* __restrict__ start, u8* __restrict__ buf,
-                                                        u64 buf_cap) {
+                                                        const unsigned long long* __restrict__ coltot,
+                                                        u8* __restrict__ buf, u64 buf_cap, long long* __restrict__ xchg,
+                                                        long long extra, const u32* __restrict__ ovf,
+                                                        const int* __restrict__ errs, u32 nerr,
+                                                        unsigned long long* __restrict__ rows_out) {
   __shared__ u32 rc[MAXW], bc[MAXW];
+  extern __shared__ unsigned long long start[];  // [2W]: destination d's records, then its key bytes
   for (u32 k = threadIdx.x; k < W; k += CP) rc[k] = bc[k] = 0;
+  if (threadIdx.x == 0) {
+    unsigned long long off = 0, rows = 0;
+    for (u32 d = 0; d < W; ++d) {
+      start[d] = off;
+      start[W + d] = off + 32 * coltot[d];
+      off += seg_bytes(coltot[d], coltot[W + d]);
+      rows += coltot[d];
+    }
+    if (blockIdx.x == 0) {
+      // the count-exchange row and the status (the map's checks, a send
+      // buffer too small for the segments: the exchange is redone)
+      bool redo = (ovf && *ovf) || off > buf_cap;
+      for (u32 k = 0; errs && k < nerr; ++k) redo |= errs[k] != 0;
+      for (u32 d = 0; d < W; ++d) {
+        xchg[3 * d] = (long long)coltot[d];
+        xchg[3 * d + 1] = (long long)coltot[W + d];
+        xchg[3 * d + 2] = extra + (redo ? STATUS_REDO : 0);
+      }
+      *rows_out = rows;
+    }
+  }
   __syncthreads();
   const u64 nb = gridDim.x;
   const u64 i0 = (u64)blockIdx.x * CP * CP_PER + threadIdx.x;
@@ -472,14 +452,14 @@ int mr_compact_pack(void* tag, void* hi, void* lo, void* val, void* rep, void* c
   g.src = (const u8*)src;
   const u64 nb = (cap + pk::CP * pk::CP_PER - 1) / (pk::CP * pk::CP_PER);
   u32* bcnt = (u32*)ws;
-  unsigned long long* start = (unsigned long long*)((u8*)ws + ((nb * 2 * W * 4 + 255) & ~255ull));
+  unsigned long long* coltot = (unsigned long long*)((u8*)ws + ((nb * 2 * W * 4 + 255) & ~255ull));
   hipLaunchKernelGGL(pk::cp_count_kernel, dim3((unsigned)nb), dim3(pk::CP), 0, s, g, cap, nparts, W, (const u8*)src,
                      bcnt);
-  hipLaunchKernelGGL(pk::cp_scan_kernel, dim3(1), dim3(pk::CS), 2 * W * sizeof(unsigned long long), s, bcnt, nb, W,
-                     start, (long long*)xchg, extra,
-                     (const u32*)ctrl + 1, (const int*)errs, nerr, (unsigned long long*)rows_out, buf_cap);
-  hipLaunchKernelGGL(pk::cp_scatter_kernel, dim3((unsigned)nb), dim3(pk::CP), 0, s, g, cap, nparts, W, (const u8*)src,
-                     (const u32*)bcnt, (const unsigned long long*)start, (u8*)buf, buf_cap);
+  hipLaunchKernelGGL(pk::cp_scan_kernel, dim3(2 * W), dim3(pk::CS), 0, s, bcnt, nb, coltot);
+  hipLaunchKernelGGL(pk::cp_scatter_kernel, dim3((unsigned)nb), dim3(pk::CP), 2 * W * sizeof(unsigned long long), s, g,
+                     cap, nparts, W, (const u8*)src, (const u32*)bcnt, (const unsigned long long*)coltot, (u8*)buf,
+                     buf_cap, (long long*)xchg, extra, (const u32*)ctrl + 1, (const int*)errs, nerr,
+                     (unsigned long long*)rows_out);
   return (int)hipGetLastError();
 }
 
