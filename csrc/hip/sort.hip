@@ -622,6 +622,21 @@ extern "C" {
 
 u64 mr_scan_partials_len(u64 n) { return (n + SC_TILE - 1) / SC_TILE + 1; }
 
+// The first two launches of the multi-tile exclusive scan: per-tile sums of
+// `in` (tiles of mr_scan_tile() items) -> their exclusive scan in partials,
+// the total in *total.  A consumer applies partials[tile] itself (the W > 1
+// tail: tail.hip's offsets + key-bytes kernel).
+u64 mr_scan_tile() { return (u64)SC_TILE; }
+int mr_scan_partials_i64(const void* in, u64 n, void* partials, void* total, hipStream_t s) {
+  if (n == 0) return 0;
+  const u64 nt = (n + SC_TILE - 1) / SC_TILE;
+  hipLaunchKernelGGL(scan_reduce_kernel<long long>, dim3((unsigned)nt), dim3(SC_THREADS), 0, s, (const long long*)in,
+                     n, (long long*)partials);
+  hipLaunchKernelGGL(scan_partials_kernel<long long>, dim3(1), dim3(SC_THREADS), 0, s, (long long*)partials, nt,
+                     (long long*)total);
+  return (int)hipGetLastError();
+}
+
 // exclusive scans; `total` (device, 1 element, may be null) receives the sum
 int mr_exclusive_scan_u32(const void* in, void* out, u64 n, void* partials, void* total, hipStream_t s) {
   return scan_impl<u32>((const u32*)in, (u32*)out, n, (u32*)partials, (u32*)total, s);

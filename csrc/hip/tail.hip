@@ -234,6 +234,60 @@ __global__ void __launch_bounds__(T) tail_padhist_kernel(const unsigned long lon
   }
 }
 
+// Key offsets and key bytes of the sorted rows in one launch (the scan's
+// apply step fused with the key-byte gather): block b takes rows
+// [b * 4096, (b + 1) * 4096) (the scan's tiles; partials[b] = their base),
+// 16 consecutive rows per thread; offs[i] = the exclusive prefix of the key
+// lengths, and key i's bytes go to dst[offs[i] ..) (writes stop at dst_cap).
+constexpr int OB_T = 256, OB_ITEMS = 16;
+__global__ void __launch_bounds__(OB_T) tail_offbytes_kernel(const long long* __restrict__ len, u64 n,
+                                                             long long* __restrict__ offs,
+                                                             const long long* __restrict__ partials,
+                                                             const u64* __restrict__ hi, const u64* __restrict__ lo,
+                                                             const u64* __restrict__ rep, const u8* __restrict__ src,
+                                                             u8* __restrict__ dst, u64 dst_cap) {
+  __shared__ long long wsum[OB_T / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const u64 my = (u64)blockIdx.x * OB_T * OB_ITEMS + (u64)t * OB_ITEMS;
+  long long v[OB_ITEMS];
+  long long sum = 0;
+#pragma unroll
+  for (int r = 0; r < OB_ITEMS; ++r) {
+    v[r] = my + r < n ? len[my + r] : 0;
+    sum += v[r];
+  }
+  long long incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  long long off = partials[blockIdx.x] + incl - sum;
+#pragma unroll
+  for (int w = 0; w < OB_T / 64; ++w) off += w < wave ? wsum[w] : 0;
+  for (int r = 0; r < OB_ITEMS; ++r) {
+    const u64 i = my + r;
+    if (i >= n) break;
+    offs[i] = off;
+    const u64 o = (u64)off;
+    off += v[r];
+    if (o >= dst_cap) continue;
+    u8* d = dst + o;
+    const u64 room = dst_cap - o;
+    const u64 h = hi[i], l = lo[i];
+    if (!key_is_long(l)) {
+      const u32 kl = packed_len(l);
+      for (u32 k = 0; k < kl && k < room; ++k) d[k] = (u8)packed_byte(h, l, k);
+    } else {
+      const u64 kl = rep_len(rep[i]) < room ? rep_len(rep[i]) : room;
+      const u8* p = src + rep_off(rep[i]);
+      for (u64 k = 0; k < kl; ++k) d[k] = p[k];
+    }
+  }
+}
+
 __global__ void tail_gather_kernel(const u32* __restrict__ perm, u64 n, const u64* __restrict__ hi,
                                    const u64* __restrict__ lo, const long long* __restrict__ val,
                                    const u64* __restrict__ rep, const u32* __restrict__ part, u64* __restrict__ o_hi,
@@ -390,6 +444,8 @@ int mr_tail_pack(const void* val, const void* off, u64 n, const void* counts, u3
 
 int mr_exclusive_scan_i64(const void* in, void* out, u64 n, void* partials, void* total, hipStream_t s);
 u64 mr_scan_partials_len(u64 n);
+u64 mr_scan_tile();
+int mr_scan_partials_i64(const void* in, u64 n, void* partials, void* total, hipStream_t s);
 u64 mr_onesweep_tiles(u64 n);
 int mr_radix_onesweep_u32v(const void* keys_in, const void* vals_in, void* keys_out, void* vals_out, u64 n, int shift,
                            const void* ghist, void* granules, void* tile_counter, u32 epoch, void* err, int iota,
@@ -468,13 +524,24 @@ int mr_tail_run(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl,
   rc = mr_tie_fixup(kin, P(TB_HI), P(TB_LO), P(TB_VAL), P(TB_REP), P(TB_PART), n, z + TZ_BAD, src, P(TB_LN), s);
   if (rc) return rc;
   long long* offs = (long long*)P(TB_OFF);
-  if (n) {
-    rc = mr_exclusive_scan_i64(P(TB_LN), offs, n, P(TB_PARTIALS), offs + n, s);
+  if (n > 16384 && mr_scan_tile() == (u64)tl::OB_T * tl::OB_ITEMS) {
+    // tile sums + their scan, then offsets and key bytes in one launch
+    rc = mr_scan_partials_i64(P(TB_LN), n, P(TB_PARTIALS), offs + n, s);
+    if (rc) return rc;
+    const u64 nt = (n + mr_scan_tile() - 1) / mr_scan_tile();
+    hipLaunchKernelGGL(tl::tail_offbytes_kernel, dim3((unsigned)nt), dim3(tl::OB_T), 0, s, (const long long*)P(TB_LN),
+                       n, offs, (const long long*)P(TB_PARTIALS), (const u64*)P(TB_HI), (const u64*)P(TB_LO),
+                       (const u64*)P(TB_REP), (const u8*)src, (u8*)P(TB_BLOB), blob_cap ? blob_cap : 1);
+    rc = (int)hipGetLastError();
   } else {
-    rc = (int)hipMemsetAsync(offs, 0, 8, s);
+    if (n) {
+      rc = mr_exclusive_scan_i64(P(TB_LN), offs, n, P(TB_PARTIALS), offs + n, s);
+    } else {
+      rc = (int)hipMemsetAsync(offs, 0, 8, s);
+    }
+    if (rc) return rc;
+    rc = mr_gather_key_bytes(P(TB_HI), P(TB_LO), P(TB_REP), offs, n, src, P(TB_BLOB), blob_cap ? blob_cap : 1, s);
   }
-  if (rc) return rc;
-  rc = mr_gather_key_bytes(P(TB_HI), P(TB_LO), P(TB_REP), offs, n, src, P(TB_BLOB), blob_cap ? blob_cap : 1, s);
   if (rc) return rc;
   rc = mr_tail_pack(P(TB_VAL), offs, n, z + TZ_PCOUNT, nparts, z + TZ_BAD, z + TZ_ERR, P(TB_PACKED), s);
   if (rc) return rc;
