@@ -237,9 +237,9 @@ __global__ void __launch_bounds__(T) tail_padhist_kernel(const unsigned long lon
 // Key offsets and key bytes of the sorted rows in one launch (the scan's
 // apply step fused with the key-byte gather): block b takes rows
 // [b * 4096, (b + 1) * 4096) (the scan's tiles; partials[b] = their base),
-// 16 consecutive rows per thread; offs[i] = the exclusive prefix of the key
+// 4 consecutive rows per thread; offs[i] = the exclusive prefix of the key
 // lengths, and key i's bytes go to dst[offs[i] ..) (writes stop at dst_cap).
-constexpr int OB_T = 256, OB_ITEMS = 16;
+constexpr int OB_T = 1024, OB_ITEMS = 4;  // (256 x 16: 44.7 us vs 36.5 for the two launches)
 __global__ void __launch_bounds__(OB_T) tail_offbytes_kernel(const long long* __restrict__ len, u64 n,
                                                              long long* __restrict__ offs,
                                                              const long long* __restrict__ partials,
