@@ -510,7 +510,7 @@ def host_read(t: torch.Tensor) -> np.ndarray:
 
 class HostRead:
     """Small device tensors queued for download (host_read_begin); wait()
-    returns their host copies.  Up to 8 tensors of <= 64 KiB in total go in
+    returns their host copies.  Up to 8 tensors of <= 16 KiB in total go in
     one launch that also signals the host (mr_small_d2h); the host work done
     between begin and wait overlaps the download."""
 
@@ -524,14 +524,19 @@ class HostRead:
         self.device = d
         sizes = [t.numel() * t.element_size() for t in self.ts]
         total = sum((n + 15) & ~15 for n in sizes)
-        if len(self.ts) > 8 or total > (1 << 16) or _hip.SPIN_S <= 0:
+        if len(self.ts) > 8 or total > _SMALL_SLOT or _hip.SPIN_S <= 0:
             return  # host_read_many's blits + wait
-        buf = _SMALL_READ.get(d)
-        if buf is None:
-            p = _hip.lib().mr_host_alloc(1 << 16)
+        ring = _SMALL_READ.get(d)
+        if ring is None:
+            p = _hip.lib().mr_host_alloc(_SMALL_SLOT * _SMALL_SLOTS)
             if not p:
                 raise RuntimeError("hipHostMalloc of the small-download buffer failed")
-            buf = _SMALL_READ[d] = (p, np.ctypeslib.as_array((ctypes.c_uint8 * (1 << 16)).from_address(p)))
+            ring = _SMALL_READ[d] = [p, np.ctypeslib.as_array((ctypes.c_uint8 * (_SMALL_SLOT * _SMALL_SLOTS)).from_address(p)),
+                                     0]
+        # a ring of slots: up to _SMALL_SLOTS reads may be outstanding at once
+        k = ring[2]
+        ring[2] = (k + 1) % _SMALL_SLOTS
+        buf = (ring[0] + k * _SMALL_SLOT, ring[1][k * _SMALL_SLOT:(k + 1) * _SMALL_SLOT])
         offs, off = [], 0
         for n in sizes:
             offs.append(off)
@@ -552,6 +557,7 @@ class HostRead:
 
 
 _SMALL_READ: dict = {}
+_SMALL_SLOT, _SMALL_SLOTS = 1 << 14, 4  # bytes per read, reads outstanding at once
 
 
 def host_read_begin(ts: list) -> HostRead:

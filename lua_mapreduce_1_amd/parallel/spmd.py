@@ -783,18 +783,26 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         guess = getattr(self, "_red_distinct", None)
         want = 2 * (guess + guess // 4) if guess is not None else 2 * rows
         cap = ops.next_pow2(max(1 << 16, min(2 * rows, want)))
-        ev, self._red_reset_ev = getattr(self, "_red_reset_ev", None), None
+        cleared = self._wait_red_reset()
         if self.red_table is None or self.red_table.cap != cap:
             self.red_table = ops.HashTable(cap, device=self.device, op=self.op)
-        elif ev is not None:
-            torch.cuda.current_stream(self.device).wait_event(ev)  # reset after the last tail (off this chain)
-        else:
+        elif not cleared:
             self.red_table.reset()
         self.red_table.insert_received(rbuf, recv_counts, self.world, rows=rows)
         if guess is None:
             return max(rows, 1)
         b = guess + guess // 4 + 4096
         return max(1, min(rows, (b + 0xFFF) & ~0xFFF))
+
+    def _wait_red_reset(self) -> bool:
+        """If the last padded tail queued the reduce table's reset (on its own
+        stream, after its results were read), order this stream after it;
+        True when that reset happened."""
+        ev, self._red_reset_ev = getattr(self, "_red_reset_ev", None), None
+        if ev is None:
+            return False
+        torch.cuda.current_stream(self.device).wait_event(ev)
+        return True
 
     def _reduce_insert_received(self, rbuf, recv_counts, rows: int) -> int:
         """Received records -> this rank's reduce table (one insert launch);
@@ -806,6 +814,7 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         guess = getattr(self, "_red_distinct", None)
         want = 2 * (guess + guess // 4) if guess is not None else 2 * n
         cap = ops.next_pow2(max(1 << 16, min(2 * n, want)))
+        self._wait_red_reset()
         while True:
             if self.red_table is None or self.red_table.cap != cap:
                 self.red_table = ops.HashTable(cap, device=self.device, op=self.op)
