@@ -291,6 +291,8 @@ def main() -> int:
     last = None
     for i in range(args.steps):
         last = eng.run_iteration(prefetch_next=i < args.steps - 1, lookahead=args.steps - 1 - i)
+    if hasattr(last, "wait"):
+        last.wait()  # the last step's result columns are in host memory (a lazy download landed)
     sync()
     D.barrier(device=device)
     elapsed = time.perf_counter() - t0
@@ -319,6 +321,8 @@ def main() -> int:
         r2 = None
         for i in range(args.steps):
             r2 = e2.run_iteration(prefetch_next=i < args.steps - 1, lookahead=args.steps - 1 - i)
+        if hasattr(r2, "wait"):
+            r2.wait()
         sync()
         D.barrier(device=device)
         fs_ms = 1000.0 * D.all_reduce_max(time.perf_counter() - t0, device) / max(1, args.steps)

@@ -8,7 +8,9 @@
 // and the CPU agent uses the SDMA engines instead; the caller issues it once
 // the producing kernels are done (their stream was waited on), and the copies
 // of one batch complete together on one signal.  Any failure falls back to
-// hipMemcpy (the caller's data is always produced).
+// hipMemcpy (the caller's data is always produced).  mr_sdma_d2h_begin
+// returns with the copies in flight, so the host can queue the next
+// iteration's kernels while its results land (mr_sdma_wait before reading).
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -64,10 +66,13 @@ extern "C" {
 // 1 when the SDMA download path is usable in this process.
 int mr_sdma_available() { return ready() ? 1 : 0; }
 
-// n downloads dsts[i] <- srcs[i] (sizes[i] bytes; device memory -> pinned
-// host memory), all issued on the SDMA engines, then waited for.  Returns 0,
-// or 1 when the copies went through hipMemcpy instead (SDMA unusable).
-int mr_sdma_d2h(void* const* dsts, const void* const* srcs, const uint64_t* sizes, int n) {
+// Issue n downloads dsts[i] <- srcs[i] (sizes[i] bytes; device memory ->
+// pinned host memory) on the SDMA engines, all completing on one signal, and
+// return without waiting: > 0 = the batch's handle for mr_sdma_wait.  0 = the
+// copies are done already (through hipMemcpy: SDMA unusable, or nothing to
+// copy); -1 = a hipMemcpy fallback failed.  *fell_back = 1 when hipMemcpy ran.
+uint64_t mr_sdma_d2h_begin(void* const* dsts, const void* const* srcs, const uint64_t* sizes, int n, int* fell_back) {
+  *fell_back = 0;
   if (n <= 0) return 0;
   bool ok = ready();
   hsa_signal_t sig{0};
@@ -88,18 +93,44 @@ int mr_sdma_d2h(void* const* dsts, const void* const* srcs, const uint64_t* size
     ++issued;
   }
   if (sig.handle) {
-    // the issued copies must finish before anything else reuses their buffers
-    // (value < 1: done, or an error set it negative)
-    hsa_signal_subtract_screlease(sig, n - issued);
-    const hsa_signal_value_t v =
-        hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
-    if (v < 0) ok = false;
+    hsa_signal_subtract_screlease(sig, n - issued);  // the copies never issued
+    if (ok) return sig.handle;
+    // a copy failed to issue: the issued ones must finish before hipMemcpy
+    // rewrites their buffers
+    hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
     hsa_signal_destroy(sig);
   }
-  if (ok) return 0;
+  *fell_back = 1;
   for (int i = 0; i < n; ++i)
-    if (sizes[i] && hipMemcpy(dsts[i], srcs[i], sizes[i], hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return 1;
+    if (sizes[i] && hipMemcpy(dsts[i], srcs[i], sizes[i], hipMemcpyDeviceToHost) != hipSuccess) return (uint64_t)-1;
+  return 0;
+}
+
+// Wait for a batch of mr_sdma_d2h_begin and release its signal: 0, or -1
+// when a copy reported an error (the signal went negative).
+int mr_sdma_wait(uint64_t handle) {
+  if (handle == 0) return 0;
+  hsa_signal_t sig;
+  sig.handle = handle;
+  const hsa_signal_value_t v =
+      hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+  hsa_signal_destroy(sig);
+  return v < 0 ? -1 : 0;
+}
+
+// The blocking form: begin + wait.  Returns 0, 1 when the copies went
+// through hipMemcpy instead (SDMA unusable), -1 on failure.
+int mr_sdma_d2h(void* const* dsts, const void* const* srcs, const uint64_t* sizes, int n) {
+  int fell_back = 0;
+  const uint64_t h = mr_sdma_d2h_begin(dsts, srcs, sizes, n, &fell_back);
+  if (h == (uint64_t)-1) return -1;
+  if (fell_back) return 1;
+  if (mr_sdma_wait(h) < 0) {  // a copy failed on the engine: redo them all
+    for (int i = 0; i < n; ++i)
+      if (sizes[i] && hipMemcpy(dsts[i], srcs[i], sizes[i], hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return 1;
+  }
+  return 0;
 }
 
 }  // extern "C"

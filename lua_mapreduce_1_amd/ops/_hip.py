@@ -126,9 +126,11 @@ _SIGS = {
                         _p, _p],
     "mr_sdma_available": [],
     "mr_sdma_d2h": [_p, _p, _p, _i32],
+    "mr_sdma_d2h_begin": [_p, _p, _p, _i32, _p],
+    "mr_sdma_wait": [_u64],
 }
 _RESTYPE_U64 = {"mr_compact_pack_ws_bytes", "mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
-                "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words"}
+                "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words", "mr_sdma_d2h_begin"}
 
 
 def lib():

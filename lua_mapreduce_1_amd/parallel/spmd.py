@@ -147,11 +147,21 @@ class IterationResult:
         """The result columns of the fold plane alias the process's pinned
         download buffers (no copy per iteration); a later tail — the next
         iteration, or another engine — overwrites them.  Reading them after
-        that raises instead of returning another iteration's data."""
+        that raises instead of returning another iteration's data.  Columns
+        still landing (the lazy download of an unfused tail) are waited for."""
         g = getattr(self, "_gen", None)
         if g is not None and g != devmod.pool_generation() and self._parts is None:
             raise RuntimeError("this iteration's result columns were overwritten by a later device tail: read "
                                "them (partitions, gather_results, total_value) before the next iteration runs")
+        self.wait()
+
+    def wait(self) -> None:
+        """Block until this iteration's result columns are in host memory
+        (they may still be landing from the device when run_iteration returns)."""
+        dl = getattr(self, "_dl", None)
+        if dl is not None:
+            dl.wait()
+            self._dl = None
 
     @property
     def partitions(self) -> dict[int, dict]:
@@ -1050,7 +1060,7 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         with trace.range("mr.finalize_host"):
             for attempt in range(4):
                 try:
-                    cols = devmod.finalize_host(pend, self.partmod)
+                    cols = devmod.finalize_host(pend, self.partmod, lazy=True)
                     break
                 except devmod.TailBoundError as e:
                     # the padded tail's bound was too small or its table
@@ -1096,6 +1106,7 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                 r.real_time = r.written - t1
                 res.red_jobs.append(r)
         res.distinct_keys = int(cols["val"].size)
+        res._dl = cols.pop("_downloads", None)  # still landing: IterationResult.wait()
         res._vals = cols["val"]
         res._cols, res._parts = cols, None
         res._gen = devmod.pool_generation() if self.device.type == "cuda" else None

@@ -22,6 +22,7 @@ bytes mod N, examples/WordCount/partitionfn.lua) or, failing that, the host
 """
 from __future__ import annotations
 
+import atexit
 import numpy as np
 import torch
 
@@ -294,6 +295,8 @@ class _PinnedPool:
     def get(self, name: str, n: int, dtype) -> torch.Tensor:
         b = self.bufs.get(name)
         if b is None or b.numel() < n or b.dtype != dtype:
+            if b is not None:
+                wait_downloads()  # a download in flight may still write the buffer being replaced
             b = torch.empty(max(n, 1024) * 5 // 4, dtype=dtype, pin_memory=default_device().type == "cuda")
             self.bufs[name] = b
         return b[:n]
@@ -304,6 +307,7 @@ _BLOB_EST: dict = {}  # device -> expected key-blob bytes of the next finalize()
 
 
 _SDMA: dict = {}  # device -> [(dst, src, nbytes)] downloads deferred to flush_downloads
+_INFLIGHT: dict = {}  # device -> the Downloads batch still landing (flush_downloads(wait=False))
 
 
 def _sdma_ok() -> bool:
@@ -331,27 +335,94 @@ def dma_to_host(dst: torch.Tensor, src: torch.Tensor) -> None:
     if TUNABLES.sdma_min_mb > 0 and nb >= TUNABLES.sdma_min_mb * (1 << 20) and _sdma_ok():
         _SDMA.setdefault(src.device, []).append((dst, src, nb))
         return
+    b = _INFLIGHT.get(src.device)
+    if b is not None and b.writes(dst.data_ptr(), nb):
+        b.wait()  # a lazy batch still fills this buffer: it must not land over this copy
     _hip.call("mr_d2h_async", _hip.ptr(dst), _hip.ptr(src), nb, _hip.stream(src.device))
 
 
-def flush_downloads(device) -> None:
+class Downloads:
+    """A batch of SDMA downloads still landing in pinned host memory
+    (``flush_downloads(wait=False)``).  It holds the device sources, so their
+    memory is not reused before the copies are done; :meth:`wait` blocks until
+    the bytes are in place (and redoes the copies through hipMemcpy if the
+    engine reported an error)."""
+
+    def __init__(self, device, handle: int, pend: list):
+        self.device, self.handle, self.pend = device, handle, pend
+
+    @property
+    def done(self) -> bool:
+        return self.pend is None
+
+    def writes(self, ptr: int, nbytes: int) -> bool:
+        """True if a copy of this batch (still in flight) writes into [ptr, ptr + nbytes)."""
+        return any(d.data_ptr() < ptr + nbytes and ptr < d.data_ptr() + nb for d, _s, nb in (self.pend or ()))
+
+    def wait(self) -> None:
+        if self.pend is None:
+            return
+        from ..ops import _hip
+        pend, self.pend = self.pend, None
+        if _INFLIGHT.get(self.device) is self:
+            del _INFLIGHT[self.device]
+        if _hip.lib().mr_sdma_wait(self.handle) < 0:
+            _SDMA["ok"] = False
+            for dst, src, nb in pend:  # blocking runtime copies
+                dst.view(torch.uint8)[:nb].copy_(src.view(torch.uint8)[:nb])
+
+
+def wait_downloads(device=None) -> None:
+    """Wait for the in-flight download batch of ``device`` (None: of every
+    device) — before anything rewrites or frees the pinned buffers it fills."""
+    for d in ([device] if device is not None else list(_INFLIGHT)):
+        b = _INFLIGHT.get(d)
+        if b is not None:
+            b.wait()
+
+
+atexit.register(wait_downloads)  # no copy may still read device memory the process is freeing
+
+
+def discard_downloads(device) -> None:
+    """Drop the downloads deferred for a tail whose results are thrown away."""
+    _SDMA.pop(device, None)
+
+
+def flush_downloads(device, wait: bool = True):
     """Run the downloads deferred by :func:`dma_to_host` on the SDMA engines
-    and wait for them (call after waiting for the stream that produced
-    them)."""
+    (call after waiting for the stream that produced them).  ``wait=True``:
+    return once they landed.  ``wait=False``: return a :class:`Downloads`
+    batch still in flight (None when nothing is left to wait for); the caller
+    waits on it before reading the buffers.  A batch still landing from an
+    earlier call is waited for first (the pinned buffers are shared)."""
+    wait_downloads(device)
     pend = _SDMA.pop(device, None)
     if not pend:
-        return
+        return None
     import ctypes
     from ..ops import _hip
     n = len(pend)
     dsts = (ctypes.c_void_p * n)(*[t[0].data_ptr() for t in pend])
     srcs = (ctypes.c_void_p * n)(*[t[1].data_ptr() for t in pend])
     sizes = (ctypes.c_uint64 * n)(*[t[2] for t in pend])
-    rc = _hip.lib().mr_sdma_d2h(dsts, srcs, sizes, n)
-    if rc < 0:
+    if wait:
+        rc = _hip.lib().mr_sdma_d2h(dsts, srcs, sizes, n)
+        if rc < 0:
+            raise RuntimeError("device -> host download failed (SDMA and hipMemcpy)")
+        if rc == 1:
+            _SDMA["ok"] = False  # the SDMA path failed once: plain runtime copies from now on
+        return None
+    fell = ctypes.c_int(0)
+    h = int(_hip.lib().mr_sdma_d2h_begin(dsts, srcs, sizes, n, ctypes.byref(fell)))
+    if h == (1 << 64) - 1:
         raise RuntimeError("device -> host download failed (SDMA and hipMemcpy)")
-    if rc == 1:
-        _SDMA["ok"] = False  # the SDMA path failed once: plain runtime copies from now on
+    if fell.value:
+        _SDMA["ok"] = False
+    if h == 0:
+        return None
+    b = _INFLIGHT[device] = Downloads(device, h, pend)
+    return b
 
 
 def _to_host(t: torch.Tensor, name: str) -> torch.Tensor:
@@ -438,9 +509,10 @@ def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, p
         dma_to_host(hb[:est], blob[:est])
     else:
         hb = _POOL.get("blob", max(1 << 20, 16 * n), torch.uint8)
+        wait_downloads(hi.device)  # (a lazy batch may still fill hb)
         ops.copy_to_host(blob, hb, off[n:])  # size read on the device: no sync before the copy
     pend.update(off=off, blob=blob, est=est, hv=hv, ho=ho, hb=hb, hc=_to_host(counts, "counts"),
-                hbad=_to_host(bad, "bad"))
+                hbad=_to_host(bad, "bad"), hnb=_to_host(off[n:n + 1], "offn"))  # the key-byte total
     return pend
 
 
@@ -544,6 +616,9 @@ def finalize_table_native(table, n: int, src, nparts: int, blob_cap: int | None 
     else:
         hb = _POOL.get("blob", max(1 << 20, 16 * n), torch.uint8)
         est_arg = -1
+    b = _INFLIGHT.get(d)
+    if b is not None and (b.writes(hp.data_ptr(), hp.numel()) or b.writes(hb.data_ptr(), hb.numel())):
+        b.wait()  # the native tail downloads into these pinned buffers on its stream
     _hip.call("mr_tail_run", *table._gtab(), table.cap, n, nparts, _hip.ptr(src), _hip.ptr(ws), cap, _hip.ptr(hp),
               _hip.ptr(hb), est_arg, hb.numel(), 1 if padded else 0, _hip.stream(d))
     return {"n": n, "nparts": nparts, "args": v["args"], "src": src, "presorted": False, "hi": v["hi"], "lo": v["lo"],
@@ -636,15 +711,27 @@ def pool_generation() -> int:
     return _POOL.gen
 
 
-def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) -> dict:
-    """The host half of :func:`finalize`: one synchronisation, then numpy."""
+def finalize_host(pend: dict, partition_module=None, need_keys: bool = False, lazy: bool = False) -> dict:
+    """The host half of :func:`finalize`: one synchronisation, then numpy.
+
+    ``lazy=True`` (the unfused tail, e.g. the exact key order of n-grams):
+    the large downloads (values, key offsets, key bytes) are left landing on
+    the SDMA engines and the returned dict carries their
+    :class:`Downloads` batch under ``"_downloads"``; its arrays may be read
+    only after ``wait()``.  The host can meanwhile queue the next iteration's
+    tail, so the GPU does not idle through the transfer.  The counts, the
+    flags and the key-byte total are small stream-ordered copies and are read
+    here either way, so every error below is still raised eagerly."""
     _POOL.gen += 1
     n, nparts = pend["n"], pend["nparts"]
     hi, lo = pend["hi"], pend["lo"]
+    defer = False
     if hi.is_cuda:
         from ..ops import _hip
         _hip.wait_stream(hi.device)
-        flush_downloads(hi.device)  # large downloads: on the SDMA engines, now that their data is produced
+        defer = lazy and not pend.get("fused") and not need_keys and "hnb" in pend
+        if not defer:
+            flush_downloads(hi.device)  # large downloads: on the SDMA engines, now that their data is produced
         hb, est, blob = pend["hb"], pend["est"], pend["blob"]
         if pend.get("fused"):
             f_val, f_off, f_counts, f_bad = _unpack_fused(pend)
@@ -660,8 +747,17 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
             nbytes = int(f_off[n]) if n else 0
         else:
             ho = pend["ho"]
-            nbytes = int(ho[n]) if n else 0
-        if nbytes > blob.numel() and not (flag0 := (f_bad if pend.get("fused") else int(pend["hbad"][0]))) & 4:
+            nbytes = int(pend["hnb"][0]) if n and "hnb" in pend else (int(ho[n]) if n else 0)
+        flag = f_bad if pend.get("fused") else int(pend["hbad"][0])
+        if defer and (flag & 7 or nbytes > blob.numel() or (est is not None and nbytes > est)
+                      or nbytes > hb.numel() or (pend["presorted"] and not pend.get("exact"))):
+            # a re-run, a top-up copy or the host fix-up follows: nothing stays in flight
+            if flag & 5 or (nbytes > blob.numel() and not flag & 4):
+                discard_downloads(hi.device)  # these results are thrown away
+            else:
+                flush_downloads(hi.device)
+            defer = False
+        if nbytes > blob.numel() and not flag & 4:
             raise BlobCapacityError(nbytes, blob.numel())
         if nbytes > blob.numel():
             nbytes = blob.numel()  # a given-up sort's rows: discarded below (re-sort)
@@ -673,7 +769,6 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
             hb.copy_(blob[:nbytes])
         _BLOB_EST[hi.device] = nbytes + nbytes // 16 + 4096
         hb = hb[:nbytes]
-        flag = f_bad if pend.get("fused") else int(pend["hbad"][0])
         if flag & 5:
             # bit 0: a tie run was too long for the fixup kernel; bit 2: the
             # radix sort's decoupled look-back gave up (its order is invalid)
@@ -713,6 +808,9 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False) ->
     bounds = np.zeros(nparts + 1, np.int64)
     np.cumsum(h_counts, out=bounds[1:])
     out = {"hi": h_hi, "lo": h_lo, "val": h_val, "key_off": h_off, "key_blob": h_blob, "bounds": bounds}
+    if defer:
+        out["_downloads"] = flush_downloads(hi.device, wait=False)
+        return out
     if need_fix:
         # exact bytewise order inside each partition (long keys sharing a prefix)
         perms = []

@@ -53,3 +53,68 @@ def test_signal_order_helper():
     from lua_mapreduce_1_amd.ops import _hip
     assert _hip._done(5, 5) and _hip._done(6, 5) and not _hip._done(4, 5) and not _hip._done(0, 5)
     assert _hip._done(2, 0x7FFFFFFF)  # wrapped
+
+
+def test_lazy_batch_lands_and_guards_buffers():
+    """flush_downloads(wait=False): the batch is in flight when it returns,
+    its bytes are in place after wait(); a small stream copy into a buffer
+    the batch fills waits for it first (the batch must not land over it)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lua_mapreduce_1_amd.ops import _hip
+    from lua_mapreduce_1_amd.runtime import device as dv
+    d = torch.device("cuda", 0)
+    src = torch.randint(0, 2**62, (9 << 20,), dtype=torch.int64, device=d)
+    dst = torch.empty(src.numel(), dtype=torch.int64, pin_memory=True)
+    dv.dma_to_host(dst, src)
+    _hip.wait_stream(d)
+    b = dv.flush_downloads(d, wait=False)
+    assert b is not None and not b.done and dv._INFLIGHT.get(d) is b
+    assert b.writes(dst.data_ptr() + 8, 16) and not b.writes(dst.data_ptr() + dst.numel() * 8, 8)
+    small = torch.full((4,), -7, dtype=torch.int64, device=d)
+    dv.dma_to_host(dst[:4], small)  # overlaps the batch: waits for it, then copies on the stream
+    assert b.done and d not in dv._INFLIGHT
+    _hip.wait_stream(d)
+    assert dst[:4].tolist() == [-7] * 4 and torch.equal(dst[4:], src[4:].cpu())
+    b2 = None
+    dv.dma_to_host(dst, src)
+    _hip.wait_stream(d)
+    b2 = dv.flush_downloads(d, wait=False)
+    dv.wait_downloads()
+    assert b2.done and torch.equal(dst, src.cpu())
+
+
+def test_lazy_exact_tail_results(monkeypatch):
+    """The exact-order tail (n-gram keys) returns its iteration's results
+    while their download is still landing; reading them waits.  Three
+    pipelined iterations, each checked against the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import dataclasses
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_generic_plane import BG, close_lists, make_data, oracle
+    from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore
+    from lua_mapreduce_1_amd.runtime import codec
+    from lua_mapreduce_1_amd.utils import config
+    monkeypatch.setattr(config, "TUNABLES", dataclasses.replace(config.TUNABLES, sdma_min_mb=1e-4))
+    d = torch.device("cuda", 0)
+    splits = make_data("text")
+    exp = oracle("text", "bigram", splits)
+    eng = SPMDEngine(dict(taskfn=BG, mapfn=BG, partitionfn=BG, reducefn=BG, finalfn=None,
+                          init_args={"mode": "bigram", "nsplits": len(splits)}),
+                     split_store=SplitStore(splits, pin=True), device=d)
+    eng.prefetch, eng.pipeline = True, True
+    eng._exact_tail = True  # the order a long n-gram run falls back to, from the first iteration
+    steps, lazy = 3, 0
+    for k in range(steps):
+        res = eng.run_iteration(prefetch_next=k < steps - 1, lookahead=steps - 1 - k)
+        lazy += getattr(res, "_dl", None) is not None
+        got = {}
+        for _n, cols in eng.gather_results(res):
+            for key, v in codec.iter_columnar(cols):
+                got[key] = list(v)
+        assert close_lists(got, exp), k
+        assert res.distinct_keys == len(exp)
+    assert lazy == steps

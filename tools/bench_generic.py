@@ -61,6 +61,8 @@ def _time(eng, steps: int, warmup: int, device) -> float:
     t0 = time.perf_counter()
     for k in range(steps):
         res = eng.run_iteration(prefetch_next=k < steps - 1, lookahead=steps - 1 - k)
+    if hasattr(res, "wait"):
+        res.wait()  # inside the clock: the last step's results landed in host memory
     torch.cuda.synchronize(device)
     return (time.perf_counter() - t0) * 1000.0 / steps, res
 
