@@ -441,10 +441,11 @@ __global__ void key_word_kernel(const u64* __restrict__ hi, const u64* __restric
   }
 }
 
-// Exact key order after the (partition, bytes 0-15, min(len, 16)) sort of
-// ops.exact_key_perm: only long keys sharing their first 16 bytes can still
-// be out of order.  exact_hash_kernel gives every row a 64-bit hash of its
-// sort columns; on those hashes in sorted order, exact_fix_kernel finds each
+// Exact key order after the (partition, bytes 0-15[, min(len, 16)]) sort of
+// ops.exact_key_perm: only keys sharing their first 16 bytes can still be out
+// of order (long keys; without the length column also a key and the same key
+// with trailing NUL bytes).  exact_hash_kernel gives every row a 64-bit hash
+// of its sort columns; on those hashes in sorted order, exact_fix_kernel finds each
 // run of equal hashes (one thread per run start) and insertion-sorts the run
 // by the full key: (partition, bytes 0-15, and for two long keys their bytes
 // from 16 on and their lengths; else min(len, 16)) — the order the columns
@@ -456,7 +457,7 @@ __global__ void exact_hash_kernel(const int* __restrict__ part, const u64* __res
                                   const long long* __restrict__ klen, u64 n, u64* __restrict__ out) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const u64 lc = klen[i] < 16 ? (u64)klen[i] : 16ull;
+    const u64 lc = !klen ? 0ull : (klen[i] < 16 ? (u64)klen[i] : 16ull);  // no klen: the length is not a sort column
     out[i] = fmix64((u64)(unsigned)part[i] * 0x9E3779B97F4A7C15ull ^ fmix64(hi[i] ^ fmix64(w1[i] + lc)));
   }
 }

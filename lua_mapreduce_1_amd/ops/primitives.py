@@ -830,7 +830,7 @@ def key_word(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.T
 
 def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor,
                    src: torch.Tensor | None, nparts: int, klen: torch.Tensor | None = None,
-                   with_part: bool = False):
+                   with_part: bool = False, with_counts: bool = False):
     """Stable permutation ordering rows by (partition, exact key bytes) on the
     device, for key sets the (partition, hi, lo) sort plus the tie fix-up
     cannot order (long keys — whose lo is a hash — in long runs of a shared
@@ -847,7 +847,15 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     than 8 * EXACT_MAX_WORDS bytes (the caller orders on the host).
     ``klen``: the keys' lengths when the caller has them (key_meta).
     ``with_part``: return (perm, partitions in the new order as int64) —
-    the sort's major word, so no gather is needed for it."""
+    the sort's major word, so no gather is needed for it.  ``with_counts``
+    (GPU): also the rows per partition (int64 [nparts]), which the sort's
+    digit histogram of its partition word already holds.
+
+    Keys longer than 16 bytes go through the tie fix-up below, which orders
+    rows equal in (partition, bytes 0-15) by their full bytes and then their
+    lengths; for them the GPU sort leaves the length column out (one pass,
+    its histograms and a gather fewer) and falls back to the four-column
+    sort only when a tie run is too long for the fix-up."""
     n = hi.numel()
     d = hi.device
     if n == 0:
@@ -863,20 +871,39 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     w1 = key_word(hi, lo, rep, src, 1)
     lc = klen.clamp(max=16)
     cols = [part.to(torch.int64), hi, w1, lc]
-    p32, spart = sort_keys_checked(cols, bits=[pbits, 64, 64, 8], return_keys=True)
-    # every later step reorders rows only inside runs of one partition
-    done = (lambda p: (p, spart)) if with_part else (lambda p: p)  # noqa: E731
-    if max_len <= 16:
-        return done(p32.long())
+    counts = None
+
+    def sort_cols(cs, bits):
+        nonlocal counts
+        out = sort_keys_checked(cs, bits=bits, return_keys=True)
+        if with_counts and hi.is_cuda and pbits == 8:  # the partition word's digit histogram (sort_keys' workspace)
+            counts = _SORT_WS[d]["small"][:max(nparts, 1)].to(torch.int64)
+        return out
+
+    def done(p):
+        # every later step reorders rows only inside runs of one partition
+        out = (p, spart) if with_part else p
+        if with_counts:
+            c = counts if counts is not None else bincount(spart, max(nparts, 1))
+            out = (*out, c) if with_part else (out, c)
+        return out
+
+    if max_len <= 16 or not hi.is_cuda:
+        p32, spart = sort_cols(cols, [pbits, 64, 64, 8])
+        if max_len <= 16:
+            return done(p32.long())
+    else:
+        p32, spart = sort_cols(cols[:3], [pbits, 64, 64])
     if hi.is_cuda:
         # runs of rows equal in the sort columns (long keys sharing 16 bytes),
         # found through a hash of the columns in sorted order and insertion-
-        # sorted by their full bytes, one thread per run (mr_exact_fix); runs
-        # longer than its limit go to the refinement rounds below
+        # sorted by their full bytes and lengths, one thread per run
+        # (mr_exact_fix); runs longer than its limit go to the refinement
+        # rounds below, after the four-column sort
         s = _hip.stream(d)
         part32 = part.to(torch.int32).contiguous()
         h = torch.empty(n, dtype=torch.int64, device=d)
-        _hip.call("mr_exact_hash", _hip.ptr(part32), _hip.ptr(hi), _hip.ptr(w1), _hip.ptr(klen), n, _hip.ptr(h), s)
+        _hip.call("mr_exact_hash", _hip.ptr(part32), _hip.ptr(hi), _hip.ptr(w1), None, n, _hip.ptr(h), s)
         sh = torch.empty(n, dtype=torch.int64, device=d)
         _hip.call("mr_gather_u64", _hip.ptr(h), _hip.ptr(p32), _hip.ptr(sh), n, s)
         bad = torch.zeros(1, dtype=torch.int32, device=d)
@@ -884,6 +911,7 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
                   _hip.ptr(klen), _hip.ptr(rep), _hip.ptr(src), _hip.ptr(bad), s)
         if not int(bad.item()):
             return done(p32.long())
+        p32, spart = sort_cols(cols, [pbits, 64, 64, 8])
     perm = p32.long()
     scols = [c[perm] for c in cols]
     pos = torch.arange(n, dtype=torch.int64, device=d)

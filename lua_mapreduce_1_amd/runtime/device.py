@@ -474,10 +474,12 @@ class BlobCapacityError(RuntimeError):
 
 def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, part: torch.Tensor | None = None,
                     _presorted: bool = False, blob_cap: int | None = None,
-                    lengths: torch.Tensor | None = None) -> dict:
+                    lengths: torch.Tensor | None = None, counts: torch.Tensor | None = None) -> dict:
     """The device half of :func:`finalize`: every kernel and device->pinned
     copy, no host synchronisation (so it can be captured in a hipGraph once
-    the pinned buffers exist).  Returns the pending state for finalize_host."""
+    the pinned buffers exist).  Returns the pending state for finalize_host.
+    ``counts`` (presorted rows): the rows per partition when the caller has
+    them (int64 [nparts] on the device)."""
     n = hi.numel()
     if part is None:
         part = partition_of(hi, lo, rep, src, nparts, partition_module)
@@ -497,7 +499,8 @@ def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, p
     # source (a caller whose keys overlap there passes blob_cap)
     cap = max(src.numel() if src is not None else max(16 * n, 1), blob_cap or 0)
     off, blob = ops.gather_key_bytes(hi, lo, rep, src, lengths=lengths if _presorted else None, capacity=cap)
-    counts = ops.bincount(part, nparts) if n else torch.zeros(nparts, dtype=torch.int64, device=hi.device)
+    if counts is None or not _presorted:
+        counts = ops.bincount(part, nparts) if n else torch.zeros(nparts, dtype=torch.int64, device=hi.device)
     hv = _to_host(val, "val")
     ho = _to_host(off.to(torch.int32), "off32") if cap < 2**31 else _to_host(off, "off64")
     est = _BLOB_EST.get(hi.device)
@@ -641,12 +644,15 @@ def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=N
         part, klen = ops.key_meta(hi, lo, rep, src, nparts=nparts)
     else:
         part = partition_of(hi, lo, rep, src, nparts, partition_module)
-    got = ops.exact_key_perm(part, hi, lo, rep, src, nparts, klen=klen, with_part=True) if src is not None else None
+    got = ops.exact_key_perm(part, hi, lo, rep, src, nparts, klen=klen, with_part=True,
+                             with_counts=hi.is_cuda) if src is not None else None
     exact = got is not None
-    spart = None
+    spart = counts = None
     if got is None:
         perm = ops.sort_keys_checked([part.to(torch.int64), hi, lo],
                                      bits=[max(8, int(nparts - 1).bit_length()), 64, 64]).long()
+    elif hi.is_cuda:
+        perm, spart, counts = got
     else:
         perm, spart = got
     if hi.is_cuda and spart is not None:
@@ -664,7 +670,7 @@ def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=N
                       _hip.stream(hi.device))
         _, slen = ops.key_meta(cols[0], cols[1], cols[3], src, want_part=False)
         pend = finalize_device(*cols, src, nparts, partition_module, part=spart.to(torch.int32), _presorted=True,
-                               blob_cap=blob_cap, lengths=slen)
+                               blob_cap=blob_cap, lengths=slen, counts=counts)
     else:
         pend = finalize_device(hi[perm], lo[perm], val[perm], rep[perm], src, nparts, partition_module,
                                part=part[perm], _presorted=True, blob_cap=blob_cap)

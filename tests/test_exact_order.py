@@ -104,3 +104,26 @@ def test_exact_key_perm_returns_sorted_partitions_cpu():
     perm, spart = ops.exact_key_perm(part, hi, lo, rep, src, 7, with_part=True)
     assert torch.equal(spart, part.to(torch.int64)[perm])
     assert torch.equal(perm, ops.exact_key_perm(part, hi, lo, rep, src, 7))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nparts", [1, 10])
+def test_exact_key_perm_trailing_nul_gpu(gpu, nparts):
+    """Keys past 16 bytes: the GPU sort leaves the length column out, so a
+    short key and the same key followed by NUL bytes tie on the sort columns
+    and the fix-up orders them (shorter first).  The partition counts come
+    from the sort's histogram."""
+    rng = random.Random(6)
+    keys = _short_runs(6, 20_000)
+    extra = []
+    for k in keys[:4000]:
+        stem = k[:rng.randrange(1, 14)]
+        extra += [stem, stem + b"\x00", stem + b"\x00\x00", stem + b"\x00\x01"]
+    keys = list(dict.fromkeys(keys + extra))
+    rng.shuffle(keys)
+    _check(keys, nparts, gpu)
+    hi, lo, rep, src = (x.to(gpu) for x in _columns(keys))
+    part = torch.tensor([K.fnv1(k) % nparts for k in keys], dtype=torch.int32, device=gpu)
+    perm, spart, counts = ops.exact_key_perm(part, hi, lo, rep, src, nparts, with_part=True, with_counts=True)
+    assert torch.equal(spart, part.to(torch.int64)[perm])
+    assert counts.tolist() == torch.bincount(part.long().cpu(), minlength=nparts).tolist()
