@@ -285,10 +285,12 @@ __global__ void __launch_bounds__(256) table_compact_kernel(GTab g, u64 cap, u64
 }
 
 // Rows of 32-byte records {hi, lo, val, rep} gathered by an int32 permutation
-// into four columns (two 16-byte loads per row from one 32-byte record).
+// into four columns (two 16-byte loads per row from one 32-byte record), and
+// (olen given) the key lengths of the gathered rows (from lo / rep: no key
+// bytes read).
 __global__ void __launch_bounds__(256) gather_aos4_kernel(const u32* __restrict__ perm, u64 n,
                                                           const u64* __restrict__ aos, u64* o0, u64* o1, u64* o2,
-                                                          u64* o3) {
+                                                          u64* o3, long long* olen) {
   typedef u64 v2u __attribute__((ext_vector_type(2)));
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -300,13 +302,17 @@ __global__ void __launch_bounds__(256) gather_aos4_kernel(const u32* __restrict_
     o1[i] = a.y;
     o2[i] = b.x;
     o3[i] = b.y;
+    if (olen) olen[i] = (long long)(key_is_long(a.y) ? rep_len(b.y) : packed_len(a.y));
   }
 }
 
 // Key length and (optional) FNV-1 partition of each key.  Long-key bytes are
 // read from `src` at rep offsets.
+// out_w1 (optional, with out_part): key bytes 8..15 as a big-endian word,
+// zero past the key's end (key_word_kernel's word 1), from the same pass over
+// a long key's bytes.
 __global__ void key_meta_kernel(const u64* hi, const u64* lo, const u64* rep, u64 n, const u8* src, u32 nparts,
-                                u32* out_part, long long* out_len) {
+                                u32* out_part, long long* out_len, u64* out_w1) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const u64 h = hi[i], l = lo[i];
@@ -315,13 +321,20 @@ __global__ void key_meta_kernel(const u64* hi, const u64* lo, const u64* rep, u6
     if (out_len) out_len[i] = (long long)len;
     if (!out_part) continue;  // lengths only: no key bytes read
     u32 f = FNV_OFFSET;
+    u64 w1 = 0;
     if (!lng) {
       for (u32 k = 0; k < len; ++k) f = fnv1_step(f, packed_byte(h, l, k));
+      w1 = l & ~0xFFull;
     } else {
       const u8* p = src + rep_off(rep[i]);
-      for (u64 k = 0; k < len; ++k) f = fnv1_step(f, p[k]);
+      for (u64 k = 0; k < len; ++k) {
+        const u32 b = p[k];
+        f = fnv1_step(f, b);
+        if (k - 8 < 8) w1 |= (u64)b << (8 * (15 - k));
+      }
     }
     out_part[i] = nparts ? f % nparts : f;
+    if (out_w1) out_w1[i] = w1;
   }
 }
 
@@ -563,12 +576,12 @@ int mr_table_compact(void* tag, void* hi, void* lo, void* val, void* rep, void* 
 }
 
 // out[c][i] = aos[perm[i]].c for the four columns {hi, lo, val, rep}
-int mr_gather_aos4(const void* perm, u64 n, const void* aos, void* o0, void* o1, void* o2, void* o3,
+int mr_gather_aos4(const void* perm, u64 n, const void* aos, void* o0, void* o1, void* o2, void* o3, void* olen,
                    hipStream_t stream) {
   if (n == 0) return 0;
   const u64 g = (n + 255) / 256;
   hipLaunchKernelGGL(gather_aos4_kernel, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, stream,
-                     (const u32*)perm, n, (const u64*)aos, (u64*)o0, (u64*)o1, (u64*)o2, (u64*)o3);
+                     (const u32*)perm, n, (const u64*)aos, (u64*)o0, (u64*)o1, (u64*)o2, (u64*)o3, (long long*)olen);
   return (int)hipGetLastError();
 }
 
@@ -594,10 +607,11 @@ int mr_key_word(const void* hi, const void* lo, const void* rep, const void* src
 }
 
 int mr_key_meta(const void* hi, const void* lo, const void* rep, u64 n, const void* src, u32 nparts, void* out_part,
-                void* out_len, hipStream_t stream) {
+                void* out_len, void* out_w1, hipStream_t stream) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(key_meta_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)hi, (const u64*)lo,
-                     (const u64*)rep, n, (const u8*)src, nparts, (u32*)out_part, (long long*)out_len);
+                     (const u64*)rep, n, (const u8*)src, nparts, (u32*)out_part, (long long*)out_len,
+                     (u64*)out_w1);
   return (int)hipGetLastError();
 }
 

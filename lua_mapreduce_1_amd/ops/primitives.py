@@ -362,15 +362,17 @@ class HashTable:
             ((None,) if aos else ())
 
 
-def gather_aos4(perm: torch.Tensor, aos: torch.Tensor):
+def gather_aos4(perm: torch.Tensor, aos: torch.Tensor, want_len: bool = False):
     """(hi, lo, val, rep) of the 32-byte records ``aos[perm]`` (GPU: one
-    launch, one 32-byte record read per row instead of one line per column)."""
+    launch, one 32-byte record read per row instead of one line per column)
+    — and, with ``want_len``, the gathered keys' lengths as a fifth column
+    (key_meta's lengths, from the same launch)."""
     n = perm.numel()
     d = aos.device
-    out = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(4)]
+    out = [torch.empty(n, dtype=torch.int64, device=d) for _ in range(5 if want_len else 4)]
     if n:
         _hip.call("mr_gather_aos4", _hip.ptr(perm.to(torch.int32).contiguous()), n, _hip.ptr(aos),
-                  *[_hip.ptr(o) for o in out], _hip.stream(d))
+                  *[_hip.ptr(o) for o in out[:4]], _hip.ptr(out[4]) if want_len else None, _hip.stream(d))
     return tuple(out)
 
 
@@ -397,11 +399,13 @@ def tokenize(text: torch.Tensor, rep_base: int = 0, chunk_bytes: int = 64 * 1024
 
 
 def key_meta(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.Tensor | None,
-             nparts: int = 0, want_part: bool = True, want_len: bool = True):
+             nparts: int = 0, want_part: bool = True, want_len: bool = True, want_w1: bool = False):
     """(partition id int32 | None, key length int64 | None).
 
     Partition = exact uint32 FNV-1 of the key bytes mod ``nparts`` (raw hash
     when nparts == 0).  Long-key bytes are read from ``src`` at rep offsets.
+    ``want_w1`` (with ``want_part``): a third value, ``key_word(..., 1)``
+    computed in the same pass over the key bytes.
     """
     n = hi.numel()
     if hi.is_cuda:
@@ -409,16 +413,19 @@ def key_meta(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.T
         d = hi.device
         part = torch.empty(n, dtype=torch.int32, device=d) if want_part else None
         ln = torch.empty(n, dtype=torch.int64, device=d) if want_len else None
+        w1 = torch.empty(n, dtype=torch.int64, device=d) if (want_w1 and want_part) else None
         srcp = _hip.ptr(src) if src is not None else None
         _hip.call("mr_key_meta", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), n, srcp, nparts, _hip.ptr(part),
-                  _hip.ptr(ln), _hip.stream(d))
-        return part, ln
+                  _hip.ptr(ln), _hip.ptr(w1), _hip.stream(d))
+        return (part, ln, w1) if want_w1 else (part, ln)
     b = key_bytes_list(hi, lo, rep, src)
     part = None
     if want_part:
         h = np.array([K.fnv1(x) for x in b], dtype=np.uint64)
         part = torch.from_numpy((h % np.uint64(nparts) if nparts else h).astype(np.uint32).view(np.int32))
     ln = torch.tensor([len(x) for x in b], dtype=torch.int64) if want_len else None
+    if want_w1:
+        return part, ln, (key_word(hi, lo, rep, src, 1) if want_part else None)
     return part, ln
 
 
@@ -830,7 +837,7 @@ def key_word(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.T
 
 def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor,
                    src: torch.Tensor | None, nparts: int, klen: torch.Tensor | None = None,
-                   with_part: bool = False, with_counts: bool = False):
+                   with_part: bool = False, with_counts: bool = False, w1: torch.Tensor | None = None):
     """Stable permutation ordering rows by (partition, exact key bytes) on the
     device, for key sets the (partition, hi, lo) sort plus the tie fix-up
     cannot order (long keys — whose lo is a hash — in long runs of a shared
@@ -845,7 +852,8 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     groups, and so on.  Each round is a stable LSD radix sort, so rows of one
     key set keep their input order where they tie.  None when a key is longer
     than 8 * EXACT_MAX_WORDS bytes (the caller orders on the host).
-    ``klen``: the keys' lengths when the caller has them (key_meta).
+    ``klen``: the keys' lengths when the caller has them (key_meta); ``w1``:
+    their ``key_word(..., 1)`` likewise (key_meta(want_w1=True)).
     ``with_part``: return (perm, partitions in the new order as int64) —
     the sort's major word, so no gather is needed for it.  ``with_counts``
     (GPU): also the rows per partition (int64 [nparts]), which the sort's
@@ -868,7 +876,8 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     if (max_len + 7) // 8 > EXACT_MAX_WORDS:
         return None
     pbits = max(8, int(max(nparts, 1) - 1).bit_length())
-    w1 = key_word(hi, lo, rep, src, 1)
+    if w1 is None:
+        w1 = key_word(hi, lo, rep, src, 1)
     lc = klen.clamp(max=16)
     cols = [part.to(torch.int64), hi, w1, lc]
     counts = None

@@ -639,13 +639,14 @@ def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=N
     the compaction when given: one record read per row instead of one line
     per column)."""
     spec = getattr(partition_module, "device_partition", None) if partition_module is not None else ("fnv1", nparts)
-    klen = None
+    klen = w1 = None
     if hi.is_cuda and spec is not None and spec[0] == "fnv1" and int(spec[1]) == nparts:
-        part, klen = ops.key_meta(hi, lo, rep, src, nparts=nparts)
+        # partitions, lengths and key bytes 8..15 (the sort's second word) in one pass over the key bytes
+        part, klen, w1 = ops.key_meta(hi, lo, rep, src, nparts=nparts, want_w1=src is not None)
     else:
         part = partition_of(hi, lo, rep, src, nparts, partition_module)
     got = ops.exact_key_perm(part, hi, lo, rep, src, nparts, klen=klen, with_part=True,
-                             with_counts=hi.is_cuda) if src is not None else None
+                             with_counts=hi.is_cuda, w1=w1) if src is not None else None
     exact = got is not None
     spart = counts = None
     if got is None:
@@ -662,13 +663,13 @@ def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=N
         from ..ops import _hip
         n = hi.numel()
         if aos is not None:
-            cols = list(ops.gather_aos4(perm, aos))
+            *cols, slen = ops.gather_aos4(perm, aos, want_len=True)
         else:
             cols = [torch.empty(n, dtype=torch.int64, device=hi.device) for _ in range(4)]
             _hip.call("mr_gather_cols", _hip.ptr(perm.to(torch.int32)), n, _hip.ptr(hi), _hip.ptr(lo),
                       _hip.ptr(val), _hip.ptr(rep), None, None, *[_hip.ptr(c) for c in cols], None, None,
                       _hip.stream(hi.device))
-        _, slen = ops.key_meta(cols[0], cols[1], cols[3], src, want_part=False)
+            _, slen = ops.key_meta(cols[0], cols[1], cols[3], src, want_part=False)
         pend = finalize_device(*cols, src, nparts, partition_module, part=spart.to(torch.int32), _presorted=True,
                                blob_cap=blob_cap, lengths=slen, counts=counts)
     else:

@@ -127,3 +127,20 @@ def test_exact_key_perm_trailing_nul_gpu(gpu, nparts):
     perm, spart, counts = ops.exact_key_perm(part, hi, lo, rep, src, nparts, with_part=True, with_counts=True)
     assert torch.equal(spart, part.to(torch.int64)[perm])
     assert counts.tolist() == torch.bincount(part.long().cpu(), minlength=nparts).tolist()
+
+
+@pytest.mark.gpu
+def test_key_meta_w1_and_gathered_lengths_gpu(gpu):
+    """key_meta(want_w1=True)'s third column is key_word(..., 1); the
+    lengths gather_aos4(want_len=True) derives are key_meta's."""
+    keys = _key_set(7, 20_000)
+    hi, lo, rep, src = (x.to(gpu) for x in _columns(keys))
+    part, ln, w1 = ops.key_meta(hi, lo, rep, src, nparts=10, want_w1=True)
+    p2, l2 = ops.key_meta(hi, lo, rep, src, nparts=10)
+    assert torch.equal(part, p2) and torch.equal(ln, l2)
+    from lua_mapreduce_1_amd.ops import primitives as P
+    assert torch.equal(w1, P.key_word(hi, lo, rep, src, 1))
+    aos = torch.stack([hi, lo, torch.arange(len(keys), device=gpu), rep], 1).contiguous()
+    perm = torch.randperm(len(keys), device=gpu)
+    g = ops.gather_aos4(perm, aos, want_len=True)
+    assert torch.equal(g[0], hi[perm]) and torch.equal(g[3], rep[perm]) and torch.equal(g[4], ln[perm])
