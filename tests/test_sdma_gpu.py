@@ -117,4 +117,6 @@ def test_lazy_exact_tail_results(monkeypatch):
                 got[key] = list(v)
         assert close_lists(got, exp), k
         assert res.distinct_keys == len(exp)
-    assert lazy == steps
+    # the first tail can grow past the key-byte estimate a previous engine
+    # left (a top-up copy, eager); the later ones stay in flight
+    assert lazy >= steps - 1
