@@ -12,10 +12,11 @@
 // per-workgroup phase stamps of profiles/r1/map_v3/) are archived as
 // profiles/r3/pruned/map_configs/wc_map3_configs.patch.
 //
-// The map is bound by memory-side atomics: the flush folds ~0.63
-// (workgroup, distinct word) entries per token, one device-scope atomic add
-// each, and device atomics execute at the memory side at ~24 G/s chip-wide
-// (profiles/r3/map_pmc/README.md: TCC_EA0_ATOMIC = flush entries).
+// The flush folds ~0.63 (workgroup, distinct word) entries per token, one
+// device-scope atomic add each (memory-side atomics, profiles/r3/map_pmc/),
+// but it is not the bound: dropping three quarters of the flush saved 12 %
+// of the kernel (profiles/r5/map_probe/).  The tile work — staging, masks,
+// token list, LDS hash inserts — is, latency-bound at 4 waves per SIMD.
 #include <hip/hip_runtime.h>
 #include "mr_common.h"
 #include "hashtab.h"
