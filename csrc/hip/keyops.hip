@@ -310,9 +310,24 @@ __global__ void __launch_bounds__(256) gather_aos4_kernel(const u32* __restrict_
 // read from `src` at rep offsets.
 // out_w1 (optional, with out_part): key bytes 8..15 as a big-endian word,
 // zero past the key's end (key_word_kernel's word 1), from the same pass over
-// a long key's bytes.
+// a long key's bytes.  out_k7 (optional, with out_w1; nparts <= 256): the
+// two words of a 15-pass exact sort of 7-bit (ASCII) keys, k7[i] = partition
+// << 56 | bytes 0..7 as 7-bit digits, k7[n + i] = bytes 8..15 likewise (the
+// same order as (partition, hi, w1) when no byte has its top bit set);
+// *k7_bad |= 1 when some key's first 16 bytes have a byte >= 0x80.
+__device__ __forceinline__ u64 pack7(u64 w, u32& top) {
+  u64 r = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const u64 b = (w >> (56 - 8 * j)) & 0xFFull;
+    top |= (u32)b;
+    r = (r << 7) | (b & 0x7Full);
+  }
+  return r;
+}
+
 __global__ void key_meta_kernel(const u64* hi, const u64* lo, const u64* rep, u64 n, const u8* src, u32 nparts,
-                                u32* out_part, long long* out_len, u64* out_w1) {
+                                u32* out_part, long long* out_len, u64* out_w1, u64* out_k7, u32* k7_bad) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const u64 h = hi[i], l = lo[i];
@@ -335,6 +350,13 @@ __global__ void key_meta_kernel(const u64* hi, const u64* lo, const u64* rep, u6
     }
     out_part[i] = nparts ? f % nparts : f;
     if (out_w1) out_w1[i] = w1;
+    if (out_k7) {
+      u32 top = 0;
+      const u64 a = pack7(h, top), b = pack7(w1, top);
+      out_k7[i] = ((u64)(nparts ? f % nparts : f) << 56) | a;
+      out_k7[n + i] = b;
+      if (top & 0x80u) atomicOr(k7_bad, 1u);
+    }
   }
 }
 
@@ -607,11 +629,12 @@ int mr_key_word(const void* hi, const void* lo, const void* rep, const void* src
 }
 
 int mr_key_meta(const void* hi, const void* lo, const void* rep, u64 n, const void* src, u32 nparts, void* out_part,
-                void* out_len, void* out_w1, hipStream_t stream) {
+                void* out_len, void* out_w1, void* out_k7, void* k7_bad, hipStream_t stream) {
   if (n == 0) return 0;
+  if (out_k7 && (!out_w1 || !out_part || !k7_bad || nparts == 0 || nparts > 256)) return -1;
   hipLaunchKernelGGL(key_meta_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)hi, (const u64*)lo,
                      (const u64*)rep, n, (const u8*)src, nparts, (u32*)out_part, (long long*)out_len,
-                     (u64*)out_w1);
+                     (u64*)out_w1, (u64*)out_k7, (u32*)k7_bad);
   return (int)hipGetLastError();
 }
 

@@ -399,13 +399,19 @@ def tokenize(text: torch.Tensor, rep_base: int = 0, chunk_bytes: int = 64 * 1024
 
 
 def key_meta(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.Tensor | None,
-             nparts: int = 0, want_part: bool = True, want_len: bool = True, want_w1: bool = False):
+             nparts: int = 0, want_part: bool = True, want_len: bool = True, want_w1: bool = False,
+             want_k7: bool = False):
     """(partition id int32 | None, key length int64 | None).
 
     Partition = exact uint32 FNV-1 of the key bytes mod ``nparts`` (raw hash
     when nparts == 0).  Long-key bytes are read from ``src`` at rep offsets.
     ``want_w1`` (with ``want_part``): a third value, ``key_word(..., 1)``
-    computed in the same pass over the key bytes.
+    computed in the same pass over the key bytes.  ``want_k7`` (GPU, with
+    ``want_w1``, 1 <= nparts <= 256): a fourth, ``(k7, bad)`` — the two words
+    of the 15-pass sort of 7-bit keys (``k7[0]`` = partition << 56 | bytes
+    0-7 as 7-bit digits, ``k7[1]`` = bytes 8-15 likewise) and a device int32
+    flag, nonzero when some key has a byte >= 0x80 in its first 16 (k7's
+    order is then not the key order).
     """
     n = hi.numel()
     if hi.is_cuda:
@@ -414,9 +420,15 @@ def key_meta(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.T
         part = torch.empty(n, dtype=torch.int32, device=d) if want_part else None
         ln = torch.empty(n, dtype=torch.int64, device=d) if want_len else None
         w1 = torch.empty(n, dtype=torch.int64, device=d) if (want_w1 and want_part) else None
+        k7 = bad = None
+        if want_k7 and w1 is not None and 1 <= nparts <= 256:
+            k7 = torch.empty((2, n), dtype=torch.int64, device=d)
+            bad = torch.zeros(1, dtype=torch.int32, device=d)
         srcp = _hip.ptr(src) if src is not None else None
         _hip.call("mr_key_meta", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), n, srcp, nparts, _hip.ptr(part),
-                  _hip.ptr(ln), _hip.ptr(w1), _hip.stream(d))
+                  _hip.ptr(ln), _hip.ptr(w1), _hip.ptr(k7), _hip.ptr(bad), _hip.stream(d))
+        if want_k7:
+            return part, ln, w1, (None if k7 is None else (k7, bad))
         return (part, ln, w1) if want_w1 else (part, ln)
     b = key_bytes_list(hi, lo, rep, src)
     part = None
@@ -424,8 +436,9 @@ def key_meta(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.T
         h = np.array([K.fnv1(x) for x in b], dtype=np.uint64)
         part = torch.from_numpy((h % np.uint64(nparts) if nparts else h).astype(np.uint32).view(np.int32))
     ln = torch.tensor([len(x) for x in b], dtype=torch.int64) if want_len else None
-    if want_w1:
-        return part, ln, (key_word(hi, lo, rep, src, 1) if want_part else None)
+    if want_w1 or want_k7:
+        w1 = key_word(hi, lo, rep, src, 1) if want_part else None
+        return (part, ln, w1, None) if want_k7 else (part, ln, w1)
     return part, ln
 
 
@@ -837,7 +850,8 @@ def key_word(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.T
 
 def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor,
                    src: torch.Tensor | None, nparts: int, klen: torch.Tensor | None = None,
-                   with_part: bool = False, with_counts: bool = False, w1: torch.Tensor | None = None):
+                   with_part: bool = False, with_counts: bool = False, w1: torch.Tensor | None = None,
+                   k7=None):
     """Stable permutation ordering rows by (partition, exact key bytes) on the
     device, for key sets the (partition, hi, lo) sort plus the tie fix-up
     cannot order (long keys — whose lo is a hash — in long runs of a shared
@@ -853,7 +867,11 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     key set keep their input order where they tie.  None when a key is longer
     than 8 * EXACT_MAX_WORDS bytes (the caller orders on the host).
     ``klen``: the keys' lengths when the caller has them (key_meta); ``w1``:
-    their ``key_word(..., 1)`` likewise (key_meta(want_w1=True)).
+    their ``key_word(..., 1)`` likewise (key_meta(want_w1=True)); ``k7``:
+    key_meta(want_k7=True)'s 7-bit sort words and flag — when every key's
+    first 16 bytes are 7-bit, the GPU sort of keys past 16 bytes runs over
+    those two words (15 passes and one gather instead of 17 and two: the
+    partition rides in the top byte).
     ``with_part``: return (perm, partitions in the new order as int64) —
     the sort's major word, so no gather is needed for it.  ``with_counts``
     (GPU): also the rows per partition (int64 [nparts]), which the sort's
@@ -872,7 +890,10 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     if klen is None:
         _, klen = key_meta(hi, lo, rep, src, want_part=False)
     klen = klen.to(torch.int64)
-    max_len = int(klen.max())
+    if k7 is not None:  # the longest key and the 7-bit flag in one read
+        max_len, k7_bad = (int(x) for x in host_read(torch.stack([klen.max(), k7[1][0].to(torch.int64)])))
+    else:
+        max_len, k7_bad = int(klen.max()), 1
     if (max_len + 7) // 8 > EXACT_MAX_WORDS:
         return None
     pbits = max(8, int(max(nparts, 1) - 1).bit_length())
@@ -901,6 +922,12 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
         p32, spart = sort_cols(cols, [pbits, 64, 64, 8])
         if max_len <= 16:
             return done(p32.long())
+    elif not k7_bad and pbits == 8:
+        # 7-bit keys: (partition, bytes 0-15) as two words of 64 and 56 bits
+        p32, sk = sort_keys_checked([k7[0][0], k7[0][1]], bits=[64, 56], return_keys=True)
+        spart = (sk >> 56) & 0xFF
+        if with_counts:  # the top digit's histogram of the last word sorted
+            counts = _SORT_WS[d]["small"][7 * 256:7 * 256 + max(nparts, 1)].to(torch.int64)
     else:
         p32, spart = sort_cols(cols[:3], [pbits, 64, 64])
     if hi.is_cuda:

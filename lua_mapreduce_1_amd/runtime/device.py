@@ -639,14 +639,17 @@ def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=N
     the compaction when given: one record read per row instead of one line
     per column)."""
     spec = getattr(partition_module, "device_partition", None) if partition_module is not None else ("fnv1", nparts)
-    klen = w1 = None
+    klen = w1 = k7 = None
     if hi.is_cuda and spec is not None and spec[0] == "fnv1" and int(spec[1]) == nparts:
-        # partitions, lengths and key bytes 8..15 (the sort's second word) in one pass over the key bytes
-        part, klen, w1 = ops.key_meta(hi, lo, rep, src, nparts=nparts, want_w1=src is not None)
+        # partitions, lengths, key bytes 8..15 and the 7-bit sort words in one pass over the key bytes
+        if src is not None:
+            part, klen, w1, k7 = ops.key_meta(hi, lo, rep, src, nparts=nparts, want_w1=True, want_k7=True)
+        else:
+            part, klen = ops.key_meta(hi, lo, rep, src, nparts=nparts)
     else:
         part = partition_of(hi, lo, rep, src, nparts, partition_module)
     got = ops.exact_key_perm(part, hi, lo, rep, src, nparts, klen=klen, with_part=True,
-                             with_counts=hi.is_cuda, w1=w1) if src is not None else None
+                             with_counts=hi.is_cuda, w1=w1, k7=k7) if src is not None else None
     exact = got is not None
     spart = counts = None
     if got is None:

@@ -144,3 +144,43 @@ def test_key_meta_w1_and_gathered_lengths_gpu(gpu):
     perm = torch.randperm(len(keys), device=gpu)
     g = ops.gather_aos4(perm, aos, want_len=True)
     assert torch.equal(g[0], hi[perm]) and torch.equal(g[3], rep[perm]) and torch.equal(g[4], ln[perm])
+
+
+def _check_k7(keys, nparts, gpu, expect_7bit):
+    hi, lo, rep, src = (x.to(gpu) for x in _columns(keys))
+    part, klen, w1, k7 = ops.key_meta(hi, lo, rep, src, nparts=nparts, want_w1=True, want_k7=True)
+    assert (int(k7[1][0]) == 0) == expect_7bit
+    exp_part = torch.tensor([K.fnv1(k) % nparts for k in keys], dtype=torch.int32)
+    assert torch.equal(part.cpu(), exp_part)
+    perm, spart, counts = ops.exact_key_perm(part, hi, lo, rep, src, nparts, klen=klen, with_part=True,
+                                             with_counts=True, w1=w1, k7=k7)
+    got = [(int(exp_part[i]), keys[i]) for i in perm.cpu().tolist()]
+    assert got == sorted((int(p), k) for p, k in zip(exp_part.tolist(), keys))
+    assert torch.equal(spart.cpu(), exp_part.to(torch.int64)[perm.cpu()])
+    assert counts.tolist() == torch.bincount(exp_part.long(), minlength=nparts).tolist()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nparts", [1, 10, 256])
+def test_exact_key_perm_7bit_words_gpu(gpu, nparts):
+    """ASCII keys past 16 bytes (n-gram-like, shared prefixes, short keys and
+    their NUL-padded twins): the 15-pass sort over the 7-bit words."""
+    rng = random.Random(8)
+    stems = [b"of the ", b"in the european ", b"the commission and the council ", b"x" * 15]
+    keys = set()
+    while len(keys) < 60_000:
+        k = rng.choice(stems)[:rng.randrange(1, 40)] + bytes(rng.choice(b"abcdefgh \t~") for _ in
+                                                              range(rng.randrange(0, 12)))
+        keys.add(k)
+        if rng.random() < 0.05:
+            keys.add(k[:rng.randrange(1, 15)] + b"\x00" * rng.randrange(1, 3))
+    keys = sorted(keys, key=lambda _: rng.random())
+    _check_k7(keys, nparts, gpu, True)
+
+
+@pytest.mark.gpu
+def test_exact_key_perm_8bit_keys_fall_back_gpu(gpu):
+    """A byte >= 0x80 in some key's first 16 bytes: the flag is set and the
+    sort takes the byte-word columns."""
+    keys = _short_runs(9, 5_000) + [b"\xff" * 20]
+    _check_k7(list(dict.fromkeys(keys)), 10, gpu, False)
