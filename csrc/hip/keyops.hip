@@ -342,10 +342,18 @@ __global__ void key_meta_kernel(const u64* hi, const u64* lo, const u64* rep, u6
       w1 = l & ~0xFFull;
     } else {
       const u8* p = src + rep_off(rep[i]);
-      for (u64 k = 0; k < len; ++k) {
-        const u32 b = p[k];
-        f = fnv1_step(f, b);
-        if (k - 8 < 8) w1 |= (u64)b << (8 * (15 - k));
+      for (u64 k0 = 0; k0 < len; k0 += 16) {  // 16 loads in flight per batch
+        u32 b[16];
+#pragma unroll
+        for (u64 j = 0; j < 16; ++j) b[j] = k0 + j < len ? (u32)p[k0 + j] : 0u;
+#pragma unroll
+        for (u64 j = 0; j < 16; ++j) {
+          const u64 k = k0 + j;
+          if (k < len) {
+            f = fnv1_step(f, b[j]);
+            if (k - 8 < 8) w1 |= (u64)b[j] << (8 * (15 - k));
+          }
+        }
       }
     }
     out_part[i] = nparts ? f % nparts : f;
@@ -378,7 +386,16 @@ __global__ void gather_key_bytes_kernel(const u64* hi, const u64* lo, const u64*
     } else {
       const u64 len = rep_len(rep[i]) < room ? rep_len(rep[i]) : room;
       const u8* p = src + rep_off(rep[i]);
-      for (u64 k = 0; k < len; ++k) d[k] = p[k];
+      // 16 loads in flight per batch: a byte loop waits out one memory round
+      // trip per byte (n-gram keys of 16-40 bytes)
+      for (u64 k0 = 0; k0 < len; k0 += 16) {
+        u8 b[16];
+#pragma unroll
+        for (u64 j = 0; j < 16; ++j) b[j] = k0 + j < len ? p[k0 + j] : (u8)0;
+#pragma unroll
+        for (u64 j = 0; j < 16; ++j)
+          if (k0 + j < len) d[k0 + j] = b[j];
+      }
     }
   }
 }
