@@ -136,6 +136,29 @@ MR_HD u64 make_rep(u64 off, u64 len) { return (off << REP_LEN_BITS) | (len < REP
 MR_HD u64 rep_off(u64 rep) { return rep >> REP_LEN_BITS; }
 MR_HD u64 rep_len(u64 rep) { return rep & REP_LEN_MASK; }
 
+// Copy n bytes of a key from global memory, 16 loads in flight per batch (a
+// byte loop waits out one memory round trip per byte: n-gram keys of 16-40
+// bytes).
+MR_HD void copy_key_bytes(u8* dst, const u8* p, u64 n) {
+  for (u64 k0 = 0; k0 < n; k0 += 16) {
+    u8 b[16];
+#pragma unroll
+    for (u64 j = 0; j < 16; ++j) b[j] = k0 + j < n ? p[k0 + j] : (u8)0;
+#pragma unroll
+    for (u64 j = 0; j < 16; ++j)
+      if (k0 + j < n) dst[k0 + j] = b[j];
+  }
+}
+
+// Little-endian word of bytes p[0 .. min(n, 8)) (zero past the end), its
+// loads issued together (long-key hash words).
+MR_HD u64 load_word_le(const u8* p, u64 n) {
+  u64 w = 0;
+#pragma unroll
+  for (u64 j = 0; j < 8; ++j) w |= (j < n ? (u64)p[j] : 0ull) << (8 * j);
+  return w;
+}
+
 // FNV-1 of a table key's bytes (packed in (hi, lo), or at rep in src for a
 // long key) and its length.
 MR_HD u32 key_fnv(u64 h, u64 l, u64 r, const u8* src, u32* len_out) {
@@ -147,7 +170,14 @@ MR_HD u32 key_fnv(u64 h, u64 l, u64 r, const u8* src, u32* len_out) {
   } else {
     len = (u32)rep_len(r);
     const u8* p = src + rep_off(r);
-    for (u32 k = 0; k < len; ++k) f = fnv1_step(f, p[k]);
+    for (u32 k0 = 0; k0 < len; k0 += 16) {  // 16 loads in flight per batch
+      u32 b[16];
+#pragma unroll
+      for (u32 j = 0; j < 16; ++j) b[j] = k0 + j < len ? (u32)p[k0 + j] : 0u;
+#pragma unroll
+      for (u32 j = 0; j < 16; ++j)
+        if (k0 + j < len) f = fnv1_step(f, b[j]);
+    }
   }
   *len_out = len;
   return f;

@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(T) pk_scatter_kernel(const u64* __restrict__ h
     for (u32 k = 0; k < len; ++k) out[k] = (u8)packed_byte(h, l, k);
   } else {
     const u8* p = src + rep_off(rep[i]);
-    for (u32 k = 0; k < len; ++k) out[k] = p[k];
+    copy_key_bytes(out, p, len);
   }
 }
 
@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(CP) cp_scatter_kernel(GTab g, u64 cap, u32 npa
       for (u32 k = 0; k < len; ++k) out[k] = (u8)packed_byte(h, l, k);
     } else {
       const u8* p = src + rep_off(r);
-      for (u32 k = 0; k < len; ++k) out[k] = p[k];
+      copy_key_bytes(out, p, len);
     }
   }
 }

@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(OB_T) tail_offbytes_kernel(const long long* __
     } else {
       const u64 kl = rep_len(rep[i]) < room ? rep_len(rep[i]) : room;
       const u8* p = src + rep_off(rep[i]);
-      for (u64 k = 0; k < kl; ++k) d[k] = p[k];
+      copy_key_bytes(d, p, kl);
     }
   }
 }

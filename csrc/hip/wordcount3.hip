@@ -74,9 +74,8 @@ __device__ __forceinline__ u32 funnel(u32 a, u32 b, u32 r8) { return r8 ? ((a >>
 __device__ u64 long_lo_global(const u8* text, u64 p0, u64 len) {
   u64 h = long_hash_init(len);
   for (u64 w = 0; w < len; w += 8) {
-    u64 word = 0;
     const u64 n = (len - w) < 8 ? (len - w) : 8;
-    for (u64 j = 0; j < n; ++j) word |= (u64)text[p0 + w + j] << (8 * j);
+    const u64 word = load_word_le(text + p0 + w, n);
     h = long_hash_step(h, word);
   }
   return long_lo(h, mr_long_mask);
