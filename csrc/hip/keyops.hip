@@ -648,7 +648,10 @@ int mr_key_meta(const void* hi, const void* lo, const void* rep, u64 n, const vo
                 void* out_len, void* out_w1, void* out_k7, void* k7_bad, hipStream_t stream) {
   if (n == 0) return 0;
   if (out_k7 && (!out_w1 || !out_part || !k7_bad || nparts == 0 || nparts > 256)) return -1;
-  hipLaunchKernelGGL(key_meta_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)hi, (const u64*)lo,
+  // one key per thread (no grid cap): a thread's keys are latency chains of
+  // random key-byte loads, and a capped grid ran ~11 of them in series
+  hipLaunchKernelGGL(key_meta_kernel, dim3(grid_for(n, 256, 1 << 20)), dim3(256), 0, stream, (const u64*)hi,
+                     (const u64*)lo,
                      (const u64*)rep, n, (const u8*)src, nparts, (u32*)out_part, (long long*)out_len,
                      (u64*)out_w1, (u64*)out_k7, (u32*)k7_bad);
   return (int)hipGetLastError();
@@ -657,7 +660,7 @@ int mr_key_meta(const void* hi, const void* lo, const void* rep, u64 n, const vo
 int mr_gather_key_bytes(const void* hi, const void* lo, const void* rep, const void* off, u64 n, const void* src,
                         void* dst, u64 dst_cap, hipStream_t stream) {
   if (n == 0) return 0;
-  hipLaunchKernelGGL(gather_key_bytes_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)hi,
+  hipLaunchKernelGGL(gather_key_bytes_kernel, dim3(grid_for(n, 256, 1 << 20)), dim3(256), 0, stream, (const u64*)hi,
                      (const u64*)lo, (const u64*)rep, (const long long*)off, n, (const u8*)src, (u8*)dst, dst_cap);
   return (int)hipGetLastError();
 }
