@@ -30,9 +30,7 @@ __device__ __forceinline__ u32 key_len(u64 lo, u64 rep) { return key_is_long(lo)
 
 __global__ void __launch_bounds__(T) pk_count_kernel(const u64* __restrict__ lo, const u64* __restrict__ rep,
                                                      const u32* __restrict__ part, u64 n, u32 W,
-                                                     unsigned long long* __restrict__ cnt /*[2W]*/,
-                                                     const unsigned long long* __restrict__ n_dev) {
-  if (n_dev && *n_dev < n) n = *n_dev;
+                                                     unsigned long long* __restrict__ cnt /*[2W]*/) {
   __shared__ u32 rc[MAXW];
   __shared__ unsigned long long bc[MAXW];
   for (u32 d = threadIdx.x; d < W; d += T) {
@@ -64,21 +62,17 @@ __host__ __device__ __forceinline__ u64 seg_bytes(u64 rows, u64 bytes) { return 
 // layout: ONE buffer of per-destination segments [records | key bytes], so
 // the payload is a single all_to_all_single.
 //
-// Status (the W > 1 single-sync iteration): the map's completion checks ride
-// on the count exchange instead of a host read before it.  If the map table
-// overflowed (*ovf), a map chunk set its error word (errs[0..nerr)) or the
-// compaction found more rows than its bound (*n_dev > n_cap), extra gets
-// STATUS_REDO added: every rank sees it in the exchanged counts and the
-// exchange is redone after the flagged rank fixed its map.
+// Status (the W > 1 single-sync iteration, cp_scatter_kernel below): the map's
+// completion checks ride on the count exchange instead of a host read before
+// it.  If the map table overflowed, a map chunk set its error word or the send
+// buffer is too small, extra gets STATUS_REDO added: every rank sees it in the
+// exchanged counts and the exchange is redone after the flagged rank fixed its
+// map (or grew its buffer to the exchanged totals).
 constexpr long long STATUS_REDO = 1ll << 40;
 __global__ void pk_scan_kernel(const unsigned long long* __restrict__ cnt, u32 W, unsigned long long* __restrict__ start,
                                unsigned long long* __restrict__ cursor, long long* __restrict__ xchg, long long extra,
-                               int combined, const u32* __restrict__ ovf, const int* __restrict__ errs, u32 nerr,
-                               const unsigned long long* __restrict__ n_dev, u64 n_cap) {
+                               int combined) {
   if (threadIdx.x != 0) return;
-  bool redo = (ovf && *ovf) || (n_dev && *n_dev > n_cap);
-  for (u32 k = 0; errs && k < nerr; ++k) redo |= errs[k] != 0;
-  if (redo) extra += STATUS_REDO;
   unsigned long long r = 0, b = 0;
   for (u32 d = 0; d < W; ++d) {
     if (combined) {
@@ -106,9 +100,7 @@ __global__ void __launch_bounds__(T) pk_scatter_kernel(const u64* __restrict__ h
                                                        const unsigned long long* __restrict__ start,
                                                        unsigned long long* __restrict__ cursor,
                                                        u8* __restrict__ rec /*records, byte-addressed*/,
-                                                       u8* __restrict__ blob,
-                                                       const unsigned long long* __restrict__ n_dev) {
-  if (n_dev && *n_dev < n) n = *n_dev;
+                                                       u8* __restrict__ blob) {
   __shared__ u32 rc[MAXW];
   __shared__ u32 bc[MAXW];
   __shared__ unsigned long long rbase[MAXW];
@@ -154,13 +146,15 @@ __global__ void __launch_bounds__(T) pk_scatter_kernel(const u64* __restrict__ h
 // Send side straight from the map's hash table (the W > 1 single-sync
 // iteration): three launches instead of the compaction's three plus the
 // pack's four, and no dense intermediate columns.
-//   cp_count   : per table block (4096 slots, 8 per thread), per destination, the
-//                rows and key bytes of its occupied slots -> bcnt[2W][block]
-//   cp_scan    : one workgroup: per (destination, rows | bytes) column, the
-//                exclusive prefix over the blocks (one wave per column),
-//                segment starts, the count-exchange row and the status
-//                (table overflow, chunk errors, send buffer too small)
-//   cp_scatter : each slot again -> its record + key bytes at the block's
+//   cp_count   : per table block (CP * CP_PER = 512 slots, one per thread), per
+//                destination, the rows and key bytes of its occupied slots ->
+//                bcnt[2W][block] (u64: the exclusive bases of the byte columns
+//                reach 4 GiB for a destination of large key sets)
+//   cp_scan    : one workgroup per (destination, rows | bytes) column: the
+//                exclusive prefix over the blocks and the column's total
+//   cp_scatter : (block 0) segment starts, the count-exchange row and the
+//                status (table overflow, chunk errors, send buffer too small)
+//                then each slot again -> its record + key bytes at the block's
 //                base in its destination's segment (LDS-atomic ranks inside
 //                the block: order inside a segment is irrelevant, the
 //                receiver re-aggregates by key)
@@ -179,7 +173,7 @@ __device__ __forceinline__ bool cp_slot(const GTab& g, u64 cap, u64 i, u32 npart
 }
 
 __global__ void __launch_bounds__(CP) cp_count_kernel(GTab g, u64 cap, u32 nparts, u32 W, const u8* __restrict__ src,
-                                                      u32* __restrict__ bcnt) {
+                                                      unsigned long long* __restrict__ bcnt) {
   __shared__ u32 rc[MAXW], bc[MAXW];
   for (u32 k = threadIdx.x; k < W; k += CP) rc[k] = bc[k] = 0;
   __syncthreads();
@@ -210,18 +204,18 @@ __global__ void __launch_bounds__(CP) cp_count_kernel(GTab g, u64 cap, u32 npart
 // serially.)
 constexpr int CS = 256;
 constexpr int CS_K = 8;
-__global__ void __launch_bounds__(CS) cp_scan_kernel(u32* __restrict__ bcnt, u64 nb,
+__global__ void __launch_bounds__(CS) cp_scan_kernel(unsigned long long* __restrict__ bcnt, u64 nb,
                                                      unsigned long long* __restrict__ coltot) {
   __shared__ unsigned long long ws[CS / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  u32* col = bcnt + (u64)blockIdx.x * nb;
+  unsigned long long* col = bcnt + (u64)blockIdx.x * nb;
   const u64 per = (nb + CS - 1) / CS;
   const u64 a = (u64)t * per < nb ? (u64)t * per : nb, b = a + per < nb ? a + per : nb;
   unsigned long long sum = 0;
   for (u64 j = a; j < b; j += CS_K) {
-    u32 v[CS_K];
+    unsigned long long v[CS_K];
 #pragma unroll
-    for (int k = 0; k < CS_K; ++k) v[k] = j + k < b ? col[j + k] : 0u;
+    for (int k = 0; k < CS_K; ++k) v[k] = j + k < b ? col[j + k] : 0ull;
 #pragma unroll
     for (int k = 0; k < CS_K; ++k) sum += v[k];
   }
@@ -240,12 +234,12 @@ __global__ void __launch_bounds__(CS) cp_scan_kernel(u32* __restrict__ bcnt, u64
     all += ws[w];
   }
   for (u64 j = a; j < b; j += CS_K) {
-    u32 v[CS_K];
+    unsigned long long v[CS_K];
 #pragma unroll
-    for (int k = 0; k < CS_K; ++k) v[k] = j + k < b ? col[j + k] : 0u;
+    for (int k = 0; k < CS_K; ++k) v[k] = j + k < b ? col[j + k] : 0ull;
 #pragma unroll
     for (int k = 0; k < CS_K; ++k) {
-      if (j + k < b) col[j + k] = (u32)run;  // exclusive base of block j + k
+      if (j + k < b) col[j + k] = run;  // exclusive base of block j + k
       run += v[k];
     }
   }
@@ -253,7 +247,7 @@ __global__ void __launch_bounds__(CS) cp_scan_kernel(u32* __restrict__ bcnt, u64
 }
 
 __global__ void __launch_bounds__(CP) cp_scatter_kernel(GTab g, u64 cap, u32 nparts, u32 W, const u8* __restrict__ src,
-                                                        const u32* __restrict__ bcnt,
+                                                        const unsigned long long* __restrict__ bcnt,
                                                         const unsigned long long* __restrict__ coltot,
                                                         u8* __restrict__ buf, u64 buf_cap, long long* __restrict__ xchg,
                                                         long long extra, const u32* __restrict__ ovf,
@@ -293,10 +287,10 @@ __global__ void __launch_bounds__(CP) cp_scatter_kernel(GTab g, u64 cap, u32 npa
     if (!cp_slot(g, cap, i, nparts, W, src, h, l, r, d, len)) continue;
     const u32 rpos = atomicAdd(&rc[d], 1u);
     const u32 bpos = atomicAdd(&bc[d], len);
-    const u64 ro = start[d] + 32 * ((u64)bcnt[(u64)d * nb + blockIdx.x] + rpos);
-    const u64 boff = (u64)bcnt[(u64)(W + d) * nb + blockIdx.x] + bpos;  // inside destination d's byte segment
+    const u64 ro = start[d] + 32 * (bcnt[(u64)d * nb + blockIdx.x] + rpos);
+    const u64 boff = bcnt[(u64)(W + d) * nb + blockIdx.x] + bpos;  // inside destination d's byte segment
     const u64 bo = start[W + d] + boff;
-    if (ro + 32 > buf_cap || bo + len > buf_cap) continue;  // too small: flagged by cp_scan, the exchange is redone
+    if (ro + 32 > buf_cap || bo + len > buf_cap) continue;  // too small: flagged by block 0 above, the exchange is redone
     u64* rr = reinterpret_cast<u64*>(buf + ro);
     rr[0] = h;
     rr[1] = l;
@@ -397,12 +391,9 @@ extern "C" {
 // ws: 6*W u64 (cnt[2W], start[2W], cursor[2W]); xchg: 3*W int64 (device)
 // combined != 0: rec == blob == one buffer of per-destination [records | key
 // bytes] segments (mr_pack_seg_bytes), sent with a single all-to-all.
-// n_dev (may be null): the row count on the device, n then being a bound
-// (rows [0, min(n, *n_dev)) are packed); ovf / errs / n_dev: the status
-// folded into the exchanged extra column (pk_scan_kernel).
 int mr_pack_by_dest(const void* hi, const void* lo, const void* val, const void* rep, const void* part, u64 n, u32 W,
                     const void* src, void* ws, void* xchg, long long extra, void* rec, void* blob, int combined,
-                    const void* n_dev, const void* ovf, const void* errs, u32 nerr, hipStream_t s) {
+                    hipStream_t s) {
   if (W == 0 || W > (u32)pk::MAXW) return -1;
   unsigned long long* cnt = (unsigned long long*)ws;
   unsigned long long* start = cnt + 2 * W;
@@ -410,31 +401,30 @@ int mr_pack_by_dest(const void* hi, const void* lo, const void* val, const void*
   hipMemsetAsync(cnt, 0, 2 * W * sizeof(unsigned long long), s);
   if (n) {
     hipLaunchKernelGGL(pk::pk_count_kernel, dim3(pk_grid(n, 1024)), dim3(pk::T), 0, s, (const u64*)lo,
-                       (const u64*)rep, (const u32*)part, n, W, cnt, (const unsigned long long*)n_dev);
+                       (const u64*)rep, (const u32*)part, n, W, cnt);
   }
   hipLaunchKernelGGL(pk::pk_scan_kernel, dim3(1), dim3(64), 0, s, (const unsigned long long*)cnt, W, start, cursor,
-                     (long long*)xchg, extra, combined, (const u32*)ovf, (const int*)errs, nerr,
-                     (const unsigned long long*)n_dev, n);
+                     (long long*)xchg, extra, combined);
   if (n) {
     // one record per thread (the per-block reservation needs every key of the
     // block in flight at once): grid = ceil(n / 256), not capped
     const u64 g = (n + pk::T - 1) / pk::T;
     hipLaunchKernelGGL(pk::pk_scatter_kernel, dim3((unsigned)g), dim3(pk::T), 0, s, (const u64*)hi, (const u64*)lo,
                        (const long long*)val, (const u64*)rep, (const u32*)part, n, W, (const u8*)src,
-                       (const unsigned long long*)start, cursor, (u8*)rec, (u8*)blob, (const unsigned long long*)n_dev);
+                       (const unsigned long long*)start, cursor, (u8*)rec, (u8*)blob);
   }
   return (int)hipGetLastError();
 }
 
 // The send side from the map's table in three launches (cp_* above): ws =
-// u32 [2W][nb] block counts (nb = ceil(cap / 4096)) + 2W u64; buf (buf_cap
+// u64 [2W][nb] block counts (nb = ceil(cap / 512)) + 2W u64; buf (buf_cap
 // bytes) receives the per-destination segments [records | key bytes];
 // xchg = the count-exchange row [W][3]; rows_out (u64, device) = the table's
 // occupied slots.  extra gets STATUS_REDO when the table overflowed, a chunk
 // error word is set or the segments do not fit buf.
 u64 mr_compact_pack_ws_bytes(u64 cap, u32 W) {
   const u64 nb = (cap + pk::CP * pk::CP_PER - 1) / (pk::CP * pk::CP_PER);
-  return ((nb * 2 * W * 4 + 255) & ~255ull) + 2 * (u64)W * 8;
+  return ((nb * 2 * W * 8 + 255) & ~255ull) + 2 * (u64)W * 8;
 }
 
 int mr_compact_pack(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, u32 nparts, u32 W,
@@ -451,13 +441,13 @@ int mr_compact_pack(void* tag, void* hi, void* lo, void* val, void* rep, void* c
   g.mask = cap - 1;
   g.src = (const u8*)src;
   const u64 nb = (cap + pk::CP * pk::CP_PER - 1) / (pk::CP * pk::CP_PER);
-  u32* bcnt = (u32*)ws;
-  unsigned long long* coltot = (unsigned long long*)((u8*)ws + ((nb * 2 * W * 4 + 255) & ~255ull));
+  unsigned long long* bcnt = (unsigned long long*)ws;
+  unsigned long long* coltot = (unsigned long long*)((u8*)ws + ((nb * 2 * W * 8 + 255) & ~255ull));
   hipLaunchKernelGGL(pk::cp_count_kernel, dim3((unsigned)nb), dim3(pk::CP), 0, s, g, cap, nparts, W, (const u8*)src,
                      bcnt);
   hipLaunchKernelGGL(pk::cp_scan_kernel, dim3(2 * W), dim3(pk::CS), 0, s, bcnt, nb, coltot);
   hipLaunchKernelGGL(pk::cp_scatter_kernel, dim3((unsigned)nb), dim3(pk::CP), 2 * W * sizeof(unsigned long long), s, g,
-                     cap, nparts, W, (const u8*)src, (const u32*)bcnt, (const unsigned long long*)coltot, (u8*)buf,
+                     cap, nparts, W, (const u8*)src, (const unsigned long long*)bcnt, (const unsigned long long*)coltot, (u8*)buf,
                      buf_cap, (long long*)xchg, extra, (const u32*)ctrl + 1, (const int*)errs, nerr,
                      (unsigned long long*)rows_out);
   return (int)hipGetLastError();

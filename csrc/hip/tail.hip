@@ -385,9 +385,14 @@ static int tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, voi
   hipLaunchKernelGGL(tl::tail_scatter_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, g, cap, nparts, (const u8*)src,
                      (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
                      (const u32*)bcount, out_cap);
-  if (pad && n > 0 && ghist != nullptr && n <= (u64)tl::HIST_BLOCKS * 65535u) {
-    u64 hb = (n + 4 * tl::T - 1) / (4 * tl::T);
-    if (hb > (u64)tl::HIST_BLOCKS) hb = tl::HIST_BLOCKS;  // (<= 65535 rows per block: 16-bit counters)
+  u64 phb = (n + 4 * tl::T - 1) / (4 * tl::T);
+  if (phb > (u64)tl::HIST_BLOCKS) phb = tl::HIST_BLOCKS;
+  // 16-bit counters: a block walks ceil(n / (hb * T)) grid strides of T rows,
+  // all of which may fall in one bin — that must stay <= 65535 (a bound on the
+  // rows per BLOCK, not on the total: the grid is capped at HIST_BLOCKS)
+  const u64 rows_per_block = phb ? (n + phb * tl::T - 1) / (phb * tl::T) * tl::T : 0;
+  if (pad && n > 0 && ghist != nullptr && rows_per_block <= 65535u) {
+    const u64 hb = phb;
     hipLaunchKernelGGL(tl::tail_padhist_kernel, dim3((unsigned)hb), dim3(tl::T), 0, s, (const unsigned long long*)counter,
                        n, (u64*)out_hi, (u64*)out_lo, (long long*)out_val, (u64*)out_rep, (u32*)out_part, (u64*)out_c,
                        (const u32*)ctrl + 1, (u32*)bad, (u32*)ghist, nparts, (long long*)pcount);

@@ -38,6 +38,12 @@ def main(argv=None) -> int:
         signal.signal(signal.SIGTERM, _dump)
         prof_dir = os.path.abspath(prof_dir)
         prof.enable()
+    else:
+        import signal
+
+        def _term(*_):
+            raise SystemExit(143)  # unwind: the worker frees its hbm arena (/dev/shm chunks on a CPU node)
+        signal.signal(signal.SIGTERM, _term)
     w = worker.new(a.connection_string, a.dbname)
     cfg = dict(max_iter=a.max_iter, max_sleep=a.max_sleep, max_tasks=a.max_tasks, verbose=not a.quiet,
                gpu=a.gpu if a.gpu in ("auto", "none") else int(a.gpu))

@@ -77,8 +77,7 @@ _SIGS = {
     "mr_ts_keys": [_p, _u64, _p, _p, _p, _p],
     "mr_ts_checksum": [_p, _u64, _p, _p],
     "mr_ts_unsorted": [_p, _p, _u64, _p, _p],
-    "mr_pack_by_dest": [_p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, ctypes.c_longlong, _p, _p, _i32, _p, _p, _p,
-                        _u32, _p],
+    "mr_pack_by_dest": [_p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, ctypes.c_longlong, _p, _p, _i32, _p],
     "mr_fix_loc": [_p, _u64, _p, _p, _u32, _p, _p],
     "mr_tail_compact": [_p, _p, _p, _p, _p, _p, _u64, _u32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _u64, _u64,
                         _i32, _p, _p],
@@ -128,9 +127,18 @@ _SIGS = {
     "mr_sdma_d2h": [_p, _p, _p, _i32],
     "mr_sdma_d2h_begin": [_p, _p, _p, _i32, _p],
     "mr_sdma_wait": [_u64],
+    "mr_ipc_alloc": [_u64, ctypes.POINTER(ctypes.c_void_p)],
+    "mr_ipc_free": [_p],
+    "mr_ipc_handle": [_p, _p],
+    "mr_ipc_open": [_p, ctypes.POINTER(ctypes.c_void_p)],
+    "mr_ipc_close": [_p],
+    "mr_gather_copy": [_p, _u32, _u64, _p],
+    "mr_gather_copy_chunk": [],
+    "mr_mrc1_decode": [_p, _p, _u32, _u64, _p, _p, _p, _p, _p],
 }
 _RESTYPE_U64 = {"mr_compact_pack_ws_bytes", "mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
-                "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words", "mr_sdma_d2h_begin"}
+                "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words", "mr_sdma_d2h_begin",
+                "mr_gather_copy_chunk"}
 
 
 def lib():

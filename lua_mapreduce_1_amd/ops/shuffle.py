@@ -31,7 +31,7 @@ def pack_by_dest(hi, lo, val, rep, part, W: int, src, extra: int = 0, blob_capac
         xchg = torch.empty(3 * W, dtype=torch.int64, device=d)
         _hip.call("mr_pack_by_dest", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), n, W,
                   _hip.ptr(src) if src is not None else None, _hip.ptr(ws), _hip.ptr(xchg), int(extra),
-                  _hip.ptr(rec), _hip.ptr(blob), 0, None, None, None, 0, _hip.stream(d))
+                  _hip.ptr(rec), _hip.ptr(blob), 0, _hip.stream(d))
         return rec, blob, xchg
     dest = (part.numpy().astype(np.int64) % W)
     order = np.argsort(dest, kind="stable")
@@ -62,16 +62,11 @@ def seg_bytes(rows: int, nbytes: int) -> int:
 STATUS_REDO = 1 << 40  # csrc/hip/shuffle.hip: added to the exchanged extra column by a rank that must redo its map
 
 
-def pack_by_dest_combined(hi, lo, val, rep, part, W: int, src, extra: int = 0, n_dev=None, status=None):
+def pack_by_dest_combined(hi, lo, val, rep, part, W: int, src, extra: int = 0):
     """GPU: ONE uint8 buffer of per-destination segments [records (32 B:
     hi, lo, val, loc) | key bytes, padded to 8] + the count-exchange row
     [records, bytes, extra] per destination; destination d's segment is
     seg_bytes(rows_d, bytes_d) long, so the payload is a single all-to-all.
-    ``n_dev``: the row count as a device int64 (the columns then hold a
-    bound of rows, not the count: nothing is read on the host).
-    ``status`` = (table ctrl, chunk error words): a rank whose map table
-    overflowed, whose map reported a device error or whose rows exceed the
-    bound adds STATUS_REDO to its exchanged extra column.
     -> (buf uint8, xchg int64 [3W])."""
     assert hi.is_cuda
     n = hi.numel()
@@ -80,20 +75,14 @@ def pack_by_dest_combined(hi, lo, val, rep, part, W: int, src, extra: int = 0, n
     cap = 32 * n + ((src.numel() if src is not None else 0) + 16 * n) + 8 * W
     ws, buf = _combined_bufs(d, W, cap)
     xchg = torch.empty(3 * W, dtype=torch.int64, device=d)
-    ovf = errs = None
-    nerr = 0
-    if status is not None:
-        ctrl, ew = status
-        ovf = _hip.ptr(ctrl[1:2])
-        if ew is not None and ew.numel():
-            errs, nerr = _hip.ptr(ew), int(ew.numel())
     _hip.call("mr_pack_by_dest", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), n, W,
               _hip.ptr(src) if src is not None else None, _hip.ptr(ws), _hip.ptr(xchg), int(extra),
-              _hip.ptr(buf), _hip.ptr(buf), 1, _hip.ptr(n_dev), ovf, errs, nerr, _hip.stream(d))
+              _hip.ptr(buf), _hip.ptr(buf), 1, _hip.stream(d))
     return buf, xchg
 
 
-def compact_pack(table, src, nparts: int, W: int, bound: int, extra: int = 0, errs=None, cap_bytes: int | None = None):
+def compact_pack(table, src, nparts: int, W: int, bound: int, extra: int = 0, errs=None, cap_bytes: int | None = None,
+                 min_bytes: int = 0):
     """The W > 1 single-sync send side straight from the map's hash table
     (csrc/hip/shuffle.hip mr_compact_pack: three launches, no dense
     columns): every occupied slot -> its destination (FNV-1 partition of the
@@ -103,11 +92,14 @@ def compact_pack(table, src, nparts: int, W: int, bound: int, extra: int = 0, er
     whose table overflowed, whose chunk error words are set (``errs``) or
     whose segments outgrow the buffer adds STATUS_REDO to its exchanged
     extra column.  ``cap_bytes`` (tests): the buffer capacity the kernels
-    assume, instead of the bound's.  -> (buf uint8, xchg int64 [3W], rows
+    assume, instead of the bound's.  ``min_bytes``: a floor on the capacity
+    (the segment total a flagged exchange reported: keys that overlap in
+    their source, e.g. n-gram spans, can need more key bytes than the
+    bound-derived capacity holds).  -> (buf uint8, xchg int64 [3W], rows
     int64 [1])."""
     d = table.device
     lib = _hip.lib()
-    cap = 32 * bound + (src.numel() if src is not None else 0) + 16 * bound + 8 * W
+    cap = max(32 * bound + (src.numel() if src is not None else 0) + 16 * bound + 8 * W, int(min_bytes))
     ws, buf = _combined_bufs(d, W, cap)
     ncap = buf.numel() if cap_bytes is None else min(int(cap_bytes), buf.numel())
     nws = int(lib.mr_compact_pack_ws_bytes(table.cap, W))

@@ -729,7 +729,8 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
             with trace.range("mr.compact_pack"):
                 # table -> per-destination segments in three launches (no dense columns)
                 buf, xchg, cnt = SH.compact_pack(self.table, src, self.nparts, W, bound, extra=failed, errs=errs,
-                                                 cap_bytes=getattr(self, "_send_cap_test", None))
+                                                 cap_bytes=getattr(self, "_send_cap_test", None),
+                                                 min_bytes=getattr(self, "_send_cap_min", 0))
                 self._send_cap_test = None  # (a test's one-shot: a send buffer too small)
             with trace.range("mr.count_exchange"):
                 recv = D.exchange_counts(xchg, self.group)
@@ -750,6 +751,13 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                 break
             # a redo: this rank fixes what it flagged, every rank exchanges again
             self._send_est = n_claimed
+            # the exchanged row holds the true per-destination totals even when
+            # the send buffer was too small: the next buffer holds them all, so
+            # a redo for capacity always makes progress (the floor is kept:
+            # the key-byte total of overlapping keys does not shrink)
+            need = sum(SH.seg_bytes(r[0], r[1]) for r in send_h)
+            if need > getattr(self, "_send_cap_min", 0):
+                self._send_cap_min = need + need // 8
             bad = [k for k in range(nch) if e is not None and e[k]]
             if bad:
                 self._mark_broken(jobs, recs, bad)
@@ -1071,6 +1079,9 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
                         self._red_distinct = None
                     n_red = self._reduce_insert_received(src, rcounts, rows) if e.overflow else \
                         self.red_table.stats()[0]
+                    # the next iteration's bound guess follows the grown key
+                    # count (else every later iteration fails the bound again)
+                    self._red_distinct = int(n_red)
                     padded = False
                     pend = self._finalize_table(self.red_table, n_red, src)
                 except devmod.BlobCapacityError as e:

@@ -556,16 +556,11 @@ def _tail_ws(d, n: int, nparts: int, blob_cap: int, cap: int):
 _CP_WS: dict = {}
 
 
-def compact_partition(table, n: int, src, nparts: int, bound: bool = False):
+def compact_partition(table, n: int, src, nparts: int):
     """Occupied slots of a table -> dense (hi, lo, val, rep) + exact FNV-1
     partition (int32), in ONE kernel (tail_compact; its composite sort key and
     digit histograms are by-products).  The send side of the shuffle; buffers
-    are reused across iterations (valid until the next call).
-
-    ``bound=True``: ``n`` is a bound on the rows, not their count (which is
-    then never read on the host before the shuffle): rows past it are
-    dropped, and the count comes back as a sixth value, a device int64[1]
-    (it exceeds ``n`` when rows were dropped)."""
+    are reused across iterations (valid until the next call)."""
     from ..ops import _hip
     d = table.device
     ws = _CP_WS.get(d)
@@ -584,8 +579,6 @@ def compact_partition(table, n: int, src, nparts: int, bound: bool = False):
     _hip.call("mr_tail_compact", *table._gtab(), table.cap, nparts, _hip.ptr(src), _hip.ptr(hi), _hip.ptr(lo),
               _hip.ptr(val), _hip.ptr(rep), _hip.ptr(part), _hip.ptr(c), _hip.ptr(small[:1]),
               None, None, _hip.ptr(ws["bhist"]), n, n, 0, None, _hip.stream(d))  # no digit histograms here
-    if bound:
-        return hi, lo, val, rep, part[:n], small[:1]
     return hi, lo, val, rep, part[:n]
 
 

@@ -9,8 +9,10 @@ make_lines_iterator)`` exactly like fs.lua:185-208:
 * ``sshfs``  — mappers write locally, reducers pull the partition's files from
   each mapper host with ``scp -CB`` (fs.lua:141-181); falls back to ``shared``
   when all mappers are local or no hostnames are given (fs.lua:200-201);
-* ``hbm``    — new: files kept in this process's memory (the in-HBM/in-memory
-  store used by single-process and SPMD runs).
+* ``hbm``    — new: node-local files that stay in device memory
+  (runtime/hbm_store.py): the coordinator holds a descriptor per file, the
+  bytes stay in the map worker's exported HBM arena and reducers pull them
+  peer to peer; works across the worker processes of one node.
 
 ``make_lines_iterator(name)`` yields decoded ``(key, [values])`` records.
 """
@@ -129,59 +131,59 @@ class SSHFS(SharedFS):
         shutil.rmtree(getattr(self, "tmpname", ""), ignore_errors=True)
 
 
-class MemFS:
-    """Process-local in-memory store (``hbm`` storage)."""
-    _files: dict[str, object] = {}
-    _lock = threading.Lock()
+class HBMFS:
+    """``hbm`` storage: the coordinator's blob store holds a descriptor per
+    file (runtime/hbm_store.py), the bytes stay in the writer's device arena.
+    Listing and removal are the coordinator's; reads resolve the descriptor."""
 
-    def __init__(self, path: str = "", hostnames=None):
-        self.path = path
+    def __init__(self, cnn, gen=None):
+        self.g = cnn.gridfs()
+        self.gen = gen
 
-    def list(self, match=None) -> list[dict]:
-        rx = _rx(match)
-        with self._lock:
-            names = sorted(self._files)
-        return [{"filename": n} for n in names if rx is None or rx.search(n)]
+    def list(self, match=None, prefix: str = "") -> list[dict]:
+        return self.g.list(match, prefix=prefix)
 
     def remove_file(self, filename: str) -> bool:
-        with self._lock:
-            return self._files.pop(filename, None) is not None
+        return self.g.remove_file(filename)
 
-    def put(self, filename: str, obj) -> None:
-        with self._lock:
-            self._files[filename] = obj
-
-    def get(self, filename: str):
-        with self._lock:
-            return self._files.get(filename)
+    def get(self, filename: str) -> bytes | None:
+        from . import hbm_store
+        d = self.g.get(filename)
+        if d is None or not hbm_store.is_descriptor(d):
+            return d
+        return hbm_store.store().read_bytes(d)
 
     read = get
 
 
-class MemBuilder:
-    def __init__(self, fs: MemFS):
+class HBMBuilder:
+    def __init__(self, fs: HBMFS):
         self.fs = fs
         self.parts: list[bytes] = []
 
     def append(self, data) -> bool:
-        self.parts.append(data if isinstance(data, bytes) else str(data).encode())
+        self.parts.append(data if isinstance(data, bytes) else str(data).encode("utf-8", "surrogateescape"))
         return True
 
     write = append
 
     def build(self, filename: str) -> bool:
-        self.fs.put(filename, b"".join(self.parts))
+        from . import hbm_store
+        (name, desc), = hbm_store.store().put_many([(filename, b"".join(self.parts))], self.fs.gen)
+        self.fs.g.store_many([(name, desc)])
         self.parts = []
         return True
 
 
-def router(cnn, hostnames, storage: str, path: str):
+def router(cnn, hostnames, storage: str, path: str, gen=None):
+    """``gen``: the task iteration a writer's files belong to (``hbm``: the
+    arena of an earlier iteration is released when the next one writes)."""
     if storage == "gridfs":
         g = cnn.gridfs()
         return g, (lambda: cnn.grid_file_builder()), (lambda name: codec.decode_records(g.get(name) or b""))
     if storage == "hbm":
-        m = MemFS(path)
-        return m, (lambda: MemBuilder(m)), (lambda name: codec.decode_records(m.get(name) or b""))
+        m = HBMFS(cnn, gen)
+        return m, (lambda: HBMBuilder(m)), (lambda name: codec.decode_records(m.get(name) or b""))
     if storage == "sshfs" and hostnames:
         s = SSHFS(path, hostnames)
 
@@ -201,7 +203,7 @@ def read_blob(cnn, storage: str, path: str, name: str) -> bytes:
     if storage == "gridfs":
         return cnn.gridfs().get(name) or b""
     if storage == "hbm":
-        return MemFS(path).get(name) or b""
+        return HBMFS(cnn).get(name) or b""
     with open(name, "rb") as f:
         return f.read()
 

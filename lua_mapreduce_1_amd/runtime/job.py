@@ -33,6 +33,21 @@ _NAME = "job"
 
 _cache: dict = {}
 
+# diagnosis (tools/bench_server_worker.py --dump): every device map output and
+# every device reduce's inputs (name, size, crc32) and result are also written
+# to this directory, so a wrong final answer can be traced to the job and the
+# stage (map kernel, transport, reduce) that produced it
+_DUMP = os.environ.get("MR_DEBUG_DUMP") or None
+
+
+def _dump(kind: str, name: str, blob: bytes) -> None:
+    if _DUMP is None:
+        return
+    os.makedirs(_DUMP, exist_ok=True)
+    path = os.path.join(_DUMP, f"{kind}.{os.path.basename(name)}.{os.getpid()}.{_time.monotonic_ns()}")
+    with open(path, "wb") as f:
+        f.write(blob)
+
 
 def cached(func):
     """Memoise a 1-argument function (job.lua:42-55; used for partitionfn)."""
@@ -200,7 +215,7 @@ class job:  # noqa: N801
 
             g(map_key, map_value, emit)
             self.mark_as_finished()
-            fs, make_builder, _ = fsmod.router(self.cnn, None, self.storage, self.path)
+            fs, make_builder, _ = fsmod.router(self.cnn, None, self.storage, self.path, self._gen())
             parts: dict[int, list] = {}
             for key in utils.keys_sorted(result):
                 values = result[key]
@@ -225,6 +240,11 @@ class job:  # noqa: N801
             self.mark_as_written(elapsed)
             return elapsed
         return run
+
+    def _gen(self):
+        """The task iteration this job's outputs belong to (hbm storage:
+        the arena of an earlier iteration is released by the next one)."""
+        return (self.cnn.dbname, self.task_tbl.get("iteration"))
 
     def _register_output(self, name: str) -> None:
         """Index the file in the coordinator so the server can find partitions
@@ -310,10 +330,16 @@ class job:  # noqa: N801
         return elapsed
 
     def _store_outputs(self, outputs, index) -> None:
-        fs, make_builder, _ = fsmod.router(self.cnn, None, self.storage, self.path)
+        """A map job's partition files and their index entries: ONE
+        coordinator request for gridfs (the bytes) and hbm (descriptors of
+        the bytes just copied into this worker's device arena)."""
+        fs, make_builder, _ = fsmod.router(self.cnn, None, self.storage, self.path, self._gen())
         gfs = self.cnn.gridfs()
         if self.storage == "gridfs":
             gfs.store_many(outputs + index)
+        elif self.storage == "hbm":
+            from . import hbm_store
+            gfs.store_many(hbm_store.store().put_many(outputs, self._gen()) + index)
         else:
             for name, blob in outputs:
                 b = make_builder()
@@ -333,7 +359,6 @@ class job:  # noqa: N801
         ctx.flush_host_pairs()
         self.mark_as_finished()
         cols = dev.finalize_table(ctx.table, ctx.source(), nparts, pmod, need_keys=True)
-        fs, make_builder, _ = fsmod.router(self.cnn, None, self.storage, self.path)
         # every storage's build replaces an existing file (BLOB_PUT overwrites,
         # file builders rename over), so the reference's remove-before-build
         # (job.lua:217-221) is one round trip per file with no effect; with the
@@ -348,15 +373,8 @@ class job:  # noqa: N801
             name = f"{self.path}/{self.results_ns}.P{p}.M{map_key}"
             outputs.append((name, codec.encode_columnar(s["hi"], s["lo"], s["val"], s["key_off"], s["key_blob"])))
             index.append((INDEX_PREFIX + name + INDEX_SEP + host, b""))
-        gfs = self.cnn.gridfs()
-        if self.storage == "gridfs":
-            gfs.store_many(outputs + index)
-        else:
-            for name, blob in outputs:
-                b = make_builder()
-                b.append(blob)
-                b.build(name)
-            gfs.store_many(index)
+            _dump("map", name, outputs[-1][1])
+        self._store_outputs(outputs, index)
         elapsed = _time.process_time() - clock1
         self.mark_as_written(elapsed)
         return elapsed
@@ -376,26 +394,44 @@ class job:  # noqa: N801
             fs, _, make_lines_iterator = fsmod.router(self.cnn, mappers, self.storage, self.path)
             import re
             match = {"filename": {"$regex": "^" + re.escape(job_file) + r"\..*"}}
-            if self.storage == "gridfs":
+            if self.storage in ("gridfs", "hbm"):
                 filenames = [v["filename"] for v in fs.list(match, prefix=job_file + ".")]
             else:
                 filenames = [v["filename"] for v in fs.list(match)]
             rstore, rbuilder = result_store(self.cnn, self.storage, self.path)
             rstore.remove_file(res_file)
             blobs = None
+            pulled = None
             cols_op = dev_op is not None and dev_op not in FOLD_OPS and _is_cols(dev_op)
             if (dev_op in FOLD_OPS or cols_op) and filenames:
-                if self.storage == "gridfs":  # all inputs in one round trip per shard
+                if self.storage in ("gridfs", "hbm"):  # all inputs (or descriptors) in one round trip per shard
                     blobs = [b or b"" for b in self.cnn.gridfs().get_many(filenames)]
                 else:
                     blobs = [fsmod.read_blob(self.cnn, self.storage, self.path, n) for n in filenames]
+                if self.storage == "hbm":
+                    from . import hbm_store
+                    if not all(hbm_store.is_descriptor(b) for b in blobs):
+                        raise RuntimeError("hbm storage: a map file's descriptor is missing")
+                    if dev_op in FOLD_OPS and dev.default_device().type == "cuda":
+                        pulled = blobs  # the files stay on the device (pulled peer to peer below)
+                    else:
+                        blobs = hbm_store.store().read_many(blobs)
                 magic = codec.MAGIC_COL2 if cols_op else codec.MAGIC_COL
-                if not all(b[:4] == magic for b in blobs):
+                if pulled is None and not all(b[:4] == magic for b in blobs):
                     blobs = None
             b = rbuilder()
             if blobs is not None:
                 with dev.PLANE_LOCK:
-                    b.append(_device_reduce_cols(blobs, dev_op) if cols_op else _device_reduce(blobs, dev_op))
+                    if pulled is not None:
+                        out = _device_reduce_hbm(pulled, dev_op)
+                    else:
+                        out = _device_reduce_cols(blobs, dev_op) if cols_op else _device_reduce(blobs, dev_op)
+                b.append(out)
+                if _DUMP is not None and pulled is None:
+                    import zlib
+                    _dump("redin", res_file, "\n".join(f"{n}\t{len(x)}\t{zlib.crc32(x)}" for n, x in
+                                                      zip(filenames, blobs)).encode())
+                    _dump("redout", res_file, out)
             else:
                 merged = utils.merge_iterator(fs, filenames, make_lines_iterator)
                 recs = None
@@ -417,7 +453,7 @@ class job:  # noqa: N801
             if not self.mark_as_written(elapsed):
                 return elapsed
             gfs = self.cnn.gridfs()
-            if self.storage == "gridfs":
+            if self.storage in ("gridfs", "hbm"):
                 gfs.remove_many(filenames)
             else:
                 for n in filenames:
@@ -428,11 +464,69 @@ class job:  # noqa: N801
         return run
 
 
+def _aligned_bases(lens) -> tuple[list[int], int]:
+    """Offsets of files laid out back to back at 4 mod 16 (an MRC1 file's
+    8-byte columns follow its 20-byte header: they are then aligned)."""
+    bases, total = [], 0
+    for n in lens:
+        off = (total + 15) // 16 * 16 + 4
+        bases.append(off)
+        total = off + n
+    return bases, total
+
+
+def _decode_files(buf: torch.Tensor, bases: list[int], rows: list[int]):
+    """MRC1 files at ``bases`` of one device buffer -> (hi, lo, val, rep)
+    columns, ONE launch (csrc/hip/ipc.hip); rep words index ``buf``."""
+    from ..ops import _hip
+    d = buf.device
+    rstart = np.zeros(len(rows) + 1, np.int64)
+    np.cumsum(rows, out=rstart[1:])
+    n = int(rstart[-1])
+    meta = torch.from_numpy(np.concatenate([np.asarray(bases, np.int64), rstart])).to(d)
+    cols = torch.empty((4, max(n, 1)), dtype=torch.int64, device=d)
+    hi, lo, val, rep = (cols[i, :n] for i in range(4))
+    _hip.call("mr_mrc1_decode", _hip.ptr(buf), _hip.ptr(meta), len(rows), n, _hip.ptr(hi), _hip.ptr(lo),
+              _hip.ptr(val), _hip.ptr(rep), _hip.stream(d))
+    return hi, lo, val, rep
+
+
+def _reduce_device_cols(hi, lo, val, rep, src, op: str) -> bytes:
+    d = hi.device
+    tab = _reduce_table(d, op, 2 * hi.numel())
+    tab.insert(hi, lo, val, rep, src=src)  # long keys verified against their bytes
+    out = dev.finalize_table(tab, src, 1, None, need_keys=True)  # one partition: the job's own
+    return codec.encode_columnar(out["hi"], out["lo"], out["val"], out["key_off"], out["key_blob"])
+
+
+def _device_reduce_hbm(descs: list[bytes], op: str) -> bytes:
+    """``hbm`` storage: the partition's files are pulled from the map
+    workers' device arenas (peer to peer, one launch) and decoded on the
+    device (one launch) — no host copy of the intermediate data."""
+    from . import hbm_store
+    d = dev.default_device()
+    buf, bases, ds = hbm_store.store().pull_device(descs, d)
+    hi, lo, val, rep = _decode_files(buf, bases, [x["rows"] for x in ds])
+    return _reduce_device_cols(hi, lo, val, rep, buf, op)
+
+
 def _device_reduce(blobs: list[bytes], op: str) -> bytes:
     """Merge columnar partition files on the device: hash-aggregate all
-    (key, value) rows, sort, write one columnar result."""
-    cols = [codec.decode_columnar(b) for b in blobs]
+    (key, value) rows, sort, write one columnar result.  On the GPU the files
+    go up as they are (one pinned staging copy, one H2D copy) and are decoded
+    there by one launch."""
     d = dev.default_device()
+    if d.type == "cuda":
+        bases, total = _aligned_bases([len(b) for b in blobs])
+        stage = torch.empty(max(total, 16), dtype=torch.uint8, pin_memory=True)
+        a = stage.numpy()
+        for off, b in zip(bases, blobs):
+            a[off:off + len(b)] = np.frombuffer(b, np.uint8)
+        buf = stage.to(d, non_blocking=True)
+        rows = [int(np.frombuffer(b, np.uint64, 1, 4)[0]) for b in blobs]
+        hi, lo, val, rep = _decode_files(buf, bases, rows)
+        return _reduce_device_cols(hi, lo, val, rep, buf, op)
+    cols = [codec.decode_columnar(b) for b in blobs]
     n = sum(int(c["hi"].size) for c in cols)
     hi = torch.from_numpy(np.concatenate([c["hi"] for c in cols]).view(np.int64)).to(d)
     lo = torch.from_numpy(np.concatenate([c["lo"] for c in cols]).view(np.int64)).to(d)
@@ -547,11 +641,9 @@ def _device_reduce_lists(merged: list, rmod) -> list | None:
 
 
 def result_store(cnn, storage: str, path: str):
-    """Where reduce results live: the coordinator blob store (results always go
-    to GridFS in the reference, job.lua:249-251), or process memory for hbm."""
-    if storage == "hbm":
-        m = fsmod.MemFS(path)
-        return m, (lambda: fsmod.MemBuilder(m))
+    """Where reduce results live: the coordinator blob store, whatever the
+    storage of the intermediate files (results always go to GridFS in the
+    reference, job.lua:249-251)."""
     g = cnn.gridfs()
     return g, (lambda: cnn.grid_file_builder())
 

@@ -23,7 +23,7 @@ from .. import utils
 from ..utils.config import TUNABLES
 from ..utils import STATUS, TASK_STATUS
 from ..utils.tuple import tuple as tuple_
-from . import codec, fs as fsmod, modules
+from . import codec, modules
 from .cnn import cnn as cnn_cls
 from .job import result_store
 from .task import task as task_cls
@@ -203,15 +203,12 @@ class server:  # noqa: N801
         else:
             self.finished = True
             self.task.set_task_status(TASK_STATUS.FINISHED)
+        # (hbm storage: the coordinator holds the files' descriptors, removed
+        # here like gridfs files; the workers free their arenas at task end)
         g = self.cnn.gridfs()
         for f in g.list():
             if not re.match(match, f["filename"]) or remove_all:
                 g.remove_file(f["filename"])
-        if storage == "hbm":
-            m = fsmod.MemFS(path)
-            for f in m.list():
-                if not re.match(match, f["filename"]) or remove_all:
-                    m.remove_file(f["filename"])
 
     # ------------------------------------------------------------------------
     def loop(self) -> None:

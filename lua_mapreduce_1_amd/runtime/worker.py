@@ -155,6 +155,10 @@ class worker:  # noqa: N801
             self.cnn.flush_pending_inserts()
             if job_done:
                 self._print("# TASK done")
+                # hbm storage: every reduce of the task has read this worker's
+                # map files (the task finished): free its device arena
+                from . import hbm_store
+                hbm_store.release()
                 it = 0
                 iter_sleep = self.poll_sleep
                 ntasks += 1
@@ -221,6 +225,8 @@ class worker:  # noqa: N801
                 raise RuntimeError("Maximum number of retries achieved")
         finally:
             self._hb_stop.set()
+            from . import hbm_store
+            hbm_store.release()
 
 
 def utest() -> None:

@@ -200,3 +200,55 @@ def test_single_sync_iteration_rccl_one_gpu(mode):
     if mode in ("map_overflow", "device_error"):
         steady = waits[4:]
     assert max(steady) <= 2, waits
+
+
+def _long_keys_worker(port, q):
+    """One-rank nccl group, W>1 path forced, keys that overlap in their
+    source (tests/long_key_modules.py): the send buffer sized from the row
+    bound is too small for their key bytes every iteration."""
+    import sys
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import datetime
+    from collections import Counter
+    import torch
+    import torch.distributed as dist
+    import long_key_modules as LK
+    from lua_mapreduce_1_amd.parallel.spmd import SPMDEngine, SplitStore
+    from lua_mapreduce_1_amd.runtime import codec
+    from lua_mapreduce_1_amd.utils.corpus import europarl_like
+    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}",
+                            timeout=datetime.timedelta(seconds=120), device_id=torch.device("cuda", 0))
+    splits = europarl_like(seed=9, lines=8_000, words=120_000, vocab_size=8_000, split_lines=1000)
+    want = Counter(w.decode("utf-8", "surrogateescape") for s in splits for w in LK.windows(s))
+    L = "long_key_modules"
+    eng = SPMDEngine(dict(taskfn=L, mapfn=L, partitionfn=L, reducefn=L, finalfn=L,
+                          init_args={"nsplits": len(splits), "num_reducers": 7}, force_shuffle=True),
+                     split_store=SplitStore(splits, pin=True), device=torch.device("cuda", 0))
+    ok = []
+    for i in range(3):
+        res = eng.run_iteration()
+        got = {}
+        for _n, cols in eng.gather_results(res):
+            for k, v in codec.iter_columnar(cols):
+                got[k] = got.get(k, 0) + v[0]
+        ok.append(got == want)
+    q.put((ok, eng._single_sync_ok(True, True), getattr(eng, "_send_cap_min", 0)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_single_sync_send_capacity_redo_long_keys():
+    """a capacity redo of the single-sync count exchange grows the
+    send buffer from the exchanged per-destination totals, so keys whose bytes
+    exceed the bound-derived capacity finish (they looped forever before)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_long_keys_worker, args=(_free_port(), q))
+    p.start()
+    p.join(240)
+    if p.exitcode is None:
+        p.kill()
+    assert p.exitcode == 0
+    ok, single, floor = q.get(timeout=5)
+    assert single and all(ok) and floor > 0, (ok, single, floor)
