@@ -444,8 +444,9 @@ int mr_tail_pack(const void* val, const void* off, u64 n, const void* counts, u3
 // queued from C++ instead of ~20 Python-level calls and tensor allocations per
 // iteration (at 8-GPU strong scaling the per-iteration host time was a large
 // part of the ~1 ms step).  All buffers live in one caller-owned workspace
-// (layout below, mr_tail_ws_layout), reused across iterations; the
-// decoupled-look-back granules of its sort are its own (own epoch counter).
+// (layout below, mr_tail_ws_layout), reused across iterations — except the
+// decoupled-look-back granules of its sort, which have a buffer of their own
+// (own epoch counter; see mr_tail_run).
 
 int mr_exclusive_scan_i64(const void* in, void* out, u64 n, void* partials, void* total, hipStream_t s);
 u64 mr_scan_partials_len(u64 n);
@@ -464,7 +465,7 @@ int mr_d2h_async(void* host_dst, const void* src, u64 nbytes, hipStream_t s);
 
 enum TailBuf : int {
   TB_HI0, TB_LO0, TB_VAL0, TB_REP0, TB_C, TB_PART0, TB_ZERO /* counter|ghist|pcount|sort ctrs|err|bad */,
-  TB_K0, TB_K1, TB_P0, TB_P1, TB_GRAN, TB_HI, TB_LO, TB_VAL, TB_REP, TB_PART, TB_LN, TB_OFF, TB_PARTIALS,
+  TB_K0, TB_K1, TB_P0, TB_P1, TB_HI, TB_LO, TB_VAL, TB_REP, TB_PART, TB_LN, TB_OFF, TB_PARTIALS,
   TB_BLOB, TB_PACKED, TB_BHIST, TB_COUNT
 };
 // TB_ZERO sub-layout (bytes): counter u64 @0 | ghist u32[2048] @8 | pcount i64[256] @8200 |
@@ -474,9 +475,8 @@ constexpr u64 TZ_GHIST = 8, TZ_PCOUNT = 8200, TZ_TILES = 10248, TZ_ERR = 10504, 
 u64 mr_tail_ws_layout(u64 n, u32 nparts, u64 blob_cap, u64 cap, u64* off) {
   (void)nparts;
   const u64 m = n ? n : 1;
-  const u64 tiles = mr_onesweep_tiles(m);
   const u64 sz[TB_COUNT] = {8 * m, 8 * m, 8 * m, 8 * m, 8 * m, 4 * m, TZ_BYTES, 8 * m, 8 * m, 4 * m, 4 * m,
-                            tiles * 256 * 8, 8 * m, 8 * m, 8 * m, 8 * m, 4 * m, 8 * m, 8 * (m + 1),
+                            8 * m, 8 * m, 8 * m, 8 * m, 4 * m, 8 * m, 8 * (m + 1),
                             8 * mr_scan_partials_len(m), blob_cap ? blob_cap : 1, mr_tail_pack_bytes(m, 256),
                             mr_tail_bhist_bytes(cap)};
   u64 o = 0;
@@ -495,9 +495,18 @@ static u32 g_tail_epoch = 0;
 // padded != 0: n is a row bound, not the count (tail_pad_kernel): the host
 // learns the count from the downloaded partition counts, and bits 3/4 of the
 // downloaded flag word if the bound was too small / the table overflowed.
+// gran: the sort's look-back granules, >= 256 * mr_onesweep_tiles(n) u64 of a
+// buffer that holds nothing else (zeroed when allocated).  They used to be a
+// region of ws, whose layout moves with n: a later tail's granule rows then lay
+// over an earlier tail's permutation words, whose top bits can read as a live
+// epoch tag — a late predecessor's granule was taken from that stale word and
+// the pass scattered with a wrong prefix, silently (seen with 4 worker
+// processes sharing one GPU, whose contention makes predecessors late, and
+// whose fresh processes run small epochs; profiles/r6/server_worker/).
 int mr_tail_run(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, u64 n, u32 nparts,
-                const void* src, void* ws, u64 blob_cap, void* hp, void* hb, long long est, u64 hb_cap, int padded,
-                hipStream_t s) {
+                const void* src, void* ws, void* gran, u64 blob_cap, void* hp, void* hb, long long est, u64 hb_cap,
+                int padded, hipStream_t s) {
+  if (gran == nullptr) return -1;
   if (nparts > 256 || (padded && nparts > 255)) return -1;
   u64 off[TB_COUNT];
   mr_tail_ws_layout(n, nparts, blob_cap, cap, off);
@@ -517,7 +526,7 @@ int mr_tail_run(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl,
     if (!g_tail_epoch) g_tail_epoch = 1;
     void* kout = P(pass & 1 ? TB_K1 : TB_K0);
     void* pout = P(pass & 1 ? TB_P1 : TB_P0);
-    rc = mr_radix_onesweep_u32v(kin, pin, kout, pout, n, 8 * pass, z + TZ_GHIST + 4 * 256 * pass, P(TB_GRAN),
+    rc = mr_radix_onesweep_u32v(kin, pin, kout, pout, n, 8 * pass, z + TZ_GHIST + 4 * 256 * pass, gran,
                                 z + TZ_TILES + 4 * pass, g_tail_epoch, z + TZ_ERR, pass == 0 ? 1 : 0, s);
     if (rc) return rc;
     kin = kout;

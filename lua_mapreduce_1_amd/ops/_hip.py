@@ -33,8 +33,8 @@ _SIGS = {
     "mr_d2h_async": [_p, _p, _u64, _p],
     "mr_h2d_pull": [_p, _p, _u64, _i32, _p],
     "mr_signal_host": [_p, _u32, _p],
-    "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64, _i32,
-                    _p],
+    "mr_tail_run": [_p, _p, _p, _p, _p, _p, _u64, _u64, _u32, _p, _p, _p, _u64, _p, _p, ctypes.c_longlong, _u64,
+                    _i32, _p],
     "mr_tokenize": [_p, _u64, _u64, _u64, _p, _p, _p, _u64, _p, _p],
     "mr_hash_agg": [_p, _p, _p, _p, _u64, _u64, _i32, _p, _p, _p, _p, _p, _p, _u64, _p, _p],
     "mr_table_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p, _p],

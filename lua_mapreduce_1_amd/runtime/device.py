@@ -521,7 +521,21 @@ def finalize_device(hi, lo, val, rep, src, nparts: int, partition_module=None, p
 
 _TAIL_WS: dict = {}  # device -> (workspace uint8 tensor, {layout key: (offsets, views)})
 _TB = {name: i for i, name in enumerate(
-    "HI0 LO0 VAL0 REP0 C PART0 ZERO K0 K1 P0 P1 GRAN HI LO VAL REP PART LN OFF PARTIALS BLOB PACKED BHIST".split())}
+    "HI0 LO0 VAL0 REP0 C PART0 ZERO K0 K1 P0 P1 HI LO VAL REP PART LN OFF PARTIALS BLOB PACKED BHIST".split())}
+_TAIL_GRAN: dict = {}  # device -> the tail sort's look-back granules (a buffer of their own: mr_tail_run)
+
+
+def _tail_gran(d, n: int) -> torch.Tensor:
+    """Look-back granules of the fused tail's sort: zeroed when allocated and
+    never holding anything else, so a granule slot a pass reads before its
+    predecessor published is either zero or an older pass's epoch-tagged
+    entry — never a stale data word whose bits look like a live tag."""
+    from ..ops import _hip
+    need = 256 * int(_hip.lib().mr_onesweep_tiles(max(n, 1)))
+    g = _TAIL_GRAN.get(d)
+    if g is None or g.numel() < need:
+        g = _TAIL_GRAN[d] = torch.zeros(max(need, 256 * 64), dtype=torch.int64, device=d)
+    return g
 
 
 def _tail_ws(d, n: int, nparts: int, blob_cap: int, cap: int):
@@ -536,7 +550,7 @@ def _tail_ws(d, n: int, nparts: int, blob_cap: int, cap: int):
                                      ctypes.c_uint64(cap), offs))
     ws, views = _TAIL_WS.get(d, (None, {}))
     if ws is None or ws.numel() < need:
-        ws = torch.zeros(need + need // 4, dtype=torch.uint8, device=d)  # zeroed once: sort look-back granules
+        ws = torch.zeros(need + need // 4, dtype=torch.uint8, device=d)
         views = {}
     key = (n, nparts, blob_cap, cap)
     v = views.get(key)
@@ -545,7 +559,10 @@ def _tail_ws(d, n: int, nparts: int, blob_cap: int, cap: int):
         m = max(n, 1)
         i64 = lambda b, k: ws[o[_TB[b]]:o[_TB[b]] + 8 * k].view(torch.int64)  # noqa: E731
         v = {"args": tuple(i64(b, n) for b in ("HI0", "LO0", "VAL0", "REP0")), "hi": i64("HI", n), "lo": i64("LO", n),
-             "off": i64("OFF", m + 1), "blob": ws[o[_TB["BLOB"]]:o[_TB["BLOB"]] + max(blob_cap, 1)]}
+             "off": i64("OFF", m + 1), "blob": ws[o[_TB["BLOB"]]:o[_TB["BLOB"]] + max(blob_cap, 1)],
+             # (MR_DEBUG_TAIL: the packed download, the final permutation and sorted keys)
+             "packed": ws[o[_TB["PACKED"]]:], "p1": ws[o[_TB["P1"]]:o[_TB["P1"]] + 4 * n],
+             "k1": i64("K1", n), "c": i64("C", n), "zero": ws[o[_TB["ZERO"]]:o[_TB["ZERO"]] + 10512]}
         if len(views) > 8:
             views.clear()
         views[key] = v
@@ -615,10 +632,60 @@ def finalize_table_native(table, n: int, src, nparts: int, blob_cap: int | None 
     b = _INFLIGHT.get(d)
     if b is not None and (b.writes(hp.data_ptr(), hp.numel()) or b.writes(hb.data_ptr(), hb.numel())):
         b.wait()  # the native tail downloads into these pinned buffers on its stream
-    _hip.call("mr_tail_run", *table._gtab(), table.cap, n, nparts, _hip.ptr(src), _hip.ptr(ws), cap, _hip.ptr(hp),
-              _hip.ptr(hb), est_arg, hb.numel(), 1 if padded else 0, _hip.stream(d))
-    return {"n": n, "nparts": nparts, "args": v["args"], "src": src, "presorted": False, "hi": v["hi"], "lo": v["lo"],
-            "fused": True, "hp": hp, "off": v["off"], "blob": v["blob"], "est": est, "hb": hb, "padded": padded}
+    _hip.call("mr_tail_run", *table._gtab(), table.cap, n, nparts, _hip.ptr(src), _hip.ptr(ws),
+              _hip.ptr(_tail_gran(d, n)), cap, _hip.ptr(hp), _hip.ptr(hb), est_arg, hb.numel(), 1 if padded else 0,
+              _hip.stream(d))
+    out = {"n": n, "nparts": nparts, "args": v["args"], "src": src, "presorted": False, "hi": v["hi"], "lo": v["lo"],
+           "fused": True, "hp": hp, "off": v["off"], "blob": v["blob"], "est": est, "hb": hb, "padded": padded}
+    if _DEBUG_TAIL:
+        out.update(dbg_packed=v["packed"][:nb], dbg_perm=v["p1"], dbg_keys=v["k1"], dbg_c=v["c"], dbg_zero=v["zero"])
+    return out
+
+
+# diagnosis: MR_DEBUG_TAIL=1 checks every fused tail after a full device sync:
+# the pinned download as the host read it against the device buffer, the
+# final sort permutation (a bijection) and the sorted keys' order; a
+# difference is reported on stderr as "# DEBUG TAIL"
+import os as _os  # noqa: E402
+_DEBUG_TAIL = bool(_os.environ.get("MR_DEBUG_TAIL"))
+
+
+def _debug_tail_check(pend: dict, snap: np.ndarray, blob_snap) -> None:
+    import sys
+    torch.cuda.synchronize()
+    n = pend["n"]
+    dev_pack = pend["dbg_packed"].cpu().numpy()
+    bad_pack = np.flatnonzero(dev_pack[:snap.size] != snap[:dev_pack.size])
+    perm = pend["dbg_perm"].cpu().numpy().view(np.uint32)[:n] if n else np.zeros(0, np.uint32)
+    perm_ok = bool(n == 0 or (int(perm.max()) < n and np.bincount(perm, minlength=n).max() == 1))
+    keys = pend["dbg_keys"].cpu().numpy().view(np.uint64)[:n]
+    order_ok = bool(n < 2 or (keys[1:] >= keys[:-1]).all())
+    bad_blob = 0
+    if blob_snap is not None and blob_snap.size:
+        dev_blob = pend["blob"][:blob_snap.size].cpu().numpy()
+        bad_blob = int((dev_blob != blob_snap).sum())
+    if bad_pack.size or not perm_ok or not order_ok or bad_blob:
+        sys.stderr.write(f"# DEBUG TAIL: n={n} pack bytes {dev_pack.size}: {bad_pack.size} stale (first "
+                         f"{bad_pack[:4].tolist()}), perm ok {perm_ok}, order ok {order_ok}, stale blob bytes "
+                         f"{bad_blob}\n")
+        # the sort's inputs and control words: the composite keys (unchanged by
+        # the sort), their digit histograms as the compaction counted them,
+        # the per-pass tile counters and the error word
+        c = pend["dbg_c"].cpu().numpy().view(np.uint64)[:n]
+        z = pend["dbg_zero"].cpu().numpy()
+        gh = z[8:8 + 8192].view(np.uint32).reshape(8, 256)
+        want = np.stack([np.bincount(((c >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.int64), minlength=256)
+                         for b in range(8)]).astype(np.uint32)
+        tiles = z[10248:10248 + 32].view(np.uint32)
+        err, badw = z[10504:10508].view(np.uint32)[0], z[10508:10512].view(np.uint32)[0]
+        ref = np.sort(c)
+        wrong = np.flatnonzero(ref != keys)
+        from ..ops import _hip
+        sys.stderr.write(f"#   ghist ok {bool((gh == want).all())} (bad digits {np.flatnonzero((gh != want).any(1)).tolist()}),"
+                         f" tile counters {tiles.tolist()} (tiles {int(_hip.lib().mr_onesweep_tiles(n))}), err {err}, "
+                         f"bad {badw}, keys out of place {wrong.size} first {wrong[:3].tolist()} last "
+                         f"{wrong[-3:].tolist()}, distinct keys {np.unique(c).size}\n")
+        sys.stderr.flush()
 
 
 def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=None,
@@ -736,6 +803,11 @@ def finalize_host(pend: dict, partition_module=None, need_keys: bool = False, la
         if not defer:
             flush_downloads(hi.device)  # large downloads: on the SDMA engines, now that their data is produced
         hb, est, blob = pend["hb"], pend["est"], pend["blob"]
+        if pend.get("fused") and _DEBUG_TAIL:
+            snap = pend["hp"].numpy().copy()  # the download as the host reads it now
+            nb0 = int(snap[8 * pend["n"]:8 * pend["n"] + 4 * (pend["n"] + 1)].view(np.int32)[-1]) if pend["n"] else 0
+            bsnap = hb.numpy()[:min(nb0, hb.numel(), est if est is not None else nb0)].copy() if nb0 > 0 else None
+            _debug_tail_check(pend, snap, bsnap)
         if pend.get("fused"):
             f_val, f_off, f_counts, f_bad = _unpack_fused(pend)
             if pend.get("padded"):

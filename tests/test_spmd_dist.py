@@ -219,12 +219,16 @@ def _long_keys_worker(port, q):
     from lua_mapreduce_1_amd.utils.corpus import europarl_like
     dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}",
                             timeout=datetime.timedelta(seconds=120), device_id=torch.device("cuda", 0))
-    splits = europarl_like(seed=9, lines=8_000, words=120_000, vocab_size=8_000, split_lines=1000)
+    # long lines (60 words): nearly every window is WIDTH bytes long
+    splits = europarl_like(seed=9, lines=2_000, words=120_000, vocab_size=8_000, split_lines=250)
     want = Counter(w.decode("utf-8", "surrogateescape") for s in splits for w in LK.windows(s))
     L = "long_key_modules"
     eng = SPMDEngine(dict(taskfn=L, mapfn=L, partitionfn=L, reducefn=L, finalfn=L,
                           init_args={"nsplits": len(splits), "num_reducers": 7}, force_shuffle=True),
                      split_store=SplitStore(splits, pin=True), device=torch.device("cuda", 0))
+    # the first exchange sized from a small row bound (a fresh process: the
+    # reused send buffer has not been grown by an earlier, larger bound)
+    eng._send_est = 100
     ok = []
     for i in range(3):
         res = eng.run_iteration()

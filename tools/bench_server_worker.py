@@ -165,7 +165,7 @@ def run_once(a, rep: int, files_dir: str, logs: str, env: dict) -> dict:
     warn = []
     for i in range(a.workers):
         txt = open(os.path.join(logs, f"worker{i}.r{rep}.log")).read()
-        warn += [ln for ln in txt.splitlines() if "warning" in ln.lower() or "error" in ln.lower()][:5]
+        warn += [ln for ln in txt.splitlines() if any(w in ln.lower() for w in ("warning", "error", "debug tail"))][:5]
     out["worker_warnings"] = warn
     if server.returncode != 0 or not os.path.exists(final):
         out["valid"] = False
