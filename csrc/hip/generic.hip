@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(256) slot_compact_kernel(GTab g, u64 cap, long
 #pragma unroll
   for (int k = 0; k < SC_ITEMS; ++k) {
     const u64 i = b0 + (u64)k * 256 + t;
-    const bool o = i < cap && g.tag[i] != 0;
+    const bool o = i < cap && g.s[i].tag != 0;
     occ |= (o ? 1u : 0u) << k;
     const unsigned long long m = __ballot(o);
     rank[k] = (u32)__popcll(m & below);
@@ -229,8 +229,8 @@ __global__ void __launch_bounds__(256) slot_compact_kernel(GTab g, u64 cap, long
       const u64 i = b0 + (u64)k * 256 + t;
       const u64 o = base + wc[k * NW + wave] + rank[k];
       out_slot[o] = (long long)i;
-      out_hi[o] = g.hi[i];
-      out_lo[o] = g.lo[i];
+      out_hi[o] = g.s[i].hi;
+      out_lo[o] = g.s[i].lo;
       out_rep[o] = g.rep[i];
     }
   }
@@ -747,15 +747,7 @@ static inline unsigned ag_grid(u64 n, unsigned block, unsigned cap = 8192) {
 }
 
 static inline GTab ag_gtab(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, const void* src) {
-  GTab g;
-  g.tag = (u64*)tag;
-  g.hi = (u64*)hi;
-  g.lo = (u64*)lo;
-  g.val = (long long*)val;
-  g.rep = (u64*)rep;
-  g.ctrl = (u32*)ctrl;
-  g.mask = cap - 1;
-  g.src = (const u8*)src;
+  GTab g = gtab_make(tag, rep, ctrl, cap, (const u8*)src);
   return g;
 }
 

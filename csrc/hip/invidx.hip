@@ -660,15 +660,9 @@ int mr_ii_map(const void* text, u64 nbytes, u64 chunk, u64 rep_base, const void*
               hipStream_t s) {
   if (nbytes == 0) return 0;
   if (chunk % ii::TILE) return -1;
-  GTab g;
-  g.tag = (u64*)tag;
-  g.hi = (u64*)hi;
-  g.lo = (u64*)lo;
-  g.val = (long long*)val;
-  g.rep = (u64*)rep;
-  g.ctrl = (u32*)ctrl;
-  g.mask = cap - 1;
-  g.src = (const u8*)text - rep_base;  // the vocabulary's rep words index the caller's byte source
+  (void)hi, (void)lo, (void)val;  // (slot records: their fields are at tag)
+  // the vocabulary's rep words index the caller's byte source
+  GTab g = gtab_make(tag, rep, ctrl, cap, (const u8*)text - rep_base);
   const u64 nb = (nbytes + chunk - 1) / chunk;
   hipLaunchKernelGGL(ii::ii_map_kernel, dim3((unsigned)nb), dim3(ii::T), 0, s, (const u8*)text, nbytes, chunk,
                      rep_base, (const u32*)chunk_line_base, (const u32*)chunk_tok_base,
@@ -751,15 +745,7 @@ extern "C" int mr_ii_insert_slots(void* tag, void* thi, void* tlo, void* val, vo
                                   const void* hi, const void* lo, const void* rep, u64 n, void* out_slot,
                                   const void* src, hipStream_t s) {
   if (n == 0) return 0;
-  GTab g;
-  g.tag = (u64*)tag;
-  g.hi = (u64*)thi;
-  g.lo = (u64*)tlo;
-  g.val = (long long*)val;
-  g.rep = (u64*)trep;
-  g.ctrl = (u32*)ctrl;
-  g.mask = cap - 1;
-  g.src = (const u8*)src;
+  GTab g = gtab_make(tag, trep, ctrl, cap, (const u8*)src);
   hipLaunchKernelGGL(ii::ii_insert_slots_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, g, (const u64*)hi,
                      (const u64*)lo, (const u64*)rep, n, (long long*)out_slot);
   return (int)hipGetLastError();

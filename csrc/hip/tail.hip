@@ -45,13 +45,13 @@ constexpr int HIST_BLOCKS = 64;
 // zero (optional): the tail's zeroed scratch (histograms, tile counters,
 // flags), cleared by block 0 here instead of by a separate memset launch
 // (everything that uses it runs after this kernel)
-__global__ void __launch_bounds__(CT) tail_count_kernel(const u64* __restrict__ tag, u64 cap, u32* __restrict__ bcount,
+__global__ void __launch_bounds__(CT) tail_count_kernel(const GSlot* __restrict__ slots, u64 cap, u32* __restrict__ bcount,
                                                         u32* __restrict__ zero, u32 zwords) {
   __shared__ u32 wc[CT / 64];
   if (zero && blockIdx.x == 0)
     for (u32 k = threadIdx.x; k < zwords; k += CT) zero[k] = 0u;
   const u64 i = (u64)blockIdx.x * CT + threadIdx.x;
-  const bool o = i < cap && tag[i] != 0;
+  const bool o = i < cap && slots[i].tag != 0;
   const u64 m = __ballot(o);
   if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = (u32)__popcll(m);
   __syncthreads();
@@ -103,7 +103,7 @@ __global__ void __launch_bounds__(CT) tail_scatter_kernel(GTab g, u64 cap, u32 n
   __shared__ u32 wc[CT / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const u64 i = (u64)blockIdx.x * CT + t;
-  const bool occ = i < cap && g.tag[i] != 0;
+  const bool occ = i < cap && g.s[i].tag != 0;
   const u64 m = __ballot(occ);
   if (lane == 0) wc[wave] = (u32)__popcll(m);
   __syncthreads();
@@ -113,13 +113,13 @@ __global__ void __launch_bounds__(CT) tail_scatter_kernel(GTab g, u64 cap, u32 n
   if (!occ) return;
   o += (u64)__popcll(m & ((1ull << lane) - 1ull));
   if (o >= out_cap) return;  // more rows than the caller's bound: flagged by tail_pad_kernel / the host
-  const u64 h = g.hi[i], l = g.lo[i], r = g.rep[i];
+  const u64 h = g.s[i].hi, l = g.s[i].lo, r = g.rep[i];
   u32 len;
   const u32 f = key_fnv(h, l, r, src, &len);
   const u32 p = nparts ? f % nparts : f;
   out_hi[o] = h;
   out_lo[o] = l;
-  out_val[o] = g.val[i];
+  out_val[o] = g.s[i].val;
   out_rep[o] = r;
   out_part[o] = p;
   out_c[o] = ((u64)p << 56) | (h >> 8);
@@ -368,18 +368,10 @@ static int tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, voi
                         void* out_c, void* counter, void* ghist, void* pcount, void* bhist, u64 n, u64 out_cap, int pad,
                         void* bad, void* zero, u32 zbytes, hipStream_t s) {
   if (nparts > 256 || bhist == nullptr || (pad && (nparts > 255 || bad == nullptr))) return -1;
-  GTab g;
-  g.tag = (u64*)tag;
-  g.hi = (u64*)hi;
-  g.lo = (u64*)lo;
-  g.val = (long long*)val;
-  g.rep = (u64*)rep;
-  g.ctrl = (u32*)ctrl;
-  g.mask = cap - 1;
-  g.src = nullptr;
+  GTab g = gtab_make(tag, rep, ctrl, cap, nullptr);
   const u64 nb = (cap + tl::CT - 1) / tl::CT;
   u32* bcount = (u32*)bhist;
-  hipLaunchKernelGGL(tl::tail_count_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, (const u64*)tag, cap, bcount,
+  hipLaunchKernelGGL(tl::tail_count_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, (const GSlot*)tag, cap, bcount,
                      (u32*)zero, zbytes / 4);
   hipLaunchKernelGGL(tl::tail_bscan_kernel, dim3(1), dim3(tl::BS), 0, s, bcount, nb, (unsigned long long*)counter);
   hipLaunchKernelGGL(tl::tail_scatter_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, g, cap, nparts, (const u8*)src,

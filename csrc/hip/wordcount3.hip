@@ -324,10 +324,11 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (kcnt[k]) {
-      gt[k] = ld_agent(&g.tag[kslot[k]]);
+      // (one slot record: tag, lo and hi share a line)
+      gt[k] = ld_agent(&g.s[kslot[k]].tag);
       if (!gtab_tag_exact(ktag[k])) {
-        gl[k] = ld_agent(&g.lo[kslot[k]]);
-        gh[k] = ld_agent(&g.hi[kslot[k]]);
+        gl[k] = ld_agent(&g.s[kslot[k]].lo);
+        gh[k] = ld_agent(&g.s[kslot[k]].hi);
       } else {
         gl[k] = klo[k];
         gh[k] = khi[k];
@@ -345,7 +346,7 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
       state |= 1u << k;
     } else if (gt[k] == ktag[k] && gl[k] == klo[k] && gh[k] == khi[k] && !key_is_long(klo[k])) {
       // (a long key takes gtab_insert below: its bytes are verified there)
-      fold_value(&g.val[kslot[k]], (long long)kcnt[k], OP_SUM);
+      fold_value(&g.s[kslot[k]].val, (long long)kcnt[k], OP_SUM);
       state |= 1u << k;
     }
   }
@@ -354,7 +355,7 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
   for (int k = 0; k < PER; ++k) {
     if (!(state & (1u << k)) && gt[k] == 0) {
       u64 expected = 0;
-      if (__hip_atomic_compare_exchange_strong(&g.tag[kslot[k]], &expected, ktag[k], __ATOMIC_RELAXED,
+      if (__hip_atomic_compare_exchange_strong(&g.s[kslot[k]].tag, &expected, ktag[k], __ATOMIC_RELAXED,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         won |= 1u << k;
     }
@@ -364,15 +365,15 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
     for (int k = 0; k < PER; ++k) {
       if (won & (1u << k)) {
         const u32 r = krep[k];
-        st_agent(&g.hi[kslot[k]], khi[k]);
+        st_agent(&g.s[kslot[k]].hi, khi[k]);
         st_agent(&g.rep[kslot[k]], make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16));
-        fold_value(&g.val[kslot[k]], (long long)kcnt[k], OP_SUM);
+        fold_value(&g.s[kslot[k]].val, (long long)kcnt[k], OP_SUM);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-      if (won & (1u << k)) st_agent(&g.lo[kslot[k]], klo[k]);
+      if (won & (1u << k)) st_agent(&g.s[kslot[k]].lo, klo[k]);
     claims += __builtin_popcount(won);
     state |= won;
   }
@@ -425,15 +426,9 @@ int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, 
                void* ctrl, u64 cap, void* ovf_hi, void* ovf_lo, void* ovf_rep, u64 ovf_cap, void* ovf_counter,
                hipStream_t stream) {
   if (nbytes == 0) return 0;
-  GTab g;
-  g.tag = (u64*)tag;
-  g.hi = (u64*)hi;
-  g.lo = (u64*)lo;
-  g.val = (long long*)val;
-  g.rep = (u64*)rep;
-  g.ctrl = (u32*)ctrl;
-  g.mask = cap - 1;
-  g.src = (const u8*)text - rep_base;  // every rep word of this table indexes the caller's byte source
+  (void)hi, (void)lo, (void)val;  // (slot records: their fields are at tag)
+  // every rep word of this table indexes the caller's byte source
+  GTab g = gtab_make(tag, rep, ctrl, cap, (const u8*)text - rep_base);
   v3::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter};
   const int aligned = ((uintptr_t)text & 15) == 0;
   const u8* t = (const u8*)text;
