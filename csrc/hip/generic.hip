@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(256) slot_compact_kernel(GTab g, u64 cap, long
       out_slot[o] = (long long)i;
       out_hi[o] = g.s[i].hi;
       out_lo[o] = g.s[i].lo;
-      out_rep[o] = g.rep[i];
+      out_rep[o] = g.s[i].rep;
     }
   }
 }
@@ -747,7 +747,7 @@ static inline unsigned ag_grid(u64 n, unsigned block, unsigned cap = 8192) {
 }
 
 static inline GTab ag_gtab(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap, const void* src) {
-  GTab g = gtab_make(tag, rep, ctrl, cap, (const u8*)src);
+  GTab g = gtab_make(tag, val, ctrl, cap, (const u8*)src);
   return g;
 }
 

@@ -4,14 +4,17 @@
 // combined with the combiner (job.lua:92-96,198-202): values are folded with
 // an associative op at insert time instead of being appended to Lua tables.
 //
-// Layout: array-of-structures — slot i is ONE 32-byte record {tag, lo, hi,
-// val} (four slots per 128-byte line), the rep words beside it in their own
-// array (read only for long keys and by the compactions), plus a control
-// block {nclaimed, overflow, claim shards}.  A probe, its key compare and the
-// fold of its value touch one line (the structure-of-arrays table touched 4-5:
-// tag, lo, hi, val, rep — VERDICT r5: the bigram's agg_combine waited on 82 %
-// of its cycles).  The Python side sees the four fields as strided views of one
-// int64 [cap, 4] tensor (ops/primitives.HashTable).
+// Layout: slot i's KEY is one 32-byte record {tag, lo, hi, rep} (four slots
+// per 128-byte line): a probe, its key compare and a long key's byte check
+// touch one line (the structure-of-arrays table touched 4: tag, lo, hi, rep —
+// the bigram's agg_combine waited on 82 % of its cycles).  The
+// values stay in their own array: the folds are memory-side atomics, which
+// serialise per line, and a hot word's line takes an add from every
+// workgroup's flush — with the value inside the record, every probe of the
+// four keys sharing that line queued behind those adds (the resident map ran
+// 4.0 instead of 2.0 ms; profiles/r6/aos/).  Plus a control block {nclaimed,
+// overflow, claim shards}.  The Python side sees the record fields as strided
+// views of one int64 [cap, 4] tensor (ops/primitives.HashTable).
 //
 // Concurrency protocol (agent scope, placement independent — guide §6 G16):
 //   claim:   CAS tag 0 -> gtab_tag(hi,lo)           (relaxed, agent); for keys of <= 7
@@ -33,12 +36,12 @@ struct alignas(32) GSlot {
   u64 tag;
   u64 lo;
   u64 hi;
-  long long val;
+  u64 rep;
 };
 
 struct GTab {
-  GSlot* s;       // cap slot records
-  u64* rep;       // cap rep words
+  GSlot* s;        // cap key records
+  long long* val;  // cap values
   u32* ctrl;      // [0] = claimed slots (host-side inserts), [1] = overflow flag,
                   // [CTRL_SHARD0 + CTRL_STRIDE * s] = claim-count shard s (s < CTRL_SHARDS)
   u64 mask;       // capacity - 1 (capacity is a power of two)
@@ -46,12 +49,12 @@ struct GTab {
                   // verification); null = identity on (prefix, 56-bit hash)
 };
 
-// The host passes a table as (slot records, rep words, ctrl): the slot base
+// The host passes a table as (key records, values, ctrl): the record base
 // arrives in the historical "tag" argument of the entry points.
-__host__ inline GTab gtab_make(void* slots, void* rep, void* ctrl, u64 cap, const void* src) {
+__host__ inline GTab gtab_make(void* slots, void* val, void* ctrl, u64 cap, const void* src) {
   GTab g;
   g.s = static_cast<GSlot*>(slots);
-  g.rep = static_cast<u64*>(rep);
+  g.val = static_cast<long long*>(val);
   g.ctrl = static_cast<u32*>(ctrl);
   g.mask = cap - 1;
   g.src = static_cast<const u8*>(src);
@@ -111,8 +114,8 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
         // no buffer_wbl2 L2 write-back (a release fence per new key cost ~1 ms
         // over the 3e5 claims of the benchmark corpus).
         st_agent(&sl.hi, hi);
-        st_agent(&t.rep[slot], rep);
-        fold_value(&sl.val, v, op);
+        st_agent(&sl.rep, rep);
+        fold_value(&t.val[slot], v, op);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         st_agent(&sl.lo, lo);
         if (out_slot) *out_slot = slot;
@@ -121,7 +124,7 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
       cur = expected;
     }
     if (cur == tag && exact) {  // the tag is the key: fold without waiting for the payload
-      fold_value(&sl.val, v, op);
+      fold_value(&t.val[slot], v, op);
       if (out_slot) *out_slot = slot;
       return 1;
     }
@@ -144,7 +147,7 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
           h = ld_agent(&sl.hi);
         }
         if (h == hi && (!key_is_long(lo) || t.src == nullptr || gtab_long_equal(t, slot, rep))) {
-          fold_value(&sl.val, v, op);
+          fold_value(&t.val[slot], v, op);
           if (out_slot) *out_slot = slot;
           return 1;
         }
@@ -164,10 +167,10 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
 }
 
 __device__ __forceinline__ bool gtab_long_equal(const GTab& t, u64 slot, u64 rep) {
-  u64 r = ld_agent(&t.rep[slot]);
+  u64 r = ld_agent(&t.s[slot].rep);
   if (rep_bytes_equal(t.src, r, rep)) return true;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  r = ld_agent(&t.rep[slot]);
+  r = ld_agent(&t.s[slot].rep);
   return rep_bytes_equal(t.src, r, rep);
 }
 

@@ -662,7 +662,7 @@ int mr_ii_map(const void* text, u64 nbytes, u64 chunk, u64 rep_base, const void*
   if (chunk % ii::TILE) return -1;
   (void)hi, (void)lo, (void)val;  // (slot records: their fields are at tag)
   // the vocabulary's rep words index the caller's byte source
-  GTab g = gtab_make(tag, rep, ctrl, cap, (const u8*)text - rep_base);
+  GTab g = gtab_make(tag, val, ctrl, cap, (const u8*)text - rep_base);
   const u64 nb = (nbytes + chunk - 1) / chunk;
   hipLaunchKernelGGL(ii::ii_map_kernel, dim3((unsigned)nb), dim3(ii::T), 0, s, (const u8*)text, nbytes, chunk,
                      rep_base, (const u32*)chunk_line_base, (const u32*)chunk_tok_base,
@@ -745,7 +745,7 @@ extern "C" int mr_ii_insert_slots(void* tag, void* thi, void* tlo, void* val, vo
                                   const void* hi, const void* lo, const void* rep, u64 n, void* out_slot,
                                   const void* src, hipStream_t s) {
   if (n == 0) return 0;
-  GTab g = gtab_make(tag, trep, ctrl, cap, (const u8*)src);
+  GTab g = gtab_make(tag, val, ctrl, cap, (const u8*)src);
   hipLaunchKernelGGL(ii::ii_insert_slots_kernel, dim3(grid_n(n, 256)), dim3(256), 0, s, g, (const u64*)hi,
                      (const u64*)lo, (const u64*)rep, n, (long long*)out_slot);
   return (int)hipGetLastError();

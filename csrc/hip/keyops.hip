@@ -267,8 +267,8 @@ __global__ void __launch_bounds__(256) table_compact_kernel(GTab g, u64 cap, u64
     if (occ & (1u << k)) {
       const u64 i = b0 + (u64)k * 256 + t;
       const u64 o = base + wc[k * NW + wave] + rank[k];
-      const u64 h = g.s[i].hi, l = g.s[i].lo, r = g.rep[i];
-      const long long v = g.s[i].val;
+      const u64 h = g.s[i].hi, l = g.s[i].lo, r = g.s[i].rep;
+      const long long v = g.val[i];
       out_hi[o] = h;
       out_lo[o] = l;
       out_val[o] = v;
@@ -405,13 +405,12 @@ __global__ void gather_key_bytes_kernel(const u64* hi, const u64* lo, const u64*
 // at the front of `buf` (bump allocator `heap[0]`, capacity heap_cap) and
 // their rep re-pointed there, so the slot can be refilled by a later round.
 // heap[1] is set when the heap is full (the host raises).
-__global__ void table_rehome_kernel(const GSlot* __restrict__ slots, u64* __restrict__ rep,
-                                    u64 cap, u8* __restrict__ buf, u64 lo_off, u64 hi_off,
+__global__ void table_rehome_kernel(GSlot* __restrict__ slots, u64 cap, u8* __restrict__ buf, u64 lo_off, u64 hi_off,
                                     unsigned long long* __restrict__ heap, u64 heap_cap) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
     if (slots[i].tag == 0 || !key_is_long(slots[i].lo)) continue;
-    const u64 r = rep[i];
+    const u64 r = slots[i].rep;
     const u64 o = rep_off(r), n = rep_len(r);
     if (o < lo_off || o >= hi_off) continue;
     const unsigned long long d = atomicAdd(&heap[0], (unsigned long long)n);
@@ -420,19 +419,18 @@ __global__ void table_rehome_kernel(const GSlot* __restrict__ slots, u64* __rest
       continue;
     }
     for (u64 k = 0; k < n; ++k) buf[d + k] = buf[o + k];
-    rep[i] = make_rep(d, n);
+    slots[i].rep = make_rep(d, n);
   }
 }
 
-// Reset a table in one launch: tag = lo = 0, val = init, ctrl = 0 (hi is
-// never read before a claim publishes it).  One 16-byte store of {tag, lo}
-// and one of {hi, val} per slot record.
-__global__ void table_reset_kernel(GSlot* slots, u32* ctrl, u64 cap, long long init) {
+// Reset a table in one launch: tag = lo = 0 (one 16-byte store per key
+// record; hi and rep are never read before a claim publishes them), val =
+// init, ctrl = 0.
+__global__ void table_reset_kernel(GSlot* slots, long long* val, u32* ctrl, u64 cap, long long init) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
-    ulonglong2* p = reinterpret_cast<ulonglong2*>(&slots[i]);
-    p[0] = make_ulonglong2(0ull, 0ull);
-    p[1] = make_ulonglong2(0ull, (unsigned long long)init);
+    *reinterpret_cast<ulonglong2*>(&slots[i]) = make_ulonglong2(0ull, 0ull);
+    val[i] = init;
   }
   if (blockIdx.x == 0)
     for (u32 w = threadIdx.x; w < CTRL_WORDS; w += blockDim.x) ctrl[w] = 0;
@@ -447,7 +445,7 @@ using namespace mr;
 
 static inline GTab make_gtab(void* tag, void* hi, void* lo, void* val, void* rep, void* ctrl, u64 cap,
                              const void* src = nullptr) {
-  GTab g = gtab_make(tag, rep, ctrl, cap, (const u8*)src);
+  GTab g = gtab_make(tag, val, ctrl, cap, (const u8*)src);
   return g;
 }
 
@@ -617,17 +615,17 @@ int mr_gather_aos4(const void* perm, u64 n, const void* aos, void* o0, void* o1,
   return (int)hipGetLastError();
 }
 
-// slots: the table's slot records (hashtab.h GSlot)
-int mr_table_rehome(const void* slots, void* rep, u64 cap, void* buf, u64 lo_off, u64 hi_off, void* heap,
-                    u64 heap_cap, hipStream_t stream) {
-  hipLaunchKernelGGL(table_rehome_kernel, dim3(grid_for(cap, 256)), dim3(256), 0, stream, (const GSlot*)slots,
-                     (u64*)rep, cap, (u8*)buf, lo_off, hi_off, (unsigned long long*)heap, heap_cap);
+// slots: the table's key records (hashtab.h GSlot)
+int mr_table_rehome(void* slots, u64 cap, void* buf, u64 lo_off, u64 hi_off, void* heap, u64 heap_cap,
+                    hipStream_t stream) {
+  hipLaunchKernelGGL(table_rehome_kernel, dim3(grid_for(cap, 256)), dim3(256), 0, stream, (GSlot*)slots, cap,
+                     (u8*)buf, lo_off, hi_off, (unsigned long long*)heap, heap_cap);
   return (int)hipGetLastError();
 }
 
-int mr_table_reset(void* slots, void* ctrl, u64 cap, long long init, hipStream_t stream) {
-  hipLaunchKernelGGL(table_reset_kernel, dim3(grid_for(cap, 256)), dim3(256), 0, stream, (GSlot*)slots, (u32*)ctrl,
-                     cap, init);
+int mr_table_reset(void* slots, void* val, void* ctrl, u64 cap, long long init, hipStream_t stream) {
+  hipLaunchKernelGGL(table_reset_kernel, dim3(grid_for(cap, 256)), dim3(256), 0, stream, (GSlot*)slots,
+                     (long long*)val, (u32*)ctrl, cap, init);
   return (int)hipGetLastError();
 }
 

@@ -166,7 +166,7 @@ __device__ __forceinline__ bool cp_slot(const GTab& g, u64 cap, u64 i, u32 npart
   if (i >= cap || g.s[i].tag == 0) return false;
   h = g.s[i].hi;
   l = g.s[i].lo;
-  r = g.rep[i];
+  r = g.s[i].rep;
   const u32 f = key_fnv(h, l, r, src, &len);
   d = (nparts ? f % nparts : f) % W;
   return true;
@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(CP) cp_scatter_kernel(GTab g, u64 cap, u32 npa
     u64* rr = reinterpret_cast<u64*>(buf + ro);
     rr[0] = h;
     rr[1] = l;
-    rr[2] = (u64)g.s[i].val;
+    rr[2] = (u64)g.val[i];
     rr[3] = make_rep(boff, len);
     u8* out = buf + bo;
     if (!key_is_long(l)) {
@@ -431,7 +431,7 @@ int mr_compact_pack(void* tag, void* hi, void* lo, void* val, void* rep, void* c
                     const void* src, void* ws, void* buf, u64 buf_cap, void* xchg, long long extra, const void* errs,
                     u32 nerr, void* rows_out, hipStream_t s) {
   if (W == 0 || W > (u32)pk::MAXW || cap == 0) return -1;
-  GTab g = gtab_make(tag, rep, ctrl, cap, (const u8*)src);
+  GTab g = gtab_make(tag, val, ctrl, cap, (const u8*)src);
   const u64 nb = (cap + pk::CP * pk::CP_PER - 1) / (pk::CP * pk::CP_PER);
   unsigned long long* bcnt = (unsigned long long*)ws;
   unsigned long long* coltot = (unsigned long long*)((u8*)ws + ((nb * 2 * W * 8 + 255) & ~255ull));
@@ -451,7 +451,7 @@ int mr_insert_received(const void* rec, u64 n, const void* recv, u32 W, void* ta
                        void* rep, void* ctrl, u64 cap, int op, int combined, const void* src, hipStream_t s) {
   if (n == 0) return 0;
   if (W == 0 || W > (u32)pk::MAXW_RECV) return -1;
-  GTab g = gtab_make(tag, rep, ctrl, cap, (const u8*)(combined ? rec : src));
+  GTab g = gtab_make(tag, val, ctrl, cap, (const u8*)(combined ? rec : src));
   hipLaunchKernelGGL(pk::pk_insert_received_kernel, dim3(pk_grid(n, 2048)), dim3(256),
                      3 * (W + 1) * sizeof(long long), s, (const u8*)rec, n, (const long long*)recv, W, g, op, combined);
   return (int)hipGetLastError();

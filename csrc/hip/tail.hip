@@ -113,13 +113,13 @@ __global__ void __launch_bounds__(CT) tail_scatter_kernel(GTab g, u64 cap, u32 n
   if (!occ) return;
   o += (u64)__popcll(m & ((1ull << lane) - 1ull));
   if (o >= out_cap) return;  // more rows than the caller's bound: flagged by tail_pad_kernel / the host
-  const u64 h = g.s[i].hi, l = g.s[i].lo, r = g.rep[i];
+  const u64 h = g.s[i].hi, l = g.s[i].lo, r = g.s[i].rep;
   u32 len;
   const u32 f = key_fnv(h, l, r, src, &len);
   const u32 p = nparts ? f % nparts : f;
   out_hi[o] = h;
   out_lo[o] = l;
-  out_val[o] = g.s[i].val;
+  out_val[o] = g.val[i];
   out_rep[o] = r;
   out_part[o] = p;
   out_c[o] = ((u64)p << 56) | (h >> 8);
@@ -368,7 +368,7 @@ static int tail_compact(void* tag, void* hi, void* lo, void* val, void* rep, voi
                         void* out_c, void* counter, void* ghist, void* pcount, void* bhist, u64 n, u64 out_cap, int pad,
                         void* bad, void* zero, u32 zbytes, hipStream_t s) {
   if (nparts > 256 || bhist == nullptr || (pad && (nparts > 255 || bad == nullptr))) return -1;
-  GTab g = gtab_make(tag, rep, ctrl, cap, nullptr);
+  GTab g = gtab_make(tag, val, ctrl, cap, nullptr);
   const u64 nb = (cap + tl::CT - 1) / tl::CT;
   u32* bcount = (u32*)bhist;
   hipLaunchKernelGGL(tl::tail_count_kernel, dim3((unsigned)nb), dim3(tl::CT), 0, s, (const GSlot*)tag, cap, bcount,

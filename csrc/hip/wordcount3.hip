@@ -161,9 +161,13 @@ __device__ __forceinline__ bool lds_insert(Lds<T, SLOTS>& L, u64 hi, u64 lo, u32
 // lane i taking tokens i, i+T, ... — every lane busy in every iteration,
 // instead of each lane walking the 0..8 tokens that start in its own 16 bytes
 // (the wave would run as long as its busiest lane).
-template <int T, int SLOTS, int TPC>
+// STAMPS (tools/map_stamps.py, a separate instantiation): every wave records
+// where its time goes — waits at the tile's workgroup barriers, staging, the
+// start masks + scan, the token list, the token loop, the flush — as 8 u64
+// (wall_clock64 ticks) at stamps[(block * waves + wave) * 8].
+template <int T, int SLOTS, int TPC, bool STAMPS = false>
 __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text, u64 nbytes, u64 rep_base, GTab g,
-                                                    Ovf ovf, int aligned) {
+                                                    Ovf ovf, int aligned, u64* __restrict__ stamps = nullptr) {
   using L_t = Lds<T, SLOTS>;
   constexpr int TILE = L_t::TILE;
   constexpr int STAGED = L_t::STAGED;
@@ -174,6 +178,17 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
   const u64 chunk_begin = (u64)blockIdx.x * CHUNK;
   if (chunk_begin >= nbytes) return;
   const u64 chunk_end = min(chunk_begin + CHUNK, nbytes);
+  [[maybe_unused]] u64 st_bar = 0, st_stage = 0, st_scan = 0, st_list = 0, st_loop = 0, st_flush = 0, st_p = 0;
+  auto clk = [&]() -> u64 {
+    if constexpr (STAMPS) return wall_clock64();
+    return 0;
+  };
+  [[maybe_unused]] const u64 st_t0 = clk();
+  auto bar = [&]() {  // a workgroup barrier (timed under STAMPS)
+    const u64 a = clk();
+    __syncthreads();
+    if constexpr (STAMPS) st_bar += clk() - a;
+  };
   for (int s = t; s < SLOTS; s += T) {
     L.tag[s] = 0;
     L.cnt[s] = 0;
@@ -198,14 +213,17 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
     // thread T-1 held (nobody reads txt[PAD-1] between the previous tile's
     // final barrier and this tile's staging barrier)
     if (t == T - 1 && tile_base != chunk_begin) L.txt[PAD - 1] = L.txt[PAD + TILE - 1];
-    __syncthreads();
+    bar();
+    st_p = clk();
     *reinterpret_cast<uint4*>(L.txt + PAD + t * SEG) = q;
     ws16[t] = (u16)ws_mask16(q);
     if (t < NH) {
       *reinterpret_cast<uint4*>(L.txt + PAD + TILE + t * SEG) = qh;
       ws16[T + t] = (u16)ws_mask16(qh);
     }
-    __syncthreads();
+    if constexpr (STAMPS) st_stage += clk() - st_p;
+    bar();
+    st_p = clk();
     const u64 next = tile_base + TILE;
     if (next < chunk_end) {  // prefetch: consumed after this tile's token loop
       q = load16(text, next + (u64)t * SEG, nbytes, aligned);
@@ -280,7 +298,9 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
         if (lane >= o) incl += v;
       }
       if (lane == 63) L.wsum[wave] = incl;
-      __syncthreads();
+      if constexpr (STAMPS) st_scan += clk() - st_p;
+      bar();
+      st_p = clk();
       u32 base = 0, total = 0;
 #pragma unroll
       for (int w = 0; w < T / 64; ++w) {
@@ -296,12 +316,16 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
         else process((u32)t * SEG + i);  // a tile denser than the list (one-letter words): in place
         ++k;
       }
-      __syncthreads();
+      if constexpr (STAMPS) st_list += clk() - st_p;
+      bar();
+      st_p = clk();
       const u32 ntok = total < (u32)MAXTOK ? total : (u32)MAXTOK;
       for (u32 x = t; x < ntok; x += T) process(L.tokpos[x]);
     }
-    __syncthreads();
+    if constexpr (STAMPS) st_loop += clk() - st_p;
+    bar();
   }
+  [[maybe_unused]] const u64 st_f0 = clk();
   // flush: each thread folds its PER slots.  The common case is a key already
   // in the HBM table at its home slot, so tag/lo/hi of every home slot are
   // loaded speculatively in ONE batch (one memory round trip instead of a
@@ -346,7 +370,7 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
       state |= 1u << k;
     } else if (gt[k] == ktag[k] && gl[k] == klo[k] && gh[k] == khi[k] && !key_is_long(klo[k])) {
       // (a long key takes gtab_insert below: its bytes are verified there)
-      fold_value(&g.s[kslot[k]].val, (long long)kcnt[k], OP_SUM);
+      fold_value(&g.val[kslot[k]], (long long)kcnt[k], OP_SUM);
       state |= 1u << k;
     }
   }
@@ -366,8 +390,8 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
       if (won & (1u << k)) {
         const u32 r = krep[k];
         st_agent(&g.s[kslot[k]].hi, khi[k]);
-        st_agent(&g.rep[kslot[k]], make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16));
-        fold_value(&g.s[kslot[k]].val, (long long)kcnt[k], OP_SUM);
+        st_agent(&g.s[kslot[k]].rep, make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16));
+        fold_value(&g.val[kslot[k]], (long long)kcnt[k], OP_SUM);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -385,6 +409,21 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
                           make_rep(rep_base + chunk_begin + (r & 0xFFFFu), r >> 16), OP_SUM) == 2;
   }
   gtab_count_claims(g, claims);
+  if constexpr (STAMPS) {
+    const u64 now = clk();
+    st_flush = now - st_f0;
+    if ((t & 63) == 0) {
+      u64* o = stamps + ((u64)blockIdx.x * (T / 64) + (t >> 6)) * 8;
+      o[0] = now - st_t0;
+      o[1] = st_bar;
+      o[2] = st_stage;
+      o[3] = st_scan;
+      o[4] = st_list;
+      o[5] = st_loop;
+      o[6] = st_flush;
+      o[7] = claims;
+    }
+  }
 }
 
 __global__ void __launch_bounds__(256) ovf_agg3_kernel(Ovf o, GTab g) {
@@ -408,11 +447,15 @@ static_assert(sizeof(Lds<MAP_T, MAP_SLOTS>) <= 80 * 1024, "two workgroups per CU
 
 template <int T, int SLOTS, int TPC>
 static void launch_map3(const u8* text, u64 nbytes, u64 rep_base, const GTab& g, const Ovf& o, int aligned,
-                        hipStream_t stream) {
+                        hipStream_t stream, u64* stamps = nullptr) {
   constexpr u64 CHUNK = (u64)T * SEG * TPC;
   const u64 nblocks = (nbytes + CHUNK - 1) / CHUNK;
-  hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC>), dim3((unsigned)nblocks), dim3(T), 0, stream, text, nbytes,
-                     rep_base, g, o, aligned);
+  if (stamps)
+    hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC, true>), dim3((unsigned)nblocks), dim3(T), 0, stream, text,
+                       nbytes, rep_base, g, o, aligned, stamps);
+  else
+    hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC>), dim3((unsigned)nblocks), dim3(T), 0, stream, text, nbytes,
+                       rep_base, g, o, aligned, nullptr);
 }
 
 }  // namespace v3
@@ -428,11 +471,26 @@ int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, 
   if (nbytes == 0) return 0;
   (void)hi, (void)lo, (void)val;  // (slot records: their fields are at tag)
   // every rep word of this table indexes the caller's byte source
-  GTab g = gtab_make(tag, rep, ctrl, cap, (const u8*)text - rep_base);
+  GTab g = gtab_make(tag, val, ctrl, cap, (const u8*)text - rep_base);
   v3::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter};
   const int aligned = ((uintptr_t)text & 15) == 0;
   const u8* t = (const u8*)text;
   v3::launch_map3<v3::MAP_T, v3::MAP_SLOTS, v3::MAP_TPC>(t, nbytes, rep_base, g, o, aligned, stream);
+  hipLaunchKernelGGL(v3::ovf_agg3_kernel, dim3(1024), dim3(256), 0, stream, o, g);
+  return (int)hipGetLastError();
+}
+
+// The same map with per-wave phase stamps (diagnosis; tools/map_stamps.py):
+// stamps = u64 [blocks * MAP_T / 64 * 8], blocks = ceil(nbytes / 8 KiB).
+int mr_wc_map3_stamped(const void* text, u64 nbytes, u64 rep_base, void* tag, void* val, void* ctrl, u64 cap,
+                       void* ovf_hi, void* ovf_lo, void* ovf_rep, u64 ovf_cap, void* ovf_counter, void* stamps,
+                       hipStream_t stream) {
+  if (nbytes == 0 || stamps == nullptr) return nbytes ? -1 : 0;
+  GTab g = gtab_make(tag, val, ctrl, cap, (const u8*)text - rep_base);
+  v3::Ovf o{(u64*)ovf_hi, (u64*)ovf_lo, (u64*)ovf_rep, ovf_cap, (unsigned long long*)ovf_counter};
+  const int aligned = ((uintptr_t)text & 15) == 0;
+  v3::launch_map3<v3::MAP_T, v3::MAP_SLOTS, v3::MAP_TPC>((const u8*)text, nbytes, rep_base, g, o, aligned, stream,
+                                                          (u64*)stamps);
   hipLaunchKernelGGL(v3::ovf_agg3_kernel, dim3(1024), dim3(256), 0, stream, o, g);
   return (int)hipGetLastError();
 }

@@ -93,8 +93,8 @@ _SIGS = {
     "mr_set_long_mask_invidx": [_u64],
     "mr_tail_pack_bytes": [_u64, _u32],
     "mr_tail_ws_layout": [_u64, _u32, _u64, _u64, ctypes.POINTER(ctypes.c_uint64)],
-    "mr_table_reset": [_p, _p, _u64, ctypes.c_longlong, _p],
-    "mr_table_rehome": [_p, _p, _u64, _p, _u64, _u64, _p, _u64, _p],
+    "mr_table_reset": [_p, _p, _p, _u64, ctypes.c_longlong, _p],
+    "mr_table_rehome": [_p, _u64, _p, _u64, _u64, _p, _u64, _p],
     "mr_scan_partials_len": [_u64],
     "mr_radix_onesweep_k32": [_p, _p, _p, _p, _u64, _i32, _p, _p, _p, _u32, _p, _i32, _p],
     "mr_rec_keys32": [_p, _u64, _i32, _i32, _p, _p, _p],

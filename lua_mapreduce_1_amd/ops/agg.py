@@ -197,22 +197,11 @@ class AggTable:
         self.src: torch.Tensor | None = None
         self.cap = next_pow2(max(1024, int(capacity)))
         self.cstride = 1  # slot stride of the value columns (one array per column)
-        self._in_slots = False
         if self.is_cuda:
-            if not self.list_mode and len(cols) == 1 and DTYPES[cols[0][0]].itemsize == 8:
-                # ONE 8-byte fold column lives in the key table's slot records
-                # (their value field, stride 4): the fold of a row touches the
-                # line its key probe already brought in (csrc/hip/hashtab.h)
-                dt, op, _i = cols[0]
-                bits = int(torch.tensor([_identity(dt, op)], dtype=DTYPES[dt]).view(torch.int64)[0])
-                self.keys = HashTable(self.cap, self.device, op="none", val_init=bits)
-                self.cols = [self.keys.val.view(DTYPES[dt])]
-                self.cstride, self._in_slots = 4, True
-            else:
-                self.keys = HashTable(self.cap, self.device, op="none")
-                self.cols = [] if self.list_mode else [torch.empty(self.cap, dtype=DTYPES[dt], device=self.device)
-                                                       for dt, _op, _i in cols]
-                self._fill_cols()
+            self.keys = HashTable(self.cap, self.device, op="none")
+            self.cols = [] if self.list_mode else [torch.empty(self.cap, dtype=DTYPES[dt], device=self.device)
+                                                   for dt, _op, _i in cols]
+            self._fill_cols()
             self.post_slot = self.post_val = None
         else:
             self._pending: list = []
@@ -239,8 +228,6 @@ class AggTable:
         return self.device.type == "cuda"
 
     def _fill_cols(self) -> None:
-        if self._in_slots:
-            return  # (the key table's reset writes the column's identity)
         for c, (dt, op, _i) in zip(self.cols, self.cols_spec or []):
             c.fill_(_identity(dt, op))
 

@@ -49,8 +49,8 @@ class Vocab:
 
     def arrays(self):
         if self.table is not None:
-            # (the table's hi / lo are strided fields of its slot records)
-            return self.table.hi.contiguous(), self.table.lo.contiguous(), self.table.rep
+            # (the table's hi / lo / rep are strided fields of its key records)
+            return self.table.hi.contiguous(), self.table.lo.contiguous(), self.table.rep.contiguous()
         return self.hi, self.lo, self.rep
 
     def reset(self) -> None:

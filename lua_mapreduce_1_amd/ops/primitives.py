@@ -100,22 +100,19 @@ class HashTable:
     def __init__(self, capacity: int, device="cpu", op: str = "sum", val_init: int | None = None):
         self.device = torch.device(device)
         self.op = op
-        # the value field's reset value (default: the op's identity; a key
-        # table whose owner keeps a typed fold column in the value field sets
-        # that column's identity bits: ops/agg.AggTable)
+        # the values' reset value (default: the op's identity)
         self.val_init = _op_init(op) if val_init is None else int(val_init)
         self.cap = next_pow2(max(1024, int(capacity)))
         self.src: torch.Tensor | None = None
         if self.device.type == "cuda":
             d = self.device
-            # slot records {tag, lo, hi, val} (csrc/hip/hashtab.h GSlot: a probe,
-            # its key compare and its fold touch one line); the four fields
-            # are strided views of one [cap, 4] tensor, the rep words beside
+            # key records {tag, lo, hi, rep} (csrc/hip/hashtab.h GSlot: a probe
+            # and its key compare touch one line); the four fields are strided
+            # views of one [cap, 4] tensor; the values in their own array (the
+            # folds' memory-side atomics off the probed lines)
             self.slots = torch.zeros((self.cap, 4), dtype=torch.int64, device=d)
-            self.tag, self.lo, self.hi, self.val = (self.slots[:, j] for j in range(4))
-            if self.val_init:
-                self.val.fill_(self.val_init)
-            self.rep = torch.zeros(self.cap, dtype=torch.int64, device=d)
+            self.tag, self.lo, self.hi, self.rep = (self.slots[:, j] for j in range(4))
+            self.val = torch.full((self.cap,), self.val_init, dtype=torch.int64, device=d)
             # [0] claims, [1] overflow flag, then 64 claim-count shards 128 B
             # apart (csrc/hip/hashtab.h CTRL_*): stats() sums them
             self.ctrl = torch.zeros(_CTRL_WORDS, dtype=torch.int32, device=d)
@@ -129,8 +126,8 @@ class HashTable:
     def reset(self) -> None:
         self.src = None
         if self.is_cuda:
-            _hip.call("mr_table_reset", _hip.ptr(self.slots), _hip.ptr(self.ctrl), self.cap, self.val_init,
-                      _hip.stream(self.device))
+            _hip.call("mr_table_reset", _hip.ptr(self.slots), _hip.ptr(self.val), _hip.ptr(self.ctrl), self.cap,
+                      self.val_init, _hip.stream(self.device))
             if getattr(self, "_ovf_counters", None) is not None and self._ovf_next:
                 self._ovf_counters.zero_()
                 self._ovf_next = 0
@@ -139,14 +136,14 @@ class HashTable:
 
     def _gtab(self):
         """ctypes pointers (tag, hi, lo, val, rep, ctrl) of the table, as the
-        native entry points take them: tag = the slot records' base (the
-        kernels read every field from it), hi / lo / val = the fields of slot
-        0 (cached: the columns of a table never move)."""
+        native entry points take them: tag = the key records' base (the
+        kernels read every record field from it), hi / lo / rep = the fields
+        of record 0 (cached: the columns of a table never move)."""
         g = self.__dict__.get("_gtab_ptrs")
         if g is None or g[0] is not self.slots:
             b = self.slots.data_ptr()
             g = self._gtab_ptrs = (self.slots, (ctypes.c_void_p(b), ctypes.c_void_p(b + 16), ctypes.c_void_p(b + 8),
-                                                ctypes.c_void_p(b + 24), _hip.ptr(self.rep), _hip.ptr(self.ctrl)))
+                                                _hip.ptr(self.val), ctypes.c_void_p(b + 24), _hip.ptr(self.ctrl)))
         return g[1]
 
     # -- inserts -------------------------------------------------------------
@@ -195,7 +192,6 @@ class HashTable:
             else:
                 a.stype[0], a.sbits[0] = A._VT_SCALAR, int(1 if val is None else val)
             a.dst[0], a.dtype[0], a.op[0] = self.val.data_ptr(), 0, OPS[self.op]
-            a.cstride = 4  # (the value field of the slot records)
             st = starts.to(torch.int64).contiguous()
             ln = lens.to(torch.int32).contiguous()
             _hip.call("mr_agg_insert", *self._gtab(), self.cap, _hip.ptr(self.src), None, None, None, 0,
@@ -295,8 +291,8 @@ class HashTable:
         to the key heap at the front of ``buf`` (``heap`` = int64[2] bump
         counter + full flag) and re-point their reps (streaming map rounds)."""
         if self.is_cuda:
-            _hip.call("mr_table_rehome", _hip.ptr(self.slots), _hip.ptr(self.rep), self.cap,
-                      _hip.ptr(buf), lo_off, hi_off, _hip.ptr(heap), heap_cap, _hip.stream(self.device))
+            _hip.call("mr_table_rehome", _hip.ptr(self.slots), self.cap, _hip.ptr(buf), lo_off, hi_off,
+                      _hip.ptr(heap), heap_cap, _hip.stream(self.device))
             return
         b = _np(buf) if not buf.is_cuda else None
         h = heap.numpy()
