@@ -42,6 +42,7 @@ struct Lds {
   u32 ws[WSW];
   u16 tokpos[MAXTOK];
   u32 wsum[T / 64];
+  u32 tnext;  // (DYN) the next unclaimed entry of the tile's token list
   u64 tag[SLOTS];  // gtab_tag-style: a packed key of <= 7 bytes IS its tag
   u32 cnt[SLOTS];
   u32 rep[SLOTS];  // local offset (16 bits) | len (16 bits) << 16
@@ -165,7 +166,12 @@ __device__ __forceinline__ bool lds_insert(Lds<T, SLOTS>& L, u64 hi, u64 lo, u32
 // where its time goes — waits at the tile's workgroup barriers, staging, the
 // start masks + scan, the token list, the token loop, the flush — as 8 u64
 // (wall_clock64 ticks) at stamps[(block * waves + wave) * 8].
-template <int T, int SLOTS, int TPC, bool STAMPS = false>
+// DYN: the waves take the tile's token list 64 entries at a time from an LDS
+// counter instead of each thread walking the entries t, t + T, ...: a wave
+// whose tokens were cheap takes more (round-6 stamps: the slowest wave's token
+// loop ran 40 % over its workgroup's mean, and a quarter of the waves' time
+// was spent waiting at the tile's barriers; profiles/r6/map_stamps/).
+template <int T, int SLOTS, int TPC, bool STAMPS = false, bool DYN = false>
 __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text, u64 nbytes, u64 rep_base, GTab g,
                                                     Ovf ovf, int aligned, u64* __restrict__ stamps = nullptr) {
   using L_t = Lds<T, SLOTS>;
@@ -298,6 +304,7 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
         if (lane >= o) incl += v;
       }
       if (lane == 63) L.wsum[wave] = incl;
+      if (DYN && t == 0) L.tnext = 0;
       if constexpr (STAMPS) st_scan += clk() - st_p;
       bar();
       st_p = clk();
@@ -320,7 +327,17 @@ __global__ void __launch_bounds__(T) wc_map3_kernel(const u8* __restrict__ text,
       bar();
       st_p = clk();
       const u32 ntok = total < (u32)MAXTOK ? total : (u32)MAXTOK;
-      for (u32 x = t; x < ntok; x += T) process(L.tokpos[x]);
+      if constexpr (DYN) {
+        for (;;) {
+          u32 b0 = 0;
+          if (lane == 0) b0 = __hip_atomic_fetch_add(&L.tnext, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          b0 = __shfl(b0, 0);
+          if (b0 >= ntok) break;
+          if (b0 + lane < ntok) process(L.tokpos[b0 + lane]);
+        }
+      } else {
+        for (u32 x = t; x < ntok; x += T) process(L.tokpos[x]);
+      }
     }
     if constexpr (STAMPS) st_loop += clk() - st_p;
     bar();
@@ -445,17 +462,26 @@ static_assert(sizeof(Lds<MAP_T, MAP_SLOTS>) <= 80 * 1024, "two workgroups per CU
 // cut the flush's atomics by 18 % but ran 3.40 vs 2.04 ms; removed in round 5,
 // archived in profiles/r5/pruned/, numbers in profiles/r4/map_shapes/.)
 
+static int g_map_dyn = 1;  // mr_wc3_set_dyn (MR_MAP_DYN, default on): DYN token lists
+
 template <int T, int SLOTS, int TPC>
 static void launch_map3(const u8* text, u64 nbytes, u64 rep_base, const GTab& g, const Ovf& o, int aligned,
                         hipStream_t stream, u64* stamps = nullptr) {
   constexpr u64 CHUNK = (u64)T * SEG * TPC;
   const u64 nblocks = (nbytes + CHUNK - 1) / CHUNK;
-  if (stamps)
-    hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC, true>), dim3((unsigned)nblocks), dim3(T), 0, stream, text,
-                       nbytes, rep_base, g, o, aligned, stamps);
+  const dim3 grid((unsigned)nblocks), block(T);
+  if (stamps && g_map_dyn)
+    hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC, true, true>), grid, block, 0, stream, text, nbytes, rep_base, g,
+                       o, aligned, stamps);
+  else if (stamps)
+    hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC, true>), grid, block, 0, stream, text, nbytes, rep_base, g, o,
+                       aligned, stamps);
+  else if (g_map_dyn)
+    hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC, false, true>), grid, block, 0, stream, text, nbytes, rep_base,
+                       g, o, aligned, nullptr);
   else
-    hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC>), dim3((unsigned)nblocks), dim3(T), 0, stream, text, nbytes,
-                       rep_base, g, o, aligned, nullptr);
+    hipLaunchKernelGGL((wc_map3_kernel<T, SLOTS, TPC>), grid, block, 0, stream, text, nbytes, rep_base, g, o, aligned,
+                       nullptr);
 }
 
 }  // namespace v3
@@ -464,6 +490,11 @@ static void launch_map3(const u8* text, u64 nbytes, u64 rep_base, const GTab& g,
 using namespace mr;
 
 extern "C" {
+
+int mr_wc3_set_dyn(int on) {
+  v3::g_map_dyn = on ? 1 : 0;
+  return 0;
+}
 
 int mr_wc_map3(const void* text, u64 nbytes, u64 rep_base, void* tag, void* hi, void* lo, void* val, void* rep,
                void* ctrl, u64 cap, void* ovf_hi, void* ovf_lo, void* ovf_rep, u64 ovf_cap, void* ovf_counter,

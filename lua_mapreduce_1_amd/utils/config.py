@@ -104,6 +104,9 @@ class Tunables:
                                "API, csrc/hip/sdma.hip) after the tail's kernels, not as a runtime blit kernel on "
                                "the CUs beside the next map (0 = never)")
     spin_us: float = _knob("MR_SPIN_US", 2000.0, "host spin on completion words before hipStreamSynchronize, us")
+    map_dyn: bool = _knob("MR_MAP_DYN", True,
+                          "word-count map kernel: waves take the tile's token list 64 entries at a time from an "
+                          "LDS counter (csrc/hip/wordcount3.hip DYN) instead of a fixed stride")
     force_shuffle: bool = _knob("MR_FORCE_SHUFFLE", False,
                                 "SPMD: run the W>1 shuffle (pack, count exchange, all-to-all, receive insert) also "
                                 "at world size 1 (needs an initialised process group; tests RCCL on one GPU)")

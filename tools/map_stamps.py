@@ -30,6 +30,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--cap-log2", type=int, default=23)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--dyn", type=int, default=None, help="DYN token lists on/off (default: MR_MAP_DYN)")
     a = ap.parse_args()
     import bench
     from lua_mapreduce_1_amd import ops
@@ -41,6 +42,8 @@ def main() -> int:
     n = text.numel()
     tab = ops.HashTable(1 << a.cap_log2, device=d, op="sum")
     lib = _hip.lib()
+    if a.dyn is not None:
+        lib.mr_wc3_set_dyn(a.dyn)
     f = lib.mr_wc_map3_stamped
     P, U64 = ctypes.c_void_p, ctypes.c_uint64
     f.argtypes = [P, U64, U64, P, P, P, U64, P, P, P, U64, P, P, P]
@@ -76,7 +79,7 @@ def main() -> int:
     other = T - (bar + stage + scan + lst + loop + flush).sum()
     loop_imb = (loop.max(1) - loop.mean(1)).sum() / max(loop.sum() / waves, 1.0)
     out = {
-        "bytes": n, "blocks": nblocks, "table_cap": tab.cap, "distinct": got, "overflow": ovf_,
+        "dyn": a.dyn, "bytes": n, "blocks": nblocks, "table_cap": tab.cap, "distinct": got, "overflow": ovf_,
         "map_ms_plain_min": plain[0], "map_ms_plain_median": plain[len(plain) // 2],
         "map_ms_stamped_min": stamped[0], "map_ms_stamped_median": stamped[len(stamped) // 2],
         "share_of_wave_time": {
