@@ -11,7 +11,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 HEAD = """# tools/ — benchmarks, probes and profiling scripts
 
 Benchmarks and probes behind the files under `profiles/`. `prof_*.sh` are `gpurun` command scripts; the one-shot
-checkpoint scripts of rounds 1-3 are archived in `profiles/scripts/`. The Python tools run on one GPU unless noted. Generated from each
+checkpoint scripts of rounds 1-5 are archived in `profiles/scripts/`; `run_steps.sh` chains GPU steps with
+per-step time limits and stops at the first fault. The Python tools run on one GPU unless noted. Generated from each
 file's docstring or header comment by `tools/gen_tools_readme.py`.
 
 | File | What it does |
