@@ -382,6 +382,10 @@ __device__ __forceinline__ u32 cb_row_keys(const Keys& ks, u64 r0, int items, u6
 // smaller blocks so the launch still covers the chip (a 2-8 MiB CSV chunk at
 // 4096 rows per block ran 37-150 blocks on 256 CUs, 72 % of wave cycles
 // waiting: profiles/r4/general/csv_pmc/)
+// BATCH (mr_agg_set_batch): the rows that go to the HBM table directly, and
+// the flush of the LDS-combined keys, probe their home slots in batches
+// (gtab_find_or_claim_home) instead of one gtab_insert per key.
+template <bool BATCH>
 __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 n, Cols c, u32 rows) {
   constexpr int CB_ITEMS = CB_ROWS / CB_T;
   const int items = (int)(rows / CB_T);
@@ -404,6 +408,13 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
   const u64 r0 = (u64)blockIdx.x * rows;
   u64 khi_r[CB_ITEMS], klo_r[CB_ITEMS], krep_r[CB_ITEMS];
   const u32 ok = cb_row_keys<CB_ITEMS>(ks, r0, items, n, khi_r, klo_r, krep_r);
+  // rows whose key found no room in the LDS table (or is long) go to the HBM
+  // table directly — BATCH: all of a thread's such rows probe their home
+  // slots together (gtab_find_or_claim_home), the rest one by one.  With few
+  // repeats inside a block (bigrams: 23 M distinct of 47 M) that is most rows,
+  // and one dependent claim chain per row had kept 82 % of the wave cycles
+  // waiting (profiles/r5/bigram/pmc/).
+  u32 direct = 0;
 #pragma unroll
   for (int it = 0; it < CB_ITEMS; ++it) {
     const u64 i = r0 + (u64)it * CB_T + t;
@@ -412,6 +423,8 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
     const int s = key_is_long(lo) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, hi, lo, rep);
     if (s >= 0) {
       for (int j = 0; j < c.k; ++j) cb_lds_fold(&acc[j * CB_SLOTS + s], c, j, i);
+    } else if constexpr (BATCH) {
+      direct |= 1u << it;
     } else {
       u64 slot = 0;
       const int r = gtab_insert(g, hi, lo, 0, rep, OP_NONE, &slot);
@@ -420,14 +433,69 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
         for (int j = 0; j < c.k; ++j) fold_col(c, j, i, slot);
     }
   }
+  if (BATCH && direct) {
+    u64 dslot[CB_ITEMS];
+    u32 won = 0, w2 = 0;
+    static_assert(CB_ITEMS == 8, "two batches of four");
+    u32 done = gtab_find_or_claim_home<4, 0>(g, khi_r, klo_r, krep_r, direct, dslot, won);
+    done |= gtab_find_or_claim_home<4, 4>(g, khi_r, klo_r, krep_r, direct, dslot, w2);
+    claims += __builtin_popcount(won | w2);
+#pragma unroll
+    for (int it = 0; it < CB_ITEMS; ++it) {
+      if (!(direct & (1u << it))) continue;
+      const u64 i = r0 + (u64)it * CB_T + t;
+      u64 slot = dslot[it];
+      int r = 1;
+      if (!(done & (1u << it))) {
+        r = gtab_insert(g, khi_r[it], klo_r[it], 0, krep_r[it], OP_NONE, &slot);
+        claims += r == 2;
+      }
+      if (r)
+        for (int j = 0; j < c.k; ++j) fold_col(c, j, i, slot);
+    }
+  }
   __syncthreads();
-  for (int s = t; s < CB_SLOTS; s += CB_T) {
-    if (!tag[s]) continue;
-    u64 slot = 0;
-    const int r = gtab_insert(g, khi[s], klo[s], 0, krep[s], OP_NONE, &slot);
-    claims += r == 2;
-    if (r)
-      for (int j = 0; j < c.k; ++j) cb_global_fold(c, j, slot, acc[j * CB_SLOTS + s]);
+  if constexpr (!BATCH) {
+    for (int s = t; s < CB_SLOTS; s += CB_T) {
+      if (!tag[s]) continue;
+      u64 slot = 0;
+      const int r = gtab_insert(g, khi[s], klo[s], 0, krep[s], OP_NONE, &slot);
+      claims += r == 2;
+      if (r)
+        for (int j = 0; j < c.k; ++j) cb_global_fold(c, j, slot, acc[j * CB_SLOTS + s]);
+    }
+    gtab_count_claims(g, claims);
+    return;
+  }
+  // the block's LDS-combined keys: the same batched probe, 2 per thread
+  constexpr int PER = CB_SLOTS / CB_T;
+  u64 fhi[PER], flo[PER], frep[PER], fslot[PER];
+  u32 occ = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int s = t + k * CB_T;
+    fhi[k] = khi[s];
+    flo[k] = klo[s];
+    frep[k] = krep[s];
+    if (tag[s]) occ |= 1u << k;
+  }
+  if (occ) {
+    u32 won = 0;
+    const u32 done = gtab_find_or_claim_home<PER, 0>(g, fhi, flo, frep, occ, fslot, won);
+    claims += __builtin_popcount(won);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (!(occ & (1u << k))) continue;
+      const int s = t + k * CB_T;
+      u64 slot = fslot[k];
+      int r = 1;
+      if (!(done & (1u << k))) {
+        r = gtab_insert(g, fhi[k], flo[k], 0, frep[k], OP_NONE, &slot);
+        claims += r == 2;
+      }
+      if (r)
+        for (int j = 0; j < c.k; ++j) cb_global_fold(c, j, slot, acc[j * CB_SLOTS + s]);
+    }
   }
   gtab_count_claims(g, claims);
 }
@@ -789,12 +857,19 @@ static Cols to_cols(const ColsArg* a) {
 // reducefn3 6.57-6.62 vs 6.60-6.91 vs 6.73-6.76 ms, profiles/r4/agg_grid_ab);
 // set from Tunables.agg_insert_grid (MR_AGG_INSERT_GRID) by the binding
 static unsigned g_ins_cap = 65536u;
+// agg_combine_kernel<BATCH> (Tunables.agg_batch, MR_AGG_BATCH)
+static bool g_agg_batch = false;
 
 extern "C" {
 
 int mr_agg_set_insert_grid(int cap) {
   if (cap < 256) return -1;
   g_ins_cap = (unsigned)cap;
+  return 0;
+}
+
+int mr_agg_set_batch(int on) {
+  g_agg_batch = on != 0;
   return 0;
 }
 
@@ -822,7 +897,9 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
     const size_t lds = (size_t)CB_SLOTS * (4 + (size_t)a->k) * sizeof(u64);
     static bool lds_attr = false;  // dynamic LDS above 64 KiB (k > 4 columns) must be allowed once
     if (!lds_attr) {
-      (void)hipFuncSetAttribute((const void*)agg_combine_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (void)hipFuncSetAttribute((const void*)agg_combine_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)((size_t)CB_SLOTS * (4 + MAXC) * sizeof(u64)));
+      (void)hipFuncSetAttribute((const void*)agg_combine_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)((size_t)CB_SLOTS * (4 + MAXC) * sizeof(u64)));
       lds_attr = true;
     }
@@ -830,8 +907,12 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
     u32 rows = (u32)CB_ROWS;
     while (rows > (u32)CB_T && (n + rows - 1) / rows < 1024) rows >>= 1;
     const u64 nb = (n + rows - 1) / rows;
-    hipLaunchKernelGGL(agg_combine_kernel, dim3((unsigned)nb), dim3(CB_T), lds, stream,
-                       ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
+    if (g_agg_batch)
+      hipLaunchKernelGGL(agg_combine_kernel<true>, dim3((unsigned)nb), dim3(CB_T), lds, stream,
+                         ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
+    else
+      hipLaunchKernelGGL(agg_combine_kernel<false>, dim3((unsigned)nb), dim3(CB_T), lds, stream,
+                         ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256, g_ins_cap)), dim3(256), 0, stream,

@@ -166,6 +166,82 @@ __device__ __forceinline__ int gtab_insert(const GTab& t, u64 hi, u64 lo, long l
   return 0;
 }
 
+// Up to N keys of one thread at once (bit k of `todo`): their home slots'
+// records are loaded together, keys found there are done (their slot in
+// `slot`), empty home slots are claimed with all CASes issued together, one
+// vmcnt drain after the claims' payload stores, then their publishing `lo`
+// stores (the claim protocol above, batched: one thread's keys pay about three
+// memory round trips together instead of three each).  No value is folded
+// (the caller folds its own columns at `slot`).  Returns the keys done; the
+// others (a home slot holding another key, a lost CAS, a long key found, a
+// claim not yet published) take gtab_insert.  `claimed`: the keys this call
+// claimed.
+// (Keys B .. B+N-1 of the caller's M-entry arrays: a batch of N = 4 keeps the
+// probe state in ~40 VGPRs, so a 512-thread kernel keeps two blocks per CU.)
+template <int N, int B, int M>
+__device__ __forceinline__ u32 gtab_find_or_claim_home(const GTab& t, const u64 (&hi_)[M], const u64 (&lo_)[M],
+                                                       const u64 (&rep_)[M], u32 todo, u64 (&slot)[M], u32& claimed) {
+  static_assert(B + N <= M, "batch past the arrays");
+  const u64* hi = hi_ + B;
+  const u64* lo = lo_ + B;
+  const u64* rep = rep_ + B;
+  todo = (todo >> B) & ((1u << N) - 1u);
+  u64 tg[N], gt[N], gl[N], gh[N], sl_[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    tg[k] = gtab_tag(hi[k], lo[k]);
+    sl_[k] = gtab_home(tg[k], t.mask);
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    gt[k] = gl[k] = gh[k] = 0;
+    if (todo & (1u << k)) {
+      const GSlot& sl = t.s[sl_[k]];
+      gt[k] = ld_agent(&sl.tag);
+      if (!gtab_tag_exact(tg[k])) {
+        gl[k] = ld_agent(&sl.lo);
+        gh[k] = ld_agent(&sl.hi);
+      }
+    }
+  }
+  u32 done = 0, cas = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    if (!(todo & (1u << k))) continue;
+    if (gt[k] == tg[k] && (gtab_tag_exact(tg[k]) || (gl[k] == lo[k] && gh[k] == hi[k] && !key_is_long(lo[k]))))
+      done |= 1u << k;
+    else if (gt[k] == 0)
+      cas |= 1u << k;
+  }
+  u32 won = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    if (cas & (1u << k)) {
+      u64 expected = 0;
+      if (__hip_atomic_compare_exchange_strong(&t.s[sl_[k]].tag, &expected, tg[k], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT))
+        won |= 1u << k;
+    }
+  }
+  if (won) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      if (won & (1u << k)) {
+        st_agent(&t.s[sl_[k]].hi, hi[k]);
+        st_agent(&t.s[sl_[k]].rep, rep[k]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if (won & (1u << k)) st_agent(&t.s[sl_[k]].lo, lo[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) slot[B + k] = sl_[k];
+  claimed = won << B;
+  return (done | won) << B;
+}
+
 __device__ __forceinline__ bool gtab_long_equal(const GTab& t, u64 slot, u64 rep) {
   u64 r = ld_agent(&t.s[slot].rep);
   if (rep_bytes_equal(t.src, r, rep)) return true;

@@ -267,7 +267,8 @@ __global__ void __launch_bounds__(256) rec_gather_kernel(const u32* __restrict__
 }
 
 // Row gather through LDS with 16-byte accesses on both sides, for rows of rb
-// bytes (rb % 4 == 0, 16 <= rb <= 244) and 16-byte aligned buffers.  A row
+// bytes (rb % 4 == 0, 16 <= rb <= 244; buffers 4-byte aligned: row slices
+// of a larger block take the 16-byte path too, with head bytes).  A row
 // starts 0/4/8/12 bytes into an aligned 16-byte chunk, so C = ceil((rb + 12) /
 // 16) aligned chunks cover it whatever its position: the block loads the C
 // chunks of each of its R rows (one dwordx4 per lane, all independent),
@@ -280,13 +281,13 @@ __global__ void __launch_bounds__(256) rec_gather_kernel(const u32* __restrict__
 template <int C, int R, bool PIPE>
 __global__ void __launch_bounds__(256) rec_gather16_kernel(const u8* __restrict__ in, u64 nin,
                                                            const u32* __restrict__ perm, u64 n, u32 rb,
-                                                           u8* __restrict__ out) {
+                                                           u8* __restrict__ out, u32 ih, u32 oh) {
   typedef u32 v4u __attribute__((ext_vector_type(4)));
   __shared__ v4u img[R * C];
   __shared__ u32 mis[R];
   constexpr int PER = (R * C + 255) / 256;
   const u32 t = threadIdx.x;
-  const u64 in_bytes = nin * (u64)rb;
+  const u64 in_bytes = nin * (u64)rb + ih;
   const u64 nbatch = (n + R - 1) / R;
   const float inv_rb = 1.0f / (float)rb;
   const u32* img32 = reinterpret_cast<const u32*>(img);
@@ -305,7 +306,7 @@ __global__ void __launch_bounds__(256) rec_gather16_kernel(const u8* __restrict_
       v[k] = v4u{0u, 0u, 0u, 0u};
       mv[k] = 0xFFFFFFFFu;
       if (idx < (u32)(R * C) && row < qrows) {
-        const u64 sb = (u64)clamp_row(perm[q0 + row], nin) * rb;
+        const u64 sb = (u64)clamp_row(perm[q0 + row], nin) * rb + ih;
         const u64 a = (sb & ~15ull) + 16ull * c;
         if (a + 16 <= in_bytes) {
           v[k] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + a));
@@ -332,31 +333,37 @@ __global__ void __launch_bounds__(256) rec_gather16_kernel(const u8* __restrict_
     __syncthreads();
     if (PIPE && b + gridDim.x < nbatch) load(b + gridDim.x);
     const u32 obytes = rows * rb;  // < 2^16 for R <= 256, rb <= 244
+    // the batch's bytes sit oh bytes into aligned 16-byte chunks (R * rb is a
+    // multiple of 16): chunks wholly inside them are dwordx4 stores, the
+    // first (oh != 0) and the last partial chunk dword stores
     u8* ob = out + r0 * rb;
-    const u32 nch = obytes >> 4;
-    for (u32 oc = t; oc < nch + 1; oc += 256) {
-      const u32 byte0 = oc * 16u;
-      if (byte0 >= obytes) break;
-      u32 row = (u32)((float)byte0 * inv_rb);  // exact after the corrections (byte0 < 2^24)
-      if (row * rb > byte0) --row;
-      if ((row + 1) * rb <= byte0) ++row;
-      const u32 off = byte0 - row * rb;
+    const u32 nch = (obytes + oh + 15) >> 4;
+    for (u32 oc = t; oc < nch; oc += 256) {
+      const int b0 = (int)(oc * 16u) - (int)oh;  // batch byte of the chunk's word 0 (< 0: before the batch)
+      const u32 s0 = b0 < 0 ? 0u : (u32)b0;
+      u32 row = (u32)((float)s0 * inv_rb);  // exact after the corrections (s0 < 2^24)
+      if (row * rb > s0) --row;
+      if ((row + 1) * rb <= s0) ++row;
+      const u32 off = s0 - row * rb;
       u32 w[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        u32 rr = row, oo = off + 4u * j;
+        const int lb = b0 + 4 * j;
+        u32 rr = row, oo = off + (u32)(lb - (int)s0);
         if (oo >= rb) {
           ++rr;
           oo -= rb;
         }
-        w[j] = rr < rows ? img32[(rr * (u32)C * 16u + mis[rr] + oo) >> 2] : 0u;
+        w[j] = lb >= 0 && rr < rows ? img32[(rr * (u32)C * 16u + mis[rr] + oo) >> 2] : 0u;
       }
-      if (oc < nch) {
-        __builtin_nontemporal_store(v4u{w[0], w[1], w[2], w[3]}, reinterpret_cast<v4u*>(ob + byte0));
-      } else {  // the batch's last partial chunk (rows * rb % 16 != 0): dwords
+      if (b0 >= 0 && (u32)b0 + 16u <= obytes) {
+        __builtin_nontemporal_store(v4u{w[0], w[1], w[2], w[3]}, reinterpret_cast<v4u*>(ob + oc * 16u));
+      } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (byte0 + 4u * j < obytes) *reinterpret_cast<u32*>(ob + byte0 + 4u * j) = w[j];
+        for (int j = 0; j < 4; ++j) {
+          const int lb = b0 + 4 * j;
+          if (lb >= 0 && (u32)lb < obytes) *reinterpret_cast<u32*>(ob + oc * 16u + 4u * j) = w[j];
+        }
       }
     }
     __syncthreads();
@@ -402,12 +409,15 @@ static inline unsigned rc_grid(u64 n, unsigned cap = 8192) {
   return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
+// in / out need only be 4-byte aligned (rows of a slice): the kernel takes
+// their 16-byte aligned bases and the head bytes before them
 template <int C, int R, bool PIPE>
 static void launch_gather16_t(const void* in, u64 nin, const void* perm, u64 n, int rb, void* out, hipStream_t s) {
   const u64 nb = (n + R - 1) / R;
   const unsigned g = (unsigned)(nb < 65536 ? nb : 65536);
-  hipLaunchKernelGGL((rc::rec_gather16_kernel<C, R, PIPE>), dim3(g), dim3(256), 0, s, (const u8*)in, nin,
-                     (const u32*)perm, n, (u32)rb, (u8*)out);
+  const u32 ih = (u32)((uintptr_t)in & 15), oh = (u32)((uintptr_t)out & 15);
+  hipLaunchKernelGGL((rc::rec_gather16_kernel<C, R, PIPE>), dim3(g), dim3(256), 0, s, (const u8*)in - ih, nin,
+                     (const u32*)perm, n, (u32)rb, (u8*)out - oh, ih, oh);
 }
 
 static bool g_gather_pipe = true;  // mr_rec_gather mode 2 forces the unpipelined form (A/B)
@@ -494,7 +504,7 @@ int mr_rec_gather(const void* in, u64 nin, const void* perm, u64 n, int rb, void
                        (const u8*)in, nin, (const u32*)perm, n, (u64)rb, (u8*)out);
     return (int)hipGetLastError();
   }
-  const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+  const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 3) == 0;  // (see launch_gather16_t)
   g_gather_pipe = mode != 2;
   if (mode == 2) mode = 0;
   if (mode == 0 && aligned && rb >= 16 && rb <= 244) {

@@ -271,6 +271,11 @@ __global__ void __launch_bounds__(RS_THREADS) rs_onesweep_kernel(const K* keys_i
   for (u32 i = t; i < cnt; i += RS_THREADS) {
     const K k = sk[i];
     const u32 pos = gout[(k >> shift) & 0xFF] + i;
+    // After a give-up (here or in an earlier pass of the same sort) the input
+    // holds rows left over from other data, whose digits no longer match the
+    // precomputed histograms: positions can then run past n.  The order is
+    // reported invalid through `err`; the writes must still stay in bounds.
+    if (pos >= n) continue;
     keys_out[pos] = k;
     if (has_v) vals_out[pos] = sv[i];
   }

@@ -72,17 +72,22 @@ def _tie_ws(d, words: int) -> torch.Tensor:
     return w
 
 
-def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: torch.Tensor | None = None):
+def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: torch.Tensor | None = None,
+         defer: bool = False):
     """(permutation int32 (int64 on CPU), sorted 32-bit key prefixes) of the
     rows in key order (stable).  GPU: pass ``k32``/``ghist`` from
-    :func:`keys32` to skip recomputing them."""
-    from .primitives import sort_error, sort_keys32, sort_keys_checked
+    :func:`keys32` to skip recomputing them.  ``defer``: no host sync — returns
+    (perm, sk, bad) with ``bad`` a device int32[1], non-zero when the fast
+    sort's order is invalid (a tie run too long for the fix-up, or a given-up
+    look-back); the caller checks it later and then takes :func:`sort_full`."""
+    from .primitives import sort_error, sort_error_word, sort_keys32
     n, rb = _check(rec, kb)
     if not rec.is_cuda:
         hi, lo = keys(rec, kb)
         from .primitives import sort_keys
         perm = sort_keys([hi, lo], bits=[64, 64])
-        return perm, keys32(rec, kb)[perm]
+        sk = keys32(rec, kb)[perm]
+        return (perm, sk, torch.zeros(1, dtype=torch.int32)) if defer else (perm, sk)
     d = rec.device
     if k32 is None or ghist is None:
         ghist = torch.zeros(2048, dtype=torch.int32, device=d)
@@ -93,25 +98,43 @@ def sort(rec: torch.Tensor, kb: int, k32: torch.Tensor | None = None, ghist: tor
     ws = _tie_ws(d, int(_hip.lib().mr_rec_tie_ws_words(n, cap)))
     _hip.call("mr_rec_tie_fixup", _hip.ptr(sk), _hip.ptr(perm), _hip.ptr(rec), n, rb, kb, _hip.ptr(bad),
               _hip.ptr(ws), cap, _hip.stream(d))
+    if defer:
+        err = sort_error_word(d)
+        if err is not None:
+            bad.bitwise_or_((err != 0).to(torch.int32) * 2)
+        return perm, sk, bad
     if int(bad.item()) or sort_error(d):
         # skewed keys (a prefix shared by more than 64 rows), or a given-up
         # look-back: sort the full key words
-        hi, lo = keys(rec, kb)
-        perm = sort_keys_checked([hi, lo], bits=[64, 64])
-        sk = k32[perm.long()]
+        return sort_full(rec, kb, k32)
     return perm, sk
 
 
-def gather(rec: torch.Tensor, perm: torch.Tensor, mode: int = 0) -> torch.Tensor:
+def sort_full(rec: torch.Tensor, kb: int, k32: torch.Tensor):
+    """:func:`sort` by the full (hi, lo) key words (checked sort): the
+    fallback when the prefix sort's fix-up cannot order the ties."""
+    from .primitives import sort_keys_checked
+    hi, lo = keys(rec, kb)
+    perm = sort_keys_checked([hi, lo], bits=[64, 64])
+    return perm, k32[perm.long()]
+
+
+def gather(rec: torch.Tensor, perm: torch.Tensor, mode: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
     """rec[perm] (rows).  GPU: 16-byte LDS-staged row gather for rows of
-    16-244 bytes (a multiple of 4) in 16-byte aligned buffers, else the dword
+    16-244 bytes (a multiple of 4; any row slice of a block), else the dword
     (or byte) gather; ``mode=1`` forces the dword gather (A/B probes, tests).
+    ``out``: rows written there (contiguous [len(perm), row_bytes] uint8, e.g.
+    a row slice of a larger block) instead of a new tensor.
     (A scatter through the inverse permutation lost: 16.6 vs 10.1 ms per
     10 GB, removed in round 5, profiles/r5/pruned/.)"""
     n = perm.numel()
     rb = int(rec.shape[1])
+    if out is not None and (tuple(out.shape) != (n, rb) or out.dtype != torch.uint8 or not out.is_contiguous()
+                            or out.device != rec.device):
+        raise ValueError("gather: out must be a contiguous uint8 [len(perm), row_bytes] tensor on rec's device")
     if rec.is_cuda:
-        out = torch.empty((n, rb), dtype=torch.uint8, device=rec.device)
+        if out is None:
+            out = torch.empty((n, rb), dtype=torch.uint8, device=rec.device)
         if n == 0:
             return out
         if rec.shape[0] == 0:
@@ -120,6 +143,8 @@ def gather(rec: torch.Tensor, perm: torch.Tensor, mode: int = 0) -> torch.Tensor
         _hip.call("mr_rec_gather", _hip.ptr(rec), int(rec.shape[0]), _hip.ptr(p.contiguous()), n, rb, _hip.ptr(out),
                   int(mode), _hip.stream(rec.device))
         return out
+    if out is not None:
+        return torch.index_select(rec, 0, perm.long(), out=out)
     return rec[perm.long()]
 
 

@@ -123,6 +123,19 @@ def all_to_all_v(payload: torch.Tensor, send_counts: list[int], recv_counts: lis
     return out
 
 
+def all_to_all_v_into(out: torch.Tensor, payload: torch.Tensor, send_counts: list[int], recv_counts: list[int],
+                      group=None, async_op: bool = False):
+    """all_to_all_v into a caller's buffer ``out`` (rows of ``sum(recv_counts)``).
+    ``async_op`` (RCCL): returns the work handle right away — the exchange
+    runs on the collective's own stream while the caller queues more work on
+    its stream; ``wait()`` before reading ``out`` (gloo: done on return, None)."""
+    if async_op and not _is_gloo(group):
+        return dist.all_to_all_single(out, payload.contiguous(), list(recv_counts), list(send_counts), group=group,
+                                      async_op=True)
+    _a2a(out, payload.contiguous(), list(recv_counts), list(send_counts), group)
+    return None
+
+
 def all_to_all_bytes(payloads: list, device=None, group=None) -> list:
     """payloads[d] (bytes) goes to rank d; returns the byte strings every rank
     sent here, in rank order.  Two collectives whatever the world size: the

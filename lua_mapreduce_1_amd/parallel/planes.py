@@ -977,15 +977,17 @@ class RecordPlane:
             return torch.zeros((0, self.shape[0]), dtype=torch.uint8, device=eng.device)
         return self._out[0] if len(self._out) == 1 else torch.cat(self._out)
 
-    def _sample_splitters(self, k32: torch.Tensor | None, R: int, host_rows: list | None = None) -> torch.Tensor:
+    def _sample_splitters(self, k32: torch.Tensor | None, R: int, host_rows: list | None = None,
+                          per: int | None = None) -> torch.Tensor:
         """R-1 splitters (32-bit key prefixes, unsigned, as int32 bit
         patterns) from a sample of every rank's keys (TeraSort's sampled
         total-order partitioner).  ``host_rows``: the sample is drawn from
-        spilled blocks instead."""
+        spilled blocks instead.  ``per``: keys sampled per rank (default
+        oversample x R)."""
         eng = self.eng
         # the same sample size on every rank (all_gather), drawn with
         # replacement; a rank without rows contributes -1s, dropped below
-        k = self.oversample * R
+        k = per or self.oversample * R
         g = torch.Generator().manual_seed(self.seed * 7919 + eng.rank)
         if host_rows is not None:
             samp = _host_sample32(host_rows, self.shape[1], k, g).to(eng.device)
@@ -1123,6 +1125,77 @@ class RecordPlane:
             buckets[j] = None  # release the bucket's host rows
         return out, counts.tolist()
 
+    def _exchange_ranges(self, rec: torch.Tensor, kb: int, sub: torch.Tensor, K: int, failed: int,
+                         k32: torch.Tensor):
+        """The W > 1 exchange pipelined by key range: every
+        destination's key range is cut into ``K`` sub-ranges (``sub``: the
+        R*K - 1 sub-splitters, global — from the all-gathered sample), and the
+        exchange runs in K rounds, round k moving every rank's rows of
+        sub-range k of every destination.  Sub-range k of a rank's range holds
+        only keys below those of sub-range k+1, so the rank's output is its K
+        received pieces each sorted on its own, in round order — the receive
+        side sorts round k while the all-to-alls of rounds > k are still on
+        the wire (RCCL's stream, xGMI), and only the last round's sort is left
+        after the exchange.  Send side: one stable sort by (round, destination)
+        bucket and a row gather per round, each handed to an asynchronous
+        all-to-all as soon as it is queued.  Needs R <= W (destination =
+        partition: monotone in the key).  Returns (rows of this rank in key
+        order, failed maps of every rank)."""
+        from ..ops import records as RC
+        eng = self.eng
+        W = eng.world
+        dev = rec.device
+        n, rb = int(rec.shape[0]), int(rec.shape[1])
+        B = K * W
+        if n:
+            s = RC.dest32(k32, sub) if sub.numel() else torch.zeros(n, dtype=torch.int32, device=dev)
+            # sub-range s: partition (= destination) s // K, round s % K -> bucket round * W + destination
+            b = torch.remainder(s, K).mul_(W).add_(torch.div(s, K, rounding_mode="floor"))
+            perm = ops.sort_keys_checked([b.to(torch.int64)], bits=[max(8, _bits(B))])
+            if perm.dtype != torch.int32:
+                perm = perm.to(torch.int32)
+            counts = ops.bincount(b, B)
+        else:
+            perm = torch.zeros(0, dtype=torch.int32, device=dev)
+            counts = torch.zeros(B, dtype=torch.int64, device=dev)
+        # per destination: its rows of each round, then this rank's failed maps
+        xchg = torch.cat([counts.view(K, W).t().to(torch.int64),
+                          torch.full((W, 1), failed, dtype=torch.int64, device=counts.device)], 1).contiguous()
+        recv = D.exchange_counts(xchg.view(-1), eng.group).view(W, K + 1)
+        both = torch.cat([xchg, recv]).cpu().numpy()
+        failed = int(both[W:, K].sum())
+        send, rcv = both[:W, :K], both[W:, :K]  # [destination][round], [source][round]
+        recv_buf = torch.empty((int(rcv.sum()), rb), dtype=torch.uint8, device=dev)
+        out = torch.empty_like(recv_buf)
+        rounds, s0, r0 = [], 0, 0
+        for k in range(K):
+            ssz, rsz = [int(x) for x in send[:, k]], [int(x) for x in rcv[:, k]]
+            ms, mr = sum(ssz), sum(rsz)
+            buf = RC.gather(rec, perm[s0:s0 + ms]) if ms else torch.zeros((0, rb), dtype=torch.uint8, device=dev)
+            work = D.all_to_all_v_into(recv_buf[r0:r0 + mr], buf, ssz, rsz, eng.group, async_op=True)
+            rounds.append((work, buf, r0, mr))
+            s0 += ms
+            r0 += mr
+        bads = []
+        for work, _buf, r0, mr in rounds:
+            if work is not None:
+                work.wait()
+            if not mr:
+                continue
+            piece = recv_buf[r0:r0 + mr]
+            gh = torch.zeros(2048, dtype=torch.int32, device=dev) if piece.is_cuda else None
+            pk = RC.keys32(piece, kb, gh)
+            p, _sk, bad = RC.sort(piece, kb, pk, gh, defer=True)
+            RC.gather(piece, p, out=out[r0:r0 + mr])
+            bads.append((bad, pk, r0, mr))
+        if bads and bool(torch.cat([x[0] for x in bads]).any()):
+            for bad, pk, r0, mr in bads:  # rare: skewed prefixes or a given-up look-back
+                if int(bad.item()):
+                    piece = recv_buf[r0:r0 + mr]
+                    p, _sk = RC.sort_full(piece, kb, pk)
+                    RC.gather(piece, p, out=out[r0:r0 + mr])
+        return out, failed
+
     def run_iteration(self, prefetch_next, lookahead):
         from ..ops import records as RC
         eng = self.eng
@@ -1157,12 +1230,23 @@ class RecordPlane:
             return res
         k32 = None
         sp = self.splitters
-        if R > 1 and sp is None:
-            k32 = RC.keys32(rec, kb)
-            sp = self._sample_splitters(k32, R)
-        elif sp is not None:
-            sp = sp.to(eng.device)
-        if W > 1 or eng.force_shuffle:
+        K = min(max(0, int(TUNABLES.rec_chunks)), 1024 // max(R, 1))  # (rec_dest32: <= 1023 splitters)
+        ranged = (W > 1 or eng.force_shuffle) and K >= 1 and sp is None and R <= W
+        out = None
+        if ranged:
+            with trace.range("mr.rec.shuffle"):
+                k32 = RC.keys32(rec, kb)
+                sub = self._sample_splitters(k32, R * K, per=self.oversample * R)
+                sp = sub[K - 1::K].contiguous() if R > 1 else None
+                out, failed = self._exchange_ranges(rec, kb, sub, K, failed, k32)
+                del rec
+        else:
+            if R > 1 and sp is None:
+                k32 = RC.keys32(rec, kb)
+                sp = self._sample_splitters(k32, R)
+            elif sp is not None:
+                sp = sp.to(eng.device)
+        if not ranged and (W > 1 or eng.force_shuffle):
             with trace.range("mr.rec.shuffle"):
                 if k32 is None:
                     k32 = RC.keys32(rec, kb)
@@ -1182,19 +1266,26 @@ class RecordPlane:
                 del packed
         T["shuffle"] = time.time() - t1
         t2 = time.time()
-        with trace.range("mr.rec.sort"):
-            # the sort's digit histograms come out of the key extraction
-            gh = torch.zeros(2048, dtype=torch.int32, device=rec.device) if rec.is_cuda else None
-            k32 = RC.keys32(rec, kb, gh)
-            perm, sk = RC.sort(rec, kb, k32, gh)
-            out = RC.gather(rec, perm)
-            if R > 1:
-                pcount = ops.bincount(RC.dest32(sk, sp), R)
-            else:
-                pcount = torch.tensor([out.shape[0]], dtype=torch.int64)
-        counts = pcount.cpu().tolist()
+        if ranged:
+            # the received rows are this rank's partition, already in key order
+            counts = [0] * R
+            if eng.rank < R:
+                counts[eng.rank] = int(out.shape[0])
+        else:
+            with trace.range("mr.rec.sort"):
+                # the sort's digit histograms come out of the key extraction
+                gh = torch.zeros(2048, dtype=torch.int32, device=rec.device) if rec.is_cuda else None
+                k32 = RC.keys32(rec, kb, gh)
+                perm, sk = RC.sort(rec, kb, k32, gh)
+                out = RC.gather(rec, perm)
+                if R > 1:
+                    pcount = ops.bincount(RC.dest32(sk, sp), R)
+                else:
+                    pcount = torch.tensor([out.shape[0]], dtype=torch.int64)
+            counts = pcount.cpu().tolist()
         _result_jobs(eng, res, counts, t1)
-        res.device = {"records": out, "counts_host": counts, "splitters": sp, "key_bytes": kb}
+        res.device = {"records": out, "counts_host": counts, "splitters": sp, "key_bytes": kb,
+                      "subsplitters": sub if ranged else None}
         res.distinct_keys = int(out.shape[0])
         res.total_value = int(out.shape[0])
         res.failed_maps = failed

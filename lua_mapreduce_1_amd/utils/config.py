@@ -104,6 +104,14 @@ class Tunables:
                                "API, csrc/hip/sdma.hip) after the tail's kernels, not as a runtime blit kernel on "
                                "the CUs beside the next map (0 = never)")
     spin_us: float = _knob("MR_SPIN_US", 2000.0, "host spin on completion words before hipStreamSynchronize, us")
+    rec_chunks: int = _knob("MR_REC_CHUNKS", 4,
+                            "record plane at W > 1 (R <= W partitions, sampled splitters): rounds of the exchange "
+                            "pipelined by key range — every destination's range cut in this many sub-ranges, round "
+                            "k's all-to-all overlapping the receive-side sort of round k-1 (0: one exchange, then "
+                            "one sort of everything received)")
+    agg_batch: bool = _knob("MR_AGG_BATCH", False,
+                            "generic combine kernel: rows for the HBM table probe their home slots in batches of "
+                            "four per thread (csrc/hip/hashtab.h gtab_find_or_claim_home) instead of one insert each")
     map_dyn: bool = _knob("MR_MAP_DYN", True,
                           "word-count map kernel: waves take the tile's token list 64 entries at a time from an "
                           "LDS counter (csrc/hip/wordcount3.hip DYN) instead of a fixed stride")

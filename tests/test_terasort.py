@@ -95,10 +95,14 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, on_gpu=False, backend="gloo", force_shuffle=False):
+def _worker(rank, world, port, q, on_gpu=False, backend="gloo", force_shuffle=False, chunks=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
+    import dataclasses
     import datetime
+    if chunks is not None:  # rounds of the exchange pipelined by key range (0: one exchange)
+        from lua_mapreduce_1_amd.parallel import planes as PL
+        PL.TUNABLES = dataclasses.replace(PL.TUNABLES, rec_chunks=chunks)
     import torch.distributed as dist
     from lua_mapreduce_1_amd.parallel import dist as D
     if force_shuffle:
@@ -140,6 +144,24 @@ def test_gloo_multi_rank_sort(world):
 
 def test_gloo_forced_shuffle_one_rank():
     _run(1, force_shuffle=True)
+
+
+@pytest.mark.parametrize("chunks", [0, 1, 3])
+def test_gloo_exchange_rounds(chunks):
+    """Both W > 1 exchanges: one exchange + one sort (0), and the exchange
+    pipelined by key range in 1 or 3 rounds, each round's rows sorted apart."""
+    _run(3, chunks=chunks)
+
+
+def test_gather_into_row_slices_cpu():
+    from lua_mapreduce_1_amd.ops import records as RC
+    rec = TS.generate(1000, 5, 99)
+    out = torch.zeros((1010, 100), dtype=torch.uint8)
+    perm = torch.randperm(1000)[:700]
+    RC.gather(rec[3:], perm, out=out[7:707])
+    assert torch.equal(out[7:707], rec[3:][perm])
+    with pytest.raises(ValueError):
+        RC.gather(rec, perm, out=out[:10])
 
 
 @pytest.mark.gpu
@@ -242,6 +264,24 @@ def test_gpu_single_rank_sort(gpu, partitions):
 @pytest.mark.gpu
 def test_gpu_multi_rank_on_one_gpu(gpu):
     _run(2, on_gpu=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rb", [16, 20, 100, 244])
+def test_gpu_gather_row_slices(gpu, rb):
+    """The 16-byte row gather on row slices that start 4/8/12 bytes into a
+    16-byte chunk (input and output heads), against torch indexing."""
+    from lua_mapreduce_1_amd.ops import records as RC
+    g = torch.Generator().manual_seed(rb)
+    base = torch.randint(0, 256, (70_001, rb), dtype=torch.uint8, generator=g)
+    src = base.to(gpu)
+    for i0, o0, n in [(0, 0, 50_000), (1, 3, 49_999), (3, 1, 12_345), (2, 2, 257), (5, 7, 1)]:
+        perm = torch.randint(0, 70_001 - i0, (n,), dtype=torch.int32, generator=g)
+        out = torch.full((n + 20, rb), 0xA5, dtype=torch.uint8, device=gpu)
+        RC.gather(src[i0:], perm.to(gpu), out=out[o0:o0 + n])
+        host = out.cpu()
+        assert torch.equal(host[o0:o0 + n], base[i0:][perm.long()]), (rb, i0, o0, n)
+        assert bool((host[:o0] == 0xA5).all()) and bool((host[o0 + n:] == 0xA5).all()), "wrote outside the slice"
 
 
 @pytest.mark.gpu
