@@ -385,7 +385,7 @@ __device__ __forceinline__ u32 cb_row_keys(const Keys& ks, u64 r0, int items, u6
 // BATCH (mr_agg_set_batch): the rows that go to the HBM table directly, and
 // the flush of the LDS-combined keys, probe their home slots in batches
 // (gtab_find_or_claim_home) instead of one gtab_insert per key.
-template <bool BATCH>
+template <bool BATCH, int PH>
 __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 n, Cols c, u32 rows) {
   constexpr int CB_ITEMS = CB_ROWS / CB_T;
   const int items = (int)(rows / CB_T);
@@ -406,52 +406,80 @@ __global__ void __launch_bounds__(CB_T) agg_combine_kernel(GTab g, Keys ks, u64 
   __syncthreads();
   u32 claims = 0;
   const u64 r0 = (u64)blockIdx.x * rows;
-  u64 khi_r[CB_ITEMS], klo_r[CB_ITEMS], krep_r[CB_ITEMS];
-  const u32 ok = cb_row_keys<CB_ITEMS>(ks, r0, items, n, khi_r, klo_r, krep_r);
   // rows whose key found no room in the LDS table (or is long) go to the HBM
   // table directly — BATCH: all of a thread's such rows probe their home
   // slots together (gtab_find_or_claim_home), the rest one by one.  With few
   // repeats inside a block (bigrams: 23 M distinct of 47 M) that is most rows,
   // and one dependent claim chain per row had kept 82 % of the wave cycles
   // waiting (profiles/r5/bigram/pmc/).
-  u32 direct = 0;
+  if constexpr (!BATCH && PH > 1) {
+    // PH phases of CB_ITEMS / PH rows per thread: PH = 2 holds half the row
+    // keys in registers (56 VGPRs: 7 waves per SIMD instead of 6)
+    constexpr int HI = CB_ITEMS / PH;
 #pragma unroll
-  for (int it = 0; it < CB_ITEMS; ++it) {
-    const u64 i = r0 + (u64)it * CB_T + t;
-    if (!(ok & (1u << it))) continue;
-    const u64 hi = khi_r[it], lo = klo_r[it], rep = krep_r[it];
-    const int s = key_is_long(lo) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, hi, lo, rep);
-    if (s >= 0) {
-      for (int j = 0; j < c.k; ++j) cb_lds_fold(&acc[j * CB_SLOTS + s], c, j, i);
-    } else if constexpr (BATCH) {
-      direct |= 1u << it;
-    } else {
-      u64 slot = 0;
-      const int r = gtab_insert(g, hi, lo, 0, rep, OP_NONE, &slot);
-      claims += r == 2;
-      if (r)
-        for (int j = 0; j < c.k; ++j) fold_col(c, j, i, slot);
+    for (int ph = 0; ph < PH; ++ph) {
+      u64 khi_r[HI], klo_r[HI], krep_r[HI];
+      const u64 rb = r0 + (u64)ph * HI * CB_T;
+      const u32 ok = cb_row_keys<HI>(ks, rb, items - ph * HI, n, khi_r, klo_r, krep_r);
+#pragma unroll
+      for (int it = 0; it < HI; ++it) {
+        const u64 i = rb + (u64)it * CB_T + t;
+        if (!(ok & (1u << it))) continue;
+        const u64 hi = khi_r[it], lo = klo_r[it], rep = krep_r[it];
+        const int s = key_is_long(lo) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, hi, lo, rep);
+        if (s >= 0) {
+          for (int j = 0; j < c.k; ++j) cb_lds_fold(&acc[j * CB_SLOTS + s], c, j, i);
+        } else {
+          u64 slot = 0;
+          const int r = gtab_insert(g, hi, lo, 0, rep, OP_NONE, &slot);
+          claims += r == 2;
+          if (r)
+            for (int j = 0; j < c.k; ++j) fold_col(c, j, i, slot);
+        }
+      }
     }
-  }
-  if (BATCH && direct) {
-    u64 dslot[CB_ITEMS];
-    u32 won = 0, w2 = 0;
-    static_assert(CB_ITEMS == 8, "two batches of four");
-    u32 done = gtab_find_or_claim_home<4, 0>(g, khi_r, klo_r, krep_r, direct, dslot, won);
-    done |= gtab_find_or_claim_home<4, 4>(g, khi_r, klo_r, krep_r, direct, dslot, w2);
-    claims += __builtin_popcount(won | w2);
+  } else {
+    u64 khi_r[CB_ITEMS], klo_r[CB_ITEMS], krep_r[CB_ITEMS];
+    const u32 ok = cb_row_keys<CB_ITEMS>(ks, r0, items, n, khi_r, klo_r, krep_r);
+    u32 direct = 0;
 #pragma unroll
     for (int it = 0; it < CB_ITEMS; ++it) {
-      if (!(direct & (1u << it))) continue;
       const u64 i = r0 + (u64)it * CB_T + t;
-      u64 slot = dslot[it];
-      int r = 1;
-      if (!(done & (1u << it))) {
-        r = gtab_insert(g, khi_r[it], klo_r[it], 0, krep_r[it], OP_NONE, &slot);
+      if (!(ok & (1u << it))) continue;
+      const u64 hi = khi_r[it], lo = klo_r[it], rep = krep_r[it];
+      const int s = key_is_long(lo) ? -1 : cb_slot(tag, khi, klo, krep, &nclaimed, hi, lo, rep);
+      if (s >= 0) {
+        for (int j = 0; j < c.k; ++j) cb_lds_fold(&acc[j * CB_SLOTS + s], c, j, i);
+      } else if constexpr (BATCH) {
+        direct |= 1u << it;
+      } else {
+        u64 slot = 0;
+        const int r = gtab_insert(g, hi, lo, 0, rep, OP_NONE, &slot);
         claims += r == 2;
+        if (r)
+          for (int j = 0; j < c.k; ++j) fold_col(c, j, i, slot);
       }
-      if (r)
-        for (int j = 0; j < c.k; ++j) fold_col(c, j, i, slot);
+    }
+    if (BATCH && direct) {
+      u64 dslot[CB_ITEMS];
+      u32 won = 0, w2 = 0;
+      static_assert(CB_ITEMS == 8, "two batches of four");
+      u32 done = gtab_find_or_claim_home<4, 0>(g, khi_r, klo_r, krep_r, direct, dslot, won);
+      done |= gtab_find_or_claim_home<4, 4>(g, khi_r, klo_r, krep_r, direct, dslot, w2);
+      claims += __builtin_popcount(won | w2);
+#pragma unroll
+      for (int it = 0; it < CB_ITEMS; ++it) {
+        if (!(direct & (1u << it))) continue;
+        const u64 i = r0 + (u64)it * CB_T + t;
+        u64 slot = dslot[it];
+        int r = 1;
+        if (!(done & (1u << it))) {
+          r = gtab_insert(g, khi_r[it], klo_r[it], 0, krep_r[it], OP_NONE, &slot);
+          claims += r == 2;
+        }
+        if (r)
+          for (int j = 0; j < c.k; ++j) fold_col(c, j, i, slot);
+      }
     }
   }
   __syncthreads();
@@ -859,6 +887,8 @@ static Cols to_cols(const ColsArg* a) {
 static unsigned g_ins_cap = 65536u;
 // agg_combine_kernel<BATCH> (Tunables.agg_batch, MR_AGG_BATCH)
 static bool g_agg_batch = false;
+// agg_combine_kernel<false, PH> (Tunables.agg_phases, MR_AGG_PHASES)
+static int g_agg_phases = 1;
 
 extern "C" {
 
@@ -870,6 +900,12 @@ int mr_agg_set_insert_grid(int cap) {
 
 int mr_agg_set_batch(int on) {
   g_agg_batch = on != 0;
+  return 0;
+}
+
+int mr_agg_set_phases(int ph) {
+  if (ph != 1 && ph != 2 && ph != 4) return -1;
+  g_agg_phases = ph;
   return 0;
 }
 
@@ -897,22 +933,29 @@ int mr_agg_insert(void* tag, void* thi, void* tlo, void* tval, void* trep, void*
     const size_t lds = (size_t)CB_SLOTS * (4 + (size_t)a->k) * sizeof(u64);
     static bool lds_attr = false;  // dynamic LDS above 64 KiB (k > 4 columns) must be allowed once
     if (!lds_attr) {
-      (void)hipFuncSetAttribute((const void*)agg_combine_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)((size_t)CB_SLOTS * (4 + MAXC) * sizeof(u64)));
-      (void)hipFuncSetAttribute((const void*)agg_combine_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)((size_t)CB_SLOTS * (4 + MAXC) * sizeof(u64)));
+      for (const void* f : {(const void*)agg_combine_kernel<false, 1>, (const void*)agg_combine_kernel<false, 2>,
+                            (const void*)agg_combine_kernel<false, 4>, (const void*)agg_combine_kernel<true, 1>})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)((size_t)CB_SLOTS * (4 + MAXC) * sizeof(u64)));
       lds_attr = true;
     }
     // rows per block: 4096, or fewer (down to 512) so the grid has >= 1024 blocks
     u32 rows = (u32)CB_ROWS;
     while (rows > (u32)CB_T && (n + rows - 1) / rows < 1024) rows >>= 1;
     const u64 nb = (n + rows - 1) / rows;
+    const GTab gt = ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src);
     if (g_agg_batch)
-      hipLaunchKernelGGL(agg_combine_kernel<true>, dim3((unsigned)nb), dim3(CB_T), lds, stream,
-                         ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
+      hipLaunchKernelGGL((agg_combine_kernel<true, 1>), dim3((unsigned)nb), dim3(CB_T), lds, stream, gt, ks, n,
+                         to_cols(a), rows);
+    else if (g_agg_phases == 2)
+      hipLaunchKernelGGL((agg_combine_kernel<false, 2>), dim3((unsigned)nb), dim3(CB_T), lds, stream, gt, ks, n,
+                         to_cols(a), rows);
+    else if (g_agg_phases == 4)
+      hipLaunchKernelGGL((agg_combine_kernel<false, 4>), dim3((unsigned)nb), dim3(CB_T), lds, stream, gt, ks, n,
+                         to_cols(a), rows);
     else
-      hipLaunchKernelGGL(agg_combine_kernel<false>, dim3((unsigned)nb), dim3(CB_T), lds, stream,
-                         ag_gtab(tag, thi, tlo, tval, trep, ctrl, cap, src), ks, n, to_cols(a), rows);
+      hipLaunchKernelGGL((agg_combine_kernel<false, 1>), dim3((unsigned)nb), dim3(CB_T), lds, stream, gt, ks, n,
+                         to_cols(a), rows);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(agg_insert_kernel, dim3(ag_grid(n, 256, g_ins_cap)), dim3(256), 0, stream,

@@ -399,6 +399,80 @@ __global__ void rec_dest32_kernel(const u32* __restrict__ k32, u64 n, const u32*
   }
 }
 
+// The exchange bucket of every row for the record plane's exchange pipelined
+// by key range (parallel/planes.py _exchange_ranges): sub-range a = number of
+// sub-splitters <= k32, partition a / K, round a % K -> bucket
+// (a % K) * W + a / K, plus the buckets' histogram (= the rows per bucket, and
+// digit 0 of the one-pass u32 sort that orders the rows by bucket): one pass
+// instead of dest32 + four elementwise ops + an 8-bit u64 sort + bincount.
+__global__ void __launch_bounds__(256) rec_bucket32_kernel(const u32* __restrict__ k32, u64 n,
+                                                           const u32* __restrict__ split, u32 nsplit, u32 K, u32 W,
+                                                           u32* __restrict__ bucket, u32* __restrict__ ghist) {
+  __shared__ u32 s[1024];
+  __shared__ u32 h[256];
+  const int t = threadIdx.x;
+  for (u32 k = t; k < nsplit; k += blockDim.x) s[k] = split[k];
+  h[t] = 0;
+  __syncthreads();
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + t; i < n; i += stride) {
+    const u32 x = k32[i];
+    u32 a = 0, b = nsplit;
+    while (a < b) {
+      const u32 m = (a + b) >> 1;
+      if (s[m] <= x) a = m + 1;
+      else b = m;
+    }
+    const u32 q = a / K;
+    const u32 bk = (a - q * K) * W + q;
+    bucket[i] = bk;
+    atomicAdd(&h[bk], 1u);
+  }
+  __syncthreads();
+  if (h[t]) atomicAdd(&ghist[t], h[t]);
+}
+
+// Splitter sampling of the record plane (parallel/planes.py
+// _sample_splitters) in three launches instead of ~20 small torch ops (the
+// W = 8 step's preparation was host-bound on them, ~25 us of host time each):
+// rec_sample32 draws k rows with a counter-based hash (row = fmix64(seed, j)
+// mod n) and writes their 32-bit key prefixes as int64 (-1 for a rank
+// without rows); after the all-gather and a sort, rec_pick takes the R - 1
+// splitters at evenly spaced ranks of the non-negative entries.
+__global__ void rec_sample32_kernel(const u32* __restrict__ k32, u64 n, u32 k, u64 seed, long long* __restrict__ out) {
+  const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= k) return;
+  out[j] = n ? (long long)k32[fmix64(seed * 0x9E3779B97F4A7C15ull + j) % n] : -1ll;
+}
+
+__global__ void rec_pick_kernel(const long long* __restrict__ srt, u64 N, u32 R, u32* __restrict__ sp) {
+  // the negatives (empty ranks) sort first: the first non-negative index
+  u64 a = 0, b = N;
+  while (a < b) {
+    const u64 m = (a + b) >> 1;
+    if (srt[m] < 0) a = m + 1;
+    else b = m;
+  }
+  const u64 m = N - a;
+  for (u32 j = threadIdx.x + 1; j < R; j += blockDim.x) {
+    u64 i = a + m * j / R;
+    if (i >= N) i = N - 1;
+    sp[j - 1] = m ? (u32)srt[i] : 0u;
+  }
+}
+
+// The count-exchange rows of the range-pipelined exchange, from the bucket
+// histogram: xchg[d][k] = rows for destination d in round k (bucket k*W + d),
+// xchg[d][K] = this rank's failed maps; flag = the bucket sort gave up.
+__global__ void rec_xchg_kernel(const u32* __restrict__ gh, u32 K, u32 W, long long failed, const u32* __restrict__ err,
+                                long long* __restrict__ xchg, long long* __restrict__ flag) {
+  for (u32 i = threadIdx.x; i < W * (K + 1); i += blockDim.x) {
+    const u32 d = i / (K + 1), k = i - d * (K + 1);
+    xchg[i] = k < K ? (long long)gh[k * W + d] : failed;
+  }
+  if (threadIdx.x == 0) flag[0] = (err && err[0]) ? 1 : 0;
+}
+
 }  // namespace rc
 }  // namespace mr
 
@@ -535,6 +609,39 @@ int mr_rec_gather(const void* in, u64 nin, const void* perm, u64 n, int rb, void
   else
     hipLaunchKernelGGL((rc::rec_gather_kernel<0, 8>), dim3(g), dim3(256), 0, s, (const u32*)in, nin,
                        (const u32*)perm, n, words, (u32*)out);
+  return (int)hipGetLastError();
+}
+
+// ghist: zeroed u32 [>= 256]; K * W <= 256 buckets, nsplit = R * K - 1 <= 1023
+int mr_rec_bucket32(const void* k32, u64 n, const void* split, u32 nsplit, u32 K, u32 W, void* bucket, void* ghist,
+                    hipStream_t s) {
+  if (n == 0) return 0;
+  if (nsplit > 1024 || K == 0 || W == 0 || (u64)K * W > 256 || (nsplit + 1 + K - 1) / K > W) return -1;
+  hipLaunchKernelGGL(rc::rec_bucket32_kernel, dim3(rc_grid(n, 2048)), dim3(256), 0, s, (const u32*)k32, n,
+                     (const u32*)split, nsplit, K, W, (u32*)bucket, (u32*)ghist);
+  return (int)hipGetLastError();
+}
+
+int mr_rec_sample32(const void* k32, u64 n, u32 k, u64 seed, void* out, hipStream_t s) {
+  if (k == 0) return 0;
+  hipLaunchKernelGGL(rc::rec_sample32_kernel, dim3((k + 255) / 256), dim3(256), 0, s, (const u32*)k32, n, k, seed,
+                     (long long*)out);
+  return (int)hipGetLastError();
+}
+
+// srt: N sorted int64 (negatives = no sample); sp: R - 1 u32
+int mr_rec_pick(const void* srt, u64 N, u32 R, void* sp, hipStream_t s) {
+  if (R <= 1) return 0;
+  if (N == 0) return -1;
+  hipLaunchKernelGGL(rc::rec_pick_kernel, dim3(1), dim3(256), 0, s, (const long long*)srt, N, R, (u32*)sp);
+  return (int)hipGetLastError();
+}
+
+int mr_rec_xchg(const void* gh, u32 K, u32 W, long long failed, const void* err, void* xchg, void* flag,
+                hipStream_t s) {
+  if ((u64)K * W > 256) return -1;
+  hipLaunchKernelGGL(rc::rec_xchg_kernel, dim3(1), dim3(256), 0, s, (const u32*)gh, K, W, failed, (const u32*)err,
+                     (long long*)xchg, (long long*)flag);
   return (int)hipGetLastError();
 }
 

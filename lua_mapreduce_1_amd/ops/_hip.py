@@ -102,6 +102,10 @@ _SIGS = {
     "mr_rec_tie_fixup": [_p, _p, _p, _u64, _i32, _i32, _p, _p, _u64, _p],
     "mr_rec_gather": [_p, _u64, _p, _u64, _i32, _p, _i32, _p],
     "mr_rec_dest32": [_p, _u64, _p, _u32, _p, _p],
+    "mr_rec_bucket32": [_p, _u64, _p, _u32, _u32, _u32, _p, _p, _p],
+    "mr_rec_sample32": [_p, _u64, _u32, _u64, _p, _p],
+    "mr_rec_pick": [_p, _u64, _u32, _p, _p],
+    "mr_rec_xchg": [_p, _u32, _u32, ctypes.c_longlong, _p, _p, _p, _p],
     "mr_agg_insert": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _u64, _p, _p],
     "mr_slot_compact": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _p, _p],
     "mr_col_fill": [_p, _u64, ctypes.c_longlong, _i32, _p],
@@ -137,6 +141,7 @@ _SIGS = {
     "mr_mrc1_decode": [_p, _p, _u32, _u64, _p, _p, _p, _p, _p],
     "mr_wc3_set_dyn": [_i32],
     "mr_agg_set_batch": [_i32],
+    "mr_agg_set_phases": [_i32],
 }
 _RESTYPE_U64 = {"mr_compact_pack_ws_bytes", "mr_ii_unique_tiles", "mr_text_tiles", "mr_scan_partials_len", "mr_tail_pack_bytes", "mr_tail_ws_layout",
                 "mr_tail_bhist_bytes", "mr_onesweep_tiles", "mr_rec_tie_ws_words", "mr_sdma_d2h_begin",
@@ -171,6 +176,7 @@ def lib():
             raise ValueError(f"MR_AGG_INSERT_GRID={TUNABLES.agg_insert_grid}: must be >= 256")
         L.mr_wc3_set_dyn(1 if TUNABLES.map_dyn else 0)
         L.mr_agg_set_batch(1 if TUNABLES.agg_batch else 0)
+        L.mr_agg_set_phases(TUNABLES.agg_phases if TUNABLES.agg_phases in (1, 2, 4) else 1)
         if L.mr_rec_gather_set_rows(TUNABLES.rec_gather_rows) != 0:
             raise ValueError(f"MR_REC_GATHER_ROWS={TUNABLES.rec_gather_rows}: must be 128 or 256")
         _LIB = L

@@ -163,6 +163,57 @@ def dest32(k32: torch.Tensor, splitters: torch.Tensor) -> torch.Tensor:
     return torch.from_numpy(np.searchsorted(s, h, side="right").astype(np.int32))
 
 
+def bucket32(k32: torch.Tensor, sub: torch.Tensor, K: int, W: int):
+    """Exchange buckets of the record plane's range-pipelined exchange:
+    sub-range a = number of sub-splitters <= the 32-bit key prefix
+    (``sub``: R*K - 1 of them, R <= W), bucket (a % K) * W + a // K (round,
+    then destination).  Returns (bucket int32, ghist): GPU — ghist is the
+    int32 [2048] digit-histogram block of the buckets (digit 0 = rows per
+    bucket; K * W <= 256), ready for ``sort_keys32(bucket, ghist, bits=8)``;
+    CPU — ghist is None."""
+    n = k32.numel()
+    if k32.is_cuda and K * W <= 256 and sub.numel() <= 1023:
+        out = torch.empty(n, dtype=torch.int32, device=k32.device)
+        gh = torch.zeros(2048, dtype=torch.int32, device=k32.device)
+        sp = sub.to(device=k32.device, dtype=torch.int32).contiguous()
+        _hip.call("mr_rec_bucket32", _hip.ptr(k32), n, _hip.ptr(sp), sp.numel(), K, W, _hip.ptr(out), _hip.ptr(gh),
+                  _hip.stream(k32.device))
+        return out, gh
+    a = dest32(k32, sub) if sub.numel() else torch.zeros(n, dtype=torch.int32, device=k32.device)
+    return torch.remainder(a, K).mul_(W).add_(torch.div(a, K, rounding_mode="floor")), None
+
+
+def sample32(k32: torch.Tensor, k: int, seed: int) -> torch.Tensor:
+    """GPU: ``k`` 32-bit key prefixes (int64, unsigned values) of rows drawn
+    with replacement by a counter-based hash of ``seed`` (-1s when there are
+    no rows) — one launch."""
+    out = torch.empty(k, dtype=torch.int64, device=k32.device)
+    _hip.call("mr_rec_sample32", _hip.ptr(k32), k32.numel(), k, seed & 0xFFFFFFFFFFFFFFFF, _hip.ptr(out),
+              _hip.stream(k32.device))
+    return out
+
+
+def pick_splitters(srt: torch.Tensor, R: int) -> torch.Tensor:
+    """GPU: the R - 1 splitters (int32 bit patterns) at evenly spaced ranks of
+    the non-negative entries of the sorted int64 sample ``srt`` (zeros when
+    there are none) — one launch, no host round trip."""
+    sp = torch.empty(max(R - 1, 0), dtype=torch.int32, device=srt.device)
+    if R > 1:
+        _hip.call("mr_rec_pick", _hip.ptr(srt), srt.numel(), R, _hip.ptr(sp), _hip.stream(srt.device))
+    return sp
+
+
+def xchg_rows(gh: torch.Tensor, K: int, W: int, failed: int, err: torch.Tensor | None):
+    """GPU: the count-exchange rows [W][K+1] (int64: rows per round for each
+    destination from the bucket histogram ``gh``, then ``failed``) and an
+    int64[1] flag (the bucket sort's look-back gave up) — one launch."""
+    xchg = torch.empty((W, K + 1), dtype=torch.int64, device=gh.device)
+    flag = torch.empty(1, dtype=torch.int64, device=gh.device)
+    _hip.call("mr_rec_xchg", _hip.ptr(gh), K, W, int(failed), _hip.ptr(err) if err is not None else None,
+              _hip.ptr(xchg), _hip.ptr(flag), _hip.stream(gh.device))
+    return xchg, flag
+
+
 def unsorted_pairs(rec: torch.Tensor, kb: int) -> int:
     """Adjacent rows out of key order (0 for a sorted block)."""
     hi, lo = keys(rec, kb)

@@ -988,6 +988,13 @@ class RecordPlane:
         # the same sample size on every rank (all_gather), drawn with
         # replacement; a rank without rows contributes -1s, dropped below
         k = per or self.oversample * R
+        if host_rows is None and k32.is_cuda:
+            # no host round trip and four launches: rows drawn by a hash on the
+            # device, the -1s of empty ranks sort first and the picks skip them
+            from ..ops import records as RC
+            samp = RC.sample32(k32, k, self.seed * 7919 + eng.rank)
+            allv = D.all_gather_tensor(samp, eng.group) if D.initialized() else samp
+            return RC.pick_splitters(torch.sort(allv).values, R)
         g = torch.Generator().manual_seed(self.seed * 7919 + eng.rank)
         if host_rows is not None:
             samp = _host_sample32(host_rows, self.shape[1], k, g).to(eng.device)
@@ -998,7 +1005,7 @@ class RecordPlane:
         allv = D.all_gather_tensor(samp, eng.group) if D.initialized() else samp
         allv = allv[allv >= 0]
         if allv.numel() == 0:
-            allv = torch.zeros(1, dtype=torch.int64, device=k32.device)
+            allv = torch.zeros(1, dtype=torch.int64, device=allv.device)
         srt = torch.sort(allv).values  # non-negative: unsigned order
         m = srt.numel()
         pick = torch.tensor([(m * j) // R for j in range(1, R)], dtype=torch.int64, device=srt.device)
@@ -1142,44 +1149,70 @@ class RecordPlane:
         partition: monotone in the key).  Returns (rows of this rank in key
         order, failed maps of every rank)."""
         from ..ops import records as RC
+        from ..ops.primitives import sort_error_word, sort_keys32
         eng = self.eng
         W = eng.world
         dev = rec.device
         n, rb = int(rec.shape[0]), int(rec.shape[1])
         B = K * W
+        xchg = flag = None
         if n:
-            s = RC.dest32(k32, sub) if sub.numel() else torch.zeros(n, dtype=torch.int32, device=dev)
-            # sub-range s: partition (= destination) s // K, round s % K -> bucket round * W + destination
-            b = torch.remainder(s, K).mul_(W).add_(torch.div(s, K, rounding_mode="floor"))
-            perm = ops.sort_keys_checked([b.to(torch.int64)], bits=[max(8, _bits(B))])
+            # bucket = round * W + destination (RC.bucket32); rows stably by bucket
+            b, gh = RC.bucket32(k32, sub, K, W)
+            if gh is not None:  # one 8-bit u32 pass; the buckets' histogram is their row counts
+                perm = sort_keys32(b, gh, bits=8)[0]
+                # (the sort's look-back flag is read with the counts: no sync of its own)
+                xchg, flag = RC.xchg_rows(gh, K, W, failed, sort_error_word(dev))
+            else:
+                perm = ops.sort_keys_checked([b.to(torch.int64)], bits=[max(8, _bits(B))])
+                counts = ops.bincount(b, B)
             if perm.dtype != torch.int32:
                 perm = perm.to(torch.int32)
-            counts = ops.bincount(b, B)
         else:
             perm = torch.zeros(0, dtype=torch.int32, device=dev)
             counts = torch.zeros(B, dtype=torch.int64, device=dev)
-        # per destination: its rows of each round, then this rank's failed maps
-        xchg = torch.cat([counts.view(K, W).t().to(torch.int64),
-                          torch.full((W, 1), failed, dtype=torch.int64, device=counts.device)], 1).contiguous()
+        if xchg is None:
+            # per destination: its rows of each round, then this rank's failed maps
+            xchg = torch.cat([counts.view(K, W).t().to(torch.int64),
+                              torch.full((W, 1), failed, dtype=torch.int64, device=counts.device)], 1).contiguous()
+            flag = torch.zeros(1, dtype=torch.int64, device=xchg.device)
         recv = D.exchange_counts(xchg.view(-1), eng.group).view(W, K + 1)
-        both = torch.cat([xchg, recv]).cpu().numpy()
+        both = torch.cat([xchg.view(-1), recv.view(-1), flag]).cpu().numpy()
+        if both[-1]:  # the bucket sort's look-back gave up: its order is invalid (the counts are not)
+            perm = ops.sort_keys_checked([b.to(torch.int64)], bits=[8]).to(torch.int32)
+        both = both[:-1].reshape(2 * W, K + 1)
         failed = int(both[W:, K].sum())
         send, rcv = both[:W, :K], both[W:, :K]  # [destination][round], [source][round]
         recv_buf = torch.empty((int(rcv.sum()), rb), dtype=torch.uint8, device=dev)
         out = torch.empty_like(recv_buf)
+        # the send side (row gathers, each round's all-to-all queued behind its
+        # gather) runs on a stream of its own: the receive side's sort of round
+        # k does not wait behind the gathers of rounds > k on one stream
+        main = torch.cuda.current_stream(dev) if rec.is_cuda else None
+        side = None
+        if main is not None:
+            side = self._send_stream = getattr(self, "_send_stream", None) or torch.cuda.Stream(dev)
+            side.wait_stream(main)
         rounds, s0, r0 = [], 0, 0
-        for k in range(K):
-            ssz, rsz = [int(x) for x in send[:, k]], [int(x) for x in rcv[:, k]]
-            ms, mr = sum(ssz), sum(rsz)
-            buf = RC.gather(rec, perm[s0:s0 + ms]) if ms else torch.zeros((0, rb), dtype=torch.uint8, device=dev)
-            work = D.all_to_all_v_into(recv_buf[r0:r0 + mr], buf, ssz, rsz, eng.group, async_op=True)
-            rounds.append((work, buf, r0, mr))
-            s0 += ms
-            r0 += mr
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            for k in range(K):
+                ssz, rsz = [int(x) for x in send[:, k]], [int(x) for x in rcv[:, k]]
+                ms, mr = sum(ssz), sum(rsz)
+                buf = RC.gather(rec, perm[s0:s0 + ms]) if ms else torch.zeros((0, rb), dtype=torch.uint8,
+                                                                              device=dev)
+                work = D.all_to_all_v_into(recv_buf[r0:r0 + mr], buf, ssz, rsz, eng.group, async_op=True)
+                rounds.append((work, buf, r0, mr))
+                s0 += ms
+                r0 += mr
+        if side is not None:
+            for t in (rec, perm, recv_buf):  # read / written under the side stream
+                t.record_stream(side)
         bads = []
         for work, _buf, r0, mr in rounds:
             if work is not None:
                 work.wait()
+            elif side is not None:  # (a synchronous exchange, e.g. gloo: its copies ran on the side stream)
+                main.wait_stream(side)
             if not mr:
                 continue
             piece = recv_buf[r0:r0 + mr]
@@ -1194,6 +1227,8 @@ class RecordPlane:
                     piece = recv_buf[r0:r0 + mr]
                     p, _sk = RC.sort_full(piece, kb, pk)
                     RC.gather(piece, p, out=out[r0:r0 + mr])
+        if side is not None:
+            main.wait_stream(side)  # (the send buffers are released on the main stream's order)
         return out, failed
 
     def run_iteration(self, prefetch_next, lookahead):

@@ -112,6 +112,9 @@ class Tunables:
     agg_batch: bool = _knob("MR_AGG_BATCH", False,
                             "generic combine kernel: rows for the HBM table probe their home slots in batches of "
                             "four per thread (csrc/hip/hashtab.h gtab_find_or_claim_home) instead of one insert each")
+    agg_phases: int = _knob("MR_AGG_PHASES", 1,
+                            "generic combine kernel: a thread's 8 rows in 1, 2 or 4 phases (fewer row keys held in "
+                            "registers: 79 / 56 / fewer VGPRs, 6 / 7 / more waves per SIMD)")
     map_dyn: bool = _knob("MR_MAP_DYN", True,
                           "word-count map kernel: waves take the tile's token list 64 entries at a time from an "
                           "LDS counter (csrc/hip/wordcount3.hip DYN) instead of a fixed stride")

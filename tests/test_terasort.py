@@ -6,7 +6,9 @@ order-independent record checksum on CPU, over gloo (2 and 4 ranks, forced
 shuffle), on the GPU (HIP kernels vs the NumPy specification, forced RCCL
 shuffle) and through server/worker."""
 import os
+import queue
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -95,7 +97,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, on_gpu=False, backend="gloo", force_shuffle=False, chunks=None):
+def _worker(rank, world, port, q, on_gpu=False, backend="gloo", force_shuffle=False, chunks=None, sort_fail=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import dataclasses
@@ -116,6 +118,9 @@ def _worker(rank, world, port, q, on_gpu=False, backend="gloo", force_shuffle=Fa
     if force_shuffle:
         extra["force_shuffle"] = True
     eng = _engine(40001, device, blocks=max(world, 2), **extra)
+    if sort_fail:  # forced look-back give-ups in the next sorts (the bucket sort, then the rounds' sorts)
+        from lua_mapreduce_1_amd import ops
+        ops.debug_sort_fail(sort_fail)
     eng.run()
     if rank == 0:
         q.put(_validation())
@@ -130,7 +135,14 @@ def _run(world, **kw):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q), kwargs=kw) for r in range(world)]
     for p in procs:
         p.start()
-    v = q.get(timeout=300)
+    t_end = time.time() + 300
+    while True:  # a rank that dies fails the test at once (not after the queue's timeout)
+        try:
+            v = q.get(timeout=2)
+            break
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead and time.time() < t_end, f"rank exit codes {[p.exitcode for p in procs]}"
     for p in procs:
         p.join(120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
@@ -157,7 +169,7 @@ def test_gather_into_row_slices_cpu():
     from lua_mapreduce_1_amd.ops import records as RC
     rec = TS.generate(1000, 5, 99)
     out = torch.zeros((1010, 100), dtype=torch.uint8)
-    perm = torch.randperm(1000)[:700]
+    perm = torch.randperm(997)[:700]
     RC.gather(rec[3:], perm, out=out[7:707])
     assert torch.equal(out[7:707], rec[3:][perm])
     with pytest.raises(ValueError):
@@ -282,6 +294,58 @@ def test_gpu_gather_row_slices(gpu, rb):
         host = out.cpu()
         assert torch.equal(host[o0:o0 + n], base[i0:][perm.long()]), (rb, i0, o0, n)
         assert bool((host[:o0] == 0xA5).all()) and bool((host[o0 + n:] == 0xA5).all()), "wrote outside the slice"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,K,W", [(8, 4, 8), (3, 8, 4), (1, 5, 2), (8, 32, 8)])
+def test_gpu_exchange_buckets(gpu, R, K, W):
+    """The fused exchange-bucket kernel against the CPU specification, and its
+    histogram against the bucket counts."""
+    from lua_mapreduce_1_amd.ops import records as RC
+    g = torch.Generator().manual_seed(R * 100 + K)
+    k32 = torch.randint(-2**31, 2**31 - 1, (300_001,), dtype=torch.int32, generator=g)
+    sub = torch.sort(torch.randint(0, 2**32 - 1, (R * K - 1,), dtype=torch.int64, generator=g)).values
+    sub = sub.to(torch.int32)  # unsigned bit patterns
+    want, _ = RC.bucket32(k32, sub, K, W)
+    got, gh = RC.bucket32(k32.to(gpu), sub.to(gpu), K, W)
+    assert gh is not None and torch.equal(got.cpu(), want)
+    assert torch.equal(gh[:256].cpu().long(), torch.bincount(want.long(), minlength=256))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fails", [1, 2])
+def test_gpu_exchange_rounds_sort_giveups(gpu, fails):
+    """A given-up look-back in the exchange's bucket sort is caught (its flag
+    rides on the counts download) and the rows re-sorted by the checked sort
+    (2: whose first try gives up too): the output stays sorted and complete.
+    (Give-ups that do not stop raise — sort_keys_checked's retry limit.)"""
+    _run(1, on_gpu=True, force_shuffle=True, sort_fail=fails)
+
+
+@pytest.mark.gpu
+def test_gpu_sampling_and_count_rows(gpu):
+    """The record plane's native sampling, splitter picks (empty ranks' -1s
+    skipped) and count-exchange rows against plain torch."""
+    from lua_mapreduce_1_amd.ops import records as RC
+    g = torch.Generator().manual_seed(5)
+    k32 = torch.randint(-2**31, 2**31 - 1, (100_003,), dtype=torch.int32, generator=g).to(gpu)
+    s = RC.sample32(k32, 4096, 77)
+    assert s.shape == (4096,) and bool((s >= 0).all()) and bool((s < 2**32).all())
+    assert bool(torch.isin(s, k32.long() & 0xFFFFFFFF).all())
+    assert torch.equal(RC.sample32(k32[:0], 5, 1).cpu(), torch.full((5,), -1))
+    allv = torch.cat([torch.full((3000,), -1, device=gpu), s])
+    srt = torch.sort(allv).values
+    for R in (1, 2, 8, 33):
+        want = s.sort().values[[(4096 * j) // R for j in range(1, R)]].to(torch.int32)
+        assert torch.equal(RC.pick_splitters(srt, R).cpu(), want.cpu())
+    assert torch.equal(RC.pick_splitters(torch.full((10,), -1, device=gpu), 4).cpu(), torch.zeros(3, dtype=torch.int32))
+    gh = torch.randint(0, 1000, (2048,), dtype=torch.int32, generator=g).to(gpu)
+    K, W = 4, 8
+    xchg, flag = RC.xchg_rows(gh, K, W, 3, None)
+    want = torch.cat([gh[:K * W].view(K, W).t().long().cpu(), torch.full((W, 1), 3)], 1)
+    assert torch.equal(xchg.cpu(), want) and int(flag) == 0
+    _, flag = RC.xchg_rows(gh, K, W, 0, torch.ones(1, dtype=torch.int32, device=gpu))
+    assert int(flag) == 1
 
 
 @pytest.mark.gpu

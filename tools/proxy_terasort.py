@@ -7,9 +7,10 @@ partition, exchange, receive-side sort and gather.  The collectives are a
 model: what peer p sends rank 0 is computed before timing from peer p's own
 TeraGen block (its rows of rank 0's range, in the order the exchange being
 measured sends them: distinct keys, the real receive-side work), copied in
-on an exchange stream that then holds for bytes / ``--xgmi-gbs`` (the
-all-to-all's link time, which the copy itself does not model), so an
-asynchronous exchange overlaps the compute stream as RCCL's would.
+on a copy stream beside an exchange stream that holds for bytes /
+``--xgmi-gbs`` (the all-to-all's link time; the exchange ends when both are
+done, and the next one starts after it), so an asynchronous exchange overlaps
+the compute stream as RCCL's would.
 
 Both W>1 exchanges of the record plane, selected by MR_REC_CHUNKS: K >= 1
 (round 6) = the exchange pipelined by key range (K rounds, each round's
@@ -80,30 +81,53 @@ def main() -> int:
         if ms > 0:
             torch.cuda._sleep(int(ms * cycles_per_ms))
 
+    peer_counts = []  # device [W-1][rounds]: filled with peers
+
     def exchange_counts(counts, group=None):
         c = counts.view(W, -1).clone()  # [source][rounds..., failed maps]
-        for p in range(1, W):
-            if peers:
-                c[p, :-1] = torch.tensor([r.shape[0] for r in peers[p - 1]], dtype=c.dtype)
-            else:  # (the run that finds the splitters: peers send what rank 0 sends itself)
-                c[p, :-1] = c[0, :-1]
-            c[p, -1] = c[0, -1]
+        if peer_counts:
+            c[1:, :-1] = peer_counts[0]
+        else:  # (the run that finds the splitters: peers send what rank 0 sends itself)
+            c[1:, :-1] = c[0, :-1]
+        c[1:, -1] = c[0, -1]
         return c.reshape(-1)
 
+    cats = []  # [round] -> peers 1..W-1's rows of that round, concatenated (filled with peers)
+
     def fill(out, payload, own, k):
-        """out <- [this rank's own rows of round k | peer 1's | ...]"""
+        """out <- [this rank's own rows of round k | peer 1's | ...] (two copies)"""
         out[:own].copy_(payload[:own])
-        o = own
-        for p in range(1, W):
-            src = peers[p - 1][k] if peers else payload[:0]
-            m = min(src.shape[0], out.shape[0] - o)
-            out[o:o + m].copy_(src[:m])
-            o += m
+        if cats:
+            m = min(cats[k].shape[0], out.shape[0] - own)
+            out[own:own + m].copy_(cats[k][:m])
+
+    xc = torch.cuda.Stream(device)  # the model's copy of the transfer's bytes (beside the link hold)
+
+    def exchange(out, payload, send, k):
+        """One all-to-all on the model's streams: the copy (xc) and the link
+        hold (xs) run side by side — the transfer takes the longer of the two
+        — and after the previous exchange (one all-to-all at a time, as on
+        RCCL's stream).  Returns its completion event."""
+        cur = torch.cuda.current_stream()
+        xs.wait_stream(cur)
+        xc.wait_stream(cur)
+        xc.wait_stream(xs)
+        with torch.cuda.stream(xc):
+            fill(out, payload, send[0], k)
+            evc = torch.cuda.Event()
+            evc.record(xc)
+        with torch.cuda.stream(xs):
+            link_hold((sum(send) - send[0]) * payload.shape[1])
+            xs.wait_event(evc)
+            ev = torch.cuda.Event()
+            ev.record(xs)
+        payload.record_stream(xc)
+        out.record_stream(xc)
+        return ev
 
     def all_to_all_v(payload, send, recv, group=None):
         out = torch.empty((sum(recv),) + tuple(payload.shape[1:]), dtype=payload.dtype, device=payload.device)
-        fill(out, payload, send[0], 0)
-        link_hold((sum(send) - send[0]) * payload.shape[1])
+        torch.cuda.current_stream().wait_event(exchange(out, payload, send, 0))
         return out
 
     class _Work:
@@ -118,15 +142,7 @@ def main() -> int:
     def all_to_all_v_into(out, payload, send, recv, group=None, async_op=False):
         k = rnd[0] % max(K, 1)
         rnd[0] += 1
-        xs.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(xs):
-            fill(out, payload, send[0], k)
-            link_hold((sum(send) - send[0]) * payload.shape[1])
-            ev = torch.cuda.Event()
-            ev.record(xs)
-        payload.record_stream(xs)
-        out.record_stream(xs)
-        return _Work(ev)
+        return _Work(exchange(out, payload, send, k))
 
     def all_gather_tensor(t, group=None):
         return t.repeat((W,) + (1,) * (t.dim() - 1))
@@ -155,6 +171,8 @@ def main() -> int:
         else:
             peers.append([blk[RC.dest32(k32, sp).to(torch.int64) == 0]])
         del blk, k32
+    cats.extend(torch.cat([pr[k] for pr in peers]) for k in range(len(peers[0])))
+    peer_counts.append(torch.tensor([[r.shape[0] for r in pr] for pr in peers], dtype=torch.int64, device=device))
     for _ in range(a.warmup):
         rnd[0] = 0
         res = eng.run_iteration()
