@@ -104,7 +104,7 @@ class Tunables:
                                "API, csrc/hip/sdma.hip) after the tail's kernels, not as a runtime blit kernel on "
                                "the CUs beside the next map (0 = never)")
     spin_us: float = _knob("MR_SPIN_US", 2000.0, "host spin on completion words before hipStreamSynchronize, us")
-    rec_chunks: int = _knob("MR_REC_CHUNKS", 4,
+    rec_chunks: int = _knob("MR_REC_CHUNKS", 3,
                             "record plane at W > 1 (R <= W partitions, sampled splitters): rounds of the exchange "
                             "pipelined by key range — every destination's range cut in this many sub-ranges, round "
                             "k's all-to-all overlapping the receive-side sort of round k-1 (0: one exchange, then "
