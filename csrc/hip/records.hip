@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(256) rec_gather_kernel(const u32* __restrict__
 // (rec_gather_kernel) issues 4x the vector-memory instructions for the same
 // bytes; the windowed-permutation probe (profiles/r3/check1/ts_move.log: 8 MB
 // windows no faster than random rows) says instructions, not DRAM, bound it.
-template <int C, int R, bool PIPE>
+template <int C, int R, bool PIPE, bool HEAD>
 __global__ void __launch_bounds__(256) rec_gather16_kernel(const u8* __restrict__ in, u64 nin,
                                                            const u32* __restrict__ perm, u64 n, u32 rb,
                                                            u8* __restrict__ out, u32 ih, u32 oh) {
@@ -287,6 +287,9 @@ __global__ void __launch_bounds__(256) rec_gather16_kernel(const u8* __restrict_
   __shared__ u32 mis[R];
   constexpr int PER = (R * C + 255) / 256;
   const u32 t = threadIdx.x;
+  // HEAD: a buffer starts ih / oh bytes past a 16-byte boundary (row slices);
+  // the aligned instantiation keeps round 5's store loop
+  if constexpr (!HEAD) ih = oh = 0;
   const u64 in_bytes = nin * (u64)rb + ih;
   const u64 nbatch = (n + R - 1) / R;
   const float inv_rb = 1.0f / (float)rb;
@@ -332,37 +335,68 @@ __global__ void __launch_bounds__(256) rec_gather16_kernel(const u8* __restrict_
     }
     __syncthreads();
     if (PIPE && b + gridDim.x < nbatch) load(b + gridDim.x);
-    const u32 obytes = rows * rb;  // < 2^16 for R <= 256, rb <= 244
-    // the batch's bytes sit oh bytes into aligned 16-byte chunks (R * rb is a
-    // multiple of 16): chunks wholly inside them are dwordx4 stores, the
-    // first (oh != 0) and the last partial chunk dword stores
-    u8* ob = out + r0 * rb;
-    const u32 nch = (obytes + oh + 15) >> 4;
-    for (u32 oc = t; oc < nch; oc += 256) {
-      const int b0 = (int)(oc * 16u) - (int)oh;  // batch byte of the chunk's word 0 (< 0: before the batch)
-      const u32 s0 = b0 < 0 ? 0u : (u32)b0;
-      u32 row = (u32)((float)s0 * inv_rb);  // exact after the corrections (s0 < 2^24)
-      if (row * rb > s0) --row;
-      if ((row + 1) * rb <= s0) ++row;
-      const u32 off = s0 - row * rb;
-      u32 w[4];
+    if constexpr (!HEAD) {
+      const u32 obytes = rows * rb;  // < 2^16 for R <= 256, rb <= 244
+      u8* ob = out + r0 * rb;
+      const u32 nch = obytes >> 4;
+      for (u32 oc = t; oc < nch + 1; oc += 256) {
+        const u32 byte0 = oc * 16u;
+        if (byte0 >= obytes) break;
+        u32 row = (u32)((float)byte0 * inv_rb);  // exact after the corrections (byte0 < 2^24)
+        if (row * rb > byte0) --row;
+        if ((row + 1) * rb <= byte0) ++row;
+        const u32 off = byte0 - row * rb;
+        u32 w[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int lb = b0 + 4 * j;
-        u32 rr = row, oo = off + (u32)(lb - (int)s0);
-        if (oo >= rb) {
-          ++rr;
-          oo -= rb;
+        for (int j = 0; j < 4; ++j) {
+          u32 rr = row, oo = off + 4u * j;
+          if (oo >= rb) {
+            ++rr;
+            oo -= rb;
+          }
+          w[j] = rr < rows ? img32[(rr * (u32)C * 16u + mis[rr] + oo) >> 2] : 0u;
         }
-        w[j] = lb >= 0 && rr < rows ? img32[(rr * (u32)C * 16u + mis[rr] + oo) >> 2] : 0u;
+        if (oc < nch) {
+          __builtin_nontemporal_store(v4u{w[0], w[1], w[2], w[3]}, reinterpret_cast<v4u*>(ob + byte0));
+        } else {  // the batch's last partial chunk (rows * rb % 16 != 0): dwords
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (byte0 + 4u * j < obytes) *reinterpret_cast<u32*>(ob + byte0 + 4u * j) = w[j];
+        }
       }
-      if (b0 >= 0 && (u32)b0 + 16u <= obytes) {
-        __builtin_nontemporal_store(v4u{w[0], w[1], w[2], w[3]}, reinterpret_cast<v4u*>(ob + oc * 16u));
-      } else {
+    } else {
+      const u32 obytes = rows * rb;  // < 2^16 for R <= 256, rb <= 244
+      // the batch's bytes sit oh bytes into aligned 16-byte chunks (R * rb is a
+      // multiple of 16): chunks wholly inside them are dwordx4 stores, the
+      // first (oh != 0) and the last partial chunk dword stores
+      u8* ob = out + r0 * rb;
+      const u32 nch = (obytes + oh + 15) >> 4;
+      for (u32 oc = t; oc < nch; oc += 256) {
+        const int b0 = (int)(oc * 16u) - (int)oh;  // batch byte of the chunk's word 0 (< 0: before the batch)
+        const u32 s0 = b0 < 0 ? 0u : (u32)b0;
+        u32 row = (u32)((float)s0 * inv_rb);  // exact after the corrections (s0 < 2^24)
+        if (row * rb > s0) --row;
+        if ((row + 1) * rb <= s0) ++row;
+        const u32 off = s0 - row * rb;
+        u32 w[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int lb = b0 + 4 * j;
-          if (lb >= 0 && (u32)lb < obytes) *reinterpret_cast<u32*>(ob + oc * 16u + 4u * j) = w[j];
+          u32 rr = row, oo = off + (u32)(lb - (int)s0);
+          if (oo >= rb) {
+            ++rr;
+            oo -= rb;
+          }
+          w[j] = lb >= 0 && rr < rows ? img32[(rr * (u32)C * 16u + mis[rr] + oo) >> 2] : 0u;
+        }
+        if (b0 >= 0 && (u32)b0 + 16u <= obytes) {
+          __builtin_nontemporal_store(v4u{w[0], w[1], w[2], w[3]}, reinterpret_cast<v4u*>(ob + oc * 16u));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int lb = b0 + 4 * j;
+            if (lb >= 0 && (u32)lb < obytes) *reinterpret_cast<u32*>(ob + oc * 16u + 4u * j) = w[j];
+          }
         }
       }
     }
@@ -490,8 +524,12 @@ static void launch_gather16_t(const void* in, u64 nin, const void* perm, u64 n, 
   const u64 nb = (n + R - 1) / R;
   const unsigned g = (unsigned)(nb < 65536 ? nb : 65536);
   const u32 ih = (u32)((uintptr_t)in & 15), oh = (u32)((uintptr_t)out & 15);
-  hipLaunchKernelGGL((rc::rec_gather16_kernel<C, R, PIPE>), dim3(g), dim3(256), 0, s, (const u8*)in - ih, nin,
-                     (const u32*)perm, n, (u32)rb, (u8*)out - oh, ih, oh);
+  if (ih | oh)
+    hipLaunchKernelGGL((rc::rec_gather16_kernel<C, R, PIPE, true>), dim3(g), dim3(256), 0, s, (const u8*)in - ih,
+                       nin, (const u32*)perm, n, (u32)rb, (u8*)out - oh, ih, oh);
+  else
+    hipLaunchKernelGGL((rc::rec_gather16_kernel<C, R, PIPE, false>), dim3(g), dim3(256), 0, s, (const u8*)in, nin,
+                       (const u32*)perm, n, (u32)rb, (u8*)out, 0u, 0u);
 }
 
 static bool g_gather_pipe = true;  // mr_rec_gather mode 2 forces the unpipelined form (A/B)
