@@ -325,8 +325,54 @@ __device__ __forceinline__ u64 pack7(u64 w, u32& top) {
   return r;
 }
 
+// Alphabet-adaptive exact sort words (ops.exact_key_perm): the 16 7-bit key
+// bytes of k7 (key_meta's words) re-coded through `code` (a byte's rank among
+// the byte values present, zero padding -> 0) as `bits`-bit digits, most
+// significant first, after the partition's `pbits` bits: word 0 = partition |
+// codes of bytes 0..c0-1 (c0 = (64 - pbits) / bits, left-aligned), word 1 =
+// the codes of the rest (right-aligned).  The same order as k7 — codes keep
+// the byte order — in fewer radix passes: 5-bit codes with a 4-bit partition
+// are 8 + 3 passes instead of 8 + 7.
+__global__ void pack_alpha_kernel(const u64* __restrict__ k7, u64 n, const u8* __restrict__ code, u32 bits, u32 pbits,
+                                  u64* __restrict__ out) {
+  __shared__ u8 cd[128];
+  if (threadIdx.x < 128) cd[threadIdx.x] = code[threadIdx.x];
+  __syncthreads();
+  const u32 c0 = min((64u - pbits) / bits, 16u);
+  const u32 used = pbits + c0 * bits;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 a = k7[i], b = k7[n + i];
+    u64 w0 = pbits ? (a >> 56) : 0ull, w1 = 0;
+#pragma unroll
+    for (u32 j = 0; j < 16; ++j) {
+      const u32 ch = (u32)((j < 8 ? a : b) >> (49 - 7 * (j & 7))) & 0x7Fu;
+      const u64 c = cd[ch];
+      if (j < c0) w0 = (w0 << bits) | c;
+      else w1 = (w1 << bits) | c;
+    }
+    out[i] = used < 64 ? w0 << (64 - used) : w0;
+    out[n + i] = w1;
+  }
+}
+
+// The 7-bit byte values of a key word's 8 bytes marked present in an LDS
+// byte table (plain stores: every writer writes 1; a presence mask kept in
+// registers cost ~0.2 ms of VALU per 23 M keys).
+__device__ __forceinline__ void alpha_mark(u64 w, volatile u8* seen) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) seen[(u32)(w >> (8 * j)) & 0x7Fu] = 1;
+}
+
+// alpha (optional, with out_k7): the byte values present in the keys' first
+// 16 bytes (zero padding included) as a 128-bit mask, for the
+// alphabet-adaptive sort words (mr_pack_alpha)
 __global__ void key_meta_kernel(const u64* hi, const u64* lo, const u64* rep, u64 n, const u8* src, u32 nparts,
-                                u32* out_part, long long* out_len, u64* out_w1, u64* out_k7, u32* k7_bad) {
+                                u32* out_part, long long* out_len, u64* out_w1, u64* out_k7, u32* k7_bad,
+                                u32* alpha) {
+  __shared__ u8 seen[128];
+  if (alpha && threadIdx.x < 128) seen[threadIdx.x] = 0;
+  if (alpha) __syncthreads();
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const u64 h = hi[i], l = lo[i];
@@ -363,6 +409,24 @@ __global__ void key_meta_kernel(const u64* hi, const u64* lo, const u64* rep, u6
       out_k7[i] = ((u64)(nparts ? f % nparts : f) << 56) | a;
       out_k7[n + i] = b;
       if (top & 0x80u) atomicOr(k7_bad, 1u);
+      if (alpha) {
+        alpha_mark(h, seen);
+        alpha_mark(w1, seen);
+      }
+    }
+  }
+  if (alpha) {  // (uniform: every thread reaches this point)
+    __syncthreads();
+    // the block's table as a 128-bit mask (two waves, a ballot each); one
+    // memory-side OR per word only for bits not yet seen (after the first
+    // few blocks the mask is complete: no atomics)
+    if (threadIdx.x < 128) {
+      const unsigned long long m = __ballot(seen[threadIdx.x] != 0);
+      const int lane = threadIdx.x & 63, q = (threadIdx.x >> 6) * 2 + (lane >> 5);
+      if ((lane & 31) == 0) {
+        const u32 v = (u32)(m >> (lane & 32));
+        if (v & ~__hip_atomic_load(&alpha[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicOr(&alpha[q], v);
+      }
     }
   }
 }
@@ -641,15 +705,26 @@ int mr_key_word(const void* hi, const void* lo, const void* rep, const void* src
 }
 
 int mr_key_meta(const void* hi, const void* lo, const void* rep, u64 n, const void* src, u32 nparts, void* out_part,
-                void* out_len, void* out_w1, void* out_k7, void* k7_bad, hipStream_t stream) {
+                void* out_len, void* out_w1, void* out_k7, void* k7_bad, void* alpha, hipStream_t stream) {
   if (n == 0) return 0;
   if (out_k7 && (!out_w1 || !out_part || !k7_bad || nparts == 0 || nparts > 256)) return -1;
+  if (alpha && !out_k7) return -1;
   // one key per thread (no grid cap): a thread's keys are latency chains of
   // random key-byte loads, and a capped grid ran ~11 of them in series
   hipLaunchKernelGGL(key_meta_kernel, dim3(grid_for(n, 256, 1 << 20)), dim3(256), 0, stream, (const u64*)hi,
                      (const u64*)lo,
                      (const u64*)rep, n, (const u8*)src, nparts, (u32*)out_part, (long long*)out_len,
-                     (u64*)out_w1, (u64*)out_k7, (u32*)k7_bad);
+                     (u64*)out_w1, (u64*)out_k7, (u32*)k7_bad, (u32*)alpha);
+  return (int)hipGetLastError();
+}
+
+// code: u8 [128]; out: u64 [2 x n]; 1 <= bits <= 7, pbits <= 8, the rest's
+// (16 - c0) * bits <= 64
+int mr_pack_alpha(const void* k7, u64 n, const void* code, u32 bits, u32 pbits, void* out, hipStream_t stream) {
+  if (n == 0) return 0;
+  if (bits < 1 || bits > 7 || pbits > 8) return -1;
+  hipLaunchKernelGGL(pack_alpha_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u64*)k7, n,
+                     (const u8*)code, bits, pbits, (u64*)out);
   return (int)hipGetLastError();
 }
 

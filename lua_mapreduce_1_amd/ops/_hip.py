@@ -42,7 +42,8 @@ _SIGS = {
     "mr_rec_gather_set_rows": [_i32],
     "mr_csv_fold": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _u64, _u64, _p, _p, _p, _p],
     "mr_key_word": [_p, _p, _p, _p, _u64, _u32, _p, _p],
-    "mr_key_meta": [_p, _p, _p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p],
+    "mr_key_meta": [_p, _p, _p, _u64, _p, _u32, _p, _p, _p, _p, _p, _p, _p],
+    "mr_pack_alpha": [_p, _u64, _p, _u32, _u32, _p, _p],
     "mr_gather_key_bytes": [_p, _p, _p, _p, _u64, _p, _p, _u64, _p],
     "mr_exclusive_scan_u32": [_p, _p, _u64, _p, _p, _p],
     "mr_exclusive_scan_i64": [_p, _p, _u64, _p, _p, _p],

@@ -427,15 +427,17 @@ def key_meta(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.T
         part = torch.empty(n, dtype=torch.int32, device=d) if want_part else None
         ln = torch.empty(n, dtype=torch.int64, device=d) if want_len else None
         w1 = torch.empty(n, dtype=torch.int64, device=d) if (want_w1 and want_part) else None
-        k7 = bad = None
+        k7 = bad = alpha = None
         if want_k7 and w1 is not None and 1 <= nparts <= 256:
             k7 = torch.empty((2, n), dtype=torch.int64, device=d)
             bad = torch.zeros(1, dtype=torch.int32, device=d)
+            if TUNABLES.exact_alpha:
+                alpha = torch.zeros(4, dtype=torch.int32, device=d)
         srcp = _hip.ptr(src) if src is not None else None
         _hip.call("mr_key_meta", _hip.ptr(hi), _hip.ptr(lo), _hip.ptr(rep), n, srcp, nparts, _hip.ptr(part),
-                  _hip.ptr(ln), _hip.ptr(w1), _hip.ptr(k7), _hip.ptr(bad), _hip.stream(d))
+                  _hip.ptr(ln), _hip.ptr(w1), _hip.ptr(k7), _hip.ptr(bad), _hip.ptr(alpha), _hip.stream(d))
         if want_k7:
-            return part, ln, w1, (None if k7 is None else (k7, bad))
+            return part, ln, w1, (None if k7 is None else (k7, bad, alpha))
         return (part, ln, w1) if want_w1 else (part, ln)
     b = key_bytes_list(hi, lo, rep, src)
     part = None
@@ -855,6 +857,32 @@ def key_word(hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor, src: torch.T
     return torch.from_numpy(out.view(np.int64))
 
 
+def _alpha_words(k7, alpha: list, nparts: int):
+    """The exact sort's words re-coded to the byte values present
+    (csrc/hip/keyops.hip pack_alpha_kernel) when that takes fewer radix passes
+    than the 7-bit words' 15: ([word0, word1], bits, partition bits), or
+    (None, None, 8).  Codes keep the byte order (zero padding -> 0), so the
+    sorted order is the same."""
+    present = [b for b in range(1, 128) if alpha[b >> 5] >> (b & 31) & 1]
+    cbits = max(1, len(present).bit_length())
+    pb = int(max(nparts, 1) - 1).bit_length()
+    if cbits >= 7 or pb > 8:
+        return None, None, 8
+    c0 = min((64 - pb) // cbits, 16)
+    rest = (16 - c0) * cbits
+    passes = 8 + (rest + 7) // 8
+    if passes >= 15 or rest > 64:
+        return None, None, 8
+    code = np.zeros(128, np.uint8)
+    code[present] = np.arange(1, len(present) + 1, dtype=np.uint8)
+    d = k7[0].device
+    out = torch.empty((2, k7[0].shape[1]), dtype=torch.int64, device=d)
+    _hip.call("mr_pack_alpha", _hip.ptr(k7[0]), k7[0].shape[1], _hip.ptr(torch.from_numpy(code).to(d)), cbits, pb,
+              _hip.ptr(out), _hip.stream(d))
+    words, bits = ([out[0], out[1]], [64, rest]) if rest else ([out[0]], [64])
+    return words, bits, pb
+
+
 def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor,
                    src: torch.Tensor | None, nparts: int, klen: torch.Tensor | None = None,
                    with_part: bool = False, with_counts: bool = False, w1: torch.Tensor | None = None,
@@ -897,8 +925,13 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     if klen is None:
         _, klen = key_meta(hi, lo, rep, src, want_part=False)
     klen = klen.to(torch.int64)
-    if k7 is not None:  # the longest key and the 7-bit flag in one read
-        max_len, k7_bad = (int(x) for x in host_read(torch.stack([klen.max(), k7[1][0].to(torch.int64)])))
+    alpha = None
+    if k7 is not None:  # the longest key, the 7-bit flag and the byte alphabet in one read
+        extra = [k7[2].to(torch.int64)] if len(k7) > 2 and k7[2] is not None else []
+        got = host_read(torch.cat([torch.stack([klen.max(), k7[1][0].to(torch.int64)])] + extra))
+        max_len, k7_bad = int(got[0]), int(got[1])
+        if extra:
+            alpha = [int(x) & 0xFFFFFFFF for x in got[2:6]]
     else:
         max_len, k7_bad = int(klen.max()), 1
     if (max_len + 7) // 8 > EXACT_MAX_WORDS:
@@ -930,11 +963,15 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
         if max_len <= 16:
             return done(p32.long())
     elif not k7_bad and pbits == 8:
-        # 7-bit keys: (partition, bytes 0-15) as two words of 64 and 56 bits
-        p32, sk = sort_keys_checked([k7[0][0], k7[0][1]], bits=[64, 56], return_keys=True)
-        spart = (sk >> 56) & 0xFF
-        if with_counts:  # the top digit's histogram of the last word sorted
-            counts = _SORT_WS[d]["small"][7 * 256:7 * 256 + max(nparts, 1)].to(torch.int64)
+        words, bits, pb = _alpha_words(k7, alpha, nparts) if alpha is not None else (None, None, 8)
+        if words is None:
+            # 7-bit keys: (partition, bytes 0-15) as two words of 64 and 56 bits
+            words, bits = [k7[0][0], k7[0][1]], [64, 56]
+        p32, sk = sort_keys_checked(words, bits=bits, return_keys=True)
+        spart = ((sk >> (64 - pb)) & ((1 << pb) - 1)) if pb else torch.zeros_like(sk)
+        if with_counts:  # the top digit's histogram of the last word sorted: partitions in its top pb bits
+            top = _SORT_WS[d]["small"][7 * 256:8 * 256].to(torch.int64)
+            counts = top.view(1 << pb, 1 << (8 - pb)).sum(1)[:max(nparts, 1)] if pb else top.sum().view(1)
     else:
         p32, spart = sort_cols(cols[:3], [pbits, 64, 64])
     if hi.is_cuda:

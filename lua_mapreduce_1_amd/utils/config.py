@@ -109,6 +109,9 @@ class Tunables:
                             "pipelined by key range — every destination's range cut in this many sub-ranges, round "
                             "k's all-to-all overlapping the receive-side sort of round k-1 (0: one exchange, then "
                             "one sort of everything received)")
+    exact_alpha: bool = _knob("MR_EXACT_ALPHA", True,
+                              "exact key order of 7-bit keys: sort words re-coded to the byte values present "
+                              "(5-bit digits for 17-31 values, 6-bit for 32-63: 11-13 radix passes instead of 15)")
     agg_batch: bool = _knob("MR_AGG_BATCH", False,
                             "generic combine kernel: rows for the HBM table probe their home slots in batches of "
                             "four per thread (csrc/hip/hashtab.h gtab_find_or_claim_home) instead of one insert each")

@@ -184,3 +184,23 @@ def test_exact_key_perm_8bit_keys_fall_back_gpu(gpu):
     sort takes the byte-word columns."""
     keys = _short_runs(9, 5_000) + [b"\xff" * 20]
     _check_k7(list(dict.fromkeys(keys)), 10, gpu, False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alphabet", [b"ab", b"abcdefghijklmnopqrstuvwxyz ", b"0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ"
+                                      b"abcdefghijklmnopqrstuvwxyz .", bytes(range(32, 127))],
+                         ids=["2", "27", "64", "95"])
+@pytest.mark.parametrize("nparts", [1, 15, 256])
+def test_exact_key_perm_alphabet_words_gpu(gpu, alphabet, nparts):
+    """The sort words re-coded to the byte values present (1-6 bit digits:
+    fewer radix passes than the 7-bit words; 7 bits: the 7-bit words), over
+    keys of 1-40 bytes with shared prefixes and NUL-padded twins."""
+    rng = random.Random(len(alphabet) * 1000 + nparts)
+    stems = [bytes(rng.choice(alphabet) for _ in range(rng.randrange(1, 30))) for _ in range(50)]
+    keys = set()
+    while len(keys) < 40_000:
+        k = rng.choice(stems)[:rng.randrange(1, 30)] + bytes(rng.choice(alphabet) for _ in range(rng.randrange(0, 12)))
+        keys.add(k)
+        if rng.random() < 0.03:
+            keys.add(k[:rng.randrange(1, 15)] + b"\x00" * rng.randrange(1, 3))
+    _check_k7(sorted(keys, key=lambda _: rng.random()), nparts, gpu, True)
