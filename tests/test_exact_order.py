@@ -187,13 +187,15 @@ def test_exact_key_perm_8bit_keys_fall_back_gpu(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("alphabet", [b"ab", b"abcdefghijklmnopqrstuvwxyz ", b"0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ"
-                                      b"abcdefghijklmnopqrstuvwxyz .", bytes(range(32, 127))],
-                         ids=["2", "27", "64", "95"])
+@pytest.mark.parametrize("alphabet", [b"ab", b"abcdefghijklmnopqrstuvwxyz ", b"0123456789abcdefghijklmnopqrstuvwxyz .",
+                                      b"0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz .",
+                                      bytes(range(32, 127))],
+                         ids=["2", "27", "38", "64", "95"])
 @pytest.mark.parametrize("nparts", [1, 15, 256])
 def test_exact_key_perm_alphabet_words_gpu(gpu, alphabet, nparts):
-    """The sort words re-coded to the byte values present (1-6 bit digits:
-    fewer radix passes than the 7-bit words; 7 bits: the 7-bit words), over
+    """The sort words re-coded to the byte values present (2-, 5- and 6-bit
+    digits: fewer radix passes than the 7-bit words; 64 or more values: the
+    7-bit words), over
     keys of 1-40 bytes with shared prefixes and NUL-padded twins."""
     rng = random.Random(len(alphabet) * 1000 + nparts)
     stems = [bytes(rng.choice(alphabet) for _ in range(rng.randrange(1, 30))) for _ in range(50)]
