@@ -939,8 +939,14 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     pbits = max(8, int(max(nparts, 1) - 1).bit_length())
     if w1 is None:
         w1 = key_word(hi, lo, rep, src, 1)
-    lc = klen.clamp(max=16)
-    cols = [part.to(torch.int64), hi, w1, lc]
+    cols_ = []
+
+    def cols():
+        # (partition, hi, w1, min(len, 16)): built when a path sorts by them
+        # (the 7-bit / alphabet words need none of the four conversions)
+        if not cols_:
+            cols_.extend([part.to(torch.int64), hi, w1, klen.clamp(max=16)])
+        return cols_
     counts = None
 
     def sort_cols(cs, bits):
@@ -959,7 +965,7 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
         return out
 
     if max_len <= 16 or not hi.is_cuda:
-        p32, spart = sort_cols(cols, [pbits, 64, 64, 8])
+        p32, spart = sort_cols(cols(), [pbits, 64, 64, 8])
         if max_len <= 16:
             return done(p32.long())
     elif not k7_bad and pbits == 8:
@@ -973,7 +979,7 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
             top = _SORT_WS[d]["small"][7 * 256:8 * 256].to(torch.int64)
             counts = top.view(1 << pb, 1 << (8 - pb)).sum(1)[:max(nparts, 1)] if pb else top.sum().view(1)
     else:
-        p32, spart = sort_cols(cols[:3], [pbits, 64, 64])
+        p32, spart = sort_cols(cols()[:3], [pbits, 64, 64])
     if hi.is_cuda:
         # runs of rows equal in the sort columns (long keys sharing 16 bytes),
         # found through a hash of the columns in sorted order and insertion-
@@ -991,9 +997,9 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
                   _hip.ptr(klen), _hip.ptr(rep), _hip.ptr(src), _hip.ptr(bad), s)
         if not int(bad.item()):
             return done(p32.long())
-        p32, spart = sort_cols(cols, [pbits, 64, 64, 8])
+        p32, spart = sort_cols(cols(), [pbits, 64, 64, 8])
     perm = p32.long()
-    scols = [c[perm] for c in cols]
+    scols = [c[perm] for c in cols()]
     pos = torch.arange(n, dtype=torch.int64, device=d)
     cap = 16
     while True:
@@ -1015,11 +1021,11 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
         k = cap // 8
         rh, rl, rr = hi[rows], lo[rows], rep[rows]
         cap += 16
-        cols = [grp, key_word(rh, rl, rr, src, k), key_word(rh, rl, rr, src, k + 1), klen[rows].clamp(max=cap)]
+        rcols = [grp, key_word(rh, rl, rr, src, k), key_word(rh, rl, rr, src, k + 1), klen[rows].clamp(max=cap)]
         gbits = max(8, int(grp[-1]).bit_length())
-        sub = sort_keys_checked(cols, bits=[gbits, 64, 64, max(8, cap.bit_length())]).long()
+        sub = sort_keys_checked(rcols, bits=[gbits, 64, 64, max(8, cap.bit_length())]).long()
         perm[pos] = rows[sub]  # a group's rows stay inside its positions (grp is the major column)
-        scols = [c[sub] for c in cols]
+        scols = [c[sub] for c in rcols]
 
 
 def sort_keys_checked(words, bits=None, retries: int = 2, **kw):

@@ -66,6 +66,8 @@ from . import dist as D
 from . import reducers as RD
 from . import values as VL
 
+_BIG_TABLE = 1 << 24  # (slots) map tables this large are refitted from 2x their fit, not 4x
+
 
 def _bits(n: int) -> int:
     return max(1, int(max(n, 1) - 1).bit_length())
@@ -902,8 +904,12 @@ class GenericPlane:
             fit = max(ops.next_pow2(2 * max(n, 1)), self._cap0)  # load 1/4 - 1/2
             if n > mp.table.cap // 8 and self._cap < fit:
                 self._cap = fit  # next iteration's table
-            elif mp.table.cap >= 4 * fit:
-                self._cap = fit  # grown past the key count (16x after an overflow): fitted for the next maps
+            elif mp.table.cap >= (2 if fit >= _BIG_TABLE else 4) * fit:
+                # grown past the key count (4x on a regrowth, 16x after an
+                # overflow): fitted for the next maps — large tables from 2x
+                # already, their reset and compaction stream every slot (the
+                # bigram job's 2^27-slot table: ~2 ms of each step)
+                self._cap = fit
             return
         raise RuntimeError("general plane: the map did not converge (table regrowth / retries)")
 

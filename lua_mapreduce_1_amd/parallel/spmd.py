@@ -48,6 +48,7 @@ from .staging import N_ARENAS, StagingMixin
 
 # largest map table the sparsity rule asks for (2^25 slots = 1.3 GB of HBM)
 _MAX_SPARSE_CAP = 1 << 25
+_BIG_TABLE = 1 << 24  # (slots) map tables this large shrink to their fit from 2x it, not 4x
 
 
 def _tensor_ops() -> tuple:
@@ -377,7 +378,8 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         reset, or replaced by a larger one once an earlier map's distinct-key
         count has raised the target capacity (``_map_sync``)."""
         t = self.tables[self.tslot]
-        if t is not None and (t.cap < self._table_capacity or t.cap >= 4 * self._table_capacity):
+        shrink = 2 if self._table_capacity >= _BIG_TABLE else 4  # (as _adapt_capacity)
+        if t is not None and (t.cap < self._table_capacity or t.cap >= shrink * self._table_capacity):
             self.tables[self.tslot] = t = None  # grown, or far too large (every tail scans each slot)
         if t is None:
             self.tables[self.tslot] = ops.HashTable(self._table_capacity, device=self.device, op=self.op)
@@ -573,7 +575,11 @@ class SPMDEngine(StagingMixin, CheckpointMixin):
         # tail's compaction reads every slot's line of every column)
         fit = max(ops.next_pow2(2 * max(n_claimed, 1)), self._initial_capacity,
                   min(ops.next_pow2(TUNABLES.map_sparsity * max(n_claimed, 1)), _MAX_SPARSE_CAP) if big else 0)
-        if self._table_capacity >= 4 * fit:
+        # large tables come down to `fit` from twice it already: the reset and
+        # the compaction stream every slot, and the grown table of 23 M bigram
+        # keys (2^27 slots, 5.4 GB with the values) cost 2 ms of the step in
+        # those two passes alone (profiles/r6/bigram/)
+        if self._table_capacity >= (2 if fit >= _BIG_TABLE else 4) * fit:
             self._table_capacity = fit
 
     def _device_spans(self, res, recs, j0: int, j1: int) -> None:

@@ -64,3 +64,25 @@ def test_overflowed_table_is_fitted_for_later_maps_gpu(gpu):
         pytest.skip("corpus too small to overflow")
     assert caps[0] == 16 << 12  # grown 16x after the overflow
     assert caps[2] == 1 << (2 * len(want) - 1).bit_length()  # fitted: next_pow2(2 n)
+
+
+def test_big_tables_come_down_to_their_fit():
+    """A map table of 2^24 slots or more comes down to next_pow2(2 n) from
+    twice that (the reset and the compaction stream every slot); smaller ones
+    keep the 4x hysteresis; a fitted big table stays put."""
+    from types import SimpleNamespace
+
+    from lua_mapreduce_1_amd.parallel import spmd as S
+
+    def eng(cap, mapped_mb):
+        return SimpleNamespace(table=SimpleNamespace(cap=cap), _table_capacity=cap, _initial_capacity=1 << 20,
+                               _mapped_bytes=mapped_mb << 20)
+    e = eng(1 << 27, 300)  # 23 M bigram keys after the 4x regrowth
+    S.SPMDEngine._adapt_capacity(e, 23_000_000)
+    assert e._table_capacity == 1 << 26
+    e.table.cap = e._table_capacity
+    S.SPMDEngine._adapt_capacity(e, 23_000_000)
+    assert e._table_capacity == 1 << 26
+    small = eng(1 << 22, 0)
+    S.SPMDEngine._adapt_capacity(small, 600_000)
+    assert small._table_capacity == 1 << 22

@@ -115,6 +115,14 @@ def run_job(name: str, mod_name: str, store, nbytes: int, check_splits: list[byt
            "bytes": int(nbytes), "GB_per_s": nbytes / (ms / 1000.0) / 1e9, "distinct_keys": res.distinct_keys,
            "total_value": res.total_value, "timings_last_step": res.timings}
     mp = getattr(eng.plane, "map", None)
+    # the map tables' capacities (slots): the reset and the compaction stream every slot
+    caps = [int(t.cap) for t in getattr(eng, "tables", []) if t is not None]
+    for m in getattr(eng.plane, "_maps", None) or []:
+        if getattr(m, "table", None) is not None:
+            caps.append(int(m.table.cap))
+    if getattr(mp, "table", None) is not None:
+        caps.append(int(mp.table.cap))
+    out["table_caps"] = sorted(set(caps))
     if getattr(mp, "reducers", None) is not None:
         out["combines_last_step"] = mp.combines
         out["values_after_combine"] = int(mp.table.npost)
