@@ -886,7 +886,7 @@ def _alpha_words(k7, alpha: list, nparts: int):
 def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: torch.Tensor,
                    src: torch.Tensor | None, nparts: int, klen: torch.Tensor | None = None,
                    with_part: bool = False, with_counts: bool = False, w1: torch.Tensor | None = None,
-                   k7=None):
+                   k7=None, perm32: bool = False):
     """Stable permutation ordering rows by (partition, exact key bytes) on the
     device, for key sets the (partition, hi, lo) sort plus the tie fix-up
     cannot order (long keys — whose lo is a hash — in long runs of a shared
@@ -902,7 +902,9 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     key set keep their input order where they tie.  None when a key is longer
     than 8 * EXACT_MAX_WORDS bytes (the caller orders on the host).
     ``klen``: the keys' lengths when the caller has them (key_meta); ``w1``:
-    their ``key_word(..., 1)`` likewise (key_meta(want_w1=True)); ``k7``:
+    their ``key_word(..., 1)`` likewise (key_meta(want_w1=True)); ``perm32``
+    (GPU): the permutation as the sort's int32 (no int64 round trip for a
+    caller whose gathers take int32 rows); ``k7``:
     key_meta(want_k7=True)'s 7-bit sort words and flag — when every key's
     first 16 bytes are 7-bit, the GPU sort of keys past 16 bytes runs over
     those two words (15 passes and one gather instead of 17 and two: the
@@ -958,6 +960,10 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
 
     def done(p):
         # every later step reorders rows only inside runs of one partition
+        if perm32 and p.is_cuda:
+            p = p if p.dtype == torch.int32 else p.to(torch.int32)
+        elif p.dtype != torch.int64:
+            p = p.long()
         out = (p, spart) if with_part else p
         if with_counts:
             c = counts if counts is not None else bincount(spart, max(nparts, 1))
@@ -967,7 +973,7 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
     if max_len <= 16 or not hi.is_cuda:
         p32, spart = sort_cols(cols(), [pbits, 64, 64, 8])
         if max_len <= 16:
-            return done(p32.long())
+            return done(p32)
     elif not k7_bad and pbits == 8:
         words, bits, pb = _alpha_words(k7, alpha, nparts) if alpha is not None else (None, None, 8)
         if words is None:
@@ -996,7 +1002,7 @@ def exact_key_perm(part: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor, rep: 
         _hip.call("mr_exact_fix", _hip.ptr(sh), _hip.ptr(p32), n, _hip.ptr(part32), _hip.ptr(hi), _hip.ptr(w1),
                   _hip.ptr(klen), _hip.ptr(rep), _hip.ptr(src), _hip.ptr(bad), s)
         if not int(bad.item()):
-            return done(p32.long())
+            return done(p32)
         p32, spart = sort_cols(cols(), [pbits, 64, 64, 8])
     perm = p32.long()
     scols = [c[perm] for c in cols()]

@@ -709,7 +709,7 @@ def finalize_exact_device(hi, lo, val, rep, src, nparts: int, partition_module=N
     else:
         part = partition_of(hi, lo, rep, src, nparts, partition_module)
     got = ops.exact_key_perm(part, hi, lo, rep, src, nparts, klen=klen, with_part=True,
-                             with_counts=hi.is_cuda, w1=w1, k7=k7) if src is not None else None
+                             with_counts=hi.is_cuda, w1=w1, k7=k7, perm32=True) if src is not None else None
     exact = got is not None
     spart = counts = None
     if got is None:
