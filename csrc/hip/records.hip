@@ -466,6 +466,27 @@ __global__ void __launch_bounds__(256) rec_bucket32_kernel(const u32* __restrict
   if (h[t]) atomicAdd(&ghist[t], h[t]);
 }
 
+// Digit histograms ([4][256], digits 0..3) of 32-bit key prefixes already
+// extracted (the range-pipelined exchange ships them with the rows, so the
+// receiver's sort skips its key pass over the rows).
+__global__ void __launch_bounds__(256) rec_hist32_kernel(const u32* __restrict__ k32, u64 n, u32* __restrict__ ghist) {
+  __shared__ u32 h[4][256];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) h[b][t] = 0;
+  __syncthreads();
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + t; i < n; i += stride) {
+    const u32 k = k32[i];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 0xFFu], 1u);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    if (h[b][t]) atomicAdd(&ghist[b * 256 + t], h[b][t]);
+}
+
 // Splitter sampling of the record plane (parallel/planes.py
 // _sample_splitters) in three launches instead of ~20 small torch ops (the
 // W = 8 step's preparation was host-bound on them, ~25 us of host time each):
@@ -657,6 +678,14 @@ int mr_rec_bucket32(const void* k32, u64 n, const void* split, u32 nsplit, u32 K
   if (nsplit > 1024 || K == 0 || W == 0 || (u64)K * W > 256 || (nsplit + 1 + K - 1) / K > W) return -1;
   hipLaunchKernelGGL(rc::rec_bucket32_kernel, dim3(rc_grid(n, 2048)), dim3(256), 0, s, (const u32*)k32, n,
                      (const u32*)split, nsplit, K, W, (u32*)bucket, (u32*)ghist);
+  return (int)hipGetLastError();
+}
+
+// ghist: zeroed u32 [>= 1024]
+int mr_rec_hist32(const void* k32, u64 n, void* ghist, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(rc::rec_hist32_kernel, dim3(rc_grid(n, 2048)), dim3(256), 0, s, (const u32*)k32, n,
+                     (u32*)ghist);
   return (int)hipGetLastError();
 }
 

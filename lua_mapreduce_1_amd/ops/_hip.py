@@ -105,6 +105,7 @@ _SIGS = {
     "mr_rec_dest32": [_p, _u64, _p, _u32, _p, _p],
     "mr_rec_bucket32": [_p, _u64, _p, _u32, _u32, _u32, _p, _p, _p],
     "mr_rec_sample32": [_p, _u64, _u32, _u64, _p, _p],
+    "mr_rec_hist32": [_p, _u64, _p, _p],
     "mr_rec_pick": [_p, _u64, _u32, _p, _p],
     "mr_rec_xchg": [_p, _u32, _u32, ctypes.c_longlong, _p, _p, _p, _p],
     "mr_agg_insert": [_p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p, _u64, _p, _p, _p, _u64, _u64, _p, _p],

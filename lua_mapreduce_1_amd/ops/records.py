@@ -183,6 +183,15 @@ def bucket32(k32: torch.Tensor, sub: torch.Tensor, K: int, W: int):
     return torch.remainder(a, K).mul_(W).add_(torch.div(a, K, rounding_mode="floor")), None
 
 
+def hist32(k32: torch.Tensor) -> torch.Tensor:
+    """GPU: the radix sort's digit histograms of 32-bit key prefixes (an int32
+    [2048] block, digits 0..3 filled — the layout keys32(ghist=) gives) for
+    prefixes that are already extracted."""
+    gh = torch.zeros(2048, dtype=torch.int32, device=k32.device)
+    _hip.call("mr_rec_hist32", _hip.ptr(k32), k32.numel(), _hip.ptr(gh), _hip.stream(k32.device))
+    return gh
+
+
 def sample32(k32: torch.Tensor, k: int, seed: int) -> torch.Tensor:
     """GPU: ``k`` 32-bit key prefixes (int64, unsigned values) of rows drawn
     with replacement by a counter-based hash of ``seed`` (-1s when there are

@@ -1185,6 +1185,11 @@ class RecordPlane:
         send, rcv = both[:W, :K], both[W:, :K]  # [destination][round], [source][round]
         recv_buf = torch.empty((int(rcv.sum()), rb), dtype=torch.uint8, device=dev)
         out = torch.empty_like(recv_buf)
+        # GPU: each round's 32-bit key prefixes travel beside its rows (4 more
+        # bytes per row on the wire, hidden behind the receive sorts): the
+        # receiver's sort then skips its key pass over the rows
+        ship = rec.is_cuda and k32 is not None and TUNABLES.rec_ship_keys
+        recv_k32 = torch.empty(int(rcv.sum()), dtype=torch.int32, device=dev) if ship else None
         # the send side (row gathers, each round's all-to-all queued behind its
         # gather) runs on a stream of its own: the receive side's sort of round
         # k does not wait behind the gathers of rounds > k on one stream
@@ -1201,23 +1206,33 @@ class RecordPlane:
                 buf = RC.gather(rec, perm[s0:s0 + ms]) if ms else torch.zeros((0, rb), dtype=torch.uint8,
                                                                               device=dev)
                 work = D.all_to_all_v_into(recv_buf[r0:r0 + mr], buf, ssz, rsz, eng.group, async_op=True)
-                rounds.append((work, buf, r0, mr))
+                kwork = kbuf = None
+                if ship:
+                    kbuf = k32.index_select(0, perm[s0:s0 + ms]) if ms else torch.zeros(0, dtype=torch.int32,
+                                                                                         device=dev)
+                    kwork = D.all_to_all_v_into(recv_k32[r0:r0 + mr], kbuf, ssz, rsz, eng.group, async_op=True)
+                rounds.append((work, kwork, (buf, kbuf), r0, mr))
                 s0 += ms
                 r0 += mr
         if side is not None:
-            for t in (rec, perm, recv_buf):  # read / written under the side stream
+            for t in (rec, perm, recv_buf, k32) + ((recv_k32,) if ship else ()):  # used under the side stream
                 t.record_stream(side)
         bads = []
-        for work, _buf, r0, mr in rounds:
-            if work is not None:
-                work.wait()
-            elif side is not None:  # (a synchronous exchange, e.g. gloo: its copies ran on the side stream)
-                main.wait_stream(side)
+        for work, kwork, _bufs, r0, mr in rounds:
+            for w in (work, kwork):
+                if w is not None:
+                    w.wait()
+            if side is not None and (work is None or (ship and kwork is None)):
+                main.wait_stream(side)  # (a synchronous exchange, e.g. gloo: its copies ran on the side stream)
             if not mr:
                 continue
             piece = recv_buf[r0:r0 + mr]
-            gh = torch.zeros(2048, dtype=torch.int32, device=dev) if piece.is_cuda else None
-            pk = RC.keys32(piece, kb, gh)
+            if ship:
+                pk = recv_k32[r0:r0 + mr]
+                gh = RC.hist32(pk)
+            else:
+                gh = torch.zeros(2048, dtype=torch.int32, device=dev) if piece.is_cuda else None
+                pk = RC.keys32(piece, kb, gh)
             p, _sk, bad = RC.sort(piece, kb, pk, gh, defer=True)
             RC.gather(piece, p, out=out[r0:r0 + mr])
             bads.append((bad, pk, r0, mr))

@@ -118,6 +118,11 @@ class Tunables:
     agg_phases: int = _knob("MR_AGG_PHASES", 1,
                             "generic combine kernel: a thread's 8 rows in 1, 2 or 4 phases (fewer row keys held in "
                             "registers: 79 / 56 / fewer VGPRs, 6 / 7 / more waves per SIMD)")
+    rec_ship_keys: bool = _knob("MR_REC_SHIP_KEYS", False,
+                                "range-pipelined exchange on the GPU: each round's 32-bit key prefixes travel beside "
+                                "its rows (the receive-side sort skips its key pass over the rows; W = 8 proxy: "
+                                "-6 % at a 1000 GB/s link model, +3 % at 400, even at 700 — off: one collective per "
+                                "round)")
     map_dyn: bool = _knob("MR_MAP_DYN", True,
                           "word-count map kernel: waves take the tile's token list 64 entries at a time from an "
                           "LDS counter (csrc/hip/wordcount3.hip DYN) instead of a fixed stride")

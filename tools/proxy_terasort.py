@@ -93,13 +93,15 @@ def main() -> int:
         return c.reshape(-1)
 
     cats = []  # [round] -> peers 1..W-1's rows of that round, concatenated (filled with peers)
+    cats_k32 = []  # [round] -> their 32-bit key prefixes (shipped beside the rows on the GPU)
 
     def fill(out, payload, own, k):
-        """out <- [this rank's own rows of round k | peer 1's | ...] (two copies)"""
+        """out <- [this rank's own rows (or key prefixes) of round k | peer 1's | ...] (two copies)"""
         out[:own].copy_(payload[:own])
-        if cats:
-            m = min(cats[k].shape[0], out.shape[0] - own)
-            out[own:own + m].copy_(cats[k][:m])
+        src = cats if payload.dim() == 2 else cats_k32
+        if src:
+            m = min(src[k].shape[0], out.shape[0] - own)
+            out[own:own + m].copy_(src[k][:m])
 
     xc = torch.cuda.Stream(device)  # the model's copy of the transfer's bytes (beside the link hold)
 
@@ -117,7 +119,7 @@ def main() -> int:
             evc = torch.cuda.Event()
             evc.record(xc)
         with torch.cuda.stream(xs):
-            link_hold((sum(send) - send[0]) * payload.shape[1])
+            link_hold((sum(send) - send[0]) * payload[:1].numel() * payload.element_size())
             xs.wait_event(evc)
             ev = torch.cuda.Event()
             ev.record(xs)
@@ -137,11 +139,12 @@ def main() -> int:
         def wait(self):
             torch.cuda.current_stream().wait_event(self.ev)
 
-    rnd = [0]
+    rnd = [0, 0]  # rounds of row exchanges, of key-prefix exchanges
 
     def all_to_all_v_into(out, payload, send, recv, group=None, async_op=False):
-        k = rnd[0] % max(K, 1)
-        rnd[0] += 1
+        j = 0 if payload.dim() == 2 else 1
+        k = rnd[j] % max(K, 1)
+        rnd[j] += 1
         return _Work(exchange(out, payload, send, k))
 
     def all_gather_tensor(t, group=None):
@@ -172,9 +175,10 @@ def main() -> int:
             peers.append([blk[RC.dest32(k32, sp).to(torch.int64) == 0]])
         del blk, k32
     cats.extend(torch.cat([pr[k] for pr in peers]) for k in range(len(peers[0])))
+    cats_k32.extend(RC.keys32(c, TS.KEY) for c in cats)
     peer_counts.append(torch.tensor([[r.shape[0] for r in pr] for pr in peers], dtype=torch.int64, device=device))
     for _ in range(a.warmup):
-        rnd[0] = 0
+        rnd[0] = rnd[1] = 0
         res = eng.run_iteration()
         del res
     torch.cuda.synchronize()
@@ -182,7 +186,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for _ in range(a.steps):
         t1 = time.perf_counter()
-        rnd[0] = 0
+        rnd[0] = rnd[1] = 0
         res = eng.run_iteration()
         torch.cuda.synchronize()
         per.append(1000 * (time.perf_counter() - t1))
