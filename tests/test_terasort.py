@@ -349,6 +349,15 @@ def test_gpu_sampling_and_count_rows(gpu):
 
 
 @pytest.mark.gpu
+def test_gpu_forced_shuffle_rccl_shipped_keys(gpu, monkeypatch):
+    """The exchange rounds with each round's key prefixes shipped beside its
+    rows (MR_REC_SHIP_KEYS=1: a second asynchronous all-to-all per round, the
+    receive-side sort from the shipped prefixes), one-rank RCCL."""
+    monkeypatch.setenv("MR_REC_SHIP_KEYS", "1")  # (read by the spawned rank at import)
+    _run(1, on_gpu=True, backend="nccl", force_shuffle=True)
+
+
+@pytest.mark.gpu
 def test_gpu_forced_shuffle_rccl(gpu):
     """The record plane's all_to_all_single of 100-byte rows on RCCL."""
     _run(1, on_gpu=True, backend="nccl", force_shuffle=True)
